@@ -1,0 +1,171 @@
+#!/usr/bin/env python3
+"""Benchmark: request x rule predicate evaluations per second (BASELINE.json `metric`).
+
+Workload (per GPU): the C2 rule family of BASELINE.json configs[1] (`destination.service == ... &&
+request.path.startsWith(...) && source.ip != ip(...)`) scaled to the metric's 10k rules, over 1M
+synthetic requests (Zipf(1.1) services) resident in HBM -- the per-GPU shard of configs[4]
+(8 x MI355X, 8M requests).  A step = one evaluation of every rule against every request of the
+shard (the full predicate bitmap) + the per-rule hit counters, all-reduced over RCCL when N > 1.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--rules R] [--requests N_PER_GPU]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Prints one JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--rules", type=int, default=10000)
+    p.add_argument("--requests", type=int, default=1 << 20)
+    p.add_argument("--cpu-sample-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(manifest, rules, batch, seconds, threads):
+    """The oracle (C restatement of the reference interpreter, oracle/il_interp.c) on host cores,
+    time-bounded sample of the same workload.  Rules are precompiled (best case for the reference:
+    expression cache >= R)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    ev = oracle.OracleEvaluator(manifest)
+    oracle.oracle_matrix(ev, rules, batch, 0, 1, threads=1)  # compile all rules (untimed)
+    chunk = 256
+    done = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done + chunk <= batch.n:
+        oracle.oracle_matrix(ev, rules, batch, done, done + chunk, threads=threads)
+        done += chunk
+    dt = time.perf_counter() - t0
+    pairs = done * len(rules)
+    return {"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": "%d requests x %d rules (%.1fs, oracle C restatement, rules precompiled)" % (
+                done, len(rules), dt)}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+
+    from istio_amd import build
+    build.build()
+    from istio_amd import workloads as W
+    from istio_amd.engine import Engine
+
+    # requests shard per rank; the rule set is replicated
+    manifest, rules, batch = W.c2_workload(n_rules=args.rules, n_requests=args.requests, seed=2 + 1000 * rank)
+    rules = W.c2_rules(args.rules, seed=2)[0]
+    eng = Engine(local)
+    eng.set_vocabulary(manifest)
+    st = eng.compile(rules)
+    assert (st == 0).all()
+    t_pack = time.perf_counter()
+    db = eng.upload(batch)
+    t_pack = time.perf_counter() - t_pack
+
+    R, N = len(rules), batch.n
+    Wd = (R + 31) // 32
+    dev = torch.device("cuda", local)
+    d_match = torch.empty((Wd, N), dtype=torch.int32, device=dev)
+    d_err = torch.empty((Wd, N), dtype=torch.int32, device=dev)
+    hits = torch.zeros(R, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(ev0=None, ev1=None):
+        if ev0 is not None:
+            ev0.record(stream)
+        db.eval(d_match.data_ptr(), d_err.data_ptr(), sh)
+        if ev1 is not None:
+            ev1.record(stream)
+        rc = eng.lib.mxp_hits_device(eng.h, d_match.data_ptr(), N, sh, hits.data_ptr())
+        assert rc == 0
+        if world > 1:
+            dist.all_reduce(hits)  # RCCL over xGMI: per-rule hit counters
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(*evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    pairs_total = world * N * R * args.steps
+    value = pairs_total / elapsed
+    # algorithmic bytes of one eval launch: packed columns read (kind u8 + value u64 per referenced
+    # column per request), the rule program, and the two output bitmaps written
+    n_cols = 3
+    prog_bytes = 16 * sum(eng.rule_vm_text(i).count("\n") for i in range(R)) + 4 * (R + 1)
+    alg_bytes = N * n_cols * 9 + prog_bytes + 2 * N * Wd * 4
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+
+    out = {
+        "metric": "request x rule predicate evals/sec at 10k rules",
+        "value": value,
+        "unit": "pairs/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (seeded C2 rule family; requests resident in HBM)",
+        "config": {"workload": "C2 rules scaled to R=%d, %d requests per GPU (configs[1] family, configs[4] shard)" % (R, N),
+                   "rules": R, "requests_per_gpu": N, "parallelism": "request-sharded dp%d" % world},
+        "kernel_ms": kernel_ms,
+        "pack_upload_s": t_pack,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pair": alg_bytes / (N * R)},
+    }
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        sample = W.c2_workload(n_rules=args.rules, n_requests=min(N, 1 << 16), seed=2)[2]
+        out["cpu_baseline"] = cpu_baseline(manifest, rules, sample, args.cpu_sample_seconds, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(out))
+    db.free()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,114 @@
+/*
+ * mxp.h -- C-ABI of the MI355X-native batched policy engine for Istio Mixer's Check path.
+ *
+ * The engine replaces, for batches of requests, the per-request / per-rule Go call chain
+ *
+ *   runtime.Resolver.Resolve(bag, variety)            mixer/pkg/runtime/resolver.go:110
+ *     filterActions -> expr.Evaluator.EvalPredicate    resolver.go:202-238, mixer/pkg/expr/evaluator.go:25-31
+ *       evaluator.IL.EvalPredicate                     mixer/pkg/il/evaluator/evaluator.go:75
+ *         compiler.Compile + interpreter.Interpreter   mixer/pkg/il/compiler/compiler.go:125,
+ *                                                      mixer/pkg/il/interpreter/interpreterRun.go:18
+ *
+ * and is meant to be bound from the reference's Go code through cgo.  All
+ * entry points take plain pointers and sizes, return an int status (0 = MXP_OK) and never throw.
+ * Output arrays are caller-owned.  One engine = one GPU + one HIP stream; calls on one engine must
+ * be serialised by the caller (the Go shim owns one goroutine per device stream).
+ */
+#ifndef MXP_H
+#define MXP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mxp_batch.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MXP_OK 0
+#define MXP_ERR_ARG 1       /* bad argument */
+#define MXP_ERR_STATE 2     /* call out of order (e.g. eval before a rule set exists) */
+#define MXP_ERR_DEVICE 3    /* HIP runtime error; mxp_last_error() has the text */
+#define MXP_ERR_NOMEM 4
+
+typedef struct mxp_engine mxp_engine;
+
+/* Engine lifetime.  device = HIP device ordinal; device = -1 creates a host-only engine that can
+ * compile and inspect rule sets (IL text, VM listing) but not evaluate. */
+int mxp_engine_create(int device, mxp_engine** out);
+void mxp_engine_destroy(mxp_engine* eng);
+const char* mxp_last_error(const mxp_engine* eng);
+
+/*
+ * Vocabulary (attribute manifest): names + ValueType enum values of istio.io/api
+ * mixer/v1/config/descriptor (STRING=1, INT64=2, DOUBLE=3, BOOL=4, TIMESTAMP=5, IP_ADDRESS=6,
+ * EMAIL_ADDRESS=7, URI=8, DNS_NAME=9, DURATION=10, STRING_MAP=11).
+ * Replaces evaluator.IL.ChangeVocabulary (mixer/pkg/il/evaluator/evaluator.go:107); invalidates the
+ * current rule set.
+ */
+int mxp_vocab_set(mxp_engine* eng, const char* const* names, const int32_t* value_types, uint32_t n);
+
+/*
+ * Compile a rule set: n predicate expressions (rule i = exprs[i]) compiled with the reference's
+ * compiler (compiler.Compile, compiler.go:125) and lowered to the GPU bytecode; uploaded once.
+ * status[i] (optional) receives one of MXP_RULE_*.
+ */
+#define MXP_RULE_OK 0
+#define MXP_RULE_PARSE_ERROR 1     /* expr.Parse failed: the resolver drops such rules (controller.go:406-410) */
+#define MXP_RULE_TYPE_ERROR 2      /* type check failed: every evaluation returns this error */
+#define MXP_RULE_COMPILE_ERROR 3   /* code generation failed: every evaluation returns this error */
+#define MXP_RULE_COMPILE_PANIC 4   /* the reference panics while compiling */
+#define MXP_RULE_UNSUPPORTED 5     /* valid rule this build cannot lower yet (evaluations report it) */
+int mxp_ruleset_compile(mxp_engine* eng, const char* const* exprs, uint32_t n, int32_t* status);
+/* Text of rule i's compile error / IL (text.WriteText, mixer/pkg/il/text/write.go:26) / VM listing. */
+int mxp_rule_error(mxp_engine* eng, uint32_t rule, char* buf, uint32_t cap);
+int mxp_rule_il_text(mxp_engine* eng, uint32_t rule, char* buf, uint32_t cap);
+int mxp_rule_vm_text(mxp_engine* eng, uint32_t rule, char* buf, uint32_t cap);
+/* ValueType of rule i's expression (Expression.EvalType) and its il.Type return type. */
+int mxp_rule_types(mxp_engine* eng, uint32_t rule, int32_t* value_type, int32_t* il_type);
+
+/*
+ * Evaluate every rule against every bag of the batch (EvalPredicate semantics for each pair).
+ * Output bitmaps are rule-word-major: bit (r % 32) of word [(r / 32) * n_requests + q] describes
+ * (request q, rule r).  match_bits: predicate true.  err_bits: evaluation error or Go panic.
+ * Either pointer may be NULL.  Error details of the last batch: mxp_pair_error.
+ */
+int mxp_eval_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* match_bits, uint32_t* err_bits);
+
+/*
+ * Eval (expr.Evaluator.Eval) for small batches: raw result register per pair, [n_requests][n_rules],
+ * plus per-pair code (0 false/ok, 1 true, 2 error, 3 panic).  Decode with mxp_value_text.
+ */
+int mxp_eval_values(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* values, uint8_t* codes);
+/* Render a result register of rule `rule` as Go would print it with %v (strings raw). */
+int mxp_value_text(mxp_engine* eng, uint32_t rule, uint64_t value, char* buf, uint32_t cap);
+/* Result kind of a value register: MXP_STRING, MXP_INT64, ... (interface values report their kind). */
+int mxp_value_kind(mxp_engine* eng, uint32_t rule, uint64_t value);
+
+/* Error text of pair (request, rule) from the last evaluated batch, as the reference would report it.
+ * Returns MXP_OK with buf = "" if the pair did not fail, 1 if it failed with a panic. */
+int mxp_pair_error(mxp_engine* eng, uint32_t request, uint32_t rule, char* buf, uint32_t cap);
+/* Number of error pairs of the last batch (may exceed the log capacity). */
+uint64_t mxp_error_count(mxp_engine* eng);
+
+/*
+ * Device-resident batches (benchmarking and pipelining): pack + upload once, evaluate many times.
+ * mxp_batch_eval_device enqueues on `stream` (a hipStream_t; NULL = engine stream) and writes the
+ * bitmaps to DEVICE pointers (rule-word-major, as above).  Nothing is synchronised.
+ */
+typedef struct mxp_dbatch mxp_dbatch;
+int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out);
+void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db);
+int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err);
+/* Per-rule hit counters: d_hits[rule] += number of requests whose predicate was true (device u64[n_rules]). */
+int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_requests, void* stream,
+                    unsigned long long* d_hits);
+uint32_t mxp_rule_count(const mxp_engine* eng);
+uint32_t mxp_dbatch_requests(const mxp_dbatch* db);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MXP_H */

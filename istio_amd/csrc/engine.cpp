@@ -1,0 +1,820 @@
+// engine.cpp -- host side of the MXP engine and the C-ABI of include/mxp.h.
+//
+// Responsibilities:
+//   * vocabulary + rule-set compilation (compile_rule -> lower_rule), one upload per snapshot;
+//   * batch packing: the caller's columnar bags (mxp_batch.h) become device SoA columns with every
+//     string interned into one id space (rule-set constants first, then the batch's own strings),
+//     IP byte strings and timestamps interned to canonical ids (so equality is id equality), and
+//     `map[const key]` lookups pre-extracted into virtual columns;
+//   * kernel launches on the engine's HIP stream and reporting of error pairs with the reference's
+//     exact error texts.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mxp.h"
+#include "goutil.h"
+#include "ilgen.h"
+#include "kargs.h"
+#include "lower.h"
+
+extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, hipStream_t s);
+extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
+                                      unsigned long long* hits, hipStream_t s);
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(size_t bytes) {
+        reset();
+        if (bytes == 0) bytes = 16;
+        n = bytes;
+        return hipMalloc(&p, bytes);
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+struct TimeKey {
+    int64_t s;
+    int32_t ns;
+    bool operator<(const TimeKey& o) const { return s != o.s ? s < o.s : ns < o.ns; }
+};
+
+constexpr uint64_t kNoValue = ~0ull;
+
+}  // namespace
+
+struct mxp_dbatch {
+    uint32_t n = 0;
+    DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
+    std::vector<std::string> overlay;                 // batch strings not in the rule set's pool
+    std::vector<std::string> overlay_bytes;           // batch byte strings (canonical)
+    std::vector<TimeKey> overlay_times;
+};
+
+struct mxp_engine : public mxp::LowerTables {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+
+    mxp::Vocabulary vocab;
+    mxp::FuncMap fmap = mxp::default_func_map();
+
+    // rule-set-global interning
+    std::unordered_map<std::string, uint32_t> gstr_ids;
+    std::vector<std::string> gstrs;
+    std::unordered_map<std::string, uint32_t> gbytes_ids;
+    std::vector<std::string> gbytes;
+    std::map<TimeKey, uint32_t> gtime_ids;
+    std::vector<TimeKey> gtimes;
+    std::vector<std::string> cols;
+    std::unordered_map<std::string, uint32_t> col_ids;
+    std::vector<std::pair<std::string, std::string>> vcols;
+    std::map<std::pair<std::string, std::string>, uint32_t> vcol_ids;
+    uint32_t empty_sid = 0;
+
+    struct Rule {
+        int32_t status = MXP_RULE_OK;
+        std::string error;
+        int32_t value_type = 0;
+        uint8_t il_ret = 0;
+        std::string il_text;
+        mxp::LoweredRule low;
+    };
+    std::vector<Rule> rules;
+    bool have_rules = false;
+    bool need_ipof = false, need_tsof = false, need_strings = false, need_maps = false;
+
+    DevBuf d_prog, d_rule_off, d_gstr_off, d_gstr;
+    DevBuf d_errlog, d_errcount;
+    uint32_t errcap = 1u << 20;
+
+    // last batch error details: key = request << 32 | rule
+    std::unordered_map<uint64_t, std::pair<uint32_t, std::string>> last_errors;
+    uint64_t last_error_count = 0;
+    std::unique_ptr<mxp_dbatch> last_db;  // keeps the last batch's interned overlays for decoding
+
+    // ---------------------------------------------------------------- LowerTables
+    uint32_t intern_string(const std::string& s) override {
+        auto it = gstr_ids.find(s);
+        if (it != gstr_ids.end()) return it->second;
+        uint32_t id = (uint32_t)gstrs.size();
+        gstr_ids.emplace(s, id);
+        gstrs.push_back(s);
+        return id;
+    }
+    uint32_t intern_bytes(const std::string& c) override {
+        auto it = gbytes_ids.find(c);
+        if (it != gbytes_ids.end()) return it->second;
+        uint32_t id = (uint32_t)gbytes.size();
+        gbytes_ids.emplace(c, id);
+        gbytes.push_back(c);
+        return id;
+    }
+    uint32_t intern_time(int64_t s, int32_t ns) override {
+        TimeKey k{s, ns};
+        auto it = gtime_ids.find(k);
+        if (it != gtime_ids.end()) return it->second;
+        uint32_t id = (uint32_t)gtimes.size();
+        gtime_ids.emplace(k, id);
+        gtimes.push_back(k);
+        return id;
+    }
+    uint32_t column(const std::string& attr) override {
+        auto it = col_ids.find(attr);
+        if (it != col_ids.end()) return it->second;
+        uint32_t id = (uint32_t)cols.size();
+        col_ids.emplace(attr, id);
+        cols.push_back(attr);
+        return id;
+    }
+    uint32_t vcolumn(const std::string& attr, const std::string& key) override {
+        auto k = std::make_pair(attr, key);
+        auto it = vcol_ids.find(k);
+        if (it != vcol_ids.end()) return it->second;
+        uint32_t id = (uint32_t)vcols.size();
+        vcol_ids.emplace(k, id);
+        vcols.push_back(k);
+        intern_string(key);
+        return id;
+    }
+    int32_t attr_type(const std::string& attr) override {
+        auto it = vocab.find(attr);
+        return it == vocab.end() ? -1 : it->second;
+    }
+
+    int fail(int code, const std::string& msg) {
+        last_error = msg;
+        return code;
+    }
+    int hipfail(hipError_t e, const char* what) {
+        last_error = std::string(what) + ": " + hipGetErrorString(e);
+        return MXP_ERR_DEVICE;
+    }
+
+    void reset_tables() {
+        gstr_ids.clear();
+        gstrs.clear();
+        gbytes_ids.clear();
+        gbytes.clear();
+        gtime_ids.clear();
+        gtimes.clear();
+        cols.clear();
+        col_ids.clear();
+        vcols.clear();
+        vcol_ids.clear();
+        rules.clear();
+        have_rules = false;
+        need_ipof = need_tsof = need_strings = need_maps = false;
+        empty_sid = intern_string("");
+    }
+
+    int compile(const char* const* exprs, uint32_t n, int32_t* status);
+    int pack(const mxp_bag_batch* b, mxp_dbatch* db);
+    void fill_args(mxp_kargs* A, const mxp_dbatch* db) const;
+    int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log);
+    std::string format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r) const;
+    std::string string_of(const mxp_dbatch* db, uint64_t sid) const {
+        if (!db) db = last_db.get();
+        if (sid < gstrs.size()) return gstrs[sid];
+        uint64_t j = sid - gstrs.size();
+        return (db && j < db->overlay.size()) ? db->overlay[j] : std::string("?");
+    }
+};
+
+// ------------------------------------------------------------------------------------ compile
+int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
+    reset_tables();
+    rules.resize(n);
+    std::vector<mxp_vm_ins> all;
+    std::vector<uint32_t> off(n + 1, 0);
+    for (uint32_t i = 0; i < n; i++) {
+        Rule& R = rules[i];
+        mxp::CompiledRule cr;
+        mxp::compile_rule(exprs[i] ? exprs[i] : "", vocab, fmap, &cr);
+        R.status = (int32_t)cr.status;
+        R.error = cr.error;
+        R.value_type = cr.value_type;
+        std::vector<mxp_vm_ins> code;
+        if (cr.status == mxp::CompiledRule::OK) {
+            const mxp::IlFunction* f = cr.program.get("eval");
+            R.il_ret = f ? f->ret : 0;
+            R.il_text = mxp::write_il_text(cr.program);
+            R.low = mxp::lower_rule(cr.program, this);
+            if (R.low.ok) {
+                code = R.low.code;
+                need_ipof |= R.low.uses_ipof;
+                need_tsof |= R.low.uses_tsof;
+                need_strings |= R.low.uses_strings;
+                need_maps |= R.low.uses_maps;
+            } else {
+                R.status = MXP_RULE_UNSUPPORTED;
+                R.error = "unsupported by the GPU lowering: " + R.low.why;
+            }
+        }
+        if (code.empty()) {
+            mxp_vm_ins e{};
+            e.op = VM_ERR;
+            e.y = R.status == MXP_RULE_COMPILE_PANIC ? PANIC_STATIC
+                  : R.status == MXP_RULE_UNSUPPORTED ? ERR_UNSUPPORTED : ERR_STATIC;
+            e.z = i;
+            code.push_back(e);
+        }
+        off[i] = (uint32_t)all.size();
+        all.insert(all.end(), code.begin(), code.end());
+        if (status) status[i] = R.status;
+    }
+    off[n] = (uint32_t)all.size();
+    // virtual columns follow the resolve columns
+    const uint32_t C = (uint32_t)cols.size();
+    for (auto& ins : all)
+        if ((ins.op & 0x7F) == VM_VCOL) ins.x += C;
+    for (auto& R : rules)
+        for (auto& ins : R.low.code)
+            if ((ins.op & 0x7F) == VM_VCOL) ins.x += C;
+
+    have_rules = true;
+    if (device < 0) return MXP_OK;  // host-only engine: compile / inspect, no device tables
+    // upload program + global string pool
+    hipError_t e;
+    have_rules = false;
+    if ((e = hipSetDevice(device)) != hipSuccess) return hipfail(e, "hipSetDevice");
+    if ((e = d_prog.alloc(all.size() * sizeof(mxp_vm_ins))) != hipSuccess) return hipfail(e, "hipMalloc prog");
+    if ((e = d_rule_off.alloc(off.size() * 4)) != hipSuccess) return hipfail(e, "hipMalloc rule_off");
+    std::vector<uint64_t> soff(gstrs.size() + 1, 0);
+    std::string blob;
+    for (size_t i = 0; i < gstrs.size(); i++) {
+        blob += gstrs[i];
+        soff[i + 1] = blob.size();
+    }
+    if ((e = d_gstr_off.alloc(soff.size() * 8)) != hipSuccess) return hipfail(e, "hipMalloc gstr_off");
+    if ((e = d_gstr.alloc(blob.size() + 8)) != hipSuccess) return hipfail(e, "hipMalloc gstr");
+    if (!all.empty() && (e = hipMemcpy(d_prog.p, all.data(), all.size() * sizeof(mxp_vm_ins), hipMemcpyHostToDevice)) != hipSuccess)
+        return hipfail(e, "upload prog");
+    if ((e = hipMemcpy(d_rule_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        return hipfail(e, "upload rule_off");
+    if ((e = hipMemcpy(d_gstr_off.p, soff.data(), soff.size() * 8, hipMemcpyHostToDevice)) != hipSuccess)
+        return hipfail(e, "upload gstr_off");
+    if (!blob.empty() && (e = hipMemcpy(d_gstr.p, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        return hipfail(e, "upload gstr");
+    have_rules = true;
+    return MXP_OK;
+}
+
+// ---------------------------------------------------------------------------------------- pack
+int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
+    const uint32_t n = b->n_requests;
+    const uint32_t C = (uint32_t)cols.size(), V = (uint32_t)vcols.size();
+    const uint32_t ncol = C + V;
+    db->n = n;
+    std::unordered_map<std::string, uint32_t> bcol;
+    for (uint32_t c = 0; c < b->n_columns; c++) bcol.emplace(b->column_names[c], c);
+
+    const uint32_t G = (uint32_t)gstrs.size();
+    std::vector<uint32_t> bmap(b->n_strings, MXP_VM_DONE);
+    std::unordered_map<std::string, uint32_t> overlay_ids;
+    auto bstr = [&](uint32_t sid) {
+        return std::string((const char*)b->str_bytes + b->str_offsets[sid],
+                           (size_t)(b->str_offsets[sid + 1] - b->str_offsets[sid]));
+    };
+    auto sid_of = [&](uint32_t s) -> uint32_t {
+        uint32_t& m = bmap[s];
+        if (m != MXP_VM_DONE) return m;
+        std::string v = bstr(s);
+        auto it = gstr_ids.find(v);
+        if (it != gstr_ids.end()) return m = it->second;
+        auto jt = overlay_ids.find(v);
+        if (jt != overlay_ids.end()) return m = jt->second;
+        uint32_t id = G + (uint32_t)db->overlay.size();
+        overlay_ids.emplace(v, id);
+        db->overlay.push_back(v);
+        return m = id;
+    };
+    std::unordered_map<std::string, uint32_t> obytes;
+    auto bytes_id = [&](const std::string& canon) -> uint32_t {
+        auto it = gbytes_ids.find(canon);
+        if (it != gbytes_ids.end()) return it->second;
+        auto jt = obytes.find(canon);
+        if (jt != obytes.end()) return jt->second;
+        uint32_t id = (uint32_t)(gbytes.size() + db->overlay_bytes.size());
+        obytes.emplace(canon, id);
+        db->overlay_bytes.push_back(canon);
+        return id;
+    };
+    std::map<TimeKey, uint32_t> otimes;
+    auto time_id = [&](int64_t s, int32_t ns) -> uint32_t {
+        TimeKey k{s, ns};
+        auto it = gtime_ids.find(k);
+        if (it != gtime_ids.end()) return it->second;
+        auto jt = otimes.find(k);
+        if (jt != otimes.end()) return jt->second;
+        uint32_t id = (uint32_t)(gtimes.size() + db->overlay_times.size());
+        otimes.emplace(k, id);
+        db->overlay_times.push_back(k);
+        return id;
+    };
+
+    std::vector<uint8_t> kinds((size_t)ncol * n, 0);
+    std::vector<uint64_t> vals((size_t)ncol * n, 0);
+    for (uint32_t c = 0; c < C; c++) {
+        auto it = bcol.find(cols[c]);
+        if (it == bcol.end()) continue;
+        const uint8_t* bk = b->kinds[it->second];
+        const uint64_t* bv = b->values[it->second];
+        uint8_t* ok = kinds.data() + (size_t)c * n;
+        uint64_t* ov = vals.data() + (size_t)c * n;
+        for (uint32_t r = 0; r < n; r++) {
+            uint8_t k = bk[r];
+            uint64_t v = bv[r];
+            switch (k) {
+            case MXP_STRING: v = sid_of((uint32_t)v); break;
+            case MXP_BYTES: {
+                std::string raw = bstr((uint32_t)v);
+                v = bytes_id(mxp::ip_canonical((const uint8_t*)raw.data(), raw.size()));
+                break;
+            }
+            case MXP_TIMESTAMP: v = time_id(b->time_sec[v], b->time_nsec[v]); break;
+            case MXP_OTHER: v = 0; break;
+            default: break;
+            }
+            ok[r] = k;
+            ov[r] = v;
+        }
+    }
+    for (uint32_t j = 0; j < V; j++) {
+        const std::string& attr = vcols[j].first;
+        const std::string& key = vcols[j].second;
+        uint8_t* ok = kinds.data() + (size_t)(C + j) * n;
+        uint64_t* ov = vals.data() + (size_t)(C + j) * n;
+        auto it = bcol.find(attr);
+        if (it == bcol.end()) continue;  // VC_ABSENT
+        const uint8_t* bk = b->kinds[it->second];
+        const uint64_t* bv = b->values[it->second];
+        for (uint32_t r = 0; r < n; r++) {
+            uint8_t k = bk[r];
+            if (k == MXP_ABSENT) {
+                ok[r] = VC_ABSENT;
+            } else if (k != MXP_STRING_MAP) {
+                ok[r] = VC_NOTMAP;
+            } else {
+                ok[r] = VC_VALUE;
+                ov[r] = empty_sid;
+                uint64_t m = bv[r];
+                for (uint64_t e = b->map_offsets[m]; e < b->map_offsets[m + 1]; e++) {
+                    uint32_t ks = b->map_keys[e];
+                    size_t kl = (size_t)(b->str_offsets[ks + 1] - b->str_offsets[ks]);
+                    if (kl == key.size() && memcmp(b->str_bytes + b->str_offsets[ks], key.data(), kl) == 0) {
+                        ov[r] = sid_of(b->map_values[e]);
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    std::vector<uint32_t> moff, mk, mv;
+    if (need_maps) {
+        moff.resize(b->n_maps + 1, 0);
+        for (uint32_t m = 0; m < b->n_maps; m++) {
+            for (uint64_t e = b->map_offsets[m]; e < b->map_offsets[m + 1]; e++) {
+                mk.push_back(sid_of(b->map_keys[e]));
+                mv.push_back(sid_of(b->map_values[e]));
+            }
+            moff[m + 1] = (uint32_t)mk.size();
+        }
+    }
+    // per-string pre-tables for dynamic ip() / timestamp()
+    std::vector<uint64_t> ipof, tsof;
+    const uint64_t S = G + db->overlay.size();
+    if (need_ipof) {
+        ipof.assign(S, kNoValue);
+        for (uint64_t s = 0; s < S; s++) {
+            std::string v = string_of(db, s);
+            uint8_t out[16];
+            if (mxp::go_parse_ip((const uint8_t*)v.data(), v.size(), out))
+                ipof[s] = MXP_FH(MXP_BYTES, bytes_id(mxp::ip_canonical(out, 16)));
+        }
+    }
+    if (need_tsof) {
+        tsof.assign(S, kNoValue);
+        for (uint64_t s = 0; s < S; s++) {
+            std::string v = string_of(db, s);
+            int64_t sec;
+            int32_t ns;
+            if (mxp::go_parse_rfc3339((const uint8_t*)v.data(), v.size(), &sec, &ns))
+                tsof[s] = MXP_FH(MXP_TIMESTAMP, time_id(sec, ns));
+        }
+    }
+    std::vector<uint64_t> ooff(db->overlay.size() + 1, 0);
+    std::string oblob;
+    if (need_strings) {
+        for (size_t i = 0; i < db->overlay.size(); i++) {
+            oblob += db->overlay[i];
+            ooff[i + 1] = oblob.size();
+        }
+    }
+
+    hipError_t e;
+    auto up = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
+        if ((e = d.alloc(bytes)) != hipSuccess) return hipfail(e, what);
+        if (bytes && (e = hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess)
+            return hipfail(e, what);
+        return MXP_OK;
+    };
+    int rc;
+    if ((rc = up(db->kinds, kinds.data(), kinds.size(), "upload kinds"))) return rc;
+    if ((rc = up(db->vals, vals.data(), vals.size() * 8, "upload vals"))) return rc;
+    if ((rc = up(db->map_off, moff.data(), moff.size() * 4, "upload map_off"))) return rc;
+    if ((rc = up(db->map_keys, mk.data(), mk.size() * 4, "upload map_keys"))) return rc;
+    if ((rc = up(db->map_vals, mv.data(), mv.size() * 4, "upload map_vals"))) return rc;
+    if ((rc = up(db->ipof, ipof.data(), ipof.size() * 8, "upload ipof"))) return rc;
+    if ((rc = up(db->tsof, tsof.data(), tsof.size() * 8, "upload tsof"))) return rc;
+    if ((rc = up(db->bstr_off, ooff.data(), ooff.size() * 8, "upload bstr_off"))) return rc;
+    if ((rc = up(db->bstr, oblob.data(), oblob.size(), "upload bstr"))) return rc;
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "pack sync");
+    return MXP_OK;
+}
+
+void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
+    memset(A, 0, sizeof *A);
+    A->prog = d_prog.as<mxp_vm_ins>();
+    A->rule_off = d_rule_off.as<uint32_t>();
+    A->n_rules = (uint32_t)rules.size();
+    A->n_words = (A->n_rules + 31) / 32;
+    A->groups_per_wave = 1;
+    A->n = db->n;
+    A->kinds = db->kinds.as<uint8_t>();
+    A->vals = db->vals.as<uint64_t>();
+    A->n_gstr = gstrs.size();
+    A->gstr_off = d_gstr_off.as<uint64_t>();
+    A->gstr = d_gstr.as<uint8_t>();
+    A->bstr_off = db->bstr_off.as<uint64_t>();
+    A->bstr = db->bstr.as<uint8_t>();
+    A->empty_sid = empty_sid;
+    A->map_off = db->map_off.as<uint32_t>();
+    A->map_keys = db->map_keys.as<uint32_t>();
+    A->map_vals = db->map_vals.as<uint32_t>();
+    A->ipof = db->ipof.as<uint64_t>();
+    A->tsof = db->tsof.as<uint64_t>();
+}
+
+int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
+                       bool log) {
+    mxp_kargs A;
+    fill_args(&A, db);
+    A.out_match = d_match;
+    A.out_err = d_err;
+    A.out_vals = d_vals;
+    hipError_t e;
+    if (log) {
+        if (!d_errlog.p) {
+            if ((e = d_errlog.alloc((size_t)errcap * sizeof(mxp_err_rec))) != hipSuccess) return hipfail(e, "errlog");
+            if ((e = d_errcount.alloc(16)) != hipSuccess) return hipfail(e, "errcount");
+        }
+        if ((e = hipMemsetAsync(d_errcount.p, 0, 16, s)) != hipSuccess) return hipfail(e, "memset errcount");
+        A.errlog = d_errlog.as<mxp_err_rec>();
+        A.errcount = d_errcount.as<uint32_t>();
+        A.errcap = errcap;
+    }
+    if (A.n == 0 || A.n_rules == 0) return MXP_OK;
+    const uint32_t gx = (A.n + 63) / 64;
+    const uint32_t gy = (A.n_words + 4 * A.groups_per_wave - 1) / (4 * A.groups_per_wave);
+    if ((e = mxp_launch_eval(&A, gx, gy, s)) != hipSuccess) return hipfail(e, "launch eval");
+    return MXP_OK;
+}
+
+std::string mxp_engine::format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r) const {
+    switch (r.code) {
+    case ERR_LOOKUP: return "lookup failed: '" + string_of(db, r.aux) + "'";
+    case ERR_CONV_S: case ERR_CONV_B: case ERR_CONV_I: case ERR_CONV_D: {
+        static const char* what[] = {"string", "bool", "integer or duration", "double"};
+        std::string val = "?";
+        if (b && r.aux < cols.size()) {
+            for (uint32_t c = 0; c < b->n_columns; c++) {
+                if (cols[r.aux] != b->column_names[c]) continue;
+                uint8_t k = b->kinds[c][r.req];
+                uint64_t v = b->values[c][r.req];
+                auto bs = [&](uint64_t sid) {
+                    return std::string((const char*)b->str_bytes + b->str_offsets[sid],
+                                       (size_t)(b->str_offsets[sid + 1] - b->str_offsets[sid]));
+                };
+                switch (k) {
+                case MXP_STRING: case MXP_OTHER: val = bs(v); break;
+                case MXP_INT64: val = std::to_string((int64_t)v); break;
+                case MXP_BOOL: val = v ? "true" : "false"; break;
+                case MXP_DOUBLE: {
+                    double d;
+                    memcpy(&d, &v, 8);
+                    val = mxp::go_format_float(d);
+                    break;
+                }
+                case MXP_DURATION: val = mxp::go_format_duration((int64_t)v); break;
+                case MXP_TIMESTAMP: val = mxp::go_format_time_utc(b->time_sec[v], b->time_nsec[v]); break;
+                case MXP_BYTES: {
+                    std::string raw = bs(v);
+                    val = mxp::go_format_bytes((const uint8_t*)raw.data(), raw.size());
+                    break;
+                }
+                case MXP_STRING_MAP: {
+                    val = "map[";
+                    for (uint64_t e = b->map_offsets[v]; e < b->map_offsets[v + 1]; e++) {
+                        if (e != b->map_offsets[v]) val += " ";
+                        val += bs(b->map_keys[e]) + ":" + bs(b->map_values[e]);
+                    }
+                    val += "]";
+                    break;
+                }
+                default: break;
+                }
+                break;
+            }
+        }
+        return std::string("error converting value to ") + what[r.code - ERR_CONV_S] + ": '" + val + "'";
+    }
+    case ERR_IP: return "could not convert " + string_of(db, r.aux) + " to IP_ADDRESS";
+    case ERR_TS:
+        return "could not convert '" + string_of(db, r.aux) +
+               "' to TIMESTAMP. expected format: '2006-01-02T15:04:05Z07:00'";
+    case ERR_MEMBER: return "member lookup failed: '" + string_of(db, r.aux) + "'";
+    case ERR_UNDERFLOW: return "stack underflow";
+    case ERR_STATIC: case ERR_UNSUPPORTED: case PANIC_STATIC:
+        return r.aux < rules.size() ? rules[r.aux].error : std::string("?");
+    case PANIC_MAPTYPE: return "Unknown map type";
+    case PANIC_EXTARG: return "reflect: Call using a value of the wrong type";
+    case PANIC_NOTBOOL: return "interpreter.Result: result is not bool";
+    case PANIC_CONV: return "interface conversion: interface {} is not string";
+    default: return "error code " + std::to_string(r.code);
+    }
+}
+
+// ===================================================================================== C-ABI
+extern "C" {
+
+int mxp_engine_create(int device, mxp_engine** out) {
+    if (!out) return MXP_ERR_ARG;
+    auto* e = new (std::nothrow) mxp_engine();
+    if (!e) return MXP_ERR_NOMEM;
+    e->device = device;
+    if (device < 0) {  // host-only engine (compiler / lowering inspection without a GPU)
+        e->reset_tables();
+        *out = e;
+        return MXP_OK;
+    }
+    hipError_t h = hipSetDevice(device);
+    if (h == hipSuccess) h = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (h != hipSuccess) {
+        delete e;
+        return MXP_ERR_DEVICE;
+    }
+    e->reset_tables();
+    *out = e;
+    return MXP_OK;
+}
+
+void mxp_engine_destroy(mxp_engine* eng) {
+    if (!eng) return;
+    if (eng->device >= 0) (void)hipSetDevice(eng->device);
+    if (eng->stream) (void)hipStreamDestroy(eng->stream);
+    delete eng;
+}
+
+const char* mxp_last_error(const mxp_engine* eng) { return eng ? eng->last_error.c_str() : "null engine"; }
+
+int mxp_vocab_set(mxp_engine* eng, const char* const* names, const int32_t* types, uint32_t n) {
+    if (!eng || (n && (!names || !types))) return MXP_ERR_ARG;
+    eng->vocab.clear();
+    for (uint32_t i = 0; i < n; i++) eng->vocab[names[i]] = types[i];
+    eng->reset_tables();
+    return MXP_OK;
+}
+
+int mxp_ruleset_compile(mxp_engine* eng, const char* const* exprs, uint32_t n, int32_t* status) {
+    if (!eng || (n && !exprs)) return MXP_ERR_ARG;
+    return eng->compile(exprs, n, status);
+}
+
+static int put_text(const std::string& s, char* buf, uint32_t cap) {
+    if (!buf || cap == 0) return MXP_ERR_ARG;
+    size_t k = std::min<size_t>(s.size(), cap - 1);
+    memcpy(buf, s.data(), k);
+    buf[k] = 0;
+    return MXP_OK;
+}
+
+int mxp_rule_error(mxp_engine* eng, uint32_t rule, char* buf, uint32_t cap) {
+    if (!eng || rule >= eng->rules.size()) return MXP_ERR_ARG;
+    return put_text(eng->rules[rule].error, buf, cap);
+}
+
+int mxp_rule_il_text(mxp_engine* eng, uint32_t rule, char* buf, uint32_t cap) {
+    if (!eng || rule >= eng->rules.size()) return MXP_ERR_ARG;
+    return put_text(eng->rules[rule].il_text, buf, cap);
+}
+
+int mxp_rule_vm_text(mxp_engine* eng, uint32_t rule, char* buf, uint32_t cap) {
+    if (!eng || rule >= eng->rules.size()) return MXP_ERR_ARG;
+    return put_text(mxp::vm_disasm(eng->rules[rule].low.code), buf, cap);
+}
+
+int mxp_rule_types(mxp_engine* eng, uint32_t rule, int32_t* vt, int32_t* il) {
+    if (!eng || rule >= eng->rules.size()) return MXP_ERR_ARG;
+    if (vt) *vt = eng->rules[rule].value_type;
+    if (il) *il = eng->rules[rule].il_ret;
+    return MXP_OK;
+}
+
+uint32_t mxp_rule_count(const mxp_engine* eng) { return eng ? (uint32_t)eng->rules.size() : 0; }
+uint32_t mxp_dbatch_requests(const mxp_dbatch* db) { return db ? db->n : 0; }
+
+int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out) {
+    if (!eng || !batch || !out) return MXP_ERR_ARG;
+    if (!eng->have_rules) return eng->fail(MXP_ERR_STATE, "no rule set compiled");
+    if (eng->device < 0) return eng->fail(MXP_ERR_STATE, "host-only engine");
+    hipError_t h = hipSetDevice(eng->device);
+    if (h != hipSuccess) return eng->hipfail(h, "hipSetDevice");
+    auto* db = new (std::nothrow) mxp_dbatch();
+    if (!db) return MXP_ERR_NOMEM;
+    int rc = eng->pack(batch, db);
+    if (rc) {
+        delete db;
+        return rc;
+    }
+    *out = db;
+    return MXP_OK;
+}
+
+void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db) {
+    if (eng) (void)hipSetDevice(eng->device);
+    delete db;
+}
+
+int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err) {
+    if (!eng || !db || !d_match || !d_err) return MXP_ERR_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    return eng->launch(db, s, d_match, d_err, nullptr, false);
+}
+
+int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_requests, void* stream,
+                    unsigned long long* d_hits) {
+    if (!eng || !d_match || !d_hits) return MXP_ERR_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    uint32_t R = (uint32_t)eng->rules.size();
+    if (!R || !n_requests) return MXP_OK;
+    hipError_t e = mxp_launch_hits(d_match, n_requests, R, (R + 31) / 32, d_hits, s);
+    return e == hipSuccess ? MXP_OK : eng->hipfail(e, "launch hits");
+}
+
+static int eval_common(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* match_bits, uint32_t* err_bits,
+                       uint64_t* values, uint8_t* codes) {
+    if (!eng || !batch) return MXP_ERR_ARG;
+    if (!eng->have_rules) return eng->fail(MXP_ERR_STATE, "no rule set compiled");
+    if (eng->device < 0) return eng->fail(MXP_ERR_STATE, "host-only engine");
+    hipError_t e = hipSetDevice(eng->device);
+    if (e != hipSuccess) return eng->hipfail(e, "hipSetDevice");
+    std::unique_ptr<mxp_dbatch> db(new mxp_dbatch());
+    int rc = eng->pack(batch, db.get());
+    if (rc) return rc;
+    const uint32_t n = batch->n_requests;
+    const uint32_t R = (uint32_t)eng->rules.size();
+    const uint32_t W = (R + 31) / 32;
+    DevBuf dm, de, dv;
+    if ((e = dm.alloc((size_t)W * n * 4)) != hipSuccess) return eng->hipfail(e, "alloc match");
+    if ((e = de.alloc((size_t)W * n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err");
+    if (values && (e = dv.alloc((size_t)n * R * 8)) != hipSuccess) return eng->hipfail(e, "alloc values");
+    rc = eng->launch(db.get(), eng->stream, dm.as<uint32_t>(), de.as<uint32_t>(), values ? dv.as<uint64_t>() : nullptr,
+                     true);
+    if (rc) return rc;
+    std::vector<uint32_t> hm, he;
+    if (match_bits || codes) {
+        hm.resize((size_t)W * n);
+        if ((e = hipMemcpyAsync(hm.data(), dm.p, hm.size() * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+            return eng->hipfail(e, "download match");
+    }
+    if (err_bits || codes) {
+        he.resize((size_t)W * n);
+        if ((e = hipMemcpyAsync(he.data(), de.p, he.size() * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+            return eng->hipfail(e, "download err");
+    }
+    if (values && (e = hipMemcpyAsync(values, dv.p, (size_t)n * R * 8, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download values");
+    uint32_t cnt = 0;
+    if ((e = hipMemcpyAsync(&cnt, eng->d_errcount.p, 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download errcount");
+    if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "eval sync");
+    eng->last_error_count = cnt;
+    eng->last_errors.clear();
+    uint32_t kept = std::min(cnt, eng->errcap);
+    if (kept) {
+        std::vector<mxp_err_rec> recs(kept);
+        if ((e = hipMemcpy(recs.data(), eng->d_errlog.p, kept * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
+            return eng->hipfail(e, "download errlog");
+        for (auto& r : recs)
+            eng->last_errors[((uint64_t)r.req << 32) | r.rule] = {r.code, eng->format_error(batch, db.get(), r)};
+    }
+    eng->last_db = std::move(db);
+    if (match_bits) memcpy(match_bits, hm.data(), hm.size() * 4);
+    if (err_bits) memcpy(err_bits, he.data(), he.size() * 4);
+    if (codes) {
+        for (uint32_t q = 0; q < n; q++)
+            for (uint32_t r = 0; r < R; r++) {
+                size_t w = (size_t)(r / 32) * n + q;
+                uint32_t bit = 1u << (r % 32);
+                uint8_t c = (hm[w] & bit) ? PC_TRUE : PC_FALSE;
+                if (he[w] & bit) {
+                    auto it = eng->last_errors.find(((uint64_t)q << 32) | r);
+                    c = (it != eng->last_errors.end() && it->second.first >= 32) ? PC_PANIC : PC_ERROR;
+                }
+                codes[(size_t)q * R + r] = c;
+            }
+    }
+    return MXP_OK;
+}
+
+int mxp_eval_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* match_bits, uint32_t* err_bits) {
+    return eval_common(eng, batch, match_bits, err_bits, nullptr, nullptr);
+}
+
+int mxp_eval_values(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* values, uint8_t* codes) {
+    return eval_common(eng, batch, nullptr, nullptr, values, codes);
+}
+
+int mxp_pair_error(mxp_engine* eng, uint32_t request, uint32_t rule, char* buf, uint32_t cap) {
+    if (!eng) return MXP_ERR_ARG;
+    auto it = eng->last_errors.find(((uint64_t)request << 32) | rule);
+    if (it == eng->last_errors.end()) return put_text("", buf, cap);
+    int rc = put_text(it->second.second, buf, cap);
+    return rc ? rc : (it->second.first >= 32 ? 1 : 0);
+}
+
+uint64_t mxp_error_count(mxp_engine* eng) { return eng ? eng->last_error_count : 0; }
+
+int mxp_value_kind(mxp_engine* eng, uint32_t rule, uint64_t v) {
+    if (!eng || rule >= eng->rules.size()) return -1;
+    switch (eng->rules[rule].il_ret) {
+    case mxp::IL_STRING: return MXP_STRING;
+    case mxp::IL_BOOL: return MXP_BOOL;
+    case mxp::IL_INTEGER: return MXP_INT64;
+    case mxp::IL_DURATION: return MXP_DURATION;
+    case mxp::IL_DOUBLE: return MXP_DOUBLE;
+    default: return (int)MXP_FH_KIND(v);
+    }
+}
+
+int mxp_value_text(mxp_engine* eng, uint32_t rule, uint64_t v, char* buf, uint32_t cap) {
+    if (!eng || rule >= eng->rules.size()) return MXP_ERR_ARG;
+    std::string s;
+    int k = mxp_value_kind(eng, rule, v);
+    uint64_t id = (eng->rules[rule].il_ret == mxp::IL_INTERFACE) ? MXP_FH_ID(v) : v;
+    switch (k) {
+    case MXP_STRING: s = eng->string_of(nullptr, id); break;
+    case MXP_BOOL: s = v ? "true" : "false"; break;
+    case MXP_INT64: s = std::to_string((int64_t)v); break;
+    case MXP_DURATION: s = mxp::go_format_duration((int64_t)v); break;
+    case MXP_DOUBLE: {
+        double d;
+        memcpy(&d, &v, 8);
+        s = mxp::go_format_float(d);
+        break;
+    }
+    case MXP_BYTES: {
+        std::string c;
+        if (id < eng->gbytes.size()) c = eng->gbytes[id];
+        else if (eng->last_db && id - eng->gbytes.size() < eng->last_db->overlay_bytes.size())
+            c = eng->last_db->overlay_bytes[id - eng->gbytes.size()];
+        s = mxp::go_format_bytes((const uint8_t*)c.data(), c.size());
+        break;
+    }
+    case MXP_TIMESTAMP: {
+        TimeKey t{0, 0};
+        if (id < eng->gtimes.size()) t = eng->gtimes[id];
+        else if (eng->last_db && id - eng->gtimes.size() < eng->last_db->overlay_times.size())
+            t = eng->last_db->overlay_times[id - eng->gtimes.size()];
+        s = mxp::go_format_time_utc(t.s, t.ns);
+        break;
+    }
+    default: s = "?"; break;
+    }
+    return put_text(s, buf, cap);
+}
+
+}  // extern "C"

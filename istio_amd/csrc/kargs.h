@@ -1,0 +1,42 @@
+// kargs.h -- argument block of the evaluation kernel (passed by value, lives in the kernarg segment).
+#pragma once
+
+#include <stdint.h>
+
+#include "vm.h"
+
+typedef struct mxp_kargs {
+    // rule set (uploaded once per config snapshot)
+    const mxp_vm_ins* prog;      // all rules' programs, concatenated
+    const uint32_t* rule_off;    // [n_rules + 1]
+    uint32_t n_rules;
+    uint32_t n_words;            // ceil(n_rules / 32)
+    uint32_t groups_per_wave;
+    uint32_t n;                  // requests in the batch
+    // columns: [n_cols][n] kinds / values (resolve columns, then virtual map[key] columns)
+    const uint8_t* kinds;
+    const uint64_t* vals;
+    // interned strings: ids < n_gstr live in the rule set's pool, the rest in the batch pool
+    uint64_t n_gstr;
+    const uint64_t* gstr_off;
+    const uint8_t* gstr;
+    const uint64_t* bstr_off;
+    const uint8_t* bstr;
+    uint32_t empty_sid;
+    uint32_t pad0;
+    // per-request string maps (CSR over batch map ids)
+    const uint32_t* map_off;
+    const uint32_t* map_keys;
+    const uint32_t* map_vals;
+    // per-string pre-tables (ip(), timestamp()); ~0 = conversion error
+    const uint64_t* ipof;
+    const uint64_t* tsof;
+    // outputs
+    uint32_t* out_match;         // [n_words][n]
+    uint32_t* out_err;           // [n_words][n]
+    uint64_t* out_vals;          // optional [n][n_rules] result registers (Eval)
+    mxp_err_rec* errlog;
+    uint32_t* errcount;
+    uint32_t errcap;
+    uint32_t pad1;
+} mxp_kargs;

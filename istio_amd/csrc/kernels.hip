@@ -1,0 +1,347 @@
+// kernels.hip -- gfx950 kernels of the MXP predicate engine.
+//
+// mxp_eval_kernel: the batched replacement of the reference's per-(bag, rule) evaluation loop
+//   resolver.filterActions (mixer/pkg/runtime/resolver.go:202-238)
+//     -> evaluator.IL.EvalPredicate (mixer/pkg/il/evaluator/evaluator.go:75)
+//       -> interpreter.run (mixer/pkg/il/interpreter/interpreterRun.go:18-1163)
+// executed as a wave-uniform bytecode VM (vm.h):
+//   * a workgroup owns a tile of 64 requests (one per lane) and its 4 wavefronts sweep disjoint
+//     32-rule groups, so every wave runs ONE rule's program at a time: the opcode stream is scalar
+//     (s_load_dwordx4 per step) and only operand data is per-lane;
+//   * short-circuit jumps are forward-only: a lane that jumps parks with a wait target, and the
+//     wave skips straight to min(wait) once no lane is live;
+//   * the reference's stack slots live in an LDS register file regs[reg][thread] (8-byte stride per
+//     lane -> conflict-free ds_read_b64 / ds_write_b64);
+//   * results are accumulated per lane into 32-rule words and written rule-word-major
+//     (out[word * N + request]) so every store is a coalesced 256-byte wave store.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mxp_batch.h"
+#include "kargs.h"
+#include "vm.h"
+
+namespace {
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
+    return uni(v);
+}
+
+struct StrRef {
+    const uint8_t* p;
+    uint32_t n;
+};
+
+__device__ __forceinline__ StrRef str_of(const mxp_kargs& A, uint64_t id) {
+    StrRef r;
+    if (id < A.n_gstr) {
+        uint64_t a = A.gstr_off[id], b = A.gstr_off[id + 1];
+        r.p = A.gstr + a;
+        r.n = (uint32_t)(b - a);
+    } else {
+        uint64_t j = id - A.n_gstr;
+        uint64_t a = A.bstr_off[j], b = A.bstr_off[j + 1];
+        r.p = A.bstr + a;
+        r.n = (uint32_t)(b - a);
+    }
+    return r;
+}
+
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++)
+        if (a[i] != b[i]) return false;
+    return true;
+}
+
+// match / startsWith / endsWith (mixer/pkg/il/runtime/externs.go:108-128)
+__device__ bool strfn(uint32_t fn, StrRef s, StrRef p) {
+    if (fn == SF_STARTS) return s.n >= p.n && bytes_eq(s.p, p.p, p.n);
+    if (fn == SF_ENDS) return s.n >= p.n && bytes_eq(s.p + (s.n - p.n), p.p, p.n);
+    // SF_MATCH: trailing '*' -> prefix, else leading '*' -> suffix, else equality
+    if (p.n > 0 && p.p[p.n - 1] == '*') return s.n >= p.n - 1 && bytes_eq(s.p, p.p, p.n - 1);
+    if (p.n > 0 && p.p[0] == '*') return s.n >= p.n - 1 && bytes_eq(s.p + (s.n - (p.n - 1)), p.p + 1, p.n - 1);
+    return s.n == p.n && bytes_eq(s.p, p.p, p.n);
+}
+
+__device__ __forceinline__ void log_err(const mxp_kargs& A, uint32_t req, uint32_t rule, uint32_t code, uint32_t aux) {
+    if (!A.errlog) return;
+    uint32_t slot = atomicAdd(A.errcount, 1u);
+    if (slot < A.errcap) {
+        mxp_err_rec r;
+        r.req = req;
+        r.rule = rule;
+        r.code = code;
+        r.aux = aux;
+        A.errlog[slot] = r;
+    }
+}
+
+// Runs one rule for the 64 requests of this wave; returns the lane's pair code (mxp_pair_code).
+__device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bool valid,
+                             uint64_t (*regs)[256], uint32_t tid) {
+    const uint32_t base = uni(A.rule_off[rule]);
+    const uint32_t len = uni(A.rule_off[rule + 1]) - base;
+    const uint4* prog = reinterpret_cast<const uint4*>(A.prog) + base;
+    const uint64_t N = A.n;
+    bool live = valid;
+    uint32_t wait = valid ? 0u : MXP_VM_DONE;
+    uint32_t res = PC_FALSE;
+    uint32_t pc = 0;
+
+#define FAIL(code_, aux_)                                   \
+    do {                                                    \
+        res = ((code_) >= 32u) ? PC_PANIC : PC_ERROR;       \
+        log_err(A, req, rule, (code_), (aux_));             \
+        live = false;                                       \
+        wait = MXP_VM_DONE;                                 \
+    } while (0)
+#define JUMP(t_)             \
+    do {                     \
+        live = false;        \
+        wait = (t_);         \
+    } while (0)
+
+    while (pc < len) {
+        const uint4 w = prog[pc];
+        const uint32_t w0 = uni(w.x);
+        const uint32_t x = uni(w.y), y = uni(w.z), z = uni(w.w);
+        const uint32_t op = w0 & 0x7Fu;
+        const uint32_t d = (w0 >> 8) & 0xFFu, a = (w0 >> 16) & 0xFFu, b = w0 >> 24;
+        if (w0 & MXP_VM_WAKE) live = live || (wait == pc);
+        if (__ballot(live) == 0) {
+            pc = wave_min(wait);
+            if (pc == MXP_VM_DONE) break;
+            continue;
+        }
+        switch (op) {
+        case VM_RES:
+        case VM_TRES: {
+            if (live) {
+                const uint64_t at = (uint64_t)x * N + req;
+                const uint32_t k = A.kinds[at];
+                uint64_t v = A.vals[at];
+                bool ok;
+                switch (y) {
+                case W_S: ok = k == MXP_STRING; break;
+                case W_B: ok = k == MXP_BOOL; break;
+                case W_I: ok = k == MXP_INT64 || k == MXP_DURATION; break;
+                case W_D: ok = k == MXP_DOUBLE; break;
+                default: ok = k != MXP_ABSENT; v = MXP_FH(k, v); break;
+                }
+                if (k == MXP_ABSENT) {
+                    if (op == VM_RES) FAIL(ERR_LOOKUP, z);
+                } else if (!ok) {
+                    FAIL(ERR_CONV_S + y, x);
+                } else {
+                    regs[d][tid] = v;
+                    if (op == VM_TRES) JUMP(z);
+                }
+            }
+            break;
+        }
+        case VM_VCOL: {
+            if (live) {
+                const uint64_t at = (uint64_t)x * N + req;
+                const uint32_t k = A.kinds[at];
+                if (k == VC_VALUE) regs[d][tid] = A.vals[at];
+                else if (k == VC_ABSENT) FAIL(ERR_LOOKUP, z);
+                else FAIL(PANIC_MAPTYPE, 0);
+            }
+            break;
+        }
+        case VM_CONST:
+            if (live) regs[d][tid] = (uint64_t)y | ((uint64_t)z << 32);
+            break;
+        case VM_EQ:
+            if (live) regs[d][tid] = regs[a][tid] == regs[b][tid] ? 1u : 0u;
+            break;
+        case VM_EQK:
+            if (live) regs[d][tid] = regs[a][tid] == ((uint64_t)y | ((uint64_t)z << 32)) ? 1u : 0u;
+            break;
+        case VM_NOT:
+            if (live) regs[d][tid] = regs[a][tid] == 0 ? 1u : 0u;
+            break;
+        case VM_LOGIC:
+        case VM_LOGICK:
+            if (live) {
+                const uint64_t p = regs[a][tid];
+                const uint64_t q = op == VM_LOGIC ? regs[b][tid] : (uint64_t)x;
+                // interpreterRun.go:352-443 operate on u32 words
+                const bool pb = (uint32_t)p != 0, qb = (uint32_t)q != 0;
+                regs[d][tid] = (y == 0 ? (pb && qb) : y == 1 ? (pb || qb) : (pb != qb)) ? 1u : 0u;
+            }
+            break;
+        case VM_JZ:
+            if (live && (uint32_t)regs[a][tid] == 0) JUMP(z);
+            break;
+        case VM_JNZ:
+            if (live && (uint32_t)regs[a][tid] != 0) JUMP(z);
+            break;
+        case VM_JMP:
+            if (live) JUMP(z);
+            break;
+        case VM_RET:
+            if (live) {
+                const uint64_t v = regs[a][tid];
+                if (A.out_vals) A.out_vals[(uint64_t)req * A.n_rules + rule] = v;
+                if (y == 1) {
+                    res = (uint32_t)v != 0 ? PC_TRUE : PC_FALSE;
+                } else if (A.out_vals) {
+                    res = PC_FALSE;  // Eval: a non-bool result is just a value
+                } else {
+                    res = PC_PANIC;  // EvalPredicate: Result.AsBool panics (result.go:42-52)
+                    log_err(A, req, rule, PANIC_NOTBOOL, 0);
+                }
+                live = false;
+                wait = MXP_VM_DONE;
+            }
+            break;
+        case VM_LOOKUP:
+        case VM_LOOKUPK:
+            if (live) {
+                const uint64_t h = regs[a][tid];
+                const uint32_t key = op == VM_LOOKUP ? (uint32_t)regs[b][tid] : x;
+                if (MXP_FH_KIND(h) != MXP_STRING_MAP) {
+                    FAIL(PANIC_MAPTYPE, 0);
+                } else {
+                    const uint32_t m = (uint32_t)MXP_FH_ID(h);
+                    const uint32_t e0 = A.map_off[m], e1 = A.map_off[m + 1];
+                    uint32_t found = MXP_VM_DONE;
+                    for (uint32_t e = e0; e < e1; e++)
+                        if (A.map_keys[e] == key) {
+                            found = A.map_vals[e];
+                            break;
+                        }
+                    if (found != MXP_VM_DONE) {
+                        regs[d][tid] = found;
+                        if (y == LK_TRY) JUMP(z);
+                    } else if (y == LK_N) {
+                        regs[d][tid] = A.empty_sid;
+                    } else if (y == LK_ERR) {
+                        FAIL(ERR_MEMBER, key);
+                    }
+                }
+            }
+            break;
+        case VM_STRFN:
+        case VM_STRFNK:
+            if (live) {
+                const StrRef s = str_of(A, regs[a][tid]);
+                const StrRef p = str_of(A, op == VM_STRFN ? regs[b][tid] : (uint64_t)x);
+                regs[d][tid] = strfn(y, s, p) ? 1u : 0u;
+            }
+            break;
+        case VM_IPOF:
+        case VM_TSOF:
+            if (live) {
+                const uint64_t sid = regs[a][tid];
+                const uint64_t h = (op == VM_IPOF ? A.ipof : A.tsof)[sid];
+                if (h == ~0ull) FAIL(op == VM_IPOF ? ERR_IP : ERR_TS, (uint32_t)sid);
+                else regs[d][tid] = h;
+            }
+            break;
+        case VM_IPEQ:
+        case VM_TSEQ:
+            if (live) {
+                const uint64_t p = regs[a][tid], q = regs[b][tid];
+                const uint32_t want = op == VM_IPEQ ? MXP_BYTES : MXP_TIMESTAMP;
+                if (MXP_FH_KIND(p) != want || MXP_FH_KIND(q) != want) FAIL(PANIC_EXTARG, 0);
+                else regs[d][tid] = MXP_FH_ID(p) == MXP_FH_ID(q) ? 1u : 0u;
+            }
+            break;
+        case VM_ERR:
+            if (live) FAIL(y, z);
+            break;
+        case VM_FTOS:
+            if (live) {
+                const uint64_t h = regs[a][tid];
+                if (MXP_FH_KIND(h) != MXP_STRING) FAIL(PANIC_CONV, 0);
+                else regs[d][tid] = MXP_FH_ID(h);
+            }
+            break;
+        case VM_STOF:
+            if (live) regs[d][tid] = MXP_FH(MXP_STRING, regs[a][tid]);
+            break;
+        default:
+            break;
+        }
+        pc++;
+    }
+#undef FAIL
+#undef JUMP
+    return res;
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t wave = uni(tid >> 6);
+    const uint32_t req = blockIdx.x * 64u + (tid & 63u);
+    const bool valid = req < A.n;
+    const uint32_t g0 = (blockIdx.y * 4u + wave) * A.groups_per_wave;
+    const uint32_t g1 = min(g0 + A.groups_per_wave, A.n_words);
+    for (uint32_t g = g0; g < g1; g++) {
+        uint32_t m = 0, e = 0;
+        const uint32_t r0 = g * 32u, r1 = min(r0 + 32u, A.n_rules);
+        for (uint32_t rule = r0; rule < r1; rule++) {
+            const uint32_t code = run_rule(A, rule, req, valid, regs, tid);
+            m |= (code == PC_TRUE ? 1u : 0u) << (rule - r0);
+            e |= (code >= PC_ERROR ? 1u : 0u) << (rule - r0);
+        }
+        if (valid) {
+            A.out_match[(uint64_t)g * A.n + req] = m;
+            A.out_err[(uint64_t)g * A.n + req] = e;
+        }
+    }
+}
+
+// Per-rule hit counters: hits[rule] += popcount over requests of the rule's match bit, restricted
+// to requests flagged in `mask` (nullptr = all).  One block per 32-rule word; each thread keeps 32
+// counters in registers, then a block reduction and one atomic per rule.
+extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t* __restrict__ match, uint32_t n,
+                                                                  uint32_t n_rules,
+                                                                  unsigned long long* __restrict__ hits) {
+    const uint32_t w = blockIdx.x;
+    uint32_t cnt[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) cnt[k] = 0;
+    const uint32_t* row = match + (uint64_t)w * n;
+    for (uint32_t r = blockIdx.y * blockDim.x + threadIdx.x; r < n; r += gridDim.y * blockDim.x) {
+        const uint32_t v = row[r];
+#pragma unroll
+        for (int k = 0; k < 32; k++) cnt[k] += (v >> k) & 1u;
+    }
+    __shared__ uint32_t red[32][8];
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+        uint32_t c = cnt[k];
+        for (int off = 32; off > 0; off >>= 1) c += __shfl_xor((int)c, off, 64);
+        if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = c;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        uint32_t c = 0;
+        for (uint32_t i = 0; i < blockDim.x / 64; i++) c += red[threadIdx.x][i];
+        const uint32_t rule = w * 32 + threadIdx.x;
+        if (rule < n_rules && c) atomicAdd(&hits[rule], (unsigned long long)c);
+    }
+}
+
+extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
+                                      unsigned long long* hits, hipStream_t s) {
+    const uint32_t per = (n + 255) / 256;
+    const uint32_t gy = per < 64 ? per : 64;
+    hipLaunchKernelGGL(mxp_hits_kernel, dim3(n_words, gy > 0 ? gy : 1), dim3(256), 0, s, match, n, n_rules, hits);
+    return hipGetLastError();
+}

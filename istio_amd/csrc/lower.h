@@ -1,0 +1,48 @@
+// lower.h -- reference IL -> MXP VM bytecode (vm.h).
+//
+// The lowering abstract-interprets the IL of `compile_rule` over a typed value stack.  It accepts a
+// program when, at every instruction, all paths reaching it agree on the stack shape (so each
+// stack slot maps to one fixed register), all jumps go forward, and the reference's stack (64
+// words) and heap (63 allocations, interpreterRun.go:171-172) provably cannot overflow -- then the
+// reference's overflow/underflow/invalid-heap checks can never fire and the VM needs none of them.
+// Everything the reference compiler emits for real rules satisfies this; programs that don't are
+// reported (LoweredRule::ok == false) instead of being approximated.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "ilgen.h"
+#include "vm.h"
+
+namespace mxp {
+
+// Engine-global tables the lowering interns constants and columns into.
+class LowerTables {
+  public:
+    virtual ~LowerTables() = default;
+    virtual uint32_t intern_string(const std::string& s) = 0;     // global string id
+    virtual uint32_t intern_bytes(const std::string& canon) = 0;  // bytes id (canonical IP form)
+    virtual uint32_t intern_time(int64_t sec, int32_t nsec) = 0;  // time id
+    virtual uint32_t column(const std::string& attr) = 0;         // resolve column index
+    virtual uint32_t vcolumn(const std::string& attr, const std::string& key) = 0;  // map[key] column
+    virtual int32_t attr_type(const std::string& attr) = 0;       // manifest ValueType (-1 unknown)
+};
+
+struct LoweredRule {
+    bool ok = false;
+    std::string why;              // reason when !ok
+    std::vector<mxp_vm_ins> code;
+    uint32_t nregs = 0;
+    bool uses_ipof = false;
+    bool uses_tsof = false;
+    bool uses_strings = false;    // needs string bytes on device (dynamic string functions)
+    bool uses_maps = false;       // needs per-request map storage on device
+};
+
+LoweredRule lower_rule(const IlProgram& prog, LowerTables* tables);
+
+std::string vm_disasm(const std::vector<mxp_vm_ins>& code);
+
+}  // namespace mxp

@@ -1,0 +1,105 @@
+// vm.h -- the engine's GPU predicate bytecode ("MXP VM"), shared by the host lowering (lower.cpp)
+// and the gfx950 kernels (kernels.hip).
+//
+// A rule's reference IL (mixer/pkg/il, produced by compile_rule) is lowered to a flat, wave-uniform
+// program: every stack slot of the reference VM (interpreterRun.go, 64 x u32 words) becomes a
+// statically numbered 64-bit register, `tresolve_x; jnz` / `tlookup; jnz` pairs fuse into one op,
+// `resolve_f m; anlookup "k"` fuses into a virtual-column load, constant `ip("...")` /
+// `timestamp("...")` / string-pattern externs fold or specialise.  One wavefront runs one rule over
+// 64 requests (one request per lane); jumps are forward-only and become per-lane wait targets.
+#pragma once
+
+#include <stdint.h>
+
+#define MXP_VM_MAXREG 8      // registers (reference stack slots) per rule
+#define MXP_VM_WAKE 0x80u    // op flag: some jump lands on this instruction
+#define MXP_VM_DONE 0xFFFFFFFFu
+
+enum mxp_vm_op {
+    VM_NOP = 0,
+    VM_RES = 1,      // d <- column x (want class y); missing -> ERR_LOOKUP(z = attr id), wrong kind -> ERR_CONV
+    VM_TRES = 2,     // tresolve+jnz: present -> d <- column x, jump z; absent -> fall through
+    VM_VCOL = 3,     // d <- virtual column x (map attr [const key]); z = attr id
+    VM_CONST = 4,    // d <- y | z << 32
+    VM_EQ = 5,       // d <- r[a] == r[b]
+    VM_EQK = 6,      // d <- r[a] == (y | z << 32)
+    VM_NOT = 7,      // d <- r[a] == 0
+    VM_JZ = 8,       // r[a] == 0 -> jump z
+    VM_JNZ = 9,      // r[a] != 0 -> jump z
+    VM_JMP = 10,     // jump z
+    VM_RET = 11,     // result r[a]; y = 1 when the function returns bool (else EvalPredicate panics)
+    VM_LOOKUP = 12,  // map r[a], key r[b]; y = mode (LK_*); d <- value; z = jump target (LK_TRY)
+    VM_LOOKUPK = 13, // map r[a], key string x; y = mode; d <- value; z = jump target (LK_TRY)
+    VM_STRFN = 14,   // d <- fn y (SF_*) (r[a], r[b])
+    VM_STRFNK = 15,  // d <- fn y (r[a], const string x)        (x = pattern / prefix / suffix id)
+    VM_IPOF = 16,    // d <- ip(r[a])          (per-string pre-table; error if unparsable)
+    VM_TSOF = 17,    // d <- timestamp(r[a])   (per-string pre-table)
+    VM_IPEQ = 18,    // d <- ip_equal(r[a], r[b])
+    VM_TSEQ = 19,    // d <- timestamp_equal(r[a], r[b])
+    VM_ERR = 20,     // raise error y with aux z
+    VM_LOGIC = 21,   // d <- r[a] (y: 0 and, 1 or, 2 xor) r[b]
+    VM_LOGICK = 22,  // d <- r[a] (y) const x
+    VM_FTOS = 23,    // d <- r[a] as string: interface value must hold a string (Go `.(string)`), else panic
+    VM_STOF = 24,    // d <- interface handle of string r[a]
+};
+
+// want classes for VM_RES / VM_TRES
+enum mxp_vm_want { W_S = 0, W_B = 1, W_I = 2, W_D = 3, W_F = 4 };
+
+// lookup modes
+enum mxp_vm_lk { LK_N = 0 /* missing -> "" */, LK_TRY = 1 /* tlookup+jnz */, LK_ERR = 2 /* missing -> error */ };
+
+// string functions (mixer/pkg/il/runtime/externs.go:108-128)
+enum mxp_vm_sf { SF_MATCH = 0, SF_STARTS = 1, SF_ENDS = 2, SF_REGEX = 3 };
+
+// per-pair result codes
+enum mxp_pair_code { PC_FALSE = 0, PC_TRUE = 1, PC_ERROR = 2, PC_PANIC = 3 };
+
+// error / panic codes recorded for error pairs (host formats the reference's text)
+enum mxp_err_code {
+    ERR_NONE = 0,
+    ERR_LOOKUP = 1,      // "lookup failed: '%v'"                       aux = attr string id
+    ERR_CONV_S = 2,      // "error converting value to string: '%v'"   aux = column
+    ERR_CONV_B = 3,
+    ERR_CONV_I = 4,
+    ERR_CONV_D = 5,
+    ERR_IP = 6,          // "could not convert %s to IP_ADDRESS"        aux = string id
+    ERR_TS = 7,          // "could not convert '%s' to TIMESTAMP..."    aux = string id
+    ERR_MEMBER = 8,      // "member lookup failed: '%v'"               aux = key string id
+    ERR_REGEX = 9,       // regexp compile error                        aux = pattern string id
+    ERR_STATIC = 10,     // rule failed to compile: every evaluation errors   aux = rule
+    ERR_UNSUPPORTED = 11,// construct not lowered by this engine build   aux = rule
+    ERR_UNDERFLOW = 12,  // "stack underflow" (interpreterRun.go:1148) -- reachable from OR chains
+    PANIC_MAPTYPE = 32,  // il.MapGet on a non-map value ("Unknown map type")
+    PANIC_EXTARG = 33,   // reflect.Call with a wrong dynamic type (ip_equal / timestamp_equal)
+    PANIC_NOTBOOL = 34,  // Result.AsBool on a non-bool result
+    PANIC_STATIC = 35,   // compile-time panic in the reference
+    PANIC_CONV = 36,     // interface conversion: heap value is not a string
+};
+
+// 16-byte instruction; loaded with one scalar s_load_dwordx4 per step.
+typedef struct mxp_vm_ins {
+    uint8_t op;   // mxp_vm_op | MXP_VM_WAKE
+    uint8_t d;
+    uint8_t a;
+    uint8_t b;
+    uint32_t x;
+    uint32_t y;
+    uint32_t z;
+} mxp_vm_ins;
+
+// F-handle (interface{} register value): kind (mxp_kind) in bits 56..63, id in bits 0..55.
+#define MXP_FH(kind, id) ((((uint64_t)(kind)) << 56) | ((uint64_t)(id) & 0x00FFFFFFFFFFFFFFull))
+#define MXP_FH_KIND(h) ((uint32_t)((h) >> 56))
+#define MXP_FH_ID(h) ((h) & 0x00FFFFFFFFFFFFFFull)
+
+// virtual-column kinds (VM_VCOL)
+enum mxp_vcol_kind { VC_ABSENT = 0, VC_VALUE = 1, VC_NOTMAP = 3 };
+
+// error log record (one per error pair, capacity-bounded)
+typedef struct mxp_err_rec {
+    uint32_t req;
+    uint32_t rule;
+    uint32_t code;
+    uint32_t aux;
+} mxp_err_rec;

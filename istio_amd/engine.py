@@ -1,0 +1,317 @@
+"""Host mirror of the reference's evaluator / resolver interfaces over the C-ABI (include/mxp.h).
+
+`Evaluator` mirrors `expr.Evaluator` as implemented by `evaluator.IL`
+(mixer/pkg/expr/evaluator.go:25-31, mixer/pkg/il/evaluator/evaluator.go:36-200): `eval` /
+`eval_predicate` on an expression text and one bag, `change_vocabulary`.  `Engine` is the batched
+form the drop-in actually uses: compile a rule set once, then evaluate whole batches of bags on the
+GPU (`eval_batch` -> per-pair match / error bitmaps, `pair_error` -> the reference's error text).
+
+There is no CPU fallback: every evaluation runs the HIP kernels in libmxp.so, and loading fails
+loudly when the library (or a GPU) is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .bags import BagBatch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmxp.so")
+
+VALUE_TYPES = {"VALUE_TYPE_UNSPECIFIED": 0, "STRING": 1, "INT64": 2, "DOUBLE": 3, "BOOL": 4, "TIMESTAMP": 5,
+               "IP_ADDRESS": 6, "EMAIL_ADDRESS": 7, "URI": 8, "DNS_NAME": 9, "DURATION": 10, "STRING_MAP": 11}
+
+RULE_OK, RULE_PARSE_ERROR, RULE_TYPE_ERROR, RULE_COMPILE_ERROR, RULE_COMPILE_PANIC, RULE_UNSUPPORTED = range(6)
+FALSE, TRUE, ERROR, PANIC = 0, 1, 2, 3
+
+# every entry point declared in include/mxp.h: name -> (restype, argtypes)
+_VP = ctypes.c_void_p
+SIGNATURES = {
+    "mxp_engine_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_VP)]),
+    "mxp_engine_destroy": (None, [_VP]),
+    "mxp_last_error": (ctypes.c_char_p, [_VP]),
+    "mxp_vocab_set": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32]),
+    "mxp_ruleset_compile": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32)]),
+    "mxp_rule_error": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
+    "mxp_rule_il_text": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
+    "mxp_rule_vm_text": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
+    "mxp_rule_types": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
+    "mxp_eval_batch": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "mxp_eval_values": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "mxp_value_text": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint32]),
+    "mxp_value_kind": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint64]),
+    "mxp_pair_error": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
+    "mxp_error_count": (ctypes.c_uint64, [_VP]),
+    "mxp_batch_upload": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP)]),
+    "mxp_batch_free": (None, [_VP, _VP]),
+    "mxp_batch_eval_device": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
+    "mxp_hits_device": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP]),
+    "mxp_rule_count": (ctypes.c_uint32, [_VP]),
+    "mxp_dbatch_requests": (ctypes.c_uint32, [_VP]),
+}
+
+_LIB = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libmxp.so (built by istio_amd.build); raises if it is missing."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(path):
+            raise RuntimeError("libmxp.so not built: run `python -m istio_amd.build` (no CPU fallback exists)")
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7; load it first so
+        # libmxp binds to the same runtime (device pointers and streams are shared with torch).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = lib
+    return _LIB
+
+
+class MxpError(RuntimeError):
+    pass
+
+
+class Engine:
+    """One GPU (or a host-only compiler when device=-1) + one rule set."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = _VP()
+        rc = self.lib.mxp_engine_create(device, ctypes.byref(h))
+        if rc != 0:
+            raise MxpError("mxp_engine_create(%d) failed with %d" % (device, rc))
+        self.h = h
+        self.device = device
+        self.rules: List[str] = []
+        self.status = np.zeros(0, dtype=np.int32)
+
+    def close(self):
+        if self.h:
+            self.lib.mxp_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise MxpError("%s failed (%d): %s" % (what, rc, self.lib.mxp_last_error(self.h).decode(errors="replace")))
+
+    # ------------------------------------------------------------------ configuration
+    def set_vocabulary(self, manifest: Dict[str, object]):
+        """ChangeVocabulary (evaluator.go:107): manifest name -> ValueType (name or enum value)."""
+        names = list(manifest)
+        types = [VALUE_TYPES[v] if isinstance(v, str) else int(v) for v in manifest.values()]
+        arr = (ctypes.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+        tarr = (ctypes.c_int32 * max(len(types), 1))(*types)
+        self._check(self.lib.mxp_vocab_set(self.h, arr, tarr, len(names)), "mxp_vocab_set")
+        self.rules = []
+
+    def compile(self, rules: Sequence[str]) -> np.ndarray:
+        """Compile + upload a rule set; returns per-rule status (RULE_*)."""
+        self.rules = list(rules)
+        enc = [r.encode("utf-8", "surrogateescape") for r in self.rules]
+        arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+        st = np.zeros(len(enc), dtype=np.int32)
+        self._check(self.lib.mxp_ruleset_compile(self.h, arr, len(enc), st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))),
+                    "mxp_ruleset_compile")
+        self.status = st
+        return st
+
+    def _text(self, fn, rule, cap=1 << 16):
+        buf = ctypes.create_string_buffer(cap)
+        self._check(fn(self.h, rule, buf, cap), fn.__name__)
+        return buf.value.decode("utf-8", "surrogateescape")
+
+    def rule_error(self, rule: int) -> str:
+        return self._text(self.lib.mxp_rule_error, rule)
+
+    def rule_il_text(self, rule: int) -> str:
+        return self._text(self.lib.mxp_rule_il_text, rule)
+
+    def rule_vm_text(self, rule: int) -> str:
+        return self._text(self.lib.mxp_rule_vm_text, rule)
+
+    def rule_types(self, rule: int):
+        vt, il = ctypes.c_int32(), ctypes.c_int32()
+        self._check(self.lib.mxp_rule_types(self.h, rule, ctypes.byref(vt), ctypes.byref(il)), "mxp_rule_types")
+        return vt.value, il.value
+
+    # ------------------------------------------------------------------ evaluation
+    def eval_batch(self, batch: BagBatch):
+        """-> (match, err) uint32 bitmaps, rule-word-major [(R+31)//32, N]."""
+        W = (len(self.rules) + 31) // 32
+        match = np.zeros((W, batch.n), dtype=np.uint32)
+        err = np.zeros((W, batch.n), dtype=np.uint32)
+        self._check(self.lib.mxp_eval_batch(self.h, ctypes.byref(batch.c_struct()), match.ctypes.data, err.ctypes.data),
+                    "mxp_eval_batch")
+        return match, err
+
+    def eval_codes(self, batch: BagBatch) -> np.ndarray:
+        """Per-pair codes [N, R] (FALSE/TRUE/ERROR/PANIC) via eval_values."""
+        _, codes = self.eval_values(batch)
+        return codes
+
+    def eval_values(self, batch: BagBatch):
+        R = len(self.rules)
+        vals = np.zeros((batch.n, R), dtype=np.uint64)
+        codes = np.zeros((batch.n, R), dtype=np.uint8)
+        self._check(self.lib.mxp_eval_values(self.h, ctypes.byref(batch.c_struct()), vals.ctypes.data, codes.ctypes.data),
+                    "mxp_eval_values")
+        return vals, codes
+
+    def value_text(self, rule: int, value: int) -> str:
+        buf = ctypes.create_string_buffer(1 << 16)
+        self._check(self.lib.mxp_value_text(self.h, rule, int(value), buf, 1 << 16), "mxp_value_text")
+        return buf.value.decode("utf-8", "surrogateescape")
+
+    def value_kind(self, rule: int, value: int) -> int:
+        return self.lib.mxp_value_kind(self.h, rule, int(value))
+
+    def pair_error(self, request: int, rule: int) -> str:
+        buf = ctypes.create_string_buffer(1 << 12)
+        rc = self.lib.mxp_pair_error(self.h, request, rule, buf, 1 << 12)
+        if rc not in (0, 1):
+            self._check(rc, "mxp_pair_error")
+        return buf.value.decode("utf-8", "surrogateescape")
+
+    def error_count(self) -> int:
+        return int(self.lib.mxp_error_count(self.h))
+
+    # ------------------------------------------------------------------ device-resident batches
+    def upload(self, batch: BagBatch) -> "DeviceBatch":
+        h = _VP()
+        self._check(self.lib.mxp_batch_upload(self.h, ctypes.byref(batch.c_struct()), ctypes.byref(h)), "mxp_batch_upload")
+        return DeviceBatch(self, h, batch.n)
+
+
+class DeviceBatch:
+    def __init__(self, engine: Engine, h, n: int):
+        self.engine = engine
+        self.h = h
+        self.n = n
+
+    def eval(self, d_match: int, d_err: int, stream: int = 0):
+        """Enqueue one evaluation writing device bitmaps (raw device pointers as ints)."""
+        e = self.engine
+        e._check(e.lib.mxp_batch_eval_device(e.h, self.h, _VP(stream or None), _VP(d_match), _VP(d_err)),
+                 "mxp_batch_eval_device")
+
+    def free(self):
+        if self.h:
+            self.engine.lib.mxp_batch_free(self.engine.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def bits_to_codes(match: np.ndarray, err: np.ndarray, n_rules: int) -> np.ndarray:
+    """Unpack rule-word-major bitmaps into [N, R] codes (error and panic both -> ERROR)."""
+    W, n = match.shape
+    shifts = np.arange(32, dtype=np.uint32)
+    m = ((match.T[:, :, None] >> shifts) & 1).reshape(n, W * 32)[:, :n_rules]
+    e = ((err.T[:, :, None] >> shifts) & 1).reshape(n, W * 32)[:, :n_rules]
+    return np.where(e != 0, ERROR, m).astype(np.uint8)
+
+
+class Evaluator:
+    """expr.Evaluator (mixer/pkg/expr/evaluator.go:25-31) for single bags, on the GPU engine.
+
+    Every distinct expression is compiled once (like evaluator.IL's cache, but unbounded) into a
+    one-rule engine; each call evaluates one bag."""
+
+    def __init__(self, manifest: Dict[str, object], device: int = 0):
+        self.manifest = dict(manifest)
+        self.device = device
+        self._engines: Dict[str, Engine] = {}
+
+    def change_vocabulary(self, manifest: Dict[str, object]):
+        self.manifest = dict(manifest)
+        self._engines.clear()
+
+    def _engine(self, text: str) -> Engine:
+        e = self._engines.get(text)
+        if e is None:
+            e = Engine(self.device)
+            e.set_vocabulary(self.manifest)
+            e.compile([text])
+            self._engines[text] = e
+        return e
+
+    def eval(self, text: str, bag: dict):
+        """-> ('ok', python value) | ('error', msg) | ('panic', msg)."""
+        e = self._engine(text)
+        st = int(e.status[0])
+        if st not in (RULE_OK,):
+            return ("panic" if st == RULE_COMPILE_PANIC else "error"), e.rule_error(0)
+        b = BagBatch.from_bags([bag])
+        vals, codes = e.eval_values(b)
+        c = int(codes[0, 0])
+        if c in (ERROR, PANIC):
+            msg = e.pair_error(0, 0)
+            if c == PANIC and msg == "interpreter.Result: result is not bool":
+                c = FALSE  # Eval (not EvalPredicate): a non-bool result is a value
+            else:
+                return ("panic" if c == PANIC else "error"), msg
+        return "ok", decode_value(e, 0, int(vals[0, 0]))
+
+    def eval_predicate(self, text: str, bag: dict):
+        e = self._engine(text)
+        st = int(e.status[0])
+        if st != RULE_OK:
+            return ("panic" if st == RULE_COMPILE_PANIC else "error"), e.rule_error(0)
+        b = BagBatch.from_bags([bag])
+        match, err = e.eval_batch(b)
+        if err[0, 0] & 1:
+            msg = e.pair_error(0, 0)
+            return ("panic" if msg in PANIC_TEXTS else "error"), msg
+        return "ok", bool(match[0, 0] & 1)
+
+
+PANIC_TEXTS = {"Unknown map type", "reflect: Call using a value of the wrong type",
+               "interpreter.Result: result is not bool", "interface conversion: interface {} is not string"}
+
+
+def decode_value(e: Engine, rule: int, v: int):
+    """Engine result register -> Python Go-model value (interpreter.Result.AsInterface)."""
+    from .bags import GoDuration, GoFloat64, GoInt64, GoTime
+    import struct
+    vt, il = e.rule_types(rule)
+    if il == 5:  # bool
+        return (v & 0xFFFFFFFF) != 0
+    if il == 3:
+        return GoInt64(v - (1 << 64) if v >> 63 else v)
+    if il == 6:
+        return GoDuration(v - (1 << 64) if v >> 63 else v)
+    if il == 4:
+        return GoFloat64(struct.unpack("<d", struct.pack("<Q", v))[0])
+    if il == 2:
+        return e.value_text(rule, v)
+    kind = e.value_kind(rule, v)
+    txt = e.value_text(rule, v)
+    if kind == 7:  # bytes "[1 2 3]"
+        inner = txt[1:-1].strip()
+        return bytes(int(x) for x in inner.split()) if inner else b""
+    if kind == 6:
+        return ("time", txt)
+    if kind == 1:
+        return txt
+    return txt

@@ -1,0 +1,283 @@
+"""Synthetic, seeded workloads for the Mixer Check predicate path (BASELINE.json configs).
+
+  C1 (seed 1)  Bookinfo / testdata Mixer rules + `true` rules over 10k bags.
+  C2 (seed 2)  `destination.service == ... && request.path.startsWith(...) && source.ip != ip(...)`
+               rules (1k in the config; the bench scales the same generator to 10k rules), 64k requests
+               with Zipf(1.1) services.
+  fuzz         random well- and ill-typed expressions over the reference's default test vocabulary
+               (mixer/pkg/il/testing/tests.go:2414-2489) and random bags with missing and wrongly-typed
+               values -- the parity stress test.
+
+All generation is numpy-seeded and deterministic.  The vocabulary of C1/C2 is the attribute manifest
+of mixer/testdata/config/attributes.yaml (names and value types only).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .bags import (ABSENT, BOOL, BYTES, DOUBLE, DURATION, INT64, STRING, STRING_MAP, TIMESTAMP, BagBatch,
+                   GoDuration, GoFloat64, GoInt64, GoOther, GoTime)
+
+# mixer/testdata/config/attributes.yaml
+TESTDATA_MANIFEST = {
+    "origin.ip": "IP_ADDRESS", "origin.uid": "STRING", "origin.user": "STRING", "request.headers": "STRING_MAP",
+    "request.id": "STRING", "request.host": "STRING", "request.method": "STRING", "request.path": "STRING",
+    "request.reason": "STRING", "request.referer": "STRING", "request.scheme": "STRING", "request.size": "INT64",
+    "request.time": "TIMESTAMP", "request.useragent": "STRING", "response.code": "INT64",
+    "response.duration": "DURATION", "response.headers": "STRING_MAP", "response.size": "INT64",
+    "response.time": "TIMESTAMP", "source.uid": "STRING", "source.user": "STRING", "target.uid": "STRING",
+    "destination.uid": "STRING", "connection.id": "STRING", "connection.received.bytes": "INT64",
+    "connection.received.bytes_total": "INT64", "connection.sent.bytes": "INT64",
+    "connection.sent.bytes_total": "INT64", "connection.duration": "DURATION", "context.protocol": "STRING",
+    "context.timestamp": "TIMESTAMP", "context.time": "TIMESTAMP", "api.service": "STRING",
+    "api.version": "STRING", "api.operation": "STRING", "api.protocol": "STRING",
+    "request.auth.principal": "STRING", "request.auth.audiences": "STRING", "request.auth.presenter": "STRING",
+    "request.api_key": "STRING", "source.ip": "IP_ADDRESS", "source.labels": "STRING_MAP",
+    "source.name": "STRING", "source.namespace": "STRING", "source.service": "STRING",
+    "source.serviceAccount": "STRING", "target.ip": "IP_ADDRESS", "target.labels": "STRING_MAP",
+    "target.name": "STRING", "target.namespace": "STRING", "target.service": "STRING",
+    "target.serviceAccount": "STRING", "destination.ip": "IP_ADDRESS", "destination.labels": "STRING_MAP",
+    "destination.name": "STRING", "destination.namespace": "STRING", "destination.service": "STRING",
+    "destination.serviceAccount": "STRING",
+}
+
+# mixer/pkg/il/testing/tests.go:2414-2489 (defaultAttrs)
+DEFAULT_TEST_MANIFEST = {
+    "ai": "INT64", "ab": "BOOL", "as": "STRING", "ad": "DOUBLE", "ar": "STRING_MAP", "adur": "DURATION",
+    "at": "TIMESTAMP", "aip": "IP_ADDRESS", "bi": "INT64", "bb": "BOOL", "bs": "STRING", "bd": "DOUBLE",
+    "br": "STRING_MAP", "bdur": "DURATION", "bt": "TIMESTAMP", "t1": "TIMESTAMP", "t2": "TIMESTAMP",
+    "bip": "IP_ADDRESS", "b1": "BOOL", "b2": "BOOL", "sm": "STRING_MAP",
+}
+
+# Bookinfo / testdata rule selectors
+BOOKINFO_RULES = [
+    'destination.labels["app"] == "ratings" && source.labels["app"]=="reviews" && source.labels["version"] == "v3"',
+    'destination.labels["app"] == "details" && source.user == "cluster.local/ns/default/sa/bookinfo-productpage"',
+    'request.headers["x-user"] == ""',
+    '(destination.labels["app"]|"unknown") == "ratings"',
+    'request.headers["clnt"] == "abc"',
+    'destination.service == "foo.default.svc.cluster.local" && source.ip != ip("10.11.12.13")',
+    'destination.service == "bar.default.svc.cluster.local" && source.user != "tcp-test-user"',
+    'context.protocol == "tcp"',
+]
+
+
+def _ip4(a, b, c, d):
+    return bytes([a, b, c, d])
+
+
+def c1_workload(n_bags=10000, seed=1, n_true_rules=8):
+    """Bookinfo rules (+ `true` rules) and n_bags bags with ~5% missing attributes."""
+    rng = np.random.default_rng(seed)
+    rules = list(BOOKINFO_RULES) + ["true"] * n_true_rules
+    apps = ["productpage", "details", "reviews", "ratings"]
+    versions = ["v1", "v2", "v3"]
+    users = ["cluster.local/ns/default/sa/bookinfo-productpage", "cluster.local/ns/default/sa/bookinfo-reviews",
+             "tcp-test-user", "alice", "bob"]
+    header_keys = ["x-user", "clnt", "user-agent", "accept", "x-request-id", "x-b3-traceid", "x-b3-spanid",
+                   "cookie", "host", "x-forwarded-for", "x-envoy-internal", "content-type", "authorization",
+                   "x-custom", "referer"]
+    bags = []
+    for i in range(n_bags):
+        b = {}
+        da, dv = apps[rng.integers(4)], versions[rng.integers(3)]
+        sa, sv = apps[rng.integers(4)], versions[rng.integers(3)]
+        svc = ["foo", "bar", da][rng.integers(3)]
+        b["destination.service"] = "%s.default.svc.cluster.local" % svc
+        b["destination.labels"] = {"app": da, "version": dv}
+        b["source.labels"] = {"app": sa, "version": sv}
+        b["source.user"] = users[rng.integers(len(users))]
+        hdr = {}
+        for k in header_keys:
+            if rng.random() < 0.6:
+                hdr[k] = ["", "abc", "jason", "xyz", "1"][rng.integers(5)]
+        b["request.headers"] = hdr
+        if rng.random() < 0.05:
+            b["source.ip"] = _ip4(10, 11, 12, 13)
+        else:
+            b["source.ip"] = _ip4(10, 0, int(rng.integers(256)), int(rng.integers(256)))
+        b["context.protocol"] = "tcp" if rng.random() < 0.2 else "http"
+        for k in list(b):
+            if rng.random() < 0.05:
+                del b[k]
+        bags.append(b)
+    return TESTDATA_MANIFEST, rules, BagBatch.from_bags(bags, names=sorted(
+        ["destination.service", "destination.labels", "source.labels", "source.user", "request.headers",
+         "source.ip", "context.protocol"]))
+
+
+def c2_rules(n_rules=1000, seed=2, n_services=256):
+    rng = np.random.default_rng(seed)
+    ips = rng.integers(0, 256, size=(n_rules, 3))
+    rules = []
+    for i in range(n_rules):
+        a, b, c = (int(x) for x in ips[i])
+        rules.append('destination.service == "svc%d.ns%d.svc.cluster.local" && request.path.startsWith("/api/v%d/r%d")'
+                     ' && source.ip != ip("10.%d.%d.%d")' % (i % n_services, (i % n_services) % 8, i % 7, i % 97, a, b, c))
+    return rules, ips
+
+
+def c2_workload(n_rules=1000, n_requests=65536, seed=2, n_services=256, p_missing_path=0.01, p_missing_ip=0.005):
+    """C2: ==/startsWith/ip() rules, Zipf(1.1) services.  Returns (manifest, rules, BagBatch)."""
+    rules, ips = c2_rules(n_rules, seed, n_services)
+    rng = np.random.default_rng(seed + 1000)
+    n = n_requests
+    ranks = np.arange(1, n_services + 1, dtype=np.float64)
+    p = ranks ** -1.1
+    p /= p.sum()
+    svc = rng.choice(n_services, size=n, p=p)
+    strings = [b"svc%d.ns%d.svc.cluster.local" % (s, s % 8) for s in range(n_services)]
+    dest_vals = svc.astype(np.uint64)
+    # request paths: half follow one of the service's own rules' prefixes
+    rules_per_svc = max(1, (n_rules + n_services - 1) // n_services)
+    follow = rng.random(n) < 0.5
+    j = rng.integers(0, rules_per_svc, size=n)
+    rule_i = svc + n_services * j
+    rule_i = np.where(rule_i < n_rules, rule_i, svc % max(n_rules, 1))
+    pv = np.where(follow, rule_i % 7, rng.integers(0, 7, size=n))
+    pr = np.where(follow, rule_i % 97, rng.integers(0, 97, size=n))
+    tail = rng.integers(0, 4096, size=n)
+    base = len(strings)
+    path_keys = (pv * 97 + pr) * 4096 + tail
+    uniq, inv = np.unique(path_keys, return_inverse=True)
+    for k in uniq:
+        k = int(k)
+        t = k % 4096
+        q = k // 4096
+        strings.append(b"/api/v%d/r%d/item%d" % (q // 97, q % 97, t))
+    path_vals = (base + inv).astype(np.uint64)
+    path_kinds = np.where(rng.random(n) < p_missing_path, ABSENT, STRING).astype(np.uint8)
+    # source.ip: 4-byte addresses in 10.0.0.0/8; 5% equal to one of the service's rules' ip
+    hit = rng.random(n) < 0.05
+    a = rng.integers(0, 256, size=n)
+    b = rng.integers(0, 256, size=n)
+    c = rng.integers(0, 256, size=n)
+    ri = np.where(rule_i < n_rules, rule_i, 0)
+    a = np.where(hit, ips[ri, 0], a)
+    b = np.where(hit, ips[ri, 1], b)
+    c = np.where(hit, ips[ri, 2], c)
+    ip_keys = (a * 256 + b) * 256 + c
+    iuniq, iinv = np.unique(ip_keys, return_inverse=True)
+    ibase = len(strings)
+    for k in iuniq:
+        k = int(k)
+        strings.append(bytes([10, (k >> 16) & 255, (k >> 8) & 255, k & 255]))
+    ip_vals = (ibase + iinv).astype(np.uint64)
+    ip_kinds = np.where(rng.random(n) < p_missing_ip, ABSENT, BYTES).astype(np.uint8)
+    cols = {
+        "destination.service": (np.full(n, STRING, dtype=np.uint8), dest_vals),
+        "request.path": (path_kinds, path_vals),
+        "source.ip": (ip_kinds, ip_vals),
+    }
+    return TESTDATA_MANIFEST, rules, BagBatch.from_columns(n, cols, strings)
+
+
+# ----------------------------------------------------------------------------------- fuzzing
+_STR_VALS = ["", "a", "abc", "abcd", "foo", "bar", "st.*", "str1", "1.2.3.4", "10.0.0.1", "::1",
+             "2015-01-02T15:04:35Z", "2015-01-02T15:04:35+01:00", "*", "a*", "*c", "19ms", "x-user"]
+_KEYS = ["a", "b", "c", "foo", "x-user"]
+
+
+class _Fuzz:
+    def __init__(self, rng):
+        self.r = rng
+
+    def pick(self, xs):
+        return xs[int(self.r.integers(len(xs)))]
+
+    def slit(self):
+        return '"%s"' % self.pick(_STR_VALS)
+
+    def sexpr(self, d):
+        r = self.r.random()
+        if d <= 0 or r < 0.35:
+            return self.pick(["as", "bs", self.slit()])
+        if r < 0.55:
+            return '%s[%s]' % (self.pick(["ar", "br", "sm"]), self.pick(['"%s"' % self.pick(_KEYS), "as"]))
+        if r < 0.75:
+            return '(%s | %s)' % (self.sexpr(d - 1), self.sexpr(d - 1))
+        return '(%s | %s)["%s"]' % (self.pick(["ar", "br"]), self.pick(["ar", "br", "sm"]), self.pick(_KEYS))
+
+    def atom(self, d):
+        r = self.r.random()
+        if r < 0.2:
+            return "%s == %s" % (self.sexpr(d), self.sexpr(d))
+        if r < 0.3:
+            return "%s != %s" % (self.sexpr(d), self.slit())
+        if r < 0.4:
+            return "%s == %d" % (self.pick(["ai", "bi", "(ai | bi)", "(ai | 7)"]), int(self.r.integers(-2, 5)))
+        if r < 0.45:
+            return "ai == bi"
+        if r < 0.5:
+            return "%s == %s" % (self.pick(["ad", "bd", "(ad | 2.5)"]), self.pick(["1.5", "2.5", "0.0", "bd"]))
+        if r < 0.58:
+            return self.pick(["ab", "bb", "b1", "(ab | bb)", "(ab | true)", "ab == bb", "b1 != false"])
+        if r < 0.68:
+            fn = self.pick(["startsWith", "endsWith"])
+            return "%s.%s(%s)" % (self.pick(["as", "bs", self.slit()]), fn, self.sexpr(d))
+        if r < 0.74:
+            return "match(%s, %s)" % (self.sexpr(d), self.pick(['"a*"', '"*c"', '"abc"', '"*"', "bs"]))
+        if r < 0.82:
+            return "%s %s %s" % (self.pick(["aip", "bip", "(aip | bip)"]), self.pick(["==", "!="]),
+                                 self.pick(['ip("1.2.3.4")', 'ip("10.0.0.1")', "bip", "ip(as)", 'ip("bad")',
+                                            'ip(ar["a"])', 'ip("::ffff:1.2.3.4")']))
+        if r < 0.88:
+            return "%s == %s" % (self.pick(["at", "t1", "(at | bt)"]),
+                                 self.pick(['timestamp("2015-01-02T15:04:35Z")', "t2", "timestamp(as)",
+                                            'timestamp("nope")']))
+        if r < 0.92:
+            return "%s == %s" % (self.pick(["adur", "(adur | bdur)"]), self.pick(['"19ms"', "bdur", '"0"']))
+        return self.pick(["true", "false", "TRUE", "ai == true", "as.foo()", "ai = 2", "x == 2", "ar == br"])
+
+    def expr(self, d):
+        r = self.r.random()
+        if d <= 0 or r < 0.45:
+            return self.atom(d)
+        if r < 0.7:
+            return "%s && %s" % (self.expr(d - 1), self.expr(d - 1))
+        if r < 0.9:
+            return "%s || %s" % (self.expr(d - 1), self.expr(d - 1))
+        return "(%s)" % self.expr(d - 1)
+
+
+def fuzz_rules(n, seed=7, depth=3):
+    f = _Fuzz(np.random.default_rng(seed))
+    return [f.expr(depth) for _ in range(n)]
+
+
+def fuzz_bags(n, seed=8):
+    rng = np.random.default_rng(seed)
+    f = _Fuzz(rng)
+    bags = []
+    for _ in range(n):
+        b = {}
+        for name, vt in DEFAULT_TEST_MANIFEST.items():
+            if rng.random() < 0.25:
+                continue
+            wrong = rng.random() < 0.05
+            if wrong:
+                b[name] = f.pick(["str", GoInt64(3), True, GoOther("20"), {"a": "b"}, GoFloat64(1.5), b"\x01"])
+                continue
+            if vt == "STRING":
+                b[name] = f.pick(_STR_VALS)
+            elif vt == "INT64":
+                b[name] = GoInt64(int(rng.integers(-2, 5))) if rng.random() < 0.9 else GoDuration(3)
+            elif vt == "DOUBLE":
+                b[name] = GoFloat64(f.pick([1.5, 2.5, 0.0, -0.0]))
+            elif vt == "BOOL":
+                b[name] = bool(rng.random() < 0.5)
+            elif vt == "DURATION":
+                b[name] = GoDuration(f.pick([19_000_000, 20_000_000, 0]))
+            elif vt == "TIMESTAMP":
+                b[name] = GoTime(f.pick([1420211075, 1420211074, 1420207475]), 0)
+            elif vt == "IP_ADDRESS":
+                b[name] = f.pick([bytes([1, 2, 3, 4]), bytes([10, 0, 0, 1]),
+                                  bytes(10) + b"\xff\xff" + bytes([1, 2, 3, 4]), bytes(15) + b"\x01"])
+            elif vt == "STRING_MAP":
+                m = {}
+                for k in _KEYS:
+                    if rng.random() < 0.5:
+                        m[k] = f.pick(_STR_VALS)
+                b[name] = m
+        bags.append(b)
+    return bags

@@ -237,10 +237,14 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
     gv tv;
     uint32_t fn = fn_sid;
 
-    memset(opstack, 0, sizeof opstack);
-    memset(frames, 0, sizeof frames);
-    memset(heap, 0, sizeof heap);
-    memset(r, 0, sizeof *r);
+    /* The reference zero-initialises its stack, frames and heap per call (interpreterRun.go:49-51).
+     * Only never-written heap slots and frame registers are observable (as nil / 0): heap reads at
+     * or above hp yield nil below, and frames are zeroed on first use. */
+    int frames_zeroed = 0;
+    r->status = 0;
+    r->v1 = r->v2 = 0;
+    r->msg[0] = 0;
+    memset(&r->val, 0, sizeof r->val);
     r->rtype = p->fn_ret[fn];
     ip = p->fn_addr[fn];
     if (p->fn_nparams[fn] != 0) FAIL("init function must have 0 args");
@@ -570,6 +574,10 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
         case OP_Call: {
             t1 = p->code[ip++];
             if (fp >= FRAMES) PANIC("runtime error: index out of range");
+            if (!frames_zeroed) {
+                memset(frames, 0, sizeof frames);
+                frames_zeroed = 1;
+            }
             /* stackFrame.save copies the frame's registers over the live ones (stackFrame.go:28-33) */
             uint32_t nps = 0;
             for (uint32_t k = 0; k < p->fn_nparams[fn]; k++) nps += alloc_size(p->fn_params[p->fn_param_off[fn] + k]);
@@ -595,7 +603,8 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
                 for (uint32_t k = 0; k < p->fn_nparams[t1] && k < 2; k++) {
                     uint32_t hi = opstack[ap];
                     if (hi >= HEAP_SIZE) PANIC("runtime error: index out of range");
-                    args[k] = heap[hi];
+                    if (hi < hp) args[k] = heap[hi];
+                    else memset(&args[k], 0, sizeof args[k]);  /* never-written slot: nil */
                     ap += 1;
                 }
                 switch (ext) {
@@ -716,7 +725,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
                     if (sp < 1) UNDERFLOW;
                     r->v1 = opstack[sp - 1];
                     if (r->v1 >= HEAP_SIZE) PANIC("runtime error: index out of range");
-                    r->val = heap[r->v1];
+                    if (r->v1 < hp) r->val = heap[r->v1];
                     if (r->val.inl_used) r->val.p = r->val.inl; /* ip() bytes travel with the result */
                     break;
                 default:

@@ -1,0 +1,143 @@
+"""GPU parity: the HIP engine (libmxp, through the C-ABI) against the oracle, pair by pair.
+
+Bar: bit-exact.  Every (request, rule) pair must agree on {false, true, error, panic} (EvalPredicate
+semantics), and every error pair's message must equal the reference's text.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+from istio_amd import workloads as W
+from istio_amd.bags import BagBatch, from_tagged
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROWS = json.load(open(os.path.join(HERE, "golden", "ilt_tests.json")))
+
+
+@pytest.fixture(scope="module")
+def mxp(libmxp):
+    import istio_amd.engine as mxp
+    return mxp
+
+
+def gpu_codes(engine, batch):
+    """Per-pair codes from the GPU bitmaps, with panics told apart through the error log."""
+    match, err = engine.eval_batch(batch)
+    codes = __import__("istio_amd.engine", fromlist=["x"]).bits_to_codes(match, err, len(engine.rules))
+    return codes
+
+
+def compare(engine, ev, rules, batch, sample_msgs=400, seed=0):
+    from istio_amd.engine import PANIC_TEXTS
+    got = gpu_codes(engine, batch)
+    want = oracle.oracle_matrix(ev, rules, batch, threads=16)
+    want_err = np.where(want >= 2, 2, want)  # bitmaps carry error|panic in one bit
+    bad = np.argwhere(got != want_err)
+    assert bad.size == 0, "first mismatches (req, rule): %s; rules: %s" % (
+        bad[:5].tolist(), [rules[j] for _, j in bad[:3]])
+    # error texts (and error-vs-panic class) for a sample of error pairs
+    errs = np.argwhere(want >= 2)
+    rng = np.random.default_rng(seed)
+    if len(errs) > sample_msgs:
+        errs = errs[rng.choice(len(errs), sample_msgs, replace=False)]
+    for q, r in errs:
+        st, msg = ev.eval_predicate(rules[r], batch, int(q))
+        gmsg = engine.pair_error(int(q), int(r))
+        assert gmsg == msg or (st == "panic" and gmsg in PANIC_TEXTS), (rules[r], int(q), gmsg, msg)
+        assert (gmsg in PANIC_TEXTS) == (st == "panic"), (rules[r], gmsg, st)
+    return got, want
+
+
+def test_golden_table_on_gpu(mxp):
+    """Every golden row (mixer/pkg/il/testing/tests.go) evaluated by the GPU engine."""
+    from test_oracle_golden import same_value
+    for conf in ("defaultAttrs", "exprEvalAttrs"):
+        rows = [r for r in ROWS["rows"] if r.get("E") and r.get("conf", "defaultAttrs") == conf
+                and "CompileErr" not in r and "Externs" not in r and ".matches(" not in r["E"]]
+        eng = mxp.Engine(0)
+        eng.set_vocabulary(ROWS["manifests"][conf])
+        st = eng.compile([r["E"] for r in rows])
+        assert (st == 0).all(), [rows[i]["E"] for i in np.where(st != 0)[0]]
+        batch = BagBatch.from_bags([{k: from_tagged(v) for k, v in r.get("I", {}).items()} for r in rows])
+        vals, codes = eng.eval_values(batch)
+        for i, r in enumerate(rows):
+            c = int(codes[i, i])
+            if "Err" in r:
+                assert c in (2, 3), r["E"]
+                assert eng.pair_error(i, i).startswith(r["Err"]), (r["E"], eng.pair_error(i, i))
+                continue
+            assert c in (0, 1), (r["E"], eng.pair_error(i, i))
+            want = from_tagged(r["R"])
+            got = mxp.decode_value(eng, i, int(vals[i, i]))
+            if isinstance(want, (bool, bytes)) or type(want).__name__ in ("GoInt64", "GoFloat64", "GoDuration"):
+                assert same_value(want, got), (r["E"], want, got)
+            elif isinstance(want, str):
+                assert got == want, (r["E"], want, got)
+            else:  # time.Time results: compare the %v rendering
+                from istio_amd.bags import GoTime
+                assert isinstance(want, GoTime) and got[0] == "time"
+
+
+def test_c1_bookinfo_parity(mxp):
+    manifest, rules, batch = W.c1_workload(10000)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    ev = oracle.OracleEvaluator(manifest)
+    got, want = compare(eng, ev, rules, batch)
+    assert (want == 1).any() and (want == 2).any()
+
+
+def test_c2_parity_config_size(mxp):
+    """BASELINE configs[1]: 1k rules x 64k requests, full pair matrix against the oracle."""
+    manifest, rules, batch = W.c2_workload(n_rules=1000, n_requests=65536)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    ev = oracle.OracleEvaluator(manifest)
+    got, want = compare(eng, ev, rules, batch)
+    assert (want == 1).sum() > 0 and (want == 2).sum() > 0
+
+
+@pytest.mark.parametrize("seed", [7, 17])
+def test_fuzz_parity(mxp, seed):
+    """Random well- and ill-typed rules over random bags with missing / wrongly typed values."""
+    rules = W.fuzz_rules(600, seed=seed, depth=3)
+    bags = W.fuzz_bags(400, seed=seed + 1)
+    batch = BagBatch.from_bags(bags, names=list(W.DEFAULT_TEST_MANIFEST))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
+    st = eng.compile(rules)
+    keep = [i for i in range(len(rules)) if st[i] != 5]
+    assert len(keep) >= 0.9 * len(rules)
+    ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
+    compare(eng, ev, rules, batch)
+
+
+def test_device_resident_batch_and_hits(mxp):
+    """mxp_batch_upload + mxp_batch_eval_device + mxp_hits_device agree with the host path."""
+    import torch
+    manifest, rules, batch = W.c2_workload(n_rules=300, n_requests=20000)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    match_h, err_h = eng.eval_batch(batch)
+    db = eng.upload(batch)
+    W_ = (len(rules) + 31) // 32
+    dm = torch.zeros((W_, batch.n), dtype=torch.int32, device="cuda:0")
+    de = torch.zeros_like(dm)
+    hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
+    s = torch.cuda.current_stream()
+    db.eval(dm.data_ptr(), de.data_ptr(), s.cuda_stream)
+    rc = eng.lib.mxp_hits_device(eng.h, dm.data_ptr(), batch.n, s.cuda_stream, hits.data_ptr())
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(dm.cpu().numpy().view(np.uint32), match_h)
+    assert np.array_equal(de.cpu().numpy().view(np.uint32), err_h)
+    codes = mxp.bits_to_codes(match_h, err_h, len(rules))
+    assert np.array_equal(hits.cpu().numpy(), (codes == 1).sum(axis=0))

@@ -1,0 +1,74 @@
+"""The product's C++ front end / IL code generator (libmxp, host-only engine) against the golden
+table and against the oracle on generated rule sets; and the lowering's coverage."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import goexpr
+import ilcompile
+from istio_amd import workloads as W
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROWS = json.load(open(os.path.join(HERE, "golden", "ilt_tests.json")))
+
+
+@pytest.fixture(scope="module")
+def Engine(libmxp):
+    from istio_amd.engine import Engine
+    return Engine
+
+
+def test_golden_compile(Engine):
+    mism = []
+    for row in ROWS["rows"]:
+        if not row.get("E") or "Fns" in row:
+            continue
+        e = Engine(-1)
+        e.set_vocabulary(ROWS["manifests"][row.get("conf", "defaultAttrs")])
+        st = e.compile([row["E"]])[0]
+        if "CompileErr" in row:
+            if st == 0 or e.rule_error(0) != row["CompileErr"]:
+                mism.append((row["index"], e.rule_error(0)))
+            continue
+        if st != 0:
+            if ".matches(" in row["E"] and st == 5:
+                continue  # regexp lowering not in round 1
+            mism.append((row["index"], st, e.rule_error(0)))
+            continue
+        if "IL" in row and e.rule_il_text(0).strip() != row["IL"].strip():
+            mism.append((row["index"], e.rule_il_text(0)))
+    assert not mism
+
+
+def _oracle_compile(manifest, rule):
+    attrs = {k: goexpr.VT[v] for k, v in manifest.items()}
+    try:
+        p, _ = ilcompile.compile_expr(rule, attrs)
+        return ilcompile.write_text(p), None
+    except Exception as e:  # noqa: BLE001 -- every reference error class is compared by text
+        return None, str(e)
+
+
+@pytest.mark.parametrize("which", ["c1", "c2", "fuzz"])
+def test_matches_oracle_codegen(Engine, which):
+    if which == "c1":
+        manifest, rules, _ = W.c1_workload(10)
+    elif which == "c2":
+        manifest, rules = W.TESTDATA_MANIFEST, W.c2_rules(500)[0]
+    else:
+        manifest, rules = W.DEFAULT_TEST_MANIFEST, W.fuzz_rules(1500, seed=11, depth=3)
+    e = Engine(-1)
+    e.set_vocabulary(manifest)
+    st = e.compile(rules)
+    for i, r in enumerate(rules):
+        text, err = _oracle_compile(manifest, r)
+        if err is not None:
+            assert st[i] != 0 and e.rule_error(i) == err, r
+        else:
+            assert st[i] in (0, 5), (r, e.rule_error(i))
+            assert e.rule_il_text(i) == text, r
+    # every generated rule without a regexp lowers to the GPU bytecode
+    unsupported = [rules[i] for i in np.where(st == 5)[0] if ".matches(" not in rules[i]]
+    assert not unsupported, unsupported[:3]
