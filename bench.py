@@ -93,7 +93,8 @@ def main():
     d_match = torch.empty((Wd, N), dtype=torch.int32, device=dev)
     d_err = torch.empty((Wd, N), dtype=torch.int32, device=dev)
     hits = torch.zeros(R, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # a real (non-null) HIP stream shared by libmxp, events and RCCL
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
 
     def step(ev0=None, ev1=None):

@@ -84,8 +84,10 @@ struct mxp_engine : public mxp::LowerTables {
     // rule-set-global interning
     std::unordered_map<std::string, uint32_t> gstr_ids;
     std::vector<std::string> gstrs;
-    std::unordered_map<std::string, uint32_t> gbytes_ids;
+    std::unordered_map<std::string, uint32_t> gbytes_ids;   // exact []byte values
     std::vector<std::string> gbytes;
+    std::unordered_map<std::string, uint32_t> gcanon_ids;   // their net.IP.Equal classes
+    std::vector<std::string> gcanon;
     std::map<TimeKey, uint32_t> gtime_ids;
     std::vector<TimeKey> gtimes;
     std::vector<std::string> cols;
@@ -124,12 +126,17 @@ struct mxp_engine : public mxp::LowerTables {
         gstrs.push_back(s);
         return id;
     }
-    uint32_t intern_bytes(const std::string& c) override {
-        auto it = gbytes_ids.find(c);
-        if (it != gbytes_ids.end()) return it->second;
-        uint32_t id = (uint32_t)gbytes.size();
-        gbytes_ids.emplace(c, id);
-        gbytes.push_back(c);
+    uint64_t intern_bytes(const std::string& raw) override {
+        std::string canon = mxp::ip_canonical((const uint8_t*)raw.data(), raw.size());
+        return MXP_BYTES_ID(intern_in(gcanon_ids, gcanon, canon), intern_in(gbytes_ids, gbytes, raw));
+    }
+    static uint32_t intern_in(std::unordered_map<std::string, uint32_t>& ids, std::vector<std::string>& v,
+                              const std::string& s) {
+        auto it = ids.find(s);
+        if (it != ids.end()) return it->second;
+        uint32_t id = (uint32_t)v.size();
+        ids.emplace(s, id);
+        v.push_back(s);
         return id;
     }
     uint32_t intern_time(int64_t s, int32_t ns) override {
@@ -178,6 +185,8 @@ struct mxp_engine : public mxp::LowerTables {
         gstrs.clear();
         gbytes_ids.clear();
         gbytes.clear();
+        gcanon_ids.clear();
+        gcanon.clear();
         gtime_ids.clear();
         gtimes.clear();
         cols.clear();
@@ -311,16 +320,38 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
         db->overlay.push_back(v);
         return m = id;
     };
-    std::unordered_map<std::string, uint32_t> obytes;
-    auto bytes_id = [&](const std::string& canon) -> uint32_t {
-        auto it = gbytes_ids.find(canon);
-        if (it != gbytes_ids.end()) return it->second;
-        auto jt = obytes.find(canon);
-        if (jt != obytes.end()) return jt->second;
-        uint32_t id = (uint32_t)(gbytes.size() + db->overlay_bytes.size());
-        obytes.emplace(canon, id);
-        db->overlay_bytes.push_back(canon);
-        return id;
+    std::unordered_map<std::string, uint32_t> obytes, ocanon;
+    std::vector<std::string> overlay_canon;
+    auto bytes_id = [&](const std::string& raw) -> uint64_t {
+        uint32_t rid, cid;
+        auto it = gbytes_ids.find(raw);
+        if (it != gbytes_ids.end()) {
+            rid = it->second;
+        } else {
+            auto jt = obytes.find(raw);
+            if (jt != obytes.end()) {
+                rid = jt->second;
+            } else {
+                rid = (uint32_t)(gbytes.size() + db->overlay_bytes.size());
+                obytes.emplace(raw, rid);
+                db->overlay_bytes.push_back(raw);
+            }
+        }
+        std::string canon = mxp::ip_canonical((const uint8_t*)raw.data(), raw.size());
+        auto ct = gcanon_ids.find(canon);
+        if (ct != gcanon_ids.end()) {
+            cid = ct->second;
+        } else {
+            auto dt = ocanon.find(canon);
+            if (dt != ocanon.end()) {
+                cid = dt->second;
+            } else {
+                cid = (uint32_t)(gcanon.size() + overlay_canon.size());
+                ocanon.emplace(canon, cid);
+                overlay_canon.push_back(canon);
+            }
+        }
+        return MXP_BYTES_ID(cid, rid);
     };
     std::map<TimeKey, uint32_t> otimes;
     auto time_id = [&](int64_t s, int32_t ns) -> uint32_t {
@@ -349,11 +380,7 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
             uint64_t v = bv[r];
             switch (k) {
             case MXP_STRING: v = sid_of((uint32_t)v); break;
-            case MXP_BYTES: {
-                std::string raw = bstr((uint32_t)v);
-                v = bytes_id(mxp::ip_canonical((const uint8_t*)raw.data(), raw.size()));
-                break;
-            }
+            case MXP_BYTES: v = bytes_id(bstr((uint32_t)v)); break;
             case MXP_TIMESTAMP: v = time_id(b->time_sec[v], b->time_nsec[v]); break;
             case MXP_OTHER: v = 0; break;
             default: break;
@@ -412,7 +439,7 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
             std::string v = string_of(db, s);
             uint8_t out[16];
             if (mxp::go_parse_ip((const uint8_t*)v.data(), v.size(), out))
-                ipof[s] = MXP_FH(MXP_BYTES, bytes_id(mxp::ip_canonical(out, 16)));
+                ipof[s] = MXP_FH(MXP_BYTES, bytes_id(std::string((const char*)out, 16)));
         }
     }
     if (need_tsof) {
@@ -798,9 +825,10 @@ int mxp_value_text(mxp_engine* eng, uint32_t rule, uint64_t v, char* buf, uint32
     }
     case MXP_BYTES: {
         std::string c;
-        if (id < eng->gbytes.size()) c = eng->gbytes[id];
-        else if (eng->last_db && id - eng->gbytes.size() < eng->last_db->overlay_bytes.size())
-            c = eng->last_db->overlay_bytes[id - eng->gbytes.size()];
+        uint64_t raw = MXP_BYTES_RAW(id);
+        if (raw < eng->gbytes.size()) c = eng->gbytes[raw];
+        else if (eng->last_db && raw - eng->gbytes.size() < eng->last_db->overlay_bytes.size())
+            c = eng->last_db->overlay_bytes[raw - eng->gbytes.size()];
         s = mxp::go_format_bytes((const uint8_t*)c.data(), c.size());
         break;
     }

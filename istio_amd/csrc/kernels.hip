@@ -250,7 +250,10 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bo
                 const uint64_t p = regs[a][tid], q = regs[b][tid];
                 const uint32_t want = op == VM_IPEQ ? MXP_BYTES : MXP_TIMESTAMP;
                 if (MXP_FH_KIND(p) != want || MXP_FH_KIND(q) != want) FAIL(PANIC_EXTARG, 0);
-                else regs[d][tid] = MXP_FH_ID(p) == MXP_FH_ID(q) ? 1u : 0u;
+                else if (op == VM_IPEQ)  // net.IP.Equal: same canonical class
+                    regs[d][tid] = MXP_BYTES_CANON(MXP_FH_ID(p)) == MXP_BYTES_CANON(MXP_FH_ID(q)) ? 1u : 0u;
+                else  // time.Time.Equal: same instant
+                    regs[d][tid] = MXP_FH_ID(p) == MXP_FH_ID(q) ? 1u : 0u;
             }
             break;
         case VM_ERR:

@@ -456,7 +456,7 @@ class Lowerer {
                 if (ip) {
                     uint8_t b[16];
                     if (go_parse_ip((const uint8_t*)txt.data(), txt.size(), b)) {
-                        uint64_t h = MXP_FH(MXP_BYTES, t_->intern_bytes(ip_canonical(b, 16)));
+                        uint64_t h = MXP_FH(MXP_BYTES, t_->intern_bytes(std::string((const char*)b, 16)));
                         emit(VM_CONST, top(), 0, 0, 0, (uint32_t)h, (uint32_t)(h >> 32));
                     } else {
                         emit(VM_ERR, top(), 0, 0, 0, ERR_IP, (uint32_t)s.kval);

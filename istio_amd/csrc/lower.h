@@ -23,7 +23,8 @@ class LowerTables {
   public:
     virtual ~LowerTables() = default;
     virtual uint32_t intern_string(const std::string& s) = 0;     // global string id
-    virtual uint32_t intern_bytes(const std::string& canon) = 0;  // bytes id (canonical IP form)
+    // []byte value -> packed id: canonical-form id (net.IP.Equal classes) << 28 | raw-bytes id
+    virtual uint64_t intern_bytes(const std::string& raw) = 0;
     virtual uint32_t intern_time(int64_t sec, int32_t nsec) = 0;  // time id
     virtual uint32_t column(const std::string& attr) = 0;         // resolve column index
     virtual uint32_t vcolumn(const std::string& attr, const std::string& key) = 0;  // map[key] column

@@ -92,6 +92,10 @@ typedef struct mxp_vm_ins {
 #define MXP_FH(kind, id) ((((uint64_t)(kind)) << 56) | ((uint64_t)(id) & 0x00FFFFFFFFFFFFFFull))
 #define MXP_FH_KIND(h) ((uint32_t)((h) >> 56))
 #define MXP_FH_ID(h) ((h) & 0x00FFFFFFFFFFFFFFull)
+// []byte ids: canonical (net.IP.Equal) class in bits 28..55, exact bytes in bits 0..27
+#define MXP_BYTES_CANON(id) ((id) >> 28)
+#define MXP_BYTES_RAW(id) ((id) & 0x0FFFFFFFull)
+#define MXP_BYTES_ID(canon, raw) ((((uint64_t)(canon)) << 28) | (uint64_t)(raw))
 
 // virtual-column kinds (VM_VCOL)
 enum mxp_vcol_kind { VC_ABSENT = 0, VC_VALUE = 1, VC_NOTMAP = 3 };

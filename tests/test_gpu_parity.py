@@ -132,7 +132,8 @@ def test_device_resident_batch_and_hits(mxp):
     dm = torch.zeros((W_, batch.n), dtype=torch.int32, device="cuda:0")
     de = torch.zeros_like(dm)
     hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
-    s = torch.cuda.current_stream()
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
     db.eval(dm.data_ptr(), de.data_ptr(), s.cuda_stream)
     rc = eng.lib.mxp_hits_device(eng.h, dm.data_ptr(), batch.n, s.cuda_stream, hits.data_ptr())
     assert rc == 0
