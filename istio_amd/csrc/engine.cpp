@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -24,6 +25,7 @@
 #include "ilgen.h"
 #include "kargs.h"
 #include "lower.h"
+#include "vmopt.h"
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
@@ -108,7 +110,9 @@ struct mxp_engine : public mxp::LowerTables {
     bool have_rules = false;
     bool need_ipof = false, need_tsof = false, need_strings = false, need_maps = false;
 
-    DevBuf d_prog, d_rule_off, d_gstr_off, d_gstr;
+    DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
+    uint32_t n_guarded = 0;
+    uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS (ablation only; results are not valid with flags set)
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 20;
 
@@ -262,6 +266,14 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     for (auto& R : rules)
         for (auto& ins : R.low.code)
             if ((ins.op & 0x7F) == VM_VCOL) ins.x += C;
+    // leading-atom guards (evaluated for a whole 32-rule group at once by the kernel)
+    std::vector<mxp_guard> guards(n);
+    for (uint32_t i = 0; i < n; i++) {
+        std::vector<mxp_vm_ins> code(all.begin() + off[i], all.begin() + off[i + 1]);
+        guards[i] = mxp::extract_guard(code);
+    }
+    n_guarded = 0;
+    for (auto& g : guards) n_guarded += (g.mode & 0xFF) != GM_NONE;
 
     have_rules = true;
     if (device < 0) return MXP_OK;  // host-only engine: compile / inspect, no device tables
@@ -271,6 +283,10 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((e = hipSetDevice(device)) != hipSuccess) return hipfail(e, "hipSetDevice");
     if ((e = d_prog.alloc(all.size() * sizeof(mxp_vm_ins))) != hipSuccess) return hipfail(e, "hipMalloc prog");
     if ((e = d_rule_off.alloc(off.size() * 4)) != hipSuccess) return hipfail(e, "hipMalloc rule_off");
+    if ((e = d_guards.alloc(guards.size() * sizeof(mxp_guard))) != hipSuccess) return hipfail(e, "hipMalloc guards");
+    if (!guards.empty() &&
+        (e = hipMemcpy(d_guards.p, guards.data(), guards.size() * sizeof(mxp_guard), hipMemcpyHostToDevice)) != hipSuccess)
+        return hipfail(e, "upload guards");
     std::vector<uint64_t> soff(gstrs.size() + 1, 0);
     std::string blob;
     for (size_t i = 0; i < gstrs.size(); i++) {
@@ -486,6 +502,8 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     memset(A, 0, sizeof *A);
     A->prog = d_prog.as<mxp_vm_ins>();
     A->rule_off = d_rule_off.as<uint32_t>();
+    A->guards = d_guards.as<mxp_guard>();
+    A->flags = debug_flags;
     A->n_rules = (uint32_t)rules.size();
     A->n_words = (A->n_rules + 31) / 32;
     A->groups_per_wave = 1;
@@ -602,6 +620,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     auto* e = new (std::nothrow) mxp_engine();
     if (!e) return MXP_ERR_NOMEM;
     e->device = device;
+    if (const char* f = getenv("MXP_DEBUG_FLAGS")) e->debug_flags = (uint32_t)atoi(f);
     if (device < 0) {  // host-only engine (compiler / lowering inspection without a GPU)
         e->reset_tables();
         *out = e;

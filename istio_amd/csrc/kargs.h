@@ -9,6 +9,7 @@ typedef struct mxp_kargs {
     // rule set (uploaded once per config snapshot)
     const mxp_vm_ins* prog;      // all rules' programs, concatenated
     const uint32_t* rule_off;    // [n_rules + 1]
+    const mxp_guard* guards;     // [n_rules] leading-atom guards (vmopt.h)
     uint32_t n_rules;
     uint32_t n_words;            // ceil(n_rules / 32)
     uint32_t groups_per_wave;
@@ -38,5 +39,5 @@ typedef struct mxp_kargs {
     mxp_err_rec* errlog;
     uint32_t* errcount;
     uint32_t errcap;
-    uint32_t pad1;
+    uint32_t flags;              // debug / ablation: 1 = skip phase 2 (VM), 2 = no guards
 } mxp_kargs;

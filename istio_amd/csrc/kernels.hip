@@ -80,17 +80,37 @@ __device__ __forceinline__ void log_err(const mxp_kargs& A, uint32_t req, uint32
     }
 }
 
-// Runs one rule for the 64 requests of this wave; returns the lane's pair code (mxp_pair_code).
-__device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bool valid,
-                             uint64_t (*regs)[256], uint32_t tid) {
-    const uint32_t base = uni(A.rule_off[rule]);
-    const uint32_t len = uni(A.rule_off[rule + 1]) - base;
-    const uint4* prog = reinterpret_cast<const uint4*>(A.prog) + base;
+// constant-address-space views: uniform loads through them become scalar s_load_dwordxN
+typedef __attribute__((address_space(4))) const uint32_t cuint32;
+
+// Runs rule `rule` (program prog[base, base+len)) from `pc0` for the lanes in `live` (the others
+// keep their phase-1 result); returns the pair code of every lane that ran.
+//
+// Programs of up to 64 instructions are fetched ONCE with a coalesced vector load -- lane l holds
+// instruction l in four VGPRs -- and each step reads its instruction with v_readlane (no memory
+// latency on the dispatch path).  Longer programs fall back to scalar loads per step.
+template <bool kPriv>
+__device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t base, uint32_t len, uint32_t pc0,
+                             bool live, uint32_t req, uint64_t (*regs)[256], uint32_t tid) {
+    cuint32* prog = ((cuint32*)A.prog) + (uint64_t)base * 4u;
+    const bool inreg = len <= 64u;
+    uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
+    if (inreg) {
+        const uint32_t lane = tid & 63u;
+        if (lane < len) {
+            const uint4 v = ((const uint4*)A.prog)[(uint64_t)base + lane];
+            p0 = v.x;
+            p1 = v.y;
+            p2 = v.z;
+            p3 = v.w;
+        }
+    }
+    uint64_t R[MXP_VM_MAXREG];  // kPriv: register file in VGPRs (uniform index -> s_set_gpr_idx)
+#define REG(i) (kPriv ? R[i] : regs[i][tid])
     const uint64_t N = A.n;
-    bool live = valid;
-    uint32_t wait = valid ? 0u : MXP_VM_DONE;
+    uint32_t wait = live ? pc0 : MXP_VM_DONE;
     uint32_t res = PC_FALSE;
-    uint32_t pc = 0;
+    uint32_t pc = pc0;
 
 #define FAIL(code_, aux_)                                   \
     do {                                                    \
@@ -104,11 +124,32 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bo
         live = false;        \
         wait = (t_);         \
     } while (0)
+#define FINISH(code_)         \
+    do {                      \
+        res = (code_);        \
+        live = false;         \
+        wait = MXP_VM_DONE;   \
+    } while (0)
+#define FINISHV(code_)                                                              \
+    do {                                                                            \
+        if (A.out_vals) A.out_vals[(uint64_t)req * A.n_rules + rule] = (code_);     \
+        FINISH(code_);                                                              \
+    } while (0)
 
     while (pc < len) {
-        const uint4 w = prog[pc];
-        const uint32_t w0 = uni(w.x);
-        const uint32_t x = uni(w.y), y = uni(w.z), z = uni(w.w);
+        uint32_t w0, x, y, z;
+        if (inreg) {
+            w0 = __builtin_amdgcn_readlane(p0, pc);
+            x = __builtin_amdgcn_readlane(p1, pc);
+            y = __builtin_amdgcn_readlane(p2, pc);
+            z = __builtin_amdgcn_readlane(p3, pc);
+        } else {
+            cuint32* ip = prog + (uint64_t)pc * 4u;
+            w0 = uni(ip[0]);
+            x = uni(ip[1]);
+            y = uni(ip[2]);
+            z = uni(ip[3]);
+        }
         const uint32_t op = w0 & 0x7Fu;
         const uint32_t d = (w0 >> 8) & 0xFFu, a = (w0 >> 16) & 0xFFu, b = w0 >> 24;
         if (w0 & MXP_VM_WAKE) live = live || (wait == pc);
@@ -137,7 +178,7 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bo
                 } else if (!ok) {
                     FAIL(ERR_CONV_S + y, x);
                 } else {
-                    regs[d][tid] = v;
+                    REG(d) = v;
                     if (op == VM_TRES) JUMP(z);
                 }
             }
@@ -147,64 +188,71 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bo
             if (live) {
                 const uint64_t at = (uint64_t)x * N + req;
                 const uint32_t k = A.kinds[at];
-                if (k == VC_VALUE) regs[d][tid] = A.vals[at];
+                if (k == VC_VALUE) REG(d) = A.vals[at];
                 else if (k == VC_ABSENT) FAIL(ERR_LOOKUP, z);
                 else FAIL(PANIC_MAPTYPE, 0);
             }
             break;
         }
         case VM_CONST:
-            if (live) regs[d][tid] = (uint64_t)y | ((uint64_t)z << 32);
+            if (live) REG(d) = (uint64_t)y | ((uint64_t)z << 32);
             break;
         case VM_EQ:
-            if (live) regs[d][tid] = regs[a][tid] == regs[b][tid] ? 1u : 0u;
+            if (live) REG(d) = REG(a) == REG(b) ? 1u : 0u;
             break;
         case VM_EQK:
-            if (live) regs[d][tid] = regs[a][tid] == ((uint64_t)y | ((uint64_t)z << 32)) ? 1u : 0u;
+            if (live) REG(d) = REG(a) == ((uint64_t)y | ((uint64_t)z << 32)) ? 1u : 0u;
             break;
         case VM_NOT:
-            if (live) regs[d][tid] = regs[a][tid] == 0 ? 1u : 0u;
+            if (live) REG(d) = REG(a) == 0 ? 1u : 0u;
             break;
         case VM_LOGIC:
         case VM_LOGICK:
             if (live) {
-                const uint64_t p = regs[a][tid];
-                const uint64_t q = op == VM_LOGIC ? regs[b][tid] : (uint64_t)x;
+                const uint64_t p = REG(a);
+                const uint64_t q = op == VM_LOGIC ? REG(b) : (uint64_t)x;
                 // interpreterRun.go:352-443 operate on u32 words
                 const bool pb = (uint32_t)p != 0, qb = (uint32_t)q != 0;
-                regs[d][tid] = (y == 0 ? (pb && qb) : y == 1 ? (pb || qb) : (pb != qb)) ? 1u : 0u;
+                REG(d) = (y == 0 ? (pb && qb) : y == 1 ? (pb || qb) : (pb != qb)) ? 1u : 0u;
             }
             break;
         case VM_JZ:
-            if (live && (uint32_t)regs[a][tid] == 0) JUMP(z);
+            if (live && (uint32_t)REG(a) == 0) JUMP(z);
             break;
         case VM_JNZ:
-            if (live && (uint32_t)regs[a][tid] != 0) JUMP(z);
+            if (live && (uint32_t)REG(a) != 0) JUMP(z);
+            break;
+        // folded bool results (vmopt.cpp): y is PC_FALSE / PC_TRUE, i.e. also the value 0 / 1
+        case VM_JZRET:
+            if (live && (uint32_t)REG(a) == 0) FINISHV(y);
+            break;
+        case VM_JNZRET:
+            if (live && (uint32_t)REG(a) != 0) FINISHV(y);
+            break;
+        case VM_RETK:
+            if (live) FINISHV(y);
             break;
         case VM_JMP:
             if (live) JUMP(z);
             break;
         case VM_RET:
             if (live) {
-                const uint64_t v = regs[a][tid];
+                const uint64_t v = REG(a);
                 if (A.out_vals) A.out_vals[(uint64_t)req * A.n_rules + rule] = v;
                 if (y == 1) {
-                    res = (uint32_t)v != 0 ? PC_TRUE : PC_FALSE;
+                    FINISH((uint32_t)v != 0 ? PC_TRUE : PC_FALSE);
                 } else if (A.out_vals) {
-                    res = PC_FALSE;  // Eval: a non-bool result is just a value
+                    FINISH(PC_FALSE);  // Eval: a non-bool result is just a value
                 } else {
-                    res = PC_PANIC;  // EvalPredicate: Result.AsBool panics (result.go:42-52)
-                    log_err(A, req, rule, PANIC_NOTBOOL, 0);
+                    FAIL(PANIC_NOTBOOL, 0);  // EvalPredicate: Result.AsBool panics (result.go:42-52)
                 }
-                live = false;
-                wait = MXP_VM_DONE;
             }
             break;
         case VM_LOOKUP:
         case VM_LOOKUPK:
             if (live) {
-                const uint64_t h = regs[a][tid];
-                const uint32_t key = op == VM_LOOKUP ? (uint32_t)regs[b][tid] : x;
+                const uint64_t h = REG(a);
+                const uint32_t key = op == VM_LOOKUP ? (uint32_t)REG(b) : x;
                 if (MXP_FH_KIND(h) != MXP_STRING_MAP) {
                     FAIL(PANIC_MAPTYPE, 0);
                 } else {
@@ -217,10 +265,10 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bo
                             break;
                         }
                     if (found != MXP_VM_DONE) {
-                        regs[d][tid] = found;
+                        REG(d) = found;
                         if (y == LK_TRY) JUMP(z);
                     } else if (y == LK_N) {
-                        regs[d][tid] = A.empty_sid;
+                        REG(d) = A.empty_sid;
                     } else if (y == LK_ERR) {
                         FAIL(ERR_MEMBER, key);
                     }
@@ -230,30 +278,30 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bo
         case VM_STRFN:
         case VM_STRFNK:
             if (live) {
-                const StrRef s = str_of(A, regs[a][tid]);
-                const StrRef p = str_of(A, op == VM_STRFN ? regs[b][tid] : (uint64_t)x);
-                regs[d][tid] = strfn(y, s, p) ? 1u : 0u;
+                const StrRef s = str_of(A, REG(a));
+                const StrRef p = str_of(A, op == VM_STRFN ? REG(b) : (uint64_t)x);
+                REG(d) = strfn(y, s, p) ? 1u : 0u;
             }
             break;
         case VM_IPOF:
         case VM_TSOF:
             if (live) {
-                const uint64_t sid = regs[a][tid];
+                const uint64_t sid = REG(a);
                 const uint64_t h = (op == VM_IPOF ? A.ipof : A.tsof)[sid];
                 if (h == ~0ull) FAIL(op == VM_IPOF ? ERR_IP : ERR_TS, (uint32_t)sid);
-                else regs[d][tid] = h;
+                else REG(d) = h;
             }
             break;
         case VM_IPEQ:
         case VM_TSEQ:
             if (live) {
-                const uint64_t p = regs[a][tid], q = regs[b][tid];
+                const uint64_t p = REG(a), q = REG(b);
                 const uint32_t want = op == VM_IPEQ ? MXP_BYTES : MXP_TIMESTAMP;
                 if (MXP_FH_KIND(p) != want || MXP_FH_KIND(q) != want) FAIL(PANIC_EXTARG, 0);
                 else if (op == VM_IPEQ)  // net.IP.Equal: same canonical class
-                    regs[d][tid] = MXP_BYTES_CANON(MXP_FH_ID(p)) == MXP_BYTES_CANON(MXP_FH_ID(q)) ? 1u : 0u;
+                    REG(d) = MXP_BYTES_CANON(MXP_FH_ID(p)) == MXP_BYTES_CANON(MXP_FH_ID(q)) ? 1u : 0u;
                 else  // time.Time.Equal: same instant
-                    regs[d][tid] = MXP_FH_ID(p) == MXP_FH_ID(q) ? 1u : 0u;
+                    REG(d) = MXP_FH_ID(p) == MXP_FH_ID(q) ? 1u : 0u;
             }
             break;
         case VM_ERR:
@@ -261,13 +309,13 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bo
             break;
         case VM_FTOS:
             if (live) {
-                const uint64_t h = regs[a][tid];
+                const uint64_t h = REG(a);
                 if (MXP_FH_KIND(h) != MXP_STRING) FAIL(PANIC_CONV, 0);
-                else regs[d][tid] = MXP_FH_ID(h);
+                else REG(d) = MXP_FH_ID(h);
             }
             break;
         case VM_STOF:
-            if (live) regs[d][tid] = MXP_FH(MXP_STRING, regs[a][tid]);
+            if (live) REG(d) = MXP_FH(MXP_STRING, REG(a));
             break;
         default:
             break;
@@ -276,32 +324,123 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t req, bo
     }
 #undef FAIL
 #undef JUMP
+#undef FINISH
+#undef FINISHV
+#undef REG
     return res;
 }
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
-    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+// Phase 1 (guards) + phase 2 (VM for undecided lanes) over 32-rule groups.
+template <bool kPriv>
+__device__ __forceinline__ void eval_tile(const mxp_kargs& A, uint64_t (*regs)[256]) {
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
     const uint32_t req = blockIdx.x * 64u + (tid & 63u);
     const bool valid = req < A.n;
+    const uint64_t N = A.n;
     const uint32_t g0 = (blockIdx.y * 4u + wave) * A.groups_per_wave;
     const uint32_t g1 = min(g0 + A.groups_per_wave, A.n_words);
+    const uint32_t lane = tid & 63u;
+    // Eval mode (out_vals) needs every result register: run whole programs
+    const bool guards_on = !(A.out_vals || (A.flags & 2u));
     for (uint32_t g = g0; g < g1; g++) {
-        uint32_t m = 0, e = 0;
-        const uint32_t r0 = g * 32u, r1 = min(r0 + 32u, A.n_rules);
-        for (uint32_t rule = r0; rule < r1; rule++) {
-            const uint32_t code = run_rule(A, rule, req, valid, regs, tid);
-            m |= (code == PC_TRUE ? 1u : 0u) << (rule - r0);
-            e |= (code >= PC_ERROR ? 1u : 0u) << (rule - r0);
+        const uint32_t r0 = g * 32u, nr = min(32u, A.n_rules - r0);
+        // the group's guards (lane k < 32: guard k) and rule offsets (lane k <= 32: rule_off[r0 + k])
+        // in VGPRs, read back per rule with v_readlane
+        uint32_t G0 = 0, G1 = GM_NONE, G2 = 0, G3 = 0, RO = 0;
+        if (lane < nr) {
+            const uint4 v = ((const uint4*)A.guards)[r0 + lane];
+            G0 = v.x;
+            G1 = v.y;
+            G2 = v.z;
+            G3 = v.w;
+        }
+        if (lane <= nr) RO = A.rule_off[r0 + lane];
+        uint32_t m = 0, e = 0, cont = 0;
+        // ---- phase 1: leading atoms of the whole group: vector compares against scalar constants
+        uint32_t cached = MXP_VM_DONE;
+        uint32_t ck = 0;
+        uint64_t cv = 0;
+        for (uint32_t k = 0; k < nr; k++) {
+            const uint32_t gc = __builtin_amdgcn_readlane(G0, k), gm = __builtin_amdgcn_readlane(G1, k);
+            const uint64_t K = (uint64_t)__builtin_amdgcn_readlane(G2, k) |
+                               ((uint64_t)__builtin_amdgcn_readlane(G3, k) << 32);
+            const uint32_t mode = guards_on ? (gm & 0xFFu) : (uint32_t)GM_NONE;
+            const uint32_t bit = 1u << k;
+            if (mode == GM_NONE) {
+                cont |= valid ? bit : 0u;
+                continue;
+            }
+            const uint32_t col = gc & 0xFFFFFFu, gk = gc >> 24;
+            if (col != cached) {
+                cached = col;
+                if (valid) {
+                    ck = A.kinds[(uint64_t)col * N + req];
+                    cv = A.vals[(uint64_t)col * N + req];
+                }
+            }
+            bool ok;
+            uint32_t ecode = 0;
+            if (gk == GK_VCOL) {
+                ok = ck == VC_VALUE;
+                if (!ok) ecode = ck == VC_ABSENT ? ERR_LOOKUP : PANIC_MAPTYPE;
+            } else {
+                ok = gk == W_S ? ck == MXP_STRING : gk == W_B ? ck == MXP_BOOL
+                     : gk == W_I ? (ck == MXP_INT64 || ck == MXP_DURATION) : ck == MXP_DOUBLE;
+                if (!ok) ecode = ck == MXP_ABSENT ? ERR_LOOKUP : ERR_CONV_S + gk;
+            }
+            const bool atom = (cv == K) != (((gm >> 8) & 1u) != 0);
+            if (valid) {
+                if (!ok) {
+                    e |= bit;
+                    if (A.errlog) {
+                        const uint32_t aux = ecode == ERR_LOOKUP
+                                                 ? A.prog[__builtin_amdgcn_readlane(RO, k)].z
+                                                 : (gk == GK_VCOL ? 0u : col);
+                        log_err(A, req, r0 + k, ecode, aux);
+                    }
+                } else if (mode == GM_ONLY) {
+                    m |= atom ? bit : 0u;
+                } else if (mode == GM_AND) {
+                    cont |= atom ? bit : 0u;
+                } else {  // GM_OR
+                    m |= atom ? bit : 0u;
+                    cont |= atom ? 0u : bit;
+                }
+            }
+        }
+        // ---- phase 2: the VM, only for rules some lane still needs
+        for (uint32_t k = 0; k < nr && !(A.flags & 1u); k++) {
+            const uint32_t bit = 1u << k;
+            const bool need = (cont & bit) != 0;
+            if (__ballot(need) == 0) continue;
+            const uint32_t gm = __builtin_amdgcn_readlane(G1, k);
+            const uint32_t pc0 = (!guards_on || (gm & 0xFFu) == GM_NONE) ? 0u : (gm >> 16);
+            const uint32_t base = __builtin_amdgcn_readlane(RO, k);
+            const uint32_t len = __builtin_amdgcn_readlane(RO, k + 1) - base;
+            const uint32_t code = run_rule<kPriv>(A, r0 + k, base, len, pc0, need, req, regs, tid);
+            if (need) {
+                m |= code == PC_TRUE ? bit : 0u;
+                e |= code >= PC_ERROR ? bit : 0u;
+            }
         }
         if (valid) {
             A.out_match[(uint64_t)g * A.n + req] = m;
             A.out_err[(uint64_t)g * A.n + req] = e;
         }
     }
+}
+
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    eval_tile<false>(A, regs);
+}
+
+// ablation (flags & 4): the VM register file in VGPRs instead of LDS
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel_vregs(mxp_kargs A) {
+    eval_tile<true>(A, nullptr);
 }
 
 // Per-rule hit counters: hits[rule] += popcount over requests of the rule's match bit, restricted
@@ -337,7 +476,10 @@ extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t
 }
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    if (args->flags & 4u)
+        hipLaunchKernelGGL(mxp_eval_kernel_vregs, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    else
+        hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

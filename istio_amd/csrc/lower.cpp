@@ -17,6 +17,7 @@
 #include <set>
 
 #include "goutil.h"
+#include "vmopt.h"
 #include "../../include/mxp_batch.h"
 
 namespace mxp {
@@ -552,6 +553,11 @@ class Lowerer {
             if (jumps && out[i].z <= i) throw Irregular{"non-forward jump after layout"};
         }
         code_ = out;
+        try {
+            optimize_vm(code_);
+        } catch (std::exception& e) {
+            throw Irregular{e.what()};
+        }
     }
 
     const IlProgram& p_;
@@ -578,7 +584,7 @@ LoweredRule lower_rule(const IlProgram& prog, LowerTables* tables) { return Lowe
 std::string vm_disasm(const std::vector<mxp_vm_ins>& code) {
     static const char* names[] = {"nop", "res", "tres", "vcol", "const", "eq", "eqk", "not", "jz", "jnz", "jmp",
                                   "ret", "lookup", "lookupk", "strfn", "strfnk", "ipof", "tsof", "ipeq", "tseq",
-                                  "err", "logic", "logick", "ftos", "stof"};
+                                  "err", "logic", "logick", "ftos", "stof", "jzret", "jnzret", "retk"};
     std::string o;
     char buf[160];
     for (size_t i = 0; i < code.size(); i++) {

@@ -41,7 +41,29 @@ enum mxp_vm_op {
     VM_LOGICK = 22,  // d <- r[a] (y) const x
     VM_FTOS = 23,    // d <- r[a] as string: interface value must hold a string (Go `.(string)`), else panic
     VM_STOF = 24,    // d <- interface handle of string r[a]
+    VM_JZRET = 25,   // r[a] == 0 -> finish with bool result y
+    VM_JNZRET = 26,  // r[a] != 0 -> finish with bool result y
+    VM_RETK = 27,    // finish with bool result y
 };
+
+// Leading-atom guard of a rule (vmopt.cpp): the rule's program starts with
+//   RES col (want S/B/I/D) | VCOL col ; EQK K ; [NOT]
+// followed by a decision.  The kernel evaluates the guards of a whole 32-rule group with vector
+// compares and runs the VM (from `cont`) only for lanes the guard leaves undecided.
+enum mxp_guard_mode {
+    GM_NONE = 0,  // run the whole program
+    GM_AND = 1,   // atom false -> result false; atom true -> continue at cont
+    GM_ONLY = 2,  // result = atom
+    GM_OR = 3,    // atom true -> result true; atom false -> continue at cont
+};
+#define GK_VCOL 5  // guard kind: virtual map[key] column (else a want class W_S..W_D)
+
+typedef struct mxp_guard {
+    uint32_t col;    // column index (resolve or virtual); bits 24..31: kind (W_* or GK_VCOL)
+    uint32_t mode;   // bits 0..7 mode, 8..15 negate, 16..31 continuation pc
+    uint32_t klo;    // constant (register value) compared against
+    uint32_t khi;
+} mxp_guard;
 
 // want classes for VM_RES / VM_TRES
 enum mxp_vm_want { W_S = 0, W_B = 1, W_I = 2, W_D = 3, W_F = 4 };

@@ -65,6 +65,12 @@ def test_golden_table_on_gpu(mxp):
         assert (st == 0).all(), [rows[i]["E"] for i in np.where(st != 0)[0]]
         batch = BagBatch.from_bags([{k: from_tagged(v) for k, v in r.get("I", {}).items()} for r in rows])
         vals, codes = eng.eval_values(batch)
+        # predicate mode (guards + VM) must agree with Eval mode on every bool row
+        pm, pe = eng.eval_batch(batch)
+        pcodes = mxp.bits_to_codes(pm, pe, len(rows))
+        for i, r in enumerate(rows):
+            if r.get("Type") == "BOOL" or "Err" in r:
+                assert pcodes[i, i] == min(int(codes[i, i]), 2), r["E"]
         for i, r in enumerate(rows):
             c = int(codes[i, i])
             if "Err" in r:
