@@ -105,6 +105,10 @@ int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_
 int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_requests, void* stream,
                     unsigned long long* d_hits);
 uint32_t mxp_rule_count(const mxp_engine* eng);
+/* Shape of the compiled rule set as the kernels see it: out[0] guarded rules (leading atom evaluated
+ * group-wide), out[1] rules with a continuation template, out[2] distinct templates, out[3] column
+ * segments.  Returns the number of values written (<= cap). */
+uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap);
 uint32_t mxp_dbatch_requests(const mxp_dbatch* db);
 
 #ifdef __cplusplus

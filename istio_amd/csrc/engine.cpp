@@ -28,6 +28,7 @@
 #include "vmopt.h"
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, hipStream_t s);
+extern "C" hipError_t mxp_launch_queue(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
                                       unsigned long long* hits, hipStream_t s);
 
@@ -64,6 +65,7 @@ struct TimeKey {
 };
 
 constexpr uint64_t kNoValue = ~0ull;
+constexpr uint32_t kQueueSub = 8192;  // pair sub-queues (one queue-kernel workgroup each)
 
 }  // namespace
 
@@ -111,10 +113,17 @@ struct mxp_engine : public mxp::LowerTables {
     bool need_ipof = false, need_tsof = false, need_strings = false, need_maps = false;
 
     DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
-    uint32_t n_guarded = 0;
-    uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS (ablation only; results are not valid with flags set)
+    DevBuf d_groups, d_segs, d_gk, d_tqmask, d_tmpls, d_rule_tmpl, d_rconst;
+    uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
+    // pair queue (phase 1 -> dense template phase 2); sized per batch, grown on demand
+    DevBuf d_queue, d_qcount;
+    uint64_t queue_cap = 0;
+    uint32_t queue_per_req = 64;  // MXP_QUEUE_PER_REQ
+    uint32_t dense_min = 32;      // MXP_DENSE_MIN
+    uint32_t groups_per_wave = 4; // MXP_GPW
+    uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS: ablation only (1 no VM, 2 no guards: results invalid; 8 no pair queue)
     DevBuf d_errlog, d_errcount;
-    uint32_t errcap = 1u << 20;
+    uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
 
     // last batch error details: key = request << 32 | rule
     std::unordered_map<uint64_t, std::pair<uint32_t, std::string>> last_errors;
@@ -275,6 +284,100 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     n_guarded = 0;
     for (auto& g : guards) n_guarded += (g.mode & 0xFF) != GM_NONE;
 
+    // continuation templates (vmopt.h hoist_continuation): rules whose continuations are identical
+    // up to constants share one program; template code is appended after the rules' programs
+    std::map<std::string, uint32_t> tmpl_ids;
+    std::vector<mxp_tmpl> tmpls;
+    std::vector<mxp_vm_ins> tcode;
+    std::vector<uint32_t> rule_tmpl(n, MXP_VM_DONE);
+    std::vector<uint64_t> rconst((size_t)n * MXP_VM_MAXREG, 0);
+    const uint32_t prog_end = (uint32_t)all.size();
+    n_templated = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t mode = guards[i].mode & 0xFF, pc0 = guards[i].mode >> 16;
+        if (mode != GM_AND && mode != GM_OR) continue;
+        std::vector<mxp_vm_ins> code(all.begin() + off[i], all.begin() + off[i + 1]);
+        mxp::HoistedCont h;
+        if (!mxp::hoist_continuation(code, pc0, &h)) continue;
+        uint32_t hdr[4] = {pc0, (uint32_t)code.size(), h.creg0, (uint32_t)h.consts.size()};
+        std::string key((const char*)hdr, sizeof hdr);
+        key.append((const char*)h.code.data(), h.code.size() * sizeof(mxp_vm_ins));
+        auto it = tmpl_ids.find(key);
+        uint32_t id;
+        if (it != tmpl_ids.end()) {
+            id = it->second;
+        } else {
+            id = (uint32_t)tmpls.size();
+            tmpl_ids.emplace(key, id);
+            mxp_tmpl t{};
+            t.off = prog_end + (uint32_t)tcode.size();
+            t.pc0 = pc0;
+            t.len = (uint32_t)code.size();
+            t.nconst = (uint32_t)h.consts.size();
+            t.creg0 = h.creg0;
+            tmpls.push_back(t);
+            tcode.insert(tcode.end(), h.code.begin(), h.code.end());
+        }
+        rule_tmpl[i] = id;
+        for (size_t j = 0; j < h.consts.size(); j++) rconst[(size_t)i * MXP_VM_MAXREG + j] = h.consts[j];
+        n_templated++;
+    }
+    n_tmpls = (uint32_t)tmpls.size();
+    all.insert(all.end(), tcode.begin(), tcode.end());
+
+    // phase-1 group tables: mode masks, column segments, guard constants, template masks
+    const uint32_t W = (n + 31) / 32;
+    std::vector<mxp_group> groups(W);
+    std::vector<mxp_seg> segs;
+    std::vector<uint64_t> gk((size_t)W * 32, 0);
+    std::vector<uint32_t> tqmask;
+    for (uint32_t g = 0; g < W; g++) {
+        mxp_group& G = groups[g];
+        memset(&G, 0, sizeof G);
+        std::vector<std::pair<uint32_t, uint32_t>> seg_of;   // (col | kind << 24, rules)
+        std::vector<std::pair<uint32_t, uint32_t>> tq_of;    // (template, rules)
+        for (uint32_t k = 0; k < 32 && g * 32 + k < n; k++) {
+            const uint32_t r = g * 32 + k, bit = 1u << k;
+            const mxp_guard& gd = guards[r];
+            const uint32_t mode = gd.mode & 0xFF;
+            G.all |= bit;
+            if (mode == GM_NONE) continue;
+            G.guarded |= bit;
+            if (mode == GM_ONLY) G.only |= bit;
+            if (mode == GM_OR) G.orm |= bit;
+            if ((gd.mode >> 8) & 1) G.neg |= bit;
+            gk[r] = (uint64_t)gd.klo | ((uint64_t)gd.khi << 32);
+            auto sit = std::find_if(seg_of.begin(), seg_of.end(), [&](auto& p) { return p.first == gd.col; });
+            if (sit == seg_of.end()) seg_of.emplace_back(gd.col, bit);
+            else sit->second |= bit;
+            if (rule_tmpl[r] != MXP_VM_DONE) {
+                auto tit = std::find_if(tq_of.begin(), tq_of.end(), [&](auto& p) { return p.first == rule_tmpl[r]; });
+                if (tit == tq_of.end()) tq_of.emplace_back(rule_tmpl[r], bit);
+                else tit->second |= bit;
+            }
+        }
+        G.seg0 = (uint32_t)segs.size();
+        G.nseg = (uint32_t)seg_of.size();
+        for (auto& p : seg_of) {
+            mxp_seg sg{};
+            sg.col = p.first & 0xFFFFFFu;
+            sg.kind = p.first >> 24;
+            sg.rules = p.second;
+            switch (sg.kind) {
+            case W_S: sg.okset = 1u << MXP_STRING; break;
+            case W_B: sg.okset = 1u << MXP_BOOL; break;
+            case W_I: sg.okset = (1u << MXP_INT64) | (1u << MXP_DURATION); break;
+            case W_D: sg.okset = 1u << MXP_DOUBLE; break;
+            default: sg.okset = 1u << VC_VALUE; break;  // GK_VCOL
+            }
+            segs.push_back(sg);
+        }
+        G.tq0 = (uint32_t)tqmask.size();
+        G.ntq = (uint32_t)tq_of.size();
+        for (auto& p : tq_of) tqmask.push_back(p.second);
+    }
+    n_segs = (uint32_t)segs.size();
+
     have_rules = true;
     if (device < 0) return MXP_OK;  // host-only engine: compile / inspect, no device tables
     // upload program + global string pool
@@ -283,10 +386,20 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((e = hipSetDevice(device)) != hipSuccess) return hipfail(e, "hipSetDevice");
     if ((e = d_prog.alloc(all.size() * sizeof(mxp_vm_ins))) != hipSuccess) return hipfail(e, "hipMalloc prog");
     if ((e = d_rule_off.alloc(off.size() * 4)) != hipSuccess) return hipfail(e, "hipMalloc rule_off");
-    if ((e = d_guards.alloc(guards.size() * sizeof(mxp_guard))) != hipSuccess) return hipfail(e, "hipMalloc guards");
-    if (!guards.empty() &&
-        (e = hipMemcpy(d_guards.p, guards.data(), guards.size() * sizeof(mxp_guard), hipMemcpyHostToDevice)) != hipSuccess)
-        return hipfail(e, "upload guards");
+    auto put = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
+        if ((e = d.alloc(bytes ? bytes : 16)) != hipSuccess) return hipfail(e, what);
+        if (bytes && (e = hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice)) != hipSuccess) return hipfail(e, what);
+        return MXP_OK;
+    };
+    int rc;
+    if ((rc = put(d_guards, guards.data(), guards.size() * sizeof(mxp_guard), "upload guards"))) return rc;
+    if ((rc = put(d_groups, groups.data(), groups.size() * sizeof(mxp_group), "upload groups"))) return rc;
+    if ((rc = put(d_segs, segs.data(), segs.size() * sizeof(mxp_seg), "upload segs"))) return rc;
+    if ((rc = put(d_gk, gk.data(), gk.size() * 8, "upload gk"))) return rc;
+    if ((rc = put(d_tqmask, tqmask.data(), tqmask.size() * 4, "upload tqmask"))) return rc;
+    if ((rc = put(d_tmpls, tmpls.data(), tmpls.size() * sizeof(mxp_tmpl), "upload tmpls"))) return rc;
+    if ((rc = put(d_rule_tmpl, rule_tmpl.data(), rule_tmpl.size() * 4, "upload rule_tmpl"))) return rc;
+    if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
     std::vector<uint64_t> soff(gstrs.size() + 1, 0);
     std::string blob;
     for (size_t i = 0; i < gstrs.size(); i++) {
@@ -503,10 +616,18 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->prog = d_prog.as<mxp_vm_ins>();
     A->rule_off = d_rule_off.as<uint32_t>();
     A->guards = d_guards.as<mxp_guard>();
+    A->groups = d_groups.as<mxp_group>();
+    A->segs = d_segs.as<mxp_seg>();
+    A->gk = d_gk.as<uint64_t>();
+    A->tqmask = d_tqmask.as<uint32_t>();
+    A->tmpls = d_tmpls.as<mxp_tmpl>();
+    A->rule_tmpl = d_rule_tmpl.as<uint32_t>();
+    A->rconst = d_rconst.as<uint64_t>();
+    A->dense_min = dense_min;
     A->flags = debug_flags;
     A->n_rules = (uint32_t)rules.size();
     A->n_words = (A->n_rules + 31) / 32;
-    A->groups_per_wave = 1;
+    A->groups_per_wave = groups_per_wave;
     A->n = db->n;
     A->kinds = db->kinds.as<uint8_t>();
     A->vals = db->vals.as<uint64_t>();
@@ -542,9 +663,29 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         A.errcap = errcap;
     }
     if (A.n == 0 || A.n_rules == 0) return MXP_OK;
+    // pair queue: only in predicate mode, only when some rule has a continuation template
+    const bool use_queue = !d_vals && n_templated > 0 && !(debug_flags & 8u);
     const uint32_t gx = (A.n + 63) / 64;
+    uint32_t qsub = 0;
+    if (use_queue) {
+        qsub = std::min<uint32_t>(gx, kQueueSub);
+        const uint64_t want = std::min<uint64_t>(std::max<uint64_t>((uint64_t)A.n * queue_per_req, 1u << 10), 1u << 28);
+        if (want > queue_cap) {
+            if ((e = d_queue.alloc(want * 8)) != hipSuccess) return hipfail(e, "hipMalloc queue");
+            queue_cap = want;
+        }
+        if (!d_qcount.p && (e = d_qcount.alloc((size_t)kQueueSub * MXP_QSTRIDE * 4)) != hipSuccess)
+            return hipfail(e, "hipMalloc qcount");
+        if ((e = hipMemsetAsync(d_qcount.p, 0, (size_t)qsub * MXP_QSTRIDE * 4, s)) != hipSuccess)
+            return hipfail(e, "memset qcount");
+        A.queue = d_queue.as<uint2>();
+        A.qcount = d_qcount.as<uint32_t>();
+        A.qsub = qsub;
+        A.qsubcap = (uint32_t)(queue_cap / qsub);
+    }
     const uint32_t gy = (A.n_words + 4 * A.groups_per_wave - 1) / (4 * A.groups_per_wave);
     if ((e = mxp_launch_eval(&A, gx, gy, s)) != hipSuccess) return hipfail(e, "launch eval");
+    if (use_queue && (e = mxp_launch_queue(&A, qsub, s)) != hipSuccess) return hipfail(e, "launch queue");
     return MXP_OK;
 }
 
@@ -621,6 +762,11 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (!e) return MXP_ERR_NOMEM;
     e->device = device;
     if (const char* f = getenv("MXP_DEBUG_FLAGS")) e->debug_flags = (uint32_t)atoi(f);
+    // tuning knobs (results are identical for every setting)
+    if (const char* f = getenv("MXP_QUEUE_PER_REQ")) e->queue_per_req = (uint32_t)atoi(f);
+    if (const char* f = getenv("MXP_DENSE_MIN")) e->dense_min = (uint32_t)atoi(f);
+    if (const char* f = getenv("MXP_GPW")) e->groups_per_wave = std::max(1, atoi(f));
+    if (const char* f = getenv("MXP_ERRCAP")) e->errcap = (uint32_t)std::max(1, atoi(f));
     if (device < 0) {  // host-only engine (compiler / lowering inspection without a GPU)
         e->reset_tables();
         *out = e;
@@ -691,6 +837,14 @@ int mxp_rule_types(mxp_engine* eng, uint32_t rule, int32_t* vt, int32_t* il) {
 
 uint32_t mxp_rule_count(const mxp_engine* eng) { return eng ? (uint32_t)eng->rules.size() : 0; }
 uint32_t mxp_dbatch_requests(const mxp_dbatch* db) { return db ? db->n : 0; }
+
+uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
+    if (!eng || !out) return 0;
+    const uint32_t v[4] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs};
+    uint32_t k = 0;
+    for (; k < cap && k < 4; k++) out[k] = v[k];
+    return k;
+}
 
 int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out) {
     if (!eng || !batch || !out) return MXP_ERR_ARG;

@@ -83,30 +83,14 @@ __device__ __forceinline__ void log_err(const mxp_kargs& A, uint32_t req, uint32
 // constant-address-space views: uniform loads through them become scalar s_load_dwordxN
 typedef __attribute__((address_space(4))) const uint32_t cuint32;
 
-// Runs rule `rule` (program prog[base, base+len)) from `pc0` for the lanes in `live` (the others
-// keep their phase-1 result); returns the pair code of every lane that ran.
-//
-// Programs of up to 64 instructions are fetched ONCE with a coalesced vector load -- lane l holds
-// instruction l in four VGPRs -- and each step reads its instruction with v_readlane (no memory
-// latency on the dispatch path).  Longer programs fall back to scalar loads per step.
-template <bool kPriv>
-__device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t base, uint32_t len, uint32_t pc0,
-                             bool live, uint32_t req, uint64_t (*regs)[256], uint32_t tid) {
-    cuint32* prog = ((cuint32*)A.prog) + (uint64_t)base * 4u;
-    const bool inreg = len <= 64u;
-    uint32_t p0 = 0, p1 = 0, p2 = 0, p3 = 0;
-    if (inreg) {
-        const uint32_t lane = tid & 63u;
-        if (lane < len) {
-            const uint4 v = ((const uint4*)A.prog)[(uint64_t)base + lane];
-            p0 = v.x;
-            p1 = v.y;
-            p2 = v.z;
-            p3 = v.w;
-        }
-    }
-    uint64_t R[MXP_VM_MAXREG];  // kPriv: register file in VGPRs (uniform index -> s_set_gpr_idx)
-#define REG(i) (kPriv ? R[i] : regs[i][tid])
+// Runs one program from `pc0` for the lanes in `live` (the others keep their phase-1 result) and
+// returns the pair code of every lane that ran.  The program is wave-uniform: instruction pc is
+// P[pc] (pc in [pc0, len)), fetched with one scalar s_load_dwordx4 per step.  `rule` may differ
+// per lane (template batches of the pair queue); it only names the pair in error records and
+// Eval results.  The register file is regs[reg][thread] in LDS.
+__device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint32_t pc0, bool live, uint32_t rule,
+                             uint32_t req, uint64_t (*regs)[256], uint32_t tid) {
+#define REG(i) regs[i][tid]
     const uint64_t N = A.n;
     uint32_t wait = live ? pc0 : MXP_VM_DONE;
     uint32_t res = PC_FALSE;
@@ -137,19 +121,9 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t base, u
     } while (0)
 
     while (pc < len) {
-        uint32_t w0, x, y, z;
-        if (inreg) {
-            w0 = __builtin_amdgcn_readlane(p0, pc);
-            x = __builtin_amdgcn_readlane(p1, pc);
-            y = __builtin_amdgcn_readlane(p2, pc);
-            z = __builtin_amdgcn_readlane(p3, pc);
-        } else {
-            cuint32* ip = prog + (uint64_t)pc * 4u;
-            w0 = uni(ip[0]);
-            x = uni(ip[1]);
-            y = uni(ip[2]);
-            z = uni(ip[3]);
-        }
+        cuint32* ip = P + (uint64_t)pc * 4u;
+        const uint32_t w0 = uni(ip[0]);
+        const uint32_t x = uni(ip[1]), y = uni(ip[2]), z = uni(ip[3]);
         const uint32_t op = w0 & 0x7Fu;
         const uint32_t d = (w0 >> 8) & 0xFFu, a = (w0 >> 16) & 0xFFu, b = w0 >> 24;
         if (w0 & MXP_VM_WAKE) live = live || (wait == pc);
@@ -317,6 +291,9 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t base, u
         case VM_STOF:
             if (live) REG(d) = MXP_FH(MXP_STRING, REG(a));
             break;
+        case VM_MOV:
+            if (live) REG(d) = REG(a);
+            break;
         default:
             break;
         }
@@ -333,114 +310,223 @@ __device__ uint32_t run_rule(const mxp_kargs& A, uint32_t rule, uint32_t base, u
 }  // namespace
 
 // Phase 1 (guards) + phase 2 (VM for undecided lanes) over 32-rule groups.
-template <bool kPriv>
-__device__ __forceinline__ void eval_tile(const mxp_kargs& A, uint64_t (*regs)[256]) {
+namespace {
+
+typedef __attribute__((address_space(4))) const uint64_t cuint64;
+
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v |= (uint32_t)__shfl_xor((int)v, off, 64);
+    return uni(v);
+}
+
+// inclusive prefix sum over the 64 lanes
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v, uint32_t lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)v, off, 64);
+        if (lane >= (uint32_t)off) v += t;
+    }
+    return v;
+}
+
+// Bits k of `rules` whose guard constant K[k] equals this lane's column value.  Wide segments
+// compare against all 32 constants (scalar-loaded, one v_cmp_eq_u64 + select each); narrow ones
+// walk their rule bits.
+__device__ __forceinline__ uint32_t seg_eq(cuint64* K, uint32_t rules, uint64_t cv) {
+    uint32_t eq = 0;
+    if (__builtin_popcount(rules) >= 8) {
+        for (int c = 0; c < 32; c += 8) {
+            if (((rules >> c) & 0xFFu) == 0) continue;
+#pragma unroll
+            for (int k = 0; k < 8; k++) eq |= (cv == K[c + k]) ? (1u << (c + k)) : 0u;
+        }
+        return eq & rules;
+    }
+    for (uint32_t r = rules; r; r &= r - 1) {
+        const uint32_t k = __builtin_ctz(r);
+        eq |= (cv == K[k]) ? (1u << k) : 0u;
+    }
+    return eq;
+}
+
+// Error records of the rules whose guard column failed for this lane (missing attribute, wrong
+// dynamic type, map attribute that is not a map): the same codes the VM's RES / VCOL raise.
+__device__ __forceinline__ void log_guard_errors(const mxp_kargs& A, uint32_t e, uint32_t r0, uint32_t req) {
+    for (uint32_t bits = e; bits; bits &= bits - 1) {
+        const uint32_t r = r0 + __builtin_ctz(bits);
+        const mxp_guard G = A.guards[r];
+        const uint32_t col = G.col & 0xFFFFFFu, gk = G.col >> 24;
+        const uint32_t ck = A.kinds[(uint64_t)col * A.n + req];
+        uint32_t code, aux;
+        if (gk == GK_VCOL) {
+            code = ck == VC_ABSENT ? ERR_LOOKUP : PANIC_MAPTYPE;
+            aux = 0;
+        } else {
+            code = ck == MXP_ABSENT ? ERR_LOOKUP : ERR_CONV_S + gk;
+            aux = col;
+        }
+        if (code == ERR_LOOKUP) aux = A.prog[A.rule_off[r]].z;
+        log_err(A, req, r, code, aux);
+    }
+}
+
+}  // namespace
+
+// Phase 1 + in-wave phase 2 over 32-rule groups.
+//
+// Workgroup = 4 wavefronts over one tile of 64 requests (one per lane); wave w sweeps groups
+// [g0, g0 + groups_per_wave).  Per group:
+//   phase 1  every rule's leading atom at once: each column segment loads its column value once per
+//            lane and compares it with the segment's constants (scalar operands), giving per lane the
+//            32-bit words eq / ok; the group's mode masks turn them into match / error / continue
+//            words with a handful of bit operations;
+//   hand-off continuing pairs of templated rules whose survivors are sparse in this tile go to the
+//            pair queue (evaluated densely by mxp_queue_kernel);
+//   phase 2  the VM runs, rule by rule, for the remaining continuing lanes.
+// Results: one coalesced store per word and plane, out[g * N + request].
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
     const uint32_t wave = uni(tid >> 6);
-    const uint32_t req = blockIdx.x * 64u + (tid & 63u);
+    const uint32_t req = blockIdx.x * 64u + lane;
     const bool valid = req < A.n;
     const uint64_t N = A.n;
     const uint32_t g0 = (blockIdx.y * 4u + wave) * A.groups_per_wave;
     const uint32_t g1 = min(g0 + A.groups_per_wave, A.n_words);
-    const uint32_t lane = tid & 63u;
-    // Eval mode (out_vals) needs every result register: run whole programs
+    // Eval mode (out_vals) needs every result register: whole programs, no guards, no queue
     const bool guards_on = !(A.out_vals || (A.flags & 2u));
+    const bool queue_on = guards_on && A.queue != nullptr;
+    uint32_t cached = MXP_VM_DONE;
+    uint32_t ck = MXP_ABSENT;
+    uint64_t cv = 0;
     for (uint32_t g = g0; g < g1; g++) {
-        const uint32_t r0 = g * 32u, nr = min(32u, A.n_rules - r0);
-        // the group's guards (lane k < 32: guard k) and rule offsets (lane k <= 32: rule_off[r0 + k])
-        // in VGPRs, read back per rule with v_readlane
-        uint32_t G0 = 0, G1 = GM_NONE, G2 = 0, G3 = 0, RO = 0;
-        if (lane < nr) {
-            const uint4 v = ((const uint4*)A.guards)[r0 + lane];
-            G0 = v.x;
-            G1 = v.y;
-            G2 = v.z;
-            G3 = v.w;
-        }
-        if (lane <= nr) RO = A.rule_off[r0 + lane];
+        const mxp_group* G = A.groups + g;
+        const uint32_t all = uni(G->all), guarded = uni(G->guarded), only = uni(G->only), orm = uni(G->orm),
+                       neg = uni(G->neg), seg0 = uni(G->seg0), nseg = uni(G->nseg);
+        const uint32_t r0 = g * 32u;
         uint32_t m = 0, e = 0, cont = 0;
-        // ---- phase 1: leading atoms of the whole group: vector compares against scalar constants
-        uint32_t cached = MXP_VM_DONE;
-        uint32_t ck = 0;
-        uint64_t cv = 0;
-        for (uint32_t k = 0; k < nr; k++) {
-            const uint32_t gc = __builtin_amdgcn_readlane(G0, k), gm = __builtin_amdgcn_readlane(G1, k);
-            const uint64_t K = (uint64_t)__builtin_amdgcn_readlane(G2, k) |
-                               ((uint64_t)__builtin_amdgcn_readlane(G3, k) << 32);
-            const uint32_t mode = guards_on ? (gm & 0xFFu) : (uint32_t)GM_NONE;
-            const uint32_t bit = 1u << k;
-            if (mode == GM_NONE) {
-                cont |= valid ? bit : 0u;
-                continue;
-            }
-            const uint32_t col = gc & 0xFFFFFFu, gk = gc >> 24;
-            if (col != cached) {
-                cached = col;
-                if (valid) {
-                    ck = A.kinds[(uint64_t)col * N + req];
-                    cv = A.vals[(uint64_t)col * N + req];
-                }
-            }
-            bool ok;
-            uint32_t ecode = 0;
-            if (gk == GK_VCOL) {
-                ok = ck == VC_VALUE;
-                if (!ok) ecode = ck == VC_ABSENT ? ERR_LOOKUP : PANIC_MAPTYPE;
-            } else {
-                ok = gk == W_S ? ck == MXP_STRING : gk == W_B ? ck == MXP_BOOL
-                     : gk == W_I ? (ck == MXP_INT64 || ck == MXP_DURATION) : ck == MXP_DOUBLE;
-                if (!ok) ecode = ck == MXP_ABSENT ? ERR_LOOKUP : ERR_CONV_S + gk;
-            }
-            const bool atom = (cv == K) != (((gm >> 8) & 1u) != 0);
-            if (valid) {
-                if (!ok) {
-                    e |= bit;
-                    if (A.errlog) {
-                        const uint32_t aux = ecode == ERR_LOOKUP
-                                                 ? A.prog[__builtin_amdgcn_readlane(RO, k)].z
-                                                 : (gk == GK_VCOL ? 0u : col);
-                        log_err(A, req, r0 + k, ecode, aux);
+        if (guards_on) {
+            // ---- phase 1
+            uint32_t eq = 0, ok = 0;
+            for (uint32_t s = seg0; s < seg0 + nseg; s++) {
+                const uint32_t col = uni(A.segs[s].col), okset = uni(A.segs[s].okset), rules = uni(A.segs[s].rules);
+                if (col != cached) {
+                    cached = col;
+                    if (valid) {
+                        ck = A.kinds[(uint64_t)col * N + req];
+                        cv = A.vals[(uint64_t)col * N + req];
                     }
-                } else if (mode == GM_ONLY) {
-                    m |= atom ? bit : 0u;
-                } else if (mode == GM_AND) {
-                    cont |= atom ? bit : 0u;
-                } else {  // GM_OR
-                    m |= atom ? bit : 0u;
-                    cont |= atom ? 0u : bit;
+                }
+                ok |= ((okset >> ck) & 1u) ? rules : 0u;
+                eq |= seg_eq((cuint64*)A.gk + r0, rules, cv);
+            }
+            const uint32_t atom = eq ^ neg;
+            const uint32_t andm = guarded & ~(only | orm);
+            m = atom & (only | orm) & ok;
+            cont = (((atom & andm) | (~atom & orm)) & ok) | (all & ~guarded);
+            e = guarded & ~ok;
+            if (!valid) m = e = cont = 0;
+            if (e && A.errlog) log_guard_errors(A, e, r0, req);
+        } else {
+            cont = valid ? all : 0u;
+        }
+        // ---- hand-off to the pair queue
+        uint32_t inwave = cont;
+        if (queue_on) {
+            const uint32_t tq0 = uni(G->tq0), ntq = uni(G->ntq);
+            for (uint32_t j = tq0; j < tq0 + ntq; j++) {
+                uint32_t qb = cont & uni(A.tqmask[j]);
+                const uint32_t anyq = wave_or(qb);
+                if (anyq == 0) continue;
+                // rules with many survivors in this tile run in-wave (dense enough already)
+                for (uint32_t bits = anyq; bits; bits &= bits - 1) {
+                    const uint32_t k = __builtin_ctz(bits);
+                    const uint64_t bal = __ballot((qb >> k) & 1u);
+                    if ((uint32_t)__popcll(bal) >= A.dense_min) qb &= ~(1u << k);
+                }
+                const uint32_t cnt = __builtin_popcount(qb);
+                const uint32_t incl = wave_incl_sum(cnt, lane);
+                const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+                if (total == 0) continue;
+                const uint32_t sq = blockIdx.x % A.qsub;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(A.qcount + (uint64_t)sq * MXP_QSTRIDE, total);
+                base = uni(base);
+                uint2* Q = A.queue + (uint64_t)sq * A.qsubcap;
+                uint32_t pos = base + incl - cnt;
+                for (uint32_t bits = qb; bits && pos < A.qsubcap; bits &= bits - 1, pos++) {
+                    const uint32_t k = __builtin_ctz(bits);
+                    Q[pos] = make_uint2(req, r0 + k);
+                    inwave &= ~(1u << k);
                 }
             }
         }
-        // ---- phase 2: the VM, only for rules some lane still needs
-        for (uint32_t k = 0; k < nr && !(A.flags & 1u); k++) {
+        // ---- phase 2 (in-wave)
+        for (uint32_t bits = wave_or(inwave); bits && !(A.flags & 1u); bits &= bits - 1) {
+            const uint32_t k = __builtin_ctz(bits);
             const uint32_t bit = 1u << k;
-            const bool need = (cont & bit) != 0;
-            if (__ballot(need) == 0) continue;
-            const uint32_t gm = __builtin_amdgcn_readlane(G1, k);
+            const bool need = (inwave & bit) != 0;
+            const uint32_t rule = r0 + k;
+            const uint32_t gm = uni(A.guards[rule].mode);
             const uint32_t pc0 = (!guards_on || (gm & 0xFFu) == GM_NONE) ? 0u : (gm >> 16);
-            const uint32_t base = __builtin_amdgcn_readlane(RO, k);
-            const uint32_t len = __builtin_amdgcn_readlane(RO, k + 1) - base;
-            const uint32_t code = run_rule<kPriv>(A, r0 + k, base, len, pc0, need, req, regs, tid);
+            const uint32_t base = uni(A.rule_off[rule]);
+            const uint32_t len = uni(A.rule_off[rule + 1]) - base;
+            const uint32_t code = run_rule(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, pc0, need, rule, req,
+                                           regs, tid);
             if (need) {
                 m |= code == PC_TRUE ? bit : 0u;
                 e |= code >= PC_ERROR ? bit : 0u;
             }
         }
         if (valid) {
-            A.out_match[(uint64_t)g * A.n + req] = m;
-            A.out_err[(uint64_t)g * A.n + req] = e;
+            if (A.out_match) A.out_match[(uint64_t)g * N + req] = m;
+            if (A.out_err) A.out_err[(uint64_t)g * N + req] = e;
         }
     }
 }
 
-extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
+// Dense phase 2 for the pair queue: one workgroup per sub-queue, each wavefront takes 64 queued
+// (request, rule) pairs at a time; lanes whose rules share a continuation template run that
+// template's program together (constants of each lane's own rule preloaded into its registers),
+// one template after another.  Results land
+// with atomicOr in the bitmaps mxp_eval_kernel wrote (same stream, so its stores are complete).
+extern "C" __global__ __launch_bounds__(256) void mxp_queue_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
-    eval_tile<false>(A, regs);
-}
-
-// ablation (flags & 4): the VM register file in VGPRs instead of LDS
-extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel_vregs(mxp_kargs A) {
-    eval_tile<true>(A, nullptr);
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = uni(tid >> 6);
+    const uint32_t sq = blockIdx.x;  // one workgroup per sub-queue; its 4 waves stride over the batches
+    const uint32_t n = min(uni(A.qcount[(uint64_t)sq * MXP_QSTRIDE]), A.qsubcap);
+    const uint2* Q = A.queue + (uint64_t)sq * A.qsubcap;
+    const uint64_t N = A.n;
+    for (uint32_t b = wave; b * 64u < n; b += 4u) {
+        const uint32_t i = b * 64u + lane;
+        bool pending = i < n;
+        uint2 en = make_uint2(0, 0);
+        if (pending) en = Q[i];
+        const uint32_t req = en.x, rule = en.y;
+        const uint32_t t = pending ? A.rule_tmpl[rule] : MXP_VM_DONE;
+        for (uint64_t bal = __ballot(pending); bal; bal = __ballot(pending)) {
+            const uint32_t tt = __builtin_amdgcn_readlane(t, (uint32_t)__builtin_ctzll(bal));
+            const bool mine = pending && t == tt;
+            const mxp_tmpl* T = A.tmpls + tt;
+            const uint32_t off = uni(T->off), pc0 = uni(T->pc0), len = uni(T->len), nconst = uni(T->nconst),
+                           creg0 = uni(T->creg0);
+            if (mine)
+                for (uint32_t j = 0; j < nconst; j++) regs[creg0 + j][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + j];
+            cuint32* P = ((cuint32*)A.prog) + ((uint64_t)off - pc0) * 4u;
+            const uint32_t code = run_rule(A, P, len, pc0, mine, rule, req, regs, tid);
+            if (mine) {
+                const uint64_t w = (uint64_t)(rule >> 5) * N + req;
+                const uint32_t bit = 1u << (rule & 31u);
+                if (code == PC_TRUE && A.out_match) atomicOr(A.out_match + w, bit);
+                if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
+            }
+            pending = pending && !mine;
+        }
+    }
 }
 
 // Per-rule hit counters: hits[rule] += popcount over requests of the rule's match bit, restricted
@@ -476,10 +562,12 @@ extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t
 }
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, hipStream_t s) {
-    if (args->flags & 4u)
-        hipLaunchKernelGGL(mxp_eval_kernel_vregs, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
-    else
-        hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_queue(const mxp_kargs* args, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_queue_kernel, dim3(grid), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

@@ -44,6 +44,7 @@ enum mxp_vm_op {
     VM_JZRET = 25,   // r[a] == 0 -> finish with bool result y
     VM_JNZRET = 26,  // r[a] != 0 -> finish with bool result y
     VM_RETK = 27,    // finish with bool result y
+    VM_MOV = 28,     // d <- r[a]                 (templates: hoisted CONST)
 };
 
 // Leading-atom guard of a rule (vmopt.cpp): the rule's program starts with
@@ -64,6 +65,44 @@ typedef struct mxp_guard {
     uint32_t klo;    // constant (register value) compared against
     uint32_t khi;
 } mxp_guard;
+
+// Per 32-rule group: the guard masks the kernel's phase 1 works with (bit k = rule 32 g + k), and
+// the group's guarded rules split into column segments (runs of rules whose guard reads the same
+// column with the same want class), so each segment loads its column once and compares all its
+// rules' constants (kargs.gk[32 g + k]) against it.
+typedef struct mxp_group {
+    uint32_t all;      // rules present in the group
+    uint32_t guarded;  // mode != GM_NONE
+    uint32_t only;     // GM_ONLY
+    uint32_t orm;      // GM_OR  (GM_AND = guarded & ~only & ~orm)
+    uint32_t neg;      // negated atoms
+    uint32_t seg0;     // segments [seg0, seg0 + nseg) of kargs.segs
+    uint32_t nseg;
+    uint32_t tq0;      // template masks [tq0, tq0 + ntq) of kargs.tqmask: continuation rules of one
+    uint32_t ntq;      //   template each, handed to the pair queue when their survivors are sparse
+    uint32_t pad[3];
+} mxp_group;
+
+typedef struct mxp_seg {
+    uint32_t col;      // column read by the guards of the segment
+    uint32_t okset;    // bit (kind) set when a column value of that kind passes the want class
+    uint32_t rules;    // rules of the group in this segment
+    uint32_t kind;     // want class (W_*) or GK_VCOL, for the error code
+} mxp_seg;
+
+// Continuation templates: the continuations (code from the guard's cont pc) of many rules differ
+// only in constants (C2: the path prefix and the ip literal).  Hoisting every constant operand
+// into a register (EQK -> EQ, STRFNK -> STRFN, LOOKUPK -> LOOKUP, LOGICK -> LOGIC, CONST -> MOV)
+// makes them byte-identical; such rules share one template program and keep only a per-rule
+// constant vector, so survivors of DIFFERENT rules can run side by side in one wavefront.
+typedef struct mxp_tmpl {
+    uint32_t off;      // template code: prog[off - pc0 + pc] for pc >= pc0 (jump targets unchanged)
+    uint32_t pc0;      // continuation start
+    uint32_t len;      // program length (pcs < len)
+    uint32_t nconst;   // constants per rule, loaded into registers creg0 .. creg0 + nconst - 1
+    uint32_t creg0;
+    uint32_t pad[3];
+} mxp_tmpl;
 
 // want classes for VM_RES / VM_TRES
 enum mxp_vm_want { W_S = 0, W_B = 1, W_I = 2, W_D = 3, W_F = 4 };

@@ -26,6 +26,7 @@ static uint32_t reads(const mxp_vm_ins& i) {
         return (1u << i.a) | (1u << i.b);
     case VM_EQK: case VM_NOT: case VM_LOGICK: case VM_JZ: case VM_JNZ: case VM_RET: case VM_LOOKUPK:
     case VM_STRFNK: case VM_IPOF: case VM_TSOF: case VM_FTOS: case VM_STOF: case VM_JZRET: case VM_JNZRET:
+    case VM_MOV:
         return 1u << i.a;
     default:
         return 0;
@@ -36,7 +37,7 @@ static uint32_t writes(const mxp_vm_ins& i) {
     switch (opof(i)) {
     case VM_RES: case VM_TRES: case VM_VCOL: case VM_CONST: case VM_EQ: case VM_EQK: case VM_NOT: case VM_LOGIC:
     case VM_LOGICK: case VM_LOOKUP: case VM_LOOKUPK: case VM_STRFN: case VM_STRFNK: case VM_IPOF: case VM_TSOF:
-    case VM_IPEQ: case VM_TSEQ: case VM_FTOS: case VM_STOF:
+    case VM_IPEQ: case VM_TSEQ: case VM_FTOS: case VM_STOF: case VM_MOV:
         return 1u << i.d;
     default:
         return 0;
@@ -47,7 +48,7 @@ static uint32_t writes(const mxp_vm_ins& i) {
 static bool is_pure(const mxp_vm_ins& i) {
     switch (opof(i)) {
     case VM_CONST: case VM_EQ: case VM_EQK: case VM_NOT: case VM_LOGIC: case VM_LOGICK: case VM_STRFN:
-    case VM_STRFNK: case VM_STOF: case VM_NOP:
+    case VM_STRFNK: case VM_STOF: case VM_NOP: case VM_MOV:
         return true;
     default:
         return false;
@@ -275,6 +276,33 @@ mxp_guard extract_guard(const std::vector<mxp_vm_ins>& c) {
     g.klo = b.y;
     g.khi = b.z;
     return g;
+}
+
+bool hoist_continuation(const std::vector<mxp_vm_ins>& code, uint32_t pc0, HoistedCont* out) {
+    out->code.assign(code.begin() + pc0, code.end());
+    out->consts.clear();
+    uint32_t used = 0;
+    for (const auto& i : out->code) used |= reads(i) | writes(i);
+    uint32_t next = 0;
+    while (used >> next) next++;
+    out->creg0 = next;
+    for (auto& i : out->code) {
+        const uint8_t wake = i.op & MXP_VM_WAKE;
+        uint64_t k;
+        switch (opof(i)) {
+        case VM_EQK: k = (uint64_t)i.y | ((uint64_t)i.z << 32); i.op = VM_EQ; i.b = (uint8_t)next; i.y = i.z = 0; break;
+        case VM_STRFNK: k = i.x; i.op = VM_STRFN; i.b = (uint8_t)next; i.x = 0; break;
+        case VM_LOOKUPK: k = i.x; i.op = VM_LOOKUP; i.b = (uint8_t)next; i.x = 0; break;
+        case VM_LOGICK: k = i.x; i.op = VM_LOGIC; i.b = (uint8_t)next; i.x = 0; break;
+        case VM_CONST: k = (uint64_t)i.y | ((uint64_t)i.z << 32); i.op = VM_MOV; i.a = (uint8_t)next; i.y = i.z = 0; break;
+        default: continue;
+        }
+        if (next >= MXP_VM_MAXREG) return false;
+        i.op |= wake;
+        out->consts.push_back(k);
+        next++;
+    }
+    return true;
 }
 
 }  // namespace mxp

@@ -17,4 +17,15 @@ mxp_guard extract_guard(const std::vector<mxp_vm_ins>& code);
 
 bool vm_is_jump(const mxp_vm_ins& i);
 
+// Continuation template of a guarded rule: code[pc0, end) with every constant operand hoisted into
+// a fresh register (EQK -> EQ, STRFNK -> STRFN, LOOKUPK -> LOOKUP, LOGICK -> LOGIC, CONST -> MOV),
+// consts[j] being the value register creg0 + j must hold.  Jump targets keep their absolute pcs.
+// Returns false when the continuation has no room for the extra registers.
+struct HoistedCont {
+    std::vector<mxp_vm_ins> code;
+    std::vector<uint64_t> consts;
+    uint32_t creg0 = 0;
+};
+bool hoist_continuation(const std::vector<mxp_vm_ins>& code, uint32_t pc0, HoistedCont* out);
+
 }  // namespace mxp

@@ -52,6 +52,7 @@ SIGNATURES = {
     "mxp_hits_device": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP]),
     "mxp_rule_count": (ctypes.c_uint32, [_VP]),
     "mxp_dbatch_requests": (ctypes.c_uint32, [_VP]),
+    "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
 }
 
 _LIB = None
@@ -150,6 +151,12 @@ class Engine:
         vt, il = ctypes.c_int32(), ctypes.c_int32()
         self._check(self.lib.mxp_rule_types(self.h, rule, ctypes.byref(vt), ctypes.byref(il)), "mxp_rule_types")
         return vt.value, il.value
+
+    def ruleset_info(self) -> dict:
+        """Kernel-side shape of the rule set (guards, continuation templates, column segments)."""
+        out = (ctypes.c_uint32 * 4)()
+        k = self.lib.mxp_ruleset_info(self.h, out, 4)
+        return dict(zip(("guarded", "templated", "templates", "segments"), list(out)[:k]))
 
     # ------------------------------------------------------------------ evaluation
     def eval_batch(self, batch: BagBatch):

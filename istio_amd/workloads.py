@@ -245,6 +245,38 @@ def fuzz_rules(n, seed=7, depth=3):
     return [f.expr(depth) for _ in range(n)]
 
 
+def guarded_fuzz_rules(n, seed=11, depth=2):
+    """Rules whose programs start with a leading atom (guard) -- `attr == K`, `attr != K`,
+    `map["k"] == K` -- joined by &&, || or alone to a continuation that is either random or one of a
+    few constant-varying shapes (so continuation templates are shared).  Columns, want classes,
+    negations and modes mix inside every 32-rule group."""
+    rng = np.random.default_rng(seed)
+    f = _Fuzz(rng)
+    guards = [lambda: 'as == "%s"' % f.pick(_STR_VALS),
+              lambda: 'bs != "%s"' % f.pick(_STR_VALS),
+              lambda: 'ar["%s"] == "%s"' % (f.pick(_KEYS), f.pick(_STR_VALS)),
+              lambda: 'sm["%s"] != "%s"' % (f.pick(_KEYS), f.pick(_STR_VALS)),
+              lambda: "ai == %d" % int(rng.integers(0, 5)),
+              lambda: "ab == %s" % f.pick(["true", "false"]),
+              lambda: "ad == %s" % f.pick(["1.5", "2.5", "0.0"])]
+    shapes = [lambda: '%s.startsWith("%s") && aip != ip("%s")' % (f.pick(["as", "bs"]), f.pick(["a", "ab", "st", ""]),
+                                                                   f.pick(["1.2.3.4", "10.0.0.1"])),
+              lambda: 'br["%s"] == "%s"' % (f.pick(_KEYS), f.pick(_STR_VALS)),
+              lambda: 'match(bs, "%s") || bi == %d' % (f.pick(["a*", "*c", "abc", "*"]), int(rng.integers(0, 5))),
+              lambda: f.expr(depth)]
+    out = []
+    for _ in range(n):
+        g = f.pick(guards)()
+        r = rng.random()
+        if r < 0.1:
+            out.append(g)
+        elif r < 0.75:
+            out.append("%s && %s" % (g, f.pick(shapes)()))
+        else:
+            out.append("%s || %s" % (g, f.pick(shapes)()))
+    return out
+
+
 def fuzz_bags(n, seed=8):
     rng = np.random.default_rng(seed)
     f = _Fuzz(rng)
