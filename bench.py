@@ -58,6 +58,19 @@ def cpu_baseline(manifest, rules, batch, seconds, threads):
                 done, len(rules), dt)}
 
 
+def measured_traffic(rules, requests):
+    """HBM bytes per evaluation from the committed PMC profile (tools/pmc_summarize.py: FETCH_SIZE
+    and WRITE_SIZE in separate rocprofv3 passes, FETCH doubled for gfx950), when one exists for this
+    workload size; else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    if d.get("rules") != rules or d.get("requests") != requests:
+        return None
+    return d.get("bytes_per_eval")
+
+
 def main():
     args = parse()
     import numpy as np
@@ -130,12 +143,26 @@ def main():
 
     pairs_total = world * N * R * args.steps
     value = pairs_total / elapsed
-    # algorithmic bytes of one eval launch: packed columns read (kind u8 + value u64 per referenced
-    # column per request), the rule program, and the two output bitmaps written
+
+    # per-kernel durations (HIP events recorded by libmxp around each launch, on `stream`), in a
+    # separate pass so the timed region above carries no extra synchronisation
+    eng.set_timing(True)
+    per = []
+    for _ in range(args.steps):
+        db.eval(d_match.data_ptr(), d_err.data_ptr(), sh)
+        per.append(eng.kernel_times())
+    eng.set_timing(False)
+    k_eval = float(np.mean([p[0] for p in per]))
+    k_queue = float(np.mean([p[1] for p in per])) if per and len(per[0]) > 1 else 0.0
+    eval_ms = k_eval + k_queue
+
+    # algorithmic bytes of one evaluation: every referenced column read once per
+    # request (kind u8 + value u64), the rule tables, and the two output bitmaps written
     n_cols = 3
     prog_bytes = 16 * sum(eng.rule_vm_text(i).count("\n") for i in range(R)) + 4 * (R + 1)
     alg_bytes = N * n_cols * 9 + prog_bytes + 2 * N * Wd * 4
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    achieved = alg_bytes / (eval_ms * 1e-3) / 1e9
+    traffic = measured_traffic(R, N)
 
     out = {
         "metric": "request x rule predicate evals/sec at 10k rules",
@@ -152,10 +179,12 @@ def main():
         "data": "synthetic (seeded C2 rule family; requests resident in HBM)",
         "config": {"workload": "C2 rules scaled to R=%d, %d requests per GPU (configs[1] family, configs[4] shard)" % (R, N),
                    "rules": R, "requests_per_gpu": N, "parallelism": "request-sharded dp%d" % world},
-        "kernel_ms": kernel_ms,
+        "eval_ms": kernel_ms,
+        "kernels_ms": {"mxp_eval_kernel": k_eval, "mxp_queue_kernel": k_queue},
         "pack_upload_s": t_pack,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "mxp_eval_kernel + mxp_queue_kernel (one evaluation)",
                      "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pair": alg_bytes / (N * R)},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:

@@ -121,6 +121,10 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t queue_per_req = 64;  // MXP_QUEUE_PER_REQ
     uint32_t dense_min = 32;      // MXP_DENSE_MIN
     uint32_t groups_per_wave = 4; // MXP_GPW
+    // optional per-kernel timing of device evaluations (mxp_set_timing): events around each launch
+    bool timing = false;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool ev_queue = false;
     uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS: ablation only (1 no VM, 2 no guards: results invalid; 8 no pair queue)
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
@@ -684,8 +688,12 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         A.qsubcap = (uint32_t)(queue_cap / qsub);
     }
     const uint32_t gy = (A.n_words + 4 * A.groups_per_wave - 1) / (4 * A.groups_per_wave);
+    if (timing && (e = hipEventRecord(ev[0], s)) != hipSuccess) return hipfail(e, "event");
     if ((e = mxp_launch_eval(&A, gx, gy, s)) != hipSuccess) return hipfail(e, "launch eval");
+    if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
     if (use_queue && (e = mxp_launch_queue(&A, qsub, s)) != hipSuccess) return hipfail(e, "launch queue");
+    if (timing && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hipfail(e, "event");
+    ev_queue = use_queue;
     return MXP_OK;
 }
 
@@ -787,6 +795,8 @@ void mxp_engine_destroy(mxp_engine* eng) {
     if (!eng) return;
     if (eng->device >= 0) (void)hipSetDevice(eng->device);
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
+    for (auto& x : eng->ev)
+        if (x) (void)hipEventDestroy(x);
     delete eng;
 }
 
@@ -837,6 +847,32 @@ int mxp_rule_types(mxp_engine* eng, uint32_t rule, int32_t* vt, int32_t* il) {
 
 uint32_t mxp_rule_count(const mxp_engine* eng) { return eng ? (uint32_t)eng->rules.size() : 0; }
 uint32_t mxp_dbatch_requests(const mxp_dbatch* db) { return db ? db->n : 0; }
+
+int mxp_set_timing(mxp_engine* eng, int on) {
+    if (!eng || eng->device < 0) return MXP_ERR_ARG;
+    hipError_t e = hipSetDevice(eng->device);
+    if (e != hipSuccess) return eng->hipfail(e, "hipSetDevice");
+    for (auto& x : eng->ev)
+        if (on && !x && (e = hipEventCreate(&x)) != hipSuccess) return eng->hipfail(e, "hipEventCreate");
+    eng->timing = on != 0;
+    return MXP_OK;
+}
+
+int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) {
+    if (!eng || !ms || !n_out) return MXP_ERR_ARG;
+    *n_out = 0;
+    if (!eng->timing) return eng->fail(MXP_ERR_STATE, "timing not enabled");
+    hipError_t e;
+    float t[2] = {0.f, 0.f};
+    if ((e = hipEventSynchronize(eng->ev[2])) != hipSuccess) return eng->hipfail(e, "event sync");
+    if ((e = hipEventElapsedTime(&t[0], eng->ev[0], eng->ev[1])) != hipSuccess) return eng->hipfail(e, "elapsed");
+    if (eng->ev_queue && (e = hipEventElapsedTime(&t[1], eng->ev[1], eng->ev[2])) != hipSuccess)
+        return eng->hipfail(e, "elapsed");
+    uint32_t k = 0;
+    for (; k < cap && k < 2; k++) ms[k] = t[k];
+    *n_out = k;
+    return MXP_OK;
+}
 
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
     if (!eng || !out) return 0;

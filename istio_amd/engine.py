@@ -52,6 +52,8 @@ SIGNATURES = {
     "mxp_hits_device": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP]),
     "mxp_rule_count": (ctypes.c_uint32, [_VP]),
     "mxp_dbatch_requests": (ctypes.c_uint32, [_VP]),
+    "mxp_set_timing": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
 }
 
@@ -151,6 +153,16 @@ class Engine:
         vt, il = ctypes.c_int32(), ctypes.c_int32()
         self._check(self.lib.mxp_rule_types(self.h, rule, ctypes.byref(vt), ctypes.byref(il)), "mxp_rule_types")
         return vt.value, il.value
+
+    def set_timing(self, on: bool = True):
+        self._check(self.lib.mxp_set_timing(self.h, int(on)), "mxp_set_timing")
+
+    def kernel_times(self):
+        """[guard/VM kernel ms, pair-queue kernel ms] of the last device evaluation (timing on)."""
+        ms = (ctypes.c_float * 2)()
+        n = ctypes.c_uint32()
+        self._check(self.lib.mxp_kernel_times(self.h, ms, 2, ctypes.byref(n)), "mxp_kernel_times")
+        return list(ms)[: n.value]
 
     def ruleset_info(self) -> dict:
         """Kernel-side shape of the rule set (guards, continuation templates, column segments)."""
