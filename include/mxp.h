@@ -107,13 +107,13 @@ int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_request
 uint32_t mxp_rule_count(const mxp_engine* eng);
 /* Per-kernel timing of device evaluations (off by default): with timing on, every evaluation
  * records HIP events around its launches on the evaluation stream; mxp_kernel_times waits for the
- * last one and returns its kernel durations in ms: [0] guard/VM kernel, [1] pair-queue kernel
+ * last one and returns its kernel durations in ms: [0] guard/VM kernel, [1] guard-index kernel
  * (0 when it did not run).  *n_out = values written. */
 int mxp_set_timing(mxp_engine* eng, int on);
 int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out);
 /* Shape of the compiled rule set as the kernels see it: out[0] guarded rules (leading atom evaluated
  * group-wide), out[1] rules with a continuation template, out[2] distinct templates, out[3] column
- * segments.  Returns the number of values written (<= cap). */
+ * segments, out[4] rules served by the guard index.  Returns the number of values written (<= cap). */
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap);
 uint32_t mxp_dbatch_requests(const mxp_dbatch* db);
 

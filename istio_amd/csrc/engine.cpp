@@ -28,7 +28,7 @@
 #include "vmopt.h"
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, hipStream_t s);
-extern "C" hipError_t mxp_launch_queue(const mxp_kargs* args, uint32_t grid, hipStream_t s);
+extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
                                       unsigned long long* hits, hipStream_t s);
 
@@ -65,7 +65,17 @@ struct TimeKey {
 };
 
 constexpr uint64_t kNoValue = ~0ull;
-constexpr uint32_t kQueueSub = 8192;  // pair sub-queues (one queue-kernel workgroup each)
+
+// column kinds that pass a guard's want class (W_*) or a virtual-column guard (GK_VCOL)
+uint32_t okset_of(uint32_t kind) {
+    switch (kind) {
+    case W_S: return 1u << MXP_STRING;
+    case W_B: return 1u << MXP_BOOL;
+    case W_I: return (1u << MXP_INT64) | (1u << MXP_DURATION);
+    case W_D: return 1u << MXP_DOUBLE;
+    default: return 1u << VC_VALUE;  // GK_VCOL
+    }
+}
 
 }  // namespace
 
@@ -113,19 +123,15 @@ struct mxp_engine : public mxp::LowerTables {
     bool need_ipof = false, need_tsof = false, need_strings = false, need_maps = false;
 
     DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
-    DevBuf d_groups, d_segs, d_gk, d_tqmask, d_tmpls, d_rule_tmpl, d_rconst;
+    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rconst, d_idx, d_hents, d_postings;
+    uint32_t n_idx = 0, n_indexed = 0;
     uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
-    // pair queue (phase 1 -> dense template phase 2); sized per batch, grown on demand
-    DevBuf d_queue, d_qcount;
-    uint64_t queue_cap = 0;
-    uint32_t queue_per_req = 64;  // MXP_QUEUE_PER_REQ
-    uint32_t dense_min = 32;      // MXP_DENSE_MIN
     uint32_t groups_per_wave = 4; // MXP_GPW
     // optional per-kernel timing of device evaluations (mxp_set_timing): events around each launch
     bool timing = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    bool ev_queue = false;
-    uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS: ablation only (1 no VM, 2 no guards: results invalid; 8 no pair queue)
+    bool ev_index = false;
+    uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS: ablation only (1 no in-wave VM, 2 no guards: results invalid; 8 no guard index)
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
 
@@ -329,17 +335,57 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     n_tmpls = (uint32_t)tmpls.size();
     all.insert(all.end(), tcode.begin(), tcode.end());
 
-    // phase-1 group tables: mode masks, column segments, guard constants, template masks
+    // guard index: GM_AND, non-negated, templated rules -- their continuing pairs are the requests
+    // whose guard column equals K; per (column, want class) a hash table K -> postings
+    std::vector<uint8_t> indexed(n, 0);
+    std::map<uint32_t, std::map<uint64_t, std::vector<uint32_t>>> index_of;  // col|kind<<24 -> K -> rules
+    n_indexed = 0;
+    if (!(debug_flags & 8u)) {
+        for (uint32_t i = 0; i < n; i++) {
+            const mxp_guard& gd = guards[i];
+            if ((gd.mode & 0xFF) != GM_AND || ((gd.mode >> 8) & 1) || rule_tmpl[i] == MXP_VM_DONE) continue;
+            indexed[i] = 1;
+            index_of[gd.col][(uint64_t)gd.klo | ((uint64_t)gd.khi << 32)].push_back(i);
+            n_indexed++;
+        }
+    }
+    std::vector<mxp_index> idx;
+    std::vector<mxp_hent> hents;
+    std::vector<uint32_t> postings;
+    for (auto& ci : index_of) {
+        mxp_index x{};
+        x.col = ci.first & 0xFFFFFFu;
+        x.okset = okset_of(ci.first >> 24);
+        uint32_t cap = 1;
+        while (cap < 2 * ci.second.size()) cap <<= 1;
+        x.hmask = cap - 1;
+        x.hoff = (uint32_t)hents.size();
+        hents.resize(hents.size() + cap, mxp_hent{0, 0, 0, 0});
+        for (auto& kv : ci.second) {
+            std::vector<uint32_t> rs = kv.second;
+            std::stable_sort(rs.begin(), rs.end(), [&](uint32_t a, uint32_t b) { return rule_tmpl[a] < rule_tmpl[b]; });
+            uint32_t h = mxp_hash64(kv.first) & x.hmask;
+            while (hents[x.hoff + h].len) h = (h + 1) & x.hmask;
+            mxp_hent& E = hents[x.hoff + h];
+            E.klo = (uint32_t)kv.first;
+            E.khi = (uint32_t)(kv.first >> 32);
+            E.start = (uint32_t)postings.size();
+            E.len = (uint32_t)rs.size();
+            postings.insert(postings.end(), rs.begin(), rs.end());
+        }
+        idx.push_back(x);
+    }
+    n_idx = (uint32_t)idx.size();
+
+    // phase-1 group tables: mode masks, column segments, guard constants
     const uint32_t W = (n + 31) / 32;
     std::vector<mxp_group> groups(W);
     std::vector<mxp_seg> segs;
     std::vector<uint64_t> gk((size_t)W * 32, 0);
-    std::vector<uint32_t> tqmask;
     for (uint32_t g = 0; g < W; g++) {
         mxp_group& G = groups[g];
         memset(&G, 0, sizeof G);
-        std::vector<std::pair<uint32_t, uint32_t>> seg_of;   // (col | kind << 24, rules)
-        std::vector<std::pair<uint32_t, uint32_t>> tq_of;    // (template, rules)
+        std::vector<mxp_seg> seg_of;
         for (uint32_t k = 0; k < 32 && g * 32 + k < n; k++) {
             const uint32_t r = g * 32 + k, bit = 1u << k;
             const mxp_guard& gd = guards[r];
@@ -350,35 +396,21 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
             if (mode == GM_ONLY) G.only |= bit;
             if (mode == GM_OR) G.orm |= bit;
             if ((gd.mode >> 8) & 1) G.neg |= bit;
+            if (indexed[r]) G.indexed |= bit;
             gk[r] = (uint64_t)gd.klo | ((uint64_t)gd.khi << 32);
-            auto sit = std::find_if(seg_of.begin(), seg_of.end(), [&](auto& p) { return p.first == gd.col; });
-            if (sit == seg_of.end()) seg_of.emplace_back(gd.col, bit);
-            else sit->second |= bit;
-            if (rule_tmpl[r] != MXP_VM_DONE) {
-                auto tit = std::find_if(tq_of.begin(), tq_of.end(), [&](auto& p) { return p.first == rule_tmpl[r]; });
-                if (tit == tq_of.end()) tq_of.emplace_back(rule_tmpl[r], bit);
-                else tit->second |= bit;
+            const uint32_t col = gd.col & 0xFFFFFFu, kind = gd.col >> 24;
+            auto sit = std::find_if(seg_of.begin(), seg_of.end(),
+                                    [&](const mxp_seg& q) { return q.col == col && (q.okset >> 24) == kind; });
+            if (sit == seg_of.end()) {
+                seg_of.push_back(mxp_seg{col, okset_of(kind) | (kind << 24), 0, 0});
+                sit = seg_of.end() - 1;
             }
+            sit->rules |= bit;
+            if (!indexed[r]) sit->cmp |= bit;
         }
         G.seg0 = (uint32_t)segs.size();
         G.nseg = (uint32_t)seg_of.size();
-        for (auto& p : seg_of) {
-            mxp_seg sg{};
-            sg.col = p.first & 0xFFFFFFu;
-            sg.kind = p.first >> 24;
-            sg.rules = p.second;
-            switch (sg.kind) {
-            case W_S: sg.okset = 1u << MXP_STRING; break;
-            case W_B: sg.okset = 1u << MXP_BOOL; break;
-            case W_I: sg.okset = (1u << MXP_INT64) | (1u << MXP_DURATION); break;
-            case W_D: sg.okset = 1u << MXP_DOUBLE; break;
-            default: sg.okset = 1u << VC_VALUE; break;  // GK_VCOL
-            }
-            segs.push_back(sg);
-        }
-        G.tq0 = (uint32_t)tqmask.size();
-        G.ntq = (uint32_t)tq_of.size();
-        for (auto& p : tq_of) tqmask.push_back(p.second);
+        segs.insert(segs.end(), seg_of.begin(), seg_of.end());
     }
     n_segs = (uint32_t)segs.size();
 
@@ -400,7 +432,9 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_groups, groups.data(), groups.size() * sizeof(mxp_group), "upload groups"))) return rc;
     if ((rc = put(d_segs, segs.data(), segs.size() * sizeof(mxp_seg), "upload segs"))) return rc;
     if ((rc = put(d_gk, gk.data(), gk.size() * 8, "upload gk"))) return rc;
-    if ((rc = put(d_tqmask, tqmask.data(), tqmask.size() * 4, "upload tqmask"))) return rc;
+    if ((rc = put(d_idx, idx.data(), idx.size() * sizeof(mxp_index), "upload idx"))) return rc;
+    if ((rc = put(d_hents, hents.data(), hents.size() * sizeof(mxp_hent), "upload hents"))) return rc;
+    if ((rc = put(d_postings, postings.data(), postings.size() * 4, "upload postings"))) return rc;
     if ((rc = put(d_tmpls, tmpls.data(), tmpls.size() * sizeof(mxp_tmpl), "upload tmpls"))) return rc;
     if ((rc = put(d_rule_tmpl, rule_tmpl.data(), rule_tmpl.size() * 4, "upload rule_tmpl"))) return rc;
     if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
@@ -623,11 +657,13 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->groups = d_groups.as<mxp_group>();
     A->segs = d_segs.as<mxp_seg>();
     A->gk = d_gk.as<uint64_t>();
-    A->tqmask = d_tqmask.as<uint32_t>();
+    A->idx = d_idx.as<mxp_index>();
+    A->hents = d_hents.as<mxp_hent>();
+    A->postings = d_postings.as<uint32_t>();
+    A->n_idx = n_idx;
     A->tmpls = d_tmpls.as<mxp_tmpl>();
     A->rule_tmpl = d_rule_tmpl.as<uint32_t>();
     A->rconst = d_rconst.as<uint64_t>();
-    A->dense_min = dense_min;
     A->flags = debug_flags;
     A->n_rules = (uint32_t)rules.size();
     A->n_words = (A->n_rules + 31) / 32;
@@ -667,33 +703,17 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         A.errcap = errcap;
     }
     if (A.n == 0 || A.n_rules == 0) return MXP_OK;
-    // pair queue: only in predicate mode, only when some rule has a continuation template
-    const bool use_queue = !d_vals && n_templated > 0 && !(debug_flags & 8u);
+    // guard-index phase: predicate mode only (Eval runs whole programs in mxp_eval_kernel)
+    const bool use_index = !d_vals && !(debug_flags & 2u) && n_idx > 0;
+    if (!use_index) A.n_idx = 0;
     const uint32_t gx = (A.n + 63) / 64;
-    uint32_t qsub = 0;
-    if (use_queue) {
-        qsub = std::min<uint32_t>(gx, kQueueSub);
-        const uint64_t want = std::min<uint64_t>(std::max<uint64_t>((uint64_t)A.n * queue_per_req, 1u << 10), 1u << 28);
-        if (want > queue_cap) {
-            if ((e = d_queue.alloc(want * 8)) != hipSuccess) return hipfail(e, "hipMalloc queue");
-            queue_cap = want;
-        }
-        if (!d_qcount.p && (e = d_qcount.alloc((size_t)kQueueSub * MXP_QSTRIDE * 4)) != hipSuccess)
-            return hipfail(e, "hipMalloc qcount");
-        if ((e = hipMemsetAsync(d_qcount.p, 0, (size_t)qsub * MXP_QSTRIDE * 4, s)) != hipSuccess)
-            return hipfail(e, "memset qcount");
-        A.queue = d_queue.as<uint2>();
-        A.qcount = d_qcount.as<uint32_t>();
-        A.qsub = qsub;
-        A.qsubcap = (uint32_t)(queue_cap / qsub);
-    }
     const uint32_t gy = (A.n_words + 4 * A.groups_per_wave - 1) / (4 * A.groups_per_wave);
     if (timing && (e = hipEventRecord(ev[0], s)) != hipSuccess) return hipfail(e, "event");
     if ((e = mxp_launch_eval(&A, gx, gy, s)) != hipSuccess) return hipfail(e, "launch eval");
     if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
-    if (use_queue && (e = mxp_launch_queue(&A, qsub, s)) != hipSuccess) return hipfail(e, "launch queue");
+    if (use_index && (e = mxp_launch_index(&A, (gx + 3) / 4, s)) != hipSuccess) return hipfail(e, "launch index");
     if (timing && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hipfail(e, "event");
-    ev_queue = use_queue;
+    ev_index = use_index;
     return MXP_OK;
 }
 
@@ -771,8 +791,6 @@ int mxp_engine_create(int device, mxp_engine** out) {
     e->device = device;
     if (const char* f = getenv("MXP_DEBUG_FLAGS")) e->debug_flags = (uint32_t)atoi(f);
     // tuning knobs (results are identical for every setting)
-    if (const char* f = getenv("MXP_QUEUE_PER_REQ")) e->queue_per_req = (uint32_t)atoi(f);
-    if (const char* f = getenv("MXP_DENSE_MIN")) e->dense_min = (uint32_t)atoi(f);
     if (const char* f = getenv("MXP_GPW")) e->groups_per_wave = std::max(1, atoi(f));
     if (const char* f = getenv("MXP_ERRCAP")) e->errcap = (uint32_t)std::max(1, atoi(f));
     if (device < 0) {  // host-only engine (compiler / lowering inspection without a GPU)
@@ -866,7 +884,7 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) 
     float t[2] = {0.f, 0.f};
     if ((e = hipEventSynchronize(eng->ev[2])) != hipSuccess) return eng->hipfail(e, "event sync");
     if ((e = hipEventElapsedTime(&t[0], eng->ev[0], eng->ev[1])) != hipSuccess) return eng->hipfail(e, "elapsed");
-    if (eng->ev_queue && (e = hipEventElapsedTime(&t[1], eng->ev[1], eng->ev[2])) != hipSuccess)
+    if (eng->ev_index && (e = hipEventElapsedTime(&t[1], eng->ev[1], eng->ev[2])) != hipSuccess)
         return eng->hipfail(e, "elapsed");
     uint32_t k = 0;
     for (; k < cap && k < 2; k++) ms[k] = t[k];
@@ -876,9 +894,9 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) 
 
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
     if (!eng || !out) return 0;
-    const uint32_t v[4] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs};
+    const uint32_t v[5] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed};
     uint32_t k = 0;
-    for (; k < cap && k < 4; k++) out[k] = v[k];
+    for (; k < cap && k < 5; k++) out[k] = v[k];
     return k;
 }
 

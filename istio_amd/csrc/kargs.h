@@ -7,8 +7,6 @@
 
 #include "vm.h"
 
-#define MXP_QSTRIDE 32  // u32 stride between sub-queue counters (one 128-byte line each)
-
 typedef struct mxp_kargs {
     // rule set (uploaded once per config snapshot)
     const mxp_vm_ins* prog;      // all rules' programs, concatenated
@@ -17,10 +15,14 @@ typedef struct mxp_kargs {
     const mxp_group* groups;     // [n_words] per-group guard masks
     const mxp_seg* segs;         // column segments of the groups
     const uint64_t* gk;          // [n_words * 32] guard constants (0 for unguarded slots)
-    const uint32_t* tqmask;      // per-group template masks (mxp_group.tq0 / ntq)
     const mxp_tmpl* tmpls;       // continuation templates
     const uint32_t* rule_tmpl;   // [n_rules] template of the rule's continuation (~0: none)
     const uint64_t* rconst;      // [n_rules][MXP_VM_MAXREG] per-rule template constants
+    const mxp_index* idx;        // guard indexes (mxp_index_kernel)
+    const mxp_hent* hents;
+    const uint32_t* postings;
+    uint32_t n_idx;
+    uint32_t pad2;
     uint32_t n_rules;
     uint32_t n_words;            // ceil(n_rules / 32)
     uint32_t groups_per_wave;
@@ -50,14 +52,5 @@ typedef struct mxp_kargs {
     mxp_err_rec* errlog;
     uint32_t* errcount;
     uint32_t errcap;
-    uint32_t flags;              // debug / ablation: 1 = skip phase 2 (VM), 2 = no guards
-    // pair queue (phase 1 -> mxp_queue_kernel); queue == nullptr disables the hand-off.  The queue
-    // is split into qsub sub-queues (tile t appends to sub-queue t % qsub) so the append counters
-    // do not serialise on one address.
-    uint2* queue;                // [qsub][qsubcap] (request, rule)
-    uint32_t* qcount;            // [qsub * MXP_QSTRIDE] appended pairs (may exceed qsubcap: the excess ran in-wave)
-    uint32_t qsub;
-    uint32_t qsubcap;
-    uint32_t dense_min;          // survivors per tile from which a rule stays in-wave
-    uint32_t pad1;
+    uint32_t flags;              // debug / ablation: 1 = skip in-wave VM, 2 = no guards (results invalid)
 } mxp_kargs;

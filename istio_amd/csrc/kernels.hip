@@ -86,7 +86,7 @@ typedef __attribute__((address_space(4))) const uint32_t cuint32;
 // Runs one program from `pc0` for the lanes in `live` (the others keep their phase-1 result) and
 // returns the pair code of every lane that ran.  The program is wave-uniform: instruction pc is
 // P[pc] (pc in [pc0, len)), fetched with one scalar s_load_dwordx4 per step.  `rule` may differ
-// per lane (template batches of the pair queue); it only names the pair in error records and
+// per lane (template batches of the guard-index kernel); it only names the pair in error records and
 // Eval results.  The register file is regs[reg][thread] in LDS.
 __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint32_t pc0, bool live, uint32_t rule,
                              uint32_t req, uint64_t (*regs)[256], uint32_t tid) {
@@ -381,9 +381,8 @@ __device__ __forceinline__ void log_guard_errors(const mxp_kargs& A, uint32_t e,
 //            lane and compares it with the segment's constants (scalar operands), giving per lane the
 //            32-bit words eq / ok; the group's mode masks turn them into match / error / continue
 //            words with a handful of bit operations;
-//   hand-off continuing pairs of templated rules whose survivors are sparse in this tile go to the
-//            pair queue (evaluated densely by mxp_queue_kernel);
-//   phase 2  the VM runs, rule by rule, for the remaining continuing lanes.
+//   phase 2  the VM runs, rule by rule, for the continuing lanes (indexed rules excepted: their
+//            continuing pairs are enumerated by mxp_index_kernel).
 // Results: one coalesced store per word and plane, out[g * N + request].
 extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
@@ -395,23 +394,23 @@ extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
     const uint64_t N = A.n;
     const uint32_t g0 = (blockIdx.y * 4u + wave) * A.groups_per_wave;
     const uint32_t g1 = min(g0 + A.groups_per_wave, A.n_words);
-    // Eval mode (out_vals) needs every result register: whole programs, no guards, no queue
+    // Eval mode (out_vals) needs every result register: whole programs, no guards, no index
     const bool guards_on = !(A.out_vals || (A.flags & 2u));
-    const bool queue_on = guards_on && A.queue != nullptr;
     uint32_t cached = MXP_VM_DONE;
     uint32_t ck = MXP_ABSENT;
     uint64_t cv = 0;
     for (uint32_t g = g0; g < g1; g++) {
         const mxp_group* G = A.groups + g;
         const uint32_t all = uni(G->all), guarded = uni(G->guarded), only = uni(G->only), orm = uni(G->orm),
-                       neg = uni(G->neg), seg0 = uni(G->seg0), nseg = uni(G->nseg);
+                       neg = uni(G->neg), seg0 = uni(G->seg0), nseg = uni(G->nseg), indexed = uni(G->indexed);
         const uint32_t r0 = g * 32u;
         uint32_t m = 0, e = 0, cont = 0;
         if (guards_on) {
             // ---- phase 1
             uint32_t eq = 0, ok = 0;
             for (uint32_t s = seg0; s < seg0 + nseg; s++) {
-                const uint32_t col = uni(A.segs[s].col), okset = uni(A.segs[s].okset), rules = uni(A.segs[s].rules);
+                const uint32_t col = uni(A.segs[s].col), okset = uni(A.segs[s].okset), rules = uni(A.segs[s].rules),
+                               cmp = uni(A.segs[s].cmp);
                 if (col != cached) {
                     cached = col;
                     if (valid) {
@@ -420,49 +419,21 @@ extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
                     }
                 }
                 ok |= ((okset >> ck) & 1u) ? rules : 0u;
-                eq |= seg_eq((cuint64*)A.gk + r0, rules, cv);
+                if (cmp) eq |= seg_eq((cuint64*)A.gk + r0, cmp, cv);
             }
             const uint32_t atom = eq ^ neg;
             const uint32_t andm = guarded & ~(only | orm);
+            // indexed rules: atom unknown here (no compare), match 0, continuing pairs enumerated
+            // by mxp_index_kernel
             m = atom & (only | orm) & ok;
-            cont = (((atom & andm) | (~atom & orm)) & ok) | (all & ~guarded);
+            cont = (((atom & andm) | (~atom & orm)) & ok & ~indexed) | (all & ~guarded);
             e = guarded & ~ok;
             if (!valid) m = e = cont = 0;
             if (e && A.errlog) log_guard_errors(A, e, r0, req);
         } else {
             cont = valid ? all : 0u;
         }
-        // ---- hand-off to the pair queue
-        uint32_t inwave = cont;
-        if (queue_on) {
-            const uint32_t tq0 = uni(G->tq0), ntq = uni(G->ntq);
-            for (uint32_t j = tq0; j < tq0 + ntq; j++) {
-                uint32_t qb = cont & uni(A.tqmask[j]);
-                const uint32_t anyq = wave_or(qb);
-                if (anyq == 0) continue;
-                // rules with many survivors in this tile run in-wave (dense enough already)
-                for (uint32_t bits = anyq; bits; bits &= bits - 1) {
-                    const uint32_t k = __builtin_ctz(bits);
-                    const uint64_t bal = __ballot((qb >> k) & 1u);
-                    if ((uint32_t)__popcll(bal) >= A.dense_min) qb &= ~(1u << k);
-                }
-                const uint32_t cnt = __builtin_popcount(qb);
-                const uint32_t incl = wave_incl_sum(cnt, lane);
-                const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-                if (total == 0) continue;
-                const uint32_t sq = blockIdx.x % A.qsub;
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(A.qcount + (uint64_t)sq * MXP_QSTRIDE, total);
-                base = uni(base);
-                uint2* Q = A.queue + (uint64_t)sq * A.qsubcap;
-                uint32_t pos = base + incl - cnt;
-                for (uint32_t bits = qb; bits && pos < A.qsubcap; bits &= bits - 1, pos++) {
-                    const uint32_t k = __builtin_ctz(bits);
-                    Q[pos] = make_uint2(req, r0 + k);
-                    inwave &= ~(1u << k);
-                }
-            }
-        }
+        const uint32_t inwave = cont;
         // ---- phase 2 (in-wave)
         for (uint32_t bits = wave_or(inwave); bits && !(A.flags & 1u); bits &= bits - 1) {
             const uint32_t k = __builtin_ctz(bits);
@@ -487,44 +458,63 @@ extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
     }
 }
 
-// Dense phase 2 for the pair queue: one workgroup per sub-queue, each wavefront takes 64 queued
-// (request, rule) pairs at a time; lanes whose rules share a continuation template run that
-// template's program together (constants of each lane's own rule preloaded into its registers),
-// one template after another.  Results land
-// with atomicOr in the bitmaps mxp_eval_kernel wrote (same stream, so its stores are complete).
-extern "C" __global__ __launch_bounds__(256) void mxp_queue_kernel(mxp_kargs A) {
+// Guard-index phase: the continuing pairs of indexed rules (`attr == K && <continuation>`), found
+// per request by a hash lookup of its column value instead of by comparing against every rule.
+// Workgroup = 4 wavefronts, one tile of 64 requests each (one request per lane).  Lanes walk their
+// own posting lists in lockstep; at every step the lanes whose rules share a continuation template
+// run it together (each lane's rule constants preloaded into its registers).  mxp_eval_kernel has
+// already written both bitmaps for these rules (match 0, error on a failed guard type check); true
+// and error results are OR-ed in.
+extern "C" __global__ __launch_bounds__(256) void mxp_index_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
     const uint32_t wave = uni(tid >> 6);
-    const uint32_t sq = blockIdx.x;  // one workgroup per sub-queue; its 4 waves stride over the batches
-    const uint32_t n = min(uni(A.qcount[(uint64_t)sq * MXP_QSTRIDE]), A.qsubcap);
-    const uint2* Q = A.queue + (uint64_t)sq * A.qsubcap;
+    const uint32_t req = (blockIdx.x * 4u + wave) * 64u + (tid & 63u);
+    const bool valid = req < A.n;
     const uint64_t N = A.n;
-    for (uint32_t b = wave; b * 64u < n; b += 4u) {
-        const uint32_t i = b * 64u + lane;
-        bool pending = i < n;
-        uint2 en = make_uint2(0, 0);
-        if (pending) en = Q[i];
-        const uint32_t req = en.x, rule = en.y;
-        const uint32_t t = pending ? A.rule_tmpl[rule] : MXP_VM_DONE;
-        for (uint64_t bal = __ballot(pending); bal; bal = __ballot(pending)) {
-            const uint32_t tt = __builtin_amdgcn_readlane(t, (uint32_t)__builtin_ctzll(bal));
-            const bool mine = pending && t == tt;
-            const mxp_tmpl* T = A.tmpls + tt;
-            const uint32_t off = uni(T->off), pc0 = uni(T->pc0), len = uni(T->len), nconst = uni(T->nconst),
-                           creg0 = uni(T->creg0);
-            if (mine)
-                for (uint32_t j = 0; j < nconst; j++) regs[creg0 + j][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + j];
-            cuint32* P = ((cuint32*)A.prog) + ((uint64_t)off - pc0) * 4u;
-            const uint32_t code = run_rule(A, P, len, pc0, mine, rule, req, regs, tid);
-            if (mine) {
-                const uint64_t w = (uint64_t)(rule >> 5) * N + req;
-                const uint32_t bit = 1u << (rule & 31u);
-                if (code == PC_TRUE && A.out_match) atomicOr(A.out_match + w, bit);
-                if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
+    for (uint32_t x = 0; x < A.n_idx; x++) {
+        const uint32_t col = uni(A.idx[x].col), okset = uni(A.idx[x].okset), hmask = uni(A.idx[x].hmask),
+                       hoff = uni(A.idx[x].hoff);
+        uint32_t start = 0, len = 0;
+        if (valid) {
+            const uint32_t k = A.kinds[(uint64_t)col * N + req];
+            if ((okset >> k) & 1u) {
+                const uint64_t v = A.vals[(uint64_t)col * N + req];
+                const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+                for (uint32_t h = mxp_hash64(v) & hmask;; h = (h + 1) & hmask) {
+                    const mxp_hent E = A.hents[hoff + h];
+                    if (E.len == 0) break;
+                    if (E.klo == lo && E.khi == hi) {
+                        start = E.start;
+                        len = E.len;
+                        break;
+                    }
+                }
             }
-            pending = pending && !mine;
+        }
+        for (uint32_t j = 0; __ballot(j < len); j++) {
+            bool pending = j < len;
+            const uint32_t rule = pending ? A.postings[start + j] : 0u;
+            const uint32_t t = pending ? A.rule_tmpl[rule] : MXP_VM_DONE;
+            for (uint64_t bal = __ballot(pending); bal; bal = __ballot(pending)) {
+                const uint32_t tt = __builtin_amdgcn_readlane(t, (uint32_t)__builtin_ctzll(bal));
+                const bool mine = pending && t == tt;
+                const mxp_tmpl* T = A.tmpls + tt;
+                const uint32_t off = uni(T->off), pc0 = uni(T->pc0), len_t = uni(T->len), nconst = uni(T->nconst),
+                               creg0 = uni(T->creg0);
+                if (mine)
+                    for (uint32_t c = 0; c < nconst; c++)
+                        regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
+                cuint32* P = ((cuint32*)A.prog) + ((uint64_t)off - pc0) * 4u;
+                const uint32_t code = run_rule(A, P, len_t, pc0, mine, rule, req, regs, tid);
+                if (mine) {
+                    const uint64_t w = (uint64_t)(rule >> 5) * N + req;
+                    const uint32_t bit = 1u << (rule & 31u);
+                    if (code == PC_TRUE && A.out_match) atomicOr(A.out_match + w, bit);
+                    if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
+                }
+                pending = pending && !mine;
+            }
         }
     }
 }
@@ -566,8 +556,8 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
     return hipGetLastError();
 }
 
-extern "C" hipError_t mxp_launch_queue(const mxp_kargs* args, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_queue_kernel, dim3(grid), dim3(256), 0, s, *args);
+extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_index_kernel, dim3(grid), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

@@ -67,9 +67,9 @@ typedef struct mxp_guard {
 } mxp_guard;
 
 // Per 32-rule group: the guard masks the kernel's phase 1 works with (bit k = rule 32 g + k), and
-// the group's guarded rules split into column segments (runs of rules whose guard reads the same
-// column with the same want class), so each segment loads its column once and compares all its
-// rules' constants (kargs.gk[32 g + k]) against it.
+// the group's guarded rules split into column segments (the rules whose guard reads the same
+// column with the same want class), so each segment loads its column once per request and compares
+// its rules' constants (kargs.gk[32 g + k]) against it.
 typedef struct mxp_group {
     uint32_t all;      // rules present in the group
     uint32_t guarded;  // mode != GM_NONE
@@ -78,17 +78,47 @@ typedef struct mxp_group {
     uint32_t neg;      // negated atoms
     uint32_t seg0;     // segments [seg0, seg0 + nseg) of kargs.segs
     uint32_t nseg;
-    uint32_t tq0;      // template masks [tq0, tq0 + ntq) of kargs.tqmask: continuation rules of one
-    uint32_t ntq;      //   template each, handed to the pair queue when their survivors are sparse
-    uint32_t pad[3];
+    uint32_t indexed;  // rules whose continuing pairs come from the guard index (mxp_index_kernel)
 } mxp_group;
 
 typedef struct mxp_seg {
     uint32_t col;      // column read by the guards of the segment
-    uint32_t okset;    // bit (kind) set when a column value of that kind passes the want class
-    uint32_t rules;    // rules of the group in this segment
-    uint32_t kind;     // want class (W_*) or GK_VCOL, for the error code
+    uint32_t okset;    // bits 0..15: kinds that pass the want class; bits 24..31: want class / GK_VCOL
+    uint32_t rules;    // rules of the group in this segment (all need the column's type check)
+    uint32_t cmp;      // the subset whose atom phase 1 computes (indexed rules need no compare)
 } mxp_seg;
+
+// Guard index: for `attr == K && <continuation>` rules (GM_AND, not negated, templated), the pairs
+// that continue are exactly the requests whose column value equals K.  Per (column, want class) an
+// open-addressing hash table maps a value K to the rules guarded by it (a range of kargs.postings,
+// sorted by template), so each request enumerates its own surviving rules instead of comparing
+// against all of them.
+typedef struct mxp_index {
+    uint32_t col;
+    uint32_t okset;    // as mxp_seg.okset (bits 0..15)
+    uint32_t hmask;    // table size - 1 (power of two)
+    uint32_t hoff;     // first entry in kargs.hents
+} mxp_index;
+
+typedef struct mxp_hent {
+    uint32_t klo, khi; // key (column value register)
+    uint32_t start;    // postings [start, start + len); len == 0: empty slot
+    uint32_t len;
+} mxp_hent;
+
+#if defined(__HIPCC__)
+#define MXP_HD __host__ __device__
+#else
+#define MXP_HD
+#endif
+static inline MXP_HD uint32_t mxp_hash64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdull;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ull;
+    k ^= k >> 33;
+    return (uint32_t)k;
+}
 
 // Continuation templates: the continuations (code from the guard's cont pc) of many rules differ
 // only in constants (C2: the path prefix and the ip literal).  Hoisting every constant operand

@@ -158,7 +158,7 @@ class Engine:
         self._check(self.lib.mxp_set_timing(self.h, int(on)), "mxp_set_timing")
 
     def kernel_times(self):
-        """[guard/VM kernel ms, pair-queue kernel ms] of the last device evaluation (timing on)."""
+        """[guard/VM kernel ms, guard-index kernel ms] of the last device evaluation (timing on)."""
         ms = (ctypes.c_float * 2)()
         n = ctypes.c_uint32()
         self._check(self.lib.mxp_kernel_times(self.h, ms, 2, ctypes.byref(n)), "mxp_kernel_times")
@@ -166,9 +166,9 @@ class Engine:
 
     def ruleset_info(self) -> dict:
         """Kernel-side shape of the rule set (guards, continuation templates, column segments)."""
-        out = (ctypes.c_uint32 * 4)()
-        k = self.lib.mxp_ruleset_info(self.h, out, 4)
-        return dict(zip(("guarded", "templated", "templates", "segments"), list(out)[:k]))
+        out = (ctypes.c_uint32 * 5)()
+        k = self.lib.mxp_ruleset_info(self.h, out, 5)
+        return dict(zip(("guarded", "templated", "templates", "segments", "indexed"), list(out)[:k]))
 
     # ------------------------------------------------------------------ evaluation
     def eval_batch(self, batch: BagBatch):

@@ -125,13 +125,12 @@ def test_fuzz_parity(mxp, seed):
     compare(eng, ev, rules, batch)
 
 
-@pytest.mark.parametrize("knobs", [{}, {"MXP_DENSE_MIN": "1"}, {"MXP_DENSE_MIN": "65"},
-                                   {"MXP_DENSE_MIN": "65", "MXP_QUEUE_PER_REQ": "1"}, {"MXP_GPW": "1"}])
+@pytest.mark.parametrize("knobs", [{}, {"MXP_DEBUG_FLAGS": "8"}, {"MXP_GPW": "1"}])
 def test_guarded_fuzz_parity(mxp, knobs, monkeypatch):
     """Guard-led rules (mixed columns / want classes / negations / modes per group, shared and
-    singleton continuation templates) under every phase-2 routing: default, all in-wave
-    (dense_min 1), all through the pair queue (dense_min 65), queue overflow falling back in-wave
-    (1 slot per request), one group per wave."""
+    singleton continuation templates, indexed and in-wave continuations) under each routing:
+    default (guard index on), guard index off (MXP_DEBUG_FLAGS=8: every continuation in-wave), one
+    group per wave."""
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
     rules = W.guarded_fuzz_rules(2000, seed=11)
@@ -142,6 +141,7 @@ def test_guarded_fuzz_parity(mxp, knobs, monkeypatch):
     eng.compile(rules)
     info = eng.ruleset_info()
     assert info["templated"] > 500 and info["templates"] > 50
+    assert info["indexed"] > 300 or knobs.get("MXP_DEBUG_FLAGS") == "8"
     ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
     got, want = compare(eng, ev, rules, batch, sample_msgs=200)
     assert (want == 1).sum() > 1000 and (want >= 2).sum() > 1000
