@@ -77,9 +77,8 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from istio_amd import dist as D
+    rank, world, local = D.world()
     if world > 1:
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
@@ -118,8 +117,7 @@ def main():
             ev1.record(stream)
         rc = eng.lib.mxp_hits_device(eng.h, d_match.data_ptr(), N, sh, hits.data_ptr())
         assert rc == 0
-        if world > 1:
-            dist.all_reduce(hits)  # RCCL over xGMI: per-rule hit counters
+        D.reduce_counters(hits)  # RCCL over xGMI when world > 1: per-rule hit counters
 
     for _ in range(args.warmup):
         step()
@@ -136,10 +134,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.max_over_ranks(elapsed, dev)
 
     pairs_total = world * N * R * args.steps
     value = pairs_total / elapsed
