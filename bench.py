@@ -175,11 +175,11 @@ def main():
         "config": {"workload": "C2 rules scaled to R=%d, %d requests per GPU (configs[1] family, configs[4] shard)" % (R, N),
                    "rules": R, "requests_per_gpu": N, "parallelism": "request-sharded dp%d" % world},
         "eval_ms": kernel_ms,
-        "kernels_ms": {"mxp_eval_kernel": k_eval, "mxp_index_kernel": k_index},
+        "kernels_ms": {"mxp_guard_kernel+mxp_eval_kernel": k_eval, "mxp_index_kernel": k_index},
         "pack_upload_s": t_pack,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "mxp_eval_kernel + mxp_index_kernel (one evaluation)",
+                     "kernel": "mxp_guard_kernel + mxp_eval_kernel + mxp_index_kernel (one evaluation)",
                      "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pair": alg_bytes / (N * R)},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:

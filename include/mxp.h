@@ -107,7 +107,7 @@ int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_request
 uint32_t mxp_rule_count(const mxp_engine* eng);
 /* Per-kernel timing of device evaluations (off by default): with timing on, every evaluation
  * records HIP events around its launches on the evaluation stream; mxp_kernel_times waits for the
- * last one and returns its kernel durations in ms: [0] guard/VM kernel, [1] guard-index kernel
+ * last one and returns its kernel durations in ms: [0] guard + VM kernels, [1] guard-index kernel
  * (0 when it did not run).  *n_out = values written. */
 int mxp_set_timing(mxp_engine* eng, int on);
 int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out);

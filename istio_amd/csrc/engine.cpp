@@ -27,7 +27,7 @@
 #include "lower.h"
 #include "vmopt.h"
 
-extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, hipStream_t s);
+extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
                                       unsigned long long* hits, hipStream_t s);
@@ -65,6 +65,22 @@ struct TimeKey {
 };
 
 constexpr uint64_t kNoValue = ~0ull;
+
+// Device string pool: every string starts 8-byte aligned (zero padded), with 16 bytes of slack at
+// the end, so the kernels compare strings a u64 word at a time (two aligned loads + funnel shift for
+// unaligned operands) without reading past the allocation.  desc[i] = offset << 24 | length.
+bool string_pool(const std::vector<std::string>& strs, std::vector<uint64_t>* desc, std::string* blob) {
+    desc->assign(strs.size(), 0);
+    blob->clear();
+    for (size_t i = 0; i < strs.size(); i++) {
+        if (strs[i].size() >= (1u << 24)) return false;
+        (*desc)[i] = ((uint64_t)blob->size() << 24) | strs[i].size();
+        blob->append(strs[i]);
+        blob->append((8 - blob->size() % 8) % 8, '\0');
+    }
+    blob->append(16, '\0');
+    return true;
+}
 
 // column kinds that pass a guard's want class (W_*) or a virtual-column guard (GK_VCOL)
 uint32_t okset_of(uint32_t kind) {
@@ -124,6 +140,8 @@ struct mxp_engine : public mxp::LowerTables {
 
     DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
     DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rconst, d_idx, d_hents, d_postings;
+    DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
+    uint32_t n_glean = 0, n_gvm = 0;
     uint32_t n_idx = 0, n_indexed = 0;
     uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
     uint32_t groups_per_wave = 4; // MXP_GPW
@@ -408,10 +426,28 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
             sit->rules |= bit;
             if (!indexed[r]) sit->cmp |= bit;
         }
-        G.seg0 = (uint32_t)segs.size();
+        G.id = g;
         G.nseg = (uint32_t)seg_of.size();
-        segs.insert(segs.end(), seg_of.begin(), seg_of.end());
+        G.seg0 = (uint32_t)segs.size();
+        if (!seg_of.empty()) {
+            G.s_col = seg_of[0].col;
+            G.s_okset = seg_of[0].okset;
+            G.s_rules = seg_of[0].rules;
+            G.s_cmp = seg_of[0].cmp;
+            segs.insert(segs.end(), seg_of.begin() + 1, seg_of.end());
+        }
+        // continuing lanes after phase 1 need the VM: rules without a guard, OR guards, AND guards
+        // that are not indexed (ONLY guards and indexed AND guards never continue in-wave)
+        const uint32_t andm = G.guarded & ~(G.only | G.orm);
+        G.vm = ((G.all & ~G.guarded) | G.orm | (andm & ~G.indexed)) != 0;
     }
+    std::vector<uint32_t> glean, gvm, gall(W);
+    for (uint32_t g = 0; g < W; g++) {
+        gall[g] = g;
+        (groups[g].vm ? gvm : glean).push_back(g);
+    }
+    n_glean = (uint32_t)glean.size();
+    n_gvm = (uint32_t)gvm.size();
     n_segs = (uint32_t)segs.size();
 
     have_rules = true;
@@ -431,6 +467,9 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_guards, guards.data(), guards.size() * sizeof(mxp_guard), "upload guards"))) return rc;
     if ((rc = put(d_groups, groups.data(), groups.size() * sizeof(mxp_group), "upload groups"))) return rc;
     if ((rc = put(d_segs, segs.data(), segs.size() * sizeof(mxp_seg), "upload segs"))) return rc;
+    if ((rc = put(d_glean, glean.data(), glean.size() * 4, "upload glean"))) return rc;
+    if ((rc = put(d_gvm, gvm.data(), gvm.size() * 4, "upload gvm"))) return rc;
+    if ((rc = put(d_gall, gall.data(), gall.size() * 4, "upload gall"))) return rc;
     if ((rc = put(d_gk, gk.data(), gk.size() * 8, "upload gk"))) return rc;
     if ((rc = put(d_idx, idx.data(), idx.size() * sizeof(mxp_index), "upload idx"))) return rc;
     if ((rc = put(d_hents, hents.data(), hents.size() * sizeof(mxp_hent), "upload hents"))) return rc;
@@ -438,14 +477,11 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_tmpls, tmpls.data(), tmpls.size() * sizeof(mxp_tmpl), "upload tmpls"))) return rc;
     if ((rc = put(d_rule_tmpl, rule_tmpl.data(), rule_tmpl.size() * 4, "upload rule_tmpl"))) return rc;
     if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
-    std::vector<uint64_t> soff(gstrs.size() + 1, 0);
+    std::vector<uint64_t> soff;
     std::string blob;
-    for (size_t i = 0; i < gstrs.size(); i++) {
-        blob += gstrs[i];
-        soff[i + 1] = blob.size();
-    }
+    if (!string_pool(gstrs, &soff, &blob)) return fail(MXP_ERR_ARG, "rule-set string longer than 16 MiB");
     if ((e = d_gstr_off.alloc(soff.size() * 8)) != hipSuccess) return hipfail(e, "hipMalloc gstr_off");
-    if ((e = d_gstr.alloc(blob.size() + 8)) != hipSuccess) return hipfail(e, "hipMalloc gstr");
+    if ((e = d_gstr.alloc(blob.size())) != hipSuccess) return hipfail(e, "hipMalloc gstr");
     if (!all.empty() && (e = hipMemcpy(d_prog.p, all.data(), all.size() * sizeof(mxp_vm_ins), hipMemcpyHostToDevice)) != hipSuccess)
         return hipfail(e, "upload prog");
     if ((e = hipMemcpy(d_rule_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
@@ -619,14 +655,10 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
                 tsof[s] = MXP_FH(MXP_TIMESTAMP, time_id(sec, ns));
         }
     }
-    std::vector<uint64_t> ooff(db->overlay.size() + 1, 0);
+    std::vector<uint64_t> ooff;
     std::string oblob;
-    if (need_strings) {
-        for (size_t i = 0; i < db->overlay.size(); i++) {
-            oblob += db->overlay[i];
-            ooff[i + 1] = oblob.size();
-        }
-    }
+    if (need_strings && !string_pool(db->overlay, &ooff, &oblob))
+        return fail(MXP_ERR_ARG, "batch string longer than 16 MiB");
 
     hipError_t e;
     auto up = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
@@ -707,9 +739,23 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     const bool use_index = !d_vals && !(debug_flags & 2u) && n_idx > 0;
     if (!use_index) A.n_idx = 0;
     const uint32_t gx = (A.n + 63) / 64;
-    const uint32_t gy = (A.n_words + 4 * A.groups_per_wave - 1) / (4 * A.groups_per_wave);
+    auto gy_of = [&](uint32_t ng) { return (ng + 4 * A.groups_per_wave - 1) / (4 * A.groups_per_wave); };
     if (timing && (e = hipEventRecord(ev[0], s)) != hipSuccess) return hipfail(e, "event");
-    if ((e = mxp_launch_eval(&A, gx, gy, s)) != hipSuccess) return hipfail(e, "launch eval");
+    // guards on: guard-only groups through the lean kernel, the rest through the VM kernel;
+    // guards off (Eval, ablation): every group through the VM kernel
+    const bool guards_on = !d_vals && !(debug_flags & 2u);
+    struct Part {
+        const DevBuf* list;
+        uint32_t n;
+        int vm;
+    } parts[2] = {{guards_on ? &d_glean : &d_gall, guards_on ? n_glean : 0u, 0},
+                  {guards_on ? &d_gvm : &d_gall, guards_on ? n_gvm : A.n_words, 1}};
+    for (const Part& P : parts) {
+        if (!P.n) continue;
+        A.glist = P.list->as<uint32_t>();
+        A.n_glist = P.n;
+        if ((e = mxp_launch_eval(&A, gx, gy_of(P.n), P.vm, s)) != hipSuccess) return hipfail(e, "launch eval");
+    }
     if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
     if (use_index && (e = mxp_launch_index(&A, (gx + 3) / 4, s)) != hipSuccess) return hipfail(e, "launch index");
     if (timing && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hipfail(e, "event");

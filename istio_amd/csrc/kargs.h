@@ -13,6 +13,9 @@ typedef struct mxp_kargs {
     const uint32_t* rule_off;    // [n_rules + 1]
     const mxp_guard* guards;     // [n_rules] leading-atom guards (vmopt.h)
     const mxp_group* groups;     // [n_words] per-group guard masks
+    const uint32_t* glist;       // groups this launch evaluates (ids into groups)
+    uint32_t n_glist;
+    uint32_t pad3;
     const mxp_seg* segs;         // column segments of the groups
     const uint64_t* gk;          // [n_words * 32] guard constants (0 for unguarded slots)
     const mxp_tmpl* tmpls;       // continuation templates
@@ -32,9 +35,9 @@ typedef struct mxp_kargs {
     const uint64_t* vals;
     // interned strings: ids < n_gstr live in the rule set's pool, the rest in the batch pool
     uint64_t n_gstr;
-    const uint64_t* gstr_off;
+    const uint64_t* gstr_off;    // [n_gstr] offset << 24 | length (8-aligned pool, engine.cpp string_pool)
     const uint8_t* gstr;
-    const uint64_t* bstr_off;
+    const uint64_t* bstr_off;    // batch overlay strings, same encoding
     const uint8_t* bstr;
     uint32_t empty_sid;
     uint32_t pad0;

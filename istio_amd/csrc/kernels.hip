@@ -37,24 +37,30 @@ struct StrRef {
 };
 
 __device__ __forceinline__ StrRef str_of(const mxp_kargs& A, uint64_t id) {
+    const bool g = id < A.n_gstr;
+    const uint64_t d = g ? A.gstr_off[id] : A.bstr_off[id - A.n_gstr];
     StrRef r;
-    if (id < A.n_gstr) {
-        uint64_t a = A.gstr_off[id], b = A.gstr_off[id + 1];
-        r.p = A.gstr + a;
-        r.n = (uint32_t)(b - a);
-    } else {
-        uint64_t j = id - A.n_gstr;
-        uint64_t a = A.bstr_off[j], b = A.bstr_off[j + 1];
-        r.p = A.bstr + a;
-        r.n = (uint32_t)(b - a);
-    }
+    r.p = (g ? A.gstr : A.bstr) + (d >> 24);
+    r.n = (uint32_t)(d & 0xFFFFFFu);
     return r;
 }
 
+// 8 bytes at any address of a string pool (pools are 8-aligned with 16 bytes of tail slack)
+__device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7) * 8u;
+    const uint64_t lo = q[0];
+    return sh == 0 ? lo : (lo >> sh) | (q[1] << (64u - sh));
+}
+
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
-    for (uint32_t i = 0; i < n; i++)
-        if (a[i] != b[i]) return false;
-    return true;
+    uint32_t i = 0;
+    for (; i + 8 <= n; i += 8)
+        if (ld8(a + i) != ld8(b + i)) return false;
+    if (i == n) return true;
+    const uint64_t mask = (1ull << ((n - i) * 8u)) - 1ull;
+    return ((ld8(a + i) ^ ld8(b + i)) & mask) == 0;
 }
 
 // match / startsWith / endsWith (mixer/pkg/il/runtime/externs.go:108-128)
@@ -375,88 +381,117 @@ __device__ __forceinline__ void log_guard_errors(const mxp_kargs& A, uint32_t e,
 
 // Phase 1 + in-wave phase 2 over 32-rule groups.
 //
-// Workgroup = 4 wavefronts over one tile of 64 requests (one per lane); wave w sweeps groups
-// [g0, g0 + groups_per_wave).  Per group:
+// Workgroup = 4 wavefronts over one tile of 64 requests (one per lane); wave w takes
+// `groups_per_wave` consecutive entries of the group list (kargs.glist).  Per group:
 //   phase 1  every rule's leading atom at once: each column segment loads its column value once per
 //            lane and compares it with the segment's constants (scalar operands), giving per lane the
 //            32-bit words eq / ok; the group's mode masks turn them into match / error / continue
 //            words with a handful of bit operations;
-//   phase 2  the VM runs, rule by rule, for the continuing lanes (indexed rules excepted: their
-//            continuing pairs are enumerated by mxp_index_kernel).
-// Results: one coalesced store per word and plane, out[g * N + request].
-extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
-    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+//   phase 2  (kVM only) the VM runs, rule by rule, for the continuing lanes -- indexed rules
+//            excepted: their continuing pairs are enumerated by mxp_index_kernel.
+// The host splits the groups: those that can leave phase 1 with continuing lanes (rules without a
+// guard, OR guards, non-indexed AND guards) go to mxp_eval_kernel (kVM), the rest to the lean
+// mxp_guard_kernel, which carries no VM and so keeps far fewer registers.  Group descriptors are
+// fetched four at a time with one vector load (lane 16 j + f = word f of the j-th group) and read
+// back with v_readlane.  Results: one coalesced store per word and plane, out[g * N + request].
+template <bool kVM>
+__device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)[256]) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = uni(tid >> 6);
     const uint32_t req = blockIdx.x * 64u + lane;
     const bool valid = req < A.n;
     const uint64_t N = A.n;
-    const uint32_t g0 = (blockIdx.y * 4u + wave) * A.groups_per_wave;
-    const uint32_t g1 = min(g0 + A.groups_per_wave, A.n_words);
+    const uint32_t i0 = (blockIdx.y * 4u + wave) * A.groups_per_wave;
+    const uint32_t i1 = min(i0 + A.groups_per_wave, A.n_glist);
     // Eval mode (out_vals) needs every result register: whole programs, no guards, no index
     const bool guards_on = !(A.out_vals || (A.flags & 2u));
     uint32_t cached = MXP_VM_DONE;
     uint32_t ck = MXP_ABSENT;
     uint64_t cv = 0;
-    for (uint32_t g = g0; g < g1; g++) {
-        const mxp_group* G = A.groups + g;
-        const uint32_t all = uni(G->all), guarded = uni(G->guarded), only = uni(G->only), orm = uni(G->orm),
-                       neg = uni(G->neg), seg0 = uni(G->seg0), nseg = uni(G->nseg), indexed = uni(G->indexed);
-        const uint32_t r0 = g * 32u;
-        uint32_t m = 0, e = 0, cont = 0;
-        if (guards_on) {
-            // ---- phase 1
-            uint32_t eq = 0, ok = 0;
-            for (uint32_t s = seg0; s < seg0 + nseg; s++) {
-                const uint32_t col = uni(A.segs[s].col), okset = uni(A.segs[s].okset), rules = uni(A.segs[s].rules),
-                               cmp = uni(A.segs[s].cmp);
-                if (col != cached) {
-                    cached = col;
-                    if (valid) {
-                        ck = A.kinds[(uint64_t)col * N + req];
-                        cv = A.vals[(uint64_t)col * N + req];
+    for (uint32_t c0 = i0; c0 < i1; c0 += 4) {
+        uint32_t D = 0;
+        if (c0 + (lane >> 4) < i1) D = ((const uint32_t*)(A.groups + A.glist[c0 + (lane >> 4)]))[lane & 15u];
+        const uint32_t cn = min(4u, i1 - c0);
+        for (uint32_t j = 0; j < cn; j++) {
+#define GF(f) __builtin_amdgcn_readlane(D, j * 16u + (f))
+            const uint32_t all = GF(0), guarded = GF(1), only = GF(2), orm = GF(3), neg = GF(4), indexed = GF(5),
+                           seg0 = GF(6), nseg = GF(7), g = GF(12);
+            const uint32_t r0 = g * 32u;
+            uint32_t m = 0, e = 0, cont = 0;
+            if (guards_on) {
+                // ---- phase 1
+                uint32_t eq = 0, ok = 0;
+                for (uint32_t s = 0; s < nseg; s++) {
+                    uint32_t col, okset, rules, cmp;
+                    if (s == 0) {
+                        col = GF(8);
+                        okset = GF(9);
+                        rules = GF(10);
+                        cmp = GF(11);
+                    } else {
+                        const mxp_seg* S = A.segs + seg0 + s - 1;
+                        col = uni(S->col);
+                        okset = uni(S->okset);
+                        rules = uni(S->rules);
+                        cmp = uni(S->cmp);
+                    }
+                    if (col != cached) {
+                        cached = col;
+                        if (valid) {
+                            ck = A.kinds[(uint64_t)col * N + req];
+                            cv = A.vals[(uint64_t)col * N + req];
+                        }
+                    }
+                    ok |= ((okset >> ck) & 1u) ? rules : 0u;
+                    if (cmp) eq |= seg_eq((cuint64*)A.gk + r0, cmp, cv);
+                }
+#undef GF
+                const uint32_t atom = eq ^ neg;
+                const uint32_t andm = guarded & ~(only | orm);
+                // indexed rules: atom unknown here (no compare), match 0, continuing pairs
+                // enumerated by mxp_index_kernel
+                m = atom & (only | orm) & ok;
+                cont = (((atom & andm) | (~atom & orm)) & ok & ~indexed) | (all & ~guarded);
+                e = guarded & ~ok;
+                if (!valid) m = e = cont = 0;
+                if (e && A.errlog) log_guard_errors(A, e, r0, req);
+            } else {
+                cont = valid ? all : 0u;
+            }
+            // ---- phase 2 (in-wave)
+            if (kVM) {
+                for (uint32_t bits = wave_or(cont); bits && !(A.flags & 1u); bits &= bits - 1) {
+                    const uint32_t k = __builtin_ctz(bits);
+                    const uint32_t bit = 1u << k;
+                    const bool need = (cont & bit) != 0;
+                    const uint32_t rule = r0 + k;
+                    const uint32_t gm = uni(A.guards[rule].mode);
+                    const uint32_t pc0 = (!guards_on || (gm & 0xFFu) == GM_NONE) ? 0u : (gm >> 16);
+                    const uint32_t base = uni(A.rule_off[rule]);
+                    const uint32_t len = uni(A.rule_off[rule + 1]) - base;
+                    const uint32_t code = run_rule(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, pc0, need, rule,
+                                                   req, regs, tid);
+                    if (need) {
+                        m |= code == PC_TRUE ? bit : 0u;
+                        e |= code >= PC_ERROR ? bit : 0u;
                     }
                 }
-                ok |= ((okset >> ck) & 1u) ? rules : 0u;
-                if (cmp) eq |= seg_eq((cuint64*)A.gk + r0, cmp, cv);
             }
-            const uint32_t atom = eq ^ neg;
-            const uint32_t andm = guarded & ~(only | orm);
-            // indexed rules: atom unknown here (no compare), match 0, continuing pairs enumerated
-            // by mxp_index_kernel
-            m = atom & (only | orm) & ok;
-            cont = (((atom & andm) | (~atom & orm)) & ok & ~indexed) | (all & ~guarded);
-            e = guarded & ~ok;
-            if (!valid) m = e = cont = 0;
-            if (e && A.errlog) log_guard_errors(A, e, r0, req);
-        } else {
-            cont = valid ? all : 0u;
-        }
-        const uint32_t inwave = cont;
-        // ---- phase 2 (in-wave)
-        for (uint32_t bits = wave_or(inwave); bits && !(A.flags & 1u); bits &= bits - 1) {
-            const uint32_t k = __builtin_ctz(bits);
-            const uint32_t bit = 1u << k;
-            const bool need = (inwave & bit) != 0;
-            const uint32_t rule = r0 + k;
-            const uint32_t gm = uni(A.guards[rule].mode);
-            const uint32_t pc0 = (!guards_on || (gm & 0xFFu) == GM_NONE) ? 0u : (gm >> 16);
-            const uint32_t base = uni(A.rule_off[rule]);
-            const uint32_t len = uni(A.rule_off[rule + 1]) - base;
-            const uint32_t code = run_rule(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, pc0, need, rule, req,
-                                           regs, tid);
-            if (need) {
-                m |= code == PC_TRUE ? bit : 0u;
-                e |= code >= PC_ERROR ? bit : 0u;
+            if (valid) {
+                if (A.out_match) A.out_match[(uint64_t)g * N + req] = m;
+                if (A.out_err) A.out_err[(uint64_t)g * N + req] = e;
             }
-        }
-        if (valid) {
-            if (A.out_match) A.out_match[(uint64_t)g * N + req] = m;
-            if (A.out_err) A.out_err[(uint64_t)g * N + req] = e;
         }
     }
 }
+
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    eval_groups<true>(A, regs);
+}
+
+extern "C" __global__ __launch_bounds__(256) void mxp_guard_kernel(mxp_kargs A) { eval_groups<false>(A, nullptr); }
 
 // Guard-index phase: the continuing pairs of indexed rules (`attr == K && <continuation>`), found
 // per request by a hash lookup of its column value instead of by comparing against every rule.
@@ -551,8 +586,11 @@ extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t
     }
 }
 
-extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s) {
+    if (vm)
+        hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    else
+        hipLaunchKernelGGL(mxp_guard_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

@@ -76,10 +76,17 @@ typedef struct mxp_group {
     uint32_t only;     // GM_ONLY
     uint32_t orm;      // GM_OR  (GM_AND = guarded & ~only & ~orm)
     uint32_t neg;      // negated atoms
-    uint32_t seg0;     // segments [seg0, seg0 + nseg) of kargs.segs
-    uint32_t nseg;
     uint32_t indexed;  // rules whose continuing pairs come from the guard index (mxp_index_kernel)
-} mxp_group;
+    uint32_t seg0;     // segments 1 .. nseg-1 are kargs.segs[seg0 .. seg0 + nseg - 2]
+    uint32_t nseg;
+    uint32_t s_col;    // segment 0, inline (mxp_seg fields)
+    uint32_t s_okset;
+    uint32_t s_rules;
+    uint32_t s_cmp;
+    uint32_t id;       // group index g (rules 32 g .. 32 g + 31)
+    uint32_t vm;       // 1: some rule can leave phase 1 with continuing lanes (mxp_eval_kernel)
+    uint32_t pad[2];
+} mxp_group;           // 64 B: fetched four at a time by one wavefront-wide load
 
 typedef struct mxp_seg {
     uint32_t col;      // column read by the guards of the segment
