@@ -93,6 +93,36 @@ int mxp_pair_error(mxp_engine* eng, uint32_t request, uint32_t rule, char* buf, 
 uint64_t mxp_error_count(mxp_engine* eng);
 
 /*
+ * Batched runtime.resolver (mixer/pkg/runtime/resolver.go:110-238).
+ *
+ * mxp_resolver_set configures resolution for the compiled rule set (call after mxp_ruleset_compile;
+ * a new compile clears it).  Per rule: its config namespace, the varieties it has actions for (bit v
+ * = adptTmpl.TemplateVariety v), whether it is a TCP rule (rule.rtype.IsTCP()), and whether its
+ * match is empty (selected without evaluation).  Rules of one namespace must be contiguous and in
+ * the reference's resolution order (the order of the namespace's rule slice); MXP_ERR_ARG otherwise.
+ * identity_attr names the destination attribute (`destination.service`), default_ns the config
+ * default namespace.
+ *
+ * mxp_resolve_batch evaluates every rule against every bag and resolves each request for `variety`:
+ *   status[q]   MXP_RESOLVE_OK, or the reason Resolve returns an error:
+ *               NO_IDENTITY / BAD_IDENTITY  (destAndNamespace, resolver.go:180-199),
+ *               PRED_ERROR  (first predicate error in resolution order, resolver.go:226-228):
+ *               err_rule[q] is that rule, mxp_pair_error(q, err_rule[q]) its error text;
+ *   sel_off[q] .. sel_off[q+1]  the selected rules, in resolution order (sel_off has n+1 entries);
+ *   sel_rules   capacity sel_cap entries; when too small, MXP_ERR_NOMEM is returned with status,
+ *               err_rule and sel_off complete, so the caller can retry with sel_off[n].
+ */
+#define MXP_RESOLVE_OK 0
+#define MXP_RESOLVE_NO_IDENTITY 1
+#define MXP_RESOLVE_BAD_IDENTITY 2
+#define MXP_RESOLVE_PRED_ERROR 3
+int mxp_resolver_set(mxp_engine* eng, const char* identity_attr, const char* default_ns,
+                     const char* const* rule_ns, const uint32_t* variety_mask, const uint8_t* is_tcp,
+                     const uint8_t* empty_match, uint32_t n);
+int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
+                      uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap);
+
+/*
  * Device-resident batches (benchmarking and pipelining): pack + upload once, evaluate many times.
  * mxp_batch_eval_device enqueues on `stream` (a hipStream_t; NULL = engine stream) and writes the
  * bitmaps to DEVICE pointers (rule-word-major, as above).  Nothing is synchronised.

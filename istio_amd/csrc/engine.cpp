@@ -8,250 +8,7 @@
 //     `map[const key]` lookups pre-extracted into virtual columns;
 //   * kernel launches on the engine's HIP stream and reporting of error pairs with the reference's
 //     exact error texts.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <map>
-#include <memory>
-#include <string>
-#include <unordered_map>
-#include <vector>
-
-#include "../../include/mxp.h"
-#include "goutil.h"
-#include "ilgen.h"
-#include "kargs.h"
-#include "lower.h"
-#include "vmopt.h"
-
-extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
-extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
-extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
-                                      unsigned long long* hits, hipStream_t s);
-
-namespace {
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t n = 0;
-    DevBuf() = default;
-    DevBuf(const DevBuf&) = delete;
-    DevBuf& operator=(const DevBuf&) = delete;
-    ~DevBuf() { reset(); }
-    void reset() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-    }
-    hipError_t alloc(size_t bytes) {
-        reset();
-        if (bytes == 0) bytes = 16;
-        n = bytes;
-        return hipMalloc(&p, bytes);
-    }
-    template <class T>
-    T* as() const {
-        return static_cast<T*>(p);
-    }
-};
-
-struct TimeKey {
-    int64_t s;
-    int32_t ns;
-    bool operator<(const TimeKey& o) const { return s != o.s ? s < o.s : ns < o.ns; }
-};
-
-constexpr uint64_t kNoValue = ~0ull;
-
-// Device string pool: every string starts 8-byte aligned (zero padded), with 16 bytes of slack at
-// the end, so the kernels compare strings a u64 word at a time (two aligned loads + funnel shift for
-// unaligned operands) without reading past the allocation.  desc[i] = offset << 24 | length.
-bool string_pool(const std::vector<std::string>& strs, std::vector<uint64_t>* desc, std::string* blob) {
-    desc->assign(strs.size(), 0);
-    blob->clear();
-    for (size_t i = 0; i < strs.size(); i++) {
-        if (strs[i].size() >= (1u << 24)) return false;
-        (*desc)[i] = ((uint64_t)blob->size() << 24) | strs[i].size();
-        blob->append(strs[i]);
-        blob->append((8 - blob->size() % 8) % 8, '\0');
-    }
-    blob->append(16, '\0');
-    return true;
-}
-
-// column kinds that pass a guard's want class (W_*) or a virtual-column guard (GK_VCOL)
-uint32_t okset_of(uint32_t kind) {
-    switch (kind) {
-    case W_S: return 1u << MXP_STRING;
-    case W_B: return 1u << MXP_BOOL;
-    case W_I: return (1u << MXP_INT64) | (1u << MXP_DURATION);
-    case W_D: return 1u << MXP_DOUBLE;
-    default: return 1u << VC_VALUE;  // GK_VCOL
-    }
-}
-
-}  // namespace
-
-struct mxp_dbatch {
-    uint32_t n = 0;
-    DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
-    std::vector<std::string> overlay;                 // batch strings not in the rule set's pool
-    std::vector<std::string> overlay_bytes;           // batch byte strings (canonical)
-    std::vector<TimeKey> overlay_times;
-};
-
-struct mxp_engine : public mxp::LowerTables {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    std::string last_error;
-
-    mxp::Vocabulary vocab;
-    mxp::FuncMap fmap = mxp::default_func_map();
-
-    // rule-set-global interning
-    std::unordered_map<std::string, uint32_t> gstr_ids;
-    std::vector<std::string> gstrs;
-    std::unordered_map<std::string, uint32_t> gbytes_ids;   // exact []byte values
-    std::vector<std::string> gbytes;
-    std::unordered_map<std::string, uint32_t> gcanon_ids;   // their net.IP.Equal classes
-    std::vector<std::string> gcanon;
-    std::map<TimeKey, uint32_t> gtime_ids;
-    std::vector<TimeKey> gtimes;
-    std::vector<std::string> cols;
-    std::unordered_map<std::string, uint32_t> col_ids;
-    std::vector<std::pair<std::string, std::string>> vcols;
-    std::map<std::pair<std::string, std::string>, uint32_t> vcol_ids;
-    uint32_t empty_sid = 0;
-
-    struct Rule {
-        int32_t status = MXP_RULE_OK;
-        std::string error;
-        int32_t value_type = 0;
-        uint8_t il_ret = 0;
-        std::string il_text;
-        mxp::LoweredRule low;
-    };
-    std::vector<Rule> rules;
-    bool have_rules = false;
-    bool need_ipof = false, need_tsof = false, need_strings = false, need_maps = false;
-
-    DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
-    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rconst, d_idx, d_hents, d_postings;
-    DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
-    uint32_t n_glean = 0, n_gvm = 0;
-    uint32_t n_idx = 0, n_indexed = 0;
-    uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
-    uint32_t groups_per_wave = 4; // MXP_GPW
-    // optional per-kernel timing of device evaluations (mxp_set_timing): events around each launch
-    bool timing = false;
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    bool ev_index = false;
-    uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS: ablation only (1 no in-wave VM, 2 no guards: results invalid; 8 no guard index)
-    DevBuf d_errlog, d_errcount;
-    uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
-
-    // last batch error details: key = request << 32 | rule
-    std::unordered_map<uint64_t, std::pair<uint32_t, std::string>> last_errors;
-    uint64_t last_error_count = 0;
-    std::unique_ptr<mxp_dbatch> last_db;  // keeps the last batch's interned overlays for decoding
-
-    // ---------------------------------------------------------------- LowerTables
-    uint32_t intern_string(const std::string& s) override {
-        auto it = gstr_ids.find(s);
-        if (it != gstr_ids.end()) return it->second;
-        uint32_t id = (uint32_t)gstrs.size();
-        gstr_ids.emplace(s, id);
-        gstrs.push_back(s);
-        return id;
-    }
-    uint64_t intern_bytes(const std::string& raw) override {
-        std::string canon = mxp::ip_canonical((const uint8_t*)raw.data(), raw.size());
-        return MXP_BYTES_ID(intern_in(gcanon_ids, gcanon, canon), intern_in(gbytes_ids, gbytes, raw));
-    }
-    static uint32_t intern_in(std::unordered_map<std::string, uint32_t>& ids, std::vector<std::string>& v,
-                              const std::string& s) {
-        auto it = ids.find(s);
-        if (it != ids.end()) return it->second;
-        uint32_t id = (uint32_t)v.size();
-        ids.emplace(s, id);
-        v.push_back(s);
-        return id;
-    }
-    uint32_t intern_time(int64_t s, int32_t ns) override {
-        TimeKey k{s, ns};
-        auto it = gtime_ids.find(k);
-        if (it != gtime_ids.end()) return it->second;
-        uint32_t id = (uint32_t)gtimes.size();
-        gtime_ids.emplace(k, id);
-        gtimes.push_back(k);
-        return id;
-    }
-    uint32_t column(const std::string& attr) override {
-        auto it = col_ids.find(attr);
-        if (it != col_ids.end()) return it->second;
-        uint32_t id = (uint32_t)cols.size();
-        col_ids.emplace(attr, id);
-        cols.push_back(attr);
-        return id;
-    }
-    uint32_t vcolumn(const std::string& attr, const std::string& key) override {
-        auto k = std::make_pair(attr, key);
-        auto it = vcol_ids.find(k);
-        if (it != vcol_ids.end()) return it->second;
-        uint32_t id = (uint32_t)vcols.size();
-        vcol_ids.emplace(k, id);
-        vcols.push_back(k);
-        intern_string(key);
-        return id;
-    }
-    int32_t attr_type(const std::string& attr) override {
-        auto it = vocab.find(attr);
-        return it == vocab.end() ? -1 : it->second;
-    }
-
-    int fail(int code, const std::string& msg) {
-        last_error = msg;
-        return code;
-    }
-    int hipfail(hipError_t e, const char* what) {
-        last_error = std::string(what) + ": " + hipGetErrorString(e);
-        return MXP_ERR_DEVICE;
-    }
-
-    void reset_tables() {
-        gstr_ids.clear();
-        gstrs.clear();
-        gbytes_ids.clear();
-        gbytes.clear();
-        gcanon_ids.clear();
-        gcanon.clear();
-        gtime_ids.clear();
-        gtimes.clear();
-        cols.clear();
-        col_ids.clear();
-        vcols.clear();
-        vcol_ids.clear();
-        rules.clear();
-        have_rules = false;
-        need_ipof = need_tsof = need_strings = need_maps = false;
-        empty_sid = intern_string("");
-    }
-
-    int compile(const char* const* exprs, uint32_t n, int32_t* status);
-    int pack(const mxp_bag_batch* b, mxp_dbatch* db);
-    void fill_args(mxp_kargs* A, const mxp_dbatch* db) const;
-    int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log);
-    std::string format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r) const;
-    std::string string_of(const mxp_dbatch* db, uint64_t sid) const {
-        if (!db) db = last_db.get();
-        if (sid < gstrs.size()) return gstrs[sid];
-        uint64_t j = sid - gstrs.size();
-        return (db && j < db->overlay.size()) ? db->overlay[j] : std::string("?");
-    }
-};
+#include "engine_impl.h"
 
 // ------------------------------------------------------------------------------------ compile
 int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
@@ -984,26 +741,55 @@ int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_request
     return e == hipSuccess ? MXP_OK : eng->hipfail(e, "launch hits");
 }
 
+int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv,
+                         std::unique_ptr<mxp_dbatch>& db) {
+    if (!batch) return MXP_ERR_ARG;
+    if (!have_rules) return fail(MXP_ERR_STATE, "no rule set compiled");
+    if (device < 0) return fail(MXP_ERR_STATE, "host-only engine");
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hipfail(e, "hipSetDevice");
+    db.reset(new mxp_dbatch());
+    int rc = pack(batch, db.get());
+    if (rc) return rc;
+    const uint32_t n = batch->n_requests;
+    const uint32_t R = (uint32_t)rules.size();
+    const uint32_t W = (R + 31) / 32;
+    if ((e = dm.alloc((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc match");
+    if ((e = de.alloc((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc err");
+    if (dv && (e = dv->alloc((size_t)n * R * 8)) != hipSuccess) return hipfail(e, "alloc values");
+    return launch(db.get(), stream, dm.as<uint32_t>(), de.as<uint32_t>(), dv ? dv->as<uint64_t>() : nullptr, true);
+}
+
+int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_dbatch>& db) {
+    hipError_t e;
+    uint32_t cnt = 0;
+    if ((e = hipMemcpyAsync(&cnt, d_errcount.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        return hipfail(e, "download errcount");
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "eval sync");
+    last_error_count = cnt;
+    last_errors.clear();
+    uint32_t kept = std::min(cnt, errcap);
+    if (kept) {
+        std::vector<mxp_err_rec> recs(kept);
+        if ((e = hipMemcpy(recs.data(), d_errlog.p, kept * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
+            return hipfail(e, "download errlog");
+        for (auto& r : recs) last_errors[((uint64_t)r.req << 32) | r.rule] = {r.code, format_error(batch, db.get(), r)};
+    }
+    last_db = std::move(db);
+    return MXP_OK;
+}
+
 static int eval_common(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* match_bits, uint32_t* err_bits,
                        uint64_t* values, uint8_t* codes) {
     if (!eng || !batch) return MXP_ERR_ARG;
-    if (!eng->have_rules) return eng->fail(MXP_ERR_STATE, "no rule set compiled");
-    if (eng->device < 0) return eng->fail(MXP_ERR_STATE, "host-only engine");
-    hipError_t e = hipSetDevice(eng->device);
-    if (e != hipSuccess) return eng->hipfail(e, "hipSetDevice");
-    std::unique_ptr<mxp_dbatch> db(new mxp_dbatch());
-    int rc = eng->pack(batch, db.get());
+    std::unique_ptr<mxp_dbatch> db;
+    DevBuf dm, de, dv;
+    int rc = eng->evaluate(batch, dm, de, values ? &dv : nullptr, db);
     if (rc) return rc;
     const uint32_t n = batch->n_requests;
     const uint32_t R = (uint32_t)eng->rules.size();
     const uint32_t W = (R + 31) / 32;
-    DevBuf dm, de, dv;
-    if ((e = dm.alloc((size_t)W * n * 4)) != hipSuccess) return eng->hipfail(e, "alloc match");
-    if ((e = de.alloc((size_t)W * n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err");
-    if (values && (e = dv.alloc((size_t)n * R * 8)) != hipSuccess) return eng->hipfail(e, "alloc values");
-    rc = eng->launch(db.get(), eng->stream, dm.as<uint32_t>(), de.as<uint32_t>(), values ? dv.as<uint64_t>() : nullptr,
-                     true);
-    if (rc) return rc;
+    hipError_t e;
     std::vector<uint32_t> hm, he;
     if (match_bits || codes) {
         hm.resize((size_t)W * n);
@@ -1017,21 +803,7 @@ static int eval_common(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* ma
     }
     if (values && (e = hipMemcpyAsync(values, dv.p, (size_t)n * R * 8, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
         return eng->hipfail(e, "download values");
-    uint32_t cnt = 0;
-    if ((e = hipMemcpyAsync(&cnt, eng->d_errcount.p, 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-        return eng->hipfail(e, "download errcount");
-    if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "eval sync");
-    eng->last_error_count = cnt;
-    eng->last_errors.clear();
-    uint32_t kept = std::min(cnt, eng->errcap);
-    if (kept) {
-        std::vector<mxp_err_rec> recs(kept);
-        if ((e = hipMemcpy(recs.data(), eng->d_errlog.p, kept * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
-            return eng->hipfail(e, "download errlog");
-        for (auto& r : recs)
-            eng->last_errors[((uint64_t)r.req << 32) | r.rule] = {r.code, eng->format_error(batch, db.get(), r)};
-    }
-    eng->last_db = std::move(db);
+    if ((rc = eng->collect_errors(batch, db))) return rc;
     if (match_bits) memcpy(match_bits, hm.data(), hm.size() * 4);
     if (err_bits) memcpy(err_bits, he.data(), he.size() * 4);
     if (codes) {

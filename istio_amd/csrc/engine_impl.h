@@ -1,0 +1,263 @@
+// engine_impl.h -- engine internals shared by the host sources of libmxp (engine.cpp: rule sets,
+// packing, evaluation, C-ABI; resolver.cpp: batched runtime.resolver).  Not part of the C-ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mxp.h"
+#include "goutil.h"
+#include "ilgen.h"
+#include "kargs.h"
+#include "lower.h"
+#include "vmopt.h"
+
+extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
+extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
+extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
+                                      unsigned long long* hits, hipStream_t s);
+
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(size_t bytes) {
+        reset();
+        if (bytes == 0) bytes = 16;
+        n = bytes;
+        return hipMalloc(&p, bytes);
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+struct TimeKey {
+    int64_t s;
+    int32_t ns;
+    bool operator<(const TimeKey& o) const { return s != o.s ? s < o.s : ns < o.ns; }
+};
+
+constexpr uint64_t kNoValue = ~0ull;
+
+// Device string pool: every string starts 8-byte aligned (zero padded), with 16 bytes of slack at
+// the end, so the kernels compare strings a u64 word at a time (two aligned loads + funnel shift for
+// unaligned operands) without reading past the allocation.  desc[i] = offset << 24 | length.
+inline bool string_pool(const std::vector<std::string>& strs, std::vector<uint64_t>* desc, std::string* blob) {
+    desc->assign(strs.size(), 0);
+    blob->clear();
+    for (size_t i = 0; i < strs.size(); i++) {
+        if (strs[i].size() >= (1u << 24)) return false;
+        (*desc)[i] = ((uint64_t)blob->size() << 24) | strs[i].size();
+        blob->append(strs[i]);
+        blob->append((8 - blob->size() % 8) % 8, '\0');
+    }
+    blob->append(16, '\0');
+    return true;
+}
+
+// column kinds that pass a guard's want class (W_*) or a virtual-column guard (GK_VCOL)
+inline uint32_t okset_of(uint32_t kind) {
+    switch (kind) {
+    case W_S: return 1u << MXP_STRING;
+    case W_B: return 1u << MXP_BOOL;
+    case W_I: return (1u << MXP_INT64) | (1u << MXP_DURATION);
+    case W_D: return 1u << MXP_DOUBLE;
+    default: return 1u << VC_VALUE;  // GK_VCOL
+    }
+}
+
+struct mxp_dbatch {
+    uint32_t n = 0;
+    DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
+    std::vector<std::string> overlay;                 // batch strings not in the rule set's pool
+    std::vector<std::string> overlay_bytes;           // batch byte strings (canonical)
+    std::vector<TimeKey> overlay_times;
+};
+
+struct mxp_engine : public mxp::LowerTables {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+
+    mxp::Vocabulary vocab;
+    mxp::FuncMap fmap = mxp::default_func_map();
+
+    // rule-set-global interning
+    std::unordered_map<std::string, uint32_t> gstr_ids;
+    std::vector<std::string> gstrs;
+    std::unordered_map<std::string, uint32_t> gbytes_ids;   // exact []byte values
+    std::vector<std::string> gbytes;
+    std::unordered_map<std::string, uint32_t> gcanon_ids;   // their net.IP.Equal classes
+    std::vector<std::string> gcanon;
+    std::map<TimeKey, uint32_t> gtime_ids;
+    std::vector<TimeKey> gtimes;
+    std::vector<std::string> cols;
+    std::unordered_map<std::string, uint32_t> col_ids;
+    std::vector<std::pair<std::string, std::string>> vcols;
+    std::map<std::pair<std::string, std::string>, uint32_t> vcol_ids;
+    uint32_t empty_sid = 0;
+
+    struct Rule {
+        int32_t status = MXP_RULE_OK;
+        std::string error;
+        int32_t value_type = 0;
+        uint8_t il_ret = 0;
+        std::string il_text;
+        mxp::LoweredRule low;
+    };
+    std::vector<Rule> rules;
+    bool have_rules = false;
+    bool need_ipof = false, need_tsof = false, need_strings = false, need_maps = false;
+
+    DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
+    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rconst, d_idx, d_hents, d_postings;
+    DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
+    uint32_t n_glean = 0, n_gvm = 0;
+    uint32_t n_idx = 0, n_indexed = 0;
+    uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
+    uint32_t groups_per_wave = 4; // MXP_GPW
+    // optional per-kernel timing of device evaluations (mxp_set_timing): events around each launch
+    bool timing = false;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    bool ev_index = false;
+    uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS: ablation only (1 no in-wave VM, 2 no guards: results invalid; 8 no guard index)
+    DevBuf d_errlog, d_errcount;
+    uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
+
+    // last batch error details: key = request << 32 | rule
+    std::unordered_map<uint64_t, std::pair<uint32_t, std::string>> last_errors;
+    uint64_t last_error_count = 0;
+    std::unique_ptr<mxp_dbatch> last_db;  // keeps the last batch's interned overlays for decoding
+
+    // ---------------------------------------------------------------- LowerTables
+    uint32_t intern_string(const std::string& s) override {
+        auto it = gstr_ids.find(s);
+        if (it != gstr_ids.end()) return it->second;
+        uint32_t id = (uint32_t)gstrs.size();
+        gstr_ids.emplace(s, id);
+        gstrs.push_back(s);
+        return id;
+    }
+    uint64_t intern_bytes(const std::string& raw) override {
+        std::string canon = mxp::ip_canonical((const uint8_t*)raw.data(), raw.size());
+        return MXP_BYTES_ID(intern_in(gcanon_ids, gcanon, canon), intern_in(gbytes_ids, gbytes, raw));
+    }
+    static uint32_t intern_in(std::unordered_map<std::string, uint32_t>& ids, std::vector<std::string>& v,
+                              const std::string& s) {
+        auto it = ids.find(s);
+        if (it != ids.end()) return it->second;
+        uint32_t id = (uint32_t)v.size();
+        ids.emplace(s, id);
+        v.push_back(s);
+        return id;
+    }
+    uint32_t intern_time(int64_t s, int32_t ns) override {
+        TimeKey k{s, ns};
+        auto it = gtime_ids.find(k);
+        if (it != gtime_ids.end()) return it->second;
+        uint32_t id = (uint32_t)gtimes.size();
+        gtime_ids.emplace(k, id);
+        gtimes.push_back(k);
+        return id;
+    }
+    uint32_t column(const std::string& attr) override {
+        auto it = col_ids.find(attr);
+        if (it != col_ids.end()) return it->second;
+        uint32_t id = (uint32_t)cols.size();
+        col_ids.emplace(attr, id);
+        cols.push_back(attr);
+        return id;
+    }
+    uint32_t vcolumn(const std::string& attr, const std::string& key) override {
+        auto k = std::make_pair(attr, key);
+        auto it = vcol_ids.find(k);
+        if (it != vcol_ids.end()) return it->second;
+        uint32_t id = (uint32_t)vcols.size();
+        vcol_ids.emplace(k, id);
+        vcols.push_back(k);
+        intern_string(key);
+        return id;
+    }
+    int32_t attr_type(const std::string& attr) override {
+        auto it = vocab.find(attr);
+        return it == vocab.end() ? -1 : it->second;
+    }
+
+    int fail(int code, const std::string& msg) {
+        last_error = msg;
+        return code;
+    }
+    int hipfail(hipError_t e, const char* what) {
+        last_error = std::string(what) + ": " + hipGetErrorString(e);
+        return MXP_ERR_DEVICE;
+    }
+
+    void reset_tables() {
+        resolver = ResolverConf();  // a new rule set needs a new resolver configuration
+        gstr_ids.clear();
+        gstrs.clear();
+        gbytes_ids.clear();
+        gbytes.clear();
+        gcanon_ids.clear();
+        gcanon.clear();
+        gtime_ids.clear();
+        gtimes.clear();
+        cols.clear();
+        col_ids.clear();
+        vcols.clear();
+        vcol_ids.clear();
+        rules.clear();
+        have_rules = false;
+        need_ipof = need_tsof = need_strings = need_maps = false;
+        empty_sid = intern_string("");
+    }
+
+    // batched runtime.resolver configuration (resolver.cpp)
+    struct ResolverConf {
+        bool set = false;
+        std::string identity, default_ns;
+        std::vector<std::string> ns_names;               // namespaces that have rules
+        std::unordered_map<std::string, uint32_t> ns_ids;
+        std::vector<uint32_t> ns_lo, ns_hi;              // contiguous rule range per namespace
+        std::vector<uint32_t> vmask;                     // per rule: varieties with actions
+        std::vector<uint8_t> tcp, empty;                 // per rule: TCP rule; empty match
+        uint32_t default_id = 0xFFFFFFFFu;
+    } resolver;
+
+    int compile(const char* const* exprs, uint32_t n, int32_t* status);
+    // pack + launch into fresh device bitmaps (dm, de; dv = Eval registers when non-null)
+    int evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv, std::unique_ptr<mxp_dbatch>& db);
+    // wait for the evaluation, fetch and format its error records, keep `db` as the last batch
+    int collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_dbatch>& db);
+    int pack(const mxp_bag_batch* b, mxp_dbatch* db);
+    void fill_args(mxp_kargs* A, const mxp_dbatch* db) const;
+    int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log);
+    std::string format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r) const;
+    std::string string_of(const mxp_dbatch* db, uint64_t sid) const {
+        if (!db) db = last_db.get();
+        if (sid < gstrs.size()) return gstrs[sid];
+        uint64_t j = sid - gstrs.size();
+        return (db && j < db->overlay.size()) ? db->overlay[j] : std::string("?");
+    }
+};
+

@@ -1,0 +1,184 @@
+// resolver.cpp -- batched runtime.resolver on top of the predicate bitmaps (include/mxp.h,
+// resolve.hip).
+//
+// Reference: resolver.Resolve (mixer/pkg/runtime/resolver.go:110-168), destAndNamespace
+// (:180-199), filterActions (:202-238).  The host derives each request's namespace and TCP flag
+// from its bag exactly as destAndNamespace / filterActions do; the GPU walks the namespace rule
+// ranges over the bitmaps mxp_eval_kernel / mxp_index_kernel produced.
+#include <cstring>
+#include <numeric>
+
+#include "engine_impl.h"
+#include "resolve_args.h"
+
+extern "C" hipError_t mxp_launch_resolve(const mxp_resolve_args* a, int write, hipStream_t s);
+
+namespace {
+
+const char* const kProtocolAttr = "context.protocol";  // ContextProtocolAttributeName (resolver.go:95)
+
+// namespace info of every request: destAndNamespace + the tcp flag of filterActions
+int request_info(mxp_engine* eng, const mxp_bag_batch* b, std::vector<uint32_t>* info) {
+    const auto& R = eng->resolver;
+    const uint32_t n = b->n_requests;
+    int idc = -1, pc = -1;
+    for (uint32_t c = 0; c < b->n_columns; c++) {
+        if (R.identity == b->column_names[c]) idc = (int)c;
+        if (strcmp(kProtocolAttr, b->column_names[c]) == 0) pc = (int)c;
+    }
+    auto str = [&](uint64_t sid, size_t* len) {
+        *len = (size_t)(b->str_offsets[sid + 1] - b->str_offsets[sid]);
+        return (const char*)b->str_bytes + b->str_offsets[sid];
+    };
+    info->assign(n, MXP_NS_MISSING);
+    std::string ns;
+    for (uint32_t q = 0; q < n; q++) {
+        // attrs.Get(idAttr): nil -> "identity not found"; not a string -> "identity must be string"
+        if (idc < 0 || b->kinds[idc][q] == MXP_ABSENT) continue;
+        if (b->kinds[idc][q] != MXP_STRING) {
+            (*info)[q] = MXP_NS_NOTSTRING;
+            continue;
+        }
+        size_t len;
+        const char* d = str(b->values[idc][q], &len);
+        // strings.SplitN(dest, ".", 3): ns = splits[1] when there is at least one '.'
+        const char* dot1 = (const char*)memchr(d, '.', len);
+        ns.clear();
+        if (dot1) {
+            const char* rest = dot1 + 1;
+            const char* dot2 = (const char*)memchr(rest, '.', (size_t)(d + len - rest));
+            ns.assign(rest, dot2 ? (size_t)(dot2 - rest) : (size_t)(d + len - rest));
+        }
+        auto it = R.ns_ids.find(ns);
+        uint32_t v = it == R.ns_ids.end() ? MXP_NS_NONE : it->second;
+        // tcp := attrs.Get("context.protocol") == "tcp": an interface compare, so only a string
+        bool tcp = false;
+        if (pc >= 0 && b->kinds[pc][q] == MXP_STRING) {
+            size_t pl;
+            const char* p = str(b->values[pc][q], &pl);
+            tcp = pl == 3 && memcmp(p, "tcp", 3) == 0;
+        }
+        (*info)[q] = v | (tcp ? 0x80000000u : 0u);
+    }
+    return MXP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxp_resolver_set(mxp_engine* eng, const char* identity_attr, const char* default_ns, const char* const* rule_ns,
+                     const uint32_t* variety_mask, const uint8_t* is_tcp, const uint8_t* empty_match, uint32_t n) {
+    if (!eng || !identity_attr || !default_ns || (n && (!rule_ns || !variety_mask || !is_tcp || !empty_match)))
+        return MXP_ERR_ARG;
+    if (!eng->have_rules) return eng->fail(MXP_ERR_STATE, "no rule set compiled");
+    if (n != eng->rules.size()) return eng->fail(MXP_ERR_ARG, "resolver: rule count differs from the rule set");
+    mxp_engine::ResolverConf R;
+    R.identity = identity_attr;
+    R.default_ns = default_ns;
+    R.vmask.assign(variety_mask, variety_mask + n);
+    R.tcp.assign(is_tcp, is_tcp + n);
+    R.empty.assign(empty_match, empty_match + n);
+    for (uint32_t i = 0; i < n; i++) {
+        const std::string ns = rule_ns[i] ? rule_ns[i] : "";
+        auto it = R.ns_ids.find(ns);
+        if (it == R.ns_ids.end()) {
+            const uint32_t id = (uint32_t)R.ns_names.size();
+            if (id >= MXP_NS_NONE) return eng->fail(MXP_ERR_ARG, "resolver: too many namespaces");
+            R.ns_ids.emplace(ns, id);
+            R.ns_names.push_back(ns);
+            R.ns_lo.push_back(i);
+            R.ns_hi.push_back(i + 1);
+        } else if (R.ns_hi[it->second] != i) {
+            return eng->fail(MXP_ERR_ARG, "resolver: rules of namespace '" + ns + "' are not contiguous");
+        } else {
+            R.ns_hi[it->second] = i + 1;
+        }
+    }
+    auto d = R.ns_ids.find(R.default_ns);
+    R.default_id = d == R.ns_ids.end() ? MXP_NS_NONE : d->second;
+    R.set = true;
+    eng->resolver = std::move(R);
+    return MXP_OK;
+}
+
+int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
+                      uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap) {
+    if (!eng || !batch || !status || !err_rule || !sel_off || (sel_cap && !sel_rules) || variety >= 32)
+        return MXP_ERR_ARG;
+    if (!eng->resolver.set) return eng->fail(MXP_ERR_STATE, "resolver not configured (mxp_resolver_set)");
+    const auto& R = eng->resolver;
+    const uint32_t n = batch->n_requests;
+    const uint32_t NR = (uint32_t)eng->rules.size();
+    const uint32_t W = (NR + 31) / 32;
+    std::unique_ptr<mxp_dbatch> db;
+    DevBuf dm, de;
+    int rc = eng->evaluate(batch, dm, de, nullptr, db);
+    if (rc) return rc;
+    // per-word masks: applicability for the variety (per request tcp flag), empty matches
+    std::vector<uint32_t> amask(2 * (size_t)W, 0), empty(W, 0);
+    for (uint32_t r = 0; r < NR; r++) {
+        const uint32_t bit = 1u << (r & 31);
+        if ((R.vmask[r] >> variety) & 1u) amask[(size_t)R.tcp[r] * W + r / 32] |= bit;
+        if (R.empty[r]) empty[r / 32] |= bit;
+    }
+    std::vector<uint32_t> info;
+    request_info(eng, batch, &info);
+    hipError_t e;
+    DevBuf d_info, d_lo, d_hi, d_amask, d_empty, d_status, d_err_rule, d_count, d_off, d_sel;
+    auto up = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
+        if ((e = d.alloc(bytes)) != hipSuccess) return eng->hipfail(e, what);
+        if (bytes && (e = hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, eng->stream)) != hipSuccess)
+            return eng->hipfail(e, what);
+        return MXP_OK;
+    };
+    if ((rc = up(d_info, info.data(), info.size() * 4, "upload nsinfo"))) return rc;
+    if ((rc = up(d_lo, R.ns_lo.data(), R.ns_lo.size() * 4, "upload ns_lo"))) return rc;
+    if ((rc = up(d_hi, R.ns_hi.data(), R.ns_hi.size() * 4, "upload ns_hi"))) return rc;
+    if ((rc = up(d_amask, amask.data(), amask.size() * 4, "upload amask"))) return rc;
+    if ((rc = up(d_empty, empty.data(), empty.size() * 4, "upload empty"))) return rc;
+    if ((e = d_status.alloc(n)) != hipSuccess) return eng->hipfail(e, "alloc status");
+    if ((e = d_err_rule.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err_rule");
+    if ((e = d_count.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc count");
+    mxp_resolve_args A;
+    memset(&A, 0, sizeof A);
+    A.n = n;
+    A.n_words = W;
+    A.nsinfo = d_info.as<uint32_t>();
+    A.ns_lo = d_lo.as<uint32_t>();
+    A.ns_hi = d_hi.as<uint32_t>();
+    A.default_id = R.default_id;
+    A.amask = d_amask.as<uint32_t>();
+    A.empty = d_empty.as<uint32_t>();
+    A.match = dm.as<uint32_t>();
+    A.err = de.as<uint32_t>();
+    A.status = d_status.as<uint8_t>();
+    A.err_rule = d_err_rule.as<uint32_t>();
+    A.count = d_count.as<uint32_t>();
+    if (n && (e = mxp_launch_resolve(&A, 0, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve");
+    std::vector<uint32_t> count(n);
+    if (n && (e = hipMemcpyAsync(count.data(), d_count.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download count");
+    if (n && (e = hipMemcpyAsync(status, d_status.p, n, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download status");
+    if (n && (e = hipMemcpyAsync(err_rule, d_err_rule.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download err_rule");
+    if ((rc = eng->collect_errors(batch, db))) return rc;  // synchronises the stream
+    sel_off[0] = 0;
+    for (uint32_t q = 0; q < n; q++) sel_off[q + 1] = sel_off[q] + count[q];
+    const uint64_t total = sel_off[n];
+    if (total > sel_cap) return MXP_ERR_NOMEM;
+    if (total) {
+        if ((rc = up(d_off, sel_off, ((size_t)n + 1) * 8, "upload sel_off"))) return rc;
+        if ((e = d_sel.alloc(total * 4)) != hipSuccess) return eng->hipfail(e, "alloc sel");
+        A.sel_off = d_off.as<uint64_t>();
+        A.sel_rules = d_sel.as<uint32_t>();
+        if ((e = mxp_launch_resolve(&A, 1, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
+        if ((e = hipMemcpyAsync(sel_rules, d_sel.p, total * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+            return eng->hipfail(e, "download sel");
+        if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "resolve sync");
+    }
+    return MXP_OK;
+}
+
+}  // extern "C"

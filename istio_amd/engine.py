@@ -52,6 +52,10 @@ SIGNATURES = {
     "mxp_hits_device": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP]),
     "mxp_rule_count": (ctypes.c_uint32, [_VP]),
     "mxp_dbatch_requests": (ctypes.c_uint32, [_VP]),
+    "mxp_resolver_set": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
+    "mxp_resolve_batch": (ctypes.c_int, [_VP, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "mxp_set_timing": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
@@ -207,6 +211,39 @@ class Engine:
         if rc not in (0, 1):
             self._check(rc, "mxp_pair_error")
         return buf.value.decode("utf-8", "surrogateescape")
+
+    # ------------------------------------------------------------------ batched resolver
+    RESOLVE_OK, RESOLVE_NO_IDENTITY, RESOLVE_BAD_IDENTITY, RESOLVE_PRED_ERROR = 0, 1, 2, 3
+
+    def set_resolver(self, identity_attr: str, default_ns: str, rule_ns, variety_mask, is_tcp, empty_match):
+        """runtime.resolver configuration (mxp_resolver_set): per rule its namespace (rules of a
+        namespace contiguous, in resolution order), variety bit mask, TCP flag, empty-match flag."""
+        n = len(rule_ns)
+        ns = (ctypes.c_char_p * max(n, 1))(*[x.encode() for x in rule_ns])
+        vm = np.ascontiguousarray(variety_mask, dtype=np.uint32)
+        tcp = np.ascontiguousarray(is_tcp, dtype=np.uint8)
+        em = np.ascontiguousarray(empty_match, dtype=np.uint8)
+        self._check(self.lib.mxp_resolver_set(self.h, identity_attr.encode(), default_ns.encode(), ns,
+                                              vm.ctypes.data, tcp.ctypes.data, em.ctypes.data, n), "mxp_resolver_set")
+
+    def resolve(self, batch: BagBatch, variety: int):
+        """Resolve every request (mxp_resolve_batch) -> (status u8[n], err_rule u32[n], selected:
+        list of per-request rule-id arrays in resolution order)."""
+        n = batch.n
+        status = np.zeros(n, dtype=np.uint8)
+        err_rule = np.zeros(n, dtype=np.uint32)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        cap = max(16, n * 4)
+        for _ in range(2):
+            sel = np.zeros(cap, dtype=np.uint32)
+            rc = self.lib.mxp_resolve_batch(self.h, ctypes.byref(batch.c_struct()), variety, status.ctypes.data,
+                                             err_rule.ctypes.data, off.ctypes.data, sel.ctypes.data, cap)
+            if rc == 4:  # MXP_ERR_NOMEM: retry with the exact size
+                cap = int(off[n])
+                continue
+            self._check(rc, "mxp_resolve_batch")
+            break
+        return status, err_rule, [sel[int(off[q]):int(off[q + 1])] for q in range(n)]
 
     def error_count(self) -> int:
         return int(self.lib.mxp_error_count(self.h))

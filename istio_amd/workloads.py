@@ -245,7 +245,7 @@ def fuzz_rules(n, seed=7, depth=3):
     return [f.expr(depth) for _ in range(n)]
 
 
-def guarded_fuzz_rules(n, seed=11, depth=2):
+def guarded_fuzz_rules(n, seed=11, depth=2, random_tail=True):
     """Rules whose programs start with a leading atom (guard) -- `attr == K`, `attr != K`,
     `map["k"] == K` -- joined by &&, || or alone to a continuation that is either random or one of a
     few constant-varying shapes (so continuation templates are shared).  Columns, want classes,
@@ -264,6 +264,8 @@ def guarded_fuzz_rules(n, seed=11, depth=2):
               lambda: 'br["%s"] == "%s"' % (f.pick(_KEYS), f.pick(_STR_VALS)),
               lambda: 'match(bs, "%s") || bi == %d' % (f.pick(["a*", "*c", "abc", "*"]), int(rng.integers(0, 5))),
               lambda: f.expr(depth)]
+    if not random_tail:
+        shapes = shapes[:3]
     out = []
     for _ in range(n):
         g = f.pick(guards)()
@@ -277,16 +279,16 @@ def guarded_fuzz_rules(n, seed=11, depth=2):
     return out
 
 
-def fuzz_bags(n, seed=8):
+def fuzz_bags(n, seed=8, p_missing=0.25, p_wrong=0.05):
     rng = np.random.default_rng(seed)
     f = _Fuzz(rng)
     bags = []
     for _ in range(n):
         b = {}
         for name, vt in DEFAULT_TEST_MANIFEST.items():
-            if rng.random() < 0.25:
+            if rng.random() < p_missing:
                 continue
-            wrong = rng.random() < 0.05
+            wrong = rng.random() < p_wrong
             if wrong:
                 b[name] = f.pick(["str", GoInt64(3), True, GoOther("20"), {"a": "b"}, GoFloat64(1.5), b"\x01"])
                 continue
@@ -313,3 +315,58 @@ def fuzz_bags(n, seed=8):
                 b[name] = m
         bags.append(b)
     return bags
+
+
+# ----------------------------------------------------------------------------------- resolver
+RESOLVER_NAMESPACES = ["istio-system", "default", "ns1", "ns2", "bookinfo"]
+
+
+def resolver_workload(n_rules=600, n_requests=2000, seed=21):
+    """Rules grouped by namespace (contiguous, resolution order) with random variety masks (4
+    varieties), TCP flags and some empty matches; requests whose `destination.service` names one of
+    the namespaces, an unknown one, none (no dot), is missing or is not a string, and whose
+    `context.protocol` is tcp / http / missing / not a string.
+    Returns (manifest, rules, conf, batch) with conf = dict(rule_ns, variety_mask, is_tcp,
+    empty_match, identity_attr, default_ns)."""
+    rng = np.random.default_rng(seed)
+    manifest = dict(DEFAULT_TEST_MANIFEST)
+    manifest["destination.service"] = "STRING"
+    manifest["context.protocol"] = "STRING"
+    body = guarded_fuzz_rules(n_rules, seed=seed + 1, random_tail=False)
+    counts = rng.multinomial(n_rules, [0.4, 0.2, 0.15, 0.15, 0.1])
+    rule_ns = [ns for ns, c in zip(RESOLVER_NAMESPACES, counts) for _ in range(c)]
+    empty = rng.random(n_rules) < 0.05
+    # "19ms" is a DURATION literal (expr.go:143-146): keep it out so most rules type-check, then make
+    # two rules of ns2 always-error (type error) so that namespace's requests fail
+    rules = ["" if e else r.replace('"19ms"', '"abc"') for e, r in zip(empty, body)]
+    ns2 = [i for i, ns in enumerate(rule_ns) if ns == "ns2" and not empty[i]]
+    for i in ns2[:2]:
+        rules[i] = 'as == "19ms"'
+    conf = dict(rule_ns=rule_ns,
+                variety_mask=[int(x) for x in rng.integers(0, 16, size=n_rules)],
+                is_tcp=[int(x) for x in (rng.random(n_rules) < 0.2)],
+                empty_match=[int(x) for x in empty],
+                identity_attr="destination.service", default_ns="istio-system")
+    bags = fuzz_bags(n_requests, seed=seed + 2, p_missing=0.0005, p_wrong=0.0002)
+    f = _Fuzz(rng)
+    for b in bags:
+        r = rng.random()
+        if r < 0.05:
+            b.pop("destination.service", None)
+        elif r < 0.08:
+            b["destination.service"] = GoInt64(7)
+        elif r < 0.12:
+            b["destination.service"] = "nodots"
+        elif r < 0.2:
+            b["destination.service"] = "svc.unknown.svc.cluster.local"
+        else:
+            b["destination.service"] = "svc%d.%s.svc.cluster.local" % (rng.integers(0, 9), f.pick(RESOLVER_NAMESPACES))
+        r = rng.random()
+        if r < 0.25:
+            b["context.protocol"] = "tcp"
+        elif r < 0.8:
+            b["context.protocol"] = "http"
+        elif r < 0.85:
+            b["context.protocol"] = GoInt64(1)
+    names = list(manifest)
+    return manifest, rules, conf, BagBatch.from_bags(bags, names=names)

@@ -1,0 +1,76 @@
+"""GPU batched resolver (mxp_resolve_batch) against the resolver restatement (oracle/resolver.py):
+the reference's own resolver table, then randomized namespaces / varieties / TCP flags / empty
+matches / identity failures over guard-heavy rules.  Bar: identical status, first-error rule (and
+its error text) and selected-rule lists, per request."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import resolver as oracle_resolver
+from istio_amd import workloads as W
+from istio_amd.bags import BagBatch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+CASES = json.load(open(os.path.join(HERE, "golden", "resolver_cases.json")))
+MANIFEST = {"destination.service": "STRING", "context.protocol": "STRING", "as": "STRING"}
+
+
+@pytest.fixture(scope="module")
+def mxp(libmxp):
+    import istio_amd.engine as mxp
+    return mxp
+
+
+@pytest.mark.parametrize("case", CASES["cases"], ids=[c["desc"] for c in CASES["cases"]])
+def test_reference_resolver_table_on_gpu(mxp, case):
+    from test_resolver_oracle import case_inputs
+    rule_ns, lengths, _ = case_inputs(case)
+    match = 'as == "x"' if case.get("selectError") else ("false" if case.get("selectReject") else "true")
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(MANIFEST)
+    assert (eng.compile([match] * len(rule_ns)) == 0).all()
+    n = len(rule_ns)
+    eng.set_resolver(CASES["identity_attr"], CASES["default_ns"], rule_ns, [1] * n, [0] * n, [0] * n)
+    batch = BagBatch.from_bags([dict(case["bag"])], names=list(MANIFEST))
+    status, err_rule, sel = eng.resolve(batch, case.get("callVariety", 0))
+    if "err" in case:
+        if "identity" in case["err"]:
+            assert status[0] == eng.RESOLVE_NO_IDENTITY
+        else:
+            assert status[0] == eng.RESOLVE_PRED_ERROR
+            assert eng.pair_error(0, int(err_rule[0])) == "lookup failed: 'as'"
+        return
+    assert status[0] == eng.RESOLVE_OK
+    assert sum(lengths[int(r)] for r in sel[0]) == case["nactions"]
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_resolver_random_parity(mxp, seed):
+    manifest, rules, conf, batch = W.resolver_workload(n_rules=600, n_requests=3000, seed=seed)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    st = eng.compile(rules)
+    eng.set_resolver(conf["identity_attr"], conf["default_ns"], conf["rule_ns"], conf["variety_mask"],
+                     conf["is_tcp"], conf["empty_match"])
+    ev = oracle.OracleEvaluator(manifest)
+    codes = oracle.oracle_matrix(ev, rules, batch, threads=16)
+    seen = set()
+    for variety in (0, 2, 3):
+        status, err_rule, sel = eng.resolve(batch, variety)
+        want = oracle_resolver.resolve(batch, codes, conf["rule_ns"], conf["variety_mask"], conf["is_tcp"],
+                                       conf["empty_match"], conf["identity_attr"], conf["default_ns"], variety)
+        for q, (ws, we, wsel) in enumerate(want):
+            assert status[q] == ws, (q, variety, status[q], ws)
+            seen.add(ws)
+            if ws == oracle_resolver.PRED_ERROR:
+                assert err_rule[q] == we, (q, variety)
+                st_, msg = ev.eval_predicate(rules[we], batch, q)
+                gmsg = eng.pair_error(q, int(we))
+                assert gmsg == msg or (st_ == "panic" and gmsg in mxp.PANIC_TEXTS), (rules[we], gmsg, msg)
+            else:
+                assert list(sel[q]) == wsel, (q, variety)
+    assert seen == {0, 1, 2, 3}
