@@ -123,6 +123,47 @@ int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t vari
                       uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap);
 
 /*
+ * List adapter (mixer/adapter/list): membership checks of a batch of symbols against one list.
+ *
+ * mxp_list_create compiles a list the way the handler's parse*List functions build it
+ * (list.go:182-204): entry_type is config.Params.ListEntryType (STRINGS 0,
+ * CASE_INSENSITIVE_STRINGS 1, IP_ADDRESSES 2, REGEX 3).  `entries` are the provider payload's entries
+ * -- the '\n'-split lines for STRINGS / CASE_INSENSITIVE / REGEX (stringList.go:29, regexList.go:44;
+ * empty lines are skipped here), the YAML whitelist for IP_ADDRESSES (ipList.go:35) -- and
+ * `overrides` are config.Params.Overrides.  Strings are (pointer, length) pairs.  An IP entry that
+ * does not parse fails the whole list with MXP_ERR_ARG and mxp_last_error = the reference's text
+ * ("could not parse list entry %s: invalid CIDR address: %s", ipList.go:62-75); override entries
+ * that do not parse are ignored (ipList.go:47-51).
+ *
+ * mxp_list_check runs HandleListEntry (list.go:68-101) for n symbols (string blob + offsets,
+ * mxp_bag_batch style) and writes the google.rpc code of each: OK 0, INVALID_ARGUMENT 3 (symbol is
+ * not an IP address, IP lists), NOT_FOUND 5 (whitelist miss), PERMISSION_DENIED 7 (blacklist hit).
+ * The status message follows from the code and the symbol ("%s is not whitelisted", "%s is
+ * blacklisted", "%s is not a valid IP address").
+ */
+#define MXP_LIST_STRINGS 0
+#define MXP_LIST_CASE_INSENSITIVE_STRINGS 1
+#define MXP_LIST_IP_ADDRESSES 2
+#define MXP_LIST_REGEX 3
+#define MXP_RPC_OK 0
+#define MXP_RPC_INVALID_ARGUMENT 3
+#define MXP_RPC_NOT_FOUND 5
+#define MXP_RPC_PERMISSION_DENIED 7
+typedef struct mxp_list mxp_list;
+int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries, const uint32_t* entry_lens,
+                    uint32_t n_entries, const char* const* overrides, const uint32_t* override_lens,
+                    uint32_t n_overrides, mxp_list** out);
+void mxp_list_destroy(mxp_engine* eng, mxp_list* list);
+/* list.numEntries(): distinct strings for string lists, entries (duplicates included) otherwise */
+uint64_t mxp_list_entries(const mxp_list* list);
+int mxp_list_check(mxp_engine* eng, const mxp_list* list, int blacklist, const uint8_t* sym_bytes,
+                   const uint64_t* sym_offsets, uint32_t n, int32_t* codes);
+/* Device-resident variant: symbols already in device memory (blob with >= 16 bytes of readable
+ * slack after the last symbol), codes written to device memory, enqueued on `stream`. */
+int mxp_list_check_device(mxp_engine* eng, const mxp_list* list, int blacklist, const uint8_t* d_sym_bytes,
+                          const uint64_t* d_sym_offsets, uint32_t n, void* stream, int32_t* d_codes);
+
+/*
  * Device-resident batches (benchmarking and pipelining): pack + upload once, evaluate many times.
  * mxp_batch_eval_device enqueues on `stream` (a hipStream_t; NULL = engine stream) and writes the
  * bitmaps to DEVICE pointers (rule-word-major, as above).  Nothing is synchronised.

@@ -1,5 +1,6 @@
 // goutil.cpp -- see goutil.h.  Algorithms follow the Go 1.9 standard library sources named there.
 #include "goutil.h"
+#include "netparse.h"
 
 #include <cerrno>
 #include <cmath>
@@ -257,120 +258,8 @@ bool go_parse_duration(const std::string& orig, int64_t* out, std::string* err) 
 }
 
 // ------------------------------------------------------------------------------- net.ParseIP
-namespace {
-constexpr int kBig = 0xFFFFFF;
-
-bool dec_to_int(const uint8_t* s, size_t n, int* v, size_t* used) {
-    int x = 0;
-    size_t i = 0;
-    for (; i < n && s[i] >= '0' && s[i] <= '9'; i++) {
-        x = x * 10 + (s[i] - '0');
-        if (x >= kBig) return false;
-    }
-    if (i == 0) return false;
-    *v = x;
-    *used = i;
-    return true;
-}
-
-bool hex_to_int(const uint8_t* s, size_t n, int* v, size_t* used) {
-    int x = 0;
-    size_t i = 0;
-    for (; i < n; i++) {
-        int h = hexval((char)s[i]);
-        if (h < 0) break;
-        x = x * 16 + h;
-        if (x >= kBig) return false;
-    }
-    if (i == 0) return false;
-    *v = x;
-    *used = i;
-    return true;
-}
-
-bool v4(const uint8_t* s, size_t n, uint8_t out[16]) {
-    uint8_t q[4];
-    for (int i = 0; i < 4; i++) {
-        if (n == 0) return false;
-        if (i) {
-            if (*s != '.') return false;
-            s++;
-            n--;
-        }
-        int v;
-        size_t c;
-        if (!dec_to_int(s, n, &v, &c) || v > 255) return false;
-        q[i] = (uint8_t)v;
-        s += c;
-        n -= c;
-    }
-    if (n) return false;
-    static const uint8_t pre[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xff, 0xff};
-    memcpy(out, pre, 12);
-    memcpy(out + 12, q, 4);
-    return true;
-}
-
-bool v6(const uint8_t* s, size_t n, uint8_t ip[16]) {
-    memset(ip, 0, 16);
-    int ell = -1;
-    if (n >= 2 && s[0] == ':' && s[1] == ':') {
-        ell = 0;
-        s += 2;
-        n -= 2;
-        if (!n) return true;
-    }
-    int i = 0;
-    while (i < 16) {
-        int v;
-        size_t c;
-        if (!hex_to_int(s, n, &v, &c) || v > 0xFFFF) return false;
-        if (c < n && s[c] == '.') {
-            if (ell < 0 && i != 12) return false;
-            if (i + 4 > 16) return false;
-            uint8_t t[16];
-            if (!v4(s, n, t)) return false;
-            memcpy(ip + i, t + 12, 4);
-            n = 0;
-            i += 4;
-            break;
-        }
-        ip[i] = (uint8_t)(v >> 8);
-        ip[i + 1] = (uint8_t)v;
-        i += 2;
-        s += c;
-        n -= c;
-        if (!n) break;
-        if (*s != ':' || n == 1) return false;
-        s++;
-        n--;
-        if (*s == ':') {
-            if (ell >= 0) return false;
-            ell = i;
-            s++;
-            n--;
-            if (!n) break;
-        }
-    }
-    if (n) return false;
-    if (i < 16) {
-        if (ell < 0) return false;
-        int k = 16 - i;
-        for (int j = i - 1; j >= ell; j--) ip[j + k] = ip[j];
-        for (int j = ell + k - 1; j >= ell; j--) ip[j] = 0;
-    } else if (ell >= 0) {
-        return false;
-    }
-    return true;
-}
-}  // namespace
-
 bool go_parse_ip(const uint8_t* s, size_t n, uint8_t out[16]) {
-    for (size_t i = 0; i < n; i++) {
-        if (s[i] == '.') return v4(s, n, out);
-        if (s[i] == ':') return v6(s, n, out);
-    }
-    return false;
+    return n < (1u << 31) && mxpnet::parse_ip(s, (uint32_t)n, out);
 }
 
 std::string ip_canonical(const uint8_t* b, size_t n) {

@@ -1,0 +1,308 @@
+// lists.cpp -- list adapter (mixer/adapter/list) compile + batched checks (include/mxp.h).
+//
+// Compilation follows the handler's list builders:
+//   STRINGS / CASE_INSENSITIVE_STRINGS  parseStringList / parseCaseInsensitiveStringList
+//                                       (stringList.go:29-67): a set of the non-empty entries and
+//                                       overrides (upper-cased for the case-insensitive kind);
+//   IP_ADDRESSES                        parseIPList / addEntry (ipList.go:35-75): "/32" appended when
+//                                       the entry has no '/', net.ParseCIDR; the IPNets become
+//                                       disjoint sorted address intervals (IPNet.Contains per
+//                                       family after To4), so a check is a binary search instead of
+//                                       the reference's linear scan (ipList.go:77-92).
+// Checks run HandleListEntry (list.go:68-101) on the GPU (lists.hip).
+#include <algorithm>
+#include <cstring>
+#include <limits>
+
+#include "engine_impl.h"
+#include "lists.h"
+
+extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s);
+
+struct mxp_list {
+    int type = 0;
+    uint64_t n_entries = 0;
+    uint32_t hmask = 0;
+    DevBuf htab, ent_desc, ent_pool, v4lo, v4hi, v6lo, v6hi;
+    uint32_t n4 = 0, n6 = 0;
+};
+
+namespace {
+
+std::string ascii_upper(const std::string& s) {
+    std::string o = s;
+    for (auto& c : o)
+        if (c >= 'a' && c <= 'z') c = (char)(c - 32);
+    return o;
+}
+
+uint64_t host_hash(const std::string& s, bool upper) {
+    uint64_t h = 0;
+    for (size_t i = 0; i < s.size(); i += 8) {
+        uint64_t w = 0;
+        memcpy(&w, s.data() + i, std::min<size_t>(8, s.size() - i));
+        h = mxp_hash_step(h, upper ? mxp_upper8(w) : w);
+    }
+    return mxp_hash_final(h, s.size());
+}
+
+// net.ParseCIDR (Go 1.9 src/net/ip.go) -> IPNet{IP: ip.Mask(m), Mask: m}; false on ParseError
+struct Net {
+    uint8_t ip[16];
+    int iplen;
+    uint8_t mask[16];
+    int masklen;
+};
+
+bool parse_cidr(const std::string& s, Net* out) {
+    const size_t slash = s.find('/');
+    if (slash == std::string::npos) return false;
+    const uint8_t* a = (const uint8_t*)s.data();
+    uint8_t ip[16];
+    int iplen = 4;
+    if (!mxpnet::parse_v4(a, (uint32_t)slash, ip)) {
+        iplen = 16;
+        if (!mxpnet::parse_v6(a, (uint32_t)slash, ip)) return false;
+    }
+    int n;
+    uint32_t used;
+    const uint8_t* m = a + slash + 1;
+    const uint32_t ml = (uint32_t)(s.size() - slash - 1);
+    if (!mxpnet::dtoi(m, ml, &n, &used) || used != ml || n < 0 || n > 8 * iplen) return false;
+    // CIDRMask(n, 8 * iplen)
+    uint8_t mask[16] = {0};
+    for (int i = 0; i < iplen; i++) {
+        const int bits = std::min(8, std::max(0, n - 8 * i));
+        mask[i] = (uint8_t)(0xFF00u >> bits);
+    }
+    // ip.Mask(m): a 4-byte mask on a v4-in-v6 address masks its last 4 bytes
+    Net r{};
+    r.masklen = iplen;
+    memcpy(r.mask, mask, iplen);
+    const uint8_t* src = ip;
+    int srclen = 16;
+    if (iplen == 4 && mxpnet::is_v4(ip)) {
+        src = ip + 12;
+        srclen = 4;
+    }
+    if (srclen != iplen) return false;  // not reachable from ParseCIDR
+    r.iplen = iplen;
+    for (int i = 0; i < iplen; i++) r.ip[i] = src[i] & mask[i];
+    *out = r;
+    return true;
+}
+
+// networkNumberAndMask (ip.go): the family a net matches after IP.To4, or false (never matches)
+bool net_number_and_mask(const Net& n, uint8_t nn[16], int* nnlen, uint8_t m[16]) {
+    uint8_t ip16[16];
+    const uint8_t* ip = n.ip;
+    int iplen = n.iplen;
+    if (iplen == 16 && mxpnet::is_v4(n.ip)) {  // To4 of a v4-in-v6 network number
+        memcpy(ip16, n.ip + 12, 4);
+        ip = ip16;
+        iplen = 4;
+    }
+    const uint8_t* mk = n.mask;
+    int mlen = n.masklen;
+    if (mlen == 4) {
+        if (iplen != 4) return false;
+    } else if (mlen == 16) {
+        if (iplen == 4) {
+            mk = n.mask + 12;
+            mlen = 4;
+        }
+    } else {
+        return false;
+    }
+    memcpy(nn, ip, iplen);
+    memcpy(m, mk, mlen);
+    *nnlen = iplen;
+    return true;
+}
+
+template <class T>
+void merge(std::vector<std::pair<T, T>>& v) {
+    std::sort(v.begin(), v.end());
+    std::vector<std::pair<T, T>> o;
+    for (auto& p : v) {
+        if (!o.empty() && (p.first <= o.back().second || (o.back().second != std::numeric_limits<T>::max() &&
+                                                          p.first == o.back().second + 1)))
+            o.back().second = std::max(o.back().second, p.second);
+        else
+            o.push_back(p);
+    }
+    v.swap(o);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries, const uint32_t* entry_lens,
+                    uint32_t n_entries, const char* const* overrides, const uint32_t* override_lens,
+                    uint32_t n_overrides, mxp_list** out) {
+    if (!eng || !out || (n_entries && (!entries || !entry_lens)) || (n_overrides && (!overrides || !override_lens)))
+        return MXP_ERR_ARG;
+    if (eng->device < 0) return eng->fail(MXP_ERR_STATE, "host-only engine");
+    std::unique_ptr<mxp_list> L(new mxp_list());
+    L->type = entry_type;
+    hipError_t e;
+    if ((e = hipSetDevice(eng->device)) != hipSuccess) return eng->hipfail(e, "hipSetDevice");
+    auto put = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
+        if ((e = d.alloc(bytes ? bytes : 16)) != hipSuccess) return eng->hipfail(e, what);
+        if (bytes && (e = hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice)) != hipSuccess) return eng->hipfail(e, what);
+        return MXP_OK;
+    };
+    int rc;
+    auto str = [](const char* p, uint32_t n) { return std::string(p, n); };
+    if (entry_type == MXP_LIST_STRINGS || entry_type == MXP_LIST_CASE_INSENSITIVE_STRINGS) {
+        const bool upper = entry_type == MXP_LIST_CASE_INSENSITIVE_STRINGS;
+        std::unordered_map<std::string, uint32_t> ids;
+        std::vector<std::string> uniq;
+        auto add = [&](const std::string& s) {
+            if (s.empty()) return;  // empty lines / overrides are skipped
+            std::string k = upper ? ascii_upper(s) : s;
+            if (ids.emplace(k, (uint32_t)uniq.size()).second) uniq.push_back(k);
+        };
+        for (uint32_t i = 0; i < n_entries; i++) add(str(entries[i], entry_lens[i]));
+        for (uint32_t i = 0; i < n_overrides; i++) add(str(overrides[i], override_lens[i]));
+        uint32_t cap = 2;
+        while (cap < 2 * uniq.size()) cap <<= 1;
+        std::vector<uint64_t> tab(cap, MXP_LIST_EMPTY);
+        for (uint32_t i = 0; i < uniq.size(); i++) {
+            const uint64_t h = host_hash(uniq[i], false);  // entries are already upper-cased
+            uint32_t s = (uint32_t)h & (cap - 1);
+            while (tab[s] != MXP_LIST_EMPTY) s = (s + 1) & (cap - 1);
+            tab[s] = (h >> 32) << 32 | i;
+        }
+        std::vector<uint64_t> desc;
+        std::string pool;
+        if (!string_pool(uniq, &desc, &pool)) return eng->fail(MXP_ERR_ARG, "list entry longer than 16 MiB");
+        L->n_entries = uniq.size();
+        L->hmask = cap - 1;
+        if ((rc = put(L->htab, tab.data(), tab.size() * 8, "upload list table"))) return rc;
+        if ((rc = put(L->ent_desc, desc.data(), desc.size() * 8, "upload list desc"))) return rc;
+        if ((rc = put(L->ent_pool, pool.data(), pool.size(), "upload list pool"))) return rc;
+    } else if (entry_type == MXP_LIST_IP_ADDRESSES) {
+        std::vector<std::pair<uint32_t, uint32_t>> r4;
+        std::vector<std::pair<unsigned __int128, unsigned __int128>> r6;
+        auto add = [&](const std::string& orig, bool strict) -> int {
+            std::string ip = orig;
+            if (ip.find('/') == std::string::npos) ip += "/32";
+            Net n;
+            if (!parse_cidr(ip, &n)) {
+                if (!strict) return MXP_OK;  // overrides: errors ignored (config was validated)
+                return eng->fail(MXP_ERR_ARG, "could not parse list entry " + orig + ": invalid CIDR address: " + ip);
+            }
+            L->n_entries++;
+            uint8_t nn[16], m[16];
+            int len;
+            if (!net_number_and_mask(n, nn, &len, m)) return MXP_OK;  // an IPNet that contains nothing
+            if (len == 4) {
+                uint32_t lo = 0, mm = 0;
+                for (int i = 0; i < 4; i++) {
+                    lo = lo << 8 | (uint32_t)(nn[i] & m[i]);
+                    mm = mm << 8 | m[i];
+                }
+                r4.emplace_back(lo, lo | ~mm);
+            } else {
+                unsigned __int128 lo = 0, mm = 0;
+                for (int i = 0; i < 16; i++) {
+                    lo = lo << 8 | (unsigned __int128)(nn[i] & m[i]);
+                    mm = mm << 8 | m[i];
+                }
+                r6.emplace_back(lo, lo | ~mm);
+            }
+            return MXP_OK;
+        };
+        for (uint32_t i = 0; i < n_entries; i++)
+            if ((rc = add(str(entries[i], entry_lens[i]), true))) return rc;
+        for (uint32_t i = 0; i < n_overrides; i++) add(str(overrides[i], override_lens[i]), false);
+        merge(r4);
+        merge(r6);
+        std::vector<uint32_t> lo4, hi4;
+        std::vector<uint64_t> lo6, hi6;
+        for (auto& p : r4) {
+            lo4.push_back(p.first);
+            hi4.push_back(p.second);
+        }
+        for (auto& p : r6) {
+            lo6.push_back((uint64_t)(p.first >> 64));
+            lo6.push_back((uint64_t)p.first);
+            hi6.push_back((uint64_t)(p.second >> 64));
+            hi6.push_back((uint64_t)p.second);
+        }
+        L->n4 = (uint32_t)r4.size();
+        L->n6 = (uint32_t)r6.size();
+        if ((rc = put(L->v4lo, lo4.data(), lo4.size() * 4, "upload v4lo"))) return rc;
+        if ((rc = put(L->v4hi, hi4.data(), hi4.size() * 4, "upload v4hi"))) return rc;
+        if ((rc = put(L->v6lo, lo6.data(), lo6.size() * 8, "upload v6lo"))) return rc;
+        if ((rc = put(L->v6hi, hi6.data(), hi6.size() * 8, "upload v6hi"))) return rc;
+    } else if (entry_type == MXP_LIST_REGEX) {
+        return eng->fail(MXP_ERR_STATE, "REGEX lists: not supported by this engine build yet");
+    } else {
+        return eng->fail(MXP_ERR_ARG, "unknown list entry type");
+    }
+    *out = L.release();
+    return MXP_OK;
+}
+
+void mxp_list_destroy(mxp_engine* eng, mxp_list* list) {
+    if (eng && eng->device >= 0) (void)hipSetDevice(eng->device);
+    delete list;
+}
+
+uint64_t mxp_list_entries(const mxp_list* list) { return list ? list->n_entries : 0; }
+
+int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, const uint8_t* d_sym_bytes,
+                          const uint64_t* d_sym_offsets, uint32_t n, void* stream, int32_t* d_codes) {
+    if (!eng || !L || (n && (!d_sym_bytes || !d_sym_offsets || !d_codes))) return MXP_ERR_ARG;
+    if (!n) return MXP_OK;
+    mxp_list_args A;
+    memset(&A, 0, sizeof A);
+    A.type = (uint32_t)L->type;
+    A.blacklist = blacklist ? 1u : 0u;
+    A.n = n;
+    A.hmask = L->hmask;
+    A.sym = d_sym_bytes;
+    A.sym_off = d_sym_offsets;
+    A.htab = L->htab.as<uint64_t>();
+    A.ent_desc = L->ent_desc.as<uint64_t>();
+    A.ent_pool = L->ent_pool.as<uint8_t>();
+    A.v4lo = L->v4lo.as<uint32_t>();
+    A.v4hi = L->v4hi.as<uint32_t>();
+    A.v6lo = L->v6lo.as<uint64_t>();
+    A.v6hi = L->v6hi.as<uint64_t>();
+    A.n4 = L->n4;
+    A.n6 = L->n6;
+    A.codes = d_codes;
+    hipError_t e = mxp_launch_list(&A, stream ? (hipStream_t)stream : eng->stream);
+    return e == hipSuccess ? MXP_OK : eng->hipfail(e, "launch list check");
+}
+
+int mxp_list_check(mxp_engine* eng, const mxp_list* L, int blacklist, const uint8_t* sym_bytes,
+                   const uint64_t* sym_offsets, uint32_t n, int32_t* codes) {
+    if (!eng || !L || (n && (!sym_bytes || !sym_offsets || !codes))) return MXP_ERR_ARG;
+    if (!n) return MXP_OK;
+    hipError_t e;
+    if ((e = hipSetDevice(eng->device)) != hipSuccess) return eng->hipfail(e, "hipSetDevice");
+    const uint64_t bytes = sym_offsets[n];
+    DevBuf d_sym, d_off, d_codes;
+    if ((e = d_sym.alloc(bytes + 16)) != hipSuccess) return eng->hipfail(e, "alloc symbols");
+    if ((e = d_off.alloc(((size_t)n + 1) * 8)) != hipSuccess) return eng->hipfail(e, "alloc offsets");
+    if ((e = d_codes.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc codes");
+    if ((e = hipMemsetAsync(d_sym.p, 0, bytes + 16, eng->stream)) != hipSuccess) return eng->hipfail(e, "memset");
+    if (bytes && (e = hipMemcpyAsync(d_sym.p, sym_bytes, bytes, hipMemcpyHostToDevice, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "upload symbols");
+    if ((e = hipMemcpyAsync(d_off.p, sym_offsets, ((size_t)n + 1) * 8, hipMemcpyHostToDevice, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "upload offsets");
+    int rc = mxp_list_check_device(eng, L, blacklist, d_sym.as<uint8_t>(), d_off.as<uint64_t>(), n, eng->stream,
+                                   d_codes.as<int32_t>());
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(codes, d_codes.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download codes");
+    if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "list sync");
+    return MXP_OK;
+}
+
+}  // extern "C"

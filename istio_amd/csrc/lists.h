@@ -1,0 +1,49 @@
+// lists.h -- list-adapter tables and kernel arguments shared by lists.cpp (host compile) and
+// lists.hip (gfx950 check kernel).  Reference: mixer/adapter/list/{list,stringList,ipList}.go.
+#pragma once
+
+#include <stdint.h>
+
+#include "netparse.h"
+
+// string hash table slot: hash32 << 32 | entry index; empty slot = ~0
+#define MXP_LIST_EMPTY 0xFFFFFFFFFFFFFFFFull
+
+typedef struct mxp_list_args {
+    uint32_t type;              // MXP_LIST_*
+    uint32_t blacklist;
+    uint32_t n;                 // symbols
+    uint32_t hmask;             // string table size - 1
+    const uint8_t* sym;         // symbol blob (>= 16 bytes of slack)
+    const uint64_t* sym_off;    // [n + 1]
+    const uint64_t* htab;       // string lists: open-addressing slots
+    const uint64_t* ent_desc;   // entry offset << 24 | length (8-aligned pool)
+    const uint8_t* ent_pool;
+    const uint32_t* v4lo;       // IP lists: disjoint sorted IPv4 intervals
+    const uint32_t* v4hi;
+    const uint64_t* v6lo;       // disjoint sorted IPv6 intervals, [2 i] high / [2 i + 1] low 64 bits
+    const uint64_t* v6hi;
+    uint32_t n4, n6;
+    int32_t* codes;             // [n] google.rpc codes
+} mxp_list_args;
+
+// ASCII upper-casing of 8 packed bytes (bytes >= 0x80 untouched): strings.ToUpper's ASCII path
+MXP_NHD uint64_t mxp_upper8(uint64_t x) {
+    const uint64_t h = x & 0x7F7F7F7F7F7F7F7Full;
+    const uint64_t ge_a = h + 0x1F1F1F1F1F1F1F1Full;  // high bit set where byte >= 'a'
+    const uint64_t gt_z = h + 0x0505050505050505ull;  // high bit set where byte > 'z'
+    const uint64_t lower = ge_a & ~gt_z & ~x & 0x8080808080808080ull;
+    return x ^ (lower >> 2);
+}
+
+// word-at-a-time string hash; `w` is the next 8 bytes (little-endian, zero beyond the end)
+MXP_NHD uint64_t mxp_hash_step(uint64_t h, uint64_t w) {
+    h ^= w;
+    h *= 0x9E3779B97F4A7C15ull;
+    return h ^ (h >> 31);
+}
+MXP_NHD uint64_t mxp_hash_final(uint64_t h, uint64_t len) {
+    h ^= len * 0xC2B2AE3D27D4EB4Full;
+    h *= 0xFF51AFD7ED558CCDull;
+    return h ^ (h >> 33);
+}

@@ -1,0 +1,125 @@
+// lists.hip -- gfx950 list-adapter check kernel (lists.cpp builds the tables).
+//
+// One symbol per lane.  HandleListEntry (mixer/adapter/list/list.go:68-101) on each:
+//   string lists   hash the symbol 8 bytes at a time (ASCII upper-cased on the fly for the
+//                  case-insensitive kind, strings.ToUpper's ASCII path), probe the open-addressing
+//                  table, compare bytes on a hash hit (stringList.go:73-80);
+//   IP lists       net.ParseIP on the symbol (netparse.h, the same code the host uses), then a
+//                  binary search of the disjoint interval set of the address family
+//                  (ipList.go:77-92; "is not a valid IP address" -> INVALID_ARGUMENT);
+// then the whitelist / blacklist decision.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mxp.h"
+#include "lists.h"
+
+namespace {
+
+// 8 bytes at any address of a blob with >= 16 bytes of slack (two aligned loads + funnel shift)
+__device__ __forceinline__ uint64_t ld8u(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7) * 8u;
+    const uint64_t lo = q[0];
+    return sh == 0 ? lo : (lo >> sh) | (q[1] << (64u - sh));
+}
+
+__device__ __forceinline__ uint64_t tail_mask(uint32_t rem) {
+    return rem >= 8 ? ~0ull : ((1ull << (rem * 8u)) - 1ull);
+}
+
+__device__ bool string_member(const mxp_list_args& A, const uint8_t* s, uint32_t n, bool upper) {
+    uint64_t h = 0;
+    for (uint32_t i = 0; i < n; i += 8) {
+        uint64_t w = ld8u(s + i) & tail_mask(n - i);
+        h = mxp_hash_step(h, upper ? mxp_upper8(w) : w);
+    }
+    h = mxp_hash_final(h, n);
+    const uint32_t tag = (uint32_t)(h >> 32);
+    for (uint32_t slot = (uint32_t)h & A.hmask;; slot = (slot + 1) & A.hmask) {
+        const uint64_t t = A.htab[slot];
+        if (t == MXP_LIST_EMPTY) return false;
+        if ((uint32_t)(t >> 32) != tag) continue;
+        const uint64_t d = A.ent_desc[(uint32_t)t];
+        if ((uint32_t)(d & 0xFFFFFFu) != n) continue;
+        const uint8_t* e = A.ent_pool + (d >> 24);
+        bool eq = true;
+        for (uint32_t i = 0; i < n && eq; i += 8) {
+            const uint64_t m = tail_mask(n - i);
+            uint64_t w = ld8u(s + i) & m;
+            if (upper) w = mxp_upper8(w);
+            eq = w == (ld8u(e + i) & m);
+        }
+        if (eq) return true;
+    }
+}
+
+// index of the last interval starting at or below x (or -1)
+__device__ __forceinline__ int find4(const uint32_t* lo, uint32_t n, uint32_t x) {
+    int a = 0, b = (int)n - 1, r = -1;
+    while (a <= b) {
+        const int m = (a + b) >> 1;
+        if (lo[m] <= x) {
+            r = m;
+            a = m + 1;
+        } else {
+            b = m - 1;
+        }
+    }
+    return r;
+}
+
+__device__ __forceinline__ bool le128(uint64_t ah, uint64_t al, uint64_t bh, uint64_t bl) {
+    return ah < bh || (ah == bh && al <= bl);
+}
+
+__device__ bool ip_member(const mxp_list_args& A, const uint8_t ip[16]) {
+    if (mxpnet::is_v4(ip)) {
+        const uint32_t x = (uint32_t)ip[12] << 24 | (uint32_t)ip[13] << 16 | (uint32_t)ip[14] << 8 | ip[15];
+        const int k = find4(A.v4lo, A.n4, x);
+        return k >= 0 && x <= A.v4hi[k];
+    }
+    uint64_t xh = 0, xl = 0;
+    for (int i = 0; i < 8; i++) xh = xh << 8 | ip[i];
+    for (int i = 8; i < 16; i++) xl = xl << 8 | ip[i];
+    int a = 0, b = (int)A.n6 - 1, r = -1;
+    while (a <= b) {
+        const int m = (a + b) >> 1;
+        if (le128(A.v6lo[2 * m], A.v6lo[2 * m + 1], xh, xl)) {
+            r = m;
+            a = m + 1;
+        } else {
+            b = m - 1;
+        }
+    }
+    return r >= 0 && le128(xh, xl, A.v6hi[2 * r], A.v6hi[2 * r + 1]);
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args A) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (q >= A.n) return;
+    const uint64_t o0 = A.sym_off[q], o1 = A.sym_off[q + 1];
+    const uint8_t* s = A.sym + o0;
+    const uint32_t n = (uint32_t)(o1 - o0);
+    bool found;
+    if (A.type == MXP_LIST_IP_ADDRESSES) {
+        uint8_t ip[16];
+        if (!mxpnet::parse_ip(s, n, ip)) {
+            A.codes[q] = MXP_RPC_INVALID_ARGUMENT;
+            return;
+        }
+        found = ip_member(A, ip);
+    } else {
+        found = string_member(A, s, n, A.type == MXP_LIST_CASE_INSENSITIVE_STRINGS);
+    }
+    A.codes[q] = A.blacklist ? (found ? MXP_RPC_PERMISSION_DENIED : MXP_RPC_OK)
+                             : (found ? MXP_RPC_OK : MXP_RPC_NOT_FOUND);
+}
+
+extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_list_kernel, dim3((a->n + 255u) / 256u), dim3(256), 0, s, *a);
+    return hipGetLastError();
+}

@@ -56,6 +56,14 @@ SIGNATURES = {
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     "mxp_resolve_batch": (ctypes.c_int, [_VP, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
+    "mxp_list_create": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(_VP)]),
+    "mxp_list_destroy": (None, [_VP, _VP]),
+    "mxp_list_entries": (ctypes.c_uint64, [_VP]),
+    "mxp_list_check": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+                                      ctypes.c_void_p]),
+    "mxp_list_check_device": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "mxp_set_timing": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
@@ -245,6 +253,22 @@ class Engine:
             break
         return status, err_rule, [sel[int(off[q]):int(off[q + 1])] for q in range(n)]
 
+    # ------------------------------------------------------------------ list adapter
+    def list_create(self, entry_type: int, entries, overrides=()) -> "ListHandle":
+        """mxp_list_create: entries / overrides as str or bytes."""
+        def arr(xs):
+            bs = [x.encode("utf-8", "surrogateescape") if isinstance(x, str) else bytes(x) for x in xs]
+            bufs = [ctypes.create_string_buffer(b, len(b) + 1) for b in bs]
+            ptrs = (ctypes.c_char_p * max(len(bs), 1))(*[ctypes.cast(b, ctypes.c_char_p) for b in bufs])
+            lens = np.array([len(b) for b in bs] or [0], dtype=np.uint32)
+            return bufs, ptrs, lens, len(bs)
+        eb, ep, el, en = arr(entries)
+        ob, op, ol, on = arr(overrides)
+        h = _VP()
+        self._check(self.lib.mxp_list_create(self.h, entry_type, ep, el.ctypes.data, en, op, ol.ctypes.data, on,
+                                             ctypes.byref(h)), "mxp_list_create")
+        return ListHandle(self, h)
+
     def error_count(self) -> int:
         return int(self.lib.mxp_error_count(self.h))
 
@@ -371,3 +395,33 @@ def decode_value(e: Engine, rule: int, v: int):
     if kind == 1:
         return txt
     return txt
+
+
+class ListHandle:
+    """A compiled list (mxp_list): HandleListEntry for batches of symbols."""
+    STRINGS, CASE_INSENSITIVE_STRINGS, IP_ADDRESSES, REGEX = 0, 1, 2, 3
+
+    def __init__(self, eng: Engine, h):
+        self.eng, self.h = eng, h
+
+    def num_entries(self) -> int:
+        return int(self.eng.lib.mxp_list_entries(self.h))
+
+    def check(self, symbols, blacklist: bool = False) -> np.ndarray:
+        """google.rpc codes (0 OK, 3 INVALID_ARGUMENT, 5 NOT_FOUND, 7 PERMISSION_DENIED) per symbol."""
+        bs = [x.encode("utf-8", "surrogateescape") if isinstance(x, str) else bytes(x) for x in symbols]
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(b) for b in bs]) if bs else []
+        blob = np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)
+        codes = np.zeros(len(bs), dtype=np.int32)
+        self.eng._check(self.eng.lib.mxp_list_check(self.eng.h, self.h, int(blacklist), blob.ctypes.data,
+                                                    off.ctypes.data, len(bs), codes.ctypes.data), "mxp_list_check")
+        return codes
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.eng.lib.mxp_list_destroy(self.eng.h, self.h)
+                self.h = None
+        except Exception:
+            pass

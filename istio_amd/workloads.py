@@ -370,3 +370,71 @@ def resolver_workload(n_rules=600, n_requests=2000, seed=21):
             b["context.protocol"] = GoInt64(1)
     names = list(manifest)
     return manifest, rules, conf, BagBatch.from_bags(bags, names=names)
+
+
+# ----------------------------------------------------------------------------------- lists (C3)
+def c3_ip_list(n_entries=100_000, n_lookups=1_000_000, seed=3, p_v6=0.1, hit_rate=0.5):
+    """C3 CIDR list: IPv4 /8../32 (uniform prefix) and 10% IPv6 /32../128 entries (some without a
+    prefix length -> "/32" appended, as ipList.addEntry does, even for IPv6); lookups are address
+    strings, half drawn inside entries, plus a few invalid symbols.  Returns (entries, symbols)."""
+    rng = np.random.default_rng(seed)
+    entries, nets = [], []
+    for _ in range(n_entries):
+        if rng.random() < p_v6:
+            bits = int(rng.integers(32, 129))
+            words = rng.integers(0, 1 << 16, size=8)
+            words[0] = 0x2001
+            a = ":".join("%x" % w for w in words)
+            entries.append(a if rng.random() < 0.05 else "%s/%d" % (a, bits))
+            nets.append(("6", words, bits))
+        else:
+            bits = int(rng.integers(8, 33))
+            q = rng.integers(0, 256, size=4)
+            a = "%d.%d.%d.%d" % tuple(q)
+            entries.append(a if bits == 32 and rng.random() < 0.5 else "%s/%d" % (a, bits))
+            nets.append(("4", q, bits))
+    syms = []
+    for _ in range(n_lookups):
+        r = rng.random()
+        if r < 0.01:
+            syms.append("not-an-ip")
+            continue
+        kind, base, bits = nets[int(rng.integers(0, n_entries))]
+        hit = rng.random() < hit_rate
+        if kind == "4":
+            x = int(base[0]) << 24 | int(base[1]) << 16 | int(base[2]) << 8 | int(base[3])
+            host = int(rng.integers(0, 1 << 32))
+            if hit:
+                keep = (0xFFFFFFFF << (32 - bits)) & 0xFFFFFFFF if bits else 0
+                x = (x & keep) | (host & ~keep & 0xFFFFFFFF)
+            else:
+                x = host
+            s = "%d.%d.%d.%d" % (x >> 24, (x >> 16) & 255, (x >> 8) & 255, x & 255)
+            syms.append(s if rng.random() > 0.02 else "::ffff:" + s)
+        else:
+            w = [int(v) for v in base] if hit else [int(v) for v in rng.integers(0, 1 << 16, size=8)]
+            if hit:
+                for i in range(bits // 16 + 1, 8):
+                    w[i] = int(rng.integers(0, 1 << 16))
+            syms.append(":".join("%x" % v for v in w))
+    return entries, syms
+
+
+def c3_string_list(n_entries=100_000, n_lookups=1_000_000, seed=3, hit_rate=0.5):
+    """C3 string list: ASCII entries of 8..64 bytes; lookups half hits (some with case changed,
+    for the case-insensitive kind), half misses.  Returns (entries, symbols)."""
+    rng = np.random.default_rng(seed + 7)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789-_./", dtype=np.uint8)
+    lens = rng.integers(8, 65, size=n_entries)
+    entries = [bytes(alpha[rng.integers(0, len(alpha), size=int(n))]).decode() for n in lens]
+    idx = rng.integers(0, n_entries, size=n_lookups)
+    hit = rng.random(n_lookups) < hit_rate
+    syms = []
+    for i, h in zip(idx, hit):
+        e = entries[int(i)]
+        if not h:
+            e = e[:-1] + ("#" if e[-1] != "#" else "%")
+        elif rng.random() < 0.3:
+            e = e.swapcase()
+        syms.append(e)
+    return entries, syms

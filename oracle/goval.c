@@ -116,6 +116,10 @@ int oracle_parse_ip(const uint8_t* s, size_t n, uint8_t out[16]) {
 
 static const uint8_t v4InV6Prefix[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xff, 0xff};
 
+int oracle_parse_ipv4(const uint8_t* s, size_t n, uint8_t out[16]) { return parse_ipv4(s, n, out); }
+int oracle_parse_ipv6(const uint8_t* s, size_t n, uint8_t out[16]) { return parse_ipv6(s, n, out); }
+int oracle_dtoi(const uint8_t* s, size_t n, int* out, size_t* used) { return dtoi(s, n, out, used); }
+
 int oracle_ip_equal(const uint8_t* a, size_t na, const uint8_t* b, size_t nb) {
     if (na == nb) return na == 0 || memcmp(a, b, na) == 0;
     if (na == 4 && nb == 16) return memcmp(b, v4InV6Prefix, 12) == 0 && memcmp(a, b + 12, 4) == 0;

@@ -40,6 +40,10 @@ typedef struct gv {
 
 /* net.ParseIP: returns 16 on success (16-byte form), 0 on failure. */
 int oracle_parse_ip(const uint8_t* s, size_t n, uint8_t out[16]);
+/* parseIPv4 / parseIPv6 (zone not allowed) / dtoi of src/net/ip.go, as ParseCIDR calls them */
+int oracle_parse_ipv4(const uint8_t* s, size_t n, uint8_t out[16]);
+int oracle_parse_ipv6(const uint8_t* s, size_t n, uint8_t out[16]);
+int oracle_dtoi(const uint8_t* s, size_t n, int* out, size_t* used);
 /* net.IP.Equal */
 int oracle_ip_equal(const uint8_t* a, size_t na, const uint8_t* b, size_t nb);
 /* time.Parse(time.RFC3339, s): returns 1 and the instant on success. */

@@ -1,0 +1,116 @@
+"""ORACLE (test infrastructure only) -- restatement of Mixer's list adapter (mixer/adapter/list).
+
+  HandleListEntry            list.go:68-101     code: INVALID_ARGUMENT on a check error, else
+                                                 blacklist: PERMISSION_DENIED if found / whitelist:
+                                                 NOT_FOUND if not found, OK otherwise
+  parseStringList            stringList.go:29-47 set of non-empty lines + overrides
+  parseCaseInsensitive...    stringList.go:49-67 the same after strings.ToUpper
+  checkList (strings)        stringList.go:73-80 exact / ToUpper membership
+  parseIPList / addEntry     ipList.go:35-75    "/32" appended without '/', net.ParseCIDR; a bad
+                                                 entry fails the list, bad overrides are ignored
+  checkList (IP)             ipList.go:77-92    net.ParseIP, linear IPNet.Contains scan (C, lists_oracle.c)
+
+strings.ToUpper (Go 1.9 src/strings/strings.go): ASCII-only strings take the byte path restated
+here exactly; strings with non-ASCII bytes go through unicode.ToUpper per rune -- approximated with
+Python's single-character upper() and U+FFFD for invalid UTF-8: PARITY UNPINNED (no reference
+fixture covers it; the tests keep to ASCII).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+OK, INVALID_ARGUMENT, NOT_FOUND, PERMISSION_DENIED = 0, 3, 5, 7
+STRINGS, CASE_INSENSITIVE_STRINGS, IP_ADDRESSES, REGEX = 0, 1, 2, 3
+
+
+def _b(x):
+    return x.encode("utf-8", "surrogateescape") if isinstance(x, str) else bytes(x)
+
+
+def go_to_upper(s: bytes) -> bytes:
+    if all(c < 0x80 for c in s):
+        return bytes(c - 32 if 0x61 <= c <= 0x7A else c for c in s)
+    out = []
+    for ch in s.decode("utf-8", "replace"):  # invalid bytes -> U+FFFD (strings.Map)
+        u = ch.upper()
+        out.append(u if len(u) == 1 else ch)
+    return "".join(out).encode("utf-8")
+
+
+class StringList:
+    def __init__(self, lines, overrides=(), case_insensitive=False):
+        self.ci = case_insensitive
+        self.entries = set()
+        for s in list(lines) + list(overrides):
+            s = _b(s)
+            if s:
+                self.entries.add(go_to_upper(s) if self.ci else s)
+
+    def num_entries(self):
+        return len(self.entries)
+
+    def found(self, symbols):
+        return np.array([1 if (go_to_upper(_b(s)) if self.ci else _b(s)) in self.entries else 0 for s in symbols],
+                        dtype=np.int8)
+
+
+class ListParseError(Exception):
+    pass
+
+
+class IPList:
+    def __init__(self, whitelist, overrides=()):
+        import oracle  # liboracle.so
+        self.lib = oracle.lib()
+        self.lib.oracle_parse_cidr.restype = ctypes.c_int
+        self.lib.oracle_parse_cidr.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p]
+        self.lib.oracle_onet_size.restype = ctypes.c_size_t
+        self.size = self.lib.oracle_onet_size()
+        nets = []
+        for ip in whitelist:
+            n = self._add(_b(ip))
+            if n is None:
+                orig = _b(ip).decode("utf-8", "surrogateescape")
+                full = orig if "/" in orig else orig + "/32"
+                raise ListParseError("could not parse list entry %s: invalid CIDR address: %s" % (orig, full))
+            nets.append(n)
+        for ip in overrides:
+            n = self._add(_b(ip))
+            if n is not None:
+                nets.append(n)
+        self.nets = b"".join(nets)
+        self.n = len(nets)
+
+    def _add(self, ip: bytes):
+        if b"/" not in ip:
+            ip += b"/32"
+        buf = ctypes.create_string_buffer(self.size)
+        return bytes(buf.raw) if self.lib.oracle_parse_cidr(ip, len(ip), buf) else None
+
+    def num_entries(self):
+        return self.n
+
+    def found(self, symbols, threads=8):
+        """1 found, 0 not found, -1 not a valid IP address."""
+        bs = [_b(s) for s in symbols]
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        if bs:
+            off[1:] = np.cumsum([len(b) for b in bs])
+        blob = np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)
+        out = np.zeros(len(bs), dtype=np.int8)
+        nets = ctypes.create_string_buffer(self.nets, max(len(self.nets), 1))
+        self.lib.oracle_iplist_check(nets, ctypes.c_size_t(self.n), blob.ctypes.data_as(ctypes.c_void_p),
+                                     off.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(len(bs)),
+                                     out.ctypes.data_as(ctypes.c_void_p), ctypes.c_int(threads))
+        return out
+
+
+def codes(found: np.ndarray, blacklist: bool) -> np.ndarray:
+    """HandleListEntry's status code per symbol from found (1 / 0 / -1 = check error)."""
+    if blacklist:
+        c = np.where(found == 1, PERMISSION_DENIED, OK)
+    else:
+        c = np.where(found == 1, OK, NOT_FOUND)
+    return np.where(found < 0, INVALID_ARGUMENT, c).astype(np.int32)

@@ -1,0 +1,43 @@
+"""List-adapter restatement (oracle/lists.py + lists_oracle.c) against the reference's list tests
+(mixer/adapter/list/list_test.go, transcribed into tests/golden/list_cases.json)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import lists as L
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CASES = json.load(open(os.path.join(HERE, "golden", "list_cases.json")))
+
+
+def oracle_list(spec):
+    if spec["type"] == L.IP_ADDRESSES:
+        return L.IPList(spec["entries"], spec["overrides"])
+    return L.StringList(spec["entries"], spec["overrides"], case_insensitive=spec["type"] == L.CASE_INSENSITIVE_STRINGS)
+
+
+@pytest.mark.parametrize("spec", [s for s in CASES["lists"] if s["type"] != L.REGEX], ids=lambda s: s["name"])
+def test_reference_list_table(spec):
+    if "parse_error" in spec:
+        with pytest.raises(L.ListParseError) as ei:
+            oracle_list(spec)
+        assert str(ei.value) == spec["parse_error"]
+        return
+    lst = oracle_list(spec)
+    syms = [c[0] for c in spec["cases"]]
+    got = L.codes(lst.found(syms), spec["blacklist"])
+    assert list(got) == [c[1] for c in spec["cases"]]
+
+
+def test_ip_semantics_edges():
+    lst = L.IPList(["10.0.0.0/8", "::1", "::ffff:1.2.3.0/120", "2001:db8::/32", "1.2.3.4/0"])
+    # "::1" -> "::1/32" (IPv6 /32); v4-mapped IPv6 net acts as IPv4 1.2.3.0/24; /0 matches every IPv4
+    syms = ["10.1.2.3", "::1", "0:0::5", "1.2.3.200", "2001:db8:ffff::1", "2001:db9::1", "8.8.8.8",
+            "::ffff:10.0.0.1", "010.1.1.1", "1.2.3", "::ffff:8.8.8.8"]
+    assert list(lst.found(syms)) == [1, 1, 1, 1, 1, 0, 1, 1, 1, -1, 1]
+
+
+def test_to_upper_ascii():
+    assert L.go_to_upper(b"AbC-z{") == b"ABC-Z{"
