@@ -1,0 +1,91 @@
+"""Go regexp restatement (oracle/goregex.py).
+
+Pinned: the reference's `matches` rows (mixer/pkg/il/testing/tests.go:2064-2121) and its regex
+list test (mixer/adapter/list/list_test.go:397-431).  The known-answer table below restates Go
+regexp behaviour from its documented semantics (RE2 syntax, OneLine/ClassNL Perl flags, UTF-8
+decoding, empty-width assertions, syntax.Error texts): PARITY UNPINNED -- no reference fixture
+holds these outputs."""
+import pytest
+
+import goregex as G
+
+GOLDEN = [("abc", "abc", True), (".*", "abc", True), ("ab.*d", "abc", False), ("st.*", "str1", True),
+          ("st.*", "sqr1", False),
+          ("a+.*", "abc", True), ("efg", "abc", False), ("a+.*", "B", False), ("efg", "B", False)]
+
+KAT = [
+    ("abc", "xabcx", True), ("^abc", "xabc", False), ("abc$", "abcx", False), ("abc$", "xabc", True),
+    ("a.c", "a\nc", False), ("(?s)a.c", "a\nc", True), ("a+", "aaa", True), ("a{2,3}", "aa", True),
+    ("^a{2,3}$", "aaaa", False), ("^a{2,}$", "aaaa", True), ("^a{2}$", "aaa", False), ("(?i)ABC", "xabc", True),
+    ("(?i:a)b", "AB", False), ("(?i:a)b", "Ab", True), ("a(?i)b", "aB", True), ("(a(?i)b)c", "aBC", False),
+    ("[^a]", "a", False), ("[^a]", "\n", True), ("\\bfoo\\b", "a foo b", True), ("\\bfoo\\b", "afoo", False),
+    ("\\Bfoo", "afoo", True), ("(?m)^b", "a\nb", True), ("^b", "a\nb", False), ("a$", "a\n", False),
+    ("(?m)a$", "a\nb", True), ("\\Aa", "ba", False), ("a\\z", "ab", False), ("\\d+", "x12", True),
+    ("\\D", "123", False), ("\\s", "a b", True), ("\\s", "a\vb", False), ("[[:alpha:]]+", "123", False),
+    ("[[:^alpha:]]", "abc", False), ("[[:space:]]", "a\vb", True), ("\\x41", "A", True),
+    ("\\x{263a}", "☺", True), ("\\101", "A", True), ("\\Qa.b\\E", "axb", False), ("\\Qa.b\\E", "a.b", True),
+    ("\\Qa.b", "a.b", True), ("a|", "xyz", True), ("", "", True), ("x*", "", True), ("(?i)k", "K", True),
+    ("(?i)s", "ſ", True), (".", "\udcff", True), ("^.$", "\udcff", True), ("^..$", "é", False),
+    ("^.$", "é", True), ("[]a]", "]", True), ("[^]a]", "]", False), ("[a-]", "-", True),
+    ("[\\d-z]", "-", True), ("a\\.b", "a.b", True), ("a\\_b", "a_b", True), ("x{", "x{", True),
+    ("x{1", "x{1", True), ("x{,2}", "x{,2}", True), ("x{01}", "x{01}", True), ("(a|b)*c", "ababc", True),
+    ("^(a|b)*$", "abca", False), ("a*?b", "aab", True), ("a+?", "a", True), ("(?U)a+", "aa", True),
+    ("^[a-c]+$", "abcabc", True), ("^[a-c]+$", "abcd", False), ("(?i)[a-c]+", "ABC", True),
+    ("^\\w+@\\w+\\.com$", "joe@example.com", True), ("\\b", "", False), ("\\B", "", True),
+    ("^$", "", True), ("(?m)^$", "a\n", True), ("^\\x{10FFFF}$", "\U0010ffff", True), ("\\0", "\x00", True),
+    ("[\\x00-\\x{10FFFF}]", "z", True), ("^(?:ab)+$", "ababab", True), ("^(?P<x>ab)+$", "abab", True),
+]
+
+ERRORS = [
+    ("a**", "invalid nested repetition operator: `**`"),
+    ("a*?*", "invalid nested repetition operator: `*?*`"),
+    ("a{2}*", "invalid nested repetition operator: `{2}*`"),
+    ("(abc", "missing closing ): `(abc`"),
+    ("abc)", "unexpected ): `abc)`"),
+    ("[abc", "missing closing ]: `[abc`"),
+    ("a[b", "missing closing ]: `[b`"),
+    ("[z-a]", "invalid character class range: `z-a`"),
+    ("a{1001}", "invalid repeat count: `{1001}`"),
+    ("a{2,1}", "invalid repeat count: `{2,1}`"),
+    ("*a", "missing argument to repetition operator: `*`"),
+    ("a|*", "missing argument to repetition operator: `*`"),
+    ("(*a)", "missing argument to repetition operator: `*`"),
+    ("\\", "trailing backslash at end of expression: ``"),
+    ("\\q", "invalid escape sequence: `\\q`"),
+    ("\\8", "invalid escape sequence: `\\8`"),
+    ("\\1", "invalid escape sequence: `\\1`"),
+    ("\\C", "invalid escape sequence: `\\C`"),
+    ("\\xZZ", "invalid escape sequence: `\\xZ`" if False else "invalid escape sequence: `\\xZZ`"),
+    ("\\x{}", "invalid escape sequence: `\\x{}`"),
+    ("[a-\\d]", "invalid escape sequence: `\\d`"),
+    ("(?z)", "invalid or unsupported Perl syntax: `(?z`"),
+    ("(?i-)", "invalid or unsupported Perl syntax: `(?i-)`"),
+    ("(?P<>a)", "invalid named capture: `(?P<>`"),
+    ("(?P<a-b>x)", "invalid named capture: `(?P<a-b>`"),
+    ("[[:foo:]]", "invalid character class range: `[:foo:]`"),
+]
+
+
+@pytest.mark.parametrize("pat,subj,want", GOLDEN)
+def test_reference_rows(pat, subj, want):
+    assert G.match_string(pat, subj) == (want, None)
+
+
+@pytest.mark.parametrize("pat,subj,want", KAT)
+def test_known_answers(pat, subj, want):
+    assert G.match(G.compile(pat), subj) is want, (pat, subj)
+
+
+@pytest.mark.parametrize("pat,msg", ERRORS)
+def test_error_texts(pat, msg):
+    with pytest.raises(G.RegexError) as ei:
+        G.compile(pat)
+    assert str(ei.value) == "error parsing regexp: " + msg
+
+
+def test_unsupported_is_explicit():
+    for pat in ["\\pL", "\\p{Greek}", "(?i)é"]:
+        with pytest.raises(G.Unsupported):
+            G.compile(pat)
+    G.compile("(?i)\\W")  # full non-ASCII coverage: folds only the k / s partners
+    assert G.match(G.compile("(?i)\\W"), "k")
