@@ -164,6 +164,16 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* list, int blacklist, 
                           const uint64_t* d_sym_offsets, uint32_t n, void* stream, int32_t* d_codes);
 
 /*
+ * Regex compiler check (host only; test and tooling hook): compiles `pattern` with the engine's Go
+ * regexp restatement and DFA builder, then matches `subject` on the host DFA.  Returns 1 / 0 for
+ * match / no match, -1 for a syntax error (err = Go's "error parsing regexp: ..." text), -2 when the
+ * pattern uses a construct the engine does not support (err says which), -3 when the DFA exceeds
+ * the state budget.
+ */
+int mxp_regex_match_host(const char* pattern, uint32_t pattern_len, const char* subject, uint32_t subject_len,
+                         char* err, uint32_t err_cap);
+
+/*
  * Device-resident batches (benchmarking and pipelining): pack + upload once, evaluate many times.
  * mxp_batch_eval_device enqueues on `stream` (a hipStream_t; NULL = engine stream) and writes the
  * bitmaps to DEVICE pointers (rule-word-major, as above).  Nothing is synchronised.

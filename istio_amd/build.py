@@ -17,9 +17,9 @@ LIB = os.path.join(HERE, "libmxp.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MXP_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["goutil.cpp", "frontend.cpp", "ilgen.cpp", "lower.cpp", "vmopt.cpp", "engine.cpp", "resolver.cpp",
-           "lists.cpp", "kernels.hip", "resolve.hip", "lists.hip"]
-HEADERS = ["goutil.h", "frontend.h", "ilgen.h", "lower.h", "vmopt.h", "vm.h", "kargs.h", "engine_impl.h", "resolve_args.h", "netparse.h", "lists.h"]
+SOURCES = ["goutil.cpp", "frontend.cpp", "ilgen.cpp", "lower.cpp", "vmopt.cpp", "regex.cpp", "engine.cpp",
+           "resolver.cpp", "lists.cpp", "kernels.hip", "resolve.hip", "lists.hip"]
+HEADERS = ["goutil.h", "frontend.h", "ilgen.h", "lower.h", "vmopt.h", "vm.h", "kargs.h", "engine_impl.h", "resolve_args.h", "netparse.h", "lists.h", "regex.h"]
 
 
 def _stale():

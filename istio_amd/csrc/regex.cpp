@@ -1,0 +1,895 @@
+// regex.cpp -- see regex.h.  Parser follows Go 1.9 src/regexp/syntax/parse.go (Perl flags).
+#include "regex.h"
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <unordered_map>
+
+namespace mxp {
+namespace {
+
+constexpr uint32_t kMaxRune = 0x10FFFF;
+constexpr int kMaxRepeat = 1000;
+constexpr uint32_t kMaxInsts = 200000;
+
+// empty-width assertions (syntax.EmptyOp)
+enum : uint8_t { BEGIN_LINE = 1, END_LINE = 2, BEGIN_TEXT = 4, END_TEXT = 8, WORD_B = 16, NO_WORD_B = 32 };
+
+using Ranges = std::vector<std::pair<uint32_t, uint32_t>>;
+
+struct SyntaxError {
+    std::string code, expr;
+};
+struct UnsupportedError {
+    std::string why;
+};
+
+// utf8.DecodeRune: (rune, width); invalid -> (0xFFFD, 1)
+uint32_t decode_rune(const std::string& b, size_t i, size_t* w) {
+    const uint8_t c = (uint8_t)b[i];
+    const size_t n = b.size() - i;
+    auto at = [&](size_t k) { return (uint8_t)b[i + k]; };
+    *w = 1;
+    if (c < 0x80) return c;
+    if (c >= 0xC2 && c <= 0xDF && n >= 2 && at(1) >= 0x80 && at(1) <= 0xBF) {
+        *w = 2;
+        return ((c & 0x1Fu) << 6) | (at(1) & 0x3Fu);
+    }
+    if (c >= 0xE0 && c <= 0xEF && n >= 3) {
+        uint8_t lo = 0x80, hi = 0xBF;
+        if (c == 0xE0) lo = 0xA0;
+        if (c == 0xED) hi = 0x9F;
+        if (at(1) >= lo && at(1) <= hi && at(2) >= 0x80 && at(2) <= 0xBF) {
+            *w = 3;
+            return ((c & 0x0Fu) << 12) | ((at(1) & 0x3Fu) << 6) | (at(2) & 0x3Fu);
+        }
+    }
+    if (c >= 0xF0 && c <= 0xF4 && n >= 4) {
+        uint8_t lo = 0x80, hi = 0xBF;
+        if (c == 0xF0) lo = 0x90;
+        if (c == 0xF4) hi = 0x8F;
+        if (at(1) >= lo && at(1) <= hi && at(2) >= 0x80 && at(2) <= 0xBF && at(3) >= 0x80 && at(3) <= 0xBF) {
+            *w = 4;
+            return ((c & 0x07u) << 18) | ((at(1) & 0x3Fu) << 12) | ((at(2) & 0x3Fu) << 6) | (at(3) & 0x3Fu);
+        }
+    }
+    return 0xFFFD;
+}
+
+bool is_word(int64_t r) {
+    return r >= 0 && ((r >= '0' && r <= '9') || (r >= 'A' && r <= 'Z') || (r >= 'a' && r <= 'z') || r == '_');
+}
+
+bool is_alnum(uint32_t c) { return (c >= '0' && c <= '9') || (c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z'); }
+
+int unhex(uint32_t c) {
+    if (c >= '0' && c <= '9') return (int)(c - '0');
+    if (c >= 'a' && c <= 'f') return (int)(c - 'a' + 10);
+    if (c >= 'A' && c <= 'F') return (int)(c - 'A' + 10);
+    return -1;
+}
+
+Ranges norm(Ranges rs) {
+    std::sort(rs.begin(), rs.end());
+    Ranges o;
+    for (auto& p : rs) {
+        if (p.first > p.second) continue;
+        if (!o.empty() && p.first <= o.back().second + 1)
+            o.back().second = std::max(o.back().second, p.second);
+        else
+            o.push_back(p);
+    }
+    return o;
+}
+
+Ranges negate(const Ranges& in) {
+    Ranges o;
+    uint32_t nxt = 0;
+    for (auto& p : norm(in)) {
+        if (p.first > nxt) o.emplace_back(nxt, p.first - 1);
+        nxt = p.second + 1;
+    }
+    if (nxt <= kMaxRune) o.emplace_back(nxt, kMaxRune);
+    return o;
+}
+
+// Runes >= 0x80 that have case mappings, conservatively: every Unicode block that holds cased
+// letters up to U+1FFFF.  Folding such a rune needs Unicode tables -> unsupported.
+bool maybe_cased(uint32_t r) {
+    static const uint32_t blocks[][2] = {
+        {0x00B5, 0x00B5}, {0x00C0, 0x024F}, {0x0250, 0x02AF}, {0x0345, 0x0345}, {0x0370, 0x03FF},
+        {0x0400, 0x052F}, {0x0531, 0x0587}, {0x10A0, 0x10FF}, {0x13A0, 0x13FD}, {0x1C80, 0x1CBF},
+        {0x1D79, 0x1D8E}, {0x1E00, 0x1FFF}, {0x2126, 0x2133}, {0x214E, 0x2184}, {0x24B6, 0x24E9},
+        {0x2C00, 0x2D2D}, {0xA640, 0xA69F}, {0xA722, 0xA7FF}, {0xAB53, 0xABBF}, {0xFB00, 0xFB17},
+        {0xFF21, 0xFF5A}, {0x10400, 0x104FF}, {0x10C80, 0x10CFF}, {0x118A0, 0x118DF}, {0x16E40, 0x16E7F},
+        {0x1E900, 0x1E94B}};
+    for (auto& b : blocks)
+        if (r >= b[0] && r <= b[1]) return true;
+    return false;
+}
+
+bool range_has_cased(uint32_t lo, uint32_t hi) {
+    static const uint32_t blocks[][2] = {
+        {0x00B5, 0x00B5}, {0x00C0, 0x024F}, {0x0250, 0x02AF}, {0x0345, 0x0345}, {0x0370, 0x03FF},
+        {0x0400, 0x052F}, {0x0531, 0x0587}, {0x10A0, 0x10FF}, {0x13A0, 0x13FD}, {0x1C80, 0x1CBF},
+        {0x1D79, 0x1D8E}, {0x1E00, 0x1FFF}, {0x2126, 0x2133}, {0x214E, 0x2184}, {0x24B6, 0x24E9},
+        {0x2C00, 0x2D2D}, {0xA640, 0xA69F}, {0xA722, 0xA7FF}, {0xAB53, 0xABBF}, {0xFB00, 0xFB17},
+        {0xFF21, 0xFF5A}, {0x10400, 0x104FF}, {0x10C80, 0x10CFF}, {0x118A0, 0x118DF}, {0x16E40, 0x16E7F},
+        {0x1E900, 0x1E94B}};
+    for (auto& b : blocks) {
+        uint32_t a = std::max(lo, b[0]), z = std::min(hi, b[1]);
+        if (a > z) continue;
+        // the two runes whose fold orbits reach ASCII are handled exactly
+        for (uint32_t r = a; r <= z; r++)
+            if (r != 0x212A && r != 0x17F) return true;
+    }
+    return false;
+}
+
+// appendFoldedRange for ASCII letters and U+212A / U+017F (orbits k K U+212A, s S U+017F)
+Ranges fold_ranges(const Ranges& rs) {
+    Ranges o = rs;
+    for (auto& p : rs) {
+        const uint32_t lo = p.first, hi = p.second;
+        for (int up = 0; up < 2; up++) {
+            const uint32_t a = up ? 'A' : 'a', b = up ? 'Z' : 'z';
+            const uint32_t x = std::max(lo, a), y = std::min(hi, b);
+            if (x <= y) o.emplace_back(up ? x + 32 : x - 32, up ? y + 32 : y - 32);
+        }
+        auto has = [&](uint32_t r) { return lo <= r && r <= hi; };
+        if (has('k') || has('K') || has(0x212A)) {
+            o.emplace_back('k', 'k');
+            o.emplace_back('K', 'K');
+            o.emplace_back(0x212A, 0x212A);
+        }
+        if (has('s') || has('S') || has(0x17F)) {
+            o.emplace_back('s', 's');
+            o.emplace_back('S', 'S');
+            o.emplace_back(0x17F, 0x17F);
+        }
+        // a range over every non-ASCII rune keeps its non-ASCII orbits inside; others need tables
+        if (hi >= 0x80 && !(lo <= 0x80 && hi == kMaxRune) && range_has_cased(std::max(lo, 0x80u), hi))
+            throw UnsupportedError{"case folding of non-ASCII runes"};
+    }
+    return norm(o);
+}
+
+// ---------------------------------------------------------------------------------- AST
+enum NodeKind { N_LIT, N_CLASS, N_ANY, N_ANYNL, N_EMPTY, N_CAT, N_ALT, N_STAR, N_PLUS, N_QUEST, N_REP, N_GROUP };
+
+struct Node {
+    NodeKind k;
+    uint32_t rune = 0;
+    Ranges cls;
+    uint8_t empty = 0;
+    int lo = 0, hi = 0;
+    std::vector<std::unique_ptr<Node>> sub;
+};
+using NodeP = std::unique_ptr<Node>;
+
+NodeP mk(NodeKind k) {
+    NodeP n(new Node());
+    n->k = k;
+    return n;
+}
+
+struct Flags {
+    bool i = false, m = false, s = false, U = false;
+};
+
+class Parser {
+  public:
+    explicit Parser(const std::string& src) : s_(src) {}
+
+    NodeP parse() { return alt(true); }
+
+  private:
+    const std::string& s_;
+    size_t i_ = 0;
+    Flags f_;
+
+    [[noreturn]] void err(const char* code, const std::string& expr) { throw SyntaxError{code, expr}; }
+    std::string text(size_t a, size_t b = std::string::npos) const {
+        return s_.substr(a, b == std::string::npos ? std::string::npos : b - a);
+    }
+    bool at(size_t k, char c) const { return k < s_.size() && s_[k] == c; }
+
+    // nextRune: invalid UTF-8 -> ErrInvalidUTF8 with the rest of the text
+    uint32_t next_rune() {
+        size_t w;
+        const uint32_t r = decode_rune(s_, i_, &w);
+        if (r == 0xFFFD && w == 1 && s_.compare(i_, 3, "\xEF\xBF\xBD") != 0) err("invalid UTF-8", text(i_));
+        i_ += w;
+        return r;
+    }
+
+    NodeP lit(uint32_t r) {
+        if (f_.i) {
+            Ranges orbit;
+            if (r == 'k' || r == 'K' || r == 0x212A)
+                orbit = {{'K', 'K'}, {'k', 'k'}, {0x212A, 0x212A}};
+            else if (r == 's' || r == 'S' || r == 0x17F)
+                orbit = {{'S', 'S'}, {'s', 's'}, {0x17F, 0x17F}};
+            else if ((r >= 'a' && r <= 'z') || (r >= 'A' && r <= 'Z'))
+                orbit = {{r | 0x20u, r | 0x20u}, {r & ~0x20u, r & ~0x20u}};
+            else if (r >= 0x80 && maybe_cased(r))
+                throw UnsupportedError{"case folding of a non-ASCII letter"};
+            if (!orbit.empty()) {
+                NodeP n = mk(N_CLASS);
+                n->cls = norm(orbit);
+                return n;
+            }
+        }
+        NodeP n = mk(N_LIT);
+        n->rune = r;
+        return n;
+    }
+
+    NodeP cls_node(Ranges rs, bool fold) {
+        NodeP n = mk(N_CLASS);
+        n->cls = fold ? fold_ranges(rs) : norm(rs);
+        return n;
+    }
+
+    NodeP alt(bool top) {
+        std::vector<std::vector<NodeP>> alts(1);
+        const Flags saved = f_;
+        while (i_ < s_.size()) {
+            const char c = s_[i_];
+            if (c == '|') {
+                i_++;
+                alts.emplace_back();
+                continue;
+            }
+            if (c == ')') {
+                if (top) err("unexpected )", s_);
+                break;
+            }
+            piece(alts.back());
+        }
+        if (!top) {
+            if (i_ >= s_.size()) err("missing closing )", s_);
+            i_++;
+            f_ = saved;
+        }
+        std::vector<NodeP> cats;
+        for (auto& a : alts) {
+            NodeP c = mk(N_CAT);
+            c->sub = std::move(a);
+            cats.push_back(std::move(c));
+        }
+        if (cats.size() == 1) return std::move(cats[0]);
+        NodeP n = mk(N_ALT);
+        n->sub = std::move(cats);
+        return n;
+    }
+
+    // parseRepeat at i_ ('{'): {n} {n,} {n,m} -> advance; false = literal '{'
+    bool try_repeat(int* lo, int* hi) {
+        size_t j = i_ + 1;
+        auto num = [&](int* v) -> bool {
+            const size_t k0 = j;
+            while (j < s_.size() && s_[j] >= '0' && s_[j] <= '9') j++;
+            if (j == k0) return false;
+            if (j - k0 > 1 && s_[k0] == '0') return false;  // leading zeros
+            long x = 0;
+            for (size_t k = k0; k < j; k++) {
+                x = x * 10 + (s_[k] - '0');
+                if (x > kMaxRepeat) x = kMaxRepeat + 1;
+            }
+            *v = (int)x;
+            return true;
+        };
+        if (!num(lo)) return false;
+        if (at(j, ',')) {
+            j++;
+            if (at(j, '}')) {
+                *hi = -1;
+            } else if (!num(hi)) {
+                return false;
+            }
+        } else {
+            *hi = *lo;
+        }
+        if (!at(j, '}')) return false;
+        j++;
+        const size_t start = i_;
+        i_ = j;
+        if (*lo > kMaxRepeat || *hi > kMaxRepeat || (*hi >= 0 && *lo > *hi)) err("invalid repeat count", text(start, j));
+        return true;
+    }
+
+    void repeat(std::vector<NodeP>& seq, char op, size_t start, int lo = 0, int hi = 0) {
+        if (seq.empty()) err("missing argument to repetition operator", text(start, i_));
+        if (at(i_, '?')) i_++;  // lazy form; irrelevant for a boolean match
+        if (i_ < s_.size() && (s_[i_] == '*' || s_[i_] == '+' || s_[i_] == '?'))
+            err("invalid nested repetition operator", text(start, i_ + 1));
+        if (at(i_, '{')) {
+            const size_t save = i_;
+            int a, b;
+            if (try_repeat(&a, &b)) err("invalid nested repetition operator", text(start, i_));
+            i_ = save;
+        }
+        NodeP sub = std::move(seq.back());
+        seq.pop_back();
+        NodeP n = mk(op == '*' ? N_STAR : op == '+' ? N_PLUS : op == '?' ? N_QUEST : N_REP);
+        n->lo = lo;
+        n->hi = hi;
+        n->sub.push_back(std::move(sub));
+        seq.push_back(std::move(n));
+    }
+
+    void piece(std::vector<NodeP>& seq) {
+        const size_t start = i_;
+        const char c = s_[i_];
+        switch (c) {
+        case '*': case '+': case '?':
+            i_++;
+            repeat(seq, c, start);
+            return;
+        case '{': {
+            int lo, hi;
+            if (try_repeat(&lo, &hi)) {
+                repeat(seq, '{', start, lo, hi);
+                return;
+            }
+            i_++;
+            seq.push_back(lit('{'));
+            return;
+        }
+        case '(':
+            group(seq);
+            return;
+        case '[':
+            seq.push_back(cls_node(parse_class(), false));
+            return;
+        case '.':
+            i_++;
+            seq.push_back(mk(f_.s ? N_ANY : N_ANYNL));
+            return;
+        case '^': {
+            i_++;
+            NodeP n = mk(N_EMPTY);
+            n->empty = f_.m ? BEGIN_LINE : BEGIN_TEXT;
+            seq.push_back(std::move(n));
+            return;
+        }
+        case '$': {
+            i_++;
+            NodeP n = mk(N_EMPTY);
+            n->empty = f_.m ? END_LINE : END_TEXT;
+            seq.push_back(std::move(n));
+            return;
+        }
+        case '\\':
+            escape_atom(seq);
+            return;
+        default:
+            seq.push_back(lit(next_rune()));
+        }
+    }
+
+    void group(std::vector<NodeP>& seq) {
+        const size_t start = i_;
+        if (at(i_ + 1, '?')) {
+            if (s_.size() > i_ + 4 && s_[i_ + 2] == 'P' && s_[i_ + 3] == '<') {
+                const size_t end = s_.find('>', i_ + 4);
+                if (end == std::string::npos) err("invalid named capture", text(start));
+                bool ok = end > i_ + 4;
+                for (size_t k = i_ + 4; k < end; k++) ok = ok && is_word((uint8_t)s_[k]);
+                if (!ok) err("invalid named capture", text(start, end + 1));
+                i_ = end + 1;
+                NodeP g = mk(N_GROUP);
+                g->sub.push_back(alt(false));
+                seq.push_back(std::move(g));
+                return;
+            }
+            size_t j = i_ + 2;
+            bool sign = true, neg = false, seen = false;
+            Flags nf = f_;
+            while (true) {
+                if (j >= s_.size()) err("invalid or unsupported Perl syntax", text(start));
+                const char c = s_[j++];
+                if (c == 'i' || c == 'm' || c == 's' || c == 'U') {
+                    (c == 'i' ? nf.i : c == 'm' ? nf.m : c == 's' ? nf.s : nf.U) = sign;
+                    seen = true;
+                } else if (c == '-') {
+                    if (neg) err("invalid or unsupported Perl syntax", text(start, j));
+                    neg = true;
+                    sign = false;
+                    seen = false;
+                } else if (c == ':' || c == ')') {
+                    if (neg && !seen) err("invalid or unsupported Perl syntax", text(start, j));
+                    i_ = j;
+                    if (c == ')') {
+                        f_ = nf;  // rest of the current group
+                        return;
+                    }
+                    const Flags outer = f_;
+                    f_ = nf;
+                    NodeP g = mk(N_GROUP);
+                    g->sub.push_back(alt(false));
+                    f_ = outer;
+                    seq.push_back(std::move(g));
+                    return;
+                } else {
+                    // the offending rune (possibly multi-byte) is part of the error text
+                    size_t w;
+                    decode_rune(s_, j - 1, &w);
+                    err("invalid or unsupported Perl syntax", text(start, j - 1 + w));
+                }
+            }
+        }
+        i_++;
+        NodeP g = mk(N_GROUP);
+        g->sub.push_back(alt(false));
+        seq.push_back(std::move(g));
+    }
+
+    // parsePerlClassEscape: \d \s \w (and negations); \p \P unsupported
+    bool perl_class(Ranges* out) {
+        if (!at(i_, '\\') || i_ + 1 >= s_.size()) return false;
+        const char c = s_[i_ + 1];
+        Ranges r;
+        switch (c | 0x20) {
+        case 'd': r = {{'0', '9'}}; break;
+        case 's': r = {{'\t', '\n'}, {'\f', '\r'}, {' ', ' '}}; break;
+        case 'w': r = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}; break;
+        case 'p':
+            if (c == 'p' || c == 'P') throw UnsupportedError{"Unicode character classes (\\p)"};
+            return false;
+        default: return false;
+        }
+        if (c != 'd' && c != 's' && c != 'w' && c != 'D' && c != 'S' && c != 'W') return false;
+        i_ += 2;
+        *out = (c >= 'A' && c <= 'Z') ? negate(r) : r;
+        return true;
+    }
+
+    // parseEscape: one escaped rune; errors carry the text consumed so far
+    uint32_t escape() {
+        const size_t start = i_;
+        i_++;
+        if (i_ >= s_.size()) err("trailing backslash at end of expression", "");
+        const uint32_t c = next_rune();
+        auto fail = [&]() { err("invalid escape sequence", text(start, i_)); };
+        if (c < 0x80 && !is_alnum(c)) return c;
+        if (c >= '1' && c <= '7' && !(i_ < s_.size() && s_[i_] >= '0' && s_[i_] <= '7')) fail();
+        if (c >= '0' && c <= '7') {
+            uint32_t r = c - '0';
+            for (int k = 1; k < 3 && i_ < s_.size() && s_[i_] >= '0' && s_[i_] <= '7'; k++) r = r * 8 + (s_[i_++] - '0');
+            return r;
+        }
+        if (c == 'x') {
+            if (i_ >= s_.size()) fail();
+            const uint32_t c2 = next_rune();
+            if (c2 == '{') {
+                int nhex = 0;
+                uint32_t r = 0;
+                while (true) {
+                    if (i_ >= s_.size()) fail();
+                    const uint32_t d = next_rune();
+                    if (d == '}') break;
+                    const int v = unhex(d);
+                    if (v < 0) fail();
+                    r = r * 16 + (uint32_t)v;
+                    if (r > kMaxRune) fail();
+                    nhex++;
+                }
+                if (!nhex) fail();
+                return r;
+            }
+            const int x = unhex(c2);
+            const uint32_t c3 = i_ < s_.size() ? next_rune() : 0xFFFD;
+            const int y = unhex(c3);
+            if (x < 0 || y < 0) fail();
+            return (uint32_t)(x * 16 + y);
+        }
+        switch (c) {
+        case 'a': return 7;
+        case 'f': return 12;
+        case 'n': return 10;
+        case 'r': return 13;
+        case 't': return 9;
+        case 'v': return 11;
+        default: fail();
+        }
+        return 0;
+    }
+
+    void escape_atom(std::vector<NodeP>& seq) {
+        if (i_ + 1 < s_.size()) {
+            const char c = s_[i_ + 1];
+            uint8_t e = c == 'A' ? BEGIN_TEXT : c == 'z' ? END_TEXT : c == 'b' ? WORD_B : c == 'B' ? NO_WORD_B : 0;
+            if (e) {
+                i_ += 2;
+                NodeP n = mk(N_EMPTY);
+                n->empty = e;
+                seq.push_back(std::move(n));
+                return;
+            }
+            if (c == 'C') err("invalid escape sequence", "\\C");
+            if (c == 'Q') {
+                i_ += 2;
+                const size_t end = s_.find("\\E", i_);
+                const size_t stop = end == std::string::npos ? s_.size() : end;
+                while (i_ < stop) seq.push_back(lit(next_rune()));
+                i_ = end == std::string::npos ? s_.size() : end + 2;
+                return;
+            }
+        }
+        Ranges r;
+        if (perl_class(&r)) {
+            seq.push_back(cls_node(r, f_.i));
+            return;
+        }
+        seq.push_back(lit(escape()));
+    }
+
+    uint32_t class_char(size_t class_start) {
+        if (i_ >= s_.size()) err("missing closing ]", text(class_start));
+        if (s_[i_] == '\\') return escape();
+        return next_rune();
+    }
+
+    Ranges parse_class() {
+        static const std::map<std::string, Ranges> posix = {
+            {"alnum", {{'0', '9'}, {'A', 'Z'}, {'a', 'z'}}},
+            {"alpha", {{'A', 'Z'}, {'a', 'z'}}},
+            {"ascii", {{0, 0x7F}}},
+            {"blank", {{'\t', '\t'}, {' ', ' '}}},
+            {"cntrl", {{0, 0x1F}, {0x7F, 0x7F}}},
+            {"digit", {{'0', '9'}}},
+            {"graph", {{'!', '~'}}},
+            {"lower", {{'a', 'z'}}},
+            {"print", {{' ', '~'}}},
+            {"punct", {{'!', '/'}, {':', '@'}, {'[', '`'}, {'{', '~'}}},
+            {"space", {{'\t', '\r'}, {' ', ' '}}},
+            {"upper", {{'A', 'Z'}}},
+            {"word", {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}},
+            {"xdigit", {{'0', '9'}, {'A', 'F'}, {'a', 'f'}}}};
+        const size_t start = i_;
+        i_++;
+        bool neg = false;
+        if (at(i_, '^')) {
+            neg = true;
+            i_++;
+        }
+        Ranges rs;
+        bool first = true;
+        while (true) {
+            if (i_ >= s_.size()) err("missing closing ]", text(start));
+            if (s_[i_] == ']' && !first) {
+                i_++;
+                break;
+            }
+            if (s_[i_] == '[' && at(i_ + 1, ':')) {
+                const size_t end = s_.find(":]", i_ + 2);
+                if (end != std::string::npos) {
+                    std::string name = s_.substr(i_ + 2, end - i_ - 2);
+                    const bool pneg = !name.empty() && name[0] == '^';
+                    if (pneg) name = name.substr(1);
+                    auto it = posix.find(name);
+                    if (it == posix.end()) err("invalid character class range", text(i_, end + 2));
+                    const Ranges g = pneg ? negate(it->second) : it->second;
+                    rs.insert(rs.end(), g.begin(), g.end());
+                    i_ = end + 2;
+                    first = false;
+                    continue;
+                }
+            }
+            Ranges pc;
+            if (perl_class(&pc)) {
+                rs.insert(rs.end(), pc.begin(), pc.end());
+                first = false;
+                continue;
+            }
+            const size_t rstart = i_;
+            const uint32_t lo = class_char(start);
+            if (i_ + 1 < s_.size() && s_[i_] == '-' && s_[i_ + 1] != ']') {
+                i_++;
+                const uint32_t hi = class_char(start);
+                if (hi < lo) err("invalid character class range", text(rstart, i_));
+                rs.emplace_back(lo, hi);
+            } else {
+                rs.emplace_back(lo, lo);
+            }
+            first = false;
+        }
+        if (f_.i) rs = fold_ranges(rs);
+        rs = norm(rs);
+        return neg ? negate(rs) : rs;
+    }
+};
+
+// ---------------------------------------------------------------------------------- NFA
+enum InstOp : uint8_t { I_RUNE, I_SPLIT, I_EMPTY, I_MATCH };
+struct Inst {
+    InstOp op;
+    uint8_t empty = 0;
+    int32_t x = -1, y = -1;  // next (RUNE/EMPTY) or the two branches (SPLIT)
+    Ranges r;
+};
+
+struct Prog {
+    std::vector<Inst> ins;
+    int emit(Inst i) {
+        if (ins.size() >= kMaxInsts) throw UnsupportedError{"regular expression too large for the DFA compiler"};
+        ins.push_back(std::move(i));
+        return (int)ins.size() - 1;
+    }
+    int rune(Ranges r, int nxt) {
+        Inst i{I_RUNE};
+        i.r = std::move(r);
+        i.x = nxt;
+        return emit(std::move(i));
+    }
+    int split(int a, int b) {
+        Inst i{I_SPLIT};
+        i.x = a;
+        i.y = b;
+        return emit(std::move(i));
+    }
+
+    int compile(const Node& n, int nxt) {
+        switch (n.k) {
+        case N_LIT: return rune({{n.rune, n.rune}}, nxt);
+        case N_CLASS: return rune(n.cls, nxt);
+        case N_ANY: return rune({{0, kMaxRune}}, nxt);
+        case N_ANYNL: return rune({{0, 9}, {11, kMaxRune}}, nxt);
+        case N_EMPTY: {
+            Inst i{I_EMPTY};
+            i.empty = n.empty;
+            i.x = nxt;
+            return emit(std::move(i));
+        }
+        case N_GROUP: return compile(*n.sub[0], nxt);
+        case N_CAT: {
+            int pc = nxt;
+            for (size_t k = n.sub.size(); k-- > 0;) pc = compile(*n.sub[k], pc);
+            return pc;
+        }
+        case N_ALT: {
+            std::vector<int> e;
+            for (auto& s : n.sub) e.push_back(compile(*s, nxt));
+            int pc = e.back();
+            for (size_t k = e.size() - 1; k-- > 0;) pc = split(e[k], pc);
+            return pc;
+        }
+        case N_QUEST: return split(compile(*n.sub[0], nxt), nxt);
+        case N_STAR: {
+            const int loop = split(-1, nxt);
+            ins[loop].x = compile(*n.sub[0], loop);
+            return loop;
+        }
+        case N_PLUS: {
+            const int loop = split(-1, nxt);
+            const int body = compile(*n.sub[0], loop);
+            ins[loop].x = body;
+            return body;
+        }
+        case N_REP: {
+            int pc = nxt;
+            if (n.hi < 0) {
+                const int loop = split(-1, pc);
+                ins[loop].x = compile(*n.sub[0], loop);
+                pc = loop;
+            } else {
+                for (int k = 0; k < n.hi - n.lo; k++) pc = split(compile(*n.sub[0], pc), pc);
+            }
+            for (int k = 0; k < n.lo; k++) pc = compile(*n.sub[0], pc);
+            return pc;
+        }
+        }
+        return nxt;
+    }
+};
+
+// ---------------------------------------------------------------------------------- DFA
+struct StateKey {
+    std::vector<int32_t> pcs;  // sorted unclosed thread set
+    uint8_t ctx;               // bit0 at text begin, bit1 previous '\n', bit2 previous word rune
+    bool operator==(const StateKey& o) const { return ctx == o.ctx && pcs == o.pcs; }
+};
+struct StateHash {
+    size_t operator()(const StateKey& k) const {
+        uint64_t h = k.ctx * 0x9E3779B97F4A7C15ull;
+        for (int32_t p : k.pcs) h = (h ^ (uint64_t)p) * 0xBF58476D1CE4E5B9ull;
+        return (size_t)(h ^ (h >> 31));
+    }
+};
+
+}  // namespace
+
+int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states, Dfa* out, std::string* err,
+                  uint32_t* bad) {
+    Prog p;
+    std::vector<int> starts;
+    const int match = p.emit(Inst{I_MATCH});
+    try {
+        for (size_t k = 0; k < patterns.size(); k++) {
+            if (bad) *bad = (uint32_t)k;
+            Parser ps(patterns[k]);
+            NodeP ast = ps.parse();
+            starts.push_back(p.compile(*ast, match));
+        }
+    } catch (const SyntaxError& e) {
+        *err = "error parsing regexp: " + e.code + ": `" + e.expr + "`";
+        return RX_SYNTAX;
+    } catch (const UnsupportedError& e) {
+        *err = e.why;
+        return RX_UNSUPPORTED;
+    }
+    // union: one start thread per pattern
+    // alphabet: boundaries of every rune range, '\n', the ASCII word ranges
+    std::vector<uint32_t> cuts = {0, 0x80, '\n', '\n' + 1, '0', '9' + 1, 'A', 'Z' + 1, '_', '_' + 1, 'a', 'z' + 1,
+                                  kMaxRune + 1};
+    for (auto& i : p.ins)
+        if (i.op == I_RUNE)
+            for (auto& r : i.r) {
+                cuts.push_back(r.first);
+                cuts.push_back(r.second + 1);
+            }
+    std::sort(cuts.begin(), cuts.end());
+    cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
+    while (!cuts.empty() && cuts.back() > kMaxRune + 1) cuts.pop_back();
+    // class k = [cuts[k], cuts[k+1]); representatives decide rune membership
+    const uint32_t nrc = (uint32_t)cuts.size() - 1;
+    if (nrc + 1 > 0xFFFF) {
+        *err = "too many rune classes";
+        return RX_TOO_BIG;
+    }
+    Dfa d;
+    d.ncls = nrc + 1;  // + END
+    for (uint32_t k = 0; k < nrc; k++) {
+        if (cuts[k] < 0x80)
+            for (uint32_t r = cuts[k]; r < std::min<uint32_t>(cuts[k + 1], 0x80); r++) d.ascii[r] = (uint16_t)k;
+        if (cuts[k + 1] > 0x80) {
+            d.hi_lo.push_back(std::max<uint32_t>(cuts[k], 0x80));
+            d.hi_cls.push_back((uint16_t)k);
+        }
+    }
+    // per instruction, per class: does the rune instruction accept the class?
+    std::vector<std::vector<uint8_t>> accepts(p.ins.size());
+    for (size_t k = 0; k < p.ins.size(); k++) {
+        if (p.ins[k].op != I_RUNE) continue;
+        accepts[k].assign(nrc, 0);
+        for (auto& r : p.ins[k].r) {
+            auto a = std::lower_bound(cuts.begin(), cuts.end(), r.first) - cuts.begin();
+            auto b = std::lower_bound(cuts.begin(), cuts.end(), r.second + 1) - cuts.begin();
+            for (auto c = a; c < b; c++) accepts[k][c] = 1;
+        }
+    }
+    std::unordered_map<StateKey, uint32_t, StateHash> ids;
+    std::vector<StateKey> states;
+    auto intern = [&](StateKey k) -> uint32_t {
+        auto it = ids.find(k);
+        if (it != ids.end()) return it->second;
+        const uint32_t id = (uint32_t)states.size();
+        ids.emplace(k, id);
+        states.push_back(std::move(k));
+        return id;
+    };
+    // epsilon closure under assertion flags; rune instructions go to `out`
+    std::vector<uint32_t> mark(p.ins.size(), 0);
+    uint32_t stamp = 0;
+    std::vector<int32_t> stack;
+    auto close = [&](const int32_t* pcs, size_t n, uint8_t flags, std::vector<int32_t>& out) -> bool {
+        bool matched = false;
+        stack.assign(pcs, pcs + n);
+        std::reverse(stack.begin(), stack.end());
+        while (!stack.empty()) {
+            const int32_t pc = stack.back();
+            stack.pop_back();
+            if (pc < 0 || mark[pc] == stamp) continue;
+            mark[pc] = stamp;
+            const Inst& in = p.ins[pc];
+            if (in.op == I_SPLIT) {
+                stack.push_back(in.y);
+                stack.push_back(in.x);
+            } else if (in.op == I_EMPTY) {
+                if ((in.empty & flags) == in.empty) stack.push_back(in.x);
+            } else if (in.op == I_MATCH) {
+                matched = true;
+            } else {
+                out.push_back(pc);
+            }
+        }
+        return matched;
+    };
+    // the start threads' closure depends only on the assertion flags: computed once per flags value
+    std::vector<std::vector<int32_t>> start_cl(64);
+    std::vector<int8_t> start_match(64, -1);
+    auto start_closure = [&](uint8_t f) -> const std::vector<int32_t>& {
+        if (start_match[f] < 0) {
+            ++stamp;
+            start_match[f] = close(starts.data(), starts.size(), f, start_cl[f]) ? 1 : 0;
+        }
+        return start_cl[f];
+    };
+    d.start = intern(StateKey{{}, 1});
+    std::vector<int32_t> closure;
+    for (uint32_t sidx = 0; sidx < states.size(); sidx++) {
+        if (states.size() > max_states) {
+            *err = "DFA exceeds the state budget";
+            return RX_TOO_BIG;
+        }
+        const StateKey cur = states[sidx];
+        const bool begin = cur.ctx & 1, prev_nl = cur.ctx & 2, prev_word = cur.ctx & 4;
+        for (uint32_t c = 0; c <= nrc; c++) {
+            const bool end = c == nrc;
+            const uint32_t rep = end ? 0 : cuts[c];
+            uint8_t flags = 0;
+            if (begin) flags |= BEGIN_TEXT | BEGIN_LINE;
+            if (prev_nl) flags |= BEGIN_LINE;
+            if (end) flags |= END_TEXT | END_LINE;
+            if (!end && rep == '\n') flags |= END_LINE;
+            flags |= (prev_word != (!end && is_word(rep))) ? WORD_B : NO_WORD_B;
+            // pending threads, then a fresh start thread per pattern (unanchored search)
+            const std::vector<int32_t>& sc = start_closure(flags);
+            closure.clear();
+            ++stamp;
+            bool matched = close(cur.pcs.data(), cur.pcs.size(), flags, closure) || start_match[flags] == 1;
+            uint32_t next;
+            if (matched) {
+                next = kDfaAccept;
+            } else if (end) {
+                next = kDfaReject;
+            } else {
+                StateKey nk;
+                for (int32_t pc : closure)
+                    if (accepts[pc][c]) nk.pcs.push_back(p.ins[pc].x);
+                for (int32_t pc : sc)
+                    if (mark[pc] != stamp && accepts[pc][c]) nk.pcs.push_back(p.ins[pc].x);
+                std::sort(nk.pcs.begin(), nk.pcs.end());
+                nk.pcs.erase(std::unique(nk.pcs.begin(), nk.pcs.end()), nk.pcs.end());
+                nk.ctx = (uint8_t)((rep == '\n' ? 2 : 0) | (is_word(rep) ? 4 : 0));
+                next = intern(std::move(nk));
+            }
+            d.trans.push_back(next);
+        }
+    }
+    d.nstates = (uint32_t)states.size();
+    *out = std::move(d);
+    return RX_OK;
+}
+
+bool dfa_match_host(const Dfa& d, const std::string& s) {
+    uint32_t st = d.start;
+    size_t i = 0;
+    while (i < s.size()) {
+        size_t w;
+        const uint32_t r = decode_rune(s, i, &w);
+        i += w;
+        uint32_t c;
+        if (r < 0x80) {
+            c = d.ascii[r];
+        } else {
+            size_t k = std::upper_bound(d.hi_lo.begin(), d.hi_lo.end(), r) - d.hi_lo.begin() - 1;
+            c = d.hi_cls[k];
+        }
+        st = d.trans[(size_t)st * d.ncls + c];
+        if (st == kDfaAccept) return true;
+    }
+    return d.trans[(size_t)st * d.ncls + d.ncls - 1] == kDfaAccept;
+}
+
+}  // namespace mxp
+
+extern "C" int mxp_regex_match_host(const char* pattern, uint32_t pattern_len, const char* subject,
+                                    uint32_t subject_len, char* err, uint32_t err_cap) {
+    mxp::Dfa d;
+    std::string e;
+    const int rc = mxp::regex_compile({std::string(pattern ? pattern : "", pattern_len)}, 1u << 20, &d, &e);
+    if (err && err_cap) {
+        const size_t n = std::min<size_t>(e.size(), err_cap - 1);
+        memcpy(err, e.data(), n);
+        err[n] = 0;
+    }
+    if (rc == mxp::RX_SYNTAX) return -1;
+    if (rc == mxp::RX_UNSUPPORTED) return -2;
+    if (rc != mxp::RX_OK) return -3;
+    return mxp::dfa_match_host(d, std::string(subject ? subject : "", subject_len)) ? 1 : 0;
+}

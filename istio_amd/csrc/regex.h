@@ -1,0 +1,53 @@
+// regex.h -- Go regexp (RE2 syntax) compiled to a DFA the GPU steps one rune at a time.
+//
+// The reference matches with regexp.MatchString (mixer/pkg/il/runtime/externs.go:118-120) and
+// regexList.checkList (mixer/adapter/list/regexList.go:26-33): compile with syntax.Perl flags, then
+// an unanchored search whose only output is "some match exists".  That boolean is a regular-language
+// membership test, so the engine compiles it ahead of time:
+//
+//   parse     Go 1.9 regexp/syntax parse.go semantics (same grammar, flags, error codes and texts
+//             as the oracle restatement oracle/goregex.py);
+//   NFA       Thompson program over rune ranges with empty-width assertions;
+//   DFA       subset construction over rune classes (the partition of all runes by every range
+//             boundary, '\n' and the ASCII word characters) plus an END symbol; a DFA state is an
+//             unclosed NFA thread set plus the context the assertions need (at text begin,
+//             previous rune '\n', previous rune a word character), the way RE2's DFA carries flags.
+//             The start thread is re-injected at every position (unanchored search), and a step
+//             whose closure reaches MATCH goes to the absorbing ACCEPT state.
+//
+// Unsupported (reported, never approximated): Unicode classes \p / \P and case folding of non-ASCII
+// letters (both need Unicode tables), and DFAs beyond the state budget.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace mxp {
+
+constexpr uint32_t kDfaAccept = 0xFFFFFFFFu;
+constexpr uint32_t kDfaReject = 0xFFFFFFFEu;
+
+struct Dfa {
+    // alphabet: class of each ASCII rune, then non-ASCII class ranges [lo_k, lo_{k+1})
+    uint16_t ascii[128] = {};
+    std::vector<uint32_t> hi_lo;   // ascending range starts (first is 0x80)
+    std::vector<uint16_t> hi_cls;  // class of each range
+    uint32_t ncls = 0;             // rune classes + 1 (the last column is END of text)
+    uint32_t nstates = 0;
+    uint32_t start = 0;
+    std::vector<uint32_t> trans;   // [nstates][ncls]: next state, kDfaAccept or kDfaReject
+};
+
+enum RegexStatus { RX_OK = 0, RX_SYNTAX = 1, RX_UNSUPPORTED = 2, RX_TOO_BIG = 3 };
+
+// Compile the union of `patterns` (a match of any of them is a match) into `out`.  On RX_SYNTAX,
+// *err is Go's error text ("error parsing regexp: <code>: `<expr>`") of the first failing pattern
+// and *bad its index; on RX_UNSUPPORTED / RX_TOO_BIG *err says why.
+int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states, Dfa* out, std::string* err,
+                  uint32_t* bad = nullptr);
+
+// Host reference stepping of a compiled DFA (tests / debugging).
+bool dfa_match_host(const Dfa& d, const std::string& s);
+
+}  // namespace mxp

@@ -5,7 +5,7 @@
 
 #include "../../include/mxp.h"
 
-#define MXP_NS_NONE 0x7FFFFFFFu      // namespace without rules
+#define MXP_NS_NONE 0x7FFFFFFDu      // namespace without rules (with the tcp bit it stays distinct from the two codes below)
 #define MXP_NS_MISSING 0xFFFFFFFFu   // identity attribute absent
 #define MXP_NS_NOTSTRING 0xFFFFFFFEu // identity attribute not a string
 

@@ -64,6 +64,8 @@ SIGNATURES = {
                                       ctypes.c_void_p]),
     "mxp_list_check_device": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
+    "mxp_regex_match_host": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+                                            ctypes.c_char_p, ctypes.c_uint32]),
     "mxp_set_timing": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
@@ -425,3 +427,14 @@ class ListHandle:
                 self.h = None
         except Exception:
             pass
+
+
+def regex_match_host(pattern, subject):
+    """mxp_regex_match_host -> (status, text): 1 / 0 match, -1 syntax error (Go text), -2 unsupported,
+    -3 DFA too big."""
+    lib = load_library()
+    p = pattern.encode("utf-8", "surrogateescape") if isinstance(pattern, str) else bytes(pattern)
+    s = subject.encode("utf-8", "surrogateescape") if isinstance(subject, str) else bytes(subject)
+    buf = ctypes.create_string_buffer(1024)
+    rc = lib.mxp_regex_match_host(p, len(p), s, len(s), buf, 1024)
+    return rc, buf.value.decode("utf-8", "surrogateescape")
