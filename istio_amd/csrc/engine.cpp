@@ -32,6 +32,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
             if (R.low.ok) {
                 code = R.low.code;
                 need_ipof |= R.low.uses_ipof;
+                need_rxof |= R.low.uses_rxof;
                 need_tsof |= R.low.uses_tsof;
                 need_strings |= R.low.uses_strings;
                 need_maps |= R.low.uses_maps;
@@ -234,6 +235,11 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_tmpls, tmpls.data(), tmpls.size() * sizeof(mxp_tmpl), "upload tmpls"))) return rc;
     if ((rc = put(d_rule_tmpl, rule_tmpl.data(), rule_tmpl.size() * 4, "upload rule_tmpl"))) return rc;
     if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
+    if ((rc = put(d_rx_hdr, rx_set.hdr.data(), rx_set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
+    if ((rc = put(d_rx_trans, rx_set.trans.data(), rx_set.trans.size() * 4, "upload rx trans"))) return rc;
+    if ((rc = put(d_rx_ascii, rx_set.ascii.data(), rx_set.ascii.size() * 2, "upload rx ascii"))) return rc;
+    if ((rc = put(d_rx_hilo, rx_set.hilo.data(), rx_set.hilo.size() * 4, "upload rx hilo"))) return rc;
+    if ((rc = put(d_rx_hicls, rx_set.hicls.data(), rx_set.hicls.size() * 2, "upload rx hicls"))) return rc;
     std::vector<uint64_t> soff;
     std::string blob;
     if (!string_pool(gstrs, &soff, &blob)) return fail(MXP_ERR_ARG, "rule-set string longer than 16 MiB");
@@ -412,6 +418,25 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
                 tsof[s] = MXP_FH(MXP_TIMESTAMP, time_id(sec, ns));
         }
     }
+    // run-time regexp patterns: every distinct string of a pattern column, compiled once per batch
+    std::vector<uint32_t> rxof;
+    mxp::DfaSetHost rxb;
+    if (need_rxof) {
+        rxof.assign(S, MXP_RXOF_SYNTAX);
+        std::vector<uint8_t> done(S, 0);
+        for (uint32_t c : rx_cols) {
+            const uint8_t* k = kinds.data() + (size_t)c * n;
+            const uint64_t* v = vals.data() + (size_t)c * n;
+            for (uint32_t q = 0; q < n; q++) {
+                if (k[q] != MXP_STRING || v[q] >= S || done[v[q]]) continue;
+                done[v[q]] = 1;
+                mxp::Dfa d;
+                std::string e;
+                const int rc = mxp::regex_compile({string_of(db, v[q])}, kRegexStates, &d, &e);
+                rxof[v[q]] = rc == mxp::RX_OK ? rxb.add(d) : rc == mxp::RX_SYNTAX ? MXP_RXOF_SYNTAX : MXP_RXOF_UNSUPPORTED;
+            }
+        }
+    }
     std::vector<uint64_t> ooff;
     std::string oblob;
     if (need_strings && !string_pool(db->overlay, &ooff, &oblob))
@@ -434,6 +459,12 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = up(db->tsof, tsof.data(), tsof.size() * 8, "upload tsof"))) return rc;
     if ((rc = up(db->bstr_off, ooff.data(), ooff.size() * 8, "upload bstr_off"))) return rc;
     if ((rc = up(db->bstr, oblob.data(), oblob.size(), "upload bstr"))) return rc;
+    if ((rc = up(db->rxof, rxof.data(), rxof.size() * 4, "upload rxof"))) return rc;
+    if ((rc = up(db->rx_hdr, rxb.hdr.data(), rxb.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
+    if ((rc = up(db->rx_trans, rxb.trans.data(), rxb.trans.size() * 4, "upload rx trans"))) return rc;
+    if ((rc = up(db->rx_ascii, rxb.ascii.data(), rxb.ascii.size() * 2, "upload rx ascii"))) return rc;
+    if ((rc = up(db->rx_hilo, rxb.hilo.data(), rxb.hilo.size() * 4, "upload rx hilo"))) return rc;
+    if ((rc = up(db->rx_hicls, rxb.hicls.data(), rxb.hicls.size() * 2, "upload rx hicls"))) return rc;
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "pack sync");
     return MXP_OK;
 }
@@ -471,6 +502,11 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->map_vals = db->map_vals.as<uint32_t>();
     A->ipof = db->ipof.as<uint64_t>();
     A->tsof = db->tsof.as<uint64_t>();
+    A->rx = mxp_dfa_set{d_rx_hdr.as<mxp_dfa_hdr>(), d_rx_trans.as<uint32_t>(), d_rx_ascii.as<uint16_t>(),
+                        d_rx_hilo.as<uint32_t>(), d_rx_hicls.as<uint16_t>()};
+    A->rx_batch = mxp_dfa_set{db->rx_hdr.as<mxp_dfa_hdr>(), db->rx_trans.as<uint32_t>(), db->rx_ascii.as<uint16_t>(),
+                              db->rx_hilo.as<uint32_t>(), db->rx_hicls.as<uint16_t>()};
+    A->rxof = db->rxof.as<uint32_t>();
 }
 
 int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
@@ -574,6 +610,14 @@ std::string mxp_engine::format_error(const mxp_bag_batch* b, const mxp_dbatch* d
                "' to TIMESTAMP. expected format: '2006-01-02T15:04:05Z07:00'";
     case ERR_MEMBER: return "member lookup failed: '" + string_of(db, r.aux) + "'";
     case ERR_UNDERFLOW: return "stack underflow";
+    case ERR_REGEX: case ERR_REGEX_UNSUPPORTED: {
+        // regexp.MatchString's error: the pattern's compile error (Go's text); or why this engine
+        // cannot compile it (a known divergence, reported rather than approximated)
+        mxp::Dfa d;
+        std::string e;
+        mxp::regex_compile({string_of(db, r.aux)}, 1, &d, &e);
+        return r.code == ERR_REGEX ? e : "unsupported regexp (engine): " + e;
+    }
     case ERR_STATIC: case ERR_UNSUPPORTED: case PANIC_STATIC:
         return r.aux < rules.size() ? rules[r.aux].error : std::string("?");
     case PANIC_MAPTYPE: return "Unknown map type";

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -19,6 +20,7 @@
 #include "ilgen.h"
 #include "kargs.h"
 #include "lower.h"
+#include "regex.h"
 #include "vmopt.h"
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
@@ -89,6 +91,7 @@ inline uint32_t okset_of(uint32_t kind) {
 struct mxp_dbatch {
     uint32_t n = 0;
     DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
+    DevBuf rxof, rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // run-time regexp patterns
     std::vector<std::string> overlay;                 // batch strings not in the rule set's pool
     std::vector<std::string> overlay_bytes;           // batch byte strings (canonical)
     std::vector<TimeKey> overlay_times;
@@ -127,7 +130,14 @@ struct mxp_engine : public mxp::LowerTables {
     };
     std::vector<Rule> rules;
     bool have_rules = false;
-    bool need_ipof = false, need_tsof = false, need_strings = false, need_maps = false;
+    bool need_ipof = false, need_tsof = false, need_strings = false, need_maps = false, need_rxof = false;
+    // regexp DFAs of the rule set's constant patterns (device image rx_set; host copies for folding)
+    static constexpr uint32_t kRegexStates = 1u << 16;
+    std::map<std::string, std::pair<int32_t, std::string>> rx_ids;  // pattern -> (DFA | -1 | -2, error)
+    mxp::DfaSetHost rx_set;
+    std::vector<mxp::Dfa> rx_dfas;
+    std::set<uint32_t> rx_cols;  // columns holding run-time patterns
+    DevBuf d_rx_hdr, d_rx_trans, d_rx_ascii, d_rx_hilo, d_rx_hicls;
 
     DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
     DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rconst, d_idx, d_hents, d_postings;
@@ -202,6 +212,25 @@ struct mxp_engine : public mxp::LowerTables {
         auto it = vocab.find(attr);
         return it == vocab.end() ? -1 : it->second;
     }
+    int32_t regex_const(const std::string& pattern, std::string* err) override {
+        auto it = rx_ids.find(pattern);
+        if (it != rx_ids.end()) {
+            *err = it->second.second;
+            return it->second.first;
+        }
+        mxp::Dfa d;
+        std::string e;
+        const int rc = mxp::regex_compile({pattern}, kRegexStates, &d, &e);
+        int32_t id = rc == mxp::RX_OK ? (int32_t)rx_set.add(d) : rc == mxp::RX_SYNTAX ? -1 : -2;
+        if (id >= 0) rx_dfas.push_back(std::move(d));
+        rx_ids.emplace(pattern, std::make_pair(id, e));
+        *err = e;
+        return id;
+    }
+    bool regex_const_match(int32_t dfa, const std::string& subject) override {
+        return mxp::dfa_match_host(rx_dfas[(size_t)dfa], subject);
+    }
+    void regex_column(uint32_t col) override { rx_cols.insert(col); }
 
     int fail(int code, const std::string& msg) {
         last_error = msg;
@@ -228,7 +257,11 @@ struct mxp_engine : public mxp::LowerTables {
         vcol_ids.clear();
         rules.clear();
         have_rules = false;
-        need_ipof = need_tsof = need_strings = need_maps = false;
+        need_ipof = need_tsof = need_strings = need_maps = need_rxof = false;
+        rx_ids.clear();
+        rx_set = mxp::DfaSetHost();
+        rx_dfas.clear();
+        rx_cols.clear();
         empty_sid = intern_string("");
     }
 

@@ -5,7 +5,11 @@
 
 #include <hip/hip_runtime.h>
 
+#include "dfa_dev.h"
 #include "vm.h"
+
+#define MXP_RXOF_SYNTAX 0xFFFFFFFFu
+#define MXP_RXOF_UNSUPPORTED 0xFFFFFFFEu
 
 typedef struct mxp_kargs {
     // rule set (uploaded once per config snapshot)
@@ -48,6 +52,11 @@ typedef struct mxp_kargs {
     // per-string pre-tables (ip(), timestamp()); ~0 = conversion error
     const uint64_t* ipof;
     const uint64_t* tsof;
+    // regexp DFAs: constant patterns of the rule set; run-time patterns of the batch, reached through
+    // rxof[pattern string id] (DFA index in rx_batch, or MXP_RXOF_SYNTAX / MXP_RXOF_UNSUPPORTED)
+    mxp_dfa_set rx;
+    mxp_dfa_set rx_batch;
+    const uint32_t* rxof;
     // outputs
     uint32_t* out_match;         // [n_words][n]
     uint32_t* out_err;           // [n_words][n]

@@ -300,6 +300,26 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
         case VM_MOV:
             if (live) REG(d) = REG(a);
             break;
+        case VM_REGEX:
+            if (live) {
+                const StrRef sub = str_of(A, REG(a));
+                REG(d) = mxp_dfa_run(A.rx, x, sub.p, sub.n) ? 1u : 0u;
+            }
+            break;
+        case VM_REGEXD:
+            if (live) {
+                const uint64_t psid = REG(a);
+                const uint32_t dfa = A.rxof[psid];
+                if (dfa == MXP_RXOF_SYNTAX) {
+                    FAIL(ERR_REGEX, (uint32_t)psid);
+                } else if (dfa == MXP_RXOF_UNSUPPORTED) {
+                    FAIL(ERR_REGEX_UNSUPPORTED, (uint32_t)psid);
+                } else {
+                    const StrRef sub = str_of(A, REG(b));
+                    REG(d) = mxp_dfa_run(A.rx_batch, dfa, sub.p, sub.n) ? 1u : 0u;
+                }
+            }
+            break;
         default:
             break;
         }

@@ -19,11 +19,14 @@
 
 extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s);
 
+constexpr uint32_t kListRegexStates = 1u << 22;  // union DFA budget (4M states)
+
 struct mxp_list {
     int type = 0;
     uint64_t n_entries = 0;
     uint32_t hmask = 0;
     DevBuf htab, ent_desc, ent_pool, v4lo, v4hi, v6lo, v6hi;
+    DevBuf rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // REGEX: one DFA for the union
     uint32_t n4 = 0, n6 = 0;
 };
 
@@ -239,7 +242,32 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
         if ((rc = put(L->v6lo, lo6.data(), lo6.size() * 8, "upload v6lo"))) return rc;
         if ((rc = put(L->v6hi, hi6.data(), hi6.size() * 8, "upload v6hi"))) return rc;
     } else if (entry_type == MXP_LIST_REGEX) {
-        return eng->fail(MXP_ERR_STATE, "REGEX lists: not supported by this engine build yet");
+        // parseRegexList (regexList.go:44-65): every non-empty line, then every override, must
+        // compile (the first failure fails the list with regexp's error); checkList = any matches,
+        // i.e. one DFA for the union
+        std::vector<std::string> pats;
+        for (uint32_t i = 0; i < n_entries; i++)
+            if (entry_lens[i]) pats.push_back(str(entries[i], entry_lens[i]));
+        for (uint32_t i = 0; i < n_overrides; i++) pats.push_back(str(overrides[i], override_lens[i]));
+        for (const auto& p : pats) {  // per-pattern errors, in the reference's order
+            mxp::Dfa one;
+            std::string e;
+            const int prc = mxp::regex_compile({p}, 1u << 16, &one, &e);
+            if (prc == mxp::RX_SYNTAX) return eng->fail(MXP_ERR_ARG, e);
+            if (prc == mxp::RX_UNSUPPORTED) return eng->fail(MXP_ERR_ARG, "unsupported regexp (engine): " + e);
+        }
+        mxp::Dfa d;
+        std::string e;
+        const int prc = mxp::regex_compile(pats, kListRegexStates, &d, &e);
+        if (prc != mxp::RX_OK) return eng->fail(MXP_ERR_ARG, "regex list: " + e);
+        mxp::DfaSetHost set;
+        set.add(d);
+        L->n_entries = pats.size();
+        if ((rc = put(L->rx_hdr, set.hdr.data(), set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
+        if ((rc = put(L->rx_trans, set.trans.data(), set.trans.size() * 4, "upload rx trans"))) return rc;
+        if ((rc = put(L->rx_ascii, set.ascii.data(), set.ascii.size() * 2, "upload rx ascii"))) return rc;
+        if ((rc = put(L->rx_hilo, set.hilo.data(), set.hilo.size() * 4, "upload rx hilo"))) return rc;
+        if ((rc = put(L->rx_hicls, set.hicls.data(), set.hicls.size() * 2, "upload rx hicls"))) return rc;
     } else {
         return eng->fail(MXP_ERR_ARG, "unknown list entry type");
     }
@@ -275,6 +303,8 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, con
     A.v6hi = L->v6hi.as<uint64_t>();
     A.n4 = L->n4;
     A.n6 = L->n6;
+    A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
+                       L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes;
     hipError_t e = mxp_launch_list(&A, stream ? (hipStream_t)stream : eng->stream);
     return e == hipSuccess ? MXP_OK : eng->hipfail(e, "launch list check");

@@ -4,6 +4,7 @@
 
 #include <stdint.h>
 
+#include "dfa_dev.h"
 #include "netparse.h"
 
 // string hash table slot: hash32 << 32 | entry index; empty slot = ~0
@@ -24,6 +25,7 @@ typedef struct mxp_list_args {
     const uint64_t* v6lo;       // disjoint sorted IPv6 intervals, [2 i] high / [2 i + 1] low 64 bits
     const uint64_t* v6hi;
     uint32_t n4, n6;
+    mxp_dfa_set rx;             // REGEX lists: DFA 0 = the union of the list's patterns
     int32_t* codes;             // [n] google.rpc codes
 } mxp_list_args;
 

@@ -4,6 +4,8 @@
 //   string lists   hash the symbol 8 bytes at a time (ASCII upper-cased on the fly for the
 //                  case-insensitive kind, strings.ToUpper's ASCII path), probe the open-addressing
 //                  table, compare bytes on a hash hit (stringList.go:73-80);
+//   regex lists    one DFA for the union of the patterns (regexList.go:26-33: first match wins,
+//                  and only "found" is reported), stepped rune by rune (dfa_dev.h);
 //   IP lists       net.ParseIP on the symbol (netparse.h, the same code the host uses), then a
 //                  binary search of the disjoint interval set of the address family
 //                  (ipList.go:77-92; "is not a valid IP address" -> INVALID_ARGUMENT);
@@ -16,14 +18,7 @@
 
 namespace {
 
-// 8 bytes at any address of a blob with >= 16 bytes of slack (two aligned loads + funnel shift)
-__device__ __forceinline__ uint64_t ld8u(const uint8_t* p) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
-    const uint32_t sh = (uint32_t)(a & 7) * 8u;
-    const uint64_t lo = q[0];
-    return sh == 0 ? lo : (lo >> sh) | (q[1] << (64u - sh));
-}
+__device__ __forceinline__ uint64_t ld8u(const uint8_t* p) { return mxp_ld8(p); }
 
 __device__ __forceinline__ uint64_t tail_mask(uint32_t rem) {
     return rem >= 8 ? ~0ull : ((1ull << (rem * 8u)) - 1ull);
@@ -112,6 +107,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args 
             return;
         }
         found = ip_member(A, ip);
+    } else if (A.type == MXP_LIST_REGEX) {
+        found = mxp_dfa_run(A.rx, 0, s, n);  // regexList.checkList: any pattern matches
     } else {
         found = string_member(A, s, n, A.type == MXP_LIST_CASE_INSENSITIVE_STRINGS);
     }

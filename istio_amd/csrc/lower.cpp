@@ -97,6 +97,7 @@ class Lowerer {
         out.code = code_;
         out.nregs = maxregs_;
         out.uses_ipof = ipof_;
+        out.uses_rxof = rxof_;
         out.uses_tsof = tsof_;
         out.uses_strings = strings_;
         out.uses_maps = maps_;
@@ -494,7 +495,31 @@ class Lowerer {
         Slot b = pop(C_S);
         Slot a = pop(C_S);
         push(C_B);
-        if (fn == SF_REGEX) throw Irregular{"regexp matches() not yet lowered"};
+        if (fn == SF_REGEX) {  // externMatches(pattern = receiver, subject): regexp.MatchString
+            if (a.konst) {
+                std::string e;
+                const int32_t id = t_->regex_const(a.ktext, &e);
+                if (id == -2) throw Irregular{"regexp: " + e};
+                if (id < 0) {
+                    emit(VM_ERR, top(), 0, 0, 0, ERR_REGEX, (uint32_t)a.kval);
+                    return;
+                }
+                if (b.konst) {
+                    emit(VM_CONST, top(), 0, 0, 0, t_->regex_const_match(id, b.ktext) ? 1 : 0, 0);
+                    return;
+                }
+                strings_ = true;
+                emit(VM_REGEX, top(), top() + 1, 0, (uint32_t)id, 0, 0);
+                return;
+            }
+            // run-time pattern: only straight from a string attribute, whose values the packer compiles
+            if (a.attr.empty() || a.cls != C_S) throw Irregular{"regexp pattern computed at run time"};
+            t_->regex_column(t_->column(a.attr));
+            strings_ = true;
+            rxof_ = true;
+            emit(VM_REGEXD, top(), top(), top() + 1, 0, 0, 0);
+            return;
+        }
         if (a.konst && b.konst) {
             const std::string& s = a.ktext;
             const std::string& q = b.ktext;
@@ -574,7 +599,7 @@ class Lowerer {
     size_t ncontexts_ = 0;
     std::vector<mxp_vm_ins> code_;
     uint32_t maxregs_ = 0;
-    bool ipof_ = false, tsof_ = false, strings_ = false, maps_ = false;
+    bool ipof_ = false, tsof_ = false, strings_ = false, maps_ = false, rxof_ = false;
 };
 
 }  // namespace
@@ -584,7 +609,7 @@ LoweredRule lower_rule(const IlProgram& prog, LowerTables* tables) { return Lowe
 std::string vm_disasm(const std::vector<mxp_vm_ins>& code) {
     static const char* names[] = {"nop", "res", "tres", "vcol", "const", "eq", "eqk", "not", "jz", "jnz", "jmp",
                                   "ret", "lookup", "lookupk", "strfn", "strfnk", "ipof", "tsof", "ipeq", "tseq",
-                                  "err", "logic", "logick", "ftos", "stof", "jzret", "jnzret", "retk", "mov"};
+                                  "err", "logic", "logick", "ftos", "stof", "jzret", "jnzret", "retk", "mov", "regex", "regexd"};
     std::string o;
     char buf[160];
     for (size_t i = 0; i < code.size(); i++) {

@@ -29,6 +29,11 @@ class LowerTables {
     virtual uint32_t column(const std::string& attr) = 0;         // resolve column index
     virtual uint32_t vcolumn(const std::string& attr, const std::string& key) = 0;  // map[key] column
     virtual int32_t attr_type(const std::string& attr) = 0;       // manifest ValueType (-1 unknown)
+    // constant regexp pattern -> rule-set DFA index; -1 syntax error, -2 unsupported (err says why)
+    virtual int32_t regex_const(const std::string& pattern, std::string* err) = 0;
+    virtual bool regex_const_match(int32_t dfa, const std::string& subject) = 0;
+    // string column whose values are used as run-time regexp patterns (the packer compiles them)
+    virtual void regex_column(uint32_t col) = 0;
 };
 
 struct LoweredRule {
@@ -40,6 +45,7 @@ struct LoweredRule {
     bool uses_tsof = false;
     bool uses_strings = false;    // needs string bytes on device (dynamic string functions)
     bool uses_maps = false;       // needs per-request map storage on device
+    bool uses_rxof = false;       // run-time regexp patterns (per-batch pattern DFAs)
 };
 
 LoweredRule lower_rule(const IlProgram& prog, LowerTables* tables);

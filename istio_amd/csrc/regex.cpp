@@ -856,6 +856,22 @@ int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states,
     return RX_OK;
 }
 
+uint32_t DfaSetHost::add(const Dfa& d) {
+    mxp_dfa_hdr h{};
+    h.ncls = d.ncls;
+    h.start = d.start;
+    h.trans = (uint32_t)trans.size();
+    h.ascii = (uint32_t)ascii.size();
+    h.hi = (uint32_t)hilo.size();
+    h.hi_n = (uint32_t)d.hi_lo.size();
+    trans.insert(trans.end(), d.trans.begin(), d.trans.end());
+    ascii.insert(ascii.end(), d.ascii, d.ascii + 128);
+    hilo.insert(hilo.end(), d.hi_lo.begin(), d.hi_lo.end());
+    hicls.insert(hicls.end(), d.hi_cls.begin(), d.hi_cls.end());
+    hdr.push_back(h);
+    return (uint32_t)hdr.size() - 1;
+}
+
 bool dfa_match_host(const Dfa& d, const std::string& s) {
     uint32_t st = d.start;
     size_t i = 0;

@@ -51,3 +51,19 @@ int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states,
 bool dfa_match_host(const Dfa& d, const std::string& s);
 
 }  // namespace mxp
+
+#include "dfa_dev.h"
+
+namespace mxp {
+
+// Host image of a set of DFAs in the device layout of dfa_dev.h (upload each vector as is).
+struct DfaSetHost {
+    std::vector<mxp_dfa_hdr> hdr;
+    std::vector<uint32_t> trans;
+    std::vector<uint16_t> ascii;
+    std::vector<uint32_t> hilo;
+    std::vector<uint16_t> hicls;
+    uint32_t add(const Dfa& d);  // -> DFA index
+};
+
+}  // namespace mxp

@@ -45,6 +45,8 @@ enum mxp_vm_op {
     VM_JNZRET = 26,  // r[a] != 0 -> finish with bool result y
     VM_RETK = 27,    // finish with bool result y
     VM_MOV = 28,     // d <- r[a]                 (templates: hoisted CONST)
+    VM_REGEX = 29,   // d <- regexp.MatchString(<rule-set DFA x>, string r[a])
+    VM_REGEXD = 30,  // d <- regexp.MatchString(string r[a], string r[b]): pattern DFA from the batch's rxof table
 };
 
 // Leading-atom guard of a rule (vmopt.cpp): the rule's program starts with
@@ -164,10 +166,11 @@ enum mxp_err_code {
     ERR_IP = 6,          // "could not convert %s to IP_ADDRESS"        aux = string id
     ERR_TS = 7,          // "could not convert '%s' to TIMESTAMP..."    aux = string id
     ERR_MEMBER = 8,      // "member lookup failed: '%v'"               aux = key string id
-    ERR_REGEX = 9,       // regexp compile error                        aux = pattern string id
+    ERR_REGEX = 9,       // regexp compile error ("error parsing regexp: ...")   aux = pattern string id
     ERR_STATIC = 10,     // rule failed to compile: every evaluation errors   aux = rule
     ERR_UNSUPPORTED = 11,// construct not lowered by this engine build   aux = rule
     ERR_UNDERFLOW = 12,  // "stack underflow" (interpreterRun.go:1148) -- reachable from OR chains
+    ERR_REGEX_UNSUPPORTED = 13,  // batch pattern this engine cannot compile (Unicode classes / folding)   aux = pattern string id
     PANIC_MAPTYPE = 32,  // il.MapGet on a non-map value ("Unknown map type")
     PANIC_EXTARG = 33,   // reflect.Call with a wrong dynamic type (ip_equal / timestamp_equal)
     PANIC_NOTBOOL = 34,  // Result.AsBool on a non-bool result

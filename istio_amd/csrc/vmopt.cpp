@@ -22,11 +22,11 @@ static bool is_terminal(const mxp_vm_ins& i) {
 // registers read / written (bit masks)
 static uint32_t reads(const mxp_vm_ins& i) {
     switch (opof(i)) {
-    case VM_EQ: case VM_LOGIC: case VM_LOOKUP: case VM_STRFN: case VM_IPEQ: case VM_TSEQ:
+    case VM_EQ: case VM_LOGIC: case VM_LOOKUP: case VM_STRFN: case VM_IPEQ: case VM_TSEQ: case VM_REGEXD:
         return (1u << i.a) | (1u << i.b);
     case VM_EQK: case VM_NOT: case VM_LOGICK: case VM_JZ: case VM_JNZ: case VM_RET: case VM_LOOKUPK:
     case VM_STRFNK: case VM_IPOF: case VM_TSOF: case VM_FTOS: case VM_STOF: case VM_JZRET: case VM_JNZRET:
-    case VM_MOV:
+    case VM_MOV: case VM_REGEX:
         return 1u << i.a;
     default:
         return 0;
@@ -37,7 +37,7 @@ static uint32_t writes(const mxp_vm_ins& i) {
     switch (opof(i)) {
     case VM_RES: case VM_TRES: case VM_VCOL: case VM_CONST: case VM_EQ: case VM_EQK: case VM_NOT: case VM_LOGIC:
     case VM_LOGICK: case VM_LOOKUP: case VM_LOOKUPK: case VM_STRFN: case VM_STRFNK: case VM_IPOF: case VM_TSOF:
-    case VM_IPEQ: case VM_TSEQ: case VM_FTOS: case VM_STOF: case VM_MOV:
+    case VM_IPEQ: case VM_TSEQ: case VM_FTOS: case VM_STOF: case VM_MOV: case VM_REGEX: case VM_REGEXD:
         return 1u << i.d;
     default:
         return 0;
@@ -48,7 +48,7 @@ static uint32_t writes(const mxp_vm_ins& i) {
 static bool is_pure(const mxp_vm_ins& i) {
     switch (opof(i)) {
     case VM_CONST: case VM_EQ: case VM_EQK: case VM_NOT: case VM_LOGIC: case VM_LOGICK: case VM_STRFN:
-    case VM_STRFNK: case VM_STOF: case VM_NOP: case VM_MOV:
+    case VM_STRFNK: case VM_STOF: case VM_NOP: case VM_MOV: case VM_REGEX:
         return true;
     default:
         return false;
@@ -92,7 +92,7 @@ static int det_result(const std::vector<mxp_vm_ins>& c, size_t pc) {
             pc++;
             break;
         }
-        case VM_STRFN: case VM_STRFNK: case VM_STOF:
+        case VM_STRFN: case VM_STRFNK: case VM_STOF: case VM_REGEX:
             known[i.d] = false;
             pc++;
             break;

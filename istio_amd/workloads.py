@@ -173,9 +173,10 @@ def c2_workload(n_rules=1000, n_requests=65536, seed=2, n_services=256, p_missin
 
 
 # ----------------------------------------------------------------------------------- fuzzing
-_STR_VALS = ["", "a", "abc", "abcd", "foo", "bar", "st.*", "str1", "1.2.3.4", "10.0.0.1", "::1",
+_STR_VALS = ["", "a", "abc", "abcd", "foo", "bar", "st.*", "str1", "1.2.3.4", "10.0.0.1", "::1", "(x", "a+b",
              "2015-01-02T15:04:35Z", "2015-01-02T15:04:35+01:00", "*", "a*", "*c", "19ms", "x-user"]
 _KEYS = ["a", "b", "c", "foo", "x-user"]
+_REGEXES = ["^a", "b.*c", "^(abc|foo)$", "[0-9]+", "\\d\\.\\d", "(?i)ABC", "st.*", "^$", "x*", "\\bfoo\\b"]
 
 
 class _Fuzz:
@@ -227,6 +228,9 @@ class _Fuzz:
                                             'timestamp("nope")']))
         if r < 0.92:
             return "%s == %s" % (self.pick(["adur", "(adur | bdur)"]), self.pick(['"19ms"', "bdur", '"0"']))
+        if r < 0.96:
+            return self.pick(['"%s".matches(%s)' % (self.pick(_REGEXES), self.sexpr(d)), "as.matches(bs)",
+                              'bs.matches("abc")', '"(bad".matches(as)'])
         return self.pick(["true", "false", "TRUE", "ai == true", "as.foo()", "ai = 2", "x == 2", "ar == br"])
 
     def expr(self, d):
@@ -438,3 +442,72 @@ def c3_string_list(n_entries=100_000, n_lookups=1_000_000, seed=3, hit_rate=0.5)
             e = e.swapcase()
         syms.append(e)
     return entries, syms
+
+
+def c3_regex_list(n_patterns=10_000, n_lookups=1_000_000, seed=3, hit_rate=0.5):
+    """C3 regex list: patterns `^prefix[a-z0-9]{m,n}(suffix)?$`; lookups half built
+    to match a random pattern, half near misses.  Returns (patterns, symbols)."""
+    rng = np.random.default_rng(seed + 11)
+    letters = "abcdefghijklmnopqrstuvwxyz"
+    alnum = letters + "0123456789"
+
+    def word(lo, hi):
+        return "".join(letters[int(i)] for i in rng.integers(0, 26, size=int(rng.integers(lo, hi + 1))))
+    specs, pats = [], []
+    for _ in range(n_patterns):
+        pre, suf = word(3, 8), word(2, 5)
+        m = int(rng.integers(1, 4))
+        n = m + int(rng.integers(0, 6))
+        specs.append((pre, m, n, suf))
+        pats.append("^%s[a-z0-9]{%d,%d}(%s)?$" % (pre, m, n, suf))
+    syms = []
+    for _ in range(n_lookups):
+        pre, m, n, suf = specs[int(rng.integers(0, n_patterns))]
+        body = "".join(alnum[int(i)] for i in rng.integers(0, 36, size=int(rng.integers(m, n + 1))))
+        s = pre + body + (suf if rng.random() < 0.5 else "")
+        if rng.random() >= hit_rate:
+            s = s + ("-" if rng.random() < 0.5 else "X")  # outside the class / past the anchor
+        syms.append(s)
+    return pats, syms
+
+
+# ----------------------------------------------------------------------------------- C4 routes
+C4_MANIFEST = {"request.path": "STRING", "request.headers": "STRING_MAP", "destination.service": "STRING"}
+_C4_HEADERS = ["x-user", "x-env", "x-canary", "user-agent", "x-region"]
+
+
+def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512):
+    """C4: Pilot-shaped HTTP route rules in the Mixer language: 60%
+    request.path.startsWith("/p..") (Pilot prefix), 20% "^...".matches(request.path) (Pilot regex:
+    prefix -> ^QuoteMeta(p).*), 20% request.headers["h"] == "v" or "re".matches(request.headers["h"]).
+    Requests: paths of depth 1..6 over a `vocab`-word vocabulary, 3 headers each.
+    Returns (manifest, rules, BagBatch)."""
+    rng = np.random.default_rng(seed)
+    words = ["w%d" % i for i in range(vocab)]
+    vals = ["v%d" % i for i in range(16)]
+
+    def path(depth):
+        return "/" + "/".join(words[int(i)] for i in rng.integers(0, vocab, size=depth))
+    rules = []
+    for i in range(n_rules):
+        r = rng.random()
+        p = path(int(rng.integers(1, 4)))
+        if r < 0.6:
+            rules.append('request.path.startsWith("%s")' % p)
+        elif r < 0.8:
+            rx = "^" + p + ("(/.*)?$" if rng.random() < 0.5 else "[0-9a-z/]*")
+            rules.append('"%s".matches(request.path)' % rx)
+        elif r < 0.9:
+            rules.append('request.headers["%s"] == "%s"' % (_C4_HEADERS[int(rng.integers(0, 5))],
+                                                          vals[int(rng.integers(0, 16))]))
+        else:
+            rules.append('"^v(1|%d)[0-9]?$".matches(request.headers["%s"])' % (int(rng.integers(2, 9)),
+                                                                             _C4_HEADERS[int(rng.integers(0, 5))]))
+    bags = []
+    for _ in range(n_requests):
+        b = {"request.path": path(int(rng.integers(1, 7))),
+             "destination.service": "svc.default.svc.cluster.local",
+             "request.headers": {_C4_HEADERS[int(k)]: vals[int(rng.integers(0, 16))]
+                                 for k in rng.choice(5, size=3, replace=False)}}
+        bags.append(b)
+    return C4_MANIFEST, rules, BagBatch.from_bags(bags, names=list(C4_MANIFEST))

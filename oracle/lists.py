@@ -107,6 +107,28 @@ class IPList:
         return out
 
 
+class RegexList:
+    """parseRegexList (regexList.go:44-65): non-empty lines then overrides, each regexp.Compile'd
+    (the first error fails the list); checkList: any pattern matches (Go regexp restatement)."""
+
+    def __init__(self, lines, overrides=()):
+        import goregex
+        self.progs = []
+        for p in [x for x in lines if _b(x)] + list(overrides):
+            try:
+                self.progs.append(goregex.compile(_b(p)))
+            except goregex.RegexError as e:
+                raise ListParseError(str(e))
+
+    def num_entries(self):
+        return len(self.progs)
+
+    def found(self, symbols):
+        import goregex
+        return np.array([1 if any(goregex.match(p, _b(s)) for p in self.progs) else 0 for s in symbols],
+                        dtype=np.int8)
+
+
 def codes(found: np.ndarray, blacklist: bool) -> np.ndarray:
     """HandleListEntry's status code per symbol from found (1 / 0 / -1 = check error)."""
     if blacklist:

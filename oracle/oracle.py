@@ -53,6 +53,42 @@ class _Result(ctypes.Structure):
                 ("v2", ctypes.c_uint32), ("val", _Gv), ("msg", ctypes.c_char * 512)]
 
 
+# `matches`: the C interpreter calls back into the Go regexp restatement (goregex.py)
+_REGEX_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                             ctypes.c_void_p, ctypes.c_size_t)
+_RX_CACHE = {}
+
+
+def _regex_py(pat: bytes, subj: bytes):
+    import goregex
+    prog = _RX_CACHE.get(pat)
+    if prog is None:
+        try:
+            prog = goregex.compile(pat)
+        except goregex.RegexError as e:
+            prog = ("err", -1, str(e))
+        except goregex.Unsupported as e:
+            prog = ("err", -2, "unsupported regexp (oracle): %s" % e)
+        _RX_CACHE[pat] = prog
+    if isinstance(prog, tuple):
+        return prog[1], prog[2]
+    return (1 if goregex.match(prog, subj) else 0), ""
+
+
+def _regex_cb_impl(pat, npat, s, n, err, errcap):
+    try:
+        m, msg = _regex_py(ctypes.string_at(pat, npat) if npat else b"", ctypes.string_at(s, n) if n else b"")
+    except Exception as e:  # never unwind through C
+        m, msg = -2, "oracle regex failure: %r" % e
+    if m < 0 and errcap:
+        b = msg.encode("utf-8", "surrogateescape")[: errcap - 1] + b"\0"
+        ctypes.memmove(err, b, len(b))
+    return m
+
+
+_regex_cb = _REGEX_FN(_regex_cb_impl)
+
+
 def lib():
     global _LIB
     if _LIB is None:
@@ -69,6 +105,8 @@ def lib():
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
         L.oracle_result_size.restype = ctypes.c_size_t
         assert L.oracle_result_size() == ctypes.sizeof(_Result), "oracle_result layout mismatch"
+        L.oracle_set_regex_fn.argtypes = [_REGEX_FN]
+        L.oracle_set_regex_fn(_regex_cb)
         _LIB = L
     return _LIB
 

@@ -22,7 +22,7 @@ def eng(libmxp):
     return mxp.Engine(0)
 
 
-@pytest.mark.parametrize("spec", [s for s in CASES["lists"] if s["type"] != L.REGEX], ids=lambda s: s["name"])
+@pytest.mark.parametrize("spec", CASES["lists"], ids=lambda s: s["name"])
 def test_reference_list_table_on_gpu(eng, spec):
     from istio_amd.engine import MxpError
     if "parse_error" in spec:
@@ -59,3 +59,22 @@ def test_c3_string_list_parity(eng, kind):
     got = lst.check(syms)
     assert np.array_equal(got, want)
     assert (want == 0).sum() > 1000 and (want == 5).sum() > 1000
+
+
+def test_c3_regex_list_parity(eng):
+    pats, syms = W.c3_regex_list(n_patterns=200, n_lookups=1500, seed=33)
+    lst = eng.list_create(L.REGEX, pats[:150] + [""], pats[150:])
+    ref = L.RegexList(pats[:150] + [""], pats[150:])
+    assert lst.num_entries() == ref.num_entries() == 200
+    want = L.codes(ref.found(syms), False)
+    got = lst.check(syms)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(syms[i], int(got[i]), int(want[i])) for i in bad[:5]]
+    assert (want == 0).sum() > 300 and (want == 5).sum() > 300
+
+
+def test_regex_list_compile_error(eng):
+    from istio_amd.engine import MxpError
+    with pytest.raises(MxpError) as ei:
+        eng.list_create(L.REGEX, ["a+", "(b"], [])
+    assert str(ei.value).endswith("error parsing regexp: missing closing ): `(b`")

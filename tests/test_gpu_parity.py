@@ -58,7 +58,7 @@ def test_golden_table_on_gpu(mxp):
     from test_oracle_golden import same_value
     for conf in ("defaultAttrs", "exprEvalAttrs"):
         rows = [r for r in ROWS["rows"] if r.get("E") and r.get("conf", "defaultAttrs") == conf
-                and "CompileErr" not in r and "Externs" not in r and ".matches(" not in r["E"]]
+                and "CompileErr" not in r and "Externs" not in r]
         eng = mxp.Engine(0)
         eng.set_vocabulary(ROWS["manifests"][conf])
         st = eng.compile([r["E"] for r in rows])
@@ -108,6 +108,18 @@ def test_c2_parity_config_size(mxp):
     ev = oracle.OracleEvaluator(manifest)
     got, want = compare(eng, ev, rules, batch)
     assert (want == 1).sum() > 0 and (want == 2).sum() > 0
+
+
+def test_c4_routes_parity(mxp):
+    """BASELINE configs[3] family (Pilot-style routes: prefixes, regexes on the path and on headers),
+    300 rules x 2000 requests against the oracle (Go regexp restatement for `matches`)."""
+    manifest, rules, batch = W.c4_workload(n_rules=300, n_requests=2000, seed=4)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    ev = oracle.OracleEvaluator(manifest)
+    got, want = compare(eng, ev, rules, batch)
+    assert (want == 1).sum() > 500
 
 
 @pytest.mark.parametrize("seed", [7, 17])

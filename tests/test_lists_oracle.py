@@ -13,12 +13,14 @@ CASES = json.load(open(os.path.join(HERE, "golden", "list_cases.json")))
 
 
 def oracle_list(spec):
+    if spec["type"] == L.REGEX:
+        return L.RegexList(spec["entries"], spec["overrides"])
     if spec["type"] == L.IP_ADDRESSES:
         return L.IPList(spec["entries"], spec["overrides"])
     return L.StringList(spec["entries"], spec["overrides"], case_insensitive=spec["type"] == L.CASE_INSENSITIVE_STRINGS)
 
 
-@pytest.mark.parametrize("spec", [s for s in CASES["lists"] if s["type"] != L.REGEX], ids=lambda s: s["name"])
+@pytest.mark.parametrize("spec", CASES["lists"], ids=lambda s: s["name"])
 def test_reference_list_table(spec):
     if "parse_error" in spec:
         with pytest.raises(L.ListParseError) as ei:
@@ -41,3 +43,9 @@ def test_ip_semantics_edges():
 
 def test_to_upper_ascii():
     assert L.go_to_upper(b"AbC-z{") == b"ABC-Z{"
+
+
+def test_regex_list_errors():
+    with pytest.raises(L.ListParseError) as ei:
+        L.RegexList(["a+", "(b"], [])
+    assert str(ei.value) == "error parsing regexp: missing closing ): `(b`"

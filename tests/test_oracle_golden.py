@@ -16,7 +16,6 @@ from istio_amd.bags import BagBatch, from_tagged
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROWS = json.load(open(os.path.join(HERE, "golden", "ilt_tests.json")))
-REGEX_ROWS = {r["index"] for r in ROWS["rows"] if ".matches(" in r.get("E", "")}
 
 
 def fmap_for(row):
@@ -53,8 +52,6 @@ def test_golden_row(row):
         assert ilcompile.write_text(prog).strip() == row["IL"].strip()
     if "Externs" in row:
         return  # custom test-only extern (`reverse`), not part of the product surface
-    if row["index"] in REGEX_ROWS:
-        pytest.skip("regexp restatement not in the round-1 oracle")
     batch = BagBatch.from_bags([{k: from_tagged(v) for k, v in row.get("I", {}).items()}])
     st, v = ev.eval(row["E"], batch, 0)
     if "Err" in row:

@@ -33,8 +33,6 @@ def test_golden_compile(Engine):
                 mism.append((row["index"], e.rule_error(0)))
             continue
         if st != 0:
-            if ".matches(" in row["E"] and st == 5:
-                continue  # regexp lowering not in round 1
             mism.append((row["index"], st, e.rule_error(0)))
             continue
         if "IL" in row and e.rule_il_text(0).strip() != row["IL"].strip():
@@ -70,5 +68,5 @@ def test_matches_oracle_codegen(Engine, which):
             assert st[i] in (0, 5), (r, e.rule_error(i))
             assert e.rule_il_text(i) == text, r
     # every generated rule without a regexp lowers to the GPU bytecode
-    unsupported = [rules[i] for i in np.where(st == 5)[0] if ".matches(" not in rules[i]]
+    unsupported = [rules[i] for i in np.where(st == 5)[0]]
     assert not unsupported, unsupported[:3]
