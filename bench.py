@@ -34,10 +34,13 @@ def parse():
     p.add_argument("--cpu-sample-seconds", type=float, default=12.0)
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--workload", default="c2", choices=["c2", "c4", "c3-ip", "c3-str", "c3-regex"],
+                   help="c2 (default, the BASELINE metric); secondary measurements: c4 route rules, C3 lists")
+    p.add_argument("--list-entries", type=int, default=100_000)
     return p.parse_args()
 
 
-def cpu_baseline(manifest, rules, batch, seconds, threads):
+def cpu_baseline(manifest, rules, batch, seconds, threads, chunk=256):
     """The oracle (C restatement of the reference interpreter, oracle/il_interp.c) on host cores,
     time-bounded sample of the same workload.  Rules are precompiled (best case for the reference:
     expression cache >= R)."""
@@ -45,7 +48,6 @@ def cpu_baseline(manifest, rules, batch, seconds, threads):
     import oracle
     ev = oracle.OracleEvaluator(manifest)
     oracle.oracle_matrix(ev, rules, batch, 0, 1, threads=1)  # compile all rules (untimed)
-    chunk = 256
     done = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds and done + chunk <= batch.n:
@@ -71,6 +73,101 @@ def measured_traffic(rules, requests):
     return d.get("bytes_per_eval")
 
 
+def list_bench(args, rank, world, local):
+    """C3 (BASELINE configs[2]): 100k-entry CIDR / string / regex lists, 1M lookups per GPU resident
+    in HBM; one step = HandleListEntry for every lookup (mxp_list_check_device, one kernel)."""
+    import numpy as np
+    import torch
+    from istio_amd import dist as D
+    from istio_amd import workloads as W
+    from istio_amd.engine import Engine
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import lists as L
+    kind = args.workload
+    n_look = args.requests
+    if kind == "c3-ip":
+        entries, syms = W.c3_ip_list(n_entries=args.list_entries, n_lookups=n_look, seed=3 + 1000 * rank)
+        etype = L.IP_ADDRESSES
+    elif kind == "c3-str":
+        entries, syms = W.c3_string_list(n_entries=args.list_entries, n_lookups=n_look, seed=3 + 1000 * rank)
+        etype = L.CASE_INSENSITIVE_STRINGS
+    else:
+        entries, syms = W.c3_regex_list(n_patterns=min(args.list_entries, 10_000), n_lookups=n_look,
+                                        seed=3 + 1000 * rank)
+        etype = L.REGEX
+    eng = Engine(local)
+    t0 = time.perf_counter()
+    lst = eng.list_create(etype, entries)
+    t_compile = time.perf_counter() - t0
+    bs = [x.encode() for x in syms]
+    off = np.zeros(len(bs) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum([len(b) for b in bs])
+    blob = np.frombuffer(b"".join(bs) + bytes(16), dtype=np.uint8)
+    dev = torch.device("cuda", local)
+    d_blob = torch.from_numpy(blob.copy()).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64).copy()).to(dev)
+    d_codes = torch.empty(len(bs), dtype=torch.int32, device=dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+
+    def step(e0=None, e1=None):
+        if e0 is not None:
+            e0.record(stream)
+        lst.check_device(d_blob.data_ptr(), d_off.data_ptr(), len(bs), stream.cuda_stream, d_codes.data_ptr())
+        if e1 is not None:
+            e1.record(stream)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(*evs[k])
+    torch.cuda.synchronize()
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    n = len(bs)
+    alg = int(off[-1]) + 8 * (n + 1) + 4 * n  # symbol bytes + offsets read, one code written each
+    achieved = alg / (kernel_ms * 1e-3) / 1e9
+    out = {"metric": "list-adapter lookups/sec (%s, %d entries)" % (kind, lst.num_entries()),
+           "value": world * n * args.steps / elapsed, "unit": "lookups/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (seeded C3 %s list and lookups; symbols resident in HBM)" % kind[3:],
+           "config": {"workload": "C3 %s list, %d entries, %d lookups per GPU (configs[2])" % (kind[3:], len(entries), n),
+                      "entries": len(entries), "lookups_per_gpu": n, "parallelism": "lookup-sharded dp%d" % world},
+           "kernel_ms": kernel_ms, "list_compile_s": t_compile,
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "mxp_list_kernel",
+                        "alg_bytes_per_launch": alg}}
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        out["cpu_baseline"] = list_cpu_baseline(L, kind, entries, syms, args.cpu_sample_seconds, args.cpu_threads)
+    if rank == 0:
+        print(json.dumps(out))
+
+
+def list_cpu_baseline(L, kind, entries, syms, seconds, threads):
+    """The list restatement timed on host cores: the IP list is the reference's linear IPNet scan
+    (ipList.go:77-92, C + OpenMP); strings a hash set (Python); regexes the Go regexp restatement
+    (Python Pike VM, single thread -- far slower than Go's regexp)."""
+    if kind == "c3-ip":
+        ref, threads_used = L.IPList(entries), threads
+    elif kind == "c3-str":
+        ref, threads_used = L.StringList(entries, case_insensitive=True), 1
+    else:
+        ref, threads_used = L.RegexList(entries), 1
+    chunk, done = 64, 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds and done + chunk <= len(syms):
+        part = syms[done:done + chunk]
+        ref.found(part, threads=threads) if kind == "c3-ip" else ref.found(part)
+        done += chunk
+        chunk = min(chunk * 2, 1 << 16)
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "lookups/s", "cores": threads_used, "kind": "port",
+            "sample": "%d lookups (%.1fs) against all %d entries, oracle restatement" % (done, dt, len(entries))}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -88,9 +185,18 @@ def main():
     from istio_amd import workloads as W
     from istio_amd.engine import Engine
 
+    if args.workload.startswith("c3"):
+        return list_bench(args, rank, world, local)
     # requests shard per rank; the rule set is replicated
-    manifest, rules, batch = W.c2_workload(n_rules=args.rules, n_requests=args.requests, seed=2 + 1000 * rank)
-    rules = W.c2_rules(args.rules, seed=2)[0]
+    if args.workload == "c4":
+        manifest, rules, batch = W.c4_workload(n_rules=args.rules, n_requests=args.requests, seed=4 + 1000 * rank)
+        metric, workload = ("request x rule predicate evals/sec at 10k rules (C4 route rules)",
+                            "C4 Pilot-style route rules R=%d, %d requests per GPU (configs[3])")
+    else:
+        manifest, rules, batch = W.c2_workload(n_rules=args.rules, n_requests=args.requests, seed=2 + 1000 * rank)
+        rules = W.c2_rules(args.rules, seed=2)[0]
+        metric, workload = ("request x rule predicate evals/sec at 10k rules",
+                            "C2 rules scaled to R=%d, %d requests per GPU (configs[1] family, configs[4] shard)")
     eng = Engine(local)
     eng.set_vocabulary(manifest)
     st = eng.compile(rules)
@@ -153,14 +259,14 @@ def main():
 
     # algorithmic bytes of one evaluation: every referenced column read once per
     # request (kind u8 + value u64), the rule tables, and the two output bitmaps written
-    n_cols = 3
+    n_cols = eng.ruleset_info()["columns"]
     prog_bytes = 16 * sum(eng.rule_vm_text(i).count("\n") for i in range(R)) + 4 * (R + 1)
     alg_bytes = N * n_cols * 9 + prog_bytes + 2 * N * Wd * 4
     achieved = alg_bytes / (eval_ms * 1e-3) / 1e9
     traffic = measured_traffic(R, N)
 
     out = {
-        "metric": "request x rule predicate evals/sec at 10k rules",
+        "metric": metric,
         "value": value,
         "unit": "pairs/s",
         "n_gpus": world,
@@ -171,8 +277,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic (seeded C2 rule family; requests resident in HBM)",
-        "config": {"workload": "C2 rules scaled to R=%d, %d requests per GPU (configs[1] family, configs[4] shard)" % (R, N),
+        "data": "synthetic (seeded %s workload; requests resident in HBM)" % args.workload.upper(),
+        "config": {"workload": workload % (R, N),
                    "rules": R, "requests_per_gpu": N, "parallelism": "request-sharded dp%d" % world},
         "eval_ms": kernel_ms,
         "kernels_ms": {"mxp_guard_kernel+mxp_eval_kernel": k_eval, "mxp_index_kernel": k_index},
@@ -183,8 +289,13 @@ def main():
                      "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pair": alg_bytes / (N * R)},
     }
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        sample = W.c2_workload(n_rules=args.rules, n_requests=min(N, 1 << 16), seed=2)[2]
-        out["cpu_baseline"] = cpu_baseline(manifest, rules, sample, args.cpu_sample_seconds, args.cpu_threads)
+        if args.workload == "c4":
+            sample = W.c4_workload(n_rules=args.rules, n_requests=512, seed=4)[2]
+            out["cpu_baseline"] = cpu_baseline(manifest, rules, sample, args.cpu_sample_seconds, args.cpu_threads,
+                                               chunk=16)
+        else:
+            sample = W.c2_workload(n_rules=args.rules, n_requests=min(N, 1 << 18), seed=2)[2]
+            out["cpu_baseline"] = cpu_baseline(manifest, rules, sample, args.cpu_sample_seconds, args.cpu_threads)
     if rank == 0:
         print(json.dumps(out))
     db.free()

@@ -741,9 +741,10 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) 
 
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
     if (!eng || !out) return 0;
-    const uint32_t v[5] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed};
+    const uint32_t v[6] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed,
+                           (uint32_t)(eng->cols.size() + eng->vcols.size())};
     uint32_t k = 0;
-    for (; k < cap && k < 5; k++) out[k] = v[k];
+    for (; k < cap && k < 6; k++) out[k] = v[k];
     return k;
 }
 

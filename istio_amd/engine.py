@@ -180,9 +180,9 @@ class Engine:
 
     def ruleset_info(self) -> dict:
         """Kernel-side shape of the rule set (guards, continuation templates, column segments)."""
-        out = (ctypes.c_uint32 * 5)()
-        k = self.lib.mxp_ruleset_info(self.h, out, 5)
-        return dict(zip(("guarded", "templated", "templates", "segments", "indexed"), list(out)[:k]))
+        out = (ctypes.c_uint32 * 6)()
+        k = self.lib.mxp_ruleset_info(self.h, out, 6)
+        return dict(zip(("guarded", "templated", "templates", "segments", "indexed", "columns"), list(out)[:k]))
 
     # ------------------------------------------------------------------ evaluation
     def eval_batch(self, batch: BagBatch):
@@ -419,6 +419,11 @@ class ListHandle:
         self.eng._check(self.eng.lib.mxp_list_check(self.eng.h, self.h, int(blacklist), blob.ctypes.data,
                                                     off.ctypes.data, len(bs), codes.ctypes.data), "mxp_list_check")
         return codes
+
+    def check_device(self, d_sym: int, d_off: int, n: int, stream: int, d_codes: int, blacklist: bool = False):
+        """mxp_list_check_device: symbols (blob with >= 16 bytes of slack) and codes in device memory."""
+        self.eng._check(self.eng.lib.mxp_list_check_device(self.eng.h, self.h, int(blacklist), d_sym, d_off, n,
+                                                           stream, d_codes), "mxp_list_check_device")
 
     def __del__(self):
         try:
