@@ -34,7 +34,7 @@ def parse():
     p.add_argument("--cpu-sample-seconds", type=float, default=12.0)
     p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--workload", default="c2", choices=["c2", "c4", "c3-ip", "c3-str", "c3-regex"],
+    p.add_argument("--workload", default="c2", choices=["c2", "c4", "c3-ip", "c3-str", "c3-regex", "c5-quota"],
                    help="c2 (default, the BASELINE metric); secondary measurements: c4 route rules, C3 lists")
     p.add_argument("--list-entries", type=int, default=100_000)
     return p.parse_args()
@@ -146,6 +146,78 @@ def list_bench(args, rank, world, local):
         print(json.dumps(out))
 
 
+def quota_bench(args, rank, world, local):
+    """C5 memquota (BASELINE configs[4]): K = 1024 quota keys, 1M quota requests per GPU in arrival
+    order; a step = batched HandleQuota (sort by key + per-key replay) and, when N > 1, the RCCL
+    all-reduce of the per-key granted deltas."""
+    import numpy as np
+    import torch
+    from istio_amd import dist as D
+    from istio_amd import workloads as W
+    from istio_amd.engine import Engine
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import memquota as M
+    K = 1024
+    mx, vd, keys, amounts, be = W.quota_workload(n_keys=K, n_requests=args.requests, seed=5 + 1000 * rank)
+    eng = Engine(local)
+    q = eng.quota_create(mx, vd)
+    dev = torch.device("cuda", local)
+    dk = torch.from_numpy(keys.view(np.int32).copy()).to(dev)
+    da = torch.from_numpy(amounts.copy()).to(dev)
+    db = torch.from_numpy(be.copy()).to(dev)
+    dg = torch.empty(len(keys), dtype=torch.int64, device=dev)
+    delta = torch.zeros(K, dtype=torch.int64, device=dev)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    now = [1_500_000_000 * 10**9]
+
+    def step(e0=None, e1=None):
+        if e0 is not None:
+            e0.record(stream)
+        q.alloc_device(len(keys), dk.data_ptr(), da.data_ptr(), db.data_ptr(), now[0], stream.cuda_stream,
+                       dg.data_ptr(), delta.data_ptr())
+        if e1 is not None:
+            e1.record(stream)
+        D.reduce_counters(delta)  # RCCL over xGMI when N > 1: per-key quota deltas
+        now[0] += 10**8
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(*evs[k])
+    torch.cuda.synchronize()
+    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    n = len(keys)
+    alg = n * (4 + 8 + 1 + 8)  # key, amount, best effort read; granted written
+    achieved = alg / (kernel_ms * 1e-3) / 1e9
+    out = {"metric": "memquota HandleQuota requests/sec (%d keys)" % K, "value": world * n * args.steps / elapsed,
+           "unit": "requests/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "int64", "data": "synthetic (seeded C5 quota requests; resident in HBM)",
+           "config": {"workload": "C5 memquota, %d keys, %d requests per GPU (configs[4])" % (K, n), "keys": K,
+                      "requests_per_gpu": n, "parallelism": "request-sharded dp%d" % world},
+           "kernel_ms": kernel_ms,
+           "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                        "kernel": "hipcub radix sort + mxp_quota_kernel", "alg_bytes_per_launch": alg}}
+    if rank == 0 and not args.no_cpu_baseline and world == 1:
+        ref = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
+        t0 = time.perf_counter()
+        done = 0
+        while time.perf_counter() - t0 < args.cpu_sample_seconds and done < n:
+            for i in range(done, min(done + 4096, n)):
+                ref.handle(int(keys[i]), int(amounts[i]), bool(be[i]), 1_500_000_000 * 10**9)
+            done = min(done + 4096, n)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": done / dt, "unit": "requests/s", "cores": 1, "kind": "port",
+                               "sample": "%d requests (%.1fs), memquota restatement (Python, sequential)" % (done, dt)}
+    if rank == 0:
+        print(json.dumps(out))
+
+
 def list_cpu_baseline(L, kind, entries, syms, seconds, threads):
     """The list restatement timed on host cores: the IP list is the reference's linear IPNet scan
     (ipList.go:77-92, C + OpenMP); strings a hash set (Python); regexes the Go regexp restatement
@@ -187,6 +259,8 @@ def main():
 
     if args.workload.startswith("c3"):
         return list_bench(args, rank, world, local)
+    if args.workload == "c5-quota":
+        return quota_bench(args, rank, world, local)
     # requests shard per rank; the rule set is replicated
     if args.workload == "c4":
         manifest, rules, batch = W.c4_workload(n_rules=args.rules, n_requests=args.requests, seed=4 + 1000 * rank)

@@ -164,6 +164,31 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* list, int blacklist, 
                           const uint64_t* d_sym_offsets, uint32_t n, void* stream, int32_t* d_codes);
 
 /*
+ * memquota (mixer/adapter/memquota): batched HandleQuota with the reference's sequential semantics.
+ *
+ * mxp_quota_create: n_keys quota keys with their limit (config.Params_Quota MaxAmount /
+ * ValidDuration, or the matching override: limit(), memquota.go:88-105, is resolved by the caller,
+ * as is the key itself, makeKey(instance.Name, instance.Dimensions)).  ValidDuration 0 = a
+ * non-expiring cell, else a rolling window of ceil(ValidDuration / 1s) * 10 ticks (rollingWindow.go).
+ *
+ * mxp_quota_alloc: n requests in arrival order -- key id, QuotaArgs.QuotaAmount (> 0 alloc, < 0
+ * free, 0 nothing), QuotaArgs.BestEffort -- all at time now_ns (currentTick = now_ns / 100 ms).
+ * granted[i] = QuotaResult.Amount.  State persists across calls.  DeduplicationID handling
+ * (dedup.go handleDedup) stays with the caller.  mxp_quota_alloc_device takes device arrays and can
+ * accumulate per-key granted deltas (allocs - frees) into d_delta (i64[n_keys]) for the cross-GPU
+ * all-reduce.
+ */
+typedef struct mxp_quota mxp_quota;
+int mxp_quota_create(mxp_engine* eng, uint32_t n_keys, const int64_t* max_amount, const int64_t* valid_duration_ns,
+                     mxp_quota** out);
+void mxp_quota_destroy(mxp_engine* eng, mxp_quota* quota);
+int mxp_quota_alloc(mxp_engine* eng, mxp_quota* quota, uint32_t n, const uint32_t* key, const int64_t* amount,
+                    const uint8_t* best_effort, int64_t now_ns, int64_t* granted);
+int mxp_quota_alloc_device(mxp_engine* eng, mxp_quota* quota, uint32_t n, const uint32_t* d_key,
+                           const int64_t* d_amount, const uint8_t* d_best_effort, int64_t now_ns, void* stream,
+                           int64_t* d_granted, int64_t* d_delta);
+
+/*
  * Regex compiler check (host only; test and tooling hook): compiles `pattern` with the engine's Go
  * regexp restatement and DFA builder, then matches `subject` on the host DFA.  Returns 1 / 0 for
  * match / no match, -1 for a syntax error (err = Go's "error parsing regexp: ..." text), -2 when the

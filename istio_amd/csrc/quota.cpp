@@ -1,0 +1,144 @@
+// quota.cpp -- batched memquota host side (include/mxp.h; kernels in quota.hip).
+//
+// Reference: mixer/adapter/memquota/memquota.go (HandleQuota, alloc, free), rollingWindow.go,
+// dedup.go (ticksPerSecond = 10, currentTick = now.UnixNano() / nanosPerTick).  The caller resolves
+// each request's quota key (makeKey(instance.Name, instance.Dimensions)) to a dense key id and the
+// key's limit (limit(): the first override whose dimensions match, else the default), and keeps
+// DeduplicationID handling (handleDedup) -- the engine owns the per-key state and the arithmetic.
+#include <cstring>
+
+#include "engine_impl.h"
+#include "quota_args.h"
+
+extern "C" hipError_t mxp_quota_sort(void* tmp, size_t* tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
+                                     uint32_t* idx_in, uint32_t* idx_out, uint32_t n, int bits, hipStream_t s);
+extern "C" hipError_t mxp_launch_quota(const mxp_quota_args* a, const uint32_t* skeys, uint32_t* seg_start,
+                                       hipStream_t s);
+
+struct mxp_quota {
+    uint32_t n_keys = 0;
+    DevBuf max_amount, ticks, cells, avail, win_cur, win_tick, slot_off, slots;
+    DevBuf keys_sorted, idx_in, order, seg_start, tmp;
+    size_t cap = 0, tmp_bytes = 0;
+};
+
+extern "C" {
+
+int mxp_quota_create(mxp_engine* eng, uint32_t n_keys, const int64_t* max_amount, const int64_t* valid_duration_ns,
+                     mxp_quota** out) {
+    if (!eng || !out || (n_keys && (!max_amount || !valid_duration_ns))) return MXP_ERR_ARG;
+    if (eng->device < 0) return eng->fail(MXP_ERR_STATE, "host-only engine");
+    hipError_t e;
+    if ((e = hipSetDevice(eng->device)) != hipSuccess) return eng->hipfail(e, "hipSetDevice");
+    std::unique_ptr<mxp_quota> Q(new mxp_quota());
+    Q->n_keys = n_keys;
+    std::vector<uint32_t> ticks(n_keys);
+    std::vector<uint64_t> off(n_keys + 1, 0);
+    for (uint32_t k = 0; k < n_keys; k++) {
+        // newRollingWindow(limit, seconds * ticksPerSecond), seconds = ceil(ValidDuration / 1s)
+        const int64_t vd = valid_duration_ns[k];
+        ticks[k] = vd <= 0 ? 0u : (uint32_t)((vd + 999999999) / 1000000000) * 10u;
+        off[k + 1] = off[k] + ticks[k];
+    }
+    std::vector<int64_t> zero64(n_keys, 0), avail(max_amount, max_amount + n_keys);
+    std::vector<uint32_t> zero32(n_keys, 0);
+    auto put = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
+        if ((e = d.alloc(bytes ? bytes : 16)) != hipSuccess) return eng->hipfail(e, what);
+        if (bytes && (e = hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice)) != hipSuccess) return eng->hipfail(e, what);
+        return MXP_OK;
+    };
+    int rc;
+    if ((rc = put(Q->max_amount, max_amount, n_keys * 8, "quota max"))) return rc;
+    if ((rc = put(Q->ticks, ticks.data(), n_keys * 4, "quota ticks"))) return rc;
+    if ((rc = put(Q->cells, zero64.data(), n_keys * 8, "quota cells"))) return rc;
+    if ((rc = put(Q->avail, avail.data(), n_keys * 8, "quota avail"))) return rc;
+    if ((rc = put(Q->win_cur, zero32.data(), n_keys * 4, "quota cur"))) return rc;
+    if ((rc = put(Q->win_tick, zero64.data(), n_keys * 8, "quota tick"))) return rc;
+    if ((rc = put(Q->slot_off, off.data(), off.size() * 8, "quota slot_off"))) return rc;
+    if ((e = Q->slots.alloc(off[n_keys] * 8 + 16)) != hipSuccess) return eng->hipfail(e, "quota slots");
+    if ((e = hipMemset(Q->slots.p, 0, off[n_keys] * 8 + 16)) != hipSuccess) return eng->hipfail(e, "quota slots");
+    if ((e = Q->seg_start.alloc(((size_t)n_keys + 1) * 4)) != hipSuccess) return eng->hipfail(e, "quota seg");
+    *out = Q.release();
+    return MXP_OK;
+}
+
+void mxp_quota_destroy(mxp_engine* eng, mxp_quota* q) {
+    if (eng && eng->device >= 0) (void)hipSetDevice(eng->device);
+    delete q;
+}
+
+int mxp_quota_alloc_device(mxp_engine* eng, mxp_quota* Q, uint32_t n, const uint32_t* d_key, const int64_t* d_amount,
+                           const uint8_t* d_best_effort, int64_t now_ns, void* stream, int64_t* d_granted,
+                           int64_t* d_delta) {
+    if (!eng || !Q || (n && (!d_key || !d_amount || !d_best_effort || !d_granted))) return MXP_ERR_ARG;
+    if (!n || !Q->n_keys) return MXP_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    hipError_t e;
+    if (n > Q->cap) {
+        if ((e = Q->keys_sorted.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota keys");
+        if ((e = Q->idx_in.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota idx");
+        if ((e = Q->order.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota order");
+        size_t need = 0;
+        if ((e = mxp_quota_sort(nullptr, &need, nullptr, nullptr, nullptr, nullptr, n, 32, s)) != hipSuccess)
+            return eng->hipfail(e, "quota sort size");
+        if ((e = Q->tmp.alloc(need)) != hipSuccess) return eng->hipfail(e, "quota sort tmp");
+        Q->tmp_bytes = need;
+        Q->cap = n;
+    }
+    int bits = 1;
+    while (bits < 32 && (1ull << bits) < Q->n_keys) bits++;
+    size_t tb = Q->tmp_bytes;
+    if ((e = mxp_quota_sort(Q->tmp.p, &tb, d_key, Q->keys_sorted.as<uint32_t>(), Q->idx_in.as<uint32_t>(),
+                            Q->order.as<uint32_t>(), n, bits, s)) != hipSuccess)
+        return eng->hipfail(e, "quota sort");
+    mxp_quota_args A;
+    memset(&A, 0, sizeof A);
+    A.n = n;
+    A.n_keys = Q->n_keys;
+    A.tick = now_ns / 100000000;  // nanosPerTick = 1e9 / ticksPerSecond
+    A.key = d_key;
+    A.amount = d_amount;
+    A.best_effort = d_best_effort;
+    A.order = Q->order.as<uint32_t>();
+    A.seg_start = Q->seg_start.as<uint32_t>();
+    A.granted = d_granted;
+    A.delta = d_delta;
+    A.max_amount = Q->max_amount.as<int64_t>();
+    A.ticks = Q->ticks.as<uint32_t>();
+    A.cells = Q->cells.as<int64_t>();
+    A.avail = Q->avail.as<int64_t>();
+    A.win_cur = Q->win_cur.as<uint32_t>();
+    A.win_tick = Q->win_tick.as<int64_t>();
+    A.slot_off = Q->slot_off.as<uint64_t>();
+    A.slots = Q->slots.as<int64_t>();
+    if ((e = mxp_launch_quota(&A, Q->keys_sorted.as<uint32_t>(), Q->seg_start.as<uint32_t>(), s)) != hipSuccess)
+        return eng->hipfail(e, "launch quota");
+    return MXP_OK;
+}
+
+int mxp_quota_alloc(mxp_engine* eng, mxp_quota* Q, uint32_t n, const uint32_t* key, const int64_t* amount,
+                    const uint8_t* best_effort, int64_t now_ns, int64_t* granted) {
+    if (!eng || !Q || (n && (!key || !amount || !best_effort || !granted))) return MXP_ERR_ARG;
+    if (!n) return MXP_OK;
+    for (uint32_t i = 0; i < n; i++)
+        if (key[i] >= Q->n_keys) return eng->fail(MXP_ERR_ARG, "quota key id out of range");
+    hipError_t e;
+    if ((e = hipSetDevice(eng->device)) != hipSuccess) return eng->hipfail(e, "hipSetDevice");
+    DevBuf dk, da, db, dg;
+    if ((e = dk.alloc((size_t)n * 4)) != hipSuccess || (e = da.alloc((size_t)n * 8)) != hipSuccess ||
+        (e = db.alloc(n)) != hipSuccess || (e = dg.alloc((size_t)n * 8)) != hipSuccess)
+        return eng->hipfail(e, "quota buffers");
+    if ((e = hipMemcpyAsync(dk.p, key, (size_t)n * 4, hipMemcpyHostToDevice, eng->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(da.p, amount, (size_t)n * 8, hipMemcpyHostToDevice, eng->stream)) != hipSuccess ||
+        (e = hipMemcpyAsync(db.p, best_effort, n, hipMemcpyHostToDevice, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "quota upload");
+    int rc = mxp_quota_alloc_device(eng, Q, n, dk.as<uint32_t>(), da.as<int64_t>(), db.as<uint8_t>(), now_ns,
+                                    eng->stream, dg.as<int64_t>(), nullptr);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(granted, dg.p, (size_t)n * 8, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "quota download");
+    if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "quota sync");
+    return MXP_OK;
+}
+
+}  // extern "C"

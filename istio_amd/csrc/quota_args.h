@@ -1,0 +1,27 @@
+// quota_args.h -- argument block of the batched memquota kernel (quota.hip / quota.cpp).
+#pragma once
+
+#include <stdint.h>
+
+typedef struct mxp_quota_args {
+    uint32_t n;                  // requests
+    uint32_t n_keys;
+    int64_t tick;                // currentTick of the batch (now / 100 ms)
+    // requests
+    const uint32_t* key;
+    const int64_t* amount;       // QuotaArgs.QuotaAmount (> 0 alloc, < 0 free)
+    const uint8_t* best_effort;
+    const uint32_t* order;       // arrival indices sorted by key (stable)
+    const uint32_t* seg_start;   // [n_keys + 1] key k's requests: order[seg_start[k] .. seg_start[k+1])
+    int64_t* granted;            // QuotaResult.Amount per request
+    int64_t* delta;              // optional [n_keys] += granted allocs - frees
+    // per-key state (HBM, persistent across batches)
+    const int64_t* max_amount;
+    const uint32_t* ticks;       // window length in ticks; 0 = non-expiring cell
+    int64_t* cells;              // in-use amount of non-expiring cells
+    int64_t* avail;              // rolling windows: available units
+    uint32_t* win_cur;           // current slot
+    int64_t* win_tick;           // tick of the current slot
+    const uint64_t* slot_off;    // first slot of each window
+    int64_t* slots;
+} mxp_quota_args;

@@ -66,6 +66,13 @@ SIGNATURES = {
                                              ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]),
     "mxp_regex_match_host": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
                                             ctypes.c_char_p, ctypes.c_uint32]),
+    "mxp_quota_create": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(_VP)]),
+    "mxp_quota_destroy": (None, [_VP, _VP]),
+    "mxp_quota_alloc": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_int64, ctypes.c_void_p]),
+    "mxp_quota_alloc_device": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p]),
     "mxp_set_timing": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
@@ -271,6 +278,15 @@ class Engine:
                                              ctypes.byref(h)), "mxp_list_create")
         return ListHandle(self, h)
 
+    # ------------------------------------------------------------------ memquota
+    def quota_create(self, max_amount, valid_duration_ns) -> "QuotaHandle":
+        mx = np.ascontiguousarray(max_amount, dtype=np.int64)
+        vd = np.ascontiguousarray(valid_duration_ns, dtype=np.int64)
+        h = _VP()
+        self._check(self.lib.mxp_quota_create(self.h, len(mx), mx.ctypes.data, vd.ctypes.data, ctypes.byref(h)),
+                    "mxp_quota_create")
+        return QuotaHandle(self, h)
+
     def error_count(self) -> int:
         return int(self.lib.mxp_error_count(self.h))
 
@@ -443,3 +459,32 @@ def regex_match_host(pattern, subject):
     buf = ctypes.create_string_buffer(1024)
     rc = lib.mxp_regex_match_host(p, len(p), s, len(s), buf, 1024)
     return rc, buf.value.decode("utf-8", "surrogateescape")
+
+
+class QuotaHandle:
+    """Batched memquota state (mxp_quota): HandleQuota for requests in arrival order."""
+
+    def __init__(self, eng: Engine, h):
+        self.eng, self.h = eng, h
+
+    def alloc(self, keys, amounts, best_effort, now_ns: int) -> np.ndarray:
+        k = np.ascontiguousarray(keys, dtype=np.uint32)
+        a = np.ascontiguousarray(amounts, dtype=np.int64)
+        b = np.ascontiguousarray(best_effort, dtype=np.uint8)
+        out = np.zeros(len(k), dtype=np.int64)
+        self.eng._check(self.eng.lib.mxp_quota_alloc(self.eng.h, self.h, len(k), k.ctypes.data, a.ctypes.data,
+                                                     b.ctypes.data, int(now_ns), out.ctypes.data), "mxp_quota_alloc")
+        return out
+
+    def alloc_device(self, n, d_keys, d_amounts, d_be, now_ns, stream, d_granted, d_delta=None):
+        self.eng._check(self.eng.lib.mxp_quota_alloc_device(self.eng.h, self.h, n, d_keys, d_amounts, d_be,
+                                                            int(now_ns), stream, d_granted, d_delta or None),
+                        "mxp_quota_alloc_device")
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.eng.lib.mxp_quota_destroy(self.eng.h, self.h)
+                self.h = None
+        except Exception:
+            pass

@@ -511,3 +511,21 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512):
                                  for k in rng.choice(5, size=3, replace=False)}}
         bags.append(b)
     return C4_MANIFEST, rules, BagBatch.from_bags(bags, names=list(C4_MANIFEST))
+
+
+# ----------------------------------------------------------------------------------- memquota (C5)
+def quota_workload(n_keys=1024, n_requests=1_000_000, seed=5, p_free=0.1, p_zero=0.02, p_be=0.5):
+    """C5 memquota deltas: K quota keys (a third non-expiring cells, the rest 1 s / 60 s rolling
+    windows) with limits 50..5000, requests in arrival order (Zipf keys, amounts 1..20, some frees
+    and zero amounts, best effort half the time).  Returns (max_amount, valid_ns, keys, amounts, be)."""
+    rng = np.random.default_rng(seed)
+    max_amount = rng.integers(50, 5001, size=n_keys).astype(np.int64)
+    valid = np.choose(rng.integers(0, 3, size=n_keys), [0, 10**9, 60 * 10**9]).astype(np.int64)
+    p = np.arange(1, n_keys + 1, dtype=np.float64) ** -1.05
+    keys = rng.choice(n_keys, size=n_requests, p=p / p.sum()).astype(np.uint32)
+    amounts = rng.integers(1, 21, size=n_requests).astype(np.int64)
+    r = rng.random(n_requests)
+    amounts = np.where(r < p_free, -amounts, amounts)
+    amounts = np.where(r > 1 - p_zero, 0, amounts)
+    be = (rng.random(n_requests) < p_be).astype(np.uint8)
+    return max_amount, valid, keys, amounts, be
