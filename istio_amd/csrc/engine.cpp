@@ -70,6 +70,33 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     n_guarded = 0;
     for (auto& g : guards) n_guarded += (g.mode & 0xFF) != GM_NONE;
 
+    // regexp rules `"^lit...".matches(col)` (program RES|VCOL x; REGEX y <- x; RET y): a subject can
+    // only match when it starts with the pattern's literal prefix -- a necessary-condition guard
+    // (GM_AND, continuation = the whole program) that the prefix index can serve
+    {
+        std::vector<std::string> pattern_of(rx_set.hdr.size());
+        for (auto& kv : rx_ids)
+            if (kv.second.first >= 0) pattern_of[kv.second.first] = kv.first;
+        for (uint32_t i = 0; i < n; i++) {
+            if ((guards[i].mode & 0xFF) != GM_NONE || off[i + 1] - off[i] != 3) continue;
+            const mxp_vm_ins& r = all[off[i]];
+            const mxp_vm_ins& x = all[off[i] + 1];
+            const mxp_vm_ins& t = all[off[i] + 2];
+            const uint32_t rop = r.op & 0x7F;
+            const bool col_ok = (rop == VM_RES && r.y == W_S) || rop == VM_VCOL;
+            if (!col_ok || (x.op & 0x7F) != VM_REGEX || x.a != r.d || (t.op & 0x7F) != VM_RET || t.a != x.d ||
+                t.y != 1 || ((x.op | t.op) & MXP_VM_WAKE))
+                continue;
+            std::string prefix;
+            if (!mxp::regex_required_prefix(pattern_of[x.x], &prefix)) continue;
+            mxp_guard g{};
+            g.col = r.x | ((rop == VM_VCOL ? (uint32_t)GK_VCOL : (uint32_t)W_S) << 24);
+            g.mode = GM_AND | GT_PREFIX;  // continuation pc 0: the whole program
+            g.klo = intern_string(prefix);
+            guards[i] = g;
+        }
+    }
+
     // continuation templates (vmopt.h hoist_continuation): rules whose continuations are identical
     // up to constants share one program; template code is appended after the rules' programs
     std::map<std::string, uint32_t> tmpl_ids;
@@ -111,44 +138,73 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     n_tmpls = (uint32_t)tmpls.size();
     all.insert(all.end(), tcode.begin(), tcode.end());
 
-    // guard index: GM_AND, non-negated, templated rules -- their continuing pairs are the requests
-    // whose guard column equals K; per (column, want class) a hash table K -> postings
+    // guard index.  Equality: GM_AND, non-negated, templated rules -- their continuing pairs are the
+    // requests whose column value equals K.  Prefix: `col.startsWith(K)` alone (GM_ONLY: a posting IS
+    // a true pair) or followed by `&& ...` (GM_AND, templated), and the regexp prefix guards above.
+    // Per (column, want class, kind) a hash table K -> postings.  A prefix guard the index cannot
+    // serve falls back to a guard-less rule (phase 1 only compares equality atoms).
     std::vector<uint8_t> indexed(n, 0);
-    std::map<uint32_t, std::map<uint64_t, std::vector<uint32_t>>> index_of;  // col|kind<<24 -> K -> rules
+    std::map<std::pair<uint32_t, bool>, std::map<uint64_t, std::vector<uint32_t>>> index_of;
     n_indexed = 0;
-    if (!(debug_flags & 8u)) {
-        for (uint32_t i = 0; i < n; i++) {
-            const mxp_guard& gd = guards[i];
-            if ((gd.mode & 0xFF) != GM_AND || ((gd.mode >> 8) & 1) || rule_tmpl[i] == MXP_VM_DONE) continue;
-            indexed[i] = 1;
-            index_of[gd.col][(uint64_t)gd.klo | ((uint64_t)gd.khi << 32)].push_back(i);
-            n_indexed++;
+    for (uint32_t i = 0; i < n; i++) {
+        mxp_guard& gd = guards[i];
+        const uint32_t mode = gd.mode & 0xFF;
+        const bool prefix = (gd.mode & GT_PREFIX) != 0, neg = (gd.mode >> 8) & 1;
+        bool ok = !(debug_flags & 8u) && !neg &&
+                  ((mode == GM_AND && rule_tmpl[i] != MXP_VM_DONE) || (prefix && mode == GM_ONLY));
+        if (!ok) {
+            if (prefix) {
+                gd = mxp_guard{0, GM_NONE, 0, 0};
+                rule_tmpl[i] = MXP_VM_DONE;
+            }
+            continue;
         }
+        if (prefix && mode == GM_ONLY) rule_tmpl[i] = MXP_TMPL_DIRECT;
+        indexed[i] = 1;
+        index_of[{gd.col, prefix}][(uint64_t)gd.klo | ((uint64_t)gd.khi << 32)].push_back(i);
+        n_indexed++;
     }
     std::vector<mxp_index> idx;
     std::vector<mxp_hent> hents;
-    std::vector<uint32_t> postings;
+    std::vector<uint32_t> postings, plens;
     for (auto& ci : index_of) {
+        const bool prefix = ci.first.second;
         mxp_index x{};
-        x.col = ci.first & 0xFFFFFFu;
-        x.okset = okset_of(ci.first >> 24);
+        x.col = ci.first.first & 0xFFFFFFu;
+        x.okset = okset_of(ci.first.first >> 24);
+        x.prefix = prefix ? 1u : 0u;
         uint32_t cap = 1;
         while (cap < 2 * ci.second.size()) cap <<= 1;
         x.hmask = cap - 1;
         x.hoff = (uint32_t)hents.size();
         hents.resize(hents.size() + cap, mxp_hent{0, 0, 0, 0});
+        std::set<uint32_t> lens;
         for (auto& kv : ci.second) {
             std::vector<uint32_t> rs = kv.second;
             std::stable_sort(rs.begin(), rs.end(), [&](uint32_t a, uint32_t b) { return rule_tmpl[a] < rule_tmpl[b]; });
-            uint32_t h = mxp_hash64(kv.first) & x.hmask;
+            uint64_t hh;
+            uint32_t tag;
+            if (prefix) {  // hash of the key bytes, as the kernel hashes the request's leading bytes
+                const std::string& key = gstrs[(uint32_t)kv.first];
+                lens.insert((uint32_t)key.size());
+                hh = mxp_str_hash((const uint8_t*)key.data(), key.size());
+                tag = (uint32_t)(hh >> 32);
+            } else {
+                hh = mxp_hash64(kv.first);
+                tag = (uint32_t)(kv.first >> 32);
+            }
+            uint32_t h = (uint32_t)hh & x.hmask;
             while (hents[x.hoff + h].len) h = (h + 1) & x.hmask;
             mxp_hent& E = hents[x.hoff + h];
             E.klo = (uint32_t)kv.first;
-            E.khi = (uint32_t)(kv.first >> 32);
+            E.khi = tag;
             E.start = (uint32_t)postings.size();
             E.len = (uint32_t)rs.size();
             postings.insert(postings.end(), rs.begin(), rs.end());
         }
+        x.plen0 = (uint32_t)plens.size();
+        x.nplen = (uint32_t)lens.size();
+        plens.insert(plens.end(), lens.begin(), lens.end());
         idx.push_back(x);
     }
     n_idx = (uint32_t)idx.size();
@@ -232,6 +288,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_idx, idx.data(), idx.size() * sizeof(mxp_index), "upload idx"))) return rc;
     if ((rc = put(d_hents, hents.data(), hents.size() * sizeof(mxp_hent), "upload hents"))) return rc;
     if ((rc = put(d_postings, postings.data(), postings.size() * 4, "upload postings"))) return rc;
+    if ((rc = put(d_plens, plens.data(), plens.size() * 4, "upload plens"))) return rc;
     if ((rc = put(d_tmpls, tmpls.data(), tmpls.size() * sizeof(mxp_tmpl), "upload tmpls"))) return rc;
     if ((rc = put(d_rule_tmpl, rule_tmpl.data(), rule_tmpl.size() * 4, "upload rule_tmpl"))) return rc;
     if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
@@ -480,6 +537,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->idx = d_idx.as<mxp_index>();
     A->hents = d_hents.as<mxp_hent>();
     A->postings = d_postings.as<uint32_t>();
+    A->plens = d_plens.as<uint32_t>();
     A->n_idx = n_idx;
     A->tmpls = d_tmpls.as<mxp_tmpl>();
     A->rule_tmpl = d_rule_tmpl.as<uint32_t>();

@@ -140,7 +140,7 @@ struct mxp_engine : public mxp::LowerTables {
     DevBuf d_rx_hdr, d_rx_trans, d_rx_ascii, d_rx_hilo, d_rx_hicls;
 
     DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
-    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rconst, d_idx, d_hents, d_postings;
+    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rconst, d_idx, d_hents, d_postings, d_plens;
     DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
     uint32_t n_glean = 0, n_gvm = 0;
     uint32_t n_idx = 0, n_indexed = 0;

@@ -28,6 +28,7 @@ typedef struct mxp_kargs {
     const mxp_index* idx;        // guard indexes (mxp_index_kernel)
     const mxp_hent* hents;
     const uint32_t* postings;
+    const uint32_t* plens;       // prefix indexes: distinct key lengths
     uint32_t n_idx;
     uint32_t pad2;
     uint32_t n_rules;

@@ -301,22 +301,29 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
             if (live) REG(d) = REG(a);
             break;
         case VM_REGEX:
-            if (live) {
-                const StrRef sub = str_of(A, REG(a));
-                REG(d) = mxp_dfa_run(A.rx, x, sub.p, sub.n) ? 1u : 0u;
-            }
-            break;
+        case VM_REGEXR:
         case VM_REGEXD:
             if (live) {
-                const uint64_t psid = REG(a);
-                const uint32_t dfa = A.rxof[psid];
-                if (dfa == MXP_RXOF_SYNTAX) {
-                    FAIL(ERR_REGEX, (uint32_t)psid);
-                } else if (dfa == MXP_RXOF_UNSUPPORTED) {
-                    FAIL(ERR_REGEX_UNSUPPORTED, (uint32_t)psid);
-                } else {
-                    const StrRef sub = str_of(A, REG(b));
-                    REG(d) = mxp_dfa_run(A.rx_batch, dfa, sub.p, sub.n) ? 1u : 0u;
+                // one stepping loop for the three forms (a single inlined copy of the DFA walk)
+                const mxp_dfa_set* S = &A.rx;
+                uint32_t dfa = x;
+                uint64_t subj = REG(a);
+                bool run = true;
+                if (op == VM_REGEXR) {
+                    dfa = (uint32_t)REG(b);
+                } else if (op == VM_REGEXD) {
+                    const uint64_t psid = REG(a);
+                    dfa = A.rxof[psid];
+                    subj = REG(b);
+                    S = &A.rx_batch;
+                    if (dfa == MXP_RXOF_SYNTAX || dfa == MXP_RXOF_UNSUPPORTED) {
+                        FAIL(dfa == MXP_RXOF_SYNTAX ? ERR_REGEX : ERR_REGEX_UNSUPPORTED, (uint32_t)psid);
+                        run = false;
+                    }
+                }
+                if (run) {
+                    const StrRef sub = str_of(A, subj);
+                    REG(d) = mxp_dfa_run(*S, dfa, sub.p, sub.n) ? 1u : 0u;
                 }
             }
             break;
@@ -520,6 +527,52 @@ extern "C" __global__ __launch_bounds__(256) void mxp_guard_kernel(mxp_kargs A) 
 // run it together (each lane's rule constants preloaded into its registers).  mxp_eval_kernel has
 // already written both bitmaps for these rules (match 0, error on a failed guard type check); true
 // and error results are OR-ed in.
+namespace {
+
+// One posting list per lane (lanes may hold different lists, or none: len 0), walked in lockstep.
+// Direct postings (MXP_TMPL_DIRECT) are true pairs; the others run their template, lanes sharing a
+// template together, each with its own rule's constants preloaded.  Results are OR-ed into the
+// bitmaps.
+__device__ void run_postings(const mxp_kargs& A, uint32_t start, uint32_t len, uint32_t req, uint64_t (*regs)[256],
+                             uint32_t tid) {
+    const uint64_t N = A.n;
+    for (uint32_t j = 0; __ballot(j < len); j++) {
+        bool pending = j < len;
+        const uint32_t rule = pending ? A.postings[start + j] : 0u;
+        const uint32_t t = pending ? A.rule_tmpl[rule] : MXP_VM_DONE;
+        if (pending && t == MXP_TMPL_DIRECT) {
+            if (A.out_match) atomicOr(A.out_match + (uint64_t)(rule >> 5) * N + req, 1u << (rule & 31u));
+            pending = false;
+        }
+        for (uint64_t bal = __ballot(pending); bal; bal = __ballot(pending)) {
+            const uint32_t tt = __builtin_amdgcn_readlane(t, (uint32_t)__builtin_ctzll(bal));
+            const bool mine = pending && t == tt;
+            const mxp_tmpl* T = A.tmpls + tt;
+            const uint32_t off = uni(T->off), pc0 = uni(T->pc0), len_t = uni(T->len), nconst = uni(T->nconst),
+                           creg0 = uni(T->creg0);
+            if (mine)
+                for (uint32_t c = 0; c < nconst; c++) regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
+            cuint32* P = ((cuint32*)A.prog) + ((uint64_t)off - pc0) * 4u;
+            const uint32_t code = run_rule(A, P, len_t, pc0, mine, rule, req, regs, tid);
+            if (mine) {
+                const uint64_t w = (uint64_t)(rule >> 5) * N + req;
+                const uint32_t bit = 1u << (rule & 31u);
+                if (code == PC_TRUE && A.out_match) atomicOr(A.out_match + w, bit);
+                if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
+            }
+            pending = pending && !mine;
+        }
+    }
+}
+
+}  // namespace
+
+// Guard-index phase: the pairs of indexed rules, found per request by hash lookups of its column
+// value (equality indexes) or of its leading bytes at every key length the index holds (prefix
+// indexes: `startsWith` atoms and anchored regexp literals) instead of by testing every rule.
+// Workgroup = 4 wavefronts, one tile of 64 requests each (one request per lane).  mxp_eval_kernel
+// has already written both bitmaps for these rules (match 0, error on a failed type check of the
+// guard column); true and error results are OR-ed in.
 extern "C" __global__ __launch_bounds__(256) void mxp_index_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     const uint32_t tid = threadIdx.x;
@@ -529,47 +582,58 @@ extern "C" __global__ __launch_bounds__(256) void mxp_index_kernel(mxp_kargs A) 
     const uint64_t N = A.n;
     for (uint32_t x = 0; x < A.n_idx; x++) {
         const uint32_t col = uni(A.idx[x].col), okset = uni(A.idx[x].okset), hmask = uni(A.idx[x].hmask),
-                       hoff = uni(A.idx[x].hoff);
-        uint32_t start = 0, len = 0;
+                       hoff = uni(A.idx[x].hoff), prefix = uni(A.idx[x].prefix);
+        bool ok = false;
+        uint64_t v = 0;
         if (valid) {
             const uint32_t k = A.kinds[(uint64_t)col * N + req];
-            if ((okset >> k) & 1u) {
-                const uint64_t v = A.vals[(uint64_t)col * N + req];
-                const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-                for (uint32_t h = mxp_hash64(v) & hmask;; h = (h + 1) & hmask) {
-                    const mxp_hent E = A.hents[hoff + h];
-                    if (E.len == 0) break;
-                    if (E.klo == lo && E.khi == hi) {
-                        start = E.start;
-                        len = E.len;
-                        break;
+            ok = ((okset >> k) & 1u) != 0;
+            if (ok) v = A.vals[(uint64_t)col * N + req];
+        }
+        // probes: one for an equality index; one per key length (shortest first) for a prefix index
+        StrRef s{nullptr, 0};
+        if (ok && prefix) s = str_of(A, v);
+        uint64_t h = 0;
+        uint32_t words = 0;
+        const uint32_t plen0 = uni(A.idx[x].plen0), nprobe = prefix ? uni(A.idx[x].nplen) : 1u;
+        for (uint32_t pi = 0; pi < nprobe; pi++) {
+            uint32_t start = 0, len = 0;
+            if (!prefix) {
+                if (ok) {
+                    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+                    for (uint32_t slot = mxp_hash64(v) & hmask;; slot = (slot + 1) & hmask) {
+                        const mxp_hent E = A.hents[hoff + slot];
+                        if (E.len == 0) break;
+                        if (E.klo == lo && E.khi == hi) {
+                            start = E.start;
+                            len = E.len;
+                            break;
+                        }
+                    }
+                }
+            } else {
+                const uint32_t L = uni(A.plens[plen0 + pi]);
+                if (ok && L <= s.n) {
+                    for (; (words + 1) * 8u <= L; words++) h = mxp_str_step(h, ld8(s.p + words * 8u));
+                    uint64_t hl = h;
+                    const uint32_t rem = L - words * 8u;
+                    if (rem) hl = mxp_str_step(hl, ld8(s.p + words * 8u) & ((1ull << (rem * 8u)) - 1ull));
+                    const uint64_t hf = mxp_str_final(hl, L);
+                    const uint32_t tag = (uint32_t)(hf >> 32);
+                    for (uint32_t slot = (uint32_t)hf & hmask;; slot = (slot + 1) & hmask) {
+                        const mxp_hent E = A.hents[hoff + slot];
+                        if (E.len == 0) break;
+                        if (E.khi != tag) continue;
+                        const StrRef k = str_of(A, E.klo);
+                        if (k.n == L && bytes_eq(s.p, k.p, L)) {
+                            start = E.start;
+                            len = E.len;
+                            break;
+                        }
                     }
                 }
             }
-        }
-        for (uint32_t j = 0; __ballot(j < len); j++) {
-            bool pending = j < len;
-            const uint32_t rule = pending ? A.postings[start + j] : 0u;
-            const uint32_t t = pending ? A.rule_tmpl[rule] : MXP_VM_DONE;
-            for (uint64_t bal = __ballot(pending); bal; bal = __ballot(pending)) {
-                const uint32_t tt = __builtin_amdgcn_readlane(t, (uint32_t)__builtin_ctzll(bal));
-                const bool mine = pending && t == tt;
-                const mxp_tmpl* T = A.tmpls + tt;
-                const uint32_t off = uni(T->off), pc0 = uni(T->pc0), len_t = uni(T->len), nconst = uni(T->nconst),
-                               creg0 = uni(T->creg0);
-                if (mine)
-                    for (uint32_t c = 0; c < nconst; c++)
-                        regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
-                cuint32* P = ((cuint32*)A.prog) + ((uint64_t)off - pc0) * 4u;
-                const uint32_t code = run_rule(A, P, len_t, pc0, mine, rule, req, regs, tid);
-                if (mine) {
-                    const uint64_t w = (uint64_t)(rule >> 5) * N + req;
-                    const uint32_t bit = 1u << (rule & 31u);
-                    if (code == PC_TRUE && A.out_match) atomicOr(A.out_match + w, bit);
-                    if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
-                }
-                pending = pending && !mine;
-            }
+            if (__ballot(len != 0)) run_postings(A, start, len, req, regs, tid);
         }
     }
 }

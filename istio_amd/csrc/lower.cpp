@@ -609,7 +609,7 @@ LoweredRule lower_rule(const IlProgram& prog, LowerTables* tables) { return Lowe
 std::string vm_disasm(const std::vector<mxp_vm_ins>& code) {
     static const char* names[] = {"nop", "res", "tres", "vcol", "const", "eq", "eqk", "not", "jz", "jnz", "jmp",
                                   "ret", "lookup", "lookupk", "strfn", "strfnk", "ipof", "tsof", "ipeq", "tseq",
-                                  "err", "logic", "logick", "ftos", "stof", "jzret", "jnzret", "retk", "mov", "regex", "regexd"};
+                                  "err", "logic", "logick", "ftos", "stof", "jzret", "jnzret", "retk", "mov", "regex", "regexd", "regexr"};
     std::string o;
     char buf[160];
     for (size_t i = 0; i < code.size(); i++) {

@@ -703,6 +703,55 @@ struct StateHash {
 
 }  // namespace
 
+namespace {
+void append_utf8(std::string* o, uint32_t r) {
+    if (r < 0x80) {
+        o->push_back((char)r);
+    } else if (r < 0x800) {
+        o->push_back((char)(0xC0 | (r >> 6)));
+        o->push_back((char)(0x80 | (r & 0x3F)));
+    } else if (r < 0x10000) {
+        o->push_back((char)(0xE0 | (r >> 12)));
+        o->push_back((char)(0x80 | ((r >> 6) & 0x3F)));
+        o->push_back((char)(0x80 | (r & 0x3F)));
+    } else {
+        o->push_back((char)(0xF0 | (r >> 18)));
+        o->push_back((char)(0x80 | ((r >> 12) & 0x3F)));
+        o->push_back((char)(0x80 | ((r >> 6) & 0x3F)));
+        o->push_back((char)(0x80 | (r & 0x3F)));
+    }
+}
+
+// the concatenation that starts the pattern (descending through single-alternative groups)
+const Node* leading_cat(const Node* n) {
+    while (n->k == N_GROUP) n = n->sub[0].get();
+    return n->k == N_CAT ? n : nullptr;
+}
+}  // namespace
+
+bool regex_required_prefix(const std::string& pattern, std::string* prefix) {
+    prefix->clear();
+    try {
+        Parser ps(pattern);
+        NodeP ast = ps.parse();
+        const Node* cat = leading_cat(ast.get());
+        if (!cat || cat->sub.empty()) return false;
+        const Node* first = cat->sub[0].get();
+        if (first->k != N_EMPTY || first->empty != BEGIN_TEXT) return false;
+        // literal runes right after \A / ^ (no (?m)): every match starts with their UTF-8 bytes.
+        // (an invalid-UTF-8 subject byte decodes to U+FFFD, so a U+FFFD literal is not a byte prefix)
+        for (size_t k = 1; k < cat->sub.size(); k++) {
+            const Node* n = cat->sub[k].get();
+            while (n->k == N_GROUP && n->sub[0]->k == N_CAT && n->sub[0]->sub.size() == 1) n = n->sub[0]->sub[0].get();
+            if (n->k != N_LIT || n->rune == 0xFFFD) break;
+            append_utf8(prefix, n->rune);
+        }
+        return !prefix->empty();
+    } catch (...) {
+        return false;
+    }
+}
+
 int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states, Dfa* out, std::string* err,
                   uint32_t* bad) {
     Prog p;

@@ -47,6 +47,10 @@ enum RegexStatus { RX_OK = 0, RX_SYNTAX = 1, RX_UNSUPPORTED = 2, RX_TOO_BIG = 3 
 int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states, Dfa* out, std::string* err,
                   uint32_t* bad = nullptr);
 
+// A pattern anchored at text begin (^ without (?m), or \A) followed by literal runes only matches
+// subjects that start with those runes' UTF-8 bytes: the engine indexes such rules by that prefix.
+bool regex_required_prefix(const std::string& pattern, std::string* prefix);
+
 // Host reference stepping of a compiled DFA (tests / debugging).
 bool dfa_match_host(const Dfa& d, const std::string& s);
 

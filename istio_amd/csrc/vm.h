@@ -47,6 +47,7 @@ enum mxp_vm_op {
     VM_MOV = 28,     // d <- r[a]                 (templates: hoisted CONST)
     VM_REGEX = 29,   // d <- regexp.MatchString(<rule-set DFA x>, string r[a])
     VM_REGEXD = 30,  // d <- regexp.MatchString(string r[a], string r[b]): pattern DFA from the batch's rxof table
+    VM_REGEXR = 31,  // d <- regexp.MatchString(<rule-set DFA r[b]>, string r[a])   (templates: hoisted REGEX)
 };
 
 // Leading-atom guard of a rule (vmopt.cpp): the rule's program starts with
@@ -60,10 +61,11 @@ enum mxp_guard_mode {
     GM_OR = 3,    // atom true -> result true; atom false -> continue at cont
 };
 #define GK_VCOL 5  // guard kind: virtual map[key] column (else a want class W_S..W_D)
+#define GT_PREFIX (1u << 9)  // mxp_guard.mode flag: the atom is `column startsWith K` (K = string id)
 
 typedef struct mxp_guard {
     uint32_t col;    // column index (resolve or virtual); bits 24..31: kind (W_* or GK_VCOL)
-    uint32_t mode;   // bits 0..7 mode, 8..15 negate, 16..31 continuation pc
+    uint32_t mode;   // bits 0..7 mode, bit 8 negate, bit 9 GT_PREFIX, 16..31 continuation pc
     uint32_t klo;    // constant (register value) compared against
     uint32_t khi;
 } mxp_guard;
@@ -107,19 +109,49 @@ typedef struct mxp_index {
     uint32_t okset;    // as mxp_seg.okset (bits 0..15)
     uint32_t hmask;    // table size - 1 (power of two)
     uint32_t hoff;     // first entry in kargs.hents
+    uint32_t prefix;   // 0: equality index (key = the column value); 1: prefix index (key = leading bytes)
+    uint32_t plen0;    // prefix index: distinct key lengths kargs.plens[plen0 .. plen0 + nplen), ascending
+    uint32_t nplen;
+    uint32_t pad;
 } mxp_index;
 
 typedef struct mxp_hent {
-    uint32_t klo, khi; // key (column value register)
+    uint32_t klo, khi; // equality: the key (column value register); prefix: string id of the key, hash tag
     uint32_t start;    // postings [start, start + len); len == 0: empty slot
     uint32_t len;
 } mxp_hent;
+
+// kargs.rule_tmpl value of indexed rules whose atom IS the result (`col.startsWith(K)` alone): a
+// posting is a true pair, no continuation to run
+#define MXP_TMPL_DIRECT 0xFFFFFFFEu
 
 #if defined(__HIPCC__)
 #define MXP_HD __host__ __device__
 #else
 #define MXP_HD
 #endif
+// word-at-a-time byte-string hash (little-endian 8-byte words, zero beyond the end), shared by the
+// prefix index builder (host) and the index kernel, which hashes a request's leading bytes
+static inline MXP_HD uint64_t mxp_str_step(uint64_t h, uint64_t w) {
+    h ^= w;
+    h *= 0x9E3779B97F4A7C15ull;
+    return h ^ (h >> 31);
+}
+static inline MXP_HD uint64_t mxp_str_final(uint64_t h, uint64_t len) {
+    h ^= len * 0xC2B2AE3D27D4EB4Full;
+    h *= 0xFF51AFD7ED558CCDull;
+    return h ^ (h >> 33);
+}
+static inline uint64_t mxp_str_hash(const uint8_t* p, uint64_t n) {
+    uint64_t h = 0;
+    for (uint64_t i = 0; i < n; i += 8) {
+        uint64_t w = 0;
+        for (uint64_t k = 0; k < 8 && i + k < n; k++) w |= (uint64_t)p[i + k] << (8 * k);
+        h = mxp_str_step(h, w);
+    }
+    return mxp_str_final(h, n);
+}
+
 static inline MXP_HD uint32_t mxp_hash64(uint64_t k) {
     k ^= k >> 33;
     k *= 0xff51afd7ed558ccdull;

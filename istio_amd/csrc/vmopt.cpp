@@ -23,6 +23,7 @@ static bool is_terminal(const mxp_vm_ins& i) {
 static uint32_t reads(const mxp_vm_ins& i) {
     switch (opof(i)) {
     case VM_EQ: case VM_LOGIC: case VM_LOOKUP: case VM_STRFN: case VM_IPEQ: case VM_TSEQ: case VM_REGEXD:
+    case VM_REGEXR:
         return (1u << i.a) | (1u << i.b);
     case VM_EQK: case VM_NOT: case VM_LOGICK: case VM_JZ: case VM_JNZ: case VM_RET: case VM_LOOKUPK:
     case VM_STRFNK: case VM_IPOF: case VM_TSOF: case VM_FTOS: case VM_STOF: case VM_JZRET: case VM_JNZRET:
@@ -38,6 +39,7 @@ static uint32_t writes(const mxp_vm_ins& i) {
     case VM_RES: case VM_TRES: case VM_VCOL: case VM_CONST: case VM_EQ: case VM_EQK: case VM_NOT: case VM_LOGIC:
     case VM_LOGICK: case VM_LOOKUP: case VM_LOOKUPK: case VM_STRFN: case VM_STRFNK: case VM_IPOF: case VM_TSOF:
     case VM_IPEQ: case VM_TSEQ: case VM_FTOS: case VM_STOF: case VM_MOV: case VM_REGEX: case VM_REGEXD:
+    case VM_REGEXR:
         return 1u << i.d;
     default:
         return 0;
@@ -48,7 +50,7 @@ static uint32_t writes(const mxp_vm_ins& i) {
 static bool is_pure(const mxp_vm_ins& i) {
     switch (opof(i)) {
     case VM_CONST: case VM_EQ: case VM_EQK: case VM_NOT: case VM_LOGIC: case VM_LOGICK: case VM_STRFN:
-    case VM_STRFNK: case VM_STOF: case VM_NOP: case VM_MOV: case VM_REGEX:
+    case VM_STRFNK: case VM_STOF: case VM_NOP: case VM_MOV: case VM_REGEX: case VM_REGEXR:
         return true;
     default:
         return false;
@@ -251,7 +253,10 @@ mxp_guard extract_guard(const std::vector<mxp_vm_ins>& c) {
     if (opof(a) == VM_RES && a.y <= W_D) kind = a.y;
     else if (opof(a) == VM_VCOL) kind = GK_VCOL;
     else return g;
-    if (a.d != 0 || opof(b) != VM_EQK || b.a != 0 || b.d != 0 || (b.op & MXP_VM_WAKE)) return g;
+    // `col.startsWith(K)`: a prefix atom (indexed by the leading bytes of the column value)
+    const bool prefix = (kind == W_S || kind == GK_VCOL) && opof(b) == VM_STRFNK && b.y == SF_STARTS && b.a == 0 && b.d == 0 &&
+                        !(b.op & MXP_VM_WAKE);
+    if (a.d != 0 || (!prefix && (opof(b) != VM_EQK || b.a != 0 || b.d != 0 || (b.op & MXP_VM_WAKE)))) return g;
     size_t p = 2;
     uint32_t neg = 0;
     if (opof(c[p]) == VM_NOT && c[p].a == 0 && c[p].d == 0 && !(c[p].op & MXP_VM_WAKE)) {
@@ -272,9 +277,9 @@ mxp_guard extract_guard(const std::vector<mxp_vm_ins>& c) {
         // the decision popped r0: continuation code never reads it before writing (stack discipline)
     }
     g.col = a.x | (kind << 24);
-    g.mode = mode | (neg << 8) | (cont << 16);
-    g.klo = b.y;
-    g.khi = b.z;
+    g.mode = mode | (neg << 8) | (cont << 16) | (prefix ? GT_PREFIX : 0u);
+    g.klo = prefix ? b.x : b.y;
+    g.khi = prefix ? 0u : b.z;
     return g;
 }
 
@@ -295,6 +300,7 @@ bool hoist_continuation(const std::vector<mxp_vm_ins>& code, uint32_t pc0, Hoist
         case VM_LOOKUPK: k = i.x; i.op = VM_LOOKUP; i.b = (uint8_t)next; i.x = 0; break;
         case VM_LOGICK: k = i.x; i.op = VM_LOGIC; i.b = (uint8_t)next; i.x = 0; break;
         case VM_CONST: k = (uint64_t)i.y | ((uint64_t)i.z << 32); i.op = VM_MOV; i.a = (uint8_t)next; i.y = i.z = 0; break;
+        case VM_REGEX: k = i.x; i.op = VM_REGEXR; i.b = (uint8_t)next; i.x = 0; break;
         default: continue;
         }
         if (next >= MXP_VM_MAXREG) return false;

@@ -117,6 +117,7 @@ def test_c4_routes_parity(mxp):
     eng = mxp.Engine(0)
     eng.set_vocabulary(manifest)
     assert (eng.compile(rules) == 0).all()
+    assert eng.ruleset_info()["indexed"] > 0.7 * len(rules)  # prefix index: startsWith + anchored regexps
     ev = oracle.OracleEvaluator(manifest)
     got, want = compare(eng, ev, rules, batch)
     assert (want == 1).sum() > 500
