@@ -305,7 +305,12 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
         case VM_REGEXD:
             if (live) {
                 // one stepping loop for the three forms (a single inlined copy of the DFA walk)
-                const mxp_dfa_set* S = &A.rx;
+                // the set is chosen by value (a pointer into the by-value kernarg block would spill
+                // the whole block to scratch)
+                const bool bat = op == VM_REGEXD;
+                const mxp_dfa_set S{bat ? A.rx_batch.hdr : A.rx.hdr, bat ? A.rx_batch.trans : A.rx.trans,
+                                    bat ? A.rx_batch.ascii : A.rx.ascii, bat ? A.rx_batch.hilo : A.rx.hilo,
+                                    bat ? A.rx_batch.hicls : A.rx.hicls};
                 uint32_t dfa = x;
                 uint64_t subj = REG(a);
                 bool run = true;
@@ -315,7 +320,6 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
                     const uint64_t psid = REG(a);
                     dfa = A.rxof[psid];
                     subj = REG(b);
-                    S = &A.rx_batch;
                     if (dfa == MXP_RXOF_SYNTAX || dfa == MXP_RXOF_UNSUPPORTED) {
                         FAIL(dfa == MXP_RXOF_SYNTAX ? ERR_REGEX : ERR_REGEX_UNSUPPORTED, (uint32_t)psid);
                         run = false;
@@ -323,7 +327,7 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
                 }
                 if (run) {
                     const StrRef sub = str_of(A, subj);
-                    REG(d) = mxp_dfa_run(*S, dfa, sub.p, sub.n) ? 1u : 0u;
+                    REG(d) = mxp_dfa_run(S, dfa, sub.p, sub.n) ? 1u : 0u;
                 }
             }
             break;

@@ -264,7 +264,7 @@ def guarded_fuzz_rules(n, seed=11, depth=2, random_tail=True):
               lambda: "ab == %s" % f.pick(["true", "false"]),
               lambda: "ad == %s" % f.pick(["1.5", "2.5", "0.0"]),
               lambda: 'as.startsWith("%s")' % f.pick(["", "a", "ab", "abc", "st", "1.2", "x"]),
-              lambda: '!bs.startsWith("%s")' % f.pick(["a", "ab"]),
+              lambda: 'bs.startsWith("%s") == false' % f.pick(["a", "ab"]),
               lambda: '"^%s".matches(bs)' % f.pick(["a", "ab", "st", "str", "a[bc]", "1.2"]),
               lambda: '"^%s".matches(ar["%s"])' % (f.pick(["a", "fo", "ba"]), f.pick(_KEYS))]
     shapes = [lambda: '%s.startsWith("%s") && aip != ip("%s")' % (f.pick(["as", "bs"]), f.pick(["a", "ab", "st", ""]),

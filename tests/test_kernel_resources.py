@@ -1,0 +1,44 @@
+"""Resource budget of the gfx950 kernels (compile-time, no GPU): every kernel must run without
+scratch (a spill to private memory, or a by-value kernarg block whose address escapes, costs a
+scratch round trip per access) and keep the occupancy its launch configuration is tuned for."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "istio_amd", "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+# minimum waves/SIMD per kernel (launch_bounds(256) kernels; the values the launches were tuned at)
+MIN_OCCUPANCY = {"mxp_guard_kernel": 8, "mxp_eval_kernel": 4, "mxp_index_kernel": 5}
+
+
+def resource_usage(src):
+    cmd = [HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "-c", os.path.join(CSRC, src), "-o", os.devnull,
+           "-Rpass-analysis=kernel-resource-usage"]
+    out = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, check=True).stdout.decode()
+    usage, name = {}, None
+    for line in out.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            usage[name] = {}
+            continue
+        m = re.search(r"remark: \s*([A-Za-z ]+?)(?: \[[^\]]*\])?: (\d+) \[", line)
+        if m and name:
+            usage[name][m.group(1).strip()] = int(m.group(2))
+    return usage
+
+
+@pytest.mark.parametrize("src", ["kernels.hip", "lists.hip", "resolve.hip", "quota.hip"])
+def test_no_scratch(src):
+    usage = resource_usage(src)
+    assert usage, "no kernels found in %s" % src
+    ours = {k: v for k, v in usage.items() if k.startswith("mxp_")}
+    assert ours, "no mxp_ kernels found in %s" % src
+    for name, u in ours.items():  # (library kernels, e.g. rocPRIM's radix sort, are not ours to budget)
+        assert u.get("ScratchSize", 0) == 0, (name, u)
+        if name in MIN_OCCUPANCY:
+            assert u.get("Occupancy", 0) >= MIN_OCCUPANCY[name], (name, u)
