@@ -145,7 +145,12 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     // serve falls back to a guard-less rule (phase 1 only compares equality atoms).
     std::vector<uint8_t> indexed(n, 0);
     std::map<std::pair<uint32_t, bool>, std::map<uint64_t, std::vector<uint32_t>>> index_of;
+    // composite: (A column, B column) -> (K1, K2 string id) -> rules
+    std::map<std::pair<uint32_t, uint32_t>, std::map<std::pair<uint64_t, uint32_t>, std::vector<uint32_t>>> comp_of;
+    std::vector<uint32_t> rule_tmpl2(n, MXP_VM_DONE);
+    std::map<std::pair<uint32_t, uint32_t>, uint32_t> tmpl2_ids;  // (template, resume pc) -> template
     n_indexed = 0;
+    n_composite = 0;
     for (uint32_t i = 0; i < n; i++) {
         mxp_guard& gd = guards[i];
         const uint32_t mode = gd.mode & 0xFF;
@@ -161,18 +166,64 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         }
         if (prefix && mode == GM_ONLY) rule_tmpl[i] = MXP_TMPL_DIRECT;
         indexed[i] = 1;
-        index_of[{gd.col, prefix}][(uint64_t)gd.klo | ((uint64_t)gd.khi << 32)].push_back(i);
         n_indexed++;
+        const uint64_t k1 = (uint64_t)gd.klo | ((uint64_t)gd.khi << 32);
+        mxp::SecondAtom sa;
+        std::vector<mxp_vm_ins> code(all.begin() + off[i], all.begin() + off[i + 1]);
+        if (!prefix && !(debug_flags & 16u) && mxp::extract_second_prefix(code, gd.mode >> 16, &sa)) {
+            if (sa.direct) {
+                rule_tmpl2[i] = MXP_TMPL_DIRECT;
+            } else {
+                const uint32_t t1 = rule_tmpl[i];
+                auto it = tmpl2_ids.find({t1, sa.cont});
+                if (it == tmpl2_ids.end()) {
+                    mxp_tmpl t = tmpls[t1];
+                    t.off += sa.cont - t.pc0;
+                    t.pc0 = sa.cont;
+                    it = tmpl2_ids.emplace(std::make_pair(t1, sa.cont), (uint32_t)tmpls.size()).first;
+                    tmpls.push_back(t);
+                }
+                rule_tmpl2[i] = it->second;
+            }
+            comp_of[{gd.col, sa.col}][{k1, sa.k2}].push_back(i);
+            n_composite++;
+            continue;
+        }
+        index_of[{gd.col, prefix}][k1].push_back(i);
     }
+    n_tmpls = (uint32_t)tmpls.size();
     std::vector<mxp_index> idx;
     std::vector<mxp_hent> hents;
     std::vector<uint32_t> postings, plens;
+    // open-addressing table of `groups` (key -> rules) at hents[hoff ..): returns hmask
+    auto add_eq_table = [&](const std::map<uint64_t, std::vector<uint32_t>>& groups, const std::vector<uint32_t>& tmpl_of,
+                            uint32_t* hoff) -> uint32_t {
+        uint32_t cap = 1;
+        while (cap < 2 * groups.size()) cap <<= 1;
+        *hoff = (uint32_t)hents.size();
+        hents.resize(hents.size() + cap, mxp_hent{0, 0, 0, 0});
+        for (auto& kv : groups) {
+            std::vector<uint32_t> rs = kv.second;
+            std::stable_sort(rs.begin(), rs.end(), [&](uint32_t a, uint32_t b) { return tmpl_of[a] < tmpl_of[b]; });
+            uint32_t h = mxp_hash64(kv.first) & (cap - 1);
+            while (hents[*hoff + h].len) h = (h + 1) & (cap - 1);
+            hents[*hoff + h] = mxp_hent{(uint32_t)kv.first, (uint32_t)(kv.first >> 32), (uint32_t)postings.size(),
+                                        (uint32_t)rs.size()};
+            postings.insert(postings.end(), rs.begin(), rs.end());
+        }
+        return cap - 1;
+    };
     for (auto& ci : index_of) {
         const bool prefix = ci.first.second;
         mxp_index x{};
         x.col = ci.first.first & 0xFFFFFFu;
         x.okset = okset_of(ci.first.first >> 24);
-        x.prefix = prefix ? 1u : 0u;
+        x.prefix = prefix ? MXP_IX_PREFIX : MXP_IX_EQ;
+        if (!prefix) {
+            x.hmask = add_eq_table(ci.second, rule_tmpl, &x.hoff);
+            idx.push_back(x);
+            continue;
+        }
         uint32_t cap = 1;
         while (cap < 2 * ci.second.size()) cap <<= 1;
         x.hmask = cap - 1;
@@ -182,24 +233,55 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         for (auto& kv : ci.second) {
             std::vector<uint32_t> rs = kv.second;
             std::stable_sort(rs.begin(), rs.end(), [&](uint32_t a, uint32_t b) { return rule_tmpl[a] < rule_tmpl[b]; });
-            uint64_t hh;
-            uint32_t tag;
-            if (prefix) {  // hash of the key bytes, as the kernel hashes the request's leading bytes
-                const std::string& key = gstrs[(uint32_t)kv.first];
-                lens.insert((uint32_t)key.size());
-                hh = mxp_str_hash((const uint8_t*)key.data(), key.size());
-                tag = (uint32_t)(hh >> 32);
-            } else {
-                hh = mxp_hash64(kv.first);
-                tag = (uint32_t)(kv.first >> 32);
-            }
+            // hash of the key bytes, as the kernel hashes the request's leading bytes
+            const std::string& key = gstrs[(uint32_t)kv.first];
+            lens.insert((uint32_t)key.size());
+            const uint64_t hh = mxp_str_hash((const uint8_t*)key.data(), key.size());
             uint32_t h = (uint32_t)hh & x.hmask;
             while (hents[x.hoff + h].len) h = (h + 1) & x.hmask;
-            mxp_hent& E = hents[x.hoff + h];
-            E.klo = (uint32_t)kv.first;
-            E.khi = tag;
-            E.start = (uint32_t)postings.size();
-            E.len = (uint32_t)rs.size();
+            hents[x.hoff + h] = mxp_hent{(uint32_t)kv.first, (uint32_t)(hh >> 32), (uint32_t)postings.size(),
+                                         (uint32_t)rs.size()};
+            postings.insert(postings.end(), rs.begin(), rs.end());
+        }
+        x.plen0 = (uint32_t)plens.size();
+        x.nplen = (uint32_t)lens.size();
+        plens.insert(plens.end(), lens.begin(), lens.end());
+        idx.push_back(x);
+    }
+    for (auto& ci : comp_of) {
+        mxp_index x{};
+        x.col = ci.first.first & 0xFFFFFFu;
+        x.okset = okset_of(ci.first.first >> 24);
+        x.prefix = MXP_IX_COMPOSITE;
+        x.col2 = ci.first.second;
+        x.okset2 = okset_of(W_S);
+        // fallback equality table over K1 (B not a string): every rule of the key, continuation after A
+        std::map<uint64_t, std::vector<uint32_t>> by_k1;
+        for (auto& kv : ci.second) {
+            auto& v = by_k1[kv.first.first];
+            v.insert(v.end(), kv.second.begin(), kv.second.end());
+        }
+        for (auto& kv : by_k1) std::sort(kv.second.begin(), kv.second.end());
+        x.hmask = add_eq_table(by_k1, rule_tmpl, &x.hoff);
+        // composite table: entry pairs
+        uint32_t cap = 1;
+        while (cap < 2 * ci.second.size()) cap <<= 1;
+        x.hmask2 = cap - 1;
+        x.hoff2 = (uint32_t)hents.size();
+        hents.resize(hents.size() + 2 * (size_t)cap, mxp_hent{0, 0, 0, 0});
+        std::set<uint32_t> lens;
+        for (auto& kv : ci.second) {
+            std::vector<uint32_t> rs = kv.second;
+            std::stable_sort(rs.begin(), rs.end(), [&](uint32_t a, uint32_t b) { return rule_tmpl2[a] < rule_tmpl2[b]; });
+            const uint64_t k1 = kv.first.first;
+            const std::string& key = gstrs[kv.first.second];
+            lens.insert((uint32_t)key.size());
+            const uint64_t hh = mxp_str_hash_seeded(mxp_composite_seed(k1), (const uint8_t*)key.data(), key.size());
+            uint32_t h = (uint32_t)hh & x.hmask2;
+            while (hents[x.hoff2 + 2 * h].len) h = (h + 1) & x.hmask2;
+            hents[x.hoff2 + 2 * h] = mxp_hent{kv.first.second, (uint32_t)(hh >> 32), (uint32_t)postings.size(),
+                                              (uint32_t)rs.size()};
+            hents[x.hoff2 + 2 * h + 1] = mxp_hent{(uint32_t)k1, (uint32_t)(k1 >> 32), 0, 0};
             postings.insert(postings.end(), rs.begin(), rs.end());
         }
         x.plen0 = (uint32_t)plens.size();
@@ -291,6 +373,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_plens, plens.data(), plens.size() * 4, "upload plens"))) return rc;
     if ((rc = put(d_tmpls, tmpls.data(), tmpls.size() * sizeof(mxp_tmpl), "upload tmpls"))) return rc;
     if ((rc = put(d_rule_tmpl, rule_tmpl.data(), rule_tmpl.size() * 4, "upload rule_tmpl"))) return rc;
+    if ((rc = put(d_rule_tmpl2, rule_tmpl2.data(), rule_tmpl2.size() * 4, "upload rule_tmpl2"))) return rc;
     if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
     if ((rc = put(d_rx_hdr, rx_set.hdr.data(), rx_set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
     if ((rc = put(d_rx_trans, rx_set.trans.data(), rx_set.trans.size() * 4, "upload rx trans"))) return rc;
@@ -541,6 +624,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->n_idx = n_idx;
     A->tmpls = d_tmpls.as<mxp_tmpl>();
     A->rule_tmpl = d_rule_tmpl.as<uint32_t>();
+    A->rule_tmpl2 = d_rule_tmpl2.as<uint32_t>();
     A->rconst = d_rconst.as<uint64_t>();
     A->flags = debug_flags;
     A->n_rules = (uint32_t)rules.size();
@@ -799,10 +883,10 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) 
 
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
     if (!eng || !out) return 0;
-    const uint32_t v[6] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed,
-                           (uint32_t)(eng->cols.size() + eng->vcols.size())};
+    const uint32_t v[7] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed,
+                           (uint32_t)(eng->cols.size() + eng->vcols.size()), eng->n_composite};
     uint32_t k = 0;
-    for (; k < cap && k < 6; k++) out[k] = v[k];
+    for (; k < cap && k < 7; k++) out[k] = v[k];
     return k;
 }
 

@@ -140,10 +140,10 @@ struct mxp_engine : public mxp::LowerTables {
     DevBuf d_rx_hdr, d_rx_trans, d_rx_ascii, d_rx_hilo, d_rx_hicls;
 
     DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
-    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rconst, d_idx, d_hents, d_postings, d_plens;
+    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_rconst, d_idx, d_hents, d_postings, d_plens;
     DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
     uint32_t n_glean = 0, n_gvm = 0;
-    uint32_t n_idx = 0, n_indexed = 0;
+    uint32_t n_idx = 0, n_indexed = 0, n_composite = 0;
     uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
     uint32_t groups_per_wave = 4; // MXP_GPW
     // optional per-kernel timing of device evaluations (mxp_set_timing): events around each launch

@@ -24,6 +24,7 @@ typedef struct mxp_kargs {
     const uint64_t* gk;          // [n_words * 32] guard constants (0 for unguarded slots)
     const mxp_tmpl* tmpls;       // continuation templates
     const uint32_t* rule_tmpl;   // [n_rules] template of the rule's continuation (~0: none)
+    const uint32_t* rule_tmpl2;  // [n_rules] composite-indexed rules: template resuming after the second atom
     const uint64_t* rconst;      // [n_rules][MXP_VM_MAXREG] per-rule template constants
     const mxp_index* idx;        // guard indexes (mxp_index_kernel)
     const mxp_hent* hents;

@@ -537,13 +537,13 @@ namespace {
 // Direct postings (MXP_TMPL_DIRECT) are true pairs; the others run their template, lanes sharing a
 // template together, each with its own rule's constants preloaded.  Results are OR-ed into the
 // bitmaps.
-__device__ void run_postings(const mxp_kargs& A, uint32_t start, uint32_t len, uint32_t req, uint64_t (*regs)[256],
-                             uint32_t tid) {
+__device__ void run_postings(const mxp_kargs& A, const uint32_t* __restrict__ tmpl_of, uint32_t start, uint32_t len,
+                             uint32_t req, uint64_t (*regs)[256], uint32_t tid) {
     const uint64_t N = A.n;
     for (uint32_t j = 0; __ballot(j < len); j++) {
         bool pending = j < len;
         const uint32_t rule = pending ? A.postings[start + j] : 0u;
-        const uint32_t t = pending ? A.rule_tmpl[rule] : MXP_VM_DONE;
+        const uint32_t t = pending ? tmpl_of[rule] : MXP_VM_DONE;
         if (pending && t == MXP_TMPL_DIRECT) {
             if (A.out_match) atomicOr(A.out_match + (uint64_t)(rule >> 5) * N + req, 1u << (rule & 31u));
             pending = false;
@@ -569,11 +569,45 @@ __device__ void run_postings(const mxp_kargs& A, uint32_t start, uint32_t len, u
     }
 }
 
+// equality probe: postings of the entry whose key is v (len 0: none)
+__device__ __forceinline__ void eq_probe(const mxp_kargs& A, uint32_t hoff, uint32_t hmask, uint64_t v, uint32_t& start,
+                                         uint32_t& len) {
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    uint32_t fi = 0xFFFFFFFFu;
+    for (uint32_t slot = mxp_hash64(v) & hmask;; slot = (slot + 1) & hmask) {
+        const mxp_hent E = A.hents[hoff + slot];
+        if (E.len == 0) break;
+        if (E.klo == lo && E.khi == hi) {
+            fi = hoff + slot;
+            break;
+        }
+    }
+    if (fi != 0xFFFFFFFFu) {
+        start = A.hents[fi].start;
+        len = A.hents[fi].len;
+    }
+}
+
+// Incremental hash of a string's leading bytes (vm.h mxp_str_step / mxp_str_final): key lengths are
+// probed in ascending order, so whole 8-byte words are folded in once.
+struct PrefixHash {
+    uint64_t h;
+    uint32_t words;
+    __device__ __forceinline__ uint64_t at(const uint8_t* p, uint32_t L) {
+        for (; (words + 1) * 8u <= L; words++) h = mxp_str_step(h, ld8(p + words * 8u));
+        uint64_t hl = h;
+        const uint32_t rem = L - words * 8u;
+        if (rem) hl = mxp_str_step(hl, ld8(p + words * 8u) & ((1ull << (rem * 8u)) - 1ull));
+        return mxp_str_final(hl, L);
+    }
+};
+
 }  // namespace
 
 // Guard-index phase: the pairs of indexed rules, found per request by hash lookups of its column
-// value (equality indexes) or of its leading bytes at every key length the index holds (prefix
-// indexes: `startsWith` atoms and anchored regexp literals) instead of by testing every rule.
+// value (equality indexes), of its leading bytes at every key length the index holds (prefix
+// indexes: `startsWith` atoms and anchored regexp literals), or of both (composite indexes:
+// `A == K1 && B.startsWith(K2) && ...`) instead of by testing every rule.
 // Workgroup = 4 wavefronts, one tile of 64 requests each (one request per lane).  mxp_eval_kernel
 // has already written both bitmaps for these rules (match 0, error on a failed type check of the
 // guard column); true and error results are OR-ed in.
@@ -585,8 +619,10 @@ extern "C" __global__ __launch_bounds__(256) void mxp_index_kernel(mxp_kargs A) 
     const bool valid = req < A.n;
     const uint64_t N = A.n;
     for (uint32_t x = 0; x < A.n_idx; x++) {
-        const uint32_t col = uni(A.idx[x].col), okset = uni(A.idx[x].okset), hmask = uni(A.idx[x].hmask),
-                       hoff = uni(A.idx[x].hoff), prefix = uni(A.idx[x].prefix);
+        const mxp_index* X = A.idx + x;
+        const uint32_t col = uni(X->col), okset = uni(X->okset), hmask = uni(X->hmask), hoff = uni(X->hoff),
+                       kind = uni(X->prefix), plen0 = uni(X->plen0), nplen = uni(X->nplen);
+        const bool comp = kind == MXP_IX_COMPOSITE;
         bool ok = false;
         uint64_t v = 0;
         if (valid) {
@@ -594,74 +630,151 @@ extern "C" __global__ __launch_bounds__(256) void mxp_index_kernel(mxp_kargs A) 
             ok = ((okset >> k) & 1u) != 0;
             if (ok) v = A.vals[(uint64_t)col * N + req];
         }
-        // probes: one for an equality index; one per key length (shortest first) for a prefix index
+        // the string whose leading bytes are probed: the column itself (prefix index) or, for a
+        // composite (A == K1 && B.startsWith(K2) && ...), B -- when B is not a string the lane takes
+        // the composite's equality table over K1 instead (continuation after A: it raises B's error)
+        bool sok = ok && kind == MXP_IX_PREFIX;
+        uint64_t sv = v;
+        uint32_t pmask = hmask, poff = hoff;
+        if (comp) {
+            const uint32_t col2 = uni(X->col2), okset2 = uni(X->okset2);
+            pmask = uni(X->hmask2);
+            poff = uni(X->hoff2);
+            if (ok) {
+                const uint32_t k = A.kinds[(uint64_t)col2 * N + req];
+                sok = ((okset2 >> k) & 1u) != 0;
+                if (sok) sv = A.vals[(uint64_t)col2 * N + req];
+            }
+        }
         StrRef s{nullptr, 0};
-        if (ok && prefix) s = str_of(A, v);
-        uint64_t h = 0;
-        uint32_t words = 0;
-        const uint32_t plen0 = uni(A.idx[x].plen0), nprobe = prefix ? uni(A.idx[x].nplen) : 1u;
-        for (uint32_t pi = 0; pi < nprobe; pi++) {
+        if (sok) s = str_of(A, sv);
+        PrefixHash ph{comp ? mxp_composite_seed(v) : 0ull, 0};
+        const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
+        // probe slots: equality 1; prefix one per key length (shortest first); composite the
+        // equality fallback, then one per K2 length
+        const uint32_t nslot = kind == MXP_IX_EQ ? 1u : nplen + (comp ? 1u : 0u);
+        for (uint32_t p = 0; p < nslot; p++) {
             uint32_t start = 0, len = 0;
-            if (!prefix) {
-                if (ok) {
-                    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-                    for (uint32_t slot = mxp_hash64(v) & hmask;; slot = (slot + 1) & hmask) {
-                        const mxp_hent E = A.hents[hoff + slot];
-                        if (E.len == 0) break;
-                        if (E.klo == lo && E.khi == hi) {
-                            start = E.start;
-                            len = E.len;
-                            break;
-                        }
-                    }
-                }
+            const bool eq_slot = kind == MXP_IX_EQ || (comp && p == 0);
+            if (eq_slot) {
+                if (ok && (!comp || !sok)) eq_probe(A, hoff, hmask, v, start, len);
             } else {
-                const uint32_t L = uni(A.plens[plen0 + pi]);
-                if (ok && L <= s.n) {
-                    for (; (words + 1) * 8u <= L; words++) h = mxp_str_step(h, ld8(s.p + words * 8u));
-                    uint64_t hl = h;
-                    const uint32_t rem = L - words * 8u;
-                    if (rem) hl = mxp_str_step(hl, ld8(s.p + words * 8u) & ((1ull << (rem * 8u)) - 1ull));
-                    const uint64_t hf = mxp_str_final(hl, L);
+                const uint32_t L = uni(A.plens[plen0 + p - (comp ? 1u : 0u)]);
+                // the probe yields the entry's index; its postings range is read after the loop (reading
+                // start / len from the loop's 16-byte entry value was miscompiled at -O3 by this
+                // ROCm 7.2 hipcc: lanes resumed with another entry's range)
+                uint32_t fi = 0xFFFFFFFFu;
+                if (sok && L <= s.n) {
+                    const uint64_t hf = ph.at(s.p, L);
                     const uint32_t tag = (uint32_t)(hf >> 32);
-                    for (uint32_t slot = (uint32_t)hf & hmask;; slot = (slot + 1) & hmask) {
-                        const mxp_hent E = A.hents[hoff + slot];
+                    const uint32_t stride = comp ? 2u : 1u;
+                    for (uint32_t slot = (uint32_t)hf & pmask;; slot = (slot + 1) & pmask) {
+                        const uint32_t at = poff + stride * slot;
+                        const mxp_hent E = A.hents[at];
                         if (E.len == 0) break;
                         if (E.khi != tag) continue;
+                        if (comp) {
+                            const mxp_hent K = A.hents[at + 1u];
+                            if (K.klo != vlo || K.khi != vhi) continue;
+                        }
                         const StrRef k = str_of(A, E.klo);
                         if (k.n == L && bytes_eq(s.p, k.p, L)) {
-                            start = E.start;
-                            len = E.len;
+                            fi = at;
                             break;
                         }
                     }
                 }
+                if (fi != 0xFFFFFFFFu) {
+                    start = A.hents[fi].start;
+                    len = A.hents[fi].len;
+                }
             }
-            if (__ballot(len != 0)) run_postings(A, start, len, req, regs, tid);
+            if (__ballot(len != 0))
+                run_postings(A, comp && p > 0 ? A.rule_tmpl2 : A.rule_tmpl, start, len, req, regs, tid);
         }
     }
 }
 
-// Per-rule hit counters: hits[rule] += popcount over requests of the rule's match bit, restricted
-// to requests flagged in `mask` (nullptr = all).  One block per 32-rule word; each thread keeps 32
-// counters in registers, then a block reduction and one atomic per rule.
-extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t* __restrict__ match, uint32_t n,
-                                                                  uint32_t n_rules,
-                                                                  unsigned long long* __restrict__ hits) {
+// Per-rule hit counters: hits[rule] += number of requests whose match bit for the rule is set.
+// The bitmap is streamed once (1.3 GB at R = 10k, N = 1M), so the counting must cost well under one
+// VALU op per word and lane: each lane folds its words into bit-sliced counters with a Harley-Seal
+// carry-save adder tree (ones / twos / fours / eights / sixteens planes, then one byte-packed
+// "thirty-twos" counter per bit: P[j] byte f counts bit 8 f + j), about 3.3 VALU ops per word.
+// The per-bit counts are unpacked once at the end, reduced over the block and added with one
+// atomic per rule.  Grid: x = 32-rule word, y = request slices (sized so that no byte counter
+// exceeds 255 steps).  Loads: 8 x 16 B per lane per step, each a contiguous 1 KB per wavefront.
+namespace {
+
+__device__ __forceinline__ void csa(uint32_t& h, uint32_t& l, uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t u = a ^ b;
+    h = (a & b) | (u & c);
+    l = u ^ c;
+}
+
+// 16 words into the running planes; returns the sixteens carry-out
+__device__ __forceinline__ uint32_t hs16(const uint32_t* d, uint32_t& ones, uint32_t& twos, uint32_t& fours,
+                                         uint32_t& eights) {
+    uint32_t twosA, twosB, foursA, foursB, eightsA, eightsB, sixteens;
+    csa(twosA, ones, ones, d[0], d[1]);
+    csa(twosB, ones, ones, d[2], d[3]);
+    csa(foursA, twos, twos, twosA, twosB);
+    csa(twosA, ones, ones, d[4], d[5]);
+    csa(twosB, ones, ones, d[6], d[7]);
+    csa(foursB, twos, twos, twosA, twosB);
+    csa(eightsA, fours, fours, foursA, foursB);
+    csa(twosA, ones, ones, d[8], d[9]);
+    csa(twosB, ones, ones, d[10], d[11]);
+    csa(foursA, twos, twos, twosA, twosB);
+    csa(twosA, ones, ones, d[12], d[13]);
+    csa(twosB, ones, ones, d[14], d[15]);
+    csa(foursB, twos, twos, twosA, twosB);
+    csa(eightsB, fours, fours, foursA, foursB);
+    csa(sixteens, eights, eights, eightsA, eightsB);
+    return sixteens;
+}
+
+template <bool kVec>
+__device__ __forceinline__ void hits_body(const uint32_t* __restrict__ row, uint32_t n, uint32_t n_rules,
+                                          unsigned long long* __restrict__ hits) {
     const uint32_t w = blockIdx.x;
-    uint32_t cnt[32];
+    const uint32_t nthreads = gridDim.y * blockDim.x;
+    const uint32_t t = blockIdx.y * blockDim.x + threadIdx.x;
+    uint32_t ones = 0, twos = 0, fours = 0, eights = 0, sixteens = 0;
+    uint32_t P[8];
 #pragma unroll
-    for (int k = 0; k < 32; k++) cnt[k] = 0;
-    const uint32_t* row = match + (uint64_t)w * n;
-    for (uint32_t r = blockIdx.y * blockDim.x + threadIdx.x; r < n; r += gridDim.y * blockDim.x) {
-        const uint32_t v = row[r];
+    for (int j = 0; j < 8; j++) P[j] = 0;
+    for (uint64_t base = 0; base < n; base += nthreads * 32u) {
+        uint32_t d[32];
+        if (kVec) {
 #pragma unroll
-        for (int k = 0; k < 32; k++) cnt[k] += (v >> k) & 1u;
+            for (int j = 0; j < 8; j++) {
+                const uint64_t i = base + ((uint64_t)j * nthreads + t) * 4u;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (i < n) v = *(const uint4*)(row + i);
+                d[4 * j] = v.x;
+                d[4 * j + 1] = v.y;
+                d[4 * j + 2] = v.z;
+                d[4 * j + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 32; j++) {
+                const uint64_t i = base + (uint64_t)j * nthreads + t;
+                d[j] = i < n ? row[i] : 0u;
+            }
+        }
+        const uint32_t sA = hs16(d, ones, twos, fours, eights);
+        const uint32_t sB = hs16(d + 16, ones, twos, fours, eights);
+        uint32_t thirtytwos;
+        csa(thirtytwos, sixteens, sixteens, sA, sB);
+#pragma unroll
+        for (int j = 0; j < 8; j++) P[j] += (thirtytwos >> j) & 0x01010101u;
     }
     __shared__ uint32_t red[32][8];
 #pragma unroll
     for (int k = 0; k < 32; k++) {
-        uint32_t c = cnt[k];
+        uint32_t c = 32u * ((P[k & 7] >> (8 * (k >> 3))) & 0xFFu) + 16u * ((sixteens >> k) & 1u) +
+                     8u * ((eights >> k) & 1u) + 4u * ((fours >> k) & 1u) + 2u * ((twos >> k) & 1u) + ((ones >> k) & 1u);
         for (int off = 32; off > 0; off >>= 1) c += __shfl_xor((int)c, off, 64);
         if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = c;
     }
@@ -672,6 +785,21 @@ extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t
         const uint32_t rule = w * 32 + threadIdx.x;
         if (rule < n_rules && c) atomicAdd(&hits[rule], (unsigned long long)c);
     }
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t* __restrict__ match, uint32_t n,
+                                                                  uint32_t n_rules,
+                                                                  unsigned long long* __restrict__ hits) {
+    hits_body<true>(match + (uint64_t)blockIdx.x * n, n, n_rules, hits);
+}
+
+// ragged n (rows not 16-byte aligned): one word per load
+extern "C" __global__ __launch_bounds__(256) void mxp_hits_ragged_kernel(const uint32_t* __restrict__ match, uint32_t n,
+                                                                         uint32_t n_rules,
+                                                                         unsigned long long* __restrict__ hits) {
+    hits_body<false>(match + (uint64_t)blockIdx.x * n, n, n_rules, hits);
 }
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s) {
@@ -689,8 +817,18 @@ extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hip
 
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
                                       unsigned long long* hits, hipStream_t s) {
-    const uint32_t per = (n + 255) / 256;
-    const uint32_t gy = per < 64 ? per : 64;
-    hipLaunchKernelGGL(mxp_hits_kernel, dim3(n_words, gy > 0 ? gy : 1), dim3(256), 0, s, match, n, n_rules, hits);
+    // slices: enough blocks to fill the chip (~16 per CU), at least 32 words per thread, and at most
+    // 255 32-word steps per thread (the byte-packed counters)
+    const uint64_t per_block = 256ull * 32u;
+    uint64_t gy = (4096u + n_words - 1) / (n_words ? n_words : 1);
+    const uint64_t most = (n + per_block - 1) / per_block, least = (n + per_block * 255u - 1) / (per_block * 255u);
+    if (gy > most) gy = most;
+    if (gy < least) gy = least;
+    if (gy < 1) gy = 1;
+    if (gy > 65535) return hipErrorInvalidValue;
+    if ((n & 3u) == 0 && (((uintptr_t)match) & 15u) == 0)
+        hipLaunchKernelGGL(mxp_hits_kernel, dim3(n_words, (uint32_t)gy), dim3(256), 0, s, match, n, n_rules, hits);
+    else
+        hipLaunchKernelGGL(mxp_hits_ragged_kernel, dim3(n_words, (uint32_t)gy), dim3(256), 0, s, match, n, n_rules, hits);
     return hipGetLastError();
 }

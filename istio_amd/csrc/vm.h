@@ -109,11 +109,24 @@ typedef struct mxp_index {
     uint32_t okset;    // as mxp_seg.okset (bits 0..15)
     uint32_t hmask;    // table size - 1 (power of two)
     uint32_t hoff;     // first entry in kargs.hents
-    uint32_t prefix;   // 0: equality index (key = the column value); 1: prefix index (key = leading bytes)
-    uint32_t plen0;    // prefix index: distinct key lengths kargs.plens[plen0 .. plen0 + nplen), ascending
+    uint32_t prefix;   // MXP_IX_EQ / MXP_IX_PREFIX / MXP_IX_COMPOSITE
+    uint32_t plen0;    // prefix / composite: distinct key lengths kargs.plens[plen0 .. plen0 + nplen), ascending
     uint32_t nplen;
-    uint32_t pad;
-} mxp_index;
+    uint32_t col2;     // composite: the prefix column (string want class)
+    uint32_t okset2;
+    uint32_t hmask2;   // composite table: pairs of entries {K2 string id, tag, start, len}, {K1 lo, K1 hi, 0, 0}
+    uint32_t hoff2;
+    uint32_t pad[5];
+} mxp_index;           // 64 B
+
+// index kinds.  Composite: rules `A == K1 && B.startsWith(K2) && ...` (vmopt.h SecondAtom), keyed by
+// (K1, K2): a request probes its A value with B's leading bytes at every K2 length and resumes the
+// rules it finds after both atoms (kargs.rule_tmpl2).  Requests whose B fails the string type check
+// use the composite's equality table over K1 instead (hmask / hoff) and run the continuation after
+// the first atom (kargs.rule_tmpl), which raises the reference's error.
+#define MXP_IX_EQ 0u
+#define MXP_IX_PREFIX 1u
+#define MXP_IX_COMPOSITE 2u
 
 typedef struct mxp_hent {
     uint32_t klo, khi; // equality: the key (column value register); prefix: string id of the key, hash tag
@@ -142,8 +155,9 @@ static inline MXP_HD uint64_t mxp_str_final(uint64_t h, uint64_t len) {
     h *= 0xFF51AFD7ED558CCDull;
     return h ^ (h >> 33);
 }
-static inline uint64_t mxp_str_hash(const uint8_t* p, uint64_t n) {
-    uint64_t h = 0;
+// composite keys: the hash of K2's bytes seeded with the A value (K1)
+static inline MXP_HD uint64_t mxp_composite_seed(uint64_t k1) { return mxp_str_step(0x2545F4914F6CDD1Dull, k1); }
+static inline uint64_t mxp_str_hash_seeded(uint64_t h, const uint8_t* p, uint64_t n) {
     for (uint64_t i = 0; i < n; i += 8) {
         uint64_t w = 0;
         for (uint64_t k = 0; k < 8 && i + k < n; k++) w |= (uint64_t)p[i + k] << (8 * k);
@@ -151,6 +165,7 @@ static inline uint64_t mxp_str_hash(const uint8_t* p, uint64_t n) {
     }
     return mxp_str_final(h, n);
 }
+static inline uint64_t mxp_str_hash(const uint8_t* p, uint64_t n) { return mxp_str_hash_seeded(0, p, n); }
 
 static inline MXP_HD uint32_t mxp_hash64(uint64_t k) {
     k ^= k >> 33;

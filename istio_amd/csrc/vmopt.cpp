@@ -311,4 +311,44 @@ bool hoist_continuation(const std::vector<mxp_vm_ins>& code, uint32_t pc0, Hoist
     return true;
 }
 
+bool extract_second_prefix(const std::vector<mxp_vm_ins>& c, uint32_t pc0, SecondAtom* out) {
+    if (pc0 + 3 > c.size()) return false;
+    const mxp_vm_ins& r = c[pc0];
+    const mxp_vm_ins& f = c[pc0 + 1];
+    const mxp_vm_ins& d = c[pc0 + 2];
+    if (((r.op | f.op | d.op) & MXP_VM_WAKE) || opof(r) != VM_RES || r.y != W_S) return false;
+    if (opof(f) != VM_STRFNK || f.y != SF_STARTS || f.a != r.d) return false;
+    out->col = r.x;
+    out->k2 = f.x;
+    if (opof(d) == VM_RET && d.a == f.d && d.y == 1) {
+        out->direct = true;
+        out->cont = pc0 + 3;
+        return true;
+    }
+    if (opof(d) != VM_JZRET || d.a != f.d || d.y != 0) return false;
+    const uint32_t cont = pc0 + 3;
+    if (cont >= c.size()) return false;
+    // forward dataflow over the continuation: registers that may still hold r / s (never rewritten
+    // on some path from cont) must not be read
+    std::vector<uint32_t> stale(c.size() + 1, 0);
+    stale[cont] = (1u << r.d) | (1u << f.d);
+    for (size_t pc = cont; pc < c.size(); pc++) {
+        const mxp_vm_ins& i = c[pc];
+        const uint32_t st = stale[pc];
+        if (reads(i) & st) return false;
+        const uint32_t w = writes(i);
+        if (vm_is_jump(i)) {
+            // TRES / try-LOOKUP write d only on the jump path
+            if (i.z <= pc || i.z > c.size()) return false;
+            stale[i.z] |= st & ~w;
+            if (opof(i) != VM_JMP) stale[pc + 1] |= st;
+        } else if (!is_terminal(i)) {
+            stale[pc + 1] |= st & ~w;
+        }
+    }
+    out->direct = false;
+    out->cont = cont;
+    return true;
+}
+
 }  // namespace mxp

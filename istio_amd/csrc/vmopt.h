@@ -28,4 +28,18 @@ struct HoistedCont {
 };
 bool hoist_continuation(const std::vector<mxp_vm_ins>& code, uint32_t pc0, HoistedCont* out);
 
+// Second atom of an indexed `A == K1 && ...` rule: the continuation at pc0 starts with
+//   RES col (want S) -> r ; STRFNK startsWith(r, K2) -> s ; JZRET s, false   (more code follows)
+//                                                      or RET s (bool)      (the atom is the rest)
+// and no later instruction can read r or s before rewriting them, so a lane whose column value
+// starts with K2 may resume at `cont` with nothing else computed.  `direct`: the rule's result is
+// the atom (a matching prefix is a true pair).
+struct SecondAtom {
+    uint32_t col = 0;
+    uint32_t k2 = 0;    // prefix string id
+    uint32_t cont = 0;  // resume pc (JZRET form)
+    bool direct = false;
+};
+bool extract_second_prefix(const std::vector<mxp_vm_ins>& code, uint32_t pc0, SecondAtom* out);
+
 }  // namespace mxp

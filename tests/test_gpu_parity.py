@@ -38,8 +38,8 @@ def compare(engine, ev, rules, batch, sample_msgs=400, seed=0):
     want = oracle.oracle_matrix(ev, rules, batch, threads=16)
     want_err = np.where(want >= 2, 2, want)  # bitmaps carry error|panic in one bit
     bad = np.argwhere(got != want_err)
-    assert bad.size == 0, "first mismatches (req, rule): %s; rules: %s" % (
-        bad[:5].tolist(), [rules[j] for _, j in bad[:3]])
+    assert bad.size == 0, "first mismatches (req, rule, got, want): %s; rules: %s" % (
+        [(int(q), int(r), int(got[q, r]), int(want_err[q, r])) for q, r in bad[:5]], [rules[j] for _, j in bad[:3]])
     # error texts (and error-vs-panic class) for a sample of error pairs
     errs = np.argwhere(want >= 2)
     rng = np.random.default_rng(seed)
@@ -183,3 +183,59 @@ def test_device_resident_batch_and_hits(mxp):
     assert np.array_equal(de.cpu().numpy().view(np.uint32), err_h)
     codes = mxp.bits_to_codes(match_h, err_h, len(rules))
     assert np.array_equal(hits.cpu().numpy(), (codes == 1).sum(axis=0))
+
+
+@pytest.mark.parametrize("n", [1, 3, 64, 1001, 4100, 1 << 20, (1 << 20) + 7])
+def test_hits_counts_random_bitmaps(mxp, n):
+    """mxp_hits_device's bit-sliced counting against numpy on random bitmaps of every density: the
+    16-byte path (n % 4 == 0), the scalar path (ragged n) and partial last steps."""
+    import torch
+    rng = np.random.default_rng(n)
+    R = 70  # three words, the last one partial
+    Wd = (R + 31) // 32
+    dens = rng.choice([0.0, 0.01, 0.5, 0.99, 1.0], size=(Wd, 1, 32))
+    bits = rng.random((Wd, n, 32)) < dens
+    words = np.ascontiguousarray(np.packbits(bits, axis=2, bitorder="little")).view("<u4").reshape(Wd, n)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary({"a": "STRING"})
+    eng.compile(['a == "x"'] * R)
+    dm = torch.from_numpy(words.view(np.int32)).to("cuda:0")
+    hits = torch.full((R,), 5, dtype=torch.int64, device="cuda:0")
+    rc = eng.lib.mxp_hits_device(eng.h, dm.data_ptr(), n, torch.cuda.current_stream().cuda_stream, hits.data_ptr())
+    assert rc == 0
+    torch.cuda.synchronize()
+    want = bits.sum(axis=1).reshape(-1)[:R] + 5
+    assert np.array_equal(hits.cpu().numpy(), want)
+
+
+def composite_rules(n, seed=31):
+    """`A == K1 && B.startsWith(K2) [&& tail]` rules (composite index), mixed with look-alikes the
+    index must not take: a tail that re-reads B, `||` forms, negated atoms, VCOL columns."""
+    rng = np.random.default_rng(seed)
+    vals = W._STR_VALS
+    pre = ["", "a", "ab", "abc", "abcd", "st", "1.2", "10.0", "2015-01-02T", "*"]
+    tails = ["", ' && ai == %d' % 2, ' && aip != ip("1.2.3.4")', ' && bs == "abc"', ' && ab', ' || ai == 1',
+             ' && "^a".matches(bs)', ' && ar["a"] == "abc"']
+    out = []
+    for _ in range(n):
+        a = rng.choice(["as", "bs", 'ar["%s"]' % rng.choice(W._KEYS)])
+        b = rng.choice(["bs", "as", "bs"])
+        out.append('%s == "%s" && %s.startsWith("%s")%s' % (a, rng.choice(vals), b, rng.choice(pre),
+                                                           rng.choice(tails)))
+    return out
+
+
+def test_composite_index_parity(mxp):
+    """Composite guard index (A == K1 && B.startsWith(K2) && ...): B missing, of the wrong type,
+    shorter than K2, K2 empty, several K2 lengths per K1, direct and templated forms."""
+    rules = composite_rules(1500)
+    bags = W.fuzz_bags(6000, seed=33, p_missing=0.2, p_wrong=0.05)
+    batch = BagBatch.from_bags(bags, names=list(W.DEFAULT_TEST_MANIFEST))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
+    st = eng.compile(rules)
+    info = eng.ruleset_info()
+    assert info["composite"] > 400, info
+    ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
+    got, want = compare(eng, ev, rules, batch, sample_msgs=300)
+    assert (want == 1).sum() > 2000 and (want >= 2).sum() > 2000
