@@ -14,101 +14,144 @@
 
 namespace {
 
-__device__ void roll(const mxp_quota_args& A, uint32_t k, int64_t tick) {
-    const uint32_t len = A.ticks[k];
-    int64_t* slots = A.slots + A.slot_off[k];
-    int64_t behind = tick - A.win_tick[k];
-    if (behind > (int64_t)len) behind = len;
-    if (behind < 0) behind = 0;  // batch times are non-decreasing (the reference would index out of range)
-    uint32_t cur = A.win_cur[k];
-    for (int64_t i = 0; i < behind; i++) {
-        const uint32_t idx = (uint32_t)((cur + 1 + i) % len);
-        A.avail[k] += slots[idx];
-        slots[idx] = 0;
-    }
-    A.win_cur[k] = (uint32_t)((cur + behind) % len);
-    A.win_tick[k] = tick;
+// loads of per-key state the kernel also writes: relaxed atomics keep them on the vector memory path
+// (a uniform address would otherwise invite a scalar-cache load that cannot see the vector stores)
+__device__ __forceinline__ int64_t vload(const int64_t* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, uint32_t l) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)(uint64_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
 }
+
 
 }  // namespace
 
-// one lane per key: replay the key's requests (sorted by arrival) against its state
+// One wavefront per key.  A key's requests are sequential (each grant depends on the state the
+// previous one left), so the wave streams them 64 at a time -- order / amount / best-effort loaded
+// lane-parallel -- and replays them in order in scalar registers, the key's state (cell in-use, or
+// window avail + current slot) held in registers for the whole batch; granted amounts are written
+// back lane-parallel.  Window slots other than the current one are touched only by releases that
+// walk back past it.  The batch has one tick, so the window rolls once, at the key's first non-zero
+// request (later rolls in the batch are no-ops: rollingWindow.roll with behind == 0).
 extern "C" __global__ __launch_bounds__(256) void mxp_quota_kernel(mxp_quota_args A) {
-    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6);
     if (k >= A.n_keys) return;
     const uint32_t b = A.seg_start[k], e = A.seg_start[k + 1];
+    if (b == e) return;
     const int64_t maxv = A.max_amount[k];
-    const bool window = A.ticks[k] != 0;
-    int64_t delta = 0;
-    for (uint32_t j = b; j < e; j++) {
-        const uint32_t i = A.order[j];
-        int64_t amount = A.amount[i];
-        const bool be = A.best_effort[i] != 0;
-        int64_t result = 0;
-        if (amount > 0) {  // alloc
-            result = amount;
-            if (!window) {
-                const int64_t in_use = A.cells[k];
-                if (result > maxv - in_use) {
-                    if (!be) {
-                        result = 0;
-                        A.granted[i] = 0;
-                        continue;
-                    }
-                    result = maxv - in_use;  // grab as much as we can
-                }
-                A.cells[k] = in_use + result;
-            } else {
-                roll(A, k, A.tick);
-                if (result > A.avail[k]) {
-                    if (!be) {
-                        A.granted[i] = 0;
-                        continue;
-                    }
-                    result = A.avail[k];
-                }
-                A.slots[A.slot_off[k] + A.win_cur[k]] += result;
-                A.avail[k] -= result;
-            }
-            delta += result;
-        } else if (amount < 0) {  // free
-            amount = -amount;
-            result = amount;
-            if (!window) {
-                const int64_t in_use = A.cells[k];
-                if (result >= in_use) {
-                    A.cells[k] = 0;  // the cell is deleted: same as an empty one
-                    result = in_use;
-                } else {
-                    A.cells[k] = in_use - result;
-                }
-            } else {
-                // release from the leading edge of the window backwards (rollingWindow.release)
-                roll(A, k, A.tick);
-                const uint32_t len = A.ticks[k];
-                int64_t* slots = A.slots + A.slot_off[k];
-                int64_t total = 0;
-                int64_t idx = A.win_cur[k];
-                for (uint32_t s = 0; s < len; s++) {
-                    const int64_t av = slots[idx];
-                    if (av >= amount) {
-                        slots[idx] -= amount;
-                        total += amount;
-                        break;
-                    }
-                    slots[idx] = 0;
-                    total += av;
-                    amount -= av;
-                    idx = idx == 0 ? (int64_t)len - 1 : idx - 1;
-                }
-                A.avail[k] += total;
-                result = total;
-            }
-            delta -= result;
-        }
-        A.granted[i] = result;
+    const uint32_t len = A.ticks[k];
+    const bool window = len != 0;
+    int64_t* slots = window ? A.slots + A.slot_off[k] : nullptr;
+    int64_t in_use = 0, avail = 0, cur_val = 0;
+    uint32_t cur = 0;
+    bool rolled = false;
+    if (!window) {
+        in_use = vload(A.cells + k);
+    } else {
+        avail = vload(A.avail + k);
+        cur = (uint32_t)__atomic_load_n(A.win_cur + k, __ATOMIC_RELAXED);
     }
-    if (A.delta) A.delta[k] += delta;
+    int64_t delta = 0;
+    for (uint32_t base = b; base < e; base += 64u) {
+        const uint32_t j = base + lane;
+        const bool act = j < e;
+        const uint32_t i = act ? A.order[j] : 0u;
+        const int64_t amt = act ? A.amount[i] : 0;
+        const uint32_t bef = act ? (uint32_t)A.best_effort[i] : 0u;
+        int64_t res = 0;
+        const uint32_t cnt = min(64u, e - base);
+        for (uint32_t t = 0; t < cnt; t++) {
+            int64_t amount = readlane64(amt, t);
+            if (amount == 0) continue;  // HandleQuota: neither alloc nor free
+            if (window && !rolled) {
+                // rollingWindow.roll(currentTick): release the slots that fell out of the window
+                rolled = true;
+                int64_t behind = A.tick - vload(A.win_tick + k);
+                if (behind > (int64_t)len) behind = len;
+                if (behind < 0) behind = 0;  // batch times are non-decreasing (the reference would index out of range)
+                int64_t freed = 0;
+                for (int64_t c = 0; c < behind; c += 64) {
+                    int64_t v = 0;
+                    if (c + lane < behind) {
+                        int64_t* sp = slots + (uint32_t)((cur + 1 + c + lane) % len);
+                        v = vload(sp);
+                        __atomic_store_n(sp, (int64_t)0, __ATOMIC_RELAXED);
+                    }
+                    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+                    freed += readlane64(v, 0);
+                }
+                avail += freed;
+                // the new current slot is one of those just released (behind > 0) or unchanged
+                cur_val = behind > 0 ? 0 : readlane64(vload(slots + cur), 0);
+                cur = (uint32_t)((cur + behind) % len);
+                __threadfence_block();  // the walk below re-reads released slots from lane 0
+            }
+            const bool be = __builtin_amdgcn_readlane(bef, t) != 0;
+            int64_t result;
+            if (amount > 0) {  // alloc (memquota.go:119-171)
+                result = amount;
+                const int64_t room = window ? avail : maxv - in_use;
+                if (result > room) {
+                    if (!be) {
+                        res = lane == t ? 0 : res;
+                        continue;
+                    }
+                    result = room;  // best effort: grab what is left
+                }
+                if (window) {
+                    cur_val += result;
+                    avail -= result;
+                } else {
+                    in_use += result;
+                }
+                delta += result;
+            } else {  // free (memquota.go:173-214)
+                amount = -amount;
+                if (!window) {
+                    result = amount >= in_use ? in_use : amount;  // a cell freed entirely is deleted: same as empty
+                    in_use -= result;
+                } else {
+                    // rollingWindow.release: from the current slot backwards
+                    int64_t total = 0;
+                    uint32_t idx = cur;
+                    for (uint32_t s = 0; s < len; s++) {
+                        const int64_t av = idx == cur ? cur_val : readlane64(vload(slots + idx), 0);
+                        const int64_t nv = av >= amount ? av - amount : 0;
+                        if (idx == cur) {
+                            cur_val = nv;
+                        } else if (lane == 0) {
+                            __atomic_store_n(slots + idx, nv, __ATOMIC_RELAXED);
+                        }
+                        if (av >= amount) {
+                            total += amount;
+                            break;
+                        }
+                        total += av;
+                        amount -= av;
+                        idx = idx == 0 ? len - 1 : idx - 1;
+                    }
+                    avail += total;
+                    result = total;
+                }
+                delta -= result;
+            }
+            res = lane == t ? result : res;
+        }
+        if (act) A.granted[i] = res;
+    }
+    if (lane == 0) {
+        if (!window) {
+            A.cells[k] = in_use;
+        } else if (rolled) {
+            A.avail[k] = avail;
+            A.win_cur[k] = cur;
+            A.win_tick[k] = A.tick;
+            __atomic_store_n(slots + cur, cur_val, __ATOMIC_RELAXED);
+        }
+        if (A.delta) A.delta[k] += delta;
+    }
 }
 
 extern "C" __global__ void mxp_quota_iota(uint32_t* v, uint32_t n) {
@@ -135,6 +178,6 @@ extern "C" hipError_t mxp_launch_quota(const mxp_quota_args* a, const uint32_t* 
                                        hipStream_t s) {
     hipLaunchKernelGGL(mxp_quota_segments, dim3((a->n + 1 + 255) / 256), dim3(256), 0, s, skeys, a->n, a->n_keys,
                        seg_start);
-    hipLaunchKernelGGL(mxp_quota_kernel, dim3((a->n_keys + 255) / 256), dim3(256), 0, s, *a);
+    hipLaunchKernelGGL(mxp_quota_kernel, dim3((a->n_keys + 3) / 4), dim3(256), 0, s, *a);
     return hipGetLastError();
 }

@@ -8,7 +8,7 @@ out=gpurun_out/$1
 shift
 mkdir -p "$out"
 for c in FETCH_SIZE WRITE_SIZE; do
-    timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d "$out/$c" -o pmc -- \
+    timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$out/$c" -o pmc -- \
         python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 "$@" > "$out/$c.log" 2>&1
     rc=$?
     echo "pmc $c rc=$rc"

@@ -1,17 +1,25 @@
 #!/bin/bash
-# SQ counters (issue / wait breakdown, instruction mix) of the bench's kernels in one rocprofv3
-# --pmc pass (SQ has 8 slots on gfx950); counter list first, for reference.
+# SQ counters of the bench's kernels (issue / wait breakdown, instruction mix, LDS bank conflicts),
+# one rocprofv3 --pmc pass per group (SQ has 8 slots per pass on gfx950), each under its own limit.
+#   bash tools/sq_session.sh <outdir> [bench args]
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 out=gpurun_out/$1
 shift
 mkdir -p "$out"
-timeout -k 10 120 rocprofv3 -L > "$out/counters.txt" 2>&1 || true
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU \
-    --output-format csv -d "$out/sq1" -o pmc -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 "$@" > "$out/sq1.log" 2>&1
-rc=$?; echo "sq1 rc=$rc"; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_SENDMSG SQ_INST_CYCLES_SALU \
-    --output-format csv -d "$out/sq2" -o pmc -- python3 bench.py --no-cpu-baseline --steps 3 --warmup 1 "$@" > "$out/sq2.log" 2>&1
-rc=$?; echo "sq2 rc=$rc"
-exit $rc
+passes=(
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"
+  "SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_BRANCH"
+)
+i=0
+for p in "${passes[@]}"; do
+    i=$((i + 1))
+    timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d "$out/sq$i" -o pmc -- \
+        python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 "$@" > "$out/sq$i.log" 2>&1
+    rc=$?
+    echo "sq$i rc=$rc"
+    [ $rc -ne 0 ] && exit $rc
+done
+python3 tools/pmc_table.py "$out"/sq* > "$out/sq_table.txt"
+cat "$out/sq_table.txt"
