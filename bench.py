@@ -60,7 +60,7 @@ def cpu_baseline(manifest, rules, batch, seconds, threads, chunk=256):
                 done, len(rules), dt)}
 
 
-def measured_traffic(rules, requests):
+def measured_traffic(workload, rules, requests):
     """HBM bytes per evaluation from the committed PMC profile (tools/pmc_summarize.py: FETCH_SIZE
     and WRITE_SIZE in separate rocprofv3 passes, FETCH doubled for gfx950), when one exists for this
     workload size; else None."""
@@ -68,7 +68,7 @@ def measured_traffic(rules, requests):
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
-    if d.get("rules") != rules or d.get("requests") != requests:
+    if d.get("workload", "c2") != workload or d.get("rules") != rules or d.get("requests") != requests:
         return None
     return d.get("bytes_per_eval")
 
@@ -337,7 +337,7 @@ def main():
     prog_bytes = 16 * sum(eng.rule_vm_text(i).count("\n") for i in range(R)) + 4 * (R + 1)
     alg_bytes = N * n_cols * 9 + prog_bytes + 2 * N * Wd * 4
     achieved = alg_bytes / (eval_ms * 1e-3) / 1e9
-    traffic = measured_traffic(R, N)
+    traffic = measured_traffic(args.workload, R, N)
 
     out = {
         "metric": metric,

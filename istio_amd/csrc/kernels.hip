@@ -54,6 +54,19 @@ __device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
     return sh == 0 ? lo : (lo >> sh) | (q[1] << (64u - sh));
 }
 
+// 8 bytes at an 8-aligned address (string starts in the pools, and whole words after them)
+__device__ __forceinline__ uint64_t ld8a(const uint8_t* p) { return *(const uint64_t*)p; }
+
+// equality of n bytes at two 8-aligned addresses
+__device__ __forceinline__ bool bytes_eq_a(const uint8_t* a, const uint8_t* b, uint32_t n) {
+    uint32_t i = 0;
+    for (; i + 8 <= n; i += 8)
+        if (ld8a(a + i) != ld8a(b + i)) return false;
+    if (i == n) return true;
+    const uint64_t mask = (1ull << ((n - i) * 8u)) - 1ull;
+    return ((ld8a(a + i) ^ ld8a(b + i)) & mask) == 0;
+}
+
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, uint32_t n) {
     uint32_t i = 0;
     for (; i + 8 <= n; i += 8)
@@ -569,6 +582,101 @@ __device__ void run_postings(const mxp_kargs& A, const uint32_t* __restrict__ tm
     }
 }
 
+// In-wave pair queue (LDS): the postings the probes find are appended as (rule, request) pairs and
+// run 64 at a time -- one pair per lane, lanes sharing a template together -- so the VM runs on
+// dense wavefronts however sparse the hits are per request.  Entry: rule | table << 31 (table 1:
+// kargs.rule_tmpl2, the composite resume point), request.
+#define MXP_IXQ 256u
+__shared__ uint32_t g_ixq[4][MXP_IXQ][2];  // per wave of the index kernel's workgroup
+struct PairQueue {
+    uint32_t wave;
+    uint32_t n;        // pending entries (wave-uniform)
+};
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// run entries [off, off + cnt) of the queue, cnt <= 64
+__device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32_t cnt, uint64_t (*regs)[256],
+                          uint32_t tid) {
+    const uint64_t N = A.n;
+    const uint32_t lane = tid & 63u;
+    wave_sync_lds();
+    bool pending = lane < cnt;
+    uint32_t rule = 0, req = 0, t = MXP_VM_DONE;
+    if (pending) {
+        const uint32_t e = g_ixq[Q.wave][off + lane][0];
+        req = g_ixq[Q.wave][off + lane][1];
+        pending = e != 0xFFFFFFFFu;  // a direct posting, already OR-ed
+        rule = e & 0x7FFFFFFFu;
+        if (pending) t = (e >> 31) ? A.rule_tmpl2[rule] : A.rule_tmpl[rule];
+    }
+    wave_sync_lds();
+    for (uint64_t bal = __ballot(pending); bal; bal = __ballot(pending)) {
+        const uint32_t tt = __builtin_amdgcn_readlane(t, (uint32_t)__builtin_ctzll(bal));
+        const bool mine = pending && t == tt;
+        const mxp_tmpl* T = A.tmpls + tt;
+        const uint32_t toff = uni(T->off), pc0 = uni(T->pc0), len_t = uni(T->len), nconst = uni(T->nconst),
+                       creg0 = uni(T->creg0);
+        if (mine)
+            for (uint32_t c = 0; c < nconst; c++) regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
+        cuint32* P = ((cuint32*)A.prog) + ((uint64_t)toff - pc0) * 4u;
+        const uint32_t code = run_rule(A, P, len_t, pc0, mine, rule, req, regs, tid);
+        if (mine) {
+            const uint64_t w = (uint64_t)(rule >> 5) * N + req;
+            const uint32_t bit = 1u << (rule & 31u);
+            if (code == PC_TRUE && A.out_match) atomicOr(A.out_match + w, bit);
+            if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
+        }
+        pending = pending && !mine;
+    }
+}
+
+// Appends every lane's postings [start, start + len) to the queue (direct postings are true pairs:
+// OR-ed at once) and runs full 64-pair batches; `final` drains the queue.  Long lists go in rounds
+// of up to (free entries / 64) postings per lane, so the queue never overflows and the VM has one
+// call site (one inlined copy).
+__device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, uint32_t tbl, uint32_t start,
+                                             uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
+                                             uint32_t tid) {
+    const uint32_t lane = tid & 63u;
+    const uint64_t N = A.n;
+    const uint32_t* __restrict__ tmpl_of = tbl ? A.rule_tmpl2 : A.rule_tmpl;
+    uint32_t j0 = 0;
+    for (;;) {
+        if (Q.n < 64u && __ballot(j0 < len)) {
+            const uint32_t c = (MXP_IXQ - Q.n) / 64u;  // >= 3
+            const uint32_t take = min(len - j0, c);
+            const uint32_t incl = wave_incl_sum(take, lane);
+            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+            const uint32_t base = Q.n + incl - take;
+            for (uint32_t j = 0; j < take; j++) {
+                const uint32_t rule = A.postings[start + j0 + j];
+                uint32_t e = rule | (tbl << 31);
+                if (tmpl_of[rule] == MXP_TMPL_DIRECT) {
+                    if (A.out_match) atomicOr(A.out_match + (uint64_t)(rule >> 5) * N + req, 1u << (rule & 31u));
+                    e = 0xFFFFFFFFu;
+                }
+                g_ixq[Q.wave][base + j][0] = e;
+                g_ixq[Q.wave][base + j][1] = req;
+            }
+            j0 += take;
+            Q.n += total;
+        }
+        const bool more = __ballot(j0 < len) != 0;
+        if (Q.n >= 64u || (Q.n > 0u && (final || more))) {
+            const uint32_t k = min(Q.n, 64u);
+            run_pairs(A, Q, Q.n - k, k, regs, tid);
+            Q.n -= k;
+            continue;
+        }
+        if (!more) break;
+    }
+}
+
 // equality probe: postings of the entry whose key is v (len 0: none)
 __device__ __forceinline__ void eq_probe(const mxp_kargs& A, uint32_t hoff, uint32_t hmask, uint64_t v, uint32_t& start,
                                          uint32_t& len) {
@@ -594,10 +702,10 @@ struct PrefixHash {
     uint64_t h;
     uint32_t words;
     __device__ __forceinline__ uint64_t at(const uint8_t* p, uint32_t L) {
-        for (; (words + 1) * 8u <= L; words++) h = mxp_str_step(h, ld8(p + words * 8u));
+        for (; (words + 1) * 8u <= L; words++) h = mxp_str_step(h, ld8a(p + words * 8u));
         uint64_t hl = h;
         const uint32_t rem = L - words * 8u;
-        if (rem) hl = mxp_str_step(hl, ld8(p + words * 8u) & ((1ull << (rem * 8u)) - 1ull));
+        if (rem) hl = mxp_str_step(hl, ld8a(p + words * 8u) & ((1ull << (rem * 8u)) - 1ull));
         return mxp_str_final(hl, L);
     }
 };
@@ -611,15 +719,18 @@ struct PrefixHash {
 // Workgroup = 4 wavefronts, one tile of 64 requests each (one request per lane).  mxp_eval_kernel
 // has already written both bitmaps for these rules (match 0, error on a failed type check of the
 // guard column); true and error results are OR-ed in.
-extern "C" __global__ __launch_bounds__(256) void mxp_index_kernel(mxp_kargs A) {
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
+    PairQueue Q{wave, 0u};
     const uint32_t req = (blockIdx.x * 4u + wave) * 64u + (tid & 63u);
     const bool valid = req < A.n;
     const uint64_t N = A.n;
-    for (uint32_t x = 0; x < A.n_idx; x++) {
-        const mxp_index* X = A.idx + x;
+    // x == n_idx: a last pass with no probes that drains the pair queue
+    for (uint32_t x = 0; x <= A.n_idx; x++) {
+        const bool final = x == A.n_idx;
+        const mxp_index* X = A.idx + (final ? 0u : x);
         const uint32_t col = uni(X->col), okset = uni(X->okset), hmask = uni(X->hmask), hoff = uni(X->hoff),
                        kind = uni(X->prefix), plen0 = uni(X->plen0), nplen = uni(X->nplen);
         const bool comp = kind == MXP_IX_COMPOSITE;
@@ -652,11 +763,12 @@ extern "C" __global__ __launch_bounds__(256) void mxp_index_kernel(mxp_kargs A) 
         const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
         // probe slots: equality 1; prefix one per key length (shortest first); composite the
         // equality fallback, then one per K2 length
-        const uint32_t nslot = kind == MXP_IX_EQ ? 1u : nplen + (comp ? 1u : 0u);
+        const uint32_t nslot = final ? 1u : kind == MXP_IX_EQ ? 1u : nplen + (comp ? 1u : 0u);
         for (uint32_t p = 0; p < nslot; p++) {
             uint32_t start = 0, len = 0;
             const bool eq_slot = kind == MXP_IX_EQ || (comp && p == 0);
-            if (eq_slot) {
+            if (final) {
+            } else if (eq_slot) {
                 if (ok && (!comp || !sok)) eq_probe(A, hoff, hmask, v, start, len);
             } else {
                 const uint32_t L = uni(A.plens[plen0 + p - (comp ? 1u : 0u)]);
@@ -678,7 +790,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_index_kernel(mxp_kargs A) 
                             if (K.klo != vlo || K.khi != vhi) continue;
                         }
                         const StrRef k = str_of(A, E.klo);
-                        if (k.n == L && bytes_eq(s.p, k.p, L)) {
+                        if (k.n == L && bytes_eq_a(s.p, k.p, L)) {
                             fi = at;
                             break;
                         }
@@ -689,8 +801,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_index_kernel(mxp_kargs A) 
                     len = A.hents[fi].len;
                 }
             }
-            if (__ballot(len != 0))
-                run_postings(A, comp && p > 0 ? A.rule_tmpl2 : A.rule_tmpl, start, len, req, regs, tid);
+            if (final || __ballot(len != 0)) process_slot(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
         }
     }
 }

@@ -36,6 +36,7 @@ def main():
     p.add_argument("dir")
     p.add_argument("--rules", type=int, default=10000)
     p.add_argument("--requests", type=int, default=1 << 20)
+    p.add_argument("--workload", default="c2")
     a, _ = p.parse_known_args()
     fetch = per_kernel(os.path.join(a.dir, "FETCH_SIZE", "**", "*counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(a.dir, "WRITE_SIZE", "**", "*counter_collection.csv"), "WRITE_SIZE")
@@ -45,7 +46,7 @@ def main():
         table[k] = {"fetch_size_bytes": f, "write_size_bytes": w, "hbm_bytes": 2 * f + w}
         print("%-60s fetch %.4g B  write %.4g B  hbm(2F+W) %.4g B" % (k[:60], f, w, 2 * f + w))
     ev = {k: v for k, v in table.items() if any(k.startswith(e) for e in EVAL_KERNELS)}
-    out = {"rules": a.rules, "requests": a.requests, "kernels": ev,
+    out = {"workload": a.workload, "rules": a.rules, "requests": a.requests, "kernels": ev,
            "bytes_per_eval": sum(v["hbm_bytes"] for v in ev.values()) if ev else None,
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE separate passes; hbm = 2*FETCH + WRITE (gfx950)"}
     json.dump(out, open(os.path.join(a.dir, "pmc_traffic.json"), "w"), indent=1)
