@@ -292,11 +292,10 @@ def main():
     def step(ev0=None, ev1=None):
         if ev0 is not None:
             ev0.record(stream)
-        db.eval(d_match.data_ptr(), d_err.data_ptr(), sh)
+        # evaluation with the per-rule hit counters fused into the evaluation kernels
+        db.eval_hits(d_match.data_ptr(), d_err.data_ptr(), hits.data_ptr(), sh)
         if ev1 is not None:
             ev1.record(stream)
-        rc = eng.lib.mxp_hits_device(eng.h, d_match.data_ptr(), N, sh, hits.data_ptr())
-        assert rc == 0
         D.reduce_counters(hits)  # RCCL over xGMI when world > 1: per-rule hit counters
 
     for _ in range(args.warmup):

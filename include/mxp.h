@@ -207,6 +207,11 @@ typedef struct mxp_dbatch mxp_dbatch;
 int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out);
 void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db);
 int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err);
+/* mxp_batch_eval_device plus fused per-rule hit counters: d_hits[rule] += the requests of this batch
+ * whose predicate was true (device u64[n_rules], accumulated by the evaluation kernels as they set
+ * the match bits -- the bitmap is not read back).  Same result as mxp_hits_device afterwards. */
+int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err,
+                               unsigned long long* d_hits);
 /* Per-rule hit counters: d_hits[rule] += number of requests whose predicate was true (device u64[n_rules]). */
 int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_requests, void* stream,
                     unsigned long long* d_hits);

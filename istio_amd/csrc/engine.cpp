@@ -338,10 +338,32 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         G.vm = ((G.all & ~G.guarded) | G.orm | (andm & ~G.indexed)) != 0;
     }
     std::vector<uint32_t> glean, gvm, gall(W);
+    std::vector<mxp_fill> fills;
+    n_gfill = 0;
     for (uint32_t g = 0; g < W; g++) {
         gall[g] = g;
-        (groups[g].vm ? gvm : glean).push_back(g);
+        const mxp_group& G = groups[g];
+        // uniform indexed group: every rule indexed, one guard column, nothing compared in-wave
+        const bool uniform = !G.vm && G.all && G.indexed == G.all && G.guarded == G.all && G.nseg == 1 &&
+                             G.s_cmp == 0 && G.s_rules == G.all && !(debug_flags & 32u);
+        if (uniform) {
+            mxp_fill* F = fills.empty() ? nullptr : &fills.back();
+            if (F && F->col == G.s_col && F->okset == G.s_okset && F->g0 + F->n == g && F->n < MXP_FILL_CHUNK &&
+                F->last == F->all && G.all == F->all) {
+                F->n++;
+            } else if (F && F->col == G.s_col && F->okset == G.s_okset && F->g0 + F->n == g && F->n < MXP_FILL_CHUNK &&
+                       F->last == F->all) {
+                F->n++;
+                F->last = G.all;
+            } else {
+                fills.push_back(mxp_fill{G.s_col, G.s_okset, g, 1, G.all, G.all, {0, 0}});
+            }
+            n_gfill++;
+            continue;
+        }
+        (G.vm ? gvm : glean).push_back(g);
     }
+    n_fills = (uint32_t)fills.size();
     n_glean = (uint32_t)glean.size();
     n_gvm = (uint32_t)gvm.size();
     n_segs = (uint32_t)segs.size();
@@ -364,6 +386,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_groups, groups.data(), groups.size() * sizeof(mxp_group), "upload groups"))) return rc;
     if ((rc = put(d_segs, segs.data(), segs.size() * sizeof(mxp_seg), "upload segs"))) return rc;
     if ((rc = put(d_glean, glean.data(), glean.size() * 4, "upload glean"))) return rc;
+    if ((rc = put(d_fills, fills.data(), fills.size() * sizeof(mxp_fill), "upload fills"))) return rc;
     if ((rc = put(d_gvm, gvm.data(), gvm.size() * 4, "upload gvm"))) return rc;
     if ((rc = put(d_gall, gall.data(), gall.size() * 4, "upload gall"))) return rc;
     if ((rc = put(d_gk, gk.data(), gk.size() * 8, "upload gk"))) return rc;
@@ -652,9 +675,10 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
 }
 
 int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
-                       bool log) {
+                       bool log, unsigned long long* d_hits) {
     mxp_kargs A;
     fill_args(&A, db);
+    A.hits = d_vals ? nullptr : d_hits;
     A.out_match = d_match;
     A.out_err = d_err;
     A.out_vals = d_vals;
@@ -685,6 +709,10 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         int vm;
     } parts[2] = {{guards_on ? &d_glean : &d_gall, guards_on ? n_glean : 0u, 0},
                   {guards_on ? &d_gvm : &d_gall, guards_on ? n_gvm : A.n_words, 1}};
+    if (guards_on && n_fills) {
+        A.fills = d_fills.as<mxp_fill>();
+        if ((e = mxp_launch_fill(&A, n_fills, s)) != hipSuccess) return hipfail(e, "launch fill");
+    }
     for (const Part& P : parts) {
         if (!P.n) continue;
         A.glist = P.list->as<uint32_t>();
@@ -916,6 +944,13 @@ int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_
     if (!eng || !db || !d_match || !d_err) return MXP_ERR_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     return eng->launch(db, s, d_match, d_err, nullptr, false);
+}
+
+int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err,
+                               unsigned long long* d_hits) {
+    if (!eng || !db || !d_match || !d_err || !d_hits) return MXP_ERR_ARG;
+    hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
+    return eng->launch(db, s, d_match, d_err, nullptr, false, d_hits);
 }
 
 int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_requests, void* stream,

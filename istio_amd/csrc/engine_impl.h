@@ -25,6 +25,7 @@
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
+extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
                                       unsigned long long* hits, hipStream_t s);
 
@@ -143,6 +144,8 @@ struct mxp_engine : public mxp::LowerTables {
     DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_rconst, d_idx, d_hents, d_postings, d_plens;
     DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
     uint32_t n_glean = 0, n_gvm = 0;
+    DevBuf d_fills;                 // chunks of uniform indexed groups (mxp_fill_kernel)
+    uint32_t n_fills = 0, n_gfill = 0;
     uint32_t n_idx = 0, n_indexed = 0, n_composite = 0;
     uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
     uint32_t groups_per_wave = 4; // MXP_GPW
@@ -284,7 +287,8 @@ struct mxp_engine : public mxp::LowerTables {
     int collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_dbatch>& db);
     int pack(const mxp_bag_batch* b, mxp_dbatch* db);
     void fill_args(mxp_kargs* A, const mxp_dbatch* db) const;
-    int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log);
+    int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
+               unsigned long long* d_hits = nullptr);
     std::string format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r) const;
     std::string string_of(const mxp_dbatch* db, uint64_t sid) const {
         if (!db) db = last_db.get();

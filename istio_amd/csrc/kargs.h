@@ -18,6 +18,7 @@ typedef struct mxp_kargs {
     const mxp_guard* guards;     // [n_rules] leading-atom guards (vmopt.h)
     const mxp_group* groups;     // [n_words] per-group guard masks
     const uint32_t* glist;       // groups this launch evaluates (ids into groups)
+    const mxp_fill* fills;       // mxp_fill_kernel: chunks of uniform indexed groups
     uint32_t n_glist;
     uint32_t pad3;
     const mxp_seg* segs;         // column segments of the groups
@@ -63,6 +64,7 @@ typedef struct mxp_kargs {
     uint32_t* out_match;         // [n_words][n]
     uint32_t* out_err;           // [n_words][n]
     uint64_t* out_vals;          // optional [n][n_rules] result registers (Eval)
+    unsigned long long* hits;    // optional [n_rules] += true pairs of this evaluation (fused hit counters)
     mxp_err_rec* errlog;
     uint32_t* errcount;
     uint32_t errcap;

@@ -99,6 +99,19 @@ __device__ __forceinline__ void log_err(const mxp_kargs& A, uint32_t req, uint32
     }
 }
 
+// a true pair found after phase 1 (guard-index kernel): OR its match bit in and, when the caller
+// asked for fused hit counters, count it once (the bit was not set before)
+__device__ __forceinline__ void set_true(const mxp_kargs& A, uint32_t rule, uint32_t req) {
+    if (!A.out_match) return;
+    const uint32_t bit = 1u << (rule & 31u);
+    uint32_t* w = A.out_match + (uint64_t)(rule >> 5) * A.n + req;
+    if (A.hits) {
+        if (!(atomicOr(w, bit) & bit)) atomicAdd(A.hits + rule, 1ull);
+    } else {
+        atomicOr(w, bit);
+    }
+}
+
 // constant-address-space views: uniform loads through them become scalar s_load_dwordxN
 typedef __attribute__((address_space(4))) const uint32_t cuint32;
 
@@ -526,6 +539,14 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
                 if (A.out_match) A.out_match[(uint64_t)g * N + req] = m;
                 if (A.out_err) A.out_err[(uint64_t)g * N + req] = e;
             }
+            if (A.hits) {
+                // fused hit counters: per rule of the group, the lanes whose match bit is set
+                for (uint32_t bits = wave_or(m); bits; bits &= bits - 1) {
+                    const uint32_t k = __builtin_ctz(bits);
+                    const uint32_t c = (uint32_t)__builtin_popcountll(__ballot((m >> k) & 1u));
+                    if (lane == 0) atomicAdd(A.hits + r0 + k, (unsigned long long)c);
+                }
+            }
         }
     }
 }
@@ -536,6 +557,56 @@ extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
 }
 
 extern "C" __global__ __launch_bounds__(256) void mxp_guard_kernel(mxp_kargs A) { eval_groups<false>(A, nullptr); }
+
+// Chunks of uniform indexed groups (vm.h mxp_fill): every word is a function of the guard column's
+// kind alone -- match 0, error = the rules whose type check fails -- so a lane computes it once for
+// each of its four requests and streams 16-byte stores over the chunk's groups (1 KB per
+// wave-instruction).  Workgroup = 4 waves x 256 requests; grid y = chunk.
+extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uni(threadIdx.x >> 6);
+    const mxp_fill* F = A.fills + blockIdx.y;
+    const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), all = uni(F->all),
+                   last = uni(F->last);
+    const uint64_t N = A.n;
+    const uint32_t q0 = (blockIdx.x * 4u + wave) * 256u + lane * 4u;
+    if (q0 >= N) return;
+    const bool vec = (N & 3u) == 0;  // rows 16-byte aligned, the lane's 4 requests all present
+    uint32_t bad[4];                 // per request: ~0 when the guard column fails its type check
+    if (vec) {
+        const uint32_t k4 = *(const uint32_t*)(A.kinds + (uint64_t)col * N + q0);
+#pragma unroll
+        for (int r = 0; r < 4; r++) bad[r] = ((okset >> ((k4 >> (8 * r)) & 0xFFu)) & 1u) ? 0u : ~0u;
+    } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool in = q0 + r < N;
+            const uint32_t k = in ? A.kinds[(uint64_t)col * N + q0 + r] : 0u;
+            bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
+        }
+    }
+    if (A.errlog && (bad[0] | bad[1] | bad[2] | bad[3])) {
+        for (uint32_t g = 0; g < n; g++) {
+            const uint32_t mask = g + 1 == n ? last : all;
+            for (uint32_t r = 0; r < 4; r++)
+                if (bad[r] && q0 + r < N) log_guard_errors(A, mask, (g0 + g) * 32u, q0 + r);
+        }
+    }
+    for (uint32_t g = 0; g < n; g++) {
+        const uint32_t mask = g + 1 == n ? last : all;
+        const uint64_t at = (uint64_t)(g0 + g) * N + q0;
+        if (vec) {
+            if (A.out_match) *(uint4*)(A.out_match + at) = make_uint4(0, 0, 0, 0);
+            if (A.out_err) *(uint4*)(A.out_err + at) = make_uint4(bad[0] & mask, bad[1] & mask, bad[2] & mask, bad[3] & mask);
+        } else {
+            for (uint32_t r = 0; r < 4; r++) {
+                if (q0 + r >= N) break;
+                if (A.out_match) A.out_match[at + r] = 0u;
+                if (A.out_err) A.out_err[at + r] = bad[r] & mask;
+            }
+        }
+    }
+}
 
 // Guard-index phase: the continuing pairs of indexed rules (`attr == K && <continuation>`), found
 // per request by a hash lookup of its column value instead of by comparing against every rule.
@@ -558,7 +629,7 @@ __device__ void run_postings(const mxp_kargs& A, const uint32_t* __restrict__ tm
         const uint32_t rule = pending ? A.postings[start + j] : 0u;
         const uint32_t t = pending ? tmpl_of[rule] : MXP_VM_DONE;
         if (pending && t == MXP_TMPL_DIRECT) {
-            if (A.out_match) atomicOr(A.out_match + (uint64_t)(rule >> 5) * N + req, 1u << (rule & 31u));
+            set_true(A, rule, req);
             pending = false;
         }
         for (uint64_t bal = __ballot(pending); bal; bal = __ballot(pending)) {
@@ -574,7 +645,7 @@ __device__ void run_postings(const mxp_kargs& A, const uint32_t* __restrict__ tm
             if (mine) {
                 const uint64_t w = (uint64_t)(rule >> 5) * N + req;
                 const uint32_t bit = 1u << (rule & 31u);
-                if (code == PC_TRUE && A.out_match) atomicOr(A.out_match + w, bit);
+                if (code == PC_TRUE) set_true(A, rule, req);
                 if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
             }
             pending = pending && !mine;
@@ -628,7 +699,7 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
         if (mine) {
             const uint64_t w = (uint64_t)(rule >> 5) * N + req;
             const uint32_t bit = 1u << (rule & 31u);
-            if (code == PC_TRUE && A.out_match) atomicOr(A.out_match + w, bit);
+            if (code == PC_TRUE) set_true(A, rule, req);
             if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
         }
         pending = pending && !mine;
@@ -657,7 +728,7 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
                 const uint32_t rule = A.postings[start + j0 + j];
                 uint32_t e = rule | (tbl << 31);
                 if (tmpl_of[rule] == MXP_TMPL_DIRECT) {
-                    if (A.out_match) atomicOr(A.out_match + (uint64_t)(rule >> 5) * N + req, 1u << (rule & 31u));
+                    set_true(A, rule, req);
                     e = 0xFFFFFFFFu;
                 }
                 g_ixq[Q.wave][base + j][0] = e;
@@ -918,6 +989,11 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
         hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
     else
         hipLaunchKernelGGL(mxp_guard_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_fill_kernel, dim3((args->n + 1023) / 1024, n_fills), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

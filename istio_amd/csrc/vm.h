@@ -134,6 +134,22 @@ typedef struct mxp_hent {
     uint32_t len;
 } mxp_hent;
 
+// A chunk of consecutive lean groups whose rules are all served by guard indexes and whose guards all
+// read one column: in phase 1 their words depend only on that column's kind (match 0, error where
+// the guard's type check fails), so mxp_fill_kernel computes them once per request and streams the
+// stores.  Groups g0 .. g0 + n - 1 (n <= MXP_FILL_CHUNK), `all` = rules present in every group but
+// the last, `last` = those of the last.
+#define MXP_FILL_CHUNK 32u
+typedef struct mxp_fill {
+    uint32_t col;
+    uint32_t okset;    // bits 0..15: kinds that pass; bits 24..31: want class / GK_VCOL
+    uint32_t g0;
+    uint32_t n;
+    uint32_t all;
+    uint32_t last;
+    uint32_t pad[2];
+} mxp_fill;
+
 // kargs.rule_tmpl value of indexed rules whose atom IS the result (`col.startsWith(K)` alone): a
 // posting is a true pair, no continuation to run
 #define MXP_TMPL_DIRECT 0xFFFFFFFEu

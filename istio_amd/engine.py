@@ -73,6 +73,7 @@ SIGNATURES = {
     "mxp_quota_alloc_device": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p]),
+    "mxp_batch_eval_device_hits": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     "mxp_set_timing": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
@@ -309,6 +310,12 @@ class DeviceBatch:
         e = self.engine
         e._check(e.lib.mxp_batch_eval_device(e.h, self.h, _VP(stream or None), _VP(d_match), _VP(d_err)),
                  "mxp_batch_eval_device")
+
+    def eval_hits(self, d_match: int, d_err: int, d_hits: int, stream: int = 0):
+        """eval() plus fused per-rule hit counters: d_hits[rule] += true pairs (device u64)."""
+        e = self.engine
+        e._check(e.lib.mxp_batch_eval_device_hits(e.h, self.h, _VP(stream or None), _VP(d_match), _VP(d_err),
+                                                  _VP(d_hits)), "mxp_batch_eval_device_hits")
 
     def free(self):
         if self.h:

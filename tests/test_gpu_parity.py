@@ -239,3 +239,49 @@ def test_composite_index_parity(mxp):
     ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
     got, want = compare(eng, ev, rules, batch, sample_msgs=300)
     assert (want == 1).sum() > 2000 and (want >= 2).sum() > 2000
+
+
+@pytest.mark.parametrize("n", [1, 5, 1001, 4099])
+def test_c2_ragged_batches(mxp, n):
+    """Uniform indexed groups (mxp_fill_kernel) and the pair queue at batch sizes that are not a
+    multiple of the 4-request lane width or of a wavefront; error texts from the log."""
+    manifest, rules, batch = W.c2_workload(n_rules=333, n_requests=n, seed=7)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    ev = oracle.OracleEvaluator(manifest)
+    compare(eng, ev, rules, batch, sample_msgs=100)
+
+
+@pytest.mark.parametrize("family", ["c2", "fuzz"])
+def test_fused_hit_counters(mxp, family):
+    """mxp_batch_eval_device_hits: counters accumulated by the evaluation kernels (fill / guard / VM
+    kernels by ballot, index kernel per newly set bit) equal the true pairs of the bitmaps, and the
+    bitmaps equal the plain device evaluation's."""
+    import torch
+    if family == "c2":
+        manifest, rules, batch = W.c2_workload(n_rules=700, n_requests=30000)
+    else:
+        manifest = W.DEFAULT_TEST_MANIFEST
+        rules = W.guarded_fuzz_rules(1500, seed=41)
+        batch = BagBatch.from_bags(W.fuzz_bags(5000, seed=42), names=list(manifest))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    db = eng.upload(batch)
+    Wd = (len(rules) + 31) // 32
+    dm = torch.zeros((Wd, batch.n), dtype=torch.int32, device="cuda:0")
+    de = torch.zeros_like(dm)
+    dm2, de2 = torch.zeros_like(dm), torch.zeros_like(dm)
+    hits = torch.full((len(rules),), 3, dtype=torch.int64, device="cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s)
+    db.eval(dm2.data_ptr(), de2.data_ptr(), s)
+    torch.cuda.synchronize()
+    m = dm.cpu().numpy().view(np.uint32)
+    assert np.array_equal(m, dm2.cpu().numpy().view(np.uint32))
+    assert np.array_equal(de.cpu().numpy(), de2.cpu().numpy())
+    codes = mxp.bits_to_codes(m, de.cpu().numpy().view(np.uint32), len(rules))
+    want = (codes == 1).sum(axis=0) + 3
+    assert want.sum() > 3 * len(rules)
+    assert np.array_equal(hits.cpu().numpy(), want)
