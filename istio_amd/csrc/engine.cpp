@@ -151,6 +151,12 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     std::map<std::pair<uint32_t, uint32_t>, uint32_t> tmpl2_ids;  // (template, resume pc) -> template
     n_indexed = 0;
     n_composite = 0;
+    // duplicate predicates: indexed rules whose programs are identical (same code, same constants)
+    // compute identical results, so only the first one (the canonical rule) enters the index; each
+    // result the index kernel produces for it is fanned out to its aliases (kargs.alias_off / aliases)
+    std::unordered_map<std::string, uint32_t> canon_of;
+    std::vector<std::vector<uint32_t>> aliases_of(n);
+    n_alias = 0;
     for (uint32_t i = 0; i < n; i++) {
         mxp_guard& gd = guards[i];
         const uint32_t mode = gd.mode & 0xFF;
@@ -167,6 +173,16 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         if (prefix && mode == GM_ONLY) rule_tmpl[i] = MXP_TMPL_DIRECT;
         indexed[i] = 1;
         n_indexed++;
+        if (!(debug_flags & 64u)) {
+            std::string key((const char*)&gd, sizeof gd);
+            key.append((const char*)(all.data() + off[i]), (size_t)(off[i + 1] - off[i]) * sizeof(mxp_vm_ins));
+            auto ins = canon_of.emplace(std::move(key), i);
+            if (!ins.second) {
+                aliases_of[ins.first->second].push_back(i);
+                n_alias++;
+                continue;
+            }
+        }
         const uint64_t k1 = (uint64_t)gd.klo | ((uint64_t)gd.khi << 32);
         mxp::SecondAtom sa;
         std::vector<mxp_vm_ins> code(all.begin() + off[i], all.begin() + off[i + 1]);
@@ -290,6 +306,14 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         idx.push_back(x);
     }
     n_idx = (uint32_t)idx.size();
+    std::vector<uint32_t> alias_off(n_alias ? n + 1 : 0, 0), alias_list;
+    if (n_alias) {
+        for (uint32_t i = 0; i < n; i++) {
+            alias_off[i] = (uint32_t)alias_list.size();
+            alias_list.insert(alias_list.end(), aliases_of[i].begin(), aliases_of[i].end());
+        }
+        alias_off[n] = (uint32_t)alias_list.size();
+    }
 
     // phase-1 group tables: mode masks, column segments, guard constants
     const uint32_t W = (n + 31) / 32;
@@ -397,6 +421,8 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_tmpls, tmpls.data(), tmpls.size() * sizeof(mxp_tmpl), "upload tmpls"))) return rc;
     if ((rc = put(d_rule_tmpl, rule_tmpl.data(), rule_tmpl.size() * 4, "upload rule_tmpl"))) return rc;
     if ((rc = put(d_rule_tmpl2, rule_tmpl2.data(), rule_tmpl2.size() * 4, "upload rule_tmpl2"))) return rc;
+    if ((rc = put(d_alias_off, alias_off.data(), alias_off.size() * 4, "upload alias_off"))) return rc;
+    if ((rc = put(d_aliases, alias_list.data(), alias_list.size() * 4, "upload aliases"))) return rc;
     if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
     if ((rc = put(d_rx_hdr, rx_set.hdr.data(), rx_set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
     if ((rc = put(d_rx_trans, rx_set.trans.data(), rx_set.trans.size() * 4, "upload rx trans"))) return rc;
@@ -648,6 +674,8 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->tmpls = d_tmpls.as<mxp_tmpl>();
     A->rule_tmpl = d_rule_tmpl.as<uint32_t>();
     A->rule_tmpl2 = d_rule_tmpl2.as<uint32_t>();
+    A->alias_off = n_alias ? d_alias_off.as<uint32_t>() : nullptr;
+    A->aliases = d_aliases.as<uint32_t>();
     A->rconst = d_rconst.as<uint64_t>();
     A->flags = debug_flags;
     A->n_rules = (uint32_t)rules.size();
@@ -675,10 +703,11 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
 }
 
 int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
-                       bool log, unsigned long long* d_hits) {
+                       bool log, unsigned long long* d_hits, uint64_t* stats) {
     mxp_kargs A;
     fill_args(&A, db);
     A.hits = d_vals ? nullptr : d_hits;
+    A.stats = d_vals ? nullptr : stats;
     A.out_match = d_match;
     A.out_err = d_err;
     A.out_vals = d_vals;
@@ -832,6 +861,7 @@ void mxp_engine_destroy(mxp_engine* eng) {
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     for (auto& x : eng->ev)
         if (x) (void)hipEventDestroy(x);
+    if (eng->h_stats) (void)hipHostFree(eng->h_stats);  // (synchronises with a pending stats copy)
     delete eng;
 }
 
@@ -911,10 +941,10 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) 
 
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
     if (!eng || !out) return 0;
-    const uint32_t v[7] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed,
-                           (uint32_t)(eng->cols.size() + eng->vcols.size()), eng->n_composite};
+    const uint32_t v[8] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed,
+                           (uint32_t)(eng->cols.size() + eng->vcols.size()), eng->n_composite, eng->n_alias};
     uint32_t k = 0;
-    for (; k < cap && k < 7; k++) out[k] = v[k];
+    for (; k < cap && k < 8; k++) out[k] = v[k];
     return k;
 }
 
@@ -950,7 +980,30 @@ int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, ui
                                unsigned long long* d_hits) {
     if (!eng || !db || !d_match || !d_err || !d_hits) return MXP_ERR_ARG;
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
-    return eng->launch(db, s, d_match, d_err, nullptr, false, d_hits);
+    hipError_t e;
+    if (!eng->h_stats) {
+        if ((e = eng->d_stats.alloc(8)) != hipSuccess) return eng->hipfail(e, "stats");
+        if ((e = hipHostMalloc((void**)&eng->h_stats, 8, hipHostMallocDefault)) != hipSuccess) {
+            eng->h_stats = nullptr;
+            return eng->hipfail(e, "stats host");
+        }
+        *eng->h_stats = 0;
+    }
+    // Counting in the kernels costs one atomic per true pair the index kernel sets; re-reading the
+    // match bitmap costs its W x N x 4 bytes (~ a true pair per 125 bitmap words at the measured
+    // atomic and streaming rates): choose by the last evaluation's true pairs per request.
+    const uint32_t R = (uint32_t)eng->rules.size(), W = (R + 31) / 32;
+    const double tp = eng->stats_n ? (double)*eng->h_stats / eng->stats_n : 0.0;
+    const bool fused = tp * 125.0 <= (double)W;
+    if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
+    int rc = eng->launch(db, s, d_match, d_err, nullptr, false, fused ? d_hits : nullptr, eng->d_stats.as<uint64_t>());
+    if (rc) return rc;
+    if (!fused && R && db->n && (e = mxp_launch_hits(d_match, db->n, R, W, d_hits, s)) != hipSuccess)
+        return eng->hipfail(e, "launch hits");
+    if ((e = hipMemcpyAsync(eng->h_stats, eng->d_stats.p, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return eng->hipfail(e, "stats download");
+    eng->stats_n = db->n;
+    return MXP_OK;
 }
 
 int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_requests, void* stream,

@@ -141,12 +141,12 @@ struct mxp_engine : public mxp::LowerTables {
     DevBuf d_rx_hdr, d_rx_trans, d_rx_ascii, d_rx_hilo, d_rx_hicls;
 
     DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
-    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_rconst, d_idx, d_hents, d_postings, d_plens;
+    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_alias_off, d_aliases, d_rconst, d_idx, d_hents, d_postings, d_plens;
     DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
     uint32_t n_glean = 0, n_gvm = 0;
     DevBuf d_fills;                 // chunks of uniform indexed groups (mxp_fill_kernel)
     uint32_t n_fills = 0, n_gfill = 0;
-    uint32_t n_idx = 0, n_indexed = 0, n_composite = 0;
+    uint32_t n_idx = 0, n_indexed = 0, n_composite = 0, n_alias = 0;
     uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
     uint32_t groups_per_wave = 4; // MXP_GPW
     // optional per-kernel timing of device evaluations (mxp_set_timing): events around each launch
@@ -288,7 +288,12 @@ struct mxp_engine : public mxp::LowerTables {
     int pack(const mxp_bag_batch* b, mxp_dbatch* db);
     void fill_args(mxp_kargs* A, const mxp_dbatch* db) const;
     int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
-               unsigned long long* d_hits = nullptr);
+               unsigned long long* d_hits = nullptr, uint64_t* d_stats = nullptr);
+    // fused hit counters: true pairs the guard-index kernel set in a recent evaluation (pinned host
+    // copy, read one launch late) decide between counting in the kernels and the streaming hits kernel
+    DevBuf d_stats;
+    uint64_t* h_stats = nullptr;
+    uint32_t stats_n = 0;
     std::string format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r) const;
     std::string string_of(const mxp_dbatch* db, uint64_t sid) const {
         if (!db) db = last_db.get();

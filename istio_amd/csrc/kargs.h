@@ -26,6 +26,8 @@ typedef struct mxp_kargs {
     const mxp_tmpl* tmpls;       // continuation templates
     const uint32_t* rule_tmpl;   // [n_rules] template of the rule's continuation (~0: none)
     const uint32_t* rule_tmpl2;  // [n_rules] composite-indexed rules: template resuming after the second atom
+    const uint32_t* alias_off;   // [n_rules + 1] CSR of duplicate indexed rules (nullptr: none)
+    const uint32_t* aliases;
     const uint64_t* rconst;      // [n_rules][MXP_VM_MAXREG] per-rule template constants
     const mxp_index* idx;        // guard indexes (mxp_index_kernel)
     const mxp_hent* hents;
@@ -65,6 +67,7 @@ typedef struct mxp_kargs {
     uint32_t* out_err;           // [n_words][n]
     uint64_t* out_vals;          // optional [n][n_rules] result registers (Eval)
     unsigned long long* hits;    // optional [n_rules] += true pairs of this evaluation (fused hit counters)
+    uint64_t* stats;             // optional [1] += true pairs the guard-index kernel set
     mxp_err_rec* errlog;
     uint32_t* errcount;
     uint32_t errcap;

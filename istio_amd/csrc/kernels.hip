@@ -101,8 +101,7 @@ __device__ __forceinline__ void log_err(const mxp_kargs& A, uint32_t req, uint32
 
 // a true pair found after phase 1 (guard-index kernel): OR its match bit in and, when the caller
 // asked for fused hit counters, count it once (the bit was not set before)
-__device__ __forceinline__ void set_true(const mxp_kargs& A, uint32_t rule, uint32_t req) {
-    if (!A.out_match) return;
+__device__ __forceinline__ void set_true1(const mxp_kargs& A, uint32_t rule, uint32_t req) {
     const uint32_t bit = 1u << (rule & 31u);
     uint32_t* w = A.out_match + (uint64_t)(rule >> 5) * A.n + req;
     if (A.hits) {
@@ -110,6 +109,28 @@ __device__ __forceinline__ void set_true(const mxp_kargs& A, uint32_t rule, uint
     } else {
         atomicOr(w, bit);
     }
+}
+
+// ... and the same for the rule's aliases (indexed duplicates of its program, kargs.alias_off)
+// returns the number of pairs set
+__device__ __forceinline__ uint32_t set_true(const mxp_kargs& A, uint32_t rule, uint32_t req) {
+    if (!A.out_match) return 0;
+    set_true1(A, rule, req);
+    uint32_t c = 1;
+    if (A.alias_off)
+        for (uint32_t j = A.alias_off[rule]; j < A.alias_off[rule + 1]; j++, c++) set_true1(A, A.aliases[j], req);
+    return c;
+}
+
+// an error pair found by the guard-index kernel, with its aliases
+__device__ __forceinline__ void set_error(const mxp_kargs& A, uint32_t rule, uint32_t req) {
+    if (!A.out_err) return;
+    atomicOr(A.out_err + (uint64_t)(rule >> 5) * A.n + req, 1u << (rule & 31u));
+    if (A.alias_off)
+        for (uint32_t j = A.alias_off[rule]; j < A.alias_off[rule + 1]; j++) {
+            const uint32_t r = A.aliases[j];
+            atomicOr(A.out_err + (uint64_t)(r >> 5) * A.n + req, 1u << (r & 31u));
+        }
 }
 
 // constant-address-space views: uniform loads through them become scalar s_load_dwordxN
@@ -121,17 +142,19 @@ typedef __attribute__((address_space(4))) const uint32_t cuint32;
 // per lane (template batches of the guard-index kernel); it only names the pair in error records and
 // Eval results.  The register file is regs[reg][thread] in LDS.
 __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint32_t pc0, bool live, uint32_t rule,
-                             uint32_t req, uint64_t (*regs)[256], uint32_t tid) {
+                             uint32_t req, uint64_t (*regs)[256], uint32_t tid, bool fan = false) {
 #define REG(i) regs[i][tid]
     const uint64_t N = A.n;
     uint32_t wait = live ? pc0 : MXP_VM_DONE;
     uint32_t res = PC_FALSE;
+    uint32_t ecode = ERR_NONE, eaux = 0;  // the lane's error (logged once, after the loop)
     uint32_t pc = pc0;
 
 #define FAIL(code_, aux_)                                   \
     do {                                                    \
         res = ((code_) >= 32u) ? PC_PANIC : PC_ERROR;       \
-        log_err(A, req, rule, (code_), (aux_));             \
+        ecode = (code_);                                    \
+        eaux = (aux_);                                      \
         live = false;                                       \
         wait = MXP_VM_DONE;                                 \
     } while (0)
@@ -367,6 +390,11 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
 #undef FINISH
 #undef FINISHV
 #undef REG
+    if (ecode != ERR_NONE && A.errlog) {
+        log_err(A, req, rule, ecode, eaux);
+        if (fan && A.alias_off)
+            for (uint32_t j = A.alias_off[rule]; j < A.alias_off[rule + 1]; j++) log_err(A, req, A.aliases[j], ecode, eaux);
+    }
     return res;
 }
 
@@ -617,42 +645,6 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
 // and error results are OR-ed in.
 namespace {
 
-// One posting list per lane (lanes may hold different lists, or none: len 0), walked in lockstep.
-// Direct postings (MXP_TMPL_DIRECT) are true pairs; the others run their template, lanes sharing a
-// template together, each with its own rule's constants preloaded.  Results are OR-ed into the
-// bitmaps.
-__device__ void run_postings(const mxp_kargs& A, const uint32_t* __restrict__ tmpl_of, uint32_t start, uint32_t len,
-                             uint32_t req, uint64_t (*regs)[256], uint32_t tid) {
-    const uint64_t N = A.n;
-    for (uint32_t j = 0; __ballot(j < len); j++) {
-        bool pending = j < len;
-        const uint32_t rule = pending ? A.postings[start + j] : 0u;
-        const uint32_t t = pending ? tmpl_of[rule] : MXP_VM_DONE;
-        if (pending && t == MXP_TMPL_DIRECT) {
-            set_true(A, rule, req);
-            pending = false;
-        }
-        for (uint64_t bal = __ballot(pending); bal; bal = __ballot(pending)) {
-            const uint32_t tt = __builtin_amdgcn_readlane(t, (uint32_t)__builtin_ctzll(bal));
-            const bool mine = pending && t == tt;
-            const mxp_tmpl* T = A.tmpls + tt;
-            const uint32_t off = uni(T->off), pc0 = uni(T->pc0), len_t = uni(T->len), nconst = uni(T->nconst),
-                           creg0 = uni(T->creg0);
-            if (mine)
-                for (uint32_t c = 0; c < nconst; c++) regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
-            cuint32* P = ((cuint32*)A.prog) + ((uint64_t)off - pc0) * 4u;
-            const uint32_t code = run_rule(A, P, len_t, pc0, mine, rule, req, regs, tid);
-            if (mine) {
-                const uint64_t w = (uint64_t)(rule >> 5) * N + req;
-                const uint32_t bit = 1u << (rule & 31u);
-                if (code == PC_TRUE) set_true(A, rule, req);
-                if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
-            }
-            pending = pending && !mine;
-        }
-    }
-}
-
 // In-wave pair queue (LDS): the postings the probes find are appended as (rule, request) pairs and
 // run 64 at a time -- one pair per lane, lanes sharing a template together -- so the VM runs on
 // dense wavefronts however sparse the hits are per request.  Entry: rule | table << 31 (table 1:
@@ -662,6 +654,7 @@ __shared__ uint32_t g_ixq[4][MXP_IXQ][2];  // per wave of the index kernel's wor
 struct PairQueue {
     uint32_t wave;
     uint32_t n;        // pending entries (wave-uniform)
+    uint32_t ntrue;    // true pairs this lane has set (kargs.stats)
 };
 
 __device__ __forceinline__ void wave_sync_lds() {
@@ -695,12 +688,10 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
         if (mine)
             for (uint32_t c = 0; c < nconst; c++) regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
         cuint32* P = ((cuint32*)A.prog) + ((uint64_t)toff - pc0) * 4u;
-        const uint32_t code = run_rule(A, P, len_t, pc0, mine, rule, req, regs, tid);
+        const uint32_t code = run_rule(A, P, len_t, pc0, mine, rule, req, regs, tid, true);
         if (mine) {
-            const uint64_t w = (uint64_t)(rule >> 5) * N + req;
-            const uint32_t bit = 1u << (rule & 31u);
-            if (code == PC_TRUE) set_true(A, rule, req);
-            if (code >= PC_ERROR && A.out_err) atomicOr(A.out_err + w, bit);
+            if (code == PC_TRUE) Q.ntrue += set_true(A, rule, req);
+            if (code >= PC_ERROR) set_error(A, rule, req);
         }
         pending = pending && !mine;
     }
@@ -728,7 +719,7 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
                 const uint32_t rule = A.postings[start + j0 + j];
                 uint32_t e = rule | (tbl << 31);
                 if (tmpl_of[rule] == MXP_TMPL_DIRECT) {
-                    set_true(A, rule, req);
+                    Q.ntrue += set_true(A, rule, req);
                     e = 0xFFFFFFFFu;
                 }
                 g_ixq[Q.wave][base + j][0] = e;
@@ -781,6 +772,7 @@ struct PrefixHash {
     }
 };
 
+
 }  // namespace
 
 // Guard-index phase: the pairs of indexed rules, found per request by hash lookups of its column
@@ -794,7 +786,7 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
-    PairQueue Q{wave, 0u};
+    PairQueue Q{wave, 0u, 0u};
     const uint32_t req = (blockIdx.x * 4u + wave) * 64u + (tid & 63u);
     const bool valid = req < A.n;
     const uint64_t N = A.n;
@@ -874,6 +866,12 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
             }
             if (final || __ballot(len != 0)) process_slot(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
         }
+    }
+    if (A.stats) {
+        uint32_t t = Q.ntrue;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += (uint32_t)__shfl_xor((int)t, off, 64);
+        if ((tid & 63u) == 0 && t) atomicAdd((unsigned long long*)A.stats, (unsigned long long)t);
     }
 }
 

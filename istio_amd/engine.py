@@ -188,10 +188,10 @@ class Engine:
 
     def ruleset_info(self) -> dict:
         """Kernel-side shape of the rule set (guards, continuation templates, column segments)."""
-        out = (ctypes.c_uint32 * 7)()
-        k = self.lib.mxp_ruleset_info(self.h, out, 7)
-        return dict(zip(("guarded", "templated", "templates", "segments", "indexed", "columns", "composite"),
-                        list(out)[:k]))
+        out = (ctypes.c_uint32 * 8)()
+        k = self.lib.mxp_ruleset_info(self.h, out, 8)
+        return dict(zip(("guarded", "templated", "templates", "segments", "indexed", "columns", "composite",
+                         "aliases"), list(out)[:k]))
 
     # ------------------------------------------------------------------ evaluation
     def eval_batch(self, batch: BagBatch):

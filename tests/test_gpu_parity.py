@@ -253,14 +253,17 @@ def test_c2_ragged_batches(mxp, n):
     compare(eng, ev, rules, batch, sample_msgs=100)
 
 
-@pytest.mark.parametrize("family", ["c2", "fuzz"])
+@pytest.mark.parametrize("family", ["c2", "fuzz", "c4"])
 def test_fused_hit_counters(mxp, family):
     """mxp_batch_eval_device_hits: counters accumulated by the evaluation kernels (fill / guard / VM
-    kernels by ballot, index kernel per newly set bit) equal the true pairs of the bitmaps, and the
-    bitmaps equal the plain device evaluation's."""
+    kernels by ballot, index kernel per newly set bit) -- or, after an evaluation dense in true pairs
+    (C4), by the streaming hits kernel -- equal the true pairs of the bitmaps over three evaluations,
+    and the bitmaps equal the plain device evaluation's."""
     import torch
     if family == "c2":
         manifest, rules, batch = W.c2_workload(n_rules=700, n_requests=30000)
+    elif family == "c4":
+        manifest, rules, batch = W.c4_workload(n_rules=1500, n_requests=8000)
     else:
         manifest = W.DEFAULT_TEST_MANIFEST
         rules = W.guarded_fuzz_rules(1500, seed=41)
@@ -275,13 +278,38 @@ def test_fused_hit_counters(mxp, family):
     dm2, de2 = torch.zeros_like(dm), torch.zeros_like(dm)
     hits = torch.full((len(rules),), 3, dtype=torch.int64, device="cuda:0")
     s = torch.cuda.current_stream().cuda_stream
-    db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s)
+    for _ in range(3):
+        db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s)
+        torch.cuda.synchronize()
     db.eval(dm2.data_ptr(), de2.data_ptr(), s)
     torch.cuda.synchronize()
     m = dm.cpu().numpy().view(np.uint32)
     assert np.array_equal(m, dm2.cpu().numpy().view(np.uint32))
     assert np.array_equal(de.cpu().numpy(), de2.cpu().numpy())
     codes = mxp.bits_to_codes(m, de.cpu().numpy().view(np.uint32), len(rules))
-    want = (codes == 1).sum(axis=0) + 3
+    want = 3 * (codes == 1).sum(axis=0) + 3
     assert want.sum() > 3 * len(rules)
     assert np.array_equal(hits.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("knobs", [{}, {"MXP_DEBUG_FLAGS": "64"}])
+def test_duplicate_rules_parity(mxp, knobs, monkeypatch):
+    """Indexed rules with identical programs are evaluated once and fanned out (aliases): results,
+    error bits and error records of every duplicate match the oracle; MXP_DEBUG_FLAGS=64 turns the
+    dedupe off."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(61)
+    base = composite_rules(200, seed=62) + W.guarded_fuzz_rules(300, seed=63)
+    base += ['"^a[bc]?$".matches(bs)', '"^ab".matches(as)', 'as.startsWith("ab")', '"^a".matches(ar["a"])']
+    rules = [base[i] for i in rng.integers(0, len(base), size=1500)]
+    bags = W.fuzz_bags(3000, seed=64, p_missing=0.2, p_wrong=0.05)
+    batch = BagBatch.from_bags(bags, names=list(W.DEFAULT_TEST_MANIFEST))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
+    eng.compile(rules)
+    info = eng.ruleset_info()
+    assert info["aliases"] > 300 or knobs, info
+    ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
+    got, want = compare(eng, ev, rules, batch, sample_msgs=400)
+    assert (want == 1).sum() > 1000 and (want >= 2).sum() > 1000
