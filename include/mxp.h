@@ -205,6 +205,11 @@ int mxp_regex_match_host(const char* pattern, uint32_t pattern_len, const char* 
  */
 typedef struct mxp_dbatch mxp_dbatch;
 int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out);
+/* The host half of mxp_batch_upload alone (interning against the rule set's pools, column gather,
+ * ip() / timestamp() / regexp pre-tables), for timing and tests; works on a host-only engine.
+ * out[0] bytes of the packed device image, out[1] batch strings added to the overlay pool, out[2]
+ * overlay byte strings.  Host threads: MXP_PACK_THREADS, else OMP_NUM_THREADS, else all cores. */
+int mxp_batch_pack_host(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* out, uint32_t cap);
 void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db);
 int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err);
 /* mxp_batch_eval_device plus fused per-rule hit counters: d_hits[rule] += the requests of this batch
@@ -216,10 +221,19 @@ int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, ui
 int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_requests, void* stream,
                     unsigned long long* d_hits);
 uint32_t mxp_rule_count(const mxp_engine* eng);
+/* Request pipelining of device evaluations: a batch of n >= 2 * min_requests requests runs as
+ * min(max_chunks, n / min_requests) request chunks; the guard-index kernel of chunk c runs on a
+ * second HIP stream of the engine, overlapped with the fill / guard / VM kernels of chunk c + 1, and
+ * the evaluation stream waits for it before the call's work ends.  Results do not depend on it.
+ * Defaults: min_requests 131072, max_chunks 1 (off: on C2 the two kernels slow each other down more
+ * than the overlap saves); max_chunks <= 8. */
+int mxp_set_pipeline(mxp_engine* eng, uint32_t min_requests, uint32_t max_chunks);
 /* Per-kernel timing of device evaluations (off by default): with timing on, every evaluation
  * records HIP events around its launches on the evaluation stream; mxp_kernel_times waits for the
  * last one and returns its kernel durations in ms: [0] guard + VM kernels, [1] guard-index kernel
- * (0 when it did not run).  *n_out = values written. */
+ * (0 when it did not run).  Pipelined evaluations: [0] the evaluation stream's kernels of every
+ * chunk (index kernels of all but the last chunk overlapped), [1] the exposed index tail; the sum
+ * is the whole evaluation.  *n_out = values written. */
 int mxp_set_timing(mxp_engine* eng, int on);
 int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out);
 /* Shape of the compiled rule set as the kernels see it: out[0] guarded rules (leading atom evaluated

@@ -8,11 +8,14 @@
 //     `map[const key]` lookups pre-extracted into virtual columns;
 //   * kernel launches on the engine's HIP stream and reporting of error pairs with the reference's
 //     exact error texts.
+#include <deque>
+
 #include "engine_impl.h"
 
 // ------------------------------------------------------------------------------------ compile
 int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     reset_tables();
+    views_n[0] = ~(size_t)0;  // string-view indexes rebuilt at the next pack
     rules.resize(n);
     std::vector<mxp_vm_ins> all;
     std::vector<uint32_t> off(n + 1, 0);
@@ -447,63 +450,206 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
 }
 
 // ---------------------------------------------------------------------------------------- pack
-int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
+void mxp_engine::build_views() {
+    // string-view indexes of the rule set's interning tables (rebuilt when a compile grew them:
+    // the vectors may have moved their strings)
+    if (views_n[0] == gstrs.size() && views_n[1] == gbytes.size() && views_n[2] == gcanon.size()) return;
+    auto build = [](const std::vector<std::string>& v, mxp::SvMap& m) {
+        m.clear();
+        m.reserve(v.size() * 2);
+        for (size_t i = 0; i < v.size(); i++) m.emplace(std::string_view(v[i]), (uint32_t)i);
+    };
+    build(gstrs, gstr_view);
+    build(gbytes, gbytes_view);
+    build(gcanon, gcanon_view);
+    views_n[0] = gstrs.size();
+    views_n[1] = gbytes.size();
+    views_n[2] = gcanon.size();
+}
+
+// Host half of packing (mxp_batch_upload): the caller's columnar batch -> the engine's device
+// columns.  Batch strings are interned against the rule set's pool (ids < G) or a per-batch overlay
+// in four passes: (1) mark the batch strings the rule set's columns reach, (2) look them up in the
+// rule set's tables in parallel, (3) assign overlay ids to the misses in batch-string order
+// (sequential, deterministic), (4) gather the columns in parallel.
+int mxp_engine::pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H) {
     const uint32_t n = b->n_requests;
     const uint32_t C = (uint32_t)cols.size(), V = (uint32_t)vcols.size();
     const uint32_t ncol = C + V;
     db->n = n;
+    build_views();
     std::unordered_map<std::string, uint32_t> bcol;
     for (uint32_t c = 0; c < b->n_columns; c++) bcol.emplace(b->column_names[c], c);
-
+    std::vector<int32_t> src(ncol, -1);  // batch column of each engine column
+    for (uint32_t c = 0; c < ncol; c++) {
+        auto it = bcol.find(c < C ? cols[c] : vcols[c - C].first);
+        if (it != bcol.end()) src[c] = (int32_t)it->second;
+    }
+    const uint32_t NS = b->n_strings;
+    auto view = [&](uint64_t sid) {
+        return std::string_view((const char*)b->str_bytes + b->str_offsets[sid],
+                                (size_t)(b->str_offsets[sid + 1] - b->str_offsets[sid]));
+    };
+    // ---- (1) usage marks: 1 = string value, 2 = bytes value
+    std::vector<uint8_t> use(NS, 0);
+    auto mark = [&](uint64_t sid, uint8_t bit) {
+        if (sid < NS) __atomic_fetch_or(&use[sid], bit, __ATOMIC_RELAXED);
+    };
+    // virtual map[key] columns: the matching entry's value string (per request, ~0 = key absent)
+    std::vector<uint32_t> vhit((size_t)V * n, MXP_VM_DONE);
+    mxp::par_for(n, 4096, [&](uint64_t r0, uint64_t r1, unsigned) {
+        for (uint32_t c = 0; c < C; c++) {
+            if (src[c] < 0) continue;
+            const uint8_t* bk = b->kinds[src[c]];
+            const uint64_t* bv = b->values[src[c]];
+            for (uint64_t r = r0; r < r1; r++) {
+                if (bk[r] == MXP_STRING) mark(bv[r], 1);
+                else if (bk[r] == MXP_BYTES) mark(bv[r], 2);
+            }
+        }
+        for (uint32_t j = 0; j < V; j++) {
+            if (src[C + j] < 0) continue;
+            const std::string& key = vcols[j].second;
+            const uint8_t* bk = b->kinds[src[C + j]];
+            const uint64_t* bv = b->values[src[C + j]];
+            for (uint64_t r = r0; r < r1; r++) {
+                if (bk[r] != MXP_STRING_MAP) continue;
+                const uint64_t m = bv[r];
+                for (uint64_t e = b->map_offsets[m]; e < b->map_offsets[m + 1]; e++) {
+                    if (view(b->map_keys[e]) == key) {
+                        vhit[(size_t)j * n + r] = b->map_values[e];
+                        mark(b->map_values[e], 1);
+                        break;
+                    }
+                }
+            }
+        }
+    });
+    if (need_maps) {
+        const uint64_t E = b->n_maps ? b->map_offsets[b->n_maps] : 0;
+        mxp::par_for(E, 1 << 14, [&](uint64_t e0, uint64_t e1, unsigned) {
+            for (uint64_t e = e0; e < e1; e++) {
+                mark(b->map_keys[e], 1);
+                mark(b->map_values[e], 1);
+            }
+        });
+    }
+    // ---- (2) rule-set pool lookups (+ content hashes of the misses)
     const uint32_t G = (uint32_t)gstrs.size();
-    std::vector<uint32_t> bmap(b->n_strings, MXP_VM_DONE);
-    std::unordered_map<std::string, uint32_t> overlay_ids;
-    auto bstr = [&](uint32_t sid) {
-        return std::string((const char*)b->str_bytes + b->str_offsets[sid],
-                           (size_t)(b->str_offsets[sid + 1] - b->str_offsets[sid]));
+    constexpr uint32_t NONE = MXP_VM_DONE;
+    std::vector<uint32_t> sid(NS, NONE), braw(NS, NONE), bcan(NS, NONE);
+    std::vector<uint64_t> hs(NS, 0), hc;
+    bool any_bytes = false;
+    for (uint32_t s = 0; s < NS && !any_bytes; s++) any_bytes = use[s] & 2;
+    if (any_bytes) hc.assign(NS, 0);
+    // net.IP.Equal class of a byte string: 4-byte addresses in their 16-byte v4-mapped form
+    auto canon_of = [&](uint64_t s, char* buf) -> std::string_view {
+        const std::string_view v = view(s);
+        if (v.size() != 4) return v;
+        memset(buf, 0, 10);
+        buf[10] = buf[11] = (char)0xff;
+        memcpy(buf + 12, v.data(), 4);
+        return std::string_view(buf, 16);
     };
-    auto sid_of = [&](uint32_t s) -> uint32_t {
-        uint32_t& m = bmap[s];
-        if (m != MXP_VM_DONE) return m;
-        std::string v = bstr(s);
-        auto it = gstr_ids.find(v);
-        if (it != gstr_ids.end()) return m = it->second;
-        auto jt = overlay_ids.find(v);
-        if (jt != overlay_ids.end()) return m = jt->second;
-        uint32_t id = G + (uint32_t)db->overlay.size();
-        overlay_ids.emplace(v, id);
-        db->overlay.push_back(v);
-        return m = id;
+    mxp::par_for(NS, 2048, [&](uint64_t s0, uint64_t s1, unsigned) {
+        char buf[16];
+        for (uint64_t s = s0; s < s1; s++) {
+            if (!use[s]) continue;
+            const std::string_view v = view(s);
+            if (use[s] & 1) {
+                auto it = gstr_view.find(v);
+                if (it != gstr_view.end()) sid[s] = it->second;
+            }
+            if (use[s] & 2) {
+                auto it = gbytes_view.find(v);
+                if (it != gbytes_view.end()) braw[s] = it->second;
+                const std::string_view c = canon_of(s, buf);
+                auto ct = gcanon_view.find(c);
+                if (ct != gcanon_view.end()) bcan[s] = ct->second;
+                else hc[s] = mxp::hash_bytes(c.data(), c.size());
+            }
+            if (sid[s] == NONE || braw[s] == NONE) hs[s] = mxp::hash_bytes(v.data(), v.size());
+        }
+    });
+    // ---- (3) overlay ids for the misses: equal strings found in parallel (hash shards), ids
+    // assigned in batch-string order of first appearance
+    auto assign = [&](std::vector<uint32_t>& out, uint8_t bit, const std::vector<uint64_t>& hash, auto&& eq,
+                      auto&& add) {
+        std::vector<uint32_t> cand;
+        for (uint32_t s = 0; s < NS; s++)
+            if ((use[s] & bit) && out[s] == NONE) cand.push_back(s);
+        std::vector<uint32_t> rep(cand.size());
+        mxp::dedupe_first((uint32_t)cand.size(), [&](uint32_t i) { return hash[cand[i]]; },
+                          [&](uint32_t i, uint32_t j) { return eq(cand[i], cand[j]); }, rep);
+        for (uint32_t i = 0; i < cand.size(); i++)
+            out[cand[i]] = rep[i] == i ? add(cand[i]) : out[cand[rep[i]]];
+        return cand.size();
     };
-    std::unordered_map<std::string, uint32_t> obytes, ocanon;
-    std::vector<std::string> overlay_canon;
+    auto same = [&](uint32_t a, uint32_t b2) { return view(a) == view(b2); };
+    bool too_long = false;
+    assign(sid, 1, hs, same, [&](uint32_t s) {
+        too_long |= !db->overlay.push(view(s));
+        return G + (uint32_t)db->overlay.size() - 1;
+    });
+    if (too_long) return fail(MXP_ERR_ARG, "batch string longer than 16 MiB");
+    std::vector<uint32_t> canon_rep;  // overlay canonical classes: a batch string of each
+    if (any_bytes) {
+        assign(braw, 2, hs, same, [&](uint32_t s) {
+            db->overlay_bytes.push(view(s));
+            return (uint32_t)(gbytes.size() + db->overlay_bytes.size() - 1);
+        });
+        assign(bcan, 2, hc, [&](uint32_t a, uint32_t b2) {
+            char x[16], y[16];
+            return canon_of(a, x) == canon_of(b2, y);
+        }, [&](uint32_t s) {
+            canon_rep.push_back(s);
+            return (uint32_t)(gcanon.size() + canon_rep.size() - 1);
+        });
+    }
+    // bytes ids of strings outside the batch table (parsed ip() values), after the batch's own
+    // (maps built on first use; keys view `keep`, a deque: stable addresses)
+    std::deque<std::string> keep;
+    mxp::SvMap obytes, ocanon;
+    bool omaps = false;
+    uint32_t n_canon = (uint32_t)canon_rep.size();
     auto bytes_id = [&](const std::string& raw) -> uint64_t {
+        if (!omaps) {
+            omaps = true;
+            for (size_t i = 0; i < db->overlay_bytes.size(); i++)
+                obytes.emplace(db->overlay_bytes[i], (uint32_t)(gbytes.size() + i));
+            for (size_t i = 0; i < canon_rep.size(); i++) {
+                char buf[16];
+                keep.emplace_back(canon_of(canon_rep[i], buf));
+                ocanon.emplace(std::string_view(keep.back()), (uint32_t)(gcanon.size() + i));
+            }
+        }
         uint32_t rid, cid;
-        auto it = gbytes_ids.find(raw);
-        if (it != gbytes_ids.end()) {
+        auto it = gbytes_view.find(std::string_view(raw));
+        if (it != gbytes_view.end()) {
             rid = it->second;
         } else {
-            auto jt = obytes.find(raw);
+            auto jt = obytes.find(std::string_view(raw));
             if (jt != obytes.end()) {
                 rid = jt->second;
             } else {
                 rid = (uint32_t)(gbytes.size() + db->overlay_bytes.size());
-                obytes.emplace(raw, rid);
-                db->overlay_bytes.push_back(raw);
+                db->overlay_bytes.push(raw);
+                keep.push_back(raw);
+                obytes.emplace(std::string_view(keep.back()), rid);
             }
         }
-        std::string canon = mxp::ip_canonical((const uint8_t*)raw.data(), raw.size());
-        auto ct = gcanon_ids.find(canon);
-        if (ct != gcanon_ids.end()) {
+        std::string c = mxp::ip_canonical((const uint8_t*)raw.data(), raw.size());
+        auto ct = gcanon_view.find(std::string_view(c));
+        if (ct != gcanon_view.end()) {
             cid = ct->second;
         } else {
-            auto dt = ocanon.find(canon);
+            auto dt = ocanon.find(std::string_view(c));
             if (dt != ocanon.end()) {
                 cid = dt->second;
             } else {
-                cid = (uint32_t)(gcanon.size() + overlay_canon.size());
-                ocanon.emplace(canon, cid);
-                overlay_canon.push_back(canon);
+                cid = (uint32_t)gcanon.size() + n_canon++;
+                keep.push_back(c);
+                ocanon.emplace(std::string_view(keep.back()), cid);
             }
         }
         return MXP_BYTES_ID(cid, rid);
@@ -520,117 +666,141 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
         db->overlay_times.push_back(k);
         return id;
     };
-
-    std::vector<uint8_t> kinds((size_t)ncol * n, 0);
-    std::vector<uint64_t> vals((size_t)ncol * n, 0);
+    // timestamps (sequential: ordered map, rare)
+    std::vector<uint32_t> tid(b->n_times, MXP_VM_DONE);
     for (uint32_t c = 0; c < C; c++) {
-        auto it = bcol.find(cols[c]);
-        if (it == bcol.end()) continue;
-        const uint8_t* bk = b->kinds[it->second];
-        const uint64_t* bv = b->values[it->second];
-        uint8_t* ok = kinds.data() + (size_t)c * n;
-        uint64_t* ov = vals.data() + (size_t)c * n;
-        for (uint32_t r = 0; r < n; r++) {
-            uint8_t k = bk[r];
-            uint64_t v = bv[r];
-            switch (k) {
-            case MXP_STRING: v = sid_of((uint32_t)v); break;
-            case MXP_BYTES: v = bytes_id(bstr((uint32_t)v)); break;
-            case MXP_TIMESTAMP: v = time_id(b->time_sec[v], b->time_nsec[v]); break;
-            case MXP_OTHER: v = 0; break;
-            default: break;
-            }
-            ok[r] = k;
-            ov[r] = v;
-        }
+        if (src[c] < 0) continue;
+        const uint8_t* bk = b->kinds[src[c]];
+        const uint64_t* bv = b->values[src[c]];
+        for (uint32_t r = 0; r < n; r++)
+            if (bk[r] == MXP_TIMESTAMP && tid[bv[r]] == MXP_VM_DONE)
+                tid[bv[r]] = time_id(b->time_sec[bv[r]], b->time_nsec[bv[r]]);
     }
-    for (uint32_t j = 0; j < V; j++) {
-        const std::string& attr = vcols[j].first;
-        const std::string& key = vcols[j].second;
-        uint8_t* ok = kinds.data() + (size_t)(C + j) * n;
-        uint64_t* ov = vals.data() + (size_t)(C + j) * n;
-        auto it = bcol.find(attr);
-        if (it == bcol.end()) continue;  // VC_ABSENT
-        const uint8_t* bk = b->kinds[it->second];
-        const uint64_t* bv = b->values[it->second];
-        for (uint32_t r = 0; r < n; r++) {
-            uint8_t k = bk[r];
-            if (k == MXP_ABSENT) {
-                ok[r] = VC_ABSENT;
-            } else if (k != MXP_STRING_MAP) {
-                ok[r] = VC_NOTMAP;
-            } else {
-                ok[r] = VC_VALUE;
-                ov[r] = empty_sid;
-                uint64_t m = bv[r];
-                for (uint64_t e = b->map_offsets[m]; e < b->map_offsets[m + 1]; e++) {
-                    uint32_t ks = b->map_keys[e];
-                    size_t kl = (size_t)(b->str_offsets[ks + 1] - b->str_offsets[ks]);
-                    if (kl == key.size() && memcmp(b->str_bytes + b->str_offsets[ks], key.data(), kl) == 0) {
-                        ov[r] = sid_of(b->map_values[e]);
-                        break;
-                    }
+    // ---- (4) columns
+    H.kinds.assign((size_t)ncol * n, 0);
+    H.vals.assign((size_t)ncol * n, 0);
+    mxp::par_for(n, 4096, [&](uint64_t r0, uint64_t r1, unsigned) {
+        for (uint32_t c = 0; c < C; c++) {
+            if (src[c] < 0) continue;
+            const uint8_t* bk = b->kinds[src[c]];
+            const uint64_t* bv = b->values[src[c]];
+            uint8_t* ok = H.kinds.data() + (size_t)c * n;
+            uint64_t* ov = H.vals.data() + (size_t)c * n;
+            for (uint64_t r = r0; r < r1; r++) {
+                const uint8_t k = bk[r];
+                uint64_t v = bv[r];
+                switch (k) {
+                case MXP_STRING: v = sid[v]; break;
+                case MXP_BYTES: v = MXP_BYTES_ID(bcan[v], braw[v]); break;
+                case MXP_TIMESTAMP: v = tid[v]; break;
+                case MXP_OTHER: v = 0; break;
+                default: break;
+                }
+                ok[r] = k;
+                ov[r] = v;
+            }
+        }
+        for (uint32_t j = 0; j < V; j++) {
+            uint8_t* ok = H.kinds.data() + (size_t)(C + j) * n;
+            uint64_t* ov = H.vals.data() + (size_t)(C + j) * n;
+            if (src[C + j] < 0) continue;  // VC_ABSENT (0)
+            const uint8_t* bk = b->kinds[src[C + j]];
+            for (uint64_t r = r0; r < r1; r++) {
+                const uint8_t k = bk[r];
+                if (k == MXP_ABSENT) {
+                    ok[r] = VC_ABSENT;
+                } else if (k != MXP_STRING_MAP) {
+                    ok[r] = VC_NOTMAP;
+                } else {
+                    ok[r] = VC_VALUE;
+                    const uint32_t h = vhit[(size_t)j * n + r];
+                    ov[r] = h == MXP_VM_DONE ? empty_sid : sid[h];
                 }
             }
         }
-    }
-    std::vector<uint32_t> moff, mk, mv;
+    });
     if (need_maps) {
-        moff.resize(b->n_maps + 1, 0);
-        for (uint32_t m = 0; m < b->n_maps; m++) {
-            for (uint64_t e = b->map_offsets[m]; e < b->map_offsets[m + 1]; e++) {
-                mk.push_back(sid_of(b->map_keys[e]));
-                mv.push_back(sid_of(b->map_values[e]));
+        H.moff.assign(b->n_maps + 1, 0);
+        for (uint32_t m = 0; m < b->n_maps; m++) H.moff[m + 1] = (uint32_t)b->map_offsets[m + 1];
+        const uint64_t E = b->n_maps ? b->map_offsets[b->n_maps] : 0;
+        H.mk.resize(E);
+        H.mv.resize(E);
+        mxp::par_for(E, 1 << 14, [&](uint64_t e0, uint64_t e1, unsigned) {
+            for (uint64_t e = e0; e < e1; e++) {
+                H.mk[e] = sid[b->map_keys[e]];
+                H.mv[e] = sid[b->map_values[e]];
             }
-            moff[m + 1] = (uint32_t)mk.size();
-        }
+        });
     }
-    // per-string pre-tables for dynamic ip() / timestamp()
-    std::vector<uint64_t> ipof, tsof;
+    // per-string pre-tables for dynamic ip() / timestamp(): parsed in parallel, interned in order
     const uint64_t S = G + db->overlay.size();
+    auto str_at = [&](uint64_t s) -> std::string_view {
+        return s < G ? std::string_view(gstrs[s]) : db->overlay[s - G];
+    };
     if (need_ipof) {
-        ipof.assign(S, kNoValue);
-        for (uint64_t s = 0; s < S; s++) {
-            std::string v = string_of(db, s);
-            uint8_t out[16];
-            if (mxp::go_parse_ip((const uint8_t*)v.data(), v.size(), out))
-                ipof[s] = MXP_FH(MXP_BYTES, bytes_id(std::string((const char*)out, 16)));
-        }
+        H.ipof.assign(S, kNoValue);
+        std::vector<std::string> parsed(S);
+        mxp::par_for(S, 2048, [&](uint64_t s0, uint64_t s1, unsigned) {
+            for (uint64_t s = s0; s < s1; s++) {
+                const std::string_view v = str_at(s);
+                uint8_t out[16];
+                if (mxp::go_parse_ip((const uint8_t*)v.data(), v.size(), out)) parsed[s].assign((const char*)out, 16);
+            }
+        });
+        for (uint64_t s = 0; s < S; s++)
+            if (!parsed[s].empty()) H.ipof[s] = MXP_FH(MXP_BYTES, bytes_id(parsed[s]));
     }
     if (need_tsof) {
-        tsof.assign(S, kNoValue);
-        for (uint64_t s = 0; s < S; s++) {
-            std::string v = string_of(db, s);
-            int64_t sec;
-            int32_t ns;
-            if (mxp::go_parse_rfc3339((const uint8_t*)v.data(), v.size(), &sec, &ns))
-                tsof[s] = MXP_FH(MXP_TIMESTAMP, time_id(sec, ns));
-        }
+        H.tsof.assign(S, kNoValue);
+        std::vector<std::pair<int64_t, int32_t>> ts(S);
+        std::vector<uint8_t> ok(S, 0);
+        mxp::par_for(S, 2048, [&](uint64_t s0, uint64_t s1, unsigned) {
+            for (uint64_t s = s0; s < s1; s++) {
+                const std::string_view v = str_at(s);
+                ok[s] = mxp::go_parse_rfc3339((const uint8_t*)v.data(), v.size(), &ts[s].first, &ts[s].second);
+            }
+        });
+        for (uint64_t s = 0; s < S; s++)
+            if (ok[s]) H.tsof[s] = MXP_FH(MXP_TIMESTAMP, time_id(ts[s].first, ts[s].second));
     }
     // run-time regexp patterns: every distinct string of a pattern column, compiled once per batch
-    std::vector<uint32_t> rxof;
-    mxp::DfaSetHost rxb;
     if (need_rxof) {
-        rxof.assign(S, MXP_RXOF_SYNTAX);
+        H.rxof.assign(S, MXP_RXOF_SYNTAX);
         std::vector<uint8_t> done(S, 0);
         for (uint32_t c : rx_cols) {
-            const uint8_t* k = kinds.data() + (size_t)c * n;
-            const uint64_t* v = vals.data() + (size_t)c * n;
+            const uint8_t* k = H.kinds.data() + (size_t)c * n;
+            const uint64_t* v = H.vals.data() + (size_t)c * n;
             for (uint32_t q = 0; q < n; q++) {
                 if (k[q] != MXP_STRING || v[q] >= S || done[v[q]]) continue;
                 done[v[q]] = 1;
                 mxp::Dfa d;
                 std::string e;
-                const int rc = mxp::regex_compile({string_of(db, v[q])}, kRegexStates, &d, &e);
-                rxof[v[q]] = rc == mxp::RX_OK ? rxb.add(d) : rc == mxp::RX_SYNTAX ? MXP_RXOF_SYNTAX : MXP_RXOF_UNSUPPORTED;
+                const int rc = mxp::regex_compile({std::string(str_at(v[q]))}, kRegexStates, &d, &e);
+                H.rxof[v[q]] = rc == mxp::RX_OK ? H.rxb.add(d) : rc == mxp::RX_SYNTAX ? MXP_RXOF_SYNTAX : MXP_RXOF_UNSUPPORTED;
             }
         }
     }
-    std::vector<uint64_t> ooff;
-    std::string oblob;
-    if (need_strings && !string_pool(db->overlay, &ooff, &oblob))
-        return fail(MXP_ERR_ARG, "batch string longer than 16 MiB");
+    db->overlay.finish();
+    return MXP_OK;
+}
 
+int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
+    PackedHost H;
+    int rc = pack_host(b, db, H);
+    if (rc) return rc;
+    auto& kinds = H.kinds;
+    auto& vals = H.vals;
+    auto& moff = H.moff;
+    auto& mk = H.mk;
+    auto& mv = H.mv;
+    auto& ipof = H.ipof;
+    auto& tsof = H.tsof;
+    const std::vector<uint64_t> no_off;
+    const std::string no_blob;
+    const auto& ooff = need_strings ? db->overlay.desc : no_off;
+    const auto& oblob = need_strings ? db->overlay.blob : no_blob;
+    auto& rxof = H.rxof;
+    auto& rxb = H.rxb;
     hipError_t e;
     auto up = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
         if ((e = d.alloc(bytes)) != hipSuccess) return hipfail(e, what);
@@ -638,7 +808,6 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
             return hipfail(e, what);
         return MXP_OK;
     };
-    int rc;
     if ((rc = up(db->kinds, kinds.data(), kinds.size(), "upload kinds"))) return rc;
     if ((rc = up(db->vals, vals.data(), vals.size() * 8, "upload vals"))) return rc;
     if ((rc = up(db->map_off, moff.data(), moff.size() * 4, "upload map_off"))) return rc;
@@ -726,7 +895,6 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     // guard-index phase: predicate mode only (Eval runs whole programs in mxp_eval_kernel)
     const bool use_index = !d_vals && !(debug_flags & 2u) && n_idx > 0;
     if (!use_index) A.n_idx = 0;
-    const uint32_t gx = (A.n + 63) / 64;
     auto gy_of = [&](uint32_t ng) { return (ng + 4 * A.groups_per_wave - 1) / (4 * A.groups_per_wave); };
     if (timing && (e = hipEventRecord(ev[0], s)) != hipSuccess) return hipfail(e, "event");
     // guards on: guard-only groups through the lean kernel, the rest through the VM kernel;
@@ -738,18 +906,53 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         int vm;
     } parts[2] = {{guards_on ? &d_glean : &d_gall, guards_on ? n_glean : 0u, 0},
                   {guards_on ? &d_gvm : &d_gall, guards_on ? n_gvm : A.n_words, 1}};
-    if (guards_on && n_fills) {
-        A.fills = d_fills.as<mxp_fill>();
-        if ((e = mxp_launch_fill(&A, n_fills, s)) != hipSuccess) return hipfail(e, "launch fill");
+    // Pipelined request chunks: the index kernel of chunk c (which ORs its true / error bits into the
+    // words the fill, guard and VM kernels wrote) runs on the side stream while chunk c + 1's fill
+    // streams its stores -- the fill is HBM-write bound, the index kernel latency bound, so they share
+    // the chip; only the last chunk's index pass is left exposed.
+    uint32_t nchunk = 1;
+    if (use_index && chunks_max > 1 && A.n >= 2 * chunk_min) nchunk = std::min<uint32_t>(chunks_max, A.n / chunk_min);
+    // chunks start at multiples of 1024 requests (the fill kernel's 16-byte rows)
+    const uint32_t step = nchunk > 1 ? (A.n / nchunk + 1023u) / 1024u * 1024u : A.n;
+    nchunk = (A.n + step - 1) / step;
+    if (nchunk > 1 && !side) {
+        if ((e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking)) != hipSuccess) {
+            side = nullptr;
+            return hipfail(e, "side stream");
+        }
+        for (auto& x : chunk_ev)
+            if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) return hipfail(e, "chunk event");
     }
-    for (const Part& P : parts) {
-        if (!P.n) continue;
-        A.glist = P.list->as<uint32_t>();
-        A.n_glist = P.n;
-        if ((e = mxp_launch_eval(&A, gx, gy_of(P.n), P.vm, s)) != hipSuccess) return hipfail(e, "launch eval");
+    if (guards_on && n_fills) A.fills = d_fills.as<mxp_fill>();
+    for (uint32_t c = 0; c < nchunk; c++) {
+        A.q0 = c * step;
+        A.q1 = std::min(A.n, (c + 1) * step);
+        const uint32_t cx = (A.q1 - A.q0 + 63) / 64;
+        if (guards_on && n_fills && (e = mxp_launch_fill(&A, n_fills, s)) != hipSuccess) return hipfail(e, "launch fill");
+        for (const Part& P : parts) {
+            if (!P.n) continue;
+            A.glist = P.list->as<uint32_t>();
+            A.n_glist = P.n;
+            if ((e = mxp_launch_eval(&A, cx, gy_of(P.n), P.vm, s)) != hipSuccess) return hipfail(e, "launch eval");
+        }
+        if (!use_index) continue;
+        if (nchunk == 1) {
+            if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
+            if ((e = mxp_launch_index(&A, (cx + 3) / 4, s)) != hipSuccess) return hipfail(e, "launch index");
+            continue;
+        }
+        if ((e = hipEventRecord(chunk_ev[c], s)) != hipSuccess) return hipfail(e, "chunk event");
+        if ((e = hipStreamWaitEvent(side, chunk_ev[c], 0)) != hipSuccess) return hipfail(e, "side wait");
+        if ((e = mxp_launch_index(&A, (cx + 3) / 4, side)) != hipSuccess) return hipfail(e, "launch index");
     }
-    if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
-    if (use_index && (e = mxp_launch_index(&A, (gx + 3) / 4, s)) != hipSuccess) return hipfail(e, "launch index");
+    if (nchunk > 1) {
+        // join: ev[1] = the main stream done (fill / guard / VM of every chunk), then the index tail
+        if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
+        if ((e = hipEventRecord(chunk_ev[kChunksMax], side)) != hipSuccess) return hipfail(e, "join event");
+        if ((e = hipStreamWaitEvent(s, chunk_ev[kChunksMax], 0)) != hipSuccess) return hipfail(e, "join wait");
+    } else if (!use_index && timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) {
+        return hipfail(e, "event");
+    }
     if (timing && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hipfail(e, "event");
     ev_index = use_index;
     return MXP_OK;
@@ -861,6 +1064,10 @@ void mxp_engine_destroy(mxp_engine* eng) {
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     for (auto& x : eng->ev)
         if (x) (void)hipEventDestroy(x);
+    if (eng->side) (void)hipStreamSynchronize(eng->side);
+    for (auto& x : eng->chunk_ev)
+        if (x) (void)hipEventDestroy(x);
+    if (eng->side) (void)hipStreamDestroy(eng->side);
     if (eng->h_stats) (void)hipHostFree(eng->h_stats);  // (synchronises with a pending stats copy)
     delete eng;
 }
@@ -913,6 +1120,13 @@ int mxp_rule_types(mxp_engine* eng, uint32_t rule, int32_t* vt, int32_t* il) {
 uint32_t mxp_rule_count(const mxp_engine* eng) { return eng ? (uint32_t)eng->rules.size() : 0; }
 uint32_t mxp_dbatch_requests(const mxp_dbatch* db) { return db ? db->n : 0; }
 
+int mxp_set_pipeline(mxp_engine* eng, uint32_t min_requests, uint32_t max_chunks) {
+    if (!eng || min_requests == 0 || max_chunks == 0 || max_chunks > mxp_engine::kChunksMax) return MXP_ERR_ARG;
+    eng->chunk_min = min_requests;
+    eng->chunks_max = max_chunks;
+    return MXP_OK;
+}
+
 int mxp_set_timing(mxp_engine* eng, int on) {
     if (!eng || eng->device < 0) return MXP_ERR_ARG;
     hipError_t e = hipSetDevice(eng->device);
@@ -962,6 +1176,20 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
         return rc;
     }
     *out = db;
+    return MXP_OK;
+}
+
+int mxp_batch_pack_host(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* out, uint32_t cap) {
+    if (!eng || !batch) return MXP_ERR_ARG;
+    if (!eng->have_rules) return eng->fail(MXP_ERR_STATE, "no rule set compiled");
+    mxp_dbatch db;
+    mxp_engine::PackedHost H;
+    int rc = eng->pack_host(batch, &db, H);
+    if (rc) return rc;
+    const uint64_t bytes = H.kinds.size() + 8 * (H.vals.size() + H.ipof.size() + H.tsof.size() + db.overlay.size()) +
+                           4 * (H.moff.size() + H.mk.size() + H.mv.size() + H.rxof.size()) + db.overlay.blob.size();
+    const uint64_t v[3] = {bytes, db.overlay.size(), db.overlay_bytes.size()};
+    for (uint32_t i = 0; out && i < cap && i < 3; i++) out[i] = v[i];
     return MXP_OK;
 }
 
@@ -1148,7 +1376,7 @@ int mxp_value_text(mxp_engine* eng, uint32_t rule, uint64_t v, char* buf, uint32
         uint64_t raw = MXP_BYTES_RAW(id);
         if (raw < eng->gbytes.size()) c = eng->gbytes[raw];
         else if (eng->last_db && raw - eng->gbytes.size() < eng->last_db->overlay_bytes.size())
-            c = eng->last_db->overlay_bytes[raw - eng->gbytes.size()];
+            c = std::string(eng->last_db->overlay_bytes[raw - eng->gbytes.size()]);
         s = mxp::go_format_bytes((const uint8_t*)c.data(), c.size());
         break;
     }

@@ -21,6 +21,7 @@
 #include "kargs.h"
 #include "lower.h"
 #include "regex.h"
+#include "par.h"
 #include "vmopt.h"
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
@@ -89,12 +90,31 @@ inline uint32_t okset_of(uint32_t kind) {
     }
 }
 
+// Strings packed 8-aligned into one blob, in the device pool layout of string_pool (desc[i] =
+// offset << 24 | length; 16 bytes of slack after finish()).
+struct StrPool {
+    std::string blob;
+    std::vector<uint64_t> desc;
+    size_t size() const { return desc.size(); }
+    std::string_view operator[](size_t i) const {
+        return std::string_view(blob.data() + (desc[i] >> 24), (size_t)(desc[i] & 0xFFFFFFu));
+    }
+    bool push(std::string_view s) {
+        if (s.size() >= (1u << 24)) return false;
+        desc.push_back(((uint64_t)blob.size() << 24) | s.size());
+        blob.append(s.data(), s.size());
+        blob.append((8 - blob.size() % 8) % 8, '\0');
+        return true;
+    }
+    void finish() { blob.append(16, '\0'); }
+};
+
 struct mxp_dbatch {
     uint32_t n = 0;
     DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
     DevBuf rxof, rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // run-time regexp patterns
-    std::vector<std::string> overlay;                 // batch strings not in the rule set's pool
-    std::vector<std::string> overlay_bytes;           // batch byte strings (canonical)
+    StrPool overlay;                                  // batch strings not in the rule set's pool
+    StrPool overlay_bytes;                            // batch byte strings not in the rule set's
     std::vector<TimeKey> overlay_times;
 };
 
@@ -153,6 +173,11 @@ struct mxp_engine : public mxp::LowerTables {
     bool timing = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     bool ev_index = false;
+    // pipelined chunks (launch): the guard-index kernel of each request chunk on a side stream
+    static constexpr uint32_t kChunksMax = 8;
+    uint32_t chunk_min = 1u << 17, chunks_max = 1;  // off by default: measured slower
+    hipStream_t side = nullptr;
+    hipEvent_t chunk_ev[kChunksMax + 1] = {};
     uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS: ablation only (1 no in-wave VM, 2 no guards: results invalid; 8 no guard index)
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
@@ -285,6 +310,16 @@ struct mxp_engine : public mxp::LowerTables {
     int evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv, std::unique_ptr<mxp_dbatch>& db);
     // wait for the evaluation, fetch and format its error records, keep `db` as the last batch
     int collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_dbatch>& db);
+    struct PackedHost {
+        std::vector<uint8_t> kinds;
+        std::vector<uint64_t> vals, ipof, tsof;
+        std::vector<uint32_t> moff, mk, mv, rxof;
+        mxp::DfaSetHost rxb;
+    };
+    mxp::SvMap gstr_view, gbytes_view, gcanon_view;  // string-view indexes of the interning tables
+    size_t views_n[3] = {~(size_t)0, 0, 0};
+    void build_views();
+    int pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H);
     int pack(const mxp_bag_batch* b, mxp_dbatch* db);
     void fill_args(mxp_kargs* A, const mxp_dbatch* db) const;
     int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
@@ -299,7 +334,7 @@ struct mxp_engine : public mxp::LowerTables {
         if (!db) db = last_db.get();
         if (sid < gstrs.size()) return gstrs[sid];
         uint64_t j = sid - gstrs.size();
-        return (db && j < db->overlay.size()) ? db->overlay[j] : std::string("?");
+        return (db && j < db->overlay.size()) ? std::string(db->overlay[j]) : std::string("?");
     }
 };
 

@@ -38,7 +38,9 @@ typedef struct mxp_kargs {
     uint32_t n_rules;
     uint32_t n_words;            // ceil(n_rules / 32)
     uint32_t groups_per_wave;
-    uint32_t n;                  // requests in the batch
+    uint32_t n;                  // requests in the batch (row stride of columns and bitmaps)
+    uint32_t q0, q1;             // requests [q0, q1) this launch evaluates (pipelined chunks)
+    uint32_t pad4;
     // columns: [n_cols][n] kinds / values (resolve columns, then virtual map[key] columns)
     const uint8_t* kinds;
     const uint64_t* vals;

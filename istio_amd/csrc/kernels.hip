@@ -484,8 +484,8 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = uni(tid >> 6);
-    const uint32_t req = blockIdx.x * 64u + lane;
-    const bool valid = req < A.n;
+    const uint32_t req = A.q0 + blockIdx.x * 64u + lane;
+    const bool valid = req < A.q1;
     const uint64_t N = A.n;
     const uint32_t i0 = (blockIdx.y * 4u + wave) * A.groups_per_wave;
     const uint32_t i1 = min(i0 + A.groups_per_wave, A.n_glist);
@@ -597,9 +597,10 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
     const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), all = uni(F->all),
                    last = uni(F->last);
     const uint64_t N = A.n;
-    const uint32_t q0 = (blockIdx.x * 4u + wave) * 256u + lane * 4u;
-    if (q0 >= N) return;
-    const bool vec = (N & 3u) == 0;  // rows 16-byte aligned, the lane's 4 requests all present
+    const uint32_t Q1 = A.q1;        // chunk end (chunks start at multiples of 1024)
+    const uint32_t q0 = A.q0 + (blockIdx.x * 4u + wave) * 256u + lane * 4u;
+    if (q0 >= Q1) return;
+    const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0;  // rows 16-byte aligned, the lane's 4 requests all present
     uint32_t bad[4];                 // per request: ~0 when the guard column fails its type check
     if (vec) {
         const uint32_t k4 = *(const uint32_t*)(A.kinds + (uint64_t)col * N + q0);
@@ -608,7 +609,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
     } else {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const bool in = q0 + r < N;
+            const bool in = q0 + r < Q1;
             const uint32_t k = in ? A.kinds[(uint64_t)col * N + q0 + r] : 0u;
             bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
         }
@@ -617,7 +618,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
         for (uint32_t g = 0; g < n; g++) {
             const uint32_t mask = g + 1 == n ? last : all;
             for (uint32_t r = 0; r < 4; r++)
-                if (bad[r] && q0 + r < N) log_guard_errors(A, mask, (g0 + g) * 32u, q0 + r);
+                if (bad[r] && q0 + r < Q1) log_guard_errors(A, mask, (g0 + g) * 32u, q0 + r);
         }
     }
     for (uint32_t g = 0; g < n; g++) {
@@ -628,7 +629,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
             if (A.out_err) *(uint4*)(A.out_err + at) = make_uint4(bad[0] & mask, bad[1] & mask, bad[2] & mask, bad[3] & mask);
         } else {
             for (uint32_t r = 0; r < 4; r++) {
-                if (q0 + r >= N) break;
+                if (q0 + r >= Q1) break;
                 if (A.out_match) A.out_match[at + r] = 0u;
                 if (A.out_err) A.out_err[at + r] = bad[r] & mask;
             }
@@ -666,7 +667,6 @@ __device__ __forceinline__ void wave_sync_lds() {
 // run entries [off, off + cnt) of the queue, cnt <= 64
 __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32_t cnt, uint64_t (*regs)[256],
                           uint32_t tid) {
-    const uint64_t N = A.n;
     const uint32_t lane = tid & 63u;
     wave_sync_lds();
     bool pending = lane < cnt;
@@ -705,7 +705,6 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
                                              uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
                                              uint32_t tid) {
     const uint32_t lane = tid & 63u;
-    const uint64_t N = A.n;
     const uint32_t* __restrict__ tmpl_of = tbl ? A.rule_tmpl2 : A.rule_tmpl;
     uint32_t j0 = 0;
     for (;;) {
@@ -787,8 +786,8 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
     PairQueue Q{wave, 0u, 0u};
-    const uint32_t req = (blockIdx.x * 4u + wave) * 64u + (tid & 63u);
-    const bool valid = req < A.n;
+    const uint32_t req = A.q0 + (blockIdx.x * 4u + wave) * 64u + (tid & 63u);
+    const bool valid = req < A.q1;
     const uint64_t N = A.n;
     // x == n_idx: a last pass with no probes that drains the pair queue
     for (uint32_t x = 0; x <= A.n_idx; x++) {
@@ -991,7 +990,7 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
 }
 
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_fill_kernel, dim3((args->n + 1023) / 1024, n_fills), dim3(256), 0, s, *args);
+    hipLaunchKernelGGL(mxp_fill_kernel, dim3((args->q1 - args->q0 + 1023) / 1024, n_fills), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

@@ -1,0 +1,115 @@
+// par.h -- host-side parallel loops and string-view hashing for batch packing (engine.cpp pack).
+#pragma once
+
+#include <stdint.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace mxp {
+
+// Threads for host loops: OMP_NUM_THREADS / MXP_PACK_THREADS when set (the GPU box exports its
+// CPU share there), else the hardware count; at most 64.
+inline unsigned pack_threads() {
+    static const unsigned n = [] {
+        const char* e = getenv("MXP_PACK_THREADS");
+        if (!e) e = getenv("OMP_NUM_THREADS");
+        long v = e ? atol(e) : 0;
+        if (v <= 0) v = (long)std::thread::hardware_concurrency();
+        return (unsigned)std::max(1L, std::min(v, 64L));
+    }();
+    return n;
+}
+
+// f(begin, end, worker) over [0, n) in contiguous slices of at least `grain` items.
+template <class F>
+void par_for(uint64_t n, uint64_t grain, F&& f) {
+    if (n == 0) return;
+    const uint64_t T = std::min<uint64_t>(pack_threads(), std::max<uint64_t>(1, n / std::max<uint64_t>(grain, 1)));
+    if (T <= 1) {
+        f(0, n, 0u);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    const uint64_t step = (n + T - 1) / T;
+    for (uint64_t t = 1; t < T; t++) {
+        const uint64_t a = t * step, b = std::min(n, a + step);
+        if (a >= b) break;
+        th.emplace_back([&f, a, b, t] { f(a, b, (unsigned)t); });
+    }
+    f(0, std::min(n, step), 0u);
+    for (auto& x : th) x.join();
+}
+
+// 64-bit hash of a byte string (wyhash-style multiply-fold over 8-byte words)
+inline uint64_t hash_bytes(const char* p, size_t n) {
+    const uint64_t k0 = 0xa0761d6478bd642full, k1 = 0xe7037ed1a0b428dbull;
+    auto mix = [](uint64_t a, uint64_t b) {
+        __uint128_t r = (__uint128_t)a * b;
+        return (uint64_t)r ^ (uint64_t)(r >> 64);
+    };
+    uint64_t h = k0 ^ (n * k1);
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w;
+        __builtin_memcpy(&w, p + i, 8);
+        h = mix(h ^ w, k1);
+    }
+    uint64_t w = 0;
+    if (i < n) __builtin_memcpy(&w, p + i, n - i);
+    return mix(h ^ w ^ ((uint64_t)(n - i) << 56), k0);
+}
+
+struct SvHash {
+    size_t operator()(std::string_view s) const noexcept { return (size_t)hash_bytes(s.data(), s.size()); }
+};
+using SvMap = std::unordered_map<std::string_view, uint32_t, SvHash>;
+
+// rep[i], i in [0, m): the first j <= i with eq(i, j) (keys given by hash(i) and eq).  Equal keys
+// have equal hashes, so the items are split into hash shards searched in parallel, each with an
+// open-addressing table visited in index order.
+template <class H, class E>
+void dedupe_first(uint32_t m, H&& hash, E&& eq, std::vector<uint32_t>& rep) {
+    rep.resize(m);
+    if (m == 0) return;
+    const unsigned T = (unsigned)std::min<uint64_t>(pack_threads(), std::max<uint64_t>(1, m / 4096));
+    std::vector<uint8_t> shard(m);
+    std::vector<std::vector<uint32_t>> items(T);
+    for (uint32_t i = 0; i < m; i++) {
+        shard[i] = (uint8_t)((hash(i) >> 40) % T);
+        items[shard[i]].push_back(i);
+    }
+    auto run = [&](unsigned t) {
+        const std::vector<uint32_t>& it = items[t];
+        size_t cap = 16;
+        while (cap < 2 * it.size()) cap <<= 1;
+        std::vector<uint32_t> tab(cap, ~0u);
+        for (uint32_t i : it) {
+            const uint64_t h = hash(i);
+            size_t k = (size_t)h & (cap - 1);
+            for (;; k = (k + 1) & (cap - 1)) {
+                const uint32_t j = tab[k];
+                if (j == ~0u) {
+                    tab[k] = i;
+                    rep[i] = i;
+                    break;
+                }
+                if (hash(j) == h && eq(i, j)) {
+                    rep[i] = j;
+                    break;
+                }
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < T; t++) th.emplace_back(run, t);
+    run(0);
+    for (auto& x : th) x.join();
+}
+
+}  // namespace mxp

@@ -47,6 +47,7 @@ SIGNATURES = {
     "mxp_pair_error": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
     "mxp_error_count": (ctypes.c_uint64, [_VP]),
     "mxp_batch_upload": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP)]),
+    "mxp_batch_pack_host": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]),
     "mxp_batch_free": (None, [_VP, _VP]),
     "mxp_batch_eval_device": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
     "mxp_hits_device": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP]),
@@ -75,6 +76,7 @@ SIGNATURES = {
                                               ctypes.c_void_p]),
     "mxp_batch_eval_device_hits": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     "mxp_set_timing": (ctypes.c_int, [_VP, ctypes.c_int]),
+    "mxp_set_pipeline": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32]),
     "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
 }
@@ -175,6 +177,10 @@ class Engine:
         vt, il = ctypes.c_int32(), ctypes.c_int32()
         self._check(self.lib.mxp_rule_types(self.h, rule, ctypes.byref(vt), ctypes.byref(il)), "mxp_rule_types")
         return vt.value, il.value
+
+    def set_pipeline(self, min_requests: int = 1 << 17, max_chunks: int = 8):
+        """Request chunks whose guard-index pass overlaps the next chunk's fill (mxp_set_pipeline)."""
+        self._check(self.lib.mxp_set_pipeline(self.h, min_requests, max_chunks), "mxp_set_pipeline")
 
     def set_timing(self, on: bool = True):
         self._check(self.lib.mxp_set_timing(self.h, int(on)), "mxp_set_timing")
@@ -293,6 +299,12 @@ class Engine:
         return int(self.lib.mxp_error_count(self.h))
 
     # ------------------------------------------------------------------ device-resident batches
+    def pack_host(self, batch: BagBatch) -> dict:
+        """Host half of upload alone (mxp_batch_pack_host): packed bytes, overlay strings / byte strings."""
+        out = (ctypes.c_uint64 * 3)()
+        self._check(self.lib.mxp_batch_pack_host(self.h, ctypes.byref(batch.c_struct()), out, 3), "mxp_batch_pack_host")
+        return {"bytes": out[0], "overlay_strings": out[1], "overlay_bytes": out[2]}
+
     def upload(self, batch: BagBatch) -> "DeviceBatch":
         h = _VP()
         self._check(self.lib.mxp_batch_upload(self.h, ctypes.byref(batch.c_struct()), ctypes.byref(h)), "mxp_batch_upload")

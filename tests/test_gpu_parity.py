@@ -313,3 +313,42 @@ def test_duplicate_rules_parity(mxp, knobs, monkeypatch):
     ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
     got, want = compare(eng, ev, rules, batch, sample_msgs=400)
     assert (want == 1).sum() > 1000 and (want >= 2).sum() > 1000
+
+
+@pytest.mark.parametrize("family,n,min_req,chunks", [("c2", 65536, 8192, 8), ("c2", 5000, 500, 8),
+                                                     ("c4", 8000, 2048, 3), ("fuzz", 5000, 1024, 4)])
+def test_pipelined_chunks_parity(mxp, family, n, min_req, chunks):
+    """mxp_set_pipeline: request chunks whose guard-index pass runs on the side stream, overlapped with
+    the next chunk's fill / guard / VM kernels.  Host path against the oracle, the device path (with
+    fused hit counters) against the unpipelined evaluation, ragged chunk ends included."""
+    import torch
+    if family == "c2":
+        manifest, rules, batch = W.c2_workload(n_rules=700, n_requests=n, seed=9)
+    elif family == "c4":
+        manifest, rules, batch = W.c4_workload(n_rules=1500, n_requests=n)
+    else:
+        manifest = W.DEFAULT_TEST_MANIFEST
+        rules = W.guarded_fuzz_rules(1500, seed=43)
+        batch = BagBatch.from_bags(W.fuzz_bags(n, seed=44), names=list(manifest))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    eng.set_pipeline(min_req, chunks)
+    if family != "fuzz":
+        compare(eng, oracle.OracleEvaluator(manifest), rules, batch, sample_msgs=100)
+    db = eng.upload(batch)
+    Wd = (len(rules) + 31) // 32
+    outs = []
+    s = torch.cuda.current_stream().cuda_stream
+    for pipe in ((min_req, chunks), (1 << 30, 1)):
+        eng.set_pipeline(*pipe)
+        dm = torch.full((Wd, batch.n), -1, dtype=torch.int32, device="cuda:0")
+        de = torch.full_like(dm, -1)
+        hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
+        db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s)
+        torch.cuda.synchronize()
+        outs.append((dm.cpu().numpy(), de.cpu().numpy(), hits.cpu().numpy()))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    codes = mxp.bits_to_codes(outs[0][0].view(np.uint32), outs[0][1].view(np.uint32), len(rules))
+    assert np.array_equal(outs[0][2], (codes == 1).sum(axis=0))
