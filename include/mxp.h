@@ -77,6 +77,40 @@ int mxp_rule_types(mxp_engine* eng, uint32_t rule, int32_t* value_type, int32_t*
 int mxp_eval_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* match_bits, uint32_t* err_bits);
 
 /*
+ * Referenced attributes (the precondition cache key of a Check response): for every request, the
+ * attribute reads EvalPredicate of every rule performs on its bag -- ProtoBag.Get / StringMap.Get
+ * tracking (mixer/pkg/attribute/protoBag.go:78-159), the set grpcServer.Check returns as
+ * ReferencedAttributes (mixer/pkg/api/grpcServer.go:177).  Short-circuiting makes it path
+ * dependent; the engine records the reads its VM performs and adds the reads its guard and index
+ * phases stand for.
+ *   attr  position of the attribute in the mxp_vocab_set names;
+ *   key   MXP_REF_NOKEY for an attribute reference, else the string id of the map key
+ *         (StringMap.Get; text with mxp_string_text while this batch is the engine's last);
+ *   cond  MXP_REF_ABSENCE / MXP_REF_EXACT (mixer/v1 ReferencedAttributes.Condition), or MXP_REF_MAP
+ *         for a string map fetched whole: the test FakeBag lists its name (fakebag.go:54-60), a
+ *         ProtoBag does not record it (protoBag.go:109-112) -- a cgo shim drops these entries.
+ * Per request the entries are sorted by (attr, key) and distinct.  ref_off has n_requests + 1
+ * entries; when cap is too small MXP_ERR_NOMEM is returned with ref_off complete (retry with
+ * ref_off[n]).  match_bits / err_bits as mxp_eval_batch (may be NULL).  MXP_ERR_STATE when a rule is
+ * MXP_RULE_UNSUPPORTED (its reads are unknown).  destination.* -> target.* fallbacks (compatBag,
+ * grpcServer.go:93-107) happen while packing, in the caller, and are expanded there.
+ */
+#define MXP_REF_NOKEY 0xFFFFFFFFu
+#define MXP_REF_ABSENCE 1u
+#define MXP_REF_EXACT 2u
+#define MXP_REF_MAP 16u
+typedef struct mxp_attr_ref {
+    uint32_t attr;
+    uint32_t key;
+    uint32_t cond;
+    uint32_t pad;
+} mxp_attr_ref;
+int mxp_eval_refs(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* match_bits, uint32_t* err_bits,
+                  uint64_t* ref_off, mxp_attr_ref* refs, uint64_t cap);
+/* Text of an engine string id of the last evaluated batch (map keys of mxp_eval_refs). */
+int mxp_string_text(mxp_engine* eng, uint32_t sid, char* buf, uint32_t cap);
+
+/*
  * Eval (expr.Evaluator.Eval) for small batches: raw result register per pair, [n_requests][n_rules],
  * plus per-pair code (0 false/ok, 1 true, 2 error, 3 panic).  Decode with mxp_value_text.
  */
@@ -121,6 +155,15 @@ int mxp_resolver_set(mxp_engine* eng, const char* identity_attr, const char* def
                      const uint8_t* empty_match, uint32_t n);
 int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
                       uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap);
+/* mxp_resolve_batch plus each Resolve's referenced attributes (mxp_attr_ref, as mxp_eval_refs): the
+ * identity attribute; when it is a string, context.protocol (filterActions, resolver.go:208); and the
+ * reads of the predicates filterActions evaluates, in order, up to and including the first that
+ * fails.  ref_off / refs / ref_cap as mxp_eval_refs; MXP_ERR_NOMEM when either capacity is short,
+ * with both offset arrays complete.  An identity or protocol attribute outside the vocabulary is
+ * not listed (entries are vocabulary positions). */
+int mxp_resolve_refs(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
+                     uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap, uint64_t* ref_off,
+                     mxp_attr_ref* refs, uint64_t ref_cap);
 
 /*
  * List adapter (mixer/adapter/list): membership checks of a batch of symbols against one list.

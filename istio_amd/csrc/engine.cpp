@@ -15,6 +15,7 @@
 // ------------------------------------------------------------------------------------ compile
 int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     reset_tables();
+    ref_comp.clear();
     views_n[0] = ~(size_t)0;  // string-view indexes rebuilt at the next pack
     rules.resize(n);
     std::vector<mxp_vm_ins> all;
@@ -205,6 +206,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
                 rule_tmpl2[i] = it->second;
             }
             comp_of[{gd.col, sa.col}][{k1, sa.k2}].push_back(i);
+            ref_comp.push_back(RefComposite{gd.col & 0xFFFFFFu, sa.col, (uint32_t)k1, i});
             n_composite++;
             continue;
         }
@@ -394,6 +396,22 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     n_glean = (uint32_t)glean.size();
     n_gvm = (uint32_t)gvm.size();
     n_segs = (uint32_t)segs.size();
+
+    // referenced attributes (mxp_eval_refs): the guard of every guarded rule reads its column for
+    // every request; map keys of virtual columns get string ids of their own
+    ref_guard.assign(n, MXP_VM_DONE);
+    for (uint32_t i = 0; i < n; i++)
+        if ((guards[i].mode & 0xFF) != GM_NONE) ref_guard[i] = guards[i].col & 0xFFFFFFu;
+    ref_alias_off.assign(n + 1, 0);
+    ref_aliases.clear();
+    for (uint32_t i = 0; i < n; i++) {
+        ref_aliases.insert(ref_aliases.end(), aliases_of[i].begin(), aliases_of[i].end());
+        ref_alias_off[i + 1] = (uint32_t)ref_aliases.size();
+    }
+    vcol_key_sid.resize(vcols.size());
+    for (size_t j = 0; j < vcols.size(); j++) vcol_key_sid[j] = intern_string(vcols[j].second);
+    refs_exact = true;
+    for (auto& R : rules) refs_exact &= R.status != MXP_RULE_UNSUPPORTED;
 
     have_rules = true;
     if (device < 0) return MXP_OK;  // host-only engine: compile / inspect, no device tables
@@ -891,6 +909,12 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         A.errcount = d_errcount.as<uint32_t>();
         A.errcap = errcap;
     }
+    if (refs_on) {
+        if ((e = hipMemsetAsync(d_refcount.p, 0, 4, s)) != hipSuccess) return hipfail(e, "memset refcount");
+        A.refs = d_refs.as<mxp_ref_rec>();
+        A.refcount = d_refcount.as<uint32_t>();
+        A.refcap = refcap;
+    }
     if (A.n == 0 || A.n_rules == 0) return MXP_OK;
     // guard-index phase: predicate mode only (Eval runs whole programs in mxp_eval_kernel)
     const bool use_index = !d_vals && !(debug_flags & 2u) && n_idx > 0;
@@ -1077,7 +1101,11 @@ const char* mxp_last_error(const mxp_engine* eng) { return eng ? eng->last_error
 int mxp_vocab_set(mxp_engine* eng, const char* const* names, const int32_t* types, uint32_t n) {
     if (!eng || (n && (!names || !types))) return MXP_ERR_ARG;
     eng->vocab.clear();
-    for (uint32_t i = 0; i < n; i++) eng->vocab[names[i]] = types[i];
+    eng->vocab_index.clear();
+    for (uint32_t i = 0; i < n; i++) {
+        eng->vocab[names[i]] = types[i];
+        eng->vocab_index[names[i]] = i;
+    }
     eng->reset_tables();
     return MXP_OK;
 }

@@ -124,6 +124,7 @@ struct mxp_engine : public mxp::LowerTables {
     std::string last_error;
 
     mxp::Vocabulary vocab;
+    std::unordered_map<std::string, uint32_t> vocab_index;  // name -> position in mxp_vocab_set order
     mxp::FuncMap fmap = mxp::default_func_map();
 
     // rule-set-global interning
@@ -173,6 +174,30 @@ struct mxp_engine : public mxp::LowerTables {
     bool timing = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     bool ev_index = false;
+    // referenced attributes (mxp_eval_refs, refs.cpp)
+    struct RefComposite {
+        uint32_t a_col, b_col, k1, rule;  // `A == K1 && B.startsWith(K2) ...`: B is read iff A == K1
+    };
+    std::vector<RefComposite> ref_comp;
+    std::vector<uint32_t> ref_guard;               // [rule] column its guard reads (MXP_VM_DONE: none)
+    std::vector<uint32_t> ref_alias_off, ref_aliases;  // duplicate indexed rules (records name the canonical rule)
+    std::vector<uint32_t> vcol_key_sid;            // [virtual column] string id of its map key
+    bool refs_exact = true;                        // false: a rule the lowering does not support
+    bool refs_on = false;                          // launch(): use the *_refs kernels
+    DevBuf d_refs, d_refcount;
+    uint32_t refcap = 1u << 20;
+    struct RefScope {  // mxp_resolve_refs: one Resolve per request (resolver.cpp results)
+        const std::vector<uint32_t>* info;  // namespace id | tcp << 31, or MXP_NS_MISSING / MXP_NS_NOTSTRING
+        const uint8_t* status;
+        const uint32_t* err_rule;
+        uint32_t variety;
+    };
+    int refs_evaluate(const mxp_bag_batch* b, DevBuf& dm, DevBuf& de, std::unique_ptr<mxp_dbatch>& db,
+                      std::vector<mxp_ref_rec>& recs);
+    int refs_assemble(const mxp_bag_batch* b, const std::vector<mxp_ref_rec>& recs, const RefScope* scope,
+                      uint64_t* ref_off, mxp_attr_ref* out, uint64_t cap);
+    int eval_refs(const mxp_bag_batch* b, uint32_t* match, uint32_t* err, uint64_t* ref_off, mxp_attr_ref* out,
+                  uint64_t cap);
     // pipelined chunks (launch): the guard-index kernel of each request chunk on a side stream
     static constexpr uint32_t kChunksMax = 8;
     uint32_t chunk_min = 1u << 17, chunks_max = 1;  // off by default: measured slower

@@ -72,6 +72,9 @@ typedef struct mxp_kargs {
     uint64_t* stats;             // optional [1] += true pairs the guard-index kernel set
     mxp_err_rec* errlog;
     uint32_t* errcount;
+    mxp_ref_rec* refs;           // optional: referenced-attribute records (the *_refs kernels)
+    uint32_t* refcount;
+    uint32_t refcap;
     uint32_t errcap;
     uint32_t flags;              // debug / ablation: 1 = skip in-wave VM, 2 = no guards (results invalid)
 } mxp_kargs;

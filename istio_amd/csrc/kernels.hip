@@ -141,6 +141,25 @@ typedef __attribute__((address_space(4))) const uint32_t cuint32;
 // P[pc] (pc in [pc0, len)), fetched with one scalar s_load_dwordx4 per step.  `rule` may differ
 // per lane (template batches of the guard-index kernel); it only names the pair in error records and
 // Eval results.  The register file is regs[reg][thread] in LDS.
+// Referenced-attribute tracking (mxp_eval_refs): one record per attribute read the VM performs
+// (VM_RES / VM_TRES / VM_VCOL: slot = column; VM_LOOKUP[K]: the map key), appended with one atomic
+// per wavefront.  Records past refcap are counted, not stored (the host re-runs with more room).
+__device__ __forceinline__ void ref_rec(const mxp_kargs& A, bool on, uint32_t req, uint32_t rule, uint32_t slot,
+                                        uint32_t key) {
+    const uint64_t m = __ballot(on);
+    if (!m) return;
+    const uint32_t lane = __lane_id();
+    const uint32_t first = (uint32_t)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(A.refcount, (uint32_t)__builtin_popcountll(m));
+    base = __builtin_amdgcn_readlane(base, first);
+    if (on) {
+        const uint32_t i = base + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (i < A.refcap) A.refs[i] = mxp_ref_rec{req, rule, slot, key};
+    }
+}
+
+template <bool kRefs>
 __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint32_t pc0, bool live, uint32_t rule,
                              uint32_t req, uint64_t (*regs)[256], uint32_t tid, bool fan = false) {
 #define REG(i) regs[i][tid]
@@ -190,6 +209,7 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
         switch (op) {
         case VM_RES:
         case VM_TRES: {
+            if constexpr (kRefs) ref_rec(A, live, req, rule, x, MXP_VM_DONE);
             if (live) {
                 const uint64_t at = (uint64_t)x * N + req;
                 const uint32_t k = A.kinds[at];
@@ -214,6 +234,7 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
             break;
         }
         case VM_VCOL: {
+            if constexpr (kRefs) ref_rec(A, live, req, rule, x, MXP_VM_DONE);
             if (live) {
                 const uint64_t at = (uint64_t)x * N + req;
                 const uint32_t k = A.kinds[at];
@@ -278,7 +299,9 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
             }
             break;
         case VM_LOOKUP:
-        case VM_LOOKUPK:
+        case VM_LOOKUPK: {
+            bool rec = false;
+            uint32_t rslot = 0, rkey = 0;
             if (live) {
                 const uint64_t h = REG(a);
                 const uint32_t key = op == VM_LOOKUP ? (uint32_t)REG(b) : x;
@@ -293,6 +316,9 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
                             found = A.map_vals[e];
                             break;
                         }
+                    rec = true;
+                    rslot = MXP_REF_LOOKUP | (found != MXP_VM_DONE ? MXP_REF_FOUND : 0u) | (m & MXP_REF_MAPID);
+                    rkey = key;
                     if (found != MXP_VM_DONE) {
                         REG(d) = found;
                         if (y == LK_TRY) JUMP(z);
@@ -303,7 +329,9 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
                     }
                 }
             }
+            if constexpr (kRefs) ref_rec(A, rec, req, rule, rslot, rkey);
             break;
+        }
         case VM_STRFN:
         case VM_STRFNK:
             if (live) {
@@ -479,7 +507,7 @@ __device__ __forceinline__ void log_guard_errors(const mxp_kargs& A, uint32_t e,
 // mxp_guard_kernel, which carries no VM and so keeps far fewer registers.  Group descriptors are
 // fetched four at a time with one vector load (lane 16 j + f = word f of the j-th group) and read
 // back with v_readlane.  Results: one coalesced store per word and plane, out[g * N + request].
-template <bool kVM>
+template <bool kVM, bool kRefs = false>
 __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)[256]) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -555,7 +583,7 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
                     const uint32_t pc0 = (!guards_on || (gm & 0xFFu) == GM_NONE) ? 0u : (gm >> 16);
                     const uint32_t base = uni(A.rule_off[rule]);
                     const uint32_t len = uni(A.rule_off[rule + 1]) - base;
-                    const uint32_t code = run_rule(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, pc0, need, rule,
+                    const uint32_t code = run_rule<kRefs>(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, pc0, need, rule,
                                                    req, regs, tid);
                     if (need) {
                         m |= code == PC_TRUE ? bit : 0u;
@@ -585,6 +613,12 @@ extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
 }
 
 extern "C" __global__ __launch_bounds__(256) void mxp_guard_kernel(mxp_kargs A) { eval_groups<false>(A, nullptr); }
+
+// mxp_eval_kernel with referenced-attribute records (mxp_eval_refs)
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_refs_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    eval_groups<true, true>(A, regs);
+}
 
 // Chunks of uniform indexed groups (vm.h mxp_fill): every word is a function of the guard column's
 // kind alone -- match 0, error = the rules whose type check fails -- so a lane computes it once for
@@ -665,6 +699,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 }
 
 // run entries [off, off + cnt) of the queue, cnt <= 64
+template <bool kRefs>
 __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32_t cnt, uint64_t (*regs)[256],
                           uint32_t tid) {
     const uint32_t lane = tid & 63u;
@@ -688,7 +723,7 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
         if (mine)
             for (uint32_t c = 0; c < nconst; c++) regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
         cuint32* P = ((cuint32*)A.prog) + ((uint64_t)toff - pc0) * 4u;
-        const uint32_t code = run_rule(A, P, len_t, pc0, mine, rule, req, regs, tid, true);
+        const uint32_t code = run_rule<kRefs>(A, P, len_t, pc0, mine, rule, req, regs, tid, true);
         if (mine) {
             if (code == PC_TRUE) Q.ntrue += set_true(A, rule, req);
             if (code >= PC_ERROR) set_error(A, rule, req);
@@ -701,6 +736,7 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
 // OR-ed at once) and runs full 64-pair batches; `final` drains the queue.  Long lists go in rounds
 // of up to (free entries / 64) postings per lane, so the queue never overflows and the VM has one
 // call site (one inlined copy).
+template <bool kRefs>
 __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, uint32_t tbl, uint32_t start,
                                              uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
                                              uint32_t tid) {
@@ -730,7 +766,7 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
         const bool more = __ballot(j0 < len) != 0;
         if (Q.n >= 64u || (Q.n > 0u && (final || more))) {
             const uint32_t k = min(Q.n, 64u);
-            run_pairs(A, Q, Q.n - k, k, regs, tid);
+            run_pairs<kRefs>(A, Q, Q.n - k, k, regs, tid);
             Q.n -= k;
             continue;
         }
@@ -781,8 +817,10 @@ struct PrefixHash {
 // Workgroup = 4 wavefronts, one tile of 64 requests each (one request per lane).  mxp_eval_kernel
 // has already written both bitmaps for these rules (match 0, error on a failed type check of the
 // guard column); true and error results are OR-ed in.
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index_kernel(mxp_kargs A) {
-    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+namespace {
+
+template <bool kRefs>
+__device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
     PairQueue Q{wave, 0u, 0u};
@@ -863,7 +901,8 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
                     len = A.hents[fi].len;
                 }
             }
-            if (final || __ballot(len != 0)) process_slot(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
+            if (final || __ballot(len != 0))
+                process_slot<kRefs>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
         }
     }
     if (A.stats) {
@@ -872,6 +911,19 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
         for (int off = 32; off > 0; off >>= 1) t += (uint32_t)__shfl_xor((int)t, off, 64);
         if ((tid & 63u) == 0 && t) atomicAdd((unsigned long long*)A.stats, (unsigned long long)t);
     }
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    index_body<false>(A, regs);
+}
+
+// mxp_index_kernel with referenced-attribute records (mxp_eval_refs)
+extern "C" __global__ __launch_bounds__(256) void mxp_index_refs_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    index_body<true>(A, regs);
 }
 
 // Per-rule hit counters: hits[rule] += number of requests whose match bit for the rule is set.
@@ -982,7 +1034,9 @@ extern "C" __global__ __launch_bounds__(256) void mxp_hits_ragged_kernel(const u
 }
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s) {
-    if (vm)
+    if (vm && args->refs)
+        hipLaunchKernelGGL(mxp_eval_refs_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    else if (vm)
         hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
     else
         hipLaunchKernelGGL(mxp_guard_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
@@ -995,7 +1049,10 @@ extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, h
 }
 
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_index_kernel, dim3(grid), dim3(256), 0, s, *args);
+    if (args->refs)
+        hipLaunchKernelGGL(mxp_index_refs_kernel, dim3(grid), dim3(256), 0, s, *args);
+    else
+        hipLaunchKernelGGL(mxp_index_kernel, dim3(grid), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

@@ -102,8 +102,14 @@ int mxp_resolver_set(mxp_engine* eng, const char* identity_attr, const char* def
     return MXP_OK;
 }
 
-int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
-                      uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap) {
+}  // extern "C"
+
+namespace {
+
+// mxp_resolve_batch, and with ref_off its referenced attributes (mxp_resolve_refs)
+int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status, uint32_t* err_rule,
+                 uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap, uint64_t* ref_off, mxp_attr_ref* refs,
+                 uint64_t ref_cap) {
     if (!eng || !batch || !status || !err_rule || !sel_off || (sel_cap && !sel_rules) || variety >= 32)
         return MXP_ERR_ARG;
     if (!eng->resolver.set) return eng->fail(MXP_ERR_STATE, "resolver not configured (mxp_resolver_set)");
@@ -113,7 +119,8 @@ int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t vari
     const uint32_t W = (NR + 31) / 32;
     std::unique_ptr<mxp_dbatch> db;
     DevBuf dm, de;
-    int rc = eng->evaluate(batch, dm, de, nullptr, db);
+    std::vector<mxp_ref_rec> recs;
+    int rc = ref_off ? eng->refs_evaluate(batch, dm, de, db, recs) : eng->evaluate(batch, dm, de, nullptr, db);
     if (rc) return rc;
     // per-word masks: applicability for the variety (per request tcp flag), empty matches
     std::vector<uint32_t> amask(2 * (size_t)W, 0), empty(W, 0);
@@ -164,6 +171,12 @@ int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t vari
     if (n && (e = hipMemcpyAsync(err_rule, d_err_rule.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
         return eng->hipfail(e, "download err_rule");
     if ((rc = eng->collect_errors(batch, db))) return rc;  // synchronises the stream
+    int ref_rc = MXP_OK;
+    if (ref_off) {
+        const mxp_engine::RefScope scope{&info, status, err_rule, variety};
+        ref_rc = eng->refs_assemble(batch, recs, &scope, ref_off, refs, ref_cap);
+        if (ref_rc && ref_rc != MXP_ERR_NOMEM) return ref_rc;
+    }
     sel_off[0] = 0;
     for (uint32_t q = 0; q < n; q++) sel_off[q + 1] = sel_off[q] + count[q];
     const uint64_t total = sel_off[n];
@@ -178,7 +191,23 @@ int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t vari
             return eng->hipfail(e, "download sel");
         if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "resolve sync");
     }
-    return MXP_OK;
+    return ref_rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
+                      uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap) {
+    return resolve_impl(eng, batch, variety, status, err_rule, sel_off, sel_rules, sel_cap, nullptr, nullptr, 0);
+}
+
+int mxp_resolve_refs(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
+                     uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap, uint64_t* ref_off,
+                     mxp_attr_ref* refs, uint64_t ref_cap) {
+    if (!ref_off) return MXP_ERR_ARG;
+    return resolve_impl(eng, batch, variety, status, err_rule, sel_off, sel_rules, sel_cap, ref_off, refs, ref_cap);
 }
 
 }  // extern "C"

@@ -264,6 +264,19 @@ typedef struct mxp_vm_ins {
 // virtual-column kinds (VM_VCOL)
 enum mxp_vcol_kind { VC_ABSENT = 0, VC_VALUE = 1, VC_NOTMAP = 3 };
 
+// referenced-attribute record (mxp_eval_refs): an attribute read by the VM for (req, rule).
+// slot: a column index (VM_RES / VM_TRES / VM_VCOL; key = MXP_VM_DONE), or MXP_REF_LOOKUP | found |
+// batch map id for a map lookup (VM_LOOKUP[K]; key = the key's string id)
+#define MXP_REF_LOOKUP 0x80000000u
+#define MXP_REF_FOUND 0x40000000u
+#define MXP_REF_MAPID 0x3FFFFFFFu
+typedef struct mxp_ref_rec {
+    uint32_t req;
+    uint32_t rule;
+    uint32_t slot;
+    uint32_t key;
+} mxp_ref_rec;
+
 // error log record (one per error pair, capacity-bounded)
 typedef struct mxp_err_rec {
     uint32_t req;

@@ -41,6 +41,10 @@ SIGNATURES = {
     "mxp_rule_vm_text": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
     "mxp_rule_types": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)]),
     "mxp_eval_batch": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
+    "mxp_eval_refs": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64]),
+    "mxp_string_text": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
+    "mxp_resolve_refs": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP, _VP, _VP, ctypes.c_uint64, _VP, _VP,
+                                        ctypes.c_uint64]),
     "mxp_eval_values": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
     "mxp_value_text": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint32]),
     "mxp_value_kind": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint64]),
@@ -105,6 +109,21 @@ def load_library(path: str = LIB_PATH):
     return _LIB
 
 
+# referenced-attribute conditions (include/mxp.h mxp_attr_ref)
+REF_NOKEY, REF_ABSENCE, REF_EXACT, REF_MAP = 0xFFFFFFFF, 1, 2, 16
+
+
+def fakebag_list(refs_row):
+    """FakeBag.ReferencedList form (il/testing/fakebag.go:75-89): sorted "name" / "name[key]"."""
+    return sorted({a if k is None else "%s[%s]" % (a, k) for a, k, _ in refs_row})
+
+
+def protobag_set(refs_row):
+    """ProtoBag referencedAttrs form (protoBag.go:149-159): {(name, key or "", condition)}, string maps
+    fetched whole not recorded."""
+    return {(a, k or "", c) for a, k, c in refs_row if c != REF_MAP}
+
+
 class MxpError(RuntimeError):
     pass
 
@@ -146,6 +165,7 @@ class Engine:
         arr = (ctypes.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
         tarr = (ctypes.c_int32 * max(len(types), 1))(*types)
         self._check(self.lib.mxp_vocab_set(self.h, arr, tarr, len(names)), "mxp_vocab_set")
+        self.vocab_names = names
         self.rules = []
 
     def compile(self, rules: Sequence[str]) -> np.ndarray:
@@ -208,6 +228,67 @@ class Engine:
         self._check(self.lib.mxp_eval_batch(self.h, ctypes.byref(batch.c_struct()), match.ctypes.data, err.ctypes.data),
                     "mxp_eval_batch")
         return match, err
+
+    def eval_refs(self, batch: BagBatch, cap: int = 0):
+        """mxp_eval_refs -> (match, err, refs): refs[q] = [(attribute, map key or None, cond)], cond one of
+        REF_ABSENCE / REF_EXACT / REF_MAP, sorted by (vocabulary position, key id)."""
+        W = (len(self.rules) + 31) // 32
+        match = np.zeros((W, batch.n), dtype=np.uint32)
+        err = np.zeros((W, batch.n), dtype=np.uint32)
+        off = np.zeros(batch.n + 1, dtype=np.uint64)
+        cap = cap or 16 * max(batch.n, 1)
+        while True:
+            ents = np.zeros((max(cap, 1), 4), dtype=np.uint32)
+            rc = self.lib.mxp_eval_refs(self.h, ctypes.byref(batch.c_struct()), match.ctypes.data, err.ctypes.data,
+                                        off.ctypes.data, ents.ctypes.data, cap)
+            if rc == 4 and int(off[-1]) > cap:  # MXP_ERR_NOMEM: retry with the exact size
+                cap = int(off[-1])
+                continue
+            self._check(rc, "mxp_eval_refs")
+            break
+        return match, err, self._decode_refs(batch.n, off, ents)
+
+    def resolve_refs(self, batch: BagBatch, variety: int, cap: int = 0):
+        """mxp_resolve_refs -> (status, err_rule, selected, refs) (see resolve / eval_refs)."""
+        n = batch.n
+        status = np.zeros(n, dtype=np.uint8)
+        err_rule = np.zeros(n, dtype=np.uint32)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        roff = np.zeros(n + 1, dtype=np.uint64)
+        scap, rcap = max(16, n * 4), cap or 16 * max(n, 1)
+        while True:
+            sel = np.zeros(scap, dtype=np.uint32)
+            ents = np.zeros((max(rcap, 1), 4), dtype=np.uint32)
+            rc = self.lib.mxp_resolve_refs(self.h, ctypes.byref(batch.c_struct()), variety, status.ctypes.data,
+                                           err_rule.ctypes.data, off.ctypes.data, sel.ctypes.data, scap,
+                                           roff.ctypes.data, ents.ctypes.data, rcap)
+            if rc == 4 and (int(off[n]) > scap or int(roff[n]) > rcap):
+                scap, rcap = max(scap, int(off[n])), max(rcap, int(roff[n]))
+                continue
+            self._check(rc, "mxp_resolve_refs")
+            break
+        return (status, err_rule, [sel[int(off[q]):int(off[q + 1])] for q in range(n)],
+                self._decode_refs(n, roff, ents))
+
+    def _decode_refs(self, n, off, ents):
+        keys = {}
+        refs = []
+        for q in range(n):
+            row = []
+            for a, k, c, _ in ents[int(off[q]):int(off[q + 1])]:
+                key = None
+                if k != REF_NOKEY:
+                    if k not in keys:
+                        keys[k] = self.string_text(int(k))
+                    key = keys[k]
+                row.append((self.vocab_names[a], key, int(c)))
+            refs.append(row)
+        return refs
+
+    def string_text(self, sid: int) -> str:
+        buf = ctypes.create_string_buffer(1 << 16)
+        self._check(self.lib.mxp_string_text(self.h, sid, buf, 1 << 16), "mxp_string_text")
+        return buf.value.decode("utf-8", "surrogateescape")
 
     def eval_codes(self, batch: BagBatch) -> np.ndarray:
         """Per-pair codes [N, R] (FALSE/TRUE/ERROR/PANIC) via eval_values."""

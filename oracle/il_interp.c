@@ -141,10 +141,38 @@ static uint32_t alloc_size(uint8_t t) {
 }
 
 /* ---------------------------------------------------------------------------- bag access */
+/* Referenced-attribute tracking (il/testing/fakebag.go:54-60,102-115): every Get(name) records
+ * `name`, every StringMap.Get(key) records `name[key]`, found or not. */
+typedef struct ref_ent {
+    const uint8_t* name;
+    uint32_t nlen;
+    int32_t klen;            /* -1: attribute reference, else map key length */
+    const uint8_t* key;
+} ref_ent;
+typedef struct ref_track {
+    ref_ent* e;
+    uint32_t n, cap;
+} ref_track;
+
+static void track_push(ref_track* t, const uint8_t* name, uint32_t nlen, const uint8_t* key, int32_t klen) {
+    if (!t) return;
+    if (t->n == t->cap) {
+        t->cap = t->cap ? 2 * t->cap : 64;
+        t->e = (ref_ent*)realloc(t->e, sizeof(ref_ent) * t->cap);
+    }
+    t->e[t->n].name = name;
+    t->e[t->n].nlen = nlen;
+    t->e[t->n].key = key;
+    t->e[t->n].klen = klen;
+    t->n++;
+}
+
 typedef struct bagctx {
     const mxp_bag_batch* b;
     const int32_t* col_of_sid;  /* program string id -> batch column, -1 when absent */
     uint32_t req;
+    const struct oracle_prog* prog;
+    ref_track* track;           /* NULL: no tracking */
 } bagctx;
 
 static gv gv_string(const uint8_t* p, uint32_t n) {
@@ -165,6 +193,7 @@ static gv batch_str(const mxp_bag_batch* b, uint32_t sid, uint8_t kind) {
 
 /* attribute.Bag.Get(name) for the program string `sid` */
 static int bag_get(const bagctx* c, uint32_t sid, gv* out) {
+    if (c->track) track_push(c->track, str_ptr(c->prog, sid), str_len(c->prog, sid), NULL, -1);
     int32_t col = c->col_of_sid[sid];
     if (col < 0) return 0;
     const mxp_bag_batch* b = c->b;
@@ -180,15 +209,20 @@ static int bag_get(const bagctx* c, uint32_t sid, gv* out) {
     case MXP_BOOL: out->k = GV_BOOL; out->i = v ? 1 : 0; return 1;
     case MXP_DURATION: out->k = GV_DURATION; out->i = (int64_t)v; return 1;
     case MXP_TIMESTAMP: out->k = GV_TIME; out->i = b->time_sec[v]; out->ns = b->time_nsec[v]; return 1;
-    case MXP_STRING_MAP: out->k = GV_MAP; out->i = (int64_t)v; return 1;
+    case MXP_STRING_MAP:  /* the map remembers its attribute name (p / len) for StringMap.Get tracking */
+        out->k = GV_MAP; out->i = (int64_t)v;
+        out->p = str_ptr(c->prog, sid); out->len = str_len(c->prog, sid);
+        return 1;
     case MXP_OTHER: out->k = GV_OTHER; out->i = (int64_t)v; return 1;
     default: return 0;
     }
 }
 
 /* il.MapGet (il/types.go:88-98); returns -1 when the value is not a map (Go panics). */
-static int map_get(const mxp_bag_batch* b, const gv* m, const uint8_t* key, uint32_t klen, gv* out) {
+static int map_get(const bagctx* c, const gv* m, const uint8_t* key, uint32_t klen, gv* out) {
+    const mxp_bag_batch* b = c->b;
     if (m->k != GV_MAP) return -1;
+    if (c->track) track_push(c->track, m->p, m->len, key, (int32_t)klen);
     for (uint64_t e = b->map_offsets[m->i]; e < b->map_offsets[m->i + 1]; e++) {
         uint32_t ks = b->map_keys[e];
         uint32_t n = (uint32_t)(b->str_offsets[ks + 1] - b->str_offsets[ks]);
@@ -757,7 +791,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
             gv key = heap[t1];
             if (t2 >= hp) BADHEAP;
             gv m = heap[t2];
-            int f = map_get(b, &m, key.p, key.len, &tv);
+            int f = map_get(bc, &m, key.p, key.len, &tv);
             if (f < 0) PANIC("Unknown map type");
             if (code == OP_TLookup) {
                 if (f) {
@@ -792,7 +826,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
             t2 = opstack[sp];
             if (t2 >= hp) BADHEAP;
             gv m = heap[t2];
-            int f = map_get(b, &m, str_ptr(p, t1), str_len(p, t1), &tv);
+            int f = map_get(bc, &m, str_ptr(p, t1), str_len(p, t1), &tv);
             if (f < 0) PANIC("Unknown map type");
             if (!f) {
                 if (code == OP_ALookup) {
@@ -835,7 +869,7 @@ static int32_t* build_colmap(const oracle_prog* p, const mxp_bag_batch* b) {
 int oracle_eval(void* vp, uint32_t fn_sid, const mxp_bag_batch* b, uint32_t req, oracle_result* out) {
     oracle_prog* p = (oracle_prog*)vp;
     int32_t* cm = build_colmap(p, b);
-    bagctx bc = {b, cm, req};
+    bagctx bc = {b, cm, req, p, NULL};
     run(p, fn_sid, &bc, out);
     free(cm);
     return out->status;
@@ -857,7 +891,7 @@ void oracle_eval_matrix(void** progs, const uint32_t* fn_sids, uint32_t nprogs, 
         oracle_result r;
         for (uint32_t k = 0; k < nprogs; k++) {
             const oracle_prog* p = (const oracle_prog*)progs[k];
-            bagctx bc = {b, cms[k], (uint32_t)rq};
+            bagctx bc = {b, cms[k], (uint32_t)rq, p, NULL};
             run(p, fn_sids[k], &bc, &r);
             uint8_t c;
             if (r.status == 1) c = 2;
@@ -881,3 +915,71 @@ int oracle_eval_msg(void* vp, uint32_t fn_sid, const mxp_bag_batch* b, uint32_t 
 }
 
 size_t oracle_result_size(void) { return sizeof(oracle_result); }
+
+/* ------------------------------------------------------------------ referenced attributes */
+static int ref_cmp_str(const uint8_t* a, size_t na, const uint8_t* b, size_t nb) {
+    int c = memcmp(a, b, na < nb ? na : nb);
+    return c ? c : (na < nb ? -1 : na > nb ? 1 : 0);
+}
+typedef struct ref_str {
+    char* s;
+    size_t n;
+} ref_str;
+static int ref_str_cmp(const void* x, const void* y) {
+    const ref_str* a = (const ref_str*)x;
+    const ref_str* b = (const ref_str*)y;
+    return ref_cmp_str((const uint8_t*)a->s, a->n, (const uint8_t*)b->s, b->n);
+}
+
+/*
+ * FakeBag.ReferencedList (il/testing/fakebag.go:75-89) of one request after EvalPredicate of every
+ * program in order: the sorted, distinct "name" / "name[key]" strings, each followed by '\n', into
+ * out.  Returns the length written, or -(length needed) when cap is too small.
+ */
+int64_t oracle_referenced(void** progs, const uint32_t* fn_sids, uint32_t nprogs, const mxp_bag_batch* b,
+                          uint32_t req, char* out, uint64_t cap) {
+    ref_track t = {NULL, 0, 0};
+    for (uint32_t k = 0; k < nprogs; k++) {
+        const oracle_prog* p = (const oracle_prog*)progs[k];
+        int32_t* cm = build_colmap(p, b);
+        bagctx bc = {b, cm, req, p, &t};
+        oracle_result r;
+        run(p, fn_sids[k], &bc, &r);
+        /* names point into the program: copy before the next program runs */
+        free(cm);
+        for (uint32_t i = 0; i < t.n; i++) {
+            if (t.e[i].klen == -2) continue;
+            size_t n = t.e[i].nlen + (t.e[i].klen >= 0 ? (size_t)t.e[i].klen + 2 : 0);
+            char* s = (char*)malloc(n + 1);
+            memcpy(s, t.e[i].name, t.e[i].nlen);
+            if (t.e[i].klen >= 0) {
+                s[t.e[i].nlen] = '[';
+                memcpy(s + t.e[i].nlen + 1, t.e[i].key, (size_t)t.e[i].klen);
+                s[n - 1] = ']';
+            }
+            s[n] = 0;
+            t.e[i].name = (const uint8_t*)s;
+            t.e[i].nlen = (uint32_t)n;
+            t.e[i].klen = -2;  /* materialised */
+        }
+    }
+    ref_str* v = (ref_str*)malloc(sizeof(ref_str) * (t.n ? t.n : 1));
+    for (uint32_t i = 0; i < t.n; i++) {
+        v[i].s = (char*)t.e[i].name;
+        v[i].n = t.e[i].nlen;
+    }
+    qsort(v, t.n, sizeof(ref_str), ref_str_cmp);
+    uint64_t len = 0;
+    for (uint32_t i = 0; i < t.n; i++) {
+        if (i && ref_str_cmp(&v[i], &v[i - 1]) == 0) continue;
+        if (len + v[i].n + 1 <= cap) {
+            memcpy(out + len, v[i].s, v[i].n);
+            out[len + v[i].n] = '\n';
+        }
+        len += v[i].n + 1;
+    }
+    for (uint32_t i = 0; i < t.n; i++) free(v[i].s);
+    free(v);
+    free(t.e);
+    return len <= cap ? (int64_t)len : -(int64_t)len;
+}

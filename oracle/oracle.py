@@ -105,6 +105,9 @@ def lib():
                                          ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int]
         L.oracle_result_size.restype = ctypes.c_size_t
         assert L.oracle_result_size() == ctypes.sizeof(_Result), "oracle_result layout mismatch"
+        L.oracle_referenced.restype = ctypes.c_int64
+        L.oracle_referenced.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                        ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
         L.oracle_set_regex_fn.argtypes = [_REGEX_FN]
         L.oracle_set_regex_fn(_regex_cb)
         _LIB = L
@@ -284,3 +287,27 @@ def oracle_matrix(evaluator: OracleEvaluator, rules, batch: BagBatch, req_begin=
     for k, c in static.items():
         codes[:, k] = c
     return codes
+
+
+def oracle_referenced(evaluator: OracleEvaluator, rules, batch: BagBatch, req: int):
+    """FakeBag.ReferencedList (il/testing/fakebag.go:75-89) of request `req` after EvalPredicate of
+    every rule in order: sorted distinct "name" / "name[key]" strings (bytes).  Rules that fail to
+    compile read nothing (evaluator.go:157-179 returns the compile error before touching the bag)."""
+    progs = []
+    for text in rules:
+        try:
+            progs.append(evaluator.compile(text))
+        except (goexpr.ParseError, goexpr.TypeCheckError, ilcompile.CompileError, goexpr.EvalPanic):
+            pass
+    if not progs:
+        return []
+    handles = (ctypes.c_void_p * len(progs))(*[p.h for p in progs])
+    fids = np.array([p.fn_id() for p in progs], dtype=np.uint32)
+    cap = 4096
+    while True:
+        buf = ctypes.create_string_buffer(cap)
+        n = lib().oracle_referenced(handles, fids.ctypes.data, len(progs), ctypes.byref(batch.c_struct()), req,
+                                    buf, cap)
+        if n >= 0:
+            return [x for x in buf.raw[:n].split(b"\n") if x]
+        cap = -n + 16

@@ -21,8 +21,11 @@ def namespace_of(dest: str) -> str:
     return parts[1] if len(parts) > 1 else ""
 
 
-def resolve(batch, codes, rule_ns, variety_mask, is_tcp, empty_match, identity_attr, default_ns, variety):
-    """-> list of (status, err_rule or None, [selected rule ids]) per request."""
+def resolve(batch, codes, rule_ns, variety_mask, is_tcp, empty_match, identity_attr, default_ns, variety,
+            trace=False):
+    """-> list of (status, err_rule or None, [selected rule ids]) per request; with trace, a fourth
+    item: the attribute names Resolve itself reads (identity, context.protocol) and the rules whose
+    predicate it evaluates, in order (the reads behind ReferencedAttributes)."""
     by_ns = {}
     for r, ns in enumerate(rule_ns):
         by_ns.setdefault(ns, []).append(r)
@@ -30,10 +33,10 @@ def resolve(batch, codes, rule_ns, variety_mask, is_tcp, empty_match, identity_a
     for q in range(batch.n):
         v, found = batch.get(q, identity_attr)
         if not found:
-            out.append((NO_IDENTITY, None, []))
+            out.append((NO_IDENTITY, None, []) + (([identity_attr], []),) * trace)
             continue
         if not isinstance(v, str):
-            out.append((BAD_IDENTITY, None, []))
+            out.append((BAD_IDENTITY, None, []) + (([identity_attr], []),) * trace)
             continue
         ns = namespace_of(v)
         arr = []
@@ -43,7 +46,7 @@ def resolve(batch, codes, rule_ns, variety_mask, is_tcp, empty_match, identity_a
             arr.append(by_ns[ns])
         p, pf = batch.get(q, "context.protocol")
         tcp = pf and isinstance(p, str) and p == "tcp"
-        sel, err = [], None
+        sel, err, evald = [], None, []
         for rules in arr:
             for r in rules:
                 if not (variety_mask[r] >> variety) & 1:
@@ -51,6 +54,7 @@ def resolve(batch, codes, rule_ns, variety_mask, is_tcp, empty_match, identity_a
                 if bool(is_tcp[r]) != tcp:
                     continue
                 if not empty_match[r]:
+                    evald.append(r)
                     c = int(codes[q, r])
                     if c >= 2:
                         err = r
@@ -60,5 +64,15 @@ def resolve(batch, codes, rule_ns, variety_mask, is_tcp, empty_match, identity_a
                 sel.append(r)
             if err is not None:
                 break
-        out.append((PRED_ERROR, err, []) if err is not None else (OK, None, sel))
+        res = (PRED_ERROR, err, []) if err is not None else (OK, None, sel)
+        out.append(res + (([identity_attr, "context.protocol"], evald),) * trace)
     return out
+
+
+def resolve_referenced(evaluator, rules, batch, q, traced):
+    """FakeBag-form referenced list of one Resolve: its own Gets plus the evaluated predicates'."""
+    import oracle
+    names, evald = traced
+    got = {n.encode() for n in names}
+    got.update(oracle.oracle_referenced(evaluator, [rules[r] for r in evald], batch, q))
+    return sorted(got)

@@ -74,3 +74,38 @@ def test_resolver_random_parity(mxp, seed):
             else:
                 assert list(sel[q]) == wsel, (q, variety)
     assert seen == {0, 1, 2, 3}
+
+
+@pytest.mark.parametrize("seed", [23, 24])
+def test_resolver_referenced_parity(mxp, seed):
+    """mxp_resolve_refs: each Resolve's referenced attributes -- identity, context.protocol, and the
+    reads of the predicates filterActions evaluates up to the first failing one -- against the
+    resolver restatement's trace replayed through the oracle's FakeBag tracking; resolution results
+    equal mxp_resolve_batch's."""
+    from test_gpu_refs import expected_protobag
+    manifest, rules, conf, batch = W.resolver_workload(n_rules=400, n_requests=1200, seed=seed)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    st = eng.compile(rules)
+    keep = [i for i, s in enumerate(st) if s != 5]  # unsupported constructs have unknown reads
+    if len(keep) != len(rules):
+        rules = [rules[i] for i in keep]
+        conf = {k: ([v[i] for i in keep] if isinstance(v, list) else v) for k, v in conf.items()}
+        eng.compile(rules)
+    eng.set_resolver(conf["identity_attr"], conf["default_ns"], conf["rule_ns"], conf["variety_mask"],
+                     conf["is_tcp"], conf["empty_match"])
+    ev = oracle.OracleEvaluator(manifest)
+    codes = oracle.oracle_matrix(ev, rules, batch, threads=16)
+    for variety in (0, 3):
+        status, err_rule, sel, refs = eng.resolve_refs(batch, variety)
+        s2, e2, sel2 = eng.resolve(batch, variety)
+        assert np.array_equal(status, s2) and np.array_equal(err_rule[status == 3], e2[status == 3])
+        assert all(np.array_equal(a, b) for a, b in zip(sel, sel2))
+        want = oracle_resolver.resolve(batch, codes, conf["rule_ns"], conf["variety_mask"], conf["is_tcp"],
+                                       conf["empty_match"], conf["identity_attr"], conf["default_ns"], variety,
+                                       trace=True)
+        for q, w in enumerate(want):
+            exp = [x.decode("utf-8", "surrogateescape")
+                   for x in oracle_resolver.resolve_referenced(ev, rules, batch, q, w[3])]
+            assert mxp.fakebag_list(refs[q]) == exp, (q, variety, sorted(set(mxp.fakebag_list(refs[q])) ^ set(exp)))
+            assert mxp.protobag_set(refs[q]) == expected_protobag(batch, q, exp)

@@ -61,6 +61,18 @@ def test_golden_row(row):
         assert same_value(from_tagged(row["R"]), v)
 
 
+@pytest.mark.parametrize("row", [r for r in ROWS["rows"] if r.get("E") and "Referenced" in r],
+                         ids=lambda r: "%d" % r["index"])
+def test_golden_referenced(row):
+    """The oracle's referenced-attribute tracking against the rows' `Referenced` lists
+    (FakeBag.ReferencedList, il/testing/fakebag.go:75; checked by evaluator_test.go:73)."""
+    conf = ROWS["manifests"][row.get("conf", "defaultAttrs")]
+    ev = oracle.OracleEvaluator(conf, fmap_for(row))
+    batch = BagBatch.from_bags([{k: from_tagged(v) for k, v in row.get("I", {}).items()}])
+    got = [x.decode() for x in oracle.oracle_referenced(ev, [row["E"]], batch, 0)]
+    assert got == row["Referenced"]
+
+
 def test_parse_postfix_forms():
     cases = json.load(open(os.path.join(HERE, "golden", "expr_parse.json")))["cases"]
     assert len(cases) == 29
