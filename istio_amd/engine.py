@@ -229,6 +229,20 @@ class Engine:
                     "mxp_eval_batch")
         return match, err
 
+    def eval_refs_raw(self, batch: BagBatch, cap: int = 0):
+        """mxp_eval_refs without decoding: (ref_off u64[n+1], entries u32[m, 4] = attr, key, cond, 0)."""
+        off = np.zeros(batch.n + 1, dtype=np.uint64)
+        cap = cap or 16 * max(batch.n, 1)
+        while True:
+            ents = np.empty((max(cap, 1), 4), dtype=np.uint32)
+            rc = self.lib.mxp_eval_refs(self.h, ctypes.byref(batch.c_struct()), None, None, off.ctypes.data,
+                                        ents.ctypes.data, cap)
+            if rc == 4 and int(off[-1]) > cap:
+                cap = int(off[-1])
+                continue
+            self._check(rc, "mxp_eval_refs")
+            return off, ents[:int(off[-1])]
+
     def eval_refs(self, batch: BagBatch, cap: int = 0):
         """mxp_eval_refs -> (match, err, refs): refs[q] = [(attribute, map key or None, cond)], cond one of
         REF_ABSENCE / REF_EXACT / REF_MAP, sorted by (vocabulary position, key id)."""
