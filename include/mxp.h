@@ -246,6 +246,24 @@ int mxp_regex_match_host(const char* pattern, uint32_t pattern_len, const char* 
  * mxp_batch_eval_device enqueues on `stream` (a hipStream_t; NULL = engine stream) and writes the
  * bitmaps to DEVICE pointers (rule-word-major, as above).  Nothing is synchronised.
  */
+/*
+ * Wire decoding: CompressedAttributes messages (mxp_batch.h mxp_wire_batch) ->
+ * a columnar mxp_bag_batch holding one column per name, each value what ProtoBag.Get(name) returns
+ * (mixer/pkg/attribute/protoBag.go:91-239): the name's index is its message-word slot when the
+ * message lists it (last occurrence), else its global index (getIndex, :242-252); the value is
+ * probed in Strings, StringMaps, Int64S, Doubles, Bools, Timestamps, Durations, Bytes order; a string
+ * or map whose word index is defined in neither dictionary makes the attribute absent (:165-170,
+ * :190-193).  names: the columns to decode; NULL = every attribute the compiled rule set reads plus,
+ * when configured, the resolver's identity attribute and context.protocol.  The result owns its
+ * memory and works with every call that takes an mxp_bag_batch; free with mxp_wire_free.  Host
+ * threads as mxp_batch_pack_host.  No device is needed.
+ */
+typedef struct mxp_wire mxp_wire;
+int mxp_wire_decode(mxp_engine* eng, const mxp_wire_batch* wire, const char* const* names, uint32_t n_names,
+                    mxp_wire** out);
+const mxp_bag_batch* mxp_wire_view(const mxp_wire* w);
+void mxp_wire_free(mxp_wire* w);
+
 typedef struct mxp_dbatch mxp_dbatch;
 int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out);
 /* The host half of mxp_batch_upload alone (interning against the rule set's pools, column gather,

@@ -66,6 +66,39 @@ typedef struct mxp_bag_batch {
     const uint32_t* map_values;        /* [map_offsets[n_maps]] string ids                   */
 } mxp_bag_batch;
 
+/*
+ * The wire form: N `CompressedAttributes` messages (istio.io/api mixer/v1 attributes.proto, the
+ * Attributes of a CheckRequest) with their dictionary indices as sent -- index >= 0 names word i of
+ * the global word list, index < 0 names word -index-1 of the message's own Words
+ * (mixer/pkg/attribute/dictState.go, protoBag.go:254-266).  Every map field of the message is
+ * flattened into CSR arrays: request q's entries of field F are [F_off[q], F_off[q+1]) with keys
+ * F_key (attribute-name indices) and the field's values.  Go map keys are unique per message.
+ * mxp_wire_decode (mxp.h) turns it into an mxp_bag_batch the way ProtoBag.Get reads it.
+ */
+typedef struct mxp_wire_batch {
+    uint32_t n_requests;
+    uint32_t n_global;                 /* global word list (server dictionary)               */
+    const uint8_t* global_bytes;
+    const uint64_t* global_offsets;    /* [n_global + 1]                                     */
+    const uint64_t* words_off;         /* [n + 1] message words of each request:             */
+    const uint8_t* word_bytes;         /*   word w spans word_bytes[word_offsets[w] ..       */
+    const uint64_t* word_offsets;      /*   word_offsets[w + 1])                             */
+    const uint64_t* str_off;   const int32_t* str_key;   const int32_t* str_val;     /* Strings    */
+    const uint64_t* i64_off;   const int32_t* i64_key;   const int64_t* i64_val;     /* Int64S     */
+    const uint64_t* dbl_off;   const int32_t* dbl_key;   const double* dbl_val;      /* Doubles    */
+    const uint64_t* bool_off;  const int32_t* bool_key;  const uint8_t* bool_val;    /* Bools      */
+    const uint64_t* ts_off;    const int32_t* ts_key;    const int64_t* ts_sec;      /* Timestamps */
+    const int32_t* ts_nsec;
+    const uint64_t* dur_off;   const int32_t* dur_key;   const int64_t* dur_val;     /* Durations (ns) */
+    const uint64_t* byt_off;   const int32_t* byt_key;                               /* Bytes: entry e */
+    const uint64_t* byt_val_off;       /*   spans byt_bytes[byt_val_off[e] .. byt_val_off[e + 1]) */
+    const uint8_t* byt_bytes;
+    const uint64_t* sm_off;    const int32_t* sm_key;                                /* StringMaps: entry e */
+    const uint64_t* sm_ent_off;        /*   has pairs [sm_ent_off[e], sm_ent_off[e + 1]) of   */
+    const int32_t* sm_ent_key;         /*   (key, value) word indices                         */
+    const int32_t* sm_ent_val;
+} mxp_wire_batch;
+
 #ifdef __cplusplus
 }
 #endif

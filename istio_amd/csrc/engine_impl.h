@@ -346,6 +346,7 @@ struct mxp_engine : public mxp::LowerTables {
     void build_views();
     int pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H);
     int pack(const mxp_bag_batch* b, mxp_dbatch* db);
+    int wire_decode(const mxp_wire_batch* w, const char* const* names, uint32_t n_names, mxp_wire** out);  // wire.cpp
     void fill_args(mxp_kargs* A, const mxp_dbatch* db) const;
     int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
                unsigned long long* d_hits = nullptr, uint64_t* d_stats = nullptr);

@@ -43,6 +43,9 @@ SIGNATURES = {
     "mxp_eval_batch": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
     "mxp_eval_refs": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64]),
     "mxp_string_text": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
+    "mxp_wire_decode": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint32, ctypes.POINTER(_VP)]),
+    "mxp_wire_view": (_VP, [_VP]),
+    "mxp_wire_free": (None, [_VP]),
     "mxp_resolve_refs": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP, _VP, _VP, ctypes.c_uint64, _VP, _VP,
                                         ctypes.c_uint64]),
     "mxp_eval_values": (ctypes.c_int, [_VP, _VP, _VP, _VP]),

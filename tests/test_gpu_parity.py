@@ -352,3 +352,24 @@ def test_pipelined_chunks_parity(mxp, family, n, min_req, chunks):
         assert np.array_equal(a, b)
     codes = mxp.bits_to_codes(outs[0][0].view(np.uint32), outs[0][1].view(np.uint32), len(rules))
     assert np.array_equal(outs[0][2], (codes == 1).sum(axis=0))
+
+
+@pytest.mark.parametrize("family", ["c1", "c2"])
+def test_wire_path_parity(mxp, family):
+    """Bags sent as CompressedAttributes and decoded by the engine (mxp_wire_decode, names = the rule
+    set's) evaluate bit-identically to the same bags given as a columnar batch."""
+    from istio_amd import wire
+    if family == "c1":
+        manifest, rules, batch = W.c1_workload(n_bags=3000)
+    else:
+        manifest, rules, batch = W.c2_workload(n_rules=500, n_requests=8000, seed=11)
+    bags = [{n: v for n in batch.names for v, f in [batch.get(q, n)] if f and type(v).__name__ != "GoOther"}
+            for q in range(batch.n)]
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    dec = wire.decode(eng, wire.from_bags(bags, sorted(manifest)[::3]))
+    m1, e1 = eng.eval_batch(dec)
+    m2, e2 = eng.eval_batch(BagBatch.from_bags(bags, names=list(manifest)))
+    assert np.array_equal(m1, m2) and np.array_equal(e1, e2)
+    assert m1.any()
