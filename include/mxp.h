@@ -205,6 +205,17 @@ int mxp_list_check(mxp_engine* eng, const mxp_list* list, int blacklist, const u
  * slack after the last symbol), codes written to device memory, enqueued on `stream`. */
 int mxp_list_check_device(mxp_engine* eng, const mxp_list* list, int blacklist, const uint8_t* d_sym_bytes,
                           const uint64_t* d_sym_offsets, uint32_t n, void* stream, int32_t* d_codes);
+/* listentry ProcessCheck fused with HandleListEntry (mixer/template/template.gen.go
+ * :2153-2202 -> mixer/adapter/list/list.go:68-101): per request, Value = Eval of rule `value_rule` of
+ * the engine's compiled rule set (the instance's `value` expression, of type STRING), checked
+ * against `list` in the same device pass -- no host round trip between the two.  codes[q] = the
+ * google.rpc code, or MXP_LISTENTRY_EVAL_ERROR (-1) when Eval failed: the reference returns
+ * "failed to evaluate field 'Value' for instance '<name>': " + mxp_pair_error(q, value_rule).
+ * Every rule of the engine is evaluated (Eval mode), so instance expressions belong in an engine
+ * of their own. */
+#define MXP_LISTENTRY_EVAL_ERROR (-1)
+int mxp_listentry_check(mxp_engine* eng, const mxp_list* list, int blacklist, const mxp_bag_batch* batch,
+                        uint32_t value_rule, int32_t* codes);
 
 /*
  * memquota (mixer/adapter/memquota): batched HandleQuota with the reference's sequential semantics.

@@ -310,6 +310,63 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, con
     return e == hipSuccess ? MXP_OK : eng->hipfail(e, "launch list check");
 }
 
+int mxp_listentry_check(mxp_engine* eng, const mxp_list* L, int blacklist, const mxp_bag_batch* batch,
+                        uint32_t value_rule, int32_t* codes) {
+    if (!eng || !L || !batch || (batch->n_requests && !codes)) return MXP_ERR_ARG;
+    if (!eng->have_rules || value_rule >= eng->rules.size()) return eng->fail(MXP_ERR_ARG, "listentry: no such rule");
+    const auto& R = eng->rules[value_rule];
+    const bool iface = R.il_ret == mxp::IL_INTERFACE;
+    if (R.status == MXP_RULE_OK && R.il_ret != mxp::IL_STRING && !iface)
+        return eng->fail(MXP_ERR_ARG, "listentry: the value expression is not of type STRING");
+    const uint32_t n = batch->n_requests;
+    const uint32_t NR = (uint32_t)eng->rules.size();
+    // Eval of every rule (whole programs, result registers); the batch's string pool is uploaded
+    // even when no rule compares strings, since the symbols are read from it
+    std::unique_ptr<mxp_dbatch> db;
+    DevBuf dm, de, dv;
+    const bool saved = eng->need_strings;
+    eng->need_strings = true;
+    int rc = eng->evaluate(batch, dm, de, &dv, db);
+    eng->need_strings = saved;
+    if (rc) return rc;
+    if (!n) return eng->collect_errors(batch, db);
+    hipError_t e;
+    DevBuf d_codes;
+    if ((e = d_codes.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc codes");
+    mxp_list_args A;
+    memset(&A, 0, sizeof A);
+    A.type = (uint32_t)L->type;
+    A.blacklist = blacklist ? 1u : 0u;
+    A.n = n;
+    A.hmask = L->hmask;
+    A.htab = L->htab.as<uint64_t>();
+    A.ent_desc = L->ent_desc.as<uint64_t>();
+    A.ent_pool = L->ent_pool.as<uint8_t>();
+    A.v4lo = L->v4lo.as<uint32_t>();
+    A.v4hi = L->v4hi.as<uint32_t>();
+    A.v6lo = L->v6lo.as<uint64_t>();
+    A.v6hi = L->v6hi.as<uint64_t>();
+    A.n4 = L->n4;
+    A.n6 = L->n6;
+    A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
+                       L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
+    A.codes = d_codes.as<int32_t>();
+    A.vals = dv.as<uint64_t>() + value_rule;
+    A.vstride = NR;
+    A.viface = iface ? 1u : 0u;
+    A.err_word = de.as<uint32_t>() + (size_t)(value_rule / 32) * n;
+    A.err_bit = 1u << (value_rule % 32);
+    A.n_gstr = eng->gstrs.size();
+    A.gstr_off = eng->d_gstr_off.as<uint64_t>();
+    A.gstr = eng->d_gstr.as<uint8_t>();
+    A.bstr_off = db->bstr_off.as<uint64_t>();
+    A.bstr = db->bstr.as<uint8_t>();
+    if ((e = mxp_launch_list(&A, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch listentry");
+    if ((e = hipMemcpyAsync(codes, d_codes.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download codes");
+    return eng->collect_errors(batch, db);  // synchronises; error texts for mxp_pair_error
+}
+
 int mxp_list_check(mxp_engine* eng, const mxp_list* L, int blacklist, const uint8_t* sym_bytes,
                    const uint64_t* sym_offsets, uint32_t n, int32_t* codes) {
     if (!eng || !L || (n && (!sym_bytes || !sym_offsets || !codes))) return MXP_ERR_ARG;

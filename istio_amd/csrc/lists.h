@@ -27,7 +27,23 @@ typedef struct mxp_list_args {
     uint32_t n4, n6;
     mxp_dfa_set rx;             // REGEX lists: DFA 0 = the union of the list's patterns
     int32_t* codes;             // [n] google.rpc codes
+    // fused listentry (mxp_listentry_check): symbols are the Eval results of one rule instead of
+    // sym / sym_off -- a string id per request (vals[q * vstride], an interface handle when viface),
+    // with the rule's error bit err_word[q] & err_bit; ids < n_gstr in the rule set's pool
+    const uint64_t* vals;
+    const uint32_t* err_word;
+    uint32_t err_bit;
+    uint32_t vstride;
+    uint32_t viface;
+    uint32_t pad;
+    uint64_t n_gstr;
+    const uint64_t* gstr_off;   // offset << 24 | length (8-aligned pools, 16 bytes of slack)
+    const uint8_t* gstr;
+    const uint64_t* bstr_off;
+    const uint8_t* bstr;
 } mxp_list_args;
+
+#define MXP_LISTENTRY_NOT_STRING (-2)
 
 // ASCII upper-casing of 8 packed bytes (bytes >= 0x80 untouched): strings.ToUpper's ASCII path
 MXP_NHD uint64_t mxp_upper8(uint64_t x) {

@@ -15,6 +15,7 @@
 
 #include "../../include/mxp.h"
 #include "lists.h"
+#include "vm.h"
 
 namespace {
 
@@ -96,9 +97,31 @@ __device__ bool ip_member(const mxp_list_args& A, const uint8_t ip[16]) {
 extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args A) {
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
     if (q >= A.n) return;
-    const uint64_t o0 = A.sym_off[q], o1 = A.sym_off[q + 1];
-    const uint8_t* s = A.sym + o0;
-    const uint32_t n = (uint32_t)(o1 - o0);
+    const uint8_t* s;
+    uint32_t n;
+    if (A.vals) {
+        // listentry ProcessCheck (template.gen.go:2170-2183): Value = mapper.Eval(param.Value).(string)
+        if (A.err_word[q] & A.err_bit) {
+            A.codes[q] = MXP_LISTENTRY_EVAL_ERROR;
+            return;
+        }
+        uint64_t id = A.vals[(uint64_t)q * A.vstride];
+        if (A.viface) {
+            if (MXP_FH_KIND(id) != MXP_STRING) {
+                A.codes[q] = MXP_LISTENTRY_NOT_STRING;
+                return;
+            }
+            id = MXP_FH_ID(id);
+        }
+        const bool g = id < A.n_gstr;
+        const uint64_t d = g ? A.gstr_off[id] : A.bstr_off[id - A.n_gstr];
+        s = (g ? A.gstr : A.bstr) + (d >> 24);
+        n = (uint32_t)(d & 0xFFFFFFu);
+    } else {
+        const uint64_t o0 = A.sym_off[q], o1 = A.sym_off[q + 1];
+        s = A.sym + o0;
+        n = (uint32_t)(o1 - o0);
+    }
     bool found;
     if (A.type == MXP_LIST_IP_ADDRESSES) {
         uint8_t ip[16];

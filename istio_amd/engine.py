@@ -46,6 +46,7 @@ SIGNATURES = {
     "mxp_wire_decode": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint32, ctypes.POINTER(_VP)]),
     "mxp_wire_view": (_VP, [_VP]),
     "mxp_wire_free": (None, [_VP]),
+    "mxp_listentry_check": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, ctypes.c_uint32, _VP]),
     "mxp_resolve_refs": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP, _VP, _VP, ctypes.c_uint64, _VP, _VP,
                                         ctypes.c_uint64]),
     "mxp_eval_values": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
@@ -552,6 +553,14 @@ class ListHandle:
         codes = np.zeros(len(bs), dtype=np.int32)
         self.eng._check(self.eng.lib.mxp_list_check(self.eng.h, self.h, int(blacklist), blob.ctypes.data,
                                                     off.ctypes.data, len(bs), codes.ctypes.data), "mxp_list_check")
+        return codes
+
+    def check_entries(self, engine: "Engine", batch, value_rule: int, blacklist: bool = False) -> np.ndarray:
+        """mxp_listentry_check: the listentry instance's Value = Eval(rule value_rule of `engine`) per
+        request, checked against this list in one device pass; -1 where Eval failed."""
+        codes = np.zeros(batch.n, dtype=np.int32)
+        engine._check(engine.lib.mxp_listentry_check(engine.h, self.h, int(blacklist), ctypes.byref(batch.c_struct()),
+                                                      value_rule, codes.ctypes.data), "mxp_listentry_check")
         return codes
 
     def check_device(self, d_sym: int, d_off: int, n: int, stream: int, d_codes: int, blacklist: bool = False):

@@ -78,3 +78,73 @@ def test_regex_list_compile_error(eng):
     with pytest.raises(MxpError) as ei:
         eng.list_create(L.REGEX, ["a+", "(b"], [])
     assert str(ei.value).endswith("error parsing regexp: missing closing ): `(b`")
+
+
+def _listentry_bags(n, seed):
+    """Bags for listentry instances: source.labels with / without `version`, maps missing, paths,
+    forwarded-for addresses (valid, invalid, absent)."""
+    from istio_amd.bags import BagBatch
+    rng = np.random.default_rng(seed)
+    versions = ["v1", "v2", "v3", "V1", "", "canary"]
+    bags = []
+    for i in range(n):
+        b = {}
+        r = rng.random()
+        if r < 0.8:
+            labels = {"app": "ratings"}
+            if rng.random() < 0.85:
+                labels["version"] = versions[int(rng.integers(0, len(versions)))]
+            b["source.labels"] = labels
+        elif r < 0.9:
+            b["source.labels"] = "not-a-map"
+        if rng.random() < 0.9:
+            b["request.path"] = "/api/v%d/%s" % (rng.integers(0, 4), ["reviews", "Ratings", "details"][i % 3])
+        if rng.random() < 0.8:
+            b["request.headers"] = {"x-forwarded-for": ["10.1.2.%d" % rng.integers(0, 256), "fe80::%x" % rng.integers(0, 65536),
+                                                        "bogus"][int(rng.integers(0, 3))]}
+        bags.append(b)
+    manifest = {"source.labels": "STRING_MAP", "request.path": "STRING", "request.headers": "STRING_MAP"}
+    return manifest, BagBatch.from_bags(bags, names=list(manifest))
+
+
+@pytest.mark.parametrize("case", ["listcheck.yaml", "regex-path", "ci-path", "ip-header"])
+def test_listentry_fused(eng, case):
+    """mxp_listentry_check: the listentry instance's `value` expression evaluated and checked against
+    the list in one device pass (template.gen.go:2153-2202 -> list.go:68-101), against the oracle
+    evaluator's Eval feeding the list restatement; eval failures carry the reference's error text."""
+    import oracle
+    import istio_amd.engine as mxp
+    manifest, batch = _listentry_bags(3000, seed=len(case) * 7 + 1)
+    if case == "listcheck.yaml":  # mixer/testdata/config/listcheck.yaml: staticversion / appversion
+        expr, ltype, entries, overrides, black = 'source.labels["version"]', L.STRINGS, [], ["v1", "v2"], False
+        ref = L.StringList([], overrides)
+    elif case == "regex-path":
+        expr, ltype, entries, overrides, black = 'request.path | "none"', L.REGEX, ["^/api/v[12]/", "details$"], [], True
+        ref = L.RegexList(entries)
+    elif case == "ci-path":
+        expr, ltype, entries, overrides, black = 'request.path', L.CASE_INSENSITIVE_STRINGS, ["/API/V1/RATINGS", "/api/v2/reviews"], [], False
+        ref = L.StringList(entries, case_insensitive=True)
+    else:
+        expr, ltype, entries, overrides, black = 'request.headers["x-forwarded-for"]', L.IP_ADDRESSES, ["10.1.2.0/25", "fe80::/112"], [], True
+        ref = L.IPList(entries)
+    inst = mxp.Engine(0)
+    inst.set_vocabulary(manifest)
+    assert (inst.compile(["true", expr]) == 0).all()  # the value expression is rule 1
+    lst = eng.list_create(ltype, entries, overrides)
+    got = lst.check_entries(inst, batch, 1, black)
+    ev = oracle.OracleEvaluator(manifest)
+    vals, syms, errq = [], [], []
+    for q in range(batch.n):
+        st, v = ev.eval(expr, batch, q)
+        if st != "ok":
+            errq.append(q)
+            syms.append("")
+        else:
+            syms.append(v)
+    want = L.codes(ref.found(syms), black)
+    want[errq] = -1
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(q), syms[q], int(got[q]), int(want[q])) for q in bad[:5]]
+    assert (len(errq) > 0) == (case != "regex-path") and (got >= 0).sum() > batch.n // 2  # `|` never fails
+    for q in errq[:50]:
+        assert inst.pair_error(q, 1) == ev.eval(expr, batch, q)[1]
