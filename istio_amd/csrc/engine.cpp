@@ -165,8 +165,12 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         mxp_guard& gd = guards[i];
         const uint32_t mode = gd.mode & 0xFF;
         const bool prefix = (gd.mode & GT_PREFIX) != 0, neg = (gd.mode >> 8) & 1;
+        // GM_ONLY prefix atoms (`attr.startsWith(K)` alone): a posting IS a true pair.  Equality
+        // atoms alone stay with phase 1's group compares -- indexing them too (MXP_DEBUG_FLAGS 512)
+        // measured slower on C4 (header equality: 0.35 ms compared, 0.92 ms indexed)
         bool ok = !(debug_flags & 8u) && !neg &&
-                  ((mode == GM_AND && rule_tmpl[i] != MXP_VM_DONE) || (prefix && mode == GM_ONLY));
+                  ((mode == GM_AND && rule_tmpl[i] != MXP_VM_DONE) || (mode == GM_ONLY && (debug_flags & 512u)) ||
+                   (prefix && mode == GM_ONLY));
         if (!ok) {
             if (prefix) {
                 gd = mxp_guard{0, GM_NONE, 0, 0};
@@ -174,7 +178,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
             }
             continue;
         }
-        if (prefix && mode == GM_ONLY) rule_tmpl[i] = MXP_TMPL_DIRECT;
+        if (mode == GM_ONLY) rule_tmpl[i] = MXP_TMPL_DIRECT;
         indexed[i] = 1;
         n_indexed++;
         if (!(debug_flags & 64u)) {
@@ -190,7 +194,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         const uint64_t k1 = (uint64_t)gd.klo | ((uint64_t)gd.khi << 32);
         mxp::SecondAtom sa;
         std::vector<mxp_vm_ins> code(all.begin() + off[i], all.begin() + off[i + 1]);
-        if (!prefix && !(debug_flags & 16u) && mxp::extract_second_prefix(code, gd.mode >> 16, &sa)) {
+        if (!prefix && mode == GM_AND && !(debug_flags & 16u) && mxp::extract_second_prefix(code, gd.mode >> 16, &sa)) {
             if (sa.direct) {
                 rule_tmpl2[i] = MXP_TMPL_DIRECT;
             } else {
@@ -402,6 +406,39 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     ref_guard.assign(n, MXP_VM_DONE);
     for (uint32_t i = 0; i < n; i++)
         if ((guards[i].mode & 0xFF) != GM_NONE) ref_guard[i] = guards[i].col & 0xFFFFFFu;
+    // dense canonical rules: indexed rules with many duplicates, true pairs injected per bitmap word
+    // at the end of the index kernel instead of one atomic per alias (kernels.hip inject_dense)
+    {
+        std::vector<uint32_t> cand;
+        // (direct postings -- `attr.startsWith(K)` alone -- stay with per-alias atomics: their true
+        // pairs are sparse, and C4 measured them slower injected)
+        for (uint32_t i = 0; i < n; i++)
+            if (aliases_of[i].size() + 1 >= kDenseMin && rule_tmpl[i] != MXP_TMPL_DIRECT) cand.push_back(i);
+        std::stable_sort(cand.begin(), cand.end(),
+                         [&](uint32_t a, uint32_t b) { return aliases_of[a].size() > aliases_of[b].size(); });
+        if (cand.size() > 64) cand.resize(64);
+        if (debug_flags & 256u) cand.clear();  // ablation: fan out with atomics
+        dense_of.assign(n, 0xFF);
+        std::map<uint32_t, std::vector<uint32_t>> by_word;
+        for (uint32_t d = 0; d < cand.size(); d++) {
+            dense_of[cand[d]] = (uint8_t)d;
+            by_word[cand[d] >> 5].push_back((cand[d] & 31u) | (d << 5));
+            for (uint32_t a : aliases_of[cand[d]]) by_word[a >> 5].push_back((a & 31u) | (d << 5));
+        }
+        inj_off.assign(1, 0);
+        inj_word.clear();
+        inj_ent.clear();
+        inj_dmask.clear();
+        for (auto& kv : by_word) {
+            uint64_t dm = 0;
+            for (uint32_t e : kv.second) dm |= 1ull << (e >> 5);
+            inj_dmask.push_back(dm);
+            inj_word.push_back(kv.first);
+            inj_ent.insert(inj_ent.end(), kv.second.begin(), kv.second.end());
+            inj_off.push_back((uint32_t)inj_ent.size());
+        }
+        n_dense = (uint32_t)cand.size();
+    }
     ref_alias_off.assign(n + 1, 0);
     ref_aliases.clear();
     for (uint32_t i = 0; i < n; i++) {
@@ -445,6 +482,11 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_alias_off, alias_off.data(), alias_off.size() * 4, "upload alias_off"))) return rc;
     if ((rc = put(d_aliases, alias_list.data(), alias_list.size() * 4, "upload aliases"))) return rc;
     if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
+    if ((rc = put(d_dense_of, dense_of.data(), dense_of.size(), "upload dense_of"))) return rc;
+    if ((rc = put(d_inj_off, inj_off.data(), inj_off.size() * 4, "upload inj_off"))) return rc;
+    if ((rc = put(d_inj_word, inj_word.data(), inj_word.size() * 4, "upload inj_word"))) return rc;
+    if ((rc = put(d_inj_ent, inj_ent.data(), inj_ent.size() * 4, "upload inj_ent"))) return rc;
+    if ((rc = put(d_inj_dmask, inj_dmask.data(), inj_dmask.size() * 8, "upload inj_dmask"))) return rc;
     if ((rc = put(d_rx_hdr, rx_set.hdr.data(), rx_set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
     if ((rc = put(d_rx_trans, rx_set.trans.data(), rx_set.trans.size() * 4, "upload rx trans"))) return rc;
     if ((rc = put(d_rx_ascii, rx_set.ascii.data(), rx_set.ascii.size() * 2, "upload rx ascii"))) return rc;
@@ -863,6 +905,12 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->rule_tmpl2 = d_rule_tmpl2.as<uint32_t>();
     A->alias_off = n_alias ? d_alias_off.as<uint32_t>() : nullptr;
     A->aliases = d_aliases.as<uint32_t>();
+    A->dense_of = n_dense ? d_dense_of.as<uint8_t>() : nullptr;
+    A->inj_off = d_inj_off.as<uint32_t>();
+    A->inj_word = d_inj_word.as<uint32_t>();
+    A->inj_ent = d_inj_ent.as<uint32_t>();
+    A->inj_dmask = d_inj_dmask.as<uint64_t>();
+    A->n_inj = n_dense ? (uint32_t)inj_word.size() : 0u;
     A->rconst = d_rconst.as<uint64_t>();
     A->flags = debug_flags;
     A->n_rules = (uint32_t)rules.size();
@@ -948,6 +996,12 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
             if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) return hipfail(e, "chunk event");
     }
     if (guards_on && n_fills) A.fills = d_fills.as<mxp_fill>();
+    if (!use_index) A.dense_of = nullptr;
+    if (A.dense_of) {
+        if (d_dense_cm.n < (size_t)A.n * 8 && (e = d_dense_cm.alloc((size_t)A.n * 8)) != hipSuccess)
+            return hipfail(e, "dense masks");
+        A.dense_cm = d_dense_cm.as<uint64_t>();
+    }
     for (uint32_t c = 0; c < nchunk; c++) {
         A.q0 = c * step;
         A.q1 = std::min(A.n, (c + 1) * step);
@@ -963,11 +1017,13 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         if (nchunk == 1) {
             if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
             if ((e = mxp_launch_index(&A, (cx + 3) / 4, s)) != hipSuccess) return hipfail(e, "launch index");
+            if (A.dense_of && (e = mxp_launch_inject(&A, (cx + 3) / 4, s)) != hipSuccess) return hipfail(e, "launch inject");
             continue;
         }
         if ((e = hipEventRecord(chunk_ev[c], s)) != hipSuccess) return hipfail(e, "chunk event");
         if ((e = hipStreamWaitEvent(side, chunk_ev[c], 0)) != hipSuccess) return hipfail(e, "side wait");
         if ((e = mxp_launch_index(&A, (cx + 3) / 4, side)) != hipSuccess) return hipfail(e, "launch index");
+        if (A.dense_of && (e = mxp_launch_inject(&A, (cx + 3) / 4, side)) != hipSuccess) return hipfail(e, "launch inject");
     }
     if (nchunk > 1) {
         // join: ev[1] = the main stream done (fill / guard / VM of every chunk), then the index tail
@@ -1183,10 +1239,11 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) 
 
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
     if (!eng || !out) return 0;
-    const uint32_t v[8] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed,
-                           (uint32_t)(eng->cols.size() + eng->vcols.size()), eng->n_composite, eng->n_alias};
+    const uint32_t v[9] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed,
+                           (uint32_t)(eng->cols.size() + eng->vcols.size()), eng->n_composite, eng->n_alias,
+                           eng->n_dense};
     uint32_t k = 0;
-    for (; k < cap && k < 8; k++) out[k] = v[k];
+    for (; k < cap && k < 9; k++) out[k] = v[k];
     return k;
 }
 

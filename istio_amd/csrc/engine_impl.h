@@ -26,6 +26,7 @@
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
+extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
                                       unsigned long long* hits, hipStream_t s);
@@ -169,11 +170,20 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t n_fills = 0, n_gfill = 0;
     uint32_t n_idx = 0, n_indexed = 0, n_composite = 0, n_alias = 0;
     uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
-    uint32_t groups_per_wave = 4; // MXP_GPW
+    uint32_t groups_per_wave = 16; // MXP_GPW (A/B on C4: 4 6.50 ms, 8 6.55, 16 6.36; C2 flat; profiles/r1_v15_ab_gpw.log)
     // optional per-kernel timing of device evaluations (mxp_set_timing): events around each launch
     bool timing = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     bool ev_index = false;
+    // dense canonical rules (index kernel inject_dense): rule -> id < 64, and per bitmap word the
+    // (bit | id << 5) entries of those rules and their aliases
+    static constexpr size_t kDenseMin = 8;
+    std::vector<uint8_t> dense_of;
+    std::vector<uint32_t> inj_off, inj_word, inj_ent;
+    std::vector<uint64_t> inj_dmask;
+    uint32_t n_dense = 0;
+    DevBuf d_dense_of, d_inj_off, d_inj_word, d_inj_ent, d_inj_dmask;
+    DevBuf d_dense_cm;  // [n] per-request dense masks of the current evaluation
     // referenced attributes (mxp_eval_refs, refs.cpp)
     struct RefComposite {
         uint32_t a_col, b_col, k1, rule;  // `A == K1 && B.startsWith(K2) ...`: B is read iff A == K1
@@ -203,7 +213,10 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t chunk_min = 1u << 17, chunks_max = 1;  // off by default: measured slower
     hipStream_t side = nullptr;
     hipEvent_t chunk_ev[kChunksMax + 1] = {};
-    uint32_t debug_flags = 0;  // MXP_DEBUG_FLAGS: ablation only (1 no in-wave VM, 2 no guards: results invalid; 8 no guard index)
+    // MXP_DEBUG_FLAGS, ablation only: 1 no in-wave VM, 2 no guards (results invalid), 8 no guard index,
+    // 16 no composite index, 64 no duplicate folding, 128 plain fill stores, 256 no dense injection,
+    // 512 index equality-only guards too
+    uint32_t debug_flags = 0;
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
 

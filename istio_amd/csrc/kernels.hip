@@ -25,6 +25,12 @@ namespace {
 
 __device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+    return __builtin_amdgcn_readfirstlane(v);
+}
+
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
@@ -136,11 +142,6 @@ __device__ __forceinline__ void set_error(const mxp_kargs& A, uint32_t rule, uin
 // constant-address-space views: uniform loads through them become scalar s_load_dwordxN
 typedef __attribute__((address_space(4))) const uint32_t cuint32;
 
-// Runs one program from `pc0` for the lanes in `live` (the others keep their phase-1 result) and
-// returns the pair code of every lane that ran.  The program is wave-uniform: instruction pc is
-// P[pc] (pc in [pc0, len)), fetched with one scalar s_load_dwordx4 per step.  `rule` may differ
-// per lane (template batches of the guard-index kernel); it only names the pair in error records and
-// Eval results.  The register file is regs[reg][thread] in LDS.
 // Referenced-attribute tracking (mxp_eval_refs): one record per attribute read the VM performs
 // (VM_RES / VM_TRES / VM_VCOL: slot = column; VM_LOOKUP[K]: the map key), appended with one atomic
 // per wavefront.  Records past refcap are counted, not stored (the host re-runs with more room).
@@ -159,6 +160,11 @@ __device__ __forceinline__ void ref_rec(const mxp_kargs& A, bool on, uint32_t re
     }
 }
 
+// Runs one program from `pc0` for the lanes in `live` (the others keep their phase-1 result) and
+// returns the pair code of every lane that ran.  The program is wave-uniform: instruction pc is
+// P[pc] (pc in [pc0, len)), fetched with one scalar s_load_dwordx4 per step.  `rule` may differ
+// per lane (template batches of the guard-index kernel); it only names the pair in error records and
+// Eval results.  The register file is regs[reg][thread] in LDS.
 template <bool kRefs>
 __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint32_t pc0, bool live, uint32_t rule,
                              uint32_t req, uint64_t (*regs)[256], uint32_t tid, bool fan = false) {
@@ -507,6 +513,13 @@ __device__ __forceinline__ void log_guard_errors(const mxp_kargs& A, uint32_t e,
 // mxp_guard_kernel, which carries no VM and so keeps far fewer registers.  Group descriptors are
 // fetched four at a time with one vector load (lane 16 j + f = word f of the j-th group) and read
 // back with v_readlane.  Results: one coalesced store per word and plane, out[g * N + request].
+// Lean kernel's column cache: a group's segments alternate between columns (C4: the path and five
+// header columns), so instead of reloading a column whenever the segment's column changes, each
+// thread keeps the (kind, value) of columns < MXP_CC it has loaded in LDS slots of its own.
+#define MXP_CC 8u
+__shared__ uint64_t g_ccv[MXP_CC][256];
+__shared__ uint8_t g_cck[MXP_CC][256];
+
 template <bool kVM, bool kRefs = false>
 __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)[256]) {
     const uint32_t tid = threadIdx.x;
@@ -522,6 +535,7 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
     uint32_t cached = MXP_VM_DONE;
     uint32_t ck = MXP_ABSENT;
     uint64_t cv = 0;
+    uint32_t have = 0;  // (lean kernel) columns in this thread's LDS slots -- wave-uniform
     for (uint32_t c0 = i0; c0 < i1; c0 += 4) {
         uint32_t D = 0;
         if (c0 + (lane >> 4) < i1) D = ((const uint32_t*)(A.groups + A.glist[c0 + (lane >> 4)]))[lane & 15u];
@@ -551,9 +565,19 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
                     }
                     if (col != cached) {
                         cached = col;
-                        if (valid) {
-                            ck = A.kinds[(uint64_t)col * N + req];
-                            cv = A.vals[(uint64_t)col * N + req];
+                        if (!kVM && col < MXP_CC && ((have >> col) & 1u)) {
+                            ck = g_cck[col][tid];
+                            cv = g_ccv[col][tid];
+                        } else {
+                            if (valid) {
+                                ck = A.kinds[(uint64_t)col * N + req];
+                                cv = A.vals[(uint64_t)col * N + req];
+                            }
+                            if (!kVM && col < MXP_CC) {
+                                have |= 1u << col;
+                                g_cck[col][tid] = (uint8_t)ck;
+                                g_ccv[col][tid] = cv;
+                            }
                         }
                     }
                     ok |= ((okset >> ck) & 1u) ? rules : 0u;
@@ -655,6 +679,20 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
                 if (bad[r] && q0 + r < Q1) log_guard_errors(A, mask, (g0 + g) * 32u, q0 + r);
         }
     }
+    // non-temporal streaming stores (A/B on C2: 0.828 vs 0.867 ms per evaluation,
+    // profiles/r1_v15_ab_nt.log); MXP_DEBUG_FLAGS 128 = plain stores (ablation)
+    if (vec && !(A.flags & 128u)) {
+        for (uint32_t g = 0; g < n; g++) {
+            const uint32_t mask = g + 1 == n ? last : all;
+            const uint64_t at = (uint64_t)(g0 + g) * N + q0;
+            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+            if (A.out_match) __builtin_nontemporal_store(v4u{0u, 0u, 0u, 0u}, (v4u*)(A.out_match + at));
+            if (A.out_err)
+                __builtin_nontemporal_store(v4u{bad[0] & mask, bad[1] & mask, bad[2] & mask, bad[3] & mask},
+                                            (v4u*)(A.out_err + at));
+        }
+        return;
+    }
     for (uint32_t g = 0; g < n; g++) {
         const uint32_t mask = g + 1 == n ? last : all;
         const uint64_t at = (uint64_t)(g0 + g) * N + q0;
@@ -686,16 +724,32 @@ namespace {
 // kargs.rule_tmpl2, the composite resume point), request.
 #define MXP_IXQ 256u
 __shared__ uint32_t g_ixq[4][MXP_IXQ][2];  // per wave of the index kernel's workgroup
-struct PairQueue {
-    uint32_t wave;
-    uint32_t n;        // pending entries (wave-uniform)
-    uint32_t ntrue;    // true pairs this lane has set (kargs.stats)
-};
-
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__shared__ uint64_t g_cm[4][64];  // dense-alias masks of the wave's 64 requests (kargs.dense_of)
+struct PairQueue {
+    uint32_t wave;
+    uint32_t n;        // pending entries (wave-uniform)
+    uint32_t ntrue;    // true pairs this lane has set (kargs.stats)
+    uint32_t base;     // first request of the wave's tile
+};
+
+// A true pair of an indexed rule: rules with many duplicates ("dense" canonical rules, kargs.dense_of)
+// only set their bit in the request's mask (LDS) -- the wave writes the bits of the rule and all its
+// aliases once per bitmap word at the end (inject_dense); the rest OR their bits in at once.
+__device__ __forceinline__ uint32_t pair_true(const mxp_kargs& A, PairQueue& Q, uint32_t rule, uint32_t req) {
+    if (A.dense_of) {
+        const uint32_t d = A.dense_of[rule];
+        if (d != 0xFFu) {
+            atomicOr((unsigned long long*)&g_cm[Q.wave][req - Q.base], 1ull << d);
+            return 0u;  // counted by mxp_inject_kernel
+        }
+    }
+    return set_true(A, rule, req);
 }
 
 // run entries [off, off + cnt) of the queue, cnt <= 64
@@ -705,7 +759,7 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
     const uint32_t lane = tid & 63u;
     wave_sync_lds();
     bool pending = lane < cnt;
-    uint32_t rule = 0, req = 0, t = MXP_VM_DONE;
+    uint32_t rule = 0, req = 0, t = MXP_VM_DONE, res = MXP_VM_DONE;
     if (pending) {
         const uint32_t e = g_ixq[Q.wave][off + lane][0];
         req = g_ixq[Q.wave][off + lane][1];
@@ -724,12 +778,12 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
             for (uint32_t c = 0; c < nconst; c++) regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
         cuint32* P = ((cuint32*)A.prog) + ((uint64_t)toff - pc0) * 4u;
         const uint32_t code = run_rule<kRefs>(A, P, len_t, pc0, mine, rule, req, regs, tid, true);
-        if (mine) {
-            if (code == PC_TRUE) Q.ntrue += set_true(A, rule, req);
-            if (code >= PC_ERROR) set_error(A, rule, req);
-        }
+        if (mine) res = code;
         pending = pending && !mine;
     }
+    // results out after the VM loop (its registers are dead here)
+    if (res == PC_TRUE) Q.ntrue += pair_true(A, Q, rule, req);
+    if (res >= PC_ERROR && res != MXP_VM_DONE) set_error(A, rule, req);
 }
 
 // Appends every lane's postings [start, start + len) to the queue (direct postings are true pairs:
@@ -747,21 +801,30 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
         if (Q.n < 64u && __ballot(j0 < len)) {
             const uint32_t c = (MXP_IXQ - Q.n) / 64u;  // >= 3
             const uint32_t take = min(len - j0, c);
-            const uint32_t incl = wave_incl_sum(take, lane);
-            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-            const uint32_t base = Q.n + incl - take;
-            for (uint32_t j = 0; j < take; j++) {
-                const uint32_t rule = A.postings[start + j0 + j];
-                uint32_t e = rule | (tbl << 31);
-                if (tmpl_of[rule] == MXP_TMPL_DIRECT) {
-                    Q.ntrue += set_true(A, rule, req);
-                    e = 0xFFFFFFFFu;
+            // posting-major order: entry j of every lane, then entry j + 1, ...  Lanes whose requests
+            // share a posting list (a common key) put the SAME rule side by side, so a 64-pair batch
+            // runs one rule's constants and its true bits -- and its aliases' -- land in one bitmap
+            // row: coalesced atomics instead of one row per lane
+            const uint32_t tmax = wave_max(take);
+            const uint64_t below = (1ull << lane) - 1ull;
+            uint32_t pos = Q.n;
+            for (uint32_t j = 0; j < tmax; j++) {
+                const uint64_t act = __ballot(j < take);
+                if (j < take) {
+                    const uint32_t at = pos + (uint32_t)__builtin_popcountll(act & below);
+                    const uint32_t rule = A.postings[start + j0 + j];
+                    uint32_t e = rule | (tbl << 31);
+                    if (tmpl_of[rule] == MXP_TMPL_DIRECT) {
+                        Q.ntrue += pair_true(A, Q, rule, req);
+                        e = 0xFFFFFFFFu;
+                    }
+                    g_ixq[Q.wave][at][0] = e;
+                    g_ixq[Q.wave][at][1] = req;
                 }
-                g_ixq[Q.wave][base + j][0] = e;
-                g_ixq[Q.wave][base + j][1] = req;
+                pos += (uint32_t)__builtin_popcountll(act);
             }
             j0 += take;
-            Q.n += total;
+            Q.n = pos;
         }
         const bool more = __ballot(j0 < len) != 0;
         if (Q.n >= 64u || (Q.n > 0u && (final || more))) {
@@ -823,9 +886,13 @@ template <bool kRefs>
 __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
-    PairQueue Q{wave, 0u, 0u};
-    const uint32_t req = A.q0 + (blockIdx.x * 4u + wave) * 64u + (tid & 63u);
+    PairQueue Q{wave, 0u, 0u, A.q0 + (blockIdx.x * 4u + wave) * 64u};
+    const uint32_t req = Q.base + (tid & 63u);
     const bool valid = req < A.q1;
+    if (A.dense_of) {
+        g_cm[wave][tid & 63u] = 0ull;
+        wave_sync_lds();
+    }
     const uint64_t N = A.n;
     // x == n_idx: a last pass with no probes that drains the pair queue
     for (uint32_t x = 0; x <= A.n_idx; x++) {
@@ -905,6 +972,10 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 process_slot<kRefs>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
         }
     }
+    if (A.dense_of) {  // masks for mxp_inject_kernel
+        wave_sync_lds();
+        if (valid) A.dense_cm[req] = g_cm[wave][tid & 63u];
+    }
     if (A.stats) {
         uint32_t t = Q.ntrue;
 #pragma unroll
@@ -924,6 +995,47 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 extern "C" __global__ __launch_bounds__(256) void mxp_index_refs_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<true>(A, regs);
+}
+
+// After mxp_index_kernel, when the rule set has dense canonical rules (kargs.dense_of): every bitmap
+// word holding a dense rule or alias gets the bits of its requests' masks with one coalesced atomic
+// per word and wavefront (lane = request), plus the fused hit counters of those rules.  Words whose
+// dense rules are false for the whole wave are skipped.  Workgroup = 4 waves x 64 requests.
+extern "C" __global__ __launch_bounds__(256) void mxp_inject_kernel(mxp_kargs A) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t req = A.q0 + (blockIdx.x * 4u + uni(threadIdx.x >> 6)) * 64u + lane;
+    const bool valid = req < A.q1;
+    const uint64_t cm = valid ? A.dense_cm[req] : 0ull;
+    uint32_t mlo = (uint32_t)cm, mhi = (uint32_t)(cm >> 32);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        mlo |= (uint32_t)__shfl_xor((int)mlo, off, 64);
+        mhi |= (uint32_t)__shfl_xor((int)mhi, off, 64);
+    }
+    const uint64_t M = ((uint64_t)uni(mhi) << 32) | uni(mlo);
+    if (M == 0) return;
+    uint32_t t = 0;  // pairs set (kargs.stats)
+    for (uint32_t k = 0; k < A.n_inj; k++) {
+        if (!(A.inj_dmask[k] & M)) continue;
+        const uint32_t e0 = uni(A.inj_off[k]), e1 = uni(A.inj_off[k + 1]), w = uni(A.inj_word[k]);
+        uint32_t bits = 0;
+        for (uint32_t e = e0; e < e1; e++) {
+            const uint32_t ent = uni(A.inj_ent[e]);  // bit | dense id << 5
+            const uint32_t on = (uint32_t)(cm >> (ent >> 5)) & 1u;
+            bits |= on << (ent & 31u);
+            if (A.hits) {
+                const uint32_t c = (uint32_t)__builtin_popcountll(__ballot(on != 0));
+                if (lane == 0 && c) atomicAdd(A.hits + w * 32u + (ent & 31u), (unsigned long long)c);
+            }
+        }
+        if (bits) atomicOr(A.out_match + (uint64_t)w * A.n + req, bits);
+        t += (uint32_t)__builtin_popcount(bits);
+    }
+    if (A.stats) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) t += (uint32_t)__shfl_xor((int)t, off, 64);
+        if (lane == 0 && t) atomicAdd((unsigned long long*)A.stats, (unsigned long long)t);
+    }
 }
 
 // Per-rule hit counters: hits[rule] += number of requests whose match bit for the rule is set.
@@ -1045,6 +1157,11 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
 
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s) {
     hipLaunchKernelGGL(mxp_fill_kernel, dim3((args->q1 - args->q0 + 1023) / 1024, n_fills), dim3(256), 0, s, *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_inject_kernel, dim3(grid), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

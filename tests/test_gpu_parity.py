@@ -373,3 +373,37 @@ def test_wire_path_parity(mxp, family):
     m2, e2 = eng.eval_batch(BagBatch.from_bags(bags, names=list(manifest)))
     assert np.array_equal(m1, m2) and np.array_equal(e1, e2)
     assert m1.any()
+
+
+@pytest.mark.parametrize("knobs", [{}, {"MXP_DEBUG_FLAGS": "256"}])
+def test_dense_alias_injection_parity(mxp, knobs, monkeypatch):
+    """Indexed rules with many duplicates ("dense" canonical rules): their true pairs are injected
+    once per bitmap word at the end of the index kernel (MXP_DEBUG_FLAGS=256: per-alias atomics
+    instead).  Results, error bits and fused hit counters against the oracle."""
+    import torch
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    manifest, rules0, batch = W.c4_workload(n_rules=400, n_requests=6000, seed=12)
+    rng = np.random.default_rng(5)
+    hot = ['"^v(1|%d)[0-9]?$".matches(request.headers["x-user"])' % d for d in range(2, 9)] + \
+          ['request.path.startsWith("/w1")', 'request.headers["x-env"] == "v3" && request.path.startsWith("/w2")',
+           '"^/w3[0-9a-z/]*".matches(request.path)']
+    rules = list(rules0) + [hot[int(i)] for i in rng.integers(0, len(hot), size=900)]
+    rng.shuffle(rules)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    info = eng.ruleset_info()
+    assert info["dense"] == (0 if knobs else len(hot) - 1)  # startsWith alone (direct postings) is not dense
+    got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch, sample_msgs=100)
+    assert (want == 1).sum() > 10 * batch.n
+    db = eng.upload(batch)
+    Wd = (len(rules) + 31) // 32
+    dm = torch.zeros((Wd, batch.n), dtype=torch.int32, device="cuda:0")
+    de = torch.zeros_like(dm)
+    hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(2):  # the first evaluation counts in the kernels, the second (dense) by streaming
+        db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert np.array_equal(hits.cpu().numpy(), 2 * (want == 1).sum(axis=0))
