@@ -425,18 +425,22 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
             by_word[cand[d] >> 5].push_back((cand[d] & 31u) | (d << 5));
             for (uint32_t a : aliases_of[cand[d]]) by_word[a >> 5].push_back((a & 31u) | (d << 5));
         }
-        inj_off.assign(1, 0);
-        inj_word.clear();
-        inj_ent.clear();
-        inj_dmask.clear();
-        for (auto& kv : by_word) {
-            uint64_t dm = 0;
-            for (uint32_t e : kv.second) dm |= 1ull << (e >> 5);
-            inj_dmask.push_back(dm);
-            inj_word.push_back(kv.first);
-            inj_ent.insert(inj_ent.end(), kv.second.begin(), kv.second.end());
-            inj_off.push_back((uint32_t)inj_ent.size());
-        }
+        inj.clear();
+        for (auto& kv : by_word)
+            for (size_t e0 = 0; e0 < kv.second.size(); e0 += MXP_INJ_SLOT - 4) {
+                const size_t e1 = std::min(kv.second.size(), e0 + MXP_INJ_SLOT - 4);
+                uint32_t slot[MXP_INJ_SLOT] = {};
+                uint64_t dm = 0;
+                for (size_t e = e0; e < e1; e++) {
+                    dm |= 1ull << (kv.second[e] >> 5);
+                    slot[4 + e - e0] = kv.second[e];
+                }
+                slot[0] = (uint32_t)dm;
+                slot[1] = (uint32_t)(dm >> 32);
+                slot[2] = kv.first;
+                slot[3] = (uint32_t)(e1 - e0);
+                inj.insert(inj.end(), slot, slot + MXP_INJ_SLOT);
+            }
         n_dense = (uint32_t)cand.size();
     }
     ref_alias_off.assign(n + 1, 0);
@@ -483,10 +487,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     if ((rc = put(d_aliases, alias_list.data(), alias_list.size() * 4, "upload aliases"))) return rc;
     if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
     if ((rc = put(d_dense_of, dense_of.data(), dense_of.size(), "upload dense_of"))) return rc;
-    if ((rc = put(d_inj_off, inj_off.data(), inj_off.size() * 4, "upload inj_off"))) return rc;
-    if ((rc = put(d_inj_word, inj_word.data(), inj_word.size() * 4, "upload inj_word"))) return rc;
-    if ((rc = put(d_inj_ent, inj_ent.data(), inj_ent.size() * 4, "upload inj_ent"))) return rc;
-    if ((rc = put(d_inj_dmask, inj_dmask.data(), inj_dmask.size() * 8, "upload inj_dmask"))) return rc;
+    if ((rc = put(d_inj, inj.data(), inj.size() * 4, "upload inj"))) return rc;
     if ((rc = put(d_rx_hdr, rx_set.hdr.data(), rx_set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
     if ((rc = put(d_rx_trans, rx_set.trans.data(), rx_set.trans.size() * 4, "upload rx trans"))) return rc;
     if ((rc = put(d_rx_ascii, rx_set.ascii.data(), rx_set.ascii.size() * 2, "upload rx ascii"))) return rc;
@@ -906,11 +907,8 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->alias_off = n_alias ? d_alias_off.as<uint32_t>() : nullptr;
     A->aliases = d_aliases.as<uint32_t>();
     A->dense_of = n_dense ? d_dense_of.as<uint8_t>() : nullptr;
-    A->inj_off = d_inj_off.as<uint32_t>();
-    A->inj_word = d_inj_word.as<uint32_t>();
-    A->inj_ent = d_inj_ent.as<uint32_t>();
-    A->inj_dmask = d_inj_dmask.as<uint64_t>();
-    A->n_inj = n_dense ? (uint32_t)inj_word.size() : 0u;
+    A->inj = d_inj.as<uint32_t>();
+    A->n_inj = n_dense ? (uint32_t)(inj.size() / MXP_INJ_SLOT) : 0u;
     A->rconst = d_rconst.as<uint64_t>();
     A->flags = debug_flags;
     A->n_rules = (uint32_t)rules.size();

@@ -175,14 +175,13 @@ struct mxp_engine : public mxp::LowerTables {
     bool timing = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     bool ev_index = false;
-    // dense canonical rules (index kernel inject_dense): rule -> id < 64, and per bitmap word the
-    // (bit | id << 5) entries of those rules and their aliases
+    // dense canonical rules (mxp_inject_kernel): rule -> id < 64, and per bitmap word the
+    // (bit | id << 5) entries of those rules and their aliases, in slots of MXP_INJ_SLOT dwords
     static constexpr size_t kDenseMin = 8;
     std::vector<uint8_t> dense_of;
-    std::vector<uint32_t> inj_off, inj_word, inj_ent;
-    std::vector<uint64_t> inj_dmask;
+    std::vector<uint32_t> inj;  // [slots][MXP_INJ_SLOT]
     uint32_t n_dense = 0;
-    DevBuf d_dense_of, d_inj_off, d_inj_word, d_inj_ent, d_inj_dmask;
+    DevBuf d_dense_of, d_inj;
     DevBuf d_dense_cm;  // [n] per-request dense masks of the current evaluation
     // referenced attributes (mxp_eval_refs, refs.cpp)
     struct RefComposite {

@@ -29,10 +29,7 @@ typedef struct mxp_kargs {
     const uint32_t* alias_off;   // [n_rules + 1] CSR of duplicate indexed rules (nullptr: none)
     const uint32_t* aliases;
     const uint8_t* dense_of;     // [n_rules] dense canonical id (< 64) of indexed rules with many aliases, 0xFF none (nullptr: none)
-    const uint32_t* inj_off;     // [n_inj + 1] per bitmap word holding dense rules: entries (bit | dense id << 5)
-    const uint32_t* inj_word;    // [n_inj] the word
-    const uint32_t* inj_ent;
-    const uint64_t* inj_dmask;   // [n_inj] dense ids present in the word
+    const uint32_t* inj;         // [n_inj][MXP_INJ_SLOT] injection slots of the words holding dense rules
     uint64_t* dense_cm;          // [n] per request: the dense rules found true (index kernel -> inject kernel)
     uint32_t n_inj;
     uint32_t pad5;

@@ -901,12 +901,14 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
         const uint32_t col = uni(X->col), okset = uni(X->okset), hmask = uni(X->hmask), hoff = uni(X->hoff),
                        kind = uni(X->prefix), plen0 = uni(X->plen0), nplen = uni(X->nplen);
         const bool comp = kind == MXP_IX_COMPOSITE;
+        // kinds and values of both columns are loaded together (independent loads, one round trip)
         bool ok = false;
         uint64_t v = 0;
         if (valid) {
             const uint32_t k = A.kinds[(uint64_t)col * N + req];
+            const uint64_t vv = A.vals[(uint64_t)col * N + req];
             ok = ((okset >> k) & 1u) != 0;
-            if (ok) v = A.vals[(uint64_t)col * N + req];
+            v = ok ? vv : 0ull;
         }
         // the string whose leading bytes are probed: the column itself (prefix index) or, for a
         // composite (A == K1 && B.startsWith(K2) && ...), B -- when B is not a string the lane takes
@@ -918,10 +920,11 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
             const uint32_t col2 = uni(X->col2), okset2 = uni(X->okset2);
             pmask = uni(X->hmask2);
             poff = uni(X->hoff2);
-            if (ok) {
+            if (valid) {
                 const uint32_t k = A.kinds[(uint64_t)col2 * N + req];
-                sok = ((okset2 >> k) & 1u) != 0;
-                if (sok) sv = A.vals[(uint64_t)col2 * N + req];
+                const uint64_t vv = A.vals[(uint64_t)col2 * N + req];
+                sok = ok && ((okset2 >> k) & 1u) != 0;
+                if (sok) sv = vv;
             }
         }
         StrRef s{nullptr, 0};
@@ -950,12 +953,11 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                     for (uint32_t slot = (uint32_t)hf & pmask;; slot = (slot + 1) & pmask) {
                         const uint32_t at = poff + stride * slot;
                         const mxp_hent E = A.hents[at];
+                        // composite: the K1 half of the entry pair is loaded with the first half
+                        const mxp_hent K = comp ? A.hents[at + 1u] : E;
                         if (E.len == 0) break;
                         if (E.khi != tag) continue;
-                        if (comp) {
-                            const mxp_hent K = A.hents[at + 1u];
-                            if (K.klo != vlo || K.khi != vhi) continue;
-                        }
+                        if (comp && (K.klo != vlo || K.khi != vhi)) continue;
                         const StrRef k = str_of(A, E.klo);
                         if (k.n == L && bytes_eq_a(s.p, k.p, L)) {
                             fi = at;
@@ -967,6 +969,10 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                     start = A.hents[fi].start;
                     len = A.hents[fi].len;
                 }
+            }
+            if (A.flags & 1024u) {  // ablation: probes only (results invalid)
+                if (len) Q.ntrue += start & 1u;
+                continue;
             }
             if (final || __ballot(len != 0))
                 process_slot<kRefs>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
@@ -1015,12 +1021,18 @@ extern "C" __global__ __launch_bounds__(256) void mxp_inject_kernel(mxp_kargs A)
     const uint64_t M = ((uint64_t)uni(mhi) << 32) | uni(mlo);
     if (M == 0) return;
     uint32_t t = 0;  // pairs set (kargs.stats)
+    // slots of 16 dwords (vm.h MXP_INJ_*): dense-id mask, word, count, up to 12 entries -- one
+    // scalar s_load_dwordx16 each
     for (uint32_t k = 0; k < A.n_inj; k++) {
-        if (!(A.inj_dmask[k] & M)) continue;
-        const uint32_t e0 = uni(A.inj_off[k]), e1 = uni(A.inj_off[k + 1]), w = uni(A.inj_word[k]);
+        const cuint32* S = (const cuint32*)A.inj + (uint64_t)k * MXP_INJ_SLOT;
+        const uint64_t dm = (uint64_t)S[0] | ((uint64_t)S[1] << 32);
+        if (!(dm & M)) continue;
+        const uint32_t w = S[2], n = S[3];
         uint32_t bits = 0;
-        for (uint32_t e = e0; e < e1; e++) {
-            const uint32_t ent = uni(A.inj_ent[e]);  // bit | dense id << 5
+#pragma unroll
+        for (uint32_t j = 0; j < MXP_INJ_SLOT - 4; j++) {
+            if (j >= n) break;
+            const uint32_t ent = S[4 + j];  // bit | dense id << 5
             const uint32_t on = (uint32_t)(cm >> (ent >> 5)) & 1u;
             bits |= on << (ent & 31u);
             if (A.hits) {

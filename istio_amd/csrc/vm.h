@@ -150,6 +150,10 @@ typedef struct mxp_fill {
     uint32_t pad[2];
 } mxp_fill;
 
+// dense-rule injection slots (mxp_inject_kernel): 16 dwords = dense-id mask (2), bitmap word,
+// entry count, up to 12 entries (bit | dense id << 5); a word with more entries takes several slots
+#define MXP_INJ_SLOT 16u
+
 // kargs.rule_tmpl value of indexed rules whose atom IS the result (`col.startsWith(K)` alone): a
 // posting is a true pair, no continuation to run
 #define MXP_TMPL_DIRECT 0xFFFFFFFEu

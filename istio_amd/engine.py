@@ -20,7 +20,7 @@ import numpy as np
 from .bags import BagBatch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmxp.so")
+LIB_PATH = os.environ.get("MXP_LIB") or os.path.join(_HERE, "libmxp.so")  # MXP_LIB: A/B of builds
 
 VALUE_TYPES = {"VALUE_TYPE_UNSPECIFIED": 0, "STRING": 1, "INT64": 2, "DOUBLE": 3, "BOOL": 4, "TIMESTAMP": 5,
                "IP_ADDRESS": 6, "EMAIL_ADDRESS": 7, "URI": 8, "DNS_NAME": 9, "DURATION": 10, "STRING_MAP": 11}
