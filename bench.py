@@ -73,6 +73,17 @@ def measured_traffic(workload, rules, requests):
     return d.get("bytes_per_eval")
 
 
+def lds_conflicts(workload):
+    """LDS bank-conflict rate per evaluation kernel from the committed SQ counter session
+    (tools/sq_session.sh + tools/sq_summarize.py -> profiles/sq_counters_<workload>.json), or None."""
+    path = os.path.join(ROOT, "profiles", "sq_counters_%s.json" % workload)
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    return {k: {"bank_conflict_cycles": v.get("SQ_LDS_BANK_CONFLICT"), "lds_active_cycles": v.get("SQ_LDS_IDX_ACTIVE"),
+                "rate": v.get("bank_conflict_rate")} for k, v in d.get("kernels", {}).items()}
+
+
 def list_bench(args, rank, world, local):
     """C3 (BASELINE configs[2]): 100k-entry CIDR / string / regex lists, 1M lookups per GPU resident
     in HBM; one step = HandleListEntry for every lookup (mxp_list_check_device, one kernel)."""
@@ -356,6 +367,7 @@ def main():
         "eval_ms": kernel_ms,
         "kernels_ms": {"mxp_guard_kernel+mxp_eval_kernel": k_eval, "mxp_index_kernel": k_index},
         "pack_upload_s": t_pack,
+        "lds_bank_conflicts": lds_conflicts(args.workload),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "mxp_guard_kernel + mxp_eval_kernel + mxp_index_kernel (one evaluation)",

@@ -1376,22 +1376,23 @@ static int eval_common(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* ma
     const uint32_t R = (uint32_t)eng->rules.size();
     const uint32_t W = (R + 31) / 32;
     hipError_t e;
+    // bitmaps go straight into the caller's arrays; host copies only when per-pair codes are wanted
     std::vector<uint32_t> hm, he;
-    if (match_bits || codes) {
+    if (codes) {
         hm.resize((size_t)W * n);
-        if ((e = hipMemcpyAsync(hm.data(), dm.p, hm.size() * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-            return eng->hipfail(e, "download match");
-    }
-    if (err_bits || codes) {
         he.resize((size_t)W * n);
-        if ((e = hipMemcpyAsync(he.data(), de.p, he.size() * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-            return eng->hipfail(e, "download err");
     }
+    uint32_t* to_m = codes ? hm.data() : match_bits;
+    uint32_t* to_e = codes ? he.data() : err_bits;
+    if (to_m && (e = hipMemcpyAsync(to_m, dm.p, (size_t)W * n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download match");
+    if (to_e && (e = hipMemcpyAsync(to_e, de.p, (size_t)W * n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download err");
     if (values && (e = hipMemcpyAsync(values, dv.p, (size_t)n * R * 8, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
         return eng->hipfail(e, "download values");
     if ((rc = eng->collect_errors(batch, db))) return rc;
-    if (match_bits) memcpy(match_bits, hm.data(), hm.size() * 4);
-    if (err_bits) memcpy(err_bits, he.data(), he.size() * 4);
+    if (codes && match_bits) memcpy(match_bits, hm.data(), hm.size() * 4);
+    if (codes && err_bits) memcpy(err_bits, he.data(), he.size() * 4);
     if (codes) {
         for (uint32_t q = 0; q < n; q++)
             for (uint32_t r = 0; r < R; r++) {
