@@ -407,3 +407,34 @@ def test_dense_alias_injection_parity(mxp, knobs, monkeypatch):
         db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s)
     torch.cuda.synchronize()
     assert np.array_equal(hits.cpu().numpy(), 2 * (want == 1).sum(axis=0))
+
+
+def test_empty_batches_and_rule_sets(mxp):
+    """Edge sizes: an empty batch, an empty rule set, one request with every attribute absent --
+    through the host, device, refs, resolver-free and wire entry points."""
+    import torch
+    from istio_amd import wire
+    manifest, rules, batch = W.c2_workload(n_rules=64, n_requests=10, seed=3)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    empty = BagBatch.from_bags([], names=list(manifest))
+    m, e = eng.eval_batch(empty)
+    assert m.size == 0 and e.size == 0
+    _, _, refs = eng.eval_refs(empty)
+    assert refs == []
+    db = eng.upload(empty)
+    assert db.n == 0
+    bare = BagBatch.from_bags([{}], names=list(manifest))
+    m, e = eng.eval_batch(bare)
+    codes = mxp.bits_to_codes(m, e, len(rules))
+    ev = oracle.OracleEvaluator(manifest)
+    want = oracle.oracle_matrix(ev, rules, bare, threads=1)
+    assert np.array_equal(codes, np.where(want >= 2, 2, want))
+    dec = wire.decode(eng, wire.WireBatch([], ["destination.service"]))
+    assert dec.n == 0 and eng.eval_batch(dec)[0].size == 0
+    none = mxp.Engine(0)
+    none.set_vocabulary(manifest)
+    none.compile([])
+    m, e = none.eval_batch(batch)
+    assert m.size == 0 and e.size == 0
