@@ -106,15 +106,15 @@ __device__ __forceinline__ void log_err(const mxp_kargs& A, uint32_t req, uint32
 }
 
 // a true pair found after phase 1 (guard-index kernel): OR its match bit in and, when the caller
-// asked for fused hit counters, count it once (the bit was not set before)
+// asked for fused hit counters, count it.  Each (rule, request) pair is produced once per
+// evaluation (a rule sits in one index under one key; the composite and its equality fallback serve
+// disjoint lanes; aliases are distinct rules), so neither atomic needs its return value: no
+// round trip per true pair.
 __device__ __forceinline__ void set_true1(const mxp_kargs& A, uint32_t rule, uint32_t req) {
     const uint32_t bit = 1u << (rule & 31u);
-    uint32_t* w = A.out_match + (uint64_t)(rule >> 5) * A.n + req;
-    if (A.hits) {
-        if (!(atomicOr(w, bit) & bit)) atomicAdd(A.hits + rule, 1ull);
-    } else {
-        atomicOr(w, bit);
-    }
+    __hip_atomic_fetch_or(A.out_match + (uint64_t)(rule >> 5) * A.n + req, bit, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+    if (A.hits) __hip_atomic_fetch_add(A.hits + rule, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ... and the same for the rule's aliases (indexed duplicates of its program, kargs.alias_off)
