@@ -549,6 +549,10 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
             if (guards_on) {
                 // ---- phase 1
                 uint32_t eq = 0, ok = 0;
+                // segments 1..16 of the group: one vector load (lane 4 k + f = field f of segment k + 1),
+                // read back with v_readlane -- instead of a chain of scalar loads, one per segment
+                uint32_t SD = 0;
+                if (nseg > 1 && lane < 4u * min(nseg - 1u, 16u)) SD = ((const uint32_t*)(A.segs + seg0))[lane];
                 for (uint32_t s = 0; s < nseg; s++) {
                     uint32_t col, okset, rules, cmp;
                     if (s == 0) {
@@ -556,6 +560,11 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
                         okset = GF(9);
                         rules = GF(10);
                         cmp = GF(11);
+                    } else if (s <= 16u) {
+                        col = __builtin_amdgcn_readlane(SD, 4u * (s - 1u));
+                        okset = __builtin_amdgcn_readlane(SD, 4u * (s - 1u) + 1u);
+                        rules = __builtin_amdgcn_readlane(SD, 4u * (s - 1u) + 2u);
+                        cmp = __builtin_amdgcn_readlane(SD, 4u * (s - 1u) + 3u);
                     } else {
                         const mxp_seg* S = A.segs + seg0 + s - 1;
                         col = uni(S->col);
@@ -636,7 +645,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
     eval_groups<true>(A, regs);
 }
 
-extern "C" __global__ __launch_bounds__(256) void mxp_guard_kernel(mxp_kargs A) { eval_groups<false>(A, nullptr); }
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void mxp_guard_kernel(mxp_kargs A) { eval_groups<false>(A, nullptr); }
 
 // mxp_eval_kernel with referenced-attribute records (mxp_eval_refs)
 extern "C" __global__ __launch_bounds__(256) void mxp_eval_refs_kernel(mxp_kargs A) {
