@@ -381,10 +381,10 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
                              G.s_cmp == 0 && G.s_rules == G.all && !(debug_flags & 32u);
         if (uniform) {
             mxp_fill* F = fills.empty() ? nullptr : &fills.back();
-            if (F && F->col == G.s_col && F->okset == G.s_okset && F->g0 + F->n == g && F->n < MXP_FILL_CHUNK &&
+            if (F && F->col == G.s_col && F->okset == G.s_okset && F->g0 + F->n == g && F->n < fill_chunk &&
                 F->last == F->all && G.all == F->all) {
                 F->n++;
-            } else if (F && F->col == G.s_col && F->okset == G.s_okset && F->g0 + F->n == g && F->n < MXP_FILL_CHUNK &&
+            } else if (F && F->col == G.s_col && F->okset == G.s_okset && F->g0 + F->n == g && F->n < fill_chunk &&
                        F->last == F->all) {
                 F->n++;
                 F->last = G.all;
@@ -911,6 +911,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->n_inj = n_dense ? (uint32_t)(inj.size() / MXP_INJ_SLOT) : 0u;
     A->rconst = d_rconst.as<uint64_t>();
     A->flags = debug_flags;
+    A->fill_span = fill_span;
     A->n_rules = (uint32_t)rules.size();
     A->n_words = (A->n_rules + 31) / 32;
     A->groups_per_wave = groups_per_wave;
@@ -1119,6 +1120,8 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_DEBUG_FLAGS")) e->debug_flags = (uint32_t)atoi(f);
     // tuning knobs (results are identical for every setting)
     if (const char* f = getenv("MXP_GPW")) e->groups_per_wave = std::max(1, atoi(f));
+    if (const char* f = getenv("MXP_FILL_CHUNK")) e->fill_chunk = (uint32_t)std::max(1, atoi(f));
+    if (const char* f = getenv("MXP_FILL_SPAN")) e->fill_span = (uint32_t)std::min(8, std::max(1, atoi(f)));
     if (const char* f = getenv("MXP_ERRCAP")) e->errcap = (uint32_t)std::max(1, atoi(f));
     if (device < 0) {  // host-only engine (compiler / lowering inspection without a GPU)
         e->reset_tables();

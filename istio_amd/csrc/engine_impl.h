@@ -215,6 +215,10 @@ struct mxp_engine : public mxp::LowerTables {
     // MXP_DEBUG_FLAGS, ablation only: 1 no in-wave VM, 2 no guards (results invalid), 8 no guard index,
     // 16 no composite index, 64 no duplicate folding, 128 plain fill stores, 256 no dense injection,
     // 512 index equality-only guards too
+    // fill layout (same-box A/B on C2, profiles/r1_v17_ab_fill*.log: span 1 / chunk 32 0.945 ms,
+    // span 4 0.832-0.836, span 4 / chunk 16 0.831; spans 3, 5, 6, 8 and chunks 4..1000 no better)
+    uint32_t fill_chunk = MXP_FILL_CHUNK;  // MXP_FILL_CHUNK: groups per fill chunk
+    uint32_t fill_span = 4;                // MXP_FILL_SPAN: 256-request spans per fill wave (1..8)
     uint32_t debug_flags = 0;
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all

@@ -45,7 +45,7 @@ typedef struct mxp_kargs {
     uint32_t groups_per_wave;
     uint32_t n;                  // requests in the batch (row stride of columns and bitmaps)
     uint32_t q0, q1;             // requests [q0, q1) this launch evaluates (pipelined chunks)
-    uint32_t pad4;
+    uint32_t fill_span;          // mxp_fill_kernel: 256-request spans per wave (MXP_FILL_SPAN)
     // columns: [n_cols][n] kinds / values (resolve columns, then virtual map[key] columns)
     const uint8_t* kinds;
     const uint64_t* vals;

@@ -655,64 +655,81 @@ extern "C" __global__ __launch_bounds__(256) void mxp_eval_refs_kernel(mxp_kargs
 
 // Chunks of uniform indexed groups (vm.h mxp_fill): every word is a function of the guard column's
 // kind alone -- match 0, error = the rules whose type check fails -- so a lane computes it once for
-// each of its four requests and streams 16-byte stores over the chunk's groups (1 KB per
-// wave-instruction).  Workgroup = 4 waves x 256 requests; grid y = chunk.
+// each of its requests and streams 16-byte stores over the chunk's groups (1 KB per
+// wave-instruction).  A wave covers `fill_span` spans of 256 requests (span s of group g lands at
+// row g, requests q0 + 256 s ..), so one group row gets 1 KB x span contiguous bytes from the wave
+// before the next row.  Workgroup = 4 waves; grid y = chunk.
+#define MXP_FILL_SPAN_MAX 8
 extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = uni(threadIdx.x >> 6);
     const mxp_fill* F = A.fills + blockIdx.y;
     const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), all = uni(F->all),
                    last = uni(F->last);
+    const uint32_t span = uni(A.fill_span);
     const uint64_t N = A.n;
     const uint32_t Q1 = A.q1;        // chunk end (chunks start at multiples of 1024)
-    const uint32_t q0 = A.q0 + (blockIdx.x * 4u + wave) * 256u + lane * 4u;
-    if (q0 >= Q1) return;
+    const uint32_t qw = A.q0 + (blockIdx.x * 4u + wave) * 256u * span;  // the wave's first request
+    if (qw >= Q1) return;
+    const uint32_t q0 = qw + lane * 4u;
     const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0;  // rows 16-byte aligned, the lane's 4 requests all present
-    uint32_t bad[4];                 // per request: ~0 when the guard column fails its type check
-    if (vec) {
-        const uint32_t k4 = *(const uint32_t*)(A.kinds + (uint64_t)col * N + q0);
+    uint32_t bad[MXP_FILL_SPAN_MAX][4];  // per request: ~0 when the guard column fails its type check
+    uint32_t any = 0;
 #pragma unroll
-        for (int r = 0; r < 4; r++) bad[r] = ((okset >> ((k4 >> (8 * r)) & 0xFFu)) & 1u) ? 0u : ~0u;
-    } else {
+    for (uint32_t sp = 0; sp < MXP_FILL_SPAN_MAX; sp++) {
+        const uint32_t q = q0 + sp * 256u;
+        if (sp < span && vec && q < Q1) {
+            const uint32_t k4 = *(const uint32_t*)(A.kinds + (uint64_t)col * N + q);
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const bool in = q0 + r < Q1;
-            const uint32_t k = in ? A.kinds[(uint64_t)col * N + q0 + r] : 0u;
-            bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
+            for (int r = 0; r < 4; r++) bad[sp][r] = ((okset >> ((k4 >> (8 * r)) & 0xFFu)) & 1u) ? 0u : ~0u;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                const bool in = sp < span && q + r < Q1;
+                const uint32_t k = in ? A.kinds[(uint64_t)col * N + q + r] : 0u;
+                bad[sp][r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
+            }
         }
+        any |= bad[sp][0] | bad[sp][1] | bad[sp][2] | bad[sp][3];
     }
-    if (A.errlog && (bad[0] | bad[1] | bad[2] | bad[3])) {
+    if (A.errlog && any) {
         for (uint32_t g = 0; g < n; g++) {
             const uint32_t mask = g + 1 == n ? last : all;
-            for (uint32_t r = 0; r < 4; r++)
-                if (bad[r] && q0 + r < Q1) log_guard_errors(A, mask, (g0 + g) * 32u, q0 + r);
+            for (uint32_t sp = 0; sp < span; sp++)
+                for (uint32_t r = 0; r < 4; r++)
+                    if (bad[sp][r] && q0 + sp * 256u + r < Q1) log_guard_errors(A, mask, (g0 + g) * 32u, q0 + sp * 256u + r);
         }
     }
     // non-temporal streaming stores (A/B on C2: 0.828 vs 0.867 ms per evaluation,
     // profiles/r1_v15_ab_nt.log); MXP_DEBUG_FLAGS 128 = plain stores (ablation)
-    if (vec && !(A.flags & 128u)) {
-        for (uint32_t g = 0; g < n; g++) {
-            const uint32_t mask = g + 1 == n ? last : all;
-            const uint64_t at = (uint64_t)(g0 + g) * N + q0;
-            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-            if (A.out_match) __builtin_nontemporal_store(v4u{0u, 0u, 0u, 0u}, (v4u*)(A.out_match + at));
-            if (A.out_err)
-                __builtin_nontemporal_store(v4u{bad[0] & mask, bad[1] & mask, bad[2] & mask, bad[3] & mask},
-                                            (v4u*)(A.out_err + at));
-        }
-        return;
-    }
+    const bool nt = !(A.flags & 128u);
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     for (uint32_t g = 0; g < n; g++) {
         const uint32_t mask = g + 1 == n ? last : all;
-        const uint64_t at = (uint64_t)(g0 + g) * N + q0;
-        if (vec) {
-            if (A.out_match) *(uint4*)(A.out_match + at) = make_uint4(0, 0, 0, 0);
-            if (A.out_err) *(uint4*)(A.out_err + at) = make_uint4(bad[0] & mask, bad[1] & mask, bad[2] & mask, bad[3] & mask);
-        } else {
-            for (uint32_t r = 0; r < 4; r++) {
-                if (q0 + r >= Q1) break;
-                if (A.out_match) A.out_match[at + r] = 0u;
-                if (A.out_err) A.out_err[at + r] = bad[r] & mask;
+        const uint64_t row = (uint64_t)(g0 + g) * N;
+#pragma unroll
+        for (uint32_t sp = 0; sp < MXP_FILL_SPAN_MAX; sp++) {
+            const uint32_t q = q0 + sp * 256u;
+            if (sp >= span || qw + sp * 256u >= Q1) break;  // wave-uniform
+            const uint64_t at = row + q;
+            if (vec) {
+                const v4u m = v4u{0u, 0u, 0u, 0u};
+                const v4u er = v4u{bad[sp][0] & mask, bad[sp][1] & mask, bad[sp][2] & mask, bad[sp][3] & mask};
+                if (q < Q1) {
+                    if (nt) {
+                        if (A.out_match) __builtin_nontemporal_store(m, (v4u*)(A.out_match + at));
+                        if (A.out_err) __builtin_nontemporal_store(er, (v4u*)(A.out_err + at));
+                    } else {
+                        if (A.out_match) *(v4u*)(A.out_match + at) = m;
+                        if (A.out_err) *(v4u*)(A.out_err + at) = er;
+                    }
+                }
+            } else {
+                for (uint32_t r = 0; r < 4; r++) {
+                    if (q + r >= Q1) break;
+                    if (A.out_match) A.out_match[at + r] = 0u;
+                    if (A.out_err) A.out_err[at + r] = bad[sp][r] & mask;
+                }
             }
         }
     }
@@ -1177,7 +1194,8 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
 }
 
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_fill_kernel, dim3((args->q1 - args->q0 + 1023) / 1024, n_fills), dim3(256), 0, s, *args);
+    const uint32_t per_block = 1024u * (args->fill_span ? args->fill_span : 1u);
+    hipLaunchKernelGGL(mxp_fill_kernel, dim3((args->q1 - args->q0 + per_block - 1) / per_block, n_fills), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

@@ -139,7 +139,7 @@ typedef struct mxp_hent {
 // the guard's type check fails), so mxp_fill_kernel computes them once per request and streams the
 // stores.  Groups g0 .. g0 + n - 1 (n <= MXP_FILL_CHUNK), `all` = rules present in every group but
 // the last, `last` = those of the last.
-#define MXP_FILL_CHUNK 32u
+#define MXP_FILL_CHUNK 16u
 typedef struct mxp_fill {
     uint32_t col;
     uint32_t okset;    // bits 0..15: kinds that pass; bits 24..31: want class / GK_VCOL

@@ -253,6 +253,39 @@ def test_c2_ragged_batches(mxp, n):
     compare(eng, ev, rules, batch, sample_msgs=100)
 
 
+@pytest.mark.parametrize("knobs", [{"MXP_FILL_SPAN": "1", "MXP_FILL_CHUNK": "32"}, {"MXP_FILL_SPAN": "2"},
+                                   {"MXP_FILL_SPAN": "8", "MXP_FILL_CHUNK": "5"},
+                                   {"MXP_FILL_SPAN": "3", "MXP_FILL_CHUNK": "1000"}])
+@pytest.mark.parametrize("n", [5, 4099, 20000])
+def test_fill_layout_knobs_parity(mxp, knobs, n, monkeypatch):
+    """mxp_fill_kernel's store layout knobs (MXP_FILL_SPAN: 256-request spans per wave, including
+    spans past the batch end; MXP_FILL_CHUNK: groups per chunk) leave every word unchanged: oracle
+    parity on ragged batches, and the pipelined device path equal to the unpipelined one."""
+    import torch
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    manifest, rules, batch = W.c2_workload(n_rules=333, n_requests=n, seed=7)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    compare(eng, oracle.OracleEvaluator(manifest), rules, batch, sample_msgs=100)
+    if n < 4096:
+        return
+    db = eng.upload(batch)
+    Wd = (len(rules) + 31) // 32
+    outs = []
+    s = torch.cuda.current_stream().cuda_stream
+    for pipe in ((2048, 4), (1 << 30, 1)):
+        eng.set_pipeline(*pipe)
+        dm = torch.full((Wd, batch.n), -1, dtype=torch.int32, device="cuda:0")
+        de = torch.full_like(dm, -1)
+        db.eval(dm.data_ptr(), de.data_ptr(), s)
+        torch.cuda.synchronize()
+        outs.append((dm.cpu().numpy(), de.cpu().numpy()))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("family", ["c2", "fuzz", "c4"])
 def test_fused_hit_counters(mxp, family):
     """mxp_batch_eval_device_hits: counters accumulated by the evaluation kernels (fill / guard / VM
