@@ -1018,7 +1018,15 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index_kernel(mxp_kargs A) {
+// 6 waves/SIMD (80 VGPRs, two of them spilled: 12 bytes of scratch per lane).  Same-box A/B against
+// the 5-wave build without spills (MXP_DEBUG_FLAGS 8192): C4 5.31 -> 5.10 ms, C2 0.720 vs 0.718 ms
+// (profiles/r1_v17_ab_ix6_*.log)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void mxp_index_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    index_body<false>(A, regs);
+}
+// MXP_DEBUG_FLAGS 8192: the same body at 5 waves/SIMD (no scratch) -- A/B ablation
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index5_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<false>(A, regs);
 }
@@ -1208,7 +1216,10 @@ extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hip
     if (args->refs)
         hipLaunchKernelGGL(mxp_index_refs_kernel, dim3(grid), dim3(256), 0, s, *args);
     else
-        hipLaunchKernelGGL(mxp_index_kernel, dim3(grid), dim3(256), 0, s, *args);
+        if (args->flags & 8192u)
+            hipLaunchKernelGGL(mxp_index5_kernel, dim3(grid), dim3(256), 0, s, *args);
+        else
+            hipLaunchKernelGGL(mxp_index_kernel, dim3(grid), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 
