@@ -471,3 +471,32 @@ def test_empty_batches_and_rule_sets(mxp):
     none.compile([])
     m, e = none.eval_batch(batch)
     assert m.size == 0 and e.size == 0
+
+
+UTF8_PATTERNS = ["^/api/v[0-9]+/é", "日本", "^.{3}$", "[à-ÿ]+x", "^[^a-z]*$", "😀$", "^(a|é|日)+$", ".", "^$",
+                 "é.*日.*😀", "[\\x{4e00}-\\x{9fff}]{2}", "^/[a-z]+/[^/]+$", "a.b", "^[a-zé/0-9]{8,}$", "ÿ{2}|zz"]
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_regex_utf8_subjects_parity(mxp, seed):
+    """`matches` over subjects that mix ASCII with 2-, 3- and 4-byte UTF-8 runes, of lengths that
+    cross the DFA walker's 8-byte windows at every offset: constant patterns (rule-set DFAs) and a
+    pattern read from an attribute (per-batch DFAs), against the oracle's Go regexp restatement."""
+    rng = np.random.default_rng(seed)
+    alphabet = ["a", "b", "z", "x", "/", "0", "9", "A", "-", "é", "ÿ", "à", "日", "本", "😀"]
+    weights = np.array([6, 3, 2, 2, 4, 2, 2, 1, 1, 2, 2, 1, 2, 1, 1], dtype=float)
+    subjects = []
+    for _ in range(3000):
+        L = int(rng.integers(0, 41))
+        subjects.append("".join(rng.choice(alphabet, size=L, p=weights / weights.sum())))
+    subjects[:4] = ["", "/api/v12/é", "日本語", "aéa"]
+    manifest = {"request.path": "STRING", "x": "STRING"}
+    bags = [{"request.path": s, "x": UTF8_PATTERNS[i % len(UTF8_PATTERNS)]} for i, s in enumerate(subjects)]
+    batch = BagBatch.from_bags(bags, names=list(manifest))
+    rules = ['"%s".matches(request.path)' % p.replace("\\", "\\\\") for p in UTF8_PATTERNS] + \
+            ["x.matches(request.path)", '"^/api".matches(request.path) && "é$".matches(request.path)']
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all(), [eng.rule_error(i) for i in range(len(rules))]
+    got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch, sample_msgs=50)
+    assert (want == 1).sum() > 2000 and (want == 0).sum() > 2000
