@@ -259,9 +259,9 @@ def main():
 
     from istio_amd import dist as D
     rank, world, local = D.world()
-    if world > 1:
-        dist.init_process_group("nccl")
     torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from istio_amd import build
     build.build()

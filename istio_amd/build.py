@@ -34,6 +34,17 @@ def _stale():
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
+    # one builder at a time (the ranks of a multi-GPU bench all call build()): the others wait on
+    # the lock and then find the library up to date
+    import fcntl
+    with open(LIB + ".lock", "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        if not force and not _stale():
+            return LIB
+        return _build(verbose)
+
+
+def _build(verbose: bool) -> str:
     objdir = os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
     objs = []
