@@ -365,13 +365,13 @@ def main():
         "config": {"workload": workload % (R, N),
                    "rules": R, "requests_per_gpu": N, "parallelism": "request-sharded dp%d" % world},
         "eval_ms": kernel_ms,
-        "kernels_ms": {"mxp_fill_kernel+mxp_guard_kernel+mxp_eval_kernel": k_eval,
+        "kernels_ms": {"mxp_fill_kernel+mxp_guard2_kernel+mxp_eval_kernel": k_eval,
                        "mxp_index_kernel+mxp_inject_kernel": k_index},
         "pack_upload_s": t_pack,
         "lds_bank_conflicts": lds_conflicts(args.workload),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "one evaluation: mxp_fill_kernel / mxp_guard_kernel / mxp_eval_kernel (the groups "
+                     "kernel": "one evaluation: mxp_fill_kernel / mxp_guard2_kernel / mxp_eval_kernel (the groups "
                                "each serves) + mxp_index_kernel (+ mxp_inject_kernel with dense rules)",
                      "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pair": alg_bytes / (N * R)},
     }

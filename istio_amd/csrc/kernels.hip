@@ -647,6 +647,117 @@ extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
 
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void mxp_guard_kernel(mxp_kargs A) { eval_groups<false>(A, nullptr); }
 
+// The lean groups with two requests per lane (a wave covers 128 requests): the kernel is bound by
+// scalar issue, and the per-group scalar work -- descriptor decode, segment loop, branches -- is now
+// spent once per 128 requests instead of once per 64.  Column cache: [MXP_CC][512] per workgroup
+// (4 waves/SIMD).  Same-box A/B on C4: 5.068 -> 4.850 ms per evaluation
+// (profiles/r1_v18_ab_guard2.log); MXP_DEBUG_FLAGS 65536 = mxp_guard_kernel, one request per lane.
+extern "C" __global__ __launch_bounds__(256) void mxp_guard2_kernel(mxp_kargs A) {
+    __shared__ uint64_t ccv[MXP_CC][512];
+    __shared__ uint8_t cck[MXP_CC][512];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = uni(tid >> 6);
+    const uint32_t reqa = A.q0 + blockIdx.x * 128u + lane, reqb = reqa + 64u;
+    const bool va = reqa < A.q1, vb = reqb < A.q1;
+    const uint64_t N = A.n;
+    const uint32_t i0 = (blockIdx.y * 4u + wave) * A.groups_per_wave;
+    const uint32_t i1 = min(i0 + A.groups_per_wave, A.n_glist);
+    uint32_t cached = MXP_VM_DONE;
+    uint32_t cka = MXP_ABSENT, ckb = MXP_ABSENT;
+    uint64_t cva = 0, cvb = 0;
+    uint32_t have = 0;
+    for (uint32_t c0 = i0; c0 < i1; c0 += 4) {
+        uint32_t D = 0;
+        if (c0 + (lane >> 4) < i1) D = ((const uint32_t*)(A.groups + A.glist[c0 + (lane >> 4)]))[lane & 15u];
+        const uint32_t cn = min(4u, i1 - c0);
+        for (uint32_t j = 0; j < cn; j++) {
+#define GF(f) __builtin_amdgcn_readlane(D, j * 16u + (f))
+            const uint32_t guarded = GF(1), only = GF(2), orm = GF(3), neg = GF(4), seg0 = GF(6), nseg = GF(7),
+                           g = GF(12);
+            const uint32_t r0 = g * 32u;
+            uint32_t eqa = 0, oka = 0, eqb = 0, okb = 0;
+            uint32_t SD = 0;
+            if (nseg > 1 && lane < 4u * min(nseg - 1u, 16u)) SD = ((const uint32_t*)(A.segs + seg0))[lane];
+            for (uint32_t sg = 0; sg < nseg; sg++) {
+                uint32_t col, okset, rules, cmp;
+                if (sg == 0) {
+                    col = GF(8);
+                    okset = GF(9);
+                    rules = GF(10);
+                    cmp = GF(11);
+                } else if (sg <= 16u) {
+                    col = __builtin_amdgcn_readlane(SD, 4u * (sg - 1u));
+                    okset = __builtin_amdgcn_readlane(SD, 4u * (sg - 1u) + 1u);
+                    rules = __builtin_amdgcn_readlane(SD, 4u * (sg - 1u) + 2u);
+                    cmp = __builtin_amdgcn_readlane(SD, 4u * (sg - 1u) + 3u);
+                } else {
+                    const mxp_seg* S = A.segs + seg0 + sg - 1;
+                    col = uni(S->col);
+                    okset = uni(S->okset);
+                    rules = uni(S->rules);
+                    cmp = uni(S->cmp);
+                }
+                if (col != cached) {
+                    cached = col;
+                    if (col < MXP_CC && ((have >> col) & 1u)) {
+                        cka = cck[col][2u * (tid & ~63u) + lane];
+                        cva = ccv[col][2u * (tid & ~63u) + lane];
+                        ckb = cck[col][2u * (tid & ~63u) + 64u + lane];
+                        cvb = ccv[col][2u * (tid & ~63u) + 64u + lane];
+                    } else {
+                        cka = ckb = MXP_ABSENT;
+                        cva = cvb = 0;
+                        if (va) {
+                            cka = A.kinds[(uint64_t)col * N + reqa];
+                            cva = A.vals[(uint64_t)col * N + reqa];
+                        }
+                        if (vb) {
+                            ckb = A.kinds[(uint64_t)col * N + reqb];
+                            cvb = A.vals[(uint64_t)col * N + reqb];
+                        }
+                        if (col < MXP_CC) {
+                            have |= 1u << col;
+                            cck[col][2u * (tid & ~63u) + lane] = (uint8_t)cka;
+                            ccv[col][2u * (tid & ~63u) + lane] = cva;
+                            cck[col][2u * (tid & ~63u) + 64u + lane] = (uint8_t)ckb;
+                            ccv[col][2u * (tid & ~63u) + 64u + lane] = cvb;
+                        }
+                    }
+                }
+                oka |= ((okset >> cka) & 1u) ? rules : 0u;
+                okb |= ((okset >> ckb) & 1u) ? rules : 0u;
+                if (cmp) {
+                    eqa |= seg_eq((cuint64*)A.gk + r0, cmp, cva);
+                    eqb |= seg_eq((cuint64*)A.gk + r0, cmp, cvb);
+                }
+            }
+#undef GF
+            const uint32_t ma = (eqa ^ neg) & (only | orm) & oka, mb = (eqb ^ neg) & (only | orm) & okb;
+            const uint32_t ea = guarded & ~oka, eb = guarded & ~okb;
+            if (va) {
+                if (A.errlog && ea) log_guard_errors(A, ea, r0, reqa);
+                if (A.out_match) A.out_match[(uint64_t)g * N + reqa] = ma;
+                if (A.out_err) A.out_err[(uint64_t)g * N + reqa] = ea;
+            }
+            if (vb) {
+                if (A.errlog && eb) log_guard_errors(A, eb, r0, reqb);
+                if (A.out_match) A.out_match[(uint64_t)g * N + reqb] = mb;
+                if (A.out_err) A.out_err[(uint64_t)g * N + reqb] = eb;
+            }
+            if (A.hits) {
+                const uint32_t m2a = va ? ma : 0u, m2b = vb ? mb : 0u;
+                for (uint32_t bits = wave_or(m2a | m2b); bits; bits &= bits - 1) {
+                    const uint32_t k = __builtin_ctz(bits);
+                    const uint32_t c = (uint32_t)__builtin_popcountll(__ballot((m2a >> k) & 1u)) +
+                                       (uint32_t)__builtin_popcountll(__ballot((m2b >> k) & 1u));
+                    if (lane == 0) atomicAdd(A.hits + r0 + k, (unsigned long long)c);
+                }
+            }
+        }
+    }
+}
+
 // mxp_eval_kernel with referenced-attribute records (mxp_eval_refs)
 extern "C" __global__ __launch_bounds__(256) void mxp_eval_refs_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
@@ -1196,8 +1307,10 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
         hipLaunchKernelGGL(mxp_eval_refs_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
     else if (vm)
         hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
-    else
+    else if (args->flags & 65536u)
         hipLaunchKernelGGL(mxp_guard_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    else
+        hipLaunchKernelGGL(mxp_guard2_kernel, dim3((grid_x + 1) / 2, grid_y), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

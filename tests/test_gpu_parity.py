@@ -138,12 +138,12 @@ def test_fuzz_parity(mxp, seed):
     compare(eng, ev, rules, batch)
 
 
-@pytest.mark.parametrize("knobs", [{}, {"MXP_DEBUG_FLAGS": "8"}, {"MXP_GPW": "1"}])
+@pytest.mark.parametrize("knobs", [{}, {"MXP_DEBUG_FLAGS": "8"}, {"MXP_GPW": "1"}, {"MXP_DEBUG_FLAGS": "65536"}])
 def test_guarded_fuzz_parity(mxp, knobs, monkeypatch):
     """Guard-led rules (mixed columns / want classes / negations / modes per group, shared and
     singleton continuation templates, indexed and in-wave continuations) under each routing:
     default (guard index on), guard index off (MXP_DEBUG_FLAGS=8: every continuation in-wave), one
-    group per wave."""
+    group per wave, the one-request-per-lane lean kernel (MXP_DEBUG_FLAGS=65536)."""
     for k, v in knobs.items():
         monkeypatch.setenv(k, v)
     rules = W.guarded_fuzz_rules(2000, seed=11)

@@ -16,7 +16,7 @@ import os
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-EVAL_KERNELS = ("mxp_fill_kernel", "mxp_guard_kernel", "mxp_eval_kernel", "mxp_index_kernel", "mxp_inject_kernel")
+EVAL_KERNELS = ("mxp_fill_kernel", "mxp_guard_kernel", "mxp_guard2_kernel", "mxp_eval_kernel", "mxp_index_kernel", "mxp_inject_kernel")
 
 
 def per_kernel(path_glob, counter):

@@ -10,7 +10,7 @@ import json
 import os
 from collections import defaultdict
 
-EVAL = ("mxp_fill_kernel", "mxp_guard_kernel", "mxp_eval_kernel", "mxp_index_kernel", "mxp_inject_kernel")
+EVAL = ("mxp_fill_kernel", "mxp_guard_kernel", "mxp_guard2_kernel", "mxp_eval_kernel", "mxp_index_kernel", "mxp_inject_kernel")
 
 
 def main():
