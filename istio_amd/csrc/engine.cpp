@@ -398,6 +398,14 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     }
     n_fills = (uint32_t)fills.size();
     n_glean = (uint32_t)glean.size();
+    // columns < MXP_CC the lean groups read: mxp_guard2_kernel loads them into LDS up front
+    lean_cc = 0;
+    for (uint32_t g : glean) {
+        const mxp_group& G = groups[g];
+        if (G.nseg && G.s_col < MXP_CC) lean_cc |= 1u << G.s_col;
+        for (uint32_t k = 0; k + 1 < G.nseg; k++)
+            if (segs[G.seg0 + k].col < MXP_CC) lean_cc |= 1u << segs[G.seg0 + k].col;
+    }
     n_gvm = (uint32_t)gvm.size();
     n_segs = (uint32_t)segs.size();
 
@@ -912,6 +920,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->rconst = d_rconst.as<uint64_t>();
     A->flags = debug_flags;
     A->fill_span = fill_span;
+    A->lean_cols = lean_cc;
     A->n_rules = (uint32_t)rules.size();
     A->n_words = (A->n_rules + 31) / 32;
     A->groups_per_wave = groups_per_wave;

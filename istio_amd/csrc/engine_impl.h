@@ -166,6 +166,7 @@ struct mxp_engine : public mxp::LowerTables {
     DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_alias_off, d_aliases, d_rconst, d_idx, d_hents, d_postings, d_plens;
     DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
     uint32_t n_glean = 0, n_gvm = 0;
+    uint32_t lean_cc = 0;  // columns < MXP_CC read by the lean groups (kargs.lean_cols)
     DevBuf d_fills;                 // chunks of uniform indexed groups (mxp_fill_kernel)
     uint32_t n_fills = 0, n_gfill = 0;
     uint32_t n_idx = 0, n_indexed = 0, n_composite = 0, n_alias = 0;

@@ -39,7 +39,7 @@ typedef struct mxp_kargs {
     const uint32_t* postings;
     const uint32_t* plens;       // prefix indexes: distinct key lengths
     uint32_t n_idx;
-    uint32_t pad2;
+    uint32_t lean_cols;          // mxp_guard2_kernel: columns < MXP_CC its groups read (preloaded)
     uint32_t n_rules;
     uint32_t n_words;            // ceil(n_rules / 32)
     uint32_t groups_per_wave;

@@ -516,7 +516,6 @@ __device__ __forceinline__ void log_guard_errors(const mxp_kargs& A, uint32_t e,
 // Lean kernel's column cache: a group's segments alternate between columns (C4: the path and five
 // header columns), so instead of reloading a column whenever the segment's column changes, each
 // thread keeps the (kind, value) of columns < MXP_CC it has loaded in LDS slots of its own.
-#define MXP_CC 8u
 __shared__ uint64_t g_ccv[MXP_CC][256];
 __shared__ uint8_t g_cck[MXP_CC][256];
 
@@ -649,12 +648,14 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 
 // The lean groups with two requests per lane (a wave covers 128 requests): the kernel is bound by
 // scalar issue, and the per-group scalar work -- descriptor decode, segment loop, branches -- is now
-// spent once per 128 requests instead of once per 64.  Column cache: [MXP_CC][512] per workgroup
-// (4 waves/SIMD).  Same-box A/B on C4: 5.068 -> 4.850 ms per evaluation
-// (profiles/r1_v18_ab_guard2.log); MXP_DEBUG_FLAGS 65536 = mxp_guard_kernel, one request per lane.
+// spent once per 128 requests instead of once per 64 (C4 5.068 -> 4.850 ms per evaluation,
+// profiles/r1_v18_ab_guard2.log).  The columns < MXP_CC the lean groups read are loaded into LDS
+// once per workgroup and shared by its four waves (9 KB; 6 waves/SIMD): C4 4.87-4.90 -> 4.64-4.66
+// ms, builds alternated (profiles/r1_v19_ab_guard2_shared_cache.log).  MXP_DEBUG_FLAGS 65536 =
+// mxp_guard_kernel, one request per lane.
 extern "C" __global__ __launch_bounds__(256) void mxp_guard2_kernel(mxp_kargs A) {
-    __shared__ uint64_t ccv[MXP_CC][512];
-    __shared__ uint8_t cck[MXP_CC][512];
+    __shared__ uint64_t ccv[MXP_CC][128];
+    __shared__ uint8_t cck[MXP_CC][128];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = uni(tid >> 6);
@@ -663,10 +664,27 @@ extern "C" __global__ __launch_bounds__(256) void mxp_guard2_kernel(mxp_kargs A)
     const uint64_t N = A.n;
     const uint32_t i0 = (blockIdx.y * 4u + wave) * A.groups_per_wave;
     const uint32_t i1 = min(i0 + A.groups_per_wave, A.n_glist);
+    // the workgroup's 128 requests, columns < MXP_CC the lean groups read (kargs.lean_cols):
+    // loaded once into LDS, shared by the four waves
+    const uint32_t have = uni(A.lean_cols) & ((1u << MXP_CC) - 1u);
+    if (tid < 128u) {
+        const uint32_t q = A.q0 + blockIdx.x * 128u + tid;
+        for (uint32_t c = 0; c < MXP_CC; c++) {
+            if (!((have >> c) & 1u)) continue;
+            uint8_t k = MXP_ABSENT;
+            uint64_t v = 0;
+            if (q < A.q1) {
+                k = A.kinds[(uint64_t)c * N + q];
+                v = A.vals[(uint64_t)c * N + q];
+            }
+            cck[c][tid] = k;
+            ccv[c][tid] = v;
+        }
+    }
+    __syncthreads();
     uint32_t cached = MXP_VM_DONE;
     uint32_t cka = MXP_ABSENT, ckb = MXP_ABSENT;
     uint64_t cva = 0, cvb = 0;
-    uint32_t have = 0;
     for (uint32_t c0 = i0; c0 < i1; c0 += 4) {
         uint32_t D = 0;
         if (c0 + (lane >> 4) < i1) D = ((const uint32_t*)(A.groups + A.glist[c0 + (lane >> 4)]))[lane & 15u];
@@ -701,10 +719,10 @@ extern "C" __global__ __launch_bounds__(256) void mxp_guard2_kernel(mxp_kargs A)
                 if (col != cached) {
                     cached = col;
                     if (col < MXP_CC && ((have >> col) & 1u)) {
-                        cka = cck[col][2u * (tid & ~63u) + lane];
-                        cva = ccv[col][2u * (tid & ~63u) + lane];
-                        ckb = cck[col][2u * (tid & ~63u) + 64u + lane];
-                        cvb = ccv[col][2u * (tid & ~63u) + 64u + lane];
+                        cka = cck[col][lane];
+                        cva = ccv[col][lane];
+                        ckb = cck[col][64u + lane];
+                        cvb = ccv[col][64u + lane];
                     } else {
                         cka = ckb = MXP_ABSENT;
                         cva = cvb = 0;
@@ -715,13 +733,6 @@ extern "C" __global__ __launch_bounds__(256) void mxp_guard2_kernel(mxp_kargs A)
                         if (vb) {
                             ckb = A.kinds[(uint64_t)col * N + reqb];
                             cvb = A.vals[(uint64_t)col * N + reqb];
-                        }
-                        if (col < MXP_CC) {
-                            have |= 1u << col;
-                            cck[col][2u * (tid & ~63u) + lane] = (uint8_t)cka;
-                            ccv[col][2u * (tid & ~63u) + lane] = cva;
-                            cck[col][2u * (tid & ~63u) + 64u + lane] = (uint8_t)ckb;
-                            ccv[col][2u * (tid & ~63u) + 64u + lane] = cvb;
                         }
                     }
                 }

@@ -140,6 +140,8 @@ typedef struct mxp_hent {
 // stores.  Groups g0 .. g0 + n - 1 (n <= MXP_FILL_CHUNK), `all` = rules present in every group but
 // the last, `last` = those of the last.
 #define MXP_FILL_CHUNK 16u
+// columns < MXP_CC have LDS column-cache slots in the lean guard kernels (kargs.lean_cols)
+#define MXP_CC 8u
 typedef struct mxp_fill {
     uint32_t col;
     uint32_t okset;    // bits 0..15: kinds that pass; bits 24..31: want class / GK_VCOL

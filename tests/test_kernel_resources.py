@@ -12,7 +12,7 @@ CSRC = os.path.join(ROOT, "istio_amd", "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # minimum waves/SIMD per kernel (launch_bounds(256) kernels; the values the launches were tuned at)
-MIN_OCCUPANCY = {"mxp_guard_kernel": 8, "mxp_guard2_kernel": 4, "mxp_eval_kernel": 4, "mxp_index_kernel": 6, "mxp_index5_kernel": 5}
+MIN_OCCUPANCY = {"mxp_guard_kernel": 8, "mxp_guard2_kernel": 6, "mxp_eval_kernel": 4, "mxp_index_kernel": 6, "mxp_index5_kernel": 5}
 # bounded scratch, chosen by A/B: mxp_index_kernel at 6 waves/SIMD spills two VGPRs (12 bytes per
 # lane) and still beats the spill-free 5-wave build (mxp_index5_kernel) on C4 (5.10 vs 5.31 ms)
 MAX_SCRATCH = {"mxp_index_kernel": 16}
