@@ -1,14 +1,19 @@
 #!/usr/bin/env python3
 """Benchmark: request x rule predicate evaluations per second (BASELINE.json `metric`).
 
-Workload (per GPU): the C2 rule family of BASELINE.json configs[1] (`destination.service == ... &&
-request.path.startsWith(...) && source.ip != ip(...)`) scaled to the metric's 10k rules, over 1M
-synthetic requests (Zipf(1.1) services) resident in HBM -- the per-GPU shard of configs[4]
+Headline workload (per GPU): the C2 rule family of BASELINE.json configs[1] (`destination.service ==
+... && request.path.startsWith(...) && source.ip != ip(...)`) scaled to the metric's 10k rules, over
+1M synthetic requests (Zipf(1.1) services) resident in HBM -- the per-GPU shard of configs[4]
 (8 x MI355X, 8M requests).  A step = one evaluation of every rule against every request of the
-shard (the full predicate bitmap) + the per-rule hit counters, all-reduced over RCCL when N > 1.
+shard (the full predicate bitmap) + the per-rule hit counters, reduced over RCCL when N > 1 with one
+all-reduce per step (istio_amd.dist.StepCounters).
+
+The default run also measures C4 (configs[3]: 10k Pilot-style route rules x 1M requests) with the
+same step structure and reports it as the extra "c4" block of the same JSON line (--no-c4: skip).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rules R] [--requests N_PER_GPU]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+    python bench.py --workload c4 | c5 | c3-ip | c3-str | c3-regex | c5-quota
 
 Prints one JSON line (rank 0).
 """
@@ -22,6 +27,21 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+QUOTA_KEYS = 1024
+
+
+def host_threads():
+    """CPU threads for the host baselines: every CPU the process may use (os.cpu_count(), bounded by
+    its affinity set and by OMP_NUM_THREADS when the environment sets it -- the GPU box reports the
+    whole machine's CPUs but grants a share of 16)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        pass
+    if os.environ.get("OMP_NUM_THREADS"):
+        n = min(n, int(os.environ["OMP_NUM_THREADS"]))
+    return max(1, n)
 
 
 def parse():
@@ -32,10 +52,12 @@ def parse():
     p.add_argument("--rules", type=int, default=10000)
     p.add_argument("--requests", type=int, default=1 << 20)
     p.add_argument("--cpu-sample-seconds", type=float, default=12.0)
-    p.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    p.add_argument("--cpu-threads", type=int, default=host_threads())
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--workload", default="c2", choices=["c2", "c4", "c3-ip", "c3-str", "c3-regex", "c5-quota"],
-                   help="c2 (default, the BASELINE metric); secondary measurements: c4 route rules, C3 lists")
+    p.add_argument("--no-c4", action="store_true", help="default run: skip the extra C4 block")
+    p.add_argument("--workload", default="c2", choices=["c2", "c4", "c5", "c3-ip", "c3-str", "c3-regex", "c5-quota"],
+                   help="c2 (default, the BASELINE metric; + a C4 block); c4 route rules; c5 = C2 predicates + "
+                        "memquota with one combined all-reduce; C3 lists; c5-quota memquota alone")
     p.add_argument("--list-entries", type=int, default=100_000)
     return p.parse_args()
 
@@ -55,7 +77,7 @@ def cpu_baseline(manifest, rules, batch, seconds, threads, chunk=256):
         done += chunk
     dt = time.perf_counter() - t0
     pairs = done * len(rules)
-    return {"value": pairs / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+    return {"value": pairs / dt, "unit": "pairs/s", "cores": threads, "host_cpus": os.cpu_count(), "kind": "port",
             "sample": "%d requests x %d rules (%.1fs, oracle C restatement, rules precompiled)" % (
                 done, len(rules), dt)}
 
@@ -64,13 +86,14 @@ def measured_traffic(workload, rules, requests):
     """HBM bytes per evaluation from the committed PMC profile (tools/pmc_summarize.py: FETCH_SIZE
     and WRITE_SIZE in separate rocprofv3 passes, FETCH doubled for gfx950), when one exists for this
     workload size; else None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None
-    d = json.load(open(path))
-    if d.get("workload", "c2") != workload or d.get("rules") != rules or d.get("requests") != requests:
-        return None
-    return d.get("bytes_per_eval")
+    for name in ("pmc_traffic_%s.json" % workload, "pmc_traffic.json"):
+        path = os.path.join(ROOT, "profiles", name)
+        if not os.path.exists(path):
+            continue
+        d = json.load(open(path))
+        if d.get("workload", "c2") == workload and d.get("rules") == rules and d.get("requests") == requests:
+            return d.get("bytes_per_eval")
+    return None
 
 
 def lds_conflicts(workload):
@@ -84,12 +107,35 @@ def lds_conflicts(workload):
                 "rate": v.get("bank_conflict_rate")} for k, v in d.get("kernels", {}).items()}
 
 
+def timed_loop(step, steps, warmup, world, stream):
+    """W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize; returns the
+    slowest rank's seconds and the per-step HIP-event durations (ms) recorded on `stream`."""
+    import torch
+    import torch.distributed as dist
+    from istio_amd import dist as D
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(*evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ev_ms = [a.elapsed_time(b) for a, b in evs]
+    return D.max_over_ranks(elapsed, torch.device("cuda", torch.cuda.current_device())), ev_ms
+
+
 def list_bench(args, rank, world, local):
     """C3 (BASELINE configs[2]): 100k-entry CIDR / string / regex lists, 1M lookups per GPU resident
     in HBM; one step = HandleListEntry for every lookup (mxp_list_check_device, one kernel)."""
     import numpy as np
     import torch
-    from istio_amd import dist as D
     from istio_amd import workloads as W
     from istio_amd.engine import Engine
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -127,16 +173,8 @@ def list_bench(args, rank, world, local):
         lst.check_device(d_blob.data_ptr(), d_off.data_ptr(), len(bs), stream.cuda_stream, d_codes.data_ptr())
         if e1 is not None:
             e1.record(stream)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(*evs[k])
-    torch.cuda.synchronize()
-    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    elapsed, ev_ms = timed_loop(step, args.steps, args.warmup, world, stream)
+    kernel_ms = float(np.mean(ev_ms))
     n = len(bs)
     alg = int(off[-1]) + 8 * (n + 1) + 4 * n  # symbol bytes + offsets read, one code written each
     achieved = alg / (kernel_ms * 1e-3) / 1e9
@@ -157,65 +195,70 @@ def list_bench(args, rank, world, local):
         print(json.dumps(out))
 
 
-def quota_bench(args, rank, world, local):
-    """C5 memquota (BASELINE configs[4]): K = 1024 quota keys, 1M quota requests per GPU in arrival
-    order; a step = batched HandleQuota (sort by key + per-key replay) and, when N > 1, the RCCL
-    all-reduce of the per-key granted deltas."""
+def quota_setup(eng, n_requests, rank, world, dev):
+    """memquota state for QUOTA_KEYS keys and this rank's quota requests: the global arrival stream
+    routed by key owner (workloads.quota_workload, dist.key_owner), resident in HBM."""
     import numpy as np
     import torch
-    from istio_amd import dist as D
     from istio_amd import workloads as W
-    from istio_amd.engine import Engine
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import memquota as M
-    K = 1024
-    mx, vd, keys, amounts, be = W.quota_workload(n_keys=K, n_requests=args.requests, seed=5 + 1000 * rank)
-    eng = Engine(local)
+    mx, vd, keys, amounts, be = W.quota_workload(n_keys=QUOTA_KEYS, n_requests=n_requests, seed=5, rank=rank,
+                                                 world=world)
     q = eng.quota_create(mx, vd)
-    dev = torch.device("cuda", local)
     dk = torch.from_numpy(keys.view(np.int32).copy()).to(dev)
     da = torch.from_numpy(amounts.copy()).to(dev)
     db = torch.from_numpy(be.copy()).to(dev)
     dg = torch.empty(len(keys), dtype=torch.int64, device=dev)
-    delta = torch.zeros(K, dtype=torch.int64, device=dev)
+    return (mx, vd, keys, amounts, be), q, (dk, da, db, dg)
+
+
+def quota_bench(args, rank, world, local):
+    """C5 memquota (BASELINE configs[4]): K = 1024 quota keys, each owned by one rank (key % N), the
+    quota requests routed to their key's owner in arrival order (~1M per GPU); a step = batched
+    HandleQuota (sort by key + per-key replay) and, when N > 1, the all-reduce of the per-key deltas."""
+    import numpy as np
+    import torch
+    from istio_amd import dist as D
+    from istio_amd.engine import Engine
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import memquota as M
+    eng = Engine(local)
+    dev = torch.device("cuda", local)
+    (mx, vd, keys, amounts, be), q, (dk, da, db, dg) = quota_setup(eng, args.requests, rank, world, dev)
+    ctr = D.StepCounters([QUOTA_KEYS], dev)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     now = [1_500_000_000 * 10**9]
 
     def step(e0=None, e1=None):
+        ctr.begin_step()
+        (delta,) = ctr.views()
         if e0 is not None:
             e0.record(stream)
         q.alloc_device(len(keys), dk.data_ptr(), da.data_ptr(), db.data_ptr(), now[0], stream.cuda_stream,
                        dg.data_ptr(), delta.data_ptr())
         if e1 is not None:
             e1.record(stream)
-        D.reduce_counters(delta)  # RCCL over xGMI when N > 1: per-key quota deltas
+        ctr.end_step()
         now[0] += 10**8
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(*evs[k])
-    torch.cuda.synchronize()
-    elapsed = D.max_over_ranks(time.perf_counter() - t0, dev)
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    elapsed, ev_ms = timed_loop(step, args.steps, args.warmup, world, stream)
+    kernel_ms = float(np.mean(ev_ms))
     n = len(keys)
+    n_all = int(D.sum_over_ranks(float(n)))  # quota requests of all ranks (routing by key owner)
     alg = n * (4 + 8 + 1 + 8)  # key, amount, best effort read; granted written
     achieved = alg / (kernel_ms * 1e-3) / 1e9
-    out = {"metric": "memquota HandleQuota requests/sec (%d keys)" % K, "value": world * n * args.steps / elapsed,
+    out = {"metric": "memquota HandleQuota requests/sec (%d keys)" % QUOTA_KEYS,
+           "value": n_all * args.steps / elapsed,
            "unit": "requests/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-           "dtype": "int64", "data": "synthetic (seeded C5 quota requests; resident in HBM)",
-           "config": {"workload": "C5 memquota, %d keys, %d requests per GPU (configs[4])" % (K, n), "keys": K,
-                      "requests_per_gpu": n, "parallelism": "request-sharded dp%d" % world},
+           "dtype": "int64", "data": "synthetic (seeded C5 quota requests routed by key owner; resident in HBM)",
+           "config": {"workload": "C5 memquota, %d keys, %d requests per GPU (configs[4])" % (QUOTA_KEYS, n),
+                      "keys": QUOTA_KEYS, "requests_per_gpu": n, "parallelism": "key-owner-sharded dp%d" % world},
            "kernel_ms": kernel_ms,
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                         "kernel": "hipcub radix sort + mxp_quota_kernel", "alg_bytes_per_launch": alg}}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        ref = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
+        ref = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(QUOTA_KEYS)})
         t0 = time.perf_counter()
         done = 0
         while time.perf_counter() - t0 < args.cpu_sample_seconds and done < n:
@@ -223,7 +266,8 @@ def quota_bench(args, rank, world, local):
                 ref.handle(int(keys[i]), int(amounts[i]), bool(be[i]), 1_500_000_000 * 10**9)
             done = min(done + 4096, n)
         dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": done / dt, "unit": "requests/s", "cores": 1, "kind": "port",
+        out["cpu_baseline"] = {"value": done / dt, "unit": "requests/s", "cores": 1, "host_cpus": os.cpu_count(),
+                               "kind": "port",
                                "sample": "%d requests (%.1fs), memquota restatement (Python, sequential)" % (done, dt)}
     if rank == 0:
         print(json.dumps(out))
@@ -231,8 +275,7 @@ def quota_bench(args, rank, world, local):
 
 def list_cpu_baseline(L, kind, entries, syms, seconds, threads):
     """The list restatement timed on host cores: the IP list is the reference's linear IPNet scan
-    (ipList.go:77-92, C + OpenMP); strings a hash set (Python); regexes the Go regexp restatement
-    (Python Pike VM, single thread -- far slower than Go's regexp)."""
+    (ipList.go:77-92, C + OpenMP); strings a hash set (Python); regexes the Go regexp restatement."""
     if kind == "c3-ip":
         ref, threads_used = L.IPList(entries), threads
     elif kind == "c3-str":
@@ -247,33 +290,27 @@ def list_cpu_baseline(L, kind, entries, syms, seconds, threads):
         done += chunk
         chunk = min(chunk * 2, 1 << 16)
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "lookups/s", "cores": threads_used, "kind": "port",
+    return {"value": done / dt, "unit": "lookups/s", "cores": threads_used, "host_cpus": os.cpu_count(),
+            "kind": "port",
             "sample": "%d lookups (%.1fs) against all %d entries, oracle restatement" % (done, dt, len(entries))}
 
 
-def main():
-    args = parse()
+def predicate_bench(args, kind, rank, world, local, with_quota=False):
+    """One predicate workload (c2 / c4) on this rank's 1M-request shard; returns the result dict.
+
+    Step: evaluate every (request, rule) pair with the per-rule hit counters fused into the
+    evaluation kernels (accumulated into the step's counter buffer), optionally the memquota
+    HandleQuota batch of the rank's quota requests (per-key deltas into the same buffer), then ONE
+    all-reduce of hits[R] ++ quota_delta[K] when N > 1."""
     import numpy as np
     import torch
-    import torch.distributed as dist
-
     from istio_amd import dist as D
-    rank, world, local = D.world()
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
-    from istio_amd import build
-    build.build()
     from istio_amd import workloads as W
     from istio_amd.engine import Engine
 
-    if args.workload.startswith("c3"):
-        return list_bench(args, rank, world, local)
-    if args.workload == "c5-quota":
-        return quota_bench(args, rank, world, local)
-    # requests shard per rank; the rule set is replicated
-    if args.workload == "c4":
+    dev = torch.device("cuda", local)
+    # requests shard per rank (independent seeds = disjoint synthetic shards); the rule set is replicated
+    if kind == "c4":
         manifest, rules, batch = W.c4_workload(n_rules=args.rules, n_requests=args.requests, seed=4 + 1000 * rank)
         metric, workload = ("request x rule predicate evals/sec at 10k rules (C4 route rules)",
                             "C4 Pilot-style route rules R=%d, %d requests per GPU (configs[3])")
@@ -292,42 +329,35 @@ def main():
 
     R, N = len(rules), batch.n
     Wd = (R + 31) // 32
-    dev = torch.device("cuda", local)
     d_match = torch.empty((Wd, N), dtype=torch.int32, device=dev)
     d_err = torch.empty((Wd, N), dtype=torch.int32, device=dev)
-    hits = torch.zeros(R, dtype=torch.int64, device=dev)
     stream = torch.cuda.Stream(dev)  # a real (non-null) HIP stream shared by libmxp, events and RCCL
     torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
+    quota = None
+    if with_quota:
+        quota = quota_setup(eng, N, rank, world, dev)
+    ctr = D.StepCounters([R] + ([QUOTA_KEYS] if quota else []), dev)
+    now = [1_500_000_000 * 10**9]
 
     def step(ev0=None, ev1=None):
+        ctr.begin_step()
+        views = ctr.views()
         if ev0 is not None:
             ev0.record(stream)
-        # evaluation with the per-rule hit counters fused into the evaluation kernels
-        db.eval_hits(d_match.data_ptr(), d_err.data_ptr(), hits.data_ptr(), sh)
+        db.eval_hits(d_match.data_ptr(), d_err.data_ptr(), views[0].data_ptr(), sh)
+        if quota is not None:
+            (_, q, (dk, da, dbe, dg)) = quota
+            q.alloc_device(dk.numel(), dk.data_ptr(), da.data_ptr(), dbe.data_ptr(), now[0], sh, dg.data_ptr(),
+                           views[1].data_ptr())
+            now[0] += 10**8
         if ev1 is not None:
             ev1.record(stream)
-        D.reduce_counters(hits)  # RCCL over xGMI when world > 1: per-rule hit counters
+        ctr.end_step()  # the step's single collective over RCCL / xGMI when N > 1
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(*evs[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    elapsed = D.max_over_ranks(elapsed, dev)
-
-    pairs_total = world * N * R * args.steps
-    value = pairs_total / elapsed
+    elapsed, ev_ms = timed_loop(step, args.steps, args.warmup, world, stream)
+    step_kernel_ms = float(np.mean(ev_ms))
+    value = world * N * R * args.steps / elapsed
 
     # per-kernel durations (HIP events recorded by libmxp around each launch, on `stream`), in a
     # separate pass so the timed region above carries no extra synchronisation
@@ -347,7 +377,7 @@ def main():
     prog_bytes = 16 * sum(eng.rule_vm_text(i).count("\n") for i in range(R)) + 4 * (R + 1)
     alg_bytes = N * n_cols * 9 + prog_bytes + 2 * N * Wd * 4
     achieved = alg_bytes / (eval_ms * 1e-3) / 1e9
-    traffic = measured_traffic(args.workload, R, N)
+    traffic = measured_traffic(kind, R, N)
 
     out = {
         "metric": metric,
@@ -361,31 +391,69 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": "synthetic (seeded %s workload; requests resident in HBM)" % args.workload.upper(),
+        "data": "synthetic (seeded %s workload; requests resident in HBM)" % kind.upper(),
         "config": {"workload": workload % (R, N),
                    "rules": R, "requests_per_gpu": N, "parallelism": "request-sharded dp%d" % world},
-        "eval_ms": kernel_ms,
+        "eval_ms": step_kernel_ms,
         "kernels_ms": {"mxp_fill_kernel+mxp_guard2_kernel+mxp_eval_kernel": k_eval,
                        "mxp_index_kernel+mxp_inject_kernel": k_index},
         "pack_upload_s": t_pack,
-        "lds_bank_conflicts": lds_conflicts(args.workload),
+        "lds_bank_conflicts": lds_conflicts(kind),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "one evaluation: mxp_fill_kernel / mxp_guard2_kernel / mxp_eval_kernel (the groups "
                                "each serves) + mxp_index_kernel (+ mxp_inject_kernel with dense rules)",
                      "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pair": alg_bytes / (N * R)},
     }
+    if quota is not None:
+        out["quota"] = {"keys": QUOTA_KEYS, "requests_per_gpu": int(quota[2][0].numel()),
+                        "collective": "one all_reduce(sum) of hits[R] ++ quota_delta[K] per step"}
+    hits = ctr.totals()[0]
+    out["hits_total"] = int(hits.sum().item())
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        if args.workload == "c4":
+        if kind == "c4":
             sample = W.c4_workload(n_rules=args.rules, n_requests=512, seed=4)[2]
             out["cpu_baseline"] = cpu_baseline(manifest, rules, sample, args.cpu_sample_seconds, args.cpu_threads,
                                                chunk=16)
         else:
             sample = W.c2_workload(n_rules=args.rules, n_requests=min(N, 1 << 18), seed=2)[2]
             out["cpu_baseline"] = cpu_baseline(manifest, rules, sample, args.cpu_sample_seconds, args.cpu_threads)
+    db.free()
+    del d_match, d_err
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return out
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from istio_amd import dist as D
+    rank, world, local = D.world()
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from istio_amd import build
+    build.build()
+
+    if args.workload.startswith("c3"):
+        return list_bench(args, rank, world, local)
+    if args.workload == "c5-quota":
+        return quota_bench(args, rank, world, local)
+    kind = "c4" if args.workload == "c4" else "c2"
+    out = predicate_bench(args, kind, rank, world, local, with_quota=args.workload == "c5")
+    if args.workload == "c2" and not args.no_c4:
+        # the representative config BASELINE.json quotes at 10k rules (configs[3]), driver-timed too
+        c4 = predicate_bench(args, "c4", rank, world, local)
+        out["c4"] = {k: c4[k] for k in ("metric", "value", "unit", "ms_per_step", "eval_ms", "kernels_ms",
+                                        "pack_upload_s", "config", "roofline", "lds_bank_conflicts")}
+        if "cpu_baseline" in c4:
+            out["c4"]["cpu_baseline"] = c4["cpu_baseline"]
     if rank == 0:
         print(json.dumps(out))
-    db.free()
     if world > 1:
         dist.destroy_process_group()
 

@@ -230,7 +230,9 @@ int mxp_listentry_check(mxp_engine* eng, const mxp_list* list, int blacklist, co
  * granted[i] = QuotaResult.Amount.  State persists across calls.  DeduplicationID handling
  * (dedup.go handleDedup) stays with the caller.  mxp_quota_alloc_device takes device arrays and can
  * accumulate per-key granted deltas (allocs - frees) into d_delta (i64[n_keys]) for the cross-GPU
- * all-reduce.
+ * all-reduce; a device key id >= n_keys is granted 0 and touches no key's state (the
+ * host mxp_quota_alloc rejects it with MXP_ERR_ARG).  Multi-GPU: each key has one owner rank and its
+ * requests are routed there (istio_amd/dist.py key_owner), so every key's sequence stays on one GPU.
  */
 typedef struct mxp_quota mxp_quota;
 int mxp_quota_create(mxp_engine* eng, uint32_t n_keys, const int64_t* max_amount, const int64_t* valid_duration_ns,

@@ -1158,7 +1158,9 @@ void mxp_engine_destroy(mxp_engine* eng) {
     for (auto& x : eng->chunk_ev)
         if (x) (void)hipEventDestroy(x);
     if (eng->side) (void)hipStreamDestroy(eng->side);
-    if (eng->h_stats) (void)hipHostFree(eng->h_stats);  // (synchronises with a pending stats copy)
+    if (eng->stats_ev) (void)hipEventSynchronize(eng->stats_ev);
+    if (eng->stats_ev) (void)hipEventDestroy(eng->stats_ev);
+    if (eng->h_stats) (void)hipHostFree(eng->h_stats);
     delete eng;
 }
 
@@ -1311,13 +1313,24 @@ int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, ui
             return eng->hipfail(e, "stats host");
         }
         *eng->h_stats = 0;
+        if ((e = hipEventCreateWithFlags(&eng->stats_ev, hipEventDisableTiming)) != hipSuccess) {
+            eng->stats_ev = nullptr;
+            return eng->hipfail(e, "stats event");
+        }
     }
     // Counting in the kernels costs one atomic per true pair the index kernel sets; re-reading the
     // match bitmap costs its W x N x 4 bytes (~ a true pair per 125 bitmap words at the measured
-    // atomic and streaming rates): choose by the last evaluation's true pairs per request.
+    // atomic and streaming rates): choose by the true pairs per request of the latest evaluation
+    // whose stats download has COMPLETED (event query, no wait; else the previous rate stands).
     const uint32_t R = (uint32_t)eng->rules.size(), W = (R + 31) / 32;
-    const double tp = eng->stats_n ? (double)*eng->h_stats / eng->stats_n : 0.0;
-    const bool fused = tp * 125.0 <= (double)W;
+    if (eng->stats_pending && hipEventQuery(eng->stats_ev) == hipSuccess) {
+        eng->stats_tp = eng->stats_n ? (double)*eng->h_stats / eng->stats_n : 0.0;
+        eng->stats_pending = false;
+    }
+    const bool fused = eng->stats_tp * 125.0 <= (double)W;
+    // the reset follows the previous download even when the caller switched streams
+    if (eng->stats_pending && (e = hipStreamWaitEvent(s, eng->stats_ev, 0)) != hipSuccess)
+        return eng->hipfail(e, "stats wait");
     if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
     int rc = eng->launch(db, s, d_match, d_err, nullptr, false, fused ? d_hits : nullptr, eng->d_stats.as<uint64_t>());
     if (rc) return rc;
@@ -1325,6 +1338,8 @@ int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, ui
         return eng->hipfail(e, "launch hits");
     if ((e = hipMemcpyAsync(eng->h_stats, eng->d_stats.p, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
         return eng->hipfail(e, "stats download");
+    if ((e = hipEventRecord(eng->stats_ev, s)) != hipSuccess) return eng->hipfail(e, "stats event");
+    eng->stats_pending = true;
     eng->stats_n = db->n;
     return MXP_OK;
 }

@@ -372,6 +372,9 @@ struct mxp_engine : public mxp::LowerTables {
     DevBuf d_stats;
     uint64_t* h_stats = nullptr;
     uint32_t stats_n = 0;
+    hipEvent_t stats_ev = nullptr;  // recorded after each stats download
+    bool stats_pending = false;     // a download not yet seen complete
+    double stats_tp = 0.0;          // true pairs per request of the last completed download
     std::string format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r) const;
     std::string string_of(const mxp_dbatch* db, uint64_t sid) const {
         if (!db) db = last_db.get();

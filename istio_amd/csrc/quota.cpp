@@ -10,15 +10,16 @@
 #include "engine_impl.h"
 #include "quota_args.h"
 
-extern "C" hipError_t mxp_quota_sort(void* tmp, size_t* tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
-                                     uint32_t* idx_in, uint32_t* idx_out, uint32_t n, int bits, hipStream_t s);
+extern "C" hipError_t mxp_quota_sort(void* tmp, size_t* tmp_bytes, const uint32_t* key, uint32_t n_keys,
+                                     uint32_t* keys_in, uint32_t* keys_out, uint32_t* idx_in, uint32_t* idx_out,
+                                     uint32_t n, int bits, hipStream_t s);
 extern "C" hipError_t mxp_launch_quota(const mxp_quota_args* a, const uint32_t* skeys, uint32_t* seg_start,
                                        hipStream_t s);
 
 struct mxp_quota {
     uint32_t n_keys = 0;
     DevBuf max_amount, ticks, cells, avail, win_cur, win_tick, slot_off, slots;
-    DevBuf keys_sorted, idx_in, order, seg_start, tmp;
+    DevBuf keys_clamped, keys_sorted, idx_in, order, seg_start, tmp;
     size_t cap = 0, tmp_bytes = 0;
 };
 
@@ -57,7 +58,8 @@ int mxp_quota_create(mxp_engine* eng, uint32_t n_keys, const int64_t* max_amount
     if ((rc = put(Q->slot_off, off.data(), off.size() * 8, "quota slot_off"))) return rc;
     if ((e = Q->slots.alloc(off[n_keys] * 8 + 16)) != hipSuccess) return eng->hipfail(e, "quota slots");
     if ((e = hipMemset(Q->slots.p, 0, off[n_keys] * 8 + 16)) != hipSuccess) return eng->hipfail(e, "quota slots");
-    if ((e = Q->seg_start.alloc(((size_t)n_keys + 1) * 4)) != hipSuccess) return eng->hipfail(e, "quota seg");
+    // segments of keys 0 .. n_keys (the last: out-of-range key ids, mxp_quota_clamp), plus the end
+    if ((e = Q->seg_start.alloc(((size_t)n_keys + 2) * 4)) != hipSuccess) return eng->hipfail(e, "quota seg");
     *out = Q.release();
     return MXP_OK;
 }
@@ -76,20 +78,23 @@ int mxp_quota_alloc_device(mxp_engine* eng, mxp_quota* Q, uint32_t n, const uint
     hipError_t e;
     if (n > Q->cap) {
         if ((e = Q->keys_sorted.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota keys");
+        if ((e = Q->keys_clamped.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota keys");
         if ((e = Q->idx_in.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota idx");
         if ((e = Q->order.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota order");
         size_t need = 0;
-        if ((e = mxp_quota_sort(nullptr, &need, nullptr, nullptr, nullptr, nullptr, n, 32, s)) != hipSuccess)
+        if ((e = mxp_quota_sort(nullptr, &need, nullptr, 0, nullptr, nullptr, nullptr, nullptr, n, 32, s)) != hipSuccess)
             return eng->hipfail(e, "quota sort size");
         if ((e = Q->tmp.alloc(need)) != hipSuccess) return eng->hipfail(e, "quota sort tmp");
         Q->tmp_bytes = need;
         Q->cap = n;
     }
+    // sort keys 0 .. n_keys (n_keys = the sentinel of out-of-range ids): enough bits for n_keys itself
     int bits = 1;
-    while (bits < 32 && (1ull << bits) < Q->n_keys) bits++;
+    while (bits < 32 && (1ull << bits) <= Q->n_keys) bits++;
     size_t tb = Q->tmp_bytes;
-    if ((e = mxp_quota_sort(Q->tmp.p, &tb, d_key, Q->keys_sorted.as<uint32_t>(), Q->idx_in.as<uint32_t>(),
-                            Q->order.as<uint32_t>(), n, bits, s)) != hipSuccess)
+    if ((e = mxp_quota_sort(Q->tmp.p, &tb, d_key, Q->n_keys, Q->keys_clamped.as<uint32_t>(),
+                            Q->keys_sorted.as<uint32_t>(), Q->idx_in.as<uint32_t>(), Q->order.as<uint32_t>(), n, bits,
+                            s)) != hipSuccess)
         return eng->hipfail(e, "quota sort");
     mxp_quota_args A;
     memset(&A, 0, sizeof A);

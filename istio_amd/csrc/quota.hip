@@ -37,9 +37,13 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, uint32_t l) {
 extern "C" __global__ __launch_bounds__(256) void mxp_quota_kernel(mxp_quota_args A) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6);
-    if (k >= A.n_keys) return;
+    if (k > A.n_keys) return;
     const uint32_t b = A.seg_start[k], e = A.seg_start[k + 1];
     if (b == e) return;
+    if (k == A.n_keys) {  // key ids >= n_keys (mxp_quota_clamp): no state to grant from
+        for (uint32_t j = b + lane; j < e; j += 64u) A.granted[A.order[j]] = 0;
+        return;
+    }
     const int64_t maxv = A.max_amount[k];
     const uint32_t len = A.ticks[k];
     const bool window = len != 0;
@@ -168,16 +172,29 @@ extern "C" __global__ void mxp_quota_segments(const uint32_t* skeys, uint32_t n,
     for (uint32_t k = prev; k <= cur && k <= n_keys; k++) seg_start[k] = i;
 }
 
-extern "C" hipError_t mxp_quota_sort(void* tmp, size_t* tmp_bytes, const uint32_t* keys_in, uint32_t* keys_out,
-                                     uint32_t* idx_in, uint32_t* idx_out, uint32_t n, int bits, hipStream_t s) {
-    if (tmp) hipLaunchKernelGGL(mxp_quota_iota, dim3((n + 255) / 256), dim3(256), 0, s, idx_in, n);
+// key ids outside [0, n_keys) become the sentinel n_keys: the radix sort only looks at the low bits
+// of n_keys, so an out-of-range id would otherwise sort as another key and replay against its state
+extern "C" __global__ void mxp_quota_clamp(const uint32_t* key, uint32_t n, uint32_t n_keys, uint32_t* out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < n) out[i] = min(key[i], n_keys);
+}
+
+// sorts the clamped keys (keys_in is scratch of n entries, overwritten with the clamped copy)
+extern "C" hipError_t mxp_quota_sort(void* tmp, size_t* tmp_bytes, const uint32_t* key, uint32_t n_keys,
+                                     uint32_t* keys_in, uint32_t* keys_out, uint32_t* idx_in, uint32_t* idx_out,
+                                     uint32_t n, int bits, hipStream_t s) {
+    if (tmp) {
+        hipLaunchKernelGGL(mxp_quota_clamp, dim3((n + 255) / 256), dim3(256), 0, s, key, n, n_keys, keys_in);
+        hipLaunchKernelGGL(mxp_quota_iota, dim3((n + 255) / 256), dim3(256), 0, s, idx_in, n);
+    }
     return hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, keys_in, keys_out, idx_in, idx_out, (int)n, 0, bits, s);
 }
 
 extern "C" hipError_t mxp_launch_quota(const mxp_quota_args* a, const uint32_t* skeys, uint32_t* seg_start,
                                        hipStream_t s) {
-    hipLaunchKernelGGL(mxp_quota_segments, dim3((a->n + 1 + 255) / 256), dim3(256), 0, s, skeys, a->n, a->n_keys,
+    // n_keys + 1 segments: the sentinel key n_keys collects the out-of-range ids (granted 0)
+    hipLaunchKernelGGL(mxp_quota_segments, dim3((a->n + 1 + 255) / 256), dim3(256), 0, s, skeys, a->n, a->n_keys + 1,
                        seg_start);
-    hipLaunchKernelGGL(mxp_quota_kernel, dim3((a->n_keys + 3) / 4), dim3(256), 0, s, *a);
+    hipLaunchKernelGGL(mxp_quota_kernel, dim3((a->n_keys + 1 + 3) / 4), dim3(256), 0, s, *a);
     return hipGetLastError();
 }

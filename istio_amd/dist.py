@@ -1,7 +1,13 @@
-"""Multi-GPU plumbing of the engine: requests shard across ranks, rule tables are replicated, and the
-only exchange is a sum all-reduce of per-rule counters (hit counters; later memquota deltas) --
-SURVEY.md 8(e).  One process per GPU under torch.distributed (backend "nccl" = RCCL over xGMI on
-ROCm; "gloo" in the CPU tests).
+"""Multi-GPU plumbing of the engine.
+
+* Requests shard across ranks and the compiled rule / DFA / list tables are replicated: a Check
+  request's predicates read only its own bag and the immutable rule set (resolver.go:202-238).
+* memquota keys have ONE owner rank each (`key_owner`): the quota requests of a key are routed to its
+  owner, so each key's arrival sequence is replayed on one GPU exactly as memquota.go:118-211 replays
+  it in one process.  The per-key state never has to move.
+* The only exchange is one sum all-reduce per step over the concatenated per-step counters
+  `hits[R] ++ quota_delta[K]` (`StepCounters`), RCCL over xGMI ("nccl" backend on ROCm), "gloo" in
+  the CPU tests.
 """
 from __future__ import annotations
 
@@ -21,20 +27,77 @@ def shard_bounds(n_total: int, rank: int, world_size: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def reduce_counters(t):
-    """Sum a per-rule counter tensor over all ranks, in place (no-op on a single process)."""
+def key_owner(key, world_size: int):
+    """Owner rank of a memquota key id (works elementwise on numpy arrays): the rank that holds the
+    key's cell / rolling window and replays all of its requests in arrival order."""
+    return key % world_size
+
+
+def _initialized() -> bool:
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def reduce_counters(t):
+    """Sum a counter tensor over all ranks, in place (no-op on a single process)."""
+    import torch.distributed as dist
+    if _initialized():
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return t
+
+
+class StepCounters:
+    """Per-step counters reduced with ONE collective per step.
+
+    Layout: one int64 tensor = the concatenation of `sizes` (e.g. hits[R] ++ quota_delta[K]).  The
+    kernels of a step ACCUMULATE into `views()` (fused hit counters, memquota deltas); `end_step()`
+    all-reduces that step's buffer and adds it to the running `total`.  On a single process the step
+    buffer IS the total and nothing is reduced -- no extra work in the timed region.  With several
+    ranks the step buffer is zeroed by `begin_step()`, so each step reduces only that step's counts
+    (reducing a cumulative buffer every step would re-add the other ranks' earlier totals).
+    """
+
+    def __init__(self, sizes, device=None):
+        import torch
+        self.sizes = list(sizes)
+        self.multi = _initialized()
+        self.total = torch.zeros(sum(self.sizes), dtype=torch.int64, device=device)
+        self.step = torch.zeros_like(self.total) if self.multi else self.total
+
+    def views(self):
+        """The step buffer split per counter family (views share its storage)."""
+        return list(self.step.split(self.sizes))
+
+    def totals(self):
+        return list(self.total.split(self.sizes))
+
+    def begin_step(self):
+        if self.multi:
+            self.step.zero_()
+
+    def end_step(self):
+        if self.multi:
+            reduce_counters(self.step)  # the step's single collective
+            self.total.add_(self.step)
 
 
 def max_over_ranks(x: float, device=None) -> float:
     """Max of a scalar over ranks (the bench's step time is the slowest rank's)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1):
+    if not _initialized():
         return x
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, device=None) -> float:
+    """Sum of a scalar over ranks (e.g. the quota requests each owner rank received)."""
+    import torch
+    import torch.distributed as dist
+    if not _initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())

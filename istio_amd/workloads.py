@@ -518,18 +518,31 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512):
 
 
 # ----------------------------------------------------------------------------------- memquota (C5)
-def quota_workload(n_keys=1024, n_requests=1_000_000, seed=5, p_free=0.1, p_zero=0.02, p_be=0.5):
+def quota_workload(n_keys=1024, n_requests=1_000_000, seed=5, p_free=0.1, p_zero=0.02, p_be=0.5, rank=0, world=1,
+                   return_index=False):
     """C5 memquota deltas: K quota keys (a third non-expiring cells, the rest 1 s / 60 s rolling
     windows) with limits 50..5000, requests in arrival order (Zipf keys, amounts 1..20, some frees
-    and zero amounts, best effort half the time).  Returns (max_amount, valid_ns, keys, amounts, be)."""
+    and zero amounts, best effort half the time).  Returns (max_amount, valid_ns, keys, amounts, be).
+
+    Multi-GPU (world > 1): ONE global arrival stream of n_requests * world requests is drawn and
+    routed by key owner (dist.key_owner: key % world), as an upstream router would; rank `rank` gets
+    the requests of the keys it owns, in global arrival order -- so the per-key sequences are the
+    global ones and the union over ranks is exactly the single-process workload.  return_index adds
+    the positions of the rank's requests in the global stream."""
     rng = np.random.default_rng(seed)
     max_amount = rng.integers(50, 5001, size=n_keys).astype(np.int64)
     valid = np.choose(rng.integers(0, 3, size=n_keys), [0, 10**9, 60 * 10**9]).astype(np.int64)
     p = np.arange(1, n_keys + 1, dtype=np.float64) ** -1.05
-    keys = rng.choice(n_keys, size=n_requests, p=p / p.sum()).astype(np.uint32)
-    amounts = rng.integers(1, 21, size=n_requests).astype(np.int64)
-    r = rng.random(n_requests)
+    total = n_requests * world
+    keys = rng.choice(n_keys, size=total, p=p / p.sum()).astype(np.uint32)
+    amounts = rng.integers(1, 21, size=total).astype(np.int64)
+    r = rng.random(total)
     amounts = np.where(r < p_free, -amounts, amounts)
     amounts = np.where(r > 1 - p_zero, 0, amounts)
-    be = (rng.random(n_requests) < p_be).astype(np.uint8)
-    return max_amount, valid, keys, amounts, be
+    be = (rng.random(total) < p_be).astype(np.uint8)
+    idx = np.arange(total)
+    if world > 1:
+        idx = np.nonzero(keys % world == rank)[0]
+        keys, amounts, be = keys[idx], amounts[idx], be[idx]
+    out = (max_amount, valid, keys, amounts, be)
+    return out + (idx,) if return_index else out

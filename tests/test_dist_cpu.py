@@ -53,6 +53,83 @@ def _rank_main(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
+def _step_rank_main(rank, world, port, out_path, steps):
+    """bench.py's step structure with engine-free kernels: each step accumulates into the step views
+    of StepCounters (hits[R] ++ quota_delta[K]) and ends with the step's single all-reduce."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import memquota as M
+    from istio_amd import dist as D
+    from istio_amd import workloads as W
+    R, K = 37, 16
+    calls = []
+    orig = D.reduce_counters
+
+    def counting_reduce(t):
+        calls.append(t.numel())
+        return orig(t)
+    D.reduce_counters = counting_reduce
+    ctr = D.StepCounters([R, K])
+    # memquota requests routed by key owner: the rank replays its keys' sequences with the oracle
+    mx, vd, keys, amounts, be, idx = W.quota_workload(n_keys=K, n_requests=400, seed=9, rank=rank, world=world,
+                                                      return_index=True)
+    assert np.all(D.key_owner(keys, world) == rank)
+    mq = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
+    granted_all = []
+    for s in range(steps):
+        ctr.begin_step()
+        hits, delta = ctr.views()
+        hits += torch.arange(R, dtype=torch.int64) * (rank + 1) + s  # a "kernel" accumulating into the step
+        granted = [mq.handle(int(k), int(a), bool(b), 10**18 + s * 10**8) for k, a, b in zip(keys, amounts, be)]
+        for k, g in zip(keys, granted):
+            delta[int(k)] += g
+        granted_all.append(granted)
+        ctr.end_step()
+    h, d = ctr.totals()
+    if rank == 0:
+        np.save(out_path, np.concatenate([h.numpy(), d.numpy(), [len(calls)]]))
+    np.save(out_path + ".r%d.npy" % rank, np.concatenate([idx, np.array(granted_all).reshape(-1)]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_step_counters_and_quota_owners(tmp_path):
+    """bench.py's step at world_size 2: per-step buffers reduced once per step (totals are exact after
+    several steps -- no re-adding of earlier totals), and memquota requests routed to their key's
+    owner rank reproduce the single-process sequential HandleQuota exactly."""
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import memquota as M
+    from istio_amd import workloads as W
+    out = str(tmp_path / "ctr.npy")
+    steps, world, R, K = 3, 2, 37, 16
+    mp.start_processes(_step_rank_main, args=(world, _free_port(), out, steps), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    want_hits = sum(np.arange(R) * (r + 1) + s for r in range(world) for s in range(steps))
+    assert np.array_equal(got[:R], want_hits)
+    assert got[-1] == steps  # one collective per step
+    # single process: the whole arrival stream (n_requests * world requests, same draw), sequentially
+    mx, vd, keys, amounts, be = W.quota_workload(n_keys=K, n_requests=400 * world, seed=9)
+    mq = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
+    want_delta = np.zeros(K, dtype=np.int64)
+    want_granted = np.zeros((steps, len(keys)), dtype=np.int64)
+    for s in range(steps):
+        for i, (k, a, b) in enumerate(zip(keys, amounts, be)):
+            g = mq.handle(int(k), int(a), bool(b), 10**18 + s * 10**8)
+            want_granted[s, i] = g
+            want_delta[int(k)] += g
+    assert np.array_equal(got[R:R + K], want_delta)
+    for r in range(world):
+        v = np.load(out + ".r%d.npy" % r)
+        n = (len(v)) // (steps + 1)
+        idx, granted = v[:n], v[n:].reshape(steps, n)
+        assert np.array_equal(granted, want_granted[:, idx])
+
+
 def test_two_rank_gloo_hit_counters(tmp_path):
     import torch.multiprocessing as mp
     sys.path.insert(0, os.path.join(ROOT, "oracle"))

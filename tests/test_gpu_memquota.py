@@ -49,3 +49,31 @@ def test_random_batches_parity(eng):
         assert bad.size == 0, (b, bad[:5], got[bad[:5]], want[bad[:5]])
         now += [50_000_000, 400_000_000, 3 * 10**9, 0, 61 * 10**9, 10**8][b]
     assert (want == 0).any() and (want > 0).any()
+
+
+def test_device_out_of_range_keys_granted_zero(eng):
+    """Device key ids >= n_keys (no host range check on the device path): granted 0, no state touched,
+    the in-range requests unchanged -- including ids whose low bits alias a valid key."""
+    import torch
+    K = 100
+    mx, vd, keys, amounts, be = W.quota_workload(n_keys=K, n_requests=5000, seed=53)
+    bad = np.zeros(len(keys), dtype=bool)
+    bad[::7] = True
+    keys_dev = keys.copy()
+    keys_dev[bad] = np.where(np.arange(bad.sum()) % 2, K + 28, 0xFFFFFFF0)  # 128 aliases key 0 at 7 bits
+    q = eng.quota_create(mx, vd)
+    dk = torch.from_numpy(keys_dev.view(np.int32).copy()).cuda()
+    da = torch.from_numpy(amounts.copy()).cuda()
+    db = torch.from_numpy(be.copy()).cuda()
+    dg = torch.full((len(keys),), 99, dtype=torch.int64, device="cuda")
+    delta = torch.zeros(K, dtype=torch.int64, device="cuda")
+    q.alloc_device(len(keys), dk.data_ptr(), da.data_ptr(), db.data_ptr(), BASE_NS, 0, dg.data_ptr(), delta.data_ptr())
+    torch.cuda.synchronize()
+    got = dg.cpu().numpy()
+    ref = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
+    want = np.array([0 if b else ref.handle(int(k), int(a), bool(e), BASE_NS)
+                     for k, a, e, b in zip(keys, amounts, be, bad)])
+    assert np.array_equal(got, want)
+    want_delta = np.zeros(K, dtype=np.int64)
+    np.add.at(want_delta, keys[~bad].astype(np.int64), want[~bad])
+    assert np.array_equal(delta.cpu().numpy(), want_delta)
