@@ -572,7 +572,8 @@ int mxp_engine::pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H)
             const uint8_t* bk = b->kinds[src[c]];
             const uint64_t* bv = b->values[src[c]];
             for (uint64_t r = r0; r < r1; r++) {
-                if (bk[r] == MXP_STRING) mark(bv[r], 1);
+                // (OTHER values are interned too: their text is the value of a conversion error)
+                if (bk[r] == MXP_STRING || bk[r] == MXP_OTHER) mark(bv[r], 1);
                 else if (bk[r] == MXP_BYTES) mark(bv[r], 2);
             }
         }
@@ -759,10 +760,9 @@ int mxp_engine::pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H)
                 const uint8_t k = bk[r];
                 uint64_t v = bv[r];
                 switch (k) {
-                case MXP_STRING: v = sid[v]; break;
+                case MXP_STRING: case MXP_OTHER: v = sid[v]; break;
                 case MXP_BYTES: v = MXP_BYTES_ID(bcan[v], braw[v]); break;
                 case MXP_TIMESTAMP: v = tid[v]; break;
-                case MXP_OTHER: v = 0; break;
                 default: break;
                 }
                 ok[r] = k;
@@ -946,7 +946,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
 }
 
 int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
-                       bool log, unsigned long long* d_hits, uint64_t* stats) {
+                       bool log, unsigned long long* d_hits, uint64_t* stats, uint32_t q_lo, uint32_t q_hi) {
     mxp_kargs A;
     fill_args(&A, db);
     A.hits = d_vals ? nullptr : d_hits;
@@ -955,7 +955,16 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     A.out_err = d_err;
     A.out_vals = d_vals;
     hipError_t e;
-    if (log) {
+    if (log && win_log_cap) {  // a recomputed window (recompute_errors): its own log, room for every pair
+        if (d_winlog.n < (size_t)win_log_cap * sizeof(mxp_err_rec) &&
+            (e = d_winlog.alloc((size_t)win_log_cap * sizeof(mxp_err_rec))) != hipSuccess)
+            return hipfail(e, "window errlog");
+        if (!d_wincount.p && (e = d_wincount.alloc(16)) != hipSuccess) return hipfail(e, "window errcount");
+        if ((e = hipMemsetAsync(d_wincount.p, 0, 16, s)) != hipSuccess) return hipfail(e, "memset errcount");
+        A.errlog = d_winlog.as<mxp_err_rec>();
+        A.errcount = d_wincount.as<uint32_t>();
+        A.errcap = win_log_cap;
+    } else if (log) {
         if (!d_errlog.p) {
             if ((e = d_errlog.alloc((size_t)errcap * sizeof(mxp_err_rec))) != hipSuccess) return hipfail(e, "errlog");
             if ((e = d_errcount.alloc(16)) != hipSuccess) return hipfail(e, "errcount");
@@ -990,11 +999,17 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     // words the fill, guard and VM kernels wrote) runs on the side stream while chunk c + 1's fill
     // streams its stores -- the fill is HBM-write bound, the index kernel latency bound, so they share
     // the chip; only the last chunk's index pass is left exposed.
+    // a request window (error recomputation) or the whole batch, possibly in pipelined chunks
+    const bool window = q_lo != 0 || q_hi < A.n;
+    const uint32_t lo = window ? q_lo : 0u, hi = window ? std::min(q_hi, A.n) : A.n;
+    if (lo >= hi) return MXP_OK;
+    const uint32_t span = hi - lo;
     uint32_t nchunk = 1;
-    if (use_index && chunks_max > 1 && A.n >= 2 * chunk_min) nchunk = std::min<uint32_t>(chunks_max, A.n / chunk_min);
+    if (!window && use_index && chunks_max > 1 && span >= 2 * chunk_min)
+        nchunk = std::min<uint32_t>(chunks_max, span / chunk_min);
     // chunks start at multiples of 1024 requests (the fill kernel's 16-byte rows)
-    const uint32_t step = nchunk > 1 ? (A.n / nchunk + 1023u) / 1024u * 1024u : A.n;
-    nchunk = (A.n + step - 1) / step;
+    const uint32_t step = nchunk > 1 ? (span / nchunk + 1023u) / 1024u * 1024u : span;
+    nchunk = (span + step - 1) / step;
     if (nchunk > 1 && !side) {
         if ((e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking)) != hipSuccess) {
             side = nullptr;
@@ -1011,8 +1026,8 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         A.dense_cm = d_dense_cm.as<uint64_t>();
     }
     for (uint32_t c = 0; c < nchunk; c++) {
-        A.q0 = c * step;
-        A.q1 = std::min(A.n, (c + 1) * step);
+        A.q0 = lo + c * step;
+        A.q1 = std::min(hi, lo + (c + 1) * step);
         const uint32_t cx = (A.q1 - A.q0 + 63) / 64;
         if (guards_on && n_fills && (e = mxp_launch_fill(&A, n_fills, s)) != hipSuccess) return hipfail(e, "launch fill");
         for (const Part& P : parts) {
@@ -1046,12 +1061,60 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     return MXP_OK;
 }
 
-std::string mxp_engine::format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r) const {
+// %v of a packed (interned) column value, for error texts whose host batch is gone (errors
+// recomputed on demand, mxp_engine::recompute_errors): strings, byte strings and timestamps through
+// the interning tables, string maps through the device CSR
+std::string mxp_engine::packed_value_text(const mxp_dbatch* db, uint32_t kind, uint64_t v) const {
+    switch (kind) {
+    case MXP_STRING: case MXP_OTHER: return string_of(db, v);
+    case MXP_INT64: return std::to_string((int64_t)v);
+    case MXP_BOOL: return v ? "true" : "false";
+    case MXP_DOUBLE: {
+        double d;
+        memcpy(&d, &v, 8);
+        return mxp::go_format_float(d);
+    }
+    case MXP_DURATION: return mxp::go_format_duration((int64_t)v);
+    case MXP_TIMESTAMP: {
+        TimeKey t{0, 0};
+        if (v < gtimes.size()) t = gtimes[v];
+        else if (db && v - gtimes.size() < db->overlay_times.size()) t = db->overlay_times[v - gtimes.size()];
+        return mxp::go_format_time_utc(t.s, t.ns);
+    }
+    case MXP_BYTES: {
+        const uint64_t raw = MXP_BYTES_RAW(v);
+        std::string c;
+        if (raw < gbytes.size()) c = gbytes[raw];
+        else if (db && raw - gbytes.size() < db->overlay_bytes.size()) c = std::string(db->overlay_bytes[raw - gbytes.size()]);
+        return mxp::go_format_bytes((const uint8_t*)c.data(), c.size());
+    }
+    case MXP_STRING_MAP: {
+        uint32_t mo[2] = {0, 0};
+        std::string out = "map[";
+        if (!db || hipMemcpy(mo, db->map_off.as<uint32_t>() + v, 8, hipMemcpyDeviceToHost) != hipSuccess) return out + "]";
+        std::vector<uint32_t> k(mo[1] - mo[0]), w(mo[1] - mo[0]);
+        if (!k.empty() &&
+            (hipMemcpy(k.data(), db->map_keys.as<uint32_t>() + mo[0], k.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+             hipMemcpy(w.data(), db->map_vals.as<uint32_t>() + mo[0], w.size() * 4, hipMemcpyDeviceToHost) != hipSuccess))
+            return out + "]";
+        for (size_t e = 0; e < k.size(); e++) out += (e ? " " : "") + string_of(db, k[e]) + ":" + string_of(db, w[e]);
+        return out + "]";
+    }
+    default: return "?";
+    }
+}
+
+std::string mxp_engine::format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r,
+                                     const ErrWindow* win) const {
     switch (r.code) {
     case ERR_LOOKUP: return "lookup failed: '" + string_of(db, r.aux) + "'";
     case ERR_CONV_S: case ERR_CONV_B: case ERR_CONV_I: case ERR_CONV_D: {
         static const char* what[] = {"string", "bool", "integer or duration", "double"};
         std::string val = "?";
+        if (!b && win && r.aux < win->ncol && r.req >= win->q0 && r.req < win->q1) {
+            const size_t at = (size_t)r.aux * (win->q1 - win->q0) + (r.req - win->q0);
+            val = packed_value_text(db, win->kinds[at], win->vals[at]);
+        }
         if (b && r.aux < cols.size()) {
             for (uint32_t c = 0; c < b->n_columns; c++) {
                 if (cols[r.aux] != b->column_names[c]) continue;
@@ -1381,6 +1444,8 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "eval sync");
     last_error_count = cnt;
     last_errors.clear();
+    err_windows.clear();
+    errors_complete = cnt <= errcap;
     uint32_t kept = std::min(cnt, errcap);
     if (kept) {
         std::vector<mxp_err_rec> recs(kept);
@@ -1389,6 +1454,72 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
         for (auto& r : recs) last_errors[((uint64_t)r.req << 32) | r.rule] = {r.code, format_error(batch, db.get(), r)};
     }
     last_db = std::move(db);
+    return MXP_OK;
+}
+
+// Error records past the log's capacity: re-evaluate the window of kErrWindow requests holding
+// `request` (same kernels, no bitmap outputs, a fresh log) and add its records to last_errors.
+int mxp_engine::recompute_errors(uint32_t request) {
+    if (!last_db || request >= last_db->n) return MXP_OK;
+    const uint32_t w = request / kErrWindow;
+    if (!err_windows.insert(w).second) return MXP_OK;
+    hipError_t e;
+    if ((e = hipSetDevice(device)) != hipSuccess) return hipfail(e, "hipSetDevice");
+    const uint32_t q0 = w * kErrWindow, q1 = std::min(last_db->n, q0 + kErrWindow);
+    // (rules fail at most once per request and rule; aliases of an indexed rule are distinct rules)
+    win_log_cap = (q1 - q0) * (uint32_t)std::max<size_t>(rules.size(), 1);
+    int rc = launch(last_db.get(), stream, nullptr, nullptr, nullptr, true, nullptr, nullptr, q0, q1);
+    const uint32_t cap = win_log_cap;
+    win_log_cap = 0;
+    if (rc) return rc;
+    uint32_t cnt = 0;
+    if ((e = hipMemcpyAsync(&cnt, d_wincount.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        return hipfail(e, "download errcount");
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "recompute sync");
+    const uint32_t kept = std::min(cnt, cap);
+    ErrWindow win;
+    win.q0 = q0;
+    win.q1 = q1;
+    win.ncol = (uint32_t)(cols.size() + vcols.size());
+    std::vector<mxp_err_rec> recs(kept);
+    if (kept && (e = hipMemcpy(recs.data(), d_winlog.p, kept * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
+        return hipfail(e, "download errlog");
+    bool conv = false;
+    for (auto& r : recs) conv |= r.code >= ERR_CONV_S && r.code <= ERR_CONV_D;
+    if (conv) {  // the window's columns, for the values conversion errors print
+        const size_t wn = q1 - q0;
+        win.kinds.resize(win.ncol * wn);
+        win.vals.resize(win.ncol * wn);
+        for (uint32_t c = 0; c < win.ncol; c++) {
+            if ((e = hipMemcpy(win.kinds.data() + c * wn, last_db->kinds.as<uint8_t>() + (size_t)c * last_db->n + q0, wn,
+                               hipMemcpyDeviceToHost)) != hipSuccess ||
+                (e = hipMemcpy(win.vals.data() + c * wn, last_db->vals.as<uint64_t>() + (size_t)c * last_db->n + q0,
+                               wn * 8, hipMemcpyDeviceToHost)) != hipSuccess)
+                return hipfail(e, "download window columns");
+        }
+    }
+    for (auto& r : recs) {
+        const uint64_t key = ((uint64_t)r.req << 32) | r.rule;
+        if (!last_errors.count(key)) last_errors[key] = {r.code, format_error(nullptr, last_db.get(), r, &win)};
+    }
+    return MXP_OK;
+}
+
+int mxp_engine::pair_error_text(uint32_t request, uint32_t rule, std::string* text, uint32_t* code) {
+    const uint64_t key = ((uint64_t)request << 32) | rule;
+    auto it = last_errors.find(key);
+    if (it == last_errors.end() && !errors_complete) {
+        int rc = recompute_errors(request);
+        if (rc) return rc;
+        it = last_errors.find(key);
+    }
+    if (it == last_errors.end()) {
+        text->clear();
+        *code = ERR_NONE;
+    } else {
+        *text = it->second.second;
+        *code = it->second.first;
+    }
     return MXP_OK;
 }
 
@@ -1427,8 +1558,10 @@ static int eval_common(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* ma
                 uint32_t bit = 1u << (r % 32);
                 uint8_t c = (hm[w] & bit) ? PC_TRUE : PC_FALSE;
                 if (he[w] & bit) {
-                    auto it = eng->last_errors.find(((uint64_t)q << 32) | r);
-                    c = (it != eng->last_errors.end() && it->second.first >= 32) ? PC_PANIC : PC_ERROR;
+                    std::string t;
+                    uint32_t code = ERR_NONE;
+                    if ((rc = eng->pair_error_text(q, r, &t, &code))) return rc;
+                    c = code >= 32 ? PC_PANIC : PC_ERROR;
                 }
                 codes[(size_t)q * R + r] = c;
             }
@@ -1446,10 +1579,12 @@ int mxp_eval_values(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* value
 
 int mxp_pair_error(mxp_engine* eng, uint32_t request, uint32_t rule, char* buf, uint32_t cap) {
     if (!eng) return MXP_ERR_ARG;
-    auto it = eng->last_errors.find(((uint64_t)request << 32) | rule);
-    if (it == eng->last_errors.end()) return put_text("", buf, cap);
-    int rc = put_text(it->second.second, buf, cap);
-    return rc ? rc : (it->second.first >= 32 ? 1 : 0);
+    std::string t;
+    uint32_t code = ERR_NONE;
+    int rc = eng->pair_error_text(request, rule, &t, &code);
+    if (rc) return rc;
+    rc = put_text(t, buf, cap);
+    return rc ? rc : (code >= 32 ? 1 : 0);
 }
 
 uint64_t mxp_error_count(mxp_engine* eng) { return eng ? eng->last_error_count : 0; }

@@ -327,6 +327,10 @@ struct mxp_engine : public mxp::LowerTables {
         vcol_ids.clear();
         rules.clear();
         have_rules = false;
+        last_db.reset();  // the last batch's ids and error records belong to the old rule set
+        last_errors.clear();
+        err_windows.clear();
+        errors_complete = true;
         need_ipof = need_tsof = need_strings = need_maps = need_rxof = false;
         rx_ids.clear();
         rx_set = mxp::DfaSetHost();
@@ -365,8 +369,10 @@ struct mxp_engine : public mxp::LowerTables {
     int pack(const mxp_bag_batch* b, mxp_dbatch* db);
     int wire_decode(const mxp_wire_batch* w, const char* const* names, uint32_t n_names, mxp_wire** out);  // wire.cpp
     void fill_args(mxp_kargs* A, const mxp_dbatch* db) const;
+    // requests [q_lo, q_hi) of the batch (default: all); q_lo a multiple of 4
     int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
-               unsigned long long* d_hits = nullptr, uint64_t* d_stats = nullptr);
+               unsigned long long* d_hits = nullptr, uint64_t* d_stats = nullptr, uint32_t q_lo = 0,
+               uint32_t q_hi = 0xFFFFFFFFu);
     // fused hit counters: true pairs the guard-index kernel set in a recent evaluation (pinned host
     // copy, read one launch late) decide between counting in the kernels and the streaming hits kernel
     DevBuf d_stats;
@@ -375,7 +381,26 @@ struct mxp_engine : public mxp::LowerTables {
     hipEvent_t stats_ev = nullptr;  // recorded after each stats download
     bool stats_pending = false;     // a download not yet seen complete
     double stats_tp = 0.0;          // true pairs per request of the last completed download
-    std::string format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r) const;
+    // columns of a window of requests [q0, q1) of the last batch, downloaded for error texts
+    struct ErrWindow {
+        uint32_t q0 = 0, q1 = 0, ncol = 0;
+        std::vector<uint8_t> kinds;   // [ncol][q1 - q0]
+        std::vector<uint64_t> vals;
+    };
+    std::string format_error(const mxp_bag_batch* b, const mxp_dbatch* db, const mxp_err_rec& r,
+                             const ErrWindow* win = nullptr) const;
+    std::string packed_value_text(const mxp_dbatch* db, uint32_t kind, uint64_t v) const;
+    // Error records are a cache of the error bits: a pair whose bit is set but whose record is
+    // missing (log capacity exceeded, MXP_ERRCAP) is recomputed on demand by re-evaluating its
+    // window of requests of the last batch with a fresh log (recompute_errors).
+    bool errors_complete = true;
+    std::set<uint32_t> err_windows;  // windows of the last batch already recomputed
+    static constexpr uint32_t kErrWindow = 64;
+    uint32_t win_log_cap = 0;           // != 0 while launch() runs a recomputed window
+    DevBuf d_winlog, d_wincount;        // that window's error log
+    int recompute_errors(uint32_t request);
+    // the text of an error pair of the last batch ("" when it did not fail); -1 on a device failure
+    int pair_error_text(uint32_t request, uint32_t rule, std::string* text, uint32_t* code);
     std::string string_of(const mxp_dbatch* db, uint64_t sid) const {
         if (!db) db = last_db.get();
         if (sid < gstrs.size()) return gstrs[sid];

@@ -1196,7 +1196,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_inject_kernel(mxp_kargs A)
                 if (lane == 0 && c) atomicAdd(A.hits + w * 32u + (ent & 31u), (unsigned long long)c);
             }
         }
-        if (bits) atomicOr(A.out_match + (uint64_t)w * A.n + req, bits);
+        if (bits && A.out_match) atomicOr(A.out_match + (uint64_t)w * A.n + req, bits);
         t += (uint32_t)__builtin_popcount(bits);
     }
     if (A.stats) {

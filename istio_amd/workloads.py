@@ -507,14 +507,32 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512):
         else:
             rules.append('"^v(1|%d)[0-9]?$".matches(request.headers["%s"])' % (int(rng.integers(2, 9)),
                                                                              _C4_HEADERS[int(rng.integers(0, 5))]))
-    bags = []
-    for _ in range(n_requests):
-        b = {"request.path": path(int(rng.integers(1, 7))),
-             "destination.service": "svc.default.svc.cluster.local",
-             "request.headers": {_C4_HEADERS[int(k)]: vals[int(rng.integers(0, 16))]
-                                 for k in rng.choice(5, size=3, replace=False)}}
-        bags.append(b)
-    return C4_MANIFEST, rules, BagBatch.from_bags(bags, names=list(C4_MANIFEST))
+    # requests, drawn column-wise (1M requests in seconds): path of depth 1..6, the service, 3 of the
+    # 5 headers (distinct names, in draw order) with values v0..v15
+    n = n_requests
+    depth = rng.integers(1, 7, size=n)
+    w = rng.integers(0, vocab, size=(n, 6))
+    hdr = np.argsort(rng.random((n, 5)), axis=1)[:, :3]
+    hval = rng.integers(0, 16, size=(n, 3))
+    strings = [h.encode() for h in _C4_HEADERS] + [v.encode() for v in vals] + [b"svc.default.svc.cluster.local"]
+    svc_sid = len(strings) - 1
+    paths = {}
+    path_vals = np.empty(n, dtype=np.uint64)
+    wl = w.tolist()
+    for q, d in enumerate(depth.tolist()):
+        p = "/" + "/".join(words[i] for i in wl[q][:d])
+        sid = paths.get(p)
+        if sid is None:
+            sid = paths[p] = len(strings)
+            strings.append(p.encode())
+        path_vals[q] = sid
+    moff = np.arange(0, 3 * n + 1, 3, dtype=np.uint64)
+    mkeys = hdr.reshape(-1).astype(np.uint32)                    # header name sids 0..4
+    mvals = (5 + hval).reshape(-1).astype(np.uint32)             # value sids 5..20
+    cols = {"request.path": (np.full(n, STRING, dtype=np.uint8), path_vals),
+            "request.headers": (np.full(n, STRING_MAP, dtype=np.uint8), np.arange(n, dtype=np.uint64)),
+            "destination.service": (np.full(n, STRING, dtype=np.uint8), np.full(n, svc_sid, dtype=np.uint64))}
+    return C4_MANIFEST, rules, BagBatch.from_columns(n, cols, strings, maps=(moff, mkeys, mvals))
 
 
 # ----------------------------------------------------------------------------------- memquota (C5)

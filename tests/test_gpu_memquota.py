@@ -75,5 +75,5 @@ def test_device_out_of_range_keys_granted_zero(eng):
                      for k, a, e, b in zip(keys, amounts, be, bad)])
     assert np.array_equal(got, want)
     want_delta = np.zeros(K, dtype=np.int64)
-    np.add.at(want_delta, keys[~bad].astype(np.int64), want[~bad])
+    np.add.at(want_delta, keys[~bad].astype(np.int64), (np.sign(amounts) * want)[~bad])  # allocs - frees
     assert np.array_equal(delta.cpu().numpy(), want_delta)
