@@ -316,7 +316,9 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out);
  * map[key] virtual columns), out[6] of the indexed rules those served by a composite (A == K1,
  * B startsWith K2) index, out[7] indexed rules that duplicate another rule's program (evaluated once,
  * results fanned out), out[8] of those canonical rules the "dense" ones whose true pairs are
- * injected once per bitmap word instead of per alias.  Returns the number of values written (<= cap). */
+ * injected once per bitmap word instead of per alias, out[9] value-class candidate columns (columns
+ * whose rules depend on that column's value alone; a batch with few distinct values in such a column
+ * evaluates its rules once per distinct value).  Returns the number of values written (<= cap). */
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap);
 uint32_t mxp_dbatch_requests(const mxp_dbatch* db);
 

@@ -11,8 +11,11 @@ typedef struct mxp_dfa_hdr {
     uint32_t ascii;     // first ASCII class entry (128 per DFA, index into mxp_dfa_set.ascii)
     uint32_t hi;        // first non-ASCII range (index into hilo / hicls)
     uint32_t hi_n;
-    uint32_t pad[2];
+    uint32_t skip;      // subject bytes already consumed into `start` (a rule's literal prefix, verified
+                        // by the prefix index); MXP_DFA_DECIDED: the prefix alone decides a match
+    uint32_t pad;
 } mxp_dfa_hdr;
+#define MXP_DFA_DECIDED 0xFFFFFFFFu
 
 typedef struct mxp_dfa_set {
     const mxp_dfa_hdr* hdr;
@@ -41,7 +44,8 @@ __device__ __forceinline__ bool mxp_dfa_run(const mxp_dfa_set& S, uint32_t dfa, 
     const uint32_t* T = S.trans + H.trans;
     const uint16_t* asc = S.ascii + H.ascii;
     uint32_t st = H.start;
-    uint32_t i = 0;
+    uint32_t i = H.skip;
+    if (i == MXP_DFA_DECIDED) return true;
     while (i < n) {
         const uint64_t w = mxp_ld8(s + i);  // bytes i .. i+7 (only those < n are used)
         const uint32_t c0 = (uint32_t)(w & 0xFF);

@@ -16,10 +16,13 @@
 int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     reset_tables();
     ref_comp.clear();
+    plans.clear();
     views_n[0] = ~(size_t)0;  // string-view indexes rebuilt at the next pack
     rules.resize(n);
-    std::vector<mxp_vm_ins> all;
-    std::vector<uint32_t> off(n + 1, 0);
+    std::vector<mxp_vm_ins>& all = prog_h;
+    std::vector<uint32_t>& off = off_h;
+    all.clear();
+    off.assign(n + 1, 0);
     for (uint32_t i = 0; i < n; i++) {
         Rule& R = rules[i];
         mxp::CompiledRule cr;
@@ -66,7 +69,13 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         for (auto& ins : R.low.code)
             if ((ins.op & 0x7F) == VM_VCOL) ins.x += C;
     // leading-atom guards (evaluated for a whole 32-rule group at once by the kernel)
-    std::vector<mxp_guard> guards(n);
+    std::vector<mxp_guard>& guards = guards_h;
+    guards.assign(n, mxp_guard{});
+    struct RxPrefixed {
+        uint32_t rule, dfa;
+        std::string prefix;
+    };
+    std::vector<RxPrefixed> rx_prefixed;  // regexp rules guarded by their literal prefix
     for (uint32_t i = 0; i < n; i++) {
         std::vector<mxp_vm_ins> code(all.begin() + off[i], all.begin() + off[i + 1]);
         guards[i] = mxp::extract_guard(code);
@@ -98,15 +107,18 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
             g.mode = GM_AND | GT_PREFIX;  // continuation pc 0: the whole program
             g.klo = intern_string(prefix);
             guards[i] = g;
+            rx_prefixed.push_back({i, x.x, prefix});
         }
     }
 
     // continuation templates (vmopt.h hoist_continuation): rules whose continuations are identical
     // up to constants share one program; template code is appended after the rules' programs
     std::map<std::string, uint32_t> tmpl_ids;
-    std::vector<mxp_tmpl> tmpls;
+    std::vector<mxp_tmpl>& tmpls = tmpls_h;
+    tmpls.clear();
     std::vector<mxp_vm_ins> tcode;
-    std::vector<uint32_t> rule_tmpl(n, MXP_VM_DONE);
+    std::vector<uint32_t>& rule_tmpl = rule_tmpl_h;
+    rule_tmpl.assign(n, MXP_VM_DONE);
     std::vector<uint64_t> rconst((size_t)n * MXP_VM_MAXREG, 0);
     const uint32_t prog_end = (uint32_t)all.size();
     n_templated = 0;
@@ -139,8 +151,173 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         for (size_t j = 0; j < h.consts.size(); j++) rconst[(size_t)i * MXP_VM_MAXREG + j] = h.consts[j];
         n_templated++;
     }
-    n_tmpls = (uint32_t)tmpls.size();
     all.insert(all.end(), tcode.begin(), tcode.end());
+
+    // A prefix-guarded regexp rule runs (through its template, from the guard index) only for
+    // subjects that start with its literal prefix: its template constant names a derived DFA that
+    // starts in the state the prefix leads to, `skip` bytes in -- or that is decided by the prefix
+    // alone (`^/api[a-z]*`: the empty star already matches).  The rule's own program keeps the full
+    // DFA (Eval mode, referenced-attribute scopes, plans without the index).
+    for (const RxPrefixed& rp : rx_prefixed) {
+        if (rule_tmpl[rp.rule] == MXP_VM_DONE) continue;
+        const mxp_tmpl& t = tmpls[rule_tmpl[rp.rule]];
+        uint32_t creg = MXP_VM_DONE;
+        for (uint32_t pc = t.pc0; pc < t.len; pc++) {
+            const mxp_vm_ins& ti = all[t.off - t.pc0 + pc];
+            if ((ti.op & 0x7F) == VM_REGEXR) creg = ti.b;
+        }
+        if (creg == MXP_VM_DONE || creg < t.creg0 || creg >= t.creg0 + t.nconst) continue;
+        const mxp::Dfa& d = rx_dfas[rp.dfa];
+        uint32_t st = d.start;
+        for (size_t b = 0; b < rp.prefix.size() && st != mxp::kDfaAccept;) {
+            const uint8_t c = (uint8_t)rp.prefix[b];
+            uint32_t cls, w = 1;
+            if (c < 0x80) {
+                cls = d.ascii[c];
+            } else {  // a literal rune's UTF-8 bytes
+                uint32_t r = 0;
+                w = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : 2;
+                r = c & (0xFFu >> (w + 1));
+                for (uint32_t k = 1; k < w; k++) r = (r << 6) | ((uint8_t)rp.prefix[b + k] & 0x3Fu);
+                const size_t at = std::upper_bound(d.hi_lo.begin(), d.hi_lo.end(), r) - d.hi_lo.begin() - 1;
+                cls = d.hi_cls[at];
+            }
+            st = d.trans[(size_t)st * d.ncls + cls];
+            b += w;
+        }
+        if (st == mxp::kDfaReject) continue;
+        mxp_dfa_hdr h = rx_set.hdr[rp.dfa];
+        h.start = st == mxp::kDfaAccept ? 0u : st;
+        h.skip = st == mxp::kDfaAccept ? MXP_DFA_DECIDED : (uint32_t)rp.prefix.size();
+        rx_set.hdr.push_back(h);
+        rx_dfas.emplace_back();  // (keeps rx_dfas aligned with the device headers; never walked)
+        rconst[(size_t)rp.rule * MXP_VM_MAXREG + (creg - t.creg0)] = rx_set.hdr.size() - 1;
+    }
+
+    // value-class candidates: rules whose result is a function of ONE column's (kind, string value)
+    // alone, so a batch with few distinct values in that column evaluates them once per value
+    // (mxp_vt_eval_kernel) and broadcasts the words by class (vt_merge)
+    {
+        std::vector<uint32_t> vcol(n, MXP_VM_DONE);
+        std::map<uint32_t, uint32_t> count;
+        for (uint32_t i = 0; i < n; i++) {
+            if (rules[i].status != MXP_RULE_OK) continue;
+            uint32_t col = MXP_VM_DONE;
+            bool ok = true;
+            for (uint32_t p = off[i]; p < off[i + 1] && ok; p++) {
+                const mxp_vm_ins& ins = all[p];
+                uint32_t c = MXP_VM_DONE;
+                switch (ins.op & 0x7F) {
+                case VM_RES: case VM_TRES: ok = ins.y == W_S; c = ins.x; break;
+                case VM_VCOL: c = ins.x; break;
+                case VM_LOOKUP: case VM_LOOKUPK: case VM_REGEXD: ok = false; break;
+                default: break;
+                }
+                if (c != MXP_VM_DONE) {
+                    if (col == MXP_VM_DONE) col = c;
+                    else if (col != c) ok = false;
+                }
+            }
+            if (ok && col != MXP_VM_DONE) {
+                vcol[i] = col;
+                count[col]++;
+            }
+        }
+        std::vector<std::pair<uint32_t, uint32_t>> cand;  // (rules, column)
+        for (auto& kv : count)
+            if (kv.second >= kVtMinRules) cand.push_back({kv.second, kv.first});
+        std::sort(cand.begin(), cand.end(), [](auto& a, auto& b) { return a.first != b.first ? a.first > b.first : a.second < b.second; });
+        if (cand.size() > kVtCandMax) cand.resize(kVtCandMax);
+        vt_cand_col.clear();
+        vt_slot_of_rule.assign(n, 0xFF);
+        std::map<uint32_t, uint32_t> slot_of;
+        for (auto& c : cand) {
+            slot_of[c.second] = (uint32_t)vt_cand_col.size();
+            vt_cand_col.push_back(c.second);
+        }
+        for (uint32_t i = 0; i < n; i++)
+            if (vcol[i] != MXP_VM_DONE && slot_of.count(vcol[i])) vt_slot_of_rule[i] = (uint8_t)slot_of[vcol[i]];
+    }
+
+    vcol_key_sid.resize(vcols.size());
+    for (size_t j = 0; j < vcols.size(); j++) vcol_key_sid[j] = intern_string(vcols[j].second);
+    refs_exact = true;
+    for (auto& R : rules) refs_exact &= R.status != MXP_RULE_UNSUPPORTED;
+    // referenced attributes (mxp_eval_refs): the guard of every guarded rule reads its column for
+    // every request
+    ref_guard.assign(n, MXP_VM_DONE);
+    for (uint32_t i = 0; i < n; i++)
+        if ((guards[i].mode & 0xFF) != GM_NONE) ref_guard[i] = guards[i].col & 0xFFFFFFu;
+
+    have_rules = false;
+    if (device >= 0) {
+        // upload the rule-level tables: programs (+ template code), constants, regexp DFAs, strings
+        hipError_t e;
+        if ((e = hipSetDevice(device)) != hipSuccess) return hipfail(e, "hipSetDevice");
+        auto put = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
+            if ((e = d.alloc(bytes ? bytes : 16)) != hipSuccess) return hipfail(e, what);
+            if (bytes && (e = hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice)) != hipSuccess) return hipfail(e, what);
+            return MXP_OK;
+        };
+        int rc;
+        if ((rc = put(d_prog, all.data(), all.size() * sizeof(mxp_vm_ins), "upload prog"))) return rc;
+        if ((rc = put(d_rule_off, off.data(), off.size() * 4, "upload rule_off"))) return rc;
+        if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
+        if ((rc = put(d_rx_hdr, rx_set.hdr.data(), rx_set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
+        if ((rc = put(d_rx_trans, rx_set.trans.data(), rx_set.trans.size() * 4, "upload rx trans"))) return rc;
+        if ((rc = put(d_rx_ascii, rx_set.ascii.data(), rx_set.ascii.size() * 2, "upload rx ascii"))) return rc;
+        if ((rc = put(d_rx_hilo, rx_set.hilo.data(), rx_set.hilo.size() * 4, "upload rx hilo"))) return rc;
+        if ((rc = put(d_rx_hicls, rx_set.hicls.data(), rx_set.hicls.size() * 2, "upload rx hicls"))) return rc;
+    }
+    // plan 0 (no value classes) interns nothing new, so the string pool can go up after it
+    Plan* p0 = nullptr;
+    int rc = get_plan(0, &p0);
+    if (rc) return rc;
+    if (device >= 0) {
+        hipError_t e;
+        std::vector<uint64_t> soff;
+        std::string blob;
+        if (!string_pool(gstrs, &soff, &blob)) return fail(MXP_ERR_ARG, "rule-set string longer than 16 MiB");
+        if ((e = d_gstr_off.alloc(soff.size() * 8)) != hipSuccess) return hipfail(e, "hipMalloc gstr_off");
+        if ((e = d_gstr.alloc(blob.size())) != hipSuccess) return hipfail(e, "hipMalloc gstr");
+        if ((e = hipMemcpy(d_gstr_off.p, soff.data(), soff.size() * 8, hipMemcpyHostToDevice)) != hipSuccess)
+            return hipfail(e, "upload gstr_off");
+        if (!blob.empty() && (e = hipMemcpy(d_gstr.p, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess)
+            return hipfail(e, "upload gstr");
+    }
+    have_rules = true;
+    return MXP_OK;
+}
+
+int mxp_engine::get_plan(uint32_t mask, Plan** out) {
+    auto it = plans.find(mask);
+    if (it != plans.end()) {
+        *out = it->second.get();
+        return MXP_OK;
+    }
+    std::unique_ptr<Plan> P(new Plan());
+    P->mask = mask;
+    int rc = build_plan(*P);
+    if (rc) return rc;
+    *out = P.get();
+    plans.emplace(mask, std::move(P));
+    return MXP_OK;
+}
+
+// The kernels' view of the rule set for one set of value-class columns (Plan::mask): the rules the
+// value classes serve are left out of every table below -- groups, segments, guard indexes, fills,
+// aliases -- and come back as per-group merge entries (gvt) instead.
+int mxp_engine::build_plan(Plan& P) {
+    const uint32_t n = (uint32_t)rules.size();
+    const std::vector<mxp_vm_ins>& all = prog_h;
+    const std::vector<uint32_t>& off = off_h;
+    std::vector<mxp_guard> guards = guards_h;
+    std::vector<uint32_t> rule_tmpl = rule_tmpl_h;
+    std::vector<mxp_tmpl> tmpls = tmpls_h;
+    std::vector<uint8_t> excluded(n, 0);
+    for (uint32_t i = 0; i < n; i++)
+        excluded[i] = vt_slot_of_rule[i] != 0xFF && ((P.mask >> vt_slot_of_rule[i]) & 1u);
+    const bool base = P.mask == 0;  // plan 0 also fills the referenced-attribute tables
 
     // guard index.  Equality: GM_AND, non-negated, templated rules -- their continuing pairs are the
     // requests whose column value equals K.  Prefix: `col.startsWith(K)` alone (GM_ONLY: a posting IS
@@ -153,15 +330,17 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     std::map<std::pair<uint32_t, uint32_t>, std::map<std::pair<uint64_t, uint32_t>, std::vector<uint32_t>>> comp_of;
     std::vector<uint32_t> rule_tmpl2(n, MXP_VM_DONE);
     std::map<std::pair<uint32_t, uint32_t>, uint32_t> tmpl2_ids;  // (template, resume pc) -> template
-    n_indexed = 0;
-    n_composite = 0;
+    P.n_indexed = 0;
+    P.n_composite = 0;
     // duplicate predicates: indexed rules whose programs are identical (same code, same constants)
     // compute identical results, so only the first one (the canonical rule) enters the index; each
     // result the index kernel produces for it is fanned out to its aliases (kargs.alias_off / aliases)
     std::unordered_map<std::string, uint32_t> canon_of;
     std::vector<std::vector<uint32_t>> aliases_of(n);
-    n_alias = 0;
+    P.n_alias = 0;
+    if (base) ref_comp.clear();
     for (uint32_t i = 0; i < n; i++) {
+        if (excluded[i]) continue;
         mxp_guard& gd = guards[i];
         const uint32_t mode = gd.mode & 0xFF;
         const bool prefix = (gd.mode & GT_PREFIX) != 0, neg = (gd.mode >> 8) & 1;
@@ -180,14 +359,14 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         }
         if (mode == GM_ONLY) rule_tmpl[i] = MXP_TMPL_DIRECT;
         indexed[i] = 1;
-        n_indexed++;
+        P.n_indexed++;
         if (!(debug_flags & 64u)) {
             std::string key((const char*)&gd, sizeof gd);
             key.append((const char*)(all.data() + off[i]), (size_t)(off[i + 1] - off[i]) * sizeof(mxp_vm_ins));
             auto ins = canon_of.emplace(std::move(key), i);
             if (!ins.second) {
                 aliases_of[ins.first->second].push_back(i);
-                n_alias++;
+                P.n_alias++;
                 continue;
             }
         }
@@ -210,13 +389,13 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
                 rule_tmpl2[i] = it->second;
             }
             comp_of[{gd.col, sa.col}][{k1, sa.k2}].push_back(i);
-            ref_comp.push_back(RefComposite{gd.col & 0xFFFFFFu, sa.col, (uint32_t)k1, i});
-            n_composite++;
+            if (base) ref_comp.push_back(RefComposite{gd.col & 0xFFFFFFu, sa.col, (uint32_t)k1, i});
+            P.n_composite++;
             continue;
         }
         index_of[{gd.col, prefix}][k1].push_back(i);
     }
-    n_tmpls = (uint32_t)tmpls.size();
+    P.n_tmpls = (uint32_t)tmpls.size();
     std::vector<mxp_index> idx;
     std::vector<mxp_hent> hents;
     std::vector<uint32_t> postings, plens;
@@ -314,9 +493,9 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         plens.insert(plens.end(), lens.begin(), lens.end());
         idx.push_back(x);
     }
-    n_idx = (uint32_t)idx.size();
-    std::vector<uint32_t> alias_off(n_alias ? n + 1 : 0, 0), alias_list;
-    if (n_alias) {
+    P.n_idx = (uint32_t)idx.size();
+    std::vector<uint32_t> alias_off(P.n_alias ? n + 1 : 0, 0), alias_list;
+    if (P.n_alias) {
         for (uint32_t i = 0; i < n; i++) {
             alias_off[i] = (uint32_t)alias_list.size();
             alias_list.insert(alias_list.end(), aliases_of[i].begin(), aliases_of[i].end());
@@ -324,8 +503,45 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         alias_off[n] = (uint32_t)alias_list.size();
     }
 
-    // phase-1 group tables: mode masks, column segments, guard constants
+    // value-class merge entries: per group the (active slot, word position) pairs of the rules the
+    // value classes serve; per active slot its words (group, rule mask) for mxp_vt_eval_kernel
     const uint32_t W = (n + 31) / 32;
+    P.vt_cols.clear();
+    std::vector<uint32_t> act_of(vt_cand_col.size(), MXP_VM_DONE);
+    for (uint32_t s = 0; s < vt_cand_col.size(); s++)
+        if ((P.mask >> s) & 1u) {
+            act_of[s] = (uint32_t)P.vt_cols.size();
+            P.vt_cols.push_back(vt_cand_col[s]);
+        }
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>> words_of(P.vt_cols.size());  // (group, mask)
+    std::vector<uint32_t> gvt_off(W + 1, 0), gvt;
+    for (uint32_t g = 0; g < W; g++) {
+        gvt_off[g] = (uint32_t)gvt.size();
+        std::vector<uint32_t> mk(P.vt_cols.size(), 0);
+        for (uint32_t k = 0; k < 32 && g * 32 + k < n; k++)
+            if (excluded[g * 32 + k]) mk[act_of[vt_slot_of_rule[g * 32 + k]]] |= 1u << k;
+        for (uint32_t a = 0; a < P.vt_cols.size(); a++)
+            if (mk[a]) {
+                gvt.push_back((a << 24) | (uint32_t)words_of[a].size());
+                words_of[a].push_back({g, mk[a]});
+            }
+    }
+    gvt_off[W] = (uint32_t)gvt.size();
+    std::vector<uint32_t> vt_woff(P.vt_cols.size() + 1, 0), vt_words;  // pairs (group, mask)
+    P.vt_nw.clear();
+    for (uint32_t a = 0; a < P.vt_cols.size(); a++) {
+        vt_woff[a] = (uint32_t)vt_words.size() / 2;
+        P.vt_nw.push_back((uint32_t)words_of[a].size());
+        for (auto& w : words_of[a]) {
+            vt_words.push_back(w.first);
+            vt_words.push_back(w.second);
+        }
+    }
+    vt_woff[P.vt_cols.size()] = (uint32_t)vt_words.size() / 2;
+    P.vt_max_nw = 0;
+    for (uint32_t x : P.vt_nw) P.vt_max_nw = std::max(P.vt_max_nw, x);
+
+    // phase-1 group tables: mode masks, column segments, guard constants
     std::vector<mxp_group> groups(W);
     std::vector<mxp_seg> segs;
     std::vector<uint64_t> gk((size_t)W * 32, 0);
@@ -335,6 +551,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         std::vector<mxp_seg> seg_of;
         for (uint32_t k = 0; k < 32 && g * 32 + k < n; k++) {
             const uint32_t r = g * 32 + k, bit = 1u << k;
+            if (excluded[r]) continue;  // served by value classes (gvt)
             const mxp_guard& gd = guards[r];
             const uint32_t mode = gd.mode & 0xFF;
             G.all |= bit;
@@ -370,52 +587,72 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         const uint32_t andm = G.guarded & ~(G.only | G.orm);
         G.vm = ((G.all & ~G.guarded) | G.orm | (andm & ~G.indexed)) != 0;
     }
-    std::vector<uint32_t> glean, gvm, gall(W);
+    std::vector<uint32_t> glean, gvm, gall(W), fill_masks;
     std::vector<mxp_fill> fills;
-    n_gfill = 0;
+    P.n_gfill = 0;
     for (uint32_t g = 0; g < W; g++) {
         gall[g] = g;
         const mxp_group& G = groups[g];
-        // uniform indexed group: every rule indexed, one guard column, nothing compared in-wave
-        const bool uniform = !G.vm && G.all && G.indexed == G.all && G.guarded == G.all && G.nseg == 1 &&
-                             G.s_cmp == 0 && G.s_rules == G.all && !(debug_flags & 32u);
+        const bool has_vt = gvt_off[g + 1] > gvt_off[g];
+        // uniform indexed group: every rule indexed, one guard column, nothing compared in-wave --
+        // its words depend only on that column's kind (and the value classes' merge entries); a
+        // group the value classes serve entirely joins whatever chunk is open (its mask is 0)
+        const bool only_vt = G.all == 0 && has_vt;
+        const bool uniform = !G.vm && (only_vt || (G.all && G.indexed == G.all && G.guarded == G.all && G.nseg == 1 &&
+                                                   G.s_cmp == 0 && G.s_rules == G.all)) &&
+                             !(debug_flags & 32u);
         if (uniform) {
             mxp_fill* F = fills.empty() ? nullptr : &fills.back();
-            if (F && F->col == G.s_col && F->okset == G.s_okset && F->g0 + F->n == g && F->n < fill_chunk &&
-                F->last == F->all && G.all == F->all) {
+            const bool joins = F && F->g0 + F->n == g && F->n < fill_chunk &&
+                               (only_vt || (F->col == G.s_col && F->okset == G.s_okset) || F->okset == 0xFFFFu);
+            if (joins) {
+                if (!only_vt && F->okset == 0xFFFFu) {  // a chunk of value-class-only groups adopts a column
+                    F->col = G.s_col;
+                    F->okset = G.s_okset;
+                }
                 F->n++;
-            } else if (F && F->col == G.s_col && F->okset == G.s_okset && F->g0 + F->n == g && F->n < fill_chunk &&
-                       F->last == F->all) {
-                F->n++;
-                F->last = G.all;
             } else {
-                fills.push_back(mxp_fill{G.s_col, G.s_okset, g, 1, G.all, G.all, {0, 0}});
+                mxp_fill f{};
+                f.col = only_vt ? 0u : G.s_col;
+                f.okset = only_vt ? 0xFFFFu : G.s_okset;  // (every kind passes: no guard to type-check)
+                f.g0 = g;
+                f.n = 1;
+                f.moff = (uint32_t)fill_masks.size();
+                fills.push_back(f);
+                F = &fills.back();
             }
-            n_gfill++;
+            fill_masks.push_back(G.all);
+            F->vt |= has_vt ? 1u : 0u;
+            P.n_gfill++;
             continue;
         }
         (G.vm ? gvm : glean).push_back(g);
     }
-    n_fills = (uint32_t)fills.size();
-    n_glean = (uint32_t)glean.size();
+    // chunks with value-class merge entries go to mxp_vtfill_kernel
+    std::vector<mxp_fill> vtfills;
+    {
+        std::vector<mxp_fill> plain;
+        for (auto& f : fills) (f.vt ? vtfills : plain).push_back(f);
+        fills.swap(plain);
+    }
+    P.n_fills = (uint32_t)fills.size();
+    P.n_vtfills = (uint32_t)vtfills.size();
+    P.n_glean = (uint32_t)glean.size();
     // columns < MXP_CC the lean groups read: mxp_guard2_kernel loads them into LDS up front
-    lean_cc = 0;
+    P.lean_cc = 0;
     for (uint32_t g : glean) {
         const mxp_group& G = groups[g];
-        if (G.nseg && G.s_col < MXP_CC) lean_cc |= 1u << G.s_col;
+        if (G.nseg && G.s_col < MXP_CC) P.lean_cc |= 1u << G.s_col;
         for (uint32_t k = 0; k + 1 < G.nseg; k++)
-            if (segs[G.seg0 + k].col < MXP_CC) lean_cc |= 1u << segs[G.seg0 + k].col;
+            if (segs[G.seg0 + k].col < MXP_CC) P.lean_cc |= 1u << segs[G.seg0 + k].col;
     }
-    n_gvm = (uint32_t)gvm.size();
-    n_segs = (uint32_t)segs.size();
+    P.n_gvm = (uint32_t)gvm.size();
+    P.n_segs = (uint32_t)segs.size();
 
-    // referenced attributes (mxp_eval_refs): the guard of every guarded rule reads its column for
-    // every request; map keys of virtual columns get string ids of their own
-    ref_guard.assign(n, MXP_VM_DONE);
-    for (uint32_t i = 0; i < n; i++)
-        if ((guards[i].mode & 0xFF) != GM_NONE) ref_guard[i] = guards[i].col & 0xFFFFFFu;
     // dense canonical rules: indexed rules with many duplicates, true pairs injected per bitmap word
     // at the end of the index kernel instead of one atomic per alias (kernels.hip inject_dense)
+    std::vector<uint8_t> dense_of;
+    std::vector<uint32_t> inj;
     {
         std::vector<uint32_t> cand;
         // (direct postings -- `attr.startsWith(K)` alone -- stay with per-alias atomics: their true
@@ -433,7 +670,6 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
             by_word[cand[d] >> 5].push_back((cand[d] & 31u) | (d << 5));
             for (uint32_t a : aliases_of[cand[d]]) by_word[a >> 5].push_back((a & 31u) | (d << 5));
         }
-        inj.clear();
         for (auto& kv : by_word)
             for (size_t e0 = 0; e0 < kv.second.size(); e0 += MXP_INJ_SLOT - 4) {
                 const size_t e1 = std::min(kv.second.size(), e0 + MXP_INJ_SLOT - 4);
@@ -449,72 +685,52 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
                 slot[3] = (uint32_t)(e1 - e0);
                 inj.insert(inj.end(), slot, slot + MXP_INJ_SLOT);
             }
-        n_dense = (uint32_t)cand.size();
+        P.n_dense = (uint32_t)cand.size();
+        P.n_inj = P.n_dense ? (uint32_t)(inj.size() / MXP_INJ_SLOT) : 0u;
     }
-    ref_alias_off.assign(n + 1, 0);
-    ref_aliases.clear();
-    for (uint32_t i = 0; i < n; i++) {
-        ref_aliases.insert(ref_aliases.end(), aliases_of[i].begin(), aliases_of[i].end());
-        ref_alias_off[i + 1] = (uint32_t)ref_aliases.size();
+    if (base) {
+        ref_alias_off.assign(n + 1, 0);
+        ref_aliases.clear();
+        for (uint32_t i = 0; i < n; i++) {
+            ref_aliases.insert(ref_aliases.end(), aliases_of[i].begin(), aliases_of[i].end());
+            ref_alias_off[i + 1] = (uint32_t)ref_aliases.size();
+        }
     }
-    vcol_key_sid.resize(vcols.size());
-    for (size_t j = 0; j < vcols.size(); j++) vcol_key_sid[j] = intern_string(vcols[j].second);
-    refs_exact = true;
-    for (auto& R : rules) refs_exact &= R.status != MXP_RULE_UNSUPPORTED;
-
-    have_rules = true;
     if (device < 0) return MXP_OK;  // host-only engine: compile / inspect, no device tables
-    // upload program + global string pool
+
     hipError_t e;
-    have_rules = false;
     if ((e = hipSetDevice(device)) != hipSuccess) return hipfail(e, "hipSetDevice");
-    if ((e = d_prog.alloc(all.size() * sizeof(mxp_vm_ins))) != hipSuccess) return hipfail(e, "hipMalloc prog");
-    if ((e = d_rule_off.alloc(off.size() * 4)) != hipSuccess) return hipfail(e, "hipMalloc rule_off");
     auto put = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
         if ((e = d.alloc(bytes ? bytes : 16)) != hipSuccess) return hipfail(e, what);
         if (bytes && (e = hipMemcpy(d.p, src, bytes, hipMemcpyHostToDevice)) != hipSuccess) return hipfail(e, what);
         return MXP_OK;
     };
     int rc;
-    if ((rc = put(d_guards, guards.data(), guards.size() * sizeof(mxp_guard), "upload guards"))) return rc;
-    if ((rc = put(d_groups, groups.data(), groups.size() * sizeof(mxp_group), "upload groups"))) return rc;
-    if ((rc = put(d_segs, segs.data(), segs.size() * sizeof(mxp_seg), "upload segs"))) return rc;
-    if ((rc = put(d_glean, glean.data(), glean.size() * 4, "upload glean"))) return rc;
-    if ((rc = put(d_fills, fills.data(), fills.size() * sizeof(mxp_fill), "upload fills"))) return rc;
-    if ((rc = put(d_gvm, gvm.data(), gvm.size() * 4, "upload gvm"))) return rc;
-    if ((rc = put(d_gall, gall.data(), gall.size() * 4, "upload gall"))) return rc;
-    if ((rc = put(d_gk, gk.data(), gk.size() * 8, "upload gk"))) return rc;
-    if ((rc = put(d_idx, idx.data(), idx.size() * sizeof(mxp_index), "upload idx"))) return rc;
-    if ((rc = put(d_hents, hents.data(), hents.size() * sizeof(mxp_hent), "upload hents"))) return rc;
-    if ((rc = put(d_postings, postings.data(), postings.size() * 4, "upload postings"))) return rc;
-    if ((rc = put(d_plens, plens.data(), plens.size() * 4, "upload plens"))) return rc;
-    if ((rc = put(d_tmpls, tmpls.data(), tmpls.size() * sizeof(mxp_tmpl), "upload tmpls"))) return rc;
-    if ((rc = put(d_rule_tmpl, rule_tmpl.data(), rule_tmpl.size() * 4, "upload rule_tmpl"))) return rc;
-    if ((rc = put(d_rule_tmpl2, rule_tmpl2.data(), rule_tmpl2.size() * 4, "upload rule_tmpl2"))) return rc;
-    if ((rc = put(d_alias_off, alias_off.data(), alias_off.size() * 4, "upload alias_off"))) return rc;
-    if ((rc = put(d_aliases, alias_list.data(), alias_list.size() * 4, "upload aliases"))) return rc;
-    if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
-    if ((rc = put(d_dense_of, dense_of.data(), dense_of.size(), "upload dense_of"))) return rc;
-    if ((rc = put(d_inj, inj.data(), inj.size() * 4, "upload inj"))) return rc;
-    if ((rc = put(d_rx_hdr, rx_set.hdr.data(), rx_set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
-    if ((rc = put(d_rx_trans, rx_set.trans.data(), rx_set.trans.size() * 4, "upload rx trans"))) return rc;
-    if ((rc = put(d_rx_ascii, rx_set.ascii.data(), rx_set.ascii.size() * 2, "upload rx ascii"))) return rc;
-    if ((rc = put(d_rx_hilo, rx_set.hilo.data(), rx_set.hilo.size() * 4, "upload rx hilo"))) return rc;
-    if ((rc = put(d_rx_hicls, rx_set.hicls.data(), rx_set.hicls.size() * 2, "upload rx hicls"))) return rc;
-    std::vector<uint64_t> soff;
-    std::string blob;
-    if (!string_pool(gstrs, &soff, &blob)) return fail(MXP_ERR_ARG, "rule-set string longer than 16 MiB");
-    if ((e = d_gstr_off.alloc(soff.size() * 8)) != hipSuccess) return hipfail(e, "hipMalloc gstr_off");
-    if ((e = d_gstr.alloc(blob.size())) != hipSuccess) return hipfail(e, "hipMalloc gstr");
-    if (!all.empty() && (e = hipMemcpy(d_prog.p, all.data(), all.size() * sizeof(mxp_vm_ins), hipMemcpyHostToDevice)) != hipSuccess)
-        return hipfail(e, "upload prog");
-    if ((e = hipMemcpy(d_rule_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
-        return hipfail(e, "upload rule_off");
-    if ((e = hipMemcpy(d_gstr_off.p, soff.data(), soff.size() * 8, hipMemcpyHostToDevice)) != hipSuccess)
-        return hipfail(e, "upload gstr_off");
-    if (!blob.empty() && (e = hipMemcpy(d_gstr.p, blob.data(), blob.size(), hipMemcpyHostToDevice)) != hipSuccess)
-        return hipfail(e, "upload gstr");
-    have_rules = true;
+    if ((rc = put(P.d_guards, guards.data(), guards.size() * sizeof(mxp_guard), "upload guards"))) return rc;
+    if ((rc = put(P.d_groups, groups.data(), groups.size() * sizeof(mxp_group), "upload groups"))) return rc;
+    if ((rc = put(P.d_segs, segs.data(), segs.size() * sizeof(mxp_seg), "upload segs"))) return rc;
+    if ((rc = put(P.d_glean, glean.data(), glean.size() * 4, "upload glean"))) return rc;
+    if ((rc = put(P.d_fills, fills.data(), fills.size() * sizeof(mxp_fill), "upload fills"))) return rc;
+    if ((rc = put(P.d_vtfills, vtfills.data(), vtfills.size() * sizeof(mxp_fill), "upload vtfills"))) return rc;
+    if ((rc = put(P.d_fill_masks, fill_masks.data(), fill_masks.size() * 4, "upload fill masks"))) return rc;
+    if ((rc = put(P.d_gvm, gvm.data(), gvm.size() * 4, "upload gvm"))) return rc;
+    if ((rc = put(P.d_gall, gall.data(), gall.size() * 4, "upload gall"))) return rc;
+    if ((rc = put(P.d_gk, gk.data(), gk.size() * 8, "upload gk"))) return rc;
+    if ((rc = put(P.d_idx, idx.data(), idx.size() * sizeof(mxp_index), "upload idx"))) return rc;
+    if ((rc = put(P.d_hents, hents.data(), hents.size() * sizeof(mxp_hent), "upload hents"))) return rc;
+    if ((rc = put(P.d_postings, postings.data(), postings.size() * 4, "upload postings"))) return rc;
+    if ((rc = put(P.d_plens, plens.data(), plens.size() * 4, "upload plens"))) return rc;
+    if ((rc = put(P.d_tmpls, tmpls.data(), tmpls.size() * sizeof(mxp_tmpl), "upload tmpls"))) return rc;
+    if ((rc = put(P.d_rule_tmpl, rule_tmpl.data(), rule_tmpl.size() * 4, "upload rule_tmpl"))) return rc;
+    if ((rc = put(P.d_rule_tmpl2, rule_tmpl2.data(), rule_tmpl2.size() * 4, "upload rule_tmpl2"))) return rc;
+    if ((rc = put(P.d_alias_off, alias_off.data(), alias_off.size() * 4, "upload alias_off"))) return rc;
+    if ((rc = put(P.d_aliases, alias_list.data(), alias_list.size() * 4, "upload aliases"))) return rc;
+    if ((rc = put(P.d_dense_of, dense_of.data(), dense_of.size(), "upload dense_of"))) return rc;
+    if ((rc = put(P.d_inj, inj.data(), inj.size() * 4, "upload inj"))) return rc;
+    if ((rc = put(P.d_gvt_off, gvt_off.data(), gvt_off.size() * 4, "upload gvt_off"))) return rc;
+    if ((rc = put(P.d_gvt, gvt.data(), gvt.size() * 4, "upload gvt"))) return rc;
+    if ((rc = put(P.d_vt_woff, vt_woff.data(), vt_woff.size() * 4, "upload vt_woff"))) return rc;
+    if ((rc = put(P.d_vt_words, vt_words.data(), vt_words.size() * 4, "upload vt_words"))) return rc;
     return MXP_OK;
 }
 
@@ -788,6 +1004,43 @@ int mxp_engine::pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H)
             }
         }
     });
+    // value classes: the candidate columns with few distinct class keys (mxp_vt_key) in this batch
+    // -- distinct string ids by a bitmap over the id space, plus one class per other kind
+    db->vt_mask = 0;
+    db->vt_capc.assign(vt_cand_col.size(), 0);
+    if (!(debug_flags & 131072u) && n) {
+        const uint64_t S = G + db->overlay.size();
+        uint32_t active = 0;
+        std::vector<uint64_t> bits;
+        for (uint32_t s = 0; s < vt_cand_col.size() && active < MXP_VT_MAX; s++) {
+            const uint32_t c = vt_cand_col[s];
+            const uint8_t* kk = H.kinds.data() + (size_t)c * n;
+            const uint64_t* vv = H.vals.data() + (size_t)c * n;
+            bits.assign(S / 64 + 1, 0);
+            uint32_t kmask = 0;
+            mxp::par_for(n, 1 << 15, [&](uint64_t r0, uint64_t r1, unsigned) {
+                uint32_t km = 0;
+                for (uint64_t r = r0; r < r1; r++) {
+                    if (kk[r] == 1u) {
+                        const uint64_t x = vv[r] < S ? vv[r] : S;
+                        if (!(bits[x >> 6] >> (x & 63) & 1u)) __atomic_fetch_or(&bits[x >> 6], 1ull << (x & 63), __ATOMIC_RELAXED);
+                    } else {
+                        km |= 1u << (kk[r] & 31u);
+                    }
+                }
+                __atomic_fetch_or(&kmask, km, __ATOMIC_RELAXED);
+            });
+            uint64_t D = (uint64_t)__builtin_popcount(kmask);
+            for (uint64_t w : bits) D += (uint64_t)__builtin_popcountll(w);
+            const bool force = (debug_flags & 262144u) != 0;  // tests: value classes at any batch size
+            if (D > kVtMaxClasses || (!force && D * 16 > n)) continue;
+            uint32_t cap = 64;
+            while (cap < 2 * D) cap <<= 1;
+            db->vt_capc[s] = cap;
+            db->vt_mask |= 1u << s;
+            active++;
+        }
+    }
     if (need_maps) {
         H.moff.assign(b->n_maps + 1, 0);
         for (uint32_t m = 0; m < b->n_maps; m++) H.moff[m + 1] = (uint32_t)b->map_offsets[m + 1];
@@ -892,35 +1145,45 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = up(db->rx_ascii, rxb.ascii.data(), rxb.ascii.size() * 2, "upload rx ascii"))) return rc;
     if ((rc = up(db->rx_hilo, rxb.hilo.data(), rxb.hilo.size() * 4, "upload rx hilo"))) return rc;
     if ((rc = up(db->rx_hicls, rxb.hicls.data(), rxb.hicls.size() * 2, "upload rx hicls"))) return rc;
+    if (db->vt_mask) {  // value-class tables of the batch's active columns
+        uint64_t keys = 0;
+        for (uint32_t c : db->vt_capc) keys += c;
+        db->vt_keys_n = keys;
+        const uint32_t act = (uint32_t)__builtin_popcount(db->vt_mask);
+        if ((e = db->vt_cls.alloc((size_t)act * db->n * 2)) != hipSuccess) return hipfail(e, "vt classes");
+        if ((e = db->vt_keys.alloc(keys * 8)) != hipSuccess) return hipfail(e, "vt keys");
+        if ((e = db->vt_rep.alloc(keys * 4)) != hipSuccess) return hipfail(e, "vt reps");
+    }
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "pack sync");
     return MXP_OK;
 }
 
-void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
+void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) const {
     memset(A, 0, sizeof *A);
     A->prog = d_prog.as<mxp_vm_ins>();
     A->rule_off = d_rule_off.as<uint32_t>();
-    A->guards = d_guards.as<mxp_guard>();
-    A->groups = d_groups.as<mxp_group>();
-    A->segs = d_segs.as<mxp_seg>();
-    A->gk = d_gk.as<uint64_t>();
-    A->idx = d_idx.as<mxp_index>();
-    A->hents = d_hents.as<mxp_hent>();
-    A->postings = d_postings.as<uint32_t>();
-    A->plens = d_plens.as<uint32_t>();
-    A->n_idx = n_idx;
-    A->tmpls = d_tmpls.as<mxp_tmpl>();
-    A->rule_tmpl = d_rule_tmpl.as<uint32_t>();
-    A->rule_tmpl2 = d_rule_tmpl2.as<uint32_t>();
-    A->alias_off = n_alias ? d_alias_off.as<uint32_t>() : nullptr;
-    A->aliases = d_aliases.as<uint32_t>();
-    A->dense_of = n_dense ? d_dense_of.as<uint8_t>() : nullptr;
-    A->inj = d_inj.as<uint32_t>();
-    A->n_inj = n_dense ? (uint32_t)(inj.size() / MXP_INJ_SLOT) : 0u;
+    A->guards = P.d_guards.as<mxp_guard>();
+    A->groups = P.d_groups.as<mxp_group>();
+    A->segs = P.d_segs.as<mxp_seg>();
+    A->gk = P.d_gk.as<uint64_t>();
+    A->idx = P.d_idx.as<mxp_index>();
+    A->hents = P.d_hents.as<mxp_hent>();
+    A->postings = P.d_postings.as<uint32_t>();
+    A->plens = P.d_plens.as<uint32_t>();
+    A->n_idx = P.n_idx;
+    A->tmpls = P.d_tmpls.as<mxp_tmpl>();
+    A->rule_tmpl = P.d_rule_tmpl.as<uint32_t>();
+    A->rule_tmpl2 = P.d_rule_tmpl2.as<uint32_t>();
+    A->alias_off = P.n_alias ? P.d_alias_off.as<uint32_t>() : nullptr;
+    A->aliases = P.d_aliases.as<uint32_t>();
+    A->dense_of = P.n_dense ? P.d_dense_of.as<uint8_t>() : nullptr;
+    A->inj = P.d_inj.as<uint32_t>();
+    A->n_inj = P.n_inj;
+    A->fill_masks = P.d_fill_masks.as<uint32_t>();
     A->rconst = d_rconst.as<uint64_t>();
     A->flags = debug_flags;
     A->fill_span = fill_span;
-    A->lean_cols = lean_cc;
+    A->lean_cols = P.lean_cc;
     A->n_rules = (uint32_t)rules.size();
     A->n_words = (A->n_rules + 31) / 32;
     A->groups_per_wave = groups_per_wave;
@@ -943,12 +1206,66 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db) const {
     A->rx_batch = mxp_dfa_set{db->rx_hdr.as<mxp_dfa_hdr>(), db->rx_trans.as<uint32_t>(), db->rx_ascii.as<uint16_t>(),
                               db->rx_hilo.as<uint32_t>(), db->rx_hicls.as<uint16_t>()};
     A->rxof = db->rxof.as<uint32_t>();
+    if (!P.vt_cols.empty()) {
+        A->gvt_off = P.d_gvt_off.as<uint32_t>();
+        A->gvt = P.d_gvt.as<uint32_t>();
+        A->vt_words = P.d_vt_words.as<uint32_t>();
+        A->vt_meta = db->vt_meta.as<uint32_t>();
+        A->vt_cls = db->vt_cls.as<uint16_t>();
+        A->vt_tm = db->vt_t.as<uint32_t>();
+        A->vt_keys = db->vt_keys.as<unsigned long long>();
+        A->vt_rep = db->vt_rep.as<uint32_t>();
+        A->n_vt = (uint32_t)P.vt_cols.size();
+    }
+}
+
+// The batch's value-class layout under plan P (first launch of the batch): per active slot its
+// column, class table capacity, offsets into the key / representative tables and the class words.
+int mxp_engine::vt_prepare(mxp_dbatch* db, const Plan& P) {
+    if (!db->vt_meta_h.empty()) return MXP_OK;
+    const uint32_t act = (uint32_t)P.vt_cols.size();
+    std::vector<uint32_t> meta((size_t)act * 8, 0);
+    uint64_t kbase = 0, tbase = 0, woff = 0;
+    uint32_t a = 0;
+    for (uint32_t s = 0; s < vt_cand_col.size(); s++) {
+        if (!((P.mask >> s) & 1u)) continue;
+        const uint32_t cap = db->vt_capc[s];
+        meta[a * 8 + MXP_VTM_COL] = P.vt_cols[a];
+        meta[a * 8 + MXP_VTM_CAP] = cap;
+        meta[a * 8 + MXP_VTM_KBASE] = (uint32_t)kbase;
+        meta[a * 8 + MXP_VTM_TBASE] = (uint32_t)tbase;
+        meta[a * 8 + MXP_VTM_NW] = P.vt_nw[a];
+        meta[a * 8 + MXP_VTM_WOFF] = (uint32_t)woff;
+        kbase += cap;
+        tbase += (uint64_t)cap * P.vt_nw[a];
+        woff += P.vt_nw[a];
+        a++;
+    }
+    if (tbase >= (1ull << 31)) return fail(MXP_ERR_NOMEM, "value-class tables too large");
+    hipError_t e;
+    if ((e = db->vt_meta.alloc(meta.size() * 4)) != hipSuccess) return hipfail(e, "vt meta");
+    if ((e = hipMemcpy(db->vt_meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+        return hipfail(e, "upload vt meta");
+    db->vt_t_words = tbase;
+    if ((e = db->vt_t.alloc(2 * tbase * 4)) != hipSuccess) return hipfail(e, "vt class words");
+    db->vt_meta_h.swap(meta);
+    return MXP_OK;
 }
 
 int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
                        bool log, unsigned long long* d_hits, uint64_t* stats, uint32_t q_lo, uint32_t q_hi) {
+    // guards on: guard-only groups through the lean kernel, the rest through the VM kernel;
+    // guards off (Eval, ablation): every group through the VM kernel
+    const bool guards_on = !d_vals && !(debug_flags & 2u);
+    // value classes only for plain predicate evaluations: Eval mode, referenced attributes and
+    // recomputed error windows (which need every record) run plan 0
+    const uint32_t mask = (guards_on && !refs_on && !win_log_cap) ? db->vt_mask : 0u;
+    Plan* P = nullptr;
+    int rc = get_plan(mask, &P);
+    if (rc) return rc;
+    if (mask && (rc = vt_prepare(db, *P))) return rc;
     mxp_kargs A;
-    fill_args(&A, db);
+    fill_args(&A, db, *P);
     A.hits = d_vals ? nullptr : d_hits;
     A.stats = d_vals ? nullptr : stats;
     A.out_match = d_match;
@@ -969,6 +1286,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
             if ((e = d_errlog.alloc((size_t)errcap * sizeof(mxp_err_rec))) != hipSuccess) return hipfail(e, "errlog");
             if ((e = d_errcount.alloc(16)) != hipSuccess) return hipfail(e, "errcount");
         }
+        // errcount[0]: records; [1]: value-class error pairs (not logged per pair); [2]: class records
         if ((e = hipMemsetAsync(d_errcount.p, 0, 16, s)) != hipSuccess) return hipfail(e, "memset errcount");
         A.errlog = d_errlog.as<mxp_err_rec>();
         A.errcount = d_errcount.as<uint32_t>();
@@ -982,24 +1300,19 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     }
     if (A.n == 0 || A.n_rules == 0) return MXP_OK;
     // guard-index phase: predicate mode only (Eval runs whole programs in mxp_eval_kernel)
-    const bool use_index = !d_vals && !(debug_flags & 2u) && n_idx > 0;
+    const bool use_index = !d_vals && !(debug_flags & 2u) && P->n_idx > 0;
     if (!use_index) A.n_idx = 0;
     auto gy_of = [&](uint32_t ng) { return (ng + 4 * A.groups_per_wave - 1) / (4 * A.groups_per_wave); };
     if (timing && (e = hipEventRecord(ev[0], s)) != hipSuccess) return hipfail(e, "event");
-    // guards on: guard-only groups through the lean kernel, the rest through the VM kernel;
-    // guards off (Eval, ablation): every group through the VM kernel
-    const bool guards_on = !d_vals && !(debug_flags & 2u);
     struct Part {
         const DevBuf* list;
         uint32_t n;
         int vm;
-    } parts[2] = {{guards_on ? &d_glean : &d_gall, guards_on ? n_glean : 0u, 0},
-                  {guards_on ? &d_gvm : &d_gall, guards_on ? n_gvm : A.n_words, 1}};
-    // Pipelined request chunks: the index kernel of chunk c (which ORs its true / error bits into the
-    // words the fill, guard and VM kernels wrote) runs on the side stream while chunk c + 1's fill
-    // streams its stores -- the fill is HBM-write bound, the index kernel latency bound, so they share
-    // the chip; only the last chunk's index pass is left exposed.
-    // a request window (error recomputation) or the whole batch, possibly in pipelined chunks
+    } parts[2] = {{guards_on ? &P->d_glean : &P->d_gall, guards_on ? P->n_glean : 0u, 0},
+                  {guards_on ? &P->d_gvm : &P->d_gall, guards_on ? P->n_gvm : A.n_words, 1}};
+    // a request window (error recomputation) or the whole batch, possibly in pipelined chunks:
+    // the index kernel of chunk c (which ORs its true / error bits into the words the fill, guard
+    // and VM kernels wrote) runs on the side stream while chunk c + 1's fill streams its stores
     const bool window = q_lo != 0 || q_hi < A.n;
     const uint32_t lo = window ? q_lo : 0u, hi = window ? std::min(q_hi, A.n) : A.n;
     if (lo >= hi) return MXP_OK;
@@ -1018,23 +1331,48 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         for (auto& x : chunk_ev)
             if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) return hipfail(e, "chunk event");
     }
-    if (guards_on && n_fills) A.fills = d_fills.as<mxp_fill>();
+    if (guards_on && P->n_fills) A.fills = P->d_fills.as<mxp_fill>();
     if (!use_index) A.dense_of = nullptr;
     if (A.dense_of) {
         if (d_dense_cm.n < (size_t)A.n * 8 && (e = d_dense_cm.alloc((size_t)A.n * 8)) != hipSuccess)
             return hipfail(e, "dense masks");
         A.dense_cm = d_dense_cm.as<uint64_t>();
     }
+    if (A.n_vt) {
+        // value classes: classify every request of [lo, hi) per active column, then evaluate the
+        // columns' rules once per class (class records -> errcount[2], the host expands them)
+        if ((e = hipMemsetAsync(db->vt_keys.p, 0xFF, db->vt_keys_n * 8, s)) != hipSuccess) return hipfail(e, "vt reset");
+        A.q0 = lo;
+        A.q1 = hi;
+        if ((e = mxp_launch_vt_classify(&A, s)) != hipSuccess) return hipfail(e, "launch vt classify");
+        mxp_kargs AV = A;
+        if (A.errlog) {  // class records: a log of their own, counted in errcount[2]
+            if (!d_vtlog.p && (e = d_vtlog.alloc((size_t)vtlog_cap * sizeof(mxp_err_rec))) != hipSuccess)
+                return hipfail(e, "class errlog");
+            AV.errlog = d_vtlog.as<mxp_err_rec>();
+            AV.errcount = A.errcount + 2;
+            AV.errcap = vtlog_cap;
+        }
+        uint32_t tiles = 0;
+        for (uint32_t a = 0; a < A.n_vt; a++) tiles += db->vt_meta_h[a * 8 + MXP_VTM_CAP] / 64;
+        if ((e = mxp_launch_vt_eval(&AV, tiles, (P->vt_max_nw + 3) / 4, s)) != hipSuccess)
+            return hipfail(e, "launch vt eval");
+    }
     for (uint32_t c = 0; c < nchunk; c++) {
         A.q0 = lo + c * step;
         A.q1 = std::min(hi, lo + (c + 1) * step);
         const uint32_t cx = (A.q1 - A.q0 + 63) / 64;
-        if (guards_on && n_fills && (e = mxp_launch_fill(&A, n_fills, s)) != hipSuccess) return hipfail(e, "launch fill");
-        for (const Part& P : parts) {
-            if (!P.n) continue;
-            A.glist = P.list->as<uint32_t>();
-            A.n_glist = P.n;
-            if ((e = mxp_launch_eval(&A, cx, gy_of(P.n), P.vm, s)) != hipSuccess) return hipfail(e, "launch eval");
+        if (guards_on && P->n_fills && (e = mxp_launch_fill(&A, P->n_fills, s)) != hipSuccess) return hipfail(e, "launch fill");
+        if (guards_on && P->n_vtfills) {
+            mxp_kargs AF = A;
+            AF.fills = P->d_vtfills.as<mxp_fill>();
+            if ((e = mxp_launch_vtfill(&AF, P->n_vtfills, s)) != hipSuccess) return hipfail(e, "launch vtfill");
+        }
+        for (const Part& Pt : parts) {
+            if (!Pt.n) continue;
+            A.glist = Pt.list->as<uint32_t>();
+            A.n_glist = Pt.n;
+            if ((e = mxp_launch_eval(&A, cx, gy_of(Pt.n), Pt.vm, s)) != hipSuccess) return hipfail(e, "launch eval");
         }
         if (!use_index) continue;
         if (nchunk == 1) {
@@ -1058,6 +1396,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     }
     if (timing && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hipfail(e, "event");
     ev_index = use_index;
+    last_mask = mask;
     return MXP_OK;
 }
 
@@ -1314,11 +1653,13 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) 
 
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
     if (!eng || !out) return 0;
-    const uint32_t v[9] = {eng->n_guarded, eng->n_templated, eng->n_tmpls, eng->n_segs, eng->n_indexed,
-                           (uint32_t)(eng->cols.size() + eng->vcols.size()), eng->n_composite, eng->n_alias,
-                           eng->n_dense};
+    const mxp_engine::Plan* P = eng->plan0();
+    if (!P) return 0;
+    const uint32_t v[10] = {eng->n_guarded, eng->n_templated, P->n_tmpls, P->n_segs, P->n_indexed,
+                            (uint32_t)(eng->cols.size() + eng->vcols.size()), P->n_composite, P->n_alias,
+                            P->n_dense, (uint32_t)eng->vt_cand_col.size()};
     uint32_t k = 0;
-    for (; k < cap && k < 9; k++) out[k] = v[k];
+    for (; k < cap && k < 10; k++) out[k] = v[k];
     return k;
 }
 
@@ -1390,7 +1731,8 @@ int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, ui
         eng->stats_tp = eng->stats_n ? (double)*eng->h_stats / eng->stats_n : 0.0;
         eng->stats_pending = false;
     }
-    const bool fused = eng->stats_tp * 125.0 <= (double)W;
+    // (value classes set many true pairs outside the index kernel's count: stream the counters)
+    const bool fused = eng->stats_tp * 125.0 <= (double)W && !db->vt_mask;
     // the reset follows the previous download even when the caller switched streams
     if (eng->stats_pending && (e = hipStreamWaitEvent(s, eng->stats_ev, 0)) != hipSuccess)
         return eng->hipfail(e, "stats wait");
@@ -1438,22 +1780,75 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
 
 int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_dbatch>& db) {
     hipError_t e;
-    uint32_t cnt = 0;
-    if ((e = hipMemcpyAsync(&cnt, d_errcount.p, 4, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+    // [0] records of the log, [1] error pairs of value-class rules, [2] class records
+    uint32_t cnt[4] = {0, 0, 0, 0};
+    if ((e = hipMemcpyAsync(cnt, d_errcount.p, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
         return hipfail(e, "download errcount");
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "eval sync");
-    last_error_count = cnt;
+    last_error_count = (uint64_t)cnt[0] + cnt[1];
     last_errors.clear();
     err_windows.clear();
-    errors_complete = cnt <= errcap;
-    uint32_t kept = std::min(cnt, errcap);
+    errors_complete = cnt[0] <= errcap;
+    uint32_t kept = std::min(cnt[0], errcap);
     if (kept) {
         std::vector<mxp_err_rec> recs(kept);
         if ((e = hipMemcpy(recs.data(), d_errlog.p, kept * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
             return hipfail(e, "download errlog");
         for (auto& r : recs) last_errors[((uint64_t)r.req << 32) | r.rule] = {r.code, format_error(batch, db.get(), r)};
     }
+    if (cnt[2]) {
+        int rc = expand_class_errors(batch, db.get(), cnt[2], errcap > kept ? errcap - kept : 0u);
+        if (rc) return rc;
+    }
     last_db = std::move(db);
+    return MXP_OK;
+}
+
+// Class records of the last evaluation (mxp_vt_eval_kernel logs each failing (class, rule) once,
+// at the class's representative request): every request of the class fails that rule the same
+// way, so each record stands for the pairs of all of them.  Expanded here up to `room` records;
+// past it the rest are recomputed on demand like any record past the log's capacity.
+int mxp_engine::expand_class_errors(const mxp_bag_batch* batch, mxp_dbatch* db, uint32_t n_class, uint32_t room) {
+    hipError_t e;
+    if (n_class > vtlog_cap || !last_mask) {
+        errors_complete = false;
+        return MXP_OK;
+    }
+    std::vector<mxp_err_rec> recs(n_class);
+    if ((e = hipMemcpy(recs.data(), d_vtlog.p, n_class * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
+        return hipfail(e, "download class errlog");
+    const uint32_t n = db->n, act = (uint32_t)__builtin_popcount(last_mask);
+    std::vector<uint16_t> cls((size_t)act * n);
+    if ((e = hipMemcpy(cls.data(), db->vt_cls.p, cls.size() * 2, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hipfail(e, "download classes");
+    // requests of every class, per active slot (counting sort by class)
+    std::vector<std::vector<uint32_t>> start(act), reqs(act);
+    for (uint32_t a = 0; a < act; a++) {
+        const uint32_t cap = db->vt_meta_h[a * 8 + MXP_VTM_CAP];
+        const uint16_t* c = cls.data() + (size_t)a * n;
+        start[a].assign(cap + 1, 0);
+        for (uint32_t q = 0; q < n; q++) start[a][c[q] + 1]++;
+        for (uint32_t k = 0; k < cap; k++) start[a][k + 1] += start[a][k];
+        std::vector<uint32_t> at(start[a].begin(), start[a].end() - 1);
+        reqs[a].resize(n);
+        for (uint32_t q = 0; q < n; q++) reqs[a][at[c[q]]++] = q;
+    }
+    uint64_t emitted = 0;
+    for (const mxp_err_rec& r : recs) {
+        const uint32_t s = vt_slot_of_rule[r.rule];
+        const uint32_t a = (uint32_t)__builtin_popcount(last_mask & ((1u << s) - 1u));
+        const uint32_t k = cls[(size_t)a * n + r.req];
+        for (uint32_t i = start[a][k]; i < start[a][k + 1]; i++) {
+            if (emitted >= room) {
+                errors_complete = false;
+                return MXP_OK;
+            }
+            mxp_err_rec x = r;
+            x.req = reqs[a][i];
+            last_errors[((uint64_t)x.req << 32) | x.rule] = {x.code, format_error(batch, db, x)};
+            emitted++;
+        }
+    }
     return MXP_OK;
 }
 

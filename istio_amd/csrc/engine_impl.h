@@ -28,6 +28,9 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
+extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
+extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t s);
+extern "C" hipError_t mxp_launch_vt_eval(const mxp_kargs* args, uint32_t tiles, uint32_t wchunks, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
                                       unsigned long long* hits, hipStream_t s);
 
@@ -112,6 +115,13 @@ struct StrPool {
 
 struct mxp_dbatch {
     uint32_t n = 0;
+    // value classes (pack_host): candidate slots whose column has few distinct values in this batch,
+    // their class table capacities, the device class tables (vt_t: match words, then error words)
+    uint32_t vt_mask = 0;
+    std::vector<uint32_t> vt_capc;         // per candidate slot (0: inactive)
+    std::vector<uint32_t> vt_meta_h;       // kargs.vt_meta of the batch's plan (first launch)
+    DevBuf vt_cls, vt_keys, vt_rep, vt_t, vt_meta;
+    size_t vt_t_words = 0, vt_keys_n = 0;
     DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
     DevBuf rxof, rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // run-time regexp patterns
     StrPool overlay;                                  // batch strings not in the rule set's pool
@@ -162,15 +172,46 @@ struct mxp_engine : public mxp::LowerTables {
     std::set<uint32_t> rx_cols;  // columns holding run-time patterns
     DevBuf d_rx_hdr, d_rx_trans, d_rx_ascii, d_rx_hilo, d_rx_hicls;
 
-    DevBuf d_prog, d_rule_off, d_guards, d_gstr_off, d_gstr;
-    DevBuf d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_alias_off, d_aliases, d_rconst, d_idx, d_hents, d_postings, d_plens;
-    DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
-    uint32_t n_glean = 0, n_gvm = 0;
-    uint32_t lean_cc = 0;  // columns < MXP_CC read by the lean groups (kargs.lean_cols)
-    DevBuf d_fills;                 // chunks of uniform indexed groups (mxp_fill_kernel)
-    uint32_t n_fills = 0, n_gfill = 0;
-    uint32_t n_idx = 0, n_indexed = 0, n_composite = 0, n_alias = 0;
-    uint32_t n_guarded = 0, n_templated = 0, n_tmpls = 0, n_segs = 0;
+    // rule-level tables (one per compile): programs + template code, offsets, constants, strings
+    DevBuf d_prog, d_rule_off, d_gstr_off, d_gstr, d_rconst;
+    std::vector<mxp_vm_ins> prog_h;    // host copies the plans are built from
+    std::vector<uint32_t> off_h;
+    std::vector<mxp_guard> guards_h;   // leading-atom guards before any plan drops a prefix guard
+    std::vector<uint32_t> rule_tmpl_h;
+    std::vector<mxp_tmpl> tmpls_h;
+    uint32_t n_guarded = 0, n_templated = 0;
+    // Value classes (mxp_vt_*): rules whose result depends on one column's (kind, string value)
+    // only.  Candidate columns (>= kVtMinRules such rules, at most kVtCandMax) get a slot; a batch
+    // whose column has few distinct values (pack time) activates the slot, and the plan of that set
+    // of slots leaves those rules to the value-class kernels.
+    static constexpr uint32_t kVtMinRules = 8, kVtCandMax = 32, kVtMaxClasses = 4096;
+    std::vector<uint32_t> vt_cand_col;     // slot -> column
+    std::vector<uint8_t> vt_slot_of_rule;  // rule -> slot, 0xFF none
+    // The kernels' tables for one set of value-class slots (mask 0: none, built at compile)
+    struct Plan {
+        uint32_t mask = 0;
+        uint32_t n_glean = 0, n_gvm = 0, lean_cc = 0, n_fills = 0, n_gfill = 0;
+        uint32_t n_idx = 0, n_indexed = 0, n_composite = 0, n_alias = 0, n_tmpls = 0, n_segs = 0;
+        uint32_t n_dense = 0, n_inj = 0;
+        DevBuf d_guards, d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_alias_off, d_aliases;
+        DevBuf d_idx, d_hents, d_postings, d_plens;
+        DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
+        DevBuf d_fills, d_fill_masks;   // chunks of uniform indexed groups (mxp_fill_kernel)
+        DevBuf d_vtfills;               // ... those with value-class merge entries (mxp_vtfill_kernel)
+        uint32_t n_vtfills = 0;
+        DevBuf d_dense_of, d_inj;
+        // value classes: active slot a -> column vt_cols[a], words vt_nw[a]; per group merge entries
+        std::vector<uint32_t> vt_cols, vt_nw;
+        uint32_t vt_max_nw = 0;
+        DevBuf d_gvt_off, d_gvt, d_vt_woff, d_vt_words;
+    };
+    std::map<uint32_t, std::unique_ptr<Plan>> plans;
+    int get_plan(uint32_t mask, Plan** out);
+    int build_plan(Plan& P);
+    const Plan* plan0() const {
+        auto it = plans.find(0);
+        return it == plans.end() ? nullptr : it->second.get();
+    }
     uint32_t groups_per_wave = 16; // MXP_GPW (A/B on C4: 4 6.50 ms, 8 6.55, 16 6.36; C2 flat; profiles/r1_v15_ab_gpw.log)
     // optional per-kernel timing of device evaluations (mxp_set_timing): events around each launch
     bool timing = false;
@@ -179,10 +220,6 @@ struct mxp_engine : public mxp::LowerTables {
     // dense canonical rules (mxp_inject_kernel): rule -> id < 64, and per bitmap word the
     // (bit | id << 5) entries of those rules and their aliases, in slots of MXP_INJ_SLOT dwords
     static constexpr size_t kDenseMin = 8;
-    std::vector<uint8_t> dense_of;
-    std::vector<uint32_t> inj;  // [slots][MXP_INJ_SLOT]
-    uint32_t n_dense = 0;
-    DevBuf d_dense_of, d_inj;
     DevBuf d_dense_cm;  // [n] per-request dense masks of the current evaluation
     // referenced attributes (mxp_eval_refs, refs.cpp)
     struct RefComposite {
@@ -356,6 +393,9 @@ struct mxp_engine : public mxp::LowerTables {
     int evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv, std::unique_ptr<mxp_dbatch>& db);
     // wait for the evaluation, fetch and format its error records, keep `db` as the last batch
     int collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_dbatch>& db);
+    int expand_class_errors(const mxp_bag_batch* batch, mxp_dbatch* db, uint32_t n_class, uint32_t room);
+    DevBuf d_vtlog;                  // class records of the value-class kernel
+    uint32_t vtlog_cap = 1u << 20;
     struct PackedHost {
         std::vector<uint8_t> kinds;
         std::vector<uint64_t> vals, ipof, tsof;
@@ -368,7 +408,9 @@ struct mxp_engine : public mxp::LowerTables {
     int pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H);
     int pack(const mxp_bag_batch* b, mxp_dbatch* db);
     int wire_decode(const mxp_wire_batch* w, const char* const* names, uint32_t n_names, mxp_wire** out);  // wire.cpp
-    void fill_args(mxp_kargs* A, const mxp_dbatch* db) const;
+    void fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) const;
+    int vt_prepare(mxp_dbatch* db, const Plan& P);
+    uint32_t last_mask = 0;  // value-class slots of the last launch
     // requests [q_lo, q_hi) of the batch (default: all); q_lo a multiple of 4
     int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
                unsigned long long* d_hits = nullptr, uint64_t* d_stats = nullptr, uint32_t q_lo = 0,

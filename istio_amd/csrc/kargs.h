@@ -82,4 +82,17 @@ typedef struct mxp_kargs {
     uint32_t refcap;
     uint32_t errcap;
     uint32_t flags;              // debug / ablation: 1 = skip in-wave VM, 2 = no guards (results invalid)
+    const uint32_t* fill_masks;  // mxp_fill_kernel: rules of each group of a chunk (mxp_fill.moff)
+    // value classes (kernels.hip mxp_vt_*; null gvt_off: none)
+    const uint32_t* gvt_off;     // [n_words + 1] merge entries of each group
+    const uint32_t* gvt;         // active slot << 24 | word position j within the slot's words
+    const uint32_t* vt_meta;     // [n_vt][8] MXP_VTM_* fields
+    const uint32_t* vt_words;    // (group, rule mask) pairs of every slot's words
+    uint16_t* vt_cls;            // [n_vt][n] class of each request
+    uint32_t* vt_tm;             // class words, (match, error) u32 pairs: slot a, word j, class k at pair tbase + j * cap + k
+    uint32_t* vt_te;             // (unused)
+    unsigned long long* vt_keys; // class tables: keys (MXP_VT_EMPTY = free) and a representative request
+    uint32_t* vt_rep;
+    uint32_t n_vt;
+    uint32_t pad6;
 } mxp_kargs;

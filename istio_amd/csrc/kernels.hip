@@ -496,6 +496,37 @@ __device__ __forceinline__ void log_guard_errors(const mxp_kargs& A, uint32_t e,
     }
 }
 
+// Value classes: the words of group g's class-served rules for one request -- per merge entry
+// (active slot a, word position j) the class word of the request's class in that slot.
+__device__ __forceinline__ void vt_words_of(const mxp_kargs& A, uint32_t g, uint32_t req, bool valid, uint32_t& vm,
+                                            uint32_t& ve) {
+    vm = ve = 0;
+    const uint32_t i0 = uni(A.gvt_off[g]), i1 = uni(A.gvt_off[g + 1]);
+    for (uint32_t i = i0; i < i1; i++) {
+        const uint32_t ent = uni(A.gvt[i]);
+        const uint32_t a = ent >> 24, j = ent & 0xFFFFFFu;
+        const uint32_t cap = uni(A.vt_meta[a * 8u + MXP_VTM_CAP]), tb = uni(A.vt_meta[a * 8u + MXP_VTM_TBASE]);
+        if (valid) {
+            const uint32_t k = A.vt_cls[(uint64_t)a * A.n + req];
+            const uint2 w = *(const uint2*)(A.vt_tm + 2u * ((uint64_t)tb + (uint64_t)j * cap + k));
+            vm |= w.x;
+            ve |= w.y;
+        }
+    }
+}
+
+// value-class error pairs are not logged per pair (the host expands the class records): count them
+// (errcount[1]), c per lane
+__device__ __forceinline__ void vt_count_n(const mxp_kargs& A, uint32_t c) {
+    if (!A.errlog || !__ballot(c != 0)) return;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += (uint32_t)__shfl_xor((int)c, off, 64);
+    if (__lane_id() == 0) atomicAdd(A.errcount + 1, c);
+}
+__device__ __forceinline__ void vt_count_errors(const mxp_kargs& A, uint32_t ve) {
+    vt_count_n(A, (uint32_t)__builtin_popcount(ve));
+}
+
 }  // namespace
 
 // Phase 1 + in-wave phase 2 over 32-rule groups.
@@ -623,6 +654,13 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
                     }
                 }
             }
+            if (A.gvt_off) {  // value-class rules of the group (after the guard errors were logged)
+                uint32_t vm, ve;
+                vt_words_of(A, g, req, valid, vm, ve);
+                vt_count_errors(A, ve);
+                m |= vm;
+                e |= ve;
+            }
             if (valid) {
                 if (A.out_match) A.out_match[(uint64_t)g * N + req] = m;
                 if (A.out_err) A.out_err[(uint64_t)g * N + req] = e;
@@ -744,15 +782,26 @@ extern "C" __global__ __launch_bounds__(256) void mxp_guard2_kernel(mxp_kargs A)
                 }
             }
 #undef GF
-            const uint32_t ma = (eqa ^ neg) & (only | orm) & oka, mb = (eqb ^ neg) & (only | orm) & okb;
-            const uint32_t ea = guarded & ~oka, eb = guarded & ~okb;
+            uint32_t ma = (eqa ^ neg) & (only | orm) & oka, mb = (eqb ^ neg) & (only | orm) & okb;
+            uint32_t ea = guarded & ~oka, eb = guarded & ~okb;
+            if (va && A.errlog && ea) log_guard_errors(A, ea, r0, reqa);
+            if (vb && A.errlog && eb) log_guard_errors(A, eb, r0, reqb);
+            if (A.gvt_off) {  // value-class rules of the group
+                uint32_t vma, vea, vmb, veb;
+                vt_words_of(A, g, reqa, va, vma, vea);
+                vt_words_of(A, g, reqb, vb, vmb, veb);
+                vt_count_errors(A, vea);
+                vt_count_errors(A, veb);
+                ma |= vma;
+                ea |= vea;
+                mb |= vmb;
+                eb |= veb;
+            }
             if (va) {
-                if (A.errlog && ea) log_guard_errors(A, ea, r0, reqa);
                 if (A.out_match) A.out_match[(uint64_t)g * N + reqa] = ma;
                 if (A.out_err) A.out_err[(uint64_t)g * N + reqa] = ea;
             }
             if (vb) {
-                if (A.errlog && eb) log_guard_errors(A, eb, r0, reqb);
                 if (A.out_match) A.out_match[(uint64_t)g * N + reqb] = mb;
                 if (A.out_err) A.out_err[(uint64_t)g * N + reqb] = eb;
             }
@@ -786,8 +835,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = uni(threadIdx.x >> 6);
     const mxp_fill* F = A.fills + blockIdx.y;
-    const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), all = uni(F->all),
-                   last = uni(F->last);
+    const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
     const uint32_t span = uni(A.fill_span);
     const uint64_t N = A.n;
     const uint32_t Q1 = A.q1;        // chunk end (chunks start at multiples of 1024)
@@ -816,7 +864,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
     }
     if (A.errlog && any) {
         for (uint32_t g = 0; g < n; g++) {
-            const uint32_t mask = g + 1 == n ? last : all;
+            const uint32_t mask = uni(A.fill_masks[moff + g]);
             for (uint32_t sp = 0; sp < span; sp++)
                 for (uint32_t r = 0; r < 4; r++)
                     if (bad[sp][r] && q0 + sp * 256u + r < Q1) log_guard_errors(A, mask, (g0 + g) * 32u, q0 + sp * 256u + r);
@@ -827,7 +875,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
     const bool nt = !(A.flags & 128u);
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     for (uint32_t g = 0; g < n; g++) {
-        const uint32_t mask = g + 1 == n ? last : all;
+        const uint32_t mask = uni(A.fill_masks[moff + g]);
         const uint64_t row = (uint64_t)(g0 + g) * N;
 #pragma unroll
         for (uint32_t sp = 0; sp < MXP_FILL_SPAN_MAX; sp++) {
@@ -852,6 +900,251 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
                     if (A.out_match) A.out_match[at + r] = 0u;
                     if (A.out_err) A.out_err[at + r] = bad[sp][r] & mask;
                 }
+            }
+        }
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Value classes.  A rule whose program reads one column, as a string (or a map[key] virtual
+// column), computes a function of that column's (kind, string id) alone.  When a batch's column
+// holds few distinct such values (pack time: engine.cpp pack_host), the rules of that column are
+// evaluated once per distinct value -- a "class" -- and each request's words are gathered from its
+// class: C4's 2000 header rules run on 17 classes per header instead of 1M requests.
+//   mxp_vt_classify_kernel  per request and active column: the class (slot of an open-addressing
+//                           table of class keys, mxp_vt_key; the first request to claim a slot is
+//                           its representative);
+//   mxp_vt_eval_kernel      the VM over (class representative, rule) pairs: lane = class, wave =
+//                           one bitmap word of the column's rules; class words stored class-minor
+//                           (word j of class k at tbase + j * cap + k, so a wave's gathers for one
+//                           word hit one or two cache lines);
+//   vt_words_of             the writers of the bitmaps (fill, lean, VM kernels) OR the class words
+//                           of each request into its group words.
+// Requests per workgroup of mxp_vt_classify_kernel and its LDS table (twice as many slots, so
+// the workgroup's distinct keys always fit).
+#define MXP_VTC_REQ 2048u
+#define MXP_VTC_LCAP 4096u
+extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kargs A) {
+    // The hot keys of a low-cardinality column would serialise on a handful of global addresses if
+    // every request probed the global table (and L1 may keep a stale EMPTY line), so a workgroup
+    // first dedups its 2048 requests' keys in an LDS table, resolves each distinct key against the
+    // global table once (compare-and-swap, the inserter's request becomes the class
+    // representative), then hands every request its class from LDS.
+    __shared__ unsigned long long lkey[MXP_VTC_LCAP];
+    __shared__ uint32_t lcls[MXP_VTC_LCAP];
+    __shared__ uint32_t lrep[MXP_VTC_LCAP];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t N = A.n;
+    const uint32_t base = A.q0 + blockIdx.x * MXP_VTC_REQ;
+    for (uint32_t a = 0; a < A.n_vt; a++) {
+        const uint32_t col = uni(A.vt_meta[a * 8u + MXP_VTM_COL]), cap = uni(A.vt_meta[a * 8u + MXP_VTM_CAP]),
+                       kb = uni(A.vt_meta[a * 8u + MXP_VTM_KBASE]);
+        for (uint32_t i = tid; i < MXP_VTC_LCAP; i += 256u) lkey[i] = MXP_VT_EMPTY;
+        __syncthreads();
+        // 1. local slots of this thread's requests (req = base + tid + 256 r)
+        uint32_t loc[MXP_VTC_REQ / 256u];
+#pragma unroll
+        for (uint32_t r = 0; r < MXP_VTC_REQ / 256u; r++) {
+            const uint32_t req = base + tid + 256u * r;
+            loc[r] = 0xFFFFFFFFu;
+            if (req >= A.q1) continue;
+            const uint64_t key = mxp_vt_key(A.kinds[(uint64_t)col * N + req], A.vals[(uint64_t)col * N + req]);
+            uint32_t h = mxp_hash64(key) & (MXP_VTC_LCAP - 1u);
+            for (;;) {
+                const unsigned long long cur = lkey[h];
+                if (cur == key) break;
+                if (cur == MXP_VT_EMPTY) {
+                    const unsigned long long old = atomicCAS(&lkey[h], (unsigned long long)MXP_VT_EMPTY, (unsigned long long)key);
+                    if (old == MXP_VT_EMPTY) {
+                        lrep[h] = req;
+                        break;
+                    }
+                    if (old == key) break;
+                }
+                h = (h + 1u) & (MXP_VTC_LCAP - 1u);
+            }
+            loc[r] = h;
+        }
+        __syncthreads();
+        // 2. each distinct key of the workgroup against the global table (room for twice the
+        // batch's distinct keys, counted at pack time: the probe ends)
+        unsigned long long* T = A.vt_keys + kb;
+        for (uint32_t i = tid; i < MXP_VTC_LCAP; i += 256u) {
+            const unsigned long long key = lkey[i];
+            if (key == MXP_VT_EMPTY) continue;
+            uint32_t h = mxp_hash64(key) & (cap - 1u);
+            for (;;) {
+                const unsigned long long old = atomicCAS(T + h, (unsigned long long)MXP_VT_EMPTY, key);
+                if (old == MXP_VT_EMPTY) {
+                    A.vt_rep[kb + h] = lrep[i];
+                    break;
+                }
+                if (old == key) break;
+                h = (h + 1u) & (cap - 1u);
+            }
+            lcls[i] = h;
+        }
+        __syncthreads();
+        // 3. classes out
+#pragma unroll
+        for (uint32_t r = 0; r < MXP_VTC_REQ / 256u; r++) {
+            const uint32_t req = base + tid + 256u * r;
+            if (req < A.q1) A.vt_cls[(uint64_t)a * N + req] = (uint16_t)lcls[loc[r]];
+        }
+        __syncthreads();
+    }
+}
+
+// grid x: class tiles of 64 (slot by slot), y: groups of 4 words (one per wave)
+extern "C" __global__ __launch_bounds__(256) void mxp_vt_eval_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = uni(tid >> 6);
+    uint32_t t = blockIdx.x, a = 0;
+    for (; a + 1 < A.n_vt; a++) {
+        const uint32_t nt = uni(A.vt_meta[a * 8u + MXP_VTM_CAP]) / 64u;
+        if (t < nt) break;
+        t -= nt;
+    }
+    const uint32_t* M = A.vt_meta + a * 8u;
+    const uint32_t cap = uni(M[MXP_VTM_CAP]), kb = uni(M[MXP_VTM_KBASE]), tb = uni(M[MXP_VTM_TBASE]),
+                   nw = uni(M[MXP_VTM_NW]), woff = uni(M[MXP_VTM_WOFF]);
+    const uint32_t j = blockIdx.y * 4u + wave;
+    if (j >= nw || t * 64u >= cap) return;  // wave-uniform; the VM needs no block barrier
+    const uint32_t k = t * 64u + lane;
+    const bool live = __hip_atomic_load(A.vt_keys + kb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != MXP_VT_EMPTY;
+    const uint32_t rep = live ? A.vt_rep[kb + k] : 0u;
+    const uint32_t g = uni(A.vt_words[2u * (woff + j)]), mask = uni(A.vt_words[2u * (woff + j) + 1u]);
+    uint32_t m = 0, e = 0;
+    for (uint32_t bits = mask; bits; bits &= bits - 1u) {
+        const uint32_t b = __builtin_ctz(bits);
+        const uint32_t rule = g * 32u + b;
+        const uint32_t base = uni(A.rule_off[rule]);
+        const uint32_t len = uni(A.rule_off[rule + 1]) - base;
+        const uint32_t code = run_rule<false>(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, 0u, live, rule, rep, regs, tid);
+        if (live) {
+            m |= code == PC_TRUE ? 1u << b : 0u;
+            e |= code >= PC_ERROR ? 1u << b : 0u;
+        }
+    }
+    *(uint2*)(A.vt_tm + 2u * ((uint64_t)tb + (uint64_t)j * cap + k)) = make_uint2(m, e);
+}
+
+// Fill chunks with value-class merge entries: as mxp_fill_kernel (words of uniform indexed groups
+// depend on their guard column's kind), plus the class words of each request.  A lane owns 4
+// consecutive requests (one 16-byte store per plane and group), a wave 256, a workgroup 1024; the
+// requests' classes are loaded once (4 x u16 per active column) and kept in registers.
+extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uni(threadIdx.x >> 6);
+    const mxp_fill* F = A.fills + blockIdx.y;
+    const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
+    const uint64_t N = A.n;
+    const uint32_t Q1 = A.q1;
+    const uint32_t qw = A.q0 + (blockIdx.x * 4u + wave) * 256u;
+    if (qw >= Q1) return;
+    const uint32_t q0 = qw + lane * 4u;
+    const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0 && (q0 & 3u) == 0;
+    const uint32_t nvt = uni(A.n_vt);
+    uint32_t bad[4];
+    uint64_t cl[MXP_VT_MAX];  // 4 x u16 classes per active column
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const bool in = q0 + r < Q1;
+        const uint32_t k = in ? A.kinds[(uint64_t)col * N + q0 + r] : 0u;
+        bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
+    }
+#pragma unroll
+    for (uint32_t a = 0; a < MXP_VT_MAX; a++) {
+        cl[a] = 0;
+        if (a < nvt) {
+            const uint16_t* C = A.vt_cls + (uint64_t)a * N;
+            if (vec && q0 < Q1) {
+                cl[a] = *(const uint64_t*)(C + q0);
+            } else {
+                for (uint32_t r = 0; r < 4; r++)
+                    if (q0 + r < Q1) cl[a] |= (uint64_t)C[q0 + r] << (16u * r);
+            }
+        }
+    }
+    const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
+    const bool nt = !(A.flags & 128u);
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    // the active slots' (cap, tbase), the chunk's group masks and merge entries: one vector load
+    // each, read back with v_readlane -- no chain of dependent scalar loads per group
+    const uint32_t MV = lane < 2u * MXP_VT_MAX && (lane >> 1) < nvt ? A.vt_meta[(lane >> 1) * 8u + MXP_VTM_CAP + (lane & 1u)] : 0u;
+    const uint32_t FM = lane < n ? A.fill_masks[moff + lane] : 0u;
+    const uint32_t GO = lane <= n ? A.gvt_off[g0 + lane] : 0u;
+    const uint32_t e0 = __builtin_amdgcn_readlane(GO, 0), ecount = __builtin_amdgcn_readlane(GO, n) - e0;
+    uint32_t GE0 = lane < ecount ? A.gvt[e0 + lane] : 0u, GE1 = lane + 64u < ecount ? A.gvt[e0 + 64u + lane] : 0u;
+    for (uint32_t g = 0; g < n; g++) {
+        const uint32_t G = g0 + g;
+        const uint32_t mask = __builtin_amdgcn_readlane(FM, g);
+        uint32_t m[4] = {0u, 0u, 0u, 0u}, e[4], ve[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int r = 0; r < 4; r++) e[r] = bad[r] & mask;
+        if (A.errlog && any && mask)
+            for (uint32_t r = 0; r < 4; r++)
+                if (e[r] && q0 + r < Q1) log_guard_errors(A, e[r], G * 32u, q0 + r);
+        const uint32_t i0 = __builtin_amdgcn_readlane(GO, g) - e0, i1 = __builtin_amdgcn_readlane(GO, g + 1) - e0;
+        for (uint32_t i = i0; i < i1; i++) {
+            const uint32_t ent = i < 64u ? __builtin_amdgcn_readlane(GE0, i)
+                                 : i < 128u ? __builtin_amdgcn_readlane(GE1, i - 64u) : uni(A.gvt[e0 + i]);
+            const uint32_t a = ent >> 24, j = ent & 0xFFFFFFu;
+            const uint32_t cap = __builtin_amdgcn_readlane(MV, 2u * a), tb = __builtin_amdgcn_readlane(MV, 2u * a + 1u);
+            uint64_t c = cl[0];
+#pragma unroll
+            for (uint32_t x = 1; x < MXP_VT_MAX; x++) c = a == x ? cl[x] : c;
+            const uint64_t row = (uint64_t)tb + (uint64_t)j * cap;
+#pragma unroll
+            for (uint32_t r = 0; r < 4; r++) {
+                const uint2 w = *(const uint2*)(A.vt_tm + 2u * (row + ((c >> (16u * r)) & 0xFFFFu)));
+                m[r] |= w.x;
+                ve[r] |= w.y;
+            }
+        }
+        uint32_t vmask[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            vmask[r] = q0 + r < Q1 ? ~0u : 0u;
+            e[r] |= ve[r];
+        }
+        if (A.errlog) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int r = 0; r < 4; r++) c += (uint32_t)__builtin_popcount(ve[r] & vmask[r]);
+            vt_count_n(A, c);
+        }
+        if (A.hits) {
+            uint32_t u = 0;
+#pragma unroll
+            for (int r = 0; r < 4; r++) u |= m[r] & vmask[r];
+            for (uint32_t bits = wave_or(u); bits; bits &= bits - 1u) {
+                const uint32_t k = __builtin_ctz(bits);
+                uint32_t cnt = 0;
+#pragma unroll
+                for (int r = 0; r < 4; r++) cnt += (uint32_t)__builtin_popcountll(__ballot(((m[r] & vmask[r]) >> k) & 1u));
+                if (lane == 0) atomicAdd(A.hits + G * 32u + k, (unsigned long long)cnt);
+            }
+        }
+        const uint64_t at = (uint64_t)G * N + q0;
+        if (vec && q0 < Q1) {
+            const v4u mv = v4u{m[0], m[1], m[2], m[3]};
+            const v4u ev = v4u{e[0], e[1], e[2], e[3]};
+            if (nt) {
+                if (A.out_match) __builtin_nontemporal_store(mv, (v4u*)(A.out_match + at));
+                if (A.out_err) __builtin_nontemporal_store(ev, (v4u*)(A.out_err + at));
+            } else {
+                if (A.out_match) *(v4u*)(A.out_match + at) = mv;
+                if (A.out_err) *(v4u*)(A.out_err + at) = ev;
+            }
+        } else {
+            for (uint32_t r = 0; r < 4; r++) {
+                if (q0 + r >= Q1) break;
+                if (A.out_match) A.out_match[at + r] = m[r];
+                if (A.out_err) A.out_err[at + r] = e[r];
             }
         }
     }
@@ -1328,6 +1621,23 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s) {
     const uint32_t per_block = 1024u * (args->fill_span ? args->fill_span : 1u);
     hipLaunchKernelGGL(mxp_fill_kernel, dim3((args->q1 - args->q0 + per_block - 1) / per_block, n_fills), dim3(256), 0, s, *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_vtfill_kernel, dim3((args->q1 - args->q0 + 1023u) / 1024u, n_fills), dim3(256), 0, s, *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_vt_classify_kernel, dim3((args->q1 - args->q0 + MXP_VTC_REQ - 1u) / MXP_VTC_REQ), dim3(256), 0, s,
+                       *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_vt_eval(const mxp_kargs* args, uint32_t tiles, uint32_t wchunks, hipStream_t s) {
+    if (!tiles || !wchunks) return hipSuccess;
+    hipLaunchKernelGGL(mxp_vt_eval_kernel, dim3(tiles, wchunks), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

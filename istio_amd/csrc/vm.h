@@ -144,13 +144,24 @@ typedef struct mxp_hent {
 #define MXP_CC 8u
 typedef struct mxp_fill {
     uint32_t col;
-    uint32_t okset;    // bits 0..15: kinds that pass; bits 24..31: want class / GK_VCOL
+    uint32_t okset;    // bits 0..15: kinds that pass; bits 24..31: want class / GK_VCOL (0xFFFF: every kind)
     uint32_t g0;
     uint32_t n;
-    uint32_t all;
-    uint32_t last;
+    uint32_t moff;     // kargs.fill_masks[moff + i]: rules of group g0 + i this chunk writes
+    uint32_t vt;       // 1: some group has value-class merge entries (mxp_vtfill_kernel)
     uint32_t pad[2];
 } mxp_fill;
+
+// Value classes (kernels.hip mxp_vt_*): at most MXP_VT_MAX columns per batch; per active slot a
+// kargs.vt_meta[a * 8 + MXP_VTM_*]
+#define MXP_VT_MAX 8
+#define MXP_VTM_COL 0    // column
+#define MXP_VTM_CAP 1    // class table capacity (power of two >= 64): classes are its slots
+#define MXP_VTM_TBASE 2  // first (match, error) word pair in kargs.vt_tm: word j of class k at tbase + j * cap + k
+#define MXP_VTM_KBASE 3  // first entry in kargs.vt_keys / vt_rep
+#define MXP_VTM_NW 4     // bitmap words holding the slot's rules
+#define MXP_VTM_WOFF 5   // first (group, rule mask) pair in kargs.vt_words
+#define MXP_VT_EMPTY 0xFFFFFFFFFFFFFFFFull
 
 // dense-rule injection slots (mxp_inject_kernel): 16 dwords = dense-id mask (2), bitmap word,
 // entry count, up to 12 entries (bit | dense id << 5); a word with more entries takes several slots
@@ -196,6 +207,12 @@ static inline MXP_HD uint32_t mxp_hash64(uint64_t k) {
     k *= 0xc4ceb9fe1a85ec53ull;
     k ^= k >> 33;
     return (uint32_t)k;
+}
+
+// class key of a column value: the value itself matters only for kind 1 (MXP_STRING / VC_VALUE,
+// a string id); every other kind is one class per kind
+static inline MXP_HD uint64_t mxp_vt_key(uint32_t kind, uint64_t v) {
+    return kind == 1u ? ((1ull << 32) | (uint32_t)v) : ((uint64_t)kind << 32);
 }
 
 // Continuation templates: the continuations (code from the guard's cont pc) of many rules differ

@@ -218,10 +218,10 @@ class Engine:
 
     def ruleset_info(self) -> dict:
         """Kernel-side shape of the rule set (guards, continuation templates, column segments)."""
-        out = (ctypes.c_uint32 * 9)()
-        k = self.lib.mxp_ruleset_info(self.h, out, 9)
+        out = (ctypes.c_uint32 * 10)()
+        k = self.lib.mxp_ruleset_info(self.h, out, 10)
         return dict(zip(("guarded", "templated", "templates", "segments", "indexed", "columns", "composite",
-                         "aliases", "dense"), list(out)[:k]))
+                         "aliases", "dense", "value_class_columns"), list(out)[:k]))
 
     # ------------------------------------------------------------------ evaluation
     def eval_batch(self, batch: BagBatch):
