@@ -321,6 +321,10 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out);
  * evaluates its rules once per distinct value).  Returns the number of values written (<= cap). */
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap);
 uint32_t mxp_dbatch_requests(const mxp_dbatch* db);
+/* Profiling hook (engine created with MXP_WAVE_TIMES set): per wavefront of the last guard-index
+ * kernel launch, {start, end, XCC} (wall_clock64 ticks, 100 MHz), 3 x u64 per wave; *n_out = values
+ * written.  MXP_ERR_STATE when the hook is off. */
+int mxp_debug_wave_times(mxp_engine* eng, uint64_t* out, uint64_t cap, uint64_t* n_out);
 
 #ifdef __cplusplus
 }

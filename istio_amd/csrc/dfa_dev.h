@@ -46,14 +46,23 @@ __device__ __forceinline__ bool mxp_dfa_run(const mxp_dfa_set& S, uint32_t dfa, 
     uint32_t st = H.start;
     uint32_t i = H.skip;
     if (i == MXP_DFA_DECIDED) return true;
+    // ASCII bytes come out of the aligned 8-byte word that holds them: one subject load per 8 steps
+    // (the pools and symbol blobs are readable to the aligned word past their end)
+    uintptr_t wa = ((uintptr_t)(s + i)) & ~(uintptr_t)7;
+    uint64_t win = *(const uint64_t*)wa;
     while (i < n) {
-        const uint64_t w = mxp_ld8(s + i);  // bytes i .. i+7 (only those < n are used)
-        const uint32_t c0 = (uint32_t)(w & 0xFF);
+        const uintptr_t a = (uintptr_t)(s + i);
+        if ((a & ~(uintptr_t)7) != wa) {
+            wa = a & ~(uintptr_t)7;
+            win = *(const uint64_t*)wa;
+        }
+        const uint32_t c0 = (uint32_t)(win >> ((a & 7u) * 8u)) & 0xFFu;
         uint32_t cls;
         if (c0 < 0x80) {
             cls = asc[c0];
             i++;
         } else {
+            const uint64_t w = mxp_ld8(s + i);  // bytes i .. i+7 (only those < n are used)
             const uint32_t left = n - i;
             const uint32_t b1 = (uint32_t)(w >> 8) & 0xFF, b2 = (uint32_t)(w >> 16) & 0xFF, b3 = (uint32_t)(w >> 24) & 0xFF;
             uint32_t r = 0xFFFD, width = 1;

@@ -1338,6 +1338,12 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
             return hipfail(e, "dense masks");
         A.dense_cm = d_dense_cm.as<uint64_t>();
     }
+    if (wave_times) {  // profiling hook (MXP_WAVE_TIMES): per index-kernel wave start / end
+        const size_t need = ((size_t)A.n + 63) / 64 * 24;
+        if (d_wave_t.n < need && (e = d_wave_t.alloc(need)) != hipSuccess) return hipfail(e, "wave times");
+        A.wave_t = d_wave_t.as<unsigned long long>();
+        wave_t_n = (A.n + 63) / 64;
+    }
     if (A.n_vt) {
         // value classes: classify every request of [lo, hi) per active column, then evaluate the
         // columns' rules once per class (class records -> errcount[2], the host expands them)
@@ -1534,6 +1540,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_FILL_CHUNK")) e->fill_chunk = (uint32_t)std::max(1, atoi(f));
     if (const char* f = getenv("MXP_FILL_SPAN")) e->fill_span = (uint32_t)std::min(8, std::max(1, atoi(f)));
     if (const char* f = getenv("MXP_ERRCAP")) e->errcap = (uint32_t)std::max(1, atoi(f));
+    if (getenv("MXP_WAVE_TIMES")) e->wave_times = true;
     if (device < 0) {  // host-only engine (compiler / lowering inspection without a GPU)
         e->reset_tables();
         *out = e;
@@ -1647,6 +1654,19 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) 
         return eng->hipfail(e, "elapsed");
     uint32_t k = 0;
     for (; k < cap && k < 2; k++) ms[k] = t[k];
+    *n_out = k;
+    return MXP_OK;
+}
+
+int mxp_debug_wave_times(mxp_engine* eng, uint64_t* out, uint64_t cap, uint64_t* n_out) {
+    if (!eng || !out || !n_out) return MXP_ERR_ARG;
+    *n_out = 0;
+    if (!eng->wave_times || !eng->d_wave_t.p) return eng->fail(MXP_ERR_STATE, "MXP_WAVE_TIMES not set");
+    hipError_t e;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return eng->hipfail(e, "sync");
+    const uint64_t k = std::min<uint64_t>(cap, (uint64_t)eng->wave_t_n * 3);
+    if (k && (e = hipMemcpy(out, eng->d_wave_t.p, k * 8, hipMemcpyDeviceToHost)) != hipSuccess)
+        return eng->hipfail(e, "download wave times");
     *n_out = k;
     return MXP_OK;
 }

@@ -411,6 +411,9 @@ struct mxp_engine : public mxp::LowerTables {
     void fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) const;
     int vt_prepare(mxp_dbatch* db, const Plan& P);
     uint32_t last_mask = 0;  // value-class slots of the last launch
+    bool wave_times = false;  // MXP_WAVE_TIMES: index kernel waves record {start, end, XCC}
+    DevBuf d_wave_t;
+    uint32_t wave_t_n = 0;
     // requests [q_lo, q_hi) of the batch (default: all); q_lo a multiple of 4
     int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
                unsigned long long* d_hits = nullptr, uint64_t* d_stats = nullptr, uint32_t q_lo = 0,

@@ -95,4 +95,5 @@ typedef struct mxp_kargs {
     uint32_t* vt_rep;
     uint32_t n_vt;
     uint32_t pad6;
+    unsigned long long* wave_t;  // profiling (MXP_WAVE_TIMES): index kernel waves' {start, end, pairs}
 } mxp_kargs;

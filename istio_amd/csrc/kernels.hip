@@ -1325,6 +1325,7 @@ namespace {
 
 template <bool kRefs>
 __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
+    const uint64_t t_start = A.wave_t ? (uint64_t)wall_clock64() : 0ull;
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
     PairQueue Q{wave, 0u, 0u, A.q0 + (blockIdx.x * 4u + wave) * 64u};
@@ -1428,6 +1429,12 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) t += (uint32_t)__shfl_xor((int)t, off, 64);
         if ((tid & 63u) == 0 && t) atomicAdd((unsigned long long*)A.stats, (unsigned long long)t);
+    }
+    if (A.wave_t && (tid & 63u) == 0) {  // profiling: this wave's start / end (100 MHz clock), XCC
+        const uint64_t w = (uint64_t)blockIdx.x * 4u + wave;
+        A.wave_t[3 * w] = t_start;
+        A.wave_t[3 * w + 1] = (uint64_t)wall_clock64();
+        A.wave_t[3 * w + 2] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // hwreg(XCC_ID, 0, 4)
     }
 }
 

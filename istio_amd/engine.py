@@ -87,6 +87,7 @@ SIGNATURES = {
     "mxp_set_pipeline": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32]),
     "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
+    "mxp_debug_wave_times": (ctypes.c_int, [_VP, _VP, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
 }
 
 _LIB = None
@@ -106,6 +107,8 @@ def load_library(path: str = LIB_PATH):
             pass
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("MXP_LIB") and not hasattr(lib, name):
+                continue  # an older build under A/B (tools/ab_libs.sh): entry points it predates
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args
@@ -215,6 +218,15 @@ class Engine:
         n = ctypes.c_uint32()
         self._check(self.lib.mxp_kernel_times(self.h, ms, 2, ctypes.byref(n)), "mxp_kernel_times")
         return list(ms)[: n.value]
+
+    def wave_times(self, n_waves: int) -> np.ndarray:
+        """Profiling hook (MXP_WAVE_TIMES=1 at engine creation): [waves, 3] {start, end, XCC} of the
+        last guard-index kernel launch (100 MHz ticks)."""
+        out = np.zeros(3 * n_waves, dtype=np.uint64)
+        k = ctypes.c_uint64()
+        self._check(self.lib.mxp_debug_wave_times(self.h, out.ctypes.data, out.size, ctypes.byref(k)),
+                    "mxp_debug_wave_times")
+        return out[:k.value].reshape(-1, 3)
 
     def ruleset_info(self) -> dict:
         """Kernel-side shape of the rule set (guards, continuation templates, column segments)."""

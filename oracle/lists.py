@@ -109,24 +109,39 @@ class IPList:
 
 class RegexList:
     """parseRegexList (regexList.go:44-65): non-empty lines then overrides, each regexp.Compile'd
-    (the first error fails the list); checkList: any pattern matches (Go regexp restatement)."""
+    (the first error fails the list); checkList: any pattern matches (Go regexp restatement in C,
+    oracle/goregex.c, OpenMP over symbols)."""
 
     def __init__(self, lines, overrides=()):
-        import goregex
-        self.progs = []
-        for p in [x for x in lines if _b(x)] + list(overrides):
-            try:
-                self.progs.append(goregex.compile(_b(p)))
-            except goregex.RegexError as e:
-                raise ListParseError(str(e))
+        self.pats = [_b(p) for p in [x for x in lines if _b(x)] + list(overrides)]
+        if self.pats:  # compile errors surface here, as parseRegexList returns them
+            self._found([b""])
 
     def num_entries(self):
-        return len(self.progs)
+        return len(self.pats)
 
-    def found(self, symbols):
-        import goregex
-        return np.array([1 if any(goregex.match(p, _b(s)) for p in self.progs) else 0 for s in symbols],
-                        dtype=np.int8)
+    def _found(self, symbols, threads=1):
+        import oracle
+        L = oracle.lib()
+        pb, po = _blob(self.pats)
+        sb, so = _blob([_b(s) for s in symbols])
+        out = np.zeros(len(symbols), dtype=np.int8)
+        err = ctypes.create_string_buffer(600)
+        rc = L.oracle_regex_list_found(pb.ctypes.data, po.ctypes.data, len(self.pats), sb.ctypes.data, so.ctypes.data,
+                                       len(symbols), out.ctypes.data, threads, err, len(err))
+        if rc:
+            raise ListParseError(err.value.decode("utf-8", "surrogateescape"))
+        return out
+
+    def found(self, symbols, threads=16):
+        return self._found(symbols, threads)
+
+
+def _blob(items):
+    off = np.zeros(len(items) + 1, dtype=np.uint64)
+    if items:
+        off[1:] = np.cumsum([len(x) for x in items])
+    return np.frombuffer(b"".join(items) + b"\0", dtype=np.uint8), off
 
 
 def codes(found: np.ndarray, blacklist: bool) -> np.ndarray:

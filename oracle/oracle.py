@@ -53,40 +53,8 @@ class _Result(ctypes.Structure):
                 ("v2", ctypes.c_uint32), ("val", _Gv), ("msg", ctypes.c_char * 512)]
 
 
-# `matches`: the C interpreter calls back into the Go regexp restatement (goregex.py)
-_REGEX_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
-                             ctypes.c_void_p, ctypes.c_size_t)
-_RX_CACHE = {}
-
-
-def _regex_py(pat: bytes, subj: bytes):
-    import goregex
-    prog = _RX_CACHE.get(pat)
-    if prog is None:
-        try:
-            prog = goregex.compile(pat)
-        except goregex.RegexError as e:
-            prog = ("err", -1, str(e))
-        except goregex.Unsupported as e:
-            prog = ("err", -2, "unsupported regexp (oracle): %s" % e)
-        _RX_CACHE[pat] = prog
-    if isinstance(prog, tuple):
-        return prog[1], prog[2]
-    return (1 if goregex.match(prog, subj) else 0), ""
-
-
-def _regex_cb_impl(pat, npat, s, n, err, errcap):
-    try:
-        m, msg = _regex_py(ctypes.string_at(pat, npat) if npat else b"", ctypes.string_at(s, n) if n else b"")
-    except Exception as e:  # never unwind through C
-        m, msg = -2, "oracle regex failure: %r" % e
-    if m < 0 and errcap:
-        b = msg.encode("utf-8", "surrogateescape")[: errcap - 1] + b"\0"
-        ctypes.memmove(err, b, len(b))
-    return m
-
-
-_regex_cb = _REGEX_FN(_regex_cb_impl)
+# `matches`: the C interpreter runs the C restatement of Go's regexp (goregex.c); goregex.py is the
+# Python form of the same restatement, kept for the known-answer tests (the two are compared there)
 
 
 def lib():
@@ -108,10 +76,30 @@ def lib():
         L.oracle_referenced.restype = ctypes.c_int64
         L.oracle_referenced.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                         ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64]
-        L.oracle_set_regex_fn.argtypes = [_REGEX_FN]
-        L.oracle_set_regex_fn(_regex_cb)
+        L.oracle_regex_match.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_regex_cache.argtypes = [ctypes.c_int]
+        L.oracle_regex_list_found.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
+                                              ctypes.c_void_p, ctypes.c_size_t]
         _LIB = L
     return _LIB
+
+
+def regex_match(pattern, subject):
+    """regexp.MatchString(pattern, subject) by the C restatement -> (1 | 0 | -1 | -2, error text)."""
+    L = lib()
+    p = pattern.encode("utf-8", "surrogateescape") if isinstance(pattern, str) else bytes(pattern)
+    q = subject.encode("utf-8", "surrogateescape") if isinstance(subject, str) else bytes(subject)
+    err = ctypes.create_string_buffer(600)
+    m = L.oracle_regex_match(p, len(p), q, len(q), err, len(err))
+    return m, err.value.decode("utf-8", "surrogateescape") if m < 0 else ""
+
+
+def regex_cache(on: bool):
+    """The C `matches` compiles each pattern once per thread (on, default) or on every call, as
+    regexp.MatchString does (off: the CPU baseline's faithful cost)."""
+    lib().oracle_regex_cache(1 if on else 0)
 
 
 # mixer/pkg/il/runtime/externs.go:30-39 -- (params, return) il types of the standard externs

@@ -89,3 +89,66 @@ def test_unsupported_is_explicit():
             G.compile(pat)
     G.compile("(?i)\\W")  # full non-ASCII coverage: folds only the k / s partners
     assert G.match(G.compile("(?i)\\W"), "k")
+
+
+# ---- the C restatement (oracle/goregex.c, what the C interpreter and the CPU baseline run) against
+# this Python one: same answers, same error texts, same Unsupported line
+def _c(pat, subj=""):
+    import oracle
+    return oracle.regex_match(pat, subj)
+
+
+@pytest.mark.parametrize("pat,subj,want", GOLDEN + KAT)
+def test_c_restatement_known_answers(pat, subj, want):
+    assert _c(pat, subj) == (1 if want else 0, ""), (pat, subj)
+
+
+@pytest.mark.parametrize("pat,msg", ERRORS)
+def test_c_restatement_error_texts(pat, msg):
+    assert _c(pat) == (-1, "error parsing regexp: " + msg)
+
+
+def test_c_restatement_unsupported():
+    for pat in ["\\pL", "\\p{Greek}", "(?i)é", "(?i)[à-ÿ]"]:
+        assert _c(pat)[0] == -2, pat
+    assert _c("(?i)\\W", "k")[0] == 1
+
+
+def _random_pattern(rng, depth=0):
+    atoms = ["a", "b", "ab", ".", "\\d", "\\w", "\\s", "[a-c]", "[^b]", "[[:alpha:]]", "\\b", "^", "$", "(?i)a",
+             "é", "\\x41", "[a-]", "x{2}", "\\.", "(?m)^a", "\\z", "\\A", "[\\d_]", "k", "(?s).", "\\Qa.\\E",
+             "\xff", "(", ")", "[", "*", "{1,", "\\", "a{3,2}", "(?P<n>a)", "(?:b)", "|"]
+    out = []
+    for _ in range(int(rng.integers(1, 5))):
+        r = rng.random()
+        if r < 0.2 and depth < 2:
+            out.append("(" + _random_pattern(rng, depth + 1) + ")")
+        elif r < 0.3 and depth < 2:
+            out.append(_random_pattern(rng, depth + 1) + "|" + _random_pattern(rng, depth + 1))
+        else:
+            out.append(atoms[int(rng.integers(0, len(atoms)))])
+        if rng.random() < 0.3:
+            out.append(["*", "+", "?", "{1,2}", "*?", "{2}"][int(rng.integers(0, 6))])
+    return "".join(out)
+
+
+def test_c_restatement_random_patterns_match_python():
+    import numpy as np
+    rng = np.random.default_rng(5)
+    subjects = ["", "a", "ab", "abc", "a\nb", "xyz123", "Ab_9 c", "é", "\udcff", "k", "K", "aaab", "a.b", "  "]
+    n_ok = n_err = 0
+    for _ in range(1500):
+        pat = _random_pattern(rng)
+        try:
+            prog = G.compile(pat)
+        except G.RegexError as e:
+            assert _c(pat) == (-1, str(e)), pat
+            n_err += 1
+            continue
+        except G.Unsupported:
+            assert _c(pat)[0] == -2, pat
+            continue
+        for s in subjects:
+            assert _c(pat, s) == (1 if G.match(prog, s) else 0, ""), (pat, s)
+        n_ok += 1
+    assert n_ok > 500 and n_err > 100
