@@ -59,6 +59,8 @@ def parse():
                    help="c2 (default, the BASELINE metric; + a C4 block); c4 route rules; c5 = C2 predicates + "
                         "memquota with one combined all-reduce; C3 lists; c5-quota memquota alone")
     p.add_argument("--list-entries", type=int, default=100_000)
+    p.add_argument("--error-output", default="compact", choices=["compact", "bitmap"],
+                   help="compact: per-request error flags (a Resolve's view); bitmap: the full error bitmap")
     return p.parse_args()
 
 
@@ -354,7 +356,19 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     R, N = len(rules), batch.n
     Wd = (R + 31) // 32
     d_match = torch.empty((Wd, N), dtype=torch.int32, device=dev)
-    d_err = torch.empty((Wd, N), dtype=torch.int32, device=dev)
+    # error output: per-request error flags (compact, default; what a Resolve needs) or the full
+    # error bitmap (--error-output bitmap; the parity tests' reference form)
+    compact = args.error_output == "compact"
+    d_err = torch.empty((Wd, N) if not compact else (1,), dtype=torch.int32, device=dev)
+    d_req_err = torch.empty(N if compact else 1, dtype=torch.uint8, device=dev)
+
+    def evaluate(hits_ptr):
+        if compact:
+            db.eval_compact(d_match.data_ptr(), d_req_err.data_ptr(), hits_ptr, sh)
+        elif hits_ptr:
+            db.eval_hits(d_match.data_ptr(), d_err.data_ptr(), hits_ptr, sh)
+        else:
+            db.eval(d_match.data_ptr(), d_err.data_ptr(), sh)
     stream = torch.cuda.Stream(dev)  # a real (non-null) HIP stream shared by libmxp, events and RCCL
     torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
@@ -369,7 +383,7 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
         views = ctr.views()
         if ev0 is not None:
             ev0.record(stream)
-        db.eval_hits(d_match.data_ptr(), d_err.data_ptr(), views[0].data_ptr(), sh)
+        evaluate(views[0].data_ptr())
         if quota is not None:
             (_, q, (dk, da, dbe, dg)) = quota
             q.alloc_device(dk.numel(), dk.data_ptr(), da.data_ptr(), dbe.data_ptr(), now[0], sh, dg.data_ptr(),
@@ -388,7 +402,7 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     eng.set_timing(True)
     per = []
     for _ in range(args.steps):
-        db.eval(d_match.data_ptr(), d_err.data_ptr(), sh)
+        evaluate(0)
         per.append(eng.kernel_times())
     eng.set_timing(False)
     k_eval = float(np.mean([p[0] for p in per]))
@@ -396,10 +410,11 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     eval_ms = k_eval + k_index
 
     # algorithmic bytes of one evaluation: every referenced column read once per
-    # request (kind u8 + value u64), the rule tables, and the two output bitmaps written
+    # request (kind u8 + value u64), the rule tables, the match bitmap and the error output written
+    # (the error bitmap, or one flag byte per request in compact mode)
     n_cols = eng.ruleset_info()["columns"]
     prog_bytes = 16 * sum(eng.rule_vm_text(i).count("\n") for i in range(R)) + 4 * (R + 1)
-    alg_bytes = N * n_cols * 9 + prog_bytes + 2 * N * Wd * 4
+    alg_bytes = N * n_cols * 9 + prog_bytes + N * Wd * 4 + (N if compact else N * Wd * 4)
     achieved = alg_bytes / (eval_ms * 1e-3) / 1e9
     traffic = measured_traffic(kind, R, N)
 
@@ -422,6 +437,7 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
         "kernels_ms": {"mxp_fill_kernel+mxp_guard2_kernel+mxp_eval_kernel": k_eval,
                        "mxp_index_kernel+mxp_inject_kernel": k_index},
         "pack_upload_s": t_pack,
+        "error_output": "per-request flags (compact)" if compact else "error bitmap",
         "lds_bank_conflicts": lds_conflicts(kind),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -443,7 +459,7 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
             sample = W.c2_workload(n_rules=args.rules, n_requests=min(N, 1 << 18), seed=2)[2]
             out["cpu_baseline"] = cpu_baseline(manifest, rules, sample, args.cpu_sample_seconds, args.cpu_threads)
     db.free()
-    del d_match, d_err
+    del d_match, d_err, d_req_err
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return out

@@ -291,6 +291,12 @@ int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_
  * the match bits -- the bitmap is not read back).  Same result as mxp_hits_device afterwards. */
 int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err,
                                unsigned long long* d_hits);
+/* Compact error output: as mxp_batch_eval_device_hits without the error bitmap -- d_req_err[q]
+ * (device u8[n_requests], cleared by the call) = 1 when some rule fails for request q, which is all a
+ * Resolve needs to know that the request errs (resolver.go:225-227); the failing pairs and their texts
+ * come from mxp_eval_batch / mxp_resolve_batch.  d_hits may be NULL (no counters). */
+int mxp_batch_eval_device_compact(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match,
+                                  uint8_t* d_req_err, unsigned long long* d_hits);
 /* Per-rule hit counters: d_hits[rule] += number of requests whose predicate was true (device u64[n_rules]). */
 int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_requests, void* stream,
                     unsigned long long* d_hits);

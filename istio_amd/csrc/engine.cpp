@@ -626,7 +626,8 @@ int mxp_engine::build_plan(Plan& P) {
             P.n_gfill++;
             continue;
         }
-        (G.vm ? gvm : glean).push_back(g);
+        // the lean kernels carry no value-class merge: such groups go to the VM kernel
+        (G.vm || has_vt ? gvm : glean).push_back(g);
     }
     // chunks with value-class merge entries go to mxp_vtfill_kernel
     std::vector<mxp_fill> vtfills;
@@ -1266,6 +1267,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     if (mask && (rc = vt_prepare(db, *P))) return rc;
     mxp_kargs A;
     fill_args(&A, db, *P);
+    A.req_err = req_err_out;
     A.hits = d_vals ? nullptr : d_hits;
     A.stats = d_vals ? nullptr : stats;
     A.out_match = d_match;
@@ -1725,11 +1727,20 @@ int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_
     return eng->launch(db, s, d_match, d_err, nullptr, false);
 }
 
-int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err,
-                               unsigned long long* d_hits) {
-    if (!eng || !db || !d_match || !d_err || !d_hits) return MXP_ERR_ARG;
+// device evaluation with fused or streamed hit counters; error output as a bitmap (d_err) or as
+// per-request flags (d_req_err, compact)
+static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err,
+                            uint8_t* d_req_err, unsigned long long* d_hits) {
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     hipError_t e;
+    if (d_req_err && db->n && (e = hipMemsetAsync(d_req_err, 0, db->n, s)) != hipSuccess)
+        return eng->hipfail(e, "request error flags reset");
+    if (!d_hits) {
+        eng->req_err_out = d_req_err;
+        const int rc = eng->launch(db, s, d_match, d_err, nullptr, false);
+        eng->req_err_out = nullptr;
+        return rc;
+    }
     if (!eng->h_stats) {
         if ((e = eng->d_stats.alloc(8)) != hipSuccess) return eng->hipfail(e, "stats");
         if ((e = hipHostMalloc((void**)&eng->h_stats, 8, hipHostMallocDefault)) != hipSuccess) {
@@ -1757,7 +1768,9 @@ int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, ui
     if (eng->stats_pending && (e = hipStreamWaitEvent(s, eng->stats_ev, 0)) != hipSuccess)
         return eng->hipfail(e, "stats wait");
     if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
+    eng->req_err_out = d_req_err;
     int rc = eng->launch(db, s, d_match, d_err, nullptr, false, fused ? d_hits : nullptr, eng->d_stats.as<uint64_t>());
+    eng->req_err_out = nullptr;
     if (rc) return rc;
     if (!fused && R && db->n && (e = mxp_launch_hits(d_match, db->n, R, W, d_hits, s)) != hipSuccess)
         return eng->hipfail(e, "launch hits");
@@ -1767,6 +1780,18 @@ int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, ui
     eng->stats_pending = true;
     eng->stats_n = db->n;
     return MXP_OK;
+}
+
+int mxp_batch_eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err,
+                               unsigned long long* d_hits) {
+    if (!eng || !db || !d_match || !d_err || !d_hits) return MXP_ERR_ARG;
+    return eval_device_hits(eng, db, stream, d_match, d_err, nullptr, d_hits);
+}
+
+int mxp_batch_eval_device_compact(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match,
+                                  uint8_t* d_req_err, unsigned long long* d_hits) {
+    if (!eng || !db || !d_match || !d_req_err) return MXP_ERR_ARG;
+    return eval_device_hits(eng, db, stream, d_match, nullptr, d_req_err, d_hits);
 }
 
 int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_requests, void* stream,

@@ -411,6 +411,7 @@ struct mxp_engine : public mxp::LowerTables {
     void fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) const;
     int vt_prepare(mxp_dbatch* db, const Plan& P);
     uint32_t last_mask = 0;  // value-class slots of the last launch
+    uint8_t* req_err_out = nullptr;  // compact error output of the next launch (kargs.req_err)
     bool wave_times = false;  // MXP_WAVE_TIMES: index kernel waves record {start, end, XCC}
     DevBuf d_wave_t;
     uint32_t wave_t_n = 0;

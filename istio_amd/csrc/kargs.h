@@ -96,4 +96,5 @@ typedef struct mxp_kargs {
     uint32_t n_vt;
     uint32_t pad6;
     unsigned long long* wave_t;  // profiling (MXP_WAVE_TIMES): index kernel waves' {start, end, pairs}
+    uint8_t* req_err;            // optional [n]: 1 when some rule fails for the request (compact error output)
 } mxp_kargs;

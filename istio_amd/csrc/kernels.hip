@@ -130,6 +130,7 @@ __device__ __forceinline__ uint32_t set_true(const mxp_kargs& A, uint32_t rule, 
 
 // an error pair found by the guard-index kernel, with its aliases
 __device__ __forceinline__ void set_error(const mxp_kargs& A, uint32_t rule, uint32_t req) {
+    if (A.req_err) A.req_err[req] = 1;
     if (!A.out_err) return;
     atomicOr(A.out_err + (uint64_t)(rule >> 5) * A.n + req, 1u << (rule & 31u));
     if (A.alias_off)
@@ -654,7 +655,7 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
                     }
                 }
             }
-            if (A.gvt_off) {  // value-class rules of the group (after the guard errors were logged)
+            if (kVM && A.gvt_off) {  // value-class rules of the group (after the guard errors were logged)
                 uint32_t vm, ve;
                 vt_words_of(A, g, req, valid, vm, ve);
                 vt_count_errors(A, ve);
@@ -664,6 +665,7 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
             if (valid) {
                 if (A.out_match) A.out_match[(uint64_t)g * N + req] = m;
                 if (A.out_err) A.out_err[(uint64_t)g * N + req] = e;
+                if (A.req_err && e) A.req_err[req] = 1;
             }
             if (A.hits) {
                 // fused hit counters: per rule of the group, the lanes whose match bit is set
@@ -784,26 +786,18 @@ extern "C" __global__ __launch_bounds__(256) void mxp_guard2_kernel(mxp_kargs A)
 #undef GF
             uint32_t ma = (eqa ^ neg) & (only | orm) & oka, mb = (eqb ^ neg) & (only | orm) & okb;
             uint32_t ea = guarded & ~oka, eb = guarded & ~okb;
+            // (groups with value-class rules never come here: build_plan routes them to the VM kernel)
             if (va && A.errlog && ea) log_guard_errors(A, ea, r0, reqa);
             if (vb && A.errlog && eb) log_guard_errors(A, eb, r0, reqb);
-            if (A.gvt_off) {  // value-class rules of the group
-                uint32_t vma, vea, vmb, veb;
-                vt_words_of(A, g, reqa, va, vma, vea);
-                vt_words_of(A, g, reqb, vb, vmb, veb);
-                vt_count_errors(A, vea);
-                vt_count_errors(A, veb);
-                ma |= vma;
-                ea |= vea;
-                mb |= vmb;
-                eb |= veb;
-            }
             if (va) {
                 if (A.out_match) A.out_match[(uint64_t)g * N + reqa] = ma;
                 if (A.out_err) A.out_err[(uint64_t)g * N + reqa] = ea;
+                if (A.req_err && ea) A.req_err[reqa] = 1;
             }
             if (vb) {
                 if (A.out_match) A.out_match[(uint64_t)g * N + reqb] = mb;
                 if (A.out_err) A.out_err[(uint64_t)g * N + reqb] = eb;
+                if (A.req_err && eb) A.req_err[reqb] = 1;
             }
             if (A.hits) {
                 const uint32_t m2a = va ? ma : 0u, m2b = vb ? mb : 0u;
@@ -861,6 +855,14 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
             }
         }
         any |= bad[sp][0] | bad[sp][1] | bad[sp][2] | bad[sp][3];
+    }
+    if (A.req_err && any) {  // a failed type check errs every rule of the chunk's groups
+        uint32_t masks = 0;
+        for (uint32_t g = 0; g < n; g++) masks |= uni(A.fill_masks[moff + g]);
+        if (masks)
+            for (uint32_t sp = 0; sp < span; sp++)
+                for (uint32_t r = 0; r < 4; r++)
+                    if (bad[sp][r] && q0 + sp * 256u + r < Q1) A.req_err[q0 + sp * 256u + r] = 1;
     }
     if (A.errlog && any) {
         for (uint32_t g = 0; g < n; g++) {
@@ -1129,6 +1131,9 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A)
                 if (lane == 0) atomicAdd(A.hits + G * 32u + k, (unsigned long long)cnt);
             }
         }
+        if (A.req_err)
+            for (uint32_t r = 0; r < 4; r++)
+                if (e[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;
         const uint64_t at = (uint64_t)G * N + q0;
         if (vec && q0 < Q1) {
             const v4u mv = v4u{m[0], m[1], m[2], m[3]};

@@ -83,6 +83,7 @@ SIGNATURES = {
                                               ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_void_p]),
     "mxp_batch_eval_device_hits": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
+    "mxp_batch_eval_device_compact": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP]),
     "mxp_set_timing": (ctypes.c_int, [_VP, ctypes.c_int]),
     "mxp_set_pipeline": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32]),
     "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
@@ -439,6 +440,13 @@ class DeviceBatch:
         e = self.engine
         e._check(e.lib.mxp_batch_eval_device_hits(e.h, self.h, _VP(stream or None), _VP(d_match), _VP(d_err),
                                                   _VP(d_hits)), "mxp_batch_eval_device_hits")
+
+    def eval_compact(self, d_match: int, d_req_err: int, d_hits: int = 0, stream: int = 0):
+        """eval_hits() with compact error output: no error bitmap, d_req_err[q] (device u8) = 1 when some
+        rule fails for request q; d_hits 0 = no counters."""
+        e = self.engine
+        e._check(e.lib.mxp_batch_eval_device_compact(e.h, self.h, _VP(stream or None), _VP(d_match), _VP(d_req_err),
+                                                     _VP(d_hits or None)), "mxp_batch_eval_device_compact")
 
     def free(self):
         if self.h:

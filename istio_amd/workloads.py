@@ -448,9 +448,10 @@ def c3_string_list(n_entries=100_000, n_lookups=1_000_000, seed=3, hit_rate=0.5)
     return entries, syms
 
 
-def c3_regex_list(n_patterns=10_000, n_lookups=1_000_000, seed=3, hit_rate=0.5):
+def c3_regex_list(n_patterns=10_000, n_lookups=1_000_000, seed=3, hit_rate=0.5, return_hits=False):
     """C3 regex list: patterns `^prefix[a-z0-9]{m,n}(suffix)?$`; lookups half built
-    to match a random pattern, half near misses.  Returns (patterns, symbols)."""
+    to match a random pattern, half near misses.  Returns (patterns, symbols) (+ a bool array of the
+    lookups built to match, with return_hits)."""
     rng = np.random.default_rng(seed + 11)
     letters = "abcdefghijklmnopqrstuvwxyz"
     alnum = letters + "0123456789"
@@ -464,15 +465,17 @@ def c3_regex_list(n_patterns=10_000, n_lookups=1_000_000, seed=3, hit_rate=0.5):
         n = m + int(rng.integers(0, 6))
         specs.append((pre, m, n, suf))
         pats.append("^%s[a-z0-9]{%d,%d}(%s)?$" % (pre, m, n, suf))
-    syms = []
+    syms, hits = [], []
     for _ in range(n_lookups):
         pre, m, n, suf = specs[int(rng.integers(0, n_patterns))]
         body = "".join(alnum[int(i)] for i in rng.integers(0, 36, size=int(rng.integers(m, n + 1))))
         s = pre + body + (suf if rng.random() < 0.5 else "")
-        if rng.random() >= hit_rate:
+        hit = rng.random() < hit_rate
+        if not hit:
             s = s + ("-" if rng.random() < 0.5 else "X")  # outside the class / past the anchor
         syms.append(s)
-    return pats, syms
+        hits.append(hit)
+    return (pats, syms, np.array(hits)) if return_hits else (pats, syms)
 
 
 # ----------------------------------------------------------------------------------- C4 routes

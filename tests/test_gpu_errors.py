@@ -60,3 +60,39 @@ def test_resolver_pred_error_text_past_log_capacity(mxp, monkeypatch):
         texts.append([(int(q), int(err_rule[q]), eng.pair_error(int(q), int(err_rule[q]))) for q in bad])
     assert texts[0] == texts[1]
     assert all(t for _, _, t in texts[0])
+
+
+@pytest.mark.parametrize("wl", ["fuzz", "fuzz-vt", "c1", "c4"])
+def test_compact_error_output(mxp, monkeypatch, wl):
+    """mxp_batch_eval_device_compact: the same match bitmap and hit counters as the bitmap form, and
+    d_req_err[q] == (some error bit of request q is set)."""
+    import torch
+    if wl.startswith("fuzz"):
+        if wl == "fuzz-vt":
+            monkeypatch.setenv("MXP_DEBUG_FLAGS", "262144")
+        manifest = W.DEFAULT_TEST_MANIFEST
+        rules = W.fuzz_rules(500, seed=71, depth=3)
+        batch = BagBatch.from_bags(W.fuzz_bags(3000 + 13, seed=72), names=list(manifest))
+    elif wl == "c1":
+        manifest, rules, batch = W.c1_workload(5000)
+    else:
+        manifest, rules, batch = W.c4_workload(n_rules=3000, n_requests=20000, seed=73)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    db = eng.upload(batch)
+    Wd = (len(rules) + 31) // 32
+    dm = torch.zeros((Wd, batch.n), dtype=torch.int32, device="cuda:0")
+    de = torch.zeros_like(dm)
+    h1 = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
+    db.eval_hits(dm.data_ptr(), de.data_ptr(), h1.data_ptr(), 0)
+    dm2 = torch.full_like(dm, -1)
+    flags = torch.full((batch.n,), 7, dtype=torch.uint8, device="cuda:0")
+    h2 = torch.zeros_like(h1)
+    db.eval_compact(dm2.data_ptr(), flags.data_ptr(), h2.data_ptr(), 0)
+    torch.cuda.synchronize()
+    assert torch.equal(dm, dm2) and torch.equal(h1, h2)
+    want = (de != 0).any(dim=0).to(torch.uint8)
+    assert torch.equal(flags, want)
+    assert 0 < int(want.sum()) or wl == "c4"
+    db.free()
