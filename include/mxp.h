@@ -199,6 +199,10 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
 void mxp_list_destroy(mxp_engine* eng, mxp_list* list);
 /* list.numEntries(): distinct strings for string lists, entries (duplicates included) otherwise */
 uint64_t mxp_list_entries(const mxp_list* list);
+/* REGEX lists: automata the patterns were packed into (union DFAs, and bit-parallel NFAs of patterns
+ * whose own DFA is over budget); out[0] = parts, out[1] = of which NFAs.  (Engine introspection; no
+ * reference counterpart.) */
+void mxp_list_regex_parts(const mxp_list* list, uint32_t out[2]);
 int mxp_list_check(mxp_engine* eng, const mxp_list* list, int blacklist, const uint8_t* sym_bytes,
                    const uint64_t* sym_offsets, uint32_t n, int32_t* codes);
 /* Device-resident variant: symbols already in device memory (blob with >= 16 bytes of readable
@@ -246,10 +250,11 @@ int mxp_quota_alloc_device(mxp_engine* eng, mxp_quota* quota, uint32_t n, const 
 
 /*
  * Regex compiler check (host only; test and tooling hook): compiles `pattern` with the engine's Go
- * regexp restatement and DFA builder, then matches `subject` on the host DFA.  Returns 1 / 0 for
- * match / no match, -1 for a syntax error (err = Go's "error parsing regexp: ..." text), -2 when the
- * pattern uses a construct the engine does not support (err says which), -3 when the DFA exceeds
- * the state budget.
+ * regexp restatement and automaton builder under the rules' budget (a DFA of up to 65,536 states,
+ * else the bit-parallel NFA), then matches `subject` on the host form of the automaton the device
+ * would walk.  Returns 1 / 0 for match / no match, -1 for a syntax error (err = Go's "error parsing
+ * regexp: ..." text), -2 for a program too large to compile, -3 when the DFA is over budget and the
+ * program wider than the NFA (err says which).
  */
 int mxp_regex_match_host(const char* pattern, uint32_t pattern_len, const char* subject, uint32_t subject_len,
                          char* err, uint32_t err_cap);

@@ -13,9 +13,20 @@ typedef struct mxp_dfa_hdr {
     uint32_t hi_n;
     uint32_t skip;      // subject bytes already consumed into `start` (a rule's literal prefix, verified
                         // by the prefix index); MXP_DFA_DECIDED: the prefix alone decides a match
-    uint32_t pad;
+    uint32_t kind;      // MXP_RX_DFA, or MXP_RX_NFA: `trans` is the (8-byte aligned) NFA image
 } mxp_dfa_hdr;
 #define MXP_DFA_DECIDED 0xFFFFFFFFu
+#define MXP_RX_DFA 0u
+#define MXP_RX_NFA 1u
+
+// Bit-parallel NFA image (u64 words from S.trans + H.trans), for patterns whose DFA is over budget:
+//   [0]            m | W << 16 | nvar << 24   (m rune instructions; bit m of a set = MATCH; W words)
+//   [1 .. 8]       var_of[64]: assertion-flag value -> closure variant (only flags the program tests)
+//   ACC            [ncls - 1][W]   rune instructions that accept each rune class
+//   CL             [m + 1][nvar][W] epsilon closure (under the variant's flags) of each rune
+//                  instruction's successor; row m = the start threads (re-injected every step)
+#define MXP_NFA_HDR_WORDS 9u
+#define MXP_NFA_MAX_WORDS 4u
 
 typedef struct mxp_dfa_set {
     const mxp_dfa_hdr* hdr;
@@ -37,8 +48,126 @@ __device__ __forceinline__ uint64_t mxp_ld8(const uint8_t* p) {
     return sh == 0 ? lo : (lo >> sh) | (q[1] << (64u - sh));
 }
 
+// one rune at s[i] (lead byte c0 >= 0x80) as Go's inputString decodes it: invalid -> U+FFFD, width 1
+__device__ __forceinline__ uint32_t mxp_decode_hi(const uint8_t* s, uint32_t i, uint32_t n, uint32_t c0,
+                                                  uint32_t* width) {
+    const uint64_t w = mxp_ld8(s + i);  // bytes i .. i+7 (only those < n are used)
+    const uint32_t left = n - i;
+    const uint32_t b1 = (uint32_t)(w >> 8) & 0xFF, b2 = (uint32_t)(w >> 16) & 0xFF, b3 = (uint32_t)(w >> 24) & 0xFF;
+    uint32_t r = 0xFFFD;
+    *width = 1;
+    if (c0 >= 0xC2 && c0 <= 0xDF) {
+        if (left >= 2 && b1 >= 0x80 && b1 <= 0xBF) {
+            r = ((c0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
+            *width = 2;
+        }
+    } else if (c0 >= 0xE0 && c0 <= 0xEF) {
+        const uint32_t lo = c0 == 0xE0 ? 0xA0 : 0x80, hi = c0 == 0xED ? 0x9F : 0xBF;
+        if (left >= 3 && b1 >= lo && b1 <= hi && b2 >= 0x80 && b2 <= 0xBF) {
+            r = ((c0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu);
+            *width = 3;
+        }
+    } else if (c0 >= 0xF0 && c0 <= 0xF4) {
+        const uint32_t lo = c0 == 0xF0 ? 0x90 : 0x80, hi = c0 == 0xF4 ? 0x8F : 0xBF;
+        if (left >= 4 && b1 >= lo && b1 <= hi && b2 >= 0x80 && b2 <= 0xBF && b3 >= 0x80 && b3 <= 0xBF) {
+            r = ((c0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
+            *width = 4;
+        }
+    }
+    return r;
+}
+
+// class of a non-ASCII rune: the last range whose start <= r
+__device__ __forceinline__ uint32_t mxp_hi_class(const mxp_dfa_set& S, const mxp_dfa_hdr& H, uint32_t r) {
+    const uint32_t* lo = S.hilo + H.hi;
+    int a = 0, b = (int)H.hi_n - 1, k = 0;
+    while (a <= b) {
+        const int m = (a + b) >> 1;
+        if (lo[m] <= r) {
+            k = m;
+            a = m + 1;
+        } else {
+            b = m - 1;
+        }
+    }
+    return S.hicls[H.hi + k];
+}
+
+__device__ __forceinline__ bool mxp_rx_word(uint32_t r) {
+    return (r >= '0' && r <= '9') || (r >= 'A' && r <= 'Z') || (r >= 'a' && r <= 'z') || r == '_';
+}
+
+// The bit-parallel NFA walk (only over-budget patterns take it; the VM kernels that can meet one are
+// separate instantiations, so the DFA-only kernels keep their register budgets).  Per position: the closure of the pending threads
+// plus a fresh start thread under the position's assertion flags (what the DFA folds into its
+// states); MATCH in the closure -> true; else the threads whose rune instruction accepts the class.
+__device__ __forceinline__ bool mxp_nfa_run(const mxp_dfa_set& S, const mxp_dfa_hdr& H, const uint8_t* s, uint32_t n) {
+    const uint64_t* N = (const uint64_t*)(S.trans + H.trans);
+    const uint64_t h0 = N[0];
+    const uint32_t m = (uint32_t)(h0 & 0xFFFF), W = (uint32_t)(h0 >> 16) & 0xFF, nvar = (uint32_t)(h0 >> 24) & 0xFFFF;
+    const uint8_t* var_of = (const uint8_t*)(N + 1);
+    const uint64_t* ACC = N + MXP_NFA_HDR_WORDS;
+    const uint64_t* CL = ACC + (uint64_t)(H.ncls - 1) * W;
+    const uint64_t* CLS = CL + (uint64_t)m * nvar * W;
+    const uint16_t* asc = S.ascii + H.ascii;
+    uint64_t U[MXP_NFA_MAX_WORDS] = {0, 0, 0, 0};
+    bool begin = true, prev_nl = false, prev_word = false;
+    uint32_t i = 0;
+    for (;;) {
+        const bool end = i >= n;
+        uint32_t r = 0, width = 1, cls = 0;
+        if (!end) {
+            const uint32_t c0 = s[i];
+            if (c0 < 0x80) {
+                r = c0;
+                cls = asc[c0];
+            } else {
+                r = mxp_decode_hi(s, i, n, c0, &width);
+                cls = mxp_hi_class(S, H, r);
+            }
+        }
+        // syntax.EmptyOp flags: BEGIN_LINE 1, END_LINE 2, BEGIN_TEXT 4, END_TEXT 8, WORD_B 16, NO_WORD_B 32
+        uint32_t f = 0;
+        if (begin) f |= 4u | 1u;
+        if (prev_nl) f |= 1u;
+        if (end) f |= 8u | 2u;
+        if (!end && r == '\n') f |= 2u;
+        f |= (prev_word != (!end && mxp_rx_word(r))) ? 16u : 32u;
+        const uint32_t v = var_of[f];
+        uint64_t C[MXP_NFA_MAX_WORDS];
+#pragma unroll
+        for (uint32_t w = 0; w < MXP_NFA_MAX_WORDS; w++) C[w] = w < W ? CLS[(uint64_t)v * W + w] : 0;
+#pragma unroll
+        for (uint32_t w = 0; w < MXP_NFA_MAX_WORDS; w++) {
+            uint64_t bits = U[w];
+            while (bits) {
+                const uint32_t j = w * 64u + (uint32_t)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                const uint64_t* q = CL + ((uint64_t)j * nvar + v) * W;
+#pragma unroll
+                for (uint32_t x = 0; x < MXP_NFA_MAX_WORDS; x++)
+                    if (x < W) C[x] |= q[x];
+            }
+        }
+        uint64_t mw = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < MXP_NFA_MAX_WORDS; w++)
+            if (w == (m >> 6)) mw = C[w];
+        if ((mw >> (m & 63)) & 1u) return true;
+        if (end) return false;
+        const uint64_t* a = ACC + (uint64_t)cls * W;
+#pragma unroll
+        for (uint32_t w = 0; w < MXP_NFA_MAX_WORDS; w++) U[w] = w < W ? (C[w] & a[w]) : 0;
+        begin = false;
+        prev_nl = r == '\n';
+        prev_word = mxp_rx_word(r);
+        i += width;
+    }
+}
+
 // regexp.MatchString on one subject: decode runes the way Go's inputString does (utf8 rules; an
 // invalid byte is U+FFFD of width 1), map each to its class, step; END column at the end.
+// (DFA headers only: callers that may meet an NFA header use mxp_rx_run)
 __device__ __forceinline__ bool mxp_dfa_run(const mxp_dfa_set& S, uint32_t dfa, const uint8_t* s, uint32_t n) {
     const mxp_dfa_hdr H = S.hdr[dfa];
     const uint32_t* T = S.trans + H.trans;
@@ -103,6 +232,13 @@ __device__ __forceinline__ bool mxp_dfa_run(const mxp_dfa_set& S, uint32_t dfa, 
         if (st == 0xFFFFFFFFu) return true;
     }
     return T[(uint64_t)st * H.ncls + H.ncls - 1] == 0xFFFFFFFFu;
+}
+
+// a DFA or an NFA header
+__device__ __forceinline__ bool mxp_rx_run(const mxp_dfa_set& S, uint32_t dfa, const uint8_t* s, uint32_t n) {
+    const mxp_dfa_hdr H = S.hdr[dfa];
+    if (H.kind == MXP_RX_NFA) return mxp_nfa_run(S, H, s, n);
+    return mxp_dfa_run(S, dfa, s, n);
 }
 
 #endif

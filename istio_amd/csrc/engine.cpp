@@ -168,6 +168,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         }
         if (creg == MXP_VM_DONE || creg < t.creg0 || creg >= t.creg0 + t.nconst) continue;
         const mxp::Dfa& d = rx_dfas[rp.dfa];
+        if (d.is_nfa()) continue;  // the NFA walks the whole subject
         uint32_t st = d.start;
         for (size_t b = 0; b < rp.prefix.size() && st != mxp::kDfaAccept;) {
             const uint8_t c = (uint8_t)rp.prefix[b];
@@ -263,6 +264,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         if ((rc = put(d_prog, all.data(), all.size() * sizeof(mxp_vm_ins), "upload prog"))) return rc;
         if ((rc = put(d_rule_off, off.data(), off.size() * 4, "upload rule_off"))) return rc;
         if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
+        rx_nfa = rx_set.has_nfa();
         if ((rc = put(d_rx_hdr, rx_set.hdr.data(), rx_set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
         if ((rc = put(d_rx_trans, rx_set.trans.data(), rx_set.trans.size() * 4, "upload rx trans"))) return rc;
         if ((rc = put(d_rx_ascii, rx_set.ascii.data(), rx_set.ascii.size() * 2, "upload rx ascii"))) return rc;
@@ -1141,6 +1143,7 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = up(db->bstr_off, ooff.data(), ooff.size() * 8, "upload bstr_off"))) return rc;
     if ((rc = up(db->bstr, oblob.data(), oblob.size(), "upload bstr"))) return rc;
     if ((rc = up(db->rxof, rxof.data(), rxof.size() * 4, "upload rxof"))) return rc;
+    db->rx_nfa = rxb.has_nfa();
     if ((rc = up(db->rx_hdr, rxb.hdr.data(), rxb.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
     if ((rc = up(db->rx_trans, rxb.trans.data(), rxb.trans.size() * 4, "upload rx trans"))) return rc;
     if ((rc = up(db->rx_ascii, rxb.ascii.data(), rxb.ascii.size() * 2, "upload rx ascii"))) return rc;
@@ -1207,6 +1210,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
     A->rx_batch = mxp_dfa_set{db->rx_hdr.as<mxp_dfa_hdr>(), db->rx_trans.as<uint32_t>(), db->rx_ascii.as<uint16_t>(),
                               db->rx_hilo.as<uint32_t>(), db->rx_hicls.as<uint16_t>()};
     A->rxof = db->rxof.as<uint32_t>();
+    A->nfa = rx_nfa || db->rx_nfa ? 1u : 0u;
     if (!P.vt_cols.empty()) {
         A->gvt_off = P.d_gvt_off.as<uint32_t>();
         A->gvt = P.d_gvt.as<uint32_t>();

@@ -124,6 +124,7 @@ struct mxp_dbatch {
     size_t vt_t_words = 0, vt_keys_n = 0;
     DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
     DevBuf rxof, rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // run-time regexp patterns
+    bool rx_nfa = false;                              // one of them compiled to a bit-parallel NFA
     StrPool overlay;                                  // batch strings not in the rule set's pool
     StrPool overlay_bytes;                            // batch byte strings not in the rule set's
     std::vector<TimeKey> overlay_times;
@@ -171,6 +172,7 @@ struct mxp_engine : public mxp::LowerTables {
     std::vector<mxp::Dfa> rx_dfas;
     std::set<uint32_t> rx_cols;  // columns holding run-time patterns
     DevBuf d_rx_hdr, d_rx_trans, d_rx_ascii, d_rx_hilo, d_rx_hicls;
+    bool rx_nfa = false;         // some constant pattern compiled to a bit-parallel NFA (kargs.nfa)
 
     // rule-level tables (one per compile): programs + template code, offsets, constants, strings
     DevBuf d_prog, d_rule_off, d_gstr_off, d_gstr, d_rconst;

@@ -166,7 +166,7 @@ __device__ __forceinline__ void ref_rec(const mxp_kargs& A, bool on, uint32_t re
 // P[pc] (pc in [pc0, len)), fetched with one scalar s_load_dwordx4 per step.  `rule` may differ
 // per lane (template batches of the guard-index kernel); it only names the pair in error records and
 // Eval results.  The register file is regs[reg][thread] in LDS.
-template <bool kRefs>
+template <bool kRefs, bool kNfa = kRefs>
 __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint32_t pc0, bool live, uint32_t rule,
                              uint32_t req, uint64_t (*regs)[256], uint32_t tid, bool fan = false) {
 #define REG(i) regs[i][tid]
@@ -411,7 +411,12 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
                 }
                 if (run) {
                     const StrRef sub = str_of(A, subj);
-                    REG(d) = mxp_dfa_run(S, dfa, sub.p, sub.n) ? 1u : 0u;
+                    // (over-budget patterns run the bit-parallel NFA: only the kNfa instantiations,
+                    // launched for rule sets and batches that have one, carry its registers)
+                    if constexpr (kNfa)
+                        REG(d) = mxp_rx_run(S, dfa, sub.p, sub.n) ? 1u : 0u;
+                    else
+                        REG(d) = mxp_dfa_run(S, dfa, sub.p, sub.n) ? 1u : 0u;
                 }
             }
             break;
@@ -551,7 +556,7 @@ __device__ __forceinline__ void vt_count_errors(const mxp_kargs& A, uint32_t ve)
 __shared__ uint64_t g_ccv[MXP_CC][256];
 __shared__ uint8_t g_cck[MXP_CC][256];
 
-template <bool kVM, bool kRefs = false>
+template <bool kVM, bool kRefs = false, bool kNfa = kRefs>
 __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)[256]) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -647,7 +652,7 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
                     const uint32_t pc0 = (!guards_on || (gm & 0xFFu) == GM_NONE) ? 0u : (gm >> 16);
                     const uint32_t base = uni(A.rule_off[rule]);
                     const uint32_t len = uni(A.rule_off[rule + 1]) - base;
-                    const uint32_t code = run_rule<kRefs>(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, pc0, need, rule,
+                    const uint32_t code = run_rule<kRefs, kNfa>(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, pc0, need, rule,
                                                    req, regs, tid);
                     if (need) {
                         m |= code == PC_TRUE ? bit : 0u;
@@ -682,6 +687,12 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
 extern "C" __global__ __launch_bounds__(256) void mxp_eval_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     eval_groups<true>(A, regs);
+}
+
+// mxp_eval_kernel for rule sets / batches with bit-parallel NFA regexps (kargs.nfa)
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_nfa_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    eval_groups<true, false, true>(A, regs);
 }
 
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void mxp_guard_kernel(mxp_kargs A) { eval_groups<false>(A, nullptr); }
@@ -999,8 +1010,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
 }
 
 // grid x: class tiles of 64 (slot by slot), y: groups of 4 words (one per wave)
-extern "C" __global__ __launch_bounds__(256) void mxp_vt_eval_kernel(mxp_kargs A) {
-    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+template <bool kNfa>
+__device__ __forceinline__ void vt_eval_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = uni(tid >> 6);
@@ -1025,13 +1036,23 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_eval_kernel(mxp_kargs A
         const uint32_t rule = g * 32u + b;
         const uint32_t base = uni(A.rule_off[rule]);
         const uint32_t len = uni(A.rule_off[rule + 1]) - base;
-        const uint32_t code = run_rule<false>(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, 0u, live, rule, rep, regs, tid);
+        const uint32_t code = run_rule<false, kNfa>(A, ((cuint32*)A.prog) + (uint64_t)base * 4u, len, 0u, live, rule, rep, regs, tid);
         if (live) {
             m |= code == PC_TRUE ? 1u << b : 0u;
             e |= code >= PC_ERROR ? 1u << b : 0u;
         }
     }
     *(uint2*)(A.vt_tm + 2u * ((uint64_t)tb + (uint64_t)j * cap + k)) = make_uint2(m, e);
+}
+
+extern "C" __global__ __launch_bounds__(256) void mxp_vt_eval_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    vt_eval_body<false>(A, regs);
+}
+
+extern "C" __global__ __launch_bounds__(256) void mxp_vt_eval_nfa_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    vt_eval_body<true>(A, regs);
 }
 
 // Fill chunks with value-class merge entries: as mxp_fill_kernel (words of uniform indexed groups
@@ -1199,7 +1220,7 @@ __device__ __forceinline__ uint32_t pair_true(const mxp_kargs& A, PairQueue& Q, 
 }
 
 // run entries [off, off + cnt) of the queue, cnt <= 64
-template <bool kRefs>
+template <bool kRefs, bool kNfa>
 __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32_t cnt, uint64_t (*regs)[256],
                           uint32_t tid) {
     const uint32_t lane = tid & 63u;
@@ -1223,7 +1244,7 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
         if (mine)
             for (uint32_t c = 0; c < nconst; c++) regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
         cuint32* P = ((cuint32*)A.prog) + ((uint64_t)toff - pc0) * 4u;
-        const uint32_t code = run_rule<kRefs>(A, P, len_t, pc0, mine, rule, req, regs, tid, true);
+        const uint32_t code = run_rule<kRefs, kNfa>(A, P, len_t, pc0, mine, rule, req, regs, tid, true);
         if (mine) res = code;
         pending = pending && !mine;
     }
@@ -1236,7 +1257,7 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
 // OR-ed at once) and runs full 64-pair batches; `final` drains the queue.  Long lists go in rounds
 // of up to (free entries / 64) postings per lane, so the queue never overflows and the VM has one
 // call site (one inlined copy).
-template <bool kRefs>
+template <bool kRefs, bool kNfa>
 __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, uint32_t tbl, uint32_t start,
                                              uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
                                              uint32_t tid) {
@@ -1275,7 +1296,7 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
         const bool more = __ballot(j0 < len) != 0;
         if (Q.n >= 64u || (Q.n > 0u && (final || more))) {
             const uint32_t k = min(Q.n, 64u);
-            run_pairs<kRefs>(A, Q, Q.n - k, k, regs, tid);
+            run_pairs<kRefs, kNfa>(A, Q, Q.n - k, k, regs, tid);
             Q.n -= k;
             continue;
         }
@@ -1328,7 +1349,7 @@ struct PrefixHash {
 // guard column); true and error results are OR-ed in.
 namespace {
 
-template <bool kRefs>
+template <bool kRefs, bool kNfa = kRefs>
 __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
     const uint64_t t_start = A.wave_t ? (uint64_t)wall_clock64() : 0ull;
     const uint32_t tid = threadIdx.x;
@@ -1422,7 +1443,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 continue;
             }
             if (final || __ballot(len != 0))
-                process_slot<kRefs>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
+                process_slot<kRefs, kNfa>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
         }
     }
     if (A.dense_of) {  // masks for mxp_inject_kernel
@@ -1456,6 +1477,12 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index5_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<false>(A, regs);
+}
+
+// mxp_index_kernel for rule sets / batches with bit-parallel NFA regexps (kargs.nfa)
+extern "C" __global__ __launch_bounds__(256) void mxp_index_nfa_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    index_body<false, true>(A, regs);
 }
 
 // mxp_index_kernel with referenced-attribute records (mxp_eval_refs)
@@ -1621,6 +1648,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_hits_ragged_kernel(const u
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s) {
     if (vm && args->refs)
         hipLaunchKernelGGL(mxp_eval_refs_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    else if (vm && args->nfa)
+        hipLaunchKernelGGL(mxp_eval_nfa_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
     else if (vm)
         hipLaunchKernelGGL(mxp_eval_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
     else if (args->flags & 65536u)
@@ -1649,7 +1678,10 @@ extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t 
 
 extern "C" hipError_t mxp_launch_vt_eval(const mxp_kargs* args, uint32_t tiles, uint32_t wchunks, hipStream_t s) {
     if (!tiles || !wchunks) return hipSuccess;
-    hipLaunchKernelGGL(mxp_vt_eval_kernel, dim3(tiles, wchunks), dim3(256), 0, s, *args);
+    if (args->nfa)
+        hipLaunchKernelGGL(mxp_vt_eval_nfa_kernel, dim3(tiles, wchunks), dim3(256), 0, s, *args);
+    else
+        hipLaunchKernelGGL(mxp_vt_eval_kernel, dim3(tiles, wchunks), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 
@@ -1661,6 +1693,8 @@ extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hi
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s) {
     if (args->refs)
         hipLaunchKernelGGL(mxp_index_refs_kernel, dim3(grid), dim3(256), 0, s, *args);
+    else if (args->nfa)
+        hipLaunchKernelGGL(mxp_index_nfa_kernel, dim3(grid), dim3(256), 0, s, *args);
     else
         if (args->flags & 8192u)
             hipLaunchKernelGGL(mxp_index5_kernel, dim3(grid), dim3(256), 0, s, *args);

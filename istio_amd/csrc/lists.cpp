@@ -12,6 +12,7 @@
 // Checks run HandleListEntry (list.go:68-101) on the GPU (lists.hip).
 #include <algorithm>
 #include <cstring>
+#include <functional>
 #include <limits>
 
 #include "engine_impl.h"
@@ -19,15 +20,17 @@
 
 extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s);
 
-constexpr uint32_t kListRegexStates = 1u << 22;  // union DFA budget (4M states)
+constexpr uint32_t kListRegexStates = 1u << 22;  // state budget of one part's union DFA (4M states)
+constexpr uint64_t kListPartStates = 1u << 20;   // parts are packed to ~1M states of single-pattern DFAs
+constexpr uint32_t kPatternStates = 1u << 16;    // one pattern over this: its own bit-parallel NFA
 
 struct mxp_list {
     int type = 0;
     uint64_t n_entries = 0;
     uint32_t hmask = 0;
     DevBuf htab, ent_desc, ent_pool, v4lo, v4hi, v6lo, v6hi;
-    DevBuf rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // REGEX: one DFA for the union
-    uint32_t n4 = 0, n6 = 0;
+    DevBuf rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // REGEX: the parts' automata
+    uint32_t n4 = 0, n6 = 0, rx_n = 0, rx_nfa = 0;
 };
 
 namespace {
@@ -243,25 +246,63 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
         if ((rc = put(L->v6hi, hi6.data(), hi6.size() * 8, "upload v6hi"))) return rc;
     } else if (entry_type == MXP_LIST_REGEX) {
         // parseRegexList (regexList.go:44-65): every non-empty line, then every override, must
-        // compile (the first failure fails the list with regexp's error); checkList = any matches,
-        // i.e. one DFA for the union
+        // compile (the first failure fails the list with regexp's error); checkList = any matches.
+        // The patterns are packed, in order, into parts whose single-pattern DFAs sum to about
+        // kListPartStates; each part is one union DFA (a part over kListRegexStates splits in
+        // halves), and a pattern whose own DFA is over kPatternStates becomes its own NFA.  Only a
+        // pattern with both a DFA over budget and more than kNfaMaxPos rune instructions is refused.
         std::vector<std::string> pats;
         for (uint32_t i = 0; i < n_entries; i++)
             if (entry_lens[i]) pats.push_back(str(entries[i], entry_lens[i]));
         for (uint32_t i = 0; i < n_overrides; i++) pats.push_back(str(overrides[i], override_lens[i]));
-        for (const auto& p : pats) {  // per-pattern errors, in the reference's order
+        std::vector<uint64_t> cost(pats.size());
+        std::vector<uint8_t> alone(pats.size(), 0);
+        for (size_t i = 0; i < pats.size(); i++) {  // per-pattern errors, in the reference's order
             mxp::Dfa one;
             std::string e;
-            const int prc = mxp::regex_compile({p}, 1u << 16, &one, &e);
+            const int prc = mxp::regex_compile({pats[i]}, kPatternStates, &one, &e, nullptr, false);
             if (prc == mxp::RX_SYNTAX) return eng->fail(MXP_ERR_ARG, e);
             if (prc == mxp::RX_UNSUPPORTED) return eng->fail(MXP_ERR_ARG, "unsupported regexp (engine): " + e);
+            cost[i] = prc == mxp::RX_OK ? one.nstates : kPatternStates;
+            alone[i] = prc != mxp::RX_OK;
         }
-        mxp::Dfa d;
-        std::string e;
-        const int prc = mxp::regex_compile(pats, kListRegexStates, &d, &e);
-        if (prc != mxp::RX_OK) return eng->fail(MXP_ERR_ARG, "regex list: " + e);
         mxp::DfaSetHost set;
-        set.add(d);
+        std::function<int(size_t, size_t)> part = [&](size_t lo, size_t hi) -> int {
+            if (lo >= hi) return MXP_OK;
+            const std::vector<std::string> ps(pats.begin() + lo, pats.begin() + hi);
+            mxp::Dfa d;
+            std::string e;
+            const bool one = hi - lo == 1;
+            const int prc = mxp::regex_compile(ps, one ? kPatternStates : kListRegexStates, &d, &e, nullptr, one);
+            if (prc == mxp::RX_OK) {
+                set.add(d);
+                return MXP_OK;
+            }
+            if (one) return eng->fail(MXP_ERR_ARG, "regex list: pattern " + pats[lo] + ": " + e);
+            const size_t mid = lo + (hi - lo) / 2;
+            int rc2 = part(lo, mid);
+            return rc2 ? rc2 : part(mid, hi);
+        };
+        for (size_t i = 0; i < pats.size();) {
+            if (alone[i]) {
+                if ((rc = part(i, i + 1))) return rc;
+                i++;
+                continue;
+            }
+            size_t j = i;
+            uint64_t sum = 0;
+            while (j < pats.size() && !alone[j] && (j == i || sum + cost[j] <= kListPartStates)) sum += cost[j++];
+            if ((rc = part(i, j))) return rc;
+            i = j;
+        }
+        if (set.hdr.empty()) {  // no patterns: an automaton that never matches
+            mxp::Dfa d;
+            std::string e;
+            mxp::regex_compile({}, 16, &d, &e);
+            set.add(d);
+        }
+        L->rx_n = (uint32_t)set.hdr.size();
+        for (const auto& h : set.hdr) L->rx_nfa += h.kind == MXP_RX_NFA ? 1u : 0u;
         L->n_entries = pats.size();
         if ((rc = put(L->rx_hdr, set.hdr.data(), set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
         if ((rc = put(L->rx_trans, set.trans.data(), set.trans.size() * 4, "upload rx trans"))) return rc;
@@ -281,6 +322,11 @@ void mxp_list_destroy(mxp_engine* eng, mxp_list* list) {
 }
 
 uint64_t mxp_list_entries(const mxp_list* list) { return list ? list->n_entries : 0; }
+
+void mxp_list_regex_parts(const mxp_list* list, uint32_t out[2]) {
+    out[0] = list ? list->rx_n : 0;
+    out[1] = list ? list->rx_nfa : 0;
+}
 
 int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, const uint8_t* d_sym_bytes,
                           const uint64_t* d_sym_offsets, uint32_t n, void* stream, int32_t* d_codes) {
@@ -303,6 +349,7 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, con
     A.v6hi = L->v6hi.as<uint64_t>();
     A.n4 = L->n4;
     A.n6 = L->n6;
+    A.rx_n = L->rx_n;
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes;
@@ -348,6 +395,7 @@ int mxp_listentry_check(mxp_engine* eng, const mxp_list* L, int blacklist, const
     A.v6hi = L->v6hi.as<uint64_t>();
     A.n4 = L->n4;
     A.n6 = L->n6;
+    A.rx_n = L->rx_n;
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes.as<int32_t>();

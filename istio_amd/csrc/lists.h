@@ -25,7 +25,7 @@ typedef struct mxp_list_args {
     const uint64_t* v6lo;       // disjoint sorted IPv6 intervals, [2 i] high / [2 i + 1] low 64 bits
     const uint64_t* v6hi;
     uint32_t n4, n6;
-    mxp_dfa_set rx;             // REGEX lists: DFA 0 = the union of the list's patterns
+    mxp_dfa_set rx;             // REGEX lists: DFAs / NFAs 0 .. rx_n-1, each the union of a part of the patterns
     int32_t* codes;             // [n] google.rpc codes
     // fused listentry (mxp_listentry_check): symbols are the Eval results of one rule instead of
     // sym / sym_off -- a string id per request (vals[q * vstride], an interface handle when viface),
@@ -35,7 +35,7 @@ typedef struct mxp_list_args {
     uint32_t err_bit;
     uint32_t vstride;
     uint32_t viface;
-    uint32_t pad;
+    uint32_t rx_n;
     uint64_t n_gstr;
     const uint64_t* gstr_off;   // offset << 24 | length (8-aligned pools, 16 bytes of slack)
     const uint8_t* gstr;

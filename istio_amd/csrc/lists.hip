@@ -131,7 +131,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args 
         }
         found = ip_member(A, ip);
     } else if (A.type == MXP_LIST_REGEX) {
-        found = mxp_dfa_run(A.rx, 0, s, n);  // regexList.checkList: any pattern matches
+        found = false;  // regexList.checkList: any pattern matches (any part's automaton)
+        for (uint32_t k = 0; k < A.rx_n && !found; k++) found = mxp_rx_run(A.rx, k, s, n);
     } else {
         found = string_member(A, s, n, A.type == MXP_LIST_CASE_INSENSITIVE_STRINGS);
     }

@@ -7,6 +7,8 @@
 #include <memory>
 #include <unordered_map>
 
+#include "unicode_tables.h"
+
 namespace mxp {
 namespace {
 
@@ -95,65 +97,57 @@ Ranges negate(const Ranges& in) {
     return o;
 }
 
-// Runes >= 0x80 that have case mappings, conservatively: every Unicode block that holds cased
-// letters up to U+1FFFF.  Folding such a rune needs Unicode tables -> unsupported.
-bool maybe_cased(uint32_t r) {
-    static const uint32_t blocks[][2] = {
-        {0x00B5, 0x00B5}, {0x00C0, 0x024F}, {0x0250, 0x02AF}, {0x0345, 0x0345}, {0x0370, 0x03FF},
-        {0x0400, 0x052F}, {0x0531, 0x0587}, {0x10A0, 0x10FF}, {0x13A0, 0x13FD}, {0x1C80, 0x1CBF},
-        {0x1D79, 0x1D8E}, {0x1E00, 0x1FFF}, {0x2126, 0x2133}, {0x214E, 0x2184}, {0x24B6, 0x24E9},
-        {0x2C00, 0x2D2D}, {0xA640, 0xA69F}, {0xA722, 0xA7FF}, {0xAB53, 0xABBF}, {0xFB00, 0xFB17},
-        {0xFF21, 0xFF5A}, {0x10400, 0x104FF}, {0x10C80, 0x10CFF}, {0x118A0, 0x118DF}, {0x16E40, 0x16E7F},
-        {0x1E900, 0x1E94B}};
-    for (auto& b : blocks)
-        if (r >= b[0] && r <= b[1]) return true;
-    return false;
-}
-
-bool range_has_cased(uint32_t lo, uint32_t hi) {
-    static const uint32_t blocks[][2] = {
-        {0x00B5, 0x00B5}, {0x00C0, 0x024F}, {0x0250, 0x02AF}, {0x0345, 0x0345}, {0x0370, 0x03FF},
-        {0x0400, 0x052F}, {0x0531, 0x0587}, {0x10A0, 0x10FF}, {0x13A0, 0x13FD}, {0x1C80, 0x1CBF},
-        {0x1D79, 0x1D8E}, {0x1E00, 0x1FFF}, {0x2126, 0x2133}, {0x214E, 0x2184}, {0x24B6, 0x24E9},
-        {0x2C00, 0x2D2D}, {0xA640, 0xA69F}, {0xA722, 0xA7FF}, {0xAB53, 0xABBF}, {0xFB00, 0xFB17},
-        {0xFF21, 0xFF5A}, {0x10400, 0x104FF}, {0x10C80, 0x10CFF}, {0x118A0, 0x118DF}, {0x16E40, 0x16E7F},
-        {0x1E900, 0x1E94B}};
-    for (auto& b : blocks) {
-        uint32_t a = std::max(lo, b[0]), z = std::min(hi, b[1]);
-        if (a > z) continue;
-        // the two runes whose fold orbits reach ASCII are handled exactly
-        for (uint32_t r = a; r <= z; r++)
-            if (r != 0x212A && r != 0x17F) return true;
+// unicode.SimpleFold over kUniFold: the next rune of r's orbit (r itself when r does not fold)
+uint32_t simple_fold(uint32_t r) {
+    size_t a = 0, b = sizeof kUniFold / sizeof kUniFold[0];
+    while (a < b) {
+        const size_t m = (a + b) / 2;
+        if (kUniFold[m][0] < r) a = m + 1;
+        else b = m;
     }
-    return false;
+    return a < sizeof kUniFold / sizeof kUniFold[0] && kUniFold[a][0] == r ? kUniFold[a][1] : r;
 }
 
-// appendFoldedRange for ASCII letters and U+212A / U+017F (orbits k K U+212A, s S U+017F)
-Ranges fold_ranges(const Ranges& rs) {
+bool contains(const Ranges& rs, uint32_t r) {  // rs normalised
+    auto it = std::upper_bound(rs.begin(), rs.end(), std::make_pair(r, kMaxRune + 1));
+    return it != rs.begin() && (it - 1)->second >= r;
+}
+
+// appendFoldedRange over every range: the class closed under simple case folding (each member's
+// whole orbit joins)
+Ranges fold_ranges(const Ranges& in) {
+    const Ranges rs = norm(in);
     Ranges o = rs;
-    for (auto& p : rs) {
-        const uint32_t lo = p.first, hi = p.second;
-        for (int up = 0; up < 2; up++) {
-            const uint32_t a = up ? 'A' : 'a', b = up ? 'Z' : 'z';
-            const uint32_t x = std::max(lo, a), y = std::min(hi, b);
-            if (x <= y) o.emplace_back(up ? x + 32 : x - 32, up ? y + 32 : y - 32);
-        }
-        auto has = [&](uint32_t r) { return lo <= r && r <= hi; };
-        if (has('k') || has('K') || has(0x212A)) {
-            o.emplace_back('k', 'k');
-            o.emplace_back('K', 'K');
-            o.emplace_back(0x212A, 0x212A);
-        }
-        if (has('s') || has('S') || has(0x17F)) {
-            o.emplace_back('s', 's');
-            o.emplace_back('S', 'S');
-            o.emplace_back(0x17F, 0x17F);
-        }
-        // a range over every non-ASCII rune keeps its non-ASCII orbits inside; others need tables
-        if (hi >= 0x80 && !(lo <= 0x80 && hi == kMaxRune) && range_has_cased(std::max(lo, 0x80u), hi))
-            throw UnsupportedError{"case folding of non-ASCII runes"};
-    }
+    for (const auto& f : kUniFold)
+        if (contains(rs, f[0]))
+            for (uint32_t x = f[1]; x != f[0]; x = simple_fold(x)) o.emplace_back(x, x);
     return norm(o);
+}
+
+// unicodeTable (parse.go): "Any", unicode.Categories, unicode.Scripts; false when unknown
+bool unicode_table(const std::string& name, Ranges* out) {
+    if (name == "Any") {
+        *out = {{0, kMaxRune}};
+        return true;
+    }
+    const uni_class* b = kUniClasses;
+    const uni_class* e = kUniClasses + sizeof kUniClasses / sizeof kUniClasses[0];
+    const uni_class* it = std::lower_bound(b, e, name, [](const uni_class& c, const std::string& n) { return n.compare(c.name) > 0; });
+    if (it == e || name != it->name) return false;
+    out->clear();
+    for (uint32_t k = 0; k < it->n; k++) out->emplace_back(kUniRanges[it->off + k][0], kUniRanges[it->off + k][1]);
+    return true;
+}
+
+bool valid_utf8(const std::string& s, size_t a, size_t b) {  // checkUTF8 over s[a, b)
+    const std::string t = s.substr(a, b - a);
+    for (size_t i = 0; i < t.size();) {
+        size_t w;
+        const uint32_t r = decode_rune(t, i, &w);
+        if (r == 0xFFFD && w == 1 && t.compare(i, 3, "\xEF\xBF\xBD") != 0) return false;
+        i += w;
+    }
+    return true;
 }
 
 // ---------------------------------------------------------------------------------- AST
@@ -206,31 +200,28 @@ class Parser {
     }
 
     NodeP lit(uint32_t r) {
-        if (f_.i) {
-            Ranges orbit;
-            if (r == 'k' || r == 'K' || r == 0x212A)
-                orbit = {{'K', 'K'}, {'k', 'k'}, {0x212A, 0x212A}};
-            else if (r == 's' || r == 'S' || r == 0x17F)
-                orbit = {{'S', 'S'}, {'s', 's'}, {0x17F, 0x17F}};
-            else if ((r >= 'a' && r <= 'z') || (r >= 'A' && r <= 'Z'))
-                orbit = {{r | 0x20u, r | 0x20u}, {r & ~0x20u, r & ~0x20u}};
-            else if (r >= 0x80 && maybe_cased(r))
-                throw UnsupportedError{"case folding of a non-ASCII letter"};
-            if (!orbit.empty()) {
-                NodeP n = mk(N_CLASS);
-                n->cls = norm(orbit);
-                return n;
-            }
+        if (f_.i && simple_fold(r) != r) {
+            Ranges orbit{{r, r}};
+            for (uint32_t x = simple_fold(r); x != r; x = simple_fold(x)) orbit.emplace_back(x, x);
+            NodeP n = mk(N_CLASS);
+            n->cls = norm(orbit);
+            return n;
         }
         NodeP n = mk(N_LIT);
         n->rune = r;
         return n;
     }
 
-    NodeP cls_node(Ranges rs, bool fold) {
+    NodeP cls_node(Ranges rs) {
         NodeP n = mk(N_CLASS);
-        n->cls = fold ? fold_ranges(rs) : norm(rs);
+        n->cls = norm(std::move(rs));
         return n;
+    }
+
+    // appendGroup: under (?i) a group is folded BEFORE it is negated
+    Ranges group(const Ranges& rs, bool negated) const {
+        const Ranges g = f_.i ? fold_ranges(rs) : norm(rs);
+        return negated ? negate(g) : g;
     }
 
     NodeP alt(bool top) {
@@ -343,7 +334,7 @@ class Parser {
             group(seq);
             return;
         case '[':
-            seq.push_back(cls_node(parse_class(), false));
+            seq.push_back(cls_node(parse_class()));
             return;
         case '.':
             i_++;
@@ -428,24 +419,58 @@ class Parser {
         seq.push_back(std::move(g));
     }
 
-    // parsePerlClassEscape: \d \s \w (and negations); \p \P unsupported
+    // parsePerlClassEscape (\d \s \w and negations) or parseUnicodeClass (\p \P) at i_ -> the group
     bool perl_class(Ranges* out) {
         if (!at(i_, '\\') || i_ + 1 >= s_.size()) return false;
         const char c = s_[i_ + 1];
+        if (c == 'p' || c == 'P') {
+            *out = unicode_class();
+            return true;
+        }
         Ranges r;
-        switch (c | 0x20) {
-        case 'd': r = {{'0', '9'}}; break;
-        case 's': r = {{'\t', '\n'}, {'\f', '\r'}, {' ', ' '}}; break;
-        case 'w': r = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}; break;
-        case 'p':
-            if (c == 'p' || c == 'P') throw UnsupportedError{"Unicode character classes (\\p)"};
-            return false;
+        switch (c) {
+        case 'd': case 'D': r = {{'0', '9'}}; break;
+        case 's': case 'S': r = {{'\t', '\n'}, {'\f', '\r'}, {' ', ' '}}; break;
+        case 'w': case 'W': r = {{'0', '9'}, {'A', 'Z'}, {'_', '_'}, {'a', 'z'}}; break;
         default: return false;
         }
-        if (c != 'd' && c != 's' && c != 'w' && c != 'D' && c != 'S' && c != 'W') return false;
         i_ += 2;
-        *out = (c >= 'A' && c <= 'Z') ? negate(r) : r;
+        *out = group(r, c >= 'A' && c <= 'Z');
         return true;
+    }
+
+    // parseUnicodeClass: \pN \p{Name} \P.. \p{^Name}; an unknown name is an invalid class range
+    Ranges unicode_class() {
+        const size_t start = i_;
+        bool neg = s_[i_ + 1] == 'P';
+        i_ += 2;
+        std::string name;
+        size_t seq_end;
+        if (at(i_, '{')) {
+            const size_t end = s_.find('}', i_);
+            if (end == std::string::npos) {
+                if (!valid_utf8(s_, start, s_.size())) err("invalid UTF-8", text(start));
+                err("invalid character class range", text(start));
+            }
+            if (!valid_utf8(s_, i_ + 1, end)) err("invalid UTF-8", text(i_ + 1, end));
+            name = text(i_ + 1, end);
+            seq_end = end + 1;
+        } else if (i_ < s_.size()) {
+            const size_t save = i_;
+            next_rune();
+            name = text(save, i_);
+            seq_end = i_;
+        } else {
+            seq_end = i_;
+        }
+        i_ = seq_end;
+        if (!name.empty() && name[0] == '^') {
+            neg = !neg;
+            name.erase(0, 1);
+        }
+        Ranges tab;
+        if (name.empty() || !unicode_table(name, &tab)) err("invalid character class range", text(start, seq_end));
+        return group(tab, neg);
     }
 
     // parseEscape: one escaped rune; errors carry the text consumed so far
@@ -522,7 +547,7 @@ class Parser {
         }
         Ranges r;
         if (perl_class(&r)) {
-            seq.push_back(cls_node(r, f_.i));
+            seq.push_back(cls_node(r));
             return;
         }
         seq.push_back(lit(escape()));
@@ -573,7 +598,7 @@ class Parser {
                     if (pneg) name = name.substr(1);
                     auto it = posix.find(name);
                     if (it == posix.end()) err("invalid character class range", text(i_, end + 2));
-                    const Ranges g = pneg ? negate(it->second) : it->second;
+                    const Ranges g = group(it->second, pneg);
                     rs.insert(rs.end(), g.begin(), g.end());
                     i_ = end + 2;
                     first = false;
@@ -753,7 +778,7 @@ bool regex_required_prefix(const std::string& pattern, std::string* prefix) {
 }
 
 int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states, Dfa* out, std::string* err,
-                  uint32_t* bad) {
+                  uint32_t* bad, bool nfa_fallback) {
     Prog p;
     std::vector<int> starts;
     const int match = p.emit(Inst{I_MATCH});
@@ -784,31 +809,69 @@ int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states,
     std::sort(cuts.begin(), cuts.end());
     cuts.erase(std::unique(cuts.begin(), cuts.end()), cuts.end());
     while (!cuts.empty() && cuts.back() > kMaxRune + 1) cuts.pop_back();
-    // class k = [cuts[k], cuts[k+1]); representatives decide rune membership
+    // raw class k = [cuts[k], cuts[k+1]).  Raw classes no rune instruction tells apart (same word /
+    // '\n' context, same membership everywhere) share one DFA column: partition refinement, one
+    // instruction at a time, so \p{L}-sized classes cost a column per distinct behaviour, not per range.
     const uint32_t nrc = (uint32_t)cuts.size() - 1;
-    if (nrc + 1 > 0xFFFF) {
+    auto span = [&](const std::pair<uint32_t, uint32_t>& r, size_t* a, size_t* b) {
+        *a = std::lower_bound(cuts.begin(), cuts.end(), r.first) - cuts.begin();
+        *b = std::lower_bound(cuts.begin(), cuts.end(), r.second + 1) - cuts.begin();
+    };
+    constexpr uint32_t kNone = 0xFFFFFFFFu;
+    std::vector<uint32_t> cid(nrc);
+    for (uint32_t k = 0; k < nrc; k++) cid[k] = (is_word(cuts[k]) ? 1u : 0u) | (cuts[k] == '\n' ? 2u : 0u);
+    uint32_t nid = 4;
+    std::vector<uint32_t> remap(nid, kNone), touched;
+    for (auto& in : p.ins) {
+        if (in.op != I_RUNE) continue;
+        for (auto& r : in.r) {
+            size_t a, b;
+            span(r, &a, &b);
+            for (size_t c = a; c < b; c++) {
+                const uint32_t old = cid[c];
+                if (remap[old] == kNone) {
+                    remap[old] = nid++;
+                    touched.push_back(old);
+                }
+                cid[c] = remap[old];
+            }
+        }
+        for (uint32_t o : touched) remap[o] = kNone;
+        touched.clear();
+        remap.resize(nid, kNone);
+    }
+    std::vector<uint32_t> comp(nid, kNone), rep_of;
+    for (uint32_t k = 0; k < nrc; k++) {
+        if (comp[cid[k]] == kNone) {
+            comp[cid[k]] = (uint32_t)rep_of.size();
+            rep_of.push_back(cuts[k]);
+        }
+        cid[k] = comp[cid[k]];
+    }
+    const uint32_t ncc = (uint32_t)rep_of.size();
+    if (ncc + 1 > 0xFFFF) {
         *err = "too many rune classes";
         return RX_TOO_BIG;
     }
     Dfa d;
-    d.ncls = nrc + 1;  // + END
+    d.ncls = ncc + 1;  // + END
     for (uint32_t k = 0; k < nrc; k++) {
         if (cuts[k] < 0x80)
-            for (uint32_t r = cuts[k]; r < std::min<uint32_t>(cuts[k + 1], 0x80); r++) d.ascii[r] = (uint16_t)k;
-        if (cuts[k + 1] > 0x80) {
+            for (uint32_t r = cuts[k]; r < std::min<uint32_t>(cuts[k + 1], 0x80); r++) d.ascii[r] = (uint16_t)cid[k];
+        if (cuts[k + 1] > 0x80 && (d.hi_cls.empty() || d.hi_cls.back() != cid[k])) {
             d.hi_lo.push_back(std::max<uint32_t>(cuts[k], 0x80));
-            d.hi_cls.push_back((uint16_t)k);
+            d.hi_cls.push_back((uint16_t)cid[k]);
         }
     }
     // per instruction, per class: does the rune instruction accept the class?
     std::vector<std::vector<uint8_t>> accepts(p.ins.size());
     for (size_t k = 0; k < p.ins.size(); k++) {
         if (p.ins[k].op != I_RUNE) continue;
-        accepts[k].assign(nrc, 0);
+        accepts[k].assign(ncc, 0);
         for (auto& r : p.ins[k].r) {
-            auto a = std::lower_bound(cuts.begin(), cuts.end(), r.first) - cuts.begin();
-            auto b = std::lower_bound(cuts.begin(), cuts.end(), r.second + 1) - cuts.begin();
-            for (auto c = a; c < b; c++) accepts[k][c] = 1;
+            size_t a, b;
+            span(r, &a, &b);
+            for (size_t c = a; c < b; c++) accepts[k][cid[c]] = 1;
         }
     }
     std::unordered_map<StateKey, uint32_t, StateHash> ids;
@@ -858,18 +921,83 @@ int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states,
         }
         return start_cl[f];
     };
+    // over budget: the bit-parallel NFA image (dfa_dev.h) over the same alphabet -- bit j of a thread
+    // set is rune instruction j, bit m is MATCH; closures per variant of the flags the program tests
+    auto build_nfa = [&]() -> int {
+        std::vector<int32_t> pos_of(p.ins.size(), -1), pcs;
+        for (size_t k = 0; k < p.ins.size(); k++)
+            if (p.ins[k].op == I_RUNE) {
+                pos_of[k] = (int32_t)pcs.size();
+                pcs.push_back((int32_t)k);
+            }
+        const uint32_t m = (uint32_t)pcs.size();
+        if (m > kNfaMaxPos) {
+            *err = "DFA exceeds the state budget and the program the NFA width";
+            return RX_TOO_BIG;
+        }
+        const uint32_t W = (m + 1 + 63) / 64;
+        uint32_t tested = 0;
+        for (auto& in : p.ins)
+            if (in.op == I_EMPTY) tested |= in.empty;
+        std::vector<uint32_t> bits;
+        for (uint32_t b = 0; b < 6; b++)
+            if (tested >> b & 1) bits.push_back(b);
+        const uint32_t nvar = 1u << bits.size();
+        std::vector<uint64_t> img(MXP_NFA_HDR_WORDS + (size_t)ncc * W + (size_t)(m + 1) * nvar * W, 0);
+        img[0] = (uint64_t)m | ((uint64_t)W << 16) | ((uint64_t)nvar << 24);
+        uint8_t* var_of = (uint8_t*)&img[1];
+        for (uint32_t f = 0; f < 64; f++) {
+            uint32_t v = 0;
+            for (size_t k = 0; k < bits.size(); k++) v |= (f >> bits[k] & 1u) << k;
+            var_of[f] = (uint8_t)v;
+        }
+        uint64_t* acc = img.data() + MXP_NFA_HDR_WORDS;
+        for (uint32_t j = 0; j < m; j++)
+            for (uint32_t c = 0; c < ncc; c++)
+                if (accepts[pcs[j]][c]) acc[(size_t)c * W + j / 64] |= 1ull << (j % 64);
+        uint64_t* cl = acc + (size_t)ncc * W;
+        std::vector<int32_t> outv;
+        for (uint32_t v = 0; v < nvar; v++) {
+            uint8_t f = 0;
+            for (size_t k = 0; k < bits.size(); k++)
+                if (v >> k & 1) f |= (uint8_t)(1u << bits[k]);
+            for (uint32_t j = 0; j <= m; j++) {
+                outv.clear();
+                ++stamp;
+                const bool hit = j < m ? close(&p.ins[pcs[j]].x, 1, f, outv) : close(starts.data(), starts.size(), f, outv);
+                uint64_t* row = cl + ((size_t)j * nvar + v) * W;
+                for (int32_t pc : outv) row[pos_of[pc] / 64] |= 1ull << (pos_of[pc] % 64);
+                if (hit) row[m / 64] |= 1ull << (m % 64);
+            }
+        }
+        Dfa nd;
+        nd.ncls = ncc + 1;
+        std::copy(d.ascii, d.ascii + 128, nd.ascii);
+        nd.hi_lo = d.hi_lo;
+        nd.hi_cls = d.hi_cls;
+        nd.nfa = std::move(img);
+        *out = std::move(nd);
+        return RX_OK;
+    };
     d.start = intern(StateKey{{}, 1});
     std::vector<int32_t> closure;
     for (uint32_t sidx = 0; sidx < states.size(); sidx++) {
         if (states.size() > max_states) {
+            if (nfa_fallback) {
+                states.clear();
+                ids.clear();
+                d.trans.clear();
+                d.trans.shrink_to_fit();
+                return build_nfa();
+            }
             *err = "DFA exceeds the state budget";
             return RX_TOO_BIG;
         }
         const StateKey cur = states[sidx];
         const bool begin = cur.ctx & 1, prev_nl = cur.ctx & 2, prev_word = cur.ctx & 4;
-        for (uint32_t c = 0; c <= nrc; c++) {
-            const bool end = c == nrc;
-            const uint32_t rep = end ? 0 : cuts[c];
+        for (uint32_t c = 0; c <= ncc; c++) {
+            const bool end = c == ncc;
+            const uint32_t rep = end ? 0 : rep_of[c];
             uint8_t flags = 0;
             if (begin) flags |= BEGIN_TEXT | BEGIN_LINE;
             if (prev_nl) flags |= BEGIN_LINE;
@@ -909,11 +1037,20 @@ uint32_t DfaSetHost::add(const Dfa& d) {
     mxp_dfa_hdr h{};
     h.ncls = d.ncls;
     h.start = d.start;
-    h.trans = (uint32_t)trans.size();
+    if (d.is_nfa()) {  // the u64 image, 8-byte aligned in the u32 transition array
+        if (trans.size() & 1) trans.push_back(0);
+        h.kind = MXP_RX_NFA;
+        h.trans = (uint32_t)trans.size();
+        const uint32_t* w = (const uint32_t*)d.nfa.data();
+        trans.insert(trans.end(), w, w + 2 * d.nfa.size());
+    } else {
+        h.kind = MXP_RX_DFA;
+        h.trans = (uint32_t)trans.size();
+        trans.insert(trans.end(), d.trans.begin(), d.trans.end());
+    }
     h.ascii = (uint32_t)ascii.size();
     h.hi = (uint32_t)hilo.size();
     h.hi_n = (uint32_t)d.hi_lo.size();
-    trans.insert(trans.end(), d.trans.begin(), d.trans.end());
     ascii.insert(ascii.end(), d.ascii, d.ascii + 128);
     hilo.insert(hilo.end(), d.hi_lo.begin(), d.hi_lo.end());
     hicls.insert(hicls.end(), d.hi_cls.begin(), d.hi_cls.end());
@@ -921,7 +1058,52 @@ uint32_t DfaSetHost::add(const Dfa& d) {
     return (uint32_t)hdr.size() - 1;
 }
 
+namespace {
+uint32_t class_of(const Dfa& d, uint32_t r) {
+    if (r < 0x80) return d.ascii[r];
+    return d.hi_cls[std::upper_bound(d.hi_lo.begin(), d.hi_lo.end(), r) - d.hi_lo.begin() - 1];
+}
+
+// host form of mxp_nfa_run (dfa_dev.h)
+bool nfa_match_host(const Dfa& d, const std::string& s) {
+    const uint64_t* N = d.nfa.data();
+    const uint32_t m = (uint32_t)(N[0] & 0xFFFF), W = (uint32_t)(N[0] >> 16) & 0xFF, nvar = (uint32_t)(N[0] >> 24) & 0xFFFF;
+    const uint8_t* var_of = (const uint8_t*)(N + 1);
+    const uint64_t* acc = N + MXP_NFA_HDR_WORDS;
+    const uint64_t* cl = acc + (size_t)(d.ncls - 1) * W;
+    const uint64_t* cls0 = cl + (size_t)m * nvar * W;
+    uint64_t U[MXP_NFA_MAX_WORDS] = {0, 0, 0, 0};
+    bool begin = true, prev_nl = false, prev_word = false;
+    for (size_t i = 0;;) {
+        const bool end = i >= s.size();
+        size_t w = 1;
+        const uint32_t r = end ? 0 : decode_rune(s, i, &w);
+        uint8_t f = 0;
+        if (begin) f |= BEGIN_TEXT | BEGIN_LINE;
+        if (prev_nl) f |= BEGIN_LINE;
+        if (end) f |= END_TEXT | END_LINE;
+        if (!end && r == '\n') f |= END_LINE;
+        f |= (prev_word != (!end && is_word(r))) ? WORD_B : NO_WORD_B;
+        const uint32_t v = var_of[f];
+        uint64_t C[MXP_NFA_MAX_WORDS] = {0, 0, 0, 0};
+        for (uint32_t x = 0; x < W; x++) C[x] = cls0[(size_t)v * W + x];
+        for (uint32_t j = 0; j < m; j++)
+            if (U[j / 64] >> (j % 64) & 1)
+                for (uint32_t x = 0; x < W; x++) C[x] |= cl[((size_t)j * nvar + v) * W + x];
+        if (C[m / 64] >> (m % 64) & 1) return true;
+        if (end) return false;
+        const uint64_t* a = acc + (size_t)class_of(d, r) * W;
+        for (uint32_t x = 0; x < W; x++) U[x] = C[x] & a[x];
+        begin = false;
+        prev_nl = r == '\n';
+        prev_word = is_word(r);
+        i += w;
+    }
+}
+}  // namespace
+
 bool dfa_match_host(const Dfa& d, const std::string& s) {
+    if (d.is_nfa()) return nfa_match_host(d, s);
     uint32_t st = d.start;
     size_t i = 0;
     while (i < s.size()) {
@@ -945,9 +1127,20 @@ bool dfa_match_host(const Dfa& d, const std::string& s) {
 
 extern "C" int mxp_regex_match_host(const char* pattern, uint32_t pattern_len, const char* subject,
                                     uint32_t subject_len, char* err, uint32_t err_cap) {
-    mxp::Dfa d;
-    std::string e;
-    const int rc = mxp::regex_compile({std::string(pattern ? pattern : "", pattern_len)}, 1u << 20, &d, &e);
+    // (the last pattern's automaton is kept per thread: callers sweep subjects per pattern)
+    thread_local std::string last;
+    thread_local bool have = false;
+    thread_local mxp::Dfa d;
+    thread_local std::string e;
+    thread_local int rc = 0;
+    const std::string pat(pattern ? pattern : "", pattern_len);
+    if (!have || pat != last) {
+        d = mxp::Dfa();
+        e.clear();
+        rc = mxp::regex_compile({pat}, 1u << 16, &d, &e);  // the rules' budget
+        last = pat;
+        have = true;
+    }
     if (err && err_cap) {
         const size_t n = std::min<size_t>(e.size(), err_cap - 1);
         memcpy(err, e.data(), n);

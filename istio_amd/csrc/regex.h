@@ -37,21 +37,29 @@ struct Dfa {
     uint32_t nstates = 0;
     uint32_t start = 0;
     std::vector<uint32_t> trans;   // [nstates][ncls]: next state, kDfaAccept or kDfaReject
+    // A pattern whose DFA exceeds the state budget but whose program has < kNfaMaxPos rune
+    // instructions compiles to a bit-parallel NFA instead (trans empty, nfa = the MXP_NFA_* image of
+    // dfa_dev.h): the same alphabet, the thread set as a bitset over rune instructions.
+    std::vector<uint64_t> nfa;
+    bool is_nfa() const { return !nfa.empty(); }
 };
+
+constexpr uint32_t kNfaMaxPos = 255;  // rune instructions (+ the MATCH bit = 256 bits, 4 words)
 
 enum RegexStatus { RX_OK = 0, RX_SYNTAX = 1, RX_UNSUPPORTED = 2, RX_TOO_BIG = 3 };
 
 // Compile the union of `patterns` (a match of any of them is a match) into `out`.  On RX_SYNTAX,
 // *err is Go's error text ("error parsing regexp: <code>: `<expr>`") of the first failing pattern
-// and *bad its index; on RX_UNSUPPORTED / RX_TOO_BIG *err says why.
+// and *bad its index; on RX_UNSUPPORTED / RX_TOO_BIG *err says why.  A DFA over `max_states`
+// falls back to the bit-parallel NFA when `nfa_fallback` and the program is small enough.
 int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states, Dfa* out, std::string* err,
-                  uint32_t* bad = nullptr);
+                  uint32_t* bad = nullptr, bool nfa_fallback = true);
 
 // A pattern anchored at text begin (^ without (?m), or \A) followed by literal runes only matches
 // subjects that start with those runes' UTF-8 bytes: the engine indexes such rules by that prefix.
 bool regex_required_prefix(const std::string& pattern, std::string* prefix);
 
-// Host reference stepping of a compiled DFA (tests / debugging).
+// Host stepping of a compiled DFA or NFA (constant folding, tests).
 bool dfa_match_host(const Dfa& d, const std::string& s);
 
 }  // namespace mxp
@@ -68,6 +76,11 @@ struct DfaSetHost {
     std::vector<uint32_t> hilo;
     std::vector<uint16_t> hicls;
     uint32_t add(const Dfa& d);  // -> DFA index
+    bool has_nfa() const {
+        for (const auto& h : hdr)
+            if (h.kind == MXP_RX_NFA) return true;
+        return false;
+    }
 };
 
 }  // namespace mxp

@@ -69,6 +69,7 @@ SIGNATURES = {
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(_VP)]),
     "mxp_list_destroy": (None, [_VP, _VP]),
     "mxp_list_entries": (ctypes.c_uint64, [_VP]),
+    "mxp_list_regex_parts": (None, [_VP, ctypes.c_void_p]),
     "mxp_list_check": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.c_void_p]),
     "mxp_list_check_device": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -563,6 +564,12 @@ class ListHandle:
 
     def num_entries(self) -> int:
         return int(self.eng.lib.mxp_list_entries(self.h))
+
+    def regex_parts(self):
+        """(automata, of which bit-parallel NFAs) of a REGEX list."""
+        out = (ctypes.c_uint32 * 2)()
+        self.eng.lib.mxp_list_regex_parts(self.h, out)
+        return int(out[0]), int(out[1])
 
     def check(self, symbols, blacklist: bool = False) -> np.ndarray:
         """google.rpc codes (0 OK, 3 INVALID_ARGUMENT, 5 NOT_FOUND, 7 PERMISSION_DENIED) per symbol."""

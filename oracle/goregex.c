@@ -9,7 +9,8 @@
  *
  * Go 1.9 regexp/syntax is not vendored under /root/reference; PARITY UNPINNED beyond the
  * reference's own rows (tests.go:2064-2121, list_test.go:397-431).  Unicode classes (\p, \P) and
- * case folding of cased non-ASCII runes are rejected (-2), as goregex.py and the engine reject them.
+ * simple case folding read oracle/unicode_tables.h (tools/gen_unicode_tables.py, Unicode 13 where
+ * Go 1.9 has Unicode 9).
  */
 #include "regex_oracle.h"
 
@@ -18,7 +19,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "unicode_cased.h"
+#include "unicode_tables.h"
 
 #define MAX_REPEAT 1000
 #define MAX_RUNE 0x10FFFFu
@@ -75,12 +76,6 @@ static void fail_syntax(ctx* c, const char* code, const uint8_t* e, size_t n) {
     longjmp(c->jb, 1);
 }
 
-static void fail_unsupported(ctx* c, const char* what) {
-    snprintf(c->msg, sizeof c->msg, "unsupported regexp (oracle): %s", what);
-    c->code = -2;
-    longjmp(c->jb, 1);
-}
-
 #define E_RANGE "invalid character class range"
 #define E_ESCAPE "invalid escape sequence"
 #define E_NAMED "invalid named capture"
@@ -125,17 +120,6 @@ static uint32_t decode_rune(const uint8_t* b, size_t n, size_t i, int* w) {
 
 static int is_word(int64_t r) {
     return r >= 0 && ((r >= 0x30 && r <= 0x39) || (r >= 0x41 && r <= 0x5A) || (r >= 0x61 && r <= 0x7A) || r == 0x5F);
-}
-
-static int is_cased(uint32_t r) {
-    int a = 0, b = (int)(sizeof kCasedRanges / sizeof kCasedRanges[0]) - 1;
-    while (a <= b) {
-        const int m = (a + b) / 2;
-        if (r < kCasedRanges[m][0]) b = m - 1;
-        else if (r > kCasedRanges[m][1]) a = m + 1;
-        else return 1;
-    }
-    return 0;
 }
 
 /* ---------------------------------------------------------------------------- rune ranges */
@@ -192,76 +176,51 @@ static void rg_extend(ctx* c, ranges* dst, ranges src) {
     for (int i = 0; i < src.n; i++) rg_add(c, dst, src.r[i].lo, src.r[i].hi);
 }
 
-/* simple case folding orbits that involve ASCII (unicode.SimpleFold): k K U+212A, s S U+017F */
-static int special_orbit(uint32_t r, uint32_t out[2]) {
-    switch (r) {
-    case 0x6B: out[0] = 0x4B; out[1] = 0x212A; return 1;
-    case 0x4B: out[0] = 0x6B; out[1] = 0x212A; return 1;
-    case 0x212A: out[0] = 0x4B; out[1] = 0x6B; return 1;
-    case 0x73: out[0] = 0x53; out[1] = 0x17F; return 1;
-    case 0x53: out[0] = 0x73; out[1] = 0x17F; return 1;
-    case 0x17F: out[0] = 0x53; out[1] = 0x73; return 1;
-    default: return 0;
+/* unicode.SimpleFold over kUniFold: the next rune of r's orbit (r itself when r does not fold) */
+static uint32_t simple_fold(uint32_t r) {
+    int a = 0, b = (int)(sizeof kUniFold / sizeof kUniFold[0]) - 1;
+    while (a <= b) {
+        const int m = (a + b) / 2;
+        if (kUniFold[m][0] == r) return kUniFold[m][1];
+        if (kUniFold[m][0] < r) a = m + 1;
+        else b = m - 1;
     }
+    return r;
 }
-static const uint32_t kSpecial[6] = {0x6B, 0x4B, 0x212A, 0x73, 0x53, 0x17F};
 
 /* fold_orbit(r) -> number of runes written (r first) */
-static int fold_orbit(ctx* c, uint32_t r, uint32_t out[3]) {
-    uint32_t o[2];
-    out[0] = r;
-    if (special_orbit(r, o)) {
-        out[1] = o[0];
-        out[2] = o[1];
-        return 3;
-    }
-    if (r >= 0x41 && r <= 0x5A) {
-        out[1] = r + 32;
-        return 2;
-    }
-    if (r >= 0x61 && r <= 0x7A) {
-        out[1] = r - 32;
-        return 2;
-    }
-    if (r >= 0x80 && is_cased(r)) {
-        char w[64];
-        snprintf(w, sizeof w, "case folding of non-ASCII letter U+%04X", r);
-        fail_unsupported(c, w);
-    }
-    return 1;
+static int fold_orbit(uint32_t r, uint32_t out[8]) {
+    int k = 0;
+    out[k++] = r;
+    for (uint32_t x = simple_fold(r); x != r && k < 8; x = simple_fold(x)) out[k++] = x;
+    return k;
 }
 
-/* appendFoldedRange for the ASCII letters and the two non-ASCII runes whose orbits reach ASCII */
-static ranges fold_ranges(ctx* c, ranges g) {
-    ranges out = {0};
-    rg_extend(c, &out, g);
-    for (int i = 0; i < g.n; i++) {
-        const uint32_t lo = g.r[i].lo, hi = g.r[i].hi;
-        for (int t = 0; t < 2; t++) {
-            const uint32_t a = t ? 0x61 : 0x41, b = t ? 0x7A : 0x5A;
-            const uint32_t x = lo > a ? lo : a, y = hi < b ? hi : b;
-            if (x <= y) {
-                if (t) rg_add(c, &out, x - 32, y - 32);
-                else rg_add(c, &out, x + 32, y + 32);
-            }
-        }
-        for (int s = 0; s < 6; s++)
-            if (lo <= kSpecial[s] && kSpecial[s] <= hi) {
-                uint32_t o[2];
-                special_orbit(kSpecial[s], o);
-                rg_add(c, &out, o[0], o[0]);
-                rg_add(c, &out, o[1], o[1]);
-            }
-        if (hi >= 0x80 && !(lo <= 0x80 && hi == MAX_RUNE)) {
-            const uint32_t a = lo > 0x80 ? lo : 0x80, b = hi < 0x1FFFF ? hi : 0x1FFFF;
-            if (b >= a && b - a > 0x4000) fail_unsupported(c, "case folding of non-ASCII runes");
-            for (uint32_t r = a; r <= b && b >= a; r++) {
-                if (r == 0x212A || r == 0x17F) continue;
-                if (is_cased(r)) fail_unsupported(c, "case folding of non-ASCII runes");
-            }
-        }
+static int rg_contains(ranges g, uint32_t r) {  /* g normalised */
+    int a = 0, b = g.n - 1;
+    while (a <= b) {
+        const int m = (a + b) / 2;
+        if (r < g.r[m].lo) b = m - 1;
+        else if (r > g.r[m].hi) a = m + 1;
+        else return 1;
     }
+    return 0;
+}
+
+/* appendFoldedRange over every range: the class closed under simple case folding */
+static ranges fold_ranges(ctx* c, ranges g) {
+    ranges n = rg_norm(c, g), out = {0};
+    rg_extend(c, &out, n);
+    for (size_t t = 0; t < sizeof kUniFold / sizeof kUniFold[0]; t++)
+        if (rg_contains(n, kUniFold[t][0]))
+            for (uint32_t x = kUniFold[t][1]; x != kUniFold[t][0]; x = simple_fold(x)) rg_add(c, &out, x, x);
     return rg_norm(c, out);
+}
+
+/* appendGroup: under (?i) a group is folded BEFORE it is negated */
+static ranges group_ranges(int fi, ctx* c, ranges g, int negated) {
+    if (fi) g = fold_ranges(c, g);
+    return negated ? rg_negate(c, g) : rg_norm(c, g);
 }
 
 /* ---------------------------------------------------------------------------- AST */
@@ -321,8 +280,8 @@ static node* parse_alt(parser* p, int top);
 
 static node* lit(parser* p, uint32_t r) {
     if (p->fi) {
-        uint32_t orbit[3];
-        const int k = fold_orbit(p->c, r, orbit);
+        uint32_t orbit[8];
+        const int k = fold_orbit(r, orbit);
         if (k > 1) {
             node* n = mk(p->c, N_CLASS);
             ranges g = {0};
@@ -414,21 +373,100 @@ static ranges perl_class_ranges(ctx* c, char cl) {
     return g;
 }
 
-/* parsePerlClassEscape: \d \s \w (and negations) at p->i -> 1 with *out, else 0 */
+static int valid_utf8(const uint8_t* b, size_t n) {  /* checkUTF8 */
+    for (size_t i = 0; i < n;) {
+        if (!full_rune_ok(b, n, i)) return 0;
+        int w;
+        decode_rune(b, n, i, &w);
+        i += (size_t)w;
+    }
+    return 1;
+}
+
+/* unicodeTable (parse.go): "Any", unicode.Categories, unicode.Scripts -> 1 with *out, else 0 */
+static int unicode_table(ctx* c, const uint8_t* name, size_t nl, ranges* out) {
+    ranges g = {0};
+    if (nl == 3 && memcmp(name, "Any", 3) == 0) {
+        rg_add(c, &g, 0, MAX_RUNE);
+        *out = g;
+        return 1;
+    }
+    int a = 0, b = (int)(sizeof kUniClasses / sizeof kUniClasses[0]) - 1;
+    while (a <= b) {
+        const int m = (a + b) / 2;
+        const char* k = kUniClasses[m].name;
+        const size_t kl = strlen(k);
+        int d = memcmp(k, name, kl < nl ? kl : nl);
+        if (d == 0) d = kl < nl ? -1 : kl > nl;
+        if (d == 0) {
+            for (uint32_t t = 0; t < kUniClasses[m].n; t++)
+                rg_add(c, &g, kUniRanges[kUniClasses[m].off + t][0], kUniRanges[kUniClasses[m].off + t][1]);
+            *out = g;
+            return 1;
+        }
+        if (d < 0) a = m + 1;
+        else b = m - 1;
+    }
+    return 0;
+}
+
+/* parseUnicodeClass: \pN \p{Name} \P.. \p{^Name} at p->i ('\') -> the group's ranges */
+static ranges unicode_class(parser* p) {
+    const size_t start = p->i;
+    int neg = p->s[p->i + 1] == 'P';
+    p->i += 2;
+    const uint8_t* name;
+    size_t nl, seq_end;
+    if (p->i < p->n && p->s[p->i] == '{') {
+        size_t end = p->n;
+        for (size_t k = p->i; k < p->n; k++)
+            if (p->s[k] == '}') {
+                end = k;
+                break;
+            }
+        if (end == p->n) {
+            if (!valid_utf8(p->s + start, p->n - start)) fail_syntax(p->c, E_UTF8, p->s + start, p->n - start);
+            fail_syntax(p->c, E_RANGE, p->s + start, p->n - start);
+        }
+        name = p->s + p->i + 1;
+        nl = end - (p->i + 1);
+        if (!valid_utf8(name, nl)) fail_syntax(p->c, E_UTF8, name, nl);
+        seq_end = end + 1;
+    } else if (p->i < p->n) {
+        if (!full_rune_ok(p->s, p->n, p->i)) fail_syntax(p->c, E_UTF8, p->s + p->i, p->n - p->i);
+        int w;
+        decode_rune(p->s, p->n, p->i, &w);
+        name = p->s + p->i;
+        nl = (size_t)w;
+        seq_end = p->i + (size_t)w;
+    } else {
+        name = p->s + p->i;
+        nl = 0;
+        seq_end = p->i;
+    }
+    p->i = seq_end;
+    if (nl && name[0] == '^') {
+        neg = !neg;
+        name++;
+        nl--;
+    }
+    ranges tab;
+    if (!nl || !unicode_table(p->c, name, nl, &tab)) fail_syntax(p->c, E_RANGE, p->s + start, seq_end - start);
+    return group_ranges(p->fi, p->c, tab, neg);
+}
+
+/* parsePerlClassEscape (\d \s \w and negations) or parseUnicodeClass (\p \P) at p->i -> 1 with *out */
 static int perl_class(parser* p, ranges* out) {
     if (p->i + 1 < p->n && p->s[p->i] == '\\') {
         const char c = (char)p->s[p->i + 1];
         if (c && strchr("dswDSW", c)) {
             p->i += 2;
-            const char lc = (char)(c | 0x20);
-            ranges g = perl_class_ranges(p->c, lc);
-            *out = (c >= 'A' && c <= 'Z') ? rg_negate(p->c, g) : g;
+            *out = group_ranges(p->fi, p->c, perl_class_ranges(p->c, (char)(c | 0x20)), c >= 'A' && c <= 'Z');
             return 1;
         }
         if (c == 'p' || c == 'P') {
-            char w[32];
-            snprintf(w, sizeof w, "Unicode class \\%c", c);
-            fail_unsupported(p->c, w);
+            *out = unicode_class(p);
+            return 1;
         }
     }
     return 0;
@@ -559,7 +597,7 @@ static ranges parse_class(parser* p) {
                 if (found < 0) fail_syntax(p->c, E_RANGE, p->s + p->i, (size_t)(end + 2 - (p->s + p->i)));
                 ranges pr = {0};
                 for (int t = 0; t < kPosix[found].n; t++) rg_add(p->c, &pr, kPosix[found].r[t][0], kPosix[found].r[t][1]);
-                rg_extend(p->c, &g, pneg ? rg_negate(p->c, pr) : pr);
+                rg_extend(p->c, &g, group_ranges(p->fi, p->c, pr, pneg));
                 p->i = (size_t)(end + 2 - p->s);
                 first = 0;
                 continue;
@@ -616,7 +654,7 @@ static void parse_escape_atom(parser* p, node* seq) {
     ranges g;
     if (perl_class(p, &g)) {
         node* n = mk(p->c, N_CLASS);
-        n->cls = p->fi ? fold_ranges(p->c, g) : rg_norm(p->c, g);
+        n->cls = g;
         push(p->c, seq, n);
         return;
     }

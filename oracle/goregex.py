@@ -15,11 +15,15 @@ regexp.MatchString(pattern, str): compile, then an unanchored search) and for re
             (utf8.DecodeRuneInString; an invalid byte is U+FFFD of width 1) with Go's empty-width
             assertions (begin/end line and text, ASCII word boundary).
 
-PARITY UNPINNED beyond the reference's own rows (tests.go:2064-2121, list_test.go:397-431):
-Unicode classes (\\p{..}, [[:^..:]] is fine) and case folding of non-ASCII letters are NOT
-restated -- compile() raises Unsupported for them (the engine rejects them the same way).
+Unicode classes (\\p{..} / \\P{..}: unicode.Categories, unicode.Scripts, "Any") and simple case
+folding read the tables tools/gen_unicode_tables.py generates (oracle/unicode_tables.json, Unicode
+13 here where Go 1.9 has Unicode 9).  PARITY UNPINNED beyond the reference's own rows (tests.go:
+2064-2121, list_test.go:397-431).
 """
 from __future__ import annotations
+
+import json
+import os
 
 MAX_REPEAT = 1000
 MAX_RUNE = 0x10FFFF
@@ -112,6 +116,16 @@ def full_rune_ok(b: bytes, i: int) -> bool:
     return not (r == 0xFFFD and w == 1 and b[i:i + 3] != b"\xef\xbf\xbd")
 
 
+def valid_utf8(b: bytes) -> bool:
+    """checkUTF8 (parse.go)."""
+    i = 0
+    while i < len(b):
+        if not full_rune_ok(b, i):
+            return False
+        i += decode_rune(b, i)[1]
+    return True
+
+
 def is_word(r: int) -> bool:
     return r >= 0 and (0x30 <= r <= 0x39 or 0x41 <= r <= 0x5A or 0x61 <= r <= 0x7A or r == 0x5F)
 
@@ -138,48 +152,47 @@ def negate(ranges):
     return out
 
 
-# simple case folding orbits that involve ASCII (unicode.SimpleFold): k K U+212A, s S U+017F
-_SPECIAL = {0x6B: [0x4B, 0x212A], 0x4B: [0x6B, 0x212A], 0x212A: [0x4B, 0x6B],
-            0x73: [0x53, 0x17F], 0x53: [0x73, 0x17F], 0x17F: [0x53, 0x73]}
+_UNI = None
+
+
+def _uni():
+    """(classes: name -> ranges, fold: rune -> next rune of its orbit) from unicode_tables.json."""
+    global _UNI
+    if _UNI is None:
+        d = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "unicode_tables.json")))
+        _UNI = ({k: [tuple(r) for r in v] for k, v in d["classes"].items()}, {a: b for a, b in d["fold"]})
+    return _UNI
 
 
 def fold_orbit(r: int):
-    if r in _SPECIAL:
-        return [r] + _SPECIAL[r]
-    if 0x41 <= r <= 0x5A:
-        return [r, r + 32]
-    if 0x61 <= r <= 0x7A:
-        return [r, r - 32]
-    if r >= 0x80 and (chr(r).lower() != chr(r) or chr(r).upper() != chr(r)):
-        raise Unsupported("case folding of non-ASCII letter U+%04X" % r)
-    return [r]
-
-
-def _cased(r: int) -> bool:
-    c = chr(r)
-    return c.lower() != c or c.upper() != c
+    """r and the rest of its unicode.SimpleFold orbit."""
+    fold = _uni()[1]
+    out, x = [r], fold.get(r, r)
+    while x != r:
+        out.append(x)
+        x = fold[x]
+    return out
 
 
 def fold_ranges(ranges):
-    """appendFoldedRange for the ASCII letters and the two non-ASCII runes whose orbits reach ASCII
-    (U+212A KELVIN SIGN ~ k, U+017F LONG S ~ s).  A range covering every non-ASCII rune gains only
-    those ASCII partners (its other orbits stay inside it); any other range holding a cased
-    non-ASCII rune needs Unicode fold tables: Unsupported."""
-    out = list(ranges)
-    for lo, hi in ranges:
-        for a, b in ((0x41, 0x5A), (0x61, 0x7A)):
-            x, y = max(lo, a), min(hi, b)
-            if x <= y:
-                d = 32 if a == 0x41 else -32
-                out.append((x + d, y + d))
-        for r in _SPECIAL:
-            if lo <= r <= hi:
-                out.extend((o, o) for o in _SPECIAL[r])
-        if hi >= 0x80 and not (lo <= 0x80 and hi == MAX_RUNE):
-            a, b = max(lo, 0x80), min(hi, 0x1FFFF)
-            if b - a > 0x4000 or any(_cased(r) for r in range(a, b + 1) if r not in _SPECIAL):
-                raise Unsupported("case folding of non-ASCII runes")
+    """appendFoldedRange over every range: the class closed under simple case folding."""
+    fold = _uni()[1]
+    rs = norm(ranges)
+    out = list(rs)
+    import bisect
+    starts = [lo for lo, _ in rs]
+    for r in fold:
+        k = bisect.bisect_right(starts, r) - 1
+        if k >= 0 and r <= rs[k][1]:
+            out.extend((o, o) for o in fold_orbit(r))
     return norm(out)
+
+
+def unicode_class(name):
+    """unicodeTable (parse.go): "Any", unicode.Categories, unicode.Scripts; None when unknown."""
+    if name == "Any":
+        return [(0, MAX_RUNE)]
+    return _uni()[0].get(name)
 
 
 # ------------------------------------------------------------------------------- AST
@@ -388,17 +401,58 @@ class _Parser:
         self.i += 1
         seq.append(("group", self.parse_alt(top=False)))
 
+    def group(self, rs, negated):
+        """appendGroup: under (?i) the group is folded BEFORE it is negated."""
+        if self.flags["i"]:
+            rs = fold_ranges(rs)
+        return negate(rs) if negated else norm(rs)
+
     def perl_class(self):
-        """parsePerlClassEscape: \\d \\s \\w (and negations) at self.i, or None."""
+        """parsePerlClassEscape (\\d \\s \\w and negations) or parseUnicodeClass (\\p, \\P) at
+        self.i -> the group's ranges, or None."""
         s = self.src
         if self.i + 1 < len(s) and s[self.i] == ord("\\") and chr(s[self.i + 1]) in "dswDSW":
             c = chr(s[self.i + 1])
             self.i += 2
-            rs = PERL_CLASSES[c.lower()]
-            return negate(rs) if c.isupper() else list(rs)
+            return self.group(PERL_CLASSES[c.lower()], c.isupper())
         if self.i + 1 < len(s) and s[self.i] == ord("\\") and chr(s[self.i + 1]) in "pP":
-            raise Unsupported("Unicode class \\%s" % chr(s[self.i + 1]))
+            return self.unicode_class()
         return None
+
+    def unicode_class(self):
+        """parseUnicodeClass: \\pN, \\p{Name}, \\P.., \\p{^Name}; unknown -> invalid character class range."""
+        s = self.src
+        start = self.i
+        neg = s[self.i + 1] == ord("P")
+        self.i += 2
+        if self.i < len(s) and s[self.i] == ord("{"):
+            end = s.find(b"}", self.i)
+            if end < 0:
+                if not valid_utf8(s[start:]):
+                    self.err(E_UTF8, self.text(start))
+                self.err(E_RANGE, self.text(start))
+            name = s[self.i + 1:end]
+            if not valid_utf8(name):
+                self.err(E_UTF8, self.text(self.i + 1, end))
+            seq_end = end + 1
+        else:
+            if self.i < len(s):
+                if not full_rune_ok(s, self.i):
+                    self.err(E_UTF8, self.text(self.i))
+                r, w = decode_rune(s, self.i)
+                name = s[self.i:self.i + w]
+                seq_end = self.i + w
+            else:
+                name, seq_end = b"", self.i
+        self.i = seq_end
+        name = name.decode("utf-8", "surrogateescape")
+        if name.startswith("^"):
+            neg = not neg
+            name = name[1:]
+        tab = unicode_class(name) if name else None
+        if tab is None:
+            self.err(E_RANGE, self.text(start, seq_end))
+        return self.group(tab, neg)
 
     def parse_escape(self):
         """parseEscape (parse.go): one escaped rune at self.i ('\\'); errors carry the text consumed."""
@@ -476,7 +530,7 @@ class _Parser:
                 return
         rs = self.perl_class()
         if rs is not None:
-            seq.append(("class", fold_ranges(rs) if self.flags["i"] else norm(rs)))
+            seq.append(("class", rs))
             return
         seq.append(self.lit(self.parse_escape()))
 
@@ -507,8 +561,7 @@ class _Parser:
                         name = name[1:]
                     if name not in POSIX_CLASSES:
                         self.err(E_RANGE, self.text(self.i, end + 2))
-                    rs = POSIX_CLASSES[name]
-                    ranges += negate(rs) if pneg else rs
+                    ranges += self.group(POSIX_CLASSES[name], pneg)
                     self.i = end + 2
                     first = False
                     continue

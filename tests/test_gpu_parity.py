@@ -475,7 +475,10 @@ def test_empty_batches_and_rule_sets(mxp):
 
 
 UTF8_PATTERNS = ["^/api/v[0-9]+/é", "日本", "^.{3}$", "[à-ÿ]+x", "^[^a-z]*$", "😀$", "^(a|é|日)+$", ".", "^$",
-                 "é.*日.*😀", "[\\x{4e00}-\\x{9fff}]{2}", "^/[a-z]+/[^/]+$", "a.b", "^[a-zé/0-9]{8,}$", "ÿ{2}|zz"]
+                 "é.*日.*😀", "[\\x{4e00}-\\x{9fff}]{2}", "^/[a-z]+/[^/]+$", "a.b", "^[a-zé/0-9]{8,}$", "ÿ{2}|zz",
+                 # Unicode classes and non-ASCII folding (parity unpinned: see test_regex_oracle.UNICODE_KAT)
+                 "\\p{Han}{2}", "(?i)éΣ", "^\\pL{3}", "\\P{L}$", "(?i)[à-ö]x", "[\\p{Greek}\\p{Nd}]{2}", "(?i)\\W\\W",
+                 "^\\p{Ll}+$", "\\p{So}"]
 
 
 @pytest.mark.parametrize("seed", [3, 4])
@@ -484,8 +487,8 @@ def test_regex_utf8_subjects_parity(mxp, seed):
     cross the DFA walker's 8-byte windows at every offset: constant patterns (rule-set DFAs) and a
     pattern read from an attribute (per-batch DFAs), against the oracle's Go regexp restatement."""
     rng = np.random.default_rng(seed)
-    alphabet = ["a", "b", "z", "x", "/", "0", "9", "A", "-", "é", "ÿ", "à", "日", "本", "😀"]
-    weights = np.array([6, 3, 2, 2, 4, 2, 2, 1, 1, 2, 2, 1, 2, 1, 1], dtype=float)
+    alphabet = ["a", "b", "z", "x", "/", "0", "9", "A", "-", "é", "ÿ", "à", "日", "本", "😀", "Σ", "ς", "É", "K", "ſ"]
+    weights = np.array([6, 3, 2, 2, 4, 2, 2, 1, 1, 2, 2, 1, 2, 1, 1, 1, 1, 1, 1, 1], dtype=float)
     subjects = []
     for _ in range(3000):
         L = int(rng.integers(0, 41))

@@ -1,0 +1,96 @@
+"""Regexps the DFA compiler cannot hold, on the GPU: patterns whose DFA is over the rules' 65,536-state
+budget walk the bit-parallel NFA (regex.cpp build_nfa, dfa_dev.h mxp_nfa_run) -- as rule constants,
+through the guard index, in value classes and as run-time patterns -- and regex lists are packed into
+several automata so a valid list always builds (regexList.go:26-65).  Against the oracle's Go regexp
+restatement (oracle/goregex.c): identical codes per pair / per symbol.  PARITY UNPINNED beyond the
+reference rows (no reference fixture holds over-budget patterns)."""
+import numpy as np
+import pytest
+
+import lists as L
+import oracle
+from istio_amd import workloads as W
+from istio_amd.bags import BagBatch
+from test_gpu_parity import compare
+from test_regex_product import NFA_PATTERNS, _nfa_subjects
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mxp(libmxp):
+    import istio_amd.engine as mxp
+    return mxp
+
+
+def _quote(p):
+    return p.replace("\\", "\\\\")
+
+
+def _batch(seed, n=2500):
+    rng = np.random.default_rng(seed)
+    subs = _nfa_subjects(rng, n)
+    paths = ["/api/" + s if i % 3 == 0 else s for i, s in enumerate(subs)]
+    manifest = {"request.path": "STRING", "x": "STRING", "y": "STRING"}
+    bags = [{"request.path": p, "x": NFA_PATTERNS[i % len(NFA_PATTERNS)], "y": subs[(i * 7) % n]}
+            for i, p in enumerate(paths)]
+    return manifest, BagBatch.from_bags(bags, names=list(manifest))
+
+
+@pytest.mark.parametrize("flags", ["0", "262144"])  # 262144: value classes forced (mxp_vt_eval_nfa_kernel)
+def test_over_budget_rules_parity(mxp, monkeypatch, flags):
+    monkeypatch.setenv("MXP_DEBUG_FLAGS", flags)
+    manifest, batch = _batch(41)
+    rules = ['"%s".matches(request.path)' % _quote(p) for p in NFA_PATTERNS]
+    rules += ['"^/api/(a|b)*a(a|b){16}".matches(request.path)',            # prefix-indexed (index NFA kernel)
+              'request.path.startsWith("/api/") && "%s".matches(y)' % _quote(NFA_PATTERNS[0]),
+              'x.matches(request.path)',                                     # run-time NFA patterns
+              '"^/api/".matches(request.path) && "é$".matches(y)',          # DFA rules alongside
+              'y == "ab" || "(a|b)*a(a|b){16}".matches(y)']
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    st = eng.compile(rules)
+    assert (st == 0).all(), [eng.rule_error(i) for i in range(len(rules)) if st[i]]
+    got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch, sample_msgs=50)
+    assert (want == 1).sum() > 1000 and 0 < (want[:, 0] == 1).sum() < batch.n
+
+
+def test_nfa_width_limit_is_a_rule_error(mxp):
+    """Over budget and wider than 255 rune instructions: the rule is refused with that reason."""
+    manifest = {"request.path": "STRING"}
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    st = eng.compile(['"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 260), 'request.path == "a"'])
+    assert st[0] != 0 and st[1] == 0
+    assert "NFA" in eng.rule_error(0)
+
+
+def test_regex_list_with_over_budget_patterns(mxp):
+    eng = mxp.Engine(0)
+    rng = np.random.default_rng(5)
+    syms = _nfa_subjects(rng, 3000)
+    pats = ["^zz", NFA_PATTERNS[0], "x{3}", NFA_PATTERNS[2], NFA_PATTERNS[7], "^é"]
+    lst = eng.list_create(L.REGEX, pats, [])
+    parts, nfas = lst.regex_parts()
+    assert nfas >= 2 and parts == nfas + 3  # ^zz | nfa | x{3} | nfa | (nfa) | ^é: NFAs stand alone
+    want = L.codes(L.RegexList(pats).found(syms), False)
+    got = lst.check(syms)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(syms[i], int(got[i]), int(want[i])) for i in bad[:5]]
+    assert (want == 0).sum() > 300 and (want == 5).sum() > 300
+
+
+def test_regex_list_50k_patterns(mxp):
+    """A 50k-pattern list (C3 shape, 5x configs[2]) builds -- packed into several union DFAs -- and
+    matches the oracle on a sample of lookups."""
+    pats, syms, hits = W.c3_regex_list(n_patterns=50_000, n_lookups=600, seed=51, return_hits=True)
+    eng = mxp.Engine(0)
+    lst = eng.list_create(L.REGEX, pats, [])
+    parts, nfas = lst.regex_parts()
+    assert parts >= 1 and nfas == 0
+    assert lst.num_entries() == 50_000
+    want = L.codes(L.RegexList(pats).found(syms), False)
+    got = lst.check(syms)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(syms[i], int(got[i]), int(want[i])) for i in bad[:5]]
+    assert (want == 0).sum() > 200 and (want == 5).sum() > 200

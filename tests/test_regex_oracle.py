@@ -83,16 +83,54 @@ def test_error_texts(pat, msg):
     assert str(ei.value) == "error parsing regexp: " + msg
 
 
-def test_unsupported_is_explicit():
-    for pat in ["\\pL", "\\p{Greek}", "(?i)é"]:
-        with pytest.raises(G.Unsupported):
-            G.compile(pat)
-    G.compile("(?i)\\W")  # full non-ASCII coverage: folds only the k / s partners
-    assert G.match(G.compile("(?i)\\W"), "k")
+# Unicode classes and non-ASCII case folding (tables from tools/gen_unicode_tables.py, Unicode 13 where
+# Go 1.9 has Unicode 9): PARITY UNPINNED -- restated from parse.go's parseUnicodeClass / appendGroup /
+# appendFoldedRange; no reference fixture covers them.  A negated group is folded before it is negated
+# ((?i)\W excludes k, s and their non-ASCII partners, as Go's own parse tests list it).
+UNICODE_KAT = [
+    ("\\pL", "é", True), ("\\pL", "1", False), ("\\p{L}", "ж", True), ("\\PL", "ж", False), ("\\PL", "1", True),
+    ("\\p{Greek}", "α", True), ("\\p{Greek}", "a", False), ("\\P{Greek}", "α", False), ("\\p{^Greek}", "a", True),
+    ("\\P{^Greek}", "Ω", True), ("^\\p{Lu}+$", "ABC", True), ("^\\p{Lu}+$", "AbC", False), ("\\p{Nd}", "٣", True),
+    ("\\pN", "½", True), ("\\p{Han}", "中", True), ("\\p{Cyrillic}", "z", False), ("\\p{Any}", "\n", True),
+    ("^\\p{Any}$", "", False), ("[\\p{Nd}x]", "x", True), ("[^\\p{L}]", "q", False), ("[^\\p{L}]", "7", True),
+    ("[\\P{L}]", "7", True), ("\\pZ", "\u00a0", True), ("\\p{Zs}", " ", True), ("\\p{Cc}", "\x01", True),
+    ("\\p{C}", "\u200b", True), ("\\p{Sm}", "+", True), ("\\p{Latin}", "é", True),
+    ("(?i)é", "É", True), ("(?i)σ", "Σ", True), ("(?i)σ", "ς", True), ("(?i)ς", "Σ", True), ("σ", "Σ", False),
+    ("(?i)ǅ", "ǆ", True), ("(?i)µ", "μ", True), ("(?i)µ", "Μ", True), ("(?i)[à-ÿ]+", "ÀÉÎ", True),
+    ("(?i)[à-å]", "Æ", False), ("(?i)ж", "Ж", True), ("(?i)\\p{Lu}", "a", True), ("\\p{Lu}", "a", False),
+    ("(?i)\\P{Lu}", "a", False), ("(?i)\\P{Lu}", "1", True), ("(?i)\\W", "k", False), ("(?i)\\W", "K", False),
+    ("(?i)\\W", "ſ", False), ("\\W", "ſ", True), ("(?i)[\\W]", "s", False), ("(?i)[^\\W]", "K", True),
+    ("(?i)\\w", "K", True), ("(?i)[[:^lower:]]", "A", False), ("(?i)[[:^lower:]]", "1", True),
+    ("[[:^lower:]]", "A", True), ("(?i)\\D", "1", False), ("(?i)[^k]", "K", False), ("(?i)[^k]", "x", True),
+    ("(?i)ΣΑΣ", "σας", True), ("(?i)straße", "STRASSE", False), ("(?i)ß", "ẞ", True),
+]
+
+UNICODE_ERRORS = [
+    ("\\p{Foo}", "invalid character class range: `\\p{Foo}`"),
+    ("\\pX", "invalid character class range: `\\pX`"),
+    ("\\p", "invalid character class range: `\\p`"),
+    ("\\p{Greek", "invalid character class range: `\\p{Greek`"),
+    ("a\\P{}", "invalid character class range: `\\P{}`"),
+    ("[\\p{Bogus}]", "invalid character class range: `\\p{Bogus}`"),
+    ("\\p{^}", "invalid character class range: `\\p{^}`"),
+    ("\\pé", "invalid character class range: `\\pé`"),
+]
+
+
+@pytest.mark.parametrize("pat,subj,want", UNICODE_KAT)
+def test_unicode_known_answers(pat, subj, want):
+    assert G.match(G.compile(pat), subj) is want, (pat, subj)
+
+
+@pytest.mark.parametrize("pat,msg", UNICODE_ERRORS)
+def test_unicode_error_texts(pat, msg):
+    with pytest.raises(G.RegexError) as ei:
+        G.compile(pat)
+    assert str(ei.value) == "error parsing regexp: " + msg
 
 
 # ---- the C restatement (oracle/goregex.c, what the C interpreter and the CPU baseline run) against
-# this Python one: same answers, same error texts, same Unsupported line
+# this Python one: same answers, same error texts
 def _c(pat, subj=""):
     import oracle
     return oracle.regex_match(pat, subj)
@@ -108,16 +146,22 @@ def test_c_restatement_error_texts(pat, msg):
     assert _c(pat) == (-1, "error parsing regexp: " + msg)
 
 
-def test_c_restatement_unsupported():
-    for pat in ["\\pL", "\\p{Greek}", "(?i)é", "(?i)[à-ÿ]"]:
-        assert _c(pat)[0] == -2, pat
-    assert _c("(?i)\\W", "k")[0] == 1
+@pytest.mark.parametrize("pat,subj,want", UNICODE_KAT)
+def test_c_restatement_unicode(pat, subj, want):
+    assert _c(pat, subj) == (1 if want else 0, ""), (pat, subj)
+
+
+@pytest.mark.parametrize("pat,msg", UNICODE_ERRORS)
+def test_c_restatement_unicode_errors(pat, msg):
+    assert _c(pat) == (-1, "error parsing regexp: " + msg)
 
 
 def _random_pattern(rng, depth=0):
     atoms = ["a", "b", "ab", ".", "\\d", "\\w", "\\s", "[a-c]", "[^b]", "[[:alpha:]]", "\\b", "^", "$", "(?i)a",
              "é", "\\x41", "[a-]", "x{2}", "\\.", "(?m)^a", "\\z", "\\A", "[\\d_]", "k", "(?s).", "\\Qa.\\E",
-             "\xff", "(", ")", "[", "*", "{1,", "\\", "a{3,2}", "(?P<n>a)", "(?:b)", "|"]
+             "\xff", "(", ")", "[", "*", "{1,", "\\", "a{3,2}", "(?P<n>a)", "(?:b)", "|", "\\pL", "\\p{Greek}",
+             "\\PN", "(?i)é", "[\\p{Lu}x]", "\\p{^Ll}", "(?i)\\W", "[[:^lower:]]", "(?i)[\\W]", "σ", "(?i)Σ",
+             "\\p{Foo}", "(?i)[à-ÿ]", "\\p"]
     out = []
     for _ in range(int(rng.integers(1, 5))):
         r = rng.random()
@@ -135,7 +179,8 @@ def _random_pattern(rng, depth=0):
 def test_c_restatement_random_patterns_match_python():
     import numpy as np
     rng = np.random.default_rng(5)
-    subjects = ["", "a", "ab", "abc", "a\nb", "xyz123", "Ab_9 c", "é", "\udcff", "k", "K", "aaab", "a.b", "  "]
+    subjects = ["", "a", "ab", "abc", "a\nb", "xyz123", "Ab_9 c", "é", "\udcff", "k", "K", "aaab", "a.b", "  ",
+                "Σσς", "ΑΒΓ", "٣", "ǅ", "Éé", "ſ"]
     n_ok = n_err = 0
     for _ in range(1500):
         pat = _random_pattern(rng)
@@ -144,9 +189,6 @@ def test_c_restatement_random_patterns_match_python():
         except G.RegexError as e:
             assert _c(pat) == (-1, str(e)), pat
             n_err += 1
-            continue
-        except G.Unsupported:
-            assert _c(pat)[0] == -2, pat
             continue
         for s in subjects:
             assert _c(pat, s) == (1 if G.match(prog, s) else 0, ""), (pat, s)

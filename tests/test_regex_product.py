@@ -1,12 +1,12 @@
 """The engine's regex compiler (istio_amd/csrc/regex.cpp: Go regexp parse -> NFA -> DFA), stepped on
 the host through mxp_regex_match_host, against the oracle restatement (oracle/goregex.py): every
-known-answer, error and unsupported case of tests/test_regex_oracle.py plus seeded random patterns
+known-answer, error and Unicode case of tests/test_regex_oracle.py plus seeded random patterns
 over random subjects.  The GPU kernels step these same DFA tables (test_gpu_regex.py)."""
 import numpy as np
 import pytest
 
 import goregex as G
-from test_regex_oracle import ERRORS, GOLDEN, KAT
+from test_regex_oracle import ERRORS, GOLDEN, KAT, UNICODE_ERRORS, UNICODE_KAT
 
 
 @pytest.fixture(scope="module")
@@ -25,15 +25,17 @@ def test_error_texts(rx):
         assert rx(pat, "") == (-1, "error parsing regexp: " + msg), pat
 
 
-def test_unsupported(rx):
-    for pat in ["\\pL", "\\p{Greek}", "(?i)é", "(?i)[à-ÿ]"]:
-        assert rx(pat, "x")[0] == -2, pat
-    assert rx("(?i)\\W", "k") == (1, "")
+def test_unicode_classes_and_folding(rx):
+    for pat, subj, want in UNICODE_KAT:
+        assert rx(pat, subj) == (1 if want else 0, ""), (pat, subj)
+    for pat, msg in UNICODE_ERRORS:
+        assert rx(pat, "") == (-1, "error parsing regexp: " + msg), pat
 
 
 ATOMS = ["a", "b", "ab", ".", "[a-c]", "[^b]", "\\d", "\\w", "\\s", "\\b", "\\B", "^", "$", "(?i:a)", "(a|b)",
          "(?:ab|ba)", "a*", "b+", "c?", "x{2}", "a{1,2}", "[[:alpha:]]", "\\.", "é", "\\x{e9}", "(?s:.)", "(?m:^)",
-         "(?m:$)", "\\Aa", "a\\z", "[a-]", "k", "(?i)k"]
+         "(?m:$)", "\\Aa", "a\\z", "[a-]", "k", "(?i)k", "\\pL", "\\p{Greek}+", "\\P{L}", "(?i)σ", "(?i)[à-ÿ]",
+         "[\\p{Nd}_]", "(?i)\\W", "\\p{Lu}\\p{Ll}"]
 
 
 def random_patterns(n, seed):
@@ -71,10 +73,58 @@ def test_random_patterns_match_oracle(rx, seed):
         except G.RegexError as e:
             assert rx(p, "") == (-1, str(e)), p
             continue
-        except G.Unsupported:
-            assert rx(p, "")[0] == -2, p
-            continue
         for s in subs:
             want = G.match(prog, s)
             got = rx(p, s)
             assert got == (1 if want else 0, ""), (p, s, got, want)
+
+
+# Patterns whose DFA is over the rules' 65,536-state budget: the bit-parallel NFA (regex.cpp
+# build_nfa; the device walks the same image, dfa_dev.h mxp_nfa_run), against the C oracle.
+NFA_PATTERNS = ["(a|b)*a(a|b){16}", "^(a|b)*b(a|b){17}$", "(?m)^x.{16}y$", "\\b[ab]*a[ab]{16}\\b", "(?i)é.{16}z",
+                "(a|b)*a(a|b){15}(c|$)", "[^x]*x.{20}\\z", "é[\\pL ]{16}\\PL"]
+
+
+def _nfa_subjects(rng, n):
+    alpha = ["a", "b", "x", "y", "z", "é", "É", "\n", " ", "c", "1"]
+    w = np.array([8, 8, 2, 1, 1, 1, 1, 1, 1, 1, 1], dtype=float)
+    out = []
+    for _ in range(n):
+        L = int(rng.integers(0, 48))
+        out.append("".join(rng.choice(alpha, size=L, p=w / w.sum())))
+    return out
+
+
+def test_over_budget_patterns_walk_the_nfa(rx):
+    import oracle
+    rng = np.random.default_rng(9)
+    subs = _nfa_subjects(rng, 400) + ["a" + "b" * 16, "b" * 18 + "a" + "a" * 16, "x" + "0" * 16 + "y", ""]
+    for p in NFA_PATTERNS:
+        n_true = 0
+        for s in subs:
+            want = oracle.regex_match(p, s)
+            assert want[0] in (0, 1), (p, want)
+            got = rx(p, s)
+            assert got == want, (p, s, got, want)
+            n_true += got[0]
+        assert 0 < n_true < len(subs), p
+
+
+def test_nfa_width_limit(rx):
+    """Over budget AND more than 255 rune instructions: the one refusal left (-3, err says why)."""
+    p = "(a|b)*a(a|b){16}" + "c" * 260
+    rc, err = rx(p, "ab")
+    assert rc == -3 and "NFA" in err
+
+
+def test_over_budget_rules_compile(libmxp):
+    """Rule compile (host-only engine): over-budget constant patterns are accepted (their rules walk
+    the NFA); only an over-budget pattern wider than the NFA is refused, naming why."""
+    from istio_amd.engine import Engine
+    eng = Engine(-1)
+    eng.set_vocabulary({"request.path": "STRING"})
+    rules = ['"%s".matches(request.path)' % p.replace("\\", "\\\\") for p in NFA_PATTERNS]
+    rules.append('"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 260))
+    st = eng.compile(rules)
+    assert (st[:-1] == 0).all(), [eng.rule_error(i) for i in range(len(rules) - 1) if st[i]]
+    assert st[-1] != 0 and "NFA" in eng.rule_error(len(rules) - 1)
