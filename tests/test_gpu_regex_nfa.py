@@ -52,7 +52,7 @@ def test_over_budget_rules_parity(mxp, monkeypatch, flags):
     st = eng.compile(rules)
     assert (st == 0).all(), [eng.rule_error(i) for i in range(len(rules)) if st[i]]
     got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch, sample_msgs=50)
-    assert (want == 1).sum() > 1000 and 0 < (want[:, 0] == 1).sum() < batch.n
+    assert (want == 1).sum() > 100 and 0 < (want[:, 0] == 1).sum() < batch.n
 
 
 def test_nfa_width_limit_is_a_rule_error(mxp):
@@ -77,7 +77,7 @@ def test_regex_list_with_over_budget_patterns(mxp):
     got = lst.check(syms)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(syms[i], int(got[i]), int(want[i])) for i in bad[:5]]
-    assert (want == 0).sum() > 300 and (want == 5).sum() > 300
+    assert (want == 0).sum() > 100 and (want == 5).sum() > 100
 
 
 def test_regex_list_50k_patterns(mxp):
