@@ -106,6 +106,8 @@ def from_tagged(v):
         return bytes.fromhex(v["v"])
     if t == "map":
         return dict(v["v"])
+    if t == "nil":
+        return None
     raise ValueError("unsupported tagged value %r" % (v,))
 
 

@@ -170,6 +170,14 @@ class OracleProgram:
         return "ok", _result_value(r, batch)
 
 
+def eval_il(program: ilcompile.Program, fn: str, batch: BagBatch, req: int = 0):
+    """interpreter.New(program, nil).Eval(fn, bag) (interpreter.go:62-69): ('ok', value) |
+    ('error', msg) | ('panic', msg)."""
+    if program.get(fn) is None:
+        return "error", "function not found: '%s'" % fn
+    return OracleProgram(program).run(batch, req, fn)
+
+
 def _result_value(r: _Result, batch: BagBatch):
     """interpreter.Result.AsInterface (result.go:99-116)."""
     t = r.rtype

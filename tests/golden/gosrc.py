@@ -130,10 +130,17 @@ class Parser:
         return name
 
     def parse_value(self):
+        v = self.parse_term()
+        while self.peek()[1] in ("+", "-"):
+            op = self.next()[1]
+            v = ("concat" if op == "+" else "sub", v, self.parse_term())
+        return v
+
+    def parse_term(self):
         v = self.parse_unary()
-        while self.peek()[1] == "+":
+        while self.peek()[1] == "*":
             self.next()
-            v = ("concat", v, self.parse_unary())
+            v = ("mul", v, self.parse_unary())
         return v
 
     def parse_unary(self):

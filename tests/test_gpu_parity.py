@@ -504,3 +504,26 @@ def test_regex_utf8_subjects_parity(mxp, seed):
     assert (eng.compile(rules) == 0).all(), [eng.rule_error(i) for i in range(len(rules))]
     got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch, sample_msgs=50)
     assert (want == 1).sum() > 2000 and (want == 0).sum() > 2000
+
+
+def test_extern_kats_on_gpu(mxp):
+    """mixer/pkg/il/runtime/externs_test.go:24-129 (tests/golden/externs_kat.json) through the GPU
+    engine: the externs as predicates over attributes, pair by pair against the oracle, and the KATs'
+    expected outcomes themselves."""
+    from test_oracle_golden import EXTERNS, extern_bag
+    manifest = {"s1": "STRING", "s2": "STRING"}
+    rules = ["ip(s1) == ip(s2)", "timestamp(s1) == timestamp(s2)", "match(s1, s2)", "s1.matches(s2)"]
+    batch = BagBatch.from_bags([extern_bag(c) for c in EXTERNS], names=list(manifest))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    got, _ = compare(eng, oracle.OracleEvaluator(manifest), rules, batch)
+    col = {"ip": 0, "ip_equal": 0, "timestamp": 1, "timestamp_equal": 1, "match": 2, "matches": 3}
+    for q, c in enumerate(EXTERNS):
+        code = int(got[q, col[c["fn"]]])
+        if c.get("err"):
+            assert code == 2, c
+        elif isinstance(c.get("want"), bool):
+            assert code == int(c["want"]), c
+        else:  # ip(x) == ip(x), timestamp(x) == timestamp(x) of a valid x
+            assert code == 1, c

@@ -1,8 +1,9 @@
 """The oracle (CPU restatement) against the reference's own golden table and parse KATs.
 
 Pins oracle/goexpr.py + oracle/ilcompile.py + oracle/il_interp.c to
-  mixer/pkg/il/testing/tests.go:37-2258 (expressions, IL text, bags, results, errors) and
-  mixer/pkg/expr/expr_test.go:27-76 (parse -> postfix forms).
+  mixer/pkg/il/testing/tests.go:37-2258 (expressions, IL text, bags, results, errors),
+  mixer/pkg/expr/expr_test.go:27-76 (parse -> postfix forms), :190-246 (bad parses) and :258-333
+  (type checks), and mixer/pkg/il/runtime/externs_test.go:24-129 (extern KATs).
 """
 import json
 import os
@@ -80,20 +81,32 @@ def test_parse_postfix_forms():
         assert str(goexpr.parse(src)) == post
 
 
-@pytest.mark.parametrize("src,frag", [
-    ("*a != b", "unexpected expression"), ("a = bc", "unable to parse"), ("3 = 10", "unable to parse"),
-    ("(a.c).d == 300", "unexpected expression"), ("substring(*a, 20) == 12", "unexpected expression"),
-    ("(*a == 20) && 12", "unexpected expression"), ("!*a", "unexpected expression"),
-    ("request.headers[*a] == 200", "unexpected expression"), ("atr == 'aaa'", "unable to parse"),
-    ("c().e.d()", "unexpected expression"), ("foo{}", "unexpected expression"),
-    ("foo{}.bar", "unexpected expression"), ("foo{}.bar()", "unexpected expression"),
-    ("(foo{}).bar()", "unexpected expression"), ("a().b", "unexpected expression"),
-])
+CHECKS = json.load(open(os.path.join(HERE, "golden", "expr_checks.json")))
+
+
+@pytest.mark.parametrize("src,frag", CHECKS["bad_parse"])
 def test_bad_parse(src, frag):
-    """mixer/pkg/expr/expr_test.go:190-246."""
+    """mixer/pkg/expr/expr_test.go:190-246 (TestBadParse)."""
     with pytest.raises(goexpr.ParseError) as ei:
         goexpr.parse(src)
     assert frag in str(ei.value)
+
+
+@pytest.mark.parametrize("case", CHECKS["type_checks"], ids=lambda c: c["s"])
+def test_internal_type_check(case):
+    """mixer/pkg/expr/expr_test.go:258-333 (TestInternalTypeCheck): FuncMap(fns) holds the intrinsics
+    plus the case's functions only; EvalType returns the type or an error containing the fragment."""
+    fns = [goexpr.FunctionMetadata(f["Name"], f["Instance"], goexpr.VT[f["TargetType"]], goexpr.VT[f["ReturnType"]],
+                                   [goexpr.VT[a] for a in f["ArgumentTypes"]]) for f in case["fns"]]
+    attrs = {k: goexpr.VT[v] for k, v in case["attrs"].items()}
+    e = goexpr.parse(case["s"])
+    try:
+        t = goexpr.eval_type(e, attrs, goexpr.func_map(fns))
+    except goexpr.TypeCheckError as err:
+        assert case["err"] != "__SUCCESS__" and case["err"] in str(err), str(err)
+        return
+    assert case["err"] == "__SUCCESS__"
+    assert t == goexpr.VT[case["ret"]]
 
 
 def test_duration_and_constants():
@@ -108,3 +121,48 @@ def test_duration_and_constants():
     assert goexpr.go_parse_duration("-1m30s") == -90 * 10**9
     with pytest.raises(ValueError):
         goexpr.go_parse_duration("1")
+
+
+EXTERNS = json.load(open(os.path.join(HERE, "golden", "externs_kat.json")))["cases"]
+
+
+def extern_expr(case):
+    """The extern KAT as a Mixer expression over attributes s1, s2 (so it runs, not folds)."""
+    fn = case["fn"]
+    if fn == "ip":
+        return "ip(s1)"
+    if fn == "timestamp":
+        return "timestamp(s1)"
+    if fn == "ip_equal":
+        return "ip(s1) == ip(s2)"
+    if fn == "timestamp_equal":
+        return "timestamp(s1) == timestamp(s2)"
+    if fn == "match":
+        return "match(s1, s2)"
+    return "s1.matches(s2)"
+
+
+def extern_bag(case):
+    a = case["args"]
+    return {"s1": a[0], "s2": a[1] if len(a) > 1 else a[0]}
+
+
+@pytest.mark.parametrize("case", EXTERNS, ids=lambda c: "%s%s" % (c["fn"], c["args"]))
+def test_extern_kat(case):
+    import datetime
+    from istio_amd.bags import GoTime
+    ev = oracle.OracleEvaluator({"s1": "STRING", "s2": "STRING"})
+    batch = BagBatch.from_bags([extern_bag(case)])
+    st, v = ev.eval(extern_expr(case), batch, 0)
+    if case.get("err"):
+        assert st == "error", v
+        return
+    assert st == "ok", v
+    if "want_fields" in case:
+        assert isinstance(v, GoTime)
+        t = datetime.datetime.fromtimestamp(v.sec, datetime.timezone.utc)
+        assert [t.year, t.month, t.day, t.hour, t.minute] == case["want_fields"]
+    elif isinstance(case["want"], dict):
+        assert same_value(from_tagged(case["want"]), v)
+    else:
+        assert v is case["want"]
