@@ -434,15 +434,16 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
         "config": {"workload": workload % (R, N),
                    "rules": R, "requests_per_gpu": N, "parallelism": "request-sharded dp%d" % world},
         "eval_ms": step_kernel_ms,
-        "kernels_ms": {"mxp_fill_kernel+mxp_guard2_kernel+mxp_eval_kernel": k_eval,
+        "kernels_ms": {"phase1 (mxp_vt_classify/vt_eval/fill/vtfill/guard2/eval kernels)": k_eval,
                        "mxp_index_kernel+mxp_inject_kernel": k_index},
         "pack_upload_s": t_pack,
         "error_output": "per-request flags (compact)" if compact else "error bitmap",
         "lds_bank_conflicts": lds_conflicts(kind),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "one evaluation: mxp_fill_kernel / mxp_guard2_kernel / mxp_eval_kernel (the groups "
-                               "each serves) + mxp_index_kernel (+ mxp_inject_kernel with dense rules)",
+                     "kernel": "one evaluation: value classes (mxp_vt_classify/vt_eval), mxp_fill / vtfill / guard2 "
+                               "/ eval kernels (the groups each serves) + mxp_index_kernel (+ mxp_inject_kernel with "
+                               "dense rules); traffic also counts mxp_hits_kernel when the hit counters are not fused",
                      "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pair": alg_bytes / (N * R)},
     }
     if quota is not None:

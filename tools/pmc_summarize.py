@@ -16,7 +16,9 @@ import os
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-EVAL_KERNELS = ("mxp_fill_kernel", "mxp_guard_kernel", "mxp_guard2_kernel", "mxp_eval_kernel", "mxp_index_kernel", "mxp_inject_kernel")
+EVAL_KERNELS = ("mxp_fill_kernel", "mxp_vtfill_kernel", "mxp_vt_classify_kernel", "mxp_vt_eval_kernel", "mxp_guard_kernel",
+                "mxp_guard2_kernel", "mxp_eval_kernel", "mxp_index_kernel", "mxp_inject_kernel", "mxp_hits_kernel",
+                "mxp_hits_ragged_kernel")
 
 
 def per_kernel(path_glob, counter):
@@ -49,7 +51,7 @@ def main():
     out = {"workload": a.workload, "rules": a.rules, "requests": a.requests, "kernels": ev,
            "bytes_per_eval": sum(v["hbm_bytes"] for v in ev.values()) if ev else None,
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE separate passes; hbm = 2*FETCH + WRITE (gfx950)"}
-    json.dump(out, open(os.path.join(a.dir, "pmc_traffic.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(a.dir, "pmc_traffic_%s.json" % a.workload), "w"), indent=1)
     print(json.dumps(out))
 
 
