@@ -1109,7 +1109,7 @@ int mxp_engine::pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H)
     return MXP_OK;
 }
 
-int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
+int mxp_engine::pack_on_host(const mxp_bag_batch* b, mxp_dbatch* db) {
     PackedHost H;
     int rc = pack_host(b, db, H);
     if (rc) return rc;
@@ -1149,17 +1149,73 @@ int mxp_engine::pack(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = up(db->rx_ascii, rxb.ascii.data(), rxb.ascii.size() * 2, "upload rx ascii"))) return rc;
     if ((rc = up(db->rx_hilo, rxb.hilo.data(), rxb.hilo.size() * 4, "upload rx hilo"))) return rc;
     if ((rc = up(db->rx_hicls, rxb.hicls.data(), rxb.hicls.size() * 2, "upload rx hicls"))) return rc;
-    if (db->vt_mask) {  // value-class tables of the batch's active columns
-        uint64_t keys = 0;
-        for (uint32_t c : db->vt_capc) keys += c;
-        db->vt_keys_n = keys;
-        const uint32_t act = (uint32_t)__builtin_popcount(db->vt_mask);
-        if ((e = db->vt_cls.alloc((size_t)act * db->n * 2)) != hipSuccess) return hipfail(e, "vt classes");
-        if ((e = db->vt_keys.alloc(keys * 8)) != hipSuccess) return hipfail(e, "vt keys");
-        if ((e = db->vt_rep.alloc(keys * 4)) != hipSuccess) return hipfail(e, "vt reps");
-    }
+    if ((rc = pack_vt_tables(db))) return rc;
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "pack sync");
     return MXP_OK;
+}
+
+int mxp_engine::pack_vt_tables(mxp_dbatch* db) {
+    if (!db->vt_mask) return MXP_OK;  // value-class tables of the batch's active columns
+    hipError_t e;
+    uint64_t keys = 0;
+    for (uint32_t c : db->vt_capc) keys += c;
+    db->vt_keys_n = keys;
+    const uint32_t act = (uint32_t)__builtin_popcount(db->vt_mask);
+    if ((e = db->vt_cls.alloc((size_t)act * db->n * 2)) != hipSuccess) return hipfail(e, "vt classes");
+    if ((e = db->vt_keys.alloc(keys * 8)) != hipSuccess) return hipfail(e, "vt keys");
+    if ((e = db->vt_rep.alloc(keys * 4)) != hipSuccess) return hipfail(e, "vt reps");
+    if ((e = db->vt_cnt.alloc(keys * 4)) != hipSuccess) return hipfail(e, "vt counts");
+    return MXP_OK;
+}
+
+// texts of a device-packed batch's local ids, read back from the device
+bool mxp_dbatch::overlay_string(uint64_t j, std::string* out) const {
+    if (!dev_packed) {
+        if (j >= overlay.size()) return false;
+        *out = std::string(overlay[j]);
+        return true;
+    }
+    if (j >= ns) return false;
+    uint64_t d = 0;
+    if (hipMemcpy(&d, bstr_off.as<uint64_t>() + j, 8, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    out->assign((size_t)(d & 0xFFFFFFu), '\0');
+    return out->empty() || hipMemcpy(&(*out)[0], bstr.as<uint8_t>() + (d >> 24), out->size(), hipMemcpyDeviceToHost) == hipSuccess;
+}
+
+bool mxp_dbatch::overlay_bytes_at(uint64_t j, std::string* out) const {
+    if (!dev_packed) {
+        if (j >= overlay_bytes.size()) return false;
+        *out = std::string(overlay_bytes[j]);
+        return true;
+    }
+    if (j < ns) return overlay_string(j, out);  // a batch string used as bytes
+    const uint64_t q = j - ns;                  // a parsed ip() value
+    if (q >= (uint64_t)G + ns) return false;
+    out->assign(16, '\0');
+    return hipMemcpy(&(*out)[0], pip.as<uint8_t>() + 16 * q, 16, hipMemcpyDeviceToHost) == hipSuccess;
+}
+
+bool mxp_dbatch::overlay_time(uint64_t j, TimeKey* out) const {
+    if (!dev_packed) {
+        if (j >= overlay_times.size()) return false;
+        *out = overlay_times[j];
+        return true;
+    }
+    const int64_t* sec = btsec.as<int64_t>();
+    const int32_t* nsec = btnsec.as<int32_t>();
+    uint64_t k = j;
+    if (j >= nt) {  // a parsed timestamp() value
+        k = j - nt;
+        if (k >= (uint64_t)G + ns) return false;
+        sec = pts_sec.as<int64_t>();
+        nsec = pts_nsec.as<int32_t>();
+    }
+    int64_t s = 0;
+    int32_t x = 0;
+    if (hipMemcpy(&s, sec + k, 8, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    if (hipMemcpy(&x, nsec + k, 4, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    *out = TimeKey{s, x};
+    return true;
 }
 
 void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) const {
@@ -1220,6 +1276,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
         A->vt_tm = db->vt_t.as<uint32_t>();
         A->vt_keys = db->vt_keys.as<unsigned long long>();
         A->vt_rep = db->vt_rep.as<uint32_t>();
+        A->vt_cnt = db->vt_cnt.as<uint32_t>();
         A->n_vt = (uint32_t)P.vt_cols.size();
     }
 }
@@ -1354,6 +1411,8 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         // value classes: classify every request of [lo, hi) per active column, then evaluate the
         // columns' rules once per class (class records -> errcount[2], the host expands them)
         if ((e = hipMemsetAsync(db->vt_keys.p, 0xFF, db->vt_keys_n * 8, s)) != hipSuccess) return hipfail(e, "vt reset");
+        if (A.hits && (e = hipMemsetAsync(db->vt_cnt.p, 0, db->vt_keys_n * 4, s)) != hipSuccess)
+            return hipfail(e, "vt count reset");
         A.q0 = lo;
         A.q1 = hi;
         if ((e = mxp_launch_vt_classify(&A, s)) != hipSuccess) return hipfail(e, "launch vt classify");
@@ -1429,14 +1488,14 @@ std::string mxp_engine::packed_value_text(const mxp_dbatch* db, uint32_t kind, u
     case MXP_TIMESTAMP: {
         TimeKey t{0, 0};
         if (v < gtimes.size()) t = gtimes[v];
-        else if (db && v - gtimes.size() < db->overlay_times.size()) t = db->overlay_times[v - gtimes.size()];
+        else if (db) db->overlay_time(v - gtimes.size(), &t);
         return mxp::go_format_time_utc(t.s, t.ns);
     }
     case MXP_BYTES: {
         const uint64_t raw = MXP_BYTES_RAW(v);
         std::string c;
         if (raw < gbytes.size()) c = gbytes[raw];
-        else if (db && raw - gbytes.size() < db->overlay_bytes.size()) c = std::string(db->overlay_bytes[raw - gbytes.size()]);
+        else if (db) db->overlay_bytes_at(raw - gbytes.size(), &c);
         return mxp::go_format_bytes((const uint8_t*)c.data(), c.size());
     }
     case MXP_STRING_MAP: {
@@ -1547,6 +1606,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_FILL_SPAN")) e->fill_span = (uint32_t)std::min(8, std::max(1, atoi(f)));
     if (const char* f = getenv("MXP_ERRCAP")) e->errcap = (uint32_t)std::max(1, atoi(f));
     if (getenv("MXP_WAVE_TIMES")) e->wave_times = true;
+    if (const char* f = getenv("MXP_HOST_PACK")) e->host_pack = atoi(f) != 0;  // A/B: the host packer
     if (device < 0) {  // host-only engine (compiler / lowering inspection without a GPU)
         e->reset_tables();
         *out = e;
@@ -1566,6 +1626,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
 void mxp_engine_destroy(mxp_engine* eng) {
     if (!eng) return;
     if (eng->device >= 0) (void)hipSetDevice(eng->device);
+    if (eng->pk_host) (void)hipHostFree(eng->pk_host);
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     for (auto& x : eng->ev)
         if (x) (void)hipEventDestroy(x);
@@ -1766,8 +1827,10 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
         eng->stats_tp = eng->stats_n ? (double)*eng->h_stats / eng->stats_n : 0.0;
         eng->stats_pending = false;
     }
-    // (value classes set many true pairs outside the index kernel's count: stream the counters)
-    const bool fused = eng->stats_tp * 125.0 <= (double)W && !db->vt_mask;
+    // (value-class rules are counted per class -- class size x class word, mxp_vt_eval_kernel --
+    // so the index kernel's true pairs alone price the fused counters)
+    const bool fused = (eng->stats_tp * 125.0 <= (double)W && !(eng->debug_flags & 1048576u)) ||
+                       (eng->debug_flags & 524288u);
     // the reset follows the previous download even when the caller switched streams
     if (eng->stats_pending && (e = hipStreamWaitEvent(s, eng->stats_ev, 0)) != hipSuccess)
         return eng->hipfail(e, "stats wait");
@@ -2065,16 +2128,14 @@ int mxp_value_text(mxp_engine* eng, uint32_t rule, uint64_t v, char* buf, uint32
         std::string c;
         uint64_t raw = MXP_BYTES_RAW(id);
         if (raw < eng->gbytes.size()) c = eng->gbytes[raw];
-        else if (eng->last_db && raw - eng->gbytes.size() < eng->last_db->overlay_bytes.size())
-            c = std::string(eng->last_db->overlay_bytes[raw - eng->gbytes.size()]);
+        else if (eng->last_db) eng->last_db->overlay_bytes_at(raw - eng->gbytes.size(), &c);
         s = mxp::go_format_bytes((const uint8_t*)c.data(), c.size());
         break;
     }
     case MXP_TIMESTAMP: {
         TimeKey t{0, 0};
         if (id < eng->gtimes.size()) t = eng->gtimes[id];
-        else if (eng->last_db && id - eng->gtimes.size() < eng->last_db->overlay_times.size())
-            t = eng->last_db->overlay_times[id - eng->gtimes.size()];
+        else if (eng->last_db) eng->last_db->overlay_time(id - eng->gtimes.size(), &t);
         s = mxp::go_format_time_utc(t.s, t.ns);
         break;
     }

@@ -120,7 +120,7 @@ struct mxp_dbatch {
     uint32_t vt_mask = 0;
     std::vector<uint32_t> vt_capc;         // per candidate slot (0: inactive)
     std::vector<uint32_t> vt_meta_h;       // kargs.vt_meta of the batch's plan (first launch)
-    DevBuf vt_cls, vt_keys, vt_rep, vt_t, vt_meta;
+    DevBuf vt_cls, vt_keys, vt_rep, vt_cnt, vt_t, vt_meta;
     size_t vt_t_words = 0, vt_keys_n = 0;
     DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
     DevBuf rxof, rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // run-time regexp patterns
@@ -128,6 +128,16 @@ struct mxp_dbatch {
     StrPool overlay;                                  // batch strings not in the rule set's pool
     StrPool overlay_bytes;                            // batch byte strings not in the rule set's
     std::vector<TimeKey> overlay_times;
+    // device-packed batches (pack_device.cpp): batch-local ids name batch items -- strings G + s,
+    // byte strings GB + item, canonical GC + item, times GT + item (items: batch strings / times
+    // first, then parsed ip() / timestamp() values by string id) -- read back on demand
+    bool dev_packed = false;
+    uint32_t ns = 0, nt = 0, G = 0, GB = 0, GC = 0, GT = 0;
+    DevBuf pip, pip_ok, pts_sec, pts_nsec, pts_ok, btsec, btnsec;
+    size_t overlay_strings() const { return dev_packed ? ns : overlay.size(); }
+    bool overlay_string(uint64_t j, std::string* out) const;       // batch-local string j (id - G)
+    bool overlay_bytes_at(uint64_t j, std::string* out) const;     // batch-local raw bytes j (id - GB)
+    bool overlay_time(uint64_t j, TimeKey* out) const;             // batch-local time j (id - GT)
 };
 
 struct mxp_engine : public mxp::LowerTables {
@@ -408,7 +418,29 @@ struct mxp_engine : public mxp::LowerTables {
     size_t views_n[3] = {~(size_t)0, 0, 0};
     void build_views();
     int pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H);
-    int pack(const mxp_bag_batch* b, mxp_dbatch* db);
+    // mxp_batch_upload: the device packer (pack_device.cpp), or the host one (MXP_HOST_PACK=1, and
+    // rule sets reading more than MXP_PACK_MAXCOL columns)
+    int pack(const mxp_bag_batch* b, mxp_dbatch* db) { return host_pack ? pack_on_host(b, db) : pack_device(b, db); }
+    int pack_on_host(const mxp_bag_batch* b, mxp_dbatch* db);
+    int pack_device(const mxp_bag_batch* b, mxp_dbatch* db);
+    int pack_vt_tables(mxp_dbatch* db);  // the value-class tables of the active slots
+    bool host_pack = false;
+    // device copies of the interning pools (strings: d_gstr / d_gstr_off) and their hash tables:
+    // [0] strings [1] byte strings [2] canonical byte strings [3] timestamps
+    int ensure_dev_pools();
+    bool dp_built = false;
+    size_t dp_sizes[4] = {0, 0, 0, 0};
+    DevBuf dp_ht[4], dp_desc[2], dp_blob[2], dp_tsec, dp_tnsec;
+    uint32_t dp_mask[4] = {0, 0, 0, 0};
+    // device packer scratch, reused across uploads
+    DevBuf pk_soff, pk_sbytes, pk_tsec, pk_tnsec, pk_moff, pk_mkey, pk_mval, pk_ck[64], pk_cv[64];
+    DevBuf pk_sid, pk_braw, pk_bcan, pk_tid, pk_use, pk_maxlen, pk_tab[4], pk_scan, pk_scan_blocks;
+    DevBuf pk_vt_bits, pk_vt_cnt, pk_rx, pk_rxv;
+    void* pk_host = nullptr;  // pinned read-back (longest string, value-class counts)
+    uint32_t vcol_key_id(uint32_t j) const {
+        auto it = gstr_ids.find(vcols[j].second);
+        return it == gstr_ids.end() ? 0xFFFFFFFEu : it->second;
+    }
     int wire_decode(const mxp_wire_batch* w, const char* const* names, uint32_t n_names, mxp_wire** out);  // wire.cpp
     void fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) const;
     int vt_prepare(mxp_dbatch* db, const Plan& P);
@@ -453,7 +485,8 @@ struct mxp_engine : public mxp::LowerTables {
         if (!db) db = last_db.get();
         if (sid < gstrs.size()) return gstrs[sid];
         uint64_t j = sid - gstrs.size();
-        return (db && j < db->overlay.size()) ? std::string(db->overlay[j]) : std::string("?");
+        std::string out;
+        return (db && db->overlay_string(j, &out)) ? out : std::string("?");
     }
 };
 

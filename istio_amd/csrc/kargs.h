@@ -90,7 +90,7 @@ typedef struct mxp_kargs {
     const uint32_t* vt_words;    // (group, rule mask) pairs of every slot's words
     uint16_t* vt_cls;            // [n_vt][n] class of each request
     uint32_t* vt_tm;             // class words, (match, error) u32 pairs: slot a, word j, class k at pair tbase + j * cap + k
-    uint32_t* vt_te;             // (unused)
+    uint32_t* vt_cnt;            // requests of each class (mxp_vt_classify_kernel): value-class hit counters
     unsigned long long* vt_keys; // class tables: keys (MXP_VT_EMPTY = free) and a representative request
     uint32_t* vt_rep;
     uint32_t n_vt;

@@ -660,6 +660,7 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
                     }
                 }
             }
+            const uint32_t m_own = m;  // (value-class bits are counted per class, mxp_vt_eval_kernel)
             if (kVM && A.gvt_off) {  // value-class rules of the group (after the guard errors were logged)
                 uint32_t vm, ve;
                 vt_words_of(A, g, req, valid, vm, ve);
@@ -674,9 +675,10 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
             }
             if (A.hits) {
                 // fused hit counters: per rule of the group, the lanes whose match bit is set
-                for (uint32_t bits = wave_or(m); bits; bits &= bits - 1) {
+                const uint32_t mc = valid ? m_own : 0u;
+                for (uint32_t bits = wave_or(mc); bits; bits &= bits - 1) {
                     const uint32_t k = __builtin_ctz(bits);
-                    const uint32_t c = (uint32_t)__builtin_popcountll(__ballot((m >> k) & 1u));
+                    const uint32_t c = (uint32_t)__builtin_popcountll(__ballot((mc >> k) & 1u));
                     if (lane == 0) atomicAdd(A.hits + r0 + k, (unsigned long long)c);
                 }
             }
@@ -947,13 +949,18 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
     __shared__ unsigned long long lkey[MXP_VTC_LCAP];
     __shared__ uint32_t lcls[MXP_VTC_LCAP];
     __shared__ uint32_t lrep[MXP_VTC_LCAP];
+    __shared__ uint32_t lcnt[MXP_VTC_LCAP];  // requests per local slot (class sizes, with A.hits)
+    const bool count = A.hits != nullptr;
     const uint32_t tid = threadIdx.x;
     const uint64_t N = A.n;
     const uint32_t base = A.q0 + blockIdx.x * MXP_VTC_REQ;
     for (uint32_t a = 0; a < A.n_vt; a++) {
         const uint32_t col = uni(A.vt_meta[a * 8u + MXP_VTM_COL]), cap = uni(A.vt_meta[a * 8u + MXP_VTM_CAP]),
                        kb = uni(A.vt_meta[a * 8u + MXP_VTM_KBASE]);
-        for (uint32_t i = tid; i < MXP_VTC_LCAP; i += 256u) lkey[i] = MXP_VT_EMPTY;
+        for (uint32_t i = tid; i < MXP_VTC_LCAP; i += 256u) {
+            lkey[i] = MXP_VT_EMPTY;
+            lcnt[i] = 0;
+        }
         __syncthreads();
         // 1. local slots of this thread's requests (req = base + tid + 256 r)
         uint32_t loc[MXP_VTC_REQ / 256u];
@@ -978,6 +985,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
                 h = (h + 1u) & (MXP_VTC_LCAP - 1u);
             }
             loc[r] = h;
+            if (count) atomicAdd(&lcnt[h], 1u);
         }
         __syncthreads();
         // 2. each distinct key of the workgroup against the global table (room for twice the
@@ -997,6 +1005,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
                 h = (h + 1u) & (cap - 1u);
             }
             lcls[i] = h;
+            if (count) atomicAdd(A.vt_cnt + kb + h, lcnt[i]);
         }
         __syncthreads();
         // 3. classes out
@@ -1043,6 +1052,18 @@ __device__ __forceinline__ void vt_eval_body(const mxp_kargs& A, uint64_t (*regs
         }
     }
     *(uint2*)(A.vt_tm + 2u * ((uint64_t)tb + (uint64_t)j * cap + k)) = make_uint2(m, e);
+    if (A.hits) {
+        // fused hit counters of the value-class rules: per rule, the sizes of the classes whose
+        // word holds its match bit (the merge kernels count none of these bits)
+        const uint32_t c = live ? A.vt_cnt[kb + k] : 0u;
+        for (uint32_t bits = wave_or(live ? m : 0u); bits; bits &= bits - 1u) {
+            const uint32_t bb = __builtin_ctz(bits);
+            uint32_t sum = (m >> bb) & 1u ? c : 0u;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) sum += (uint32_t)__shfl_xor((int)sum, off, 64);
+            if (lane == 0 && sum) atomicAdd(A.hits + g * 32u + bb, (unsigned long long)sum);
+        }
+    }
 }
 
 extern "C" __global__ __launch_bounds__(256) void mxp_vt_eval_kernel(mxp_kargs A) {
@@ -1140,18 +1161,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A)
             for (int r = 0; r < 4; r++) c += (uint32_t)__builtin_popcount(ve[r] & vmask[r]);
             vt_count_n(A, c);
         }
-        if (A.hits) {
-            uint32_t u = 0;
-#pragma unroll
-            for (int r = 0; r < 4; r++) u |= m[r] & vmask[r];
-            for (uint32_t bits = wave_or(u); bits; bits &= bits - 1u) {
-                const uint32_t k = __builtin_ctz(bits);
-                uint32_t cnt = 0;
-#pragma unroll
-                for (int r = 0; r < 4; r++) cnt += (uint32_t)__builtin_popcountll(__ballot(((m[r] & vmask[r]) >> k) & 1u));
-                if (lane == 0) atomicAdd(A.hits + G * 32u + k, (unsigned long long)cnt);
-            }
-        }
+        // (no hit counting: a uniform group's words hold no true bit but the value classes', which
+        // mxp_vt_eval_kernel counts per class)
         if (A.req_err)
             for (uint32_t r = 0; r < 4; r++)
                 if (e[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;

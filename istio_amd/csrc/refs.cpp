@@ -344,7 +344,7 @@ int mxp_eval_refs(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* match_b
 
 int mxp_string_text(mxp_engine* eng, uint32_t sid, char* buf, uint32_t cap) {
     if (!eng) return MXP_ERR_ARG;
-    if (sid >= eng->gstrs.size() + (eng->last_db ? eng->last_db->overlay.size() : 0)) return MXP_ERR_ARG;
+    if (sid >= eng->gstrs.size() + (eng->last_db ? eng->last_db->overlay_strings() : 0)) return MXP_ERR_ARG;
     return put_text(eng->string_of(nullptr, sid), buf, cap);
 }
 

@@ -288,12 +288,15 @@ def test_fill_layout_knobs_parity(mxp, knobs, n, monkeypatch):
 
 
 @pytest.mark.parametrize("family", ["c2", "fuzz", "c4"])
-def test_fused_hit_counters(mxp, family):
+@pytest.mark.parametrize("flags", ["0", "524288", "786432"])  # auto; fused forced; fused + value classes forced
+def test_fused_hit_counters(mxp, family, flags, monkeypatch):
     """mxp_batch_eval_device_hits: counters accumulated by the evaluation kernels (fill / guard / VM
     kernels by ballot, index kernel per newly set bit) -- or, after an evaluation dense in true pairs
-    (C4), by the streaming hits kernel -- equal the true pairs of the bitmaps over three evaluations,
-    and the bitmaps equal the plain device evaluation's."""
+    (C4), by the streaming hits kernel; value-class rules per class (class size x class word) -- equal
+    the true pairs of the bitmaps over three evaluations, and the bitmaps equal the plain device
+    evaluation's."""
     import torch
+    monkeypatch.setenv("MXP_DEBUG_FLAGS", flags)
     if family == "c2":
         manifest, rules, batch = W.c2_workload(n_rules=700, n_requests=30000)
     elif family == "c4":

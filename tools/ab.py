@@ -21,6 +21,15 @@ Wd = (len(rules) + 31) // 32
 dm = torch.empty((Wd, batch.n), dtype=torch.int32, device="cuda:0")
 de = torch.empty_like(dm)
 hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
+flags = torch.empty(batch.n, dtype=torch.uint8, device="cuda:0")
+compact = bool(os.environ.get("AB_COMPACT"))  # the bench's error output (per-request flags)
+
+
+def ev(db, s):
+    if compact:
+        db.eval_compact(dm.data_ptr(), flags.data_ptr(), hits.data_ptr(), s.cuda_stream)
+    else:
+        db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s.cuda_stream)
 s = torch.cuda.Stream()
 torch.cuda.set_stream(s)
 res = {x: [] for x in settings}
@@ -38,12 +47,12 @@ for rep in range(3):
         eng.compile(rules)
         db = eng.upload(batch)
         for _ in range(3):
-            db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s.cuda_stream)
+            ev(db, s)
         ts = []
         for _ in range(15):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
-            db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s.cuda_stream)
+            ev(db, s)
             b.record(s)
             torch.cuda.synchronize()
             ts.append(a.elapsed_time(b))
