@@ -59,6 +59,7 @@ def parse():
                    help="c2 (default, the BASELINE metric; + a C4 block); c4 route rules; c5 = C2 predicates + "
                         "memquota with one combined all-reduce; C3 lists; c5-quota memquota alone")
     p.add_argument("--list-entries", type=int, default=100_000)
+    p.add_argument("--e2e-reps", type=int, default=3, help="end-to-end resolve calls timed (median)")
     p.add_argument("--error-output", default="compact", choices=["compact", "bitmap"],
                    help="compact: per-request error flags (a Resolve's view); bitmap: the full error bitmap")
     return p.parse_args()
@@ -321,6 +322,32 @@ def list_cpu_baseline(L, kind, entries, syms, seconds, threads):
             "sample": "%d lookups (%.1fs) against all %d entries, oracle restatement" % (done, dt, len(entries))}
 
 
+def end_to_end(eng, batch, n_rules, reps):
+    """The whole Check-path call from Go-owned bags to action lists: the host
+    columnar batch -> mxp_resolve_batch (device packing and interning, evaluation of every pair,
+    per-request resolution and action-list gather on the device) -> status / first-error rule /
+    selected rules back in host memory.  Every rule sits in the default namespace with one variety,
+    so each request's action list is every rule whose predicate holds (resolver.go:202-238).
+    PCIe-inclusive; not `value` (whose inputs are resident in HBM)."""
+    import numpy as np
+    eng.set_resolver("destination.service", "istio-system", ["istio-system"] * n_rules,
+                     np.ones(n_rules, dtype=np.uint32), np.zeros(n_rules, dtype=np.uint8),
+                     np.zeros(n_rules, dtype=np.uint8))
+    status, _, off, _ = eng.resolve_arrays(batch, 0)  # warm-up (allocations, first-touch of pinned pages)
+    cap = max(16, int(off[-1]))
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        status, _, off, _ = eng.resolve_arrays(batch, 0, cap)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"pairs_per_s": batch.n * n_rules / t, "requests_per_s": batch.n / t, "ms_per_batch": t * 1e3,
+            "reps": reps, "selected_per_request": float(off[-1]) / max(batch.n, 1),
+            "pred_error_requests": int((status == 3).sum()),
+            "path": "host columnar bags -> mxp_resolve_batch (device pack + evaluation + action-list gather) -> "
+                    "host action lists; median of reps, PCIe-inclusive"}
+
+
 def predicate_bench(args, kind, rank, world, local, with_quota=False):
     """One predicate workload (c2 / c4) on this rank's 1M-request shard; returns the result dict.
 
@@ -451,6 +478,7 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
                         "collective": "one all_reduce(sum) of hits[R] ++ quota_delta[K] per step"}
     hits = ctr.totals()[0]
     out["hits_total"] = int(hits.sum().item())
+    out["end_to_end"] = end_to_end(eng, batch, R, args.e2e_reps)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         if kind == "c4":
             sample = W.c4_workload(n_rules=args.rules, n_requests=1 << 14, seed=4)[2]
@@ -490,7 +518,7 @@ def main():
         # the representative config BASELINE.json quotes at 10k rules (configs[3]), driver-timed too
         c4 = predicate_bench(args, "c4", rank, world, local)
         out["c4"] = {k: c4[k] for k in ("metric", "value", "unit", "ms_per_step", "eval_ms", "kernels_ms",
-                                        "pack_upload_s", "config", "roofline", "lds_bank_conflicts")}
+                                        "pack_upload_s", "end_to_end", "config", "roofline", "lds_bank_conflicts")}
         if "cpu_baseline" in c4:
             out["c4"]["cpu_baseline"] = c4["cpu_baseline"]
     if rank == 0:

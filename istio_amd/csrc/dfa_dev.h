@@ -166,12 +166,19 @@ __device__ __forceinline__ bool mxp_nfa_run(const mxp_dfa_set& S, const mxp_dfa_
 }
 
 // regexp.MatchString on one subject: decode runes the way Go's inputString does (utf8 rules; an
-// invalid byte is U+FFFD of width 1), map each to its class, step; END column at the end.
+// invalid byte is U+FFFD of width 1), map each to its class, step; END column at the end.  A step
+// into ACCEPT decides true, a step into REJECT (a state from which no match is reachable, folded at
+// build time: regex.cpp fold_dead_states) decides false.
+//
+// kLds: the first K states' transition rows (TL, K * ncls words) and the ASCII class map (AL) are
+// staged in LDS by the caller; states >= K step from global memory.  Subset construction numbers
+// states in BFS order from the start, so the staged rows are the shallow, hot part of the DFA.
 // (DFA headers only: callers that may meet an NFA header use mxp_rx_run)
-__device__ __forceinline__ bool mxp_dfa_run(const mxp_dfa_set& S, uint32_t dfa, const uint8_t* s, uint32_t n) {
-    const mxp_dfa_hdr H = S.hdr[dfa];
+template <bool kLds>
+__device__ __forceinline__ bool mxp_dfa_walk(const mxp_dfa_set& S, const mxp_dfa_hdr& H, const uint32_t* TL,
+                                             const uint16_t* AL, uint32_t K, const uint8_t* s, uint32_t n) {
     const uint32_t* T = S.trans + H.trans;
-    const uint16_t* asc = S.ascii + H.ascii;
+    const uint16_t* asc = kLds ? AL : S.ascii + H.ascii;
     uint32_t st = H.start;
     uint32_t i = H.skip;
     if (i == MXP_DFA_DECIDED) return true;
@@ -228,10 +235,23 @@ __device__ __forceinline__ bool mxp_dfa_run(const mxp_dfa_set& S, uint32_t dfa, 
             }
             cls = S.hicls[H.hi + k];
         }
-        st = T[(uint64_t)st * H.ncls + cls];
-        if (st == 0xFFFFFFFFu) return true;
+        const uint64_t at = (uint64_t)st * H.ncls + cls;
+        if constexpr (kLds)
+            st = st < K ? TL[(uint32_t)at] : T[at];
+        else
+            st = T[at];
+        if (st >= 0xFFFFFFFEu) return st == 0xFFFFFFFFu;
     }
-    return T[(uint64_t)st * H.ncls + H.ncls - 1] == 0xFFFFFFFFu;
+    const uint64_t at = (uint64_t)st * H.ncls + H.ncls - 1;
+    if constexpr (kLds)
+        return (st < K ? TL[(uint32_t)at] : T[at]) == 0xFFFFFFFFu;
+    else
+        return T[at] == 0xFFFFFFFFu;
+}
+
+__device__ __forceinline__ bool mxp_dfa_run(const mxp_dfa_set& S, uint32_t dfa, const uint8_t* s, uint32_t n) {
+    const mxp_dfa_hdr H = S.hdr[dfa];
+    return mxp_dfa_walk<false>(S, H, nullptr, nullptr, 0u, s, n);
 }
 
 // a DFA or an NFA header

@@ -170,7 +170,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         const mxp::Dfa& d = rx_dfas[rp.dfa];
         if (d.is_nfa()) continue;  // the NFA walks the whole subject
         uint32_t st = d.start;
-        for (size_t b = 0; b < rp.prefix.size() && st != mxp::kDfaAccept;) {
+        for (size_t b = 0; b < rp.prefix.size() && st < mxp::kDfaReject;) {
             const uint8_t c = (uint8_t)rp.prefix[b];
             uint32_t cls, w = 1;
             if (c < 0x80) {

@@ -31,6 +31,8 @@ struct mxp_list {
     DevBuf htab, ent_desc, ent_pool, v4lo, v4hi, v6lo, v6hi;
     DevBuf rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // REGEX: the parts' automata
     uint32_t n4 = 0, n6 = 0, rx_n = 0, rx_nfa = 0;
+    uint32_t lds_nparts = 0;
+    DevBuf lds_plan;  // REGEX: [K per staged part][LDS word base per staged part] (lists.h)
 };
 
 namespace {
@@ -138,6 +140,11 @@ void merge(std::vector<std::pair<T, T>>& v) {
             o.push_back(p);
     }
     v.swap(o);
+}
+
+void set_lds(mxp_list_args& A, const mxp_list* L) {
+    A.lds_nparts = L->lds_nparts;
+    A.lds_plan = L->lds_plan.as<uint32_t>();
 }
 
 }  // namespace
@@ -267,6 +274,7 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             alone[i] = prc != mxp::RX_OK;
         }
         mxp::DfaSetHost set;
+        std::vector<uint32_t> part_states;  // DFA states per part (0: an NFA part)
         std::function<int(size_t, size_t)> part = [&](size_t lo, size_t hi) -> int {
             if (lo >= hi) return MXP_OK;
             const std::vector<std::string> ps(pats.begin() + lo, pats.begin() + hi);
@@ -276,6 +284,7 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             const int prc = mxp::regex_compile(ps, one ? kPatternStates : kListRegexStates, &d, &e, nullptr, one);
             if (prc == mxp::RX_OK) {
                 set.add(d);
+                part_states.push_back(d.is_nfa() ? 0u : d.nstates);
                 return MXP_OK;
             }
             if (one) return eng->fail(MXP_ERR_ARG, "regex list: pattern " + pats[lo] + ": " + e);
@@ -300,6 +309,22 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             std::string e;
             mxp::regex_compile({}, 16, &d, &e);
             set.add(d);
+            part_states.push_back(d.nstates);
+        }
+        // LDS staging (mxp_list_rx_kernel): the leading parts' first states (BFS order: the levels
+        // every lookup steps through) within MXP_LDS_DFA_WORDS; MXP_LIST_LDS=0 turns it off (A/B)
+        const char* lds_env = getenv("MXP_LIST_LDS");
+        if (!lds_env || atoi(lds_env) != 0) {
+            uint32_t plan[2 * MXP_LDS_DFA_PARTS] = {}, used = 0;
+            for (size_t k = 0; k < set.hdr.size() && k < MXP_LDS_DFA_PARTS; k++) {
+                const uint32_t ncls = set.hdr[k].ncls;
+                const uint32_t K = std::min(part_states[k], (MXP_LDS_DFA_WORDS - used) / ncls);
+                plan[k] = K;
+                plan[MXP_LDS_DFA_PARTS + k] = used;
+                used += K * ncls;
+                L->lds_nparts = (uint32_t)k + 1;
+            }
+            if ((rc = put(L->lds_plan, plan, sizeof plan, "upload lds plan"))) return rc;
         }
         L->rx_n = (uint32_t)set.hdr.size();
         for (const auto& h : set.hdr) L->rx_nfa += h.kind == MXP_RX_NFA ? 1u : 0u;
@@ -353,6 +378,7 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, con
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes;
+    set_lds(A, L);
     hipError_t e = mxp_launch_list(&A, stream ? (hipStream_t)stream : eng->stream);
     return e == hipSuccess ? MXP_OK : eng->hipfail(e, "launch list check");
 }
@@ -399,6 +425,7 @@ int mxp_listentry_check(mxp_engine* eng, const mxp_list* L, int blacklist, const
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes.as<int32_t>();
+    set_lds(A, L);
     A.vals = dv.as<uint64_t>() + value_rule;
     A.vstride = NR;
     A.viface = iface ? 1u : 0u;

@@ -10,6 +10,12 @@
 // string hash table slot: hash32 << 32 | entry index; empty slot = ~0
 #define MXP_LIST_EMPTY 0xFFFFFFFFFFFFFFFFull
 
+// LDS staging of regex-list DFAs: transition words per workgroup (60 KB of the 160 KB of a CU, so
+// two 1024-thread workgroups share a CU) and parts staged at most
+#define MXP_LDS_DFA_WORDS 15360u
+#define MXP_LDS_DFA_PARTS 8u
+#define MXP_LIST_RX_THREADS 1024u
+
 typedef struct mxp_list_args {
     uint32_t type;              // MXP_LIST_*
     uint32_t blacklist;
@@ -41,6 +47,12 @@ typedef struct mxp_list_args {
     const uint8_t* gstr;
     const uint64_t* bstr_off;
     const uint8_t* bstr;
+    // REGEX lists, LDS staging (mxp_list_rx_kernel): parts k < lds_nparts have their first
+    // lds_plan[k] transition rows copied to LDS word lds_plan[MXP_LDS_DFA_PARTS + k] (0 rows: the
+    // part walks from global memory), plus their ASCII class maps.  (A device table, not a kernarg
+    // array: a dynamically indexed by-value argument would be copied to scratch.)
+    uint32_t lds_nparts;
+    const uint32_t* lds_plan;
 } mxp_list_args;
 
 #define MXP_LISTENTRY_NOT_STRING (-2)

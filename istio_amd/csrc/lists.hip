@@ -92,6 +92,40 @@ __device__ bool ip_member(const mxp_list_args& A, const uint8_t ip[16]) {
     return r >= 0 && le128(xh, xl, A.v6hi[2 * r], A.v6hi[2 * r + 1]);
 }
 
+// The symbol of lookup q: a blob entry, or (fused listentry) the Eval result of one rule.  Returns
+// false with codes[q] written when the lookup is settled before the membership test.
+__device__ __forceinline__ bool list_symbol(const mxp_list_args& A, uint32_t q, const uint8_t** sp, uint32_t* np) {
+    if (A.vals) {
+        // listentry ProcessCheck (template.gen.go:2170-2183): Value = mapper.Eval(param.Value).(string)
+        if (A.err_word[q] & A.err_bit) {
+            A.codes[q] = MXP_LISTENTRY_EVAL_ERROR;
+            return false;
+        }
+        uint64_t id = A.vals[(uint64_t)q * A.vstride];
+        if (A.viface) {
+            if (MXP_FH_KIND(id) != MXP_STRING) {
+                A.codes[q] = MXP_LISTENTRY_NOT_STRING;
+                return false;
+            }
+            id = MXP_FH_ID(id);
+        }
+        const bool g = id < A.n_gstr;
+        const uint64_t d = g ? A.gstr_off[id] : A.bstr_off[id - A.n_gstr];
+        *sp = (g ? A.gstr : A.bstr) + (d >> 24);
+        *np = (uint32_t)(d & 0xFFFFFFu);
+    } else {
+        const uint64_t o0 = A.sym_off[q], o1 = A.sym_off[q + 1];
+        *sp = A.sym + o0;
+        *np = (uint32_t)(o1 - o0);
+    }
+    return true;
+}
+
+__device__ __forceinline__ void list_decide(const mxp_list_args& A, uint32_t q, bool found) {
+    A.codes[q] = A.blacklist ? (found ? MXP_RPC_PERMISSION_DENIED : MXP_RPC_OK)
+                             : (found ? MXP_RPC_OK : MXP_RPC_NOT_FOUND);
+}
+
 }  // namespace
 
 extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args A) {
@@ -99,29 +133,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args 
     if (q >= A.n) return;
     const uint8_t* s;
     uint32_t n;
-    if (A.vals) {
-        // listentry ProcessCheck (template.gen.go:2170-2183): Value = mapper.Eval(param.Value).(string)
-        if (A.err_word[q] & A.err_bit) {
-            A.codes[q] = MXP_LISTENTRY_EVAL_ERROR;
-            return;
-        }
-        uint64_t id = A.vals[(uint64_t)q * A.vstride];
-        if (A.viface) {
-            if (MXP_FH_KIND(id) != MXP_STRING) {
-                A.codes[q] = MXP_LISTENTRY_NOT_STRING;
-                return;
-            }
-            id = MXP_FH_ID(id);
-        }
-        const bool g = id < A.n_gstr;
-        const uint64_t d = g ? A.gstr_off[id] : A.bstr_off[id - A.n_gstr];
-        s = (g ? A.gstr : A.bstr) + (d >> 24);
-        n = (uint32_t)(d & 0xFFFFFFu);
-    } else {
-        const uint64_t o0 = A.sym_off[q], o1 = A.sym_off[q + 1];
-        s = A.sym + o0;
-        n = (uint32_t)(o1 - o0);
-    }
+    if (!list_symbol(A, q, &s, &n)) return;
     bool found;
     if (A.type == MXP_LIST_IP_ADDRESSES) {
         uint8_t ip[16];
@@ -136,11 +148,52 @@ extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args 
     } else {
         found = string_member(A, s, n, A.type == MXP_LIST_CASE_INSENSITIVE_STRINGS);
     }
-    A.codes[q] = A.blacklist ? (found ? MXP_RPC_PERMISSION_DENIED : MXP_RPC_OK)
-                             : (found ? MXP_RPC_OK : MXP_RPC_NOT_FOUND);
+    list_decide(A, q, found);
+}
+
+// REGEX lists with LDS-staged automata: each 1024-thread workgroup copies the hot rows of the parts'
+// DFAs (the first lds_states[k] states in BFS order from the start: the shallow levels every lookup
+// steps through) and their ASCII class maps into LDS once, then strides over the lookups; a lane
+// steps from LDS while its state is staged and from global memory below that.  Two workgroups fill
+// a CU's 32 wave slots while sharing one staged copy per 16 waves.
+extern "C" __global__ __launch_bounds__(1024) void mxp_list_rx_kernel(mxp_list_args A) {
+    __shared__ uint32_t TL[MXP_LDS_DFA_WORDS];
+    __shared__ uint16_t AL[MXP_LDS_DFA_PARTS * 128u];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t k = 0; k < A.lds_nparts; k++) {
+        const mxp_dfa_hdr H = A.rx.hdr[k];
+        const uint32_t words = A.lds_plan[k] * H.ncls, base = A.lds_plan[MXP_LDS_DFA_PARTS + k];
+        const uint32_t* src = A.rx.trans + H.trans;
+        for (uint32_t i = tid; i < words; i += MXP_LIST_RX_THREADS) TL[base + i] = src[i];
+        if (tid < 128u) AL[k * 128u + tid] = A.rx.ascii[H.ascii + tid];
+    }
+    __syncthreads();
+    for (uint32_t q = blockIdx.x * MXP_LIST_RX_THREADS + tid; q < A.n; q += gridDim.x * MXP_LIST_RX_THREADS) {
+        const uint8_t* s;
+        uint32_t n;
+        if (!list_symbol(A, q, &s, &n)) continue;
+        bool found = false;  // regexList.checkList: any pattern matches (any part's automaton)
+        for (uint32_t k = 0; k < A.rx_n && !found; k++) {
+            const uint32_t K = k < A.lds_nparts ? A.lds_plan[k] : 0u;
+            if (K) {
+                const mxp_dfa_hdr H = A.rx.hdr[k];
+                found = mxp_dfa_walk<true>(A.rx, H, TL + A.lds_plan[MXP_LDS_DFA_PARTS + k], AL + k * 128u, K, s, n);
+            } else {
+                found = mxp_rx_run(A.rx, k, s, n);
+            }
+        }
+        list_decide(A, q, found);
+    }
 }
 
 extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s) {
+    if (a->type == MXP_LIST_REGEX && a->lds_nparts) {
+        // enough workgroups for 2 per CU (256 CUs), fewer for small batches
+        const uint32_t need = (a->n + MXP_LIST_RX_THREADS - 1u) / MXP_LIST_RX_THREADS;
+        const uint32_t grid = need < 512u ? need : 512u;
+        hipLaunchKernelGGL(mxp_list_rx_kernel, dim3(grid), dim3(MXP_LIST_RX_THREADS), 0, s, *a);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(mxp_list_kernel, dim3((a->n + 255u) / 256u), dim3(256), 0, s, *a);
     return hipGetLastError();
 }

@@ -1029,6 +1029,7 @@ int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states,
         }
     }
     d.nstates = (uint32_t)states.size();
+    fold_dead_states(&d);
     *out = std::move(d);
     return RX_OK;
 }
@@ -1102,6 +1103,30 @@ bool nfa_match_host(const Dfa& d, const std::string& s) {
 }
 }  // namespace
 
+// Transitions into states from which ACCEPT is unreachable become kDfaReject, so walkers stop at
+// the first byte that rules out every pattern (an anchored list's near misses) instead of reading
+// the rest of the subject.  Liveness is a fixpoint over the rows; states are in BFS order, so
+// descending sweeps settle in few passes.
+void fold_dead_states(Dfa* d) {
+    const uint32_t N = d->nstates, C = d->ncls;
+    std::vector<uint8_t> live(N, 0);
+    for (bool changed = true; changed;) {
+        changed = false;
+        for (uint32_t s = N; s-- > 0;) {
+            if (live[s]) continue;
+            const uint32_t* row = d->trans.data() + (size_t)s * C;
+            for (uint32_t c = 0; c < C; c++)
+                if (row[c] == kDfaAccept || (row[c] < N && live[row[c]])) {
+                    live[s] = 1;
+                    changed = true;
+                    break;
+                }
+        }
+    }
+    for (uint32_t& t : d->trans)
+        if (t < N && !live[t]) t = kDfaReject;
+}
+
 bool dfa_match_host(const Dfa& d, const std::string& s) {
     if (d.is_nfa()) return nfa_match_host(d, s);
     uint32_t st = d.start;
@@ -1119,6 +1144,7 @@ bool dfa_match_host(const Dfa& d, const std::string& s) {
         }
         st = d.trans[(size_t)st * d.ncls + c];
         if (st == kDfaAccept) return true;
+        if (st == kDfaReject) return false;
     }
     return d.trans[(size_t)st * d.ncls + d.ncls - 1] == kDfaAccept;
 }

@@ -364,16 +364,16 @@ class Engine:
         self._check(self.lib.mxp_resolver_set(self.h, identity_attr.encode(), default_ns.encode(), ns,
                                               vm.ctypes.data, tcp.ctypes.data, em.ctypes.data, n), "mxp_resolver_set")
 
-    def resolve(self, batch: BagBatch, variety: int):
-        """Resolve every request (mxp_resolve_batch) -> (status u8[n], err_rule u32[n], selected:
-        list of per-request rule-id arrays in resolution order)."""
+    def resolve_arrays(self, batch: BagBatch, variety: int, cap: int = 0):
+        """mxp_resolve_batch -> (status u8[n], err_rule u32[n], sel_off u64[n + 1], sel_rules u32[...]):
+        request q's selected rules are sel_rules[sel_off[q]:sel_off[q + 1]], in resolution order."""
         n = batch.n
-        status = np.zeros(n, dtype=np.uint8)
-        err_rule = np.zeros(n, dtype=np.uint32)
-        off = np.zeros(n + 1, dtype=np.uint64)
-        cap = max(16, n * 4)
+        status = np.empty(n, dtype=np.uint8)
+        err_rule = np.empty(n, dtype=np.uint32)
+        off = np.empty(n + 1, dtype=np.uint64)
+        cap = cap or max(16, n * 4)
         for _ in range(2):
-            sel = np.zeros(cap, dtype=np.uint32)
+            sel = np.empty(cap, dtype=np.uint32)
             rc = self.lib.mxp_resolve_batch(self.h, ctypes.byref(batch.c_struct()), variety, status.ctypes.data,
                                              err_rule.ctypes.data, off.ctypes.data, sel.ctypes.data, cap)
             if rc == 4:  # MXP_ERR_NOMEM: retry with the exact size
@@ -381,7 +381,13 @@ class Engine:
                 continue
             self._check(rc, "mxp_resolve_batch")
             break
-        return status, err_rule, [sel[int(off[q]):int(off[q + 1])] for q in range(n)]
+        return status, err_rule, off, sel[:int(off[n])]
+
+    def resolve(self, batch: BagBatch, variety: int):
+        """Resolve every request (mxp_resolve_batch) -> (status u8[n], err_rule u32[n], selected:
+        list of per-request rule-id arrays in resolution order)."""
+        status, err_rule, off, sel = self.resolve_arrays(batch, variety)
+        return status, err_rule, [sel[int(off[q]):int(off[q + 1])] for q in range(batch.n)]
 
     # ------------------------------------------------------------------ list adapter
     def list_create(self, entry_type: int, entries, overrides=()) -> "ListHandle":

@@ -73,6 +73,37 @@ def test_c3_regex_list_parity(eng):
     assert (want == 0).sum() > 300 and (want == 5).sum() > 300
 
 
+@pytest.mark.parametrize("case", ["small", "c3-10k", "nfa-parts", "multi-part"])
+def test_regex_list_lds_staging(monkeypatch, case):
+    """mxp_list_rx_kernel (the parts' hot DFA rows staged in LDS) against the global-memory walk
+    (MXP_LIST_LDS=0, mxp_list_kernel) and the oracle: a 200-pattern list, the 10k-pattern C3 union
+    staged in part (its DFA is far larger than the LDS budget), NFA parts between staged DFAs,
+    and several union parts; ragged lookup counts past one grid-stride round (512 x 1024 lanes)."""
+    import istio_amd.engine as mxp
+    rng = np.random.default_rng(71)
+    if case == "small":
+        pats, syms = W.c3_regex_list(n_patterns=200, n_lookups=20_011, seed=72)
+    elif case == "c3-10k":
+        pats, syms = W.c3_regex_list(n_patterns=10_000, n_lookups=600_037, seed=73)
+    elif case == "nfa-parts":
+        from test_regex_product import NFA_PATTERNS, _nfa_subjects
+        pats = ["^zz", NFA_PATTERNS[0], "x{3}", NFA_PATTERNS[2], "^é", "(?i)ab+c$"]
+        syms = _nfa_subjects(rng, 5003) + ["zzz", "éa", "xxx", "ABBC", "abc", ""]
+    else:
+        pats, syms = W.c3_regex_list(n_patterns=50_000, n_lookups=80_021, seed=74)
+    out = {}
+    for lds in ("1", "0"):
+        monkeypatch.setenv("MXP_LIST_LDS", lds)
+        eng = mxp.Engine(0)
+        lst = eng.list_create(L.REGEX, pats, [])
+        out[lds] = (lst.check(syms), lst.check(syms, True))
+    assert np.array_equal(out["1"][0], out["0"][0]) and np.array_equal(out["1"][1], out["0"][1])
+    sample = rng.choice(len(syms), min(len(syms), 800), replace=False)
+    want = L.codes(L.RegexList(pats).found([syms[i] for i in sample], threads=16), False)
+    assert np.array_equal(out["1"][0][sample], want)
+    assert (want == 0).sum() > 50 and (want == 5).sum() > 50
+
+
 def test_regex_list_compile_error(eng):
     from istio_amd.engine import MxpError
     with pytest.raises(MxpError) as ei:
