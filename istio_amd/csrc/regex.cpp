@@ -1103,28 +1103,41 @@ bool nfa_match_host(const Dfa& d, const std::string& s) {
 }
 }  // namespace
 
-// Transitions into states from which ACCEPT is unreachable become kDfaReject, so walkers stop at
-// the first byte that rules out every pattern (an anchored list's near misses) instead of reading
-// the rest of the subject.  Liveness is a fixpoint over the rows; states are in BFS order, so
-// descending sweeps settle in few passes.
+// Decided states fold into the two verdicts, so walkers stop at the first byte that settles the
+// match instead of reading the rest of the subject:
+//   REJECT  states from which ACCEPT is unreachable (an anchored list's near misses): the least
+//           fixpoint of "some transition reaches ACCEPT or a live state";
+//   ACCEPT  states from which every continuation accepts, the end of text included (a `(/.*)?$`
+//           tail after its '/'): the greatest fixpoint of "END accepts and every transition is
+//           ACCEPT or stays in the set".
+// Transitions into them become kDfaReject / kDfaAccept (the walk's outcome from such a state is
+// the verdict whatever follows).  States are in BFS order, so descending sweeps settle in few passes.
 void fold_dead_states(Dfa* d) {
     const uint32_t N = d->nstates, C = d->ncls;
-    std::vector<uint8_t> live(N, 0);
+    std::vector<uint8_t> live(N, 0), sure(N, 0);
+    for (uint32_t s = 0; s < N; s++) sure[s] = d->trans[(size_t)s * C + C - 1] == kDfaAccept;
     for (bool changed = true; changed;) {
         changed = false;
         for (uint32_t s = N; s-- > 0;) {
-            if (live[s]) continue;
             const uint32_t* row = d->trans.data() + (size_t)s * C;
-            for (uint32_t c = 0; c < C; c++)
-                if (row[c] == kDfaAccept || (row[c] < N && live[row[c]])) {
-                    live[s] = 1;
-                    changed = true;
-                    break;
-                }
+            if (!live[s])
+                for (uint32_t c = 0; c < C; c++)
+                    if (row[c] == kDfaAccept || (row[c] < N && live[row[c]])) {
+                        live[s] = 1;
+                        changed = true;
+                        break;
+                    }
+            if (sure[s])
+                for (uint32_t c = 0; c + 1 < C; c++)
+                    if (row[c] != kDfaAccept && !(row[c] < N && sure[row[c]])) {
+                        sure[s] = 0;
+                        changed = true;
+                        break;
+                    }
         }
     }
     for (uint32_t& t : d->trans)
-        if (t < N && !live[t]) t = kDfaReject;
+        if (t < N) t = sure[t] ? kDfaAccept : !live[t] ? kDfaReject : t;
 }
 
 bool dfa_match_host(const Dfa& d, const std::string& s) {

@@ -61,7 +61,8 @@ bool regex_required_prefix(const std::string& pattern, std::string* prefix);
 
 // Host stepping of a compiled DFA or NFA (constant folding, tests).
 bool dfa_match_host(const Dfa& d, const std::string& s);
-// transitions into states that cannot reach ACCEPT -> kDfaReject (run by the DFA builder)
+// transitions into decided states -> kDfaReject (ACCEPT unreachable) / kDfaAccept (every continuation
+// accepts); run by the DFA builder
 void fold_dead_states(Dfa* d);
 
 }  // namespace mxp

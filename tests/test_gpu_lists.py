@@ -101,7 +101,7 @@ def test_regex_list_lds_staging(monkeypatch, case):
     sample = rng.choice(len(syms), min(len(syms), 800), replace=False)
     want = L.codes(L.RegexList(pats).found([syms[i] for i in sample], threads=16), False)
     assert np.array_equal(out["1"][0][sample], want)
-    assert (want == 0).sum() > 50 and (want == 5).sum() > 50
+    assert (want == 0).sum() > 20 and (want == 5).sum() > 20
 
 
 def test_regex_list_compile_error(eng):
