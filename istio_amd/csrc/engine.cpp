@@ -1600,6 +1600,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (!e) return MXP_ERR_NOMEM;
     e->device = device;
     if (const char* f = getenv("MXP_DEBUG_FLAGS")) e->debug_flags = (uint32_t)atoi(f);
+    if (const char* f = getenv("MXP_TRACE")) e->trace = atoi(f) != 0;
     // tuning knobs (results are identical for every setting)
     if (const char* f = getenv("MXP_GPW")) e->groups_per_wave = std::max(1, atoi(f));
     if (const char* f = getenv("MXP_FILL_CHUNK")) e->fill_chunk = (uint32_t)std::max(1, atoi(f));
@@ -1879,15 +1880,20 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return hipfail(e, "hipSetDevice");
     db.reset(new mxp_dbatch());
+    trace_mark(nullptr);
     int rc = pack(batch, db.get());
     if (rc) return rc;
+    trace_mark("pack + upload");
     const uint32_t n = batch->n_requests;
     const uint32_t R = (uint32_t)rules.size();
     const uint32_t W = (R + 31) / 32;
-    if ((e = dm.alloc((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc match");
-    if ((e = de.alloc((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc err");
-    if (dv && (e = dv->alloc((size_t)n * R * 8)) != hipSuccess) return hipfail(e, "alloc values");
-    return launch(db.get(), stream, dm.as<uint32_t>(), de.as<uint32_t>(), dv ? dv->as<uint64_t>() : nullptr, true);
+    if ((e = dm.reserve((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc match");
+    if ((e = de.reserve((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc err");
+    if (dv && (e = dv->reserve((size_t)n * R * 8)) != hipSuccess) return hipfail(e, "alloc values");
+    trace_mark("bitmap allocation");
+    rc = launch(db.get(), stream, dm.as<uint32_t>(), de.as<uint32_t>(), dv ? dv->as<uint64_t>() : nullptr, true);
+    trace_mark("evaluation kernels");
+    return rc;
 }
 
 int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_dbatch>& db) {
@@ -1898,15 +1904,20 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
         return hipfail(e, "download errcount");
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "eval sync");
     last_error_count = (uint64_t)cnt[0] + cnt[1];
-    last_errors.clear();
+    clear_errors();
     err_windows.clear();
     errors_complete = cnt[0] <= errcap;
     uint32_t kept = std::min(cnt[0], errcap);
     if (kept) {
-        std::vector<mxp_err_rec> recs(kept);
-        if ((e = hipMemcpy(recs.data(), d_errlog.p, kept * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
+        last_recs.resize(kept);
+        if ((e = hipMemcpy(last_recs.data(), d_errlog.p, kept * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
             return hipfail(e, "download errlog");
-        for (auto& r : recs) last_errors[((uint64_t)r.req << 32) | r.rule] = {r.code, format_error(batch, db.get(), r)};
+        last_rec_text.assign(kept, -1);
+        for (uint32_t i = 0; i < kept; i++)  // (conversion errors print the caller's value: now)
+            if (last_recs[i].code >= ERR_CONV_S && last_recs[i].code <= ERR_CONV_D) {
+                last_rec_text[i] = (int32_t)last_rec_texts.size();
+                last_rec_texts.push_back(format_error(batch, db.get(), last_recs[i]));
+            }
     }
     if (cnt[2]) {
         int rc = expand_class_errors(batch, db.get(), cnt[2], errcap > kept ? errcap - kept : 0u);
@@ -1950,6 +1961,12 @@ int mxp_engine::expand_class_errors(const mxp_bag_batch* batch, mxp_dbatch* db, 
         const uint32_t s = vt_slot_of_rule[r.rule];
         const uint32_t a = (uint32_t)__builtin_popcount(last_mask & ((1u << s) - 1u));
         const uint32_t k = cls[(size_t)a * n + r.req];
+        // (every request of the class prints the same value: one text per class record)
+        int32_t text = -1;
+        if (r.code >= ERR_CONV_S && r.code <= ERR_CONV_D) {
+            text = (int32_t)last_rec_texts.size();
+            last_rec_texts.push_back(format_error(batch, db, r));
+        }
         for (uint32_t i = start[a][k]; i < start[a][k + 1]; i++) {
             if (emitted >= room) {
                 errors_complete = false;
@@ -1957,7 +1974,8 @@ int mxp_engine::expand_class_errors(const mxp_bag_batch* batch, mxp_dbatch* db, 
             }
             mxp_err_rec x = r;
             x.req = reqs[a][i];
-            last_errors[((uint64_t)x.req << 32) | x.rule] = {x.code, format_error(batch, db, x)};
+            last_recs.push_back(x);
+            last_rec_text.push_back(text);
             emitted++;
         }
     }
@@ -2012,9 +2030,26 @@ int mxp_engine::recompute_errors(uint32_t request) {
     return MXP_OK;
 }
 
+// the text of record `key` when the last batch logged it (formatted now unless it already was)
+bool mxp_engine::logged_error(uint64_t key) {
+    if (!rec_indexed) {
+        rec_index.reserve(last_recs.size());
+        for (uint32_t i = 0; i < (uint32_t)last_recs.size(); i++)
+            rec_index.emplace(((uint64_t)last_recs[i].req << 32) | last_recs[i].rule, i);
+        rec_indexed = true;
+    }
+    auto it = rec_index.find(key);
+    if (it == rec_index.end()) return false;
+    const mxp_err_rec& r = last_recs[it->second];
+    const int32_t t = last_rec_text[it->second];
+    last_errors[key] = {r.code, t >= 0 ? last_rec_texts[(size_t)t] : format_error(nullptr, last_db.get(), r)};
+    return true;
+}
+
 int mxp_engine::pair_error_text(uint32_t request, uint32_t rule, std::string* text, uint32_t* code) {
     const uint64_t key = ((uint64_t)request << 32) | rule;
     auto it = last_errors.find(key);
+    if (it == last_errors.end() && logged_error(key)) it = last_errors.find(key);
     if (it == last_errors.end() && !errors_complete) {
         int rc = recompute_errors(request);
         if (rc) return rc;

@@ -53,6 +53,11 @@ struct DevBuf {
         n = bytes;
         return hipMalloc(&p, bytes);
     }
+    // grow-only: keeps the allocation when it is large enough (engine-owned scratch reused across calls)
+    hipError_t reserve(size_t bytes) {
+        if (p && n >= (bytes ? bytes : 16)) return hipSuccess;
+        return alloc(bytes);
+    }
     template <class T>
     T* as() const {
         return static_cast<T*>(p);
@@ -270,11 +275,43 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t fill_chunk = MXP_FILL_CHUNK;  // MXP_FILL_CHUNK: groups per fill chunk
     uint32_t fill_span = 4;                // MXP_FILL_SPAN: 256-request spans per fill wave (1..8)
     uint32_t debug_flags = 0;
+    // MXP_TRACE=1: phase times of evaluations / Resolves on stderr (each phase synchronises the
+    // stream first, so traced calls are slower than untraced ones)
+    bool trace = false;
+    double trace_t = 0;
+    void trace_mark(const char* what) {
+        if (!trace) return;
+        (void)hipStreamSynchronize(stream);
+        const double t = mxp::now_seconds();
+        if (trace_t > 0 && what) fprintf(stderr, "mxp trace %-28s %9.3f ms\n", what, (t - trace_t) * 1e3);
+        trace_t = t;
+    }
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
 
-    // last batch error details: key = request << 32 | rule
+    // last batch error details: key = request << 32 | rule.  The records are kept as the device
+    // wrote them (last_recs) and their texts formatted when a pair is asked for: the index over
+    // them is built on the first mxp_pair_error, so an evaluation / Resolve pays only the record
+    // download.  Conversion errors print the caller's value, so theirs are formatted eagerly (the
+    // caller's batch is gone by the time a text is asked for); texts asked for, and the records of
+    // recomputed windows, are memoized in last_errors.
     std::unordered_map<uint64_t, std::pair<uint32_t, std::string>> last_errors;
+    std::vector<mxp_err_rec> last_recs;
+    std::vector<int32_t> last_rec_text;          // per record: index into last_rec_texts, or -1 (lazy)
+    std::vector<std::string> last_rec_texts;
+    std::unordered_map<uint64_t, uint32_t> rec_index;  // key -> record (built on first use)
+    bool rec_indexed = false;
+    void clear_errors() {
+        last_errors.clear();
+        last_recs.clear();
+        last_rec_text.clear();
+        last_rec_texts.clear();
+        rec_index.clear();
+        rec_indexed = false;
+    }
+    // resolve scratch (resolver.cpp), reused across calls
+    DevBuf res_dm, res_de, res_info, res_lo, res_hi, res_amask, res_empty, res_status, res_err_rule, res_count,
+        res_off, res_sel;
     uint64_t last_error_count = 0;
     std::unique_ptr<mxp_dbatch> last_db;  // keeps the last batch's interned overlays for decoding
 
@@ -377,7 +414,7 @@ struct mxp_engine : public mxp::LowerTables {
         rules.clear();
         have_rules = false;
         last_db.reset();  // the last batch's ids and error records belong to the old rule set
-        last_errors.clear();
+        clear_errors();
         err_windows.clear();
         errors_complete = true;
         need_ipof = need_tsof = need_strings = need_maps = need_rxof = false;
@@ -481,6 +518,7 @@ struct mxp_engine : public mxp::LowerTables {
     int recompute_errors(uint32_t request);
     // the text of an error pair of the last batch ("" when it did not fail); -1 on a device failure
     int pair_error_text(uint32_t request, uint32_t rule, std::string* text, uint32_t* code);
+    bool logged_error(uint64_t key);
     std::string string_of(const mxp_dbatch* db, uint64_t sid) const {
         if (!db) db = last_db.get();
         if (sid < gstrs.size()) return gstrs[sid];

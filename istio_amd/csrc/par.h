@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <string_view>
 #include <thread>
@@ -11,6 +12,10 @@
 #include <vector>
 
 namespace mxp {
+
+inline double now_seconds() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 // Threads for host loops: OMP_NUM_THREADS / MXP_PACK_THREADS when set (the GPU box exports its
 // CPU share there), else the hardware count; at most 64.

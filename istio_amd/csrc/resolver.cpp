@@ -7,6 +7,7 @@
 // ranges over the bitmaps mxp_eval_kernel / mxp_index_kernel produced.
 #include <cstring>
 #include <numeric>
+#include <string_view>
 
 #include "engine_impl.h"
 #include "resolve_args.h"
@@ -17,7 +18,8 @@ namespace {
 
 const char* const kProtocolAttr = "context.protocol";  // ContextProtocolAttributeName (resolver.go:95)
 
-// namespace info of every request: destAndNamespace + the tcp flag of filterActions
+// namespace info of every request: destAndNamespace + the tcp flag of filterActions (parallel over
+// requests; namespace names looked up as string views)
 int request_info(mxp_engine* eng, const mxp_bag_batch* b, std::vector<uint32_t>* info) {
     const auto& R = eng->resolver;
     const uint32_t n = b->n_requests;
@@ -26,40 +28,40 @@ int request_info(mxp_engine* eng, const mxp_bag_batch* b, std::vector<uint32_t>*
         if (R.identity == b->column_names[c]) idc = (int)c;
         if (strcmp(kProtocolAttr, b->column_names[c]) == 0) pc = (int)c;
     }
-    auto str = [&](uint64_t sid, size_t* len) {
-        *len = (size_t)(b->str_offsets[sid + 1] - b->str_offsets[sid]);
-        return (const char*)b->str_bytes + b->str_offsets[sid];
+    std::unordered_map<std::string_view, uint32_t> ns_ids;
+    for (const auto& kv : R.ns_ids) ns_ids.emplace(std::string_view(kv.first), kv.second);
+    auto str = [&](uint64_t sid) {
+        return std::string_view((const char*)b->str_bytes + b->str_offsets[sid],
+                                (size_t)(b->str_offsets[sid + 1] - b->str_offsets[sid]));
     };
-    info->assign(n, MXP_NS_MISSING);
-    std::string ns;
-    for (uint32_t q = 0; q < n; q++) {
-        // attrs.Get(idAttr): nil -> "identity not found"; not a string -> "identity must be string"
-        if (idc < 0 || b->kinds[idc][q] == MXP_ABSENT) continue;
-        if (b->kinds[idc][q] != MXP_STRING) {
-            (*info)[q] = MXP_NS_NOTSTRING;
-            continue;
+    info->resize(n);
+    uint32_t* out = info->data();
+    mxp::par_for(n, 16384, [&](uint64_t q0, uint64_t q1, unsigned) {
+        for (uint64_t q = q0; q < q1; q++) {
+            // attrs.Get(idAttr): nil -> "identity not found"; not a string -> "identity must be string"
+            if (idc < 0 || b->kinds[idc][q] == MXP_ABSENT) {
+                out[q] = MXP_NS_MISSING;
+                continue;
+            }
+            if (b->kinds[idc][q] != MXP_STRING) {
+                out[q] = MXP_NS_NOTSTRING;
+                continue;
+            }
+            const std::string_view d = str(b->values[idc][q]);
+            // strings.SplitN(dest, ".", 3): ns = splits[1] when there is at least one '.'
+            std::string_view ns;
+            const size_t dot1 = d.find('.');
+            if (dot1 != std::string_view::npos) {
+                const std::string_view rest = d.substr(dot1 + 1);
+                ns = rest.substr(0, rest.find('.'));
+            }
+            auto it = ns_ids.find(ns);
+            const uint32_t v = it == ns_ids.end() ? MXP_NS_NONE : it->second;
+            // tcp := attrs.Get("context.protocol") == "tcp": an interface compare, so only a string
+            const bool tcp = pc >= 0 && b->kinds[pc][q] == MXP_STRING && str(b->values[pc][q]) == "tcp";
+            out[q] = v | (tcp ? 0x80000000u : 0u);
         }
-        size_t len;
-        const char* d = str(b->values[idc][q], &len);
-        // strings.SplitN(dest, ".", 3): ns = splits[1] when there is at least one '.'
-        const char* dot1 = (const char*)memchr(d, '.', len);
-        ns.clear();
-        if (dot1) {
-            const char* rest = dot1 + 1;
-            const char* dot2 = (const char*)memchr(rest, '.', (size_t)(d + len - rest));
-            ns.assign(rest, dot2 ? (size_t)(dot2 - rest) : (size_t)(d + len - rest));
-        }
-        auto it = R.ns_ids.find(ns);
-        uint32_t v = it == R.ns_ids.end() ? MXP_NS_NONE : it->second;
-        // tcp := attrs.Get("context.protocol") == "tcp": an interface compare, so only a string
-        bool tcp = false;
-        if (pc >= 0 && b->kinds[pc][q] == MXP_STRING) {
-            size_t pl;
-            const char* p = str(b->values[pc][q], &pl);
-            tcp = pl == 3 && memcmp(p, "tcp", 3) == 0;
-        }
-        (*info)[q] = v | (tcp ? 0x80000000u : 0u);
-    }
+    });
     return MXP_OK;
 }
 
@@ -118,7 +120,8 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     const uint32_t NR = (uint32_t)eng->rules.size();
     const uint32_t W = (NR + 31) / 32;
     std::unique_ptr<mxp_dbatch> db;
-    DevBuf dm, de;
+    DevBuf& dm = eng->res_dm;  // (engine-owned scratch: no allocation per call once large enough)
+    DevBuf& de = eng->res_de;
     std::vector<mxp_ref_rec> recs;
     int rc = ref_off ? eng->refs_evaluate(batch, dm, de, db, recs) : eng->evaluate(batch, dm, de, nullptr, db);
     if (rc) return rc;
@@ -131,10 +134,13 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     }
     std::vector<uint32_t> info;
     request_info(eng, batch, &info);
+    eng->trace_mark("request namespaces (host)");
     hipError_t e;
-    DevBuf d_info, d_lo, d_hi, d_amask, d_empty, d_status, d_err_rule, d_count, d_off, d_sel;
+    DevBuf &d_info = eng->res_info, &d_lo = eng->res_lo, &d_hi = eng->res_hi, &d_amask = eng->res_amask,
+           &d_empty = eng->res_empty, &d_status = eng->res_status, &d_err_rule = eng->res_err_rule,
+           &d_count = eng->res_count, &d_off = eng->res_off, &d_sel = eng->res_sel;
     auto up = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
-        if ((e = d.alloc(bytes)) != hipSuccess) return eng->hipfail(e, what);
+        if ((e = d.reserve(bytes)) != hipSuccess) return eng->hipfail(e, what);
         if (bytes && (e = hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, eng->stream)) != hipSuccess)
             return eng->hipfail(e, what);
         return MXP_OK;
@@ -144,9 +150,9 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     if ((rc = up(d_hi, R.ns_hi.data(), R.ns_hi.size() * 4, "upload ns_hi"))) return rc;
     if ((rc = up(d_amask, amask.data(), amask.size() * 4, "upload amask"))) return rc;
     if ((rc = up(d_empty, empty.data(), empty.size() * 4, "upload empty"))) return rc;
-    if ((e = d_status.alloc(n)) != hipSuccess) return eng->hipfail(e, "alloc status");
-    if ((e = d_err_rule.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err_rule");
-    if ((e = d_count.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc count");
+    if ((e = d_status.reserve(n)) != hipSuccess) return eng->hipfail(e, "alloc status");
+    if ((e = d_err_rule.reserve((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err_rule");
+    if ((e = d_count.reserve((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc count");
     mxp_resolve_args A;
     memset(&A, 0, sizeof A);
     A.n = n;
@@ -170,7 +176,9 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         return eng->hipfail(e, "download status");
     if (n && (e = hipMemcpyAsync(err_rule, d_err_rule.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
         return eng->hipfail(e, "download err_rule");
+    eng->trace_mark("resolve kernel + downloads");
     if ((rc = eng->collect_errors(batch, db))) return rc;  // synchronises the stream
+    eng->trace_mark("error records");
     int ref_rc = MXP_OK;
     if (ref_off) {
         const mxp_engine::RefScope scope{&info, status, err_rule, variety};
@@ -183,7 +191,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     if (total > sel_cap) return MXP_ERR_NOMEM;
     if (total) {
         if ((rc = up(d_off, sel_off, ((size_t)n + 1) * 8, "upload sel_off"))) return rc;
-        if ((e = d_sel.alloc(total * 4)) != hipSuccess) return eng->hipfail(e, "alloc sel");
+        if ((e = d_sel.reserve(total * 4)) != hipSuccess) return eng->hipfail(e, "alloc sel");
         A.sel_off = d_off.as<uint64_t>();
         A.sel_rules = d_sel.as<uint32_t>();
         if ((e = mxp_launch_resolve(&A, 1, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
@@ -191,6 +199,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
             return eng->hipfail(e, "download sel");
         if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "resolve sync");
     }
+    eng->trace_mark("action lists (gather + download)");
     return ref_rc;
 }
 
