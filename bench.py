@@ -59,7 +59,7 @@ def parse():
                    help="c2 (default, the BASELINE metric; + a C4 block); c4 route rules; c5 = C2 predicates + "
                         "memquota with one combined all-reduce; C3 lists; c5-quota memquota alone")
     p.add_argument("--list-entries", type=int, default=100_000)
-    p.add_argument("--e2e-reps", type=int, default=3, help="end-to-end resolve calls timed (median)")
+    p.add_argument("--e2e-reps", type=int, default=3, help="end-to-end resolve calls timed (median); 0 skips the end-to-end block (profiling sessions)")
     p.add_argument("--error-output", default="compact", choices=["compact", "bitmap"],
                    help="compact: per-request error flags (a Resolve's view); bitmap: the full error bitmap")
     return p.parse_args()
@@ -478,7 +478,8 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
                         "collective": "one all_reduce(sum) of hits[R] ++ quota_delta[K] per step"}
     hits = ctr.totals()[0]
     out["hits_total"] = int(hits.sum().item())
-    out["end_to_end"] = end_to_end(eng, batch, R, args.e2e_reps)
+    if args.e2e_reps > 0:
+        out["end_to_end"] = end_to_end(eng, batch, R, args.e2e_reps)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         if kind == "c4":
             sample = W.c4_workload(n_rules=args.rules, n_requests=1 << 14, seed=4)[2]
@@ -518,7 +519,8 @@ def main():
         # the representative config BASELINE.json quotes at 10k rules (configs[3]), driver-timed too
         c4 = predicate_bench(args, "c4", rank, world, local)
         out["c4"] = {k: c4[k] for k in ("metric", "value", "unit", "ms_per_step", "eval_ms", "kernels_ms",
-                                        "pack_upload_s", "end_to_end", "config", "roofline", "lds_bank_conflicts")}
+                                        "pack_upload_s", "end_to_end", "config", "roofline", "lds_bank_conflicts")
+                     if k in c4}
         if "cpu_baseline" in c4:
             out["c4"]["cpu_baseline"] = c4["cpu_baseline"]
     if rank == 0:

@@ -1628,6 +1628,10 @@ void mxp_engine_destroy(mxp_engine* eng) {
     if (!eng) return;
     if (eng->device >= 0) (void)hipSetDevice(eng->device);
     if (eng->pk_host) (void)hipHostFree(eng->pk_host);
+    for (int k = 0; k < 2; k++) {
+        if (eng->bounce_ev[k]) (void)hipEventDestroy(eng->bounce_ev[k]);
+        if (eng->bounce[k]) (void)hipHostFree(eng->bounce[k]);
+    }
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     for (auto& x : eng->ev)
         if (x) (void)hipEventDestroy(x);
@@ -1896,6 +1900,46 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
     return rc;
 }
 
+// Synchronous download of `bytes` from device memory into caller memory, ordered after the work
+// already queued on the engine stream.  Small copies go direct; large ones through the pinned
+// bounce pair (DMA of chunk k + 1 beside the parallel host copy of chunk k).
+int mxp_engine::download(void* dst, const void* dsrc, size_t bytes, const char* what) {
+    hipError_t e;
+    if (bytes < (4u << 20)) {
+        if (bytes && (e = hipMemcpyAsync(dst, dsrc, bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+            return hipfail(e, what);
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, what);
+        return MXP_OK;
+    }
+    for (int k = 0; k < 2; k++) {
+        if (!bounce[k] && (e = hipHostMalloc(&bounce[k], kBounce, hipHostMallocDefault)) != hipSuccess) {
+            bounce[k] = nullptr;
+            return hipfail(e, "bounce buffer");
+        }
+        if (!bounce_ev[k] && (e = hipEventCreateWithFlags(&bounce_ev[k], hipEventDisableTiming)) != hipSuccess) {
+            bounce_ev[k] = nullptr;
+            return hipfail(e, "bounce event");
+        }
+    }
+    const size_t nchunk = (bytes + kBounce - 1) / kBounce;
+    auto issue = [&](size_t c) -> hipError_t {
+        const size_t off = c * kBounce, len = std::min(kBounce, bytes - off);
+        hipError_t r = hipMemcpyAsync(bounce[c & 1], (const uint8_t*)dsrc + off, len, hipMemcpyDeviceToHost, stream);
+        return r == hipSuccess ? hipEventRecord(bounce_ev[c & 1], stream) : r;
+    };
+    for (size_t c = 0; c < std::min<size_t>(2, nchunk); c++)
+        if ((e = issue(c)) != hipSuccess) return hipfail(e, what);
+    for (size_t c = 0; c < nchunk; c++) {
+        if ((e = hipEventSynchronize(bounce_ev[c & 1])) != hipSuccess) return hipfail(e, what);
+        const size_t off = c * kBounce, len = std::min(kBounce, bytes - off);
+        const uint8_t* from = (const uint8_t*)bounce[c & 1];
+        uint8_t* to = (uint8_t*)dst + off;
+        mxp::par_for(len, 1u << 20, [&](uint64_t a, uint64_t b, unsigned) { memcpy(to + a, from + a, b - a); });
+        if (c + 2 < nchunk && (e = issue(c + 2)) != hipSuccess) return hipfail(e, what);
+    }
+    return MXP_OK;
+}
+
 int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_dbatch>& db) {
     hipError_t e;
     // [0] records of the log, [1] error pairs of value-class rules, [2] class records
@@ -2030,8 +2074,8 @@ int mxp_engine::recompute_errors(uint32_t request) {
     return MXP_OK;
 }
 
-// the text of record `key` when the last batch logged it (formatted now unless it already was)
-bool mxp_engine::logged_error(uint64_t key) {
+// the record the last batch logged for `key`, or -1 (the index over the records is built on first use)
+int64_t mxp_engine::logged_record(uint64_t key) {
     if (!rec_indexed) {
         rec_index.reserve(last_recs.size());
         for (uint32_t i = 0; i < (uint32_t)last_recs.size(); i++)
@@ -2039,27 +2083,37 @@ bool mxp_engine::logged_error(uint64_t key) {
         rec_indexed = true;
     }
     auto it = rec_index.find(key);
-    if (it == rec_index.end()) return false;
-    const mxp_err_rec& r = last_recs[it->second];
-    const int32_t t = last_rec_text[it->second];
-    last_errors[key] = {r.code, t >= 0 ? last_rec_texts[(size_t)t] : format_error(nullptr, last_db.get(), r)};
-    return true;
+    return it == rec_index.end() ? -1 : (int64_t)it->second;
 }
 
+// text (when `text` is non-null) and code of a pair's error in the last batch; ERR_NONE when the
+// pair did not fail
 int mxp_engine::pair_error_text(uint32_t request, uint32_t rule, std::string* text, uint32_t* code) {
     const uint64_t key = ((uint64_t)request << 32) | rule;
     auto it = last_errors.find(key);
-    if (it == last_errors.end() && logged_error(key)) it = last_errors.find(key);
+    if (it == last_errors.end()) {
+        const int64_t i = logged_record(key);
+        if (i >= 0) {
+            const mxp_err_rec& r = last_recs[(size_t)i];
+            *code = r.code;
+            if (text) {
+                const int32_t t = last_rec_text[(size_t)i];
+                *text = t >= 0 ? last_rec_texts[(size_t)t] : format_error(nullptr, last_db.get(), r);
+                last_errors[key] = {r.code, *text};
+            }
+            return MXP_OK;
+        }
+    }
     if (it == last_errors.end() && !errors_complete) {
         int rc = recompute_errors(request);
         if (rc) return rc;
         it = last_errors.find(key);
     }
     if (it == last_errors.end()) {
-        text->clear();
+        if (text) text->clear();
         *code = ERR_NONE;
     } else {
-        *text = it->second.second;
+        if (text) *text = it->second.second;
         *code = it->second.first;
     }
     return MXP_OK;
@@ -2075,7 +2129,6 @@ static int eval_common(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* ma
     const uint32_t n = batch->n_requests;
     const uint32_t R = (uint32_t)eng->rules.size();
     const uint32_t W = (R + 31) / 32;
-    hipError_t e;
     // bitmaps go straight into the caller's arrays; host copies only when per-pair codes are wanted
     std::vector<uint32_t> hm, he;
     if (codes) {
@@ -2084,12 +2137,9 @@ static int eval_common(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* ma
     }
     uint32_t* to_m = codes ? hm.data() : match_bits;
     uint32_t* to_e = codes ? he.data() : err_bits;
-    if (to_m && (e = hipMemcpyAsync(to_m, dm.p, (size_t)W * n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-        return eng->hipfail(e, "download match");
-    if (to_e && (e = hipMemcpyAsync(to_e, de.p, (size_t)W * n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-        return eng->hipfail(e, "download err");
-    if (values && (e = hipMemcpyAsync(values, dv.p, (size_t)n * R * 8, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-        return eng->hipfail(e, "download values");
+    if (to_m && (rc = eng->download(to_m, dm.p, (size_t)W * n * 4, "download match"))) return rc;
+    if (to_e && (rc = eng->download(to_e, de.p, (size_t)W * n * 4, "download err"))) return rc;
+    if (values && (rc = eng->download(values, dv.p, (size_t)n * R * 8, "download values"))) return rc;
     if ((rc = eng->collect_errors(batch, db))) return rc;
     if (codes && match_bits) memcpy(match_bits, hm.data(), hm.size() * 4);
     if (codes && err_bits) memcpy(err_bits, he.data(), he.size() * 4);
@@ -2100,9 +2150,8 @@ static int eval_common(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* ma
                 uint32_t bit = 1u << (r % 32);
                 uint8_t c = (hm[w] & bit) ? PC_TRUE : PC_FALSE;
                 if (he[w] & bit) {
-                    std::string t;
                     uint32_t code = ERR_NONE;
-                    if ((rc = eng->pair_error_text(q, r, &t, &code))) return rc;
+                    if ((rc = eng->pair_error_text(q, r, nullptr, &code))) return rc;
                     c = code >= 32 ? PC_PANIC : PC_ERROR;
                 }
                 codes[(size_t)q * R + r] = c;

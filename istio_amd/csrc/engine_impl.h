@@ -286,6 +286,13 @@ struct mxp_engine : public mxp::LowerTables {
         if (trace_t > 0 && what) fprintf(stderr, "mxp trace %-28s %9.3f ms\n", what, (t - trace_t) * 1e3);
         trace_t = t;
     }
+    // large device -> caller-memory downloads through two pinned bounce buffers: the DMA of chunk
+    // k + 1 overlaps the host threads' copy of chunk k out of pinned memory (a pageable hipMemcpy
+    // stages at a fraction of the pinned rate)
+    static constexpr size_t kBounce = 32u << 20;
+    void* bounce[2] = {nullptr, nullptr};
+    hipEvent_t bounce_ev[2] = {nullptr, nullptr};
+    int download(void* dst, const void* dsrc, size_t bytes, const char* what);
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
 
@@ -518,7 +525,7 @@ struct mxp_engine : public mxp::LowerTables {
     int recompute_errors(uint32_t request);
     // the text of an error pair of the last batch ("" when it did not fail); -1 on a device failure
     int pair_error_text(uint32_t request, uint32_t rule, std::string* text, uint32_t* code);
-    bool logged_error(uint64_t key);
+    int64_t logged_record(uint64_t key);
     std::string string_of(const mxp_dbatch* db, uint64_t sid) const {
         if (!db) db = last_db.get();
         if (sid < gstrs.size()) return gstrs[sid];

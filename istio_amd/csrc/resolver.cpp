@@ -195,9 +195,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         A.sel_off = d_off.as<uint64_t>();
         A.sel_rules = d_sel.as<uint32_t>();
         if ((e = mxp_launch_resolve(&A, 1, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
-        if ((e = hipMemcpyAsync(sel_rules, d_sel.p, total * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-            return eng->hipfail(e, "download sel");
-        if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "resolve sync");
+        if ((rc = eng->download(sel_rules, d_sel.p, total * 4, "download sel"))) return rc;
     }
     eng->trace_mark("action lists (gather + download)");
     return ref_rc;

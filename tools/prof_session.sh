@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 out=gpurun_out/$1
 shift
 mkdir -p "$out"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- python3 bench.py --no-cpu-baseline "$@" > "$out/bench.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out" -o run -- python3 bench.py --no-cpu-baseline --e2e-reps 0 "$@" > "$out/bench.log" 2>&1
 rc=$?
 echo "rocprof rc=$rc"
 find "$out" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats.csv" \;

@@ -16,7 +16,7 @@ i=0
 for p in "${passes[@]}"; do
     i=$((i + 1))
     timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d "$out/sq$i" -o pmc -- \
-        python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 "$@" > "$out/sq$i.log" 2>&1
+        python3 bench.py --no-cpu-baseline --e2e-reps 0 --steps 2 --warmup 1 "$@" > "$out/sq$i.log" 2>&1
     rc=$?
     echo "sq$i rc=$rc"
     [ $rc -ne 0 ] && exit $rc
