@@ -331,6 +331,12 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out);
  * whose rules depend on that column's value alone; a batch with few distinct values in such a column
  * evaluates its rules once per distinct value).  Returns the number of values written (<= cap). */
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap);
+/* The attribute names the compiled rule set reads -- the columns a caller must pack into an
+ * mxp_bag_batch (attribute.Bag.Get of each, protoBag.go:91-114) -- plus, once mxp_resolver_set has
+ * run, the identity attribute and context.protocol (resolver.go:180-208).  Writes up to cap
+ * pointers to engine-owned NUL-terminated names (valid until the next call on this engine) and
+ * returns the total count; names may be NULL to count.  0 without a compiled rule set. */
+uint32_t mxp_ruleset_columns(mxp_engine* eng, const char** names, uint32_t cap);
 uint32_t mxp_dbatch_requests(const mxp_dbatch* db);
 /* Profiling hook (engine created with MXP_WAVE_TIMES set): per wavefront of the last guard-index
  * kernel launch, {start, end, XCC} (wall_clock64 ticks, 100 MHz), 3 x u64 per wave; *n_out = values

@@ -1743,6 +1743,14 @@ int mxp_debug_wave_times(mxp_engine* eng, uint64_t* out, uint64_t cap, uint64_t*
     return MXP_OK;
 }
 
+uint32_t mxp_ruleset_columns(mxp_engine* eng, const char** names, uint32_t cap) {
+    if (!eng || !eng->have_rules) return 0;
+    eng->attr_names = eng->read_attributes();
+    const uint32_t n = (uint32_t)eng->attr_names.size();
+    for (uint32_t i = 0; names && i < n && i < cap; i++) names[i] = eng->attr_names[i].c_str();
+    return n;
+}
+
 uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
     if (!eng || !out) return 0;
     const mxp_engine::Plan* P = eng->plan0();

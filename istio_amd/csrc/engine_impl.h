@@ -445,6 +445,23 @@ struct mxp_engine : public mxp::LowerTables {
     } resolver;
 
     int compile(const char* const* exprs, uint32_t n, int32_t* status);
+    // the attribute names the compiled set reads (columns, then the maps of map["key"] columns), plus
+    // the resolver's identity attribute and context.protocol once it is configured
+    std::vector<std::string> read_attributes() const {
+        std::vector<std::string> out;
+        std::set<std::string> seen;
+        auto add = [&](const std::string& s) {
+            if (seen.insert(s).second) out.push_back(s);
+        };
+        for (auto& c : cols) add(c);
+        for (auto& v : vcols) add(v.first);
+        if (resolver.set) {
+            add(resolver.identity);
+            add("context.protocol");
+        }
+        return out;
+    }
+    std::vector<std::string> attr_names;  // mxp_ruleset_columns' strings (valid until the next call)
     // pack + launch into fresh device bitmaps (dm, de; dv = Eval registers when non-null)
     int evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv, std::unique_ptr<mxp_dbatch>& db);
     // wait for the evaluation, fetch and format its error records, keep `db` as the last batch

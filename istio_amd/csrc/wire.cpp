@@ -55,16 +55,7 @@ int mxp_engine::wire_decode(const mxp_wire_batch* w, const char* const* names, u
         for (uint32_t i = 0; i < n_names; i++) W->names.emplace_back(names[i] ? names[i] : "");
     } else {
         if (!have_rules) return fail(MXP_ERR_STATE, "no rule set compiled (names = NULL decodes its attributes)");
-        std::set<std::string> seen;
-        auto add = [&](const std::string& s) {
-            if (seen.insert(s).second) W->names.push_back(s);
-        };
-        for (auto& c : cols) add(c);
-        for (auto& v : vcols) add(v.first);
-        if (resolver.set) {
-            add(resolver.identity);
-            add("context.protocol");
-        }
+        W->names = read_attributes();
     }
     const uint32_t C = (uint32_t)W->names.size();
     const uint32_t n = w->n_requests;

@@ -89,6 +89,7 @@ SIGNATURES = {
     "mxp_set_pipeline": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32]),
     "mxp_kernel_times": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_float), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]),
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
+    "mxp_ruleset_columns": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32]),
     "mxp_debug_wave_times": (ctypes.c_int, [_VP, _VP, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
 }
 
@@ -236,6 +237,14 @@ class Engine:
         k = self.lib.mxp_ruleset_info(self.h, out, 10)
         return dict(zip(("guarded", "templated", "templates", "segments", "indexed", "columns", "composite",
                          "aliases", "dense", "value_class_columns"), list(out)[:k]))
+
+    def read_attributes(self) -> list:
+        """mxp_ruleset_columns: the attribute names the compiled set reads (the columns to pack),
+        plus the resolver's identity attribute and context.protocol once it is configured."""
+        n = self.lib.mxp_ruleset_columns(self.h, None, 0)
+        arr = (ctypes.c_char_p * max(n, 1))()
+        n = self.lib.mxp_ruleset_columns(self.h, arr, n)
+        return [arr[i].decode() for i in range(n)]
 
     # ------------------------------------------------------------------ evaluation
     def eval_batch(self, batch: BagBatch):

@@ -45,3 +45,19 @@ def test_host_only_engine_refuses_eval(libmxp):
 def test_gfx950_code_object(libmxp):
     data = open(os.path.join(ROOT, "istio_amd", "libmxp.so"), "rb").read()
     assert b"gfx950" in data
+
+
+def test_ruleset_columns(libmxp):
+    """mxp_ruleset_columns: the attributes a rule set reads (columns, then map attributes of
+    map["key"] reads), then the resolver's identity and context.protocol (host-only engine)."""
+    import numpy as np
+    from istio_amd.engine import Engine
+    eng = Engine(-1)
+    assert eng.read_attributes() == []
+    eng.set_vocabulary({"a": "STRING", "b": "INT64", "m": "STRING_MAP", "destination.service": "STRING",
+                        "context.protocol": "STRING"})
+    eng.compile(['a == "x" && b == 2', 'm["k"] == a', 'a.startsWith("y")'])
+    assert eng.read_attributes() == ["a", "b", "m"]
+    eng.set_resolver("destination.service", "default", ["default"] * 3, np.ones(3, np.uint32), np.zeros(3, np.uint8),
+                     np.zeros(3, np.uint8))
+    assert eng.read_attributes() == ["a", "b", "m", "destination.service", "context.protocol"]
