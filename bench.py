@@ -502,9 +502,17 @@ def main():
 
     from istio_amd import dist as D
     rank, world, local = D.world()
+    # MXP_REHEARSE_MULTI=1: rehearsal of the N > 1 path on a one-GPU box -- every rank on cuda:0,
+    # gloo collectives (RCCL refuses two ranks on one device); the line says so ("rehearsal")
+    rehearse = world > 1 and os.environ.get("MXP_REHEARSE_MULTI") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from istio_amd import build
     build.build()
@@ -523,6 +531,8 @@ def main():
                      if k in c4}
         if "cpu_baseline" in c4:
             out["c4"]["cpu_baseline"] = c4["cpu_baseline"]
+    if rehearse:
+        out["rehearsal"] = "%d ranks on one GPU over gloo: exercises the multi-rank step, not a scaling number" % world
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
