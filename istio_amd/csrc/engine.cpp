@@ -405,7 +405,7 @@ int mxp_engine::build_plan(Plan& P) {
     auto add_eq_table = [&](const std::map<uint64_t, std::vector<uint32_t>>& groups, const std::vector<uint32_t>& tmpl_of,
                             uint32_t* hoff) -> uint32_t {
         uint32_t cap = 1;
-        while (cap < 2 * groups.size()) cap <<= 1;
+        while (cap < (2u << index_sparsity) * groups.size()) cap <<= 1;
         *hoff = (uint32_t)hents.size();
         hents.resize(hents.size() + cap, mxp_hent{0, 0, 0, 0});
         for (auto& kv : groups) {
@@ -431,7 +431,7 @@ int mxp_engine::build_plan(Plan& P) {
             continue;
         }
         uint32_t cap = 1;
-        while (cap < 2 * ci.second.size()) cap <<= 1;
+        while (cap < (2u << index_sparsity) * ci.second.size()) cap <<= 1;
         x.hmask = cap - 1;
         x.hoff = (uint32_t)hents.size();
         hents.resize(hents.size() + cap, mxp_hent{0, 0, 0, 0});
@@ -471,7 +471,7 @@ int mxp_engine::build_plan(Plan& P) {
         x.hmask = add_eq_table(by_k1, rule_tmpl, &x.hoff);
         // composite table: entry pairs
         uint32_t cap = 1;
-        while (cap < 2 * ci.second.size()) cap <<= 1;
+        while (cap < (2u << index_sparsity) * ci.second.size()) cap <<= 1;
         x.hmask2 = cap - 1;
         x.hoff2 = (uint32_t)hents.size();
         hents.resize(hents.size() + 2 * (size_t)cap, mxp_hent{0, 0, 0, 0});
@@ -1601,6 +1601,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     e->device = device;
     if (const char* f = getenv("MXP_DEBUG_FLAGS")) e->debug_flags = (uint32_t)atoi(f);
     if (const char* f = getenv("MXP_TRACE")) e->trace = atoi(f) != 0;
+    if (const char* f = getenv("MXP_INDEX_SPARSITY")) e->index_sparsity = (uint32_t)std::min(4, std::max(0, atoi(f)));
     // tuning knobs (results are identical for every setting)
     if (const char* f = getenv("MXP_GPW")) e->groups_per_wave = std::max(1, atoi(f));
     if (const char* f = getenv("MXP_FILL_CHUNK")) e->fill_chunk = (uint32_t)std::max(1, atoi(f));

@@ -275,6 +275,10 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t fill_chunk = MXP_FILL_CHUNK;  // MXP_FILL_CHUNK: groups per fill chunk
     uint32_t fill_span = 4;                // MXP_FILL_SPAN: 256-request spans per fill wave (1..8)
     uint32_t debug_flags = 0;
+    // guard-index hash tables hold >= 2^(1 + index_sparsity) slots per key (MXP_INDEX_SPARSITY):
+    // a lower load factor shortens the probe chains of the many misses (prefix probes at every key
+    // length)
+    uint32_t index_sparsity = 0;
     // MXP_TRACE=1: phase times of evaluations / Resolves on stderr (each phase synchronises the
     // stream first, so traced calls are slower than untraced ones)
     bool trace = false;
