@@ -277,8 +277,9 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t debug_flags = 0;
     // guard-index hash tables hold >= 2^(1 + index_sparsity) slots per key (MXP_INDEX_SPARSITY):
     // a lower load factor shortens the probe chains of the many misses (prefix probes at every key
-    // length)
-    uint32_t index_sparsity = 0;
+    // length).  Same-box A/B (profiles/r2_v7_ab_sparse_*.log), ms per evaluation for 0 / 1 / 2 / 3:
+    // C4 2.216 / 2.188 / 2.178 / 2.178, C2 0.576 / 0.573 / 0.566 / 0.562
+    uint32_t index_sparsity = 2;
     // MXP_TRACE=1: phase times of evaluations / Resolves on stderr (each phase synchronises the
     // stream first, so traced calls are slower than untraced ones)
     bool trace = false;
