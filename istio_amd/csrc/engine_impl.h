@@ -269,7 +269,8 @@ struct mxp_engine : public mxp::LowerTables {
     hipEvent_t chunk_ev[kChunksMax + 1] = {};
     // MXP_DEBUG_FLAGS, ablation only: 1 no in-wave VM, 2 no guards (results invalid), 8 no guard index,
     // 16 no composite index, 64 no duplicate folding, 128 plain fill stores, 256 no dense injection,
-    // 512 index equality-only guards too
+    // 512 index equality-only guards too, 524288 / 1048576 fused / streaming hit counters forced,
+    // 2097152 value-class fill chunks gather from global memory (no LDS staging)
     // fill layout (same-box A/B on C2, profiles/r1_v17_ab_fill*.log: span 1 / chunk 32 0.945 ms,
     // span 4 0.832-0.836, span 4 / chunk 16 0.831; spans 3, 5, 6, 8 and chunks 4..1000 no better)
     uint32_t fill_chunk = MXP_FILL_CHUNK;  // MXP_FILL_CHUNK: groups per fill chunk

@@ -938,12 +938,12 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
 //                           of each request into its group words.
 // Requests per workgroup of mxp_vt_classify_kernel and its LDS table (twice as many slots, so
 // the workgroup's distinct keys always fit).
-#define MXP_VTC_REQ 2048u
-#define MXP_VTC_LCAP 4096u
+#define MXP_VTC_REQ 1024u
+#define MXP_VTC_LCAP 2048u
 extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kargs A) {
     // The hot keys of a low-cardinality column would serialise on a handful of global addresses if
     // every request probed the global table (and L1 may keep a stale EMPTY line), so a workgroup
-    // first dedups its 2048 requests' keys in an LDS table, resolves each distinct key against the
+    // first dedups its 1024 requests' keys in an LDS table (40 KB: 4 workgroups per CU), resolves each distinct key against the
     // global table once (compare-and-swap, the inserter's request becomes the class
     // representative), then hands every request its class from LDS.
     __shared__ unsigned long long lkey[MXP_VTC_LCAP];
@@ -967,25 +967,36 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
 #pragma unroll
         for (uint32_t r = 0; r < MXP_VTC_REQ / 256u; r++) {
             const uint32_t req = base + tid + 256u * r;
-            loc[r] = 0xFFFFFFFFu;
-            if (req >= A.q1) continue;
-            const uint64_t key = mxp_vt_key(A.kinds[(uint64_t)col * N + req], A.vals[(uint64_t)col * N + req]);
-            uint32_t h = mxp_hash64(key) & (MXP_VTC_LCAP - 1u);
-            for (;;) {
-                const unsigned long long cur = lkey[h];
-                if (cur == key) break;
-                if (cur == MXP_VT_EMPTY) {
-                    const unsigned long long old = atomicCAS(&lkey[h], (unsigned long long)MXP_VT_EMPTY, (unsigned long long)key);
-                    if (old == MXP_VT_EMPTY) {
-                        lrep[h] = req;
-                        break;
+            uint32_t h = 0xFFFFFFFFu;
+            if (req < A.q1) {
+                const uint64_t key = mxp_vt_key(A.kinds[(uint64_t)col * N + req], A.vals[(uint64_t)col * N + req]);
+                h = mxp_hash64(key) & (MXP_VTC_LCAP - 1u);
+                for (;;) {
+                    const unsigned long long cur = lkey[h];
+                    if (cur == key) break;
+                    if (cur == MXP_VT_EMPTY) {
+                        const unsigned long long old =
+                            atomicCAS(&lkey[h], (unsigned long long)MXP_VT_EMPTY, (unsigned long long)key);
+                        if (old == MXP_VT_EMPTY) {
+                            lrep[h] = req;
+                            break;
+                        }
+                        if (old == key) break;
                     }
-                    if (old == key) break;
+                    h = (h + 1u) & (MXP_VTC_LCAP - 1u);
                 }
-                h = (h + 1u) & (MXP_VTC_LCAP - 1u);
             }
             loc[r] = h;
-            if (count) atomicAdd(&lcnt[h], 1u);
+            if (count) {
+                // class sizes: one LDS add per distinct slot of the wave (a low-cardinality column puts
+                // most of a wave's lanes on a few slots: per-lane atomics there serialise)
+                for (uint64_t pend = __ballot(h != 0xFFFFFFFFu); pend;) {
+                    const uint32_t sl = __builtin_amdgcn_readlane(h, (uint32_t)__builtin_ctzll(pend));
+                    const uint64_t same = __ballot(h == sl);
+                    if ((tid & 63u) == (uint32_t)__builtin_ctzll(same)) atomicAdd(&lcnt[sl], (uint32_t)__builtin_popcountll(same));
+                    pend &= ~same;
+                }
+            }
         }
         __syncthreads();
         // 2. each distinct key of the workgroup against the global table (room for twice the
@@ -996,10 +1007,15 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
             if (key == MXP_VT_EMPTY) continue;
             uint32_t h = mxp_hash64(key) & (cap - 1u);
             for (;;) {
-                const unsigned long long old = atomicCAS(T + h, (unsigned long long)MXP_VT_EMPTY, key);
+                // (read first: every workgroup meets the column's few hot keys, and a CAS on a slot
+                // another workgroup already holds would serialise at L2 for nothing)
+                unsigned long long old = __hip_atomic_load(T + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (old == MXP_VT_EMPTY) {
-                    A.vt_rep[kb + h] = lrep[i];
-                    break;
+                    old = atomicCAS(T + h, (unsigned long long)MXP_VT_EMPTY, key);
+                    if (old == MXP_VT_EMPTY) {
+                        A.vt_rep[kb + h] = lrep[i];
+                        break;
+                    }
                 }
                 if (old == key) break;
                 h = (h + 1u) & (cap - 1u);
@@ -1078,16 +1094,17 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_eval_nfa_kernel(mxp_kar
 
 // Fill chunks with value-class merge entries: as mxp_fill_kernel (words of uniform indexed groups
 // depend on their guard column's kind), plus the class words of each request.  A lane owns 4
-// consecutive requests (one 16-byte store per plane and group), a wave 256, a workgroup 1024; the
-// requests' classes are loaded once (4 x u16 per active column) and kept in registers.
-extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A) {
+// consecutive requests (one 16-byte store per plane and group), a wave 256; the requests' classes
+// are loaded once (4 x u16 per active column) and kept in registers.  kLds: the class words of the
+// chunk's merge entries come from the workgroup's LDS copy (S; lane a of PB / PJ = LDS base and
+// first staged word position of active slot a), else from global memory (vt_tm).
+template <bool kLds>
+__device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* F, uint32_t qw, const uint2* S,
+                                            uint32_t PB, uint32_t PJ) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = uni(threadIdx.x >> 6);
-    const mxp_fill* F = A.fills + blockIdx.y;
     const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
     const uint64_t N = A.n;
     const uint32_t Q1 = A.q1;
-    const uint32_t qw = A.q0 + (blockIdx.x * 4u + wave) * 256u;
     if (qw >= Q1) return;
     const uint32_t q0 = qw + lane * 4u;
     const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0 && (q0 & 3u) == 0;
@@ -1137,16 +1154,27 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A)
             const uint32_t ent = i < 64u ? __builtin_amdgcn_readlane(GE0, i)
                                  : i < 128u ? __builtin_amdgcn_readlane(GE1, i - 64u) : uni(A.gvt[e0 + i]);
             const uint32_t a = ent >> 24, j = ent & 0xFFFFFFu;
-            const uint32_t cap = __builtin_amdgcn_readlane(MV, 2u * a), tb = __builtin_amdgcn_readlane(MV, 2u * a + 1u);
+            const uint32_t cap = __builtin_amdgcn_readlane(MV, 2u * a);
             uint64_t c = cl[0];
 #pragma unroll
             for (uint32_t x = 1; x < MXP_VT_MAX; x++) c = a == x ? cl[x] : c;
-            const uint64_t row = (uint64_t)tb + (uint64_t)j * cap;
+            if constexpr (kLds) {
+                const uint32_t row = __builtin_amdgcn_readlane(PB, a) + (j - __builtin_amdgcn_readlane(PJ, a)) * cap;
 #pragma unroll
-            for (uint32_t r = 0; r < 4; r++) {
-                const uint2 w = *(const uint2*)(A.vt_tm + 2u * (row + ((c >> (16u * r)) & 0xFFFFu)));
-                m[r] |= w.x;
-                ve[r] |= w.y;
+                for (uint32_t r = 0; r < 4; r++) {
+                    const uint2 w = S[row + ((uint32_t)(c >> (16u * r)) & 0xFFFFu)];
+                    m[r] |= w.x;
+                    ve[r] |= w.y;
+                }
+            } else {
+                const uint32_t tb = __builtin_amdgcn_readlane(MV, 2u * a + 1u);
+                const uint64_t row = (uint64_t)tb + (uint64_t)j * cap;
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++) {
+                    const uint2 w = *(const uint2*)(A.vt_tm + 2u * (row + ((c >> (16u * r)) & 0xFFFFu)));
+                    m[r] |= w.x;
+                    ve[r] |= w.y;
+                }
             }
         }
         uint32_t vmask[4];
@@ -1184,6 +1212,63 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A)
                 if (A.out_err) A.out_err[at + r] = e[r];
             }
         }
+    }
+}
+
+// MXP_DEBUG_FLAGS 2097152: every chunk gathers class words from global memory (A/B)
+extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A) {
+    const uint32_t wave = uni(threadIdx.x >> 6);
+    vtfill_wave<false>(A, A.fills + blockIdx.y, A.q0 + (blockIdx.x * 4u + wave) * 256u, nullptr, 0u, 0u);
+}
+
+// The default: a workgroup stages its chunk's class-word rows in LDS once -- per active slot a, the
+// contiguous rows of the word positions the chunk's merge entries name (slot a's positions grow
+// with the group) -- then covers MXP_VTF_TILES tiles of 1024 requests (4 waves x 256) gathering
+// from LDS instead of L1/L2 (C4: ~60 entries x 4 gathers per request and chunk).  A chunk whose
+// rows exceed the 32 KB budget gathers from global memory.  93 VGPRs, 32 KB: 5 workgroups per CU.
+#define MXP_VTF_STAGE 4096u
+#define MXP_VTF_TILES 4u
+extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_kargs A) {
+    __shared__ uint2 S[MXP_VTF_STAGE];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
+    const mxp_fill* F = A.fills + blockIdx.y;
+    const uint32_t g0 = uni(F->g0), n = uni(F->n), nvt = uni(A.n_vt);
+    // staging plan, computed alike by every wave: per slot a its [jlo, jhi] over the chunk's entries
+    const uint32_t e0 = uni(A.gvt_off[g0]), ecount = uni(A.gvt_off[g0 + n]) - e0;
+    const uint32_t E0 = lane < ecount ? A.gvt[e0 + lane] : 0xFFFFFFFFu;
+    const uint32_t E1 = lane + 64u < ecount ? A.gvt[e0 + 64u + lane] : 0xFFFFFFFFu;
+    const uint32_t capl = lane < nvt ? A.vt_meta[lane * 8u + MXP_VTM_CAP] : 0u;
+    const uint32_t tbl = lane < nvt ? A.vt_meta[lane * 8u + MXP_VTM_TBASE] : 0u;
+    uint32_t PB = 0, PJ = 0, total = 0;
+    for (uint32_t a = 0; a < nvt; a++) {
+        const uint32_t lo = wave_min(min((E0 >> 24) == a ? (E0 & 0xFFFFFFu) : 0xFFFFFFFFu,
+                                         (E1 >> 24) == a ? (E1 & 0xFFFFFFu) : 0xFFFFFFFFu));
+        const uint32_t hi = wave_max(max((E0 >> 24) == a && E0 != 0xFFFFFFFFu ? (E0 & 0xFFFFFFu) + 1u : 0u,
+                                         (E1 >> 24) == a && E1 != 0xFFFFFFFFu ? (E1 & 0xFFFFFFu) + 1u : 0u));
+        const uint32_t rows = hi > lo ? hi - lo : 0u;
+        if (lane == a) {
+            PB = total;
+            PJ = rows ? lo : 0u;
+        }
+        total += rows * __builtin_amdgcn_readlane(capl, a);
+    }
+    const bool staged = ecount <= 128u && total <= MXP_VTF_STAGE && !(A.flags & 2097152u);
+    if (staged) {
+        for (uint32_t a = 0; a < nvt; a++) {
+            const uint32_t base = __builtin_amdgcn_readlane(PB, a);
+            const uint32_t next = a + 1u < nvt ? __builtin_amdgcn_readlane(PB, a + 1u) : total;
+            const uint64_t src = (uint64_t)__builtin_amdgcn_readlane(tbl, a) +
+                                 (uint64_t)__builtin_amdgcn_readlane(PJ, a) * __builtin_amdgcn_readlane(capl, a);
+            for (uint32_t i = tid; i < next - base; i += 256u) S[base + i] = *(const uint2*)(A.vt_tm + 2u * (src + i));
+        }
+        __syncthreads();
+    }
+    for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
+        const uint32_t qw = A.q0 + ((blockIdx.x * MXP_VTF_TILES + t) * 4u + wave) * 256u;
+        if (staged)
+            vtfill_wave<true>(A, F, qw, S, PB, PJ);
+        else
+            vtfill_wave<false>(A, F, qw, nullptr, 0u, 0u);
     }
 }
 
@@ -1677,7 +1762,13 @@ extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, h
 }
 
 extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_vtfill_kernel, dim3((args->q1 - args->q0 + 1023u) / 1024u, n_fills), dim3(256), 0, s, *args);
+    if (args->flags & 2097152u) {
+        hipLaunchKernelGGL(mxp_vtfill_kernel, dim3((args->q1 - args->q0 + 1023u) / 1024u, n_fills), dim3(256), 0, s, *args);
+    } else {
+        const uint32_t per = 1024u * MXP_VTF_TILES;
+        hipLaunchKernelGGL(mxp_vtfill_lds_kernel, dim3((args->q1 - args->q0 + per - 1u) / per, n_fills), dim3(256), 0, s,
+                           *args);
+    }
     return hipGetLastError();
 }
 

@@ -3,7 +3,9 @@ distinct value of that column in the batch and their words gathered per request.
 against the oracle (and against the engine with value classes off), error texts included -- the
 class records the class kernel logs at a representative request are expanded to every request of
 the class (engine.cpp expand_class_errors).  MXP_DEBUG_FLAGS 262144 forces value classes at any
-batch size (the default wants >= 16 requests per class); 131072 turns them off."""
+batch size (the default wants >= 16 requests per class); 131072 turns them off; 2097152 makes the
+fill chunks gather class words from global memory instead of the LDS-staged rows
+(mxp_vtfill_kernel vs mxp_vtfill_lds_kernel)."""
 import numpy as np
 import pytest
 
@@ -13,7 +15,8 @@ from istio_amd.bags import BagBatch
 from test_gpu_parity import compare
 
 pytestmark = pytest.mark.gpu
-FORCE, OFF = "262144", "131072"
+FORCE, OFF, GLOBAL = "262144", "131072", "2097152"
+FORCE_GLOBAL = str(262144 | 2097152)
 
 
 @pytest.fixture(scope="module")
@@ -30,7 +33,7 @@ def engine_for(mxp, monkeypatch, flags, manifest, rules):
     return eng
 
 
-@pytest.mark.parametrize("flags", [FORCE, "0"])
+@pytest.mark.parametrize("flags", [FORCE, "0", FORCE_GLOBAL])
 def test_c4_value_classes_parity(mxp, monkeypatch, flags):
     """C4 routes: the header rules (equality and regexps on request.headers["h"]) become value
     classes (17 values per header); path rules stay with the prefix index."""
@@ -60,11 +63,13 @@ def test_guarded_fuzz_value_classes(mxp, monkeypatch):
 
 
 def test_value_classes_on_off_identical_with_hits(mxp, monkeypatch):
-    """Device path (bitmaps + fused / streamed hit counters): value classes on and off agree."""
+    """Device path (bitmaps + fused / streamed hit counters): value classes on (class words from
+    LDS-staged rows, or gathered from global memory) and off agree; a ragged batch ends inside a
+    staged workgroup's tiles."""
     import torch
     manifest, rules, batch = W.c4_workload(n_rules=2000, n_requests=50_000 + 5, seed=45)
     out = []
-    for flags in (FORCE, OFF):
+    for flags in (FORCE, FORCE_GLOBAL, OFF):
         eng = engine_for(mxp, monkeypatch, flags, manifest, rules)
         db = eng.upload(batch)
         Wd = (len(rules) + 31) // 32
@@ -76,15 +81,17 @@ def test_value_classes_on_off_identical_with_hits(mxp, monkeypatch):
         torch.cuda.synchronize()
         out.append((dm.cpu().numpy(), de.cpu().numpy(), hits.cpu().numpy()))
         db.free()
-    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
-    assert np.array_equal(out[0][2], out[1][2]) and out[0][2].sum() > 0
+    for o in out[1:]:
+        assert np.array_equal(out[0][0], o[0]) and np.array_equal(out[0][1], o[1])
+        assert np.array_equal(out[0][2], o[2])
+    assert out[0][2].sum() > 0
 
 
 def test_resolver_with_value_classes(mxp, monkeypatch):
     """mxp_resolve_batch with value classes forced equals the run without them (selected rules,
     statuses, first-error rules and their texts)."""
     res = []
-    for flags in (FORCE, OFF):
+    for flags in (FORCE, FORCE_GLOBAL, OFF):
         manifest, rules, conf, batch = W.resolver_workload(n_rules=500, n_requests=2000, seed=65)
         eng = engine_for(mxp, monkeypatch, flags, manifest, rules)
         eng.set_resolver(**conf)
