@@ -53,6 +53,36 @@ def compare(engine, ev, rules, batch, sample_msgs=400, seed=0):
     return got, want
 
 
+def test_golden_double_session_on_gpu(mxp):
+    """compiler_test.go:87-136 (TestCompiler_DoubleExpressionSession): every golden expression
+    compiled twice into one rule set; on the GPU both copies give the same code, value and error
+    text on their row's bag as the single compile."""
+    for conf in ("defaultAttrs", "exprEvalAttrs"):
+        rows = [r for r in ROWS["rows"] if r.get("E") and r.get("conf", "defaultAttrs") == conf
+                and "CompileErr" not in r and "Externs" not in r]
+        batch = BagBatch.from_bags([{k: from_tagged(v) for k, v in r.get("I", {}).items()} for r in rows])
+        single = mxp.Engine(0)
+        single.set_vocabulary(ROWS["manifests"][conf])
+        single.compile([r["E"] for r in rows])
+        sv, sc = single.eval_values(batch)
+        eng = mxp.Engine(0)
+        eng.set_vocabulary(ROWS["manifests"][conf])
+        st = eng.compile([r["E"] for r in rows for _ in (0, 1)])
+        assert (st == 0).all()
+        vals, codes = eng.eval_values(batch)
+        pm, pe = eng.eval_batch(batch)
+        pcodes = mxp.bits_to_codes(pm, pe, 2 * len(rows))
+        for i, r in enumerate(rows):
+            a, b = 2 * i, 2 * i + 1
+            assert codes[i, a] == codes[i, b] == sc[i, i], r["E"]
+            assert pcodes[i, a] == pcodes[i, b], r["E"]
+            if codes[i, a] >= 2:
+                assert eng.pair_error(i, a) == eng.pair_error(i, b) == single.pair_error(i, i), r["E"]
+            else:
+                assert eng.value_text(a, vals[i, a]) == eng.value_text(b, vals[i, b]) == \
+                    single.value_text(i, sv[i, i]), r["E"]
+
+
 def test_golden_table_on_gpu(mxp):
     """Every golden row (mixer/pkg/il/testing/tests.go) evaluated by the GPU engine."""
     from test_oracle_golden import same_value

@@ -70,3 +70,33 @@ def test_matches_oracle_codegen(Engine, which):
     # every generated rule without a regexp lowers to the GPU bytecode
     unsupported = [rules[i] for i in np.where(st == 5)[0]]
     assert not unsupported, unsupported[:3]
+
+
+def test_compiler_sessions(Engine):
+    """compiler_test.go:30-136 runs every tests.go expression through a compile *session*: once
+    (TestCompiler_SingleExpressionSession, IL as Compile writes it) and twice into the same program
+    (TestCompiler_DoubleExpressionSession, both functions evaluate alike).  The engine's session is a
+    rule set: every expression of the golden table compiled twice in ONE rule set, beside the other
+    rows, keeps its own IL, its own compile error text, and identical statuses for both copies."""
+    by_conf = {}
+    for row in ROWS["rows"]:
+        if row.get("E") and "Fns" not in row:
+            by_conf.setdefault(row.get("conf", "defaultAttrs"), []).append(row)
+    checked = 0
+    for conf, rows in by_conf.items():
+        e = Engine(-1)
+        e.set_vocabulary(ROWS["manifests"][conf])
+        exprs = [r["E"] for r in rows for _ in (0, 1)]  # each expression twice, in table order
+        st = e.compile(exprs)
+        for k, row in enumerate(rows):
+            a, b = 2 * k, 2 * k + 1
+            assert st[a] == st[b], row["E"]
+            if "CompileErr" in row:
+                assert st[a] != 0 and e.rule_error(a) == e.rule_error(b) == row["CompileErr"], row["E"]
+                continue
+            assert st[a] == 0, (row["E"], e.rule_error(a))
+            assert e.rule_il_text(a) == e.rule_il_text(b)
+            if "IL" in row:
+                assert e.rule_il_text(a).strip() == row["IL"].strip(), row["E"]
+            checked += 1
+    assert checked > 150
