@@ -1329,6 +1329,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     mxp_kargs A;
     fill_args(&A, db, *P);
     A.req_err = req_err_out;
+    A.hits_gate = hits_gate_out;
     A.hits = d_vals ? nullptr : d_hits;
     A.stats = d_vals ? nullptr : stats;
     A.out_match = d_match;
@@ -1642,7 +1643,6 @@ void mxp_engine_destroy(mxp_engine* eng) {
     if (eng->side) (void)hipStreamDestroy(eng->side);
     if (eng->stats_ev) (void)hipEventSynchronize(eng->stats_ev);
     if (eng->stats_ev) (void)hipEventDestroy(eng->stats_ev);
-    if (eng->h_stats) (void)hipHostFree(eng->h_stats);
     delete eng;
 }
 
@@ -1820,46 +1820,42 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
         eng->req_err_out = nullptr;
         return rc;
     }
-    if (!eng->h_stats) {
+    if (!eng->stats_ev) {
         if ((e = eng->d_stats.alloc(8)) != hipSuccess) return eng->hipfail(e, "stats");
-        if ((e = hipHostMalloc((void**)&eng->h_stats, 8, hipHostMallocDefault)) != hipSuccess) {
-            eng->h_stats = nullptr;
-            return eng->hipfail(e, "stats host");
-        }
-        *eng->h_stats = 0;
+        if ((e = eng->d_gate.alloc(4)) != hipSuccess) return eng->hipfail(e, "hits gate");
+        // no evaluation yet: stream the bitmap (a fused first evaluation of a rule set with many true
+        // pairs would pay one atomic per pair: C4's first evaluations took 6.5 ms instead of 1.9)
+        if ((e = hipMemsetAsync(eng->d_gate.p, 0, 4, s)) != hipSuccess) return eng->hipfail(e, "hits gate");
         if ((e = hipEventCreateWithFlags(&eng->stats_ev, hipEventDisableTiming)) != hipSuccess) {
             eng->stats_ev = nullptr;
             return eng->hipfail(e, "stats event");
         }
     }
-    // Counting in the kernels costs one atomic per true pair the index kernel sets; re-reading the
-    // match bitmap costs its W x N x 4 bytes (~ a true pair per 125 bitmap words at the measured
-    // atomic and streaming rates): choose by the true pairs per request of the latest evaluation
-    // whose stats download has COMPLETED (event query, no wait; else the previous rate stands).
+    // Fused vs streamed counters are chosen on the device (mxp_hits_gate_kernel after each
+    // evaluation sets the next one's gate from its true pairs per request): no host round trip and no
+    // stale decision when evaluations are queued back to back.
     const uint32_t R = (uint32_t)eng->rules.size(), W = (R + 31) / 32;
-    if (eng->stats_pending && hipEventQuery(eng->stats_ev) == hipSuccess) {
-        eng->stats_tp = eng->stats_n ? (double)*eng->h_stats / eng->stats_n : 0.0;
-        eng->stats_pending = false;
-    }
-    // (value-class rules are counted per class -- class size x class word, mxp_vt_eval_kernel --
-    // so the index kernel's true pairs alone price the fused counters)
-    const bool fused = (eng->stats_tp * 125.0 <= (double)W && !(eng->debug_flags & 1048576u)) ||
-                       (eng->debug_flags & 524288u);
-    // the reset follows the previous download even when the caller switched streams
+    const uint32_t force = (eng->debug_flags & 524288u) ? 1u : (eng->debug_flags & 1048576u) ? 2u : 0u;
+    // (ordered after the previous evaluation's gate update even when the caller switched streams)
     if (eng->stats_pending && (e = hipStreamWaitEvent(s, eng->stats_ev, 0)) != hipSuccess)
         return eng->hipfail(e, "stats wait");
+    if (force && (e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), 0, W, eng->d_gate.as<uint32_t>(),
+                                           force, s)) != hipSuccess)
+        return eng->hipfail(e, "hits gate");
     if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
     eng->req_err_out = d_req_err;
-    int rc = eng->launch(db, s, d_match, d_err, nullptr, false, fused ? d_hits : nullptr, eng->d_stats.as<uint64_t>());
+    eng->hits_gate_out = eng->d_gate.as<uint32_t>();
+    int rc = eng->launch(db, s, d_match, d_err, nullptr, false, d_hits, eng->d_stats.as<uint64_t>());
     eng->req_err_out = nullptr;
+    eng->hits_gate_out = nullptr;
     if (rc) return rc;
-    if (!fused && R && db->n && (e = mxp_launch_hits(d_match, db->n, R, W, d_hits, s)) != hipSuccess)
+    if (R && db->n && (e = mxp_launch_hits(d_match, db->n, R, W, d_hits, s, eng->d_gate.as<uint32_t>())) != hipSuccess)
         return eng->hipfail(e, "launch hits");
-    if ((e = hipMemcpyAsync(eng->h_stats, eng->d_stats.p, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
-        return eng->hipfail(e, "stats download");
+    if ((e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), db->n, W, eng->d_gate.as<uint32_t>(), force,
+                                  s)) != hipSuccess)
+        return eng->hipfail(e, "hits gate");
     if ((e = hipEventRecord(eng->stats_ev, s)) != hipSuccess) return eng->hipfail(e, "stats event");
     eng->stats_pending = true;
-    eng->stats_n = db->n;
     return MXP_OK;
 }
 

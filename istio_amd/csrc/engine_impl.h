@@ -32,7 +32,9 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
 extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t s);
 extern "C" hipError_t mxp_launch_vt_eval(const mxp_kargs* args, uint32_t tiles, uint32_t wchunks, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
-                                      unsigned long long* hits, hipStream_t s);
+                                      unsigned long long* hits, hipStream_t s, const uint32_t* gate = nullptr);
+extern "C" hipError_t mxp_launch_hits_gate(const unsigned long long* stats, uint32_t n, uint32_t n_words,
+                                           uint32_t* gate, uint32_t force, hipStream_t s);
 
 
 struct DevBuf {
@@ -513,6 +515,8 @@ struct mxp_engine : public mxp::LowerTables {
     int vt_prepare(mxp_dbatch* db, const Plan& P);
     uint32_t last_mask = 0;  // value-class slots of the last launch
     uint8_t* req_err_out = nullptr;  // compact error output of the next launch (kargs.req_err)
+    const uint32_t* hits_gate_out = nullptr;  // fused-counter gate of the next launch (kargs.hits_gate)
+    DevBuf d_gate;                   // u32: fused counters on for the next evaluation (mxp_hits_gate_kernel)
     bool wave_times = false;  // MXP_WAVE_TIMES: index kernel waves record {start, end, XCC}
     DevBuf d_wave_t;
     uint32_t wave_t_n = 0;
@@ -520,14 +524,11 @@ struct mxp_engine : public mxp::LowerTables {
     int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
                unsigned long long* d_hits = nullptr, uint64_t* d_stats = nullptr, uint32_t q_lo = 0,
                uint32_t q_hi = 0xFFFFFFFFu);
-    // fused hit counters: true pairs the guard-index kernel set in a recent evaluation (pinned host
-    // copy, read one launch late) decide between counting in the kernels and the streaming hits kernel
+    // fused hit counters: the true pairs the guard-index kernel set (d_stats) decide, on the device,
+    // between counting in the next evaluation's kernels and the streaming hits kernel (d_gate)
     DevBuf d_stats;
-    uint64_t* h_stats = nullptr;
-    uint32_t stats_n = 0;
-    hipEvent_t stats_ev = nullptr;  // recorded after each stats download
-    bool stats_pending = false;     // a download not yet seen complete
-    double stats_tp = 0.0;          // true pairs per request of the last completed download
+    hipEvent_t stats_ev = nullptr;  // recorded after each evaluation's gate update
+    bool stats_pending = false;     // an evaluation with a gate update has been queued
     // columns of a window of requests [q0, q1) of the last batch, downloaded for error texts
     struct ErrWindow {
         uint32_t q0 = 0, q1 = 0, ncol = 0;

@@ -74,6 +74,8 @@ typedef struct mxp_kargs {
     uint32_t* out_err;           // [n_words][n]
     uint64_t* out_vals;          // optional [n][n_rules] result registers (Eval)
     unsigned long long* hits;    // optional [n_rules] += true pairs of this evaluation (fused hit counters)
+    const uint32_t* hits_gate;   // with hits: the kernels count only while *hits_gate != 0 (set on the device
+                                 // from the previous evaluation's true-pair rate; else mxp_hits_kernel counts)
     uint64_t* stats;             // optional [1] += true pairs the guard-index kernel set
     mxp_err_rec* errlog;
     uint32_t* errcount;

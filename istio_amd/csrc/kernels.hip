@@ -110,11 +110,16 @@ __device__ __forceinline__ void log_err(const mxp_kargs& A, uint32_t req, uint32
 // evaluation (a rule sits in one index under one key; the composite and its equality fallback serve
 // disjoint lanes; aliases are distinct rules), so neither atomic needs its return value: no
 // round trip per true pair.
+// fused hit counters on for this evaluation (kargs.hits_gate: a uniform scalar load)
+__device__ __forceinline__ bool counting(const mxp_kargs& A) {
+    return A.hits && (!A.hits_gate || *A.hits_gate != 0u);
+}
+
 __device__ __forceinline__ void set_true1(const mxp_kargs& A, uint32_t rule, uint32_t req) {
     const uint32_t bit = 1u << (rule & 31u);
     __hip_atomic_fetch_or(A.out_match + (uint64_t)(rule >> 5) * A.n + req, bit, __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_AGENT);
-    if (A.hits) __hip_atomic_fetch_add(A.hits + rule, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (counting(A)) __hip_atomic_fetch_add(A.hits + rule, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ... and the same for the rule's aliases (indexed duplicates of its program, kargs.alias_off)
@@ -673,7 +678,7 @@ __device__ __forceinline__ void eval_groups(const mxp_kargs& A, uint64_t (*regs)
                 if (A.out_err) A.out_err[(uint64_t)g * N + req] = e;
                 if (A.req_err && e) A.req_err[req] = 1;
             }
-            if (A.hits) {
+            if (counting(A)) {
                 // fused hit counters: per rule of the group, the lanes whose match bit is set
                 const uint32_t mc = valid ? m_own : 0u;
                 for (uint32_t bits = wave_or(mc); bits; bits &= bits - 1) {
@@ -812,7 +817,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_guard2_kernel(mxp_kargs A)
                 if (A.out_err) A.out_err[(uint64_t)g * N + reqb] = eb;
                 if (A.req_err && eb) A.req_err[reqb] = 1;
             }
-            if (A.hits) {
+            if (counting(A)) {
                 const uint32_t m2a = va ? ma : 0u, m2b = vb ? mb : 0u;
                 for (uint32_t bits = wave_or(m2a | m2b); bits; bits &= bits - 1) {
                     const uint32_t k = __builtin_ctz(bits);
@@ -1068,7 +1073,7 @@ __device__ __forceinline__ void vt_eval_body(const mxp_kargs& A, uint64_t (*regs
         }
     }
     *(uint2*)(A.vt_tm + 2u * ((uint64_t)tb + (uint64_t)j * cap + k)) = make_uint2(m, e);
-    if (A.hits) {
+    if (counting(A)) {
         // fused hit counters of the value-class rules: per rule, the sizes of the classes whose
         // word holds its match bit (the merge kernels count none of these bits)
         const uint32_t c = live ? A.vt_cnt[kb + k] : 0u;
@@ -1619,7 +1624,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_inject_kernel(mxp_kargs A)
             const uint32_t ent = S[4 + j];  // bit | dense id << 5
             const uint32_t on = (uint32_t)(cm >> (ent >> 5)) & 1u;
             bits |= on << (ent & 31u);
-            if (A.hits) {
+            if (counting(A)) {
                 const uint32_t c = (uint32_t)__builtin_popcountll(__ballot(on != 0));
                 if (lane == 0 && c) atomicAdd(A.hits + w * 32u + (ent & 31u), (unsigned long long)c);
             }
@@ -1730,14 +1735,18 @@ __device__ __forceinline__ void hits_body(const uint32_t* __restrict__ row, uint
 
 extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t* __restrict__ match, uint32_t n,
                                                                   uint32_t n_rules,
-                                                                  unsigned long long* __restrict__ hits) {
+                                                                  unsigned long long* __restrict__ hits,
+                                                                  const uint32_t* __restrict__ gate) {
+    if (gate && *gate) return;  // the evaluation kernels counted (fused)
     hits_body<true>(match + (uint64_t)blockIdx.x * n, n, n_rules, hits);
 }
 
 // ragged n (rows not 16-byte aligned): one word per load
 extern "C" __global__ __launch_bounds__(256) void mxp_hits_ragged_kernel(const uint32_t* __restrict__ match, uint32_t n,
                                                                          uint32_t n_rules,
-                                                                         unsigned long long* __restrict__ hits) {
+                                                                         unsigned long long* __restrict__ hits,
+                                                                         const uint32_t* __restrict__ gate) {
+    if (gate && *gate) return;
     hits_body<false>(match + (uint64_t)blockIdx.x * n, n, n_rules, hits);
 }
 
@@ -1805,8 +1814,25 @@ extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hip
     return hipGetLastError();
 }
 
+// Fused or streamed hit counters, decided on the device without a host round trip: after an
+// evaluation, gate = 1 when its guard-index true pairs were few enough (stats x 125 <= words x
+// requests: one atomic per true pair costs less than re-reading the match bitmap) -- the NEXT
+// evaluation's kernels then count in place and its mxp_hits_kernel returns at once; else the kernels
+// skip counting and mxp_hits_kernel streams the bitmap.  force: 1 always fused, 2 never.
+extern "C" __global__ void mxp_hits_gate_kernel(const unsigned long long* stats, uint32_t n, uint32_t n_words,
+                                                uint32_t* gate, uint32_t force) {
+    if (threadIdx.x == 0 && blockIdx.x == 0)
+        *gate = force == 1u ? 1u : force == 2u ? 0u : (*stats * 125ull <= (unsigned long long)n_words * n ? 1u : 0u);
+}
+
+extern "C" hipError_t mxp_launch_hits_gate(const unsigned long long* stats, uint32_t n, uint32_t n_words,
+                                           uint32_t* gate, uint32_t force, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_hits_gate_kernel, dim3(1), dim3(64), 0, s, stats, n, n_words, gate, force);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
-                                      unsigned long long* hits, hipStream_t s) {
+                                      unsigned long long* hits, hipStream_t s, const uint32_t* gate) {
     // slices: enough blocks to fill the chip (~16 per CU), at least 32 words per thread, and at most
     // 255 32-word steps per thread (the byte-packed counters)
     const uint64_t per_block = 256ull * 32u;
@@ -1817,8 +1843,9 @@ extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_
     if (gy < 1) gy = 1;
     if (gy > 65535) return hipErrorInvalidValue;
     if ((n & 3u) == 0 && (((uintptr_t)match) & 15u) == 0)
-        hipLaunchKernelGGL(mxp_hits_kernel, dim3(n_words, (uint32_t)gy), dim3(256), 0, s, match, n, n_rules, hits);
+        hipLaunchKernelGGL(mxp_hits_kernel, dim3(n_words, (uint32_t)gy), dim3(256), 0, s, match, n, n_rules, hits, gate);
     else
-        hipLaunchKernelGGL(mxp_hits_ragged_kernel, dim3(n_words, (uint32_t)gy), dim3(256), 0, s, match, n, n_rules, hits);
+        hipLaunchKernelGGL(mxp_hits_ragged_kernel, dim3(n_words, (uint32_t)gy), dim3(256), 0, s, match, n, n_rules, hits,
+                           gate);
     return hipGetLastError();
 }

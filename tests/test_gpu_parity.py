@@ -318,13 +318,15 @@ def test_fill_layout_knobs_parity(mxp, knobs, n, monkeypatch):
 
 
 @pytest.mark.parametrize("family", ["c2", "fuzz", "c4"])
-@pytest.mark.parametrize("flags", ["0", "524288", "786432"])  # auto; fused forced; fused + value classes forced
-def test_fused_hit_counters(mxp, family, flags, monkeypatch):
+@pytest.mark.parametrize("flags,sync", [("0", True), ("0", False), ("524288", True), ("786432", True),
+                                        ("1048576", False)])  # auto; fused forced; + value classes; streaming
+def test_fused_hit_counters(mxp, family, flags, sync, monkeypatch):
     """mxp_batch_eval_device_hits: counters accumulated by the evaluation kernels (fill / guard / VM
     kernels by ballot, index kernel per newly set bit) -- or, after an evaluation dense in true pairs
     (C4), by the streaming hits kernel; value-class rules per class (class size x class word) -- equal
     the true pairs of the bitmaps over three evaluations, and the bitmaps equal the plain device
-    evaluation's."""
+    evaluation's.  The choice is made on the device from the previous evaluation (mxp_hits_gate_kernel),
+    so evaluations queued back to back without a host synchronisation (sync False) count alike."""
     import torch
     monkeypatch.setenv("MXP_DEBUG_FLAGS", flags)
     if family == "c2":
@@ -347,7 +349,8 @@ def test_fused_hit_counters(mxp, family, flags, monkeypatch):
     s = torch.cuda.current_stream().cuda_stream
     for _ in range(3):
         db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s)
-        torch.cuda.synchronize()
+        if sync:
+            torch.cuda.synchronize()
     db.eval(dm2.data_ptr(), de2.data_ptr(), s)
     torch.cuda.synchronize()
     m = dm.cpu().numpy().view(np.uint32)
