@@ -955,7 +955,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
     __shared__ uint32_t lcls[MXP_VTC_LCAP];
     __shared__ uint32_t lrep[MXP_VTC_LCAP];
     __shared__ uint32_t lcnt[MXP_VTC_LCAP];  // requests per local slot (class sizes, with A.hits)
-    const bool count = A.hits != nullptr;
+    const bool count = counting(A);  // class sizes feed mxp_vt_eval_kernel's fused counters
     const uint32_t tid = threadIdx.x;
     const uint64_t N = A.n;
     const uint32_t base = A.q0 + blockIdx.x * MXP_VTC_REQ;
