@@ -29,6 +29,8 @@ extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hip
 extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
 extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
+extern "C" hipError_t mxp_launch_dtp_sort(const mxp_kargs* args, hipStream_t s);
+extern "C" hipError_t mxp_launch_dtp_apply(const mxp_kargs* args, hipStream_t s);
 extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t s);
 extern "C" hipError_t mxp_launch_vt_eval(const mxp_kargs* args, uint32_t tiles, uint32_t wchunks, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
@@ -223,6 +225,11 @@ struct mxp_engine : public mxp::LowerTables {
         std::vector<uint32_t> vt_cols, vt_nw;
         uint32_t vt_max_nw = 0;
         DevBuf d_gvt_off, d_gvt, d_vt_woff, d_vt_words;
+        // deferred index pairs (kargs.dtp_*): possible when every group holding an indexed rule is
+        // written by the value-class fill (no plain fill chunks, no dense rules); per group its fill
+        // chunk << 8 | position in the chunk
+        bool dtp_ok = false;
+        DevBuf d_dtp_chunk;
     };
     std::map<uint32_t, std::unique_ptr<Plan>> plans;
     int get_plan(uint32_t mask, Plan** out);
@@ -283,6 +290,12 @@ struct mxp_engine : public mxp::LowerTables {
     // length).  Same-box A/B (profiles/r2_v7_ab_sparse_*.log), ms per evaluation for 0 / 1 / 2 / 3:
     // C4 2.216 / 2.188 / 2.178 / 2.178, C2 0.576 / 0.573 / 0.566 / 0.562
     uint32_t index_sparsity = 2;
+    // Deferred index pairs (launch, kernels.hip mxp_dtp_*; MXP_DTP=0 turns them off): per index wave
+    // room for dtp_cap pairs, then an overflow list of dtp_ovf_cap (MXP_DTP_CAP / MXP_DTP_OVF: tests)
+    bool dtp = true;
+    uint32_t dtp_cap = 2048, dtp_ovf_cap = 1u << 22;
+    DevBuf d_dtp_ent, d_dtp_n, d_dtp_ovf, d_dtp_ovf_n, d_dtp_slots, d_dtp_qn;
+    bool last_dtp = false;  // the last launch deferred its index pairs (mxp_kernel_times [2])
     // MXP_TRACE=1: phase times of evaluations / Resolves on stderr (each phase synchronises the
     // stream first, so traced calls are slower than untraced ones)
     bool trace = false;

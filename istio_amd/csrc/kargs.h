@@ -99,4 +99,17 @@ typedef struct mxp_kargs {
     uint32_t nfa;                // some regexp of the rule set or batch is a bit-parallel NFA: the *_nfa kernels
     unsigned long long* wave_t;  // profiling (MXP_WAVE_TIMES): index kernel waves' {start, end, pairs}
     uint8_t* req_err;            // optional [n]: 1 when some rule fails for the request (compact error output)
+    // Deferred true pairs (kernels.hip "Deferred pairs"; null dtp_ent / dtp_off: off).  The index
+    // kernel runs before the value-class fill and records its true / error pairs per wave instead of
+    // OR-ing them into rows nobody has written yet; mxp_dtp_sort_kernel files them by (fill chunk,
+    // lane quad); the fill ORs them into the words it streams out.
+    uint32_t* dtp_ent;           // index kernel: [waves][dtp_cap] rule | plane << 23 | lane << 24
+    uint32_t* dtp_n;             // [waves] entries recorded (<= dtp_cap)
+    uint32_t* dtp_ovf_n;         // [2]: overflow pairs, overflow list full (-> the gated index re-run)
+    uint32_t* dtp_ovf;           // [dtp_ovf_cap][2] (request, rule | plane << 31) past a wave's dtp_cap
+    const uint32_t* dtp_chunk;   // [n_words] value-class fill chunk << 8 | group within it (~0: none)
+    uint16_t* dtp_slots;         // [chunks][tiles * 256 lane quads][8] g << 8 | plane << 7 | request % 4 << 5 | bit
+    uint8_t* dtp_qn;             // [chunks][tiles * 256] entries in each quad's slots (<= 8)
+    const uint32_t* dtp_gate;    // index re-run with OR-ed pairs: returns unless *dtp_gate (list full)
+    uint32_t dtp_cap, dtp_ovf_cap, dtp_tiles, dtp_nchunks;
 } mxp_kargs;

@@ -115,8 +115,34 @@ __device__ __forceinline__ bool counting(const mxp_kargs& A) {
     return A.hits && (!A.hits_gate || *A.hits_gate != 0u);
 }
 
+// Deferred pairs (kargs.dtp_ent): the index kernel runs before the value-class fill, so a true or
+// error pair is recorded in its wave's list (LDS counter; the wave of request q is q / 64, and every
+// pair of q is produced by that wave) and OR-ed in by the fill as it streams the words out.  Pairs
+// past a wave's dtp_cap go to the overflow list (OR-ed in after the fill by mxp_dtp_apply_kernel);
+// past that list's capacity a flag re-runs the index kernel with plain OR-s after the fill.
+__shared__ uint32_t g_dtpn[4];  // entries per wave of the index kernel's workgroup
+__device__ __forceinline__ void dtp_push(const mxp_kargs& A, uint32_t rule, uint32_t req, uint32_t plane) {
+    const uint32_t slot = atomicAdd(&g_dtpn[threadIdx.x >> 6], 1u);
+    if (slot < A.dtp_cap) {
+        A.dtp_ent[(uint64_t)(req >> 6) * A.dtp_cap + slot] = rule | (plane << 23) | ((req & 63u) << 24);
+        return;
+    }
+    const uint32_t o = atomicAdd(&A.dtp_ovf_n[0], 1u);
+    if (o < A.dtp_ovf_cap) {
+        A.dtp_ovf[2ull * o] = req;
+        A.dtp_ovf[2ull * o + 1] = rule | (plane << 31);
+    } else {
+        __hip_atomic_store(&A.dtp_ovf_n[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 __device__ __forceinline__ void set_true1(const mxp_kargs& A, uint32_t rule, uint32_t req) {
     const uint32_t bit = 1u << (rule & 31u);
+    if (A.dtp_ent) {
+        dtp_push(A, rule, req, 0u);
+        if (counting(A)) __hip_atomic_fetch_add(A.hits + rule, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     __hip_atomic_fetch_or(A.out_match + (uint64_t)(rule >> 5) * A.n + req, bit, __ATOMIC_RELAXED,
                           __HIP_MEMORY_SCOPE_AGENT);
     if (counting(A)) __hip_atomic_fetch_add(A.hits + rule, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -137,6 +163,12 @@ __device__ __forceinline__ uint32_t set_true(const mxp_kargs& A, uint32_t rule, 
 __device__ __forceinline__ void set_error(const mxp_kargs& A, uint32_t rule, uint32_t req) {
     if (A.req_err) A.req_err[req] = 1;
     if (!A.out_err) return;
+    if (A.dtp_ent) {
+        dtp_push(A, rule, req, 1u);
+        if (A.alias_off)
+            for (uint32_t j = A.alias_off[rule]; j < A.alias_off[rule + 1]; j++) dtp_push(A, A.aliases[j], req, 1u);
+        return;
+    }
     atomicOr(A.out_err + (uint64_t)(rule >> 5) * A.n + req, 1u << (rule & 31u));
     if (A.alias_off)
         for (uint32_t j = A.alias_off[rule]; j < A.alias_off[rule + 1]; j++) {
@@ -1103,9 +1135,34 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_eval_nfa_kernel(mxp_kar
 // are loaded once (4 x u16 per active column) and kept in registers.  kLds: the class words of the
 // chunk's merge entries come from the workgroup's LDS copy (S; lane a of PB / PJ = LDS base and
 // first staged word position of active slot a), else from global memory (vt_tm).
+// ascending sort of 8 values (Batcher's odd-even merge network, 19 compare-exchanges)
+__device__ __forceinline__ void sort8(uint32_t (&x)[8]) {
+#define MXP_CX(a, b)                          \
+    {                                         \
+        const uint32_t lo = min(x[a], x[b]);  \
+        x[b] = max(x[a], x[b]);               \
+        x[a] = lo;                            \
+    }
+    MXP_CX(0, 1) MXP_CX(2, 3) MXP_CX(4, 5) MXP_CX(6, 7) MXP_CX(0, 2) MXP_CX(1, 3) MXP_CX(4, 6) MXP_CX(5, 7)
+    MXP_CX(1, 2) MXP_CX(5, 6) MXP_CX(0, 4) MXP_CX(1, 5) MXP_CX(2, 6) MXP_CX(3, 7) MXP_CX(2, 4) MXP_CX(3, 5)
+    MXP_CX(1, 2) MXP_CX(3, 4) MXP_CX(5, 6)
+#undef MXP_CX
+}
+
+// one sorted deferred pair x (g << 8 | plane << 7 | request % 4 << 5 | bit) into the lane's words
+__device__ __forceinline__ void dtp_merge(uint32_t x, bool on, uint32_t (&m)[4], uint32_t (&e)[4]) {
+    const uint32_t b = on ? 1u << (x & 31u) : 0u, r = (x >> 5) & 3u;
+    const uint32_t bm = (x & 128u) ? 0u : b, be = (x & 128u) ? b : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        m[k] |= r == k ? bm : 0u;
+        e[k] |= r == k ? be : 0u;
+    }
+}
+
 template <bool kLds>
-__device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* F, uint32_t qw, const uint2* S,
-                                            uint32_t PB, uint32_t PJ) {
+__device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* F, uint32_t chunk, uint32_t qw,
+                                            const uint2* S, uint32_t PB, uint32_t PJ) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
     const uint64_t N = A.n;
@@ -1136,6 +1193,28 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
         }
     }
     const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
+    // deferred index pairs of the lane's 4 requests in this chunk (mxp_dtp_sort_kernel): up to 8 u16
+    // entries, sorted here (group first) into a queue in four registers whose head the group loop
+    // consumes while it names the current group
+    uint32_t dq0 = ~0u, dq1 = ~0u, dq2 = ~0u, dq3 = ~0u;
+    if (A.dtp_slots && q0 < Q1) {
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const uint64_t qi = (uint64_t)chunk * A.dtp_tiles * 256u + (q0 >> 2);
+        const uint32_t dk = A.dtp_qn[qi];
+        const v4u sl = *(const v4u*)(A.dtp_slots + qi * 8u);
+        if (dk) {
+            const uint32_t h[4] = {sl.x, sl.y, sl.z, sl.w};
+            uint32_t x[8];
+#pragma unroll
+            for (uint32_t i = 0; i < 8; i++) x[i] = i < dk ? (h[i >> 1] >> (16u * (i & 1u))) & 0xFFFFu : 0xFFFFu;
+            sort8(x);
+            dq0 = x[0] | x[1] << 16;
+            dq1 = x[2] | x[3] << 16;
+            dq2 = x[4] | x[5] << 16;
+            dq3 = x[6] | x[7] << 16;
+        }
+    }
+    const bool dany = __ballot(dq0 != ~0u) != 0;
     const bool nt = !(A.flags & 128u);
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     // the active slots' (cap, tbase), the chunk's group masks and merge entries: one vector load
@@ -1194,6 +1273,20 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
             for (int r = 0; r < 4; r++) c += (uint32_t)__builtin_popcount(ve[r] & vmask[r]);
             vt_count_n(A, c);
         }
+        if (dany) {  // the index kernel's true / error pairs in this group's words
+            for (;;) {
+                const uint32_t x = dq0 & 0xFFFFu;
+                const bool hit = (x >> 8) == g;  // (pads, 0xFFFF, name no group)
+                if (!__ballot(hit)) break;
+                dtp_merge(x, hit, m, e);
+                if (hit) {
+                    dq0 = __builtin_amdgcn_alignbit(dq1, dq0, 16);
+                    dq1 = __builtin_amdgcn_alignbit(dq2, dq1, 16);
+                    dq2 = __builtin_amdgcn_alignbit(dq3, dq2, 16);
+                    dq3 = dq3 >> 16 | 0xFFFF0000u;
+                }
+            }
+        }
         // (no hit counting: a uniform group's words hold no true bit but the value classes', which
         // mxp_vt_eval_kernel counts per class)
         if (A.req_err)
@@ -1223,7 +1316,7 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
 // MXP_DEBUG_FLAGS 2097152: every chunk gathers class words from global memory (A/B)
 extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A) {
     const uint32_t wave = uni(threadIdx.x >> 6);
-    vtfill_wave<false>(A, A.fills + blockIdx.y, A.q0 + (blockIdx.x * 4u + wave) * 256u, nullptr, 0u, 0u);
+    vtfill_wave<false>(A, A.fills + blockIdx.y, blockIdx.y, A.q0 + (blockIdx.x * 4u + wave) * 256u, nullptr, 0u, 0u);
 }
 
 // The default: a workgroup stages its chunk's class-word rows in LDS once -- per active slot a, the
@@ -1233,7 +1326,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A)
 // rows exceed the 32 KB budget gathers from global memory.  93 VGPRs, 32 KB: 5 workgroups per CU.
 #define MXP_VTF_STAGE 4096u
 #define MXP_VTF_TILES 4u
-extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_kargs A) {
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_vtfill_lds_kernel(mxp_kargs A) {
     __shared__ uint2 S[MXP_VTF_STAGE];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
     const mxp_fill* F = A.fills + blockIdx.y;
@@ -1271,9 +1364,88 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
     for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
         const uint32_t qw = A.q0 + ((blockIdx.x * MXP_VTF_TILES + t) * 4u + wave) * 256u;
         if (staged)
-            vtfill_wave<true>(A, F, qw, S, PB, PJ);
+            vtfill_wave<true>(A, F, blockIdx.y, qw, S, PB, PJ);
         else
-            vtfill_wave<false>(A, F, qw, nullptr, 0u, 0u);
+            vtfill_wave<false>(A, F, blockIdx.y, qw, nullptr, 0u, 0u);
+    }
+}
+
+// Deferred pairs, filed for the fill (kargs.dtp_*).  One workgroup per tile of 1024 requests (16
+// index waves) files the tile's recorded pairs by (value-class fill chunk, lane quad = request / 4)
+// into 8 u16 slots per quad (counts in LDS, MXP_DTP_WIN chunks at a time); a quad's pairs past 8
+// are staged in LDS and appended to the overflow list with one global atomic per workgroup.
+#define MXP_DTP_WIN 32u
+#define MXP_DTP_OVQ 512u
+extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs A) {
+    __shared__ uint32_t cnt[MXP_DTP_WIN * 256u];
+    __shared__ uint32_t ovq[MXP_DTP_OVQ][2];
+    __shared__ uint32_t ovn, ovbase;
+    const uint32_t tid = threadIdx.x, t = blockIdx.x;
+    const uint32_t nwaves = (A.n + 63u) / 64u, w0 = t * 16u;
+    const uint32_t nw = min(16u, nwaves - w0);
+    const uint64_t nq = (uint64_t)A.dtp_tiles * 256u;  // quads per chunk row
+    for (uint32_t cw0 = 0; cw0 < A.dtp_nchunks; cw0 += MXP_DTP_WIN) {
+        const uint32_t cwn = min(MXP_DTP_WIN, A.dtp_nchunks - cw0);
+        for (uint32_t i = tid; i < cwn * 256u; i += 256u) cnt[i] = 0u;
+        if (tid == 0) ovn = 0u;
+        __syncthreads();
+        for (uint32_t w = 0; w < nw; w++) {
+            const uint32_t n = uni(A.dtp_n[w0 + w]);
+            const uint32_t* E = A.dtp_ent + (uint64_t)(w0 + w) * A.dtp_cap;
+            for (uint32_t i = tid; i < n; i += 256u) {
+                const uint32_t e = E[i];
+                const uint32_t rule = e & 0x7FFFFFu, ch = A.dtp_chunk[rule >> 5];
+                const uint32_t c = (ch >> 8) - cw0, ql = w * 64u + (e >> 24);
+                if (c >= cwn) continue;
+                const uint32_t at = atomicAdd(&cnt[c * 256u + (ql >> 2)], 1u);
+                if (at < 8u) {
+                    A.dtp_slots[((uint64_t)(cw0 + c) * nq + t * 256u + (ql >> 2)) * 8u + at] =
+                        (uint16_t)(((ch & 0xFFu) << 8) | (((e >> 23) & 1u) << 7) | ((ql & 3u) << 5) | (e & 31u));
+                    continue;
+                }
+                const uint32_t o = atomicAdd(&ovn, 1u);
+                const uint32_t rr = rule | (((e >> 23) & 1u) << 31);
+                if (o < MXP_DTP_OVQ) {
+                    ovq[o][0] = t * 1024u + ql;
+                    ovq[o][1] = rr;
+                } else {  // (the LDS stage is full: straight to the list)
+                    const uint32_t g = atomicAdd(&A.dtp_ovf_n[0], 1u);
+                    if (g < A.dtp_ovf_cap) {
+                        A.dtp_ovf[2ull * g] = t * 1024u + ql;
+                        A.dtp_ovf[2ull * g + 1] = rr;
+                    } else {
+                        __hip_atomic_store(&A.dtp_ovf_n[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < cwn * 256u; i += 256u)
+            A.dtp_qn[(uint64_t)(cw0 + (i >> 8)) * nq + t * 256u + (i & 255u)] = (uint8_t)min(cnt[i], 8u);
+        const uint32_t no = min(ovn, MXP_DTP_OVQ);
+        if (tid == 0 && no) ovbase = atomicAdd(&A.dtp_ovf_n[0], no);
+        __syncthreads();
+        for (uint32_t i = tid; i < no; i += 256u) {
+            const uint32_t g = ovbase + i;
+            if (g < A.dtp_ovf_cap) {
+                A.dtp_ovf[2ull * g] = ovq[i][0];
+                A.dtp_ovf[2ull * g + 1] = ovq[i][1];
+            } else {
+                __hip_atomic_store(&A.dtp_ovf_n[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// Deferred pairs past a wave's capacity, OR-ed in after the fill
+extern "C" __global__ __launch_bounds__(256) void mxp_dtp_apply_kernel(mxp_kargs A) {
+    const uint32_t n = min(uni(A.dtp_ovf_n[0]), A.dtp_ovf_cap);
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t req = A.dtp_ovf[2ull * i], e = A.dtp_ovf[2ull * i + 1];
+        const uint32_t rule = e & 0x7FFFFFFFu;
+        uint32_t* out = (e >> 31) ? A.out_err : A.out_match;
+        atomicOr(out + (uint64_t)(rule >> 5) * A.n + req, 1u << (rule & 31u));
     }
 }
 
@@ -1452,16 +1624,17 @@ namespace {
 
 template <bool kRefs, bool kNfa = kRefs>
 __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
+    // the re-run after an overflowed deferred-pair list (kargs.dtp_gate): nothing to do unless it filled
+    if (A.dtp_gate && uni(*A.dtp_gate) == 0u) return;
     const uint64_t t_start = A.wave_t ? (uint64_t)wall_clock64() : 0ull;
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
     PairQueue Q{wave, 0u, 0u, A.q0 + (blockIdx.x * 4u + wave) * 64u};
     const uint32_t req = Q.base + (tid & 63u);
     const bool valid = req < A.q1;
-    if (A.dense_of) {
-        g_cm[wave][tid & 63u] = 0ull;
-        wave_sync_lds();
-    }
+    if (A.dense_of) g_cm[wave][tid & 63u] = 0ull;
+    if (A.dtp_ent && (tid & 63u) == 0) g_dtpn[wave] = 0u;
+    if (A.dense_of || A.dtp_ent) wave_sync_lds();
     const uint64_t N = A.n;
     // x == n_idx: a last pass with no probes that drains the pair queue
     for (uint32_t x = 0; x <= A.n_idx; x++) {
@@ -1550,6 +1723,10 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
     if (A.dense_of) {  // masks for mxp_inject_kernel
         wave_sync_lds();
         if (valid) A.dense_cm[req] = g_cm[wave][tid & 63u];
+    }
+    if (A.dtp_ent) {  // the wave's deferred-pair count for mxp_dtp_sort_kernel
+        wave_sync_lds();
+        if ((tid & 63u) == 0) A.dtp_n[Q.base >> 6] = min(g_dtpn[wave], A.dtp_cap);
     }
     if (A.stats) {
         uint32_t t = Q.ntrue;
@@ -1778,6 +1955,16 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
         hipLaunchKernelGGL(mxp_vtfill_lds_kernel, dim3((args->q1 - args->q0 + per - 1u) / per, n_fills), dim3(256), 0, s,
                            *args);
     }
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_dtp_sort(const mxp_kargs* args, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_dtp_sort_kernel, dim3(args->dtp_tiles), dim3(256), 0, s, *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_dtp_apply(const mxp_kargs* args, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_dtp_apply_kernel, dim3(64), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

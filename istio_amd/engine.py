@@ -215,11 +215,13 @@ class Engine:
     def set_timing(self, on: bool = True):
         self._check(self.lib.mxp_set_timing(self.h, int(on)), "mxp_set_timing")
 
-    def kernel_times(self):
-        """[guard/VM kernel ms, guard-index kernel ms] of the last device evaluation (timing on)."""
-        ms = (ctypes.c_float * 2)()
+    def kernel_times(self, n_values: int = 2):
+        """[guard/VM kernel ms, guard-index kernel ms] of the last device evaluation (timing on); with
+        n_values=3 also [2] = 1.0 when it deferred its index pairs (the index kernel and the pair sort
+        are then in [0], the fills in [1])."""
+        ms = (ctypes.c_float * n_values)()
         n = ctypes.c_uint32()
-        self._check(self.lib.mxp_kernel_times(self.h, ms, 2, ctypes.byref(n)), "mxp_kernel_times")
+        self._check(self.lib.mxp_kernel_times(self.h, ms, n_values, ctypes.byref(n)), "mxp_kernel_times")
         return list(ms)[: n.value]
 
     def wave_times(self, n_waves: int) -> np.ndarray:

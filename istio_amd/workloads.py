@@ -483,11 +483,14 @@ C4_MANIFEST = {"request.path": "STRING", "request.headers": "STRING_MAP", "desti
 _C4_HEADERS = ["x-user", "x-env", "x-canary", "user-agent", "x-region"]
 
 
-def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512):
+def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_frac=0.0):
     """C4: Pilot-shaped HTTP route rules in the Mixer language: 60%
     request.path.startsWith("/p..") (Pilot prefix), 20% "^...".matches(request.path) (Pilot regex:
     prefix -> ^QuoteMeta(p).*), 20% request.headers["h"] == "v" or "re".matches(request.headers["h"]).
     Requests: paths of depth 1..6 over a `vocab`-word vocabulary, 3 headers each.
+    cont_frac > 0 (tests): that fraction of the prefix rules continue with
+    `&& source.ip == ip("10.0.0.K")`, over a source.ip column absent for 30% of the requests -- the
+    guard-index kernel then finds true pairs and lookup-error pairs.
     Returns (manifest, rules, BagBatch)."""
     rng = np.random.default_rng(seed)
     words = ["w%d" % i for i in range(vocab)]
@@ -500,7 +503,10 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512):
         r = rng.random()
         p = path(int(rng.integers(1, 4)))
         if r < 0.6:
-            rules.append('request.path.startsWith("%s")' % p)
+            if cont_frac and rng.random() < cont_frac:
+                rules.append('request.path.startsWith("%s") && source.ip == ip("10.0.0.%d")' % (p, int(rng.integers(0, 4))))
+            else:
+                rules.append('request.path.startsWith("%s")' % p)
         elif r < 0.8:
             rx = "^" + p + ("(/.*)?$" if rng.random() < 0.5 else "[0-9a-z/]*")
             rules.append('"%s".matches(request.path)' % rx)
@@ -535,7 +541,14 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512):
     cols = {"request.path": (np.full(n, STRING, dtype=np.uint8), path_vals),
             "request.headers": (np.full(n, STRING_MAP, dtype=np.uint8), np.arange(n, dtype=np.uint64)),
             "destination.service": (np.full(n, STRING, dtype=np.uint8), np.full(n, svc_sid, dtype=np.uint64))}
-    return C4_MANIFEST, rules, BagBatch.from_columns(n, cols, strings, maps=(moff, mkeys, mvals))
+    manifest = C4_MANIFEST
+    if cont_frac:
+        manifest = dict(C4_MANIFEST, **{"source.ip": "IP_ADDRESS"})
+        ip0 = len(strings)
+        strings.extend(bytes([10, 0, 0, k]) for k in range(4))
+        cols["source.ip"] = (np.where(rng.random(n) < 0.3, ABSENT, BYTES).astype(np.uint8),
+                             (ip0 + rng.integers(0, 4, size=n)).astype(np.uint64))
+    return manifest, rules, BagBatch.from_columns(n, cols, strings, maps=(moff, mkeys, mvals))
 
 
 # ----------------------------------------------------------------------------------- memquota (C5)

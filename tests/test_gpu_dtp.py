@@ -1,0 +1,106 @@
+"""Deferred index pairs (kernels.hip "Deferred pairs", engine.cpp launch): with value classes active
+and every indexed group written by the value-class fill, the guard-index kernel runs first and
+records its true / error pairs per wave; mxp_dtp_sort_kernel orders them by (fill chunk, lane
+quad) and mxp_vtfill_*_kernel ORs them into the words it writes.  Pairs past a wave's capacity go
+to an overflow list OR-ed in after the fill; past that list's capacity the index kernel re-runs
+with plain OR-s.  Bar: bit-exact against the oracle (error texts included) and against the
+engine with deferred pairs off (MXP_DTP=0), on every one of those three paths."""
+import numpy as np
+import pytest
+
+import oracle
+from istio_amd import workloads as W
+from test_gpu_parity import compare
+
+pytestmark = pytest.mark.gpu
+FORCE = "262144"  # value classes at any batch size
+
+
+@pytest.fixture(scope="module")
+def mxp(libmxp):
+    import istio_amd.engine as mxp
+    return mxp
+
+
+def engine_for(mxp, monkeypatch, env, manifest, rules, flags=FORCE):
+    for k in ("MXP_DTP", "MXP_DTP_CAP", "MXP_DTP_OVF"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("MXP_DEBUG_FLAGS", flags)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    return eng
+
+
+def deferred_ran(eng, batch, R):
+    """Whether a device evaluation of `batch` takes the deferred-pair path (mxp_kernel_times [2])."""
+    import torch
+    db = eng.upload(batch)
+    dm = torch.zeros(((R + 31) // 32, batch.n), dtype=torch.int32, device="cuda:0")
+    de = torch.zeros_like(dm)
+    hits = torch.zeros(R, dtype=torch.int64, device="cuda:0")
+    eng.set_timing(True)
+    db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), 0)
+    t = eng.kernel_times(3)
+    eng.set_timing(False)
+    db.free()
+    return len(t) == 3 and t[2] == 1.0
+
+
+# default capacity; 4 pairs per wave (most go to the overflow list); 4 per wave and an overflow
+# list of 8 (full: the gated index re-run ORs every pair)
+PATHS = [{}, {"MXP_DTP_CAP": "4"}, {"MXP_DTP_CAP": "4", "MXP_DTP_OVF": "8"}]
+
+
+@pytest.mark.parametrize("env", PATHS, ids=["lists", "overflow", "rerun"])
+def test_deferred_pairs_parity(mxp, monkeypatch, env):
+    """C4 routes with continuations (`path.startsWith(p) && source.ip == ip(..)`, source.ip absent
+    for 30%): true and lookup-error pairs from the index kernel, a ragged batch."""
+    manifest, rules, batch = W.c4_workload(n_rules=1500, n_requests=8000 + 13, seed=47, cont_frac=0.5)
+    eng = engine_for(mxp, monkeypatch, env, manifest, rules)
+    assert deferred_ran(eng, batch, len(rules))
+    got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch, sample_msgs=300)
+    cont = [i for i, r in enumerate(rules) if "source.ip" in r]
+    assert (want[:, cont] == 1).sum() > 50 and (want[:, cont] >= 2).sum() > 50
+
+
+def test_deferred_pairs_device_identical(mxp, monkeypatch):
+    """Device bitmaps and hit counters (fused and streamed), bitmap and compact error output:
+    deferred pairs on (each of the three paths) equal deferred pairs off."""
+    import torch
+    manifest, rules, batch = W.c4_workload(n_rules=2000, n_requests=50_000 + 5, seed=48, cont_frac=0.3)
+    Wd = (len(rules) + 31) // 32
+    out = []
+    for env in PATHS + [{"MXP_DTP": "0"}]:
+        eng = engine_for(mxp, monkeypatch, env, manifest, rules)
+        assert deferred_ran(eng, batch, len(rules)) == (env.get("MXP_DTP") != "0")
+        db = eng.upload(batch)
+        dm = torch.zeros((Wd, batch.n), dtype=torch.int32, device="cuda:0")
+        de = torch.zeros_like(dm)
+        cm = torch.zeros_like(dm)
+        flags = torch.zeros(batch.n, dtype=torch.uint8, device="cuda:0")
+        hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
+        hc = torch.zeros_like(hits)
+        for _ in range(3):  # the fused / streamed choice follows the previous evaluation
+            db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), 0)
+            db.eval_compact(cm.data_ptr(), flags.data_ptr(), hc.data_ptr(), 0)
+        torch.cuda.synchronize()
+        out.append([x.cpu().numpy() for x in (dm, de, hits, cm, flags, hc)])
+        db.free()
+    for o in out[:-1]:
+        for a, b in zip(o, out[-1]):
+            assert np.array_equal(a, b)
+    assert out[0][2].sum() > 0 and out[0][1].any() and out[0][4].any()
+    assert np.array_equal(out[0][0], out[0][3]) and np.array_equal(out[0][2], out[0][5])
+
+
+def test_deferred_pairs_plain_c4(mxp, monkeypatch):
+    """The bench's C4 family (no continuations, no errors) at 10k rules: against the oracle.  Value
+    classes at their default threshold: the header columns (17 values) take them, the path column
+    (a class per request) stays with the prefix index."""
+    manifest, rules, batch = W.c4_workload(n_rules=10_000, n_requests=2048 + 7, seed=4)
+    eng = engine_for(mxp, monkeypatch, {}, manifest, rules, flags="0")
+    assert deferred_ran(eng, batch, len(rules))
+    compare(eng, oracle.OracleEvaluator(manifest), rules, batch)
