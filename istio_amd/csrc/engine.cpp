@@ -1448,7 +1448,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     // lane quad and OR-ed in by the value-class fill as it writes the words -- instead of one read-modify-write
     // atomic per true pair on rows the fill wrote before (C4: ~14 per request, 0.6 ms of atomics)
     const bool dtp_on = dtp && P->dtp_ok && use_index && guards_on && nchunk == 1 && !window && lo == 0 &&
-                        !A.dense_of && !refs_on && A.out_match && P->n_vtfills;
+                        !A.dense_of && !refs_on && !A.nfa && A.out_match && P->n_vtfills;
     last_dtp = dtp_on;
     if (dtp_on) {
         A.q0 = lo;

@@ -136,9 +136,10 @@ __device__ __forceinline__ void dtp_push(const mxp_kargs& A, uint32_t rule, uint
     }
 }
 
+template <bool kDtp = false>
 __device__ __forceinline__ void set_true1(const mxp_kargs& A, uint32_t rule, uint32_t req) {
     const uint32_t bit = 1u << (rule & 31u);
-    if (A.dtp_ent) {
+    if (kDtp) {
         dtp_push(A, rule, req, 0u);
         if (counting(A)) __hip_atomic_fetch_add(A.hits + rule, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
@@ -150,20 +151,22 @@ __device__ __forceinline__ void set_true1(const mxp_kargs& A, uint32_t rule, uin
 
 // ... and the same for the rule's aliases (indexed duplicates of its program, kargs.alias_off)
 // returns the number of pairs set
+template <bool kDtp = false>
 __device__ __forceinline__ uint32_t set_true(const mxp_kargs& A, uint32_t rule, uint32_t req) {
     if (!A.out_match) return 0;
-    set_true1(A, rule, req);
+    set_true1<kDtp>(A, rule, req);
     uint32_t c = 1;
     if (A.alias_off)
-        for (uint32_t j = A.alias_off[rule]; j < A.alias_off[rule + 1]; j++, c++) set_true1(A, A.aliases[j], req);
+        for (uint32_t j = A.alias_off[rule]; j < A.alias_off[rule + 1]; j++, c++) set_true1<kDtp>(A, A.aliases[j], req);
     return c;
 }
 
 // an error pair found by the guard-index kernel, with its aliases
+template <bool kDtp = false>
 __device__ __forceinline__ void set_error(const mxp_kargs& A, uint32_t rule, uint32_t req) {
     if (A.req_err) A.req_err[req] = 1;
     if (!A.out_err) return;
-    if (A.dtp_ent) {
+    if (kDtp) {
         dtp_push(A, rule, req, 1u);
         if (A.alias_off)
             for (uint32_t j = A.alias_off[rule]; j < A.alias_off[rule + 1]; j++) dtp_push(A, A.aliases[j], req, 1u);
@@ -1481,6 +1484,7 @@ struct PairQueue {
 // A true pair of an indexed rule: rules with many duplicates ("dense" canonical rules, kargs.dense_of)
 // only set their bit in the request's mask (LDS) -- the wave writes the bits of the rule and all its
 // aliases once per bitmap word at the end (inject_dense); the rest OR their bits in at once.
+template <bool kDtp>
 __device__ __forceinline__ uint32_t pair_true(const mxp_kargs& A, PairQueue& Q, uint32_t rule, uint32_t req) {
     if (A.dense_of) {
         const uint32_t d = A.dense_of[rule];
@@ -1489,11 +1493,11 @@ __device__ __forceinline__ uint32_t pair_true(const mxp_kargs& A, PairQueue& Q, 
             return 0u;  // counted by mxp_inject_kernel
         }
     }
-    return set_true(A, rule, req);
+    return set_true<kDtp>(A, rule, req);
 }
 
 // run entries [off, off + cnt) of the queue, cnt <= 64
-template <bool kRefs, bool kNfa>
+template <bool kRefs, bool kNfa, bool kDtp>
 __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32_t cnt, uint64_t (*regs)[256],
                           uint32_t tid) {
     const uint32_t lane = tid & 63u;
@@ -1522,15 +1526,15 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
         pending = pending && !mine;
     }
     // results out after the VM loop (its registers are dead here)
-    if (res == PC_TRUE) Q.ntrue += pair_true(A, Q, rule, req);
-    if (res >= PC_ERROR && res != MXP_VM_DONE) set_error(A, rule, req);
+    if (res == PC_TRUE) Q.ntrue += pair_true<kDtp>(A, Q, rule, req);
+    if (res >= PC_ERROR && res != MXP_VM_DONE) set_error<kDtp>(A, rule, req);
 }
 
 // Appends every lane's postings [start, start + len) to the queue (direct postings are true pairs:
 // OR-ed at once) and runs full 64-pair batches; `final` drains the queue.  Long lists go in rounds
 // of up to (free entries / 64) postings per lane, so the queue never overflows and the VM has one
 // call site (one inlined copy).
-template <bool kRefs, bool kNfa>
+template <bool kRefs, bool kNfa, bool kDtp>
 __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, uint32_t tbl, uint32_t start,
                                              uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
                                              uint32_t tid) {
@@ -1555,7 +1559,7 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
                     const uint32_t rule = A.postings[start + j0 + j];
                     uint32_t e = rule | (tbl << 31);
                     if (tmpl_of[rule] == MXP_TMPL_DIRECT) {
-                        Q.ntrue += pair_true(A, Q, rule, req);
+                        Q.ntrue += pair_true<kDtp>(A, Q, rule, req);
                         e = 0xFFFFFFFFu;
                     }
                     g_ixq[Q.wave][at][0] = e;
@@ -1569,7 +1573,7 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
         const bool more = __ballot(j0 < len) != 0;
         if (Q.n >= 64u || (Q.n > 0u && (final || more))) {
             const uint32_t k = min(Q.n, 64u);
-            run_pairs<kRefs, kNfa>(A, Q, Q.n - k, k, regs, tid);
+            run_pairs<kRefs, kNfa, kDtp>(A, Q, Q.n - k, k, regs, tid);
             Q.n -= k;
             continue;
         }
@@ -1622,7 +1626,7 @@ struct PrefixHash {
 // guard column); true and error results are OR-ed in.
 namespace {
 
-template <bool kRefs, bool kNfa = kRefs>
+template <bool kRefs, bool kNfa = kRefs, bool kDtp = false>
 __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
     // the re-run after an overflowed deferred-pair list (kargs.dtp_gate): nothing to do unless it filled
     if (A.dtp_gate && uni(*A.dtp_gate) == 0u) return;
@@ -1633,8 +1637,8 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
     const uint32_t req = Q.base + (tid & 63u);
     const bool valid = req < A.q1;
     if (A.dense_of) g_cm[wave][tid & 63u] = 0ull;
-    if (A.dtp_ent && (tid & 63u) == 0) g_dtpn[wave] = 0u;
-    if (A.dense_of || A.dtp_ent) wave_sync_lds();
+    if (kDtp && (tid & 63u) == 0) g_dtpn[wave] = 0u;
+    if (A.dense_of || kDtp) wave_sync_lds();
     const uint64_t N = A.n;
     // x == n_idx: a last pass with no probes that drains the pair queue
     for (uint32_t x = 0; x <= A.n_idx; x++) {
@@ -1717,14 +1721,14 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 continue;
             }
             if (final || __ballot(len != 0))
-                process_slot<kRefs, kNfa>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
+                process_slot<kRefs, kNfa, kDtp>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
         }
     }
     if (A.dense_of) {  // masks for mxp_inject_kernel
         wave_sync_lds();
         if (valid) A.dense_cm[req] = g_cm[wave][tid & 63u];
     }
-    if (A.dtp_ent) {  // the wave's deferred-pair count for mxp_dtp_sort_kernel
+    if (kDtp) {  // the wave's deferred-pair count for mxp_dtp_sort_kernel
         wave_sync_lds();
         if ((tid & 63u) == 0) A.dtp_n[Q.base >> 6] = min(g_dtpn[wave], A.dtp_cap);
     }
@@ -1750,6 +1754,11 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void mxp_index_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<false>(A, regs);
+}
+// deferred index pairs (kargs.dtp_ent): true / error pairs recorded for the value-class fill
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void mxp_index_dtp_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    index_body<false, false, true>(A, regs);
 }
 // MXP_DEBUG_FLAGS 8192: the same body at 5 waves/SIMD (no scratch) -- A/B ablation
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index5_kernel(mxp_kargs A) {
@@ -1993,6 +2002,8 @@ extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hip
         hipLaunchKernelGGL(mxp_index_refs_kernel, dim3(grid), dim3(256), 0, s, *args);
     else if (args->nfa)
         hipLaunchKernelGGL(mxp_index_nfa_kernel, dim3(grid), dim3(256), 0, s, *args);
+    else if (args->dtp_ent)
+        hipLaunchKernelGGL(mxp_index_dtp_kernel, dim3(grid), dim3(256), 0, s, *args);
     else
         if (args->flags & 8192u)
             hipLaunchKernelGGL(mxp_index5_kernel, dim3(grid), dim3(256), 0, s, *args);
