@@ -401,6 +401,15 @@ int mxp_engine::build_plan(Plan& P) {
     std::vector<mxp_index> idx;
     std::vector<mxp_hent> hents;
     std::vector<uint32_t> postings, plens;
+    // postings carry their rule's continuation template (rule | code << 23; code 511 direct, 510
+    // look it up): the index kernel then loads no template id per posting or per pair
+    P.post_tmpl = n < (1u << 23);
+    auto post = [&](const std::vector<uint32_t>& rs, const std::vector<uint32_t>& tmpl_of) {
+        for (uint32_t r : rs) {
+            const uint32_t t = tmpl_of[r];
+            postings.push_back(!P.post_tmpl ? r : r | (t == MXP_TMPL_DIRECT ? 511u : t < 510u ? t : 510u) << 23);
+        }
+    };
     // open-addressing table of `groups` (key -> rules) at hents[hoff ..): returns hmask
     auto add_eq_table = [&](const std::map<uint64_t, std::vector<uint32_t>>& groups, const std::vector<uint32_t>& tmpl_of,
                             uint32_t* hoff) -> uint32_t {
@@ -415,7 +424,7 @@ int mxp_engine::build_plan(Plan& P) {
             while (hents[*hoff + h].len) h = (h + 1) & (cap - 1);
             hents[*hoff + h] = mxp_hent{(uint32_t)kv.first, (uint32_t)(kv.first >> 32), (uint32_t)postings.size(),
                                         (uint32_t)rs.size()};
-            postings.insert(postings.end(), rs.begin(), rs.end());
+            post(rs, tmpl_of);
         }
         return cap - 1;
     };
@@ -447,7 +456,7 @@ int mxp_engine::build_plan(Plan& P) {
             while (hents[x.hoff + h].len) h = (h + 1) & x.hmask;
             hents[x.hoff + h] = mxp_hent{(uint32_t)kv.first, (uint32_t)(hh >> 32), (uint32_t)postings.size(),
                                          (uint32_t)rs.size()};
-            postings.insert(postings.end(), rs.begin(), rs.end());
+            post(rs, rule_tmpl);
         }
         x.plen0 = (uint32_t)plens.size();
         x.nplen = (uint32_t)lens.size();
@@ -488,7 +497,7 @@ int mxp_engine::build_plan(Plan& P) {
             hents[x.hoff2 + 2 * h] = mxp_hent{kv.first.second, (uint32_t)(hh >> 32), (uint32_t)postings.size(),
                                               (uint32_t)rs.size()};
             hents[x.hoff2 + 2 * h + 1] = mxp_hent{(uint32_t)k1, (uint32_t)(k1 >> 32), 0, 0};
-            postings.insert(postings.end(), rs.begin(), rs.end());
+            post(rs, rule_tmpl2);
         }
         x.plen0 = (uint32_t)plens.size();
         x.nplen = (uint32_t)lens.size();
@@ -1243,6 +1252,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
     A->idx = P.d_idx.as<mxp_index>();
     A->hents = P.d_hents.as<mxp_hent>();
     A->postings = P.d_postings.as<uint32_t>();
+    A->post_tmpl = P.post_tmpl ? 1u : 0u;
     A->plens = P.d_plens.as<uint32_t>();
     A->n_idx = P.n_idx;
     A->tmpls = P.d_tmpls.as<mxp_tmpl>();

@@ -214,6 +214,7 @@ struct mxp_engine : public mxp::LowerTables {
         uint32_t n_glean = 0, n_gvm = 0, lean_cc = 0, n_fills = 0, n_gfill = 0;
         uint32_t n_idx = 0, n_indexed = 0, n_composite = 0, n_alias = 0, n_tmpls = 0, n_segs = 0;
         uint32_t n_dense = 0, n_inj = 0;
+        bool post_tmpl = false;  // postings carry template codes (kargs.post_tmpl)
         DevBuf d_guards, d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_alias_off, d_aliases;
         DevBuf d_idx, d_hents, d_postings, d_plens;
         DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all

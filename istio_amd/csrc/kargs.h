@@ -36,7 +36,8 @@ typedef struct mxp_kargs {
     const uint64_t* rconst;      // [n_rules][MXP_VM_MAXREG] per-rule template constants
     const mxp_index* idx;        // guard indexes (mxp_index_kernel)
     const mxp_hent* hents;
-    const uint32_t* postings;
+    const uint32_t* postings;    // rules of each index entry; with post_tmpl: rule | code << 23 (code = the
+                                 // continuation template, 511 direct, 510 look up rule_tmpl / rule_tmpl2)
     const uint32_t* plens;       // prefix indexes: distinct key lengths
     uint32_t n_idx;
     uint32_t lean_cols;          // mxp_guard2_kernel: columns < MXP_CC its groups read (preloaded)
@@ -112,4 +113,5 @@ typedef struct mxp_kargs {
     uint8_t* dtp_qn;             // [chunks][tiles * 256] entries in each quad's slots (<= 8)
     const uint32_t* dtp_gate;    // index re-run with OR-ed pairs: returns unless *dtp_gate (list full)
     uint32_t dtp_cap, dtp_ovf_cap, dtp_tiles, dtp_nchunks;
+    uint32_t post_tmpl;
 } mxp_kargs;

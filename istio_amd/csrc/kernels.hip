@@ -1505,11 +1505,11 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
     bool pending = lane < cnt;
     uint32_t rule = 0, req = 0, t = MXP_VM_DONE, res = MXP_VM_DONE;
     if (pending) {
-        const uint32_t e = g_ixq[Q.wave][off + lane][0];
-        req = g_ixq[Q.wave][off + lane][1];
+        const uint32_t e = g_ixq[Q.wave][off + lane][0], w1 = g_ixq[Q.wave][off + lane][1];
+        req = Q.base + (w1 & 63u);
         pending = e != 0xFFFFFFFFu;  // a direct posting, already OR-ed
         rule = e & 0x7FFFFFFFu;
-        if (pending) t = (e >> 31) ? A.rule_tmpl2[rule] : A.rule_tmpl[rule];
+        if (pending) t = w1 >> 8;
     }
     wave_sync_lds();
     for (uint64_t bal = __ballot(pending); bal; bal = __ballot(pending)) {
@@ -1556,14 +1556,23 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
                 const uint64_t act = __ballot(j < take);
                 if (j < take) {
                     const uint32_t at = pos + (uint32_t)__builtin_popcountll(act & below);
-                    const uint32_t rule = A.postings[start + j0 + j];
+                    const uint32_t pe = A.postings[start + j0 + j];
+                    uint32_t rule = pe, t;
+                    if (A.post_tmpl) {  // the template rides in the posting (kargs.postings)
+                        rule = pe & 0x7FFFFFu;
+                        const uint32_t code = pe >> 23;
+                        t = code == 511u ? MXP_TMPL_DIRECT : code == 510u ? tmpl_of[rule] : code;
+                    } else {
+                        t = tmpl_of[rule];
+                    }
                     uint32_t e = rule | (tbl << 31);
-                    if (tmpl_of[rule] == MXP_TMPL_DIRECT) {
+                    if (t == MXP_TMPL_DIRECT) {
                         Q.ntrue += pair_true<kDtp>(A, Q, rule, req);
                         e = 0xFFFFFFFFu;
                     }
+                    // (entry: rule | table, then the request's lane in the wave | template << 8)
                     g_ixq[Q.wave][at][0] = e;
-                    g_ixq[Q.wave][at][1] = req;
+                    g_ixq[Q.wave][at][1] = (req - Q.base) | (t << 8);
                 }
                 pos += (uint32_t)__builtin_popcountll(act);
             }
@@ -1650,7 +1659,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
         // kinds and values of both columns are loaded together (independent loads, one round trip)
         bool ok = false;
         uint64_t v = 0;
-        if (valid) {
+        if (valid && !final) {  // (the last pass only drains the queue)
             const uint32_t k = A.kinds[(uint64_t)col * N + req];
             const uint64_t vv = A.vals[(uint64_t)col * N + req];
             ok = ((okset >> k) & 1u) != 0;
@@ -1666,7 +1675,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
             const uint32_t col2 = uni(X->col2), okset2 = uni(X->okset2);
             pmask = uni(X->hmask2);
             poff = uni(X->hoff2);
-            if (valid) {
+            if (valid && !final) {
                 const uint32_t k = A.kinds[(uint64_t)col2 * N + req];
                 const uint64_t vv = A.vals[(uint64_t)col2 * N + req];
                 sok = ok && ((okset2 >> k) & 1u) != 0;
