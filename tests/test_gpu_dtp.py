@@ -104,3 +104,16 @@ def test_deferred_pairs_plain_c4(mxp, monkeypatch):
     eng = engine_for(mxp, monkeypatch, {}, manifest, rules, flags="0")
     assert deferred_ran(eng, batch, len(rules))
     compare(eng, oracle.OracleEvaluator(manifest), rules, batch)
+
+
+def test_deferred_pairs_windows_and_quad_overflow(mxp, monkeypatch):
+    """17k rules (over 32 fill chunks: mxp_dtp_sort_kernel files them in two windows) led by 64
+    copies of `request.path.startsWith("/w1")` (one canonical rule and 63 aliases in the first
+    chunk: a matching request's quad holds far more than 8 pairs there -- the rest go through the
+    overflow list).  Value classes at their default threshold (headers yes, paths no)."""
+    manifest, rules, batch = W.c4_workload(n_rules=17_000, n_requests=4000 + 3, seed=49)
+    rules = ['request.path.startsWith("/w1")'] * 64 + rules
+    eng = engine_for(mxp, monkeypatch, {}, manifest, rules, flags="0")
+    assert deferred_ran(eng, batch, len(rules))
+    got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch)
+    assert (want[:, 0] == 1).sum() > 100
