@@ -701,13 +701,16 @@ int mxp_engine::build_plan(Plan& P) {
         P.n_inj = P.n_dense ? (uint32_t)(inj.size() / MXP_INJ_SLOT) : 0u;
     }
     // deferred index pairs: every group holding an indexed rule (or an alias of one) must be a
-    // value-class fill group -- the only writer that merges them
+    // fill or value-class fill group -- the writers that merge them
+    // (chunk ids: the plain fill chunks, then the value-class ones)
     std::vector<uint32_t> dtp_chunk(W, 0xFFFFFFFFu);
     {
-        bool ok = fills.empty() && !vtfills.empty() && P.n_dense == 0 && n < (1u << 23);
-        for (uint32_t c = 0; ok && c < vtfills.size(); c++) {
-            if (vtfills[c].n > 255u || c >= (1u << 24)) ok = false;  // (group 255: the queue's pad)
-            for (uint32_t k = 0; ok && k < vtfills[c].n; k++) dtp_chunk[vtfills[c].g0 + k] = c << 8 | k;
+        bool ok = (!fills.empty() || !vtfills.empty()) && P.n_dense == 0 && n < (1u << 23);
+        const uint32_t nf = (uint32_t)fills.size();
+        for (uint32_t c = 0; ok && c < nf + vtfills.size(); c++) {
+            const mxp_fill& F = c < nf ? fills[c] : vtfills[c - nf];
+            if (F.n > 255u || c >= (1u << 24)) ok = false;  // (group 255: the queue's pad)
+            for (uint32_t k = 0; ok && k < F.n; k++) dtp_chunk[F.g0 + k] = c << 8 | k;
         }
         for (uint32_t g = 0; ok && g < W; g++)
             if (groups[g].indexed && dtp_chunk[g] == 0xFFFFFFFFu) ok = false;
@@ -1458,7 +1461,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     // lane quad and OR-ed in by the value-class fill as it writes the words -- instead of one read-modify-write
     // atomic per true pair on rows the fill wrote before (C4: ~14 per request, 0.6 ms of atomics)
     const bool dtp_on = dtp && P->dtp_ok && use_index && guards_on && nchunk == 1 && !window && lo == 0 &&
-                        !A.dense_of && !refs_on && !A.nfa && A.out_match && P->n_vtfills;
+                        !A.dense_of && !refs_on && !A.nfa && A.out_match;
     last_dtp = dtp_on;
     if (dtp_on) {
         A.q0 = lo;
@@ -1467,8 +1470,8 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         if ((e = d_dtp_ent.reserve((size_t)cx * dtp_cap * 4)) != hipSuccess ||
             (e = d_dtp_n.reserve((size_t)grid * 4 * 4)) != hipSuccess ||
             (e = d_dtp_ovf.reserve((size_t)dtp_ovf_cap * 8)) != hipSuccess || (e = d_dtp_ovf_n.reserve(16)) != hipSuccess ||
-            (e = d_dtp_slots.reserve((size_t)P->n_vtfills * tiles * 256 * 16)) != hipSuccess ||
-            (e = d_dtp_qn.reserve((size_t)P->n_vtfills * tiles * 256)) != hipSuccess)
+            (e = d_dtp_slots.reserve((size_t)(P->n_fills + P->n_vtfills) * tiles * 256 * 16)) != hipSuccess ||
+            (e = d_dtp_qn.reserve((size_t)(P->n_fills + P->n_vtfills) * tiles * 256)) != hipSuccess)
             return hipfail(e, "deferred-pair scratch");
         if ((e = hipMemsetAsync(d_dtp_ovf_n.p, 0, 16, s)) != hipSuccess) return hipfail(e, "memset dtp");
         mxp_kargs AI = A;  // the index kernel records
@@ -1482,16 +1485,18 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         AI.dtp_slots = d_dtp_slots.as<uint16_t>();
         AI.dtp_qn = d_dtp_qn.as<uint8_t>();
         AI.dtp_tiles = tiles;
-        AI.dtp_nchunks = P->n_vtfills;
+        AI.dtp_nchunks = P->n_fills + P->n_vtfills;
         if ((e = mxp_launch_index(&AI, grid, s)) != hipSuccess) return hipfail(e, "launch index");
         if ((e = mxp_launch_dtp_sort(&AI, s)) != hipSuccess) return hipfail(e, "launch dtp sort");
         if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
-        mxp_kargs AF = A;  // the value-class fill merges
-        AF.fills = P->d_vtfills.as<mxp_fill>();
+        mxp_kargs AF = A;  // the fills merge
         AF.dtp_slots = AI.dtp_slots;
         AF.dtp_qn = AI.dtp_qn;
         AF.dtp_tiles = tiles;
-        if ((e = mxp_launch_vtfill(&AF, P->n_vtfills, s)) != hipSuccess) return hipfail(e, "launch vtfill");
+        if (P->n_fills && (e = mxp_launch_fill(&AF, P->n_fills, s)) != hipSuccess) return hipfail(e, "launch fill");
+        AF.fills = P->d_vtfills.as<mxp_fill>();
+        AF.dtp_cbase = P->n_fills;
+        if (P->n_vtfills && (e = mxp_launch_vtfill(&AF, P->n_vtfills, s)) != hipSuccess) return hipfail(e, "launch vtfill");
         for (const Part& Pt : parts) {
             if (!Pt.n) continue;
             A.glist = Pt.list->as<uint32_t>();

@@ -113,5 +113,7 @@ typedef struct mxp_kargs {
     uint8_t* dtp_qn;             // [chunks][tiles * 256] entries in each quad's slots (<= 8)
     const uint32_t* dtp_gate;    // index re-run with OR-ed pairs: returns unless *dtp_gate (list full)
     uint32_t dtp_cap, dtp_ovf_cap, dtp_tiles, dtp_nchunks;
+    uint32_t dtp_cbase;          // fill launches: chunk id of blockIdx.y 0 (plain fill chunks first, then
+                                 // the value-class ones)
     uint32_t post_tmpl;
 } mxp_kargs;

@@ -1163,6 +1163,45 @@ __device__ __forceinline__ void dtp_merge(uint32_t x, bool on, uint32_t (&m)[4],
     }
 }
 
+// The deferred index pairs of a lane's quad of requests in one fill chunk (mxp_dtp_sort_kernel):
+// up to 8 u16 entries, sorted here (group first) into a queue in four registers whose head the
+// group loop consumes while it names the current group.
+struct DtpQueue {
+    uint32_t q0 = ~0u, q1 = ~0u, q2 = ~0u, q3 = ~0u;
+    __device__ __forceinline__ void load(const mxp_kargs& A, uint32_t chunk, uint32_t req0, bool in) {
+        if (!A.dtp_slots || !in) return;
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        const uint64_t qi = (uint64_t)chunk * A.dtp_tiles * 256u + (req0 >> 2);
+        const uint32_t dk = A.dtp_qn[qi];
+        const v4u sl = *(const v4u*)(A.dtp_slots + qi * 8u);
+        if (!dk) return;
+        const uint32_t h[4] = {sl.x, sl.y, sl.z, sl.w};
+        uint32_t x[8];
+#pragma unroll
+        for (uint32_t i = 0; i < 8; i++) x[i] = i < dk ? (h[i >> 1] >> (16u * (i & 1u))) & 0xFFFFu : 0xFFFFu;
+        sort8(x);
+        q0 = x[0] | x[1] << 16;
+        q1 = x[2] | x[3] << 16;
+        q2 = x[4] | x[5] << 16;
+        q3 = x[6] | x[7] << 16;
+    }
+    // OR the head entries naming group g into the words (pads, 0xFFFF, name no group)
+    __device__ __forceinline__ void merge(uint32_t g, uint32_t (&m)[4], uint32_t (&e)[4]) {
+        for (;;) {
+            const uint32_t x = q0 & 0xFFFFu;
+            const bool hit = (x >> 8) == g;
+            if (!__ballot(hit)) break;
+            dtp_merge(x, hit, m, e);
+            if (hit) {
+                q0 = __builtin_amdgcn_alignbit(q1, q0, 16);
+                q1 = __builtin_amdgcn_alignbit(q2, q1, 16);
+                q2 = __builtin_amdgcn_alignbit(q3, q2, 16);
+                q3 = q3 >> 16 | 0xFFFF0000u;
+            }
+        }
+    }
+};
+
 template <bool kLds>
 __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* F, uint32_t chunk, uint32_t qw,
                                             const uint2* S, uint32_t PB, uint32_t PJ) {
@@ -1196,28 +1235,9 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
         }
     }
     const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
-    // deferred index pairs of the lane's 4 requests in this chunk (mxp_dtp_sort_kernel): up to 8 u16
-    // entries, sorted here (group first) into a queue in four registers whose head the group loop
-    // consumes while it names the current group
-    uint32_t dq0 = ~0u, dq1 = ~0u, dq2 = ~0u, dq3 = ~0u;
-    if (A.dtp_slots && q0 < Q1) {
-        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        const uint64_t qi = (uint64_t)chunk * A.dtp_tiles * 256u + (q0 >> 2);
-        const uint32_t dk = A.dtp_qn[qi];
-        const v4u sl = *(const v4u*)(A.dtp_slots + qi * 8u);
-        if (dk) {
-            const uint32_t h[4] = {sl.x, sl.y, sl.z, sl.w};
-            uint32_t x[8];
-#pragma unroll
-            for (uint32_t i = 0; i < 8; i++) x[i] = i < dk ? (h[i >> 1] >> (16u * (i & 1u))) & 0xFFFFu : 0xFFFFu;
-            sort8(x);
-            dq0 = x[0] | x[1] << 16;
-            dq1 = x[2] | x[3] << 16;
-            dq2 = x[4] | x[5] << 16;
-            dq3 = x[6] | x[7] << 16;
-        }
-    }
-    const bool dany = __ballot(dq0 != ~0u) != 0;
+    DtpQueue dq;
+    dq.load(A, chunk, q0, q0 < Q1);
+    const bool dany = __ballot(dq.q0 != ~0u) != 0;
     const bool nt = !(A.flags & 128u);
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     // the active slots' (cap, tbase), the chunk's group masks and merge entries: one vector load
@@ -1276,20 +1296,7 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
             for (int r = 0; r < 4; r++) c += (uint32_t)__builtin_popcount(ve[r] & vmask[r]);
             vt_count_n(A, c);
         }
-        if (dany) {  // the index kernel's true / error pairs in this group's words
-            for (;;) {
-                const uint32_t x = dq0 & 0xFFFFu;
-                const bool hit = (x >> 8) == g;  // (pads, 0xFFFF, name no group)
-                if (!__ballot(hit)) break;
-                dtp_merge(x, hit, m, e);
-                if (hit) {
-                    dq0 = __builtin_amdgcn_alignbit(dq1, dq0, 16);
-                    dq1 = __builtin_amdgcn_alignbit(dq2, dq1, 16);
-                    dq2 = __builtin_amdgcn_alignbit(dq3, dq2, 16);
-                    dq3 = dq3 >> 16 | 0xFFFF0000u;
-                }
-            }
-        }
+        if (dany) dq.merge(g, m, e);  // the index kernel's true / error pairs in this group's words
         // (no hit counting: a uniform group's words hold no true bit but the value classes', which
         // mxp_vt_eval_kernel counts per class)
         if (A.req_err)
@@ -1316,20 +1323,87 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
     }
 }
 
+// mxp_fill_kernel for deferred index pairs (kargs.dtp_slots): one span of 256 requests per wave (a
+// lane owns one quad, whose sorted pairs it merges into each group's words before storing them)
+extern "C" __global__ __launch_bounds__(256) void mxp_fill_dtp_kernel(mxp_kargs A) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uni(threadIdx.x >> 6);
+    const mxp_fill* F = A.fills + blockIdx.y;
+    const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
+    const uint64_t N = A.n;
+    const uint32_t Q1 = A.q1;
+    const uint32_t qw = A.q0 + (blockIdx.x * 4u + wave) * 256u;
+    if (qw >= Q1) return;
+    const uint32_t q0 = qw + lane * 4u;
+    const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0;
+    uint32_t bad[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const bool in = q0 + r < Q1;
+        const uint32_t k = in ? A.kinds[(uint64_t)col * N + q0 + r] : 0u;
+        bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
+    }
+    const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
+    DtpQueue dq;
+    dq.load(A, A.dtp_cbase + blockIdx.y, q0, q0 < Q1);
+    const bool dany = __ballot(dq.q0 != ~0u) != 0;
+    if (A.req_err && any) {
+        uint32_t masks = 0;
+        for (uint32_t g = 0; g < n; g++) masks |= uni(A.fill_masks[moff + g]);
+        if (masks)
+            for (uint32_t r = 0; r < 4; r++)
+                if (bad[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;
+    }
+    if (A.errlog && any)
+        for (uint32_t g = 0; g < n; g++) {
+            const uint32_t mask = uni(A.fill_masks[moff + g]);
+            for (uint32_t r = 0; r < 4; r++)
+                if (bad[r] && q0 + r < Q1) log_guard_errors(A, mask, (g0 + g) * 32u, q0 + r);
+        }
+    const bool nt = !(A.flags & 128u);
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    for (uint32_t g = 0; g < n; g++) {
+        const uint32_t mask = uni(A.fill_masks[moff + g]);
+        uint32_t m[4] = {0u, 0u, 0u, 0u}, e[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) e[r] = bad[r] & mask;
+        if (dany) dq.merge(g, m, e);
+        const uint64_t at = (uint64_t)(g0 + g) * N + q0;
+        if (vec && q0 < Q1) {
+            const v4u mv = v4u{m[0], m[1], m[2], m[3]}, ev = v4u{e[0], e[1], e[2], e[3]};
+            if (nt) {
+                if (A.out_match) __builtin_nontemporal_store(mv, (v4u*)(A.out_match + at));
+                if (A.out_err) __builtin_nontemporal_store(ev, (v4u*)(A.out_err + at));
+            } else {
+                if (A.out_match) *(v4u*)(A.out_match + at) = mv;
+                if (A.out_err) *(v4u*)(A.out_err + at) = ev;
+            }
+        } else {
+            for (uint32_t r = 0; r < 4; r++) {
+                if (q0 + r >= Q1) break;
+                if (A.out_match) A.out_match[at + r] = m[r];
+                if (A.out_err) A.out_err[at + r] = e[r];
+            }
+        }
+    }
+}
+
 // MXP_DEBUG_FLAGS 2097152: every chunk gathers class words from global memory (A/B)
 extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A) {
     const uint32_t wave = uni(threadIdx.x >> 6);
-    vtfill_wave<false>(A, A.fills + blockIdx.y, blockIdx.y, A.q0 + (blockIdx.x * 4u + wave) * 256u, nullptr, 0u, 0u);
+    vtfill_wave<false>(A, A.fills + blockIdx.y, A.dtp_cbase + blockIdx.y, A.q0 + (blockIdx.x * 4u + wave) * 256u, nullptr, 0u,
+                       0u);
 }
 
 // The default: a workgroup stages its chunk's class-word rows in LDS once -- per active slot a, the
 // contiguous rows of the word positions the chunk's merge entries name (slot a's positions grow
 // with the group) -- then covers MXP_VTF_TILES tiles of 1024 requests (4 waves x 256) gathering
 // from LDS instead of L1/L2 (C4: ~60 entries x 4 gathers per request and chunk).  A chunk whose
-// rows exceed the 32 KB budget gathers from global memory.  93 VGPRs, 32 KB: 5 workgroups per CU.
+// rows exceed the 32 KB budget gathers from global memory.  100 VGPRs with the deferred-pair queue, 32 KB: 4 workgroups per CU (measured
+// faster than 96 VGPRs forced to 5: C4 1.715 vs 1.78 ms, profiles/r2_v14_ablibs_vtfill_occ_c4.log).
 #define MXP_VTF_STAGE 4096u
 #define MXP_VTF_TILES 4u
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_vtfill_lds_kernel(mxp_kargs A) {
+extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_kargs A) {
     __shared__ uint2 S[MXP_VTF_STAGE];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
     const mxp_fill* F = A.fills + blockIdx.y;
@@ -1367,9 +1441,9 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
         const uint32_t qw = A.q0 + ((blockIdx.x * MXP_VTF_TILES + t) * 4u + wave) * 256u;
         if (staged)
-            vtfill_wave<true>(A, F, blockIdx.y, qw, S, PB, PJ);
+            vtfill_wave<true>(A, F, A.dtp_cbase + blockIdx.y, qw, S, PB, PJ);
         else
-            vtfill_wave<false>(A, F, blockIdx.y, qw, nullptr, 0u, 0u);
+            vtfill_wave<false>(A, F, A.dtp_cbase + blockIdx.y, qw, nullptr, 0u, 0u);
     }
 }
 
@@ -1960,6 +2034,10 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
 }
 
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s) {
+    if (args->dtp_slots) {
+        hipLaunchKernelGGL(mxp_fill_dtp_kernel, dim3((args->q1 - args->q0 + 1023u) / 1024u, n_fills), dim3(256), 0, s, *args);
+        return hipGetLastError();
+    }
     const uint32_t per_block = 1024u * (args->fill_span ? args->fill_span : 1u);
     hipLaunchKernelGGL(mxp_fill_kernel, dim3((args->q1 - args->q0 + per_block - 1) / per_block, n_fills), dim3(256), 0, s, *args);
     return hipGetLastError();

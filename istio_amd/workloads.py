@@ -483,14 +483,15 @@ C4_MANIFEST = {"request.path": "STRING", "request.headers": "STRING_MAP", "desti
 _C4_HEADERS = ["x-user", "x-env", "x-canary", "user-agent", "x-region"]
 
 
-def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_frac=0.0):
+def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_frac=0.0, paths_only=False):
     """C4: Pilot-shaped HTTP route rules in the Mixer language: 60%
     request.path.startsWith("/p..") (Pilot prefix), 20% "^...".matches(request.path) (Pilot regex:
     prefix -> ^QuoteMeta(p).*), 20% request.headers["h"] == "v" or "re".matches(request.headers["h"]).
     Requests: paths of depth 1..6 over a `vocab`-word vocabulary, 3 headers each.
     cont_frac > 0 (tests): that fraction of the prefix rules continue with
     `&& source.ip == ip("10.0.0.K")`, over a source.ip column absent for 30% of the requests -- the
-    guard-index kernel then finds true pairs and lookup-error pairs.
+    guard-index kernel then finds true pairs and lookup-error pairs.  paths_only: the header rules'
+    share becomes path rules too (a route table matched on paths alone: no value classes).
     Returns (manifest, rules, BagBatch)."""
     rng = np.random.default_rng(seed)
     words = ["w%d" % i for i in range(vocab)]
@@ -501,6 +502,8 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_fra
     rules = []
     for i in range(n_rules):
         r = rng.random()
+        if paths_only and r >= 0.8:
+            r = 0.75 * (r - 0.8) / 0.2  # (prefix and regex rules in their 3:1 proportion)
         p = path(int(rng.integers(1, 4)))
         if r < 0.6:
             if cont_frac and rng.random() < cont_frac:

@@ -117,3 +117,44 @@ def test_deferred_pairs_windows_and_quad_overflow(mxp, monkeypatch):
     assert deferred_ran(eng, batch, len(rules))
     got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch)
     assert (want[:, 0] == 1).sum() > 100
+
+
+@pytest.mark.parametrize("env", PATHS, ids=["lists", "overflow", "rerun"])
+def test_deferred_pairs_plain_fill_parity(mxp, monkeypatch, env):
+    """Route rules matched on paths alone (no value classes): the indexed groups are plain fill
+    chunks, written by mxp_fill_dtp_kernel with the pairs merged; continuations give error pairs."""
+    manifest, rules, batch = W.c4_workload(n_rules=1500, n_requests=8000 + 13, seed=50, cont_frac=0.5,
+                                           paths_only=True)
+    eng = engine_for(mxp, monkeypatch, env, manifest, rules, flags="0")
+    assert deferred_ran(eng, batch, len(rules))
+    got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch, sample_msgs=300)
+    assert (want == 1).sum() > 1000 and (want >= 2).sum() > 50
+
+
+def test_deferred_pairs_plain_fill_device_identical(mxp, monkeypatch):
+    """Paths-only routes: device bitmaps, hit counters and compact output with deferred pairs on
+    (through mxp_fill_dtp_kernel) equal deferred pairs off."""
+    import torch
+    manifest, rules, batch = W.c4_workload(n_rules=3000, n_requests=60_000 + 7, seed=51, cont_frac=0.2,
+                                           paths_only=True)
+    Wd = (len(rules) + 31) // 32
+    out = []
+    for env in ({}, {"MXP_DTP": "0"}):
+        eng = engine_for(mxp, monkeypatch, env, manifest, rules, flags="0")
+        assert deferred_ran(eng, batch, len(rules)) == (not env)
+        db = eng.upload(batch)
+        dm = torch.zeros((Wd, batch.n), dtype=torch.int32, device="cuda:0")
+        de = torch.zeros_like(dm)
+        cm = torch.zeros_like(dm)
+        flags = torch.zeros(batch.n, dtype=torch.uint8, device="cuda:0")
+        hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
+        hc = torch.zeros_like(hits)
+        for _ in range(3):
+            db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), 0)
+            db.eval_compact(cm.data_ptr(), flags.data_ptr(), hc.data_ptr(), 0)
+        torch.cuda.synchronize()
+        out.append([x.cpu().numpy() for x in (dm, de, hits, cm, flags, hc)])
+        db.free()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
+    assert out[0][2].sum() > 0 and out[0][1].any()

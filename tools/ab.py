@@ -1,6 +1,6 @@
 """A/B timing of engine settings (environment knobs read at engine creation: MXP_GPW,
 MXP_DEBUG_FLAGS, ...) on one workload, alternated over repetitions in one process so box-to-box
-variance cancels.  usage: ab.py c2|c4 "MXP_GPW=4" "MXP_GPW=8" ..."""
+variance cancels.  usage: ab.py c2|c4|c4p "MXP_GPW=4" "MXP_GPW=8" ..."""
 import os
 import sys
 
@@ -15,6 +15,8 @@ from istio_amd.engine import Engine  # noqa: E402
 wl, settings = sys.argv[1], sys.argv[2:]
 if wl == "c4":
     manifest, rules, batch = W.c4_workload(n_rules=10000, n_requests=1 << 20, seed=4)
+elif wl == "c4p":  # C4 route rules matched on paths alone (no value classes)
+    manifest, rules, batch = W.c4_workload(n_rules=10000, n_requests=1 << 20, seed=4, paths_only=True)
 else:
     manifest, rules, batch = W.c2_workload(n_rules=10000, n_requests=1 << 20, seed=2)
 Wd = (len(rules) + 31) // 32
