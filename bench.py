@@ -439,7 +439,7 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     deferred = bool(per and len(per[0]) > 2 and per[0][2] == 1.0)
     if deferred:
         labels = ("mxp_vt_classify/vt_eval + mxp_index_kernel + mxp_dtp_sort_kernel (deferred pairs)",
-                  "mxp_vtfill/guard2/eval kernels + mxp_dtp_apply_kernel")
+                  "mxp_fill/vtfill/guard2/eval kernels + the gated index launch (overflow list)")
     else:
         labels = ("phase1 (mxp_vt_classify/vt_eval/fill/vtfill/guard2/eval kernels)",
                   "mxp_index_kernel+mxp_inject_kernel")

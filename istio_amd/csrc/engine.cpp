@@ -1469,15 +1469,22 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         const uint32_t cx = (hi + 63) / 64, grid = (cx + 3) / 4, tiles = (hi + 1023) / 1024;
         if ((e = d_dtp_ent.reserve((size_t)cx * dtp_cap * 4)) != hipSuccess ||
             (e = d_dtp_n.reserve((size_t)grid * 4 * 4)) != hipSuccess ||
-            (e = d_dtp_ovf.reserve((size_t)dtp_ovf_cap * 8)) != hipSuccess || (e = d_dtp_ovf_n.reserve(16)) != hipSuccess ||
+            (e = d_dtp_ovf.reserve((size_t)dtp_ovf_cap * 8)) != hipSuccess ||
             (e = d_dtp_slots.reserve((size_t)(P->n_fills + P->n_vtfills) * tiles * 256 * 16)) != hipSuccess ||
             (e = d_dtp_qn.reserve((size_t)(P->n_fills + P->n_vtfills) * tiles * 256)) != hipSuccess)
             return hipfail(e, "deferred-pair scratch");
-        if ((e = hipMemsetAsync(d_dtp_ovf_n.p, 0, 16, s)) != hipSuccess) return hipfail(e, "memset dtp");
+        if (!d_dtp_ovf_n.p) {  // two counter sets (count, list full): each launch's sort kernel resets the other
+            if ((e = d_dtp_ovf_n.alloc(32)) != hipSuccess) return hipfail(e, "deferred-pair counters");
+            if ((e = hipMemsetAsync(d_dtp_ovf_n.p, 0, 32, s)) != hipSuccess) return hipfail(e, "memset dtp");
+        }
+        uint32_t* const ovf_n = d_dtp_ovf_n.as<uint32_t>() + 4u * dtp_par;
+        uint32_t* const ovf_next = d_dtp_ovf_n.as<uint32_t>() + 4u * (dtp_par ^ 1u);
+        dtp_par ^= 1u;
         mxp_kargs AI = A;  // the index kernel records
         AI.dtp_ent = d_dtp_ent.as<uint32_t>();
         AI.dtp_n = d_dtp_n.as<uint32_t>();
-        AI.dtp_ovf_n = d_dtp_ovf_n.as<uint32_t>();
+        AI.dtp_ovf_n = ovf_n;
+        AI.dtp_ovf_next = ovf_next;
         AI.dtp_ovf = d_dtp_ovf.as<uint32_t>();
         AI.dtp_cap = dtp_cap;
         AI.dtp_ovf_cap = dtp_ovf_cap;
@@ -1503,10 +1510,12 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
             A.n_glist = Pt.n;
             if ((e = mxp_launch_eval(&A, cx, gy_of(Pt.n), Pt.vm, s)) != hipSuccess) return hipfail(e, "launch eval");
         }
-        if ((e = mxp_launch_dtp_apply(&AI, s)) != hipSuccess) return hipfail(e, "launch dtp apply");
-        // overflow list full: the index kernel again, OR-ing every pair (no counters, no records:
-        // the first pass kept those); it returns at once otherwise
+        // the overflow list OR-ed in; if it filled, the index kernel again, OR-ing every pair (no
+        // counters, no records: the first pass kept those) -- else it returns after the list
         mxp_kargs AR = A;
+        AR.dtp_ovf_n = AI.dtp_ovf_n;
+        AR.dtp_ovf = AI.dtp_ovf;
+        AR.dtp_ovf_cap = AI.dtp_ovf_cap;
         AR.dtp_gate = AI.dtp_ovf_n + 1;
         AR.hits = nullptr;
         AR.stats = nullptr;
@@ -1915,10 +1924,11 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
     }
     if (!eng->stats_ev) {
         if ((e = eng->d_stats.alloc(8)) != hipSuccess) return eng->hipfail(e, "stats");
-        if ((e = eng->d_gate.alloc(4)) != hipSuccess) return eng->hipfail(e, "hits gate");
+        if ((e = eng->d_gate.alloc(8)) != hipSuccess) return eng->hipfail(e, "hits gate");
+        if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
         // no evaluation yet: stream the bitmap (a fused first evaluation of a rule set with many true
         // pairs would pay one atomic per pair: C4's first evaluations took 6.5 ms instead of 1.9)
-        if ((e = hipMemsetAsync(eng->d_gate.p, 0, 4, s)) != hipSuccess) return eng->hipfail(e, "hits gate");
+        if ((e = hipMemsetAsync(eng->d_gate.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "hits gate");
         if ((e = hipEventCreateWithFlags(&eng->stats_ev, hipEventDisableTiming)) != hipSuccess) {
             eng->stats_ev = nullptr;
             return eng->hipfail(e, "stats event");
@@ -1932,21 +1942,28 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
     // (ordered after the previous evaluation's gate update even when the caller switched streams)
     if (eng->stats_pending && (e = hipStreamWaitEvent(s, eng->stats_ev, 0)) != hipSuccess)
         return eng->hipfail(e, "stats wait");
-    if (force && (e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), 0, W, eng->d_gate.as<uint32_t>(),
-                                           force, s)) != hipSuccess)
+    uint32_t* const gate = eng->d_gate.as<uint32_t>() + eng->gate_par;
+    uint32_t* const gate_next = eng->d_gate.as<uint32_t>() + (eng->gate_par ^ 1u);
+    if (force && (e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), 0, W, gate, force, s)) != hipSuccess)
         return eng->hipfail(e, "hits gate");
-    if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
     eng->req_err_out = d_req_err;
-    eng->hits_gate_out = eng->d_gate.as<uint32_t>();
+    eng->hits_gate_out = gate;
     int rc = eng->launch(db, s, d_match, d_err, nullptr, false, d_hits, eng->d_stats.as<uint64_t>());
     eng->req_err_out = nullptr;
     eng->hits_gate_out = nullptr;
     if (rc) return rc;
-    if (R && db->n && (e = mxp_launch_hits(d_match, db->n, R, W, d_hits, s, eng->d_gate.as<uint32_t>())) != hipSuccess)
-        return eng->hipfail(e, "launch hits");
-    if ((e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), db->n, W, eng->d_gate.as<uint32_t>(), force,
-                                  s)) != hipSuccess)
-        return eng->hipfail(e, "hits gate");
+    // the streaming counters (returning at once when the kernels counted); their block (0, 0) also
+    // sets the next evaluation's gate from this one's true pairs and resets the pair count
+    if (R && db->n) {
+        if ((e = mxp_launch_hits(d_match, db->n, R, W, d_hits, s, gate, eng->d_stats.as<unsigned long long>(), gate_next,
+                                 force)) != hipSuccess)
+            return eng->hipfail(e, "launch hits");
+    } else {
+        if ((e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), db->n, W, gate_next, force, s)) != hipSuccess)
+            return eng->hipfail(e, "hits gate");
+        if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
+    }
+    eng->gate_par ^= 1u;
     if ((e = hipEventRecord(eng->stats_ev, s)) != hipSuccess) return eng->hipfail(e, "stats event");
     eng->stats_pending = true;
     return MXP_OK;

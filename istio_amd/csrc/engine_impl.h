@@ -30,11 +30,12 @@ extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hi
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
 extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
 extern "C" hipError_t mxp_launch_dtp_sort(const mxp_kargs* args, hipStream_t s);
-extern "C" hipError_t mxp_launch_dtp_apply(const mxp_kargs* args, hipStream_t s);
 extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t s);
 extern "C" hipError_t mxp_launch_vt_eval(const mxp_kargs* args, uint32_t tiles, uint32_t wchunks, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
-                                      unsigned long long* hits, hipStream_t s, const uint32_t* gate = nullptr);
+                                      unsigned long long* hits, hipStream_t s, const uint32_t* gate = nullptr,
+                                      unsigned long long* stats = nullptr, uint32_t* gate_next = nullptr,
+                                      uint32_t force = 0);
 extern "C" hipError_t mxp_launch_hits_gate(const unsigned long long* stats, uint32_t n, uint32_t n_words,
                                            uint32_t* gate, uint32_t force, hipStream_t s);
 
@@ -297,6 +298,7 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t dtp_cap = 2048, dtp_ovf_cap = 1u << 22;
     DevBuf d_dtp_ent, d_dtp_n, d_dtp_ovf, d_dtp_ovf_n, d_dtp_slots, d_dtp_qn;
     bool last_dtp = false;  // the last launch deferred its index pairs (mxp_kernel_times [2])
+    uint32_t dtp_par = 0;   // d_dtp_ovf_n holds two counter sets: this launch's and the next one's
     // MXP_TRACE=1: phase times of evaluations / Resolves on stderr (each phase synchronises the
     // stream first, so traced calls are slower than untraced ones)
     bool trace = false;
@@ -530,7 +532,9 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t last_mask = 0;  // value-class slots of the last launch
     uint8_t* req_err_out = nullptr;  // compact error output of the next launch (kargs.req_err)
     const uint32_t* hits_gate_out = nullptr;  // fused-counter gate of the next launch (kargs.hits_gate)
-    DevBuf d_gate;                   // u32: fused counters on for the next evaluation (mxp_hits_gate_kernel)
+    DevBuf d_gate;                   // u32[2] by evaluation parity: fused counters on (set by the previous
+                                     // evaluation's mxp_hits_kernel block (0, 0), next_gate)
+    uint32_t gate_par = 0;
     bool wave_times = false;  // MXP_WAVE_TIMES: index kernel waves record {start, end, XCC}
     DevBuf d_wave_t;
     uint32_t wave_t_n = 0;

@@ -107,7 +107,9 @@ typedef struct mxp_kargs {
     uint32_t* dtp_ent;           // index kernel: [waves][dtp_cap] rule | plane << 23 | lane << 24
     uint32_t* dtp_n;             // [waves] entries recorded (<= dtp_cap)
     uint32_t* dtp_ovf_n;         // [2]: overflow pairs, overflow list full (-> the gated index re-run)
+    uint32_t* dtp_ovf_next;      // the other evaluation parity's [2], reset by mxp_dtp_sort_kernel
     uint32_t* dtp_ovf;           // [dtp_ovf_cap][2] (request, rule | plane << 31) past a wave's dtp_cap
+                                 // or a quad's 8 slots; OR-ed in by the gated index launch after the fill
     const uint32_t* dtp_chunk;   // [n_words] value-class fill chunk << 8 | group within it (~0: none)
     uint16_t* dtp_slots;         // [chunks][tiles * 256 lane quads][8] g << 8 | plane << 7 | request % 4 << 5 | bit
     uint8_t* dtp_qn;             // [chunks][tiles * 256] entries in each quad's slots (<= 8)

@@ -118,7 +118,7 @@ __device__ __forceinline__ bool counting(const mxp_kargs& A) {
 // Deferred pairs (kargs.dtp_ent): the index kernel runs before the value-class fill, so a true or
 // error pair is recorded in its wave's list (LDS counter; the wave of request q is q / 64, and every
 // pair of q is produced by that wave) and OR-ed in by the fill as it streams the words out.  Pairs
-// past a wave's dtp_cap go to the overflow list (OR-ed in after the fill by mxp_dtp_apply_kernel);
+// past a wave's dtp_cap go to the overflow list (OR-ed in after the fill by the gated index launch);
 // past that list's capacity a flag re-runs the index kernel with plain OR-s after the fill.
 __shared__ uint32_t g_dtpn[4];  // entries per wave of the index kernel's workgroup
 __device__ __forceinline__ void dtp_push(const mxp_kargs& A, uint32_t rule, uint32_t req, uint32_t plane) {
@@ -1454,6 +1454,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
 #define MXP_DTP_WIN 32u
 #define MXP_DTP_OVQ 512u
 extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs A) {
+    // the next evaluation's overflow counters (kargs.dtp_ovf_next): reset here, no memset launch
+    if (blockIdx.x == 0 && threadIdx.x < 2u && A.dtp_ovf_next) A.dtp_ovf_next[threadIdx.x] = 0u;
     __shared__ uint32_t cnt[MXP_DTP_WIN * 256u];
     __shared__ uint32_t ovq[MXP_DTP_OVQ][2];
     __shared__ uint32_t ovn, ovbase;
@@ -1515,16 +1517,6 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
     }
 }
 
-// Deferred pairs past a wave's capacity, OR-ed in after the fill
-extern "C" __global__ __launch_bounds__(256) void mxp_dtp_apply_kernel(mxp_kargs A) {
-    const uint32_t n = min(uni(A.dtp_ovf_n[0]), A.dtp_ovf_cap);
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const uint32_t req = A.dtp_ovf[2ull * i], e = A.dtp_ovf[2ull * i + 1];
-        const uint32_t rule = e & 0x7FFFFFFFu;
-        uint32_t* out = (e >> 31) ? A.out_err : A.out_match;
-        atomicOr(out + (uint64_t)(rule >> 5) * A.n + req, 1u << (rule & 31u));
-    }
-}
 
 // Guard-index phase: the continuing pairs of indexed rules (`attr == K && <continuation>`), found
 // per request by a hash lookup of its column value instead of by comparing against every rule.
@@ -1711,8 +1703,17 @@ namespace {
 
 template <bool kRefs, bool kNfa = kRefs, bool kDtp = false>
 __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
-    // the re-run after an overflowed deferred-pair list (kargs.dtp_gate): nothing to do unless it filled
-    if (A.dtp_gate && uni(*A.dtp_gate) == 0u) return;
+    // after the fill (kargs.dtp_gate): the deferred pairs' overflow list OR-ed in, then -- only when
+    // that list filled -- every pair again
+    if (A.dtp_gate) {
+        const uint32_t no = min(uni(A.dtp_ovf_n[0]), A.dtp_ovf_cap);
+        for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < no; i += gridDim.x * 256u) {
+            const uint32_t q = A.dtp_ovf[2ull * i], e = A.dtp_ovf[2ull * i + 1];
+            const uint32_t rule = e & 0x7FFFFFFFu;
+            atomicOr(((e >> 31) ? A.out_err : A.out_match) + (uint64_t)(rule >> 5) * A.n + q, 1u << (rule & 31u));
+        }
+        if (uni(*A.dtp_gate) == 0u) return;
+    }
     const uint64_t t_start = A.wave_t ? (uint64_t)wall_clock64() : 0ull;
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
@@ -2002,10 +2003,24 @@ __device__ __forceinline__ void hits_body(const uint32_t* __restrict__ row, uint
 
 }  // namespace
 
+// The next evaluation's fused / streamed choice (block (0, 0), before anything else reads it): gate
+// = 1 when this evaluation's guard-index true pairs were few enough (stats x 125 <= words x
+// requests: one atomic per true pair costs less than re-reading the match bitmap), and the pair
+// count reset for that evaluation.  force: 1 always fused, 2 never.
+__device__ __forceinline__ void next_gate(unsigned long long* stats, uint32_t* gate_next, uint32_t n, uint32_t force) {
+    if (!gate_next || blockIdx.x || blockIdx.y || threadIdx.x) return;
+    const unsigned long long v = *stats;
+    *gate_next = force == 1u ? 1u : force == 2u ? 0u : (v * 125ull <= (unsigned long long)gridDim.x * n ? 1u : 0u);
+    *stats = 0ull;
+}
+
 extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t* __restrict__ match, uint32_t n,
                                                                   uint32_t n_rules,
                                                                   unsigned long long* __restrict__ hits,
-                                                                  const uint32_t* __restrict__ gate) {
+                                                                  const uint32_t* __restrict__ gate,
+                                                                  unsigned long long* stats, uint32_t* gate_next,
+                                                                  uint32_t force) {
+    next_gate(stats, gate_next, n, force);
     if (gate && *gate) return;  // the evaluation kernels counted (fused)
     hits_body<true>(match + (uint64_t)blockIdx.x * n, n, n_rules, hits);
 }
@@ -2014,7 +2029,10 @@ extern "C" __global__ __launch_bounds__(256) void mxp_hits_kernel(const uint32_t
 extern "C" __global__ __launch_bounds__(256) void mxp_hits_ragged_kernel(const uint32_t* __restrict__ match, uint32_t n,
                                                                          uint32_t n_rules,
                                                                          unsigned long long* __restrict__ hits,
-                                                                         const uint32_t* __restrict__ gate) {
+                                                                         const uint32_t* __restrict__ gate,
+                                                                         unsigned long long* stats, uint32_t* gate_next,
+                                                                         uint32_t force) {
+    next_gate(stats, gate_next, n, force);
     if (gate && *gate) return;
     hits_body<false>(match + (uint64_t)blockIdx.x * n, n, n_rules, hits);
 }
@@ -2056,11 +2074,6 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
 
 extern "C" hipError_t mxp_launch_dtp_sort(const mxp_kargs* args, hipStream_t s) {
     hipLaunchKernelGGL(mxp_dtp_sort_kernel, dim3(args->dtp_tiles), dim3(256), 0, s, *args);
-    return hipGetLastError();
-}
-
-extern "C" hipError_t mxp_launch_dtp_apply(const mxp_kargs* args, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_dtp_apply_kernel, dim3(64), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 
@@ -2117,7 +2130,8 @@ extern "C" hipError_t mxp_launch_hits_gate(const unsigned long long* stats, uint
 }
 
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
-                                      unsigned long long* hits, hipStream_t s, const uint32_t* gate) {
+                                      unsigned long long* hits, hipStream_t s, const uint32_t* gate,
+                                      unsigned long long* stats, uint32_t* gate_next, uint32_t force) {
     // slices: enough blocks to fill the chip (~16 per CU), at least 32 words per thread, and at most
     // 255 32-word steps per thread (the byte-packed counters)
     const uint64_t per_block = 256ull * 32u;
@@ -2128,9 +2142,10 @@ extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_
     if (gy < 1) gy = 1;
     if (gy > 65535) return hipErrorInvalidValue;
     if ((n & 3u) == 0 && (((uintptr_t)match) & 15u) == 0)
-        hipLaunchKernelGGL(mxp_hits_kernel, dim3(n_words, (uint32_t)gy), dim3(256), 0, s, match, n, n_rules, hits, gate);
+        hipLaunchKernelGGL(mxp_hits_kernel, dim3(n_words, (uint32_t)gy), dim3(256), 0, s, match, n, n_rules, hits, gate,
+                           stats, gate_next, force);
     else
         hipLaunchKernelGGL(mxp_hits_ragged_kernel, dim3(n_words, (uint32_t)gy), dim3(256), 0, s, match, n, n_rules, hits,
-                           gate);
+                           gate, stats, gate_next, force);
     return hipGetLastError();
 }
