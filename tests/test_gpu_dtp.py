@@ -80,7 +80,7 @@ def test_deferred_pairs_device_identical(mxp, monkeypatch):
         dm = torch.zeros((Wd, batch.n), dtype=torch.int32, device="cuda:0")
         de = torch.zeros_like(dm)
         cm = torch.zeros_like(dm)
-        flags = torch.zeros(batch.n, dtype=torch.uint8, device="cuda:0")
+        flags = torch.ones(batch.n, dtype=torch.uint8, device="cuda:0")  # (stale flags must be cleared)
         hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
         hc = torch.zeros_like(hits)
         for _ in range(3):  # the fused / streamed choice follows the previous evaluation
@@ -146,7 +146,7 @@ def test_deferred_pairs_plain_fill_device_identical(mxp, monkeypatch):
         dm = torch.zeros((Wd, batch.n), dtype=torch.int32, device="cuda:0")
         de = torch.zeros_like(dm)
         cm = torch.zeros_like(dm)
-        flags = torch.zeros(batch.n, dtype=torch.uint8, device="cuda:0")
+        flags = torch.ones(batch.n, dtype=torch.uint8, device="cuda:0")  # (stale flags must be cleared)
         hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
         hc = torch.zeros_like(hits)
         for _ in range(3):
