@@ -1214,7 +1214,11 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
     const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0 && (q0 & 3u) == 0;
     const uint32_t nvt = uni(A.n_vt);
     uint32_t bad[4];
-    uint64_t cl[MXP_VT_MAX];  // 4 x u16 classes per active column
+    // 4 x u16 classes per active column, as (lo, hi) u32 pairs of one register vector: a merge
+    // entry's slot a is wave-uniform, so clv[2a] compiles to an indexed register move
+    // (s_set_gpr_idx_on) instead of a select over every slot
+    typedef uint32_t vcls __attribute__((ext_vector_type(2 * MXP_VT_MAX)));
+    vcls clv;
 #pragma unroll
     for (int r = 0; r < 4; r++) {
         const bool in = q0 + r < Q1;
@@ -1223,16 +1227,18 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
     }
 #pragma unroll
     for (uint32_t a = 0; a < MXP_VT_MAX; a++) {
-        cl[a] = 0;
+        uint64_t c = 0;
         if (a < nvt) {
             const uint16_t* C = A.vt_cls + (uint64_t)a * N;
             if (vec && q0 < Q1) {
-                cl[a] = *(const uint64_t*)(C + q0);
+                c = *(const uint64_t*)(C + q0);
             } else {
                 for (uint32_t r = 0; r < 4; r++)
-                    if (q0 + r < Q1) cl[a] |= (uint64_t)C[q0 + r] << (16u * r);
+                    if (q0 + r < Q1) c |= (uint64_t)C[q0 + r] << (16u * r);
             }
         }
+        clv[2 * a] = (uint32_t)c;
+        clv[2 * a + 1] = (uint32_t)(c >> 32);
     }
     const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
     DtpQueue dq;
@@ -1262,9 +1268,8 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
                                  : i < 128u ? __builtin_amdgcn_readlane(GE1, i - 64u) : uni(A.gvt[e0 + i]);
             const uint32_t a = ent >> 24, j = ent & 0xFFFFFFu;
             const uint32_t cap = __builtin_amdgcn_readlane(MV, 2u * a);
-            uint64_t c = cl[0];
-#pragma unroll
-            for (uint32_t x = 1; x < MXP_VT_MAX; x++) c = a == x ? cl[x] : c;
+            const uint32_t au = __builtin_amdgcn_readfirstlane(a);
+            const uint64_t c = (uint64_t)clv[2u * au] | (uint64_t)clv[2u * au + 1u] << 32;
             if constexpr (kLds) {
                 const uint32_t row = __builtin_amdgcn_readlane(PB, a) + (j - __builtin_amdgcn_readlane(PJ, a)) * cap;
 #pragma unroll
