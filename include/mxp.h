@@ -317,8 +317,10 @@ int mxp_set_pipeline(mxp_engine* eng, uint32_t min_requests, uint32_t max_chunks
  * records HIP events around its launches on the evaluation stream; mxp_kernel_times waits for the
  * last one and returns its kernel durations in ms: [0] guard + VM kernels, [1] guard-index kernel
  * (0 when it did not run).  Pipelined evaluations: [0] the evaluation stream's kernels of every
- * chunk (index kernels of all but the last chunk overlapped), [1] the exposed index tail; the sum
- * is the whole evaluation.  *n_out = values written. */
+ * chunk (index kernels of all but the last chunk overlapped), [1] the exposed index tail.
+ * Evaluations that deferred their index pairs into the fills ([2] = 1.0 when cap
+ * >= 3): [0] value-class kernels + guard-index kernel + pair sort, [1] the fills, guard / VM
+ * kernels and the overflow pass.  The sum is the whole evaluation.  *n_out = values written. */
 int mxp_set_timing(mxp_engine* eng, int on);
 int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out);
 /* Shape of the compiled rule set as the kernels see it: out[0] guarded rules (leading atom evaluated
