@@ -18,6 +18,12 @@ namespace {
 // (a uniform address would otherwise invite a scalar-cache load that cannot see the vector stores)
 __device__ __forceinline__ int64_t vload(const int64_t* p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
 
+__device__ __forceinline__ int64_t rfl64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uint64_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 __device__ __forceinline__ int64_t readlane64(int64_t v, uint32_t l) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)(uint64_t)v, l);
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), l);
@@ -36,7 +42,8 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, uint32_t l) {
 // request (later rolls in the batch are no-ops: rollingWindow.roll with behind == 0).
 extern "C" __global__ __launch_bounds__(256) void mxp_quota_kernel(mxp_quota_args A) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6);
+    // the key and its state are wave-uniform: scalar registers and branches for the whole replay
+    const uint32_t k = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
     if (k > A.n_keys) return;
     const uint32_t b = A.seg_start[k], e = A.seg_start[k + 1];
     if (b == e) return;
@@ -52,18 +59,32 @@ extern "C" __global__ __launch_bounds__(256) void mxp_quota_kernel(mxp_quota_arg
     uint32_t cur = 0;
     bool rolled = false;
     if (!window) {
-        in_use = vload(A.cells + k);
+        in_use = rfl64(vload(A.cells + k));
     } else {
-        avail = vload(A.avail + k);
-        cur = (uint32_t)__atomic_load_n(A.win_cur + k, __ATOMIC_RELAXED);
+        avail = rfl64(vload(A.avail + k));
+        cur = __builtin_amdgcn_readfirstlane((uint32_t)__atomic_load_n(A.win_cur + k, __ATOMIC_RELAXED));
     }
     int64_t delta = 0;
+    // the next 64 requests' (order, amount, best effort) gathers are issued before this batch's
+    // replay, so their latency hides behind it
+    uint32_t i_n = 0, bef_n = 0;
+    int64_t amt_n = 0;
+    if (b + lane < e) {
+        i_n = A.order[b + lane];
+        amt_n = A.amount[i_n];
+        bef_n = (uint32_t)A.best_effort[i_n];
+    }
     for (uint32_t base = b; base < e; base += 64u) {
         const uint32_t j = base + lane;
         const bool act = j < e;
-        const uint32_t i = act ? A.order[j] : 0u;
-        const int64_t amt = act ? A.amount[i] : 0;
-        const uint32_t bef = act ? (uint32_t)A.best_effort[i] : 0u;
+        const uint32_t i = i_n;
+        const int64_t amt = amt_n;
+        const uint32_t bef = bef_n;
+        if (base + 64u + lane < e) {
+            i_n = A.order[base + 64u + lane];
+            amt_n = A.amount[i_n];
+            bef_n = (uint32_t)A.best_effort[i_n];
+        }
         int64_t res = 0;
         const uint32_t cnt = min(64u, e - base);
         for (uint32_t t = 0; t < cnt; t++) {
@@ -72,7 +93,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_quota_kernel(mxp_quota_arg
             if (window && !rolled) {
                 // rollingWindow.roll(currentTick): release the slots that fell out of the window
                 rolled = true;
-                int64_t behind = A.tick - vload(A.win_tick + k);
+                int64_t behind = A.tick - rfl64(vload(A.win_tick + k));
                 if (behind > (int64_t)len) behind = len;
                 if (behind < 0) behind = 0;  // batch times are non-decreasing (the reference would index out of range)
                 int64_t freed = 0;
@@ -117,24 +138,32 @@ extern "C" __global__ __launch_bounds__(256) void mxp_quota_kernel(mxp_quota_arg
                     result = amount >= in_use ? in_use : amount;  // a cell freed entirely is deleted: same as empty
                     in_use -= result;
                 } else {
-                    // rollingWindow.release: from the current slot backwards
-                    int64_t total = 0;
-                    uint32_t idx = cur;
-                    for (uint32_t s = 0; s < len; s++) {
-                        const int64_t av = idx == cur ? cur_val : readlane64(vload(slots + idx), 0);
-                        const int64_t nv = av >= amount ? av - amount : 0;
-                        if (idx == cur) {
-                            cur_val = nv;
-                        } else if (lane == 0) {
-                            __atomic_store_n(slots + idx, nv, __ATOMIC_RELAXED);
+                    // rollingWindow.release: from the current slot backwards, each slot giving
+                    // min(its amount, what is still to release).  The current slot is in a register;
+                    // the older ones go 64 at a time: lane l holds slot cur - c - l, and an inclusive
+                    // prefix sum over the lanes says how much every slot before it gives, so the
+                    // chunk's slots are updated at once instead of one dependent step per slot
+                    int64_t total = cur_val < amount ? cur_val : amount;
+                    cur_val -= total;
+                    amount -= total;
+                    for (uint32_t c = 1; c < len && amount > 0; c += 64u) {
+                        const bool in = c + lane < len;
+                        const uint32_t idx = (cur + len - ((c + lane) % len)) % len;
+                        const int64_t av = in ? vload(slots + idx) : 0;
+                        int64_t incl = av;
+#pragma unroll
+                        for (uint32_t off = 1; off < 64u; off <<= 1) {
+                            const int64_t up = (int64_t)__shfl_up((long long)incl, off, 64);
+                            if (lane >= off) incl += up;
                         }
-                        if (av >= amount) {
-                            total += amount;
-                            break;
-                        }
-                        total += av;
-                        amount -= av;
-                        idx = idx == 0 ? len - 1 : idx - 1;
+                        const int64_t before = incl - av, want = amount - before;
+                        const int64_t give = want <= 0 ? 0 : want < av ? want : av;
+                        if (in && give > 0) __atomic_store_n(slots + idx, av - give, __ATOMIC_RELAXED);
+                        __threadfence_block();
+                        const int64_t chunk = readlane64(incl, 63);
+                        const int64_t took = chunk < amount ? chunk : amount;
+                        total += took;
+                        amount -= took;
                     }
                     avail += total;
                     result = total;

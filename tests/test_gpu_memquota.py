@@ -77,3 +77,25 @@ def test_device_out_of_range_keys_granted_zero(eng):
     want_delta = np.zeros(K, dtype=np.int64)
     np.add.at(want_delta, keys[~bad].astype(np.int64), (np.sign(amounts) * want)[~bad])  # allocs - frees
     assert np.array_equal(delta.cpu().numpy(), want_delta)
+
+
+def test_release_across_many_window_slots(eng):
+    """A 60 s window (600 slots) filled one tick at a time, then frees that walk back over more than
+    64 slots at once (the kernel releases 64 slots per step with a prefix sum over the lanes),
+    including frees larger than everything held; two keys so the workgroup has a second wave."""
+    mx = [100_000, 100_000]
+    vd = [60 * 10**9, 60 * 10**9]
+    q = eng.quota_create(mx, vd)
+    ref = M.Memquota({k: (mx[k], vd[k]) for k in range(2)})
+    rng = np.random.default_rng(7)
+    now = BASE_NS
+    for step in range(260):  # one batch per tick (100 ms): allocations land in distinct slots
+        keys = np.array([0, 1, 0, 1], dtype=np.uint32)
+        amounts = rng.integers(1, 5, size=4).astype(np.int64)
+        if step in (150, 200, 259):  # frees spanning many slots, then one larger than all held
+            amounts = np.array([-70, -90, -400, -5000], dtype=np.int64)
+        be = np.zeros(4, dtype=np.uint8)
+        got = q.alloc(keys, amounts, be, now)
+        want = np.array([ref.handle(int(k), int(a), bool(e), now) for k, a, e in zip(keys, amounts, be)])
+        assert np.array_equal(got, want), (step, got, want)
+        now += 100_000_000
