@@ -202,7 +202,8 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         std::vector<uint32_t> vcol(n, MXP_VM_DONE);
         std::map<uint32_t, uint32_t> count;
         for (uint32_t i = 0; i < n; i++) {
-            if (rules[i].status != MXP_RULE_OK) continue;
+            // (mxp_vt_eval_kernel has the MXP_VM_MAXREG register file)
+            if (rules[i].status != MXP_RULE_OK || rules[i].low.nregs > MXP_VM_MAXREG) continue;
             uint32_t col = MXP_VM_DONE;
             bool ok = true;
             for (uint32_t p = off[i]; p < off[i + 1] && ok; p++) {
@@ -598,11 +599,16 @@ int mxp_engine::build_plan(Plan& P) {
         const uint32_t andm = G.guarded & ~(G.only | G.orm);
         G.vm = ((G.all & ~G.guarded) | G.orm | (andm & ~G.indexed)) != 0;
     }
-    std::vector<uint32_t> glean, gvm, gall(W), fill_masks;
+    std::vector<uint32_t> glean, gvm, gall, gdeep, fill_masks;
     std::vector<mxp_fill> fills;
     P.n_gfill = 0;
+    // groups holding a rule with more live values than MXP_VM_MAXREG (lower.cpp colouring): their
+    // VM runs in the kernels with the MXP_VM_DEEPREG register file, in every mode
+    std::vector<uint8_t> deep(W, 0);
+    for (uint32_t i = 0; i < n; i++)
+        if (!excluded[i] && rules[i].low.ok && rules[i].low.nregs > MXP_VM_MAXREG) deep[i / 32] = 1;
     for (uint32_t g = 0; g < W; g++) {
-        gall[g] = g;
+        (deep[g] ? gdeep : gall).push_back(g);
         const mxp_group& G = groups[g];
         const bool has_vt = gvt_off[g + 1] > gvt_off[g];
         // uniform indexed group: every rule indexed, one guard column, nothing compared in-wave --
@@ -638,6 +644,7 @@ int mxp_engine::build_plan(Plan& P) {
             continue;
         }
         // the lean kernels carry no value-class merge: such groups go to the VM kernel
+        if (deep[g]) continue;
         (G.vm || has_vt ? gvm : glean).push_back(g);
     }
     // chunks with value-class merge entries go to mxp_vtfill_kernel
@@ -659,6 +666,8 @@ int mxp_engine::build_plan(Plan& P) {
             if (segs[G.seg0 + k].col < MXP_CC) P.lean_cc |= 1u << segs[G.seg0 + k].col;
     }
     P.n_gvm = (uint32_t)gvm.size();
+    P.n_gall = (uint32_t)gall.size();
+    P.n_gdeep = (uint32_t)gdeep.size();
     P.n_segs = (uint32_t)segs.size();
 
     // dense canonical rules: indexed rules with many duplicates, true pairs injected per bitmap word
@@ -744,6 +753,7 @@ int mxp_engine::build_plan(Plan& P) {
     if ((rc = put(P.d_fill_masks, fill_masks.data(), fill_masks.size() * 4, "upload fill masks"))) return rc;
     if ((rc = put(P.d_gvm, gvm.data(), gvm.size() * 4, "upload gvm"))) return rc;
     if ((rc = put(P.d_gall, gall.data(), gall.size() * 4, "upload gall"))) return rc;
+    if ((rc = put(P.d_gdeep, gdeep.data(), gdeep.size() * 4, "upload gdeep"))) return rc;
     if ((rc = put(P.d_gk, gk.data(), gk.size() * 8, "upload gk"))) return rc;
     if ((rc = put(P.d_idx, idx.data(), idx.size() * sizeof(mxp_index), "upload idx"))) return rc;
     if ((rc = put(P.d_hents, hents.data(), hents.size() * sizeof(mxp_hent), "upload hents"))) return rc;
@@ -1114,22 +1124,33 @@ int mxp_engine::pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H)
         for (uint64_t s = 0; s < S; s++)
             if (ok[s]) H.tsof[s] = MXP_FH(MXP_TIMESTAMP, time_id(ts[s].first, ts[s].second));
     }
-    // run-time regexp patterns: every distinct string of a pattern column, compiled once per batch
+    // run-time regexp patterns: every distinct string a pattern can take in this batch (pattern
+    // columns, map values, constants; lower.cpp provenance), compiled once per batch
     if (need_rxof) {
         H.rxof.assign(S, MXP_RXOF_SYNTAX);
         std::vector<uint8_t> done(S, 0);
-        for (uint32_t c : rx_cols) {
+        auto add = [&](uint64_t id) {
+            if (id >= S || done[id]) return;
+            done[id] = 1;
+            mxp::Dfa d;
+            std::string e;
+            const int rc = mxp::regex_compile({std::string(str_at(id))}, kRegexStates, &d, &e);
+            H.rxof[id] = rc == mxp::RX_OK ? H.rxb.add(d) : rc == mxp::RX_SYNTAX ? MXP_RXOF_SYNTAX : MXP_RXOF_UNSUPPORTED;
+        };
+        for (uint32_t c : rx_pattern_cols()) {
             const uint8_t* k = H.kinds.data() + (size_t)c * n;
             const uint64_t* v = H.vals.data() + (size_t)c * n;
-            for (uint32_t q = 0; q < n; q++) {
-                if (k[q] != MXP_STRING || v[q] >= S || done[v[q]]) continue;
-                done[v[q]] = 1;
-                mxp::Dfa d;
-                std::string e;
-                const int rc = mxp::regex_compile({std::string(str_at(v[q]))}, kRegexStates, &d, &e);
-                H.rxof[v[q]] = rc == mxp::RX_OK ? H.rxb.add(d) : rc == mxp::RX_SYNTAX ? MXP_RXOF_SYNTAX : MXP_RXOF_UNSUPPORTED;
-            }
+            for (uint32_t q = 0; q < n; q++)
+                if (k[q] == MXP_STRING) add(v[q]);  // (VC_VALUE == MXP_STRING for virtual columns)
         }
+        for (uint32_t c : rx_mapcols) {
+            const uint8_t* k = H.kinds.data() + (size_t)c * n;
+            const uint64_t* v = H.vals.data() + (size_t)c * n;
+            for (uint32_t q = 0; q < n; q++)
+                if (k[q] == MXP_STRING_MAP)
+                    for (uint32_t e = H.moff[v[q]]; e < H.moff[v[q] + 1]; e++) add(H.mv[e]);
+        }
+        for (uint32_t sid_c : rx_consts) add(sid_c);
     }
     db->overlay.finish();
     return MXP_OK;
@@ -1399,8 +1420,9 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         const DevBuf* list;
         uint32_t n;
         int vm;
-    } parts[2] = {{guards_on ? &P->d_glean : &P->d_gall, guards_on ? P->n_glean : 0u, 0},
-                  {guards_on ? &P->d_gvm : &P->d_gall, guards_on ? P->n_gvm : A.n_words, 1}};
+    } parts[3] = {{guards_on ? &P->d_glean : &P->d_gall, guards_on ? P->n_glean : 0u, 0},
+                  {guards_on ? &P->d_gvm : &P->d_gall, guards_on ? P->n_gvm : P->n_gall, 1},
+                  {&P->d_gdeep, P->n_gdeep, 2}};  // groups with deep rules (MXP_VM_DEEPREG registers)
     // a request window (error recomputation) or the whole batch, possibly in pipelined chunks:
     // the index kernel of chunk c (which ORs its true / error bits into the words the fill, guard
     // and VM kernels wrote) runs on the side stream while chunk c + 1's fill streams its stores
@@ -1672,6 +1694,8 @@ std::string mxp_engine::format_error(const mxp_bag_batch* b, const mxp_dbatch* d
                "' to TIMESTAMP. expected format: '2006-01-02T15:04:05Z07:00'";
     case ERR_MEMBER: return "member lookup failed: '" + string_of(db, r.aux) + "'";
     case ERR_UNDERFLOW: return "stack underflow";
+    case ERR_OVERFLOW: return "stack overflow";
+    case ERR_HEAP: return "heap overflow";
     case ERR_REGEX: case ERR_REGEX_UNSUPPORTED: {
         // regexp.MatchString's error: the pattern's compile error (Go's text); or why this engine
         // cannot compile it (a known divergence, reported rather than approximated)
@@ -1686,6 +1710,7 @@ std::string mxp_engine::format_error(const mxp_bag_batch* b, const mxp_dbatch* d
     case PANIC_EXTARG: return "reflect: Call using a value of the wrong type";
     case PANIC_NOTBOOL: return "interpreter.Result: result is not bool";
     case PANIC_CONV: return "interface conversion: interface {} is not string";
+    case PANIC_INDEX: return "runtime error: index out of range";
     default: return "error code " + std::to_string(r.code);
     }
 }

@@ -190,7 +190,17 @@ struct mxp_engine : public mxp::LowerTables {
     std::map<std::string, std::pair<int32_t, std::string>> rx_ids;  // pattern -> (DFA | -1 | -2, error)
     mxp::DfaSetHost rx_set;
     std::vector<mxp::Dfa> rx_dfas;
-    std::set<uint32_t> rx_cols;  // columns holding run-time patterns
+    // run-time regexp pattern sources (lower.cpp provenance): columns, virtual map[key] columns
+    // (indices before the resolve columns are appended), map columns whose every value is a
+    // pattern, and rule-set constants merged into a pattern by `|`
+    std::set<uint32_t> rx_cols, rx_vcols, rx_mapcols, rx_consts;
+    // the packers' view: pattern columns in the batch layout (virtual columns after the C resolve
+    // columns)
+    std::vector<uint32_t> rx_pattern_cols() const {
+        std::vector<uint32_t> v(rx_cols.begin(), rx_cols.end());
+        for (uint32_t j : rx_vcols) v.push_back((uint32_t)cols.size() + j);
+        return v;
+    }
     DevBuf d_rx_hdr, d_rx_trans, d_rx_ascii, d_rx_hilo, d_rx_hicls;
     bool rx_nfa = false;         // some constant pattern compiled to a bit-parallel NFA (kargs.nfa)
 
@@ -212,13 +222,14 @@ struct mxp_engine : public mxp::LowerTables {
     // The kernels' tables for one set of value-class slots (mask 0: none, built at compile)
     struct Plan {
         uint32_t mask = 0;
-        uint32_t n_glean = 0, n_gvm = 0, lean_cc = 0, n_fills = 0, n_gfill = 0;
+        uint32_t n_glean = 0, n_gvm = 0, n_gall = 0, n_gdeep = 0, lean_cc = 0, n_fills = 0, n_gfill = 0;
         uint32_t n_idx = 0, n_indexed = 0, n_composite = 0, n_alias = 0, n_tmpls = 0, n_segs = 0;
         uint32_t n_dense = 0, n_inj = 0;
         bool post_tmpl = false;  // postings carry template codes (kargs.post_tmpl)
         DevBuf d_guards, d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_alias_off, d_aliases;
         DevBuf d_idx, d_hents, d_postings, d_plens;
-        DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all
+        DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all but deep
+        DevBuf d_gdeep;                 // groups with deep rules (MXP_VM_DEEPREG kernels), every mode
         DevBuf d_fills, d_fill_masks;   // chunks of uniform indexed groups (mxp_fill_kernel)
         DevBuf d_vtfills;               // ... those with value-class merge entries (mxp_vtfill_kernel)
         uint32_t n_vtfills = 0;
@@ -417,7 +428,14 @@ struct mxp_engine : public mxp::LowerTables {
     bool regex_const_match(int32_t dfa, const std::string& subject) override {
         return mxp::dfa_match_host(rx_dfas[(size_t)dfa], subject);
     }
-    void regex_column(uint32_t col) override { rx_cols.insert(col); }
+    void regex_source(int kind, const std::string& attr, const std::string& key, uint32_t sid) override {
+        switch (kind) {
+        case mxp::RX_SRC_COLUMN: rx_cols.insert(column(attr)); break;
+        case mxp::RX_SRC_VCOLUMN: rx_vcols.insert(vcolumn(attr, key)); break;
+        case mxp::RX_SRC_MAPVALS: rx_mapcols.insert(column(attr)); break;
+        default: rx_consts.insert(sid); break;
+        }
+    }
 
     int fail(int code, const std::string& msg) {
         last_error = msg;
@@ -453,6 +471,9 @@ struct mxp_engine : public mxp::LowerTables {
         rx_set = mxp::DfaSetHost();
         rx_dfas.clear();
         rx_cols.clear();
+        rx_vcols.clear();
+        rx_mapcols.clear();
+        rx_consts.clear();
         empty_sid = intern_string("");
     }
 

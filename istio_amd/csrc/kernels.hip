@@ -424,6 +424,14 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
         case VM_MOV:
             if (live) REG(d) = REG(a);
             break;
+        case VM_HEAP:  // reference heap count (only rules that can reach slot 63 carry it)
+            if (live) {
+                const uint64_t h = REG(d);
+                if (y != 0u && h == 63u) FAIL(ERR_HEAP, 0);
+                else if (h >= 64u) FAIL(PANIC_INDEX, 0);
+                else REG(d) = h + 1u;
+            }
+            break;
         case VM_REGEX:
         case VM_REGEXR:
         case VM_REGEXD:
@@ -868,6 +876,22 @@ extern "C" __global__ __launch_bounds__(256) void mxp_guard2_kernel(mxp_kargs A)
 // mxp_eval_kernel with referenced-attribute records (mxp_eval_refs)
 extern "C" __global__ __launch_bounds__(256) void mxp_eval_refs_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    eval_groups<true, true>(A, regs);
+}
+
+// Groups holding deep rules (programs with more than MXP_VM_MAXREG values live at once, e.g. nine
+// right-nested comparisons; lower.cpp colouring): the same VM over a 64-register file, 128 KB of
+// LDS -- one workgroup per CU, launched only for rule sets that have such rules (Plan::d_gdeep)
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_deep_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_DEEPREG][256];
+    eval_groups<true, false, false>(A, regs);
+}
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_deep_nfa_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_DEEPREG][256];
+    eval_groups<true, false, true>(A, regs);
+}
+extern "C" __global__ __launch_bounds__(256) void mxp_eval_deep_refs_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_DEEPREG][256];
     eval_groups<true, true>(A, regs);
 }
 
@@ -2043,7 +2067,13 @@ extern "C" __global__ __launch_bounds__(256) void mxp_hits_ragged_kernel(const u
 }
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s) {
-    if (vm && args->refs)
+    if (vm == 2 && args->refs)
+        hipLaunchKernelGGL(mxp_eval_deep_refs_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    else if (vm == 2 && args->nfa)
+        hipLaunchKernelGGL(mxp_eval_deep_nfa_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    else if (vm == 2)
+        hipLaunchKernelGGL(mxp_eval_deep_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
+    else if (vm && args->refs)
         hipLaunchKernelGGL(mxp_eval_refs_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
     else if (vm && args->nfa)
         hipLaunchKernelGGL(mxp_eval_nfa_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);

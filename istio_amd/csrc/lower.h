@@ -1,12 +1,11 @@
 // lower.h -- reference IL -> MXP VM bytecode (vm.h).
 //
-// The lowering abstract-interprets the IL of `compile_rule` over a typed value stack.  It accepts a
-// program when, at every instruction, all paths reaching it agree on the stack shape (so each
-// stack slot maps to one fixed register), all jumps go forward, and the reference's stack (64
-// words) and heap (63 allocations, interpreterRun.go:171-172) provably cannot overflow -- then the
-// reference's overflow/underflow/invalid-heap checks can never fire and the VM needs none of them.
-// Everything the reference compiler emits for real rules satisfies this; programs that don't are
-// reported (LoweredRule::ok == false) instead of being approximated.
+// The lowering abstract-interprets the IL of `compile_rule` over a typed value stack, one copy of
+// the code per (IL address, stack shape), so every stack slot maps to one fixed register and all
+// jumps go forward.  The reference's stack (64 words) and heap (64 slots) limits are reproduced
+// where a path can reach them ("stack overflow", "heap overflow", Go's index panic; lower.cpp).
+// A program the lowering cannot express (more than MXP_VM_MAXREG values live at once, more than
+// kMaxContexts shape contexts) is reported (LoweredRule::ok == false), not approximated.
 #pragma once
 
 #include <cstdint>
@@ -19,6 +18,8 @@
 namespace mxp {
 
 // Engine-global tables the lowering interns constants and columns into.
+enum RxSource { RX_SRC_COLUMN = 0, RX_SRC_VCOLUMN = 1, RX_SRC_MAPVALS = 2, RX_SRC_CONST = 3 };
+
 class LowerTables {
   public:
     virtual ~LowerTables() = default;
@@ -32,8 +33,9 @@ class LowerTables {
     // constant regexp pattern -> rule-set DFA index; -1 syntax error, -2 unsupported (err says why)
     virtual int32_t regex_const(const std::string& pattern, std::string* err) = 0;
     virtual bool regex_const_match(int32_t dfa, const std::string& subject) = 0;
-    // string column whose values are used as run-time regexp patterns (the packer compiles them)
-    virtual void regex_column(uint32_t col) = 0;
+    // values used as run-time regexp patterns (the packer compiles each distinct one per batch):
+    // an attribute's string values, a map attribute's [key] values or all its values, a constant
+    virtual void regex_source(int kind, const std::string& attr, const std::string& key, uint32_t sid) = 0;
 };
 
 struct LoweredRule {

@@ -352,7 +352,7 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
             rx_v.push_back(val);
         };
         bool empty_done = false;
-        for (uint32_t c : rx_cols) {
+        for (uint32_t c : rx_pattern_cols()) {
             if (c >= ncol || src[c] < 0) continue;
             const uint8_t* k = b->kinds[src[c]];
             const uint64_t* v = b->values[src[c]];
@@ -380,6 +380,23 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
                 add(text_of(sv), (uint32_t)sv);
             }
         }
+        // every value of a map whose lookups with run-time keys are patterns
+        for (uint32_t c : rx_mapcols) {
+            if (c >= ncol || src[c] < 0) continue;
+            const uint8_t* k = b->kinds[src[c]];
+            const uint64_t* v = b->values[src[c]];
+            for (uint32_t q = 0; q < n; q++) {
+                if (k[q] != MXP_STRING_MAP) continue;
+                for (uint64_t e2 = b->map_offsets[v[q]]; e2 < b->map_offsets[v[q] + 1]; e2++) {
+                    const uint64_t sv = b->map_values[e2];
+                    if (sv >= NS || seen[sv]) continue;
+                    seen[sv] = 1;
+                    add(text_of(sv), (uint32_t)sv);
+                }
+            }
+        }
+        // rule-set constants that reach a pattern (`m["k"] | "^x"`), by their engine string id
+        for (uint32_t sid_c : rx_consts) add(std::string_view(gstrs[sid_c]), kRxDirect | sid_c);
     }
     if ((rc = alloc(db->rxof, need_rxof ? S * 4 : 0, "rxof"))) return rc;
     if (need_rxof) {

@@ -11,7 +11,8 @@
 
 #include <stdint.h>
 
-#define MXP_VM_MAXREG 8      // registers (reference stack slots) per rule
+#define MXP_VM_MAXREG 8      // registers (reference stack slots) per rule in the hot kernels
+#define MXP_VM_DEEPREG 64    // ... in the deep-rule VM kernels (rules with more values live at once)
 #define MXP_VM_WAKE 0x80u    // op flag: some jump lands on this instruction
 #define MXP_VM_DONE 0xFFFFFFFFu
 
@@ -48,6 +49,8 @@ enum mxp_vm_op {
     VM_REGEX = 29,   // d <- regexp.MatchString(<rule-set DFA x>, string r[a])
     VM_REGEXD = 30,  // d <- regexp.MatchString(string r[a], string r[b]): pattern DFA from the batch's rxof table
     VM_REGEXR = 31,  // d <- regexp.MatchString(<rule-set DFA r[b]>, string r[a])   (templates: hoisted REGEX)
+    VM_HEAP = 32,    // reference heap count r[d] (rules that can reach slot 63, lower.cpp): y = 1 checked
+                     // allocation (r[d] == 63 -> "heap overflow"); r[d] >= 64 -> index panic; else r[d]++
 };
 
 // Leading-atom guard of a rule (vmopt.cpp): the rule's program starts with
@@ -257,11 +260,15 @@ enum mxp_err_code {
     ERR_UNSUPPORTED = 11,// construct not lowered by this engine build   aux = rule
     ERR_UNDERFLOW = 12,  // "stack underflow" (interpreterRun.go:1148) -- reachable from OR chains
     ERR_REGEX_UNSUPPORTED = 13,  // batch pattern this engine cannot compile (Unicode classes / folding)   aux = pattern string id
+    ERR_OVERFLOW = 14,   // "stack overflow" (interpreterRun.go:1145-1147)
+    ERR_HEAP = 15,       // "heap overflow" (interpreterRun.go:1154-1156)
     PANIC_MAPTYPE = 32,  // il.MapGet on a non-map value ("Unknown map type")
     PANIC_EXTARG = 33,   // reflect.Call with a wrong dynamic type (ip_equal / timestamp_equal)
     PANIC_NOTBOOL = 34,  // Result.AsBool on a non-bool result
     PANIC_STATIC = 35,   // compile-time panic in the reference
     PANIC_CONV = 36,     // interface conversion: heap value is not a string
+    PANIC_INDEX = 37,    // Go "index out of range": heap slot 64 (after an extern's unchecked allocation)
+                         // or a result word past the 64-word stack (interpreterRun.go:899-900)
 };
 
 // 16-byte instruction; loaded with one scalar s_load_dwordx4 per step.

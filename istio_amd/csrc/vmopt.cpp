@@ -20,27 +20,29 @@ static bool is_terminal(const mxp_vm_ins& i) {
 }
 
 // registers read / written (bit masks)
-static uint32_t reads(const mxp_vm_ins& i) {
+static uint64_t reads(const mxp_vm_ins& i) {
     switch (opof(i)) {
     case VM_EQ: case VM_LOGIC: case VM_LOOKUP: case VM_STRFN: case VM_IPEQ: case VM_TSEQ: case VM_REGEXD:
     case VM_REGEXR:
-        return (1u << i.a) | (1u << i.b);
+        return (1ull << i.a) | (1ull << i.b);
     case VM_EQK: case VM_NOT: case VM_LOGICK: case VM_JZ: case VM_JNZ: case VM_RET: case VM_LOOKUPK:
     case VM_STRFNK: case VM_IPOF: case VM_TSOF: case VM_FTOS: case VM_STOF: case VM_JZRET: case VM_JNZRET:
     case VM_MOV: case VM_REGEX:
-        return 1u << i.a;
+        return 1ull << i.a;
+    case VM_HEAP:
+        return 1ull << i.d;
     default:
         return 0;
     }
 }
 
-static uint32_t writes(const mxp_vm_ins& i) {
+static uint64_t writes(const mxp_vm_ins& i) {
     switch (opof(i)) {
     case VM_RES: case VM_TRES: case VM_VCOL: case VM_CONST: case VM_EQ: case VM_EQK: case VM_NOT: case VM_LOGIC:
     case VM_LOGICK: case VM_LOOKUP: case VM_LOOKUPK: case VM_STRFN: case VM_STRFNK: case VM_IPOF: case VM_TSOF:
     case VM_IPEQ: case VM_TSEQ: case VM_FTOS: case VM_STOF: case VM_MOV: case VM_REGEX: case VM_REGEXD:
-    case VM_REGEXR:
-        return 1u << i.d;
+    case VM_REGEXR: case VM_HEAP:
+        return 1ull << i.d;
     default:
         return 0;
     }
@@ -59,8 +61,8 @@ static bool is_pure(const mxp_vm_ins& i) {
 
 // Deterministic bool result of executing from pc with every register unknown, or -1.
 static int det_result(const std::vector<mxp_vm_ins>& c, size_t pc) {
-    bool known[MXP_VM_MAXREG] = {false};
-    uint64_t val[MXP_VM_MAXREG] = {0};
+    bool known[MXP_VM_DEEPREG] = {false};
+    uint64_t val[MXP_VM_DEEPREG] = {0};
     for (int steps = 0; steps < 64 && pc < c.size(); steps++) {
         const mxp_vm_ins& i = c[pc];
         switch (opof(i)) {
@@ -198,7 +200,7 @@ static void optimize_once(std::vector<mxp_vm_ins>& c) {
         if (!is_terminal(c[p]) && p + 1 < n) reach[p + 1] = true;
     }
     // 4. liveness (forward-only DAG: one backward sweep) and dead pure-op elimination
-    std::vector<uint32_t> live_in(n + 1, 0);
+    std::vector<uint64_t> live_in(n + 1, 0);
     std::vector<bool> keep(n, true);
     for (size_t p = n; p-- > 0;) {
         if (!reach[p]) {
@@ -207,10 +209,10 @@ static void optimize_once(std::vector<mxp_vm_ins>& c) {
             continue;
         }
         const mxp_vm_ins& i = c[p];
-        uint32_t out = 0;
+        uint64_t out = 0;
         if (!is_terminal(i) && p + 1 < n) out |= live_in[p + 1];
         if (vm_is_jump(i)) out |= live_in[i.z];
-        uint32_t w = writes(i);
+        uint64_t w = writes(i);
         if (is_pure(i) && (w & out) == 0) {
             keep[p] = false;  // dead: forward to successor
             live_in[p] = out;
@@ -286,7 +288,7 @@ mxp_guard extract_guard(const std::vector<mxp_vm_ins>& c) {
 bool hoist_continuation(const std::vector<mxp_vm_ins>& code, uint32_t pc0, HoistedCont* out) {
     out->code.assign(code.begin() + pc0, code.end());
     out->consts.clear();
-    uint32_t used = 0;
+    uint64_t used = 0;
     for (const auto& i : out->code) used |= reads(i) | writes(i);
     uint32_t next = 0;
     while (used >> next) next++;
@@ -330,13 +332,13 @@ bool extract_second_prefix(const std::vector<mxp_vm_ins>& c, uint32_t pc0, Secon
     if (cont >= c.size()) return false;
     // forward dataflow over the continuation: registers that may still hold r / s (never rewritten
     // on some path from cont) must not be read
-    std::vector<uint32_t> stale(c.size() + 1, 0);
-    stale[cont] = (1u << r.d) | (1u << f.d);
+    std::vector<uint64_t> stale(c.size() + 1, 0);
+    stale[cont] = (1ull << r.d) | (1ull << f.d);
     for (size_t pc = cont; pc < c.size(); pc++) {
         const mxp_vm_ins& i = c[pc];
-        const uint32_t st = stale[pc];
+        const uint64_t st = stale[pc];
         if (reads(i) & st) return false;
-        const uint32_t w = writes(i);
+        const uint64_t w = writes(i);
         if (vm_is_jump(i)) {
             // TRES / try-LOOKUP write d only on the jump path
             if (i.z <= pc || i.z > c.size()) return false;

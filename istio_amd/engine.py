@@ -542,7 +542,8 @@ class Evaluator:
 
 
 PANIC_TEXTS = {"Unknown map type", "reflect: Call using a value of the wrong type",
-               "interpreter.Result: result is not bool", "interface conversion: interface {} is not string"}
+               "interpreter.Result: result is not bool", "interface conversion: interface {} is not string",
+               "runtime error: index out of range"}
 
 
 def decode_value(e: Engine, rule: int, v: int):

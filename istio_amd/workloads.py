@@ -249,6 +249,68 @@ def fuzz_rules(n, seed=7, depth=3):
     return [f.expr(depth) for _ in range(n)]
 
 
+def hard_fuzz_rules(n, seed=13):
+    """Rules at the reference VM's limits (interpreter.go:39-44): long `||` / `&&` chains whose
+    resolves and pushes reach heap slot 63 ("heap overflow", interpreterRun.go:171-172), nested
+    chains whose paths merge with different heap counts, `ip()` returns that take slot 63 without the
+    check so the next push is Go's index panic, `|` chains of comparisons that leave a value behind
+    each (up to and past the 64-word stack: "stack overflow"), right-nested comparisons with more
+    live values than the hot kernels' 8 registers (the deep kernels), and `matches` patterns
+    computed at run time (map values, `|` fallbacks, run-time map keys)."""
+    rng = np.random.default_rng(seed)
+    f = _Fuzz(rng)
+    vals = [v for v in _STR_VALS if v not in ("19ms",)]  # (a duration literal: type error)
+    atoms = [lambda: 'as == "%s"' % f.pick(vals), lambda: 'bs != "%s"' % f.pick(vals),
+             lambda: 'ar["%s"] == "%s"' % (f.pick(_KEYS), f.pick(vals)),
+             lambda: 'as.startsWith("%s")' % f.pick(["a", "ab", "st", ""]), lambda: "ai == %d" % int(rng.integers(0, 5)),
+             lambda: '"%s".matches(bs)' % f.pick(["^a", "b.*c", "^$"])]
+    pats = ['ar["%s"]' % k for k in _KEYS] + ["as", "bs", 'sm["a"]', "ar[as]", "(ar | br)[\"a\"]"]
+
+    # chain links that rarely decide the chain (false under ||, true under &&), so evaluations run
+    # deep into it; a few random atoms in between
+    quiet = {"||": [lambda: 'as == "zz%d"' % int(rng.integers(100)), lambda: 'ar["%s"] == "zz"' % f.pick(_KEYS),
+                    lambda: "ai == 99", lambda: 'bs.startsWith("zz")', lambda: '"^zz".matches(as)'],
+             "&&": [lambda: 'as != "zz%d"' % int(rng.integers(100)), lambda: 'ar["%s"] != "zz"' % f.pick(_KEYS),
+                    lambda: "ai != 99", lambda: 'bs.endsWith("zz") == false']}
+
+    def chain(k, op):
+        return (" %s " % op).join(f.pick(atoms)() if rng.random() < 0.05 else f.pick(quiet[op])()
+                                  for _ in range(k))
+
+    out = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.2:  # one chain at depth 0
+            out.append(chain(int(rng.integers(40, 90)), f.pick(["||", "&&"])))
+        elif r < 0.35:  # chains nested under && / || (merges with different heap counts)
+            out.append("(%s) && (%s)" % (chain(int(rng.integers(20, 50)), "||"), chain(int(rng.integers(10, 40)), "||")))
+        elif r < 0.45:  # slot 63 taken by an ip() return, then a checked push: index panic
+            k = int(rng.integers(58, 64))
+            out.append(chain(k, "||") + ' || ip(%s) == ip("%s") || %s' % (f.pick(["as", '"1.2.3.4"', 'ar["a"]']),
+                                                                        f.pick(["1.2.3.4", "10.0.0.1"]), f.pick(atoms)()))
+        elif r < 0.6:  # `|` garbage: each comparison leaves a bool behind
+            k = int(rng.integers(3, 80))
+            out.append(" | ".join(f.pick(["(ai == %d)" % int(rng.integers(0, 4)), "(ab == bb)", "(ad == 1.5)",
+                                          "(bi == ai)", '(as == "zz")', '(ar["a"] == "b")']) for _ in range(k)))
+        elif r < 0.75:  # right-nested comparisons: up to 70 values live
+            k = int(rng.integers(5, 72))
+            e = f.pick(["ab", "bb", "true"])
+            for _ in range(k):
+                e = "%s == (%s)" % (f.pick(["ab", "bb", "b1", "(ab | bb)"]), e)
+            out.append(e)
+        else:  # run-time patterns
+            p = f.pick(pats)
+            fb = f.pick(['"^a"', '"(x"', '"st.*"', "as", '"%s"' % f.pick(_REGEXES).replace("\\", "\\\\")])
+            form = rng.random()
+            if form < 0.4:
+                out.append("(%s | %s).matches(%s)" % (p, fb, f.pick(["as", "bs", 'ar["a"]'])))
+            elif form < 0.7:
+                out.append("(%s | %s | %s).matches(bs) && %s" % (p, f.pick(pats), fb, f.pick(atoms)()))
+            else:
+                out.append("%s || (%s | %s).matches(as)" % (f.pick(atoms)(), p, fb))
+    return out
+
+
 def guarded_fuzz_rules(n, seed=11, depth=2, random_tail=True):
     """Rules whose programs start with a leading atom (guard) -- `attr == K`, `attr != K`,
     `map["k"] == K` -- joined by &&, || or alone to a continuation that is either random or one of a

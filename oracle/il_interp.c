@@ -287,6 +287,8 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
 #define UNDERFLOW do { FAIL("stack underflow"); } while (0)
 #define OVERFLOW do { FAIL("stack overflow"); } while (0)
 #define HEAPOVF do { FAIL("heap overflow"); } while (0)
+    /* hp can reach 64 only through an extern's unchecked push (extern.go:212,235); the next
+     * checked push then writes heap[64]: Go's index panic */
 #define BADHEAP do { FAIL("invalid heap access"); } while (0)
 
     for (;;) {
@@ -348,6 +350,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
         case OP_ALoadS:
             t1 = p->code[ip++];
             if (hp == HEAP_SIZE - 1) HEAPOVF;
+            if (hp >= HEAP_SIZE) PANIC("runtime error: index out of range"); /* heap[64] after an extern push */
             if (t1 >= REGS) PANIC("runtime error: index out of range");
             t2 = hp;
             heap[hp++] = gv_string(str_ptr(p, t1), str_len(p, t1));
@@ -383,6 +386,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
             t1 = p->code[ip++];
             if (sp > STACK_SIZE - 1) OVERFLOW;
             if (hp == HEAP_SIZE - 1) HEAPOVF;
+            if (hp >= HEAP_SIZE) PANIC("runtime error: index out of range"); /* heap[64] after an extern push */
             t2 = hp;
             heap[hp++] = gv_string(str_ptr(p, t1), str_len(p, t1));
             opstack[sp++] = t2;
@@ -485,6 +489,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
             }
             if (tv.k != GV_STRING) return conv_err(r, "string", &tv, b);
             if (hp == HEAP_SIZE - 1) HEAPOVF;
+            if (hp >= HEAP_SIZE) PANIC("runtime error: index out of range"); /* heap[64] after an extern push */
             t2 = hp;
             heap[hp++] = tv;
             opstack[sp++] = t2;
@@ -539,6 +544,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
                 return 1;
             }
             if (hp == HEAP_SIZE - 1) HEAPOVF;
+            if (hp >= HEAP_SIZE) PANIC("runtime error: index out of range"); /* heap[64] after an extern push */
             t2 = hp;
             heap[hp++] = tv;
             opstack[sp++] = t2;
@@ -722,6 +728,9 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
                     PANIC("unknown extern");
                 }
                 uint32_t rsz = alloc_size(p->fn_ret[t1]);
+                /* interpreterRun.go:899-900 store two words; at sp - psz + 1 == 64 the second one is
+                 * past the 64-word opstack: Go's index panic */
+                if (sp - psz + 1 >= STACK_SIZE) PANIC("runtime error: index out of range");
                 opstack[sp - psz] = ro1;
                 opstack[sp - psz + 1] = ro2;
                 sp -= psz - rsz;
@@ -796,6 +805,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
             if (code == OP_TLookup) {
                 if (f) {
                     if (hp == HEAP_SIZE - 1) HEAPOVF;
+                    if (hp >= HEAP_SIZE) PANIC("runtime error: index out of range"); /* heap[64] after an extern push */
                     t3 = hp;
                     heap[hp++] = tv;
                     opstack[sp] = t3;
@@ -814,6 +824,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
                 tv = gv_string((const uint8_t*)"", 0);
             }
             if (hp == HEAP_SIZE - 1) HEAPOVF;
+            if (hp >= HEAP_SIZE) PANIC("runtime error: index out of range"); /* heap[64] after an extern push */
             t3 = hp;
             heap[hp++] = tv;
             opstack[sp++] = t3;
@@ -836,6 +847,7 @@ static int run(const oracle_prog* p, uint32_t fn_sid, const bagctx* bc, oracle_r
                 tv = gv_string((const uint8_t*)"", 0);
             }
             if (hp == HEAP_SIZE - 1) HEAPOVF;
+            if (hp >= HEAP_SIZE) PANIC("runtime error: index out of range"); /* heap[64] after an extern push */
             t3 = hp;
             heap[hp++] = tv;
             opstack[sp++] = t3;

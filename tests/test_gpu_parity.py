@@ -155,17 +155,56 @@ def test_c4_routes_parity(mxp):
 
 @pytest.mark.parametrize("seed", [7, 17])
 def test_fuzz_parity(mxp, seed):
-    """Random well- and ill-typed rules over random bags with missing / wrongly typed values."""
-    rules = W.fuzz_rules(600, seed=seed, depth=3)
+    """Random well- and ill-typed rules over random bags with missing / wrongly typed values, plus
+    the rules at the reference VM's limits (workloads.hard_fuzz_rules: long chains to heap slot 63,
+    index panics after an ip() return, `|` chains past the 64-word stack, right-nested comparisons
+    for the deep kernels, run-time regexp patterns).  Every rule compiles: no MXP_RULE_UNSUPPORTED."""
+    rules = W.fuzz_rules(600, seed=seed, depth=3) + W.hard_fuzz_rules(300, seed=seed + 2)
     bags = W.fuzz_bags(400, seed=seed + 1)
+    bags += W.fuzz_bags(200, seed=seed + 3, p_missing=0.03, p_wrong=0.01)
     batch = BagBatch.from_bags(bags, names=list(W.DEFAULT_TEST_MANIFEST))
     eng = mxp.Engine(0)
     eng.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
     st = eng.compile(rules)
-    keep = [i for i in range(len(rules)) if st[i] != 5]
-    assert len(keep) >= 0.9 * len(rules)
+    assert (st != 5).all(), [(rules[i][:80], eng.rule_error(i)) for i in np.where(st == 5)[0][:3]]
     ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
     compare(eng, ev, rules, batch)
+
+
+@pytest.mark.parametrize("knobs", [{}, {"MXP_DEBUG_FLAGS": "8"}, {"MXP_HOST_PACK": "1"}])
+def test_reference_limits_parity(mxp, knobs, monkeypatch):
+    """Rules that reach the reference VM's limits evaluate as the reference does instead of being
+    refused: "heap overflow" at slot 63 (interpreterRun.go:171-172), Go's index panic when an ip()
+    return took slot 63 (extern.go:232-237), "stack overflow" past 64 words, deep nesting in the
+    64-register kernels, and `matches` patterns computed at run time (externs.go:118-120).  Every
+    error pair's text is compared (compare(sample_msgs=10**6))."""
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    whitelist = " || ".join('as == "x%d"' % i for i in range(70))
+    rules = [whitelist, "(%s) && bs == \"abc\"" % whitelist, '(ar["a"] | "^x").matches(bs)',
+             '(ar["a"] | as).matches(bs)', '(ar[as] | "^a").matches(bs)', '(sm["b"] | br["a"] | "(x").matches(as)',
+             " || ".join('as == "x%d"' % i for i in range(62)) + ' || ip(as) == ip("1.2.3.4") || bs == "abc"',
+             " | ".join("(ai == %d)" % (i % 3) for i in range(70)), " | ".join('(as == "a%d")' % i for i in range(70)),
+             "ab == (" * 20 + "bb" + ")" * 20]
+    rules += W.hard_fuzz_rules(400, seed=5)
+    bags = W.fuzz_bags(600, seed=6, p_missing=0.03, p_wrong=0.01) + W.fuzz_bags(200, seed=9)
+    for i, b in enumerate(bags[:100]):  # whitelist hits at every position
+        b["as"] = "x%d" % (i % 72)
+    batch = BagBatch.from_bags(bags, names=list(W.DEFAULT_TEST_MANIFEST))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
+    st = eng.compile(rules)
+    assert (st == 0).all(), [(rules[i][:80], eng.rule_error(i)) for i in np.where(st != 0)[0][:3]]
+    ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
+    got, want = compare(eng, ev, rules, batch, sample_msgs=1500)
+    texts = {ev.eval_predicate(rules[r], batch, int(q))[1] for q, r in np.argwhere(want >= 2)[:20000:7]}
+    assert {"heap overflow", "stack overflow", "runtime error: index out of range"} <= texts, texts
+    assert (want[:, 0] == 1).sum() >= 60 and (want[:, 0] == 2).sum() > 100  # whitelist: hits, then heap overflow
+    # Eval mode runs whole programs (no guards, no index) through the same kernels
+    vals, codes = eng.eval_values(batch)
+    pc = np.where(want >= 2, 2, want)
+    boolean = np.array([eng.rule_types(i)[1] == 5 for i in range(len(rules))])
+    assert np.array_equal(np.minimum(codes[:, boolean], 2), pc[:, boolean])
 
 
 @pytest.mark.parametrize("knobs", [{}, {"MXP_DEBUG_FLAGS": "8"}, {"MXP_GPW": "1"}, {"MXP_DEBUG_FLAGS": "65536"}])

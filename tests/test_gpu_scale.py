@@ -7,6 +7,8 @@
   routing the engine has -- value classes + prefix index (default), value classes off, guard index
   off -- bit-identical bitmaps.
 * C2 at the bench size (10k x 1M): index on / off bit-identical.
+* C2 and C4 exactly as bench.py evaluates them (10k x 1M, compact output + fused hit counters, and
+  the bitmap output) against the oracle on a 4096-request sample, with error texts.
 The oracle (oracle/lists.py, lists_oracle.c, il_interp.c + goregex.c) is the checker; the engine runs
 through the C-ABI."""
 import numpy as np
@@ -112,3 +114,67 @@ def test_full_size_routings_bit_identical(mxp, monkeypatch, wl):
         assert torch.equal(dm, base[0]) and torch.equal(de, base[1]), flags
         del dm, de
     assert int(torch.count_nonzero(base[0])) > 100_000
+
+
+@pytest.mark.parametrize("wl", ["c2", "c4"])
+def test_benched_evaluations_against_oracle(mxp, wl):
+    """The evaluations bench.py times -- 10k rules x 1,048,576 requests, default routing, the compact
+    output (match bitmap + per-request error flags) with fused hit counters, three steps back to back
+    -- and the error-bitmap output, checked on a random 4096-request sample pair by pair against the
+    oracle (not only routing against routing, which would miss a bug common to all routings); the hit
+    counters against the bitmap; error texts of sampled error pairs from the host path's records."""
+    import torch
+    from istio_amd.engine import PANIC_TEXTS
+    if wl == "c4":
+        manifest, rules, batch = W.c4_workload(n_rules=10_000, n_requests=1 << 20, seed=4)
+    else:
+        manifest, rules, batch = W.c2_workload(n_rules=10_000, n_requests=1 << 20, seed=2)
+        rules = W.c2_rules(10_000, seed=2)[0]
+    R, N = len(rules), batch.n
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    db = eng.upload(batch)
+    Wd = (R + 31) // 32
+    s = torch.cuda.current_stream().cuda_stream
+    dm = torch.zeros((Wd, N), dtype=torch.int32, device="cuda:0")
+    req_err = torch.zeros(N, dtype=torch.uint8, device="cuda:0")
+    hits = torch.zeros(R, dtype=torch.int64, device="cuda:0")
+    for _ in range(3):
+        db.eval_compact(dm.data_ptr(), req_err.data_ptr(), hits.data_ptr(), s)
+    dm2 = torch.zeros_like(dm)
+    de2 = torch.zeros_like(dm)
+    db.eval(dm2.data_ptr(), de2.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(dm, dm2)
+    # hit counters: 3 x the true pairs of each rule, counted from the bitmap here
+    cnt = torch.zeros((Wd, 32), dtype=torch.int64, device="cuda:0")
+    for b in range(32):
+        cnt[:, b] = ((dm >> b) & 1).sum(dim=1)
+    assert torch.equal(hits, 3 * cnt.reshape(-1)[:R])
+    assert torch.equal(req_err.bool(), (de2 != 0).any(dim=0))
+    rng = np.random.default_rng(17)
+    sample = np.sort(rng.choice(N, 4096, replace=False))
+    m = dm2[:, torch.from_numpy(sample).to("cuda:0")].cpu().numpy().view(np.uint32)
+    e = de2[:, torch.from_numpy(sample).to("cuda:0")].cpu().numpy().view(np.uint32)
+    db.free()
+    del dm, dm2, de2, req_err, cnt
+    torch.cuda.empty_cache()
+    got = mxp.bits_to_codes(m, e, R)
+    sub = batch.subset(sample)
+    ev = oracle.OracleEvaluator(manifest)
+    want = oracle.oracle_matrix(ev, rules, sub, threads=16)
+    want_err = np.where(want >= 2, 2, want)
+    bad = np.argwhere(got != want_err)
+    assert bad.size == 0, [(int(sample[q]), int(r), int(got[q, r]), int(want_err[q, r])) for q, r in bad[:5]]
+    assert (want == 1).sum() > 4096 * (0.3 if wl == "c2" else 100)
+    # error texts: the host path over the whole batch (its bitmaps equal the device ones on the
+    # sample), then the records of sampled error pairs
+    hm, he = eng.eval_batch(batch)
+    assert np.array_equal(hm[:, sample], m) and np.array_equal(he[:, sample], e)
+    errs = np.argwhere(want >= 2)
+    assert len(errs) > 0 or wl == "c4"  # (C4's routes have no error pairs)
+    for q, r in errs[rng.choice(len(errs), min(300, len(errs)), replace=False)] if len(errs) else []:
+        st, msg = ev.eval_predicate(rules[r], sub, int(q))
+        gmsg = eng.pair_error(int(sample[q]), int(r))
+        assert gmsg == msg or (st == "panic" and gmsg in PANIC_TEXTS), (rules[r], int(sample[q]), gmsg, msg)

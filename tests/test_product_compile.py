@@ -100,3 +100,46 @@ def test_compiler_sessions(Engine):
                 assert e.rule_il_text(a).strip() == row["IL"].strip(), row["E"]
             checked += 1
     assert checked > 150
+
+
+def test_reference_limit_rules_compile(Engine):
+    """Rules at the reference VM's limits are lowered, not refused (MXP_RULE_UNSUPPORTED = 5): long
+    chains up to the heap limit (static per-path counts, or the VM_HEAP count register when paths
+    merge with different counts), `|` chains past the 64-word stack, right-nested comparisons
+    (coloured onto the deep kernels' 64 registers), run-time regexp patterns of every provenance."""
+    e = Engine(-1)
+    e.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
+    rules = W.hard_fuzz_rules(800, seed=21) + W.fuzz_rules(800, seed=22, depth=4)
+    rules.append(" | ".join('(as == "a%d")' % i for i in range(70)))  # straight line: static heap count
+    st = e.compile(rules)
+    assert (st != 5).all(), [(rules[i][:60], e.rule_error(i)) for i in np.where(st == 5)[0][:3]]
+    vm = {i: e.rule_vm_text(i) for i in range(len(rules)) if st[i] == 0}
+    assert any(" heap " in t for t in vm.values())  # the dynamic heap count
+    assert any("y=15 " in t and " err " in t for t in vm.values())  # a static "heap overflow" (ERR_HEAP)
+    assert any("y=14 " in t and " err " in t for t in vm.values())  # "stack overflow" (ERR_OVERFLOW)
+    assert any(" regexd " in t for t in vm.values())
+    # registers: the hot kernels' 8 unless the rule is deep (up to 64)
+    regs = [max(int(tok[2:]) for line in t.splitlines() for tok in line.split()[2:5]) for t in vm.values()]
+    assert max(regs) >= 8 and max(regs) < 64
+    # ordinary rules are lowered exactly as before: no heap register, registers from 0 by depth
+    plain = Engine(-1)
+    plain.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
+    assert (plain.compile(['as == "a" && bs.startsWith("b")']) == 0).all()
+    assert " heap " not in plain.rule_vm_text(0)
+
+
+def test_heap_panic_after_extern_in_oracle():
+    """The oracle's heap: an ip() return takes slot 63 without the check (extern.go:232-237); the next
+    checked push writes heap[64]: Go's "index out of range" panic, not "heap overflow"."""
+    import oracle
+    from istio_amd.bags import BagBatch
+    rule = " || ".join('as == "x%d"' % i for i in range(62)) + ' || ip(as) == ip("1.2.3.4") || bs == "abc"'
+    batch = BagBatch.from_bags([{"as": "1.2.3.4", "bs": "abc"}, {"as": "nope", "bs": "abc"}, {"as": "x3"}],
+                               names=list(W.DEFAULT_TEST_MANIFEST))
+    ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
+    assert ev.eval_predicate(rule, batch, 0) == ("panic", "runtime error: index out of range")
+    assert ev.eval_predicate(rule, batch, 1) == ("error", "could not convert nope to IP_ADDRESS")
+    assert ev.eval_predicate(rule, batch, 2) == ("ok", True)
+    chain = " || ".join('as == "x%d"' % i for i in range(70))
+    assert ev.eval_predicate(chain, batch, 1) == ("error", "heap overflow")
+    assert ev.eval_predicate(chain, batch, 2) == ("ok", True)
