@@ -103,6 +103,16 @@ UNICODE_KAT = [
     ("(?i)\\w", "K", True), ("(?i)[[:^lower:]]", "A", False), ("(?i)[[:^lower:]]", "1", True),
     ("[[:^lower:]]", "A", True), ("(?i)\\D", "1", False), ("(?i)[^k]", "K", False), ("(?i)[^k]", "x", True),
     ("(?i)ΣΑΣ", "σας", True), ("(?i)straße", "STRASSE", False), ("(?i)ß", "ẞ", True),
+    # Go 1.9's caseOrbit: U+0130 / U+0131 have upper / lower mappings but no C/S case folding, so each
+    # folds only to itself; K, k and the Kelvin sign share one orbit
+    ("(?i)i", "ı", False), ("(?i)I", "ı", False), ("(?i)[a-z]", "ı", False), ("(?i)ı", "ı", True),
+    ("(?i)ı", "i", False), ("(?i)ı", "I", False), ("(?i)İ", "i", False), ("(?i)İ", "İ", True),
+    ("(?i)[h-j]", "İ", False), ("(?i)k", "\u212a", True), ("(?i)\u212a", "K", True),
+    # Unicode 9.0 (Go 1.9): runes assigned later are Cn -- in no category, script or fold orbit
+    ("\\p{So}", "\U0001F97A", False), ("\\p{So}", "\U0001F600", True), ("\\pL", "\u08be", False),
+    ("\\pL", "\u08b6", True), ("\\PL", "\u08be", True),
+    ("(?i)\ua7b8", "\ua7b9", False), ("(?i)\ua7b4", "\ua7b5", True), ("(?i)\u10d0", "\u1c90", False), ("\\p{Georgian}", "\u1c90", False),
+    ("\\p{Adlam}", "\U0001E900", True),
 ]
 
 UNICODE_ERRORS = [
@@ -114,6 +124,9 @@ UNICODE_ERRORS = [
     ("[\\p{Bogus}]", "invalid character class range: `\\p{Bogus}`"),
     ("\\p{^}", "invalid character class range: `\\p{^}`"),
     ("\\pé", "invalid character class range: `\\pé`"),
+    # scripts added after Unicode 9.0 are unknown to Go 1.9
+    ("\\p{Dogra}", "invalid character class range: `\\p{Dogra}`"),
+    ("\\p{Yezidi}", "invalid character class range: `\\p{Yezidi}`"),
 ]
 
 
