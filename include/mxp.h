@@ -50,6 +50,21 @@ const char* mxp_last_error(const mxp_engine* eng);
 int mxp_vocab_set(mxp_engine* eng, const char* const* names, const int32_t* value_types, uint32_t n);
 
 /*
+ * Vocabulary as a finder: the expr.AttributeDescriptorFinder of
+ * runtime.VocabularyChangeListener.ChangeVocabulary(finder) (mixer/pkg/runtime/controller.go:100-102,
+ * finder.go:45-47).  The engine calls find(ctx, name) for each attribute name its rules use, the
+ * first time it meets the name after this call (at mxp_ruleset_compile / mxp_resolver_set);
+ * find returns the name's ValueType, or -1 when GetAttribute returns nil.  Names get vocabulary
+ * positions in the order they are found (mxp_vocab_name).  Invalidates the current rule set; find
+ * must stay callable until the next mxp_vocab_set / mxp_vocab_set_finder.
+ */
+typedef int32_t (*mxp_attr_finder)(void* ctx, const char* name);
+int mxp_vocab_set_finder(mxp_engine* eng, mxp_attr_finder find, void* ctx);
+
+/* Name of vocabulary position `pos` (mxp_attr_ref.attr), NUL-terminated into buf. */
+int mxp_vocab_name(mxp_engine* eng, uint32_t pos, char* buf, uint32_t cap);
+
+/*
  * Compile a rule set: n predicate expressions (rule i = exprs[i]) compiled with the reference's
  * compiler (compiler.Compile, compiler.go:125) and lowered to the GPU bytecode; uploaded once.
  * status[i] (optional) receives one of MXP_RULE_*.
@@ -83,7 +98,7 @@ int mxp_eval_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t* match_
  * ReferencedAttributes (mixer/pkg/api/grpcServer.go:177).  Short-circuiting makes it path
  * dependent; the engine records the reads its VM performs and adds the reads its guard and index
  * phases stand for.
- *   attr  position of the attribute in the mxp_vocab_set names;
+ *   attr  position of the attribute in the mxp_vocab_set names (mxp_vocab_name);
  *   key   MXP_REF_NOKEY for an attribute reference, else the string id of the map key
  *         (StringMap.Get; text with mxp_string_text while this batch is the engine's last);
  *   cond  MXP_REF_ABSENCE / MXP_REF_EXACT (mixer/v1 ReferencedAttributes.Condition), or MXP_REF_MAP
@@ -119,6 +134,26 @@ int mxp_eval_values(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* value
 int mxp_value_text(mxp_engine* eng, uint32_t rule, uint64_t value, char* buf, uint32_t cap);
 /* Result kind of a value register: MXP_STRING, MXP_INT64, ... (interface values report their kind). */
 int mxp_value_kind(mxp_engine* eng, uint32_t rule, uint64_t value);
+/*
+ * A result register of the last batch as the Go value interpreter.Result.AsInterface returns
+ * (mixer/pkg/il/interpreter/result.go): kind (MXP_*) and
+ *   MXP_BOOL / MXP_INT64 / MXP_DURATION   i
+ *   MXP_DOUBLE                            d
+ *   MXP_TIMESTAMP                         i = Unix seconds, nsec
+ *   MXP_STRING / MXP_BYTES                the bytes in buf[0 .. n)
+ *   MXP_STRING_MAP                        i entries in buf[0 .. n): u32 key length, key, u32 value
+ *                                         length, value (little endian) per entry
+ * MXP_ERR_NOMEM when n > cap (n is set: call again with room).
+ */
+typedef struct mxp_value {
+    uint32_t kind;
+    uint32_t n;
+    int64_t i;
+    double d;
+    int32_t nsec;
+    uint32_t pad;
+} mxp_value;
+int mxp_value_decode(mxp_engine* eng, uint32_t rule, uint64_t value, mxp_value* out, uint8_t* buf, uint32_t cap);
 
 /* Error text of pair (request, rule) from the last evaluated batch, as the reference would report it.
  * Returns MXP_OK with buf = "" if the pair did not fail, 1 if it failed with a panic. */

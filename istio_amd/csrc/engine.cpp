@@ -23,6 +23,22 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     std::vector<uint32_t>& off = off_h;
     all.clear();
     off.assign(n + 1, 0);
+    if (finder) {  // vocabulary through the caller's finder: resolve every name the rules use
+        std::vector<const mxp::Expr*> stack;
+        for (uint32_t i = 0; i < n; i++) {
+            std::string err;
+            mxp::ExprP e = mxp::parse_expression(exprs[i] ? exprs[i] : "", &err);
+            if (!e) continue;
+            stack.assign(1, e.get());
+            while (!stack.empty()) {
+                const mxp::Expr* x = stack.back();
+                stack.pop_back();
+                if (x->kind == mxp::Expr::VAR) vocab_pos(x->var);
+                if (x->target) stack.push_back(x->target.get());
+                for (const auto& a : x->args) stack.push_back(a.get());
+            }
+        }
+    }
     for (uint32_t i = 0; i < n; i++) {
         Rule& R = rules[i];
         mxp::CompiledRule cr;
@@ -1489,6 +1505,22 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         A.q0 = lo;
         A.q1 = hi;
         const uint32_t cx = (hi + 63) / 64, grid = (cx + 3) / 4, tiles = (hi + 1023) / 1024;
+        // the deferred-pair scratch and counters are engine-wide: a launch on another stream waits
+        // for the previous deferred launch to finish with them (its sort kernel resets the counter
+        // set this launch uses; its fills read the slots this launch's sort rewrites), and scratch
+        // that must grow is released only once that launch is done
+        if (!dtp_ev && (e = hipEventCreateWithFlags(&dtp_ev, hipEventDisableTiming)) != hipSuccess) {
+            dtp_ev = nullptr;
+            return hipfail(e, "deferred-pair event");
+        }
+        if (dtp_pending) {
+            if (dtp_stream != s && (e = hipStreamWaitEvent(s, dtp_ev, 0)) != hipSuccess) return hipfail(e, "deferred-pair wait");
+            const size_t need_slots = (size_t)(P->n_fills + P->n_vtfills) * tiles * 256 * 16;
+            if ((d_dtp_ent.n < (size_t)cx * dtp_cap * 4 || d_dtp_n.n < (size_t)grid * 16 || d_dtp_slots.n < need_slots ||
+                 d_dtp_qn.n < need_slots / 16 || d_dtp_ovf.n < (size_t)dtp_ovf_cap * 8) &&
+                (e = hipEventSynchronize(dtp_ev)) != hipSuccess)
+                return hipfail(e, "deferred-pair sync");
+        }
         if ((e = d_dtp_ent.reserve((size_t)cx * dtp_cap * 4)) != hipSuccess ||
             (e = d_dtp_n.reserve((size_t)grid * 4 * 4)) != hipSuccess ||
             (e = d_dtp_ovf.reserve((size_t)dtp_ovf_cap * 8)) != hipSuccess ||
@@ -1545,6 +1577,9 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         AR.errcount = nullptr;
         AR.wave_t = nullptr;
         if ((e = mxp_launch_index(&AR, grid, s)) != hipSuccess) return hipfail(e, "launch index re-run");
+        if ((e = hipEventRecord(dtp_ev, s)) != hipSuccess) return hipfail(e, "deferred-pair event");
+        dtp_pending = true;
+        dtp_stream = s;
         if (timing && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hipfail(e, "event");
         ev_index = true;
         last_mask = mask;
@@ -1716,6 +1751,7 @@ std::string mxp_engine::format_error(const mxp_bag_batch* b, const mxp_dbatch* d
 }
 
 // ===================================================================================== C-ABI
+static int put_text(const std::string& s, char* buf, uint32_t cap);
 extern "C" {
 
 int mxp_engine_create(int device, mxp_engine** out) {
@@ -1767,6 +1803,8 @@ void mxp_engine_destroy(mxp_engine* eng) {
     for (auto& x : eng->chunk_ev)
         if (x) (void)hipEventDestroy(x);
     if (eng->side) (void)hipStreamDestroy(eng->side);
+    if (eng->dtp_ev) (void)hipEventSynchronize(eng->dtp_ev);
+    if (eng->dtp_ev) (void)hipEventDestroy(eng->dtp_ev);
     if (eng->stats_ev) (void)hipEventSynchronize(eng->stats_ev);
     if (eng->stats_ev) (void)hipEventDestroy(eng->stats_ev);
     delete eng;
@@ -1778,12 +1816,34 @@ int mxp_vocab_set(mxp_engine* eng, const char* const* names, const int32_t* type
     if (!eng || (n && (!names || !types))) return MXP_ERR_ARG;
     eng->vocab.clear();
     eng->vocab_index.clear();
+    eng->vocab_names.clear();
+    eng->finder = nullptr;
+    eng->finder_ctx = nullptr;
+    eng->finder_missing.clear();
     for (uint32_t i = 0; i < n; i++) {
         eng->vocab[names[i]] = types[i];
         eng->vocab_index[names[i]] = i;
+        eng->vocab_names.push_back(names[i]);
     }
     eng->reset_tables();
     return MXP_OK;
+}
+
+int mxp_vocab_set_finder(mxp_engine* eng, mxp_attr_finder find, void* ctx) {
+    if (!eng || !find) return MXP_ERR_ARG;
+    eng->vocab.clear();
+    eng->vocab_index.clear();
+    eng->vocab_names.clear();
+    eng->finder = find;
+    eng->finder_ctx = ctx;
+    eng->finder_missing.clear();
+    eng->reset_tables();
+    return MXP_OK;
+}
+
+int mxp_vocab_name(mxp_engine* eng, uint32_t pos, char* buf, uint32_t cap) {
+    if (!eng || pos >= eng->vocab_names.size()) return MXP_ERR_ARG;
+    return put_text(eng->vocab_names[pos], buf, cap);
 }
 
 int mxp_ruleset_compile(mxp_engine* eng, const char* const* exprs, uint32_t n, int32_t* status) {
@@ -2330,6 +2390,63 @@ int mxp_value_kind(mxp_engine* eng, uint32_t rule, uint64_t v) {
     case mxp::IL_DOUBLE: return MXP_DOUBLE;
     default: return (int)MXP_FH_KIND(v);
     }
+}
+
+int mxp_value_decode(mxp_engine* eng, uint32_t rule, uint64_t v, mxp_value* out, uint8_t* buf, uint32_t cap) {
+    if (!eng || !out || rule >= eng->rules.size()) return MXP_ERR_ARG;
+    mxp_value r{};
+    const int k = mxp_value_kind(eng, rule, v);
+    const uint64_t id = (eng->rules[rule].il_ret == mxp::IL_INTERFACE) ? MXP_FH_ID(v) : v;
+    r.kind = (uint32_t)k;
+    std::string bytes;
+    switch (k) {
+    case MXP_STRING: bytes = eng->string_of(nullptr, id); break;
+    case MXP_BOOL: r.i = (uint32_t)v != 0; break;
+    case MXP_INT64: case MXP_DURATION: r.i = (int64_t)v; break;
+    case MXP_DOUBLE: memcpy(&r.d, &v, 8); break;
+    case MXP_BYTES: {
+        const uint64_t raw = MXP_BYTES_RAW(id);
+        if (raw < eng->gbytes.size()) bytes = eng->gbytes[raw];
+        else if (eng->last_db) eng->last_db->overlay_bytes_at(raw - eng->gbytes.size(), &bytes);
+        break;
+    }
+    case MXP_TIMESTAMP: {
+        TimeKey t{0, 0};
+        if (id < eng->gtimes.size()) t = eng->gtimes[id];
+        else if (eng->last_db) eng->last_db->overlay_time(id - eng->gtimes.size(), &t);
+        r.i = t.s;
+        r.nsec = t.ns;
+        break;
+    }
+    case MXP_STRING_MAP: {  // the batch's map CSR (device), keys and values by interned id
+        const mxp_dbatch* db = eng->last_db.get();
+        uint32_t mo[2] = {0, 0};
+        if (!db || hipMemcpy(mo, db->map_off.as<uint32_t>() + id, 8, hipMemcpyDeviceToHost) != hipSuccess)
+            return eng->fail(MXP_ERR_STATE, "map value without its batch");
+        std::vector<uint32_t> ks(mo[1] - mo[0]), vs(mo[1] - mo[0]);
+        if (!ks.empty() &&
+            (hipMemcpy(ks.data(), db->map_keys.as<uint32_t>() + mo[0], ks.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+             hipMemcpy(vs.data(), db->map_vals.as<uint32_t>() + mo[0], vs.size() * 4, hipMemcpyDeviceToHost) != hipSuccess))
+            return eng->fail(MXP_ERR_DEVICE, "map value download");
+        auto put = [&](const std::string& x) {
+            const uint32_t len = (uint32_t)x.size();
+            bytes.append((const char*)&len, 4);
+            bytes += x;
+        };
+        for (size_t e = 0; e < ks.size(); e++) {
+            put(eng->string_of(db, ks[e]));
+            put(eng->string_of(db, vs[e]));
+        }
+        r.i = (int64_t)ks.size();
+        break;
+    }
+    default: return eng->fail(MXP_ERR_ARG, "value of an unknown kind");
+    }
+    r.n = (uint32_t)bytes.size();
+    *out = r;
+    if (bytes.size() > cap) return MXP_ERR_NOMEM;
+    if (!bytes.empty()) memcpy(buf, bytes.data(), bytes.size());
+    return MXP_OK;
 }
 
 int mxp_value_text(mxp_engine* eng, uint32_t rule, uint64_t v, char* buf, uint32_t cap) {

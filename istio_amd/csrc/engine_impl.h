@@ -157,6 +157,26 @@ struct mxp_engine : public mxp::LowerTables {
 
     mxp::Vocabulary vocab;
     std::unordered_map<std::string, uint32_t> vocab_index;  // name -> position in mxp_vocab_set order
+    std::vector<std::string> vocab_names;                   // position -> name
+    // mxp_vocab_set_finder: names resolved through the caller's finder on first use
+    mxp_attr_finder finder = nullptr;
+    void* finder_ctx = nullptr;
+    std::set<std::string> finder_missing;                   // names the finder did not know
+    // vocabulary position of `name`, asking the finder the first time (-1: not in the vocabulary)
+    int64_t vocab_pos(const std::string& name) {
+        auto it = vocab_index.find(name);
+        if (it != vocab_index.end()) return it->second;
+        if (!finder || finder_missing.count(name)) return -1;
+        const int32_t vt = finder(finder_ctx, name.c_str());
+        if (vt < 0) {
+            finder_missing.insert(name);
+            return -1;
+        }
+        vocab[name] = vt;
+        vocab_index[name] = (uint32_t)vocab_names.size();
+        vocab_names.push_back(name);
+        return (int64_t)vocab_names.size() - 1;
+    }
     mxp::FuncMap fmap = mxp::default_func_map();
 
     // rule-set-global interning
@@ -310,6 +330,9 @@ struct mxp_engine : public mxp::LowerTables {
     DevBuf d_dtp_ent, d_dtp_n, d_dtp_ovf, d_dtp_ovf_n, d_dtp_slots, d_dtp_qn;
     bool last_dtp = false;  // the last launch deferred its index pairs (mxp_kernel_times [2])
     uint32_t dtp_par = 0;   // d_dtp_ovf_n holds two counter sets: this launch's and the next one's
+    hipEvent_t dtp_ev = nullptr;      // recorded after each deferred launch (its last kernel)
+    hipStream_t dtp_stream = nullptr; // ... on this stream; a launch on another stream waits for it
+    bool dtp_pending = false;
     // MXP_TRACE=1: phase times of evaluations / Resolves on stderr (each phase synchronises the
     // stream first, so traced calls are slower than untraced ones)
     bool trace = false;

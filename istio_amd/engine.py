@@ -28,6 +28,9 @@ VALUE_TYPES = {"VALUE_TYPE_UNSPECIFIED": 0, "STRING": 1, "INT64": 2, "DOUBLE": 3
 RULE_OK, RULE_PARSE_ERROR, RULE_TYPE_ERROR, RULE_COMPILE_ERROR, RULE_COMPILE_PANIC, RULE_UNSUPPORTED = range(6)
 FALSE, TRUE, ERROR, PANIC = 0, 1, 2, 3
 
+# mxp_attr_finder (mxp.h): int32_t (*)(void* ctx, const char* name)
+_FINDER = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_char_p)
+
 # every entry point declared in include/mxp.h: name -> (restype, argtypes)
 _VP = ctypes.c_void_p
 SIGNATURES = {
@@ -35,6 +38,8 @@ SIGNATURES = {
     "mxp_engine_destroy": (None, [_VP]),
     "mxp_last_error": (ctypes.c_char_p, [_VP]),
     "mxp_vocab_set": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int32), ctypes.c_uint32]),
+    "mxp_vocab_set_finder": (ctypes.c_int, [_VP, _VP, _VP]),
+    "mxp_vocab_name": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
     "mxp_ruleset_compile": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32, ctypes.POINTER(ctypes.c_int32)]),
     "mxp_rule_error": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
     "mxp_rule_il_text": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
@@ -52,6 +57,7 @@ SIGNATURES = {
     "mxp_eval_values": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
     "mxp_value_text": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_char_p, ctypes.c_uint32]),
     "mxp_value_kind": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint64]),
+    "mxp_value_decode": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint64, _VP, _VP, ctypes.c_uint32]),
     "mxp_pair_error": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
     "mxp_error_count": (ctypes.c_uint64, [_VP]),
     "mxp_batch_upload": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP)]),
@@ -177,6 +183,22 @@ class Engine:
         self._check(self.lib.mxp_vocab_set(self.h, arr, tarr, len(names)), "mxp_vocab_set")
         self.vocab_names = names
         self.rules = []
+
+    def set_vocabulary_finder(self, get_attribute):
+        """ChangeVocabulary(finder) (runtime/controller.go:100-102): `get_attribute(name)` is the
+        finder's GetAttribute -- a ValueType (name or enum value), or None when the name is not in
+        the vocabulary.  The engine asks for each name its rules use, the first time it meets it."""
+        def find(_ctx, name):
+            v = get_attribute(name.decode())
+            return -1 if v is None else (VALUE_TYPES[v] if isinstance(v, str) else int(v))
+        self._finder = _FINDER(find)  # (kept alive while the engine may call it)
+        self._check(self.lib.mxp_vocab_set_finder(self.h, ctypes.cast(self._finder, _VP), None), "mxp_vocab_set_finder")
+        self.vocab_names = None
+        self.rules = []
+
+    def vocab_name(self, pos: int) -> str:
+        """Name of vocabulary position `pos` (mxp_attr_ref.attr)."""
+        return self._text(self.lib.mxp_vocab_name, pos)
 
     def compile(self, rules: Sequence[str]) -> np.ndarray:
         """Compile + upload a rule set; returns per-rule status (RULE_*)."""
@@ -324,7 +346,7 @@ class Engine:
                     if k not in keys:
                         keys[k] = self.string_text(int(k))
                     key = keys[k]
-                row.append((self.vocab_names[a], key, int(c)))
+                row.append((self.vocab_names[a] if self.vocab_names is not None else self.vocab_name(int(a)), key, int(c)))
             refs.append(row)
         return refs
 
@@ -546,31 +568,51 @@ PANIC_TEXTS = {"Unknown map type", "reflect: Call using a value of the wrong typ
                "runtime error: index out of range"}
 
 
+class _Value(ctypes.Structure):  # mxp_value (mxp.h)
+    _fields_ = [("kind", ctypes.c_uint32), ("n", ctypes.c_uint32), ("i", ctypes.c_int64), ("d", ctypes.c_double),
+                ("nsec", ctypes.c_int32), ("pad", ctypes.c_uint32)]
+
+
 def decode_value(e: Engine, rule: int, v: int):
-    """Engine result register -> Python Go-model value (interpreter.Result.AsInterface)."""
+    """Engine result register -> Python Go-model value (interpreter.Result.AsInterface), through
+    mxp_value_decode: bool, GoInt64, GoDuration, GoFloat64, str, bytes, GoTime, dict."""
     from .bags import GoDuration, GoFloat64, GoInt64, GoTime
-    import struct
-    vt, il = e.rule_types(rule)
-    if il == 5:  # bool
-        return (v & 0xFFFFFFFF) != 0
-    if il == 3:
-        return GoInt64(v - (1 << 64) if v >> 63 else v)
-    if il == 6:
-        return GoDuration(v - (1 << 64) if v >> 63 else v)
-    if il == 4:
-        return GoFloat64(struct.unpack("<d", struct.pack("<Q", v))[0])
-    if il == 2:
-        return e.value_text(rule, v)
-    kind = e.value_kind(rule, v)
-    txt = e.value_text(rule, v)
-    if kind == 7:  # bytes "[1 2 3]"
-        inner = txt[1:-1].strip()
-        return bytes(int(x) for x in inner.split()) if inner else b""
-    if kind == 6:
-        return ("time", txt)
-    if kind == 1:
-        return txt
-    return txt
+    out = _Value()
+    cap = 1 << 12
+    while True:
+        buf = ctypes.create_string_buffer(cap)
+        rc = e.lib.mxp_value_decode(e.h, rule, v, ctypes.addressof(out), buf, cap)
+        if rc != 4:  # MXP_ERR_NOMEM: again with room for out.n bytes
+            break
+        cap = out.n + 16
+    e._check(rc, "mxp_value_decode")
+    raw = buf.raw[:out.n]
+    k = out.kind
+    if k == 4:  # MXP_BOOL
+        return bool(out.i)
+    if k == 2:
+        return GoInt64(out.i)
+    if k == 3:
+        return GoFloat64(out.d)
+    if k == 5:
+        return GoDuration(out.i)
+    if k == 1:
+        return raw.decode("utf-8", "surrogateescape")
+    if k == 7:
+        return raw
+    if k == 6:
+        return GoTime(out.i, out.nsec)
+    if k == 8:  # string map: (u32 len, bytes) key / value runs
+        m, at = {}, 0
+        for _ in range(out.i):
+            kv = []
+            for _ in range(2):
+                n = int.from_bytes(raw[at:at + 4], "little")
+                kv.append(raw[at + 4:at + 4 + n].decode("utf-8", "surrogateescape"))
+                at += 4 + n
+            m[kv[0]] = kv[1]
+        return m
+    raise MxpError("value of kind %d" % k)
 
 
 class ListHandle:

@@ -158,3 +158,43 @@ def test_deferred_pairs_plain_fill_device_identical(mxp, monkeypatch):
     for a, b in zip(out[0], out[1]):
         assert np.array_equal(a, b)
     assert out[0][2].sum() > 0 and out[0][1].any()
+
+
+@pytest.mark.parametrize("env", PATHS[:2], ids=["lists", "overflow"])
+def test_deferred_pairs_across_streams(mxp, monkeypatch, env):
+    """Deferred launches queued back to back on two streams with no host synchronisation between
+    them (two caller goroutines' streams): the second waits for the first's
+    engine-wide pair scratch and overflow counters, so both batches' bitmaps equal those of the
+    engine with deferred pairs off (MXP_DTP=0); then a bigger batch (the scratch grows) on the
+    first stream."""
+    import torch
+    manifest, rules, big = W.c4_workload(n_rules=1200, n_requests=20000, seed=14)
+    R = len(rules)
+    Wd = (R + 31) // 32
+    batches = [big.subset(np.arange(0, 9000)), big.subset(np.arange(9000, 17000)), big]
+
+    def run(eng, streams):
+        outs = []
+        dbs = [eng.upload(b) for b in batches]
+        bufs = []
+        for db, b, s in zip(dbs, batches, streams):
+            dm = torch.full((Wd, b.n), -1, dtype=torch.int32, device="cuda:0")
+            de = torch.full_like(dm, -1)
+            hits = torch.zeros(R, dtype=torch.int64, device="cuda:0")
+            db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s.cuda_stream)
+            bufs.append((dm, de, hits))
+        torch.cuda.synchronize()
+        for dm, de, hits in bufs:
+            outs.append((dm.cpu().numpy(), de.cpu().numpy(), hits.cpu().numpy()))
+        for db in dbs:
+            db.free()
+        return outs
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    eng = engine_for(mxp, monkeypatch, env, manifest, rules)
+    assert deferred_ran(eng, batches[0], R)
+    got = run(eng, [s1, s2, s1])
+    ref = run(engine_for(mxp, monkeypatch, {"MXP_DTP": "0"}, manifest, rules), [s1, s1, s1])
+    for a, b in zip(got, ref):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    assert (got[2][0] != 0).any()
