@@ -15,6 +15,10 @@ same step structure and reports it as the extra "c4" block of the same JSON line
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
     python bench.py --workload c4 | c5 | c3-ip | c3-str | c3-regex | c5-quota
 
+With N GPUs every rank evaluates its contiguous shard (istio_amd.dist.shard_bounds) of ONE seeded
+batch of N x --requests requests (configs[4]: 8 x 1M).  The default line also carries a "c5" block:
+the C2 predicates + the shard's memquota batch + one all-reduce of hits[R] ++ quota_delta[K].
+
 Prints one JSON line (rank 0).
 """
 import argparse
@@ -55,6 +59,7 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=host_threads())
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c4", action="store_true", help="default run: skip the extra C4 block")
+    p.add_argument("--no-c5", action="store_true", help="default run: skip the extra C5 block")
     p.add_argument("--workload", default="c2", choices=["c2", "c4", "c5", "c3-ip", "c3-str", "c3-regex", "c5-quota"],
                    help="c2 (default, the BASELINE metric; + a C4 block); c4 route rules; c5 = C2 predicates + "
                         "memquota with one combined all-reduce; C3 lists; c5-quota memquota alone")
@@ -109,17 +114,30 @@ def cpu_baseline(manifest, rules, batch, seconds, threads, chunk=256):
             "lru1024": lru}
 
 
+def kernel_fingerprint():
+    """sha1 of the engine's kernel and launch sources: a PMC profile is valid for this build only."""
+    import hashlib
+    h = hashlib.sha1()
+    csrc = os.path.join(ROOT, "istio_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")) or f in ("engine.cpp", "pack_device.cpp", "lower.cpp", "vmopt.cpp"):
+            h.update(f.encode())
+            h.update(open(os.path.join(csrc, f), "rb").read())
+    return h.hexdigest()
+
+
 def measured_traffic(workload, rules, requests):
-    """HBM bytes per evaluation from the committed PMC profile (tools/pmc_summarize.py: FETCH_SIZE
-    and WRITE_SIZE in separate rocprofv3 passes, FETCH doubled for gfx950), when one exists for this
-    workload size; else None."""
-    for name in ("pmc_traffic_%s.json" % workload, "pmc_traffic.json"):
-        path = os.path.join(ROOT, "profiles", name)
-        if not os.path.exists(path):
-            continue
-        d = json.load(open(path))
-        if d.get("workload", "c2") == workload and d.get("rules") == rules and d.get("requests") == requests:
-            return d.get("bytes_per_eval")
+    """HBM bytes per evaluation from the committed PMC profile of THIS build (tools/pmc_summarize.py:
+    FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes, FETCH doubled for gfx950; the profile
+    records kernel_fingerprint() of the sources it measured), when one exists for this workload
+    size; else None -- a profile of other kernels is not reported."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic_%s.json" % workload)
+    if not os.path.exists(path):
+        return None
+    d = json.load(open(path))
+    if (d.get("workload") == workload and d.get("rules") == rules and d.get("requests") == requests
+            and d.get("fingerprint") == kernel_fingerprint()):
+        return d.get("bytes_per_eval")
     return None
 
 
@@ -136,26 +154,63 @@ def lds_conflicts(workload):
 
 def timed_loop(step, steps, warmup, world, stream):
     """W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize; returns the
-    slowest rank's seconds and the per-step HIP-event durations (ms) recorded on `stream`."""
+    slowest rank's seconds and the per-step HIP-event durations (ms) recorded on `stream`.  (Without
+    a GPU -- the gloo CPU tests of the step -- there is nothing to synchronise and no events.)"""
     import torch
     import torch.distributed as dist
     from istio_amd import dist as D
+    gpu = torch.cuda.is_available()
+    sync = torch.cuda.synchronize if gpu else (lambda: None)
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    sync()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if gpu else (None, None)
+           for _ in range(steps)]
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for k in range(steps):
         step(*evs[k])
-    torch.cuda.synchronize()
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ev_ms = [a.elapsed_time(b) for a, b in evs]
-    return D.max_over_ranks(elapsed, torch.device("cuda", torch.cuda.current_device())), ev_ms
+    ev_ms = [a.elapsed_time(b) for a, b in evs] if gpu else []
+    dev = torch.device("cuda", torch.cuda.current_device()) if gpu else None
+    return D.max_over_ranks(elapsed, dev), ev_ms
+
+
+def shard_workload(kind, n_rules, requests_per_gpu, rank, world):
+    """This rank's shard of ONE seeded batch of requests_per_gpu x world requests (configs[4]: the
+    8 x 1M batch), contiguous per rank (dist.shard_bounds); the rule set is the same on every rank."""
+    from istio_amd import dist as D
+    from istio_amd import workloads as W
+    n_total = requests_per_gpu * world
+    shard = D.shard_bounds(n_total, rank, world)
+    if kind == "c4":
+        return W.c4_workload(n_rules=n_rules, n_requests=n_total, seed=4, shard=shard)
+    manifest, _, batch = W.c2_workload(n_rules=n_rules, n_requests=n_total, seed=2, shard=shard)
+    return manifest, W.c2_rules(n_rules, seed=2)[0], batch
+
+
+def make_step(ctr, evaluate, quota_alloc=None, stream=None):
+    """The bench step: evaluate every pair of the shard with the hit counters
+    accumulated into the step's hits view, optionally the shard's memquota batch with its per-key
+    deltas into the quota view, then the step's ONE all-reduce of hits[R] ++ quota_delta[K]
+    (StepCounters.end_step; nothing on a single process).  ev0 / ev1 bracket the kernels."""
+    def step(ev0=None, ev1=None):
+        ctr.begin_step()
+        views = ctr.views()
+        if ev0 is not None:
+            ev0.record(stream)
+        evaluate(views[0])
+        if quota_alloc is not None:
+            quota_alloc(views[1])
+        if ev1 is not None:
+            ev1.record(stream)
+        ctr.end_step()
+    return step
 
 
 def list_bench(args, rank, world, local):
@@ -362,16 +417,17 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     from istio_amd.engine import Engine
 
     dev = torch.device("cuda", local)
-    # requests shard per rank (independent seeds = disjoint synthetic shards); the rule set is replicated
+    # ONE seeded batch of requests_per_gpu x N requests (configs[4]: 8 x 1M), each rank evaluating
+    # its contiguous shard (dist.shard_bounds) against the replicated rule set
+    manifest, rules, batch = shard_workload(kind, args.rules, args.requests, rank, world)
     if kind == "c4":
-        manifest, rules, batch = W.c4_workload(n_rules=args.rules, n_requests=args.requests, seed=4 + 1000 * rank)
         metric, workload = ("request x rule predicate evals/sec at 10k rules (C4 route rules)",
                             "C4 Pilot-style route rules R=%d, %d requests per GPU (configs[3])")
     else:
-        manifest, rules, batch = W.c2_workload(n_rules=args.rules, n_requests=args.requests, seed=2 + 1000 * rank)
-        rules = W.c2_rules(args.rules, seed=2)[0]
         metric, workload = ("request x rule predicate evals/sec at 10k rules",
                             "C2 rules scaled to R=%d, %d requests per GPU (configs[1] family, configs[4] shard)")
+        if with_quota:
+            workload = "C5: C2 rules R=%d, %d requests per GPU + memquota (configs[4])"
     eng = Engine(local)
     eng.set_vocabulary(manifest)
     st = eng.compile(rules)
@@ -405,31 +461,25 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     ctr = D.StepCounters([R] + ([QUOTA_KEYS] if quota else []), dev)
     now = [1_500_000_000 * 10**9]
 
-    def step(ev0=None, ev1=None):
-        ctr.begin_step()
-        views = ctr.views()
-        if ev0 is not None:
-            ev0.record(stream)
-        evaluate(views[0].data_ptr())
-        if quota is not None:
-            (_, q, (dk, da, dbe, dg)) = quota
-            q.alloc_device(dk.numel(), dk.data_ptr(), da.data_ptr(), dbe.data_ptr(), now[0], sh, dg.data_ptr(),
-                           views[1].data_ptr())
-            now[0] += 10**8
-        if ev1 is not None:
-            ev1.record(stream)
-        ctr.end_step()  # the step's single collective over RCCL / xGMI when N > 1
+    def quota_alloc(delta):
+        (_, q, (dk, da, dbe, dg)) = quota
+        q.alloc_device(dk.numel(), dk.data_ptr(), da.data_ptr(), dbe.data_ptr(), now[0], sh, dg.data_ptr(),
+                       delta.data_ptr())
+        now[0] += 10**8
+    step = make_step(ctr, lambda hits: evaluate(hits.data_ptr()), quota_alloc if quota is not None else None, stream)
 
     elapsed, ev_ms = timed_loop(step, args.steps, args.warmup, world, stream)
     step_kernel_ms = float(np.mean(ev_ms))
     value = world * N * R * args.steps / elapsed
 
     # per-kernel durations (HIP events recorded by libmxp around each launch, on `stream`), in a
-    # separate pass so the timed region above carries no extra synchronisation
+    # separate pass so the timed region above carries no extra synchronisation; the evaluation as
+    # the step runs it, hit counters included (the span ends after the counters)
+    scratch_hits = torch.zeros(R, dtype=torch.int64, device=dev)
     eng.set_timing(True)
     per = []
     for _ in range(args.steps):
-        evaluate(0)
+        evaluate(scratch_hits.data_ptr())
         per.append(eng.kernel_times(3))
     eng.set_timing(False)
     k_eval = float(np.mean([p[0] for p in per]))
@@ -438,11 +488,11 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     # value-class and index kernels and the pair sort, [1] the fills and the rest
     deferred = bool(per and len(per[0]) > 2 and per[0][2] == 1.0)
     if deferred:
-        labels = ("mxp_vt_classify/vt_eval + mxp_index_kernel + mxp_dtp_sort_kernel (deferred pairs)",
-                  "mxp_fill/vtfill/guard2/eval kernels + the gated index launch (overflow list)")
+        labels = ("mxp_vt_classify/vt_eval + mxp_index_kernel + mxp_dtp_sort_kernel (deferred pairs, hit counters)",
+                  "mxp_fill/vtfill/guard2/eval kernels + the gated index launch (overflow list) + hit-counter gate")
     else:
         labels = ("phase1 (mxp_vt_classify/vt_eval/fill/vtfill/guard2/eval kernels)",
-                  "mxp_index_kernel+mxp_inject_kernel")
+                  "mxp_index_kernel+mxp_inject_kernel + mxp_hits_kernel (streams the bitmap unless the kernels counted)")
     eval_ms = k_eval + k_index
 
     # algorithmic bytes of one evaluation: every referenced column read once per
@@ -452,7 +502,7 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     prog_bytes = 16 * sum(eng.rule_vm_text(i).count("\n") for i in range(R)) + 4 * (R + 1)
     alg_bytes = N * n_cols * 9 + prog_bytes + N * Wd * 4 + (N if compact else N * Wd * 4)
     achieved = alg_bytes / (eval_ms * 1e-3) / 1e9
-    traffic = measured_traffic(kind, R, N)
+    traffic = measured_traffic(kind + ("q" if with_quota else ""), R, N)
 
     out = {
         "metric": metric,
@@ -532,14 +582,20 @@ def main():
         return quota_bench(args, rank, world, local)
     kind = "c4" if args.workload == "c4" else "c2"
     out = predicate_bench(args, kind, rank, world, local, with_quota=args.workload == "c5")
+    keys = ("metric", "value", "unit", "ms_per_step", "eval_ms", "kernels_ms", "deferred_pairs", "pack_upload_s",
+            "end_to_end", "config", "roofline", "lds_bank_conflicts", "quota", "cpu_baseline")
     if args.workload == "c2" and not args.no_c4:
         # the representative config BASELINE.json quotes at 10k rules (configs[3]), driver-timed too
         c4 = predicate_bench(args, "c4", rank, world, local)
-        out["c4"] = {k: c4[k] for k in ("metric", "value", "unit", "ms_per_step", "eval_ms", "kernels_ms", "deferred_pairs",
-                                        "pack_upload_s", "end_to_end", "config", "roofline", "lds_bank_conflicts")
-                     if k in c4}
-        if "cpu_baseline" in c4:
-            out["c4"]["cpu_baseline"] = c4["cpu_baseline"]
+        out["c4"] = {k: c4[k] for k in keys if k in c4}
+    if args.workload == "c2" and not args.no_c5:
+        # configs[4]'s step: the C2 predicates + the memquota batch of the shard, then ONE all-reduce
+        # of hits[R] ++ quota_delta[K] (at N = 1, the same step without the collective)
+        a5 = argparse.Namespace(**vars(args))
+        a5.e2e_reps = 0
+        a5.no_cpu_baseline = True
+        c5 = predicate_bench(a5, "c2", rank, world, local, with_quota=True)
+        out["c5"] = {k: c5[k] for k in keys if k in c5}
     if rehearse:
         out["rehearsal"] = "%d ranks on one GPU over gloo: exercises the multi-rank step, not a scaling number" % world
     if rank == 0:

@@ -1473,6 +1473,19 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         A.wave_t = d_wave_t.as<unsigned long long>();
         wave_t_n = (A.n + 63) / 64;
     }
+    // deferred index pairs (kargs.dtp_*): index kernel first, its pairs filed per fill chunk and
+    // lane quad and OR-ed in by the value-class fill as it writes the words -- instead of one read-modify-write
+    // atomic per true pair on rows the fill wrote before (C4: ~14 per request, 0.6 ms of atomics)
+    const bool dtp_on = dtp && P->dtp_ok && use_index && guards_on && nchunk == 1 && !window && lo == 0 &&
+                        !A.dense_of && !refs_on && !A.nfa && A.out_match;
+    last_dtp = dtp_on;
+    // ... whose true pairs are counted where they are filed (mxp_dtp_sort_kernel's per-tile
+    // histograms, summed by mxp_dtp_hits_kernel): the hit counters are fused into every kernel of
+    // the evaluation, whatever the device gate says, and the bitmap is not streamed again
+    // (eval_device_hits; MXP_DEBUG_FLAGS 1048576 keeps the streaming counters)
+    const bool dtp_count = dtp_on && A.hits && !(debug_flags & 1048576u) && A.n_rules <= kDtpHist;
+    last_dtp_counted = dtp_count;
+    if (dtp_count) A.hits_gate = nullptr;
     if (A.n_vt) {
         // value classes: classify every request of [lo, hi) per active column, then evaluate the
         // columns' rules once per class (class records -> errcount[2], the host expands them)
@@ -1495,12 +1508,6 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         if ((e = mxp_launch_vt_eval(&AV, tiles, (P->vt_max_nw + 3) / 4, s)) != hipSuccess)
             return hipfail(e, "launch vt eval");
     }
-    // deferred index pairs (kargs.dtp_*): index kernel first, its pairs filed per fill chunk and
-    // lane quad and OR-ed in by the value-class fill as it writes the words -- instead of one read-modify-write
-    // atomic per true pair on rows the fill wrote before (C4: ~14 per request, 0.6 ms of atomics)
-    const bool dtp_on = dtp && P->dtp_ok && use_index && guards_on && nchunk == 1 && !window && lo == 0 &&
-                        !A.dense_of && !refs_on && !A.nfa && A.out_match;
-    last_dtp = dtp_on;
     if (dtp_on) {
         A.q0 = lo;
         A.q1 = hi;
@@ -1517,7 +1524,8 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
             if (dtp_stream != s && (e = hipStreamWaitEvent(s, dtp_ev, 0)) != hipSuccess) return hipfail(e, "deferred-pair wait");
             const size_t need_slots = (size_t)(P->n_fills + P->n_vtfills) * tiles * 256 * 16;
             if ((d_dtp_ent.n < (size_t)cx * dtp_cap * 4 || d_dtp_n.n < (size_t)grid * 16 || d_dtp_slots.n < need_slots ||
-                 d_dtp_qn.n < need_slots / 16 || d_dtp_ovf.n < (size_t)dtp_ovf_cap * 8) &&
+                 d_dtp_qn.n < need_slots / 16 || d_dtp_ovf.n < (size_t)dtp_ovf_cap * 8 ||
+                 (dtp_count && d_dtp_part.n < (size_t)tiles * ((A.n_rules + 1) / 2) * 4)) &&
                 (e = hipEventSynchronize(dtp_ev)) != hipSuccess)
                 return hipfail(e, "deferred-pair sync");
         }
@@ -1547,8 +1555,15 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         AI.dtp_qn = d_dtp_qn.as<uint8_t>();
         AI.dtp_tiles = tiles;
         AI.dtp_nchunks = P->n_fills + P->n_vtfills;
+        if (dtp_count) {
+            if ((e = d_dtp_part.reserve((size_t)tiles * ((A.n_rules + 1) / 2) * 4)) != hipSuccess)
+                return hipfail(e, "deferred-pair histograms");
+            AI.dtp_part = d_dtp_part.as<uint32_t>();
+        }
         if ((e = mxp_launch_index(&AI, grid, s)) != hipSuccess) return hipfail(e, "launch index");
         if ((e = mxp_launch_dtp_sort(&AI, s)) != hipSuccess) return hipfail(e, "launch dtp sort");
+        if (dtp_count && (e = mxp_launch_dtp_hits(AI.dtp_part, tiles, A.n_rules, A.hits, s)) != hipSuccess)
+            return hipfail(e, "launch dtp hits");
         if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
         mxp_kargs AF = A;  // the fills merge
         AF.dtp_slots = AI.dtp_slots;
@@ -1909,7 +1924,7 @@ int mxp_kernel_times(mxp_engine* eng, float* ms, uint32_t cap, uint32_t* n_out) 
     float t[2] = {0.f, 0.f};
     if ((e = hipEventSynchronize(eng->ev[2])) != hipSuccess) return eng->hipfail(e, "event sync");
     if ((e = hipEventElapsedTime(&t[0], eng->ev[0], eng->ev[1])) != hipSuccess) return eng->hipfail(e, "elapsed");
-    if (eng->ev_index && (e = hipEventElapsedTime(&t[1], eng->ev[1], eng->ev[2])) != hipSuccess)
+    if ((e = hipEventElapsedTime(&t[1], eng->ev[1], eng->ev[2])) != hipSuccess)
         return eng->hipfail(e, "elapsed");
     const float tt[3] = {t[0], t[1], eng->last_dtp ? 1.f : 0.f};
     uint32_t k = 0;
@@ -2038,8 +2053,10 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
     eng->hits_gate_out = nullptr;
     if (rc) return rc;
     // the streaming counters (returning at once when the kernels counted); their block (0, 0) also
-    // sets the next evaluation's gate from this one's true pairs and resets the pair count
-    if (R && db->n) {
+    // sets the next evaluation's gate from this one's true pairs and resets the pair count.  A
+    // deferred-pair evaluation counted everything in its kernels: only the gate update.
+    const bool counted = eng->last_dtp_counted;
+    if (R && db->n && !counted) {
         if ((e = mxp_launch_hits(d_match, db->n, R, W, d_hits, s, gate, eng->d_stats.as<unsigned long long>(), gate_next,
                                  force)) != hipSuccess)
             return eng->hipfail(e, "launch hits");
@@ -2049,6 +2066,8 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
         if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
     }
     eng->gate_par ^= 1u;
+    // mxp_kernel_times: the evaluation's span ends after the counters too (streamed or gate only)
+    if (eng->timing && (e = hipEventRecord(eng->ev[2], s)) != hipSuccess) return eng->hipfail(e, "event");
     if ((e = hipEventRecord(eng->stats_ev, s)) != hipSuccess) return eng->hipfail(e, "stats event");
     eng->stats_pending = true;
     return MXP_OK;

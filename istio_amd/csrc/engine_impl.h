@@ -30,6 +30,8 @@ extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hi
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
 extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
 extern "C" hipError_t mxp_launch_dtp_sort(const mxp_kargs* args, hipStream_t s);
+extern "C" hipError_t mxp_launch_dtp_hits(const uint32_t* part, uint32_t tiles, uint32_t n_rules,
+                                          unsigned long long* hits, hipStream_t s);
 extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t s);
 extern "C" hipError_t mxp_launch_vt_eval(const mxp_kargs* args, uint32_t tiles, uint32_t wchunks, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
@@ -329,6 +331,9 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t dtp_cap = 2048, dtp_ovf_cap = 1u << 22;
     DevBuf d_dtp_ent, d_dtp_n, d_dtp_ovf, d_dtp_ovf_n, d_dtp_slots, d_dtp_qn;
     bool last_dtp = false;  // the last launch deferred its index pairs (mxp_kernel_times [2])
+    bool last_dtp_counted = false;  // ... and counted every true pair in its kernels (no streamed counters)
+    static constexpr uint32_t kDtpHist = 16384;  // MXP_DTP_HIST (kernels.hip): rule sets counted by histogram
+    DevBuf d_dtp_part;                // [tiles][(R + 1) / 2] per-tile true-pair histograms
     uint32_t dtp_par = 0;   // d_dtp_ovf_n holds two counter sets: this launch's and the next one's
     hipEvent_t dtp_ev = nullptr;      // recorded after each deferred launch (its last kernel)
     hipStream_t dtp_stream = nullptr; // ... on this stream; a launch on another stream waits for it

@@ -114,6 +114,9 @@ typedef struct mxp_kargs {
     uint16_t* dtp_slots;         // [chunks][tiles * 256 lane quads][8] g << 8 | plane << 7 | request % 4 << 5 | bit
     uint8_t* dtp_qn;             // [chunks][tiles * 256] entries in each quad's slots (<= 8)
     const uint32_t* dtp_gate;    // index re-run with OR-ed pairs: returns unless *dtp_gate (list full)
+    uint32_t* dtp_part;          // fused hit counters of deferred pairs: [tiles][(n_rules + 1) / 2] u16
+                                 // pairs, each sort workgroup's per-rule true pairs (LDS histogram),
+                                 // summed into kargs.hits by mxp_dtp_hits_kernel (null: counted per pair)
     uint32_t dtp_cap, dtp_ovf_cap, dtp_tiles, dtp_nchunks;
     uint32_t dtp_cbase;          // fill launches: chunk id of blockIdx.y 0 (plain fill chunks first, then
                                  // the value-class ones)

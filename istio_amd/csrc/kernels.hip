@@ -125,8 +125,11 @@ __device__ __forceinline__ void dtp_push(const mxp_kargs& A, uint32_t rule, uint
     const uint32_t slot = atomicAdd(&g_dtpn[threadIdx.x >> 6], 1u);
     if (slot < A.dtp_cap) {
         A.dtp_ent[(uint64_t)(req >> 6) * A.dtp_cap + slot] = rule | (plane << 23) | ((req & 63u) << 24);
-        return;
+        return;  // (a true pair in a wave list is counted by mxp_dtp_sort_kernel)
     }
+    // past the wave list (histogram counting): counted here, the sort kernel never sees it
+    if (plane == 0u && A.dtp_part && counting(A))
+        __hip_atomic_fetch_add(A.hits + rule, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t o = atomicAdd(&A.dtp_ovf_n[0], 1u);
     if (o < A.dtp_ovf_cap) {
         A.dtp_ovf[2ull * o] = req;
@@ -141,7 +144,9 @@ __device__ __forceinline__ void set_true1(const mxp_kargs& A, uint32_t rule, uin
     const uint32_t bit = 1u << (rule & 31u);
     if (kDtp) {
         dtp_push(A, rule, req, 0u);
-        if (counting(A)) __hip_atomic_fetch_add(A.hits + rule, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // counted per pair here, or where the pair is filed (kargs.dtp_part: mxp_dtp_sort_kernel's
+        // histogram, dtp_push past the wave list)
+        if (!A.dtp_part && counting(A)) __hip_atomic_fetch_add(A.hits + rule, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     __hip_atomic_fetch_or(A.out_match + (uint64_t)(rule >> 5) * A.n + req, bit, __ATOMIC_RELAXED,
@@ -1482,13 +1487,21 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
 // are staged in LDS and appended to the overflow list with one global atomic per workgroup.
 #define MXP_DTP_WIN 32u
 #define MXP_DTP_OVQ 512u
+#define MXP_DTP_HIST 16384u  // rule sets up to this size count deferred pairs in the sort kernel
 extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs A) {
     // the next evaluation's overflow counters (kargs.dtp_ovf_next): reset here, no memset launch
     if (blockIdx.x == 0 && threadIdx.x < 2u && A.dtp_ovf_next) A.dtp_ovf_next[threadIdx.x] = 0u;
     __shared__ uint32_t cnt[MXP_DTP_WIN * 256u];
     __shared__ uint32_t ovq[MXP_DTP_OVQ][2];
     __shared__ uint32_t ovn, ovbase;
+    // fused hit counters (kargs.dtp_part): per rule the tile's true pairs, two u16 per word (a rule
+    // has at most 1024 pairs in a tile of 1024 requests)
+    __shared__ uint32_t hc[MXP_DTP_HIST / 2u];
     const uint32_t tid = threadIdx.x, t = blockIdx.x;
+    const bool hist = A.dtp_part != nullptr;
+    const uint32_t R2 = (A.n_rules + 1u) / 2u;
+    if (hist)
+        for (uint32_t i = tid; i < R2; i += 256u) hc[i] = 0u;
     const uint32_t nwaves = (A.n + 63u) / 64u, w0 = t * 16u;
     const uint32_t nw = min(16u, nwaves - w0);
     const uint64_t nq = (uint64_t)A.dtp_tiles * 256u;  // quads per chunk row
@@ -1498,11 +1511,13 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
         if (tid == 0) ovn = 0u;
         __syncthreads();
         for (uint32_t w = 0; w < nw; w++) {
-            const uint32_t n = uni(A.dtp_n[w0 + w]);
+            const uint32_t n = min(uni(A.dtp_n[w0 + w]), A.dtp_cap);
             const uint32_t* E = A.dtp_ent + (uint64_t)(w0 + w) * A.dtp_cap;
             for (uint32_t i = tid; i < n; i += 256u) {
                 const uint32_t e = E[i];
                 const uint32_t rule = e & 0x7FFFFFu, ch = A.dtp_chunk[rule >> 5];
+                // fused hit counters (first window pass): a true pair into the workgroup's histogram
+                if (hist && cw0 == 0 && !((e >> 23) & 1u)) atomicAdd(&hc[rule >> 1], 1u << ((rule & 1u) << 4));
                 const uint32_t c = (ch >> 8) - cw0, ql = w * 64u + (e >> 24);
                 if (c >= cwn) continue;
                 const uint32_t at = atomicAdd(&cnt[c * 256u + (ql >> 2)], 1u);
@@ -1528,6 +1543,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
             }
         }
         __syncthreads();
+        if (hist && cw0 == 0)  // the tile's counts, summed over the tiles by mxp_dtp_hits_kernel
+            for (uint32_t i = tid; i < R2; i += 256u) A.dtp_part[(uint64_t)t * R2 + i] = hc[i];
         for (uint32_t i = tid; i < cwn * 256u; i += 256u)
             A.dtp_qn[(uint64_t)(cw0 + (i >> 8)) * nq + t * 256u + (i & 255u)] = (uint8_t)min(cnt[i], 8u);
         const uint32_t no = min(ovn, MXP_DTP_OVQ);
@@ -1546,6 +1563,25 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
     }
 }
 
+
+// The sort workgroups' per-tile histograms summed into the hit counters: a thread sums one u16
+// pair column over 64 tiles (grid y = tile blocks) and adds the two rules' counts.
+extern "C" __global__ __launch_bounds__(256) void mxp_dtp_hits_kernel(const uint32_t* __restrict__ part, uint32_t tiles,
+                                                                      uint32_t n_rules, unsigned long long* hits) {
+    const uint32_t R2 = (n_rules + 1u) / 2u;
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= R2) return;
+    const uint32_t t0 = blockIdx.y * 64u, t1 = min(t0 + 64u, tiles);
+    uint32_t lo = 0, hi = 0;
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; t++) {
+        const uint32_t v = part[(uint64_t)t * R2 + i];
+        lo += v & 0xFFFFu;
+        hi += v >> 16;
+    }
+    if (lo) atomicAdd(hits + 2u * i, (unsigned long long)lo);
+    if (hi && 2u * i + 1u < n_rules) atomicAdd(hits + 2u * i + 1u, (unsigned long long)hi);
+}
 
 // Guard-index phase: the continuing pairs of indexed rules (`attr == K && <continuation>`), found
 // per request by a hash lookup of its column value instead of by comparing against every rule.
@@ -2083,6 +2119,14 @@ extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, ui
         hipLaunchKernelGGL(mxp_guard_kernel, dim3(grid_x, grid_y), dim3(256), 0, s, *args);
     else
         hipLaunchKernelGGL(mxp_guard2_kernel, dim3((grid_x + 1) / 2, grid_y), dim3(256), 0, s, *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_dtp_hits(const uint32_t* part, uint32_t tiles, uint32_t n_rules,
+                                          unsigned long long* hits, hipStream_t s) {
+    const uint32_t R2 = (n_rules + 1u) / 2u;
+    hipLaunchKernelGGL(mxp_dtp_hits_kernel, dim3((R2 + 255u) / 256u, (tiles + 63u) / 64u), dim3(256), 0, s, part, tiles,
+                       n_rules, hits);
     return hipGetLastError();
 }
 

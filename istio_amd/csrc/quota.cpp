@@ -19,7 +19,7 @@ extern "C" hipError_t mxp_launch_quota(const mxp_quota_args* a, const uint32_t* 
 struct mxp_quota {
     uint32_t n_keys = 0;
     DevBuf max_amount, ticks, cells, avail, win_cur, win_tick, slot_off, slots;
-    DevBuf keys_clamped, keys_sorted, idx_in, order, seg_start, tmp;
+    DevBuf keys_clamped, keys_sorted, idx_in, order, seg_start, tmp, samt, sbe;
     size_t cap = 0, tmp_bytes = 0;
 };
 
@@ -81,6 +81,8 @@ int mxp_quota_alloc_device(mxp_engine* eng, mxp_quota* Q, uint32_t n, const uint
         if ((e = Q->keys_clamped.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota keys");
         if ((e = Q->idx_in.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota idx");
         if ((e = Q->order.alloc((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "quota order");
+        if ((e = Q->samt.alloc((size_t)n * 8)) != hipSuccess) return eng->hipfail(e, "quota sorted amounts");
+        if ((e = Q->sbe.alloc((size_t)n)) != hipSuccess) return eng->hipfail(e, "quota sorted flags");
         size_t need = 0;
         if ((e = mxp_quota_sort(nullptr, &need, nullptr, 0, nullptr, nullptr, nullptr, nullptr, n, 32, s)) != hipSuccess)
             return eng->hipfail(e, "quota sort size");
@@ -105,6 +107,8 @@ int mxp_quota_alloc_device(mxp_engine* eng, mxp_quota* Q, uint32_t n, const uint
     A.amount = d_amount;
     A.best_effort = d_best_effort;
     A.order = Q->order.as<uint32_t>();
+    A.samt = Q->samt.as<int64_t>();
+    A.sbe = Q->sbe.as<uint8_t>();
     A.seg_start = Q->seg_start.as<uint32_t>();
     A.granted = d_granted;
     A.delta = d_delta;

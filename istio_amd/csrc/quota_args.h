@@ -13,6 +13,8 @@ typedef struct mxp_quota_args {
     const uint8_t* best_effort;
     const uint32_t* order;       // arrival indices sorted by key (stable)
     const uint32_t* seg_start;   // [n_keys + 1] key k's requests: order[seg_start[k] .. seg_start[k+1])
+    int64_t* samt;               // [n] amounts in sorted order (mxp_quota_gather)
+    uint8_t* sbe;                // [n] best-effort flags in sorted order
     int64_t* granted;            // QuotaResult.Amount per request
     int64_t* delta;              // optional [n_keys] += granted allocs - frees
     // per-key state (HBM, persistent across batches)

@@ -117,17 +117,19 @@ def c2_rules(n_rules=1000, seed=2, n_services=256):
     return rules, ips
 
 
-def c2_workload(n_rules=1000, n_requests=65536, seed=2, n_services=256, p_missing_path=0.01, p_missing_ip=0.005):
-    """C2: ==/startsWith/ip() rules, Zipf(1.1) services.  Returns (manifest, rules, BagBatch)."""
+def c2_workload(n_rules=1000, n_requests=65536, seed=2, n_services=256, p_missing_path=0.01, p_missing_ip=0.005,
+                shard=None):
+    """C2: ==/startsWith/ip() rules, Zipf(1.1) services.  Returns (manifest, rules, BagBatch).
+    shard=(lo, hi): requests [lo, hi) of the n_requests-request batch (every per-request draw is made
+    for the whole batch, so the shards of one seed partition that batch exactly)."""
     rules, ips = c2_rules(n_rules, seed, n_services)
     rng = np.random.default_rng(seed + 1000)
     n = n_requests
+    lo, hi = shard if shard is not None else (0, n)
     ranks = np.arange(1, n_services + 1, dtype=np.float64)
     p = ranks ** -1.1
     p /= p.sum()
     svc = rng.choice(n_services, size=n, p=p)
-    strings = [b"svc%d.ns%d.svc.cluster.local" % (s, s % 8) for s in range(n_services)]
-    dest_vals = svc.astype(np.uint64)
     # request paths: half follow one of the service's own rules' prefixes
     rules_per_svc = max(1, (n_rules + n_services - 1) // n_services)
     follow = rng.random(n) < 0.5
@@ -137,6 +139,18 @@ def c2_workload(n_rules=1000, n_requests=65536, seed=2, n_services=256, p_missin
     pv = np.where(follow, rule_i % 7, rng.integers(0, 7, size=n))
     pr = np.where(follow, rule_i % 97, rng.integers(0, 97, size=n))
     tail = rng.integers(0, 4096, size=n)
+    path_missing = rng.random(n) < p_missing_path
+    # source.ip: 4-byte addresses in 10.0.0.0/8; 5% equal to one of the service's rules' ip
+    hit = rng.random(n) < 0.05
+    a = rng.integers(0, 256, size=n)
+    b = rng.integers(0, 256, size=n)
+    c = rng.integers(0, 256, size=n)
+    ip_missing = rng.random(n) < p_missing_ip
+    svc, rule_i, pv, pr, tail, path_missing = (x[lo:hi] for x in (svc, rule_i, pv, pr, tail, path_missing))
+    hit, a, b, c, ip_missing = (x[lo:hi] for x in (hit, a, b, c, ip_missing))
+    n = hi - lo
+    strings = [b"svc%d.ns%d.svc.cluster.local" % (s, s % 8) for s in range(n_services)]
+    dest_vals = svc.astype(np.uint64)
     base = len(strings)
     path_keys = (pv * 97 + pr) * 4096 + tail
     uniq, inv = np.unique(path_keys, return_inverse=True)
@@ -146,12 +160,7 @@ def c2_workload(n_rules=1000, n_requests=65536, seed=2, n_services=256, p_missin
         q = k // 4096
         strings.append(b"/api/v%d/r%d/item%d" % (q // 97, q % 97, t))
     path_vals = (base + inv).astype(np.uint64)
-    path_kinds = np.where(rng.random(n) < p_missing_path, ABSENT, STRING).astype(np.uint8)
-    # source.ip: 4-byte addresses in 10.0.0.0/8; 5% equal to one of the service's rules' ip
-    hit = rng.random(n) < 0.05
-    a = rng.integers(0, 256, size=n)
-    b = rng.integers(0, 256, size=n)
-    c = rng.integers(0, 256, size=n)
+    path_kinds = np.where(path_missing, ABSENT, STRING).astype(np.uint8)
     ri = np.where(rule_i < n_rules, rule_i, 0)
     a = np.where(hit, ips[ri, 0], a)
     b = np.where(hit, ips[ri, 1], b)
@@ -163,7 +172,7 @@ def c2_workload(n_rules=1000, n_requests=65536, seed=2, n_services=256, p_missin
         k = int(k)
         strings.append(bytes([10, (k >> 16) & 255, (k >> 8) & 255, k & 255]))
     ip_vals = (ibase + iinv).astype(np.uint64)
-    ip_kinds = np.where(rng.random(n) < p_missing_ip, ABSENT, BYTES).astype(np.uint8)
+    ip_kinds = np.where(ip_missing, ABSENT, BYTES).astype(np.uint8)
     cols = {
         "destination.service": (np.full(n, STRING, dtype=np.uint8), dest_vals),
         "request.path": (path_kinds, path_vals),
@@ -545,7 +554,7 @@ C4_MANIFEST = {"request.path": "STRING", "request.headers": "STRING_MAP", "desti
 _C4_HEADERS = ["x-user", "x-env", "x-canary", "user-agent", "x-region"]
 
 
-def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_frac=0.0, paths_only=False):
+def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_frac=0.0, paths_only=False, shard=None):
     """C4: Pilot-shaped HTTP route rules in the Mixer language: 60%
     request.path.startsWith("/p..") (Pilot prefix), 20% "^...".matches(request.path) (Pilot regex:
     prefix -> ^QuoteMeta(p).*), 20% request.headers["h"] == "v" or "re".matches(request.headers["h"]).
@@ -554,6 +563,7 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_fra
     `&& source.ip == ip("10.0.0.K")`, over a source.ip column absent for 30% of the requests -- the
     guard-index kernel then finds true pairs and lookup-error pairs.  paths_only: the header rules'
     share becomes path rules too (a route table matched on paths alone: no value classes).
+    shard=(lo, hi): requests [lo, hi) of the n_requests-request batch (drawn whole, then cut).
     Returns (manifest, rules, BagBatch)."""
     rng = np.random.default_rng(seed)
     words = ["w%d" % i for i in range(vocab)]
@@ -584,10 +594,12 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_fra
     # requests, drawn column-wise (1M requests in seconds): path of depth 1..6, the service, 3 of the
     # 5 headers (distinct names, in draw order) with values v0..v15
     n = n_requests
-    depth = rng.integers(1, 7, size=n)
-    w = rng.integers(0, vocab, size=(n, 6))
-    hdr = np.argsort(rng.random((n, 5)), axis=1)[:, :3]
-    hval = rng.integers(0, 16, size=(n, 3))
+    lo, hi = shard if shard is not None else (0, n)
+    depth = rng.integers(1, 7, size=n)[lo:hi]
+    w = rng.integers(0, vocab, size=(n, 6))[lo:hi]
+    hdr = np.argsort(rng.random((n, 5)), axis=1)[lo:hi, :3]
+    hval = rng.integers(0, 16, size=(n, 3))[lo:hi]
+    n_all, n = n, hi - lo
     strings = [h.encode() for h in _C4_HEADERS] + [v.encode() for v in vals] + [b"svc.default.svc.cluster.local"]
     svc_sid = len(strings) - 1
     paths = {}
@@ -611,8 +623,8 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_fra
         manifest = dict(C4_MANIFEST, **{"source.ip": "IP_ADDRESS"})
         ip0 = len(strings)
         strings.extend(bytes([10, 0, 0, k]) for k in range(4))
-        cols["source.ip"] = (np.where(rng.random(n) < 0.3, ABSENT, BYTES).astype(np.uint8),
-                             (ip0 + rng.integers(0, 4, size=n)).astype(np.uint64))
+        cols["source.ip"] = (np.where(rng.random(n_all)[lo:hi] < 0.3, ABSENT, BYTES).astype(np.uint8),
+                             (ip0 + rng.integers(0, 4, size=n_all)[lo:hi]).astype(np.uint64))
     return manifest, rules, BagBatch.from_columns(n, cols, strings, maps=(moff, mkeys, mvals))
 
 

@@ -19,7 +19,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EVAL_KERNELS = ("mxp_fill_kernel", "mxp_fill_dtp_kernel", "mxp_vtfill_kernel", "mxp_vtfill_lds_kernel", "mxp_vt_classify_kernel",
                 "mxp_vt_eval_kernel", "mxp_guard_kernel", "mxp_guard2_kernel", "mxp_eval_kernel", "mxp_index_kernel",
                 "mxp_index_dtp_kernel", "mxp_index5_kernel", "mxp_dtp_sort_kernel", "mxp_dtp_apply_kernel",
-                "mxp_inject_kernel", "mxp_hits_kernel", "mxp_hits_ragged_kernel")
+                "mxp_inject_kernel", "mxp_hits_kernel", "mxp_hits_ragged_kernel", "mxp_hits_gate_kernel",
+                "mxp_eval_deep_kernel", "mxp_quota_kernel")
 
 
 def per_kernel(path_glob, counter):
@@ -49,7 +50,11 @@ def main():
         table[k] = {"fetch_size_bytes": f, "write_size_bytes": w, "hbm_bytes": 2 * f + w}
         print("%-60s fetch %.4g B  write %.4g B  hbm(2F+W) %.4g B" % (k[:60], f, w, 2 * f + w))
     ev = {k: v for k, v in table.items() if any(k.startswith(e) for e in EVAL_KERNELS)}
-    out = {"workload": a.workload, "rules": a.rules, "requests": a.requests, "kernels": ev,
+    import sys
+    sys.path.insert(0, ROOT)
+    from bench import kernel_fingerprint
+    out = {"workload": a.workload, "rules": a.rules, "requests": a.requests, "fingerprint": kernel_fingerprint(),
+           "kernels": ev,
            "bytes_per_eval": sum(v["hbm_bytes"] for v in ev.values()) if ev else None,
            "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE separate passes; hbm = 2*FETCH + WRITE (gfx950)"}
     json.dump(out, open(os.path.join(a.dir, "pmc_traffic_%s.json" % a.workload), "w"), indent=1)
