@@ -13,6 +13,7 @@ typedef struct mxp_quota_args {
     const uint8_t* best_effort;
     const uint32_t* order;       // arrival indices sorted by key (stable)
     const uint32_t* seg_start;   // [n_keys + 1] key k's requests: order[seg_start[k] .. seg_start[k+1])
+    const uint32_t* skeys;       // [n] the sorted (clamped) key ids
     int64_t* samt;               // [n] amounts in sorted order (mxp_quota_gather)
     uint8_t* sbe;                // [n] best-effort flags in sorted order
     int64_t* granted;            // QuotaResult.Amount per request
@@ -26,4 +27,9 @@ typedef struct mxp_quota_args {
     int64_t* win_tick;           // tick of the current slot
     const uint64_t* slot_off;    // first slot of each window
     int64_t* slots;
+    // long keys cut into pieces (mxp_quota_kernel)
+    uint32_t* big;               // [n_keys + 1] keys holding amounts past +-2^55 (set by mxp_quota_gather)
+    int64_t* prec;               // [6 * (n_keys + 1 + mxp_quota_piece_waves(n))] piece records
+    uint32_t* done;              // [n_keys + 1] pieces finished (0 between batches)
+    int64_t* prof;               // optional [4 * waves] (debug, MXP_QUOTA_PROF): ticks, run steps, clocks
 } mxp_quota_args;
