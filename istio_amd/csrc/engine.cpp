@@ -1467,8 +1467,8 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
             return hipfail(e, "dense masks");
         A.dense_cm = d_dense_cm.as<uint64_t>();
     }
-    if (wave_times) {  // profiling hook (MXP_WAVE_TIMES): per index-kernel wave start / end
-        const size_t need = ((size_t)A.n + 63) / 64 * 24;
+    if (wave_times) {  // profiling hook (MXP_WAVE_TIMES): per index-kernel wave start / end / phase marks
+        const size_t need = ((size_t)A.n + 63) / 64 * 64;
         if (d_wave_t.n < need && (e = d_wave_t.alloc(need)) != hipSuccess) return hipfail(e, "wave times");
         A.wave_t = d_wave_t.as<unsigned long long>();
         wave_t_n = (A.n + 63) / 64;
@@ -1939,7 +1939,7 @@ int mxp_debug_wave_times(mxp_engine* eng, uint64_t* out, uint64_t cap, uint64_t*
     if (!eng->wave_times || !eng->d_wave_t.p) return eng->fail(MXP_ERR_STATE, "MXP_WAVE_TIMES not set");
     hipError_t e;
     if ((e = hipDeviceSynchronize()) != hipSuccess) return eng->hipfail(e, "sync");
-    const uint64_t k = std::min<uint64_t>(cap, (uint64_t)eng->wave_t_n * 3);
+    const uint64_t k = std::min<uint64_t>(cap, (uint64_t)eng->wave_t_n * 8);
     if (k && (e = hipMemcpy(out, eng->d_wave_t.p, k * 8, hipMemcpyDeviceToHost)) != hipSuccess)
         return eng->hipfail(e, "download wave times");
     *n_out = k;

@@ -98,7 +98,7 @@ typedef struct mxp_kargs {
     uint32_t* vt_rep;
     uint32_t n_vt;
     uint32_t nfa;                // some regexp of the rule set or batch is a bit-parallel NFA: the *_nfa kernels
-    unsigned long long* wave_t;  // profiling (MXP_WAVE_TIMES): index kernel waves' {start, end, pairs}
+    unsigned long long* wave_t;  // profiling (MXP_WAVE_TIMES): index kernel waves' {start, end, XCC, 5 phase marks}
     uint8_t* req_err;            // optional [n]: 1 when some rule fails for the request (compact error output)
     // Deferred true pairs (kernels.hip "Deferred pairs"; null dtp_ent / dtp_off: off).  The index
     // kernel runs before the value-class fill and records its true / error pairs per wave instead of

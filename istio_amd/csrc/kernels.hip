@@ -1789,6 +1789,9 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
     if (kDtp && (tid & 63u) == 0) g_dtpn[wave] = 0u;
     if (A.dense_of || kDtp) wave_sync_lds();
     const uint64_t N = A.n;
+    uint32_t nmark = 0;  // profiling (kargs.wave_t): slots done
+    if (A.wave_t && (tid & 63u) == 0)
+        for (uint32_t i = 3; i < 8; i++) A.wave_t[8ull * ((uint64_t)blockIdx.x * 4u + wave) + i] = 0ull;
     // x == n_idx: a last pass with no probes that drains the pair queue
     for (uint32_t x = 0; x <= A.n_idx; x++) {
         const bool final = x == A.n_idx;
@@ -1871,6 +1874,10 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
             }
             if (final || __ballot(len != 0))
                 process_slot<kRefs, kNfa, kDtp>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
+            if (A.wave_t && (tid & 63u) == 0 && (final || nmark < 4u)) {  // profiling: phase marks
+                A.wave_t[8ull * ((uint64_t)blockIdx.x * 4u + wave) + 3u + (final ? 4u : nmark)] = (uint64_t)wall_clock64();
+                nmark++;
+            }
         }
     }
     if (A.dense_of) {  // masks for mxp_inject_kernel
@@ -1889,9 +1896,9 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
     }
     if (A.wave_t && (tid & 63u) == 0) {  // profiling: this wave's start / end (100 MHz clock), XCC
         const uint64_t w = (uint64_t)blockIdx.x * 4u + wave;
-        A.wave_t[3 * w] = t_start;
-        A.wave_t[3 * w + 1] = (uint64_t)wall_clock64();
-        A.wave_t[3 * w + 2] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // hwreg(XCC_ID, 0, 4)
+        A.wave_t[8 * w] = t_start;
+        A.wave_t[8 * w + 1] = (uint64_t)wall_clock64();
+        A.wave_t[8 * w + 2] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // hwreg(XCC_ID, 0, 4)
     }
 }
 

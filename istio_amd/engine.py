@@ -247,13 +247,14 @@ class Engine:
         return list(ms)[: n.value]
 
     def wave_times(self, n_waves: int) -> np.ndarray:
-        """Profiling hook (MXP_WAVE_TIMES=1 at engine creation): [waves, 3] {start, end, XCC} of the
-        last guard-index kernel launch (100 MHz ticks)."""
-        out = np.zeros(3 * n_waves, dtype=np.uint64)
+        """Profiling hook (MXP_WAVE_TIMES=1 at engine creation): [waves, 8] {start, end, XCC} of the
+        last guard-index kernel launch (100 MHz ticks), then 5 phase marks: the end of each of the
+        first 4 probe slots and of the queue drain (0 where the wave had fewer slots)."""
+        out = np.zeros(8 * n_waves, dtype=np.uint64)
         k = ctypes.c_uint64()
         self._check(self.lib.mxp_debug_wave_times(self.h, out.ctypes.data, out.size, ctypes.byref(k)),
                     "mxp_debug_wave_times")
-        return out[:k.value].reshape(-1, 3)
+        return out[:k.value].reshape(-1, 8)
 
     def ruleset_info(self) -> dict:
         """Kernel-side shape of the rule set (guards, continuation templates, column segments)."""

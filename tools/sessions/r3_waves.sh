@@ -1,0 +1,8 @@
+# index-kernel wave timelines with phase marks: C2, C2 probes-only (flag 1024), C4
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+o=gpurun_out/r3w; mkdir -p $o
+timeout -k 10 200 python tools/wave_times.py 1048576 c2 > $o/c2.log 2>&1 || exit $?
+MXP_DEBUG_FLAGS=1024 timeout -k 10 200 python tools/wave_times.py 1048576 c2 > $o/c2_probes.log 2>&1 || exit $?
+timeout -k 10 200 python tools/wave_times.py 1048576 c4 > $o/c4.log 2>&1 || exit $?

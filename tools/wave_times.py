@@ -32,6 +32,7 @@ for _ in range(3):
 torch.cuda.synchronize()
 t = eng.wave_times((n + 63) // 64).astype(np.int64)
 start, end, xcc = t[:, 0], t[:, 1], t[:, 2]
+marks = t[:, 3:8]
 dur = (end - start) / 100.0  # us
 t0 = start.min()
 print("%s: %d waves, kernel span %.1f us (first start -> last end)" % (kind, len(t), (end.max() - t0) / 100.0))
@@ -48,3 +49,14 @@ for a, b in zip(edges[:-1], edges[1:]):
                                                                   (((start - t0) >= a) & ((start - t0) < b)).sum()))
 slow = np.argsort(-dur)[:8]
 print("slowest waves (index, us, start offset us):", [(int(i), round(float(dur[i]), 1), round(float((start[i] - t0) / 100), 1)) for i in slow])
+# phases: start -> slot 0 -> slot 1 -> ... -> drain (per wave, us; 0 marks = slot not reached)
+prev = start.copy()
+for k in range(5):
+    m = marks[:, k]
+    have = m > 0
+    if not have.any():
+        continue
+    d = (m[have] - prev[have]) / 100.0
+    print("phase %s: %d waves, p50 %.1f mean %.1f us" % ("drain" if k == 4 else "slot %d" % k, have.sum(),
+                                                       np.percentile(d, 50), d.mean()))
+    prev = np.where(have, m, prev)
