@@ -1314,6 +1314,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
     A->n = db->n;
     A->kinds = db->kinds.as<uint8_t>();
     A->vals = db->vals.as<uint64_t>();
+    A->heads = db->heads.p && db->heads_ncol == (uint32_t)(cols.size() + vcols.size()) ? db->heads.as<uint4>() : nullptr;
     A->n_gstr = gstrs.size();
     A->gstr_off = d_gstr_off.as<uint64_t>();
     A->gstr = d_gstr.as<uint8_t>();
@@ -1343,6 +1344,29 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
         A->vt_cnt = db->vt_cnt.as<uint32_t>();
         A->n_vt = (uint32_t)P.vt_cols.size();
     }
+}
+
+// String heads of a packed batch (kargs.heads): one gather over every column, on the engine stream,
+// as the last step of packing -- part of the batch layout, like the columns themselves.
+int mxp_engine::pack_heads(mxp_dbatch* db) {
+    const uint32_t ncol = (uint32_t)(cols.size() + vcols.size());
+    if (!heads_on || !db->n || !ncol) return MXP_OK;
+    hipError_t e;
+    if ((e = db->heads.alloc((size_t)ncol * db->n * 16)) != hipSuccess) return hipfail(e, "string heads");
+    mxp_kargs A;
+    memset(&A, 0, sizeof A);
+    A.n = db->n;
+    A.kinds = db->kinds.as<uint8_t>();
+    A.vals = db->vals.as<uint64_t>();
+    A.n_gstr = gstrs.size();
+    A.gstr_off = d_gstr_off.as<uint64_t>();
+    A.gstr = d_gstr.as<uint8_t>();
+    A.bstr_off = db->bstr_off.as<uint64_t>();
+    A.bstr = db->bstr.as<uint8_t>();
+    if ((e = mxp_launch_heads(&A, ncol, db->heads.as<uint4>(), stream)) != hipSuccess) return hipfail(e, "launch heads");
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "heads sync");
+    db->heads_ncol = ncol;
+    return MXP_OK;
 }
 
 // The batch's value-class layout under plan P (first launch of the batch): per active slot its
@@ -1786,6 +1810,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_FILL_SPAN")) e->fill_span = (uint32_t)std::min(8, std::max(1, atoi(f)));
     if (const char* f = getenv("MXP_ERRCAP")) e->errcap = (uint32_t)std::max(1, atoi(f));
     if (getenv("MXP_WAVE_TIMES")) e->wave_times = true;
+    if (const char* h = getenv("MXP_HEADS")) e->heads_on = atoi(h) != 0;
     if (const char* f = getenv("MXP_HOST_PACK")) e->host_pack = atoi(f) != 0;  // A/B: the host packer
     if (device < 0) {  // host-only engine (compiler / lowering inspection without a GPU)
         e->reset_tables();

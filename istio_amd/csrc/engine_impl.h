@@ -26,6 +26,7 @@
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
+extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, uint32_t ncol, uint4* heads, hipStream_t s);
 extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
 extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
@@ -135,6 +136,8 @@ struct mxp_dbatch {
     DevBuf vt_cls, vt_keys, vt_rep, vt_cnt, vt_t, vt_meta;
     size_t vt_t_words = 0, vt_keys_n = 0;
     DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
+    DevBuf heads;                                     // [n_cols][n] string heads (kargs.heads)
+    uint32_t heads_ncol = 0;                          // columns the heads cover
     DevBuf rxof, rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // run-time regexp patterns
     bool rx_nfa = false;                              // one of them compiled to a bit-parallel NFA
     StrPool overlay;                                  // batch strings not in the rule set's pool
@@ -554,7 +557,12 @@ struct mxp_engine : public mxp::LowerTables {
     int pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H);
     // mxp_batch_upload: the device packer (pack_device.cpp), or the host one (MXP_HOST_PACK=1, and
     // rule sets reading more than MXP_PACK_MAXCOL columns)
-    int pack(const mxp_bag_batch* b, mxp_dbatch* db) { return host_pack ? pack_on_host(b, db) : pack_device(b, db); }
+    int pack(const mxp_bag_batch* b, mxp_dbatch* db) {
+        const int rc = host_pack ? pack_on_host(b, db) : pack_device(b, db);
+        return rc ? rc : pack_heads(db);
+    }
+    int pack_heads(mxp_dbatch* db);  // kargs.heads of every column (MXP_HEADS=0: none)
+    bool heads_on = true;
     int pack_on_host(const mxp_bag_batch* b, mxp_dbatch* db);
     int pack_device(const mxp_bag_batch* b, mxp_dbatch* db);
     int pack_vt_tables(mxp_dbatch* db);  // the value-class tables of the active slots

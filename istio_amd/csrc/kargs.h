@@ -121,4 +121,9 @@ typedef struct mxp_kargs {
     uint32_t dtp_cbase;          // fill launches: chunk id of blockIdx.y 0 (plain fill chunks first, then
                                  // the value-class ones)
     uint32_t post_tmpl;
+    // string heads ([n_cols][n] 16 bytes, null: none): a string value's first 12 bytes (zero past its
+    // length) and its length in the last word -- the batch layout's inline view of every string
+    // value, so the index kernel hashes and verifies short prefixes without the string's descriptor
+    // and bytes (two dependent scattered loads per request)
+    const uint4* heads;
 } mxp_kargs;

@@ -1662,9 +1662,11 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
 }
 
 // Appends every lane's postings [start, start + len) to the queue (direct postings are true pairs:
-// OR-ed at once) and runs full 64-pair batches; `final` drains the queue.  Long lists go in rounds
-// of up to (free entries / 64) postings per lane, so the queue never overflows and the VM has one
-// call site (one inlined copy).
+// OR-ed at once) and runs full 64-pair batches; `final` drains the queue.  The free entries are
+// shared out by a prefix sum over the lanes' remaining postings (lower lanes first), so the queue
+// never overflows, one lane's long list fills whole batches (C2: a request without a path takes its
+// service's ~39 equality postings in one round, not ten rounds of four), and the VM has one call
+// site (one inlined copy).
 template <bool kRefs, bool kNfa, bool kDtp>
 __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, uint32_t tbl, uint32_t start,
                                              uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
@@ -1674,8 +1676,9 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
     uint32_t j0 = 0;
     for (;;) {
         if (Q.n < 64u && __ballot(j0 < len)) {
-            const uint32_t c = (MXP_IXQ - Q.n) / 64u;  // >= 3
-            const uint32_t take = min(len - j0, c);
+            const uint32_t want = j0 < len ? len - j0 : 0u, freeq = MXP_IXQ - Q.n;  // freeq > 192
+            const uint32_t before = wave_incl_sum(want, lane) - want;
+            const uint32_t take = before >= freeq ? 0u : min(want, freeq - before);
             // posting-major order: entry j of every lane, then entry j + 1, ...  Lanes whose requests
             // share a posting list (a common key) put the SAME rule side by side, so a 64-pair batch
             // runs one rule's constants and its true bits -- and its aliases' -- land in one bitmap
@@ -1752,7 +1755,26 @@ struct PrefixHash {
         if (rem) hl = mxp_str_step(hl, ld8a(p + words * 8u) & ((1ull << (rem * 8u)) - 1ull));
         return mxp_str_final(hl, L);
     }
+    // the same hash from a string head (kargs.heads): L <= 12, words w0 (bytes 0..7), w1 (8..11)
+    __device__ __forceinline__ uint64_t at_head(uint64_t w0, uint64_t w1, uint32_t L) {
+        if (words == 0u && L >= 8u) {
+            h = mxp_str_step(h, w0);
+            words = 1u;
+        }
+        uint64_t hl = h;
+        const uint32_t rem = L - words * 8u;
+        if (rem) hl = mxp_str_step(hl, (words ? w1 : w0) & ((1ull << (rem * 8u)) - 1ull));
+        return mxp_str_final(hl, L);
+    }
 };
+
+// L leading bytes of a head (words w0, w1; L <= 12) against a key string at an 8-aligned address
+__device__ __forceinline__ bool head_eq(uint64_t w0, uint64_t w1, const uint8_t* k, uint32_t L) {
+    const uint64_t m0 = L >= 8u ? ~0ull : (1ull << (L * 8u)) - 1ull;
+    if ((w0 ^ ld8a(k)) & m0) return false;
+    if (L <= 8u) return true;
+    return ((w1 ^ ld8a(k + 8)) & ((1ull << ((L - 8u) * 8u)) - 1ull)) == 0ull;
+}
 
 
 }  // namespace
@@ -1766,7 +1788,9 @@ struct PrefixHash {
 // guard column); true and error results are OR-ed in.
 namespace {
 
-template <bool kRefs, bool kNfa = kRefs, bool kDtp = false>
+// kProf: the profiling instantiations (kargs.wave_t, MXP_WAVE_TIMES) -- the hot kernels carry no
+// timing code
+template <bool kRefs, bool kNfa = kRefs, bool kDtp = false, bool kProf = false>
 __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
     // after the fill (kargs.dtp_gate): the deferred pairs' overflow list OR-ed in, then -- only when
     // that list filled -- every pair again
@@ -1779,19 +1803,20 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
         }
         if (uni(*A.dtp_gate) == 0u) return;
     }
-    const uint64_t t_start = A.wave_t ? (uint64_t)wall_clock64() : 0ull;
     const uint32_t tid = threadIdx.x;
     const uint32_t wave = uni(tid >> 6);
-    PairQueue Q{wave, 0u, 0u, A.q0 + (blockIdx.x * 4u + wave) * 64u};
+    const uint64_t N = A.n;
+    const uint32_t tile = blockIdx.x * 4u + wave;  // 64 requests per wave
+    const uint64_t t_start = kProf ? (uint64_t)wall_clock64() : 0ull;
+    PairQueue Q{wave, 0u, 0u, A.q0 + tile * 64u};
     const uint32_t req = Q.base + (tid & 63u);
     const bool valid = req < A.q1;
     if (A.dense_of) g_cm[wave][tid & 63u] = 0ull;
     if (kDtp && (tid & 63u) == 0) g_dtpn[wave] = 0u;
     if (A.dense_of || kDtp) wave_sync_lds();
-    const uint64_t N = A.n;
     uint32_t nmark = 0;  // profiling (kargs.wave_t): slots done
-    if (A.wave_t && (tid & 63u) == 0)
-        for (uint32_t i = 3; i < 8; i++) A.wave_t[8ull * ((uint64_t)blockIdx.x * 4u + wave) + i] = 0ull;
+    if (kProf && (tid & 63u) == 0)
+        for (uint32_t i = 3; i < 8; i++) A.wave_t[8ull * tile + i] = 0ull;
     // x == n_idx: a last pass with no probes that drains the pair queue
     for (uint32_t x = 0; x <= A.n_idx; x++) {
         const bool final = x == A.n_idx;
@@ -1825,8 +1850,23 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 if (sok) sv = vv;
             }
         }
+        // short keys (every key length <= 12) hash and verify from the string's head (kargs.heads):
+        // one coalesced 16-byte load instead of the descriptor and the bytes (scattered, dependent)
+        const uint32_t lmax = (!final && kind != MXP_IX_EQ && nplen) ? uni(A.plens[plen0 + nplen - 1u]) : 0u;
+        const bool by_head = A.heads && lmax <= 12u;
+        // (the head's first word rides in the string pointer's registers: one of the two is live)
         StrRef s{nullptr, 0};
-        if (sok) s = str_of(A, sv);
+        uint32_t hw1 = 0;
+        if (sok) {
+            if (by_head) {
+                const uint4 hd = A.heads[(uint64_t)(comp ? uni(X->col2) : col) * N + req];
+                s.p = (const uint8_t*)((uint64_t)hd.x | ((uint64_t)hd.y << 32));
+                hw1 = hd.z;
+                s.n = hd.w;
+            } else {
+                s = str_of(A, sv);
+            }
+        }
         PrefixHash ph{comp ? mxp_composite_seed(v) : 0ull, 0};
         const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
         // probe slots: equality 1; prefix one per key length (shortest first); composite the
@@ -1845,7 +1885,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 // ROCm 7.2 hipcc: lanes resumed with another entry's range)
                 uint32_t fi = 0xFFFFFFFFu;
                 if (sok && L <= s.n) {
-                    const uint64_t hf = ph.at(s.p, L);
+                    const uint64_t hf = by_head ? ph.at_head((uint64_t)s.p, hw1, L) : ph.at(s.p, L);
                     const uint32_t tag = (uint32_t)(hf >> 32);
                     const uint32_t stride = comp ? 2u : 1u;
                     for (uint32_t slot = (uint32_t)hf & pmask;; slot = (slot + 1) & pmask) {
@@ -1857,7 +1897,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                         if (E.khi != tag) continue;
                         if (comp && (K.klo != vlo || K.khi != vhi)) continue;
                         const StrRef k = str_of(A, E.klo);
-                        if (k.n == L && bytes_eq_a(s.p, k.p, L)) {
+                        if (k.n == L && (by_head ? head_eq((uint64_t)s.p, hw1, k.p, L) : bytes_eq_a(s.p, k.p, L))) {
                             fi = at;
                             break;
                         }
@@ -1874,8 +1914,8 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
             }
             if (final || __ballot(len != 0))
                 process_slot<kRefs, kNfa, kDtp>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
-            if (A.wave_t && (tid & 63u) == 0 && (final || nmark < 4u)) {  // profiling: phase marks
-                A.wave_t[8ull * ((uint64_t)blockIdx.x * 4u + wave) + 3u + (final ? 4u : nmark)] = (uint64_t)wall_clock64();
+            if (kProf && (tid & 63u) == 0 && (final || nmark < 4u)) {  // profiling: phase marks
+                A.wave_t[8ull * tile + 3u + (final ? 4u : nmark)] = (uint64_t)wall_clock64();
                 nmark++;
             }
         }
@@ -1884,21 +1924,20 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
         wave_sync_lds();
         if (valid) A.dense_cm[req] = g_cm[wave][tid & 63u];
     }
-    if (kDtp) {  // the wave's deferred-pair count for mxp_dtp_sort_kernel
+    if (kDtp) {  // the tile's deferred-pair count for mxp_dtp_sort_kernel
         wave_sync_lds();
         if ((tid & 63u) == 0) A.dtp_n[Q.base >> 6] = min(g_dtpn[wave], A.dtp_cap);
+    }
+    if (kProf && (tid & 63u) == 0) {  // profiling: this tile's start / end (100 MHz clock), XCC
+        A.wave_t[8ull * tile] = t_start;
+        A.wave_t[8ull * tile + 1] = (uint64_t)wall_clock64();
+        A.wave_t[8ull * tile + 2] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // hwreg(XCC_ID, 0, 4)
     }
     if (A.stats) {
         uint32_t t = Q.ntrue;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) t += (uint32_t)__shfl_xor((int)t, off, 64);
         if ((tid & 63u) == 0 && t) atomicAdd((unsigned long long*)A.stats, (unsigned long long)t);
-    }
-    if (A.wave_t && (tid & 63u) == 0) {  // profiling: this wave's start / end (100 MHz clock), XCC
-        const uint64_t w = (uint64_t)blockIdx.x * 4u + wave;
-        A.wave_t[8 * w] = t_start;
-        A.wave_t[8 * w + 1] = (uint64_t)wall_clock64();
-        A.wave_t[8 * w + 2] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // hwreg(XCC_ID, 0, 4)
     }
 }
 
@@ -1915,6 +1954,15 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void mxp_index_dtp_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<false, false, true>(A, regs);
+}
+// profiling (MXP_WAVE_TIMES): the two hot instantiations with wave start / end / phase marks
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void mxp_index_prof_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    index_body<false, false, false, true>(A, regs);
+}
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void mxp_index_dtp_prof_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    index_body<false, false, true, true>(A, regs);
 }
 // MXP_DEBUG_FLAGS 8192: the same body at 5 waves/SIMD (no scratch) -- A/B ablation
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index5_kernel(mxp_kargs A) {
@@ -2188,13 +2236,39 @@ extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hip
         hipLaunchKernelGGL(mxp_index_refs_kernel, dim3(grid), dim3(256), 0, s, *args);
     else if (args->nfa)
         hipLaunchKernelGGL(mxp_index_nfa_kernel, dim3(grid), dim3(256), 0, s, *args);
+    else if (args->dtp_ent && args->wave_t)
+        hipLaunchKernelGGL(mxp_index_dtp_prof_kernel, dim3(grid), dim3(256), 0, s, *args);
     else if (args->dtp_ent)
         hipLaunchKernelGGL(mxp_index_dtp_kernel, dim3(grid), dim3(256), 0, s, *args);
+    else if (args->wave_t)
+        hipLaunchKernelGGL(mxp_index_prof_kernel, dim3(grid), dim3(256), 0, s, *args);
     else
         if (args->flags & 8192u)
             hipLaunchKernelGGL(mxp_index5_kernel, dim3(grid), dim3(256), 0, s, *args);
         else
             hipLaunchKernelGGL(mxp_index_kernel, dim3(grid), dim3(256), 0, s, *args);
+    return hipGetLastError();
+}
+
+// String heads (kargs.heads): per column and request, a string value's first 12 bytes (zero past
+// its length; pools are 8-aligned with 16 bytes of tail slack) and its length; zero for other kinds.
+extern "C" __global__ __launch_bounds__(256) void mxp_heads_kernel(mxp_kargs A, uint4* __restrict__ heads) {
+    const uint32_t req = blockIdx.x * 256u + threadIdx.x, col = blockIdx.y;
+    if (req >= A.n) return;
+    const uint64_t at = (uint64_t)col * A.n + req;
+    uint4 h = make_uint4(0u, 0u, 0u, 0u);
+    if (A.kinds[at] == MXP_STRING) {
+        const StrRef r = str_of(A, A.vals[at]);
+        const uint64_t w0 = r.n ? ld8a(r.p) : 0ull, w1 = r.n > 8u ? ld8a(r.p + 8) : 0ull;
+        const uint64_t m0 = r.n >= 8u ? ~0ull : (1ull << (r.n * 8u)) - 1ull;
+        const uint64_t m1 = r.n >= 12u ? 0xFFFFFFFFull : r.n > 8u ? (1ull << ((r.n - 8u) * 8u)) - 1ull : 0ull;
+        h = make_uint4((uint32_t)(w0 & m0), (uint32_t)((w0 & m0) >> 32), (uint32_t)(w1 & m1), r.n);
+    }
+    heads[at] = h;
+}
+
+extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, uint32_t ncol, uint4* heads, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_heads_kernel, dim3((args->n + 255u) / 256u, ncol), dim3(256), 0, s, *args, heads);
     return hipGetLastError();
 }
 

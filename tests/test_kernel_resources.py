@@ -17,7 +17,10 @@ MIN_OCCUPANCY = {"mxp_guard_kernel": 8, "mxp_guard2_kernel": 6, "mxp_eval_kernel
 # lane) and still beats the spill-free 5-wave build (mxp_index5_kernel) on C4 (5.10 vs 5.31 ms)
 # (6 waves/SIMD: a few VGPRs spill -- windowed DFA walk, same-box A/B C4 2.67-2.77 -> 2.57-2.66 ms; the
 # 5-wave ablation kernel spills 20 bytes since the DFA walk exits at REJECT)
-MAX_SCRATCH = {"mxp_index_kernel": 40, "mxp_index_dtp_kernel": 48, "mxp_index5_kernel": 24}
+# (r3: string-head probes and the prefix-sum queue share add spills -- 36/44 -> 52/56 bytes -- and
+# still measured faster, C2 0.562 -> 0.532 ms same-box, profiles/r3_v2_ab_*.log)
+MAX_SCRATCH = {"mxp_index_kernel": 56, "mxp_index_dtp_kernel": 60, "mxp_index5_kernel": 24,
+               "mxp_index_prof_kernel": 96, "mxp_index_dtp_prof_kernel": 96}
 
 
 def resource_usage(src):

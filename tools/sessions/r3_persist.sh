@@ -1,0 +1,8 @@
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp
+o=gpurun_out/r3p; mkdir -p $o
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_dtp.py tests/test_gpu_scale.py -x -q --timeout 200 --timeout-method thread > $o/parity.log 2>&1 || exit $?
+AB_COMPACT=1 bash tools/ab_libs.sh c2 ablib/libmxp_scan.so ablib/libmxp_persist.so > $o/ab_c2.log 2>&1 || exit $?
+AB_COMPACT=1 timeout -k 10 200 python tools/ab.py c4 MXP_IX_PERSIST=0 MXP_IX_PERSIST=1 > $o/ab_c4_flag.log 2>&1 || exit $?
+timeout -k 10 200 python tools/wave_times.py 1048576 c2 > $o/waves_c2.log 2>&1 || exit $?
