@@ -1369,6 +1369,29 @@ int mxp_engine::pack_heads(mxp_dbatch* db) {
     return MXP_OK;
 }
 
+// The value-class dictionary of a packed batch, part of its layout like the interned columns: per
+// active column the distinct class keys (a hash table at most half full), the first request that
+// claimed each (its representative, on which mxp_vt_eval_kernel evaluates the column's rules) and
+// the class sizes (the value-class rules' hit counters).  Every evaluation then only looks its
+// requests' classes up (mxp_vt_lookup_kernel).
+int mxp_engine::pack_dict(mxp_dbatch* db) {
+    if (!db->vt_mask || !db->n) return MXP_OK;
+    Plan* P = nullptr;
+    int rc = get_plan(db->vt_mask, &P);
+    if (rc) return rc;
+    if ((rc = vt_prepare(db, *P))) return rc;
+    hipError_t e;
+    if ((e = hipMemsetAsync(db->vt_keys.p, 0xFF, db->vt_keys_n * 8, stream)) != hipSuccess) return hipfail(e, "vt reset");
+    if ((e = hipMemsetAsync(db->vt_cnt.p, 0, db->vt_keys_n * 4, stream)) != hipSuccess) return hipfail(e, "vt count reset");
+    mxp_kargs A;
+    fill_args(&A, db, *P);
+    A.q0 = 0;
+    A.q1 = db->n;
+    if ((e = mxp_launch_vt_classify(&A, stream)) != hipSuccess) return hipfail(e, "launch vt classify");
+    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "vt dictionary sync");
+    return MXP_OK;
+}
+
 // The batch's value-class layout under plan P (first launch of the batch): per active slot its
 // column, class table capacity, offsets into the key / representative tables and the class words.
 int mxp_engine::vt_prepare(mxp_dbatch* db, const Plan& P) {
@@ -1513,12 +1536,10 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     if (A.n_vt) {
         // value classes: classify every request of [lo, hi) per active column, then evaluate the
         // columns' rules once per class (class records -> errcount[2], the host expands them)
-        if ((e = hipMemsetAsync(db->vt_keys.p, 0xFF, db->vt_keys_n * 8, s)) != hipSuccess) return hipfail(e, "vt reset");
-        if (A.hits && (e = hipMemsetAsync(db->vt_cnt.p, 0, db->vt_keys_n * 4, s)) != hipSuccess)
-            return hipfail(e, "vt count reset");
+        // (the batch's dictionary -- keys, representatives, class sizes -- was built at upload)
         A.q0 = lo;
         A.q1 = hi;
-        if ((e = mxp_launch_vt_classify(&A, s)) != hipSuccess) return hipfail(e, "launch vt classify");
+        if ((e = mxp_launch_vt_lookup(&A, s)) != hipSuccess) return hipfail(e, "launch vt lookup");
         mxp_kargs AV = A;
         if (A.errlog) {  // class records: a log of their own, counted in errcount[2]
             if (!d_vtlog.p && (e = d_vtlog.alloc((size_t)vtlog_cap * sizeof(mxp_err_rec))) != hipSuccess)

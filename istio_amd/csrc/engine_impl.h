@@ -34,6 +34,7 @@ extern "C" hipError_t mxp_launch_dtp_sort(const mxp_kargs* args, hipStream_t s);
 extern "C" hipError_t mxp_launch_dtp_hits(const uint32_t* part, uint32_t tiles, uint32_t n_rules,
                                           unsigned long long* hits, hipStream_t s);
 extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t s);
+extern "C" hipError_t mxp_launch_vt_lookup(const mxp_kargs* args, hipStream_t s);
 extern "C" hipError_t mxp_launch_vt_eval(const mxp_kargs* args, uint32_t tiles, uint32_t wchunks, hipStream_t s);
 extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_t n_rules, uint32_t n_words,
                                       unsigned long long* hits, hipStream_t s, const uint32_t* gate = nullptr,
@@ -558,9 +559,11 @@ struct mxp_engine : public mxp::LowerTables {
     // mxp_batch_upload: the device packer (pack_device.cpp), or the host one (MXP_HOST_PACK=1, and
     // rule sets reading more than MXP_PACK_MAXCOL columns)
     int pack(const mxp_bag_batch* b, mxp_dbatch* db) {
-        const int rc = host_pack ? pack_on_host(b, db) : pack_device(b, db);
-        return rc ? rc : pack_heads(db);
+        int rc = host_pack ? pack_on_host(b, db) : pack_device(b, db);
+        if (!rc) rc = pack_heads(db);
+        return rc ? rc : pack_dict(db);
     }
+    int pack_dict(mxp_dbatch* db);   // the value-class dictionary of the batch (mxp_vt_classify_kernel)
     int pack_heads(mxp_dbatch* db);  // kargs.heads of every column (MXP_HEADS=0: none)
     bool heads_on = true;
     int pack_on_host(const mxp_bag_batch* b, mxp_dbatch* db);

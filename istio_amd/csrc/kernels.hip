@@ -1009,6 +1009,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_kernel(mxp_kargs A) {
 // the workgroup's distinct keys always fit).
 #define MXP_VTC_REQ 1024u
 #define MXP_VTC_LCAP 2048u
+// The batch's value-class dictionary, built once at upload (mxp_engine::pack_dict): per active column
+// the class keys, a representative request of each and the class sizes.
 extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kargs A) {
     // The hot keys of a low-cardinality column would serialise on a handful of global addresses if
     // every request probed the global table (and L1 may keep a stale EMPTY line), so a workgroup
@@ -1019,7 +1021,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
     __shared__ uint32_t lcls[MXP_VTC_LCAP];
     __shared__ uint32_t lrep[MXP_VTC_LCAP];
     __shared__ uint32_t lcnt[MXP_VTC_LCAP];  // requests per local slot (class sizes, with A.hits)
-    const bool count = counting(A);  // class sizes feed mxp_vt_eval_kernel's fused counters
+    const bool count = true;  // class sizes (feed mxp_vt_eval_kernel's fused hit counters)
     const uint32_t tid = threadIdx.x;
     const uint64_t N = A.n;
     const uint32_t base = A.q0 + blockIdx.x * MXP_VTC_REQ;
@@ -1093,14 +1095,30 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
             if (count) atomicAdd(A.vt_cnt + kb + h, lcnt[i]);
         }
         __syncthreads();
-        // 3. classes out
-#pragma unroll
-        for (uint32_t r = 0; r < MXP_VTC_REQ / 256u; r++) {
-            const uint32_t req = base + tid + 256u * r;
-            if (req < A.q1) A.vt_cls[(uint64_t)a * N + req] = (uint16_t)lcls[loc[r]];
-        }
+        (void)loc;  // (the classes of the requests are the evaluation's: mxp_vt_lookup_kernel)
         __syncthreads();
     }
+}
+
+// The evaluation's class of every request [q0, q1) per active column: a read-only probe of the
+// batch's dictionary (built at upload by mxp_vt_classify_kernel, so it holds every key of the
+// batch), whose few hot lines stay in L1.  grid (request blocks of 256, active columns).
+extern "C" __global__ __launch_bounds__(256) void mxp_vt_lookup_kernel(mxp_kargs A) {
+    const uint32_t a = blockIdx.y, req = A.q0 + blockIdx.x * 256u + threadIdx.x;
+    if (req >= A.q1) return;
+    const uint64_t N = A.n;
+    const uint32_t col = uni(A.vt_meta[a * 8u + MXP_VTM_COL]), cap = uni(A.vt_meta[a * 8u + MXP_VTM_CAP]),
+                   kb = uni(A.vt_meta[a * 8u + MXP_VTM_KBASE]);
+    const unsigned long long key = mxp_vt_key(A.kinds[(uint64_t)col * N + req], A.vals[(uint64_t)col * N + req]);
+    const unsigned long long* __restrict__ T = A.vt_keys + kb;
+    uint32_t h = mxp_hash64(key) & (cap - 1u);
+    // (every batch key is in the table, which is at most half full: the probe ends at the key; an
+    // empty slot -- a batch changed after upload -- ends it too, on a slot vt_eval leaves at 0)
+    for (uint32_t i = 0; i < cap; i++, h = (h + 1u) & (cap - 1u)) {
+        const unsigned long long k = T[h];
+        if (k == key || k == MXP_VT_EMPTY) break;
+    }
+    A.vt_cls[(uint64_t)a * N + req] = (uint16_t)h;
 }
 
 // grid x: class tiles of 64 (slot by slot), y: groups of 4 words (one per wave)
@@ -1950,8 +1968,11 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<false>(A, regs);
 }
-// deferred index pairs (kargs.dtp_ent): true / error pairs recorded for the value-class fill
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void mxp_index_dtp_kernel(mxp_kargs A) {
+// deferred index pairs (kargs.dtp_ent): true / error pairs recorded for the value-class fill.  5
+// waves/SIMD (96 VGPRs, 20 bytes of scratch) against 6 (80 VGPRs, 56 bytes of spills, which the PMC
+// counters see as ~80 MB of scratch writes per C2 evaluation): same-box C2 0.531 / 0.532 -> 0.524 /
+// 0.522 ms, C4 1.512 / 1.536 -> 1.491 / 1.519 ms (4 waves: 0.522, 1.514; profiles/r3_v3_ab_ix_occupancy_*.log)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index_dtp_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<false, false, true>(A, regs);
 }
@@ -1960,7 +1981,7 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<false, false, false, true>(A, regs);
 }
-extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void mxp_index_dtp_prof_kernel(mxp_kargs A) {
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index_dtp_prof_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<false, false, true, true>(A, regs);
 }
@@ -2214,6 +2235,11 @@ extern "C" hipError_t mxp_launch_dtp_sort(const mxp_kargs* args, hipStream_t s) 
 extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t s) {
     hipLaunchKernelGGL(mxp_vt_classify_kernel, dim3((args->q1 - args->q0 + MXP_VTC_REQ - 1u) / MXP_VTC_REQ), dim3(256), 0, s,
                        *args);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_vt_lookup(const mxp_kargs* args, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_vt_lookup_kernel, dim3((args->q1 - args->q0 + 255u) / 256u, args->n_vt), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 

@@ -24,14 +24,19 @@ def mxp(libmxp):
 MANIFEST = {"request.path": "STRING", "destination.service": "STRING", "request.size": "INT64"}
 
 
-def head_rules():
-    keys = ["/", "/a", "/ab", "/abcdefg", "/abcdefgh", "/abcdefgh1", "/abcdefghij", "/abcdefghijk",
-            "/abcdefghijkl", "/abcdefghijklm", "/abcdefghijklmnop", "/été/x", "/abcdefghé"]
+SHORT = ["/", "/a", "/ab", "/abcdefg", "/abcdefgh", "/abcdefgh1", "/abcdefghij", "/abcdefghijk",
+         "/été/x", "/abcdefghé", "/abcdefghi\u00e9"]
+LONG = SHORT + ["/abcdefghijkl", "/abcdefghijklm", "/abcdefghijklmnop"]
+
+
+def head_rules(keys=SHORT):
+    """keys of at most 12 bytes (the index reads heads) or some longer (it reads the strings)"""
+    assert all(len(k.encode()) <= 12 for k in SHORT)
     rules = []
     for k in keys:
         rules.append('request.path.startsWith("%s")' % k)  # prefix index
         rules.append('destination.service == "s1" && request.path.startsWith("%s")' % k)  # composite
-        rules.append('destination.service == "s2" && request.path.startsWith("%s") && request.size > 10' % k)
+        rules.append('destination.service == "s2" && request.path.startsWith("%s") && request.size == 10' % k)
     return rules, keys
 
 
@@ -54,9 +59,10 @@ def head_bags(keys, n, seed):
 
 
 @pytest.mark.parametrize("heads", ["1", "0"])
-def test_heads_prefix_parity(mxp, monkeypatch, heads):
+@pytest.mark.parametrize("keyset", ["short", "long"])
+def test_heads_prefix_parity(mxp, monkeypatch, heads, keyset):
     monkeypatch.setenv("MXP_HEADS", heads)
-    rules, keys = head_rules()
+    rules, keys = head_rules(SHORT if keyset == "short" else LONG)
     batch = head_bags(keys, 3000, seed=11)
     eng = mxp.Engine(0)
     eng.set_vocabulary(MANIFEST)

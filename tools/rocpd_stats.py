@@ -1,14 +1,23 @@
-"""Per-kernel statistics from a rocprofv3 SQLite output (run_results.db), split into the bench's
+"""Per-kernel statistics from a rocprofv3 SQLite output (run_results.db) or kernel-trace CSV, split into the bench's
 workload blocks (C2, C4, C5, in launch order) by the dispatch-order position of each launch:
     python tools/rocpd_stats.py <db> [n_blocks]"""
+import csv
 import sqlite3
 import sys
+
+
+def load(path):
+    """(name, start ns, end ns) of every dispatch, by start: a rocprofv3 SQLite output or its
+    --output-format csv kernel trace (*_kernel_trace.csv)"""
+    if path.endswith(".csv"):
+        rows = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(path))]
+        return sorted(rows, key=lambda r: r[1])
+    return list(sqlite3.connect(path).execute("select name, start, end from kernels order by start"))
 from collections import defaultdict
 
 db = sys.argv[1]
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-c = sqlite3.connect(db)
-rows = list(c.execute("select name, start, end from kernels order by start"))
+rows = load(db)
 n = len(rows)
 # block boundaries: equal share of the index-kernel launches (one per evaluation and block)
 marks = [i for i, r in enumerate(rows) if r[0].startswith("mxp_index_dtp_kernel") or r[0].startswith("mxp_index_kernel")]
