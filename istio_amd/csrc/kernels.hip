@@ -1509,12 +1509,14 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
 extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs A) {
     // the next evaluation's overflow counters (kargs.dtp_ovf_next): reset here, no memset launch
     if (blockIdx.x == 0 && threadIdx.x < 2u && A.dtp_ovf_next) A.dtp_ovf_next[threadIdx.x] = 0u;
-    __shared__ uint32_t cnt[MXP_DTP_WIN * 256u];
+    // entries per (chunk of the window, quad): two u16 counters per word (a quad gets at most 4 x 512
+    // pairs of one chunk)
+    __shared__ uint32_t cnt[MXP_DTP_WIN * 128u];
     __shared__ uint32_t ovq[MXP_DTP_OVQ][2];
     __shared__ uint32_t ovn, ovbase;
     // fused hit counters (kargs.dtp_part): per rule the tile's true pairs, two u16 per word (a rule
     // has at most 1024 pairs in a tile of 1024 requests)
-    __shared__ uint32_t hc[MXP_DTP_HIST / 2u];
+    extern __shared__ uint32_t hc[];  // (dynamic: (n_rules + 1) / 2 words when counting)
     const uint32_t tid = threadIdx.x, t = blockIdx.x;
     const bool hist = A.dtp_part != nullptr;
     const uint32_t R2 = (A.n_rules + 1u) / 2u;
@@ -1525,20 +1527,31 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
     const uint64_t nq = (uint64_t)A.dtp_tiles * 256u;  // quads per chunk row
     for (uint32_t cw0 = 0; cw0 < A.dtp_nchunks; cw0 += MXP_DTP_WIN) {
         const uint32_t cwn = min(MXP_DTP_WIN, A.dtp_nchunks - cw0);
-        for (uint32_t i = tid; i < cwn * 256u; i += 256u) cnt[i] = 0u;
+        for (uint32_t i = tid; i < cwn * 128u; i += 256u) cnt[i] = 0u;
         if (tid == 0) ovn = 0u;
         __syncthreads();
         for (uint32_t w = 0; w < nw; w++) {
             const uint32_t n = min(uni(A.dtp_n[w0 + w]), A.dtp_cap);
             const uint32_t* E = A.dtp_ent + (uint64_t)(w0 + w) * A.dtp_cap;
-            for (uint32_t i = tid; i < n; i += 256u) {
-                const uint32_t e = E[i];
-                const uint32_t rule = e & 0x7FFFFFu, ch = A.dtp_chunk[rule >> 5];
+            // four entries per thread and step: their loads (entry, then its chunk) in flight
+            // together instead of one dependent pair of round trips per entry
+            for (uint32_t i0 = tid; i0 < n; i0 += 1024u) {
+            uint32_t ev[4], cv[4];
+#pragma unroll
+            for (uint32_t u = 0; u < 4u; u++) ev[u] = i0 + 256u * u < n ? E[i0 + 256u * u] : 0xFFFFFFFFu;
+#pragma unroll
+            for (uint32_t u = 0; u < 4u; u++) cv[u] = ev[u] != 0xFFFFFFFFu ? A.dtp_chunk[(ev[u] & 0x7FFFFFu) >> 5] : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < 4u; u++) {
+                const uint32_t e = ev[u];
+                if (e == 0xFFFFFFFFu) continue;
+                const uint32_t rule = e & 0x7FFFFFu, ch = cv[u];
                 // fused hit counters (first window pass): a true pair into the workgroup's histogram
                 if (hist && cw0 == 0 && !((e >> 23) & 1u)) atomicAdd(&hc[rule >> 1], 1u << ((rule & 1u) << 4));
                 const uint32_t c = (ch >> 8) - cw0, ql = w * 64u + (e >> 24);
                 if (c >= cwn) continue;
-                const uint32_t at = atomicAdd(&cnt[c * 256u + (ql >> 2)], 1u);
+                const uint32_t qi = c * 256u + (ql >> 2), sh = (qi & 1u) << 4;
+                const uint32_t at = (atomicAdd(&cnt[qi >> 1], 1u << sh) >> sh) & 0xFFFFu;
                 if (at < 8u) {
                     A.dtp_slots[((uint64_t)(cw0 + c) * nq + t * 256u + (ql >> 2)) * 8u + at] =
                         (uint16_t)(((ch & 0xFFu) << 8) | (((e >> 23) & 1u) << 7) | ((ql & 3u) << 5) | (e & 31u));
@@ -1559,12 +1572,13 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
                     }
                 }
             }
+            }
         }
         __syncthreads();
         if (hist && cw0 == 0)  // the tile's counts, summed over the tiles by mxp_dtp_hits_kernel
             for (uint32_t i = tid; i < R2; i += 256u) A.dtp_part[(uint64_t)t * R2 + i] = hc[i];
         for (uint32_t i = tid; i < cwn * 256u; i += 256u)
-            A.dtp_qn[(uint64_t)(cw0 + (i >> 8)) * nq + t * 256u + (i & 255u)] = (uint8_t)min(cnt[i], 8u);
+            A.dtp_qn[(uint64_t)(cw0 + (i >> 8)) * nq + t * 256u + (i & 255u)] = (uint8_t)min((cnt[i >> 1] >> ((i & 1u) << 4)) & 0xFFFFu, 8u);
         const uint32_t no = min(ovn, MXP_DTP_OVQ);
         if (tid == 0 && no) ovbase = atomicAdd(&A.dtp_ovf_n[0], no);
         __syncthreads();
@@ -2228,7 +2242,8 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
 }
 
 extern "C" hipError_t mxp_launch_dtp_sort(const mxp_kargs* args, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_dtp_sort_kernel, dim3(args->dtp_tiles), dim3(256), 0, s, *args);
+    const size_t lds = args->dtp_part ? (size_t)((args->n_rules + 1u) / 2u) * 4u : 0u;
+    hipLaunchKernelGGL(mxp_dtp_sort_kernel, dim3(args->dtp_tiles), dim3(256), lds, s, *args);
     return hipGetLastError();
 }
 
