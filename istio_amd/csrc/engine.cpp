@@ -1532,7 +1532,12 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     // (eval_device_hits; MXP_DEBUG_FLAGS 1048576 keeps the streaming counters)
     const bool dtp_count = dtp_on && A.hits && !(debug_flags & 1048576u) && A.n_rules <= kDtpHist;
     last_dtp_counted = dtp_count;
-    if (dtp_count) A.hits_gate = nullptr;
+    // (and the true-pair count that steers the fused / streamed choice is not kept: one atomic per
+    // index wave on one address congests its L2 channel -- C2 0.517 -> 0.409 ms same-box, profiles/r3_v6_ab_nostats_c2.log)
+    if (dtp_count) {
+        A.hits_gate = nullptr;
+        A.stats = nullptr;
+    }
     if (A.n_vt) {
         // value classes: classify every request of [lo, hi) per active column, then evaluate the
         // columns' rules once per class (class records -> errcount[2], the host expands them)
@@ -2107,7 +2112,9 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
                                  force)) != hipSuccess)
             return eng->hipfail(e, "launch hits");
     } else {
-        if ((e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), db->n, W, gate_next, force, s)) != hipSuccess)
+        // (a counted evaluation kept no true-pair count: the next one, if not counted, streams)
+        if ((e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), db->n, W, gate_next, counted ? 2u : force,
+                                      s)) != hipSuccess)
             return eng->hipfail(e, "hits gate");
         if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
     }

@@ -1642,6 +1642,9 @@ struct PairQueue {
     uint32_t n;        // pending entries (wave-uniform)
     uint32_t ntrue;    // true pairs this lane has set (kargs.stats)
     uint32_t base;     // first request of the wave's tile
+    // profiling instantiations only (kProf): time in run_pairs, its calls, VM passes, pairs
+    uint64_t p_vm;
+    uint32_t p_runs, p_passes, p_pairs;
 };
 
 // A true pair of an indexed rule: rules with many duplicates ("dense" canonical rules, kargs.dense_of)
@@ -1660,9 +1663,10 @@ __device__ __forceinline__ uint32_t pair_true(const mxp_kargs& A, PairQueue& Q, 
 }
 
 // run entries [off, off + cnt) of the queue, cnt <= 64
-template <bool kRefs, bool kNfa, bool kDtp>
+template <bool kRefs, bool kNfa, bool kDtp, bool kProf = false>
 __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32_t cnt, uint64_t (*regs)[256],
                           uint32_t tid) {
+    const uint64_t t0 = kProf ? (uint64_t)wall_clock64() : 0ull;
     const uint32_t lane = tid & 63u;
     wave_sync_lds();
     bool pending = lane < cnt;
@@ -1687,10 +1691,16 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
         const uint32_t code = run_rule<kRefs, kNfa>(A, P, len_t, pc0, mine, rule, req, regs, tid, true);
         if (mine) res = code;
         pending = pending && !mine;
+        if (kProf) Q.p_passes++;
     }
     // results out after the VM loop (its registers are dead here)
     if (res == PC_TRUE) Q.ntrue += pair_true<kDtp>(A, Q, rule, req);
     if (res >= PC_ERROR && res != MXP_VM_DONE) set_error<kDtp>(A, rule, req);
+    if (kProf) {
+        Q.p_vm += (uint64_t)wall_clock64() - t0;
+        Q.p_runs++;
+        Q.p_pairs += cnt;
+    }
 }
 
 // Appends every lane's postings [start, start + len) to the queue (direct postings are true pairs:
@@ -1699,7 +1709,7 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
 // never overflows, one lane's long list fills whole batches (C2: a request without a path takes its
 // service's ~39 equality postings in one round, not ten rounds of four), and the VM has one call
 // site (one inlined copy).
-template <bool kRefs, bool kNfa, bool kDtp>
+template <bool kRefs, bool kNfa, bool kDtp, bool kProf = false>
 __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, uint32_t tbl, uint32_t start,
                                              uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
                                              uint32_t tid) {
@@ -1748,7 +1758,7 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
         const bool more = __ballot(j0 < len) != 0;
         if (Q.n >= 64u || (Q.n > 0u && (final || more))) {
             const uint32_t k = min(Q.n, 64u);
-            run_pairs<kRefs, kNfa, kDtp>(A, Q, Q.n - k, k, regs, tid);
+            run_pairs<kRefs, kNfa, kDtp, kProf>(A, Q, Q.n - k, k, regs, tid);
             Q.n -= k;
             continue;
         }
@@ -1840,7 +1850,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
     const uint64_t N = A.n;
     const uint32_t tile = blockIdx.x * 4u + wave;  // 64 requests per wave
     const uint64_t t_start = kProf ? (uint64_t)wall_clock64() : 0ull;
-    PairQueue Q{wave, 0u, 0u, A.q0 + tile * 64u};
+    PairQueue Q{wave, 0u, 0u, A.q0 + tile * 64u, 0ull, 0u, 0u, 0u};
     const uint32_t req = Q.base + (tid & 63u);
     const bool valid = req < A.q1;
     if (A.dense_of) g_cm[wave][tid & 63u] = 0ull;
@@ -1945,7 +1955,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 continue;
             }
             if (final || __ballot(len != 0))
-                process_slot<kRefs, kNfa, kDtp>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
+                process_slot<kRefs, kNfa, kDtp, kProf>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
             if (kProf && (tid & 63u) == 0 && (final || nmark < 4u)) {  // profiling: phase marks
                 A.wave_t[8ull * tile + 3u + (final ? 4u : nmark)] = (uint64_t)wall_clock64();
                 nmark++;
@@ -1963,7 +1973,9 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
     if (kProf && (tid & 63u) == 0) {  // profiling: this tile's start / end (100 MHz clock), XCC
         A.wave_t[8ull * tile] = t_start;
         A.wave_t[8ull * tile + 1] = (uint64_t)wall_clock64();
-        A.wave_t[8ull * tile + 2] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // hwreg(XCC_ID, 0, 4)
+        A.wave_t[8ull * tile + 2] = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) |  // hwreg(XCC_ID, 0, 4)
+                                    ((uint64_t)Q.p_passes << 8) | ((uint64_t)Q.p_runs << 24) | ((uint64_t)Q.p_pairs << 40);
+        A.wave_t[8ull * tile + 6] = Q.p_vm;  // (mark 3 of 0..3 is unused by these workloads: time in run_pairs)
     }
     if (A.stats) {
         uint32_t t = Q.ntrue;

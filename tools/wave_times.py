@@ -27,17 +27,34 @@ db = eng.upload(batch)
 Wd = (len(rules) + 31) // 32
 dm = torch.empty((Wd, batch.n), dtype=torch.int32, device="cuda:0")
 de = torch.empty_like(dm)
+compact = bool(os.environ.get("WT_COMPACT"))  # the bench's evaluation: compact errors, hit counters
+hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
+flags = torch.zeros(batch.n, dtype=torch.uint8, device="cuda:0")
+
+
+def one():
+    if compact:
+        db.eval_compact(dm.data_ptr(), flags.data_ptr(), hits.data_ptr(), 0)
+    else:
+        db.eval(dm.data_ptr(), de.data_ptr(), 0)
+
+
+eng.set_timing(True)
 for _ in range(3):
-    db.eval(dm.data_ptr(), de.data_ptr(), 0)
+    one()
 torch.cuda.synchronize()
 if os.environ.get("WT_IDLE"):  # the last evaluation after an idle GPU (no fill write-back draining)
     import time
     time.sleep(0.05)
-    db.eval(dm.data_ptr(), de.data_ptr(), 0)
+    one()
     torch.cuda.synchronize()
+print("mxp_kernel_times of the last evaluation (ms):", eng.kernel_times(3))
 t = eng.wave_times((n + 63) // 64).astype(np.int64)
-start, end, xcc = t[:, 0], t[:, 1], t[:, 2]
-marks = t[:, 3:8]
+start, end, xcc = t[:, 0], t[:, 1], t[:, 2] & 255
+passes, runs, pairs = (t[:, 2] >> 8) & 0xFFFF, (t[:, 2] >> 24) & 0xFFFF, t[:, 2] >> 40
+vm_us = t[:, 6] / 100.0
+marks = t[:, 3:8].copy()
+marks[:, 3] = 0  # (word 6 holds the run_pairs time)
 dur = (end - start) / 100.0  # us
 t0 = start.min()
 print("%s: %d waves, kernel span %.1f us (first start -> last end)" % (kind, len(t), (end.max() - t0) / 100.0))
@@ -68,3 +85,5 @@ for k in range(5):
         "drain" if k == 4 else "slot %d" % k, have.sum(), np.percentile(d, 50), d.mean(),
         np.percentile(d[f], 50) if f.any() else 0.0, np.percentile(d[~f], 50) if (~f).any() else 0.0))
     prev = np.where(have, m, prev)
+print("per wave: run_pairs time p50 %.1f mean %.1f us (%.0f%% of the wave); run_pairs calls %.1f, VM passes %.1f, pairs %.1f" % (
+    np.percentile(vm_us, 50), vm_us.mean(), 100.0 * vm_us.sum() / max(dur.sum(), 1e-9), runs.mean(), passes.mean(), pairs.mean()))
