@@ -1499,13 +1499,16 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
     // chunks start at multiples of 1024 requests (the fill kernel's 16-byte rows)
     const uint32_t step = nchunk > 1 ? (span / nchunk + 1023u) / 1024u * 1024u : span;
     nchunk = (span + step - 1) / step;
-    if (nchunk > 1 && !side) {
-        if ((e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking)) != hipSuccess) {
+    if (nchunk > 1) {
+        if (!side && (e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking)) != hipSuccess) {
             side = nullptr;
             return hipfail(e, "side stream");
         }
         for (auto& x : chunk_ev)
-            if ((e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) return hipfail(e, "chunk event");
+            if (!x && (e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) {
+                x = nullptr;
+                return hipfail(e, "chunk event");
+            }
     }
     if (guards_on && P->n_fills) A.fills = P->d_fills.as<mxp_fill>();
     if (!use_index) A.dense_of = nullptr;
@@ -1558,6 +1561,8 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         if ((e = mxp_launch_vt_eval(&AV, tiles, (P->vt_max_nw + 3) / 4, s)) != hipSuccess)
             return hipfail(e, "launch vt eval");
     }
+    if (A.req_err && !dtp_on && (e = hipMemsetAsync(A.req_err, 0, A.n, s)) != hipSuccess)
+        return hipfail(e, "request error flags reset");
     if (dtp_on) {
         A.q0 = lo;
         A.q1 = hi;
@@ -1593,6 +1598,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         uint32_t* const ovf_next = d_dtp_ovf_n.as<uint32_t>() + 4u * (dtp_par ^ 1u);
         dtp_par ^= 1u;
         mxp_kargs AI = A;  // the index kernel records
+        AI.req_err_init = A.req_err ? 1u : 0u;
         AI.dtp_ent = d_dtp_ent.as<uint32_t>();
         AI.dtp_n = d_dtp_n.as<uint32_t>();
         AI.dtp_ovf_n = ovf_n;
@@ -1610,19 +1616,58 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
                 return hipfail(e, "deferred-pair histograms");
             AI.dtp_part = d_dtp_part.as<uint32_t>();
         }
-        if ((e = mxp_launch_index(&AI, grid, s)) != hipSuccess) return hipfail(e, "launch index");
-        if ((e = mxp_launch_dtp_sort(&AI, s)) != hipSuccess) return hipfail(e, "launch dtp sort");
-        if (dtp_count && (e = mxp_launch_dtp_hits(AI.dtp_part, tiles, A.n_rules, A.hits, s)) != hipSuccess)
-            return hipfail(e, "launch dtp hits");
-        if (timing && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
+        // Request chunks (dtp_chunks > 1, tiles of 1024 requests): chunk c's index and sort kernels
+        // run on the side stream while the evaluation stream fills chunk c - 1 -- the latency-bound
+        // index waves beside the store-bound fill -- and each fill waits for its chunk's sort only.
+        // Chunks own disjoint tiles of every scratch array (wave lists, slots, counts, histograms).
+        const uint32_t K = std::max(1u, std::min(dtp_chunks, tiles));
+        hipStream_t xs = s;
+        if (K > 1) {
+            if (!side && (e = hipStreamCreateWithFlags(&side, hipStreamNonBlocking)) != hipSuccess) {
+                side = nullptr;
+                return hipfail(e, "side stream");
+            }
+            for (auto& x : dtp_cev)
+                if (!x && (e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) {
+                    x = nullptr;
+                    return hipfail(e, "chunk event");
+                }
+            // the side stream starts after everything before this evaluation on s (the previous
+            // evaluation's fills read the slots the sorts rewrite; the value classes)
+            if ((e = hipEventRecord(dtp_cev[kDtpChunksMax], s)) != hipSuccess ||
+                (e = hipStreamWaitEvent(side, dtp_cev[kDtpChunksMax], 0)) != hipSuccess)
+                return hipfail(e, "side stream wait");
+            xs = side;
+        }
         mxp_kargs AF = A;  // the fills merge
         AF.dtp_slots = AI.dtp_slots;
         AF.dtp_qn = AI.dtp_qn;
         AF.dtp_tiles = tiles;
-        if (P->n_fills && (e = mxp_launch_fill(&AF, P->n_fills, s)) != hipSuccess) return hipfail(e, "launch fill");
-        AF.fills = P->d_vtfills.as<mxp_fill>();
-        AF.dtp_cbase = P->n_fills;
-        if (P->n_vtfills && (e = mxp_launch_vtfill(&AF, P->n_vtfills, s)) != hipSuccess) return hipfail(e, "launch vtfill");
+        for (uint32_t c = 0; c < K; c++) {
+            const uint32_t t0 = (uint32_t)((uint64_t)tiles * c / K), t1 = (uint32_t)((uint64_t)tiles * (c + 1) / K);
+            AI.q0 = t0 * 1024u;
+            AI.q1 = std::min(t1 * 1024u, hi);
+            AI.dtp_t0 = t0;
+            AI.dtp_tn = t1 - t0;
+            const uint32_t gc = ((AI.q1 - AI.q0 + 63) / 64 + 3) / 4;
+            if ((e = mxp_launch_index(&AI, gc, xs)) != hipSuccess) return hipfail(e, "launch index");
+            if ((e = mxp_launch_dtp_sort(&AI, xs)) != hipSuccess) return hipfail(e, "launch dtp sort");
+            if (K > 1 && ((e = hipEventRecord(dtp_cev[c], xs)) != hipSuccess || (e = hipStreamWaitEvent(s, dtp_cev[c], 0)) != hipSuccess))
+                return hipfail(e, "chunk event");
+            if (timing && c == 0 && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hipfail(e, "event");
+            AF.q0 = AI.q0;
+            AF.q1 = AI.q1;
+            AF.fills = A.fills;
+            AF.dtp_cbase = 0;
+            if (P->n_fills && (e = mxp_launch_fill(&AF, P->n_fills, s)) != hipSuccess) return hipfail(e, "launch fill");
+            AF.fills = P->d_vtfills.as<mxp_fill>();
+            AF.dtp_cbase = P->n_fills;
+            if (P->n_vtfills && (e = mxp_launch_vtfill(&AF, P->n_vtfills, s)) != hipSuccess) return hipfail(e, "launch vtfill");
+        }
+        AI.q0 = lo;
+        AI.q1 = hi;
+        if (dtp_count && (e = mxp_launch_dtp_hits(AI.dtp_part, tiles, A.n_rules, A.hits, s)) != hipSuccess)
+            return hipfail(e, "launch dtp hits");
         for (const Part& Pt : parts) {
             if (!Pt.n) continue;
             A.glist = Pt.list->as<uint32_t>();
@@ -1641,6 +1686,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         AR.errlog = nullptr;
         AR.errcount = nullptr;
         AR.wave_t = nullptr;
+        AR.gate_out = dtp_count ? gate_next_out : nullptr;
         if ((e = mxp_launch_index(&AR, grid, s)) != hipSuccess) return hipfail(e, "launch index re-run");
         if ((e = hipEventRecord(dtp_ev, s)) != hipSuccess) return hipfail(e, "deferred-pair event");
         dtp_pending = true;
@@ -1837,6 +1883,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_ERRCAP")) e->errcap = (uint32_t)std::max(1, atoi(f));
     if (getenv("MXP_WAVE_TIMES")) e->wave_times = true;
     if (const char* h = getenv("MXP_HEADS")) e->heads_on = atoi(h) != 0;
+    if (const char* h = getenv("MXP_DTP_CHUNKS")) e->dtp_chunks = std::max(1, std::min(atoi(h), (int)mxp_engine::kDtpChunksMax));
     if (const char* f = getenv("MXP_HOST_PACK")) e->host_pack = atoi(f) != 0;  // A/B: the host packer
     if (device < 0) {  // host-only engine (compiler / lowering inspection without a GPU)
         e->reset_tables();
@@ -1867,6 +1914,8 @@ void mxp_engine_destroy(mxp_engine* eng) {
         if (x) (void)hipEventDestroy(x);
     if (eng->side) (void)hipStreamSynchronize(eng->side);
     for (auto& x : eng->chunk_ev)
+        if (x) (void)hipEventDestroy(x);
+    for (auto& x : eng->dtp_cev)
         if (x) (void)hipEventDestroy(x);
     if (eng->side) (void)hipStreamDestroy(eng->side);
     if (eng->dtp_ev) (void)hipEventSynchronize(eng->dtp_ev);
@@ -2065,8 +2114,7 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
                             uint8_t* d_req_err, unsigned long long* d_hits) {
     hipStream_t s = stream ? (hipStream_t)stream : eng->stream;
     hipError_t e;
-    if (d_req_err && db->n && (e = hipMemsetAsync(d_req_err, 0, db->n, s)) != hipSuccess)
-        return eng->hipfail(e, "request error flags reset");
+    // (the request error flags are reset in launch: by a memset, or by the deferred-pair index kernel)
     if (!d_hits) {
         eng->req_err_out = d_req_err;
         const int rc = eng->launch(db, s, d_match, d_err, nullptr, false);
@@ -2099,9 +2147,11 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
         return eng->hipfail(e, "hits gate");
     eng->req_err_out = d_req_err;
     eng->hits_gate_out = gate;
+    eng->gate_next_out = gate_next;
     int rc = eng->launch(db, s, d_match, d_err, nullptr, false, d_hits, eng->d_stats.as<uint64_t>());
     eng->req_err_out = nullptr;
     eng->hits_gate_out = nullptr;
+    eng->gate_next_out = nullptr;
     if (rc) return rc;
     // the streaming counters (returning at once when the kernels counted); their block (0, 0) also
     // sets the next evaluation's gate from this one's true pairs and resets the pair count.  A
@@ -2111,13 +2161,13 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
         if ((e = mxp_launch_hits(d_match, db->n, R, W, d_hits, s, gate, eng->d_stats.as<unsigned long long>(), gate_next,
                                  force)) != hipSuccess)
             return eng->hipfail(e, "launch hits");
-    } else {
-        // (a counted evaluation kept no true-pair count: the next one, if not counted, streams)
-        if ((e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), db->n, W, gate_next, counted ? 2u : force,
-                                      s)) != hipSuccess)
+    } else if (!counted) {
+        if ((e = mxp_launch_hits_gate(eng->d_stats.as<unsigned long long>(), db->n, W, gate_next, force, s)) != hipSuccess)
             return eng->hipfail(e, "hits gate");
         if ((e = hipMemsetAsync(eng->d_stats.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "stats reset");
     }
+    // (a counted evaluation kept no true-pair count: its post-fill index launch set the next gate to
+    // 0 -- stream, should the next evaluation not be counted -- and the count was not touched)
     eng->gate_par ^= 1u;
     // mxp_kernel_times: the evaluation's span ends after the counters too (streamed or gate only)
     if (eng->timing && (e = hipEventRecord(eng->ev[2], s)) != hipSuccess) return eng->hipfail(e, "event");

@@ -315,6 +315,11 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t chunk_min = 1u << 17, chunks_max = 1;  // off by default: measured slower
     hipStream_t side = nullptr;
     hipEvent_t chunk_ev[kChunksMax + 1] = {};
+    // deferred-pair request chunks (launch: index + sort of chunk c on the side stream beside the
+    // fill of chunk c - 1; MXP_DTP_CHUNKS)
+    static constexpr uint32_t kDtpChunksMax = 16;
+    uint32_t dtp_chunks = 1;
+    hipEvent_t dtp_cev[kDtpChunksMax + 1] = {};
     // MXP_DEBUG_FLAGS, ablation only: 1 no in-wave VM, 2 no guards (results invalid), 8 no guard index,
     // 16 no composite index, 64 no duplicate folding, 128 plain fill stores, 256 no dense injection,
     // 512 index equality-only guards too, 524288 / 1048576 fused / streaming hit counters forced,
@@ -566,6 +571,7 @@ struct mxp_engine : public mxp::LowerTables {
     int pack_dict(mxp_dbatch* db);   // the value-class dictionary of the batch (mxp_vt_classify_kernel)
     int pack_heads(mxp_dbatch* db);  // kargs.heads of every column (MXP_HEADS=0: none)
     bool heads_on = true;
+    uint32_t* gate_next_out = nullptr;  // eval_device_hits -> launch: the next evaluation's gate word
     int pack_on_host(const mxp_bag_batch* b, mxp_dbatch* db);
     int pack_device(const mxp_bag_batch* b, mxp_dbatch* db);
     int pack_vt_tables(mxp_dbatch* db);  // the value-class tables of the active slots

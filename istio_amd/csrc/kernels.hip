@@ -167,9 +167,13 @@ __device__ __forceinline__ uint32_t set_true(const mxp_kargs& A, uint32_t rule, 
 }
 
 // an error pair found by the guard-index kernel, with its aliases
+__shared__ uint8_t g_rerr[4][64];  // deferred-pair index kernel: its tile's request error flags (kargs.req_err_init)
 template <bool kDtp = false>
 __device__ __forceinline__ void set_error(const mxp_kargs& A, uint32_t rule, uint32_t req) {
-    if (A.req_err) A.req_err[req] = 1;
+    if (A.req_err) {
+        if (kDtp && A.req_err_init) g_rerr[threadIdx.x >> 6][req & 63u] = 1;  // (the wave's own tile)
+        else A.req_err[req] = 1;
+    }
     if (!A.out_err) return;
     if (kDtp) {
         dtp_push(A, rule, req, 1u);
@@ -1517,7 +1521,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
     // fused hit counters (kargs.dtp_part): per rule the tile's true pairs, two u16 per word (a rule
     // has at most 1024 pairs in a tile of 1024 requests)
     extern __shared__ uint32_t hc[];  // (dynamic: (n_rules + 1) / 2 words when counting)
-    const uint32_t tid = threadIdx.x, t = blockIdx.x;
+    const uint32_t tid = threadIdx.x, t = A.dtp_t0 + blockIdx.x;
     const bool hist = A.dtp_part != nullptr;
     const uint32_t R2 = (A.n_rules + 1u) / 2u;
     if (hist)
@@ -1843,6 +1847,8 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
             const uint32_t rule = e & 0x7FFFFFFFu;
             atomicOr(((e >> 31) ? A.out_err : A.out_match) + (uint64_t)(rule >> 5) * A.n + q, 1u << (rule & 31u));
         }
+        // a counted evaluation's gate for the next one: stream (no true-pair count was kept)
+        if (A.gate_out && blockIdx.x == 0 && threadIdx.x == 0) *A.gate_out = 0u;
         if (uni(*A.dtp_gate) == 0u) return;
     }
     const uint32_t tid = threadIdx.x;
@@ -1855,6 +1861,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
     const bool valid = req < A.q1;
     if (A.dense_of) g_cm[wave][tid & 63u] = 0ull;
     if (kDtp && (tid & 63u) == 0) g_dtpn[wave] = 0u;
+    if (kDtp && A.req_err_init) g_rerr[wave][tid & 63u] = 0;
     if (A.dense_of || kDtp) wave_sync_lds();
     uint32_t nmark = 0;  // profiling (kargs.wave_t): slots done
     if (kProf && (tid & 63u) == 0)
@@ -1969,6 +1976,9 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
     if (kDtp) {  // the tile's deferred-pair count for mxp_dtp_sort_kernel
         wave_sync_lds();
         if ((tid & 63u) == 0) A.dtp_n[Q.base >> 6] = min(g_dtpn[wave], A.dtp_cap);
+        // the evaluation's first writer of the request error flags: all of the tile's, one
+        // coalesced store (the later kernels only set flags; no memset)
+        if (A.req_err && A.req_err_init && valid) A.req_err[req] = g_rerr[wave][tid & 63u];
     }
     if (kProf && (tid & 63u) == 0) {  // profiling: this tile's start / end (100 MHz clock), XCC
         A.wave_t[8ull * tile] = t_start;
@@ -2255,7 +2265,7 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
 
 extern "C" hipError_t mxp_launch_dtp_sort(const mxp_kargs* args, hipStream_t s) {
     const size_t lds = args->dtp_part ? (size_t)((args->n_rules + 1u) / 2u) * 4u : 0u;
-    hipLaunchKernelGGL(mxp_dtp_sort_kernel, dim3(args->dtp_tiles), dim3(256), lds, s, *args);
+    hipLaunchKernelGGL(mxp_dtp_sort_kernel, dim3(args->dtp_tn ? args->dtp_tn : args->dtp_tiles), dim3(256), lds, s, *args);
     return hipGetLastError();
 }
 
