@@ -152,6 +152,9 @@ def lds_conflicts(workload):
                 "rate": v.get("bank_conflict_rate")} for k, v in d.get("kernels", {}).items()}
 
 
+LAST_ENQUEUE_MS = None
+
+
 def timed_loop(step, steps, warmup, world, stream):
     """W untimed warmup steps, then exactly K steps bracketed by barrier + synchronize; returns the
     slowest rank's seconds and the per-step HIP-event durations (ms) recorded on `stream`.  (Without
@@ -172,6 +175,8 @@ def timed_loop(step, steps, warmup, world, stream):
     t0 = time.perf_counter()
     for k in range(steps):
         step(*evs[k])
+    global LAST_ENQUEUE_MS  # host time to enqueue one step (the GPU idles between steps if >= its time)
+    LAST_ENQUEUE_MS = (time.perf_counter() - t0) / max(steps, 1) * 1e3
     sync()
     if world > 1:
         dist.barrier()
@@ -488,8 +493,8 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     # value-class and index kernels and the pair sort, [1] the fills and the rest
     deferred = bool(per and len(per[0]) > 2 and per[0][2] == 1.0)
     if deferred:
-        labels = ("mxp_vt_classify/vt_eval + mxp_index_kernel + mxp_dtp_sort_kernel (deferred pairs, hit counters)",
-                  "mxp_fill/vtfill/guard2/eval kernels + the gated index launch (overflow list) + hit-counter gate")
+        labels = ("mxp_vt_lookup/vt_eval + mxp_index_dtp_kernel + mxp_dtp_sort_kernel (deferred pairs, hit counters)",
+                  "mxp_fill/vtfill/guard2/eval kernels + mxp_dtp_hits_kernel + the post-fill index launch (overflow list, next gate)")
     else:
         labels = ("phase1 (mxp_vt_classify/vt_eval/fill/vtfill/guard2/eval kernels)",
                   "mxp_index_kernel+mxp_inject_kernel + mxp_hits_kernel (streams the bitmap unless the kernels counted)")
@@ -520,6 +525,7 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
         "config": {"workload": workload % (R, N),
                    "rules": R, "requests_per_gpu": N, "parallelism": "request-sharded dp%d" % world},
         "eval_ms": step_kernel_ms,
+        "host_enqueue_ms_per_step": LAST_ENQUEUE_MS,
         "kernels_ms": {labels[0]: k_eval, labels[1]: k_index},
         "deferred_pairs": deferred,
         "pack_upload_s": t_pack,
@@ -527,7 +533,7 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
         "lds_bank_conflicts": lds_conflicts(kind),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "one evaluation: value classes (mxp_vt_classify/vt_eval), mxp_fill / vtfill / guard2 "
+                     "kernel": "one evaluation: value classes (mxp_vt_lookup/vt_eval), mxp_fill / vtfill / guard2 "
                                "/ eval kernels (the groups each serves) + mxp_index_kernel (+ mxp_inject_kernel with "
                                "dense rules); traffic also counts mxp_hits_kernel when the hit counters are not fused",
                      "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pair": alg_bytes / (N * R)},

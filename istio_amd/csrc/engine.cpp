@@ -415,6 +415,14 @@ int mxp_engine::build_plan(Plan& P) {
         index_of[{gd.col, prefix}][k1].push_back(i);
     }
     P.n_tmpls = (uint32_t)tmpls.size();
+    // lite index kernel: no template (code from its start to its end) holds a heavy opcode
+    P.tmpl_lite = !(debug_flags & 8388608u);
+    for (const mxp_tmpl& t : tmpls)
+        for (uint32_t pc = t.pc0; pc < t.len && P.tmpl_lite; pc++) {
+            const uint32_t op = prog_h[t.off - t.pc0 + pc].op & 0x7Fu;
+            if (op == VM_VCOL || op == VM_LOOKUP || op == VM_LOOKUPK || op == VM_REGEX || op == VM_REGEXR || op == VM_REGEXD)
+                P.tmpl_lite = false;
+        }
     std::vector<mxp_index> idx;
     std::vector<mxp_hent> hents;
     std::vector<uint32_t> postings, plens;
@@ -1293,6 +1301,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
     A->hents = P.d_hents.as<mxp_hent>();
     A->postings = P.d_postings.as<uint32_t>();
     A->post_tmpl = P.post_tmpl ? 1u : 0u;
+    A->tmpl_lite = P.tmpl_lite ? 1u : 0u;
     A->plens = P.d_plens.as<uint32_t>();
     A->n_idx = P.n_idx;
     A->tmpls = P.d_tmpls.as<mxp_tmpl>();
@@ -2139,7 +2148,7 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
     const uint32_t R = (uint32_t)eng->rules.size(), W = (R + 31) / 32;
     const uint32_t force = (eng->debug_flags & 524288u) ? 1u : (eng->debug_flags & 1048576u) ? 2u : 0u;
     // (ordered after the previous evaluation's gate update even when the caller switched streams)
-    if (eng->stats_pending && (e = hipStreamWaitEvent(s, eng->stats_ev, 0)) != hipSuccess)
+    if (eng->stats_pending && eng->stats_stream != s && (e = hipStreamWaitEvent(s, eng->stats_ev, 0)) != hipSuccess)
         return eng->hipfail(e, "stats wait");
     uint32_t* const gate = eng->d_gate.as<uint32_t>() + eng->gate_par;
     uint32_t* const gate_next = eng->d_gate.as<uint32_t>() + (eng->gate_par ^ 1u);
@@ -2173,6 +2182,7 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
     if (eng->timing && (e = hipEventRecord(eng->ev[2], s)) != hipSuccess) return eng->hipfail(e, "event");
     if ((e = hipEventRecord(eng->stats_ev, s)) != hipSuccess) return eng->hipfail(e, "stats event");
     eng->stats_pending = true;
+    eng->stats_stream = s;
     return MXP_OK;
 }
 

@@ -252,6 +252,7 @@ struct mxp_engine : public mxp::LowerTables {
         uint32_t n_idx = 0, n_indexed = 0, n_composite = 0, n_alias = 0, n_tmpls = 0, n_segs = 0;
         uint32_t n_dense = 0, n_inj = 0;
         bool post_tmpl = false;  // postings carry template codes (kargs.post_tmpl)
+        bool tmpl_lite = false;  // no template holds a lookup, virtual column or regexp (kargs.tmpl_lite)
         DevBuf d_guards, d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_alias_off, d_aliases;
         DevBuf d_idx, d_hents, d_postings, d_plens;
         DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all but deep
@@ -572,6 +573,7 @@ struct mxp_engine : public mxp::LowerTables {
     int pack_heads(mxp_dbatch* db);  // kargs.heads of every column (MXP_HEADS=0: none)
     bool heads_on = true;
     uint32_t* gate_next_out = nullptr;  // eval_device_hits -> launch: the next evaluation's gate word
+    hipStream_t stats_stream = nullptr;  // stream of the last stats_ev record (a wait only across streams)
     int pack_on_host(const mxp_bag_batch* b, mxp_dbatch* db);
     int pack_device(const mxp_bag_batch* b, mxp_dbatch* db);
     int pack_vt_tables(mxp_dbatch* db);  // the value-class tables of the active slots

@@ -119,7 +119,7 @@ typedef struct mxp_kargs {
                                  // summed into kargs.hits by mxp_dtp_hits_kernel (null: counted per pair)
     uint32_t dtp_cap, dtp_ovf_cap, dtp_tiles, dtp_nchunks;
     uint32_t req_err_init;       // the deferred-pair index kernel writes every request's req_err flag
-    uint32_t pad9;
+    uint32_t tmpl_lite;          // index templates hold no lookups / virtual columns / regexps (lite kernel)
     uint32_t* gate_out;          // the gated index launch after a counted evaluation: next gate = 0
     uint32_t dtp_t0, dtp_tn;     // mxp_dtp_sort_kernel: tiles [dtp_t0, dtp_t0 + dtp_tn) (request chunks; tn 0: all)
     uint32_t dtp_cbase;          // fill launches: chunk id of blockIdx.y 0 (plain fill chunks first, then

@@ -171,8 +171,12 @@ __shared__ uint8_t g_rerr[4][64];  // deferred-pair index kernel: its tile's req
 template <bool kDtp = false>
 __device__ __forceinline__ void set_error(const mxp_kargs& A, uint32_t rule, uint32_t req) {
     if (A.req_err) {
-        if (kDtp && A.req_err_init) g_rerr[threadIdx.x >> 6][req & 63u] = 1;  // (the wave's own tile)
-        else A.req_err[req] = 1;
+        if constexpr (kDtp) {
+            if (A.req_err_init) g_rerr[threadIdx.x >> 6][req & 63u] = 1;  // (the wave's own tile)
+            else A.req_err[req] = 1;
+        } else {
+            A.req_err[req] = 1;
+        }
     }
     if (!A.out_err) return;
     if (kDtp) {
@@ -215,7 +219,10 @@ __device__ __forceinline__ void ref_rec(const mxp_kargs& A, bool on, uint32_t re
 // P[pc] (pc in [pc0, len)), fetched with one scalar s_load_dwordx4 per step.  `rule` may differ
 // per lane (template batches of the guard-index kernel); it only names the pair in error records and
 // Eval results.  The register file is regs[reg][thread] in LDS.
-template <bool kRefs, bool kNfa = kRefs>
+// kLite: the continuation-template instantiation for rule sets whose index templates hold no map
+// lookups, virtual columns or regexps (Plan::tmpl_lite) -- without those cases the index kernel
+// needs far fewer registers
+template <bool kRefs, bool kNfa = kRefs, bool kLite = false>
 __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint32_t pc0, bool live, uint32_t rule,
                              uint32_t req, uint64_t (*regs)[256], uint32_t tid, bool fan = false) {
 #define REG(i) regs[i][tid]
@@ -290,6 +297,7 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
             break;
         }
         case VM_VCOL: {
+            if constexpr (kLite) break;
             if constexpr (kRefs) ref_rec(A, live, req, rule, x, MXP_VM_DONE);
             if (live) {
                 const uint64_t at = (uint64_t)x * N + req;
@@ -356,6 +364,7 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
             break;
         case VM_LOOKUP:
         case VM_LOOKUPK: {
+            if constexpr (kLite) break;
             bool rec = false;
             uint32_t rslot = 0, rkey = 0;
             if (live) {
@@ -444,6 +453,7 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
         case VM_REGEX:
         case VM_REGEXR:
         case VM_REGEXD:
+            if (kLite) break;
             if (live) {
                 // one stepping loop for the three forms (a single inlined copy of the DFA walk)
                 // the set is chosen by value (a pointer into the by-value kernarg block would spill
@@ -1633,6 +1643,9 @@ namespace {
 // dense wavefronts however sparse the hits are per request.  Entry: rule | table << 31 (table 1:
 // kargs.rule_tmpl2, the composite resume point), request.
 #define MXP_IXQ 256u
+#ifndef MXP_LITE_WAVES
+#define MXP_LITE_WAVES 6
+#endif
 __shared__ uint32_t g_ixq[4][MXP_IXQ][2];  // per wave of the index kernel's workgroup
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1667,7 +1680,7 @@ __device__ __forceinline__ uint32_t pair_true(const mxp_kargs& A, PairQueue& Q, 
 }
 
 // run entries [off, off + cnt) of the queue, cnt <= 64
-template <bool kRefs, bool kNfa, bool kDtp, bool kProf = false>
+template <bool kRefs, bool kNfa, bool kDtp, bool kProf = false, bool kLite = false>
 __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32_t cnt, uint64_t (*regs)[256],
                           uint32_t tid) {
     const uint64_t t0 = kProf ? (uint64_t)wall_clock64() : 0ull;
@@ -1692,7 +1705,7 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
         if (mine)
             for (uint32_t c = 0; c < nconst; c++) regs[creg0 + c][tid] = A.rconst[(uint64_t)rule * MXP_VM_MAXREG + c];
         cuint32* P = ((cuint32*)A.prog) + ((uint64_t)toff - pc0) * 4u;
-        const uint32_t code = run_rule<kRefs, kNfa>(A, P, len_t, pc0, mine, rule, req, regs, tid, true);
+        const uint32_t code = run_rule<kRefs, kNfa, kLite>(A, P, len_t, pc0, mine, rule, req, regs, tid, true);
         if (mine) res = code;
         pending = pending && !mine;
         if (kProf) Q.p_passes++;
@@ -1713,7 +1726,7 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
 // never overflows, one lane's long list fills whole batches (C2: a request without a path takes its
 // service's ~39 equality postings in one round, not ten rounds of four), and the VM has one call
 // site (one inlined copy).
-template <bool kRefs, bool kNfa, bool kDtp, bool kProf = false>
+template <bool kRefs, bool kNfa, bool kDtp, bool kProf = false, bool kLite = false>
 __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, uint32_t tbl, uint32_t start,
                                              uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
                                              uint32_t tid) {
@@ -1762,7 +1775,7 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
         const bool more = __ballot(j0 < len) != 0;
         if (Q.n >= 64u || (Q.n > 0u && (final || more))) {
             const uint32_t k = min(Q.n, 64u);
-            run_pairs<kRefs, kNfa, kDtp, kProf>(A, Q, Q.n - k, k, regs, tid);
+            run_pairs<kRefs, kNfa, kDtp, kProf, kLite>(A, Q, Q.n - k, k, regs, tid);
             Q.n -= k;
             continue;
         }
@@ -1836,7 +1849,7 @@ namespace {
 
 // kProf: the profiling instantiations (kargs.wave_t, MXP_WAVE_TIMES) -- the hot kernels carry no
 // timing code
-template <bool kRefs, bool kNfa = kRefs, bool kDtp = false, bool kProf = false>
+template <bool kRefs, bool kNfa = kRefs, bool kDtp = false, bool kProf = false, bool kLite = false>
 __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
     // after the fill (kargs.dtp_gate): the deferred pairs' overflow list OR-ed in, then -- only when
     // that list filled -- every pair again
@@ -1861,7 +1874,8 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
     const bool valid = req < A.q1;
     if (A.dense_of) g_cm[wave][tid & 63u] = 0ull;
     if (kDtp && (tid & 63u) == 0) g_dtpn[wave] = 0u;
-    if (kDtp && A.req_err_init) g_rerr[wave][tid & 63u] = 0;
+    if constexpr (kDtp)
+        if (A.req_err_init) g_rerr[wave][tid & 63u] = 0;
     if (A.dense_of || kDtp) wave_sync_lds();
     uint32_t nmark = 0;  // profiling (kargs.wave_t): slots done
     if (kProf && (tid & 63u) == 0)
@@ -1962,7 +1976,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 continue;
             }
             if (final || __ballot(len != 0))
-                process_slot<kRefs, kNfa, kDtp, kProf>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
+                process_slot<kRefs, kNfa, kDtp, kProf, kLite>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
             if (kProf && (tid & 63u) == 0 && (final || nmark < 4u)) {  // profiling: phase marks
                 A.wave_t[8ull * tile + 3u + (final ? 4u : nmark)] = (uint64_t)wall_clock64();
                 nmark++;
@@ -2011,6 +2025,11 @@ extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void mxp_index_dtp_kernel(mxp_kargs A) {
     __shared__ uint64_t regs[MXP_VM_MAXREG][256];
     index_body<false, false, true>(A, regs);
+}
+// ... for lite continuation templates (kargs.tmpl_lite: no lookups, virtual columns or regexps)
+extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MXP_LITE_WAVES))) void mxp_index_dtp_lite_kernel(mxp_kargs A) {
+    __shared__ uint64_t regs[MXP_VM_MAXREG][256];
+    index_body<false, false, true, false, true>(A, regs);
 }
 // profiling (MXP_WAVE_TIMES): the two hot instantiations with wave start / end / phase marks
 extern "C" __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void mxp_index_prof_kernel(mxp_kargs A) {
@@ -2301,6 +2320,8 @@ extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hip
         hipLaunchKernelGGL(mxp_index_nfa_kernel, dim3(grid), dim3(256), 0, s, *args);
     else if (args->dtp_ent && args->wave_t)
         hipLaunchKernelGGL(mxp_index_dtp_prof_kernel, dim3(grid), dim3(256), 0, s, *args);
+    else if (args->dtp_ent && args->tmpl_lite)
+        hipLaunchKernelGGL(mxp_index_dtp_lite_kernel, dim3(grid), dim3(256), 0, s, *args);
     else if (args->dtp_ent)
         hipLaunchKernelGGL(mxp_index_dtp_kernel, dim3(grid), dim3(256), 0, s, *args);
     else if (args->wave_t)
