@@ -128,3 +128,39 @@ class Dedup:
         r = fn()
         self.seen[dedup_id] = r
         return r
+
+
+class CMemquota:
+    """The C restatement (memquota_oracle.c, liboracle.so): the same semantics for keys 0 .. K-1
+    (limits: arrays of max_amount and valid_duration_ns), a batch at a time, keys handled in
+    parallel on `threads` host threads.  The bench's CPU baseline; checked against Memquota."""
+
+    def __init__(self, max_amount, valid_ns):
+        import ctypes
+        import numpy as np
+        import oracle
+        self._L = oracle.lib()
+        mx = np.ascontiguousarray(max_amount, dtype=np.int64)
+        vd = np.ascontiguousarray(valid_ns, dtype=np.int64)
+        self.n_keys = len(mx)
+        self._h = self._L.mq_create(len(mx), mx.ctypes.data, vd.ctypes.data)
+        if not self._h:
+            raise MemoryError("mq_create")
+        self._ct = ctypes
+
+    def handle_batch(self, keys, amounts, best_effort, now_ns, threads=1):
+        import numpy as np
+        k = np.ascontiguousarray(keys, dtype=np.int32)
+        a = np.ascontiguousarray(amounts, dtype=np.int64)
+        b = np.ascontiguousarray(best_effort, dtype=np.uint8)
+        g = np.zeros(len(k), dtype=np.int64)
+        rc = self._L.mq_handle_batch(self._h, len(k), k.ctypes.data, a.ctypes.data, b.ctypes.data, int(now_ns),
+                                     g.ctypes.data, int(threads))
+        if rc:
+            raise MemoryError("mq_handle_batch")
+        return g
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.mq_destroy(self._h)
+            self._h = None

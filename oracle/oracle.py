@@ -82,6 +82,13 @@ def lib():
         L.oracle_regex_list_found.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
                                               ctypes.c_void_p, ctypes.c_size_t]
+        # memquota C restatement (memquota_oracle.c)
+        L.mq_create.restype = ctypes.c_void_p
+        L.mq_create.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+        L.mq_destroy.argtypes = [ctypes.c_void_p]
+        L.mq_handle_batch.restype = ctypes.c_int
+        L.mq_handle_batch.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int]
         _LIB = L
     return _LIB
 

@@ -44,3 +44,26 @@ def test_alloc_and_release_table():
         else:
             got = 0
         assert got == rr
+
+
+def test_c_restatement_matches_python():
+    """memquota_oracle.c (the bench's CPU baseline, keys in parallel) against the Python
+    restatement on random batches: cells and windows, best effort, frees past what is in use,
+    frees of absent keys, out-of-range keys, time moving across window slots."""
+    import numpy as np
+    rng = np.random.default_rng(5)
+    K = 40
+    mx = rng.integers(1, 200, size=K)
+    vd = np.where(rng.random(K) < 0.5, 0, rng.integers(1, 4, size=K) * 10**9)
+    py = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
+    c = M.CMemquota(mx, vd)
+    now = BASE_NS
+    for batch in range(12):
+        n = 3000
+        keys = rng.integers(-2, K + 2, size=n).astype(np.int32)
+        amounts = rng.integers(-60, 80, size=n)
+        be = rng.random(n) < 0.4
+        got = c.handle_batch(keys, amounts, be, now, threads=4)
+        want = [py.handle(int(k), int(a), bool(b), now) if 0 <= k < K else 0 for k, a, b in zip(keys, amounts, be)]
+        assert got.tolist() == want, batch
+        now += int(rng.integers(0, 7)) * 10**8
