@@ -296,8 +296,10 @@ int mxp_regex_match_host(const char* pattern, uint32_t pattern_len, const char* 
 
 /*
  * Device-resident batches (benchmarking and pipelining): pack + upload once, evaluate many times.
- * mxp_batch_eval_device enqueues on `stream` (a hipStream_t; NULL = engine stream) and writes the
- * bitmaps to DEVICE pointers (rule-word-major, as above).  Nothing is synchronised.
+ * mxp_batch_eval_device enqueues on `stream` (a hipStream_t; NULL = the engine's stream, which is
+ * ordered with the device's legacy default stream: work the caller enqueued there first -- e.g.
+ * zeroing the hit counters -- completes before the evaluation starts) and writes the bitmaps to
+ * DEVICE pointers (rule-word-major, as above).  Nothing is synchronised.
  */
 /*
  * Wire decoding: CompressedAttributes messages (mxp_batch.h mxp_wire_batch) ->

@@ -1900,7 +1900,10 @@ int mxp_engine_create(int device, mxp_engine** out) {
         return MXP_OK;
     }
     hipError_t h = hipSetDevice(device);
-    if (h == hipSuccess) h = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    // (a blocking stream: ordered with the legacy default stream, so callers that prepare outputs
+    // there and pass NULL see them done -- a non-blocking one raced a caller's zeroing of the hit
+    // counters with the first evaluation's value-class counts)
+    if (h == hipSuccess) h = hipStreamCreateWithFlags(&e->stream, hipStreamDefault);
     if (h != hipSuccess) {
         delete e;
         return MXP_ERR_DEVICE;

@@ -1318,6 +1318,21 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
     const uint32_t GO = lane <= n ? A.gvt_off[g0 + lane] : 0u;
     const uint32_t e0 = __builtin_amdgcn_readlane(GO, 0), ecount = __builtin_amdgcn_readlane(GO, n) - e0;
     uint32_t GE0 = lane < ecount ? A.gvt[e0 + lane] : 0u, GE1 = lane + 64u < ecount ? A.gvt[e0 + 64u + lane] : 0u;
+    if constexpr (kLds) {
+        // each entry's LDS row, once per wave and lane-parallel (slot a's base PB[a] and first
+        // staged position PJ[a], its class capacity from MV): the group loop then takes a and the
+        // row from one readlane -- no per-entry scalar arithmetic (the scalar unit bounds this
+        // kernel: one per CU for its four SIMDs)
+        auto row_of = [&](uint32_t ent) {
+            const uint32_t a = ent >> 24, j = ent & 0xFFFFFFu;
+            const uint32_t pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(a << 2), (int)PB);
+            const uint32_t pj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(a << 2), (int)PJ);
+            const uint32_t cp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((2u * a) << 2), (int)MV);
+            return (a << 24) | (pb + (j - pj) * cp);
+        };
+        GE0 = row_of(GE0);
+        GE1 = row_of(GE1);
+    }
     for (uint32_t g = 0; g < n; g++) {
         const uint32_t G = g0 + g;
         const uint32_t mask = __builtin_amdgcn_readlane(FM, g);
@@ -1332,11 +1347,10 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
             const uint32_t ent = i < 64u ? __builtin_amdgcn_readlane(GE0, i)
                                  : i < 128u ? __builtin_amdgcn_readlane(GE1, i - 64u) : uni(A.gvt[e0 + i]);
             const uint32_t a = ent >> 24, j = ent & 0xFFFFFFu;
-            const uint32_t cap = __builtin_amdgcn_readlane(MV, 2u * a);
             const uint32_t au = __builtin_amdgcn_readfirstlane(a);
             const uint64_t c = (uint64_t)clv[2u * au] | (uint64_t)clv[2u * au + 1u] << 32;
             if constexpr (kLds) {
-                const uint32_t row = __builtin_amdgcn_readlane(PB, a) + (j - __builtin_amdgcn_readlane(PJ, a)) * cap;
+                const uint32_t row = j;  // (the entry's LDS row, computed above; staged chunks have <= 128 entries)
 #pragma unroll
                 for (uint32_t r = 0; r < 4; r++) {
                     const uint2 w = S[row + ((uint32_t)(c >> (16u * r)) & 0xFFFFu)];
@@ -1344,6 +1358,7 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
                     ve[r] |= w.y;
                 }
             } else {
+                const uint32_t cap = __builtin_amdgcn_readlane(MV, 2u * a);
                 const uint32_t tb = __builtin_amdgcn_readlane(MV, 2u * a + 1u);
                 const uint64_t row = (uint64_t)tb + (uint64_t)j * cap;
 #pragma unroll

@@ -140,6 +140,7 @@ def test_benched_evaluations_against_oracle(mxp, wl):
     dm = torch.zeros((Wd, N), dtype=torch.int32, device="cuda:0")
     req_err = torch.zeros(N, dtype=torch.uint8, device="cuda:0")
     hits = torch.zeros(R, dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()  # (the zeroing above is on torch's stream)
     for _ in range(3):
         db.eval_compact(dm.data_ptr(), req_err.data_ptr(), hits.data_ptr(), s)
     dm2 = torch.zeros_like(dm)

@@ -31,5 +31,3 @@ bad = np.nonzero(h != 3 * c)[0]
 print("rules with bad counters:", len(bad))
 for r in bad[:10]:
     print(r, rules[r][:70], "hits", h[r], "3*bits", 3 * c[r])
-np.save(os.path.join(ROOT, "gpurun_out", "dm_%s.npy" % os.path.basename(os.environ.get("MXP_LIB", "cur"))),
-        dm[:, :65536].cpu().numpy())
