@@ -550,7 +550,7 @@ int mxp_engine::build_plan(Plan& P) {
             P.vt_cols.push_back(vt_cand_col[s]);
         }
     std::vector<std::vector<std::pair<uint32_t, uint32_t>>> words_of(P.vt_cols.size());  // (group, mask)
-    std::vector<uint32_t> gvt_off(W + 1, 0), gvt;
+    std::vector<uint32_t> gvt_off(W + 1, 0), gvt, gvt_mask(W, 0);
     for (uint32_t g = 0; g < W; g++) {
         gvt_off[g] = (uint32_t)gvt.size();
         std::vector<uint32_t> mk(P.vt_cols.size(), 0);
@@ -558,6 +558,7 @@ int mxp_engine::build_plan(Plan& P) {
             if (excluded[g * 32 + k]) mk[act_of[vt_slot_of_rule[g * 32 + k]]] |= 1u << k;
         for (uint32_t a = 0; a < P.vt_cols.size(); a++)
             if (mk[a]) {
+                gvt_mask[g] |= 1u << a;
                 gvt.push_back((a << 24) | (uint32_t)words_of[a].size());
                 words_of[a].push_back({g, mk[a]});
             }
@@ -792,6 +793,7 @@ int mxp_engine::build_plan(Plan& P) {
     if ((rc = put(P.d_inj, inj.data(), inj.size() * 4, "upload inj"))) return rc;
     if ((rc = put(P.d_gvt_off, gvt_off.data(), gvt_off.size() * 4, "upload gvt_off"))) return rc;
     if ((rc = put(P.d_gvt, gvt.data(), gvt.size() * 4, "upload gvt"))) return rc;
+    if ((rc = put(P.d_gvt_mask, gvt_mask.data(), gvt_mask.size() * 4, "upload gvt mask"))) return rc;
     if ((rc = put(P.d_vt_woff, vt_woff.data(), vt_woff.size() * 4, "upload vt_woff"))) return rc;
     if ((rc = put(P.d_vt_words, vt_words.data(), vt_words.size() * 4, "upload vt_words"))) return rc;
     return MXP_OK;
@@ -1344,6 +1346,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
     if (!P.vt_cols.empty()) {
         A->gvt_off = P.d_gvt_off.as<uint32_t>();
         A->gvt = P.d_gvt.as<uint32_t>();
+        A->gvt_mask = P.d_gvt_mask.as<uint32_t>();
         A->vt_words = P.d_vt_words.as<uint32_t>();
         A->vt_meta = db->vt_meta.as<uint32_t>();
         A->vt_cls = db->vt_cls.as<uint16_t>();

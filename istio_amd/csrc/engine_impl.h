@@ -264,7 +264,7 @@ struct mxp_engine : public mxp::LowerTables {
         // value classes: active slot a -> column vt_cols[a], words vt_nw[a]; per group merge entries
         std::vector<uint32_t> vt_cols, vt_nw;
         uint32_t vt_max_nw = 0;
-        DevBuf d_gvt_off, d_gvt, d_vt_woff, d_vt_words;
+        DevBuf d_gvt_off, d_gvt, d_gvt_mask, d_vt_woff, d_vt_words;
         // deferred index pairs (kargs.dtp_*): possible when every group holding an indexed rule is
         // written by the value-class fill (no plain fill chunks, no dense rules); per group its fill
         // chunk << 8 | position in the chunk

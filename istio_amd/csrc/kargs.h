@@ -89,6 +89,7 @@ typedef struct mxp_kargs {
     // value classes (kernels.hip mxp_vt_*; null gvt_off: none)
     const uint32_t* gvt_off;     // [n_words + 1] merge entries of each group
     const uint32_t* gvt;         // active slot << 24 | word position j within the slot's words
+    const uint32_t* gvt_mask;    // [n_words] the active slots each group's merge entries name (ascending, one each)
     const uint32_t* vt_meta;     // [n_vt][8] MXP_VTM_* fields
     const uint32_t* vt_words;    // (group, rule mask) pairs of every slot's words
     uint16_t* vt_cls;            // [n_vt][n] class of each request

@@ -1315,6 +1315,7 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
     // each, read back with v_readlane -- no chain of dependent scalar loads per group
     const uint32_t MV = lane < 2u * MXP_VT_MAX && (lane >> 1) < nvt ? A.vt_meta[(lane >> 1) * 8u + MXP_VTM_CAP + (lane & 1u)] : 0u;
     const uint32_t FM = lane < n ? A.fill_masks[moff + lane] : 0u;
+    const uint32_t GM = kLds && lane < n ? A.gvt_mask[g0 + lane] : 0u;  // slots each group names
     const uint32_t GO = lane <= n ? A.gvt_off[g0 + lane] : 0u;
     const uint32_t e0 = __builtin_amdgcn_readlane(GO, 0), ecount = __builtin_amdgcn_readlane(GO, n) - e0;
     uint32_t GE0 = lane < ecount ? A.gvt[e0 + lane] : 0u, GE1 = lane + 64u < ecount ? A.gvt[e0 + 64u + lane] : 0u;
@@ -1343,6 +1344,27 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
             for (uint32_t r = 0; r < 4; r++)
                 if (e[r] && q0 + r < Q1) log_guard_errors(A, e[r], G * 32u, q0 + r);
         const uint32_t i0 = __builtin_amdgcn_readlane(GO, g) - e0, i1 = __builtin_amdgcn_readlane(GO, g + 1) - e0;
+        if constexpr (kLds) {
+            // staged (<= 128 entries): the group's entries in slot order, one per slot it names --
+            // unrolled over the slots so each one's classes come from fixed registers (no indexed
+            // register move) and its row from one readlane
+            const uint32_t gm = __builtin_amdgcn_readlane(GM, g);
+            uint32_t k = i0;
+#pragma unroll
+            for (uint32_t a = 0; a < MXP_VT_MAX; a++) {
+                if (!(gm & (1u << a))) continue;
+                const uint32_t row = (k < 64u ? __builtin_amdgcn_readlane(GE0, k) : __builtin_amdgcn_readlane(GE1, k - 64u)) &
+                                     0xFFFFFFu;
+                k++;
+                const uint64_t c = (uint64_t)clv[2u * a] | (uint64_t)clv[2u * a + 1u] << 32;
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++) {
+                    const uint2 w = S[row + ((uint32_t)(c >> (16u * r)) & 0xFFFFu)];
+                    m[r] |= w.x;
+                    ve[r] |= w.y;
+                }
+            }
+        } else
         for (uint32_t i = i0; i < i1; i++) {
             const uint32_t ent = i < 64u ? __builtin_amdgcn_readlane(GE0, i)
                                  : i < 128u ? __builtin_amdgcn_readlane(GE1, i - 64u) : uni(A.gvt[e0 + i]);
