@@ -476,10 +476,6 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
                         run = false;
                     }
                 }
-                if (run && (A.flags & 16777216u)) {  // ablation: no DFA walk (results invalid; DESIGN row N1)
-                    REG(d) = 0u;
-                    run = false;
-                }
                 if (run) {
                     const StrRef sub = str_of(A, subj);
                     // (over-budget patterns run the bit-parallel NFA: only the kNfa instantiations,
