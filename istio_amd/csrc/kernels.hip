@@ -1265,7 +1265,7 @@ struct DtpQueue {
 
 template <bool kLds>
 __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* F, uint32_t chunk, uint32_t qw,
-                                            const uint2* S, uint32_t PB, uint32_t PJ) {
+                                            const uint2* S, const uint32_t* RW) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
     const uint64_t N = A.n;
@@ -1315,21 +1315,6 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
     const uint32_t GO = lane <= n ? A.gvt_off[g0 + lane] : 0u;
     const uint32_t e0 = __builtin_amdgcn_readlane(GO, 0), ecount = __builtin_amdgcn_readlane(GO, n) - e0;
     uint32_t GE0 = lane < ecount ? A.gvt[e0 + lane] : 0u, GE1 = lane + 64u < ecount ? A.gvt[e0 + 64u + lane] : 0u;
-    if constexpr (kLds) {
-        // each entry's LDS row, once per wave and lane-parallel (slot a's base PB[a] and first
-        // staged position PJ[a], its class capacity from MV): the group loop then takes a and the
-        // row from one readlane -- no per-entry scalar arithmetic (the scalar unit bounds this
-        // kernel: one per CU for its four SIMDs)
-        auto row_of = [&](uint32_t ent) {
-            const uint32_t a = ent >> 24, j = ent & 0xFFFFFFu;
-            const uint32_t pb = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(a << 2), (int)PB);
-            const uint32_t pj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(a << 2), (int)PJ);
-            const uint32_t cp = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((2u * a) << 2), (int)MV);
-            return (a << 24) | (pb + (j - pj) * cp);
-        };
-        GE0 = row_of(GE0);
-        GE1 = row_of(GE1);
-    }
     for (uint32_t g = 0; g < n; g++) {
         const uint32_t G = g0 + g;
         const uint32_t mask = __builtin_amdgcn_readlane(FM, g);
@@ -1345,13 +1330,12 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
             // unrolled over the slots so each one's classes come from fixed registers (no indexed
             // register move) and its row from one readlane
             const uint32_t gm = __builtin_amdgcn_readlane(GM, g);
-            uint32_t k = i0;
+            const uint4 ra = *(const uint4*)(RW + g * MXP_VT_MAX), rb = *(const uint4*)(RW + g * MXP_VT_MAX + 4u);
+            const uint32_t rows[MXP_VT_MAX] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
 #pragma unroll
             for (uint32_t a = 0; a < MXP_VT_MAX; a++) {
                 if (!(gm & (1u << a))) continue;
-                const uint32_t row = (k < 64u ? __builtin_amdgcn_readlane(GE0, k) : __builtin_amdgcn_readlane(GE1, k - 64u)) &
-                                     0xFFFFFFu;
-                k++;
+                const uint32_t row = rows[a];
                 const uint64_t c = (uint64_t)clv[2u * a] | (uint64_t)clv[2u * a + 1u] << 32;
 #pragma unroll
                 for (uint32_t r = 0; r < 4; r++) {
@@ -1494,8 +1478,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_dtp_kernel(mxp_kargs 
 // MXP_DEBUG_FLAGS 2097152: every chunk gathers class words from global memory (A/B)
 extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A) {
     const uint32_t wave = uni(threadIdx.x >> 6);
-    vtfill_wave<false>(A, A.fills + blockIdx.y, A.dtp_cbase + blockIdx.y, A.q0 + (blockIdx.x * 4u + wave) * 256u, nullptr, 0u,
-                       0u);
+    vtfill_wave<false>(A, A.fills + blockIdx.y, A.dtp_cbase + blockIdx.y, A.q0 + (blockIdx.x * 4u + wave) * 256u, nullptr,
+                       nullptr);
 }
 
 // The default: a workgroup stages its chunk's class-word rows in LDS once -- per active slot a, the
@@ -1530,7 +1514,12 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
         }
         total += rows * __builtin_amdgcn_readlane(capl, a);
     }
-    const bool staged = ecount <= 128u && total <= MXP_VTF_STAGE && !(A.flags & 2097152u);
+    const bool staged = ecount <= 128u && n <= MXP_FILL_CHUNK && total <= MXP_VTF_STAGE && !(A.flags & 2097152u);
+    // the LDS row of every (group, slot) merge entry of the chunk, so the group loop reads them with
+    // two broadcast LDS loads per group and no scalar arithmetic (the scalar unit, one per CU,
+    // bounded this kernel)
+    __shared__ uint32_t RW[MXP_FILL_CHUNK * MXP_VT_MAX];
+    __shared__ uint32_t PL[3 * MXP_VT_MAX];  // per slot: LDS base, first staged position, capacity
     if (staged) {
         for (uint32_t a = 0; a < nvt; a++) {
             const uint32_t base = __builtin_amdgcn_readlane(PB, a);
@@ -1539,14 +1528,27 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
                                  (uint64_t)__builtin_amdgcn_readlane(PJ, a) * __builtin_amdgcn_readlane(capl, a);
             for (uint32_t i = tid; i < next - base; i += 256u) S[base + i] = *(const uint2*)(A.vt_tm + 2u * (src + i));
         }
+        if (tid < nvt) {
+            PL[3u * tid] = PB;
+            PL[3u * tid + 1u] = PJ;
+            PL[3u * tid + 2u] = capl;
+        }
+        __syncthreads();
+        if (tid < n) {  // thread t: group t's entries
+            const uint32_t i1 = A.gvt_off[g0 + tid + 1u];
+            for (uint32_t i = A.gvt_off[g0 + tid]; i < i1; i++) {
+                const uint32_t ent = A.gvt[i], a = ent >> 24, j = ent & 0xFFFFFFu;
+                RW[tid * MXP_VT_MAX + a] = PL[3u * a] + (j - PL[3u * a + 1u]) * PL[3u * a + 2u];
+            }
+        }
         __syncthreads();
     }
     for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
         const uint32_t qw = A.q0 + ((blockIdx.x * MXP_VTF_TILES + t) * 4u + wave) * 256u;
         if (staged)
-            vtfill_wave<true>(A, F, A.dtp_cbase + blockIdx.y, qw, S, PB, PJ);
+            vtfill_wave<true>(A, F, A.dtp_cbase + blockIdx.y, qw, S, RW);
         else
-            vtfill_wave<false>(A, F, A.dtp_cbase + blockIdx.y, qw, nullptr, 0u, 0u);
+            vtfill_wave<false>(A, F, A.dtp_cbase + blockIdx.y, qw, nullptr, nullptr);
     }
 }
 
