@@ -1315,6 +1315,7 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
     const uint32_t GO = lane <= n ? A.gvt_off[g0 + lane] : 0u;
     const uint32_t e0 = __builtin_amdgcn_readlane(GO, 0), ecount = __builtin_amdgcn_readlane(GO, n) - e0;
     uint32_t GE0 = lane < ecount ? A.gvt[e0 + lane] : 0u, GE1 = lane + 64u < ecount ? A.gvt[e0 + 64u + lane] : 0u;
+    uint32_t anyerr[4] = {0u, 0u, 0u, 0u};
     for (uint32_t g = 0; g < n; g++) {
         const uint32_t G = g0 + g;
         const uint32_t mask = __builtin_amdgcn_readlane(FM, g);
@@ -1386,9 +1387,8 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
         if (dany) dq.merge(g, m, e);  // the index kernel's true / error pairs in this group's words
         // (no hit counting: a uniform group's words hold no true bit but the value classes', which
         // mxp_vt_eval_kernel counts per class)
-        if (A.req_err)
-            for (uint32_t r = 0; r < 4; r++)
-                if (e[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++) anyerr[r] |= e[r];  // (request error flags: once, after the loop)
         const uint64_t at = (uint64_t)G * N + q0;
         if (vec && q0 < Q1) {
             const v4u mv = v4u{m[0], m[1], m[2], m[3]};
@@ -1408,6 +1408,9 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
             }
         }
     }
+    if (A.req_err)
+        for (uint32_t r = 0; r < 4; r++)
+            if (anyerr[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;
 }
 
 // mxp_fill_kernel for deferred index pairs (kargs.dtp_slots): one span of 256 requests per wave (a

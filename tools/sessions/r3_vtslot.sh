@@ -1,9 +1,9 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-o=gpurun_out/r3vw; mkdir -p $o
+o=gpurun_out/r3ve; mkdir -p $o
 timeout -k 10 900 python -u -m pytest tests/test_gpu_vt.py tests/test_gpu_dtp.py tests/test_gpu_scale.py -x -q --timeout 300 --timeout-method thread > $o/tests.log 2>&1 || exit $?
-for lib in ablib/libmxp_vtslot.so ablib/libmxp_vtrw.so ablib/libmxp_vtslot.so ablib/libmxp_vtrw.so; do
+for lib in ablib/libmxp_vtrw.so ablib/libmxp_vterr.so ablib/libmxp_vtrw.so ablib/libmxp_vterr.so; do
   echo "== $lib" >> $o/steady_c4.log
   MXP_LIB=$lib timeout -k 10 200 python tools/steady.py c4 >> $o/steady_c4.log 2>&1 || exit $?
 done
