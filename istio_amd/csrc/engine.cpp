@@ -519,9 +519,16 @@ int mxp_engine::build_plan(Plan& P) {
             const uint64_t hh = mxp_str_hash_seeded(mxp_composite_seed(k1), (const uint8_t*)key.data(), key.size());
             uint32_t h = (uint32_t)hh & x.hmask2;
             while (hents[x.hoff2 + 2 * h].len) h = (h + 1) & x.hmask2;
-            hents[x.hoff2 + 2 * h] = mxp_hent{kv.first.second, (uint32_t)(hh >> 32), (uint32_t)postings.size(),
-                                              (uint32_t)rs.size()};
-            hents[x.hoff2 + 2 * h + 1] = mxp_hent{(uint32_t)k1, (uint32_t)(k1 >> 32), 0, 0};
+            // (vm.h MXP_COMP_*: a key of <= 12 bytes rides inline in the pair -- bytes 0..3 in the
+            // first entry's klo, 4..11 in the second's start / len -- so a probe verifies it with
+            // no key-string loads; longer keys keep their string id; the key length sits in the top
+            // byte of the posting count, 255 for 255 bytes and more)
+            if (rs.size() >= (1u << 24)) return fail(MXP_ERR_NOMEM, "composite posting list too long");
+            uint32_t kw[3] = {0, 0, 0};
+            if (key.size() <= 12) memcpy(kw, key.data(), key.size());
+            hents[x.hoff2 + 2 * h] = mxp_hent{key.size() <= 12 ? kw[0] : kv.first.second, (uint32_t)(hh >> 32),
+                                              (uint32_t)postings.size(), (uint32_t)rs.size() | ((uint32_t)std::min<size_t>(key.size(), 255) << 24)};
+            hents[x.hoff2 + 2 * h + 1] = mxp_hent{(uint32_t)k1, (uint32_t)(k1 >> 32), kw[1], kw[2]};
             post(rs, rule_tmpl2);
         }
         x.plen0 = (uint32_t)plens.size();

@@ -2000,7 +2000,21 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                         const mxp_hent K = comp ? A.hents[at + 1u] : E;
                         if (E.len == 0) break;
                         if (E.khi != tag) continue;
-                        if (comp && (K.klo != vlo || K.khi != vhi)) continue;
+                        if (comp) {
+                            if (K.klo != vlo || K.khi != vhi || (E.len >> 24) != min(L, 255u)) continue;
+                            if (L <= 12u) {  // the key inline (vm.h MXP hmask2 layout): no key-string loads
+                                const uint64_t k0 = (uint64_t)E.klo | ((uint64_t)K.start << 32);
+                                const uint64_t w0 = by_head ? (uint64_t)s.p : ld8a(s.p);
+                                const uint64_t w1 = by_head ? (uint64_t)hw1 : (L > 8u ? ld8a(s.p + 8) : 0ull);
+                                const uint64_t m0 = L >= 8u ? ~0ull : (1ull << (L * 8u)) - 1ull;
+                                const uint64_t m1 = L > 8u ? (1ull << ((L - 8u) * 8u)) - 1ull : 0ull;
+                                if (((w0 ^ k0) & m0) == 0 && ((w1 ^ (uint64_t)K.len) & m1) == 0) {
+                                    fi = at;
+                                    break;
+                                }
+                                continue;
+                            }
+                        }
                         const StrRef k = str_of(A, E.klo);
                         if (k.n == L && (by_head ? head_eq((uint64_t)s.p, hw1, k.p, L) : bytes_eq_a(s.p, k.p, L))) {
                             fi = at;
@@ -2010,7 +2024,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 }
                 if (fi != 0xFFFFFFFFu) {
                     start = A.hents[fi].start;
-                    len = A.hents[fi].len;
+                    len = A.hents[fi].len & (comp ? 0xFFFFFFu : 0xFFFFFFFFu);
                 }
             }
             if (A.flags & 1024u) {  // ablation: probes only (results invalid)

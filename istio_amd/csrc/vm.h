@@ -117,7 +117,8 @@ typedef struct mxp_index {
     uint32_t nplen;
     uint32_t col2;     // composite: the prefix column (string want class)
     uint32_t okset2;
-    uint32_t hmask2;   // composite table: pairs of entries {K2 string id, tag, start, len}, {K1 lo, K1 hi, 0, 0}
+    uint32_t hmask2;   // composite table: pairs of entries {K2 word 0 | K2 string id, tag, start,
+                       // len | min(|K2|, 255) << 24}, {K1 lo, K1 hi, K2 words 1, 2}: keys of <= 12 bytes inline
     uint32_t hoff2;
     uint32_t pad[5];
 } mxp_index;           // 64 B

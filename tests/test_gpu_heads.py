@@ -26,7 +26,8 @@ MANIFEST = {"request.path": "STRING", "destination.service": "STRING", "request.
 
 SHORT = ["/", "/a", "/ab", "/abcdefg", "/abcdefgh", "/abcdefgh1", "/abcdefghij", "/abcdefghijk",
          "/été/x", "/abcdefghé", "/abcdefghi\u00e9"]
-LONG = SHORT + ["/abcdefghijkl", "/abcdefghijklm", "/abcdefghijklmnop"]
+LONG = SHORT + ["/abcdefghijkl", "/abcdefghijklm", "/abcdefghijklmnop", "/" + "x" * 254, "/" + "x" * 299]
+# (keys of 255 bytes and more: the composite entry stores min(length, 255) -- vm.h)
 
 
 def head_rules(keys=SHORT):
