@@ -618,7 +618,7 @@ extern "C" hipError_t mxp_quota_sort(void* tmp, size_t* tmp_bytes, const uint32_
 //                      -- arrival order kept within a key -- and the group's first lane moves the
 //                      key's position past the group.  Writes order, skeys, the amounts and
 //                      best-effort flags in sorted order, and flags keys with amounts past 2^55.
-constexpr uint32_t kTile = 2048;
+constexpr uint32_t kTile = 1024;  // (same-box: 2048 0.259 / 0.260 ms, 1024 0.253 / 0.255, 512 0.270 / 0.272; profiles/r3_v16_quota_tiles.log)
 
 extern "C" __global__ __launch_bounds__(64) void mxp_quota_hist(const uint32_t* key, uint32_t n, uint32_t n_keys,
                                                                 uint32_t tiles, uint32_t* H) {
