@@ -198,3 +198,37 @@ def test_deferred_pairs_across_streams(mxp, monkeypatch, env):
         for x, y in zip(a, b):
             assert np.array_equal(x, y)
     assert (got[2][0] != 0).any()
+
+
+@pytest.mark.parametrize("chunks", ["2", "5"])
+def test_deferred_pairs_request_chunks(mxp, monkeypatch, chunks):
+    """The deferred-pair request chunks (MXP_DTP_CHUNKS: chunk c's index and sort kernels on the
+    side stream beside chunk c - 1's fill; off by default, DESIGN §8 experiments): bitmaps and hit
+    counters equal those of the unchunked engine, on C4 routes with index error pairs and on C2,
+    over a ragged batch, three evaluations back to back."""
+    import torch
+    for wl in ("c4", "c2"):
+        if wl == "c4":
+            manifest, rules, batch = W.c4_workload(n_rules=1500, n_requests=12345, seed=21)
+        else:
+            manifest, rules, batch = W.c2_workload(n_rules=1500, n_requests=12345, seed=21)
+        R = len(rules)
+        Wd = (R + 31) // 32
+        outs = []
+        for env in ({"MXP_DTP_CHUNKS": chunks}, {}):
+            monkeypatch.delenv("MXP_DTP_CHUNKS", raising=False)
+            eng = engine_for(mxp, monkeypatch, env, manifest, rules)
+            db = eng.upload(batch)
+            dm = torch.full((Wd, batch.n), -1, dtype=torch.int32, device="cuda:0")
+            de = torch.full_like(dm, -1)
+            hits = torch.zeros(R, dtype=torch.int64, device="cuda:0")
+            torch.cuda.synchronize()
+            s = torch.cuda.Stream()
+            for _ in range(3):
+                db.eval_hits(dm.data_ptr(), de.data_ptr(), hits.data_ptr(), s.cuda_stream)
+            torch.cuda.synchronize()
+            outs.append((dm.cpu().numpy(), de.cpu().numpy(), hits.cpu().numpy()))
+            db.free()
+        for x, y in zip(*outs):
+            assert np.array_equal(x, y), wl
+        assert outs[0][2].sum() > 0

@@ -20,7 +20,7 @@ nb = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 rows = load(db)
 n = len(rows)
 # block boundaries: equal share of the index-kernel launches (one per evaluation and block)
-marks = [i for i, r in enumerate(rows) if r[0].startswith("mxp_index_dtp_kernel") or r[0].startswith("mxp_index_kernel")]
+marks = [i for i, r in enumerate(rows) if r[0].startswith("mxp_index_dtp_")]
 bounds = [0]
 if nb > 1 and marks:
     per = len(marks) // nb

@@ -15,7 +15,7 @@ def load(path):
     return list(sqlite3.connect(path).execute("select name, start, end from kernels order by start"))
 
 db = sys.argv[1]
-anchor = sys.argv[2] if len(sys.argv) > 2 else "mxp_index_dtp_kernel"
+anchor = sys.argv[2] if len(sys.argv) > 2 else "mxp_index_dtp_"
 occ = int(sys.argv[3]) if len(sys.argv) > 3 else 10
 rows = load(db)
 idx = [i for i, r in enumerate(rows) if r[0].startswith(anchor)]
