@@ -537,9 +537,13 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
         "lds_bank_conflicts": lds_conflicts(kind),
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "one evaluation: value classes (mxp_vt_lookup/vt_eval), mxp_fill / vtfill / guard2 "
-                               "/ eval kernels (the groups each serves) + mxp_index_kernel (+ mxp_inject_kernel with "
-                               "dense rules); traffic also counts mxp_hits_kernel when the hit counters are not fused",
+                     "kernel": ("one evaluation: value classes (mxp_vt_lookup/vt_eval), guard index with deferred "
+                                "pairs (mxp_index_dtp[_lite]_kernel), mxp_dtp_sort_kernel, bitmap fill merging the pairs "
+                                "(mxp_fill_dtp / mxp_vtfill_lds), mxp_dtp_hits_kernel, post-fill mxp_index_kernel"
+                                if deferred else
+                                "one evaluation: value classes (mxp_vt_lookup/vt_eval), mxp_fill / vtfill / guard2 / eval "
+                                "kernels (the groups each serves) + mxp_index_kernel (+ mxp_inject_kernel with dense "
+                                "rules); traffic also counts mxp_hits_kernel when the hit counters are not fused"),
                      "alg_bytes_per_launch": alg_bytes, "alg_bytes_per_pair": alg_bytes / (N * R)},
     }
     if quota is not None:

@@ -1586,20 +1586,25 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
         for (uint32_t i = tid; i < cwn * 128u; i += 256u) cnt[i] = 0u;
         if (tid == 0) ovn = 0u;
         __syncthreads();
-        for (uint32_t w = 0; w < nw; w++) {
-            const uint32_t n = min(uni(A.dtp_n[w0 + w]), A.dtp_cap);
-            const uint32_t* E = A.dtp_ent + (uint64_t)(w0 + w) * A.dtp_cap;
-            // four entries per thread and step: their loads (entry, then its chunk) in flight
-            // together instead of one dependent pair of round trips per entry
-            for (uint32_t i0 = tid; i0 < n; i0 += 1024u) {
-            uint32_t ev[4], cv[4];
+        // four index waves' lists at a time, four entries of each per thread: 16 entries' loads (entry,
+        // then its chunk) in flight together (a list holds ~1k entries, so one step covers it)
+        for (uint32_t wb = 0; wb < nw; wb += 4u) {
+            uint32_t nl[4];
 #pragma unroll
-            for (uint32_t u = 0; u < 4u; u++) ev[u] = i0 + 256u * u < n ? E[i0 + 256u * u] : 0xFFFFFFFFu;
+            for (uint32_t g = 0; g < 4u; g++) nl[g] = wb + g < nw ? min(uni(A.dtp_n[w0 + wb + g]), A.dtp_cap) : 0u;
+            const uint32_t nmax = max(max(nl[0], nl[1]), max(nl[2], nl[3]));
+            for (uint32_t i0 = tid; i0 < nmax; i0 += 1024u) {
+            uint32_t ev[16], cv[16];
 #pragma unroll
-            for (uint32_t u = 0; u < 4u; u++) cv[u] = ev[u] != 0xFFFFFFFFu ? A.dtp_chunk[(ev[u] & 0x7FFFFFu) >> 5] : 0u;
+            for (uint32_t u = 0; u < 16u; u++) {
+                const uint32_t g = u >> 2, i = i0 + 256u * (u & 3u);
+                ev[u] = i < nl[g] ? A.dtp_ent[(uint64_t)(w0 + wb + g) * A.dtp_cap + i] : 0xFFFFFFFFu;
+            }
 #pragma unroll
-            for (uint32_t u = 0; u < 4u; u++) {
-                const uint32_t e = ev[u];
+            for (uint32_t u = 0; u < 16u; u++) cv[u] = ev[u] != 0xFFFFFFFFu ? A.dtp_chunk[(ev[u] & 0x7FFFFFu) >> 5] : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < 16u; u++) {
+                const uint32_t e = ev[u], w = wb + (u >> 2);
                 if (e == 0xFFFFFFFFu) continue;
                 const uint32_t rule = e & 0x7FFFFFu, ch = cv[u];
                 // fused hit counters (first window pass): a true pair into the workgroup's histogram
@@ -1619,10 +1624,10 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
                     ovq[o][0] = t * 1024u + ql;
                     ovq[o][1] = rr;
                 } else {  // (the LDS stage is full: straight to the list)
-                    const uint32_t g = atomicAdd(&A.dtp_ovf_n[0], 1u);
-                    if (g < A.dtp_ovf_cap) {
-                        A.dtp_ovf[2ull * g] = t * 1024u + ql;
-                        A.dtp_ovf[2ull * g + 1] = rr;
+                    const uint32_t gi = atomicAdd(&A.dtp_ovf_n[0], 1u);
+                    if (gi < A.dtp_ovf_cap) {
+                        A.dtp_ovf[2ull * gi] = t * 1024u + ql;
+                        A.dtp_ovf[2ull * gi + 1] = rr;
                     } else {
                         __hip_atomic_store(&A.dtp_ovf_n[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }

@@ -10,7 +10,9 @@ import json
 import os
 from collections import defaultdict
 
-EVAL = ("mxp_fill_kernel", "mxp_guard_kernel", "mxp_guard2_kernel", "mxp_eval_kernel", "mxp_index_kernel", "mxp_inject_kernel")
+EVAL = ("mxp_fill_kernel", "mxp_fill_dtp_kernel", "mxp_vtfill_lds_kernel", "mxp_guard_kernel", "mxp_guard2_kernel",
+        "mxp_eval_kernel", "mxp_index_kernel", "mxp_index_dtp_kernel", "mxp_index_dtp_lite_kernel", "mxp_dtp_sort_kernel",
+        "mxp_vt_lookup_kernel", "mxp_inject_kernel")
 
 
 def main():
