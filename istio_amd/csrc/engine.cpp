@@ -141,6 +141,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     for (uint32_t i = 0; i < n; i++) {
         const uint32_t mode = guards[i].mode & 0xFF, pc0 = guards[i].mode >> 16;
         if (mode != GM_AND && mode != GM_OR) continue;
+        if (rules[i].low.nregs > MXP_VM_MAXREG) continue;  // deep rule: the index kernels' registers are too few
         std::vector<mxp_vm_ins> code(all.begin() + off[i], all.begin() + off[i + 1]);
         mxp::HoistedCont h;
         if (!mxp::hoist_continuation(code, pc0, &h)) continue;
@@ -536,6 +537,23 @@ int mxp_engine::build_plan(Plan& P) {
         plens.insert(plens.end(), lens.begin(), lens.end());
         idx.push_back(x);
     }
+    // string heads: plan 0 assigns a row to every column its prefix / composite indexes probe (the
+    // other plans leave value-class rules out, so their indexes probe a subset of those columns)
+    if (base) {
+        head_cols.clear();
+        head_slot_of.assign(cols.size() + vcols.size(), MXP_VM_DONE);
+    }
+    for (mxp_index& x : idx) {
+        x.hslot = MXP_VM_DONE;
+        if (x.prefix == MXP_IX_EQ) continue;
+        const uint32_t c = x.prefix == MXP_IX_COMPOSITE ? x.col2 : x.col;
+        if (c >= head_slot_of.size()) continue;
+        if (base && head_slot_of[c] == MXP_VM_DONE) {
+            head_slot_of[c] = (uint32_t)head_cols.size();
+            head_cols.push_back(c);
+        }
+        x.hslot = head_slot_of[c];
+    }
     P.n_idx = (uint32_t)idx.size();
     std::vector<uint32_t> alias_off(P.n_alias ? n + 1 : 0, 0), alias_list;
     if (P.n_alias) {
@@ -640,6 +658,9 @@ int mxp_engine::build_plan(Plan& P) {
     for (uint32_t i = 0; i < n; i++)
         if (!excluded[i] && rules[i].low.ok && rules[i].low.nregs > MXP_VM_MAXREG) deep[i / 32] = 1;
     for (uint32_t g = 0; g < W; g++) {
+        // (a deep group is never a fill group: the deep kernel's plain stores would erase the fill's
+        // merged deferred pairs; deep rules are never templated, hence never indexed, so this only
+        // states what hoist_continuation already guarantees)
         (deep[g] ? gdeep : gall).push_back(g);
         const mxp_group& G = groups[g];
         const bool has_vt = gvt_off[g + 1] > gvt_off[g];
@@ -649,7 +670,7 @@ int mxp_engine::build_plan(Plan& P) {
         const bool only_vt = G.all == 0 && has_vt;
         const bool uniform = !G.vm && (only_vt || (G.all && G.indexed == G.all && G.guarded == G.all && G.nseg == 1 &&
                                                    G.s_cmp == 0 && G.s_rules == G.all)) &&
-                             !(debug_flags & 32u);
+                             !deep[g] && !(debug_flags & 32u);
         if (uniform) {
             mxp_fill* F = fills.empty() ? nullptr : &fills.back();
             const bool joins = F && F->g0 + F->n == g && F->n < fill_chunk &&
@@ -1332,7 +1353,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
     A->n = db->n;
     A->kinds = db->kinds.as<uint8_t>();
     A->vals = db->vals.as<uint64_t>();
-    A->heads = db->heads.p && db->heads_ncol == (uint32_t)(cols.size() + vcols.size()) ? db->heads.as<uint4>() : nullptr;
+    A->heads = db->heads.p && db->heads_ncol == (uint32_t)head_cols.size() ? db->heads.as<uint4>() : nullptr;
     A->n_gstr = gstrs.size();
     A->gstr_off = d_gstr_off.as<uint64_t>();
     A->gstr = d_gstr.as<uint8_t>();
@@ -1368,10 +1389,21 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
 // String heads of a packed batch (kargs.heads): one gather over every column, on the engine stream,
 // as the last step of packing -- part of the batch layout, like the columns themselves.
 int mxp_engine::pack_heads(mxp_dbatch* db) {
-    const uint32_t ncol = (uint32_t)(cols.size() + vcols.size());
-    if (!heads_on || !db->n || !ncol) return MXP_OK;
+    const uint32_t nrow = (uint32_t)head_cols.size();
+    db->heads_ncol = 0;
+    if (!heads_on || !db->n || !nrow) return MXP_OK;
     hipError_t e;
-    if ((e = db->heads.alloc((size_t)ncol * db->n * 16)) != hipSuccess) return hipfail(e, "string heads");
+    // heads are an accelerator, not part of the batch's meaning: without the memory the index
+    // kernel reads the strings themselves (A.heads = null)
+    if (db->heads.alloc((size_t)nrow * db->n * 16) != hipSuccess) {
+        (void)hipGetLastError();
+        db->heads.p = nullptr;
+        db->heads.reset();
+        return MXP_OK;
+    }
+    if ((e = d_head_cols.reserve(nrow * 4u)) != hipSuccess) return hipfail(e, "hipMalloc head columns");
+    if ((e = hipMemcpy(d_head_cols.p, head_cols.data(), nrow * 4u, hipMemcpyHostToDevice)) != hipSuccess)
+        return hipfail(e, "upload head columns");
     mxp_kargs A;
     memset(&A, 0, sizeof A);
     A.n = db->n;
@@ -1382,9 +1414,10 @@ int mxp_engine::pack_heads(mxp_dbatch* db) {
     A.gstr = d_gstr.as<uint8_t>();
     A.bstr_off = db->bstr_off.as<uint64_t>();
     A.bstr = db->bstr.as<uint8_t>();
-    if ((e = mxp_launch_heads(&A, ncol, db->heads.as<uint4>(), stream)) != hipSuccess) return hipfail(e, "launch heads");
+    if ((e = mxp_launch_heads(&A, d_head_cols.as<uint32_t>(), nrow, db->heads.as<uint4>(), stream)) != hipSuccess)
+        return hipfail(e, "launch heads");
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "heads sync");
-    db->heads_ncol = ncol;
+    db->heads_ncol = nrow;
     return MXP_OK;
 }
 
@@ -1446,6 +1479,9 @@ int mxp_engine::vt_prepare(mxp_dbatch* db, const Plan& P) {
 
 int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
                        bool log, unsigned long long* d_hits, uint64_t* stats, uint32_t q_lo, uint32_t q_hi) {
+    // (no stale flags from the previous evaluation survive an early return below)
+    last_dtp = false;
+    last_dtp_counted = false;
     // guards on: guard-only groups through the lean kernel, the rest through the VM kernel;
     // guards off (Eval, ablation): every group through the VM kernel
     const bool guards_on = !d_vals && !(debug_flags & 2u);

@@ -26,7 +26,7 @@
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
-extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, uint32_t ncol, uint4* heads, hipStream_t s);
+extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, const uint32_t* cols, uint32_t nrow, uint4* heads, hipStream_t s);
 extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
 extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
@@ -137,8 +137,8 @@ struct mxp_dbatch {
     DevBuf vt_cls, vt_keys, vt_rep, vt_cnt, vt_t, vt_meta;
     size_t vt_t_words = 0, vt_keys_n = 0;
     DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
-    DevBuf heads;                                     // [n_cols][n] string heads (kargs.heads)
-    uint32_t heads_ncol = 0;                          // columns the heads cover
+    DevBuf heads;                                     // [head columns][n] string heads (kargs.heads)
+    uint32_t heads_ncol = 0;                          // rows the heads cover (mxp_engine::head_cols)
     DevBuf rxof, rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // run-time regexp patterns
     bool rx_nfa = false;                              // one of them compiled to a bit-parallel NFA
     StrPool overlay;                                  // batch strings not in the rule set's pool
@@ -182,6 +182,12 @@ struct mxp_engine : public mxp::LowerTables {
         vocab_index[name] = (uint32_t)vocab_names.size();
         vocab_names.push_back(name);
         return (int64_t)vocab_names.size() - 1;
+    }
+    // ... without asking the finder (evaluation paths: positions never grow after compile /
+    // mxp_resolver_set, whatever batches are evaluated)
+    int64_t vocab_find(const std::string& name) const {
+        auto it = vocab_index.find(name);
+        return it == vocab_index.end() ? -1 : (int64_t)it->second;
     }
     mxp::FuncMap fmap = mxp::default_func_map();
 
@@ -570,8 +576,12 @@ struct mxp_engine : public mxp::LowerTables {
         return rc ? rc : pack_dict(db);
     }
     int pack_dict(mxp_dbatch* db);   // the value-class dictionary of the batch (mxp_vt_classify_kernel)
-    int pack_heads(mxp_dbatch* db);  // kargs.heads of every column (MXP_HEADS=0: none)
+    int pack_heads(mxp_dbatch* db);  // kargs.heads of the probed columns (MXP_HEADS=0: none)
     bool heads_on = true;
+    // columns a prefix or composite guard index probes (plan 0's indexes, a superset of every other
+    // plan's): heads are built for these alone; head_slot_of[col] is the row (MXP_VM_DONE: none)
+    std::vector<uint32_t> head_cols, head_slot_of;
+    DevBuf d_head_cols;
     uint32_t* gate_next_out = nullptr;  // eval_device_hits -> launch: the next evaluation's gate word
     hipStream_t stats_stream = nullptr;  // stream of the last stats_ev record (a wait only across streams)
     int pack_on_host(const mxp_bag_batch* b, mxp_dbatch* db);

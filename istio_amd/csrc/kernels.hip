@@ -1963,13 +1963,14 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
         // short keys (every key length <= 12) hash and verify from the string's head (kargs.heads):
         // one coalesced 16-byte load instead of the descriptor and the bytes (scattered, dependent)
         const uint32_t lmax = (!final && kind != MXP_IX_EQ && nplen) ? uni(A.plens[plen0 + nplen - 1u]) : 0u;
-        const bool by_head = A.heads && lmax <= 12u;
+        const uint32_t hslot = uni(X->hslot);
+        const bool by_head = A.heads && hslot != MXP_VM_DONE && lmax <= 12u;
         // (the head's first word rides in the string pointer's registers: one of the two is live)
         StrRef s{nullptr, 0};
         uint32_t hw1 = 0;
         if (sok) {
             if (by_head) {
-                const uint4 hd = A.heads[(uint64_t)(comp ? uni(X->col2) : col) * N + req];
+                const uint4 hd = A.heads[(uint64_t)hslot * N + req];
                 s.p = (const uint8_t*)((uint64_t)hd.x | ((uint64_t)hd.y << 32));
                 hw1 = hd.z;
                 s.n = hd.w;
@@ -2397,10 +2398,12 @@ extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hip
 
 // String heads (kargs.heads): per column and request, a string value's first 12 bytes (zero past
 // its length; pools are 8-aligned with 16 bytes of tail slack) and its length; zero for other kinds.
-extern "C" __global__ __launch_bounds__(256) void mxp_heads_kernel(mxp_kargs A, uint4* __restrict__ heads) {
-    const uint32_t req = blockIdx.x * 256u + threadIdx.x, col = blockIdx.y;
+// Only the columns a prefix or composite index probes have heads: row k of `heads` is column cols[k].
+extern "C" __global__ __launch_bounds__(256) void mxp_heads_kernel(mxp_kargs A, const uint32_t* __restrict__ cols,
+                                                                   uint4* __restrict__ heads) {
+    const uint32_t req = blockIdx.x * 256u + threadIdx.x, row = blockIdx.y;
     if (req >= A.n) return;
-    const uint64_t at = (uint64_t)col * A.n + req;
+    const uint64_t at = (uint64_t)cols[row] * A.n + req;
     uint4 h = make_uint4(0u, 0u, 0u, 0u);
     if (A.kinds[at] == MXP_STRING) {
         const StrRef r = str_of(A, A.vals[at]);
@@ -2409,11 +2412,11 @@ extern "C" __global__ __launch_bounds__(256) void mxp_heads_kernel(mxp_kargs A, 
         const uint64_t m1 = r.n >= 12u ? 0xFFFFFFFFull : r.n > 8u ? (1ull << ((r.n - 8u) * 8u)) - 1ull : 0ull;
         h = make_uint4((uint32_t)(w0 & m0), (uint32_t)((w0 & m0) >> 32), (uint32_t)(w1 & m1), r.n);
     }
-    heads[at] = h;
+    heads[(uint64_t)row * A.n + req] = h;
 }
 
-extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, uint32_t ncol, uint4* heads, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_heads_kernel, dim3((args->n + 255u) / 256u, ncol), dim3(256), 0, s, *args, heads);
+extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, const uint32_t* cols, uint32_t nrow, uint4* heads, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_heads_kernel, dim3((args->n + 255u) / 256u, nrow), dim3(256), 0, s, *args, cols, heads);
     return hipGetLastError();
 }
 

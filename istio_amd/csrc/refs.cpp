@@ -93,12 +93,12 @@ int mxp_engine::refs_assemble(const mxp_bag_batch* b, const std::vector<mxp_ref_
         const std::string& name = c < C ? cols[c] : vcols[c - C].first;
         auto it = bcol.find(name);
         if (it != bcol.end()) bc[c] = (int32_t)it->second;
-        const int64_t vp = vocab_pos(name);
+        const int64_t vp = vocab_find(name);
         if (vp >= 0) attr_of[c] = (uint32_t)vp;
     }
     std::vector<uint32_t> battr(b->n_columns, MXP_VM_DONE);  // vocabulary position of each batch column
     for (uint32_t c = 0; c < b->n_columns; c++) {
-        const int64_t vp = vocab_pos(b->column_names[c]);
+        const int64_t vp = vocab_find(b->column_names[c]);
         if (vp >= 0) battr[c] = (uint32_t)vp;
     }
     // the rules of each composite (A, B) pair with their K1 strings (aliases included)
@@ -170,9 +170,9 @@ int mxp_engine::refs_assemble(const mxp_bag_batch* b, const std::vector<mxp_ref_
         if (it != bcol.end()) id_col = (int32_t)it->second;
         auto pt = bcol.find(kProtocolAttr);
         if (pt != bcol.end()) proto_col = (int32_t)pt->second;
-        const int64_t vi = vocab_pos(RC.identity);
+        const int64_t vi = vocab_find(RC.identity);
         if (vi >= 0) id_attr = (uint32_t)vi;
-        const int64_t vp = vocab_pos(kProtocolAttr);
+        const int64_t vp = vocab_find(kProtocolAttr);
         if (vp >= 0) proto_attr = (uint32_t)vp;
     }
     // records bucketed by request

@@ -78,6 +78,10 @@ int mxp_resolver_set(mxp_engine* eng, const char* identity_attr, const char* def
     mxp_engine::ResolverConf R;
     R.identity = identity_attr;
     R.default_ns = default_ns;
+    // the attributes every Resolve reads get their vocabulary positions now (the finder is asked
+    // here, at snapshot time, never on the evaluation path: refs.cpp uses vocab_find)
+    (void)eng->vocab_pos(R.identity);
+    (void)eng->vocab_pos("context.protocol");
     R.vmask.assign(variety_mask, variety_mask + n);
     R.tcp.assign(is_tcp, is_tcp + n);
     R.empty.assign(empty_match, empty_match + n);

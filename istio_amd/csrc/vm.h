@@ -120,7 +120,8 @@ typedef struct mxp_index {
     uint32_t hmask2;   // composite table: pairs of entries {K2 word 0 | K2 string id, tag, start,
                        // len | min(|K2|, 255) << 24}, {K1 lo, K1 hi, K2 words 1, 2}: keys of <= 12 bytes inline
     uint32_t hoff2;
-    uint32_t pad[5];
+    uint32_t hslot;    // prefix / composite: the probed column's row in kargs.heads (MXP_VM_DONE: none)
+    uint32_t pad[4];
 } mxp_index;           // 64 B
 
 // index kinds.  Composite: rules `A == K1 && B.startsWith(K2) && ...` (vmopt.h SecondAtom), keyed by

@@ -292,6 +292,10 @@ bool hoist_continuation(const std::vector<mxp_vm_ins>& code, uint32_t pc0, Hoist
     for (const auto& i : out->code) used |= reads(i) | writes(i);
     uint32_t next = 0;
     while (used >> next) next++;
+    // the index kernels run templates in MXP_VM_MAXREG registers: a continuation that touches a
+    // register past them (a deep rule, lower.cpp colouring onto MXP_VM_DEEPREG) is not templated, so
+    // it never enters the index and keeps the deep kernels
+    if (next > MXP_VM_MAXREG) return false;
     out->creg0 = next;
     for (auto& i : out->code) {
         const uint8_t wake = i.op & MXP_VM_WAKE;

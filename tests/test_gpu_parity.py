@@ -601,3 +601,27 @@ def test_extern_kats_on_gpu(mxp):
             assert code == int(c["want"]), c
         else:  # ip(x) == ip(x), timestamp(x) == timestamp(x) of a valid x
             assert code == 1, c
+
+
+@pytest.mark.parametrize("knobs", [{}, {"MXP_DTP": "0"}, {"MXP_DEBUG_FLAGS": "8"}])
+def test_deep_continuation_guard_parity(mxp, knobs, monkeypatch):
+    """Guard-led rules whose constant-free continuation needs more than MXP_VM_MAXREG registers
+    (they must stay out of the guard index and the fill groups, and run in the deep
+    kernels), mixed with shallow indexed rules in the same groups, deferred pairs on and off."""
+    from test_product_compile import deep_continuation_rules
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    rules = deep_continuation_rules(64) + ['as == "x%d" && bs == "b%d"' % (i % 40, i % 3) for i in range(100)]
+    bags = W.fuzz_bags(1500, seed=31, p_missing=0.02, p_wrong=0.01)
+    rng = np.random.default_rng(32)
+    for b in bags:
+        if rng.random() < 0.6:
+            b["as"] = "x%d" % rng.integers(0, 70)
+            b["bs"] = "b%d" % rng.integers(0, 3)
+    batch = BagBatch.from_bags(bags, names=list(W.DEFAULT_TEST_MANIFEST))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
+    assert (eng.compile(rules) == 0).all()
+    ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
+    got, want = compare(eng, ev, rules, batch)
+    assert (want[:, :64] == 1).sum() > 100 and (want[:, 72:] == 1).sum() > 100

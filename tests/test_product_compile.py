@@ -143,3 +143,27 @@ def test_heap_panic_after_extern_in_oracle():
     chain = " || ".join('as == "x%d"' % i for i in range(70))
     assert ev.eval_predicate(chain, batch, 1) == ("error", "heap overflow")
     assert ev.eval_predicate(chain, batch, 2) == ("ok", True)
+
+
+def deep_continuation_rules(n=64):
+    """`as == K && <constant-free continuation with more than 8 values live>`: guard-led rules whose
+    continuation needs the deep kernels' registers (such a continuation must never become
+    an index template, whose kernels have MXP_VM_MAXREG registers)."""
+    deep = "(" + "bb == (" * 12 + "bb" + ")" * 12 + ")"
+    return ['as == "x%d" && %s' % (i, deep) for i in range(n)] + ['as == "y%d" && bs == "b" && %s' % (i, deep)
+                                                                    for i in range(8)]
+
+
+def test_deep_continuations_are_not_indexed(Engine):
+    e = Engine(-1)
+    e.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
+    rules = deep_continuation_rules()
+    assert (e.compile(rules) == 0).all()
+    info = e.ruleset_info()
+    assert info["guarded"] == len(rules)
+    assert info["templated"] == 0 and info["indexed"] == 0, info
+    # a shallow continuation of the same shape is still templated and indexed
+    s = Engine(-1)
+    s.set_vocabulary(W.DEFAULT_TEST_MANIFEST)
+    assert (s.compile(['as == "x%d" && (bb == (bb == bb))' % i for i in range(64)]) == 0).all()
+    assert s.ruleset_info()["indexed"] == 64
