@@ -240,6 +240,10 @@ uint64_t mxp_list_entries(const mxp_list* list);
 void mxp_list_regex_parts(const mxp_list* list, uint32_t out[2]);
 int mxp_list_check(mxp_engine* eng, const mxp_list* list, int blacklist, const uint8_t* sym_bytes,
                    const uint64_t* sym_offsets, uint32_t n, int32_t* codes);
+/* strings.ToUpper (Go 1.9: strings.Map(unicode.ToUpper, s), Unicode 9.0.0 simple uppercase) as the
+ * case-insensitive lists apply it to entries and symbols (stringList.go:59,66,79): writes
+ * min(cap, length) bytes of the result to out and its length to *out_len.  Host only, no engine. */
+int mxp_go_to_upper(const uint8_t* s, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len);
 /* Device-resident variant: symbols already in device memory (blob with >= 16 bytes of readable
  * slack after the last symbol), codes written to device memory, enqueued on `stream`. */
 int mxp_list_check_device(mxp_engine* eng, const mxp_list* list, int blacklist, const uint8_t* d_sym_bytes,

@@ -19,7 +19,7 @@ ARCH = os.environ.get("MXP_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["goutil.cpp", "frontend.cpp", "ilgen.cpp", "lower.cpp", "vmopt.cpp", "regex.cpp", "engine.cpp",
            "resolver.cpp", "refs.cpp", "wire.cpp", "lists.cpp", "quota.cpp", "pack_device.cpp", "kernels.hip", "resolve.hip", "lists.hip", "quota.hip", "pack.hip"]
-HEADERS = ["goutil.h", "frontend.h", "ilgen.h", "lower.h", "vmopt.h", "vm.h", "kargs.h", "engine_impl.h", "resolve_args.h", "netparse.h", "timeparse.h", "lists.h", "regex.h", "unicode_tables.h", "dfa_dev.h", "quota_args.h", "pack_args.h", "par.h"]
+HEADERS = ["goutil.h", "frontend.h", "ilgen.h", "lower.h", "vmopt.h", "vm.h", "kargs.h", "engine_impl.h", "resolve_args.h", "netparse.h", "timeparse.h", "lists.h", "regex.h", "unicode_tables.h", "dfa_dev.h", "quota_args.h", "pack_args.h", "par.h", "goupper.h", "upper_table.h"]
 
 
 def _stale():

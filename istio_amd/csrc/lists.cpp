@@ -3,7 +3,8 @@
 // Compilation follows the handler's list builders:
 //   STRINGS / CASE_INSENSITIVE_STRINGS  parseStringList / parseCaseInsensitiveStringList
 //                                       (stringList.go:29-67): a set of the non-empty entries and
-//                                       overrides (upper-cased for the case-insensitive kind);
+//                                       overrides (Go's strings.ToUpper for the case-insensitive
+//                                       kind, goupper.h);
 //   IP_ADDRESSES                        parseIPList / addEntry (ipList.go:35-75): "/32" appended when
 //                                       the entry has no '/', net.ParseCIDR; the IPNets become
 //                                       disjoint sorted address intervals (IPNet.Contains per
@@ -16,6 +17,7 @@
 #include <limits>
 
 #include "engine_impl.h"
+#include "goupper.h"
 #include "lists.h"
 
 extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s);
@@ -37,10 +39,16 @@ struct mxp_list {
 
 namespace {
 
-std::string ascii_upper(const std::string& s) {
-    std::string o = s;
-    for (auto& c : o)
-        if (c >= 'a' && c <= 'z') c = (char)(c - 32);
+const uint32_t kUpperRows[MXP_UPPER_N][3] = {MXP_UPPER_ROWS};
+
+// strings.ToUpper (Go 1.9; goupper.h): the key a case-insensitive list stores and looks up
+std::string go_to_upper(const std::string& s) {
+    std::string o;
+    o.reserve(s.size() + 8);
+    MxpUpperStream st((const uint8_t*)s.data(), (uint32_t)s.size(), kUpperRows);
+    uint64_t w;
+    uint32_t k;
+    while ((k = st.next8(&w)) != 0) o.append((const char*)&w, k);
     return o;
 }
 
@@ -174,7 +182,7 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
         std::vector<std::string> uniq;
         auto add = [&](const std::string& s) {
             if (s.empty()) return;  // empty lines / overrides are skipped
-            std::string k = upper ? ascii_upper(s) : s;
+            std::string k = upper ? go_to_upper(s) : s;
             if (ids.emplace(k, (uint32_t)uniq.size()).second) uniq.push_back(k);
         };
         for (uint32_t i = 0; i < n_entries; i++) add(str(entries[i], entry_lens[i]));
@@ -347,6 +355,14 @@ void mxp_list_destroy(mxp_engine* eng, mxp_list* list) {
 }
 
 uint64_t mxp_list_entries(const mxp_list* list) { return list ? list->n_entries : 0; }
+
+int mxp_go_to_upper(const uint8_t* s, uint64_t n, uint8_t* out, uint64_t cap, uint64_t* out_len) {
+    if ((n && !s) || (cap && !out) || !out_len || n >= (1ull << 32)) return MXP_ERR_ARG;
+    const std::string u = go_to_upper(std::string((const char*)s, (size_t)n));
+    if (cap) memcpy(out, u.data(), std::min<uint64_t>(cap, u.size()));
+    *out_len = u.size();
+    return MXP_OK;
+}
 
 void mxp_list_regex_parts(const mxp_list* list, uint32_t out[2]) {
     out[0] = list ? list->rx_n : 0;

@@ -57,7 +57,8 @@ typedef struct mxp_list_args {
 
 #define MXP_LISTENTRY_NOT_STRING (-2)
 
-// ASCII upper-casing of 8 packed bytes (bytes >= 0x80 untouched): strings.ToUpper's ASCII path
+// ASCII upper-casing of 8 packed bytes (bytes >= 0x80 untouched): strings.ToUpper of ASCII-only
+// strings (any other string takes goupper.h's per-rune stream)
 MXP_NHD uint64_t mxp_upper8(uint64_t x) {
     const uint64_t h = x & 0x7F7F7F7F7F7F7F7Full;
     const uint64_t ge_a = h + 0x1F1F1F1F1F1F1F1Full;  // high bit set where byte >= 'a'

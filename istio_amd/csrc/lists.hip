@@ -2,8 +2,9 @@
 //
 // One symbol per lane.  HandleListEntry (mixer/adapter/list/list.go:68-101) on each:
 //   string lists   hash the symbol 8 bytes at a time (ASCII upper-cased on the fly for the
-//                  case-insensitive kind, strings.ToUpper's ASCII path), probe the open-addressing
-//                  table, compare bytes on a hash hit (stringList.go:73-80);
+//                  case-insensitive kind; a symbol with bytes >= 0x80 takes Go's strings.ToUpper
+//                  per rune, goupper.h), probe the open-addressing table, compare bytes on a hash
+//                  hit (stringList.go:73-80);
 //   regex lists    one DFA for the union of the patterns (regexList.go:26-33: first match wins,
 //                  and only "found" is reported), stepped rune by rune (dfa_dev.h);
 //   IP lists       net.ParseIP on the symbol (netparse.h, the same code the host uses), then a
@@ -14,6 +15,7 @@
 #include <stdint.h>
 
 #include "../../include/mxp.h"
+#include "goupper.h"
 #include "lists.h"
 #include "vm.h"
 
@@ -25,13 +27,11 @@ __device__ __forceinline__ uint64_t tail_mask(uint32_t rem) {
     return rem >= 8 ? ~0ull : ((1ull << (rem * 8u)) - 1ull);
 }
 
-__device__ bool string_member(const mxp_list_args& A, const uint8_t* s, uint32_t n, bool upper) {
-    uint64_t h = 0;
-    for (uint32_t i = 0; i < n; i += 8) {
-        uint64_t w = ld8u(s + i) & tail_mask(n - i);
-        h = mxp_hash_step(h, upper ? mxp_upper8(w) : w);
-    }
-    h = mxp_hash_final(h, n);
+__constant__ uint32_t kUpperRows[MXP_UPPER_N][3] = {MXP_UPPER_ROWS};
+
+// probe the entry table for a key given by its hash and length; `same(e)` compares the entry bytes
+template <class Same>
+__device__ __forceinline__ bool string_probe(const mxp_list_args& A, uint64_t h, uint32_t n, Same same) {
     const uint32_t tag = (uint32_t)(h >> 32);
     for (uint32_t slot = (uint32_t)h & A.hmask;; slot = (slot + 1) & A.hmask) {
         const uint64_t t = A.htab[slot];
@@ -39,7 +39,42 @@ __device__ bool string_member(const mxp_list_args& A, const uint8_t* s, uint32_t
         if ((uint32_t)(t >> 32) != tag) continue;
         const uint64_t d = A.ent_desc[(uint32_t)t];
         if ((uint32_t)(d & 0xFFFFFFu) != n) continue;
-        const uint8_t* e = A.ent_pool + (d >> 24);
+        if (same(A.ent_pool + (d >> 24))) return true;
+    }
+}
+
+// a case-insensitive symbol with bytes >= 0x80: the key is Go's strings.ToUpper of it (goupper.h),
+// streamed twice -- once into the hash, once against a candidate entry's bytes
+__device__ __forceinline__ bool string_member_go(const mxp_list_args& A, const uint8_t* s, uint32_t n) {
+    MxpUpperStream st(s, n, kUpperRows);
+    uint64_t h = 0, w;
+    uint32_t len = 0, k;
+    while ((k = st.next8(&w)) != 0) {
+        h = mxp_hash_step(h, w);
+        len += k;
+    }
+    h = mxp_hash_final(h, len);
+    return string_probe(A, h, len, [&](const uint8_t* e) {
+        MxpUpperStream again(s, n, kUpperRows);
+        uint64_t x;
+        uint32_t m;
+        for (uint32_t i = 0; (m = again.next8(&x)) != 0; i += 8)
+            if (x != (ld8u(e + i) & tail_mask(m))) return false;
+        return true;
+    });
+}
+
+__device__ bool string_member(const mxp_list_args& A, const uint8_t* s, uint32_t n, bool upper) {
+    uint64_t h = 0, hi = 0;
+    for (uint32_t i = 0; i < n; i += 8) {
+        uint64_t w = ld8u(s + i) & tail_mask(n - i);
+        hi |= w;
+        h = mxp_hash_step(h, upper ? mxp_upper8(w) : w);
+    }
+    // strings.ToUpper's per-rune path (non-ASCII runes, invalid bytes)
+    if (upper && (hi & 0x8080808080808080ull)) return string_member_go(A, s, n);
+    h = mxp_hash_final(h, n);
+    return string_probe(A, h, n, [&](const uint8_t* e) {
         bool eq = true;
         for (uint32_t i = 0; i < n && eq; i += 8) {
             const uint64_t m = tail_mask(n - i);
@@ -47,8 +82,8 @@ __device__ bool string_member(const mxp_list_args& A, const uint8_t* s, uint32_t
             if (upper) w = mxp_upper8(w);
             eq = w == (ld8u(e + i) & m);
         }
-        if (eq) return true;
-    }
+        return eq;
+    });
 }
 
 // index of the last interval starting at or below x (or -1)

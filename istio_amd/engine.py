@@ -97,6 +97,8 @@ SIGNATURES = {
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "mxp_ruleset_columns": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32]),
     "mxp_debug_wave_times": (ctypes.c_int, [_VP, _VP, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    "mxp_go_to_upper": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, _VP, ctypes.c_uint64,
+                                       ctypes.POINTER(ctypes.c_uint64)]),
 }
 
 _LIB = None
@@ -123,6 +125,18 @@ def load_library(path: str = LIB_PATH):
             f.argtypes = args
         _LIB = lib
     return _LIB
+
+
+def go_to_upper(s: bytes) -> bytes:
+    """strings.ToUpper as the case-insensitive lists apply it (mxp_go_to_upper; stringList.go:59,66,79)."""
+    lib = load_library()
+    n = ctypes.c_uint64(0)
+    cap = 3 * len(s) + 8  # a rune grows to at most 3x its bytes (an invalid byte -> EF BF BD)
+    out = ctypes.create_string_buffer(cap)
+    rc = lib.mxp_go_to_upper(s, len(s), out, cap, ctypes.byref(n))
+    if rc != 0:
+        raise MxpError("mxp_go_to_upper failed (%d)" % rc)
+    return out.raw[:n.value]
 
 
 # referenced-attribute conditions (include/mxp.h mxp_attr_ref)

@@ -657,3 +657,21 @@ def quota_workload(n_keys=1024, n_requests=1_000_000, seed=5, p_free=0.1, p_zero
         keys, amounts, be = keys[idx], amounts[idx], be[idx]
     out = (max_amount, valid, keys, amounts, be)
     return out + (idx,) if return_index else out
+
+
+# pieces of case-insensitive list symbols beyond ASCII (Go 1.9 strings.ToUpper, goupper.h): case
+# pairs, runes with no simple uppercase (ß, ŉ, Georgian in 9.0), runes whose capital is ASCII (ı, ſ),
+# titlecase digraphs, Greek with iota subscripts, astral scripts, and invalid UTF-8 bytes
+CI_PIECES = ["a", "B", "z", "é", "É", "ß", "ı", "I", "İ", "ſ", "s", "S", "ǅ", "ǆ", "Ǆ", "ᾀ", "ᾈ", "ω", "Ω",
+             "σ", "ς", "Σ", "ა", "ꭓ", "Ꭓ", "\U0001e922", "\U0001e900", "\udcff", "\udcc3", "\udca9", "\udce2\udc82",
+             "0", "-", "ÿ", "Ÿ", "µ", "Μ"]
+
+
+def ci_unicode_list(n_entries=3000, n_lookups=20000, seed=41):
+    """Case-insensitive list entries and lookups mixing ASCII, non-ASCII and invalid UTF-8 (str with
+    surrogate escapes for raw bytes)."""
+    rng = np.random.default_rng(seed)
+
+    def word(lo, hi):
+        return "".join(CI_PIECES[i] for i in rng.integers(0, len(CI_PIECES), int(rng.integers(lo, hi))))
+    return [word(1, 5) for _ in range(n_entries)], [word(0, 5) for _ in range(n_lookups)]

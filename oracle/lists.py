@@ -10,10 +10,14 @@
                                                  entry fails the list, bad overrides are ignored
   checkList (IP)             ipList.go:77-92    net.ParseIP, linear IPNet.Contains scan (C, lists_oracle.c)
 
-strings.ToUpper (Go 1.9 src/strings/strings.go): ASCII-only strings take the byte path restated
-here exactly; strings with non-ASCII bytes go through unicode.ToUpper per rune -- approximated with
-Python's single-character upper() and U+FFFD for invalid UTF-8: PARITY UNPINNED (no reference
-fixture covers it; the tests keep to ASCII).
+strings.ToUpper (Go 1.9 src/strings/strings.go: Map(unicode.ToUpper, s)) is restated rune by rune:
+Go's range-loop UTF-8 decoding (an invalid byte is U+FFFD of width 1), the input's own bytes until
+the first rune whose upper case differs, utf8.EncodeRune of every rune from there on (so a later
+invalid byte becomes EF BF BD).  unicode.ToUpper above ASCII is the Unicode 9.0 simple uppercase
+mapping of oracle/unicode_upper.json (tools/gen_oracle_upper.py: UnicodeData field 12 per code point
+through Perl's charinfo, cut to runes and capitals assigned by 9.0 -- derived independently of the
+engine's range table).  PARITY UNPINNED beyond the known answers in tests/test_go_upper.py: no
+reference fixture has non-ASCII case-insensitive entries (list_test.go:286-342 is ASCII).
 """
 from __future__ import annotations
 
@@ -29,14 +33,63 @@ def _b(x):
     return x.encode("utf-8", "surrogateescape") if isinstance(x, str) else bytes(x)
 
 
+_UPPER = None
+
+
+def go_upper_rune(r: int) -> int:
+    """unicode.ToUpper (Go 1.9 src/unicode/letter.go:224-232)."""
+    global _UPPER
+    if r < 0x80:
+        return r - 32 if 0x61 <= r <= 0x7A else r
+    if _UPPER is None:
+        import json
+        import os
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "unicode_upper.json")) as f:
+            _UPPER = {a: b for a, b in json.load(f)["pairs"]}
+    return _UPPER.get(r, r)
+
+
+def go_decode_rune(s: bytes, i: int):
+    """utf8.DecodeRuneInString(s[i:]) (Go 1.9 src/unicode/utf8/utf8.go:199-245): (rune, width);
+    invalid or truncated -> (U+FFFD, 1)."""
+    c0 = s[i]
+    if c0 < 0x80:
+        return c0, 1
+    n = len(s) - i
+    if 0xC2 <= c0 <= 0xDF:
+        if n >= 2 and 0x80 <= s[i + 1] <= 0xBF:
+            return (c0 & 0x1F) << 6 | (s[i + 1] & 0x3F), 2
+    elif 0xE0 <= c0 <= 0xEF:
+        lo = 0xA0 if c0 == 0xE0 else 0x80
+        hi = 0x9F if c0 == 0xED else 0xBF
+        if n >= 3 and lo <= s[i + 1] <= hi and 0x80 <= s[i + 2] <= 0xBF:
+            return (c0 & 0x0F) << 12 | (s[i + 1] & 0x3F) << 6 | (s[i + 2] & 0x3F), 3
+    elif 0xF0 <= c0 <= 0xF4:
+        lo = 0x90 if c0 == 0xF0 else 0x80
+        hi = 0x8F if c0 == 0xF4 else 0xBF
+        if n >= 4 and lo <= s[i + 1] <= hi and 0x80 <= s[i + 2] <= 0xBF and 0x80 <= s[i + 3] <= 0xBF:
+            return (c0 & 0x07) << 18 | (s[i + 1] & 0x3F) << 12 | (s[i + 2] & 0x3F) << 6 | (s[i + 3] & 0x3F), 4
+    return 0xFFFD, 1
+
+
 def go_to_upper(s: bytes) -> bytes:
-    if all(c < 0x80 for c in s):
-        return bytes(c - 32 if 0x61 <= c <= 0x7A else c for c in s)
-    out = []
-    for ch in s.decode("utf-8", "replace"):  # invalid bytes -> U+FFFD (strings.Map)
-        u = ch.upper()
-        out.append(u if len(u) == 1 else ch)
-    return "".join(out).encode("utf-8")
+    """strings.ToUpper = strings.Map(unicode.ToUpper, s) (Go 1.9 src/strings/strings.go:398-433,
+    :541): b stays nil (the input is returned) while every rune maps to itself; at the first rune
+    that changes, the bytes before it are copied as they are and every rune from it on is
+    EncodeRune'd."""
+    out = None
+    i = 0
+    while i < len(s):
+        c, w = go_decode_rune(s, i)
+        r = go_upper_rune(c)
+        if out is None:
+            if r == c:
+                i += w
+                continue
+            out = bytearray(s[:i])
+        out += chr(r).encode("utf-8", "surrogatepass")
+        i += w
+    return bytes(s) if out is None else bytes(out)
 
 
 class StringList:

@@ -179,3 +179,50 @@ def test_listentry_fused(eng, case):
     assert (len(errq) > 0) == (case != "regex-path") and (got >= 0).sum() > batch.n // 2  # `|` never fails
     for q in errq[:50]:
         assert inst.pair_error(q, 1) == ev.eval(expr, batch, q)[1]
+
+
+@pytest.mark.parametrize("blacklist", [False, True])
+def test_case_insensitive_unicode_parity(eng, blacklist):
+    """Case-insensitive lists with non-ASCII and invalid-UTF-8 entries and symbols: Go 1.9's
+    strings.ToUpper on both sides (stringList.go:59,66,79; goupper.h on the host and in the kernel)
+    against the oracle's restatement -- codes per symbol and numEntries (entries that upper-case to
+    one key count once)."""
+    entries, syms = W.ci_unicode_list(n_entries=3000, n_lookups=40000, seed=41)
+    lst = eng.list_create(L.CASE_INSENSITIVE_STRINGS, entries[:2500] + [""], entries[2500:])
+    ref = L.StringList(entries[:2500] + [""], entries[2500:], case_insensitive=True)
+    assert lst.num_entries() == ref.num_entries() < len(set(entries))
+    want = L.codes(ref.found(syms), blacklist)
+    got = lst.check(syms, blacklist)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(syms[i].encode("utf-8", "surrogateescape"), int(got[i]), int(want[i])) for i in bad[:5]]
+    hit = 7 if blacklist else 0
+    assert (want == hit).sum() > 5000 and (want != hit).sum() > 5000
+    # symbols that only match through a non-ASCII mapping ("é" -> "É", "ı" -> "I", "ſ" -> "S")
+    assert list(lst.check(["été", "pın", "ſa"], blacklist)) == list(L.codes(ref.found(["été", "pın", "ſa"]), blacklist))
+
+
+def test_listentry_fused_unicode(eng):
+    """The fused listentry path (symbols read from the engine's string pools) on non-ASCII and
+    invalid-UTF-8 values, case-insensitive list."""
+    import oracle
+    import istio_amd.engine as mxp
+    from istio_amd.bags import BagBatch
+    entries, syms = W.ci_unicode_list(n_entries=1500, n_lookups=6000, seed=43)
+    rng = np.random.default_rng(44)
+    bags = [{"request.path": s} if rng.random() < 0.95 else {} for s in syms]
+    manifest = {"request.path": "STRING"}
+    batch = BagBatch.from_bags(bags, names=list(manifest))
+    inst = mxp.Engine(0)
+    inst.set_vocabulary(manifest)
+    assert (inst.compile(["true", "request.path"]) == 0).all()
+    lst = eng.list_create(L.CASE_INSENSITIVE_STRINGS, entries, [])
+    got = lst.check_entries(inst, batch, 1, False)
+    ev = oracle.OracleEvaluator(manifest)
+    ref = L.StringList(entries, case_insensitive=True)
+    want = np.empty(batch.n, dtype=np.int32)
+    for q in range(batch.n):
+        st, v = ev.eval("request.path", batch, q)
+        want[q] = -1 if st != "ok" else L.codes(ref.found([v]), False)[0]
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(q), int(got[q]), int(want[q])) for q in bad[:5]]
+    assert (want == 0).sum() > 1000 and (want == -1).sum() > 100
