@@ -65,6 +65,8 @@ def parse():
                         "memquota with one combined all-reduce; C3 lists; c5-quota memquota alone")
     p.add_argument("--list-entries", type=int, default=100_000)
     p.add_argument("--e2e-reps", type=int, default=3, help="end-to-end resolve calls timed (median); 0 skips the end-to-end block (profiling sessions)")
+    p.add_argument("--fresh-steps", type=int, default=10,
+                   help="steps of the fresh-batch block (upload + evaluation of a new 1M batch per step); 0 skips it")
     p.add_argument("--error-output", default="compact", choices=["compact", "bitmap"],
                    help="compact: per-request error flags (a Resolve's view); bitmap: the full error bitmap")
     return p.parse_args()
@@ -184,6 +186,76 @@ def timed_loop(step, steps, warmup, world, stream):
     ev_ms = [a.elapsed_time(b) for a, b in evs] if gpu else []
     dev = torch.device("cuda", torch.cuda.current_device()) if gpu else None
     return D.max_over_ranks(elapsed, dev), ev_ms
+
+
+PCIE_PEAK_GBS = 63.0  # PCIe Gen5 x16 host link, spec (MI355X_MICROARCH.md)
+
+
+def batch_h2d_bytes(batch):
+    """Bytes of the host columnar batch mxp_batch_upload copies to the device (Go-owned bags)."""
+    n = sum(k.nbytes for k in batch.kinds) + sum(v.nbytes for v in batch.values)
+    return int(n + batch.str_blob.nbytes + batch.str_offsets.nbytes + batch.time_sec.nbytes + batch.time_nsec.nbytes
+               + batch.map_offsets.nbytes + batch.map_keys.nbytes + batch.map_values.nbytes)
+
+
+def fresh_batches(kind, n_rules, requests_per_gpu, rank, world):
+    """Two further 1M-request batches of the same seeded stream (the shards after this rank's own,
+    as if two more batches of configs[4] arrived): the fresh-batch block alternates them."""
+    from istio_amd import dist as D
+    from istio_amd import workloads as W
+    n_total = requests_per_gpu * world
+    out = []
+    for k in (1, 2):
+        lo, hi = D.shard_bounds(n_total, rank, world)
+        shard = (lo + k * n_total, hi + k * n_total)
+        if kind == "c4":
+            out.append(W.c4_workload(n_rules=n_rules, n_requests=3 * n_total, seed=4, shard=shard)[2])
+        else:
+            out.append(W.c2_workload(n_rules=n_rules, n_requests=3 * n_total, seed=2, shard=shard)[2])
+    return out
+
+
+def fresh_batch_block(eng, batches, evaluate, steps, stream, n_rules, world):
+    """Every step takes a NEW batch from host memory: mxp_batch_upload (H2D copy of the columnar
+    batch, device interning, value-class dictionary, string heads; synchronous) + the evaluation
+    (enqueued; the next upload's copy overlaps it).  The two batches alternate; a step's device
+    batch is freed two steps later (after its evaluation has drained).  PCIe-inclusive."""
+    import numpy as np
+    import torch
+    keep, up_s = [], []
+    h2d = [batch_h2d_bytes(b) for b in batches]
+
+    def one(k):
+        t0 = time.perf_counter()
+        db = eng.upload(batches[k % len(batches)])
+        up_s.append(time.perf_counter() - t0)
+        evaluate(db)
+        keep.append(db)
+        if len(keep) > 2:
+            keep.pop(0).free()
+    for k in range(2):  # warm-up (allocations)
+        one(k)
+    torch.cuda.synchronize()
+    up_s.clear()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        one(k)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    while keep:
+        keep.pop(0).free()
+    N = batches[0].n
+    up = float(np.mean(up_s))
+    bytes_step = float(np.mean([h2d[k % len(batches)] for k in range(steps)]))
+    return {"ms_per_step": dt * 1e3, "upload_ms": up * 1e3, "requests_per_s": world * N / dt,
+            "pairs_per_s": world * N * n_rules / dt, "steps": steps, "h2d_bytes_per_batch": int(bytes_step),
+            "roofline": {"bound": "pcie", "achieved": bytes_step / up / 1e9, "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                         "frac": bytes_step / up / 1e9 / PCIE_PEAK_GBS, "traffic": None,
+                         "kernel": "mxp_batch_upload: H2D copy of the host columnar batch + the device packer "
+                                   "(intern, gather, pool, pre-tables, value-class dictionary, heads); "
+                                   "achieved = batch bytes / upload wall time"},
+            "path": "host columnar batch (a new 1M-request batch every step) -> mxp_batch_upload -> evaluation "
+                    "(compact errors, fused hit counters); wall time per step, PCIe-inclusive"}
 
 
 def shard_workload(kind, n_rules, requests_per_gpu, rank, world):
@@ -551,6 +623,14 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
                         "collective": "one all_reduce(sum) of hits[R] ++ quota_delta[K] per step"}
     hits = ctr.totals()[0]
     out["hits_total"] = int(hits.sum().item())
+    if args.fresh_steps > 0 and not with_quota:
+        def eval_db(dbx):
+            if compact:
+                dbx.eval_compact(d_match.data_ptr(), d_req_err.data_ptr(), scratch_hits.data_ptr(), sh)
+            else:
+                dbx.eval_hits(d_match.data_ptr(), d_err.data_ptr(), scratch_hits.data_ptr(), sh)
+        out["fresh_batch"] = fresh_batch_block(eng, fresh_batches(kind, args.rules, args.requests, rank, world),
+                                               eval_db, args.fresh_steps, stream, R, world)
     if args.e2e_reps > 0:
         out["end_to_end"] = end_to_end(eng, batch, R, args.e2e_reps)
     if rank == 0 and not args.no_cpu_baseline and world == 1:
@@ -597,7 +677,7 @@ def main():
     kind = "c4" if args.workload == "c4" else "c2"
     out = predicate_bench(args, kind, rank, world, local, with_quota=args.workload == "c5")
     keys = ("metric", "value", "unit", "ms_per_step", "eval_ms", "kernels_ms", "deferred_pairs", "pack_upload_s",
-            "end_to_end", "config", "roofline", "lds_bank_conflicts", "quota", "cpu_baseline")
+            "fresh_batch", "end_to_end", "config", "roofline", "lds_bank_conflicts", "quota", "cpu_baseline")
     if args.workload == "c2" and not args.no_c4:
         # the representative config BASELINE.json quotes at 10k rules (configs[3]), driver-timed too
         c4 = predicate_bench(args, "c4", rank, world, local)

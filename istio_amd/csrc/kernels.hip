@@ -1263,7 +1263,7 @@ struct DtpQueue {
     }
 };
 
-template <bool kLds>
+template <bool kLds, uint32_t NVT = 0>
 __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* F, uint32_t chunk, uint32_t qw,
                                             const uint2* S, const uint32_t* RW) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1326,7 +1326,31 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
             for (uint32_t r = 0; r < 4; r++)
                 if (e[r] && q0 + r < Q1) log_guard_errors(A, e[r], G * 32u, q0 + r);
         const uint32_t i0 = __builtin_amdgcn_readlane(GO, g) - e0, i1 = __builtin_amdgcn_readlane(GO, g + 1) - e0;
-        if constexpr (kLds) {
+        if constexpr (kLds && NVT > 0) {
+            // staged, NVT active slots known at compile time: every slot's four gathers are issued
+            // back to back with no branch between them (a slot the group does not name reads row 0
+            // -- in bounds, classes < 4096 -- and is masked off), so a group waits on its LDS loads
+            // once instead of once per slot
+            const uint32_t gm = __builtin_amdgcn_readlane(GM, g);
+            const uint4 ra = *(const uint4*)(RW + g * MXP_VT_MAX), rb = *(const uint4*)(RW + g * MXP_VT_MAX + 4u);
+            const uint32_t rows[MXP_VT_MAX] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
+            uint2 w[NVT][4];
+#pragma unroll
+            for (uint32_t a = 0; a < NVT; a++) {
+                const uint64_t c = (uint64_t)clv[2u * a] | (uint64_t)clv[2u * a + 1u] << 32;
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++) w[a][r] = S[rows[a] + ((uint32_t)(c >> (16u * r)) & 0xFFFFu)];
+            }
+#pragma unroll
+            for (uint32_t a = 0; a < NVT; a++) {
+                const uint32_t sel = (gm >> a) & 1u ? ~0u : 0u;
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++) {
+                    m[r] |= w[a][r].x & sel;
+                    ve[r] |= w[a][r].y & sel;
+                }
+            }
+        } else if constexpr (kLds) {
             // staged (<= 128 entries): the group's entries in slot order, one per slot it names --
             // unrolled over the slots so each one's classes come from fixed registers (no indexed
             // register move) and its row from one readlane
@@ -1493,7 +1517,11 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A)
 // faster than 96 VGPRs forced to 5: C4 1.715 vs 1.78 ms, profiles/r2_v14_ablibs_vtfill_occ_c4.log).
 #define MXP_VTF_STAGE 4096u
 #define MXP_VTF_TILES 4u
-extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_kargs A) {
+// NVT > 0: the instantiation for batches with exactly NVT value-class columns (mxp_vtfill_lds<NVT>_kernel:
+// each has its own register allocation, so the wide branch-free gathers of NVT = 8 do not cost the
+// NVT = 5 kernel its occupancy)
+template <uint32_t NVT>
+__device__ __forceinline__ void vtfill_lds_body(const mxp_kargs& A) {
     __shared__ uint2 S[MXP_VTF_STAGE];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
     const mxp_fill* F = A.fills + blockIdx.y;
@@ -1537,6 +1565,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
             PL[3u * tid + 2u] = capl;
         }
         __syncthreads();
+        for (uint32_t i = tid; i < n * MXP_VT_MAX; i += 256u) RW[i] = 0u;  // (unnamed slots: row 0, masked)
+        __syncthreads();
         if (tid < n) {  // thread t: group t's entries
             const uint32_t i1 = A.gvt_off[g0 + tid + 1u];
             for (uint32_t i = A.gvt_off[g0 + tid]; i < i1; i++) {
@@ -1549,11 +1579,24 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
     for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
         const uint32_t qw = A.q0 + ((blockIdx.x * MXP_VTF_TILES + t) * 4u + wave) * 256u;
         if (staged)
-            vtfill_wave<true>(A, F, A.dtp_cbase + blockIdx.y, qw, S, RW);
+            vtfill_wave<true, NVT>(A, F, A.dtp_cbase + blockIdx.y, qw, S, RW);
         else
             vtfill_wave<false>(A, F, A.dtp_cbase + blockIdx.y, qw, nullptr, nullptr);
     }
 }
+
+extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_kargs A) { vtfill_lds_body<0>(A); }
+#define MXP_VTFILL_NVT(K) \
+    extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds##K##_kernel(mxp_kargs A) { vtfill_lds_body<K>(A); }
+MXP_VTFILL_NVT(1)
+MXP_VTFILL_NVT(2)
+MXP_VTFILL_NVT(3)
+MXP_VTFILL_NVT(4)
+MXP_VTFILL_NVT(5)
+MXP_VTFILL_NVT(6)
+MXP_VTFILL_NVT(7)
+MXP_VTFILL_NVT(8)
+#undef MXP_VTFILL_NVT
 
 // Deferred pairs, filed for the fill (kargs.dtp_*).  One workgroup per tile of 1024 requests (16
 // index waves) files the tile's recorded pairs by (value-class fill chunk, lane quad = request / 4)
@@ -2338,8 +2381,24 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
         hipLaunchKernelGGL(mxp_vtfill_kernel, dim3((args->q1 - args->q0 + 1023u) / 1024u, n_fills), dim3(256), 0, s, *args);
     } else {
         const uint32_t per = 1024u * MXP_VTF_TILES;
-        hipLaunchKernelGGL(mxp_vtfill_lds_kernel, dim3((args->q1 - args->q0 + per - 1u) / per, n_fills), dim3(256), 0, s,
-                           *args);
+        const dim3 grid((args->q1 - args->q0 + per - 1u) / per, n_fills);
+        // the instantiation for this batch's active value-class columns (flag 33554432: the generic
+        // kernel, one branch per slot -- A/B)
+        void (*k)(mxp_kargs) = mxp_vtfill_lds_kernel;
+        if (!(args->flags & 33554432u)) {
+            switch (args->n_vt) {
+            case 1: k = mxp_vtfill_lds1_kernel; break;
+            case 2: k = mxp_vtfill_lds2_kernel; break;
+            case 3: k = mxp_vtfill_lds3_kernel; break;
+            case 4: k = mxp_vtfill_lds4_kernel; break;
+            case 5: k = mxp_vtfill_lds5_kernel; break;
+            case 6: k = mxp_vtfill_lds6_kernel; break;
+            case 7: k = mxp_vtfill_lds7_kernel; break;
+            case 8: k = mxp_vtfill_lds8_kernel; break;
+            default: break;
+            }
+        }
+        hipLaunchKernelGGL(k, grid, dim3(256), 0, s, *args);
     }
     return hipGetLastError();
 }

@@ -238,22 +238,51 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_copy_kernel(mxp_pack_
     }
 }
 
-// value classes: distinct string ids (bitmap over [0, S]) and other kinds of each candidate column
+// value classes: distinct string ids (bitmap over [0, S]) and other kinds of each candidate column.
+// Zipf-hot values put most requests on a few bitmap words, so a request only reaches the global
+// bitmap when nothing cheaper has seen its id: a per-workgroup LDS table of recently marked ids
+// (direct-mapped; racy stores only cost a redundant mark), then a plain load of the word (a set bit
+// is final, so a stale copy only costs a redundant atomic), then up to four rounds of in-wave dedup
+// (the first needing lane's id, readfirstlane + ballot) before the remaining lanes' atomicOr.
+#define MXP_VT_MARK_LDS 2048u
 extern "C" __global__ __launch_bounds__(256) void mxp_pack_vt_mark_kernel(mxp_pack_args A) {
+    __shared__ uint32_t seen[MXP_VT_MARK_LDS];
     const uint32_t a = blockIdx.y;
     const uint32_t c = A.vt_col[a];
     unsigned long long* bits = A.vt_bits + (uint64_t)a * (A.S / 64 + 1);
+    for (uint32_t i = threadIdx.x; i < MXP_VT_MARK_LDS; i += 256u) seen[i] = 0xFFFFFFFFu;
+    __syncthreads();
     uint32_t km = 0;
-    for (uint64_t r = gtid(); r < A.n; r += gstride()) {
-        const uint8_t k = A.kinds[(uint64_t)c * A.n + r];
-        if (k == 1u) {
-            const uint64_t x = A.vals[(uint64_t)c * A.n + r] < A.S ? A.vals[(uint64_t)c * A.n + r] : A.S;
-            const unsigned long long bit = 1ull << (x & 63u);
-            if (!(__hip_atomic_load(bits + (x >> 6), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
-                atomicOr(bits + (x >> 6), bit);
-        } else {
-            km |= 1u << (k & 31u);
+    // (uniform trip count per wave: the ballots below need every lane)
+    const uint64_t stride = gstride();
+    for (uint64_t r0 = gtid() & ~63ull; r0 < A.n; r0 += stride) {
+        const uint64_t r = r0 + (threadIdx.x & 63u);
+        bool need = false;
+        uint32_t x = 0;
+        if (r < A.n) {
+            const uint8_t k = A.kinds[(uint64_t)c * A.n + r];
+            if (k == 1u) {
+                const uint64_t v = A.vals[(uint64_t)c * A.n + r];
+                x = (uint32_t)(v < A.S ? v : A.S);
+                const uint32_t slot = (x * 0x9E3779B1u) >> (32 - 11);
+                if (seen[slot] != x) {
+                    seen[slot] = x;
+                    need = !(bits[x >> 6] & (1ull << (x & 63u)));
+                }
+            } else {
+                km |= 1u << (k & 31u);
+            }
         }
+#pragma unroll
+        for (int round = 0; round < 4; round++) {
+            const uint64_t m = __ballot(need);
+            if (!m) break;
+            const uint32_t lead = (uint32_t)__builtin_ctzll(m);
+            const uint32_t x0 = (uint32_t)__shfl((int)x, (int)lead, 64);
+            if ((threadIdx.x & 63u) == lead) atomicOr(bits + (x0 >> 6), 1ull << (x0 & 63u));
+            if (need && x == x0) need = false;
+        }
+        if (need) atomicOr(bits + (x >> 6), 1ull << (x & 63u));
     }
     if (km) atomicOr(A.vt_kmask + a, km);
 }
