@@ -254,11 +254,17 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* list, int blacklist, 
  * against `list` in the same device pass -- no host round trip between the two.  codes[q] = the
  * google.rpc code, or MXP_LISTENTRY_EVAL_ERROR (-1) when Eval failed: the reference returns
  * "failed to evaluate field 'Value' for instance '<name>': " + mxp_pair_error(q, value_rule).
+ * values (nullable): each request's Value as a result register of rule value_rule, for
+ * mxp_value_text -- the symbol HandleListEntry's status messages print ("%s is not whitelisted",
+ * "%s is blacklisted", "%s is not a valid IP address").
  * Every rule of the engine is evaluated (Eval mode), so instance expressions belong in an engine
  * of their own. */
 #define MXP_LISTENTRY_EVAL_ERROR (-1)
+/* an interface-typed Value that is not a string: the reference's `ValueInterface.(string)`
+ * (template.gen.go:2177) panics */
+#define MXP_LISTENTRY_NOT_STRING (-2)
 int mxp_listentry_check(mxp_engine* eng, const mxp_list* list, int blacklist, const mxp_bag_batch* batch,
-                        uint32_t value_rule, int32_t* codes);
+                        uint32_t value_rule, int32_t* codes, uint64_t* values);
 
 /*
  * memquota (mixer/adapter/memquota): batched HandleQuota with the reference's sequential semantics.

@@ -1383,6 +1383,9 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
         A->vt_rep = db->vt_rep.as<uint32_t>();
         A->vt_cnt = db->vt_cnt.as<uint32_t>();
         A->n_vt = (uint32_t)P.vt_cols.size();
+        A->vt_imm = db->vt_meta_h.size() >= (size_t)A->n_vt * 8 ? 1u : 0u;
+        for (uint32_t a = 0; a < A->n_vt && A->vt_imm; a++)
+            if (db->vt_meta_h[a * 8 + MXP_VTM_CAP] != 64u) A->vt_imm = 0u;
     }
 }
 

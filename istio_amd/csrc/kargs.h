@@ -98,6 +98,7 @@ typedef struct mxp_kargs {
     unsigned long long* vt_keys; // class tables: keys (MXP_VT_EMPTY = free) and a representative request
     uint32_t* vt_rep;
     uint32_t n_vt;
+    uint32_t vt_imm;             // every active class table has MXP_VTI_CAP (64) slots: mxp_vtfill_imm<n_vt>_kernel
     uint32_t nfa;                // some regexp of the rule set or batch is a bit-parallel NFA: the *_nfa kernels
     unsigned long long* wave_t;  // profiling (MXP_WAVE_TIMES): index kernel waves' {start, end, XCC, 5 phase marks}
     uint8_t* req_err;            // optional [n]: 1 when some rule fails for the request (compact error output)

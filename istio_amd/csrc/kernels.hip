@@ -1263,7 +1263,7 @@ struct DtpQueue {
     }
 };
 
-template <bool kLds, uint32_t NVT = 0>
+template <bool kLds>
 __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* F, uint32_t chunk, uint32_t qw,
                                             const uint2* S, const uint32_t* RW) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1326,31 +1326,7 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
             for (uint32_t r = 0; r < 4; r++)
                 if (e[r] && q0 + r < Q1) log_guard_errors(A, e[r], G * 32u, q0 + r);
         const uint32_t i0 = __builtin_amdgcn_readlane(GO, g) - e0, i1 = __builtin_amdgcn_readlane(GO, g + 1) - e0;
-        if constexpr (kLds && NVT > 0) {
-            // staged, NVT active slots known at compile time: every slot's four gathers are issued
-            // back to back with no branch between them (a slot the group does not name reads row 0
-            // -- in bounds, classes < 4096 -- and is masked off), so a group waits on its LDS loads
-            // once instead of once per slot
-            const uint32_t gm = __builtin_amdgcn_readlane(GM, g);
-            const uint4 ra = *(const uint4*)(RW + g * MXP_VT_MAX), rb = *(const uint4*)(RW + g * MXP_VT_MAX + 4u);
-            const uint32_t rows[MXP_VT_MAX] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z, rb.w};
-            uint2 w[NVT][4];
-#pragma unroll
-            for (uint32_t a = 0; a < NVT; a++) {
-                const uint64_t c = (uint64_t)clv[2u * a] | (uint64_t)clv[2u * a + 1u] << 32;
-#pragma unroll
-                for (uint32_t r = 0; r < 4; r++) w[a][r] = S[rows[a] + ((uint32_t)(c >> (16u * r)) & 0xFFFFu)];
-            }
-#pragma unroll
-            for (uint32_t a = 0; a < NVT; a++) {
-                const uint32_t sel = (gm >> a) & 1u ? ~0u : 0u;
-#pragma unroll
-                for (uint32_t r = 0; r < 4; r++) {
-                    m[r] |= w[a][r].x & sel;
-                    ve[r] |= w[a][r].y & sel;
-                }
-            }
-        } else if constexpr (kLds) {
+        if constexpr (kLds) {
             // staged (<= 128 entries): the group's entries in slot order, one per slot it names --
             // unrolled over the slots so each one's classes come from fixed registers (no indexed
             // register move) and its row from one readlane
@@ -1517,11 +1493,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A)
 // faster than 96 VGPRs forced to 5: C4 1.715 vs 1.78 ms, profiles/r2_v14_ablibs_vtfill_occ_c4.log).
 #define MXP_VTF_STAGE 4096u
 #define MXP_VTF_TILES 4u
-// NVT > 0: the instantiation for batches with exactly NVT value-class columns (mxp_vtfill_lds<NVT>_kernel:
-// each has its own register allocation, so the wide branch-free gathers of NVT = 8 do not cost the
-// NVT = 5 kernel its occupancy)
-template <uint32_t NVT>
-__device__ __forceinline__ void vtfill_lds_body(const mxp_kargs& A) {
+extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_kargs A) {
     __shared__ uint2 S[MXP_VTF_STAGE];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
     const mxp_fill* F = A.fills + blockIdx.y;
@@ -1565,8 +1537,6 @@ __device__ __forceinline__ void vtfill_lds_body(const mxp_kargs& A) {
             PL[3u * tid + 2u] = capl;
         }
         __syncthreads();
-        for (uint32_t i = tid; i < n * MXP_VT_MAX; i += 256u) RW[i] = 0u;  // (unnamed slots: row 0, masked)
-        __syncthreads();
         if (tid < n) {  // thread t: group t's entries
             const uint32_t i1 = A.gvt_off[g0 + tid + 1u];
             for (uint32_t i = A.gvt_off[g0 + tid]; i < i1; i++) {
@@ -1579,24 +1549,165 @@ __device__ __forceinline__ void vtfill_lds_body(const mxp_kargs& A) {
     for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
         const uint32_t qw = A.q0 + ((blockIdx.x * MXP_VTF_TILES + t) * 4u + wave) * 256u;
         if (staged)
-            vtfill_wave<true, NVT>(A, F, A.dtp_cbase + blockIdx.y, qw, S, RW);
+            vtfill_wave<true>(A, F, A.dtp_cbase + blockIdx.y, qw, S, RW);
         else
             vtfill_wave<false>(A, F, A.dtp_cbase + blockIdx.y, qw, nullptr, nullptr);
     }
 }
 
-extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_kargs A) { vtfill_lds_body<0>(A); }
-#define MXP_VTFILL_NVT(K) \
-    extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds##K##_kernel(mxp_kargs A) { vtfill_lds_body<K>(A); }
-MXP_VTFILL_NVT(1)
-MXP_VTFILL_NVT(2)
-MXP_VTFILL_NVT(3)
-MXP_VTFILL_NVT(4)
-MXP_VTFILL_NVT(5)
-MXP_VTFILL_NVT(6)
-MXP_VTFILL_NVT(7)
-MXP_VTFILL_NVT(8)
-#undef MXP_VTFILL_NVT
+// Value-class fill for batches whose active class tables all have the minimum capacity (64 slots:
+// at most 32 distinct values per column -- C4's header columns).  The workgroup stages, per active
+// slot a and group g of the chunk, the 64 class words of the bitmap word g's rules of slot a take
+// (zero where g names no rule of slot a) at a FIXED place, [a][g][class]: a request's address for
+// slot a is computed once per tile, and group g's word is then a ds_read_b32 with the immediate
+// offset g * 256 -- the group loop is unrolled, so a gather costs one LDS instruction and one OR,
+// against an address add, a 64-bit gather and two ORs in mxp_vtfill_lds_kernel, whose issue rate
+// bounded it (SQ r3: 2.2e8 VALU instructions per C4 evaluation).  Error words stay in global memory:
+// they are gathered (through the staged word positions) only when some class word of the chunk
+// holds an error bit (none in C4), so LDS holds the match words alone.
+#define MXP_VTI_CAP 64u
+template <uint32_t NVT>
+__device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
+    __shared__ uint32_t SM[NVT * MXP_FILL_CHUNK * MXP_VTI_CAP];
+    __shared__ uint32_t SJ[NVT * MXP_FILL_CHUNK];  // word position of (slot, group), ~0: none
+    __shared__ uint32_t eflag;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
+    const mxp_fill* F = A.fills + blockIdx.y;
+    const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
+    const uint32_t chunk = A.dtp_cbase + blockIdx.y;
+    // 1. staging: zero, then each (group, slot) merge entry's 64 class words into its fixed row
+    for (uint32_t i = tid; i < NVT * MXP_FILL_CHUNK * MXP_VTI_CAP; i += 256u) SM[i] = 0u;
+    if (tid < NVT * MXP_FILL_CHUNK) SJ[tid] = ~0u;
+    if (tid == 0) eflag = 0u;
+    __syncthreads();
+    const uint32_t TB = lane < NVT ? A.vt_meta[lane * 8u + MXP_VTM_TBASE] : 0u;
+    uint32_t eor = 0u;
+    for (uint32_t g = 0; g < n; g++) {
+        const uint32_t i0 = uni(A.gvt_off[g0 + g]), i1 = uni(A.gvt_off[g0 + g + 1u]);
+        for (uint32_t x = tid; x < (i1 - i0) * MXP_VTI_CAP; x += 256u) {
+            const uint32_t ent = A.gvt[i0 + x / MXP_VTI_CAP], a = ent >> 24, j = ent & 0xFFFFFFu, k = x % MXP_VTI_CAP;
+            const uint32_t tb = __builtin_amdgcn_ds_bpermute((int)(a << 2), (int)TB);
+            const uint2 w = *(const uint2*)(A.vt_tm + 2u * ((uint64_t)tb + (uint64_t)j * MXP_VTI_CAP + k));
+            SM[(a * MXP_FILL_CHUNK + g) * MXP_VTI_CAP + k] = w.x;
+            if (k == 0) SJ[a * MXP_FILL_CHUNK + g] = j;
+            eor |= w.y;
+        }
+    }
+    if (__ballot(eor != 0u)) {
+        if (lane == 0) atomicOr(&eflag, 1u);
+    }
+    __syncthreads();
+    const bool errs = eflag != 0u;
+    const uint64_t N = A.n;
+    const uint32_t Q1 = A.q1;
+    const bool nt = !(A.flags & 128u);
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    const uint32_t FM = lane < n ? A.fill_masks[moff + lane] : 0u;
+    for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
+        const uint32_t qw = A.q0 + ((blockIdx.x * MXP_VTF_TILES + t) * 4u + wave) * 256u;
+        if (qw >= Q1) break;
+        const uint32_t q0 = qw + lane * 4u;
+        const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0 && (q0 & 3u) == 0;
+        uint32_t bad[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool in = q0 + r < Q1;
+            const uint32_t k = in ? A.kinds[(uint64_t)col * N + q0 + r] : 0u;
+            bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
+        }
+        // each request's row base per slot: [a][g = 0][its class]
+        uint32_t ad[NVT][4];
+#pragma unroll
+        for (uint32_t a = 0; a < NVT; a++) {
+            const uint16_t* C = A.vt_cls + (uint64_t)a * N;
+            uint64_t c = 0;
+            if (vec && q0 < Q1) {
+                c = *(const uint64_t*)(C + q0);
+            } else {
+                for (uint32_t r = 0; r < 4; r++)
+                    if (q0 + r < Q1) c |= (uint64_t)C[q0 + r] << (16u * r);
+            }
+#pragma unroll
+            for (uint32_t r = 0; r < 4; r++)
+                ad[a][r] = a * MXP_FILL_CHUNK * MXP_VTI_CAP + ((uint32_t)(c >> (16u * r)) & (MXP_VTI_CAP - 1u));
+        }
+        const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
+        DtpQueue dq;
+        dq.load(A, chunk, q0, q0 < Q1);
+        const bool dany = __ballot(dq.q0 != ~0u) != 0;
+        uint32_t anyerr[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (uint32_t g = 0; g < MXP_FILL_CHUNK; g++) {
+            if (g >= n) break;
+            const uint32_t G = g0 + g;
+            const uint32_t mask = __builtin_amdgcn_readlane(FM, g);
+            uint32_t m[4] = {0u, 0u, 0u, 0u}, e[4], ve[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int r = 0; r < 4; r++) e[r] = bad[r] & mask;
+            if (A.errlog && any && mask)
+                for (uint32_t r = 0; r < 4; r++)
+                    if (e[r] && q0 + r < Q1) log_guard_errors(A, e[r], G * 32u, q0 + r);
+#pragma unroll
+            for (uint32_t a = 0; a < NVT; a++)
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++) m[r] |= SM[ad[a][r] + g * MXP_VTI_CAP];
+            if (errs) {
+#pragma unroll
+                for (uint32_t a = 0; a < NVT; a++) {
+                    const uint32_t j = SJ[a * MXP_FILL_CHUNK + g];
+                    if (j == ~0u) continue;
+                    const uint64_t row = (uint64_t)__builtin_amdgcn_readlane(TB, a) + (uint64_t)j * MXP_VTI_CAP;
+#pragma unroll
+                    for (uint32_t r = 0; r < 4; r++)
+                        ve[r] |= A.vt_tm[2u * (row + (ad[a][r] & (MXP_VTI_CAP - 1u))) + 1u];
+                }
+                if (A.errlog) {
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) c += q0 + r < Q1 ? (uint32_t)__builtin_popcount(ve[r]) : 0u;
+                    vt_count_n(A, c);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++) e[r] |= ve[r];
+            }
+            if (dany) dq.merge(g, m, e);
+#pragma unroll
+            for (uint32_t r = 0; r < 4; r++) anyerr[r] |= e[r];
+            const uint64_t at = (uint64_t)G * N + q0;
+            if (vec && q0 < Q1) {
+                const v4u mv = v4u{m[0], m[1], m[2], m[3]};
+                const v4u ev = v4u{e[0], e[1], e[2], e[3]};
+                if (nt) {
+                    if (A.out_match) __builtin_nontemporal_store(mv, (v4u*)(A.out_match + at));
+                    if (A.out_err) __builtin_nontemporal_store(ev, (v4u*)(A.out_err + at));
+                } else {
+                    if (A.out_match) *(v4u*)(A.out_match + at) = mv;
+                    if (A.out_err) *(v4u*)(A.out_err + at) = ev;
+                }
+            } else {
+                for (uint32_t r = 0; r < 4; r++) {
+                    if (q0 + r >= Q1) break;
+                    if (A.out_match) A.out_match[at + r] = m[r];
+                    if (A.out_err) A.out_err[at + r] = e[r];
+                }
+            }
+        }
+        if (A.req_err)
+            for (uint32_t r = 0; r < 4; r++)
+                if (anyerr[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;
+    }
+}
+#define MXP_VTFILL_IMM(K) \
+    extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_imm##K##_kernel(mxp_kargs A) { vtfill_imm_body<K>(A); }
+MXP_VTFILL_IMM(1)
+MXP_VTFILL_IMM(2)
+MXP_VTFILL_IMM(3)
+MXP_VTFILL_IMM(4)
+MXP_VTFILL_IMM(5)
+MXP_VTFILL_IMM(6)
+MXP_VTFILL_IMM(7)
+MXP_VTFILL_IMM(8)
+#undef MXP_VTFILL_IMM
 
 // Deferred pairs, filed for the fill (kargs.dtp_*).  One workgroup per tile of 1024 requests (16
 // index waves) files the tile's recorded pairs by (value-class fill chunk, lane quad = request / 4)
@@ -2382,19 +2493,19 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
     } else {
         const uint32_t per = 1024u * MXP_VTF_TILES;
         const dim3 grid((args->q1 - args->q0 + per - 1u) / per, n_fills);
-        // the instantiation for this batch's active value-class columns (flag 33554432: the generic
-        // kernel, one branch per slot -- A/B)
+        // every active class table at 64 slots: the immediate-offset kernel for this many columns
+        // (flag 33554432: mxp_vtfill_lds_kernel -- A/B)
         void (*k)(mxp_kargs) = mxp_vtfill_lds_kernel;
-        if (!(args->flags & 33554432u)) {
+        if (args->vt_imm && !(args->flags & 33554432u)) {
             switch (args->n_vt) {
-            case 1: k = mxp_vtfill_lds1_kernel; break;
-            case 2: k = mxp_vtfill_lds2_kernel; break;
-            case 3: k = mxp_vtfill_lds3_kernel; break;
-            case 4: k = mxp_vtfill_lds4_kernel; break;
-            case 5: k = mxp_vtfill_lds5_kernel; break;
-            case 6: k = mxp_vtfill_lds6_kernel; break;
-            case 7: k = mxp_vtfill_lds7_kernel; break;
-            case 8: k = mxp_vtfill_lds8_kernel; break;
+            case 1: k = mxp_vtfill_imm1_kernel; break;
+            case 2: k = mxp_vtfill_imm2_kernel; break;
+            case 3: k = mxp_vtfill_imm3_kernel; break;
+            case 4: k = mxp_vtfill_imm4_kernel; break;
+            case 5: k = mxp_vtfill_imm5_kernel; break;
+            case 6: k = mxp_vtfill_imm6_kernel; break;
+            case 7: k = mxp_vtfill_imm7_kernel; break;
+            case 8: k = mxp_vtfill_imm8_kernel; break;
             default: break;
             }
         }

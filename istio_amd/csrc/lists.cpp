@@ -400,7 +400,7 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, con
 }
 
 int mxp_listentry_check(mxp_engine* eng, const mxp_list* L, int blacklist, const mxp_bag_batch* batch,
-                        uint32_t value_rule, int32_t* codes) {
+                        uint32_t value_rule, int32_t* codes, uint64_t* values) {
     if (!eng || !L || !batch || (batch->n_requests && !codes)) return MXP_ERR_ARG;
     if (!eng->have_rules || value_rule >= eng->rules.size()) return eng->fail(MXP_ERR_ARG, "listentry: no such rule");
     const auto& R = eng->rules[value_rule];
@@ -455,6 +455,11 @@ int mxp_listentry_check(mxp_engine* eng, const mxp_list* L, int blacklist, const
     if ((e = mxp_launch_list(&A, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch listentry");
     if ((e = hipMemcpyAsync(codes, d_codes.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
         return eng->hipfail(e, "download codes");
+    // the Value registers (rule value_rule's column of the [n][NR] result registers), for the
+    // status messages' symbol text (mxp_value_text over the last batch)
+    if (values && (e = hipMemcpy2DAsync(values, 8, dv.as<uint64_t>() + value_rule, (size_t)NR * 8, 8, n,
+                                        hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+        return eng->hipfail(e, "download values");
     return eng->collect_errors(batch, db);  // synchronises; error texts for mxp_pair_error
 }
 

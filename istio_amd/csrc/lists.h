@@ -55,8 +55,6 @@ typedef struct mxp_list_args {
     const uint32_t* lds_plan;
 } mxp_list_args;
 
-#define MXP_LISTENTRY_NOT_STRING (-2)
-
 // ASCII upper-casing of 8 packed bytes (bytes >= 0x80 untouched): strings.ToUpper of ASCII-only
 // strings (any other string takes goupper.h's per-rune stream)
 MXP_NHD uint64_t mxp_upper8(uint64_t x) {

@@ -242,8 +242,9 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_copy_kernel(mxp_pack_
 // Zipf-hot values put most requests on a few bitmap words, so a request only reaches the global
 // bitmap when nothing cheaper has seen its id: a per-workgroup LDS table of recently marked ids
 // (direct-mapped; racy stores only cost a redundant mark), then a plain load of the word (a set bit
-// is final, so a stale copy only costs a redundant atomic), then up to four rounds of in-wave dedup
-// (the first needing lane's id, readfirstlane + ballot) before the remaining lanes' atomicOr.
+// is final, so a stale copy only costs a redundant atomic), then up to eight rounds of in-wave pooling
+// (the lanes whose ids share the first needing lane's word OR their bits into one atomic) before the
+// remaining lanes' own atomicOr.
 #define MXP_VT_MARK_LDS 2048u
 extern "C" __global__ __launch_bounds__(256) void mxp_pack_vt_mark_kernel(mxp_pack_args A) {
     __shared__ uint32_t seen[MXP_VT_MARK_LDS];
@@ -273,14 +274,23 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_vt_mark_kernel(mxp_pa
                 km |= 1u << (k & 31u);
             }
         }
-#pragma unroll
-        for (int round = 0; round < 4; round++) {
+        // the lanes sharing the first needing lane's bitmap WORD pool their bits (consecutive
+        // interned ids -- a column of mostly distinct values -- put a whole wave on one word)
+        for (int round = 0; round < 8; round++) {
             const uint64_t m = __ballot(need);
             if (!m) break;
             const uint32_t lead = (uint32_t)__builtin_ctzll(m);
-            const uint32_t x0 = (uint32_t)__shfl((int)x, (int)lead, 64);
-            if ((threadIdx.x & 63u) == lead) atomicOr(bits + (x0 >> 6), 1ull << (x0 & 63u));
-            if (need && x == x0) need = false;
+            const uint32_t w0 = (uint32_t)__shfl((int)(x >> 6), (int)lead, 64);
+            const bool same = need && (x >> 6) == w0;
+            uint32_t lo = same && (x & 63u) < 32u ? 1u << (x & 31u) : 0u;
+            uint32_t hi = same && (x & 63u) >= 32u ? 1u << (x & 31u) : 0u;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                lo |= (uint32_t)__shfl_xor((int)lo, off, 64);
+                hi |= (uint32_t)__shfl_xor((int)hi, off, 64);
+            }
+            if ((threadIdx.x & 63u) == lead) atomicOr(bits + w0, (unsigned long long)hi << 32 | lo);
+            if (same) need = false;
         }
         if (need) atomicOr(bits + (x >> 6), 1ull << (x & 63u));
     }

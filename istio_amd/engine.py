@@ -51,7 +51,7 @@ SIGNATURES = {
     "mxp_wire_decode": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint32, ctypes.POINTER(_VP)]),
     "mxp_wire_view": (_VP, [_VP]),
     "mxp_wire_free": (None, [_VP]),
-    "mxp_listentry_check": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, ctypes.c_uint32, _VP]),
+    "mxp_listentry_check": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, ctypes.c_uint32, _VP, _VP]),
     "mxp_resolve_refs": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP, _VP, _VP, ctypes.c_uint64, _VP, _VP,
                                         ctypes.c_uint64]),
     "mxp_eval_values": (ctypes.c_int, [_VP, _VP, _VP, _VP]),
@@ -657,13 +657,19 @@ class ListHandle:
                                                     off.ctypes.data, len(bs), codes.ctypes.data), "mxp_list_check")
         return codes
 
-    def check_entries(self, engine: "Engine", batch, value_rule: int, blacklist: bool = False) -> np.ndarray:
+    def check_entries(self, engine: "Engine", batch, value_rule: int, blacklist: bool = False, texts: bool = False):
         """mxp_listentry_check: the listentry instance's Value = Eval(rule value_rule of `engine`) per
-        request, checked against this list in one device pass; -1 where Eval failed."""
+        request, checked against this list in one device pass; -1 where Eval failed.  texts: also
+        each request's Value text (mxp_value_text of the returned registers; None where Eval failed),
+        the symbol HandleListEntry's messages print."""
         codes = np.zeros(batch.n, dtype=np.int32)
+        vals = np.zeros(batch.n if texts else 0, dtype=np.uint64)
         engine._check(engine.lib.mxp_listentry_check(engine.h, self.h, int(blacklist), ctypes.byref(batch.c_struct()),
-                                                      value_rule, codes.ctypes.data), "mxp_listentry_check")
-        return codes
+                                                      value_rule, codes.ctypes.data, vals.ctypes.data if texts else None),
+                      "mxp_listentry_check")
+        if not texts:
+            return codes
+        return codes, [engine.value_text(value_rule, int(v)) if c >= 0 else None for c, v in zip(codes, vals)]
 
     def check_device(self, d_sym: int, d_off: int, n: int, stream: int, d_codes: int, blacklist: bool = False):
         """mxp_list_check_device: symbols (blob with >= 16 bytes of slack) and codes in device memory."""

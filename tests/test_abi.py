@@ -103,5 +103,22 @@ def test_go_binding_calls_declared_symbols():
     assert not [c for c in consts if not re.search(r"\b%s\b" % c, hdr)]
     for iface in ("var _ expr.Evaluator = (*Batcher)(nil)",
                   "var _ runtime.VocabularyChangeListener = (*Batcher)(nil)",
-                  "var _ Resolver = (*mxpResolver)(nil)", "var _ Actions = (*actions)(nil)"):
+                  "var _ Resolver = (*mxpResolver)(nil)", "var _ Actions = (*actions)(nil)",
+                  "var _ list = (*gpuList)(nil)", "var _ listentry.Handler = (*gpuHandler)(nil)",
+                  "var _ listentry.BagHandler = (*gpuHandler)(nil)"):
         assert iface in go, iface
+    # the list adapter's device calls (mxp_list*) are all bound, each with the header's arity
+    hdr_decl = {m.group(1): m.group(2) for m in re.finditer(r"\b(mxp_list[a-z_]*)\(([^;]*?)\);", hdr, re.S)}
+    for name in ("mxp_list_create", "mxp_list_check", "mxp_listentry_check", "mxp_list_entries", "mxp_list_destroy"):
+        assert name in calls, name
+    for m in re.finditer(r"\bC\.(mxp_list[a-z_]*)\(", go):
+        depth, n_args, i = 1, 1, m.end()
+        if go[i] == ")":
+            n_args = 0
+        while depth:
+            ch = go[i]
+            depth += ch in "(["
+            depth -= ch in ")]"
+            n_args += ch == "," and depth == 1
+            i += 1
+        assert n_args == hdr_decl[m.group(1)].count(",") + 1, (m.group(1), go[m.end():i])

@@ -162,7 +162,7 @@ def test_listentry_fused(eng, case):
     inst.set_vocabulary(manifest)
     assert (inst.compile(["true", expr]) == 0).all()  # the value expression is rule 1
     lst = eng.list_create(ltype, entries, overrides)
-    got = lst.check_entries(inst, batch, 1, black)
+    got, texts = lst.check_entries(inst, batch, 1, black, texts=True)
     ev = oracle.OracleEvaluator(manifest)
     vals, syms, errq = [], [], []
     for q in range(batch.n):
@@ -179,6 +179,9 @@ def test_listentry_fused(eng, case):
     assert (len(errq) > 0) == (case != "regex-path") and (got >= 0).sum() > batch.n // 2  # `|` never fails
     for q in errq[:50]:
         assert inst.pair_error(q, 1) == ev.eval(expr, batch, q)[1]
+    # the symbol the status messages print ("%s is not whitelisted", list.go:84-94)
+    assert all(texts[q] == syms[q] for q in range(batch.n) if got[q] >= 0)
+    assert all(texts[q] is None for q in errq)
 
 
 @pytest.mark.parametrize("blacklist", [False, True])
@@ -216,7 +219,7 @@ def test_listentry_fused_unicode(eng):
     inst.set_vocabulary(manifest)
     assert (inst.compile(["true", "request.path"]) == 0).all()
     lst = eng.list_create(L.CASE_INSENSITIVE_STRINGS, entries, [])
-    got = lst.check_entries(inst, batch, 1, False)
+    got, texts = lst.check_entries(inst, batch, 1, False, texts=True)
     ev = oracle.OracleEvaluator(manifest)
     ref = L.StringList(entries, case_insensitive=True)
     want = np.empty(batch.n, dtype=np.int32)
@@ -226,3 +229,4 @@ def test_listentry_fused_unicode(eng):
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(q), int(got[q]), int(want[q])) for q in bad[:5]]
     assert (want == 0).sum() > 1000 and (want == -1).sum() > 100
+    assert all(texts[q] == bags[q]["request.path"] for q in range(batch.n) if got[q] >= 0)

@@ -5,7 +5,8 @@ class records the class kernel logs at a representative request are expanded to 
 the class (engine.cpp expand_class_errors).  MXP_DEBUG_FLAGS 262144 forces value classes at any
 batch size (the default wants >= 16 requests per class); 131072 turns them off; 2097152 makes the
 fill chunks gather class words from global memory instead of the LDS-staged rows
-(mxp_vtfill_kernel vs mxp_vtfill_lds_kernel)."""
+(mxp_vtfill_kernel vs mxp_vtfill_lds_kernel); 33554432 keeps batches whose class tables all have 64
+slots on mxp_vtfill_lds_kernel instead of mxp_vtfill_imm<n>_kernel."""
 import numpy as np
 import pytest
 
@@ -17,6 +18,7 @@ from test_gpu_parity import compare
 pytestmark = pytest.mark.gpu
 FORCE, OFF, GLOBAL = "262144", "131072", "2097152"
 FORCE_GLOBAL = str(262144 | 2097152)
+FORCE_LDS = str(262144 | 33554432)  # the LDS-row kernel instead of the immediate-offset one (tables of 64 slots)
 
 
 @pytest.fixture(scope="module")
@@ -33,7 +35,7 @@ def engine_for(mxp, monkeypatch, flags, manifest, rules):
     return eng
 
 
-@pytest.mark.parametrize("flags", [FORCE, "0", FORCE_GLOBAL])
+@pytest.mark.parametrize("flags", [FORCE, "0", FORCE_GLOBAL, FORCE_LDS])
 def test_c4_value_classes_parity(mxp, monkeypatch, flags):
     """C4 routes: the header rules (equality and regexps on request.headers["h"]) become value
     classes (17 values per header); path rules stay with the prefix index."""
@@ -44,12 +46,14 @@ def test_c4_value_classes_parity(mxp, monkeypatch, flags):
     assert (want == 1).sum() > 1000
 
 
-def test_fuzz_value_classes_errors(mxp, monkeypatch):
+@pytest.mark.parametrize("flags", [FORCE, FORCE_LDS])
+def test_fuzz_value_classes_errors(mxp, monkeypatch, flags):
     """Random rules over random bags with missing / wrongly typed values: class records (lookup and
-    conversion errors, panics) expanded to every request of the class, texts checked."""
+    conversion errors, panics) expanded to every request of the class, texts checked; class words
+    with error bits (the immediate-offset kernel's global error gathers)."""
     rules = W.fuzz_rules(800, seed=61, depth=3)
     batch = BagBatch.from_bags(W.fuzz_bags(900, seed=62), names=list(W.DEFAULT_TEST_MANIFEST))
-    eng = engine_for(mxp, monkeypatch, FORCE, W.DEFAULT_TEST_MANIFEST, rules)
+    eng = engine_for(mxp, monkeypatch, flags, W.DEFAULT_TEST_MANIFEST, rules)
     assert eng.ruleset_info()["value_class_columns"] >= 1
     got, want = compare(eng, oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST), rules, batch, sample_msgs=800)
     assert (want >= 2).sum() > 100
@@ -69,7 +73,7 @@ def test_value_classes_on_off_identical_with_hits(mxp, monkeypatch):
     import torch
     manifest, rules, batch = W.c4_workload(n_rules=2000, n_requests=50_000 + 5, seed=45)
     out = []
-    for flags in (FORCE, FORCE_GLOBAL, OFF):
+    for flags in (FORCE, FORCE_GLOBAL, OFF, FORCE_LDS):
         eng = engine_for(mxp, monkeypatch, flags, manifest, rules)
         db = eng.upload(batch)
         Wd = (len(rules) + 31) // 32
