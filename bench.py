@@ -9,7 +9,10 @@ shard (the full predicate bitmap) + the per-rule hit counters, reduced over RCCL
 all-reduce per step (istio_amd.dist.StepCounters).
 
 The default run also measures C4 (configs[3]: 10k Pilot-style route rules x 1M requests) with the
-same step structure and reports it as the extra "c4" block of the same JSON line (--no-c4: skip).
+same step structure and reports it as the extra "c4" block of the same JSON line (--no-c4: skip),
+and C3 (configs[2]: CIDR, case-insensitive string and regex lists, 100k entries x 1M lookups) as
+the "c3" block (--no-c3: skip).  Each predicate block also carries a "fresh_batch" figure: a new
+1M-request batch uploaded from host memory and evaluated every step (PCIe-inclusive).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--rules R] [--requests N_PER_GPU]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -57,6 +60,8 @@ def parse():
     p.add_argument("--requests", type=int, default=1 << 20)
     p.add_argument("--cpu-sample-seconds", type=float, default=12.0)
     p.add_argument("--cpu-threads", type=int, default=host_threads())
+    p.add_argument("--list-cpu-seconds", type=float, default=4.0, help="CPU-baseline sample per C3 list kind")
+    p.add_argument("--no-c3", action="store_true", help="default run: skip the extra C3 list block")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-c4", action="store_true", help="default run: skip the extra C4 block")
     p.add_argument("--no-c5", action="store_true", help="default run: skip the extra C5 block")
@@ -290,16 +295,17 @@ def make_step(ctr, evaluate, quota_alloc=None, stream=None):
     return step
 
 
-def list_bench(args, rank, world, local):
+def list_bench(args, rank, world, local, kind=None, emit=True):
     """C3 (BASELINE configs[2]): 100k-entry CIDR / string / regex lists, 1M lookups per GPU resident
-    in HBM; one step = HandleListEntry for every lookup (mxp_list_check_device, one kernel)."""
+    in HBM; one step = HandleListEntry for every lookup (mxp_list_check_device, one kernel).
+    Returns the result dict (printed as the line when emit)."""
     import numpy as np
     import torch
     from istio_amd import workloads as W
     from istio_amd.engine import Engine
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import lists as L
-    kind = args.workload
+    kind = kind or args.workload
     n_look = args.requests
     if kind == "c3-ip":
         entries, syms = W.c3_ip_list(n_entries=args.list_entries, n_lookups=n_look, seed=3 + 1000 * rank)
@@ -349,14 +355,17 @@ def list_bench(args, rank, world, local):
                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "mxp_list_kernel",
                         "alg_bytes_per_launch": alg}}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
-        out["cpu_baseline"] = list_cpu_baseline(L, kind, entries, syms, args.cpu_sample_seconds, args.cpu_threads)
-    if rank == 0:
+        out["cpu_baseline"] = list_cpu_baseline(L, kind, entries, syms, args.list_cpu_seconds, args.cpu_threads)
+    del d_blob, d_off, d_codes, lst
+    if rank == 0 and emit:
         print(json.dumps(out))
+    return out
 
 
 def quota_setup(eng, n_requests, rank, world, dev):
     """memquota state for QUOTA_KEYS keys and this rank's quota requests: the global arrival stream
-    routed by key owner (workloads.quota_workload, dist.key_owner), resident in HBM."""
+    routed by key owner (workloads.quota_workload, dist.key_owners: LPT over the keys' expected
+    frequencies), resident in HBM."""
     import numpy as np
     import torch
     from istio_amd import workloads as W
@@ -371,7 +380,7 @@ def quota_setup(eng, n_requests, rank, world, dev):
 
 
 def quota_bench(args, rank, world, local):
-    """C5 memquota (BASELINE configs[4]): K = 1024 quota keys, each owned by one rank (key % N), the
+    """C5 memquota (BASELINE configs[4]): K = 1024 quota keys, each owned by one rank (dist.key_owners), the
     quota requests routed to their key's owner in arrival order (~1M per GPU); a step = batched
     HandleQuota (sort by key + per-key replay) and, when N > 1, the all-reduce of the per-key deltas."""
     import numpy as np
@@ -437,25 +446,29 @@ def quota_bench(args, rank, world, local):
 
 
 def list_cpu_baseline(L, kind, entries, syms, seconds, threads):
-    """The list restatement timed on host cores: the IP list is the reference's linear IPNet scan
-    (ipList.go:77-92, C + OpenMP); strings a hash set (Python); regexes the Go regexp restatement."""
+    """The list restatements timed on host cores, compiled and multi-threaded (OpenMP over the
+    lookups): the IP list is the reference's linear IPNet scan (ipList.go:77-92); case-insensitive
+    strings a hash set after Go's strings.ToUpper (stringList.go:51-80, a Go map); regexes the Go
+    regexp restatement, patterns tried in order until one matches (regexList.go:26-33)."""
     if kind == "c3-ip":
-        ref, threads_used = L.IPList(entries), threads
+        ref = L.IPList(entries)
     elif kind == "c3-str":
-        ref, threads_used = L.StringList(entries, case_insensitive=True), 1
+        ref = L.CStringList(entries, case_insensitive=True)
     else:
-        ref, threads_used = L.RegexList(entries), 1
-    chunk, done = 64, 0
+        ref = L.RegexList(entries)
+    # (chunks of >= 4096 lookups: the regex restatement compiles its patterns once per call, a few
+    # percent of a chunk's time)
+    chunk, done = 4096, 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds and done + chunk <= len(syms):
-        part = syms[done:done + chunk]
-        ref.found(part, threads=threads) if kind == "c3-ip" else ref.found(part)
+        ref.found(syms[done:done + chunk], threads=threads)
         done += chunk
-        chunk = min(chunk * 2, 1 << 16)
+        chunk = min(chunk * 2, 1 << 18)
     dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "lookups/s", "cores": threads_used, "host_cpus": os.cpu_count(),
+    return {"value": done / dt, "unit": "lookups/s", "cores": threads, "host_cpus": os.cpu_count(),
             "kind": "port",
-            "sample": "%d lookups (%.1fs) against all %d entries, oracle restatement" % (done, dt, len(entries))}
+            "sample": "%d lookups (%.1fs) against all %d entries, oracle C restatement on %d threads" % (
+                done, dt, len(entries), threads)}
 
 
 def end_to_end(eng, batch, n_rules, reps):
@@ -690,6 +703,15 @@ def main():
         a5.no_cpu_baseline = True
         c5 = predicate_bench(a5, "c2", rank, world, local, with_quota=True)
         out["c5"] = {k: c5[k] for k in keys if k in c5}
+    if args.workload == "c2" and not args.no_c3:
+        # configs[2]: the three list kinds (100k entries, 1M lookups per GPU), driver-timed too
+        a3 = argparse.Namespace(**vars(args))
+        ckeys = ("metric", "value", "unit", "ms_per_step", "kernel_ms", "list_compile_s", "config", "roofline",
+                 "cpu_baseline")
+        out["c3"] = {}
+        for k in ("c3-ip", "c3-str", "c3-regex"):
+            r = list_bench(a3, rank, world, local, kind=k, emit=False)
+            out["c3"][k[3:]] = {x: r[x] for x in ckeys if x in r}
     if rehearse:
         out["rehearsal"] = "%d ranks on one GPU over gloo: exercises the multi-rank step, not a scaling number" % world
     if rank == 0:

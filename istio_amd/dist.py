@@ -2,9 +2,9 @@
 
 * Requests shard across ranks and the compiled rule / DFA / list tables are replicated: a Check
   request's predicates read only its own bag and the immutable rule set (resolver.go:202-238).
-* memquota keys have ONE owner rank each (`key_owner`): the quota requests of a key are routed to its
-  owner, so each key's arrival sequence is replayed on one GPU exactly as memquota.go:118-211 replays
-  it in one process.  The per-key state never has to move.
+* memquota keys have ONE owner rank each (`key_owners`, balanced by expected load): the quota
+  requests of a key are routed to its owner, so each key's arrival sequence is replayed on one GPU
+  exactly as memquota.go:118-211 replays it in one process.  The per-key state never has to move.
 * The only exchange is one sum all-reduce per step over the concatenated per-step counters
   `hits[R] ++ quota_delta[K]` (`StepCounters`), RCCL over xGMI ("nccl" backend on ROCm), "gloo" in
   the CPU tests.
@@ -27,10 +27,24 @@ def shard_bounds(n_total: int, rank: int, world_size: int) -> tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def key_owner(key, world_size: int):
-    """Owner rank of a memquota key id (works elementwise on numpy arrays): the rank that holds the
-    key's cell / rolling window and replays all of its requests in arrival order."""
-    return key % world_size
+def key_owners(weights, world_size: int):
+    """Owner rank of every memquota key (one owner per key: the rank that holds the key's cell /
+    rolling window and replays all of its requests in arrival order), assigned by expected load:
+    longest-processing-time first over the keys' request frequencies at snapshot time (`weights`,
+    e.g. the last batch's per-key counts), each key to the least-loaded rank, ties by rank then key.
+    Greedy LPT is within 4/3 of the best assignment; a key whose own share exceeds 1/world bounds any
+    one-owner assignment (C5's Zipf(1.05) head key: 15.5% of the requests, 1.24x the mean at 8 ranks)."""
+    import heapq
+
+    import numpy as np
+    w = np.asarray(weights, dtype=np.float64)
+    owners = np.zeros(len(w), dtype=np.int64)
+    load = [(0.0, r) for r in range(world_size)]
+    for k in np.lexsort((np.arange(len(w)), -w)):  # heaviest first, then by key id
+        l, r = heapq.heappop(load)
+        owners[k] = r
+        heapq.heappush(load, (l + float(w[k]), r))
+    return owners
 
 
 def _initialized() -> bool:

@@ -472,29 +472,35 @@ def c3_ip_list(n_entries=100_000, n_lookups=1_000_000, seed=3, p_v6=0.1, hit_rat
             a = "%d.%d.%d.%d" % tuple(q)
             entries.append(a if bits == 32 and rng.random() < 0.5 else "%s/%d" % (a, bits))
             nets.append(("4", q, bits))
+    # lookups, drawn column-wise (1M in about a second)
+    n = n_lookups
+    bad = rng.random(n) < 0.01
+    pick = rng.integers(0, n_entries, size=n)
+    hit = rng.random(n) < hit_rate
+    host = rng.integers(0, 1 << 32, size=n, dtype=np.uint64)
+    mapped = rng.random(n) <= 0.02
+    rnd6 = rng.integers(0, 1 << 16, size=(n, 8))
+    is6 = np.array([k == "6" for k, _, _ in nets])[pick]
+    base4 = np.array([int(b[0]) << 24 | int(b[1]) << 16 | int(b[2]) << 8 | int(b[3]) if k == "4" else 0
+                      for k, b, _ in nets], dtype=np.uint64)[pick]
+    bits = np.array([b for _, _, b in nets], dtype=np.uint64)[pick]
+    keep = np.where(bits > 0, (np.uint64(0xFFFFFFFF) << (np.uint64(32) - np.minimum(bits, 32))) & np.uint64(0xFFFFFFFF),
+                    np.uint64(0))
+    x4 = np.where(hit, (base4 & keep) | (host & ~keep & np.uint64(0xFFFFFFFF)), host)
     syms = []
-    for _ in range(n_lookups):
-        r = rng.random()
-        if r < 0.01:
+    for q in range(n):
+        if bad[q]:
             syms.append("not-an-ip")
-            continue
-        kind, base, bits = nets[int(rng.integers(0, n_entries))]
-        hit = rng.random() < hit_rate
-        if kind == "4":
-            x = int(base[0]) << 24 | int(base[1]) << 16 | int(base[2]) << 8 | int(base[3])
-            host = int(rng.integers(0, 1 << 32))
-            if hit:
-                keep = (0xFFFFFFFF << (32 - bits)) & 0xFFFFFFFF if bits else 0
-                x = (x & keep) | (host & ~keep & 0xFFFFFFFF)
-            else:
-                x = host
-            s = "%d.%d.%d.%d" % (x >> 24, (x >> 16) & 255, (x >> 8) & 255, x & 255)
-            syms.append(s if rng.random() > 0.02 else "::ffff:" + s)
+        elif not is6[q]:
+            x = int(x4[q])
+            v = "%d.%d.%d.%d" % (x >> 24, (x >> 16) & 255, (x >> 8) & 255, x & 255)
+            syms.append("::ffff:" + v if mapped[q] else v)
         else:
-            w = [int(v) for v in base] if hit else [int(v) for v in rng.integers(0, 1 << 16, size=8)]
-            if hit:
-                for i in range(bits // 16 + 1, 8):
-                    w[i] = int(rng.integers(0, 1 << 16))
+            _, base, b6 = nets[int(pick[q])]
+            w = [int(v) for v in base] if hit[q] else [int(v) for v in rnd6[q]]
+            if hit[q]:
+                for i in range(b6 // 16 + 1, 8):
+                    w[i] = int(rnd6[q, i])
             syms.append(":".join("%x" % v for v in w))
     return entries, syms
 
@@ -536,16 +542,21 @@ def c3_regex_list(n_patterns=10_000, n_lookups=1_000_000, seed=3, hit_rate=0.5, 
         n = m + int(rng.integers(0, 6))
         specs.append((pre, m, n, suf))
         pats.append("^%s[a-z0-9]{%d,%d}(%s)?$" % (pre, m, n, suf))
-    syms, hits = [], []
-    for _ in range(n_lookups):
-        pre, m, n, suf = specs[int(rng.integers(0, n_patterns))]
-        body = "".join(alnum[int(i)] for i in rng.integers(0, 36, size=int(rng.integers(m, n + 1))))
-        s = pre + body + (suf if rng.random() < 0.5 else "")
-        hit = rng.random() < hit_rate
-        if not hit:
-            s = s + ("-" if rng.random() < 0.5 else "X")  # outside the class / past the anchor
-        syms.append(s)
-        hits.append(hit)
+    # lookups, drawn column-wise
+    nl = n_lookups
+    sel = rng.integers(0, n_patterns, size=nl)
+    lo = np.array([sp[1] for sp in specs])[sel]
+    hi = np.array([sp[2] for sp in specs])[sel]
+    blen = lo + (rng.random(nl) * (hi - lo + 1)).astype(np.int64)
+    body = np.frombuffer(alnum.encode(), dtype=np.uint8)[rng.integers(0, 36, size=(nl, 8))].tobytes().decode()
+    with_suf = rng.random(nl) < 0.5
+    hits = rng.random(nl) < hit_rate
+    tail = np.where(rng.random(nl) < 0.5, "-", "X")
+    syms = []
+    for q in range(nl):
+        pre, _, _, suf = specs[int(sel[q])]
+        s = pre + body[8 * q:8 * q + int(blen[q])] + (suf if with_suf[q] else "")
+        syms.append(s if hits[q] else s + tail[q])  # a miss: outside the class / past the anchor
     return (pats, syms, np.array(hits)) if return_hits else (pats, syms)
 
 
@@ -629,6 +640,12 @@ def c4_workload(n_rules=10000, n_requests=1_000_000, seed=4, vocab=512, cont_fra
 
 
 # ----------------------------------------------------------------------------------- memquota (C5)
+def quota_key_weights(n_keys=1024):
+    """C5's key distribution: Zipf(1.05) over the key ids (the expected share of each key)."""
+    p = np.arange(1, n_keys + 1, dtype=np.float64) ** -1.05
+    return p / p.sum()
+
+
 def quota_workload(n_keys=1024, n_requests=1_000_000, seed=5, p_free=0.1, p_zero=0.02, p_be=0.5, rank=0, world=1,
                    return_index=False):
     """C5 memquota deltas: K quota keys (a third non-expiring cells, the rest 1 s / 60 s rolling
@@ -636,16 +653,17 @@ def quota_workload(n_keys=1024, n_requests=1_000_000, seed=5, p_free=0.1, p_zero
     and zero amounts, best effort half the time).  Returns (max_amount, valid_ns, keys, amounts, be).
 
     Multi-GPU (world > 1): ONE global arrival stream of n_requests * world requests is drawn and
-    routed by key owner (dist.key_owner: key % world), as an upstream router would; rank `rank` gets
-    the requests of the keys it owns, in global arrival order -- so the per-key sequences are the
-    global ones and the union over ranks is exactly the single-process workload.  return_index adds
-    the positions of the rank's requests in the global stream."""
+    routed by key owner (dist.key_owners over the keys' expected frequencies, quota_key_weights), as
+    an upstream router would; rank `rank` gets the requests of the keys it owns, in global arrival
+    order -- so the per-key sequences are the global ones and the union over ranks is exactly the
+    single-process workload.  return_index adds the positions of the rank's requests in the global
+    stream."""
     rng = np.random.default_rng(seed)
     max_amount = rng.integers(50, 5001, size=n_keys).astype(np.int64)
     valid = np.choose(rng.integers(0, 3, size=n_keys), [0, 10**9, 60 * 10**9]).astype(np.int64)
-    p = np.arange(1, n_keys + 1, dtype=np.float64) ** -1.05
+    p = quota_key_weights(n_keys)
     total = n_requests * world
-    keys = rng.choice(n_keys, size=total, p=p / p.sum()).astype(np.uint32)
+    keys = rng.choice(n_keys, size=total, p=p).astype(np.uint32)
     amounts = rng.integers(1, 21, size=total).astype(np.int64)
     r = rng.random(total)
     amounts = np.where(r < p_free, -amounts, amounts)
@@ -653,7 +671,8 @@ def quota_workload(n_keys=1024, n_requests=1_000_000, seed=5, p_free=0.1, p_zero
     be = (rng.random(total) < p_be).astype(np.uint8)
     idx = np.arange(total)
     if world > 1:
-        idx = np.nonzero(keys % world == rank)[0]
+        from istio_amd import dist as D
+        idx = np.nonzero(D.key_owners(p, world)[keys] == rank)[0]
         keys, amounts, be = keys[idx], amounts[idx], be[idx]
     out = (max_amount, valid, keys, amounts, be)
     return out + (idx,) if return_index else out

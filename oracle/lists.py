@@ -109,6 +109,32 @@ class StringList:
                         dtype=np.int8)
 
 
+class CStringList:
+    """The same list in the C restatement (lists_oracle.c: a hash set, Go strings.ToUpper in C):
+    the compiled, multi-threaded CPU baseline; tests check it against StringList."""
+
+    def __init__(self, lines, overrides=(), case_insensitive=False):
+        import oracle
+        self.L = oracle.lib()
+        blob, off = _blob([_b(s) for s in list(lines) + list(overrides)])
+        self.h = self.L.oracle_strlist_new(blob.ctypes.data, off.ctypes.data, len(off) - 1, int(case_insensitive))
+
+    def num_entries(self):
+        return self.L.oracle_strlist_entries(self.h)
+
+    def found(self, symbols, threads=16):
+        sb, so = _blob([_b(s) for s in symbols])
+        out = np.zeros(len(symbols), dtype=np.int8)
+        self.L.oracle_strlist_found(self.h, sb.ctypes.data, so.ctypes.data, len(symbols), out.ctypes.data, threads)
+        return out
+
+    def __del__(self):
+        try:
+            self.L.oracle_strlist_free(self.h)
+        except Exception:
+            pass
+
+
 class ListParseError(Exception):
     pass
 

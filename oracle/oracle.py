@@ -82,6 +82,23 @@ def lib():
         L.oracle_regex_list_found.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int,
                                               ctypes.c_void_p, ctypes.c_size_t]
+        # string lists (lists_oracle.c): Go map + strings.ToUpper, the table of oracle/unicode_upper.json
+        L.oracle_upper_table.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.oracle_go_to_upper.restype = ctypes.c_size_t
+        L.oracle_go_to_upper.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+        L.oracle_strlist_new.restype = ctypes.c_void_p
+        L.oracle_strlist_new.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.oracle_strlist_entries.restype = ctypes.c_size_t
+        L.oracle_strlist_entries.argtypes = [ctypes.c_void_p]
+        L.oracle_strlist_free.argtypes = [ctypes.c_void_p]
+        L.oracle_strlist_found.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_void_p, ctypes.c_int]
+        import json
+        with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "unicode_upper.json")) as f:
+            pairs = sorted(json.load(f)["pairs"])
+        import numpy as _np
+        _UPPER_PAIRS = _np.array(pairs, dtype=_np.uint32).reshape(-1)
+        L.oracle_upper_table(_UPPER_PAIRS.ctypes.data, len(pairs))
         # memquota C restatement (memquota_oracle.c)
         L.mq_create.restype = ctypes.c_void_p
         L.mq_create.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]

@@ -76,7 +76,7 @@ def _step_rank_main(rank, world, port, out_path, steps):
     # memquota requests routed by key owner: the rank replays its keys' sequences with the oracle
     mx, vd, keys, amounts, be, idx = W.quota_workload(n_keys=K, n_requests=400, seed=9, rank=rank, world=world,
                                                       return_index=True)
-    assert np.all(D.key_owner(keys, world) == rank)
+    assert np.all(D.key_owners(W.quota_key_weights(K), world)[keys] == rank)
     mq = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
     granted_all = []
     for s in range(steps):
@@ -218,3 +218,58 @@ def test_two_rank_gloo_bench_step(tmp_path):
         for k, a, b in zip(keys, amounts, be):
             want_delta[int(k)] += mq.handle(int(k), int(a), bool(b), 10**18 + s * 10**8)
     assert np.array_equal(got[R:R + K], want_delta)
+
+
+def _quota_rank_main(rank, world, port, out_path, n_keys, per_rank):
+    """One step of C5's quota half at world 8: the rank replays the requests of the keys it owns
+    (dist.key_owners, LPT by expected load) with the memquota restatement, its per-key deltas and its
+    request count go through one all-reduce each."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import memquota as M
+    from istio_amd import dist as D
+    from istio_amd import workloads as W
+    mx, vd, keys, amounts, be = W.quota_workload(n_keys=n_keys, n_requests=per_rank, seed=11, rank=rank, world=world)
+    mq = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(n_keys)})
+    ctr = D.StepCounters([n_keys, world])
+    ctr.begin_step()
+    delta, count = ctr.views()
+    for k, a, b in zip(keys, amounts, be):
+        delta[int(k)] += mq.handle(int(k), int(a), bool(b), 10**18)
+    count[rank] = len(keys)
+    ctr.end_step()
+    if rank == 0:
+        np.save(out_path, np.concatenate([t.numpy() for t in ctr.totals()]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_eight_rank_quota_owners_balanced(tmp_path):
+    """configs[4]'s quota routing at 8 ranks: keys owned by load (LPT over the Zipf(1.05) key shares)
+    put at most 1.25x the mean on a rank -- the head key's own 15.5% share bounds any one-owner
+    assignment at 1.24x (key % 8 gave 1.9x) -- and the all-reduced deltas equal the single-process
+    sequential HandleQuota (memquota.go:118-211)."""
+    import torch.multiprocessing as mp
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import memquota as M
+    from istio_amd import dist as D
+    from istio_amd import workloads as W
+    world, K, per_rank = 8, 1024, 6000
+    owners = D.key_owners(W.quota_key_weights(K), world)
+    load = np.bincount(owners, weights=W.quota_key_weights(K), minlength=world)
+    assert load.max() * world <= 1.25 and load.max() * world < np.bincount(np.arange(K) % world, weights=W.quota_key_weights(K)).max() * world
+    out = str(tmp_path / "q.npy")
+    mp.start_processes(_quota_rank_main, args=(world, _free_port(), out, K, per_rank), nprocs=world, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    counts = got[K:]
+    assert counts.sum() == world * per_rank and counts.max() <= 1.25 * counts.mean(), counts
+    mx, vd, keys, amounts, be = W.quota_workload(n_keys=K, n_requests=per_rank * world, seed=11)
+    mq = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
+    want = np.zeros(K, dtype=np.int64)
+    for k, a, b in zip(keys, amounts, be):
+        want[int(k)] += mq.handle(int(k), int(a), bool(b), 10**18)
+    assert np.array_equal(got[:K], want)

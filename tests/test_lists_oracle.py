@@ -49,3 +49,23 @@ def test_regex_list_errors():
     with pytest.raises(L.ListParseError) as ei:
         L.RegexList(["a+", "(b"], [])
     assert str(ei.value) == "error parsing regexp: missing closing ): `(b`"
+
+
+@pytest.mark.parametrize("ci", [False, True])
+def test_c_string_list_equals_python(ci):
+    """lists_oracle.c's string list (the compiled CPU baseline: hash set + Go strings.ToUpper in C)
+    against the Python restatement: entry counts and membership, non-ASCII and invalid UTF-8
+    included; its ToUpper against go_to_upper byte for byte."""
+    import oracle
+    from istio_amd import workloads as W
+    entries, syms = W.ci_unicode_list(n_entries=2000, n_lookups=20000, seed=45)
+    py, c = L.StringList(entries[:1500] + [""], entries[1500:], ci), L.CStringList(entries[:1500] + [""], entries[1500:], ci)
+    assert py.num_entries() == c.num_entries()
+    assert np.array_equal(py.found(syms), c.found(syms, threads=4))
+    lib = oracle.lib()
+    import ctypes
+    for s in syms[:3000]:
+        b = s.encode("utf-8", "surrogateescape")
+        out = ctypes.create_string_buffer(3 * len(b) + 4)
+        n = lib.oracle_go_to_upper(b, len(b), out)
+        assert out.raw[:n] == L.go_to_upper(b), b
