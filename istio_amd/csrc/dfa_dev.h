@@ -26,7 +26,8 @@ typedef struct mxp_dfa_hdr {
 //   CL             [m + 1][nvar][W] epsilon closure (under the variant's flags) of each rune
 //                  instruction's successor; row m = the start threads (re-injected every step)
 #define MXP_NFA_HDR_WORDS 9u
-#define MXP_NFA_MAX_WORDS 4u
+#define MXP_NFA_MAX_WORDS 4u    // thread sets of up to 255 rune instructions: registers
+#define MXP_NFA_WIDE_WORDS 16u  // up to 1023 (regex.h kNfaMaxPos): private memory, see mxp_nfa_run_wide
 
 typedef struct mxp_dfa_set {
     const mxp_dfa_hdr* hdr;
@@ -101,10 +102,72 @@ __device__ __forceinline__ bool mxp_rx_word(uint32_t r) {
 // separate instantiations, so the DFA-only kernels keep their register budgets).  Per position: the closure of the pending threads
 // plus a fresh start thread under the position's assertion flags (what the DFA folds into its
 // states); MATCH in the closure -> true; else the threads whose rune instruction accepts the class.
+// Programs with more than 255 rune instructions (W > 4): the same walk with the thread sets in
+// per-lane arrays indexed at run time -- private (scratch) memory, 256 bytes a lane, which only the
+// NFA kernel instantiations carry.  Only patterns whose DFA is over budget AND whose program is that
+// wide take it.
+__device__ __forceinline__ bool mxp_nfa_run_wide(const mxp_dfa_set& S, const mxp_dfa_hdr& H, const uint8_t* s,
+                                                 uint32_t n) {
+    const uint64_t* N = (const uint64_t*)(S.trans + H.trans);
+    const uint64_t h0 = N[0];
+    const uint32_t m = (uint32_t)(h0 & 0xFFFF), W = (uint32_t)(h0 >> 16) & 0xFF, nvar = (uint32_t)(h0 >> 24) & 0xFFFF;
+    const uint8_t* var_of = (const uint8_t*)(N + 1);
+    const uint64_t* ACC = N + MXP_NFA_HDR_WORDS;
+    const uint64_t* CL = ACC + (uint64_t)(H.ncls - 1) * W;
+    const uint64_t* CLS = CL + (uint64_t)m * nvar * W;
+    const uint16_t* asc = S.ascii + H.ascii;
+    // (volatile: kept in private memory -- promoted to registers they would cost every NFA kernel
+    // instantiation 64 VGPRs for a path almost no rule set takes)
+    volatile uint64_t U[MXP_NFA_WIDE_WORDS], C[MXP_NFA_WIDE_WORDS];
+    for (uint32_t w = 0; w < W; w++) U[w] = 0;
+    bool begin = true, prev_nl = false, prev_word = false;
+    uint32_t i = 0;
+    for (;;) {
+        const bool end = i >= n;
+        uint32_t r = 0, width = 1, cls = 0;
+        if (!end) {
+            const uint32_t c0 = s[i];
+            if (c0 < 0x80) {
+                r = c0;
+                cls = asc[c0];
+            } else {
+                r = mxp_decode_hi(s, i, n, c0, &width);
+                cls = mxp_hi_class(S, H, r);
+            }
+        }
+        uint32_t f = 0;
+        if (begin) f |= 4u | 1u;
+        if (prev_nl) f |= 1u;
+        if (end) f |= 8u | 2u;
+        if (!end && r == '\n') f |= 2u;
+        f |= (prev_word != (!end && mxp_rx_word(r))) ? 16u : 32u;
+        const uint32_t v = var_of[f];
+        for (uint32_t w = 0; w < W; w++) C[w] = CLS[(uint64_t)v * W + w];
+        for (uint32_t w = 0; w < W; w++) {
+            uint64_t bits = U[w];
+            while (bits) {
+                const uint32_t j = w * 64u + (uint32_t)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                const uint64_t* q = CL + ((uint64_t)j * nvar + v) * W;
+                for (uint32_t x = 0; x < W; x++) C[x] |= q[x];
+            }
+        }
+        if ((C[m >> 6] >> (m & 63)) & 1u) return true;
+        if (end) return false;
+        const uint64_t* a = ACC + (uint64_t)cls * W;
+        for (uint32_t w = 0; w < W; w++) U[w] = C[w] & a[w];
+        begin = false;
+        prev_nl = r == '\n';
+        prev_word = mxp_rx_word(r);
+        i += width;
+    }
+}
+
 __device__ __forceinline__ bool mxp_nfa_run(const mxp_dfa_set& S, const mxp_dfa_hdr& H, const uint8_t* s, uint32_t n) {
     const uint64_t* N = (const uint64_t*)(S.trans + H.trans);
     const uint64_t h0 = N[0];
     const uint32_t m = (uint32_t)(h0 & 0xFFFF), W = (uint32_t)(h0 >> 16) & 0xFF, nvar = (uint32_t)(h0 >> 24) & 0xFFFF;
+    if (W > MXP_NFA_MAX_WORDS) return mxp_nfa_run_wide(S, H, s, n);
     const uint8_t* var_of = (const uint8_t*)(N + 1);
     const uint64_t* ACC = N + MXP_NFA_HDR_WORDS;
     const uint64_t* CL = ACC + (uint64_t)(H.ncls - 1) * W;

@@ -265,7 +265,7 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
         // The patterns are packed, in order, into parts whose single-pattern DFAs sum to about
         // kListPartStates; each part is one union DFA (a part over kListRegexStates splits in
         // halves), and a pattern whose own DFA is over kPatternStates becomes its own NFA.  Only a
-        // pattern with both a DFA over budget and more than kNfaMaxPos rune instructions is refused.
+        // pattern with both a DFA over budget and more than kNfaMaxPos (1023) rune instructions is refused.
         std::vector<std::string> pats;
         for (uint32_t i = 0; i < n_entries; i++)
             if (entry_lens[i]) pats.push_back(str(entries[i], entry_lens[i]));
@@ -391,6 +391,7 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, con
     A.n4 = L->n4;
     A.n6 = L->n6;
     A.rx_n = L->rx_n;
+    A.rx_nfa = L->rx_nfa;
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes;
@@ -438,6 +439,7 @@ int mxp_listentry_check(mxp_engine* eng, const mxp_list* L, int blacklist, const
     A.n4 = L->n4;
     A.n6 = L->n6;
     A.rx_n = L->rx_n;
+    A.rx_nfa = L->rx_nfa;
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes.as<int32_t>();

@@ -53,6 +53,7 @@ typedef struct mxp_list_args {
     // array: a dynamically indexed by-value argument would be copied to scratch.)
     uint32_t lds_nparts;
     const uint32_t* lds_plan;
+    uint32_t rx_nfa;            // REGEX lists with NFA parts: the *_nfa kernel instantiations
 } mxp_list_args;
 
 // ASCII upper-casing of 8 packed bytes (bytes >= 0x80 untouched): strings.ToUpper of ASCII-only

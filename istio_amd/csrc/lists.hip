@@ -163,7 +163,18 @@ __device__ __forceinline__ void list_decide(const mxp_list_args& A, uint32_t q, 
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args A) {
+// kNfa: the list holds NFA parts (patterns whose own DFA is over budget): only the *_nfa
+// instantiations carry the NFA walk (and the wide walk's private memory)
+template <bool kNfa>
+__device__ __forceinline__ bool rx_part(const mxp_list_args& A, uint32_t k, const uint8_t* s, uint32_t n) {
+    if constexpr (kNfa)
+        return mxp_rx_run(A.rx, k, s, n);
+    else
+        return mxp_dfa_run(A.rx, k, s, n);
+}
+
+template <bool kNfa>
+__device__ __forceinline__ void list_body(const mxp_list_args& A) {
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
     if (q >= A.n) return;
     const uint8_t* s;
@@ -179,19 +190,22 @@ extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args 
         found = ip_member(A, ip);
     } else if (A.type == MXP_LIST_REGEX) {
         found = false;  // regexList.checkList: any pattern matches (any part's automaton)
-        for (uint32_t k = 0; k < A.rx_n && !found; k++) found = mxp_rx_run(A.rx, k, s, n);
+        for (uint32_t k = 0; k < A.rx_n && !found; k++) found = rx_part<kNfa>(A, k, s, n);
     } else {
         found = string_member(A, s, n, A.type == MXP_LIST_CASE_INSENSITIVE_STRINGS);
     }
     list_decide(A, q, found);
 }
+extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args A) { list_body<false>(A); }
+extern "C" __global__ __launch_bounds__(256) void mxp_list_nfa_kernel(mxp_list_args A) { list_body<true>(A); }
 
 // REGEX lists with LDS-staged automata: each 1024-thread workgroup copies the hot rows of the parts'
 // DFAs (the first lds_states[k] states in BFS order from the start: the shallow levels every lookup
 // steps through) and their ASCII class maps into LDS once, then strides over the lookups; a lane
 // steps from LDS while its state is staged and from global memory below that.  Two workgroups fill
 // a CU's 32 wave slots while sharing one staged copy per 16 waves.
-extern "C" __global__ __launch_bounds__(1024) void mxp_list_rx_kernel(mxp_list_args A) {
+template <bool kNfa>
+__device__ __forceinline__ void list_rx_body(const mxp_list_args& A) {
     __shared__ uint32_t TL[MXP_LDS_DFA_WORDS];
     __shared__ uint16_t AL[MXP_LDS_DFA_PARTS * 128u];
     const uint32_t tid = threadIdx.x;
@@ -214,21 +228,24 @@ extern "C" __global__ __launch_bounds__(1024) void mxp_list_rx_kernel(mxp_list_a
                 const mxp_dfa_hdr H = A.rx.hdr[k];
                 found = mxp_dfa_walk<true>(A.rx, H, TL + A.lds_plan[MXP_LDS_DFA_PARTS + k], AL + k * 128u, K, s, n);
             } else {
-                found = mxp_rx_run(A.rx, k, s, n);
+                found = rx_part<kNfa>(A, k, s, n);
             }
         }
         list_decide(A, q, found);
     }
 }
+extern "C" __global__ __launch_bounds__(1024) void mxp_list_rx_kernel(mxp_list_args A) { list_rx_body<false>(A); }
+extern "C" __global__ __launch_bounds__(1024) void mxp_list_rx_nfa_kernel(mxp_list_args A) { list_rx_body<true>(A); }
 
 extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s) {
     if (a->type == MXP_LIST_REGEX && a->lds_nparts) {
         // enough workgroups for 2 per CU (256 CUs), fewer for small batches
         const uint32_t need = (a->n + MXP_LIST_RX_THREADS - 1u) / MXP_LIST_RX_THREADS;
         const uint32_t grid = need < 512u ? need : 512u;
-        hipLaunchKernelGGL(mxp_list_rx_kernel, dim3(grid), dim3(MXP_LIST_RX_THREADS), 0, s, *a);
+        hipLaunchKernelGGL(a->rx_nfa ? mxp_list_rx_nfa_kernel : mxp_list_rx_kernel, dim3(grid), dim3(MXP_LIST_RX_THREADS),
+                           0, s, *a);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(mxp_list_kernel, dim3((a->n + 255u) / 256u), dim3(256), 0, s, *a);
+    hipLaunchKernelGGL(a->rx_nfa ? mxp_list_nfa_kernel : mxp_list_kernel, dim3((a->n + 255u) / 256u), dim3(256), 0, s, *a);
     return hipGetLastError();
 }

@@ -1073,7 +1073,7 @@ bool nfa_match_host(const Dfa& d, const std::string& s) {
     const uint64_t* acc = N + MXP_NFA_HDR_WORDS;
     const uint64_t* cl = acc + (size_t)(d.ncls - 1) * W;
     const uint64_t* cls0 = cl + (size_t)m * nvar * W;
-    uint64_t U[MXP_NFA_MAX_WORDS] = {0, 0, 0, 0};
+    std::vector<uint64_t> U(W, 0), C(W, 0);
     bool begin = true, prev_nl = false, prev_word = false;
     for (size_t i = 0;;) {
         const bool end = i >= s.size();
@@ -1086,7 +1086,6 @@ bool nfa_match_host(const Dfa& d, const std::string& s) {
         if (!end && r == '\n') f |= END_LINE;
         f |= (prev_word != (!end && is_word(r))) ? WORD_B : NO_WORD_B;
         const uint32_t v = var_of[f];
-        uint64_t C[MXP_NFA_MAX_WORDS] = {0, 0, 0, 0};
         for (uint32_t x = 0; x < W; x++) C[x] = cls0[(size_t)v * W + x];
         for (uint32_t j = 0; j < m; j++)
             if (U[j / 64] >> (j % 64) & 1)

@@ -44,7 +44,7 @@ struct Dfa {
     bool is_nfa() const { return !nfa.empty(); }
 };
 
-constexpr uint32_t kNfaMaxPos = 255;  // rune instructions (+ the MATCH bit = 256 bits, 4 words)
+constexpr uint32_t kNfaMaxPos = 1023;  // rune instructions (+ the MATCH bit = 1024 bits, MXP_NFA_WIDE_WORDS words)
 
 enum RegexStatus { RX_OK = 0, RX_SYNTAX = 1, RX_UNSUPPORTED = 2, RX_TOO_BIG = 3 };
 

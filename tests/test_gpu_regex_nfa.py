@@ -55,14 +55,35 @@ def test_over_budget_rules_parity(mxp, monkeypatch, flags):
     assert (want == 1).sum() > 100 and 0 < (want[:, 0] == 1).sum() < batch.n
 
 
-def test_nfa_width_limit_is_a_rule_error(mxp):
-    """Over budget and wider than 255 rune instructions: the rule is refused with that reason."""
-    manifest = {"request.path": "STRING"}
+@pytest.mark.parametrize("flags", ["0", "262144"])
+def test_wide_nfa_rules_parity(mxp, monkeypatch, flags):
+    """Over budget and wider than 255 rune instructions (the last refusal of round 3): the wide
+    NFA walk (dfa_dev.h mxp_nfa_run_wide, thread sets in private memory) as a rule constant, through
+    value classes (262144) and as a run-time pattern, against the oracle's Go regexp restatement;
+    a list of such patterns too.  Only programs wider than 1023 rune instructions stay refused."""
+    from test_regex_product import wide_subjects
+    monkeypatch.setenv("MXP_DEBUG_FLAGS", flags)
+    rng = np.random.default_rng(61)
+    tail = "c" * 260
+    p = "(a|b)*a(a|b){16}" + tail
+    subs = wide_subjects(rng, 1200, tail) + _nfa_subjects(rng, 300)
+    manifest = {"request.path": "STRING", "x": "STRING"}
+    bags = [{"request.path": s, "x": p if i % 2 else "^a"} for i, s in enumerate(subs)]
+    batch = BagBatch.from_bags(bags, names=list(manifest))
+    rules = ['"%s".matches(request.path)' % p, 'x.matches(request.path)', 'request.path == "a"',
+             '"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 1100)]
     eng = mxp.Engine(0)
     eng.set_vocabulary(manifest)
-    st = eng.compile(['"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 260), 'request.path == "a"'])
-    assert st[0] != 0 and st[1] == 0
-    assert "NFA" in eng.rule_error(0)
+    st = eng.compile(rules)
+    assert (st[:3] == 0).all() and st[3] != 0 and "NFA" in eng.rule_error(3)
+    eng3 = mxp.Engine(0)
+    eng3.set_vocabulary(manifest)
+    assert (eng3.compile(rules[:3]) == 0).all()
+    got, want = compare(eng3, oracle.OracleEvaluator(manifest), rules[:3], batch, sample_msgs=50)
+    assert 100 < (want[:, 0] == 1).sum() < batch.n - 100
+    lst = eng3.list_create(L.REGEX, ["^zz", p], [])
+    want_l = L.codes(L.RegexList(["^zz", p]).found(subs[:400]), False)
+    assert np.array_equal(lst.check(subs[:400]), want_l)
 
 
 def test_regex_list_with_over_budget_patterns(mxp):

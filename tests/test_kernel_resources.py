@@ -21,6 +21,13 @@ MIN_OCCUPANCY = {"mxp_index_dtp_lite_kernel": 6, "mxp_guard_kernel": 8, "mxp_gua
 # still measured faster, C2 0.562 -> 0.532 ms same-box, profiles/r3_v2_ab_*.log)
 MAX_SCRATCH = {"mxp_index_kernel": 56, "mxp_index_dtp_kernel": 24, "mxp_index5_kernel": 24,
                "mxp_index_prof_kernel": 96, "mxp_index_dtp_prof_kernel": 96, "mxp_index_dtp_lite_kernel": 0}
+# the NFA instantiations (launched only for rule sets / lists with over-budget patterns): the wide NFA
+# walk keeps its two 1024-bit thread sets in private memory (dfa_dev.h mxp_nfa_run_wide) rather than
+# 64 VGPRs every NFA kernel would carry
+# (the referenced-attribute instantiations include the NFA walk too)
+MAX_SCRATCH.update({k: 288 for k in ("mxp_eval_nfa_kernel", "mxp_eval_deep_nfa_kernel", "mxp_index_nfa_kernel",
+                                     "mxp_vt_eval_nfa_kernel", "mxp_list_nfa_kernel", "mxp_list_rx_nfa_kernel",
+                                     "mxp_eval_refs_kernel", "mxp_eval_deep_refs_kernel", "mxp_index_refs_kernel")})
 
 
 def resource_usage(src):

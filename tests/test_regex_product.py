@@ -110,10 +110,35 @@ def test_over_budget_patterns_walk_the_nfa(rx):
         assert 0 < n_true < len(subs), p
 
 
-def test_nfa_width_limit(rx):
-    """Over budget AND more than 255 rune instructions: the one refusal left (-3, err says why)."""
-    p = "(a|b)*a(a|b){16}" + "c" * 260
-    rc, err = rx(p, "ab")
+def wide_subjects(rng, n, tail):
+    """Subjects for the wide-NFA patterns `(a|b)*a(a|b){16}` + tail: half built to match."""
+    out = []
+    for i in range(n):
+        s = "".join(rng.choice(["a", "b"], size=int(rng.integers(0, 20)))) + "a"
+        s += "".join(rng.choice(["a", "b"], size=16)) + tail
+        if i % 2:  # a near miss: a wrong byte somewhere in the tail, or the tail cut short
+            k = int(rng.integers(0, len(tail) + 1))
+            s = s[:len(s) - len(tail) + k] + ("x" if i % 4 == 1 else "")
+        out.append(s)
+    return out
+
+
+def test_nfa_wide_programs(rx):
+    """Over budget and wider than 255 rune instructions: the wide NFA walk (private-memory thread
+    sets, up to 1023 rune instructions) against the oracle; only a program wider than that is
+    refused (-3, err says why)."""
+    import oracle
+    rng = np.random.default_rng(19)
+    for tail in ("c" * 260, "cd" * 300 + "e" * 200):
+        p = "(a|b)*a(a|b){16}" + tail
+        subs = wide_subjects(rng, 60, tail)
+        hits = 0
+        for sub in subs:
+            want = oracle.regex_match(p, sub)
+            assert rx(p, sub) == want, (p[:30], sub[:40])
+            hits += want[0]
+        assert 0 < hits < len(subs)
+    rc, err = rx("(a|b)*a(a|b){16}" + "c" * 1100, "ab")
     assert rc == -3 and "NFA" in err
 
 
@@ -124,7 +149,8 @@ def test_over_budget_rules_compile(libmxp):
     eng = Engine(-1)
     eng.set_vocabulary({"request.path": "STRING"})
     rules = ['"%s".matches(request.path)' % p.replace("\\", "\\\\") for p in NFA_PATTERNS]
-    rules.append('"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 260))
+    rules.append('"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 260))   # wide NFA: compiles
+    rules.append('"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 1100))  # wider than 1023: refused
     st = eng.compile(rules)
     assert (st[:-1] == 0).all(), [eng.rule_error(i) for i in range(len(rules) - 1) if st[i]]
     assert st[-1] != 0 and "NFA" in eng.rule_error(len(rules) - 1)
