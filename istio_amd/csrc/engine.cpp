@@ -92,6 +92,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         std::string prefix;
     };
     std::vector<RxPrefixed> rx_prefixed;  // regexp rules guarded by their literal prefix
+    rx_keys_h.assign(n, {});
     for (uint32_t i = 0; i < n; i++) {
         std::vector<mxp_vm_ins> code(all.begin() + off[i], all.begin() + off[i + 1]);
         guards[i] = mxp::extract_guard(code);
@@ -204,6 +205,16 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
             b += w;
         }
         if (st == mxp::kDfaReject) continue;
+        // a few literal continuations decide the match (`^/p(/.*)?$`: the subject is /p, or starts
+        // with /p/): direct postings on the full keys, exact-length ones where the subject must end
+        // (MXP_DEBUG_FLAGS 67108864: keep the DFA template -- A/B)
+        std::vector<mxp::LiteralKey> keys;
+        if (!(debug_flags & 67108864u) && n < (1u << 23) && mxp::dfa_literal_keys(d, st, 8, 8, &keys)) {
+            auto& rk = rx_keys_h[rp.rule];
+            for (const auto& k : keys) rk.push_back({intern_string(rp.prefix + k.bytes), k.exact ? 1u : 0u});
+            guards[rp.rule].mode = GM_ONLY | GT_PREFIX;
+            continue;
+        }
         mxp_dfa_hdr h = rx_set.hdr[rp.dfa];
         h.start = st == mxp::kDfaAccept ? 0u : st;
         h.skip = st == mxp::kDfaAccept ? MXP_DFA_DECIDED : (uint32_t)rp.prefix.size();
@@ -413,6 +424,10 @@ int mxp_engine::build_plan(Plan& P) {
             P.n_composite++;
             continue;
         }
+        if (!rx_keys_h[i].empty()) {  // a literal-key regexp rule: one posting per key
+            for (const auto& k : rx_keys_h[i]) index_of[{gd.col, true}][k.first].push_back(i | ((uint32_t)k.second << 31));
+            continue;
+        }
         index_of[{gd.col, prefix}][k1].push_back(i);
     }
     P.n_tmpls = (uint32_t)tmpls.size();
@@ -430,10 +445,13 @@ int mxp_engine::build_plan(Plan& P) {
     // postings carry their rule's continuation template (rule | code << 23; code 511 direct, 510
     // look it up): the index kernel then loads no template id per posting or per pair
     P.post_tmpl = n < (1u << 23);
+    // (code 509: a literal-key regexp rule's exact key -- true only when the subject ends at the key;
+    // a rule id with bit 31 set in `rs` is such a posting)
     auto post = [&](const std::vector<uint32_t>& rs, const std::vector<uint32_t>& tmpl_of) {
         for (uint32_t r : rs) {
-            const uint32_t t = tmpl_of[r];
-            postings.push_back(!P.post_tmpl ? r : r | (t == MXP_TMPL_DIRECT ? 511u : t < 510u ? t : 510u) << 23);
+            const uint32_t rr = r & 0x7FFFFFFFu, t = tmpl_of[rr];
+            postings.push_back(!P.post_tmpl ? rr
+                                            : rr | ((r >> 31) ? 509u : t == MXP_TMPL_DIRECT ? 511u : t < 509u ? t : 510u) << 23);
         }
     };
     // open-addressing table of `groups` (key -> rules) at hents[hoff ..): returns hmask
@@ -473,7 +491,9 @@ int mxp_engine::build_plan(Plan& P) {
         std::set<uint32_t> lens;
         for (auto& kv : ci.second) {
             std::vector<uint32_t> rs = kv.second;
-            std::stable_sort(rs.begin(), rs.end(), [&](uint32_t a, uint32_t b) { return rule_tmpl[a] < rule_tmpl[b]; });
+            std::stable_sort(rs.begin(), rs.end(), [&](uint32_t a, uint32_t b) {
+                return rule_tmpl[a & 0x7FFFFFFFu] < rule_tmpl[b & 0x7FFFFFFFu];
+            });
             // hash of the key bytes, as the kernel hashes the request's leading bytes
             const std::string& key = gstrs[(uint32_t)kv.first];
             lens.insert((uint32_t)key.size());

@@ -241,6 +241,10 @@ struct mxp_engine : public mxp::LowerTables {
     std::vector<mxp_vm_ins> prog_h;    // host copies the plans are built from
     std::vector<uint32_t> off_h;
     std::vector<mxp_guard> guards_h;   // leading-atom guards before any plan drops a prefix guard
+    // prefix-guarded regexp rules whose DFA after the literal prefix is a few literal keys
+    // (regex.h dfa_literal_keys): the prefix index serves them as direct postings, one per key
+    // (string id, exact: the subject must END there), with no VM pass
+    std::vector<std::vector<std::pair<uint32_t, uint8_t>>> rx_keys_h;
     std::vector<uint32_t> rule_tmpl_h;
     std::vector<mxp_tmpl> tmpls_h;
     uint32_t n_guarded = 0, n_templated = 0;

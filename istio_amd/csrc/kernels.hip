@@ -1927,10 +1927,12 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
 // never overflows, one lane's long list fills whole batches (C2: a request without a path takes its
 // service's ~39 equality postings in one round, not ten rounds of four), and the VM has one call
 // site (one inlined copy).
+// `exact`: the probed string ends at this slot's key length (code-509 postings -- a literal-key
+// regexp rule's exact keys -- are true pairs only then)
 template <bool kRefs, bool kNfa, bool kDtp, bool kProf = false, bool kLite = false>
 __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, uint32_t tbl, uint32_t start,
                                              uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
-                                             uint32_t tid) {
+                                             uint32_t tid, bool exact = false) {
     const uint32_t lane = tid & 63u;
     const uint32_t* __restrict__ tmpl_of = tbl ? A.rule_tmpl2 : A.rule_tmpl;
     uint32_t j0 = 0;
@@ -1955,13 +1957,16 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
                     if (A.post_tmpl) {  // the template rides in the posting (kargs.postings)
                         rule = pe & 0x7FFFFFu;
                         const uint32_t code = pe >> 23;
-                        t = code == 511u ? MXP_TMPL_DIRECT : code == 510u ? tmpl_of[rule] : code;
+                        t = code == 511u ? MXP_TMPL_DIRECT : code == 510u ? tmpl_of[rule]
+                          : code == 509u ? (exact ? MXP_TMPL_DIRECT : MXP_TMPL_SKIP) : code;
                     } else {
                         t = tmpl_of[rule];
                     }
                     uint32_t e = rule | (tbl << 31);
                     if (t == MXP_TMPL_DIRECT) {
                         Q.ntrue += pair_true<kDtp>(A, Q, rule, req);
+                        e = 0xFFFFFFFFu;
+                    } else if (t == MXP_TMPL_SKIP) {
                         e = 0xFFFFFFFFu;
                     }
                     // (entry: rule | table, then the request's lane in the wave | template << 8)
@@ -2192,7 +2197,9 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 continue;
             }
             if (final || __ballot(len != 0))
-                process_slot<kRefs, kNfa, kDtp, kProf, kLite>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid);
+                process_slot<kRefs, kNfa, kDtp, kProf, kLite>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid,
+                                                              kind == MXP_IX_PREFIX && !eq_slot && !final &&
+                                                                  s.n == uni(A.plens[plen0 + p]));
             if (kProf && (tid & 63u) == 0 && (final || nmark < 4u)) {  // profiling: phase marks
                 A.wave_t[8ull * tile + 3u + (final ? 4u : nmark)] = (uint64_t)wall_clock64();
                 nmark++;

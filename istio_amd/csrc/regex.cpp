@@ -1139,6 +1139,50 @@ void fold_dead_states(Dfa* d) {
         if (t < N) t = sure[t] ? kDfaAccept : !live[t] ? kDfaReject : t;
 }
 
+bool dfa_literal_keys(const Dfa& d, uint32_t st, uint32_t max_keys, uint32_t max_depth, std::vector<LiteralKey>* out) {
+    out->clear();
+    if (d.is_nfa() || st == kDfaReject) return false;
+    if (st == kDfaAccept) {
+        out->push_back({"", false});
+        return true;
+    }
+    const uint32_t C = d.ncls;
+    // non-ASCII runes (and invalid bytes, U+FFFD) must not lead anywhere but REJECT from the states
+    // the enumeration visits: their keys would be multi-byte runes
+    auto hi_dead = [&](uint32_t s) {
+        for (uint16_t c : d.hi_cls)
+            if (d.trans[(size_t)s * C + c] != kDfaReject) return false;
+        return true;
+    };
+    struct Item {
+        uint32_t s;
+        std::string w;
+    };
+    std::vector<Item> level{{st, ""}};
+    for (uint32_t depth = 0; !level.empty(); depth++) {
+        std::vector<Item> next;
+        for (const Item& it : level) {
+            if (!hi_dead(it.s)) return false;
+            if (d.trans[(size_t)it.s * C + C - 1] == kDfaAccept) out->push_back({it.w, true});
+            for (uint32_t b = 0; b < 128; b++) {
+                const uint32_t t = d.trans[(size_t)it.s * C + d.ascii[b]];
+                if (t == kDfaReject) continue;
+                std::string w = it.w;
+                w.push_back((char)b);
+                if (t == kDfaAccept) {
+                    out->push_back({w, false});
+                } else {
+                    if (depth + 1 >= max_depth) return false;
+                    next.push_back({t, w});
+                }
+                if (out->size() + next.size() > max_keys) return false;
+            }
+        }
+        level.swap(next);
+    }
+    return out->size() <= max_keys;
+}
+
 bool dfa_match_host(const Dfa& d, const std::string& s) {
     if (d.is_nfa()) return nfa_match_host(d, s);
     uint32_t st = d.start;

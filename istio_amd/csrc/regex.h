@@ -15,8 +15,9 @@
 //             The start thread is re-injected at every position (unanchored search), and a step
 //             whose closure reaches MATCH goes to the absorbing ACCEPT state.
 //
-// Unsupported (reported, never approximated): Unicode classes \p / \P and case folding of non-ASCII
-// letters (both need Unicode tables), and DFAs beyond the state budget.
+// Unicode classes (\p / \P) and simple case folding come from Go 1.9's Unicode 9.0 tables
+// (unicode_tables.h); a DFA beyond the state budget becomes a bit-parallel NFA (dfa_dev.h); only a
+// program wider than kNfaMaxPos rune instructions whose DFA is also over budget is refused.
 #pragma once
 
 #include <cstdint>
@@ -58,6 +59,18 @@ int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states,
 // A pattern anchored at text begin (^ without (?m), or \A) followed by literal runes only matches
 // subjects that start with those runes' UTF-8 bytes: the engine indexes such rules by that prefix.
 bool regex_required_prefix(const std::string& pattern, std::string* prefix);
+
+// The language a DFA accepts from state `st` as a few literal keys, when it is that simple: every
+// path from `st` reaches a decision within `max_depth` ASCII bytes (no non-ASCII class leads anywhere
+// but REJECT), giving `prefix` keys (a folded ACCEPT transition: any continuation matches) and
+// `exact` keys (a state whose END transition accepts: the subject ends there).  A subject read from
+// `st` is accepted iff it starts with a prefix key or equals an exact key, and at most one key fits
+// any subject.  False when there are more than `max_keys` keys or a path is undecided at max_depth.
+struct LiteralKey {
+    std::string bytes;
+    bool exact;
+};
+bool dfa_literal_keys(const Dfa& d, uint32_t st, uint32_t max_keys, uint32_t max_depth, std::vector<LiteralKey>* out);
 
 // Host stepping of a compiled DFA or NFA (constant folding, tests).
 bool dfa_match_host(const Dfa& d, const std::string& s);

@@ -175,6 +175,8 @@ typedef struct mxp_fill {
 // kargs.rule_tmpl value of indexed rules whose atom IS the result (`col.startsWith(K)` alone): a
 // posting is a true pair, no continuation to run
 #define MXP_TMPL_DIRECT 0xFFFFFFFEu
+// ... a code-509 posting (a literal-key regexp rule's exact key) whose subject does not end there
+#define MXP_TMPL_SKIP 0xFFFFFFFDu
 
 #if defined(__HIPCC__)
 #define MXP_HD __host__ __device__

@@ -625,3 +625,44 @@ def test_deep_continuation_guard_parity(mxp, knobs, monkeypatch):
     ev = oracle.OracleEvaluator(W.DEFAULT_TEST_MANIFEST)
     got, want = compare(eng, ev, rules, batch)
     assert (want[:, :64] == 1).sum() > 100 and (want[:, 72:] == 1).sum() > 100
+
+
+@pytest.mark.parametrize("flags", ["0", "67108864", "8"])
+def test_literal_key_regexp_rules(mxp, monkeypatch, flags):
+    """Prefix-guarded regexp rules whose DFA after the literal prefix is a few literal keys become
+    direct postings of the prefix index -- prefix keys (any continuation matches) and exact keys (the
+    subject ends there) -- with no VM pass (regex.cpp dfa_literal_keys); 67108864 keeps the DFA
+    templates, 8 turns the index off.  Subjects around every boundary: the prefix alone, one byte
+    more or less, the continuation bytes, non-ASCII and invalid UTF-8 after the prefix."""
+    monkeypatch.setenv("MXP_DEBUG_FLAGS", flags)
+    pats = ["^/p(/.*)?$", "^/p[0-9a-z/]*", "^/q$", "^/q(a|bc)$", "^/r[0-9]?$", "^/s(/x|/y.*)", "^/t.{0,2}$",
+            "^/u(é|e)$", "^/v\\b", "^/w(?:x|$)", "^/p/", "^/pa(b|$)"]
+    rules = ['"%s".matches(request.path)' % p.replace("\\", "\\\\") for p in pats]
+    rules += ['request.path.startsWith("/p")', 'request.path == "/q"']
+    tails = ["", "/", "/x", "/y", "/yy", "a", "b", "bc", "bcd", "0", "9", "09", "x", "é", "e", "\udcff", "\udcc3",
+             "/é", " ", "-", "ab", "abc"]
+    rng = np.random.default_rng(71)
+    heads = ["/p", "/q", "/r", "/s", "/t", "/u", "/v", "/w", "/pa", "/", "", "/P"]
+    paths = [h + t for h in heads for t in tails]
+    bags = [{"request.path": p} for p in paths] + [{}] + [{"request.path": 7}]
+    bags += [{"request.path": heads[int(rng.integers(0, len(heads)))] + tails[int(rng.integers(0, len(tails)))]
+              + tails[int(rng.integers(0, len(tails)))]} for _ in range(3000)]
+    manifest = {"request.path": "STRING"}
+    batch = BagBatch.from_bags(bags, names=list(manifest))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    got, want = compare(eng, oracle.OracleEvaluator(manifest), rules, batch)
+    assert all(0 < (want[:, j] == 1).sum() < batch.n for j in range(len(pats)))
+    # the device path (deferred pairs, fused hit counters) agrees with the bitmaps' true bits
+    import torch
+    db = eng.upload(batch)
+    Wd = (len(rules) + 31) // 32
+    dm = torch.zeros((Wd, batch.n), dtype=torch.int32, device="cuda:0")
+    flags_t = torch.zeros(batch.n, dtype=torch.uint8, device="cuda:0")
+    hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
+    for _ in range(2):
+        db.eval_compact(dm.data_ptr(), flags_t.data_ptr(), hits.data_ptr(), 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(hits.cpu().numpy(), 2 * (want == 1).sum(axis=0))
+    db.free()
