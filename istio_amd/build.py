@@ -32,6 +32,9 @@ def _stale():
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    # MXP_NO_BUILD=1 (GPU session scripts): use the library as shipped, whatever the sources' times
+    if not force and os.environ.get("MXP_NO_BUILD") == "1" and os.path.exists(LIB):
+        return LIB
     if not force and not _stale():
         return LIB
     # one builder at a time (the ranks of a multi-GPU bench all call build()): the others wait on

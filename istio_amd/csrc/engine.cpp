@@ -1439,8 +1439,7 @@ int mxp_engine::pack_heads(mxp_dbatch* db) {
     A.bstr = db->bstr.as<uint8_t>();
     if ((e = mxp_launch_heads(&A, d_head_cols.as<uint32_t>(), nrow, db->heads.as<uint4>(), stream)) != hipSuccess)
         return hipfail(e, "launch heads");
-    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "heads sync");
-    db->heads_ncol = nrow;
+    db->heads_ncol = nrow;  // (pack() synchronises once, after the dictionary)
     return MXP_OK;
 }
 
@@ -1462,8 +1461,20 @@ int mxp_engine::pack_dict(mxp_dbatch* db) {
     fill_args(&A, db, *P);
     A.q0 = 0;
     A.q1 = db->n;
-    if ((e = mxp_launch_vt_classify(&A, stream)) != hipSuccess) return hipfail(e, "launch vt classify");
-    if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "vt dictionary sync");
+    if (db->vtd_ready && !(debug_flags & 134217728u)) {
+        // the device packer's two-level dictionary (pack.hip mxp_pack_vtd_*): its provisional tables
+        // into the final ones (MXP_DEBUG_FLAGS 134217728: the one-level classify kernel -- A/B)
+        mxp_vtd_final_args F;
+        memset(&F, 0, sizeof F);
+        F.tkey = pk_vtd_tkey.as<unsigned long long>();
+        F.tcr = pk_vtd_tcr.as<uint2>();
+        uint32_t a = 0;
+        for (uint32_t s = 0; s < vt_cand_col.size() && a < MXP_VT_MAX; s++)
+            if ((db->vt_mask >> s) & 1u) F.cand[a++] = s;
+        if ((e = mxp_launch_vtd_final(&A, &F, stream)) != hipSuccess) return hipfail(e, "launch vt final");
+    } else if ((e = mxp_launch_vt_classify(&A, stream)) != hipSuccess) {
+        return hipfail(e, "launch vt classify");
+    }
     return MXP_OK;
 }
 

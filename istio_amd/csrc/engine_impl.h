@@ -26,6 +26,7 @@
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
+extern "C" hipError_t mxp_launch_vtd_final(const mxp_kargs* args, const mxp_vtd_final_args* f, hipStream_t s);
 extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, const uint32_t* cols, uint32_t nrow, uint4* heads, hipStream_t s);
 extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_fill(const mxp_kargs* args, uint32_t n_fills, hipStream_t s);
@@ -148,6 +149,7 @@ struct mxp_dbatch {
     // byte strings GB + item, canonical GC + item, times GT + item (items: batch strings / times
     // first, then parsed ip() / timestamp() values by string id) -- read back on demand
     bool dev_packed = false;
+    bool vtd_ready = false;  // the packer's provisional class tables (engine scratch) hold this batch's
     uint32_t ns = 0, nt = 0, G = 0, GB = 0, GC = 0, GT = 0;
     DevBuf pip, pip_ok, pts_sec, pts_nsec, pts_ok, btsec, btnsec;
     size_t overlay_strings() const { return dev_packed ? ns : overlay.size(); }
@@ -577,7 +579,11 @@ struct mxp_engine : public mxp::LowerTables {
     int pack(const mxp_bag_batch* b, mxp_dbatch* db) {
         int rc = host_pack ? pack_on_host(b, db) : pack_device(b, db);
         if (!rc) rc = pack_heads(db);
-        return rc ? rc : pack_dict(db);
+        if (!rc) rc = pack_dict(db);
+        // the batch is complete when the call returns (evaluations run on the caller's streams)
+        hipError_t e;
+        if (!rc && (e = hipStreamSynchronize(stream)) != hipSuccess) rc = hipfail(e, "pack sync");
+        return rc;
     }
     int pack_dict(mxp_dbatch* db);   // the value-class dictionary of the batch (mxp_vt_classify_kernel)
     int pack_heads(mxp_dbatch* db);  // kargs.heads of the probed columns (MXP_HEADS=0: none)
@@ -602,8 +608,8 @@ struct mxp_engine : public mxp::LowerTables {
     // device packer scratch, reused across uploads
     DevBuf pk_soff, pk_sbytes, pk_tsec, pk_tnsec, pk_moff, pk_mkey, pk_mval, pk_ck[64], pk_cv[64];
     DevBuf pk_sid, pk_braw, pk_bcan, pk_tid, pk_use, pk_maxlen, pk_tab[4], pk_scan, pk_scan_blocks;
-    DevBuf pk_vt_bits, pk_vt_cnt, pk_rx, pk_rxv;
-    void* pk_host = nullptr;  // pinned read-back (longest string, value-class counts)
+    DevBuf pk_vtd_lkey, pk_vtd_lcr, pk_vtd_ln, pk_vtd_tkey, pk_vtd_tcr, pk_vtd_meta, pk_rx, pk_rxv;
+    void* pk_host = nullptr;  // pinned read-back (longest string, value-class distinct counts)
     uint32_t vcol_key_id(uint32_t j) const {
         auto it = gstr_ids.find(vcols[j].second);
         return it == gstr_ids.end() ? 0xFFFFFFFEu : it->second;

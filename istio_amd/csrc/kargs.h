@@ -133,3 +133,11 @@ typedef struct mxp_kargs {
     // and bytes (two dependent scattered loads per request)
     const uint4* heads;
 } mxp_kargs;
+
+// mxp_vtd_final_kernel: the packer's provisional class tables and the candidate column of each
+// active value-class slot
+typedef struct mxp_vtd_final_args {
+    const unsigned long long* tkey;
+    const uint2* tcr;
+    uint32_t cand[MXP_VT_MAX];
+} mxp_vtd_final_args;

@@ -19,6 +19,7 @@
 
 #include "../../include/mxp_batch.h"
 #include "kargs.h"
+#include "pack_args.h"
 #include "vm.h"
 
 namespace {
@@ -1112,6 +1113,30 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_classify_kernel(mxp_kar
         (void)loc;  // (the classes of the requests are the evaluation's: mxp_vt_lookup_kernel)
         __syncthreads();
     }
+}
+
+// The batch's final class tables from the packer's provisional ones (pack.hip mxp_pack_vtd_*): every
+// key of active slot a (candidate column F.cand[a]) into its table of the capacity the host sized
+// (the keys are distinct: a compare-and-swap on an empty slot, probing on), with its class size
+// and representative request.  grid (MXP_VTD_CAP / 256, active slots).
+extern "C" __global__ __launch_bounds__(256) void mxp_vtd_final_kernel(mxp_kargs A, mxp_vtd_final_args F) {
+    const uint32_t a = blockIdx.y, i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= MXP_VTD_CAP) return;
+    const uint64_t at = (uint64_t)F.cand[a] * MXP_VTD_CAP + i;
+    const unsigned long long key = F.tkey[at];
+    if (key == MXP_VT_EMPTY) return;
+    const uint32_t cap = A.vt_meta[a * 8u + MXP_VTM_CAP], kb = A.vt_meta[a * 8u + MXP_VTM_KBASE];
+    unsigned long long* T = A.vt_keys + kb;
+    uint32_t h = mxp_hash64(key) & (cap - 1u);
+    while (atomicCAS(T + h, (unsigned long long)MXP_VT_EMPTY, key) != MXP_VT_EMPTY) h = (h + 1u) & (cap - 1u);
+    const uint2 cr = F.tcr[at];
+    A.vt_rep[kb + h] = cr.y;
+    A.vt_cnt[kb + h] = cr.x;
+}
+
+extern "C" hipError_t mxp_launch_vtd_final(const mxp_kargs* args, const mxp_vtd_final_args* f, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_vtd_final_kernel, dim3(MXP_VTD_CAP / 256u, args->n_vt), dim3(256), 0, s, *args, *f);
+    return hipGetLastError();
 }
 
 // The evaluation's class of every request [q0, q1) per active column: a read-only probe of the

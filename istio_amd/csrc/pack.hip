@@ -90,17 +90,55 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_mark_kernel(mxp_pack_
 // the batch table -- a CAS on an empty slot makes the item its content's representative; an
 // occupied slot with the same hash tag is compared byte by byte (the items are immutable input,
 // so a winner's content is readable without further ordering).  id = base + representative.
+// Strings (MXP_IK_STR) hash and compare 8 bytes at a time (the batch blob and the pools carry 16
+// bytes of slack); the longest length is a wave maximum, one atomic per wave (a per-string atomic
+// on one address serialised every wave of the pass behind it).
+__device__ __forceinline__ uint64_t ld8_any(const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7) * 8u;
+    const uint64_t lo = q[0];
+    return sh == 0 ? lo : (lo >> sh) | (q[1] << (64u - sh));
+}
+__device__ __forceinline__ uint64_t str_hash_words(const uint8_t* p, uint32_t n) {
+    uint64_t h = 0;
+    for (uint32_t i = 0; i < n; i += 8) {
+        const uint32_t r = n - i;
+        const uint64_t w = ld8_any(p + i) & (r >= 8u ? ~0ull : (1ull << (8u * r)) - 1ull);
+        h ^= w;
+        h *= 0x9E3779B97F4A7C15ull;
+        h ^= h >> 31;
+    }
+    h ^= (uint64_t)n * 0xC2B2AE3D27D4EB4Full;
+    h *= 0xFF51AFD7ED558CCDull;
+    return h ^ (h >> 33);
+}
+__device__ __forceinline__ bool same_words(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb) {
+    if (na != nb) return false;
+    for (uint32_t i = 0; i < na; i += 8) {
+        const uint32_t r = na - i;
+        const uint64_t m = r >= 8u ? ~0ull : (1ull << (8u * r)) - 1ull;
+        if ((ld8_any(a + i) ^ ld8_any(b + i)) & m) return false;
+    }
+    return true;
+}
+
 extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_kernel(mxp_pack_args A) {
     uint8_t buf[16], pbuf[16];
-    for (uint64_t idx = A.i0 + gtid(); idx < A.i1; idx += gstride()) {
+    const bool words = A.kind == MXP_IK_STR;
+    uint32_t maxlen = 0;
+    // (a uniform trip count per wave: the wave maximum below needs every lane)
+    for (uint64_t i0 = (A.i0 + gtid()) & ~63ull; i0 < A.i1; i0 += gstride()) {
+        const uint64_t idx = i0 + (threadIdx.x & 63u);
+        if (idx < A.i0 || idx >= A.i1) continue;
         const uint8_t* p;
         uint32_t n;
         if (!item_of(A, A.kind, idx, &p, &n, buf)) {
             A.out[idx] = kNone;
             continue;
         }
-        if (A.kind == MXP_IK_STR && A.max_len_out) atomicMax(A.max_len_out, n);
-        const uint64_t h = mxp_item_hash(p, n);
+        if (words) maxlen = max(maxlen, n);
+        const uint64_t h = words ? str_hash_words(p, n) : mxp_item_hash(p, n);
         const uint64_t tag = h >> 32;
         uint32_t id = kNone;
         if (A.pool.n) {
@@ -111,7 +149,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_kernel(mxp_pac
                 const uint8_t* q;
                 uint32_t m;
                 pool_item(A.pool, A.kind, (uint32_t)e - 1u, &q, &m, pbuf);
-                if (same(p, n, q, m)) {
+                if (words ? same_words(p, n, q, m) : same(p, n, q, m)) {
                     id = (uint32_t)e - 1u;
                     break;
                 }
@@ -133,13 +171,18 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_kernel(mxp_pac
                 const uint8_t* q;
                 uint32_t m;
                 item_of(A, A.kind, other, &q, &m, pbuf);
-                if (same(p, n, q, m)) {
+                if (words ? same_words(p, n, q, m) : same(p, n, q, m)) {
                     id = A.base + (uint32_t)other;
                     break;
                 }
             }
         }
         A.out[idx] = id;
+    }
+    if (words && A.max_len_out) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) maxlen = max(maxlen, (uint32_t)__shfl_xor((int)maxlen, off, 64));
+        if ((threadIdx.x & 63u) == 0 && maxlen) atomicMax(A.max_len_out, maxlen);
     }
 }
 
@@ -238,71 +281,147 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_copy_kernel(mxp_pack_
     }
 }
 
-// value classes: distinct string ids (bitmap over [0, S]) and other kinds of each candidate column.
-// Zipf-hot values put most requests on a few bitmap words, so a request only reaches the global
-// bitmap when nothing cheaper has seen its id: a per-workgroup LDS table of recently marked ids
-// (direct-mapped; racy stores only cost a redundant mark), then a plain load of the word (a set bit
-// is final, so a stale copy only costs a redundant atomic), then up to eight rounds of in-wave pooling
-// (the lanes whose ids share the first needing lane's word OR their bits into one atomic) before the
-// remaining lanes' own atomicOr.
-#define MXP_VT_MARK_LDS 2048u
-extern "C" __global__ __launch_bounds__(256) void mxp_pack_vt_mark_kernel(mxp_pack_args A) {
-    __shared__ uint32_t seen[MXP_VT_MARK_LDS];
-    const uint32_t a = blockIdx.y;
+// Value classes: the class dictionary of every candidate column, in two levels so that no hot key
+// meets more than MXP_VTD_MERGE global atomics (a column's few Zipf-hot values would otherwise take
+// one probe and one count atomic from every tile).
+// Level 1 (grid: tiles of MXP_VTD_TILE requests x candidate columns): the tile's distinct keys in an
+// LDS table -- a key's count added once per wave (ballot over the lanes holding it) -- then written
+// out as the tile's list (wave-compacted, plain stores).
+#define MXP_VTD_LCAP 2048u
+extern "C" __global__ __launch_bounds__(256) void mxp_pack_vtd_local_kernel(mxp_pack_args A) {
+    __shared__ unsigned long long lkey[MXP_VTD_LCAP];
+    __shared__ uint32_t lcnt[MXP_VTD_LCAP], lrep[MXP_VTD_LCAP];
+    __shared__ uint32_t nout;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, a = blockIdx.y, t = blockIdx.x;
     const uint32_t c = A.vt_col[a];
-    unsigned long long* bits = A.vt_bits + (uint64_t)a * (A.S / 64 + 1);
-    for (uint32_t i = threadIdx.x; i < MXP_VT_MARK_LDS; i += 256u) seen[i] = 0xFFFFFFFFu;
-    __syncthreads();
-    uint32_t km = 0;
-    // (uniform trip count per wave: the ballots below need every lane)
-    const uint64_t stride = gstride();
-    for (uint64_t r0 = gtid() & ~63ull; r0 < A.n; r0 += stride) {
-        const uint64_t r = r0 + (threadIdx.x & 63u);
-        bool need = false;
-        uint32_t x = 0;
-        if (r < A.n) {
-            const uint8_t k = A.kinds[(uint64_t)c * A.n + r];
-            if (k == 1u) {
-                const uint64_t v = A.vals[(uint64_t)c * A.n + r];
-                x = (uint32_t)(v < A.S ? v : A.S);
-                const uint32_t slot = (x * 0x9E3779B1u) >> (32 - 11);
-                if (seen[slot] != x) {
-                    seen[slot] = x;
-                    need = !(bits[x >> 6] & (1ull << (x & 63u)));
-                }
-            } else {
-                km |= 1u << (k & 31u);
-            }
-        }
-        // the lanes sharing the first needing lane's bitmap WORD pool their bits (consecutive
-        // interned ids -- a column of mostly distinct values -- put a whole wave on one word)
-        for (int round = 0; round < 8; round++) {
-            const uint64_t m = __ballot(need);
-            if (!m) break;
-            const uint32_t lead = (uint32_t)__builtin_ctzll(m);
-            const uint32_t w0 = (uint32_t)__shfl((int)(x >> 6), (int)lead, 64);
-            const bool same = need && (x >> 6) == w0;
-            uint32_t lo = same && (x & 63u) < 32u ? 1u << (x & 31u) : 0u;
-            uint32_t hi = same && (x & 63u) >= 32u ? 1u << (x & 31u) : 0u;
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                lo |= (uint32_t)__shfl_xor((int)lo, off, 64);
-                hi |= (uint32_t)__shfl_xor((int)hi, off, 64);
-            }
-            if ((threadIdx.x & 63u) == lead) atomicOr(bits + w0, (unsigned long long)hi << 32 | lo);
-            if (same) need = false;
-        }
-        if (need) atomicOr(bits + (x >> 6), 1ull << (x & 63u));
+    for (uint32_t i = tid; i < MXP_VTD_LCAP; i += 256u) {
+        lkey[i] = ~0ull;
+        lcnt[i] = 0u;
     }
-    if (km) atomicOr(A.vt_kmask + a, km);
+    if (tid == 0) nout = 0u;
+    __syncthreads();
+    const uint64_t base = (uint64_t)t * MXP_VTD_TILE;
+#pragma unroll
+    for (uint32_t r = 0; r < MXP_VTD_TILE / 256u; r++) {
+        const uint64_t req = base + tid + 256u * r;
+        uint32_t h = 0xFFFFFFFFu;
+        if (req < A.n) {
+            const unsigned long long key = mxp_vt_key(A.kinds[(uint64_t)c * A.n + req], A.vals[(uint64_t)c * A.n + req]);
+            h = (uint32_t)mxp_hash64(key) & (MXP_VTD_LCAP - 1u);
+            for (;;) {
+                const unsigned long long cur = lkey[h];
+                if (cur == key) break;
+                if (cur == ~0ull) {
+                    const unsigned long long old = atomicCAS(&lkey[h], ~0ull, key);
+                    if (old == ~0ull) {
+                        lrep[h] = (uint32_t)req;
+                        break;
+                    }
+                    if (old == key) break;
+                }
+                h = (h + 1u) & (MXP_VTD_LCAP - 1u);
+            }
+        }
+        for (uint64_t pend = __ballot(h != 0xFFFFFFFFu); pend;) {
+            const uint32_t sl = __builtin_amdgcn_readlane(h, (uint32_t)__builtin_ctzll(pend));
+            const uint64_t same = __ballot(h == sl);
+            if (lane == (uint32_t)__builtin_ctzll(same)) atomicAdd(&lcnt[sl], (uint32_t)__builtin_popcountll(same));
+            pend &= ~same;
+        }
+    }
+    __syncthreads();
+    const uint64_t lo = ((uint64_t)a * A.vtd_tiles + t) * MXP_VTD_TILE;
+    for (uint32_t i0 = 0; i0 < MXP_VTD_LCAP; i0 += 256u) {
+        const uint32_t i = i0 + tid;
+        const unsigned long long key = lkey[i];
+        const bool has = key != ~0ull;
+        const uint64_t m = __ballot(has);
+        uint32_t at = 0;
+        if (lane == 0 && m) at = atomicAdd(&nout, (uint32_t)__builtin_popcountll(m));
+        at = (uint32_t)__shfl((int)at, 0, 64) + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (has) {
+            A.vtd_lkey[lo + at] = key;
+            A.vtd_lcr[lo + at] = make_uint2(lcnt[i], lrep[i]);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) A.vtd_ln[(uint64_t)a * A.vtd_tiles + t] = nout;
 }
-extern "C" __global__ __launch_bounds__(256) void mxp_pack_vt_count_kernel(mxp_pack_args A) {
-    const uint32_t a = blockIdx.y;
-    const unsigned long long* bits = A.vt_bits + (uint64_t)a * (A.S / 64 + 1);
-    uint32_t cnt = 0;
-    for (uint64_t w = gtid(); w < A.S / 64 + 1; w += gstride()) cnt += (uint32_t)__builtin_popcountll(bits[w]);
-    for (int off = 32; off > 0; off >>= 1) cnt += (uint32_t)__shfl_xor((int)cnt, off, 64);
-    if ((threadIdx.x & 63u) == 0 && cnt) atomicAdd(A.vt_count + a, (unsigned long long)cnt);
+
+// Level 2 (grid: MXP_VTD_MERGE x candidate columns): a workgroup merges its share of the tile
+// lists in an LDS table (128 KB: one workgroup per CU), then adds its distinct keys to the column's
+// provisional table (compare-and-swap; counts added; the first inserter's representative kept) and
+// counts the new keys.  Past MXP_VTD_MAXD distinct keys -- in LDS or in the table -- the column is
+// marked overflowed and the merge stops (a column of mostly distinct values is no value-class
+// column).
+extern "C" __global__ __launch_bounds__(256) void mxp_pack_vtd_merge_kernel(mxp_pack_args A) {
+    __shared__ unsigned long long tkey[MXP_VTD_CAP];
+    __shared__ uint32_t tcnt[MXP_VTD_CAP], trep[MXP_VTD_CAP];
+    __shared__ uint32_t tn, over;
+    const uint32_t tid = threadIdx.x, a = blockIdx.y;
+    uint32_t* meta = A.vtd_meta + 2u * a;
+    for (uint32_t i = tid; i < MXP_VTD_CAP; i += 256u) {
+        tkey[i] = ~0ull;
+        tcnt[i] = 0u;
+    }
+    if (tid == 0) {
+        tn = 0u;
+        over = __hip_atomic_load(meta + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const uint32_t per = (A.vtd_tiles + MXP_VTD_MERGE - 1u) / MXP_VTD_MERGE;
+    const uint32_t t0 = blockIdx.x * per, t1 = min(t0 + per, A.vtd_tiles);
+    for (uint32_t t = t0; t < t1 && !over; t++) {
+        const uint64_t lo = ((uint64_t)a * A.vtd_tiles + t) * MXP_VTD_TILE;
+        const uint32_t k = A.vtd_ln[(uint64_t)a * A.vtd_tiles + t];
+        for (uint32_t e = tid; e < k; e += 256u) {
+            const unsigned long long key = A.vtd_lkey[lo + e];
+            const uint2 cr = A.vtd_lcr[lo + e];
+            uint32_t h = (uint32_t)mxp_hash64(key) & (MXP_VTD_CAP - 1u);
+            for (;;) {
+                const unsigned long long cur = tkey[h];
+                if (cur == key) break;
+                if (cur == ~0ull) {
+                    const unsigned long long old = atomicCAS(&tkey[h], ~0ull, key);
+                    if (old == ~0ull) {
+                        trep[h] = cr.y;
+                        if (atomicAdd(&tn, 1u) >= MXP_VTD_MAXD) over = 1u;
+                        break;
+                    }
+                    if (old == key) break;
+                }
+                h = (h + 1u) & (MXP_VTD_CAP - 1u);
+            }
+            atomicAdd(&tcnt[h], cr.x);
+        }
+        __syncthreads();  // (over: read by every thread before the next tile)
+    }
+    if (over) {
+        if (tid == 0) __hip_atomic_store(meta + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    unsigned long long* T = A.vtd_tkey + (uint64_t)a * MXP_VTD_CAP;
+    uint2* CR = A.vtd_tcr + (uint64_t)a * MXP_VTD_CAP;
+    for (uint32_t i = tid; i < MXP_VTD_CAP; i += 256u) {
+        const unsigned long long key = tkey[i];
+        if (key == ~0ull) continue;
+        uint32_t h = (uint32_t)mxp_hash64(key) & (MXP_VTD_CAP - 1u);
+        for (;;) {
+            unsigned long long old = __hip_atomic_load(T + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (old == ~0ull) {
+                old = atomicCAS(T + h, ~0ull, key);
+                if (old == ~0ull) {
+                    CR[h].y = trep[i];
+                    if (atomicAdd(meta, 1u) >= MXP_VTD_MAXD) __hip_atomic_store(meta + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+            if (old == key) break;
+            h = (h + 1u) & (MXP_VTD_CAP - 1u);
+            if (__hip_atomic_load(meta + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;  // (a full table)
+        }
+        atomicAdd(&CR[h].x, tcnt[i]);
+    }
 }
 
 // ip() / timestamp() of every string id: the rule-set pool's strings, then the batch's
@@ -382,8 +501,8 @@ extern "C" hipError_t mxp_launch_pack(const mxp_pack_args* a, uint32_t step, uin
         break;
     }
     case 5:
-        hipLaunchKernelGGL(mxp_pack_vt_mark_kernel, dim3(grid_for(a->n) < 1024 ? grid_for(a->n) : 1024, a->n_vt_cand), dim3(256), 0, s, *a);
-        hipLaunchKernelGGL(mxp_pack_vt_count_kernel, dim3(grid_for(a->S / 64 + 1), a->n_vt_cand), dim3(256), 0, s, *a);
+        hipLaunchKernelGGL(mxp_pack_vtd_local_kernel, dim3(a->vtd_tiles, a->n_vt_cand), dim3(256), 0, s, *a);
+        hipLaunchKernelGGL(mxp_pack_vtd_merge_kernel, dim3(MXP_VTD_MERGE, a->n_vt_cand), dim3(256), 0, s, *a);
         break;
     case 6: hipLaunchKernelGGL(mxp_pack_parse_kernel, dim3(grid_for(a->S)), dim3(256), 0, s, *a, arg); break;
     case 7: hipLaunchKernelGGL(mxp_pack_pretable_kernel, dim3(grid_for(a->S)), dim3(256), 0, s, *a, arg); break;

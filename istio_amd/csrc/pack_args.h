@@ -35,6 +35,10 @@ typedef struct mxp_pool_view {
 
 #define MXP_PACK_MAXCOL 64
 #define MXP_PACK_VTCAND 32  // value-class candidate columns sized per upload (engine kVtCandMax)
+#define MXP_VTD_TILE 1024u  // requests per tile list of the dictionary's first level
+#define MXP_VTD_CAP 8192u   // provisional table slots per candidate column
+#define MXP_VTD_MAXD 4096u  // more distinct keys: the column is no value-class column (engine kVtMaxClasses)
+#define MXP_VTD_MERGE 16u   // merge workgroups per candidate column
 
 #if defined(__HIPCC__)
 #define MXP_PHD __host__ __device__ inline
@@ -124,10 +128,18 @@ typedef struct mxp_pack_args {
     // pre-tables by string id [S]
     uint64_t* ipof;
     uint64_t* tsof;
-    // value classes: candidate columns' distinct-value marks
-    unsigned long long* vt_bits;    // [ncand][S / 64 + 1]
-    unsigned long long* vt_count;   // [ncand] distinct string ids
-    uint32_t* vt_kmask;             // [ncand] kinds other than string seen (one class each)
+    // value classes, the batch's class dictionary in two levels (pack.hip mxp_pack_vtd_*): per tile of
+    // MXP_VTD_TILE requests and candidate column its distinct keys (mxp_vt_key) with counts and a
+    // representative request, then per column those lists merged into a provisional table of
+    // MXP_VTD_CAP slots -- distinct count and overflow (> MXP_VTD_MAXD keys) read back at the upload's
+    // one synchronisation; the final tables are built from it (kernels.hip mxp_vtd_final_kernel)
+    unsigned long long* vtd_lkey;   // [ncand][tiles][MXP_VTD_TILE] tile lists: keys
+    uint2* vtd_lcr;                 // ... (count, representative)
+    uint32_t* vtd_ln;               // [ncand][tiles] list lengths
+    unsigned long long* vtd_tkey;   // [ncand][MXP_VTD_CAP] provisional tables (~0: empty)
+    uint2* vtd_tcr;                 // ... (count, representative)
+    uint32_t* vtd_meta;             // [ncand][2] distinct keys, overflow
+    uint32_t vtd_tiles;
     uint32_t vt_col[MXP_PACK_VTCAND];
     uint32_t n_vt_cand;
     uint32_t* max_len_out;          // longest batch string (atomic max)

@@ -17,7 +17,7 @@
 extern "C" hipError_t mxp_launch_pack(const mxp_pack_args* a, uint32_t step, uint32_t arg, hipStream_t s);
 
 namespace {
-constexpr size_t kVtBytes = 12 * MXP_PACK_VTCAND;  // value-class counts (u64) + kind masks (u32)
+constexpr size_t kVtBytes = 8 * MXP_PACK_VTCAND;  // value-class distinct counts + overflow flags (u32 pairs)
 constexpr uint32_t kRxDirect = 0x80000000u;          // rx pair keyed by an engine string id
 
 uint32_t table_size(uint64_t items) {
@@ -135,7 +135,10 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     // ---- the batch as given (scratch of the engine, reused across uploads)
     const uint64_t sbytes = NS ? b->str_offsets[NS] : 0;
     if ((rc = up(pk_soff, b->str_offsets, NS ? ((size_t)NS + 1) * 8 : 0, "upload string offsets"))) return rc;
-    if ((rc = up(pk_sbytes, b->str_bytes, sbytes, "upload string bytes"))) return rc;
+    // (16 bytes of slack: the intern kernel reads strings 8 bytes at a time)
+    if ((rc = grow(pk_sbytes, sbytes + 16, "upload string bytes"))) return rc;
+    if (sbytes && (e = hipMemcpyAsync(pk_sbytes.p, b->str_bytes, sbytes, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return hipfail(e, "upload string bytes");
     if ((rc = up(pk_tsec, b->time_sec, (size_t)NT * 8, "upload times"))) return rc;
     if ((rc = up(pk_tnsec, b->time_nsec, (size_t)NT * 4, "upload times"))) return rc;
     const uint64_t E = (any_map && NM) ? b->map_offsets[NM] : 0;
@@ -304,15 +307,26 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     // string: the one synchronisation of the upload)
     const uint32_t ncand = (uint32_t)std::min<size_t>(vt_cand_col.size(), MXP_PACK_VTCAND);
     const bool vt_on = !(debug_flags & 131072u) && n && ncand;
-    const uint64_t vw = S / 64 + 1;
+    db->vtd_ready = false;
     if (vt_on) {
-        if ((rc = grow(pk_vt_bits, (size_t)ncand * vw * 8, "vt marks"))) return rc;
-        if ((rc = grow(pk_vt_cnt, kVtBytes, "vt counts"))) return rc;
-        if ((e = hipMemsetAsync(pk_vt_bits.p, 0, (size_t)ncand * vw * 8, s)) != hipSuccess) return hipfail(e, "reset vt");
-        if ((e = hipMemsetAsync(pk_vt_cnt.p, 0, kVtBytes, s)) != hipSuccess) return hipfail(e, "reset vt");
-        A.vt_bits = pk_vt_bits.as<unsigned long long>();
-        A.vt_count = pk_vt_cnt.as<unsigned long long>();
-        A.vt_kmask = (uint32_t*)(pk_vt_cnt.as<uint8_t>() + 8 * MXP_PACK_VTCAND);
+        const uint32_t tiles = (uint32_t)((n + MXP_VTD_TILE - 1) / MXP_VTD_TILE);
+        const size_t lists = (size_t)ncand * tiles * MXP_VTD_TILE, tabs = (size_t)ncand * MXP_VTD_CAP;
+        if ((rc = grow(pk_vtd_lkey, lists * 8, "vt lists"))) return rc;
+        if ((rc = grow(pk_vtd_lcr, lists * 8, "vt lists"))) return rc;
+        if ((rc = grow(pk_vtd_ln, (size_t)ncand * tiles * 4, "vt lists"))) return rc;
+        if ((rc = grow(pk_vtd_tkey, tabs * 8, "vt tables"))) return rc;
+        if ((rc = grow(pk_vtd_tcr, tabs * 8, "vt tables"))) return rc;
+        if ((rc = grow(pk_vtd_meta, kVtBytes, "vt counts"))) return rc;
+        if ((e = hipMemsetAsync(pk_vtd_tkey.p, 0xFF, tabs * 8, s)) != hipSuccess) return hipfail(e, "reset vt");
+        if ((e = hipMemsetAsync(pk_vtd_tcr.p, 0, tabs * 8, s)) != hipSuccess) return hipfail(e, "reset vt");
+        if ((e = hipMemsetAsync(pk_vtd_meta.p, 0, kVtBytes, s)) != hipSuccess) return hipfail(e, "reset vt");
+        A.vtd_lkey = pk_vtd_lkey.as<unsigned long long>();
+        A.vtd_lcr = pk_vtd_lcr.as<uint2>();
+        A.vtd_ln = pk_vtd_ln.as<uint32_t>();
+        A.vtd_tkey = pk_vtd_tkey.as<unsigned long long>();
+        A.vtd_tcr = pk_vtd_tcr.as<uint2>();
+        A.vtd_meta = pk_vtd_meta.as<uint32_t>();
+        A.vtd_tiles = tiles;
         for (uint32_t a = 0; a < ncand; a++) A.vt_col[a] = vt_cand_col[a];
         A.n_vt_cand = ncand;
         if ((rc = launch(5))) return rc;
@@ -324,7 +338,7 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         }
     }
     if ((e = hipMemcpyAsync(pk_host, pk_maxlen.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return hipfail(e, "read back");
-    if (vt_on && (e = hipMemcpyAsync((uint8_t*)pk_host + 64, pk_vt_cnt.p, kVtBytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    if (vt_on && (e = hipMemcpyAsync((uint8_t*)pk_host + 64, pk_vtd_meta.p, kVtBytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
         return hipfail(e, "read back");
     // run-time regexp patterns meanwhile: the distinct batch strings of the pattern columns
     std::vector<uint32_t> rx_s, rx_v;
@@ -426,13 +440,13 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     db->vt_mask = 0;
     db->vt_capc.assign(vt_cand_col.size(), 0);
     if (vt_on) {
-        const uint64_t* cnt = (const uint64_t*)((uint8_t*)pk_host + 64);
-        const uint32_t* km = (const uint32_t*)((uint8_t*)pk_host + 64 + 8 * MXP_PACK_VTCAND);
+        const uint32_t* meta = (const uint32_t*)((uint8_t*)pk_host + 64);  // distinct keys, overflow
         uint32_t active = 0;
         const bool force = (debug_flags & 262144u) != 0;
+        db->vtd_ready = true;
         for (uint32_t a = 0; a < ncand && active < MXP_VT_MAX; a++) {
-            const uint64_t D = cnt[a] + (uint64_t)__builtin_popcount(km[a]);
-            if (D > kVtMaxClasses || (!force && D * 16 > n)) continue;
+            const uint64_t D = meta[2 * a];
+            if (meta[2 * a + 1] || D > kVtMaxClasses || (!force && D * 16 > n)) continue;
             uint32_t cap = 64;
             while (cap < 2 * D) cap <<= 1;
             db->vt_capc[a] = cap;
