@@ -149,12 +149,15 @@ def measured_traffic(workload, rules, requests):
 
 
 def lds_conflicts(workload):
-    """LDS bank-conflict rate per evaluation kernel from the committed SQ counter session
-    (tools/sq_session.sh + tools/sq_summarize.py -> profiles/sq_counters_<workload>.json), or None."""
+    """LDS bank-conflict rate per evaluation kernel from the committed SQ counter session of THIS
+    build and workload (tools/sq_session.sh + tools/sq_summarize.py ->
+    profiles/sq_counters_<workload>.json, keyed by kernel_fingerprint()), or None."""
     path = os.path.join(ROOT, "profiles", "sq_counters_%s.json" % workload)
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
+    if d.get("workload") != workload or d.get("fingerprint") != kernel_fingerprint():
+        return None
     return {k: {"bank_conflict_cycles": v.get("SQ_LDS_BANK_CONFLICT"), "lds_active_cycles": v.get("SQ_LDS_IDX_ACTIVE"),
                 "rate": v.get("bank_conflict_rate")} for k, v in d.get("kernels", {}).items()}
 

@@ -128,9 +128,9 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_kernel(mxp_pac
     const bool words = A.kind == MXP_IK_STR;
     uint32_t maxlen = 0;
     // (a uniform trip count per wave: the wave maximum below needs every lane)
-    for (uint64_t i0 = (A.i0 + gtid()) & ~63ull; i0 < A.i1; i0 += gstride()) {
+    for (uint64_t i0 = A.i0 + (gtid() & ~63ull); i0 < A.i1; i0 += gstride()) {
         const uint64_t idx = i0 + (threadIdx.x & 63u);
-        if (idx < A.i0 || idx >= A.i1) continue;
+        if (idx >= A.i1) continue;
         const uint8_t* p;
         uint32_t n;
         if (!item_of(A, A.kind, idx, &p, &n, buf)) {

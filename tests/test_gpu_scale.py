@@ -179,3 +179,31 @@ def test_benched_evaluations_against_oracle(mxp, wl):
         st, msg = ev.eval_predicate(rules[r], sub, int(q))
         gmsg = eng.pair_error(int(sample[q]), int(r))
         assert gmsg == msg or (st == "panic" and gmsg in PANIC_TEXTS), (rules[r], int(sample[q]), gmsg, msg)
+
+
+def test_null_stream_orders_after_legacy_zeroing(mxp):
+    """Round 3's race at bench size: counters and bitmaps zeroed by torch on the legacy default stream,
+    then evaluations with stream=NULL and no host synchronisation in between -- libmxp's NULL stream
+    must order after the zeroing (engine.cpp: a blocking stream), so the fused hit counters are exactly
+    the bitmap's true pairs, three evaluations' worth, on C4 (value classes, deferred pairs)."""
+    import torch
+    manifest, rules, batch = W.c4_workload(n_rules=10_000, n_requests=1 << 20, seed=4)
+    R, N = len(rules), batch.n
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    db = eng.upload(batch)
+    Wd = (R + 31) // 32
+    assert torch.cuda.current_stream().cuda_stream == 0  # torch's legacy default stream
+    dm = torch.full((Wd, N), -1, dtype=torch.int32, device="cuda:0")
+    req_err = torch.full((N,), 7, dtype=torch.uint8, device="cuda:0")
+    for rep in range(2):
+        hits = torch.zeros(R, dtype=torch.int64, device="cuda:0")  # (no synchronize: stream order only)
+        for _ in range(3):
+            db.eval_compact(dm.data_ptr(), req_err.data_ptr(), hits.data_ptr(), 0)
+        cnt = torch.zeros((Wd, 32), dtype=torch.int64, device="cuda:0")
+        for b in range(32):
+            cnt[:, b] = ((dm >> b) & 1).sum(dim=1)
+        assert torch.equal(hits, 3 * cnt.reshape(-1)[:R]), rep
+        assert int(hits.sum()) > 100 * N and int(req_err.max()) == 0
+    db.free()

@@ -16,11 +16,12 @@ import os
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-EVAL_KERNELS = ("mxp_fill_kernel", "mxp_fill_dtp_kernel", "mxp_vtfill_kernel", "mxp_vtfill_lds_kernel", "mxp_vt_lookup_kernel",
+# (name prefixes: the per-slot-count instantiations, e.g. mxp_vtfill_imm5_kernel, included)
+EVAL_KERNELS = ("mxp_fill_kernel", "mxp_fill_dtp_kernel", "mxp_vtfill", "mxp_vt_lookup_kernel",
                 "mxp_vt_eval_kernel", "mxp_guard_kernel", "mxp_guard2_kernel", "mxp_eval_kernel", "mxp_index_kernel",
                 "mxp_index_dtp_kernel", "mxp_index_dtp_lite_kernel", "mxp_index5_kernel", "mxp_dtp_sort_kernel", "mxp_dtp_apply_kernel",
                 "mxp_inject_kernel", "mxp_hits_kernel", "mxp_hits_ragged_kernel", "mxp_hits_gate_kernel",
-                "mxp_eval_deep_kernel", "mxp_quota_kernel", "mxp_dtp_hits_kernel")
+                "mxp_eval_deep_kernel", "mxp_quota", "mxp_dtp_hits_kernel")
 
 
 def per_kernel(path_glob, counter):

@@ -1,7 +1,7 @@
 #!/bin/bash
 # SQ counters of the bench's kernels (issue / wait breakdown, instruction mix, LDS bank conflicts),
 # one rocprofv3 --pmc pass per group (SQ has 8 slots per pass on gfx950), each under its own limit.
-#   bash tools/sq_session.sh <outdir> [bench args]
+#   bash tools/sq_session.sh <outdir> [bench args]     (per workload: C2 alone, or --workload c4)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -16,7 +16,7 @@ i=0
 for p in "${passes[@]}"; do
     i=$((i + 1))
     timeout -s KILL 120 rocprofv3 --pmc $p --output-format csv -d "$out/sq$i" -o pmc -- \
-        python3 bench.py --no-cpu-baseline --e2e-reps 0 --steps 2 --warmup 1 "$@" > "$out/sq$i.log" 2>&1
+        python3 bench.py --no-cpu-baseline --no-c4 --no-c5 --no-c3 --fresh-steps 0 --e2e-reps 0 --steps 2 --warmup 1 "$@" > "$out/sq$i.log" 2>&1
     rc=$?
     echo "sq$i rc=$rc"
     [ $rc -ne 0 ] && exit $rc

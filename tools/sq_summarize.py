@@ -10,9 +10,9 @@ import json
 import os
 from collections import defaultdict
 
-EVAL = ("mxp_fill_kernel", "mxp_fill_dtp_kernel", "mxp_vtfill_lds_kernel", "mxp_guard_kernel", "mxp_guard2_kernel",
+EVAL = ("mxp_fill_kernel", "mxp_fill_dtp_kernel", "mxp_vtfill", "mxp_guard_kernel", "mxp_guard2_kernel",
         "mxp_eval_kernel", "mxp_index_kernel", "mxp_index_dtp_kernel", "mxp_index_dtp_lite_kernel", "mxp_dtp_sort_kernel",
-        "mxp_vt_lookup_kernel", "mxp_inject_kernel")
+        "mxp_vt_lookup_kernel", "mxp_vt_eval_kernel", "mxp_inject_kernel", "mxp_dtp_hits_kernel", "mxp_quota")
 
 
 def main():
@@ -24,7 +24,10 @@ def main():
     for f in glob.glob(os.path.join(a.dir, "sq*", "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             vals[row.get("Kernel_Name", "")][row["Counter_Name"]].append(float(row["Counter_Value"]))
-    out = {"workload": a.workload, "kernels": {},
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_fingerprint
+    out = {"workload": a.workload, "fingerprint": kernel_fingerprint(), "kernels": {},
            "method": "rocprofv3 --pmc SQ counters, 2 passes of 8; per-dispatch means; "
                      "bank_conflict_rate = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE"}
     for k, cs in vals.items():
