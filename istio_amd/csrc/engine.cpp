@@ -211,7 +211,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         std::vector<mxp::LiteralKey> keys;
         if (!(debug_flags & 67108864u) && n < (1u << 23) && mxp::dfa_literal_keys(d, st, 8, 8, &keys)) {
             auto& rk = rx_keys_h[rp.rule];
-            for (const auto& k : keys) rk.push_back({intern_string(rp.prefix + k.bytes), k.exact ? 1u : 0u});
+            for (const auto& k : keys) rk.push_back({intern_string(rp.prefix + k.bytes), k.tail ? 2u : k.exact ? 1u : 0u});
             guards[rp.rule].mode = GM_ONLY | GT_PREFIX;
             continue;
         }
@@ -425,33 +425,29 @@ int mxp_engine::build_plan(Plan& P) {
             continue;
         }
         if (!rx_keys_h[i].empty()) {  // a literal-key regexp rule: one posting per key
-            for (const auto& k : rx_keys_h[i]) index_of[{gd.col, true}][k.first].push_back(i | ((uint32_t)k.second << 31));
+            for (const auto& k : rx_keys_h[i])
+                index_of[{gd.col, true}][k.first].push_back(i | (k.second == 1 ? 1u << 31 : k.second == 2 ? 1u << 30 : 0u));
             continue;
         }
         index_of[{gd.col, prefix}][k1].push_back(i);
     }
     P.n_tmpls = (uint32_t)tmpls.size();
-    // lite index kernel: no template (code from its start to its end) holds a heavy opcode
-    P.tmpl_lite = !(debug_flags & 8388608u);
-    for (const mxp_tmpl& t : tmpls)
-        for (uint32_t pc = t.pc0; pc < t.len && P.tmpl_lite; pc++) {
-            const uint32_t op = prog_h[t.off - t.pc0 + pc].op & 0x7Fu;
-            if (op == VM_VCOL || op == VM_LOOKUP || op == VM_LOOKUPK || op == VM_REGEX || op == VM_REGEXR || op == VM_REGEXD)
-                P.tmpl_lite = false;
-        }
     std::vector<mxp_index> idx;
     std::vector<mxp_hent> hents;
     std::vector<uint32_t> postings, plens;
     // postings carry their rule's continuation template (rule | code << 23; code 511 direct, 510
     // look it up): the index kernel then loads no template id per posting or per pair
     P.post_tmpl = n < (1u << 23);
-    // (code 509: a literal-key regexp rule's exact key -- true only when the subject ends at the key;
-    // a rule id with bit 31 set in `rs` is such a posting)
+    // (literal-key regexp rules, n < 2^23: code 509, an exact key -- true only when the subject ends at
+    // the key -- for a rule id with bit 31 set in `rs`; code 508, a `.*$` tail key -- true only when
+    // no '\n' follows the key in the subject -- for bit 30)
+    auto rid = [&](uint32_t r) { return r & (P.post_tmpl ? 0x3FFFFFFFu : 0x7FFFFFFFu); };
     auto post = [&](const std::vector<uint32_t>& rs, const std::vector<uint32_t>& tmpl_of) {
         for (uint32_t r : rs) {
-            const uint32_t rr = r & 0x7FFFFFFFu, t = tmpl_of[rr];
+            const uint32_t rr = rid(r), t = tmpl_of[rr];
             postings.push_back(!P.post_tmpl ? rr
-                                            : rr | ((r >> 31) ? 509u : t == MXP_TMPL_DIRECT ? 511u : t < 509u ? t : 510u) << 23);
+                                            : rr | ((r >> 31) ? 509u : ((r >> 30) & 1u) ? 508u
+                                                    : t == MXP_TMPL_DIRECT ? 511u : t < 508u ? t : 510u) << 23);
         }
     };
     // open-addressing table of `groups` (key -> rules) at hents[hoff ..): returns hmask
@@ -487,21 +483,30 @@ int mxp_engine::build_plan(Plan& P) {
         while (cap < (2u << index_sparsity) * ci.second.size()) cap <<= 1;
         x.hmask = cap - 1;
         x.hoff = (uint32_t)hents.size();
-        hents.resize(hents.size() + cap, mxp_hent{0, 0, 0, 0});
+        hents.resize(hents.size() + 2 * (size_t)cap, mxp_hent{0, 0, 0, 0});
         std::set<uint32_t> lens;
         for (auto& kv : ci.second) {
             std::vector<uint32_t> rs = kv.second;
             std::stable_sort(rs.begin(), rs.end(), [&](uint32_t a, uint32_t b) {
-                return rule_tmpl[a & 0x7FFFFFFFu] < rule_tmpl[b & 0x7FFFFFFFu];
+                return rule_tmpl[rid(a)] < rule_tmpl[rid(b)];
             });
+            for (uint32_t r : rs) x.tailk |= P.post_tmpl && ((r >> 30) & 3u) == 1u;
             // hash of the key bytes, as the kernel hashes the request's leading bytes
             const std::string& key = gstrs[(uint32_t)kv.first];
             lens.insert((uint32_t)key.size());
             const uint64_t hh = mxp_str_hash((const uint8_t*)key.data(), key.size());
             uint32_t h = (uint32_t)hh & x.hmask;
-            while (hents[x.hoff + h].len) h = (h + 1) & x.hmask;
-            hents[x.hoff + h] = mxp_hent{(uint32_t)kv.first, (uint32_t)(hh >> 32), (uint32_t)postings.size(),
-                                         (uint32_t)rs.size()};
+            while (hents[x.hoff + 2 * h].len) h = (h + 1) & x.hmask;
+            // (vm.h mxp_index: entry pairs; a key of <= 20 bytes rides inline -- bytes 0..3 in the first
+            // entry's klo, 4..19 in the second entry -- so a probe verifies it with no key-string loads;
+            // longer keys keep their string id; the key length sits in the top byte of the count)
+            if (rs.size() >= (1u << 24)) return fail(MXP_ERR_NOMEM, "prefix posting list too long");
+            uint32_t kw[5] = {0, 0, 0, 0, 0};
+            const bool inl = key.size() <= 20;
+            if (inl) memcpy(kw, key.data(), key.size());
+            hents[x.hoff + 2 * h] = mxp_hent{inl ? kw[0] : (uint32_t)kv.first, (uint32_t)(hh >> 32), (uint32_t)postings.size(),
+                                             (uint32_t)rs.size() | ((uint32_t)std::min<size_t>(key.size(), 255) << 24)};
+            hents[x.hoff + 2 * h + 1] = mxp_hent{kw[1], kw[2], kw[3], kw[4]};
             post(rs, rule_tmpl);
         }
         x.plen0 = (uint32_t)plens.size();
@@ -557,6 +562,34 @@ int mxp_engine::build_plan(Plan& P) {
         plens.insert(plens.end(), lens.begin(), lens.end());
         idx.push_back(x);
     }
+    // lite index kernel: no template the postings can run (code from its start to its end) holds a
+    // heavy opcode -- templates of rules this plan serves otherwise (value classes) or that became
+    // direct postings (literal-key regexps) do not count
+    {
+        std::vector<uint8_t> used(tmpls.size(), P.post_tmpl ? 0 : 1);
+        auto use = [&](uint32_t t) {
+            if (t < used.size()) used[t] = 1;
+        };
+        if (P.post_tmpl)
+            for (uint32_t pe : postings) {
+                const uint32_t code = pe >> 23, r = pe & 0x7FFFFFu;
+                if (code < 508u) use(code);
+                if (code == 510u) {  // (either table's template: the posting does not say which)
+                    use(rule_tmpl[r]);
+                    use(rule_tmpl2[r]);
+                }
+            }
+        P.tmpl_lite = !(debug_flags & 8388608u);
+        for (uint32_t i = 0; i < tmpls.size() && P.tmpl_lite; i++) {
+            if (!used[i]) continue;
+            const mxp_tmpl& t = tmpls[i];
+            for (uint32_t pc = t.pc0; pc < t.len && P.tmpl_lite; pc++) {
+                const uint32_t op = prog_h[t.off - t.pc0 + pc].op & 0x7Fu;
+                if (op == VM_VCOL || op == VM_LOOKUP || op == VM_LOOKUPK || op == VM_REGEX || op == VM_REGEXR || op == VM_REGEXD)
+                    P.tmpl_lite = false;
+            }
+        }
+    }
     // string heads: plan 0 assigns a row to every column its prefix / composite indexes probe (the
     // other plans leave value-class rules out, so their indexes probe a subset of those columns)
     if (base) {
@@ -565,7 +598,7 @@ int mxp_engine::build_plan(Plan& P) {
     }
     for (mxp_index& x : idx) {
         x.hslot = MXP_VM_DONE;
-        if (x.prefix == MXP_IX_EQ) continue;
+        if (x.prefix == MXP_IX_EQ || x.tailk) continue;  // (`.*$` tail keys look at the whole subject)
         const uint32_t c = x.prefix == MXP_IX_COMPOSITE ? x.col2 : x.col;
         if (c >= head_slot_of.size()) continue;
         if (base && head_slot_of[c] == MXP_VM_DONE) {

@@ -1879,6 +1879,19 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// no '\n' in bytes [L, n) of a string at an 8-aligned address (its words are read whole: the string
+// pool is padded)
+__device__ __forceinline__ bool tail_clear(StrRef s, uint32_t L) {
+    for (uint32_t w = L / 8u; w * 8u < s.n; w++) {
+        uint64_t x = ld8a(s.p + w * 8u) ^ 0x0A0A0A0A0A0A0A0Aull;  // (zero bytes: newlines)
+        if (w * 8u < L) x |= (1ull << ((L - w * 8u) * 8u)) - 1ull;  // bytes before L
+        if (s.n - w * 8u < 8u) x |= ~0ull << ((s.n - w * 8u) * 8u);  // bytes past the end
+        // 0x80 where a byte of x is zero (exact per byte: no borrow between bytes)
+        if (~(((x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | x | 0x7F7F7F7F7F7F7F7Full)) return false;
+    }
+    return true;
+}
+
 __shared__ uint64_t g_cm[4][64];  // dense-alias masks of the wave's 64 requests (kargs.dense_of)
 struct PairQueue {
     uint32_t wave;
@@ -1952,12 +1965,13 @@ __device__ void run_pairs(const mxp_kargs& A, PairQueue& Q, uint32_t off, uint32
 // never overflows, one lane's long list fills whole batches (C2: a request without a path takes its
 // service's ~39 equality postings in one round, not ten rounds of four), and the VM has one call
 // site (one inlined copy).
-// `exact`: the probed string ends at this slot's key length (code-509 postings -- a literal-key
-// regexp rule's exact keys -- are true pairs only then)
+// Literal-key regexp postings of a prefix slot (subject `s`, key length L; L = 0 elsewhere): code
+// 509, an exact key, is a true pair when the subject ends at the key; code 508, a `.*$` tail key,
+// when no '\n' follows it.  Direct postings and the dead literal-key ones take no queue entry.
 template <bool kRefs, bool kNfa, bool kDtp, bool kProf = false, bool kLite = false>
 __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, uint32_t tbl, uint32_t start,
                                              uint32_t len, uint32_t req, bool final, uint64_t (*regs)[256],
-                                             uint32_t tid, bool exact = false) {
+                                             uint32_t tid, StrRef s = StrRef{nullptr, 0}, uint32_t L = 0) {
     const uint32_t lane = tid & 63u;
     const uint32_t* __restrict__ tmpl_of = tbl ? A.rule_tmpl2 : A.rule_tmpl;
     uint32_t j0 = 0;
@@ -1974,28 +1988,31 @@ __device__ __forceinline__ void process_slot(const mxp_kargs& A, PairQueue& Q, u
             const uint64_t below = (1ull << lane) - 1ull;
             uint32_t pos = Q.n;
             for (uint32_t j = 0; j < tmax; j++) {
-                const uint64_t act = __ballot(j < take);
+                uint32_t rule = 0, t = MXP_TMPL_SKIP;
                 if (j < take) {
-                    const uint32_t at = pos + (uint32_t)__builtin_popcountll(act & below);
                     const uint32_t pe = A.postings[start + j0 + j];
-                    uint32_t rule = pe, t;
+                    rule = pe;
                     if (A.post_tmpl) {  // the template rides in the posting (kargs.postings)
                         rule = pe & 0x7FFFFFu;
                         const uint32_t code = pe >> 23;
                         t = code == 511u ? MXP_TMPL_DIRECT : code == 510u ? tmpl_of[rule]
-                          : code == 509u ? (exact ? MXP_TMPL_DIRECT : MXP_TMPL_SKIP) : code;
+                          : (code | 1u) == 509u  // (one test for both literal-key codes: no spills)
+                              ? ((code == 509u ? s.n == L : tail_clear(s, L)) && L ? MXP_TMPL_DIRECT : MXP_TMPL_SKIP)
+                              : code;
                     } else {
                         t = tmpl_of[rule];
                     }
-                    uint32_t e = rule | (tbl << 31);
                     if (t == MXP_TMPL_DIRECT) {
                         Q.ntrue += pair_true<kDtp>(A, Q, rule, req);
-                        e = 0xFFFFFFFFu;
-                    } else if (t == MXP_TMPL_SKIP) {
-                        e = 0xFFFFFFFFu;
+                        t = MXP_TMPL_SKIP;
                     }
+                }
+                const bool queued = t != MXP_TMPL_SKIP;
+                const uint64_t act = __ballot(queued);
+                if (queued) {
                     // (entry: rule | table, then the request's lane in the wave | template << 8)
-                    g_ixq[Q.wave][at][0] = e;
+                    const uint32_t at = pos + (uint32_t)__builtin_popcountll(act & below);
+                    g_ixq[Q.wave][at][0] = rule | (tbl << 31);
                     g_ixq[Q.wave][at][1] = (req - Q.base) | (t << 8);
                 }
                 pos += (uint32_t)__builtin_popcountll(act);
@@ -2182,28 +2199,30 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 if (sok && L <= s.n) {
                     const uint64_t hf = by_head ? ph.at_head((uint64_t)s.p, hw1, L) : ph.at(s.p, L);
                     const uint32_t tag = (uint32_t)(hf >> 32);
-                    const uint32_t stride = comp ? 2u : 1u;
                     for (uint32_t slot = (uint32_t)hf & pmask;; slot = (slot + 1) & pmask) {
-                        const uint32_t at = poff + stride * slot;
+                        // entry pairs (vm.h mxp_index): both halves in one 32-byte load pair
+                        const uint32_t at = poff + 2u * slot;
                         const mxp_hent E = A.hents[at];
-                        // composite: the K1 half of the entry pair is loaded with the first half
-                        const mxp_hent K = comp ? A.hents[at + 1u] : E;
+                        const mxp_hent K = A.hents[at + 1u];
                         if (E.len == 0) break;
                         if (E.khi != tag) continue;
-                        if (comp) {
-                            if (K.klo != vlo || K.khi != vhi || (E.len >> 24) != min(L, 255u)) continue;
-                            if (L <= 12u) {  // the key inline (vm.h MXP hmask2 layout): no key-string loads
-                                const uint64_t k0 = (uint64_t)E.klo | ((uint64_t)K.start << 32);
-                                const uint64_t w0 = by_head ? (uint64_t)s.p : ld8a(s.p);
-                                const uint64_t w1 = by_head ? (uint64_t)hw1 : (L > 8u ? ld8a(s.p + 8) : 0ull);
-                                const uint64_t m0 = L >= 8u ? ~0ull : (1ull << (L * 8u)) - 1ull;
-                                const uint64_t m1 = L > 8u ? (1ull << ((L - 8u) * 8u)) - 1ull : 0ull;
-                                if (((w0 ^ k0) & m0) == 0 && ((w1 ^ (uint64_t)K.len) & m1) == 0) {
-                                    fi = at;
-                                    break;
-                                }
-                                continue;
+                        if (comp && (K.klo != vlo || K.khi != vhi)) continue;
+                        if ((E.len >> 24) != min(L, 255u)) continue;  // (this order: no spills in the lite kernel)
+                        if (L <= (comp ? 12u : 20u)) {  // the key inline: no key-string loads
+                            // key words: composite {bytes 0..3 | 4..7, 8..11}, prefix {0..3 | 4..7, 8..15, 16..19}
+                            const uint64_t k0 = (uint64_t)E.klo | ((uint64_t)(comp ? K.start : K.klo) << 32);
+                            const uint64_t k1 = comp ? (uint64_t)K.len : ((uint64_t)K.khi | ((uint64_t)K.start << 32));
+                            const uint64_t w0 = by_head ? (uint64_t)s.p : ld8a(s.p);
+                            const uint64_t w1 = by_head ? (uint64_t)hw1 : (L > 8u ? ld8a(s.p + 8) : 0ull);
+                            const uint64_t w2 = L > 16u ? ld8a(s.p + 16) : 0ull;  // (prefix keys only; L <= 12 by head)
+                            const uint64_t m0 = L >= 8u ? ~0ull : (1ull << (L * 8u)) - 1ull;
+                            const uint64_t m1 = L >= 16u ? ~0ull : L > 8u ? (1ull << ((L - 8u) * 8u)) - 1ull : 0ull;
+                            const uint64_t m2 = L > 16u ? (1ull << ((L - 16u) * 8u)) - 1ull : 0ull;
+                            if (((w0 ^ k0) & m0) == 0 && ((w1 ^ k1) & m1) == 0 && ((w2 ^ (uint64_t)K.len) & m2) == 0) {
+                                fi = at;
+                                break;
                             }
+                            continue;
                         }
                         const StrRef k = str_of(A, E.klo);
                         if (k.n == L && (by_head ? head_eq((uint64_t)s.p, hw1, k.p, L) : bytes_eq_a(s.p, k.p, L))) {
@@ -2214,7 +2233,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 }
                 if (fi != 0xFFFFFFFFu) {
                     start = A.hents[fi].start;
-                    len = A.hents[fi].len & (comp ? 0xFFFFFFu : 0xFFFFFFFFu);
+                    len = A.hents[fi].len & 0xFFFFFFu;
                 }
             }
             if (A.flags & 1024u) {  // ablation: probes only (results invalid)
@@ -2223,8 +2242,8 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
             }
             if (final || __ballot(len != 0))
                 process_slot<kRefs, kNfa, kDtp, kProf, kLite>(A, Q, comp && p > 0 ? 1u : 0u, start, len, req, final, regs, tid,
-                                                              kind == MXP_IX_PREFIX && !eq_slot && !final &&
-                                                                  s.n == uni(A.plens[plen0 + p]));
+                                                              s, kind == MXP_IX_PREFIX && !eq_slot && !final
+                                                                     ? uni(A.plens[plen0 + p]) : 0u);
             if (kProf && (tid & 63u) == 0 && (final || nmark < 4u)) {  // profiling: phase marks
                 A.wave_t[8ull * tile + 3u + (final ? 4u : nmark)] = (uint64_t)wall_clock64();
                 nmark++;

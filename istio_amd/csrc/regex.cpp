@@ -1147,8 +1147,36 @@ bool dfa_literal_keys(const Dfa& d, uint32_t st, uint32_t max_keys, uint32_t max
         return true;
     }
     const uint32_t C = d.ncls;
-    // non-ASCII runes (and invalid bytes, U+FFFD) must not lead anywhere but REJECT from the states
-    // the enumeration visits: their keys would be multi-byte runes
+    // `.*$` tail states: from them a match is exactly "no '\n' in the rest of the subject" (end of
+    // text accepts, '\n' rejects, every other rune -- non-ASCII and U+FFFD included -- stays in the
+    // set): the greatest set closed under those transitions
+    std::vector<uint8_t> tail(d.nstates, 0);
+    {
+        const uint32_t nl = d.ascii['\n'];
+        for (uint32_t s = 0; s < d.nstates; s++)
+            tail[s] = d.trans[(size_t)s * C + C - 1] == kDfaAccept && d.trans[(size_t)s * C + nl] == kDfaReject;
+        for (bool changed = true; changed;) {
+            changed = false;
+            for (uint32_t s = 0; s < d.nstates; s++) {
+                if (!tail[s]) continue;
+                auto stays = [&](uint32_t c) {
+                    const uint32_t t = d.trans[(size_t)s * C + c];
+                    return t < d.nstates && tail[t];
+                };
+                bool ok = true;
+                for (uint32_t b = 0; b < 128 && ok; b++)
+                    if (b != '\n') ok = d.ascii[b] != nl && stays(d.ascii[b]);
+                for (uint16_t c : d.hi_cls)
+                    if (ok) ok = c != nl && stays(c);
+                if (!ok) {
+                    tail[s] = 0;
+                    changed = true;
+                }
+            }
+        }
+    }
+    // non-ASCII runes (and invalid bytes, U+FFFD) must not lead anywhere but REJECT from the other
+    // states the enumeration visits: their keys would be multi-byte runes
     auto hi_dead = [&](uint32_t s) {
         for (uint16_t c : d.hi_cls)
             if (d.trans[(size_t)s * C + c] != kDfaReject) return false;
@@ -1162,6 +1190,11 @@ bool dfa_literal_keys(const Dfa& d, uint32_t st, uint32_t max_keys, uint32_t max
     for (uint32_t depth = 0; !level.empty(); depth++) {
         std::vector<Item> next;
         for (const Item& it : level) {
+            if (tail[it.s]) {
+                out->push_back({it.w, false, true});
+                if (out->size() + next.size() > max_keys) return false;
+                continue;
+            }
             if (!hi_dead(it.s)) return false;
             if (d.trans[(size_t)it.s * C + C - 1] == kDfaAccept) out->push_back({it.w, true});
             for (uint32_t b = 0; b < 128; b++) {

@@ -68,7 +68,8 @@ bool regex_required_prefix(const std::string& pattern, std::string* prefix);
 // any subject.  False when there are more than `max_keys` keys or a path is undecided at max_depth.
 struct LiteralKey {
     std::string bytes;
-    bool exact;
+    bool exact;         // the subject must end here
+    bool tail = false;  // the subject's remaining bytes must hold no '\n' (a `.*$` tail)
 };
 bool dfa_literal_keys(const Dfa& d, uint32_t st, uint32_t max_keys, uint32_t max_depth, std::vector<LiteralKey>* out);
 

@@ -111,7 +111,9 @@ typedef struct mxp_index {
     uint32_t col;
     uint32_t okset;    // as mxp_seg.okset (bits 0..15)
     uint32_t hmask;    // table size - 1 (power of two)
-    uint32_t hoff;     // first entry in kargs.hents
+    uint32_t hoff;     // first entry in kargs.hents.  Prefix tables: pairs of entries {key bytes 0..3 |
+                       // key string id, tag, start, len | min(|K|, 255) << 24}, {key bytes 4..19}: keys
+                       // of <= 20 bytes inline
     uint32_t prefix;   // MXP_IX_EQ / MXP_IX_PREFIX / MXP_IX_COMPOSITE
     uint32_t plen0;    // prefix / composite: distinct key lengths kargs.plens[plen0 .. plen0 + nplen), ascending
     uint32_t nplen;
@@ -121,7 +123,9 @@ typedef struct mxp_index {
                        // len | min(|K2|, 255) << 24}, {K1 lo, K1 hi, K2 words 1, 2}: keys of <= 12 bytes inline
     uint32_t hoff2;
     uint32_t hslot;    // prefix / composite: the probed column's row in kargs.heads (MXP_VM_DONE: none)
-    uint32_t pad[4];
+    uint32_t tailk;    // prefix: some postings are `.*$` tail keys (code 508): the probe finds the
+                       // subject's last '\n'
+    uint32_t pad[3];
 } mxp_index;           // 64 B
 
 // index kinds.  Composite: rules `A == K1 && B.startsWith(K2) && ...` (vmopt.h SecondAtom), keyed by

@@ -243,7 +243,7 @@ def test_device_resident_batch_and_hits(mxp):
     de = torch.zeros_like(dm)
     hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
     s = torch.cuda.Stream()
-    torch.cuda.set_stream(s)
+    s.wait_stream(torch.cuda.current_stream())
     db.eval(dm.data_ptr(), de.data_ptr(), s.cuda_stream)
     rc = eng.lib.mxp_hits_device(eng.h, dm.data_ptr(), batch.n, s.cuda_stream, hits.data_ptr())
     assert rc == 0
@@ -633,17 +633,21 @@ def test_literal_key_regexp_rules(mxp, monkeypatch, flags):
     """Prefix-guarded regexp rules whose DFA after the literal prefix is a few literal keys become
     direct postings of the prefix index -- prefix keys (any continuation matches) and exact keys (the
     subject ends there) -- with no VM pass (regex.cpp dfa_literal_keys); 67108864 keeps the DFA
-    templates, 8 turns the index off.  Subjects around every boundary: the prefix alone, one byte
-    more or less, the continuation bytes, non-ASCII and invalid UTF-8 after the prefix."""
+    templates, 8 turns the index off.  `.*$` tails (the rest of the subject holds no newline) are
+    tail keys.  Subjects around every boundary: the prefix alone, one byte more or less, the
+    continuation bytes, newlines before / at / after the key, non-ASCII and invalid UTF-8 after the
+    prefix."""
     monkeypatch.setenv("MXP_DEBUG_FLAGS", flags)
     pats = ["^/p(/.*)?$", "^/p[0-9a-z/]*", "^/q$", "^/q(a|bc)$", "^/r[0-9]?$", "^/s(/x|/y.*)", "^/t.{0,2}$",
-            "^/u(é|e)$", "^/v\\b", "^/w(?:x|$)", "^/p/", "^/pa(b|$)"]
+            "^/u(é|e)$", "^/v\\b", "^/w(?:x|$)", "^/p/", "^/pa(b|$)", "^/n.*$", "^/k(x.*|y)$", "^/j[a-z]*.*$",
+            "^/g\\n.*$", "^/i.+$", "^/h(?s:.*)$", "^/f(/[a-z]*)?.*$"]
     rules = ['"%s".matches(request.path)' % p.replace("\\", "\\\\") for p in pats]
     rules += ['request.path.startsWith("/p")', 'request.path == "/q"']
     tails = ["", "/", "/x", "/y", "/yy", "a", "b", "bc", "bcd", "0", "9", "09", "x", "é", "e", "\udcff", "\udcc3",
-             "/é", " ", "-", "ab", "abc"]
+             "/é", " ", "-", "ab", "abc", "\n", "/\n", "/a\nb", "\nx", "x\n", "y\n", "/\udcff", "\n\n"]
     rng = np.random.default_rng(71)
-    heads = ["/p", "/q", "/r", "/s", "/t", "/u", "/v", "/w", "/pa", "/", "", "/P"]
+    heads = ["/p", "/q", "/r", "/s", "/t", "/u", "/v", "/w", "/pa", "/", "", "/P", "/n", "/k", "/j", "/g", "/i",
+             "/h", "/f", "\n/p"]
     paths = [h + t for h in heads for t in tails]
     bags = [{"request.path": p} for p in paths] + [{}] + [{"request.path": 7}]
     bags += [{"request.path": heads[int(rng.integers(0, len(heads)))] + tails[int(rng.integers(0, len(tails)))]

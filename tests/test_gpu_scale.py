@@ -194,7 +194,14 @@ def test_null_stream_orders_after_legacy_zeroing(mxp):
     assert (eng.compile(rules) == 0).all()
     db = eng.upload(batch)
     Wd = (R + 31) // 32
-    assert torch.cuda.current_stream().cuda_stream == 0  # torch's legacy default stream
+    with torch.cuda.stream(torch.cuda.default_stream()):  # (earlier tests may leave another current)
+        assert torch.cuda.current_stream().cuda_stream == 0  # torch's legacy default stream
+        _null_stream_reps(db, R, N, Wd)
+    db.free()
+
+
+def _null_stream_reps(db, R, N, Wd):
+    import torch
     dm = torch.full((Wd, N), -1, dtype=torch.int32, device="cuda:0")
     req_err = torch.full((N,), 7, dtype=torch.uint8, device="cuda:0")
     for rep in range(2):
@@ -206,4 +213,3 @@ def test_null_stream_orders_after_legacy_zeroing(mxp):
             cnt[:, b] = ((dm >> b) & 1).sum(dim=1)
         assert torch.equal(hits, 3 * cnt.reshape(-1)[:R]), rep
         assert int(hits.sum()) > 100 * N and int(req_err.max()) == 0
-    db.free()

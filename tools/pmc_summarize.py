@@ -43,6 +43,8 @@ def main():
     p.add_argument("--requests", type=int, default=1 << 20)
     p.add_argument("--workload", default="c2")
     a, _ = p.parse_known_args()
+    # bench.py --workload c5 (C2 predicates + memquota in one step) looks its traffic up as "c2q"
+    a.workload = {"c5": "c2q"}.get(a.workload, a.workload)
     fetch = per_kernel(os.path.join(a.dir, "FETCH_SIZE", "**", "*counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(a.dir, "WRITE_SIZE", "**", "*counter_collection.csv"), "WRITE_SIZE")
     table = {}
