@@ -442,13 +442,14 @@ int mxp_engine::build_plan(Plan& P) {
     // the key -- for a rule id with bit 31 set in `rs`; code 508, a `.*$` tail key -- true only when
     // no '\n' follows the key in the subject -- for bit 30)
     auto rid = [&](uint32_t r) { return r & (P.post_tmpl ? 0x3FFFFFFFu : 0x7FFFFFFFu); };
-    auto post = [&](const std::vector<uint32_t>& rs, const std::vector<uint32_t>& tmpl_of) {
+    auto post = [&](const std::vector<uint32_t>& rs, const std::vector<uint32_t>& tmpl_of) -> uint32_t {  // postings emitted
+        const size_t p0 = postings.size();
         for (uint32_t r : rs) {
             const uint32_t rr = rid(r), t = tmpl_of[rr];
-            postings.push_back(!P.post_tmpl ? rr
-                                            : rr | ((r >> 31) ? 509u : ((r >> 30) & 1u) ? 508u
-                                                    : t == MXP_TMPL_DIRECT ? 511u : t < 508u ? t : 510u) << 23);
+            const uint32_t code = (r >> 31) ? 509u : ((r >> 30) & 1u) ? 508u : t == MXP_TMPL_DIRECT ? 511u : t < 508u ? t : 510u;
+            postings.push_back(!P.post_tmpl ? rr : rr | code << 23);
         }
+        return (uint32_t)std::min<size_t>(postings.size() - p0, 0xFFFFFFFFu);
     };
     // open-addressing table of `groups` (key -> rules) at hents[hoff ..): returns hmask
     auto add_eq_table = [&](const std::map<uint64_t, std::vector<uint32_t>>& groups, const std::vector<uint32_t>& tmpl_of,
@@ -462,9 +463,8 @@ int mxp_engine::build_plan(Plan& P) {
             std::stable_sort(rs.begin(), rs.end(), [&](uint32_t a, uint32_t b) { return tmpl_of[a] < tmpl_of[b]; });
             uint32_t h = mxp_hash64(kv.first) & (cap - 1);
             while (hents[*hoff + h].len) h = (h + 1) & (cap - 1);
-            hents[*hoff + h] = mxp_hent{(uint32_t)kv.first, (uint32_t)(kv.first >> 32), (uint32_t)postings.size(),
-                                        (uint32_t)rs.size()};
-            post(rs, tmpl_of);
+            const uint32_t start = (uint32_t)postings.size();
+            hents[*hoff + h] = mxp_hent{(uint32_t)kv.first, (uint32_t)(kv.first >> 32), start, post(rs, tmpl_of)};
         }
         return cap - 1;
     };
@@ -500,14 +500,14 @@ int mxp_engine::build_plan(Plan& P) {
             // (vm.h mxp_index: entry pairs; a key of <= 20 bytes rides inline -- bytes 0..3 in the first
             // entry's klo, 4..19 in the second entry -- so a probe verifies it with no key-string loads;
             // longer keys keep their string id; the key length sits in the top byte of the count)
-            if (rs.size() >= (1u << 24)) return fail(MXP_ERR_NOMEM, "prefix posting list too long");
             uint32_t kw[5] = {0, 0, 0, 0, 0};
             const bool inl = key.size() <= 20;
             if (inl) memcpy(kw, key.data(), key.size());
-            hents[x.hoff + 2 * h] = mxp_hent{inl ? kw[0] : (uint32_t)kv.first, (uint32_t)(hh >> 32), (uint32_t)postings.size(),
-                                             (uint32_t)rs.size() | ((uint32_t)std::min<size_t>(key.size(), 255) << 24)};
+            const uint32_t start = (uint32_t)postings.size(), cnt = post(rs, rule_tmpl);
+            if (cnt >= (1u << 24)) return fail(MXP_ERR_NOMEM, "prefix posting list too long");
+            hents[x.hoff + 2 * h] = mxp_hent{inl ? kw[0] : (uint32_t)kv.first, (uint32_t)(hh >> 32), start,
+                                             cnt | ((uint32_t)std::min<size_t>(key.size(), 255) << 24)};
             hents[x.hoff + 2 * h + 1] = mxp_hent{kw[1], kw[2], kw[3], kw[4]};
-            post(rs, rule_tmpl);
         }
         x.plen0 = (uint32_t)plens.size();
         x.nplen = (uint32_t)lens.size();
@@ -552,10 +552,11 @@ int mxp_engine::build_plan(Plan& P) {
             if (rs.size() >= (1u << 24)) return fail(MXP_ERR_NOMEM, "composite posting list too long");
             uint32_t kw[3] = {0, 0, 0};
             if (key.size() <= 12) memcpy(kw, key.data(), key.size());
+            const uint32_t start = (uint32_t)postings.size();
+            post(rs, rule_tmpl2);  // (no expansion: the composite table's own templates)
             hents[x.hoff2 + 2 * h] = mxp_hent{key.size() <= 12 ? kw[0] : kv.first.second, (uint32_t)(hh >> 32),
-                                              (uint32_t)postings.size(), (uint32_t)rs.size() | ((uint32_t)std::min<size_t>(key.size(), 255) << 24)};
+                                              start, (uint32_t)rs.size() | ((uint32_t)std::min<size_t>(key.size(), 255) << 24)};
             hents[x.hoff2 + 2 * h + 1] = mxp_hent{(uint32_t)k1, (uint32_t)(k1 >> 32), kw[1], kw[2]};
-            post(rs, rule_tmpl2);
         }
         x.plen0 = (uint32_t)plens.size();
         x.nplen = (uint32_t)lens.size();

@@ -607,7 +607,7 @@ struct mxp_engine : public mxp::LowerTables {
     uint32_t dp_mask[4] = {0, 0, 0, 0};
     // device packer scratch, reused across uploads
     DevBuf pk_soff, pk_sbytes, pk_tsec, pk_tnsec, pk_moff, pk_mkey, pk_mval, pk_ck[64], pk_cv[64];
-    DevBuf pk_sid, pk_braw, pk_bcan, pk_tid, pk_use, pk_maxlen, pk_tab[4], pk_scan, pk_scan_blocks;
+    DevBuf pk_sid, pk_braw, pk_bcan, pk_tid, pk_use, pk_maxlen, pk_tab[4], pk_scan, pk_scan_blocks, pk_scan_max;
     DevBuf pk_vtd_lkey, pk_vtd_lcr, pk_vtd_ln, pk_vtd_tkey, pk_vtd_tcr, pk_vtd_meta, pk_rx, pk_rxv;
     void* pk_host = nullptr;  // pinned read-back (longest string, value-class distinct counts)
     uint32_t vcol_key_id(uint32_t j) const {

@@ -76,9 +76,9 @@ __device__ __forceinline__ bool same(const uint8_t* a, uint32_t na, const uint8_
 
 // BYTES values mark their batch strings (raw / canonical interning covers only those)
 extern "C" __global__ __launch_bounds__(256) void mxp_pack_mark_kernel(mxp_pack_args A) {
-    for (uint64_t i = gtid(); i < (uint64_t)A.ncol * A.n; i += gstride()) {
-        const uint32_t c = (uint32_t)(i / A.n), r = (uint32_t)(i % A.n);
-        if (!A.ck[c] || A.vkey[c] != kNone) continue;
+    const uint32_t c = blockIdx.y;  // (grid: requests x columns)
+    if (!A.ck[c] || A.vkey[c] != kNone) return;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < A.n; r += (uint64_t)gridDim.x * blockDim.x) {
         if (A.ck[c][r] == MXP_BYTES) {
             const uint64_t v = A.cv[c][r];
             if (v < A.ns) A.use[v] = 1;
@@ -91,8 +91,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_mark_kernel(mxp_pack_
 // occupied slot with the same hash tag is compared byte by byte (the items are immutable input,
 // so a winner's content is readable without further ordering).  id = base + representative.
 // Strings (MXP_IK_STR) hash and compare 8 bytes at a time (the batch blob and the pools carry 16
-// bytes of slack); the longest length is a wave maximum, one atomic per wave (a per-string atomic
-// on one address serialised every wave of the pass behind it).
+// bytes of slack).  (The longest string comes from the scan kernels: an atomic max per wave here --
+// 28k waves on one address for C2's 1.8M strings, ~11 ns each -- was 0.33 ms of this pass.)
 __device__ __forceinline__ uint64_t ld8_any(const uint8_t* p) {
     const uintptr_t a = (uintptr_t)p;
     const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
@@ -123,21 +123,23 @@ __device__ __forceinline__ bool same_words(const uint8_t* a, uint32_t na, const 
     return true;
 }
 
-extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_kernel(mxp_pack_args A) {
-    uint8_t buf[16], pbuf[16];
-    const bool words = A.kind == MXP_IK_STR;
-    uint32_t maxlen = 0;
-    // (a uniform trip count per wave: the wave maximum below needs every lane)
-    for (uint64_t i0 = A.i0 + (gtid() & ~63ull); i0 < A.i1; i0 += gstride()) {
-        const uint64_t idx = i0 + (threadIdx.x & 63u);
-        if (idx >= A.i1) continue;
+// (kWords: the string pass -- its items are the batch strings as given, so it needs no buffers for
+// synthesized forms and no scratch)
+template <bool kWords>
+__device__ __forceinline__ void intern_body(const mxp_pack_args& A) {
+    uint8_t buf[kWords ? 1 : 16], pbuf[kWords ? 1 : 16];
+    constexpr bool words = kWords;
+    for (uint64_t idx = A.i0 + gtid(); idx < A.i1; idx += gstride()) {
         const uint8_t* p;
         uint32_t n;
-        if (!item_of(A, A.kind, idx, &p, &n, buf)) {
+        if constexpr (kWords) {
+            const uint64_t o = A.soff[idx];
+            p = A.sbytes + o;
+            n = (uint32_t)(A.soff[idx + 1] - o);
+        } else if (!item_of(A, A.kind, idx, &p, &n, buf)) {
             A.out[idx] = kNone;
             continue;
         }
-        if (words) maxlen = max(maxlen, n);
         const uint64_t h = words ? str_hash_words(p, n) : mxp_item_hash(p, n);
         const uint64_t tag = h >> 32;
         uint32_t id = kNone;
@@ -148,7 +150,13 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_kernel(mxp_pac
                 if ((e >> 32) != tag) continue;
                 const uint8_t* q;
                 uint32_t m;
-                pool_item(A.pool, A.kind, (uint32_t)e - 1u, &q, &m, pbuf);
+                if constexpr (kWords) {
+                    const uint64_t d = A.pool.desc[(uint32_t)e - 1u];
+                    q = A.pool.blob + (d >> 24);
+                    m = (uint32_t)(d & 0xFFFFFFu);
+                } else {
+                    pool_item(A.pool, A.kind, (uint32_t)e - 1u, &q, &m, pbuf);
+                }
                 if (words ? same_words(p, n, q, m) : same(p, n, q, m)) {
                     id = (uint32_t)e - 1u;
                     break;
@@ -170,7 +178,13 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_kernel(mxp_pac
                 const uint64_t other = (uint32_t)e - 1u;
                 const uint8_t* q;
                 uint32_t m;
-                item_of(A, A.kind, other, &q, &m, pbuf);
+                if constexpr (kWords) {
+                    const uint64_t o = A.soff[other];
+                    q = A.sbytes + o;
+                    m = (uint32_t)(A.soff[other + 1] - o);
+                } else {
+                    item_of(A, A.kind, other, &q, &m, pbuf);
+                }
                 if (words ? same_words(p, n, q, m) : same(p, n, q, m)) {
                     id = A.base + (uint32_t)other;
                     break;
@@ -179,18 +193,16 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_kernel(mxp_pac
         }
         A.out[idx] = id;
     }
-    if (words && A.max_len_out) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) maxlen = max(maxlen, (uint32_t)__shfl_xor((int)maxlen, off, 64));
-        if ((threadIdx.x & 63u) == 0 && maxlen) atomicMax(A.max_len_out, maxlen);
-    }
 }
+extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_kernel(mxp_pack_args A) { intern_body<false>(A); }
+extern "C" __global__ __launch_bounds__(256) void mxp_pack_intern_str_kernel(mxp_pack_args A) { intern_body<true>(A); }
 
 // The engine's columns: kinds / values through the id maps (strings, byte strings, timestamps);
 // virtual map[key] columns: the entry whose key is the column's key (interned ids compare).
+// (grid: requests x columns, blockIdx.y = column -- no 64-bit division per element)
 extern "C" __global__ __launch_bounds__(256) void mxp_pack_gather_kernel(mxp_pack_args A) {
-    for (uint64_t i = gtid(); i < (uint64_t)A.ncol * A.n; i += gstride()) {
-        const uint32_t c = (uint32_t)(i / A.n), r = (uint32_t)(i % A.n);
+    const uint32_t c = blockIdx.y;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < A.n; r += (uint64_t)gridDim.x * blockDim.x) {
         uint8_t k = 0;
         uint64_t v = 0;
         if (A.ck[c]) {
@@ -231,14 +243,27 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_maps_kernel(mxp_pack_
 }
 
 // aligned overlay pool: exclusive scan of the 8-aligned lengths (block sums, a one-block scan of
-// them, add back), then one thread per string copies its bytes
+// them, add back), then one thread per string copies its bytes.  The scans also find the longest
+// string (block maxima, reduced by the one-block scan).
 #define MXP_SCAN_B 1024u
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, off, 64));
+    return x;
+}
 extern "C" __global__ __launch_bounds__(1024) void mxp_pack_scan1_kernel(mxp_pack_args A) {
     __shared__ uint64_t sh[MXP_SCAN_B];
+    __shared__ uint32_t bmax;
     const uint64_t i = (uint64_t)blockIdx.x * MXP_SCAN_B + threadIdx.x;
-    const uint64_t len = i < A.ns ? ((A.soff[i + 1] - A.soff[i] + 7u) & ~7ull) : 0;
+    const uint64_t raw = i < A.ns ? A.soff[i + 1] - A.soff[i] : 0;
+    const uint64_t len = (raw + 7u) & ~7ull;
+    if (threadIdx.x == 0) bmax = 0u;
     sh[threadIdx.x] = len;
     __syncthreads();
+    {
+        const uint32_t m = wave_max_u32((uint32_t)min(raw, (uint64_t)0xFFFFFFFFu));
+        if ((threadIdx.x & 63u) == 0) atomicMax(&bmax, m);  // (LDS: 16 per block)
+    }
     for (uint32_t o = 1; o < MXP_SCAN_B; o <<= 1) {
         const uint64_t x = threadIdx.x >= o ? sh[threadIdx.x - o] : 0;
         __syncthreads();
@@ -247,11 +272,22 @@ extern "C" __global__ __launch_bounds__(1024) void mxp_pack_scan1_kernel(mxp_pac
     }
     if (i < A.ns) A.scan[i] = sh[threadIdx.x] - len;  // exclusive within the block
     if (threadIdx.x == MXP_SCAN_B - 1) A.scan_blocks[blockIdx.x] = sh[threadIdx.x];
+    if (threadIdx.x == 0) A.scan_max[blockIdx.x] = bmax;  // (bmax final: the scan loop's barriers)
 }
 extern "C" __global__ __launch_bounds__(1024) void mxp_pack_scan2_kernel(mxp_pack_args A, uint32_t nblocks) {
     __shared__ uint64_t carry;
-    if (threadIdx.x == 0) carry = 0;
+    __shared__ uint32_t lmax;
+    if (threadIdx.x == 0) {
+        carry = 0;
+        lmax = 0u;
+    }
     __syncthreads();
+    {
+        uint32_t m = 0;
+        for (uint32_t b = threadIdx.x; b < nblocks; b += MXP_SCAN_B) m = max(m, A.scan_max[b]);
+        m = wave_max_u32(m);
+        if ((threadIdx.x & 63u) == 0) atomicMax(&lmax, m);
+    }
     for (uint32_t b0 = 0; b0 < nblocks; b0 += MXP_SCAN_B) {
         __shared__ uint64_t sh[MXP_SCAN_B];
         const uint32_t b = b0 + threadIdx.x;
@@ -270,14 +306,23 @@ extern "C" __global__ __launch_bounds__(1024) void mxp_pack_scan2_kernel(mxp_pac
         if (threadIdx.x == MXP_SCAN_B - 1) carry = c + sh[threadIdx.x];
         __syncthreads();
     }
-    if (threadIdx.x == 0) A.scan[A.ns] = carry;  // total
+    if (threadIdx.x == 0) {
+        A.scan[A.ns] = carry;  // total
+        if (A.max_len_out) *A.max_len_out = lmax;  // (lmax final: the loop's barriers)
+    }
 }
+// (8 bytes at a time: the destination is 8-aligned, the source is read through ld8_any -- the batch
+// blob carries 16 bytes of slack -- and the last word is zero past the string)
 extern "C" __global__ __launch_bounds__(256) void mxp_pack_copy_kernel(mxp_pack_args A) {
     for (uint64_t i = gtid(); i < A.ns; i += gstride()) {
         const uint64_t o = A.scan[i] + A.scan_blocks[i / MXP_SCAN_B];
         const uint64_t s0 = A.soff[i], n = A.soff[i + 1] - s0;
         A.bdesc[i] = (o << 24) | n;
-        for (uint64_t k = 0; k < ((n + 7u) & ~7ull); k++) A.bblob[o + k] = k < n ? A.sbytes[s0 + k] : 0;
+        uint64_t* dst = (uint64_t*)(A.bblob + o);
+        for (uint64_t k = 0; k < n; k += 8u) {
+            const uint64_t r = n - k;
+            dst[k / 8u] = ld8_any(A.sbytes + s0 + k) & (r >= 8u ? ~0ull : (1ull << (8u * r)) - 1ull);
+        }
     }
 }
 
@@ -285,67 +330,55 @@ extern "C" __global__ __launch_bounds__(256) void mxp_pack_copy_kernel(mxp_pack_
 // meets more than MXP_VTD_MERGE global atomics (a column's few Zipf-hot values would otherwise take
 // one probe and one count atomic from every tile).
 // Level 1 (grid: tiles of MXP_VTD_TILE requests x candidate columns): the tile's distinct keys in an
-// LDS table -- a key's count added once per wave (ballot over the lanes holding it) -- then written
-// out as the tile's list (wave-compacted, plain stores).
+// LDS table -- each request adds 1 to its key's count (LDS atomics; a per-wave ballot loop over the
+// distinct keys cost ~1,500 scalar instructions per wave on C4) -- then written out as the tile's
+// list, from the slots the inserting lanes listed (not a scan of the whole table).
 #define MXP_VTD_LCAP 2048u
 extern "C" __global__ __launch_bounds__(256) void mxp_pack_vtd_local_kernel(mxp_pack_args A) {
     __shared__ unsigned long long lkey[MXP_VTD_LCAP];
     __shared__ uint32_t lcnt[MXP_VTD_LCAP], lrep[MXP_VTD_LCAP];
-    __shared__ uint32_t nout;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, a = blockIdx.y, t = blockIdx.x;
+    __shared__ uint16_t lslot[MXP_VTD_TILE];  // the occupied slots, in insertion order
+    __shared__ uint32_t nins;
+    const uint32_t tid = threadIdx.x, a = blockIdx.y, t = blockIdx.x;
     const uint32_t c = A.vt_col[a];
     for (uint32_t i = tid; i < MXP_VTD_LCAP; i += 256u) {
         lkey[i] = ~0ull;
         lcnt[i] = 0u;
     }
-    if (tid == 0) nout = 0u;
+    if (tid == 0) nins = 0u;
     __syncthreads();
     const uint64_t base = (uint64_t)t * MXP_VTD_TILE;
 #pragma unroll
     for (uint32_t r = 0; r < MXP_VTD_TILE / 256u; r++) {
         const uint64_t req = base + tid + 256u * r;
-        uint32_t h = 0xFFFFFFFFu;
-        if (req < A.n) {
-            const unsigned long long key = mxp_vt_key(A.kinds[(uint64_t)c * A.n + req], A.vals[(uint64_t)c * A.n + req]);
-            h = (uint32_t)mxp_hash64(key) & (MXP_VTD_LCAP - 1u);
-            for (;;) {
-                const unsigned long long cur = lkey[h];
-                if (cur == key) break;
-                if (cur == ~0ull) {
-                    const unsigned long long old = atomicCAS(&lkey[h], ~0ull, key);
-                    if (old == ~0ull) {
-                        lrep[h] = (uint32_t)req;
-                        break;
-                    }
-                    if (old == key) break;
+        if (req >= A.n) continue;
+        const unsigned long long key = mxp_vt_key(A.kinds[(uint64_t)c * A.n + req], A.vals[(uint64_t)c * A.n + req]);
+        uint32_t h = (uint32_t)mxp_hash64(key) & (MXP_VTD_LCAP - 1u);
+        for (;;) {
+            const unsigned long long cur = lkey[h];
+            if (cur == key) break;
+            if (cur == ~0ull) {
+                const unsigned long long old = atomicCAS(&lkey[h], ~0ull, key);
+                if (old == ~0ull) {
+                    lrep[h] = (uint32_t)req;
+                    lslot[atomicAdd(&nins, 1u)] = (uint16_t)h;
+                    break;
                 }
-                h = (h + 1u) & (MXP_VTD_LCAP - 1u);
+                if (old == key) break;
             }
+            h = (h + 1u) & (MXP_VTD_LCAP - 1u);
         }
-        for (uint64_t pend = __ballot(h != 0xFFFFFFFFu); pend;) {
-            const uint32_t sl = __builtin_amdgcn_readlane(h, (uint32_t)__builtin_ctzll(pend));
-            const uint64_t same = __ballot(h == sl);
-            if (lane == (uint32_t)__builtin_ctzll(same)) atomicAdd(&lcnt[sl], (uint32_t)__builtin_popcountll(same));
-            pend &= ~same;
-        }
+        atomicAdd(&lcnt[h], 1u);
     }
     __syncthreads();
     const uint64_t lo = ((uint64_t)a * A.vtd_tiles + t) * MXP_VTD_TILE;
-    for (uint32_t i0 = 0; i0 < MXP_VTD_LCAP; i0 += 256u) {
-        const uint32_t i = i0 + tid;
-        const unsigned long long key = lkey[i];
-        const bool has = key != ~0ull;
-        const uint64_t m = __ballot(has);
-        uint32_t at = 0;
-        if (lane == 0 && m) at = atomicAdd(&nout, (uint32_t)__builtin_popcountll(m));
-        at = (uint32_t)__shfl((int)at, 0, 64) + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
-        if (has) {
-            A.vtd_lkey[lo + at] = key;
-            A.vtd_lcr[lo + at] = make_uint2(lcnt[i], lrep[i]);
-        }
+    const uint32_t k = nins;
+    for (uint32_t i = tid; i < k; i += 256u) {
+        const uint32_t h = lslot[i];
+        A.vtd_lkey[lo + i] = lkey[h];
+        A.vtd_lcr[lo + i] = make_uint2(lcnt[h], lrep[h]);
     }
-    __syncthreads();
-    if (tid == 0) A.vtd_ln[(uint64_t)a * A.vtd_tiles + t] = nout;
+    if (tid == 0) A.vtd_ln[(uint64_t)a * A.vtd_tiles + t] = k;
 }
 
 // Level 2 (grid: MXP_VTD_MERGE x candidate columns): a workgroup merges its share of the tile
@@ -488,9 +521,18 @@ uint32_t grid_for(uint64_t work) {
 
 extern "C" hipError_t mxp_launch_pack(const mxp_pack_args* a, uint32_t step, uint32_t arg, hipStream_t s) {
     switch (step) {
-    case 0: hipLaunchKernelGGL(mxp_pack_mark_kernel, dim3(grid_for((uint64_t)a->ncol * a->n)), dim3(256), 0, s, *a); break;
-    case 1: hipLaunchKernelGGL(mxp_pack_intern_kernel, dim3(grid_for(a->i1 - a->i0)), dim3(256), 0, s, *a); break;
-    case 2: hipLaunchKernelGGL(mxp_pack_gather_kernel, dim3(grid_for((uint64_t)a->ncol * a->n)), dim3(256), 0, s, *a); break;
+    case 0:
+        if (a->ncol) hipLaunchKernelGGL(mxp_pack_mark_kernel, dim3(grid_for(a->n), a->ncol), dim3(256), 0, s, *a);
+        break;
+    case 1:
+        if (a->kind == MXP_IK_STR)
+            hipLaunchKernelGGL(mxp_pack_intern_str_kernel, dim3(grid_for(a->i1 - a->i0)), dim3(256), 0, s, *a);
+        else
+            hipLaunchKernelGGL(mxp_pack_intern_kernel, dim3(grid_for(a->i1 - a->i0)), dim3(256), 0, s, *a);
+        break;
+    case 2:
+        if (a->ncol) hipLaunchKernelGGL(mxp_pack_gather_kernel, dim3(grid_for(a->n), a->ncol), dim3(256), 0, s, *a);
+        break;
     case 3: hipLaunchKernelGGL(mxp_pack_maps_kernel, dim3(grid_for(a->n_entries + a->nm + 1)), dim3(256), 0, s, *a); break;
     case 4: {
         const uint32_t nb = (a->ns + MXP_SCAN_B - 1) / MXP_SCAN_B;

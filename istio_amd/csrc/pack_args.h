@@ -142,7 +142,8 @@ typedef struct mxp_pack_args {
     uint32_t vtd_tiles;
     uint32_t vt_col[MXP_PACK_VTCAND];
     uint32_t n_vt_cand;
-    uint32_t* max_len_out;          // longest batch string (atomic max)
+    uint32_t* max_len_out;          // longest batch string (written by mxp_pack_scan2_kernel)
+    uint32_t* scan_max;             // per scan block: its longest string
     // run-time regexp patterns: (batch string | 0x80000000 + engine id, rxof value) pairs scattered
     // by interned id
     const uint32_t* rx_s;

@@ -282,10 +282,12 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((e = hipMemsetAsync(db->bstr.p, 0, sbytes + 8ull * NS + 16, s)) != hipSuccess) return hipfail(e, "reset bstr");
     if ((rc = grow(pk_scan, ((size_t)NS + 1) * 8, "scan"))) return rc;
     if ((rc = grow(pk_scan_blocks, ((size_t)NS / 1024 + 2) * 8, "scan"))) return rc;
+    if ((rc = grow(pk_scan_max, ((size_t)NS / 1024 + 2) * 4, "scan"))) return rc;
     A.bdesc = db->bstr_off.as<uint64_t>();
     A.bblob = db->bstr.as<uint8_t>();
     A.scan = pk_scan.as<uint64_t>();
     A.scan_blocks = pk_scan_blocks.as<uint64_t>();
+    A.scan_max = pk_scan_max.as<uint32_t>();
     if ((rc = launch(4))) return rc;
     // ---- ip() / timestamp() pre-tables: parse every string id, intern the parsed values
     if ((rc = alloc(db->ipof, need_ipof ? S * 8 : 0, "ipof"))) return rc;
