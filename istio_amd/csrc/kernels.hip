@@ -1722,143 +1722,6 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
                 if (anyerr[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;
     }
 }
-// The immediate-offset fill with ONE request per lane (MXP_DEBUG_FLAGS 268435456 selects it for A/B):
-// a request's class words need no per-lane selection among four requests -- its deferred pairs
-// (the quad's slot row, filtered to this request) merge with one shift, and each group's gathers,
-// ORs and store are a fifth of the quad kernel's registers -- at four times the waves and 4-byte
-// stores (a wave's 256 contiguous bytes per group row).
-template <uint32_t NVT>
-__device__ __forceinline__ void vtfill_r1_body(const mxp_kargs& A) {
-    __shared__ uint32_t SM[NVT * MXP_FILL_CHUNK * MXP_VTI_CAP];
-    __shared__ uint32_t SJ[NVT * MXP_FILL_CHUNK];
-    __shared__ uint32_t eflag;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
-    const mxp_fill* F = A.fills + blockIdx.y;
-    const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
-    const uint32_t chunk = A.dtp_cbase + blockIdx.y;
-    for (uint32_t i = tid; i < NVT * MXP_FILL_CHUNK * MXP_VTI_CAP; i += 256u) SM[i] = 0u;
-    if (tid < NVT * MXP_FILL_CHUNK) SJ[tid] = ~0u;
-    if (tid == 0) eflag = 0u;
-    __syncthreads();
-    const uint32_t TB = lane < NVT ? A.vt_meta[lane * 8u + MXP_VTM_TBASE] : 0u;
-    uint32_t eor = 0u;
-    for (uint32_t g = 0; g < n; g++) {
-        const uint32_t i0 = uni(A.gvt_off[g0 + g]), i1 = uni(A.gvt_off[g0 + g + 1u]);
-        for (uint32_t x = tid; x < (i1 - i0) * MXP_VTI_CAP; x += 256u) {
-            const uint32_t ent = A.gvt[i0 + x / MXP_VTI_CAP], a = ent >> 24, j = ent & 0xFFFFFFu, k = x % MXP_VTI_CAP;
-            const uint32_t tb = __builtin_amdgcn_ds_bpermute((int)(a << 2), (int)TB);
-            const uint2 w = *(const uint2*)(A.vt_tm + 2u * ((uint64_t)tb + (uint64_t)j * MXP_VTI_CAP + k));
-            SM[(a * MXP_FILL_CHUNK + g) * MXP_VTI_CAP + k] = w.x;
-            if (k == 0) SJ[a * MXP_FILL_CHUNK + g] = j;
-            eor |= w.y;
-        }
-    }
-    if (__ballot(eor != 0u)) {
-        if (lane == 0) atomicOr(&eflag, 1u);
-    }
-    __syncthreads();
-    const bool errs = eflag != 0u;
-    const uint64_t N = A.n;
-    const uint32_t Q1 = A.q1;
-    const bool nt = !(A.flags & 128u);
-    const uint32_t FM = lane < n ? A.fill_masks[moff + lane] : 0u;
-    // a workgroup covers the quad kernel's requests: MXP_VTF_TILES x 1024, in tiles of 256
-    for (uint32_t t = 0; t < 4u * MXP_VTF_TILES; t++) {
-        const uint32_t qw = A.q0 + (blockIdx.x * MXP_VTF_TILES * 4u + t) * 256u + wave * 64u;
-        if (qw >= Q1) break;
-        const uint32_t q = qw + lane;
-        const bool in = q < Q1;
-        const uint32_t kq = in ? A.kinds[(uint64_t)col * N + q] : 0u;
-        const uint32_t bad = (in && !((okset >> kq) & 1u)) ? ~0u : 0u;
-        uint32_t ad[NVT];
-#pragma unroll
-        for (uint32_t a = 0; a < NVT; a++)
-            ad[a] = a * MXP_FILL_CHUNK * MXP_VTI_CAP + (in ? ((uint32_t)A.vt_cls[(uint64_t)a * N + q] & (MXP_VTI_CAP - 1u)) : 0u);
-        // this request's deferred pairs of the chunk: the quad's slot row, filtered, sorted by group
-        uint32_t dq0 = ~0u, dq1 = ~0u, dq2 = ~0u, dq3 = ~0u;
-        if (A.dtp_slots && in) {
-            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-            const uint64_t qi = (uint64_t)chunk * A.dtp_tiles * 256u + (q >> 2);
-            const uint32_t dk = A.dtp_qn[qi];
-            if (dk) {
-                const v4u sl = *(const v4u*)(A.dtp_slots + qi * 8u);
-                const uint32_t h[4] = {sl.x, sl.y, sl.z, sl.w};
-                uint32_t x[8];
-#pragma unroll
-                for (uint32_t i = 0; i < 8; i++) {
-                    const uint32_t v = (h[i >> 1] >> (16u * (i & 1u))) & 0xFFFFu;
-                    x[i] = (i < dk && ((v >> 5) & 3u) == (q & 3u)) ? v : 0xFFFFu;
-                }
-                sort8(x);
-                dq0 = x[0] | x[1] << 16;
-                dq1 = x[2] | x[3] << 16;
-                dq2 = x[4] | x[5] << 16;
-                dq3 = x[6] | x[7] << 16;
-            }
-        }
-        const bool dany = __ballot(dq0 != ~0u) != 0;
-        uint32_t anyerr = 0u;
-        for (uint32_t g = 0; g < n; g++) {
-            const uint32_t G = g0 + g;
-            const uint32_t mask = __builtin_amdgcn_readlane(FM, g);
-            uint32_t m = 0u, e = bad & mask;
-            if (A.errlog && e && in) log_guard_errors(A, e, G * 32u, q);
-#pragma unroll
-            for (uint32_t a = 0; a < NVT; a++) m |= SM[ad[a] + g * MXP_VTI_CAP];
-            if (errs) {
-                uint32_t ve = 0u;
-#pragma unroll
-                for (uint32_t a = 0; a < NVT; a++) {
-                    const uint32_t j = SJ[a * MXP_FILL_CHUNK + g];
-                    if (j == ~0u) continue;
-                    const uint64_t row = (uint64_t)__builtin_amdgcn_readlane(TB, a) + (uint64_t)j * MXP_VTI_CAP;
-                    ve |= A.vt_tm[2u * (row + (ad[a] & (MXP_VTI_CAP - 1u))) + 1u];
-                }
-                if (A.errlog) vt_count_n(A, in ? (uint32_t)__builtin_popcount(ve) : 0u);
-                e |= ve;
-            }
-            if (dany) {
-                for (;;) {
-                    const uint32_t x = dq0 & 0xFFFFu;
-                    const bool hit = (x >> 8) == g;
-                    if (!__ballot(hit)) break;
-                    if (hit) {
-                        const uint32_t b = 1u << (x & 31u);
-                        if (x & 128u) e |= b;
-                        else m |= b;
-                        dq0 = __builtin_amdgcn_alignbit(dq1, dq0, 16);
-                        dq1 = __builtin_amdgcn_alignbit(dq2, dq1, 16);
-                        dq2 = __builtin_amdgcn_alignbit(dq3, dq2, 16);
-                        dq3 = dq3 >> 16 | 0xFFFF0000u;
-                    }
-                }
-            }
-            anyerr |= e;
-            if (in) {
-                const uint64_t at = (uint64_t)G * N + q;
-                if (nt) {
-                    if (A.out_match) __builtin_nontemporal_store(m, A.out_match + at);
-                    if (A.out_err) __builtin_nontemporal_store(e, A.out_err + at);
-                } else {
-                    if (A.out_match) A.out_match[at] = m;
-                    if (A.out_err) A.out_err[at] = e;
-                }
-            }
-        }
-        if (A.req_err && anyerr && in) A.req_err[q] = 1;
-    }
-}
-#define MXP_VTFILL_R1(K) \
-    extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_r1_##K##_kernel(mxp_kargs A) { vtfill_r1_body<K>(A); }
-MXP_VTFILL_R1(1)
-MXP_VTFILL_R1(2)
-MXP_VTFILL_R1(3)
-MXP_VTFILL_R1(4)
-MXP_VTFILL_R1(5)
-MXP_VTFILL_R1(6)
-MXP_VTFILL_R1(7)
-MXP_VTFILL_R1(8)
-#undef MXP_VTFILL_R1
 #define MXP_VTFILL_IMM(K) \
     extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_imm##K##_kernel(mxp_kargs A) { vtfill_imm_body<K>(A); }
 MXP_VTFILL_IMM(1)
@@ -2684,19 +2547,7 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
         // every active class table at 64 slots: the immediate-offset kernel for this many columns
         // (flag 33554432: mxp_vtfill_lds_kernel -- A/B)
         void (*k)(mxp_kargs) = mxp_vtfill_lds_kernel;
-        if (args->vt_imm && !(args->flags & 33554432u) && (args->flags & 268435456u)) {
-            switch (args->n_vt) {  // (one request per lane)
-            case 1: k = mxp_vtfill_r1_1_kernel; break;
-            case 2: k = mxp_vtfill_r1_2_kernel; break;
-            case 3: k = mxp_vtfill_r1_3_kernel; break;
-            case 4: k = mxp_vtfill_r1_4_kernel; break;
-            case 5: k = mxp_vtfill_r1_5_kernel; break;
-            case 6: k = mxp_vtfill_r1_6_kernel; break;
-            case 7: k = mxp_vtfill_r1_7_kernel; break;
-            case 8: k = mxp_vtfill_r1_8_kernel; break;
-            default: break;
-            }
-        } else if (args->vt_imm && !(args->flags & 33554432u)) {
+        if (args->vt_imm && !(args->flags & 33554432u)) {
             switch (args->n_vt) {
             case 1: k = mxp_vtfill_imm1_kernel; break;
             case 2: k = mxp_vtfill_imm2_kernel; break;

@@ -6,8 +6,7 @@ the class (engine.cpp expand_class_errors).  MXP_DEBUG_FLAGS 262144 forces value
 batch size (the default wants >= 16 requests per class); 131072 turns them off; 2097152 makes the
 fill chunks gather class words from global memory instead of the LDS-staged rows
 (mxp_vtfill_kernel vs mxp_vtfill_lds_kernel); 33554432 keeps batches whose class tables all have 64
-slots on mxp_vtfill_lds_kernel instead of mxp_vtfill_imm<n>_kernel; 268435456 takes the
-one-request-per-lane form of that kernel (mxp_vtfill_r1_<n>_kernel)."""
+slots on mxp_vtfill_lds_kernel instead of mxp_vtfill_imm<n>_kernel."""
 import numpy as np
 import pytest
 
@@ -20,7 +19,6 @@ pytestmark = pytest.mark.gpu
 FORCE, OFF, GLOBAL = "262144", "131072", "2097152"
 FORCE_GLOBAL = str(262144 | 2097152)
 FORCE_LDS = str(262144 | 33554432)  # the LDS-row kernel instead of the immediate-offset one (tables of 64 slots)
-FORCE_R1 = str(262144 | 268435456)  # the immediate-offset fill, one request per lane
 
 
 @pytest.fixture(scope="module")
@@ -37,7 +35,7 @@ def engine_for(mxp, monkeypatch, flags, manifest, rules):
     return eng
 
 
-@pytest.mark.parametrize("flags", [FORCE, "0", FORCE_GLOBAL, FORCE_LDS, FORCE_R1])
+@pytest.mark.parametrize("flags", [FORCE, "0", FORCE_GLOBAL, FORCE_LDS])
 def test_c4_value_classes_parity(mxp, monkeypatch, flags):
     """C4 routes: the header rules (equality and regexps on request.headers["h"]) become value
     classes (17 values per header); path rules stay with the prefix index."""
@@ -48,7 +46,7 @@ def test_c4_value_classes_parity(mxp, monkeypatch, flags):
     assert (want == 1).sum() > 1000
 
 
-@pytest.mark.parametrize("flags", [FORCE, FORCE_LDS, FORCE_R1])
+@pytest.mark.parametrize("flags", [FORCE, FORCE_LDS])
 def test_fuzz_value_classes_errors(mxp, monkeypatch, flags):
     """Random rules over random bags with missing / wrongly typed values: class records (lookup and
     conversion errors, panics) expanded to every request of the class, texts checked; class words
