@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--list-cpu-seconds", type=float, default=4.0, help="CPU-baseline sample per C3 list kind")
     p.add_argument("--no-c3", action="store_true", help="default run: skip the extra C3 list block")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--quota-serial", action="store_true",
+                   help="C5: the memquota batch after the evaluation on one stream (default: a second stream beside it)")
     p.add_argument("--no-c4", action="store_true", help="default run: skip the extra C4 block")
     p.add_argument("--no-c5", action="store_true", help="default run: skip the extra C5 block")
     p.add_argument("--workload", default="c2", choices=["c2", "c4", "c5", "c3-ip", "c3-str", "c3-regex", "c5-quota"],
@@ -279,19 +281,35 @@ def shard_workload(kind, n_rules, requests_per_gpu, rank, world):
     return manifest, W.c2_rules(n_rules, seed=2)[0], batch
 
 
-def make_step(ctr, evaluate, quota_alloc=None, stream=None):
+def make_step(ctr, evaluate, quota_alloc=None, stream=None, qstream=None):
     """The bench step: evaluate every pair of the shard with the hit counters
     accumulated into the step's hits view, optionally the shard's memquota batch with its per-key
     deltas into the quota view, then the step's ONE all-reduce of hits[R] ++ quota_delta[K]
-    (StepCounters.end_step; nothing on a single process).  ev0 / ev1 bracket the kernels."""
+    (StepCounters.end_step; nothing on a single process).  ev0 / ev1 bracket the kernels.
+    With `qstream` the memquota batch runs on that second stream beside the evaluation (the two
+    touch disjoint buffers; its latency-bound replay overlaps the predicate kernels), forked after
+    the counters are zeroed and joined before the all-reduce."""
+    fork = join = None
+    if qstream is not None:
+        import torch
+        fork, join = torch.cuda.Event(), torch.cuda.Event()
+
     def step(ev0=None, ev1=None):
         ctr.begin_step()
         views = ctr.views()
         if ev0 is not None:
             ev0.record(stream)
+        if quota_alloc is not None and qstream is not None:
+            fork.record(stream)
+            qstream.wait_event(fork)
+            quota_alloc(views[1], qstream.cuda_stream)
+            join.record(qstream)
         evaluate(views[0])
         if quota_alloc is not None:
-            quota_alloc(views[1])
+            if qstream is not None:
+                stream.wait_event(join)
+            else:
+                quota_alloc(views[1], stream.cuda_stream if stream is not None else None)
         if ev1 is not None:
             ev1.record(stream)
         ctr.end_step()
@@ -558,12 +576,14 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
     ctr = D.StepCounters([R] + ([QUOTA_KEYS] if quota else []), dev)
     now = [1_500_000_000 * 10**9]
 
-    def quota_alloc(delta):
+    def quota_alloc(delta, qsh):
         (_, q, (dk, da, dbe, dg)) = quota
-        q.alloc_device(dk.numel(), dk.data_ptr(), da.data_ptr(), dbe.data_ptr(), now[0], sh, dg.data_ptr(),
+        q.alloc_device(dk.numel(), dk.data_ptr(), da.data_ptr(), dbe.data_ptr(), now[0], qsh, dg.data_ptr(),
                        delta.data_ptr())
         now[0] += 10**8
-    step = make_step(ctr, lambda hits: evaluate(hits.data_ptr()), quota_alloc if quota is not None else None, stream)
+    qstream = torch.cuda.Stream(dev) if quota is not None and not args.quota_serial else None
+    step = make_step(ctr, lambda hits: evaluate(hits.data_ptr()), quota_alloc if quota is not None else None, stream,
+                     qstream)
 
     elapsed, ev_ms = timed_loop(step, args.steps, args.warmup, world, stream)
     step_kernel_ms = float(np.mean(ev_ms))

@@ -862,7 +862,20 @@ int mxp_engine::build_plan(Plan& P) {
     if ((rc = put(P.d_gall, gall.data(), gall.size() * 4, "upload gall"))) return rc;
     if ((rc = put(P.d_gdeep, gdeep.data(), gdeep.size() * 4, "upload gdeep"))) return rc;
     if ((rc = put(P.d_gk, gk.data(), gk.size() * 8, "upload gk"))) return rc;
+    // occupancy bitmaps of the pair tables: most probes of a key length end at an empty slot, which
+    // one bit of a small, L1-resident array tells without the entry pair's L2 request
+    std::vector<uint32_t> hbits;
+    for (mxp_index& x : idx) {
+        if (x.prefix == MXP_IX_EQ) continue;
+        const uint32_t off = x.prefix == MXP_IX_COMPOSITE ? x.hoff2 : x.hoff;
+        const uint32_t cap = (x.prefix == MXP_IX_COMPOSITE ? x.hmask2 : x.hmask) + 1u;
+        x.boff = (uint32_t)hbits.size();
+        hbits.resize(hbits.size() + (cap + 31u) / 32u, 0u);
+        for (uint32_t sl = 0; sl < cap; sl++)
+            if (hents[off + 2ull * sl].len) hbits[x.boff + sl / 32u] |= 1u << (sl % 32u);
+    }
     if ((rc = put(P.d_idx, idx.data(), idx.size() * sizeof(mxp_index), "upload idx"))) return rc;
+    if ((rc = put(P.d_hbits, hbits.data(), hbits.size() * 4, "upload hbits"))) return rc;
     if ((rc = put(P.d_hents, hents.data(), hents.size() * sizeof(mxp_hent), "upload hents"))) return rc;
     if ((rc = put(P.d_postings, postings.data(), postings.size() * 4, "upload postings"))) return rc;
     if ((rc = put(P.d_plens, plens.data(), plens.size() * 4, "upload plens"))) return rc;
@@ -1383,6 +1396,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
     A->gk = P.d_gk.as<uint64_t>();
     A->idx = P.d_idx.as<mxp_index>();
     A->hents = P.d_hents.as<mxp_hent>();
+    A->hbits = (debug_flags & 4u) || !P.d_hbits.p ? nullptr : P.d_hbits.as<uint32_t>();
     A->postings = P.d_postings.as<uint32_t>();
     A->post_tmpl = P.post_tmpl ? 1u : 0u;
     A->tmpl_lite = P.tmpl_lite ? 1u : 0u;

@@ -266,7 +266,7 @@ struct mxp_engine : public mxp::LowerTables {
         bool post_tmpl = false;  // postings carry template codes (kargs.post_tmpl)
         bool tmpl_lite = false;  // no template holds a lookup, virtual column or regexp (kargs.tmpl_lite)
         DevBuf d_guards, d_groups, d_segs, d_gk, d_tmpls, d_rule_tmpl, d_rule_tmpl2, d_alias_off, d_aliases;
-        DevBuf d_idx, d_hents, d_postings, d_plens;
+        DevBuf d_idx, d_hents, d_hbits, d_postings, d_plens;
         DevBuf d_glean, d_gvm, d_gall;  // group lists: guard-only groups, groups needing the VM, all but deep
         DevBuf d_gdeep;                 // groups with deep rules (MXP_VM_DEEPREG kernels), every mode
         DevBuf d_fills, d_fill_masks;   // chunks of uniform indexed groups (mxp_fill_kernel)

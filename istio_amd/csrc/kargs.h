@@ -36,6 +36,8 @@ typedef struct mxp_kargs {
     const uint64_t* rconst;      // [n_rules][MXP_VM_MAXREG] per-rule template constants
     const mxp_index* idx;        // guard indexes (mxp_index_kernel)
     const mxp_hent* hents;
+    const uint32_t* hbits;       // occupancy bitmaps of the prefix / composite pair tables (mxp_index.boff);
+                                 // null: probes load the entry pair first (MXP_DEBUG_FLAGS 4)
     const uint32_t* postings;    // rules of each index entry; with post_tmpl: rule | code << 23 (code = the
                                  // continuation template, 511 direct, 510 look up rule_tmpl / rule_tmpl2)
     const uint32_t* plens;       // prefix indexes: distinct key lengths

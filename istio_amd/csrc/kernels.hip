@@ -2164,7 +2164,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
         // short keys (every key length <= 12) hash and verify from the string's head (kargs.heads):
         // one coalesced 16-byte load instead of the descriptor and the bytes (scattered, dependent)
         const uint32_t lmax = (!final && kind != MXP_IX_EQ && nplen) ? uni(A.plens[plen0 + nplen - 1u]) : 0u;
-        const uint32_t hslot = uni(X->hslot);
+        const uint32_t hslot = uni(X->hslot), boff = uni(X->boff);
         const bool by_head = A.heads && hslot != MXP_VM_DONE && lmax <= 12u;
         // (the head's first word rides in the string pointer's registers: one of the two is live)
         StrRef s{nullptr, 0};
@@ -2200,6 +2200,8 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                     const uint64_t hf = by_head ? ph.at_head((uint64_t)s.p, hw1, L) : ph.at(s.p, L);
                     const uint32_t tag = (uint32_t)(hf >> 32);
                     for (uint32_t slot = (uint32_t)hf & pmask;; slot = (slot + 1) & pmask) {
+                        // an empty slot, told by the occupancy bitmap (no entry-pair request)
+                        if (A.hbits && !((A.hbits[boff + (slot >> 5)] >> (slot & 31u)) & 1u)) break;
                         // entry pairs (vm.h mxp_index): both halves in one 32-byte load pair
                         const uint32_t at = poff + 2u * slot;
                         const mxp_hent E = A.hents[at];

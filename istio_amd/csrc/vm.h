@@ -125,7 +125,9 @@ typedef struct mxp_index {
     uint32_t hslot;    // prefix / composite: the probed column's row in kargs.heads (MXP_VM_DONE: none)
     uint32_t tailk;    // prefix: some postings are `.*$` tail keys (code 508): the probe finds the
                        // subject's last '\n'
-    uint32_t pad[3];
+    uint32_t boff;     // prefix / composite: the pair table's occupancy bitmap at kargs.hbits[boff ..]
+                       // (bit s: slot s holds a key), read before an entry pair
+    uint32_t pad[2];
 } mxp_index;           // 64 B
 
 // index kinds.  Composite: rules `A == K1 && B.startsWith(K2) && ...` (vmopt.h SecondAtom), keyed by

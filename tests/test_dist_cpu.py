@@ -176,7 +176,7 @@ def _bench_step_rank_main(rank, world, port, out_path, steps, warmup):
     def evaluate(hits):
         hits += shard_hits
 
-    def quota_alloc(delta):
+    def quota_alloc(delta, _stream=None):
         for k, a, b in zip(keys, amounts, be):
             delta[int(k)] += mq.handle(int(k), int(a), bool(b), now[0])
         now[0] += 10**8

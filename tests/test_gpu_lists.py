@@ -48,6 +48,28 @@ def test_c3_ip_list_parity(eng, blacklist):
     assert set(np.unique(want)) >= ({0, 3, 7} if blacklist else {0, 3, 5})
 
 
+def test_ip_symbol_edges(eng):
+    """net.ParseIP edge symbols through both device parsers -- the register path for symbols of <= 15
+    bytes whose first separator is '.', the byte path for the rest -- against the restatement:
+    leading zeros, octets past 255, digit runs past Go's dtoi bound, missing / extra / empty parts,
+    trailing garbage, 15 / 16 / 17-byte quads, v4-mapped and plain IPv6, spaces, empties."""
+    entries = ["10.0.0.0/8", "1.2.3.4", "255.255.255.0/24", "0.0.0.0/32", "2001:db8::/32", "::ffff:7.7.7.0/120"]
+    quads = ["1.2.3.4", "01.002.0003.4", "010.000.000.001", "10.1.2.3", "255.255.255.255", "255.255.255.2555",
+             "0255.255.255.255", "256.1.1.1", "1.2.3", "1.2.3.4.5", "1..2.3", "1.2.3.", ".1.2.3", "1.2.3.4:80",
+             "1.2.3.4 ", " 1.2.3.4", "99999999.1.1.1", "16777215.1.1.1", "0000000000001.2", "0.0.0.0", "00.0.0.0",
+             "7.7.7.7", "::ffff:7.7.7.7", "::ffff:1.2.3.4", "2001:db8::1", "2001:db9::1", "::", "1.2.3.4/32",
+             "", ".", ":", "1", "a.b.c.d", "1.2.3.-4", "1.2.3.+4", "1.2.3.4\x00", "10.255.255.255", "11.0.0.0",
+             "10.0.0.0", "9.255.255.255", "255.255.255.1", "255.255.254.255", "1.2.3.4.", "0x1.2.3.4"]
+    lst = eng.list_create(L.IP_ADDRESSES, entries, [])
+    ref = L.IPList(entries, [])
+    for blacklist in (False, True):
+        want = L.codes(ref.found(quads, threads=1), blacklist)
+        got = lst.check(quads, blacklist)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(quads[i], int(got[i]), int(want[i])) for i in bad[:8]]
+    assert (want == 3).sum() > 10 and (want == 7).sum() > 5
+
+
 @pytest.mark.parametrize("kind", [L.STRINGS, L.CASE_INSENSITIVE_STRINGS])
 def test_c3_string_list_parity(eng, kind):
     entries, syms = W.c3_string_list(n_entries=20000, n_lookups=100000, seed=32)

@@ -213,3 +213,46 @@ def _null_stream_reps(db, R, N, Wd):
             cnt[:, b] = ((dm >> b) & 1).sum(dim=1)
         assert torch.equal(hits, 3 * cnt.reshape(-1)[:R]), rep
         assert int(hits.sum()) > 100 * N and int(req_err.max()) == 0
+
+
+def test_c5_step_quota_beside_evaluation(mxp):
+    """bench.py's C5 step with the memquota batch on a second stream beside the evaluation (the
+    default) gives the same hit counters and per-key quota deltas, step after step, as the serial
+    step -- the two touch disjoint buffers; the fork and join events order them around the counter
+    buffer's zeroing and the all-reduce."""
+    import torch
+    import bench
+    from istio_amd import dist as D
+    manifest, rules, batch = W.c2_workload(n_rules=2000, n_requests=1 << 16, seed=2)
+    R, N = len(rules), batch.n
+    dev = torch.device("cuda:0")
+    out = []
+    for two in (False, True):
+        eng = mxp.Engine(0)
+        eng.set_vocabulary(manifest)
+        assert (eng.compile(rules) == 0).all()
+        db = eng.upload(batch)
+        quota = bench.quota_setup(eng, N, 0, 1, dev)
+        d_match = torch.empty(((R + 31) // 32, N), dtype=torch.int32, device=dev)
+        d_req_err = torch.empty(N, dtype=torch.uint8, device=dev)
+        stream = torch.cuda.Stream(dev)
+        now = [1_500_000_000 * 10**9]
+
+        def quota_alloc(delta, qsh):
+            (_, q, (dk, da, dbe, dg)) = quota
+            q.alloc_device(dk.numel(), dk.data_ptr(), da.data_ptr(), dbe.data_ptr(), now[0], qsh, dg.data_ptr(),
+                           delta.data_ptr())
+            now[0] += 10**8
+        ctr = D.StepCounters([R, bench.QUOTA_KEYS], dev)
+        with torch.cuda.stream(stream):
+            step = bench.make_step(ctr, lambda hits: db.eval_compact(d_match.data_ptr(), d_req_err.data_ptr(),
+                                                                     hits.data_ptr(), stream.cuda_stream),
+                                   quota_alloc, stream, torch.cuda.Stream(dev) if two else None)
+            for _ in range(3):
+                step()
+        torch.cuda.synchronize()
+        h, d = ctr.totals()
+        out.append((h.cpu(), d.cpu()))
+        db.free()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert int(out[0][0].sum()) > 0 and int(out[0][1].abs().sum()) > 0

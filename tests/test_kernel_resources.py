@@ -19,8 +19,10 @@ MIN_OCCUPANCY = {"mxp_index_dtp_lite_kernel": 6, "mxp_guard_kernel": 8, "mxp_gua
 # 5-wave ablation kernel spills 20 bytes since the DFA walk exits at REJECT)
 # (r3: string-head probes and the prefix-sum queue share add spills -- 36/44 -> 52/56 bytes -- and
 # still measured faster, C2 0.562 -> 0.532 ms same-box, profiles/r3_v2_ab_*.log)
+# (r4: the lite kernel spills one value computed at its start and read at its end -- one scratch store
+# and one load per wave)
 MAX_SCRATCH = {"mxp_index_kernel": 56, "mxp_index_dtp_kernel": 24, "mxp_index5_kernel": 24,
-               "mxp_index_prof_kernel": 96, "mxp_index_dtp_prof_kernel": 96, "mxp_index_dtp_lite_kernel": 0}
+               "mxp_index_prof_kernel": 96, "mxp_index_dtp_prof_kernel": 96, "mxp_index_dtp_lite_kernel": 8}
 # the NFA instantiations (launched only for rule sets / lists with over-budget patterns): the wide NFA
 # walk keeps its two 1024-bit thread sets in private memory (dfa_dev.h mxp_nfa_run_wide) rather than
 # 64 VGPRs every NFA kernel would carry
