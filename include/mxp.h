@@ -336,6 +336,9 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
  * out[0] bytes of the packed device image, out[1] batch strings added to the overlay pool, out[2]
  * overlay byte strings.  Host threads: MXP_PACK_THREADS, else OMP_NUM_THREADS, else all cores. */
 int mxp_batch_pack_host(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* out, uint32_t cap);
+/* Frees a device batch without waiting for the device: its blocks are kept by the engine (up to
+ * 8 GiB) and reused by later mxp_batch_upload calls once the work enqueued before the free -- on
+ * the engine's stream and on every stream an evaluation of the batch was enqueued on -- is done. */
 void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db);
 int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err);
 /* mxp_batch_eval_device plus fused per-rule hit counters: d_hits[rule] += the requests of this batch

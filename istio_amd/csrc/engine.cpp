@@ -12,6 +12,70 @@
 
 #include "engine_impl.h"
 
+thread_local BlockBin* g_bin_take = nullptr;
+thread_local std::vector<std::pair<void*, size_t>>* g_bin_give = nullptr;
+
+// the smallest block of at least `want` bytes and at most twice that (+ 1 MB), its group's work
+// waited for once
+bool BlockBin::take(size_t want, void** p, size_t* cap) {
+    size_t bg = 0, bi = 0, best = SIZE_MAX;
+    for (size_t g = 0; g < groups.size(); g++)
+        for (size_t i = 0; i < groups[g].blks.size(); i++) {
+            const size_t c = groups[g].blks[i].second;
+            if (c >= want && c <= 2 * want + (1u << 20) && c < best) {
+                best = c;
+                bg = g;
+                bi = i;
+            }
+        }
+    if (best == SIZE_MAX) return false;
+    Group& G = groups[bg];
+    if (!G.done) {
+        for (hipEvent_t e : G.evs) (void)hipEventSynchronize(e);
+        G.done = true;
+    }
+    *p = G.blks[bi].first;
+    *cap = G.blks[bi].second;
+    bytes -= best;
+    G.blks[bi] = G.blks.back();
+    G.blks.pop_back();
+    if (G.blks.empty()) {
+        for (hipEvent_t e : G.evs) (void)hipEventDestroy(e);
+        groups.erase(groups.begin() + (ptrdiff_t)bg);
+    }
+    return true;
+}
+
+void BlockBin::put(Group&& g) {
+    for (auto& b : g.blks) bytes += b.second;
+    groups.push_back(std::move(g));
+    while (bytes > kCapBytes && !groups.empty()) {
+        Group& G = groups.front();
+        for (hipEvent_t e : G.evs) {
+            (void)hipEventSynchronize(e);
+            (void)hipEventDestroy(e);
+        }
+        for (auto& b : G.blks) {
+            (void)hipFree(b.first);
+            bytes -= b.second;
+        }
+        groups.erase(groups.begin());
+    }
+}
+
+void BlockBin::release() {
+    for (Group& G : groups) {
+        for (hipEvent_t e : G.evs) {
+            (void)hipEventSynchronize(e);
+            (void)hipEventDestroy(e);
+        }
+        for (auto& b : G.blks) (void)hipFree(b.first);
+    }
+    groups.clear();
+    bytes = 0;
+}
+
+
 // ------------------------------------------------------------------------------------ compile
 int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     reset_tables();
@@ -1561,6 +1625,7 @@ int mxp_engine::vt_prepare(mxp_dbatch* db, const Plan& P) {
 
 int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
                        bool log, unsigned long long* d_hits, uint64_t* stats, uint32_t q_lo, uint32_t q_hi) {
+    if (db && std::find(db->used.begin(), db->used.end(), s) == db->used.end()) db->used.push_back(s);
     // (no stale flags from the previous evaluation survive an early return below)
     last_dtp = false;
     last_dtp_counted = false;
@@ -2049,6 +2114,7 @@ void mxp_engine_destroy(mxp_engine* eng) {
         if (eng->bounce_ev[k]) (void)hipEventDestroy(eng->bounce_ev[k]);
         if (eng->bounce[k]) (void)hipHostFree(eng->bounce[k]);
     }
+    eng->bin.release();
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     for (auto& x : eng->ev)
         if (x) (void)hipEventDestroy(x);
@@ -2214,7 +2280,9 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
     if (h != hipSuccess) return eng->hipfail(h, "hipSetDevice");
     auto* db = new (std::nothrow) mxp_dbatch();
     if (!db) return MXP_ERR_NOMEM;
+    g_bin_take = &eng->bin;  // (the batch's blocks, recycled where the bin has them)
     int rc = eng->pack(batch, db);
+    g_bin_take = nullptr;
     if (rc) {
         delete db;
         return rc;
@@ -2237,9 +2305,38 @@ int mxp_batch_pack_host(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* o
     return MXP_OK;
 }
 
+// The batch's device blocks go to the engine's bin (no hipFree: it would wait for the whole device),
+// with an event on the engine stream (the packer) and on each stream an evaluation of the batch was
+// enqueued on: a later upload reuses a block only after those events.
 void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db) {
-    if (eng) (void)hipSetDevice(eng->device);
+    if (!db) return;
+    if (!eng || eng->device < 0) {
+        delete db;
+        return;
+    }
+    (void)hipSetDevice(eng->device);
+    BlockBin::Group g;
+    std::vector<hipStream_t> ss = db->used;
+    ss.push_back(eng->stream);
+    bool ok = true;
+    for (hipStream_t st : ss) {
+        hipEvent_t e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess || hipEventRecord(e, st) != hipSuccess) {
+            if (e) (void)hipEventDestroy(e);
+            ok = false;
+            break;
+        }
+        g.evs.push_back(e);
+    }
+    if (!ok) {  // (no events: the plain frees)
+        for (hipEvent_t e : g.evs) (void)hipEventDestroy(e);
+        delete db;
+        return;
+    }
+    g_bin_give = &g.blks;
     delete db;
+    g_bin_give = nullptr;
+    eng->bin.put(std::move(g));
 }
 
 int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err) {

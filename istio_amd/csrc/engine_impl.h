@@ -45,27 +45,57 @@ extern "C" hipError_t mxp_launch_hits_gate(const unsigned long long* stats, uint
                                            uint32_t* gate, uint32_t force, hipStream_t s);
 
 
+// Device blocks of freed batches, reused by later uploads (mxp_batch_free hands a batch's blocks to
+// its engine's bin with events recorded on every stream that read the batch; mxp_batch_upload draws
+// from it).  A hipFree synchronises the whole device -- ~0.2 ms each, ~25 per batch, so freeing one
+// batch stalled a fresh-batch step behind every kernel in flight; a drawn block waits only for the
+// events of the batch it came from (long complete in a steady upload / evaluate / free loop).
+struct BlockBin {
+    struct Group {
+        std::vector<hipEvent_t> evs;  // completion of the work that read the freed batch
+        std::vector<std::pair<void*, size_t>> blks;
+        bool done = false;
+    };
+    std::vector<Group> groups;  // oldest first
+    size_t bytes = 0;
+    static constexpr size_t kCapBytes = 8ull << 30;  // beyond: the oldest groups are freed
+    bool take(size_t want, void** p, size_t* cap);
+    void put(Group&& g);
+    void release();  // every block freed (engine teardown)
+    ~BlockBin() { release(); }
+};
+// the bin DevBuf::alloc draws from / DevBuf::reset hands blocks to (set for the duration of an
+// upload / a batch free on the calling thread; null elsewhere: plain hipMalloc / hipFree)
+extern thread_local BlockBin* g_bin_take;
+extern thread_local std::vector<std::pair<void*, size_t>>* g_bin_give;
+
 struct DevBuf {
     void* p = nullptr;
-    size_t n = 0;
+    size_t n = 0;    // bytes asked for
+    size_t cap = 0;  // bytes the block holds (>= n: a recycled block may be larger)
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() { reset(); }
     void reset() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            if (g_bin_give) g_bin_give->push_back({p, cap});
+            else (void)hipFree(p);
+        }
         p = nullptr;
-        n = 0;
+        n = cap = 0;
     }
     hipError_t alloc(size_t bytes) {
         reset();
         if (bytes == 0) bytes = 16;
         n = bytes;
+        if (g_bin_take && g_bin_take->take(bytes, &p, &cap)) return hipSuccess;
+        cap = bytes;
         return hipMalloc(&p, bytes);
     }
     // grow-only: keeps the allocation when it is large enough (engine-owned scratch reused across calls)
     hipError_t reserve(size_t bytes) {
-        if (p && n >= (bytes ? bytes : 16)) return hipSuccess;
+        if (p && cap >= (bytes ? bytes : 16)) return hipSuccess;
         return alloc(bytes);
     }
     template <class T>
@@ -149,6 +179,7 @@ struct mxp_dbatch {
     // byte strings GB + item, canonical GC + item, times GT + item (items: batch strings / times
     // first, then parsed ip() / timestamp() values by string id) -- read back on demand
     bool dev_packed = false;
+    std::vector<hipStream_t> used;  // streams evaluations of this batch were enqueued on (mxp_batch_free)
     bool vtd_ready = false;  // the packer's provisional class tables (engine scratch) hold this batch's
     uint32_t ns = 0, nt = 0, G = 0, GB = 0, GC = 0, GT = 0;
     DevBuf pip, pip_ok, pts_sec, pts_nsec, pts_ok, btsec, btnsec;
@@ -161,6 +192,7 @@ struct mxp_dbatch {
 struct mxp_engine : public mxp::LowerTables {
     int device = 0;
     hipStream_t stream = nullptr;
+    BlockBin bin;  // freed batches' device blocks (declared first: destroyed last)
     std::string last_error;
 
     mxp::Vocabulary vocab;
