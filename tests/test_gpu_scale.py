@@ -256,3 +256,48 @@ def test_c5_step_quota_beside_evaluation(mxp):
         db.free()
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     assert int(out[0][0].sum()) > 0 and int(out[0][1].abs().sum()) > 0
+
+
+@pytest.mark.parametrize("wl", ["c4", "c2"])
+def test_recycled_batch_blocks_match_fresh_engine(mxp, wl):
+    """mxp_batch_free hands a batch's device blocks to the engine's bin and later uploads reuse them
+    (engine_impl.h BlockBin): batches uploaded into recycled blocks -- a larger batch's, holding its
+    stale words, and, shrinking, blocks larger than asked for -- evaluate bit for bit as the same
+    batches uploaded by a fresh engine, with evaluations still in flight on another stream when the
+    blocks are freed."""
+    import torch
+    sizes = [(1 << 17) + 5, 50_001, 3_000]
+    if wl == "c4":
+        mk = lambda n, seed: W.c4_workload(n_rules=2000, n_requests=n, seed=seed)
+    else:
+        mk = lambda n, seed: W.c2_workload(n_rules=2000, n_requests=n, seed=seed)
+    batches = [mk(n, 40 + k) for k, n in enumerate(sizes)]
+    manifest, rules = batches[0][0], batches[0][1]
+    if wl == "c2":
+        rules = W.c2_rules(2000, seed=2)[0]
+    Wd = (len(rules) + 31) // 32
+
+    def run(eng, b, s, free_after=True):
+        db = eng.upload(b)
+        dm = torch.zeros((Wd, b.n), dtype=torch.int32, device="cuda:0")
+        de = torch.zeros_like(dm)
+        db.eval(dm.data_ptr(), de.data_ptr(), s.cuda_stream)
+        if free_after:
+            db.free()  # (the evaluation may still be running on s)
+        return dm, de
+
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    s = torch.cuda.Stream()
+    got = [run(eng, b[2], s) for b in batches]            # each upload draws the previous one's blocks
+    got += [run(eng, b[2], s) for b in reversed(batches)]  # and growing again
+    torch.cuda.synchronize()
+    ref_eng = mxp.Engine(0)
+    ref_eng.set_vocabulary(manifest)
+    ref_eng.compile(rules)
+    for k, b in enumerate(list(batches) + list(reversed(batches))):
+        dm, de = run(ref_eng, b[2], s)
+        torch.cuda.synchronize()
+        assert torch.equal(got[k][0], dm) and torch.equal(got[k][1], de), (wl, k)
+    assert int(torch.count_nonzero(got[0][0])) > 1000
