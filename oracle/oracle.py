@@ -21,14 +21,10 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 if _HERE not in sys.path:
     sys.path.insert(0, _HERE)
-_REPO = os.path.dirname(_HERE)
-if _REPO not in sys.path:
-    sys.path.insert(0, _REPO)
 
 import goexpr  # noqa: E402
 import ilcompile  # noqa: E402
-from istio_amd.bags import (BagBatch, GoDuration, GoFloat64, GoInt64, GoTime, bytes_go_str,  # noqa: E402
-                            go_str_bytes)
+from govalue import GoDuration, GoFloat64, GoInt64, GoTime, bytes_go_str, go_str_bytes  # noqa: E402
 
 _LIB = None
 
@@ -182,7 +178,7 @@ class OracleProgram:
             _LIB.oracle_prog_free(self.h)
             self.h = None
 
-    def run(self, batch: BagBatch, req: int, fn="eval"):
+    def run(self, batch, req: int, fn="eval"):
         """Interpreter.Eval(fn, bag) -> ('ok', value) | ('error', msg) | ('panic', msg)."""
         r = _Result()
         lib().oracle_eval(self.h, self.fn_id(fn), ctypes.byref(batch.c_struct()), req, ctypes.byref(r))
@@ -194,7 +190,7 @@ class OracleProgram:
         return "ok", _result_value(r, batch)
 
 
-def eval_il(program: ilcompile.Program, fn: str, batch: BagBatch, req: int = 0):
+def eval_il(program: ilcompile.Program, fn: str, batch, req: int = 0):
     """interpreter.New(program, nil).Eval(fn, bag) (interpreter.go:62-69): ('ok', value) |
     ('error', msg) | ('panic', msg)."""
     if program.get(fn) is None:
@@ -202,7 +198,7 @@ def eval_il(program: ilcompile.Program, fn: str, batch: BagBatch, req: int = 0):
     return OracleProgram(program).run(batch, req, fn)
 
 
-def _result_value(r: _Result, batch: BagBatch):
+def _result_value(r: _Result, batch):
     """interpreter.Result.AsInterface (result.go:99-116)."""
     t = r.rtype
     if t == ilcompile.T_BOOL:
@@ -259,7 +255,7 @@ class OracleEvaluator:
             self.cache[text] = p
         return p
 
-    def eval(self, text, batch: BagBatch, req: int):
+    def eval(self, text, batch, req: int):
         try:
             p = self.compile(text)
         except (goexpr.ParseError, goexpr.TypeCheckError, ilcompile.CompileError) as e:
@@ -268,7 +264,7 @@ class OracleEvaluator:
             return "panic", str(e)
         return p.run(batch, req)
 
-    def eval_predicate(self, text, batch: BagBatch, req: int):
+    def eval_predicate(self, text, batch, req: int):
         st, v = self.eval(text, batch, req)
         if st == "ok" and not isinstance(v, bool):
             return "panic", "interpreter.Result: result is not bool"
@@ -279,7 +275,7 @@ class OracleEvaluator:
 FALSE, TRUE, ERROR, PANIC = 0, 1, 2, 3
 
 
-def oracle_matrix(evaluator: OracleEvaluator, rules, batch: BagBatch, req_begin=0, req_end=None, threads=8):
+def oracle_matrix(evaluator: OracleEvaluator, rules, batch, req_begin=0, req_end=None, threads=8):
     """codes[r, k] for EvalPredicate(rules[k], bag r) over requests [req_begin, req_end)."""
     if req_end is None:
         req_end = batch.n
@@ -309,7 +305,7 @@ def oracle_matrix(evaluator: OracleEvaluator, rules, batch: BagBatch, req_begin=
     return codes
 
 
-def oracle_referenced(evaluator: OracleEvaluator, rules, batch: BagBatch, req: int):
+def oracle_referenced(evaluator: OracleEvaluator, rules, batch, req: int):
     """FakeBag.ReferencedList (il/testing/fakebag.go:75-89) of request `req` after EvalPredicate of
     every rule in order: sorted distinct "name" / "name[key]" strings (bytes).  Rules that fail to
     compile read nothing (evaluator.go:157-179 returns the compile error before touching the bag)."""

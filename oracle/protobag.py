@@ -12,7 +12,7 @@ and dictState.go for the index convention.  Messages are the dicts of istio_amd.
 """
 from __future__ import annotations
 
-from istio_amd.bags import GoDuration, GoFloat64, GoInt64, GoTime
+from govalue import GoDuration, GoFloat64, GoInt64, GoTime
 
 
 def _lookup(msg, gwords, index):
