@@ -515,11 +515,17 @@ int mxp_engine::build_plan(Plan& P) {
         }
         return (uint32_t)std::min<size_t>(postings.size() - p0, 0xFFFFFFFFu);
     };
+    // slots of a table of n keys: >= 2^(1 + index_sparsity) per key (mxp_engine.index_sparsity), the
+    // growth past 2 per key stopping at 2^22 slots
+    auto table_cap = [&](size_t n) -> uint32_t {
+        uint32_t cap = 1;
+        while (cap < 2 * n || (cap < (2ull << index_sparsity) * n && cap < (1u << 22))) cap <<= 1;
+        return cap;
+    };
     // open-addressing table of `groups` (key -> rules) at hents[hoff ..): returns hmask
     auto add_eq_table = [&](const std::map<uint64_t, std::vector<uint32_t>>& groups, const std::vector<uint32_t>& tmpl_of,
                             uint32_t* hoff) -> uint32_t {
-        uint32_t cap = 1;
-        while (cap < (2u << index_sparsity) * groups.size()) cap <<= 1;
+        const uint32_t cap = table_cap(groups.size());
         *hoff = (uint32_t)hents.size();
         hents.resize(hents.size() + cap, mxp_hent{0, 0, 0, 0});
         for (auto& kv : groups) {
@@ -543,8 +549,7 @@ int mxp_engine::build_plan(Plan& P) {
             idx.push_back(x);
             continue;
         }
-        uint32_t cap = 1;
-        while (cap < (2u << index_sparsity) * ci.second.size()) cap <<= 1;
+        const uint32_t cap = table_cap(ci.second.size());
         x.hmask = cap - 1;
         x.hoff = (uint32_t)hents.size();
         hents.resize(hents.size() + 2 * (size_t)cap, mxp_hent{0, 0, 0, 0});
@@ -594,8 +599,7 @@ int mxp_engine::build_plan(Plan& P) {
         for (auto& kv : by_k1) std::sort(kv.second.begin(), kv.second.end());
         x.hmask = add_eq_table(by_k1, rule_tmpl, &x.hoff);
         // composite table: entry pairs
-        uint32_t cap = 1;
-        while (cap < (2u << index_sparsity) * ci.second.size()) cap <<= 1;
+        const uint32_t cap = table_cap(ci.second.size());
         x.hmask2 = cap - 1;
         x.hoff2 = (uint32_t)hents.size();
         hents.resize(hents.size() + 2 * (size_t)cap, mxp_hent{0, 0, 0, 0});
@@ -2077,7 +2081,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_DTP")) e->dtp = atoi(f) != 0;
     if (const char* f = getenv("MXP_DTP_CAP")) e->dtp_cap = (uint32_t)std::min(1 << 20, std::max(1, atoi(f)));
     if (const char* f = getenv("MXP_DTP_OVF")) e->dtp_ovf_cap = (uint32_t)std::max(1, atoi(f));
-    if (const char* f = getenv("MXP_INDEX_SPARSITY")) e->index_sparsity = (uint32_t)std::min(4, std::max(0, atoi(f)));
+    if (const char* f = getenv("MXP_INDEX_SPARSITY")) e->index_sparsity = (uint32_t)std::min(8, std::max(0, atoi(f)));
     // tuning knobs (results are identical for every setting)
     if (const char* f = getenv("MXP_GPW")) e->groups_per_wave = std::max(1, atoi(f));
     if (const char* f = getenv("MXP_FILL_CHUNK")) e->fill_chunk = (uint32_t)std::max(1, atoi(f));

@@ -377,8 +377,11 @@ struct mxp_engine : public mxp::LowerTables {
     // guard-index hash tables hold >= 2^(1 + index_sparsity) slots per key (MXP_INDEX_SPARSITY):
     // a lower load factor shortens the probe chains of the many misses (prefix probes at every key
     // length).  Same-box A/B (profiles/r2_v7_ab_sparse_*.log), ms per evaluation for 0 / 1 / 2 / 3:
-    // C4 2.216 / 2.188 / 2.178 / 2.178, C2 0.576 / 0.573 / 0.566 / 0.562
-    uint32_t index_sparsity = 2;
+    // C4 2.216 / 2.188 / 2.178 / 2.178, C2 0.576 / 0.573 / 0.566 / 0.562.  Round 4, with the
+    // occupancy bitmaps (profiles/r4_s2{5,6}_ab_*_sparsity.log) for 1 / 2 / 3 / 4 / 5 / 6 / 8: C4
+    // 0.823 / 0.795 / 0.793 / 0.771-0.782 / 0.746 / 0.750 / 0.742, C2 flat (0.404-0.413): a miss
+    // whose slot bit is set costs an entry-pair load, and C4 misses at ~14 key lengths per request
+    uint32_t index_sparsity = 5;
     // Deferred index pairs (launch, kernels.hip mxp_dtp_*; MXP_DTP=0 turns them off): per index wave
     // room for dtp_cap pairs, then an overflow list of dtp_ovf_cap (MXP_DTP_CAP / MXP_DTP_OVF: tests)
     bool dtp = true;
