@@ -1711,7 +1711,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
             return hipfail(e, "side stream");
         }
         for (auto& x : chunk_ev)
-            if (!x && (e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) {
+            if (!x && (e = hipEventCreateWithFlags(&x, kOrderEvent)) != hipSuccess) {
                 x = nullptr;
                 return hipfail(e, "chunk event");
             }
@@ -1777,7 +1777,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         // for the previous deferred launch to finish with them (its sort kernel resets the counter
         // set this launch uses; its fills read the slots this launch's sort rewrites), and scratch
         // that must grow is released only once that launch is done
-        if (!dtp_ev && (e = hipEventCreateWithFlags(&dtp_ev, hipEventDisableTiming)) != hipSuccess) {
+        if (!dtp_ev && (e = hipEventCreateWithFlags(&dtp_ev, kOrderEvent)) != hipSuccess) {
             dtp_ev = nullptr;
             return hipfail(e, "deferred-pair event");
         }
@@ -1834,7 +1834,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
                 return hipfail(e, "side stream");
             }
             for (auto& x : dtp_cev)
-                if (!x && (e = hipEventCreateWithFlags(&x, hipEventDisableTiming)) != hipSuccess) {
+                if (!x && (e = hipEventCreateWithFlags(&x, kOrderEvent)) != hipSuccess) {
                     x = nullptr;
                     return hipfail(e, "chunk event");
                 }
@@ -2369,7 +2369,7 @@ static int eval_device_hits(mxp_engine* eng, mxp_dbatch* db, void* stream, uint3
         // no evaluation yet: stream the bitmap (a fused first evaluation of a rule set with many true
         // pairs would pay one atomic per pair: C4's first evaluations took 6.5 ms instead of 1.9)
         if ((e = hipMemsetAsync(eng->d_gate.p, 0, 8, s)) != hipSuccess) return eng->hipfail(e, "hits gate");
-        if ((e = hipEventCreateWithFlags(&eng->stats_ev, hipEventDisableTiming)) != hipSuccess) {
+        if ((e = hipEventCreateWithFlags(&eng->stats_ev, kOrderEvent)) != hipSuccess) {
             eng->stats_ev = nullptr;
             return eng->hipfail(e, "stats event");
         }

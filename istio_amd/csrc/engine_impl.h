@@ -24,6 +24,12 @@
 #include "par.h"
 #include "vmopt.h"
 
+// Events that only order device work (a stream waiting on another, or the host waiting before it
+// releases scratch): no system-scope release when recorded.  A default event's record writes back
+// and invalidates the caches for host visibility, which the next evaluation then waits out at its
+// start (~20 us between back-to-back evaluations, profiles/r4_final kernel trace).
+static constexpr unsigned kOrderEvent = hipEventDisableTiming | hipEventDisableSystemFence;
+
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_vtd_final(const mxp_kargs* args, const mxp_vtd_final_args* f, hipStream_t s);

@@ -25,6 +25,7 @@ de = torch.empty_like(dm)
 hits = torch.zeros(len(rules), dtype=torch.int64, device="cuda:0")
 flags = torch.empty(batch.n, dtype=torch.uint8, device="cuda:0")
 compact = bool(os.environ.get("AB_COMPACT"))  # the bench's error output (per-request flags)
+loop = int(os.environ.get("AB_LOOP", "1"))  # evaluations back to back per timed interval (the bench's loop)
 
 
 def ev(db, s):
@@ -54,10 +55,11 @@ for rep in range(3):
         for _ in range(15):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(s)
-            ev(db, s)
+            for _ in range(loop):
+                ev(db, s)
             b.record(s)
             torch.cuda.synchronize()
-            ts.append(a.elapsed_time(b))
+            ts.append(a.elapsed_time(b) / loop)
         res[st].append(float(np.median(ts)))
         db.free()
         del eng
