@@ -516,10 +516,12 @@ int mxp_engine::build_plan(Plan& P) {
         return (uint32_t)std::min<size_t>(postings.size() - p0, 0xFFFFFFFFu);
     };
     // slots of a table of n keys: >= 2^(1 + index_sparsity) per key (mxp_engine.index_sparsity), the
-    // growth past 2 per key stopping at 2^22 slots
+    // growth past 2 per key stopping at 2^20 slots per table and 2^24 entries (256 MB) over all tables
     auto table_cap = [&](size_t n) -> uint32_t {
         uint32_t cap = 1;
-        while (cap < 2 * n || (cap < (2ull << index_sparsity) * n && cap < (1u << 22))) cap <<= 1;
+        while (cap < 2 * n ||
+               (cap < (2ull << index_sparsity) * n && cap < (1u << 20) && hents.size() + 4ull * cap <= (1ull << 24)))
+            cap <<= 1;
         return cap;
     };
     // open-addressing table of `groups` (key -> rules) at hents[hoff ..): returns hmask
