@@ -613,7 +613,11 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
             db.eval_hits(d_match.data_ptr(), d_err.data_ptr(), hits_ptr, sh)
         else:
             db.eval(d_match.data_ptr(), d_err.data_ptr(), sh)
-    stream = torch.cuda.Stream(dev)  # a real (non-null) HIP stream shared by libmxp, events and RCCL
+    # a real (non-null) HIP stream shared by libmxp, events and RCCL.  C5's memquota stream runs at the
+    # higher priority: its latency-bound replay is dispatched ahead of the fill's workgroups (C5 0.5226
+    # -> 0.5186 ms per step alternated, profiles/r4_s30_c5_*.log; BENCH_STREAM_PRIO / BENCH_QSTREAM_PRIO
+    # override, a lower number is a higher priority)
+    stream = torch.cuda.Stream(dev, priority=int(os.environ.get("BENCH_STREAM_PRIO", "0")))
     torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
     quota = None
@@ -627,7 +631,8 @@ def predicate_bench(args, kind, rank, world, local, with_quota=False):
         q.alloc_device(dk.numel(), dk.data_ptr(), da.data_ptr(), dbe.data_ptr(), now[0], qsh, dg.data_ptr(),
                        delta.data_ptr())
         now[0] += 10**8
-    qstream = torch.cuda.Stream(dev) if quota is not None and not args.quota_serial else None
+    qstream = (torch.cuda.Stream(dev, priority=int(os.environ.get("BENCH_QSTREAM_PRIO", "-1")))
+               if quota is not None and not args.quota_serial else None)
     step = make_step(ctr, lambda hits: evaluate(hits.data_ptr()), quota_alloc if quota is not None else None, stream,
                      qstream)
 
