@@ -2086,7 +2086,8 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_INDEX_SPARSITY")) e->index_sparsity = (uint32_t)std::min(8, std::max(0, atoi(f)));
     // tuning knobs (results are identical for every setting)
     if (const char* f = getenv("MXP_GPW")) e->groups_per_wave = std::max(1, atoi(f));
-    if (const char* f = getenv("MXP_FILL_CHUNK")) e->fill_chunk = (uint32_t)std::max(1, atoi(f));
+    // (at most the kernels' compile-time chunk: their LDS tables are sized for MXP_FILL_CHUNK groups)
+    if (const char* f = getenv("MXP_FILL_CHUNK")) e->fill_chunk = (uint32_t)std::min((int)MXP_FILL_CHUNK, std::max(1, atoi(f)));
     if (const char* f = getenv("MXP_FILL_SPAN")) e->fill_span = (uint32_t)std::min(8, std::max(1, atoi(f)));
     if (const char* f = getenv("MXP_ERRCAP")) e->errcap = (uint32_t)std::max(1, atoi(f));
     if (getenv("MXP_WAVE_TIMES")) e->wave_times = true;

@@ -391,7 +391,11 @@ struct mxp_engine : public mxp::LowerTables {
     // Deferred index pairs (launch, kernels.hip mxp_dtp_*; MXP_DTP=0 turns them off): per index wave
     // room for dtp_cap pairs, then an overflow list of dtp_ovf_cap (MXP_DTP_CAP / MXP_DTP_OVF: tests)
     bool dtp = true;
-    uint32_t dtp_cap = 2048, dtp_ovf_cap = 1u << 22;
+    // (dtp_cap is also the lists' stride: 2080 entries = 65 lines of 128 bytes.  At 2048 -- an 8 KB,
+    // power-of-two stride -- the index waves' appends and the sort's four concurrent list reads fall
+    // on aliased HBM channels: C4 0.745 -> 0.710 ms, the path-only routes 0.630 -> 0.618 ms with 2080,
+    // settings alternated in one process, profiles/r4_s3{3,4,5}_ab_*_dtpcap.log)
+    uint32_t dtp_cap = 2080, dtp_ovf_cap = 1u << 22;
     DevBuf d_dtp_ent, d_dtp_n, d_dtp_ovf, d_dtp_ovf_n, d_dtp_slots, d_dtp_qn;
     bool last_dtp = false;  // the last launch deferred its index pairs (mxp_kernel_times [2])
     bool last_dtp_counted = false;  // ... and counted every true pair in its kernels (no streamed counters)
