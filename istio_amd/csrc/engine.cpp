@@ -1785,7 +1785,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         }
         if (dtp_pending) {
             if (dtp_stream != s && (e = hipStreamWaitEvent(s, dtp_ev, 0)) != hipSuccess) return hipfail(e, "deferred-pair wait");
-            const size_t need_slots = (size_t)(P->n_fills + P->n_vtfills) * tiles * 256 * 16;
+            const size_t need_slots = (size_t)(P->n_fills + P->n_vtfills) * MXP_DTP_ROW(tiles) * 16;
             if ((d_dtp_ent.n < (size_t)cx * dtp_cap * 4 || d_dtp_n.n < (size_t)grid * 16 || d_dtp_slots.n < need_slots ||
                  d_dtp_qn.n < need_slots / 16 || d_dtp_ovf.n < (size_t)dtp_ovf_cap * 8 ||
                  (dtp_count && d_dtp_part.n < (size_t)tiles * ((A.n_rules + 1) / 2) * 4)) &&
@@ -1795,8 +1795,8 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         if ((e = d_dtp_ent.reserve((size_t)cx * dtp_cap * 4)) != hipSuccess ||
             (e = d_dtp_n.reserve((size_t)grid * 4 * 4)) != hipSuccess ||
             (e = d_dtp_ovf.reserve((size_t)dtp_ovf_cap * 8)) != hipSuccess ||
-            (e = d_dtp_slots.reserve((size_t)(P->n_fills + P->n_vtfills) * tiles * 256 * 16)) != hipSuccess ||
-            (e = d_dtp_qn.reserve((size_t)(P->n_fills + P->n_vtfills) * tiles * 256)) != hipSuccess)
+            (e = d_dtp_slots.reserve((size_t)(P->n_fills + P->n_vtfills) * MXP_DTP_ROW(tiles) * 16)) != hipSuccess ||
+            (e = d_dtp_qn.reserve((size_t)(P->n_fills + P->n_vtfills) * MXP_DTP_ROW(tiles))) != hipSuccess)
             return hipfail(e, "deferred-pair scratch");
         if (!d_dtp_ovf_n.p) {  // two counter sets (count, list full): each launch's sort kernel resets the other
             if ((e = d_dtp_ovf_n.alloc(32)) != hipSuccess) return hipfail(e, "deferred-pair counters");

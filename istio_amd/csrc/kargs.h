@@ -11,7 +11,12 @@
 #define MXP_RXOF_SYNTAX 0xFFFFFFFFu
 #define MXP_RXOF_UNSUPPORTED 0xFFFFFFFEu
 
-typedef struct mxp_kargs {
+typedef // quads per fill-chunk row of the deferred-pair slots (kargs.dtp_slots, 16 B a quad) and counts
+// (kargs.dtp_qn, 1 B): the tiles' 256 quads each plus 8 -- a row of exactly 2^k quads (4 MB of slots
+// at 1M requests) would put every chunk's same quads on aliased HBM channels
+#define MXP_DTP_ROW(tiles) ((uint64_t)(tiles) * 256u + 8u)
+
+struct mxp_kargs {
     // rule set (uploaded once per config snapshot)
     const mxp_vm_ins* prog;      // all rules' programs, concatenated
     const uint32_t* rule_off;    // [n_rules + 1]
@@ -121,7 +126,7 @@ typedef struct mxp_kargs {
     uint32_t* dtp_part;          // fused hit counters of deferred pairs: [tiles][(n_rules + 1) / 2] u16
                                  // pairs, each sort workgroup's per-rule true pairs (LDS histogram),
                                  // summed into kargs.hits by mxp_dtp_hits_kernel (null: counted per pair)
-    uint32_t dtp_cap, dtp_ovf_cap, dtp_tiles, dtp_nchunks;
+    uint32_t dtp_cap, dtp_ovf_cap, dtp_tiles, dtp_nchunks;  // (chunk rows of dtp_slots / dtp_qn: MXP_DTP_ROW quads)
     uint32_t req_err_init;       // the deferred-pair index kernel writes every request's req_err flag
     uint32_t tmpl_lite;          // index templates hold no lookups / virtual columns / regexps (lite kernel)
     uint32_t* gate_out;          // the gated index launch after a counted evaluation: next gate = 0

@@ -1257,7 +1257,7 @@ struct DtpQueue {
     __device__ __forceinline__ void load(const mxp_kargs& A, uint32_t chunk, uint32_t req0, bool in) {
         if (!A.dtp_slots || !in) return;
         typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-        const uint64_t qi = (uint64_t)chunk * A.dtp_tiles * 256u + (req0 >> 2);
+        const uint64_t qi = (uint64_t)chunk * MXP_DTP_ROW(A.dtp_tiles) + (req0 >> 2);
         const uint32_t dk = A.dtp_qn[qi];
         const v4u sl = *(const v4u*)(A.dtp_slots + qi * 8u);
         if (!dk) return;
@@ -1759,7 +1759,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_dtp_sort_kernel(mxp_kargs 
         for (uint32_t i = tid; i < R2; i += 256u) hc[i] = 0u;
     const uint32_t nwaves = (A.n + 63u) / 64u, w0 = t * 16u;
     const uint32_t nw = min(16u, nwaves - w0);
-    const uint64_t nq = (uint64_t)A.dtp_tiles * 256u;  // quads per chunk row
+    const uint64_t nq = MXP_DTP_ROW(A.dtp_tiles);  // quads per chunk row
     for (uint32_t cw0 = 0; cw0 < A.dtp_nchunks; cw0 += MXP_DTP_WIN) {
         const uint32_t cwn = min(MXP_DTP_WIN, A.dtp_nchunks - cw0);
         for (uint32_t i = tid; i < cwn * 128u; i += 256u) cnt[i] = 0u;
