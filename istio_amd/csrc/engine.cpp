@@ -1399,7 +1399,7 @@ int mxp_engine::pack_vt_tables(mxp_dbatch* db) {
     for (uint32_t c : db->vt_capc) keys += c;
     db->vt_keys_n = keys;
     const uint32_t act = (uint32_t)__builtin_popcount(db->vt_mask);
-    if ((e = db->vt_cls.alloc((size_t)act * db->n * 2)) != hipSuccess) return hipfail(e, "vt classes");
+    if ((e = db->vt_cls.alloc((size_t)act * MXP_VT_PITCH(db->n) * 2)) != hipSuccess) return hipfail(e, "vt classes");
     if ((e = db->vt_keys.alloc(keys * 8)) != hipSuccess) return hipfail(e, "vt keys");
     if ((e = db->vt_rep.alloc(keys * 4)) != hipSuccess) return hipfail(e, "vt reps");
     if ((e = db->vt_cnt.alloc(keys * 4)) != hipSuccess) return hipfail(e, "vt counts");
@@ -2552,14 +2552,15 @@ int mxp_engine::expand_class_errors(const mxp_bag_batch* batch, mxp_dbatch* db, 
     if ((e = hipMemcpy(recs.data(), d_vtlog.p, n_class * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
         return hipfail(e, "download class errlog");
     const uint32_t n = db->n, act = (uint32_t)__builtin_popcount(last_mask);
-    std::vector<uint16_t> cls((size_t)act * n);
+    const size_t pitch = MXP_VT_PITCH(n);
+    std::vector<uint16_t> cls((size_t)act * pitch);
     if ((e = hipMemcpy(cls.data(), db->vt_cls.p, cls.size() * 2, hipMemcpyDeviceToHost)) != hipSuccess)
         return hipfail(e, "download classes");
     // requests of every class, per active slot (counting sort by class)
     std::vector<std::vector<uint32_t>> start(act), reqs(act);
     for (uint32_t a = 0; a < act; a++) {
         const uint32_t cap = db->vt_meta_h[a * 8 + MXP_VTM_CAP];
-        const uint16_t* c = cls.data() + (size_t)a * n;
+        const uint16_t* c = cls.data() + (size_t)a * pitch;
         start[a].assign(cap + 1, 0);
         for (uint32_t q = 0; q < n; q++) start[a][c[q] + 1]++;
         for (uint32_t k = 0; k < cap; k++) start[a][k + 1] += start[a][k];
@@ -2571,7 +2572,7 @@ int mxp_engine::expand_class_errors(const mxp_bag_batch* batch, mxp_dbatch* db, 
     for (const mxp_err_rec& r : recs) {
         const uint32_t s = vt_slot_of_rule[r.rule];
         const uint32_t a = (uint32_t)__builtin_popcount(last_mask & ((1u << s) - 1u));
-        const uint32_t k = cls[(size_t)a * n + r.req];
+        const uint32_t k = cls[(size_t)a * pitch + r.req];
         // (every request of the class prints the same value: one text per class record)
         int32_t text = -1;
         if (r.code >= ERR_CONV_S && r.code <= ERR_CONV_D) {

@@ -16,6 +16,10 @@ typedef // quads per fill-chunk row of the deferred-pair slots (kargs.dtp_slots,
 // at 1M requests) would put every chunk's same quads on aliased HBM channels
 #define MXP_DTP_ROW(tiles) ((uint64_t)(tiles) * 256u + 8u)
 
+// requests per row of the value-class indexes (kargs.vt_cls, u16): the batch's n rounded up to 4
+// plus 64 -- rows exactly 2^k requests apart would alias HBM channels across the fill's slots
+#define MXP_VT_PITCH(n) ((((uint64_t)(n) + 3u) & ~(uint64_t)3u) + 64u)
+
 struct mxp_kargs {
     // rule set (uploaded once per config snapshot)
     const mxp_vm_ins* prog;      // all rules' programs, concatenated
@@ -99,7 +103,7 @@ struct mxp_kargs {
     const uint32_t* gvt_mask;    // [n_words] the active slots each group's merge entries name (ascending, one each)
     const uint32_t* vt_meta;     // [n_vt][8] MXP_VTM_* fields
     const uint32_t* vt_words;    // (group, rule mask) pairs of every slot's words
-    uint16_t* vt_cls;            // [n_vt][n] class of each request
+    uint16_t* vt_cls;            // [n_vt][MXP_VT_PITCH(n)] class of each request
     uint32_t* vt_tm;             // class words, (match, error) u32 pairs: slot a, word j, class k at pair tbase + j * cap + k
     uint32_t* vt_cnt;            // requests of each class (mxp_vt_classify_kernel): value-class hit counters
     unsigned long long* vt_keys; // class tables: keys (MXP_VT_EMPTY = free) and a representative request

@@ -581,7 +581,7 @@ __device__ __forceinline__ void vt_words_of(const mxp_kargs& A, uint32_t g, uint
         const uint32_t a = ent >> 24, j = ent & 0xFFFFFFu;
         const uint32_t cap = uni(A.vt_meta[a * 8u + MXP_VTM_CAP]), tb = uni(A.vt_meta[a * 8u + MXP_VTM_TBASE]);
         if (valid) {
-            const uint32_t k = A.vt_cls[(uint64_t)a * A.n + req];
+            const uint32_t k = A.vt_cls[(uint64_t)a * MXP_VT_PITCH(A.n) + req];
             const uint2 w = *(const uint2*)(A.vt_tm + 2u * ((uint64_t)tb + (uint64_t)j * cap + k));
             vm |= w.x;
             ve |= w.y;
@@ -1157,7 +1157,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_lookup_kernel(mxp_kargs
         const unsigned long long k = T[h];
         if (k == key || k == MXP_VT_EMPTY) break;
     }
-    A.vt_cls[(uint64_t)a * N + req] = (uint16_t)h;
+    A.vt_cls[(uint64_t)a * MXP_VT_PITCH(N) + req] = (uint16_t)h;
 }
 
 // grid x: class tiles of 64 (slot by slot), y: groups of 4 words (one per wave)
@@ -1315,7 +1315,7 @@ __device__ __forceinline__ void vtfill_wave(const mxp_kargs& A, const mxp_fill* 
     for (uint32_t a = 0; a < MXP_VT_MAX; a++) {
         uint64_t c = 0;
         if (a < nvt) {
-            const uint16_t* C = A.vt_cls + (uint64_t)a * N;
+            const uint16_t* C = A.vt_cls + (uint64_t)a * MXP_VT_PITCH(N);
             if (vec && q0 < Q1) {
                 c = *(const uint64_t*)(C + q0);
             } else {
@@ -1644,7 +1644,7 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
         uint32_t ad[NVT][4];
 #pragma unroll
         for (uint32_t a = 0; a < NVT; a++) {
-            const uint16_t* C = A.vt_cls + (uint64_t)a * N;
+            const uint16_t* C = A.vt_cls + (uint64_t)a * MXP_VT_PITCH(N);
             uint64_t c = 0;
             if (vec && q0 < Q1) {
                 c = *(const uint64_t*)(C + q0);
