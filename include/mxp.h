@@ -336,10 +336,17 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
  * out[0] bytes of the packed device image, out[1] batch strings added to the overlay pool, out[2]
  * overlay byte strings.  Host threads: MXP_PACK_THREADS, else OMP_NUM_THREADS, else all cores. */
 int mxp_batch_pack_host(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* out, uint32_t cap);
-/* Frees a device batch without waiting for the device: its blocks are kept by the engine (up to
- * 8 GiB) and reused by later mxp_batch_upload calls once the work enqueued before the free -- on
- * the engine's stream and on every stream an evaluation of the batch was enqueued on -- is done. */
+/* Frees a device batch without waiting for the device: its blocks are kept by the engine and
+ * reused by later mxp_batch_upload calls once the work enqueued before the free -- on the engine's
+ * stream and on every stream an evaluation of the batch was enqueued on -- is done.  Each
+ * evaluation records the batch's completion event on its stream as it is enqueued, so the free
+ * touches no caller stream: a caller may destroy its streams before freeing the batch.  The engine
+ * keeps at most MXP_BIN_CAP_MB (environment, MiB) of such blocks, by default min(8 GiB, 1/16 of the
+ * device's memory); a device allocation that fails first frees every engine's kept blocks and
+ * retries once. */
 void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db);
+/* Bytes of freed batch blocks the engine keeps for reuse (out[0]) and its cap (out[1]). */
+int mxp_debug_bin(mxp_engine* eng, uint64_t* out);
 int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err);
 /* mxp_batch_eval_device plus fused per-rule hit counters: d_hits[rule] += the requests of this batch
  * whose predicate was true (device u64[n_rules], accumulated by the evaluation kernels as they set

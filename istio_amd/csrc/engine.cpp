@@ -8,16 +8,53 @@
 //     `map[const key]` lookups pre-extracted into virtual columns;
 //   * kernel launches on the engine's HIP stream and reporting of error pairs with the reference's
 //     exact error texts.
+#include <atomic>
 #include <deque>
 
 #include "engine_impl.h"
 
 thread_local BlockBin* g_bin_take = nullptr;
+thread_local const void* g_bin_db = nullptr;
+thread_local size_t g_bin_db_size = 0;
 thread_local std::vector<std::pair<void*, size_t>>* g_bin_give = nullptr;
+
+namespace {
+std::mutex g_bins_mu;
+std::set<BlockBin*> g_bins;  // every live engine's bin
+}  // namespace
+
+BlockBin::BlockBin() {
+    std::lock_guard<std::mutex> g(g_bins_mu);
+    g_bins.insert(this);
+}
+
+BlockBin::~BlockBin() {
+    {
+        std::lock_guard<std::mutex> g(g_bins_mu);
+        g_bins.erase(this);
+    }
+    release();
+}
+
+bool bins_release_all() {
+    std::lock_guard<std::mutex> g(g_bins_mu);
+    bool any = false;
+    for (BlockBin* b : g_bins) {
+        any |= b->held() > 0;
+        b->release();
+    }
+    return any;
+}
+
+size_t BlockBin::held() {
+    std::lock_guard<std::mutex> g(mu);
+    return bytes;
+}
 
 // the smallest block of at least `want` bytes and at most twice that (+ 1 MB), its group's work
 // waited for once
 bool BlockBin::take(size_t want, void** p, size_t* cap) {
+    std::lock_guard<std::mutex> lk(mu);
     size_t bg = 0, bi = 0, best = SIZE_MAX;
     for (size_t g = 0; g < groups.size(); g++)
         for (size_t i = 0; i < groups[g].blks.size(); i++) {
@@ -47,9 +84,20 @@ bool BlockBin::take(size_t want, void** p, size_t* cap) {
 }
 
 void BlockBin::put(Group&& g) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!cap_set) {  // (first put: the engine's device is current)
+        const char* e = getenv("MXP_BIN_CAP_MB");
+        if (e && *e) {
+            cap_bytes = (size_t)strtoull(e, nullptr, 10) << 20;
+        } else {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot) cap_bytes = std::min(cap_bytes, tot / 16);
+        }
+        cap_set = true;
+    }
     for (auto& b : g.blks) bytes += b.second;
     groups.push_back(std::move(g));
-    while (bytes > kCapBytes && !groups.empty()) {
+    while (bytes > cap_bytes && !groups.empty()) {
         Group& G = groups.front();
         for (hipEvent_t e : G.evs) {
             (void)hipEventSynchronize(e);
@@ -64,6 +112,7 @@ void BlockBin::put(Group&& g) {
 }
 
 void BlockBin::release() {
+    std::lock_guard<std::mutex> lk(mu);
     for (Group& G : groups) {
         for (hipEvent_t e : G.evs) {
             (void)hipEventSynchronize(e);
@@ -1629,9 +1678,28 @@ int mxp_engine::vt_prepare(mxp_dbatch* db, const Plan& P) {
     return MXP_OK;
 }
 
+int mxp_dbatch::note_done(hipStream_t s) {
+    hipEvent_t ev = nullptr;
+    for (auto& se : done_ev)
+        if (se.first == s) ev = se.second;
+    if (!ev) {
+        if (hipEventCreateWithFlags(&ev, kOrderEvent) != hipSuccess) return MXP_ERR_DEVICE;
+        done_ev.push_back({s, ev});
+    }
+    return hipEventRecord(ev, s) == hipSuccess ? MXP_OK : MXP_ERR_DEVICE;
+}
+
+// An evaluation of `db` on stream s, then the batch's completion event on s (whatever the body
+// enqueued before an early return also reads the batch).
 int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
                        bool log, unsigned long long* d_hits, uint64_t* stats, uint32_t q_lo, uint32_t q_hi) {
-    if (db && std::find(db->used.begin(), db->used.end(), s) == db->used.end()) db->used.push_back(s);
+    const int rc = launch_body(db, s, d_match, d_err, d_vals, log, d_hits, stats, q_lo, q_hi);
+    if (db && db->note_done(s) != MXP_OK && !rc) return fail(MXP_ERR_DEVICE, "batch completion event");
+    return rc;
+}
+
+int mxp_engine::launch_body(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
+                            bool log, unsigned long long* d_hits, uint64_t* stats, uint32_t q_lo, uint32_t q_hi) {
     // (no stale flags from the previous evaluation survive an early return below)
     last_dtp = false;
     last_dtp_counted = false;
@@ -2285,11 +2353,16 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
     if (eng->device < 0) return eng->fail(MXP_ERR_STATE, "host-only engine");
     hipError_t h = hipSetDevice(eng->device);
     if (h != hipSuccess) return eng->hipfail(h, "hipSetDevice");
+    if (int rc0 = eng->check_batch(batch)) return rc0;
     auto* db = new (std::nothrow) mxp_dbatch();
     if (!db) return MXP_ERR_NOMEM;
-    g_bin_take = &eng->bin;  // (the batch's blocks, recycled where the bin has them)
+    // (the batch's own blocks recycled where the bin has them; engine scratch grown meanwhile is not)
+    g_bin_take = &eng->bin;
+    g_bin_db = db;
+    g_bin_db_size = sizeof(mxp_dbatch);
     int rc = eng->pack(batch, db);
     g_bin_take = nullptr;
+    g_bin_db = nullptr;
     if (rc) {
         delete db;
         return rc;
@@ -2301,6 +2374,7 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
 int mxp_batch_pack_host(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* out, uint32_t cap) {
     if (!eng || !batch) return MXP_ERR_ARG;
     if (!eng->have_rules) return eng->fail(MXP_ERR_STATE, "no rule set compiled");
+    if (int rc0 = eng->check_batch(batch)) return rc0;
     mxp_dbatch db;
     mxp_engine::PackedHost H;
     int rc = eng->pack_host(batch, &db, H);
@@ -2313,8 +2387,9 @@ int mxp_batch_pack_host(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* o
 }
 
 // The batch's device blocks go to the engine's bin (no hipFree: it would wait for the whole device),
-// with an event on the engine stream (the packer) and on each stream an evaluation of the batch was
-// enqueued on: a later upload reuses a block only after those events.
+// with the completion events of the batch's evaluations (recorded by launch on each stream it was
+// evaluated on -- the free itself records nothing on a caller stream, which may be gone by now) and
+// one on the engine stream (the packer): a later upload reuses a block only after those events.
 void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db) {
     if (!db) return;
     if (!eng || eng->device < 0) {
@@ -2323,27 +2398,27 @@ void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db) {
     }
     (void)hipSetDevice(eng->device);
     BlockBin::Group g;
-    std::vector<hipStream_t> ss = db->used;
-    ss.push_back(eng->stream);
-    bool ok = true;
-    for (hipStream_t st : ss) {
-        hipEvent_t e = nullptr;
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess || hipEventRecord(e, st) != hipSuccess) {
-            if (e) (void)hipEventDestroy(e);
-            ok = false;
-            break;
-        }
-        g.evs.push_back(e);
-    }
-    if (!ok) {  // (no events: the plain frees)
-        for (hipEvent_t e : g.evs) (void)hipEventDestroy(e);
-        delete db;
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, kOrderEvent) != hipSuccess || hipEventRecord(e, eng->stream) != hipSuccess) {
+        if (e) (void)hipEventDestroy(e);
+        delete db;  // (no event: the plain frees)
         return;
     }
+    g.evs.push_back(e);
+    for (auto& se : db->done_ev) g.evs.push_back(se.second);  // (the group owns them now)
+    db->done_ev.clear();
     g_bin_give = &g.blks;
     delete db;
     g_bin_give = nullptr;
     eng->bin.put(std::move(g));
+}
+
+int mxp_debug_bin(mxp_engine* eng, uint64_t* out) {
+    if (!eng || !out) return MXP_ERR_ARG;
+    out[0] = eng->bin.held();
+    std::lock_guard<std::mutex> lk(eng->bin.mu);
+    out[1] = eng->bin.cap_bytes;
+    return MXP_OK;
 }
 
 int mxp_batch_eval_device(mxp_engine* eng, mxp_dbatch* db, void* stream, uint32_t* d_match, uint32_t* d_err) {
@@ -2443,11 +2518,115 @@ int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_request
     return e == hipSuccess ? MXP_OK : eng->hipfail(e, "launch hits");
 }
 
+int mxp_engine::check_batch(const mxp_bag_batch* b) {
+    if (!b) return MXP_ERR_ARG;
+    const uint64_t n = b->n_requests, NS = b->n_strings, NT = b->n_times, NM = b->n_maps;
+    auto bad = [&](const std::string& what) { return fail(MXP_ERR_ARG, "malformed batch: " + what); };
+    if (b->n_columns && !b->column_names) return bad("column_names is NULL");
+    if (NS && !b->str_offsets) return bad("str_offsets is NULL");
+    if (NT && (!b->time_sec || !b->time_nsec)) return bad("time_sec / time_nsec is NULL");
+    if (NM && !b->map_offsets) return bad("map_offsets is NULL");
+    // the columns read (by name; the first column of a name is the one read)
+    std::vector<std::string> names = read_attributes();
+    std::set<std::string> want(names.begin(), names.end());
+    std::vector<uint32_t> use;
+    std::set<std::string> seen;
+    std::atomic<bool> map_col{false};
+    for (uint32_t c = 0; c < b->n_columns; c++) {
+        if (!b->column_names[c]) return bad("column " + std::to_string(c) + " has no name");
+        const std::string nm(b->column_names[c]);
+        if (!want.count(nm) || !seen.insert(nm).second) continue;
+        if (n && (!b->kinds || !b->values || !b->kinds[c] || !b->values[c]))
+            return bad("column '" + nm + "' has no kinds / values");
+        use.push_back(c);
+    }
+    // first failure per worker: (request or item index, message)
+    struct Bad {
+        uint64_t at = ~0ull;
+        std::string what;
+    };
+    const unsigned T = mxp::pack_threads();
+    std::vector<Bad> errs(T);
+    auto note = [&](unsigned w, uint64_t at, std::string what) {
+        if (at < errs[w].at) errs[w] = Bad{at, std::move(what)};
+    };
+    auto first = [&]() -> const Bad* {
+        const Bad* f = nullptr;
+        for (const Bad& x : errs)
+            if (!x.what.empty() && (!f || x.at < f->at)) f = &x;
+        return f;
+    };
+    // string offsets: non-decreasing, every string < 16 MiB (the pools' descriptor limit)
+    if (NS) {
+        mxp::par_for(NS, 1u << 16, [&](uint64_t i0, uint64_t i1, unsigned w) {
+            const uint64_t* o = b->str_offsets;
+            for (uint64_t i = i0; i < i1; i++) {
+                if (o[i + 1] < o[i]) return note(w, i, "str_offsets[" + std::to_string(i + 1) + "] < str_offsets[" +
+                                                           std::to_string(i) + "]");
+                if (o[i + 1] - o[i] >= (1u << 24)) return note(w, i, "string " + std::to_string(i) + " is 16 MiB or longer");
+            }
+        });
+        if (const Bad* f = first()) return bad(f->what);
+        if (b->str_offsets[NS] && !b->str_bytes) return bad("str_bytes is NULL");
+    }
+    for (uint32_t c : use) {
+        const uint8_t* k = b->kinds[c];
+        const uint64_t* v = b->values[c];
+        const std::string nm(b->column_names[c]);
+        mxp::par_for(n, 1u << 16, [&](uint64_t q0, uint64_t q1, unsigned w) {
+            for (uint64_t q = q0; q < q1; q++) {
+                const uint8_t kd = k[q];
+                uint64_t lim = ~0ull;
+                const char* table = "";
+                switch (kd) {
+                case MXP_ABSENT: case MXP_INT64: case MXP_DOUBLE: case MXP_BOOL: case MXP_DURATION: continue;
+                case MXP_STRING: case MXP_BYTES: case MXP_OTHER: lim = NS; table = "n_strings"; break;
+                case MXP_TIMESTAMP: lim = NT; table = "n_times"; break;
+                case MXP_STRING_MAP: lim = NM; table = "n_maps"; map_col.store(true, std::memory_order_relaxed); break;
+                default:
+                    return note(w, q, "column '" + nm + "' request " + std::to_string(q) + ": kind " +
+                                          std::to_string(kd) + " > MXP_OTHER");
+                }
+                if (v[q] >= lim)
+                    return note(w, q, "column '" + nm + "' request " + std::to_string(q) + ": id " +
+                                          std::to_string(v[q]) + " >= " + table + " (" + std::to_string(lim) + ")");
+            }
+        });
+        if (const Bad* f = first()) return bad(f->what);
+    }
+    // map CSR: offsets non-decreasing, key / value ids < n_strings (read when a map is)
+    if (NM && (map_col.load() || need_maps || !vcols.empty())) {
+        const uint64_t* mo = b->map_offsets;
+        mxp::par_for(NM, 1u << 16, [&](uint64_t m0, uint64_t m1, unsigned w) {
+            for (uint64_t m = m0; m < m1; m++)
+                if (mo[m + 1] < mo[m])
+                    return note(w, m, "map_offsets[" + std::to_string(m + 1) + "] < map_offsets[" + std::to_string(m) + "]");
+        });
+        if (const Bad* f = first()) return bad(f->what);
+        const uint64_t E = mo[NM] - mo[0];
+        if (E && (!b->map_keys || !b->map_values)) return bad("map_keys / map_values is NULL");
+        const uint64_t e0 = mo[0];
+        mxp::par_for(E, 1u << 16, [&](uint64_t x0, uint64_t x1, unsigned w) {
+            for (uint64_t x = e0 + x0; x < e0 + x1; x++) {
+                if (b->map_keys[x] >= NS)
+                    return note(w, x, "map entry " + std::to_string(x) + ": key id " + std::to_string(b->map_keys[x]) +
+                                          " >= n_strings (" + std::to_string(NS) + ")");
+                if (b->map_values[x] >= NS)
+                    return note(w, x, "map entry " + std::to_string(x) + ": value id " +
+                                          std::to_string(b->map_values[x]) + " >= n_strings (" + std::to_string(NS) + ")");
+            }
+        });
+        if (const Bad* f = first()) return bad(f->what);
+    }
+    return MXP_OK;
+}
+
 int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv,
                          std::unique_ptr<mxp_dbatch>& db) {
     if (!batch) return MXP_ERR_ARG;
     if (!have_rules) return fail(MXP_ERR_STATE, "no rule set compiled");
     if (device < 0) return fail(MXP_ERR_STATE, "host-only engine");
+    if (int rc0 = check_batch(batch)) return rc0;
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return hipfail(e, "hipSetDevice");
     db.reset(new mxp_dbatch());

@@ -11,6 +11,7 @@
 #include <map>
 #include <set>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -64,15 +65,27 @@ struct BlockBin {
     };
     std::vector<Group> groups;  // oldest first
     size_t bytes = 0;
-    static constexpr size_t kCapBytes = 8ull << 30;  // beyond: the oldest groups are freed
+    // at most this many bytes kept (beyond: the oldest groups are freed): MXP_BIN_CAP_MB, else
+    // min(8 GiB, 1/16 of the device's memory)
+    size_t cap_bytes = 8ull << 30;
+    bool cap_set = false;
+    std::mutex mu;  // (a failed hipMalloc on any thread may drain every engine's bin: bins_release_all)
+    BlockBin();
+    ~BlockBin();
     bool take(size_t want, void** p, size_t* cap);
     void put(Group&& g);
-    void release();  // every block freed (engine teardown)
-    ~BlockBin() { release(); }
+    void release();  // every block freed (engine teardown, or a device allocation that failed)
+    size_t held();
 };
-// the bin DevBuf::alloc draws from / DevBuf::reset hands blocks to (set for the duration of an
-// upload / a batch free on the calling thread; null elsewhere: plain hipMalloc / hipFree)
+// every live engine's bin, drained by DevBuf::alloc when hipMalloc runs out of device memory; true
+// when any block was freed
+bool bins_release_all();
+// the bin DevBuf::alloc draws from (set for the duration of an upload, together with the batch
+// being built: only that batch's own buffers draw from the bin -- engine scratch grown meanwhile
+// is allocated plainly) / DevBuf::reset hands blocks to (a batch free); null elsewhere
 extern thread_local BlockBin* g_bin_take;
+extern thread_local const void* g_bin_db;      // the mxp_dbatch under construction
+extern thread_local size_t g_bin_db_size;
 extern thread_local std::vector<std::pair<void*, size_t>>* g_bin_give;
 
 struct DevBuf {
@@ -91,13 +104,26 @@ struct DevBuf {
         p = nullptr;
         n = cap = 0;
     }
+    bool in_batch() const {
+        return g_bin_take && (const char*)this >= (const char*)g_bin_db &&
+               (const char*)this < (const char*)g_bin_db + g_bin_db_size;
+    }
     hipError_t alloc(size_t bytes) {
         reset();
         if (bytes == 0) bytes = 16;
         n = bytes;
-        if (g_bin_take && g_bin_take->take(bytes, &p, &cap)) return hipSuccess;
+        if (in_batch() && g_bin_take->take(bytes, &p, &cap)) return hipSuccess;
         cap = bytes;
-        return hipMalloc(&p, bytes);
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipErrorOutOfMemory && bins_release_all()) {  // idle recycled blocks first
+            (void)hipGetLastError();
+            e = hipMalloc(&p, bytes);
+        }
+        if (e != hipSuccess) {
+            p = nullptr;
+            n = cap = 0;
+        }
+        return e;
     }
     // grow-only: keeps the allocation when it is large enough (engine-owned scratch reused across calls)
     hipError_t reserve(size_t bytes) {
@@ -185,7 +211,14 @@ struct mxp_dbatch {
     // byte strings GB + item, canonical GC + item, times GT + item (items: batch strings / times
     // first, then parsed ip() / timestamp() values by string id) -- read back on demand
     bool dev_packed = false;
-    std::vector<hipStream_t> used;  // streams evaluations of this batch were enqueued on (mxp_batch_free)
+    // per stream an evaluation of this batch was enqueued on: an event recorded after that
+    // evaluation's last kernel (launch), so mxp_batch_free only collects events and never touches a
+    // caller stream that may be gone by then
+    std::vector<std::pair<hipStream_t, hipEvent_t>> done_ev;
+    ~mxp_dbatch() {
+        for (auto& se : done_ev) (void)hipEventDestroy(se.second);
+    }
+    int note_done(hipStream_t s);  // record (creating on first use) the completion event of stream s
     bool vtd_ready = false;  // the packer's provisional class tables (engine scratch) hold this batch's
     uint32_t ns = 0, nt = 0, G = 0, GB = 0, GC = 0, GT = 0;
     DevBuf pip, pip_ok, pts_sec, pts_nsec, pts_ok, btsec, btnsec;
@@ -602,6 +635,12 @@ struct mxp_engine : public mxp::LowerTables {
         return out;
     }
     std::vector<std::string> attr_names;  // mxp_ruleset_columns' strings (valid until the next call)
+    // A caller's batch is checked before any packer (host or device) or host pass reads it: every
+    // column the rule set or the resolver reads, the string offsets and the map CSR -- ids past their
+    // tables, offsets running backwards, unknown kinds -- so a malformed batch is MXP_ERR_ARG with the
+    // first bad field named, never an out-of-range index into a device table (protoBag.go:255-265
+    // answers an undefined index with an error too).
+    int check_batch(const mxp_bag_batch* b);
     // pack + launch into fresh device bitmaps (dm, de; dv = Eval registers when non-null)
     int evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv, std::unique_ptr<mxp_dbatch>& db);
     // wait for the evaluation, fetch and format its error records, keep `db` as the last batch
@@ -675,6 +714,8 @@ struct mxp_engine : public mxp::LowerTables {
     int launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
                unsigned long long* d_hits = nullptr, uint64_t* d_stats = nullptr, uint32_t q_lo = 0,
                uint32_t q_hi = 0xFFFFFFFFu);
+    int launch_body(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals, bool log,
+                    unsigned long long* d_hits, uint64_t* d_stats, uint32_t q_lo, uint32_t q_hi);
     // fused hit counters: the true pairs the guard-index kernel set (d_stats) decide, on the device,
     // between counting in the next evaluation's kernels and the streaming hits kernel (d_gate)
     DevBuf d_stats;

@@ -92,7 +92,12 @@ MXP_NHD uint32_t mxp_go_encode(uint32_t r, uint32_t* bytes) {
     return 4;
 }
 
-// strings.ToUpper(s) as a byte stream (Go 1.9 strings.Map with unicode.ToUpper)
+// strings.ToUpper(s) as a byte stream (Go 1.9 strings.Map with unicode.ToUpper).  The reference
+// builds with Go 1.9 (bin/verify_go_version.sh:24-25, DOCKER_BUILDER istio/ci:go1.9 in
+// bin/envsetup.sh:38).  Go 1.9's Map encodes every mapped rune after the first change with
+// utf8.EncodeRune, so U+0080 stays C2 80 here.  The single-byte write of runes <= utf8.RuneSelf
+// (which turned U+0080 into a lone 0x80 byte) arrived with the Go 1.10 rewrite of Map and was
+// fixed again in Go 1.11; it is not the reference's behaviour.  Checked: U+0080 case.
 struct MxpUpperStream {
     const uint8_t* s;
     uint32_t n, i;

@@ -11,7 +11,7 @@
 #define MXP_RXOF_SYNTAX 0xFFFFFFFFu
 #define MXP_RXOF_UNSUPPORTED 0xFFFFFFFEu
 
-typedef // quads per fill-chunk row of the deferred-pair slots (kargs.dtp_slots, 16 B a quad) and counts
+// quads per fill-chunk row of the deferred-pair slots (kargs.dtp_slots, 16 B a quad) and counts
 // (kargs.dtp_qn, 1 B): the tiles' 256 quads each plus 8 -- a row of exactly 2^k quads (4 MB of slots
 // at 1M requests) would put every chunk's same quads on aliased HBM channels
 #define MXP_DTP_ROW(tiles) ((uint64_t)(tiles) * 256u + 8u)
@@ -20,7 +20,7 @@ typedef // quads per fill-chunk row of the deferred-pair slots (kargs.dtp_slots,
 // plus 64 -- rows exactly 2^k requests apart would alias HBM channels across the fill's slots
 #define MXP_VT_PITCH(n) ((((uint64_t)(n) + 3u) & ~(uint64_t)3u) + 64u)
 
-struct mxp_kargs {
+typedef struct mxp_kargs {
     // rule set (uploaded once per config snapshot)
     const mxp_vm_ins* prog;      // all rules' programs, concatenated
     const uint32_t* rule_off;    // [n_rules + 1]

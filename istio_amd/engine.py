@@ -97,6 +97,7 @@ SIGNATURES = {
     "mxp_ruleset_info": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32]),
     "mxp_ruleset_columns": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32]),
     "mxp_debug_wave_times": (ctypes.c_int, [_VP, _VP, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    "mxp_debug_bin": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint64)]),
     "mxp_go_to_upper": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, _VP, ctypes.c_uint64,
                                        ctypes.POINTER(ctypes.c_uint64)]),
 }
@@ -269,6 +270,12 @@ class Engine:
         self._check(self.lib.mxp_debug_wave_times(self.h, out.ctypes.data, out.size, ctypes.byref(k)),
                     "mxp_debug_wave_times")
         return out[:k.value].reshape(-1, 8)
+
+    def bin_stats(self):
+        """(bytes of freed batch blocks kept for reuse, the cap) -- mxp_debug_bin."""
+        out = (ctypes.c_uint64 * 2)()
+        self._check(self.lib.mxp_debug_bin(self.h, out), "mxp_debug_bin")
+        return int(out[0]), int(out[1])
 
     def ruleset_info(self) -> dict:
         """Kernel-side shape of the rule set (guards, continuation templates, column segments)."""
@@ -522,6 +529,37 @@ def bits_to_codes(match: np.ndarray, err: np.ndarray, n_rules: int) -> np.ndarra
     m = ((match.T[:, :, None] >> shifts) & 1).reshape(n, W * 32)[:, :n_rules]
     e = ((err.T[:, :, None] >> shifts) & 1).reshape(n, W * 32)[:, :n_rules]
     return np.where(e != 0, ERROR, m).astype(np.uint8)
+
+
+class TypeChecker:
+    """expr.TypeChecker (mixer/pkg/expr/evaluator.go:33-42) as evaluator.checker implements it
+    (mixer/pkg/il/evaluator/checker.go:29-46): the engine's own front end and type check
+    (mxp_ruleset_compile on a host-only engine, mxp_rule_types), no device needed.  `finder` maps
+    attribute names to ValueTypes (names or enum values), like an AttributeDescriptorFinder."""
+
+    _NAMES = {v: k for k, v in VALUE_TYPES.items()}
+
+    def __init__(self):
+        self.eng = Engine(-1)
+
+    def eval_type(self, expression: str, finder: Dict[str, object]):
+        """-> (ValueType name, error text or None): EvalType (checker.go:29-35)."""
+        self.eng.set_vocabulary(finder)
+        st = int(self.eng.compile([expression])[0])
+        if st == RULE_PARSE_ERROR:
+            return "VALUE_TYPE_UNSPECIFIED", "failed to parse expression '%s': %s" % (expression, self.eng.rule_error(0))
+        if st in (RULE_TYPE_ERROR, RULE_COMPILE_PANIC):
+            return "VALUE_TYPE_UNSPECIFIED", self.eng.rule_error(0)
+        return self._NAMES[self.eng.rule_types(0)[0]], None
+
+    def assert_type(self, expression: str, finder: Dict[str, object], expected: str):
+        """-> error text or None: AssertType (checker.go:37-44)."""
+        t, err = self.eval_type(expression, finder)
+        if err is not None:
+            return err
+        if t != expected:
+            return "expression '%s' evaluated to type %s, expected type %s" % (expression, t, expected)
+        return None
 
 
 class Evaluator:

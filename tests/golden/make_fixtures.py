@@ -645,6 +645,22 @@ def extract_manifest(ref):
     return {"source": "mixer/testdata/config/attributes.yaml", "attributes": attrs}
 
 
+def extract_checker(ref):
+    """mixer/pkg/il/evaluator/checker_test.go: TestTypeCheck (:26-80, the attribute finder and
+    expression -> value type or error fragment) and TestAssertType (:82-111, expression + expected
+    type -> error fragment, "" = no error)."""
+    src = open(os.path.join(ref, "mixer/pkg/il/evaluator/checker_test.go"), encoding="utf-8").read()
+    out = {"source": "mixer/pkg/il/evaluator/checker_test.go:26-111"}
+    for func, key in (("TestTypeCheck", "type_check"), ("TestAssertType", "assert_type")):
+        m = re.search(r"func %s\(t \*testing.T\) \{\s*af := newAF\(\[\]\*ad\{" % func, src)
+        attrs = {}
+        for _, e in gosrc.Parser(src, m.end() - 1).parse_composite("[]*ad")[2]:
+            attrs[conv(e[2][0][1])["v"]] = conv(e[2][1][1])["v"]
+        rows = [[conv(v)["v"] for _, v in e[2]] for _, e in _struct_table(src, func)]
+        out[key] = {"attrs": attrs, "rows": rows}
+    return out
+
+
 def main():
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     outs = {
@@ -659,6 +675,7 @@ def main():
         "resolver_cases.json": extract_resolver(ref),
         "memquota_cases.json": extract_memquota(ref),
         "protobag_cases.json": extract_protobag(ref),
+        "checker_cases.json": extract_checker(ref),
     }
     for name, data in outs.items():
         with open(os.path.join(HERE, name), "w") as f:

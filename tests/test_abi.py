@@ -105,7 +105,8 @@ def test_go_binding_calls_declared_symbols():
                   "var _ runtime.VocabularyChangeListener = (*Batcher)(nil)",
                   "var _ Resolver = (*mxpResolver)(nil)", "var _ Actions = (*actions)(nil)",
                   "var _ list = (*gpuList)(nil)", "var _ listentry.Handler = (*gpuHandler)(nil)",
-                  "var _ listentry.BagHandler = (*gpuHandler)(nil)"):
+                  "var _ listentry.BagHandler = (*gpuHandler)(nil)",
+                  "var _ expr.TypeChecker = (*TypeChecker)(nil)", "var _ compiled.Expression = Expression{}"):
         assert iface in go, iface
     # the list adapter's device calls (mxp_list*) are all bound, each with the header's arity
     hdr_decl = {m.group(1): m.group(2) for m in re.finditer(r"\b(mxp_list[a-z_]*)\(([^;]*?)\);", hdr, re.S)}

@@ -9,7 +9,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
-OBJS = ["kernels.hip.o", "resolve.hip.o", "lists.hip.o", "quota.hip.o"]
+OBJS = ["kernels.hip.o", "resolve.hip.o", "lists.hip.o", "quota.hip.o", "pack.hip.o"]
 FORBIDDEN = re.compile(r"^\s+s_(store|atomic|buffer_store|buffer_atomic|dcache_wb|dcache_discard|scratch_store)\w*",
                        re.M)
 
