@@ -410,6 +410,10 @@ def list_bench(args, rank, world, local, kind=None, emit=True):
     n = len(bs)
     alg = int(off[-1]) + 8 * (n + 1) + 4 * n  # symbol bytes + offsets read, one code written each
     achieved = alg / (kernel_ms * 1e-3) / 1e9
+    # the kernel the step launches (lists.cpp mxp_list_check_device): regex lists stage their
+    # automata in LDS unless MXP_LIST_LDS=0
+    kname = ("mxp_list_rx_kernel" if kind == "c3-regex" and os.environ.get("MXP_LIST_LDS", "1") != "0"
+             else "mxp_list_kernel")
     out = {"metric": "list-adapter lookups/sec (%s, %d entries)" % (kind, lst.num_entries()),
            "value": world * n * args.steps / elapsed, "unit": "lookups/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -418,9 +422,10 @@ def list_bench(args, rank, world, local, kind=None, emit=True):
            "config": {"workload": "C3 %s list, %d entries, %d lookups per GPU (configs[2])" % (kind[3:], len(entries), n),
                       "entries": len(entries), "lookups_per_gpu": n, "parallelism": "lookup-sharded dp%d" % world},
            "kernel_ms": kernel_ms, "list_compile_s": t_compile,
+           "lds_bank_conflicts": lds_conflicts(kind),
            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "mxp_list_kernel",
-                        "alg_bytes_per_launch": alg}}
+                        "frac": achieved / HBM_PEAK_GBS, "traffic": measured_traffic(kind, args.list_entries, n),
+                        "kernel": kname, "alg_bytes_per_launch": alg}}
     if rank == 0 and not args.no_cpu_baseline and world == 1:
         out["cpu_baseline"] = list_cpu_baseline(L, kind, entries, syms, args.list_cpu_seconds, args.cpu_threads)
     del d_blob, d_off, d_codes, lst
@@ -781,7 +786,7 @@ def main():
         # configs[2]: the three list kinds (100k entries, 1M lookups per GPU), driver-timed too
         a3 = argparse.Namespace(**vars(args))
         ckeys = ("metric", "value", "unit", "ms_per_step", "kernel_ms", "list_compile_s", "config", "roofline",
-                 "cpu_baseline")
+                 "lds_bank_conflicts", "cpu_baseline")
         out["c3"] = {}
         for k in ("c3-ip", "c3-str", "c3-regex"):
             r = list_bench(a3, rank, world, local, kind=k, emit=False)

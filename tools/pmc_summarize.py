@@ -21,7 +21,8 @@ EVAL_KERNELS = ("mxp_fill_kernel", "mxp_fill_dtp_kernel", "mxp_vtfill", "mxp_vt_
                 "mxp_vt_eval_kernel", "mxp_guard_kernel", "mxp_guard2_kernel", "mxp_eval_kernel", "mxp_index_kernel",
                 "mxp_index_dtp_kernel", "mxp_index_dtp_lite_kernel", "mxp_index5_kernel", "mxp_dtp_sort_kernel", "mxp_dtp_apply_kernel",
                 "mxp_inject_kernel", "mxp_hits_kernel", "mxp_hits_ragged_kernel", "mxp_hits_gate_kernel",
-                "mxp_eval_deep_kernel", "mxp_quota", "mxp_dtp_hits_kernel")
+                "mxp_eval_deep_kernel", "mxp_quota", "mxp_dtp_hits_kernel",
+                "mxp_list_kernel", "mxp_list_nfa_kernel", "mxp_list_rx_kernel", "mxp_list_rx_nfa_kernel")
 
 
 def per_kernel(path_glob, counter):
@@ -42,7 +43,10 @@ def main():
     p.add_argument("--rules", type=int, default=10000)
     p.add_argument("--requests", type=int, default=1 << 20)
     p.add_argument("--workload", default="c2")
+    p.add_argument("--list-entries", type=int, default=100_000)
     a, _ = p.parse_known_args()
+    if a.workload.startswith("c3"):  # list workloads are keyed by their --list-entries (bench.list_bench)
+        a.rules = a.list_entries
     # bench.py --workload c5 (C2 predicates + memquota in one step) looks its traffic up as "c2q"
     a.workload = {"c5": "c2q"}.get(a.workload, a.workload)
     fetch = per_kernel(os.path.join(a.dir, "FETCH_SIZE", "**", "*counter_collection.csv"), "FETCH_SIZE")
