@@ -46,6 +46,21 @@ bool bins_release_all() {
     return any;
 }
 
+// the cap, set on first use (an upload or free: the engine's device is current)
+size_t BlockBin::cap_locked() {
+    if (!cap_set) {
+        const char* e = getenv("MXP_BIN_CAP_MB");
+        if (e && *e) {
+            cap_bytes = (size_t)strtoull(e, nullptr, 10) << 20;
+        } else {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot) cap_bytes = std::min(cap_bytes, tot / 16);
+        }
+        cap_set = true;
+    }
+    return cap_bytes;
+}
+
 size_t BlockBin::held() {
     std::lock_guard<std::mutex> g(mu);
     return bytes;
@@ -85,19 +100,10 @@ bool BlockBin::take(size_t want, void** p, size_t* cap) {
 
 void BlockBin::put(Group&& g) {
     std::lock_guard<std::mutex> lk(mu);
-    if (!cap_set) {  // (first put: the engine's device is current)
-        const char* e = getenv("MXP_BIN_CAP_MB");
-        if (e && *e) {
-            cap_bytes = (size_t)strtoull(e, nullptr, 10) << 20;
-        } else {
-            size_t fr = 0, tot = 0;
-            if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot) cap_bytes = std::min(cap_bytes, tot / 16);
-        }
-        cap_set = true;
-    }
+    const size_t cap = cap_locked();
     for (auto& b : g.blks) bytes += b.second;
     groups.push_back(std::move(g));
-    while (bytes > cap_bytes && !groups.empty()) {
+    while (bytes > cap && !groups.empty()) {
         Group& G = groups.front();
         for (hipEvent_t e : G.evs) {
             (void)hipEventSynchronize(e);
@@ -2415,9 +2421,10 @@ void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db) {
 
 int mxp_debug_bin(mxp_engine* eng, uint64_t* out) {
     if (!eng || !out) return MXP_ERR_ARG;
+    if (eng->device >= 0) (void)hipSetDevice(eng->device);
     out[0] = eng->bin.held();
     std::lock_guard<std::mutex> lk(eng->bin.mu);
-    out[1] = eng->bin.cap_bytes;
+    out[1] = eng->bin.cap_locked();
     return MXP_OK;
 }
 

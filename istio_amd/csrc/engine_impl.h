@@ -76,6 +76,7 @@ struct BlockBin {
     void put(Group&& g);
     void release();  // every block freed (engine teardown, or a device allocation that failed)
     size_t held();
+    size_t cap_locked();  // (with mu held)
 };
 // every live engine's bin, drained by DevBuf::alloc when hipMalloc runs out of device memory; true
 // when any block was freed

@@ -5,6 +5,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdlib>
 #include <string_view>
 #include <thread>
@@ -30,6 +33,76 @@ inline unsigned pack_threads() {
     return n;
 }
 
+// Persistent host workers for the parallel loops: a par_for used to start its threads per call
+// (~10-20 us per std::thread), which the large downloads paid per 32 MB chunk and every packing /
+// validation pass per call.  One job at a time; a call made while the pool is busy (another
+// engine's thread, or a loop nested inside a job) runs on threads of its own as before.
+class Pool {
+  public:
+    static Pool& get() {
+        static Pool* p = new Pool();  // (never destroyed: workers may outlive static destructors)
+        return *p;
+    }
+    // f(t) for t in [0, T): t = 0 on the calling thread; false when the pool is busy
+    template <class F>
+    bool run(unsigned T, F&& f) {
+        if (T <= 1 || tl_inside()) return false;
+        std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+        if (!busy.owns_lock()) return false;
+        grow(T - 1);
+        std::function<void(unsigned)> job = [&f](unsigned t) { f(t); };
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &job;
+            want_ = T - 1;
+            left_ = T - 1;
+            gen_++;
+        }
+        cv_.notify_all();
+        tl_inside() = true;
+        f(0u);
+        tl_inside() = false;
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [&] { return left_ == 0; });
+        job_ = nullptr;
+        return true;
+    }
+
+  private:
+    static bool& tl_inside() {
+        static thread_local bool v = false;
+        return v;
+    }
+    void grow(unsigned k) {
+        while (workers_ < k) {
+            const unsigned id = ++workers_;  // worker id: job index id (1..)
+            std::thread([this, id] { loop(id); }).detach();
+        }
+    }
+    void loop(unsigned id) {
+        tl_inside() = true;
+        uint64_t seen = 0;
+        for (;;) {
+            std::function<void(unsigned)>* job;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (id > want_) continue;
+                job = job_;
+            }
+            (*job)(id);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--left_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_, done_;
+    std::function<void(unsigned)>* job_ = nullptr;
+    uint64_t gen_ = 0;
+    unsigned want_ = 0, left_ = 0, workers_ = 0;
+};
+
 // f(begin, end, worker) over [0, n) in contiguous slices of at least `grain` items.
 template <class F>
 void par_for(uint64_t n, uint64_t grain, F&& f) {
@@ -39,15 +112,16 @@ void par_for(uint64_t n, uint64_t grain, F&& f) {
         f(0, n, 0u);
         return;
     }
+    const uint64_t step = (n + T - 1) / T;
+    auto slice = [&](unsigned t) {
+        const uint64_t a = t * step, b = std::min(n, a + step);
+        if (a < b) f(a, b, t);
+    };
+    if (Pool::get().run((unsigned)T, slice)) return;
     std::vector<std::thread> th;
     th.reserve(T - 1);
-    const uint64_t step = (n + T - 1) / T;
-    for (uint64_t t = 1; t < T; t++) {
-        const uint64_t a = t * step, b = std::min(n, a + step);
-        if (a >= b) break;
-        th.emplace_back([&f, a, b, t] { f(a, b, (unsigned)t); });
-    }
-    f(0, std::min(n, step), 0u);
+    for (uint64_t t = 1; t < T; t++) th.emplace_back([&slice, t] { slice((unsigned)t); });
+    slice(0u);
     for (auto& x : th) x.join();
 }
 
@@ -111,6 +185,7 @@ void dedupe_first(uint32_t m, H&& hash, E&& eq, std::vector<uint32_t>& rep) {
             }
         }
     };
+    if (Pool::get().run(T, run)) return;
     std::vector<std::thread> th;
     for (unsigned t = 1; t < T; t++) th.emplace_back(run, t);
     run(0);
