@@ -276,9 +276,14 @@ def fresh_batch_block(eng, batches, evaluate, steps, stream, n_rules, world):
     """Every step takes a NEW batch from host memory: mxp_batch_upload (H2D copy of the columnar
     batch, device interning, value-class dictionary, string heads; synchronous) + the evaluation
     (enqueued; the next upload's copy overlaps it).  The two batches alternate; a step's device
-    batch is freed two steps later (after its evaluation has drained).  PCIe-inclusive."""
+    batch is freed two steps later (after its evaluation has drained).  PCIe-inclusive.  The host
+    batches live in pinned memory (mxp_host_alloc), as a binding's reused packing arenas do
+    (INTEGRATION.md 2e): their copies are DMA at the link's rate."""
     import numpy as np
     import torch
+    from istio_amd.engine import pinned_batch
+    pinned = [pinned_batch(b) for b in batches]
+    batches = [b for b, _ in pinned]
     keep, up_s = [], []
     h2d = [batch_h2d_bytes(b) for b in batches]
 
@@ -311,6 +316,7 @@ def fresh_batch_block(eng, batches, evaluate, steps, stream, n_rules, world):
                          "kernel": "mxp_batch_upload: H2D copy of the host columnar batch + the device packer "
                                    "(intern, gather, pool, pre-tables, value-class dictionary, heads); "
                                    "achieved = batch bytes / upload wall time"},
+            "host_memory": "pinned (mxp_host_alloc arenas)",
             "path": "host columnar batch (a new 1M-request batch every step) -> mxp_batch_upload -> evaluation "
                     "(compact errors, fused hit counters); wall time per step, PCIe-inclusive"}
 
@@ -551,22 +557,29 @@ def end_to_end(eng, batch, n_rules, reps):
     so each request's action list is every rule whose predicate holds (resolver.go:202-238).
     PCIe-inclusive; not `value` (whose inputs are resident in HBM)."""
     import numpy as np
+    from istio_amd.engine import pinned_batch
     eng.set_resolver("destination.service", "istio-system", ["istio-system"] * n_rules,
                      np.ones(n_rules, dtype=np.uint32), np.zeros(n_rules, dtype=np.uint8),
                      np.zeros(n_rules, dtype=np.uint8))
-    status, _, off, _ = eng.resolve_arrays(batch, 0)  # warm-up (allocations, first-touch of pinned pages)
+    batch, arena = pinned_batch(batch)  # (the binding's packing arena: pinned host memory)
+    ids16 = n_rules <= 65536  # mxp_resolve_batch_ex(MXP_RESOLVE_IDS_U16)
+    status, _, off, _ = eng.resolve_arrays(batch, 0, ids16=ids16)  # warm-up (allocations, first touch)
     cap = max(16, int(off[-1]))
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        status, _, off, _ = eng.resolve_arrays(batch, 0, cap)
+        status, _, off, _ = eng.resolve_arrays(batch, 0, cap, ids16=ids16)
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
+    sel_bytes = int(off[-1]) * (2 if ids16 else 4)
     return {"pairs_per_s": batch.n * n_rules / t, "requests_per_s": batch.n / t, "ms_per_batch": t * 1e3,
             "reps": reps, "selected_per_request": float(off[-1]) / max(batch.n, 1),
-            "pred_error_requests": int((status == 3).sum()),
-            "path": "host columnar bags -> mxp_resolve_batch (device pack + evaluation + action-list gather) -> "
-                    "host action lists; median of reps, PCIe-inclusive"}
+            "pred_error_requests": int((status == 3).sum()), "rule_ids": "u16" if ids16 else "u32",
+            "action_list_bytes": sel_bytes, "action_list_ms_at_50GBps": sel_bytes / 50e9 * 1e3,
+            "host_memory": "pinned batch (mxp_host_alloc arena)",
+            "path": "host columnar bags -> mxp_resolve_batch_ex (device pack + namespaces + compact evaluation + "
+                    "first errors from the records + device scan + action-list gather) -> host action lists; median "
+                    "of reps, PCIe-inclusive"}
 
 
 def predicate_bench(args, kind, rank, world, local, with_quota=False):

@@ -190,6 +190,12 @@ int mxp_resolver_set(mxp_engine* eng, const char* identity_attr, const char* def
                      const uint8_t* empty_match, uint32_t n);
 int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
                       uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap);
+/* mxp_resolve_batch with options: flags MXP_RESOLVE_IDS_U16 writes the selected rule ids as uint16_t
+ * (rule sets of at most 65536 rules; MXP_ERR_ARG otherwise): half the bytes of the action lists
+ * brought back.  sel_rules has room for sel_cap ids of that width. */
+#define MXP_RESOLVE_IDS_U16 1u
+int mxp_resolve_batch_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
+                         uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap);
 /* mxp_resolve_batch plus each Resolve's referenced attributes (mxp_attr_ref, as mxp_eval_refs): the
  * identity attribute; when it is a string, context.protocol (filterActions, resolver.go:208); and the
  * reads of the predicates filterActions evaluates, in order, up to and including the first that
@@ -328,6 +334,14 @@ int mxp_wire_decode(mxp_engine* eng, const mxp_wire_batch* wire, const char* con
                     mxp_wire** out);
 const mxp_bag_batch* mxp_wire_view(const mxp_wire* w);
 void mxp_wire_free(mxp_wire* w);
+
+/* Pinned (page-locked) host memory for the arrays of an mxp_bag_batch: a batch packed into such
+ * memory is copied to the device by DMA at the link's rate, and the batch check (MXP_ERR_ARG on
+ * malformed ids / offsets) runs on the host while the copies are in flight.  Pageable arrays work
+ * too; the runtime stages them through its own buffers first.  A binding keeps a few such arenas
+ * and reuses them batch after batch. */
+int mxp_host_alloc(size_t bytes, void** out);
+void mxp_host_free(void* p);
 
 typedef struct mxp_dbatch mxp_dbatch;
 int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out);

@@ -2191,6 +2191,7 @@ void mxp_engine_destroy(mxp_engine* eng) {
     if (!eng) return;
     if (eng->device >= 0) (void)hipSetDevice(eng->device);
     if (eng->pk_host) (void)hipHostFree(eng->pk_host);
+    if (eng->res_hinfo) (void)hipHostFree(eng->res_hinfo);
     for (int k = 0; k < 2; k++) {
         if (eng->bounce_ev[k]) (void)hipEventDestroy(eng->bounce_ev[k]);
         if (eng->bounce[k]) (void)hipHostFree(eng->bounce[k]);
@@ -2359,7 +2360,6 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
     if (eng->device < 0) return eng->fail(MXP_ERR_STATE, "host-only engine");
     hipError_t h = hipSetDevice(eng->device);
     if (h != hipSuccess) return eng->hipfail(h, "hipSetDevice");
-    if (int rc0 = eng->check_batch(batch)) return rc0;
     auto* db = new (std::nothrow) mxp_dbatch();
     if (!db) return MXP_ERR_NOMEM;
     // (the batch's own blocks recycled where the bin has them; engine scratch grown meanwhile is not)
@@ -2417,6 +2417,20 @@ void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db) {
     delete db;
     g_bin_give = nullptr;
     eng->bin.put(std::move(g));
+}
+
+int mxp_host_alloc(size_t bytes, void** out) {
+    if (!out) return MXP_ERR_ARG;
+    *out = nullptr;
+    if (hipHostMalloc(out, bytes ? bytes : 16, hipHostMallocDefault) != hipSuccess) {
+        *out = nullptr;
+        return MXP_ERR_NOMEM;
+    }
+    return MXP_OK;
+}
+
+void mxp_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int mxp_debug_bin(mxp_engine* eng, uint64_t* out) {
@@ -2581,6 +2595,14 @@ int mxp_engine::check_batch(const mxp_bag_batch* b) {
         const uint64_t* v = b->values[c];
         const std::string nm(b->column_names[c]);
         mxp::par_for(n, 1u << 16, [&](uint64_t q0, uint64_t q1, unsigned w) {
+            bool maps = false;  // (one store of the shared flag per slice: no cache-line ping-pong)
+            struct Flag {
+                bool& m;
+                std::atomic<bool>& out;
+                ~Flag() {
+                    if (m) out.store(true, std::memory_order_relaxed);
+                }
+            } flag{maps, map_col};
             for (uint64_t q = q0; q < q1; q++) {
                 const uint8_t kd = k[q];
                 uint64_t lim = ~0ull;
@@ -2589,7 +2611,7 @@ int mxp_engine::check_batch(const mxp_bag_batch* b) {
                 case MXP_ABSENT: case MXP_INT64: case MXP_DOUBLE: case MXP_BOOL: case MXP_DURATION: continue;
                 case MXP_STRING: case MXP_BYTES: case MXP_OTHER: lim = NS; table = "n_strings"; break;
                 case MXP_TIMESTAMP: lim = NT; table = "n_times"; break;
-                case MXP_STRING_MAP: lim = NM; table = "n_maps"; map_col.store(true, std::memory_order_relaxed); break;
+                case MXP_STRING_MAP: lim = NM; table = "n_maps"; maps = true; break;
                 default:
                     return note(w, q, "column '" + nm + "' request " + std::to_string(q) + ": kind " +
                                           std::to_string(kd) + " > MXP_OTHER");
@@ -2629,11 +2651,10 @@ int mxp_engine::check_batch(const mxp_bag_batch* b) {
 }
 
 int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv,
-                         std::unique_ptr<mxp_dbatch>& db) {
+                         std::unique_ptr<mxp_dbatch>& db, uint8_t* d_req_err) {
     if (!batch) return MXP_ERR_ARG;
     if (!have_rules) return fail(MXP_ERR_STATE, "no rule set compiled");
     if (device < 0) return fail(MXP_ERR_STATE, "host-only engine");
-    if (int rc0 = check_batch(batch)) return rc0;
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return hipfail(e, "hipSetDevice");
     db.reset(new mxp_dbatch());
@@ -2645,10 +2666,13 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
     const uint32_t R = (uint32_t)rules.size();
     const uint32_t W = (R + 31) / 32;
     if ((e = dm.reserve((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc match");
-    if ((e = de.reserve((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc err");
+    if (!d_req_err && (e = de.reserve((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc err");
     if (dv && (e = dv->reserve((size_t)n * R * 8)) != hipSuccess) return hipfail(e, "alloc values");
     trace_mark("bitmap allocation");
-    rc = launch(db.get(), stream, dm.as<uint32_t>(), de.as<uint32_t>(), dv ? dv->as<uint64_t>() : nullptr, true);
+    req_err_out = d_req_err;
+    rc = launch(db.get(), stream, dm.as<uint32_t>(), d_req_err ? nullptr : de.as<uint32_t>(),
+                dv ? dv->as<uint64_t>() : nullptr, true);
+    req_err_out = nullptr;
     trace_mark("evaluation kernels");
     return rc;
 }

@@ -20,6 +20,7 @@
 #include "goutil.h"
 #include "ilgen.h"
 #include "kargs.h"
+#include "pack_args.h"
 #include "lower.h"
 #include "regex.h"
 #include "par.h"
@@ -483,6 +484,25 @@ struct mxp_engine : public mxp::LowerTables {
     // resolve scratch (resolver.cpp), reused across calls
     DevBuf res_dm, res_de, res_info, res_lo, res_hi, res_amask, res_empty, res_status, res_err_rule, res_count,
         res_off, res_sel;
+    // compact Resolve (resolver.cpp): request error flags instead of the error bitmap, each request's
+    // first applicable erroring rule from the error records (sparse pairs scattered into res_err_in),
+    // block sums of the device scan of the counts
+    DevBuf res_flags, res_err_in, res_pairs, res_bsum;
+    std::vector<uint32_t> res_best;       // [n] host scratch: best resolution rank per request (~0 none)
+    void* res_hinfo = nullptr;            // pinned copy of the requests' namespace info
+    size_t res_hinfo_cap = 0;
+    // the namespace names of the configuration on the device (mxp_ns_kernel): open-addressing table
+    // of content hashes, descriptors, bytes
+    DevBuf res_ns_tab, res_ns_desc, res_ns_blob;
+    uint32_t res_ns_mask = 0;
+    // set by pack_device for the batch it packed (engine scratch, valid until the next upload): the
+    // raw identity / context.protocol columns as uploaded (nullptr: absent from the batch) and the
+    // raw batch strings; res_raw = false when the host packer ran or the columns were not uploaded
+    bool res_raw = false;
+    const uint8_t* res_id_kind = nullptr;
+    const uint64_t* res_id_val = nullptr;
+    const uint8_t* res_pr_kind = nullptr;
+    const uint64_t* res_pr_val = nullptr;
     uint64_t last_error_count = 0;
     std::unique_ptr<mxp_dbatch> last_db;  // keeps the last batch's interned overlays for decoding
 
@@ -643,7 +663,9 @@ struct mxp_engine : public mxp::LowerTables {
     // answers an undefined index with an error too).
     int check_batch(const mxp_bag_batch* b);
     // pack + launch into fresh device bitmaps (dm, de; dv = Eval registers when non-null)
-    int evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv, std::unique_ptr<mxp_dbatch>& db);
+    // d_req_err: compact error output (per-request flags; de is not written)
+    int evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv, std::unique_ptr<mxp_dbatch>& db,
+                 uint8_t* d_req_err = nullptr);
     // wait for the evaluation, fetch and format its error records, keep `db` as the last batch
     int collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_dbatch>& db);
     int expand_class_errors(const mxp_bag_batch* batch, mxp_dbatch* db, uint32_t n_class, uint32_t room);
@@ -661,8 +683,15 @@ struct mxp_engine : public mxp::LowerTables {
     int pack_host(const mxp_bag_batch* b, mxp_dbatch* db, PackedHost& H);
     // mxp_batch_upload: the device packer (pack_device.cpp), or the host one (MXP_HOST_PACK=1, and
     // rule sets reading more than MXP_PACK_MAXCOL columns)
+    // The batch is checked (check_batch) before any host pass reads it: by the device packer right
+    // after it has queued the batch's H2D copies (from pinned caller memory the check overlaps them;
+    // no kernel reads the batch before the check has passed), else first.
     int pack(const mxp_bag_batch* b, mxp_dbatch* db) {
-        int rc = host_pack ? pack_on_host(b, db) : pack_device(b, db);
+        res_raw = false;
+        const bool dev = !host_pack && cols.size() + vcols.size() <= MXP_PACK_MAXCOL;
+        if (!dev)
+            if (int rc0 = check_batch(b)) return rc0;
+        int rc = dev ? pack_device(b, db) : pack_on_host(b, db);
         if (!rc) rc = pack_heads(db);
         if (!rc) rc = pack_dict(db);
         // the batch is complete when the call returns (evaluations run on the caller's streams)
@@ -691,7 +720,7 @@ struct mxp_engine : public mxp::LowerTables {
     DevBuf dp_ht[4], dp_desc[2], dp_blob[2], dp_tsec, dp_tnsec;
     uint32_t dp_mask[4] = {0, 0, 0, 0};
     // device packer scratch, reused across uploads
-    DevBuf pk_soff, pk_sbytes, pk_tsec, pk_tnsec, pk_moff, pk_mkey, pk_mval, pk_ck[64], pk_cv[64];
+    DevBuf pk_soff, pk_sbytes, pk_tsec, pk_tnsec, pk_moff, pk_mkey, pk_mval, pk_ck[66], pk_cv[66];  // (+2: resolver columns)
     DevBuf pk_sid, pk_braw, pk_bcan, pk_tid, pk_use, pk_maxlen, pk_tab[4], pk_scan, pk_scan_blocks, pk_scan_max;
     DevBuf pk_vtd_lkey, pk_vtd_lcr, pk_vtd_ln, pk_vtd_tkey, pk_vtd_tcr, pk_vtd_meta, pk_rx, pk_rxv;
     void* pk_host = nullptr;  // pinned read-back (longest string, value-class distinct counts)

@@ -90,7 +90,7 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     const uint32_t n = b->n_requests;
     const uint32_t C = (uint32_t)cols.size(), V = (uint32_t)vcols.size();
     const uint32_t ncol = C + V;
-    if (ncol > MXP_PACK_MAXCOL) return pack_on_host(b, db);  // (wider rule sets: the host packer)
+    if (ncol > MXP_PACK_MAXCOL) return pack_on_host(b, db);  // (wider rule sets: pack() checked the batch)
     int rc;
     if ((rc = ensure_dev_pools())) return rc;
     hipStream_t s = stream;
@@ -149,10 +149,36 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     uint32_t nup = 0;
     for (uint32_t c = 0; c < ncol; c++)
         if (src[c] >= 0 && slot_of[src[c]] < 0) slot_of[src[c]] = (int32_t)nup++;
+    // the resolver's identity and context.protocol columns as given (mxp_ns_kernel reads them with the
+    // raw batch strings): the first batch column of each name, uploaded with the rule columns
+    int32_t res_bc[2] = {-1, -1};
+    res_raw = false;
+    if (resolver.set) {
+        const std::string_view nm[2] = {resolver.identity, "context.protocol"};
+        for (int k = 0; k < 2; k++) {
+            auto it = bcol.find(nm[k]);
+            if (it == bcol.end()) continue;
+            res_bc[k] = (int32_t)it->second;
+            if (slot_of[it->second] < 0) slot_of[it->second] = (int32_t)nup++;
+        }
+    }
     for (uint32_t bc = 0; bc < b->n_columns; bc++) {
         if (slot_of[bc] < 0) continue;
         if ((rc = up(pk_ck[slot_of[bc]], b->kinds[bc], n, "upload kinds"))) return rc;
         if ((rc = up(pk_cv[slot_of[bc]], b->values[bc], (size_t)n * 8, "upload values"))) return rc;
+    }
+    if (resolver.set) {
+        res_id_kind = res_bc[0] >= 0 ? pk_ck[slot_of[res_bc[0]]].as<uint8_t>() : nullptr;
+        res_id_val = res_bc[0] >= 0 ? pk_cv[slot_of[res_bc[0]]].as<uint64_t>() : nullptr;
+        res_pr_kind = res_bc[1] >= 0 ? pk_ck[slot_of[res_bc[1]]].as<uint8_t>() : nullptr;
+        res_pr_val = res_bc[1] >= 0 ? pk_cv[slot_of[res_bc[1]]].as<uint64_t>() : nullptr;
+        res_raw = true;
+    }
+    // ---- the batch's ids and offsets, checked on the host while the copies run (from pinned caller
+    // memory they are DMA; pageable memory is staged by the runtime before hipMemcpyAsync returns)
+    if (int rc0 = check_batch(b)) {
+        (void)hipStreamSynchronize(s);  // (the copies still read the caller's arrays)
+        return rc0;
     }
     // ---- arguments
     mxp_pack_args A;

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pack_args.h"
 #include "resolve_args.h"
 
 namespace {
@@ -27,8 +28,10 @@ __device__ __forceinline__ uint32_t range_bits(uint32_t w, uint32_t lo, uint32_t
     return upto & ~((1u << a) - 1u);
 }
 
+// Pass 1 (count): the request's status, first erroring rule and number of selected rules (returned);
+// pass 2 (write): its selected rule ids at sel_off[q].
 template <bool kWrite>
-__device__ __forceinline__ void walk(const mxp_resolve_args& A, uint32_t q) {
+__device__ __forceinline__ uint32_t walk(const mxp_resolve_args& A, uint32_t q) {
     const uint32_t info = A.nsinfo[q];
     if (info == MXP_NS_MISSING || info == MXP_NS_NOTSTRING) {
         if (!kWrite) {
@@ -36,7 +39,17 @@ __device__ __forceinline__ void walk(const mxp_resolve_args& A, uint32_t q) {
             A.err_rule[q] = 0xFFFFFFFFu;
             A.count[q] = 0;
         }
-        return;
+        return 0;
+    }
+    // compact mode: the first applicable error in resolution order is known (error records)
+    if (!kWrite && A.err_in) {
+        const uint32_t er = A.err_in[q];
+        if (er != 0xFFFFFFFFu) {
+            A.status[q] = MXP_RESOLVE_PRED_ERROR;
+            A.err_rule[q] = er;
+            A.count[q] = 0;
+            return 0;
+        }
     }
     const uint32_t ns = info & 0x7FFFFFFFu;
     const uint32_t tcp = info >> 31;
@@ -63,18 +76,23 @@ __device__ __forceinline__ void walk(const mxp_resolve_args& A, uint32_t q) {
             if (!appl) continue;
             const uint64_t at = (uint64_t)w * A.n + q;
             const uint32_t em = A.empty[w];
-            const uint32_t err = A.err[at] & appl & ~em;
+            const uint32_t err = A.err ? (A.err[at] & appl & ~em) : 0u;
             if (err) {  // the first predicate error fails the request
                 if (!kWrite) {
                     A.status[q] = MXP_RESOLVE_PRED_ERROR;
                     A.err_rule[q] = w * 32u + __builtin_ctz(err);
                     A.count[q] = 0;
                 }
-                return;
+                return 0;
             }
             const uint32_t sel = (A.match[at] | em) & appl;
             if (kWrite) {
-                for (uint32_t b = sel; b; b &= b - 1) A.sel_rules[pos++] = w * 32u + __builtin_ctz(b);
+                if (A.ids16) {
+                    uint16_t* out = (uint16_t*)A.sel_rules;
+                    for (uint32_t b = sel; b; b &= b - 1) out[pos++] = (uint16_t)(w * 32u + __builtin_ctz(b));
+                } else {
+                    for (uint32_t b = sel; b; b &= b - 1) A.sel_rules[pos++] = w * 32u + __builtin_ctz(b);
+                }
             } else {
                 cnt += __builtin_popcount(sel);
             }
@@ -85,13 +103,101 @@ __device__ __forceinline__ void walk(const mxp_resolve_args& A, uint32_t q) {
         A.err_rule[q] = 0xFFFFFFFFu;
         A.count[q] = cnt;
     }
+    return cnt;
+}
+
+// sum of v over the 256-thread block (every thread gets it)
+__device__ __forceinline__ uint64_t block_sum256(uint64_t v) {
+    __shared__ uint64_t part[4];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if ((threadIdx.x & 63u) == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const uint64_t t = part[0] + part[1] + part[2] + part[3];
+    __syncthreads();
+    return t;
+}
+
+// exclusive prefix of v over the 256-thread block; *total = the block's sum
+__device__ __forceinline__ uint64_t block_excl256(uint64_t v, uint64_t* total) {
+    __shared__ uint64_t part[4];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    uint64_t x = v;  // inclusive scan within the wave
+#pragma unroll
+    for (uint32_t off = 1; off < 64u; off <<= 1) {
+        const uint64_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+    }
+    if (lane == 63u) part[wave] = x;
+    __syncthreads();
+    uint64_t before = 0;
+    for (uint32_t k = 0; k < wave; k++) before += part[k];
+    *total = part[0] + part[1] + part[2] + part[3];
+    __syncthreads();
+    return before + x - v;
+}
+
+// namespace name [p, p + n) -> id (MXP_NS_NONE when no rule namespace has it)
+__device__ __forceinline__ uint32_t ns_lookup(const mxp_ns_args& A, const uint8_t* p, uint32_t n) {
+    const uint64_t h = mxp_item_hash(p, n);
+    const uint32_t tag = (uint32_t)(h >> 32);
+    for (uint32_t slot = (uint32_t)h & A.ns_mask;; slot = (slot + 1u) & A.ns_mask) {
+        const unsigned long long t = A.ns_tab[slot];
+        if (!t) return MXP_NS_NONE;
+        if ((uint32_t)(t >> 32) != tag) continue;
+        const uint32_t id = (uint32_t)t - 1u;
+        const uint64_t d = A.ns_desc[id];
+        if ((uint32_t)(d & 0xFFFFFFu) != n) continue;
+        const uint8_t* e = A.ns_blob + (d >> 24);
+        bool eq = true;
+        for (uint32_t i = 0; i < n && eq; i++) eq = e[i] == p[i];
+        if (eq) return id;
+    }
 }
 
 }  // namespace
 
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count_kernel(mxp_resolve_args A) {
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
-    if (q < A.n) walk<false>(A, q);
+    const uint32_t c = q < A.n ? walk<false>(A, q) : 0u;
+    if (A.block_sum) {  // (uniform per launch)
+        const uint64_t t = block_sum256(c);
+        if (threadIdx.x == 0) A.block_sum[blockIdx.x] = t;
+    }
+}
+
+// exclusive scan of the count kernel's block sums, in place (one 1024-thread block; nb <= 1024 * 64)
+extern "C" __global__ __launch_bounds__(1024) void mxp_resolve_scan_blocks_kernel(uint64_t* bs, uint32_t nb) {
+    __shared__ uint64_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (nb + 1023u) / 1024u;
+    uint64_t sum = 0;
+    for (uint32_t i = t * per; i < min(nb, (t + 1) * per); i++) sum += bs[i];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024u; off <<= 1) {  // Hillis-Steele over the 1024 partial sums
+        const uint64_t y = t >= off ? part[t - off] : 0ull;
+        __syncthreads();
+        part[t] += y;
+        __syncthreads();
+    }
+    uint64_t run = part[t] - sum;  // exclusive
+    for (uint32_t i = t * per; i < min(nb, (t + 1) * per); i++) {
+        const uint64_t v = bs[i];
+        bs[i] = run;
+        run += v;
+    }
+}
+
+// sel_off[q] = block prefix + the block's own exclusive scan of the counts; sel_off[n] = the total
+extern "C" __global__ __launch_bounds__(256) void mxp_resolve_offsets_kernel(mxp_resolve_args A) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    const uint64_t c = q < A.n ? A.count[q] : 0u;
+    uint64_t total;
+    const uint64_t ex = block_excl256(c, &total);
+    const uint64_t base = A.block_sum[blockIdx.x];
+    if (q < A.n) A.sel_off_out[q] = base + ex;
+    if (blockIdx.x == gridDim.x - 1u && threadIdx.x == 0) A.sel_off_out[A.n] = base + total;
 }
 
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_write_kernel(mxp_resolve_args A) {
@@ -99,11 +205,71 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_write_kernel(mxp_r
     if (q < A.n && A.status[q] == MXP_RESOLVE_OK) walk<true>(A, q);
 }
 
+extern "C" __global__ __launch_bounds__(256) void mxp_ns_kernel(mxp_ns_args A) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (q >= A.n) return;
+    const uint32_t k = A.id_kind ? A.id_kind[q] : (uint32_t)MXP_ABSENT;
+    if (k == MXP_ABSENT) {
+        A.nsinfo[q] = MXP_NS_MISSING;
+        return;
+    }
+    if (k != MXP_STRING) {
+        A.nsinfo[q] = MXP_NS_NOTSTRING;
+        return;
+    }
+    // strings.SplitN(dest, ".", 3): ns = splits[1] when there is at least one '.', else ""
+    const uint64_t s = A.id_val[q];
+    const uint8_t* p = A.sbytes + A.soff[s];
+    const uint32_t n = (uint32_t)(A.soff[s + 1] - A.soff[s]);
+    uint32_t a = n, b = n;  // ns = p[a, b): "" without a '.'
+    for (uint32_t i = 0; i < n; i++)
+        if (p[i] == '.') {
+            a = i + 1u;
+            break;
+        }
+    for (uint32_t i = a; i < n; i++)
+        if (p[i] == '.') {
+            b = i;
+            break;
+        }
+    const uint32_t id = ns_lookup(A, p + a, b - a);
+    // tcp := attrs.Get("context.protocol") == "tcp" (an interface compare: a string "tcp" only)
+    bool tcp = false;
+    if (A.pr_kind && A.pr_kind[q] == MXP_STRING) {
+        const uint64_t t = A.pr_val[q];
+        const uint8_t* tp = A.sbytes + A.soff[t];
+        tcp = A.soff[t + 1] - A.soff[t] == 3u && tp[0] == 't' && tp[1] == 'c' && tp[2] == 'p';
+    }
+    A.nsinfo[q] = id | (tcp ? 0x80000000u : 0u);
+}
+
+// write: 0 count (+ block sums), 1 write, 2 the device scan of the counts into sel_off_out
 extern "C" hipError_t mxp_launch_resolve(const mxp_resolve_args* a, int write, hipStream_t s) {
     const uint32_t grid = (a->n + 255u) / 256u;
-    if (write)
+    if (write == 1) {
         hipLaunchKernelGGL(mxp_resolve_write_kernel, dim3(grid), dim3(256), 0, s, *a);
-    else
+    } else if (write == 2) {
+        hipLaunchKernelGGL(mxp_resolve_scan_blocks_kernel, dim3(1), dim3(1024), 0, s, a->block_sum, grid);
+        hipLaunchKernelGGL(mxp_resolve_offsets_kernel, dim3(grid), dim3(256), 0, s, *a);
+    } else {
         hipLaunchKernelGGL(mxp_resolve_count_kernel, dim3(grid), dim3(256), 0, s, *a);
+    }
+    return hipGetLastError();
+}
+
+extern "C" hipError_t mxp_launch_ns(const mxp_ns_args* a, hipStream_t s) {
+    hipLaunchKernelGGL(mxp_ns_kernel, dim3((a->n + 255u) / 256u), dim3(256), 0, s, *a);
+    return hipGetLastError();
+}
+
+// compact Resolve: err_in[q] = rule for each (q, rule) pair of the host's first-error pass
+extern "C" __global__ __launch_bounds__(256) void mxp_resolve_scatter_kernel(const uint32_t* pairs, uint32_t m,
+                                                                             uint32_t* err_in) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i < m) err_in[pairs[2u * i]] = pairs[2u * i + 1u];
+}
+
+extern "C" hipError_t mxp_launch_resolve_scatter(const uint32_t* pairs, uint32_t m, uint32_t* err_in, hipStream_t s) {
+    if (m) hipLaunchKernelGGL(mxp_resolve_scatter_kernel, dim3((m + 255u) / 256u), dim3(256), 0, s, pairs, m, err_in);
     return hipGetLastError();
 }

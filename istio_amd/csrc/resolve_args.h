@@ -9,6 +9,26 @@
 #define MXP_NS_MISSING 0xFFFFFFFFu   // identity attribute absent
 #define MXP_NS_NOTSTRING 0xFFFFFFFEu // identity attribute not a string
 
+// destAndNamespace (resolver.go:180-199) + the tcp flag of filterActions (:208) on the device, per
+// request, from the batch as uploaded (pack_device.cpp scratch: raw kinds / values of the identity
+// and context.protocol columns, raw batch strings) and the configuration's namespace names
+typedef struct mxp_ns_args {
+    uint32_t n;
+    uint32_t ns_mask;          // namespace table size - 1
+    const uint8_t* id_kind;    // [n] identity column (nullptr: absent from the batch)
+    const uint64_t* id_val;
+    const uint8_t* pr_kind;    // [n] context.protocol column (nullptr: absent)
+    const uint64_t* pr_val;
+    const uint64_t* soff;      // raw batch strings (offsets [ns + 1], bytes with 16 B of slack)
+    const uint8_t* sbytes;
+    const unsigned long long* ns_tab;  // open addressing: hash hi 32 << 32 | namespace id + 1 (0: empty)
+    const uint64_t* ns_desc;   // [namespaces] offset << 24 | length into ns_blob
+    const uint8_t* ns_blob;
+    uint32_t* nsinfo;          // [n] out: namespace id | tcp << 31, MXP_NS_NONE / MISSING / NOTSTRING
+} mxp_ns_args;
+
+#define MXP_RES_SCAN_TILE 256u  // requests per block of the count kernel's block sums
+
 typedef struct mxp_resolve_args {
     uint32_t n;                // requests
     uint32_t n_words;          // ceil(rules / 32)
@@ -26,4 +46,12 @@ typedef struct mxp_resolve_args {
     uint32_t* count;           // [n] selected rules
     const uint64_t* sel_off;   // [n + 1] exclusive scan of count (pass 2)
     uint32_t* sel_rules;       // selected rule ids, request by request, in resolution order
+    // compact mode (resolver.cpp): no error bitmap -- err_in[q] is the request's first applicable
+    // erroring rule in resolution order (~0: none), found from the error records; the count pass
+    // also writes per-block sums for the device scan of the counts into sel_off
+    const uint32_t* err_in;
+    uint64_t* block_sum;       // [ceil(n / MXP_RES_SCAN_TILE)]
+    uint64_t* sel_off_out;     // [n + 1] (scan pass)
+    uint32_t ids16;            // pass 2 writes u16 rule ids (sel_rules as uint16_t*)
+    uint32_t pad2;
 } mxp_resolve_args;

@@ -10,9 +10,12 @@
 #include <string_view>
 
 #include "engine_impl.h"
+#include "pack_args.h"
 #include "resolve_args.h"
 
 extern "C" hipError_t mxp_launch_resolve(const mxp_resolve_args* a, int write, hipStream_t s);
+extern "C" hipError_t mxp_launch_ns(const mxp_ns_args* a, hipStream_t s);
+extern "C" hipError_t mxp_launch_resolve_scatter(const uint32_t* pairs, uint32_t m, uint32_t* err_in, hipStream_t s);
 
 namespace {
 
@@ -104,6 +107,37 @@ int mxp_resolver_set(mxp_engine* eng, const char* identity_attr, const char* def
     auto d = R.ns_ids.find(R.default_ns);
     R.default_id = d == R.ns_ids.end() ? MXP_NS_NONE : d->second;
     R.set = true;
+    // the namespace names on the device (mxp_ns_kernel): content-hash table, descriptors, bytes
+    if (eng->device >= 0) {
+        hipError_t e;
+        if ((e = hipSetDevice(eng->device)) != hipSuccess) return eng->hipfail(e, "hipSetDevice");
+        uint32_t cap = 64;
+        while (cap < 2 * R.ns_names.size()) cap <<= 1;
+        std::vector<unsigned long long> tab(cap, 0ull);
+        std::vector<uint64_t> desc;
+        std::string blob;
+        for (uint32_t id = 0; id < R.ns_names.size(); id++) {
+            const std::string& nm = R.ns_names[id];
+            desc.push_back(((uint64_t)blob.size() << 24) | nm.size());
+            blob += nm;
+            const uint64_t h = mxp_item_hash((const uint8_t*)nm.data(), (uint32_t)nm.size());
+            uint32_t slot = (uint32_t)h & (cap - 1);
+            while (tab[slot]) slot = (slot + 1) & (cap - 1);
+            tab[slot] = ((h >> 32) << 32) | (id + 1ull);
+        }
+        blob.append(16, '\0');
+        desc.push_back(0);
+        auto put = [&](DevBuf& b, const void* src, size_t bytes) -> int {
+            if ((e = b.alloc(bytes)) != hipSuccess || (e = hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice)) != hipSuccess)
+                return eng->hipfail(e, "resolver namespaces");
+            return MXP_OK;
+        };
+        int rc;
+        if ((rc = put(eng->res_ns_tab, tab.data(), tab.size() * 8)) || (rc = put(eng->res_ns_desc, desc.data(), desc.size() * 8)) ||
+            (rc = put(eng->res_ns_blob, blob.data(), blob.size())))
+            return rc;
+        eng->res_ns_mask = cap - 1;
+    }
     eng->resolver = std::move(R);
     return MXP_OK;
 }
@@ -112,10 +146,59 @@ int mxp_resolver_set(mxp_engine* eng, const char* identity_attr, const char* def
 
 namespace {
 
-// mxp_resolve_batch, and with ref_off its referenced attributes (mxp_resolve_refs)
-int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status, uint32_t* err_rule,
-                 uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap, uint64_t* ref_off, mxp_attr_ref* refs,
-                 uint64_t ref_cap) {
+// MXP_DEBUG_FLAGS: resolve through the error bitmap (the pre-round-5 path), for A/B and tests
+constexpr uint32_t kResolveBitmap = 1u << 28;
+
+// Each request's first applicable erroring rule in resolution order (filterActions returns at the
+// first EvalPredicate error, resolver.go:226-228) from the error records of a compact evaluation:
+// (request, rule) pairs for the requests that fail.  hinfo: the requests' namespace info.
+void first_errors(mxp_engine* eng, uint32_t n, uint32_t variety, const uint32_t* hinfo, std::vector<uint32_t>* pairs) {
+    const auto& R = eng->resolver;
+    std::vector<uint32_t>& best = eng->res_best;  // (kept all ~0 between calls)
+    if (best.size() < n) best.assign(n, 0xFFFFFFFFu);
+    const bool has_def = R.default_id != MXP_NS_NONE;
+    const uint32_t dlo = has_def ? R.ns_lo[R.default_id] : 0u, dhi = has_def ? R.ns_hi[R.default_id] : 0u;
+    const uint32_t dlen = dhi - dlo;
+    std::vector<uint32_t> touched;
+    for (const mxp_err_rec& rec : eng->last_recs) {
+        const uint32_t q = rec.req, r = rec.rule;
+        if (q >= n || r >= R.vmask.size()) continue;
+        const uint32_t info = hinfo[q];
+        if (info == MXP_NS_MISSING || info == MXP_NS_NOTSTRING) continue;
+        const uint32_t tcp = info >> 31, ns = info & 0x7FFFFFFFu;
+        if (R.empty[r] || !((R.vmask[r] >> variety) & 1u) || R.tcp[r] != tcp) continue;
+        uint32_t rank;
+        if (has_def && r >= dlo && r < dhi) {
+            rank = r - dlo;
+        } else if (ns != MXP_NS_NONE && ns != R.default_id && r >= R.ns_lo[ns] && r < R.ns_hi[ns]) {
+            rank = dlen + (r - R.ns_lo[ns]);
+        } else {
+            continue;
+        }
+        if (best[q] == 0xFFFFFFFFu) touched.push_back(q);
+        if (rank < best[q]) best[q] = rank;
+    }
+    pairs->clear();
+    pairs->reserve(2 * touched.size());
+    for (uint32_t q : touched) {
+        const uint32_t rank = best[q];
+        const uint32_t ns = hinfo[q] & 0x7FFFFFFFu;
+        pairs->push_back(q);
+        pairs->push_back(rank < dlen ? dlo + rank : R.ns_lo[ns] + (rank - dlen));
+        best[q] = 0xFFFFFFFFu;
+    }
+}
+
+// mxp_resolve_batch(_ex), and with ref_off its referenced attributes (mxp_resolve_refs).
+//
+// Compact path (round 5; not for referenced attributes): the evaluation writes the match bitmap and
+// per-request error flags with error records instead of the error bitmap; namespaces come from the
+// device (mxp_ns_kernel on the batch as uploaded); each failing request's first applicable error is
+// found from the records on the host and scattered to the device; the counts are scanned on the
+// device.  Records past the log's capacity fall back to the error bitmap.
+int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, bool ids16, uint8_t* status,
+                 uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap, uint64_t* ref_off,
+                 mxp_attr_ref* refs, uint64_t ref_cap) {
     if (!eng || !batch || !status || !err_rule || !sel_off || (sel_cap && !sel_rules) || variety >= 32)
         return MXP_ERR_ARG;
     if (!eng->resolver.set) return eng->fail(MXP_ERR_STATE, "resolver not configured (mxp_resolver_set)");
@@ -123,11 +206,20 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     const uint32_t n = batch->n_requests;
     const uint32_t NR = (uint32_t)eng->rules.size();
     const uint32_t W = (NR + 31) / 32;
+    if (ids16 && NR > 65536u) return eng->fail(MXP_ERR_ARG, "u16 rule ids: more than 65536 rules");
     std::unique_ptr<mxp_dbatch> db;
     DevBuf& dm = eng->res_dm;  // (engine-owned scratch: no allocation per call once large enough)
     DevBuf& de = eng->res_de;
     std::vector<mxp_ref_rec> recs;
-    int rc = ref_off ? eng->refs_evaluate(batch, dm, de, db, recs) : eng->evaluate(batch, dm, de, nullptr, db);
+    hipError_t e;
+    int rc;
+    const bool compact = !ref_off && !(eng->debug_flags & kResolveBitmap);
+    if (compact) {
+        if (eng->device >= 0 && (e = eng->res_flags.reserve(n ? n : 1)) != hipSuccess) return eng->hipfail(e, "alloc flags");
+        rc = eng->evaluate(batch, dm, de, nullptr, db, eng->res_flags.as<uint8_t>());
+    } else {
+        rc = ref_off ? eng->refs_evaluate(batch, dm, de, db, recs) : eng->evaluate(batch, dm, de, nullptr, db);
+    }
     if (rc) return rc;
     // per-word masks: applicability for the variety (per request tcp flag), empty matches
     std::vector<uint32_t> amask(2 * (size_t)W, 0), empty(W, 0);
@@ -136,10 +228,6 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         if ((R.vmask[r] >> variety) & 1u) amask[(size_t)R.tcp[r] * W + r / 32] |= bit;
         if (R.empty[r]) empty[r / 32] |= bit;
     }
-    std::vector<uint32_t> info;
-    request_info(eng, batch, &info);
-    eng->trace_mark("request namespaces (host)");
-    hipError_t e;
     DevBuf &d_info = eng->res_info, &d_lo = eng->res_lo, &d_hi = eng->res_hi, &d_amask = eng->res_amask,
            &d_empty = eng->res_empty, &d_status = eng->res_status, &d_err_rule = eng->res_err_rule,
            &d_count = eng->res_count, &d_off = eng->res_off, &d_sel = eng->res_sel;
@@ -149,7 +237,48 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
             return eng->hipfail(e, what);
         return MXP_OK;
     };
-    if ((rc = up(d_info, info.data(), info.size() * 4, "upload nsinfo"))) return rc;
+    // request namespaces: on the device from the batch as uploaded (pack_device), else on the host
+    std::vector<uint32_t> info;  // host copy (host pass; referenced attributes)
+    const uint32_t* hinfo = nullptr;
+    if (eng->res_raw && !ref_off) {
+        if ((e = d_info.reserve((size_t)n * 4 + 4)) != hipSuccess) return eng->hipfail(e, "alloc nsinfo");
+        mxp_ns_args N;
+        memset(&N, 0, sizeof N);
+        N.n = n;
+        N.ns_mask = eng->res_ns_mask;
+        N.id_kind = eng->res_id_kind;
+        N.id_val = eng->res_id_val;
+        N.pr_kind = eng->res_pr_kind;
+        N.pr_val = eng->res_pr_val;
+        N.soff = eng->pk_soff.as<uint64_t>();
+        N.sbytes = eng->pk_sbytes.as<uint8_t>();
+        N.ns_tab = eng->res_ns_tab.as<unsigned long long>();
+        N.ns_desc = eng->res_ns_desc.as<uint64_t>();
+        N.ns_blob = eng->res_ns_blob.as<uint8_t>();
+        N.nsinfo = d_info.as<uint32_t>();
+        if (n && (e = mxp_launch_ns(&N, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch namespaces");
+        if (n) {  // (the first-error pass reads it; the copy rides behind the evaluation)
+            if (eng->res_hinfo_cap < (size_t)n * 4) {
+                if (eng->res_hinfo) (void)hipHostFree(eng->res_hinfo);
+                eng->res_hinfo = nullptr;
+                eng->res_hinfo_cap = 0;
+                if ((e = hipHostMalloc(&eng->res_hinfo, (size_t)n * 4, hipHostMallocDefault)) != hipSuccess) {
+                    eng->res_hinfo = nullptr;
+                    return eng->hipfail(e, "pinned nsinfo");
+                }
+                eng->res_hinfo_cap = (size_t)n * 4;
+            }
+            if ((e = hipMemcpyAsync(eng->res_hinfo, d_info.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
+                return eng->hipfail(e, "download nsinfo");
+            hinfo = (const uint32_t*)eng->res_hinfo;
+        }
+        eng->trace_mark("request namespaces (device)");
+    } else {
+        request_info(eng, batch, &info);
+        hinfo = info.data();
+        eng->trace_mark("request namespaces (host)");
+        if ((rc = up(d_info, info.data(), info.size() * 4, "upload nsinfo"))) return rc;
+    }
     if ((rc = up(d_lo, R.ns_lo.data(), R.ns_lo.size() * 4, "upload ns_lo"))) return rc;
     if ((rc = up(d_hi, R.ns_hi.data(), R.ns_hi.size() * 4, "upload ns_hi"))) return rc;
     if ((rc = up(d_amask, amask.data(), amask.size() * 4, "upload amask"))) return rc;
@@ -157,6 +286,9 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     if ((e = d_status.reserve(n)) != hipSuccess) return eng->hipfail(e, "alloc status");
     if ((e = d_err_rule.reserve((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err_rule");
     if ((e = d_count.reserve((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc count");
+    const uint32_t grid = (n + 255u) / 256u;
+    if ((e = eng->res_bsum.reserve((size_t)grid * 8 + 8)) != hipSuccess) return eng->hipfail(e, "alloc block sums");
+    if ((e = d_off.reserve(((size_t)n + 1) * 8)) != hipSuccess) return eng->hipfail(e, "alloc sel_off");
     mxp_resolve_args A;
     memset(&A, 0, sizeof A);
     A.n = n;
@@ -168,38 +300,66 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     A.amask = d_amask.as<uint32_t>();
     A.empty = d_empty.as<uint32_t>();
     A.match = dm.as<uint32_t>();
-    A.err = de.as<uint32_t>();
+    A.err = compact ? nullptr : de.as<uint32_t>();
     A.status = d_status.as<uint8_t>();
     A.err_rule = d_err_rule.as<uint32_t>();
     A.count = d_count.as<uint32_t>();
+    A.block_sum = eng->res_bsum.as<uint64_t>();
+    A.sel_off_out = d_off.as<uint64_t>();
+    A.sel_off = d_off.as<uint64_t>();
+    A.ids16 = ids16 ? 1u : 0u;
+    if (compact) {
+        // the error records (synchronises the stream: the namespace copy has landed too)
+        if ((rc = eng->collect_errors(batch, db))) return rc;
+        eng->trace_mark("error records");
+        if (!eng->errors_complete) {
+            // records past the log's capacity: the error bitmap after all (an evaluation without a log)
+            if ((e = de.reserve((size_t)W * n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err");
+            if ((rc = eng->launch(eng->last_db.get(), eng->stream, dm.as<uint32_t>(), de.as<uint32_t>(), nullptr, false)))
+                return rc;
+            A.err = de.as<uint32_t>();
+        } else {
+            std::vector<uint32_t> pairs;
+            first_errors(eng, n, variety, hinfo, &pairs);
+            if ((e = eng->res_err_in.reserve((size_t)n * 4 + 4)) != hipSuccess) return eng->hipfail(e, "alloc err_in");
+            if (n && (e = hipMemsetAsync(eng->res_err_in.p, 0xFF, (size_t)n * 4, eng->stream)) != hipSuccess)
+                return eng->hipfail(e, "reset err_in");
+            if ((rc = up(eng->res_pairs, pairs.data(), pairs.size() * 4, "upload first errors"))) return rc;
+            if ((e = mxp_launch_resolve_scatter(eng->res_pairs.as<uint32_t>(), (uint32_t)(pairs.size() / 2),
+                                                eng->res_err_in.as<uint32_t>(), eng->stream)) != hipSuccess)
+                return eng->hipfail(e, "launch first errors");
+            A.err_in = eng->res_err_in.as<uint32_t>();
+            eng->trace_mark("first errors (host pass + scatter)");
+        }
+    }
     if (n && (e = mxp_launch_resolve(&A, 0, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve");
-    std::vector<uint32_t> count(n);
-    if (n && (e = hipMemcpyAsync(count.data(), d_count.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-        return eng->hipfail(e, "download count");
-    if (n && (e = hipMemcpyAsync(status, d_status.p, n, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-        return eng->hipfail(e, "download status");
-    if (n && (e = hipMemcpyAsync(err_rule, d_err_rule.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-        return eng->hipfail(e, "download err_rule");
-    eng->trace_mark("resolve kernel + downloads");
-    if ((rc = eng->collect_errors(batch, db))) return rc;  // synchronises the stream
-    eng->trace_mark("error records");
+    if (n && (e = mxp_launch_resolve(&A, 2, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve scan");
+    if (!n) {
+        sel_off[0] = 0;
+    } else {
+        if ((rc = eng->download(status, d_status.p, n, "download status"))) return rc;
+        if ((rc = eng->download(err_rule, d_err_rule.p, (size_t)n * 4, "download err_rule"))) return rc;
+        if ((rc = eng->download(sel_off, d_off.p, ((size_t)n + 1) * 8, "download sel_off"))) return rc;
+    }
+    eng->trace_mark("resolve kernels + downloads");
+    if (!compact) {
+        if ((rc = eng->collect_errors(batch, db))) return rc;  // synchronises the stream
+        eng->trace_mark("error records");
+    }
     int ref_rc = MXP_OK;
     if (ref_off) {
         const mxp_engine::RefScope scope{&info, status, err_rule, variety};
         ref_rc = eng->refs_assemble(batch, recs, &scope, ref_off, refs, ref_cap);
         if (ref_rc && ref_rc != MXP_ERR_NOMEM) return ref_rc;
     }
-    sel_off[0] = 0;
-    for (uint32_t q = 0; q < n; q++) sel_off[q + 1] = sel_off[q] + count[q];
     const uint64_t total = sel_off[n];
     if (total > sel_cap) return MXP_ERR_NOMEM;
     if (total) {
-        if ((rc = up(d_off, sel_off, ((size_t)n + 1) * 8, "upload sel_off"))) return rc;
-        if ((e = d_sel.reserve(total * 4)) != hipSuccess) return eng->hipfail(e, "alloc sel");
-        A.sel_off = d_off.as<uint64_t>();
+        const size_t isz = ids16 ? 2 : 4;
+        if ((e = d_sel.reserve(total * isz)) != hipSuccess) return eng->hipfail(e, "alloc sel");
         A.sel_rules = d_sel.as<uint32_t>();
         if ((e = mxp_launch_resolve(&A, 1, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
-        if ((rc = eng->download(sel_rules, d_sel.p, total * 4, "download sel"))) return rc;
+        if ((rc = eng->download(sel_rules, d_sel.p, total * isz, "download sel"))) return rc;
     }
     eng->trace_mark("action lists (gather + download)");
     return ref_rc;
@@ -211,14 +371,22 @@ extern "C" {
 
 int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
                       uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap) {
-    return resolve_impl(eng, batch, variety, status, err_rule, sel_off, sel_rules, sel_cap, nullptr, nullptr, 0);
+    return resolve_impl(eng, batch, variety, false, status, err_rule, sel_off, sel_rules, sel_cap, nullptr, nullptr, 0);
+}
+
+int mxp_resolve_batch_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
+                         uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap) {
+    if (flags & ~(uint32_t)MXP_RESOLVE_IDS_U16) return MXP_ERR_ARG;
+    return resolve_impl(eng, batch, variety, (flags & MXP_RESOLVE_IDS_U16) != 0, status, err_rule, sel_off, sel_rules,
+                        sel_cap, nullptr, nullptr, 0);
 }
 
 int mxp_resolve_refs(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,
                      uint32_t* err_rule, uint64_t* sel_off, uint32_t* sel_rules, uint64_t sel_cap, uint64_t* ref_off,
                      mxp_attr_ref* refs, uint64_t ref_cap) {
     if (!ref_off) return MXP_ERR_ARG;
-    return resolve_impl(eng, batch, variety, status, err_rule, sel_off, sel_rules, sel_cap, ref_off, refs, ref_cap);
+    return resolve_impl(eng, batch, variety, false, status, err_rule, sel_off, sel_rules, sel_cap, ref_off, refs,
+                        ref_cap);
 }
 
 }  // extern "C"

@@ -71,6 +71,8 @@ SIGNATURES = {
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     "mxp_resolve_batch": (ctypes.c_int, [_VP, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
+    "mxp_resolve_batch_ex": (ctypes.c_int, [_VP, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
     "mxp_list_create": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.POINTER(_VP)]),
     "mxp_list_destroy": (None, [_VP, _VP]),
@@ -98,6 +100,8 @@ SIGNATURES = {
     "mxp_ruleset_columns": (ctypes.c_uint32, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32]),
     "mxp_debug_wave_times": (ctypes.c_int, [_VP, _VP, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "mxp_debug_bin": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_uint64)]),
+    "mxp_host_alloc": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_VP)]),
+    "mxp_host_free": (None, [_VP]),
     "mxp_go_to_upper": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, _VP, ctypes.c_uint64,
                                        ctypes.POINTER(ctypes.c_uint64)]),
 }
@@ -126,6 +130,55 @@ def load_library(path: str = LIB_PATH):
             f.argtypes = args
         _LIB = lib
     return _LIB
+
+
+class PinnedArena:
+    """Page-locked host memory from mxp_host_alloc, handed out as numpy arrays (the arrays of a batch
+    a binding packs bags into: DMA to the device at the link's rate).  Freed with the arena."""
+
+    def __init__(self, nbytes: int):
+        self.lib = load_library()
+        self.p = _VP()
+        if self.lib.mxp_host_alloc(max(int(nbytes), 16), ctypes.byref(self.p)) != 0:
+            raise MxpError("mxp_host_alloc(%d) failed" % nbytes)
+        self.size, self.used = max(int(nbytes), 16), 0
+
+    def array(self, like: np.ndarray) -> np.ndarray:
+        """A pinned copy of `like` (same dtype and shape), 64-byte aligned within the arena."""
+        nb = like.nbytes
+        at = (self.used + 63) & ~63
+        if at + nb > self.size:
+            raise MxpError("pinned arena full")
+        self.used = at + nb
+        buf = (ctypes.c_uint8 * max(nb, 1)).from_address(self.p.value + at)
+        out = np.frombuffer(buf, dtype=like.dtype, count=like.size).reshape(like.shape)
+        out[...] = like
+        return out
+
+    def free(self):
+        if self.p:
+            self.lib.mxp_host_free(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def pinned_batch(batch: BagBatch):
+    """(a copy of `batch` whose arrays live in pinned memory, the arena that holds them)."""
+    arrays = list(batch.kinds) + list(batch.values) + [batch.str_blob, batch.str_offsets, batch.time_sec,
+                                                       batch.time_nsec, batch.map_offsets, batch.map_keys,
+                                                       batch.map_values]
+    arena = PinnedArena(sum(a.nbytes + 64 for a in arrays) + 64)
+    nc = len(batch.kinds)
+    p = [arena.array(a) for a in arrays]
+    out = BagBatch(batch.n, batch.names, p[:nc], p[nc:2 * nc], *p[2 * nc:])
+    for a, b in zip(out.kinds + out.values, p[:2 * nc]):
+        assert a.ctypes.data == b.ctypes.data  # (no copy made by the constructor)
+    return out, arena
 
 
 def go_to_upper(s: bytes) -> bytes:
@@ -419,18 +472,24 @@ class Engine:
         self._check(self.lib.mxp_resolver_set(self.h, identity_attr.encode(), default_ns.encode(), ns,
                                               vm.ctypes.data, tcp.ctypes.data, em.ctypes.data, n), "mxp_resolver_set")
 
-    def resolve_arrays(self, batch: BagBatch, variety: int, cap: int = 0):
+    def resolve_arrays(self, batch: BagBatch, variety: int, cap: int = 0, ids16: bool = False):
         """mxp_resolve_batch -> (status u8[n], err_rule u32[n], sel_off u64[n + 1], sel_rules u32[...]):
-        request q's selected rules are sel_rules[sel_off[q]:sel_off[q + 1]], in resolution order."""
+        request q's selected rules are sel_rules[sel_off[q]:sel_off[q + 1]], in resolution order.
+        ids16: mxp_resolve_batch_ex with MXP_RESOLVE_IDS_U16 (sel_rules u16)."""
         n = batch.n
         status = np.empty(n, dtype=np.uint8)
         err_rule = np.empty(n, dtype=np.uint32)
         off = np.empty(n + 1, dtype=np.uint64)
         cap = cap or max(16, n * 4)
         for _ in range(2):
-            sel = np.empty(cap, dtype=np.uint32)
-            rc = self.lib.mxp_resolve_batch(self.h, ctypes.byref(batch.c_struct()), variety, status.ctypes.data,
-                                             err_rule.ctypes.data, off.ctypes.data, sel.ctypes.data, cap)
+            sel = np.empty(cap, dtype=np.uint16 if ids16 else np.uint32)
+            if ids16:
+                rc = self.lib.mxp_resolve_batch_ex(self.h, ctypes.byref(batch.c_struct()), variety, 1,
+                                                   status.ctypes.data, err_rule.ctypes.data, off.ctypes.data,
+                                                   sel.ctypes.data, cap)
+            else:
+                rc = self.lib.mxp_resolve_batch(self.h, ctypes.byref(batch.c_struct()), variety, status.ctypes.data,
+                                                 err_rule.ctypes.data, off.ctypes.data, sel.ctypes.data, cap)
             if rc == 4:  # MXP_ERR_NOMEM: retry with the exact size
                 cap = int(off[n])
                 continue
@@ -438,10 +497,10 @@ class Engine:
             break
         return status, err_rule, off, sel[:int(off[n])]
 
-    def resolve(self, batch: BagBatch, variety: int):
+    def resolve(self, batch: BagBatch, variety: int, ids16: bool = False):
         """Resolve every request (mxp_resolve_batch) -> (status u8[n], err_rule u32[n], selected:
         list of per-request rule-id arrays in resolution order)."""
-        status, err_rule, off, sel = self.resolve_arrays(batch, variety)
+        status, err_rule, off, sel = self.resolve_arrays(batch, variety, ids16=ids16)
         return status, err_rule, [sel[int(off[q]):int(off[q + 1])] for q in range(batch.n)]
 
     # ------------------------------------------------------------------ list adapter

@@ -48,8 +48,18 @@ def test_reference_resolver_table_on_gpu(mxp, case):
     assert sum(lengths[int(r)] for r in sel[0]) == case["nactions"]
 
 
-@pytest.mark.parametrize("seed", [21, 22])
-def test_resolver_random_parity(mxp, seed):
+# resolution paths: compact (default: error flags + records, device namespaces and scan), the error
+# bitmap (MXP_DEBUG_FLAGS bit 28), records past a tiny log (the compact path falls back to the bitmap),
+# the host packer (host namespaces), u16 rule ids (mxp_resolve_batch_ex)
+MODES = {"compact": {}, "bitmap": {"MXP_DEBUG_FLAGS": "268435456"}, "errcap": {"MXP_ERRCAP": "16"},
+         "hostpack": {"MXP_HOST_PACK": "1"}, "u16": {}}
+
+
+@pytest.mark.parametrize("seed,mode", [(21, "compact"), (22, "compact"), (21, "bitmap"), (22, "errcap"),
+                                       (21, "hostpack"), (22, "u16")])
+def test_resolver_random_parity(mxp, monkeypatch, seed, mode):
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
     manifest, rules, conf, batch = W.resolver_workload(n_rules=600, n_requests=3000, seed=seed)
     eng = mxp.Engine(0)
     eng.set_vocabulary(manifest)
@@ -60,7 +70,7 @@ def test_resolver_random_parity(mxp, seed):
     codes = oracle.oracle_matrix(ev, rules, batch, threads=16)
     seen = set()
     for variety in (0, 2, 3):
-        status, err_rule, sel = eng.resolve(batch, variety)
+        status, err_rule, sel = eng.resolve(batch, variety, ids16=mode == "u16")
         want = oracle_resolver.resolve(batch, codes, conf["rule_ns"], conf["variety_mask"], conf["is_tcp"],
                                        conf["empty_match"], conf["identity_attr"], conf["default_ns"], variety)
         for q, (ws, we, wsel) in enumerate(want):
@@ -109,3 +119,39 @@ def test_resolver_referenced_parity(mxp, seed):
                    for x in oracle_resolver.resolve_referenced(ev, rules, batch, q, w[3])]
             assert mxp.fakebag_list(refs[q]) == exp, (q, variety, sorted(set(mxp.fakebag_list(refs[q])) ^ set(exp)))
             assert mxp.protobag_set(refs[q]) == expected_protobag(batch, q, exp)
+
+
+def test_resolver_compact_matches_bitmap_value_classes(mxp, monkeypatch):
+    """C4 routes and header rules (value-class columns; missing headers give class error records that
+    the compact path expands per request): the compact Resolve equals the error-bitmap Resolve, with
+    the rules spread over three namespaces and mixed varieties / TCP flags."""
+    manifest, rules, batch = W.c4_workload(n_rules=1200, n_requests=20000, seed=31)
+    manifest = dict(manifest, **{"context.protocol": "STRING"})
+    R = len(rules)
+    rng = np.random.default_rng(5)
+    counts = rng.multinomial(R, [0.5, 0.3, 0.2])
+    rule_ns = ["istio-system"] * counts[0] + ["default"] * counts[1] + ["other"] * counts[2]
+    vm = rng.integers(0, 8, size=R).astype(np.uint32)
+    tcp = (rng.random(R) < 0.1).astype(np.uint8)
+    empty = (rng.random(R) < 0.02).astype(np.uint8)
+    out = {}
+    for mode in ("compact", "bitmap", "u16"):
+        monkeypatch.setenv("MXP_DEBUG_FLAGS", MODES.get(mode, {}).get("MXP_DEBUG_FLAGS", "0"))
+        eng = mxp.Engine(0)
+        eng.set_vocabulary(manifest)
+        assert (eng.compile(rules) == 0).all()
+        eng.set_resolver("destination.service", "istio-system", rule_ns, vm, tcp, empty)
+        res = []
+        for variety in (0, 1, 2):
+            st, er, off, sel = eng.resolve_arrays(batch, variety, ids16=mode == "u16")
+            res.append((st, er, off, sel.astype(np.uint32)))
+            if mode == "compact":  # every failing request's text is there
+                for q in np.nonzero(st == 3)[0][:50]:
+                    assert eng.pair_error(int(q), int(er[q]))
+        out[mode] = res
+        eng.close()
+    for mode in ("bitmap", "u16"):
+        for (a, b) in zip(out["compact"], out[mode]):
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y), mode
+    assert any((r[0] == 3).any() for r in out["compact"]) and any((r[0] == 0).any() for r in out["compact"])
