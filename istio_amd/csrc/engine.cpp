@@ -2048,9 +2048,12 @@ std::string mxp_engine::packed_value_text(const mxp_dbatch* db, uint32_t kind, u
         return mxp::go_format_bytes((const uint8_t*)c.data(), c.size());
     }
     case MXP_STRING_MAP: {
+        if (v < snap_maps.size()) return snap_maps[v];
         uint32_t mo[2] = {0, 0};
         std::string out = "map[";
-        if (!db || hipMemcpy(mo, db->map_off.as<uint32_t>() + v, 8, hipMemcpyDeviceToHost) != hipSuccess) return out + "]";
+        if (!db || db->map_off.n < (v + 2) * 4 ||
+            hipMemcpy(mo, db->map_off.as<uint32_t>() + v, 8, hipMemcpyDeviceToHost) != hipSuccess)
+            return out + "]";
         std::vector<uint32_t> k(mo[1] - mo[0]), w(mo[1] - mo[0]);
         if (!k.empty() &&
             (hipMemcpy(k.data(), db->map_keys.as<uint32_t>() + mo[0], k.size() * 4, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -2743,6 +2746,24 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
     if (cnt[2]) {
         int rc = expand_class_errors(batch, db.get(), cnt[2], errcap > kept ? errcap - kept : 0u);
         if (rc) return rc;
+    }
+    // records past the log are recomputed after the caller's batch is gone: keep its map texts when
+    // the device batch has no map contents to print them from
+    const uint32_t NM = batch->n_maps;
+    if (!errors_complete && NM && db && db->map_off.n < ((size_t)NM + 1) * 4) {
+        snap_maps.resize(NM);
+        auto bs = [&](uint64_t sid) {
+            return std::string((const char*)batch->str_bytes + batch->str_offsets[sid],
+                               (size_t)(batch->str_offsets[sid + 1] - batch->str_offsets[sid]));
+        };
+        mxp::par_for(NM, 4096, [&](uint64_t m0, uint64_t m1, unsigned) {
+            for (uint64_t m = m0; m < m1; m++) {
+                std::string t = "map[";
+                for (uint64_t x = batch->map_offsets[m]; x < batch->map_offsets[m + 1]; x++)
+                    t += (x != batch->map_offsets[m] ? " " : "") + bs(batch->map_keys[x]) + ":" + bs(batch->map_values[x]);
+                snap_maps[m] = t + "]";
+            }
+        });
     }
     last_db = std::move(db);
     return MXP_OK;

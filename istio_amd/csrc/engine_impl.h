@@ -473,7 +473,12 @@ struct mxp_engine : public mxp::LowerTables {
     std::vector<std::string> last_rec_texts;
     std::unordered_map<uint64_t, uint32_t> rec_index;  // key -> record (built on first use)
     bool rec_indexed = false;
+    // map texts of the last batch ("map[k:v ...]" per map id, the caller's order), kept when its error
+    // records overflowed the log and the device batch holds no map contents: a recomputed window's
+    // conversion error prints the map after the caller's batch is gone
+    std::vector<std::string> snap_maps;
     void clear_errors() {
+        snap_maps.clear();
         last_errors.clear();
         last_recs.clear();
         last_rec_text.clear();

@@ -150,6 +150,13 @@ void merge(std::vector<std::pair<T, T>>& v) {
     v.swap(o);
 }
 
+// IP lists: address families in waves of their own (mxp_list_ip_kernel); MXP_LIST_IP_SPLIT=0: the
+// one-lookup-per-lane kernel (A/B)
+uint32_t ip_split() {
+    const char* e = getenv("MXP_LIST_IP_SPLIT");
+    return (uint32_t)(e ? atoi(e) != 0 : 1);
+}
+
 void set_lds(mxp_list_args& A, const mxp_list* L) {
     A.lds_nparts = L->lds_nparts;
     A.lds_plan = L->lds_plan.as<uint32_t>();
@@ -187,6 +194,10 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
         };
         for (uint32_t i = 0; i < n_entries; i++) add(str(entries[i], entry_lens[i]));
         for (uint32_t i = 0; i < n_overrides; i++) add(str(overrides[i], override_lens[i]));
+        std::vector<uint64_t> desc;
+        std::string pool;
+        if (!string_pool(uniq, &desc, &pool)) return eng->fail(MXP_ERR_ARG, "list entry longer than 16 MiB");
+        if (pool.size() / 8 >= 0xFFFFFFFFull) return eng->fail(MXP_ERR_ARG, "list entries exceed 32 GiB");
         uint32_t cap = 2;
         while (cap < 2 * uniq.size()) cap <<= 1;
         std::vector<uint64_t> tab(cap, MXP_LIST_EMPTY);
@@ -194,11 +205,9 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             const uint64_t h = host_hash(uniq[i], false);  // entries are already upper-cased
             uint32_t s = (uint32_t)h & (cap - 1);
             while (tab[s] != MXP_LIST_EMPTY) s = (s + 1) & (cap - 1);
-            tab[s] = (h >> 32) << 32 | i;
+            const size_t len = uniq[i].size();
+            tab[s] = len < MXP_LIST_LONG ? MXP_LIST_SLOT(h, len, (desc[i] >> 24) / 8) : MXP_LIST_SLOT(h, MXP_LIST_LONG, i);
         }
-        std::vector<uint64_t> desc;
-        std::string pool;
-        if (!string_pool(uniq, &desc, &pool)) return eng->fail(MXP_ERR_ARG, "list entry longer than 16 MiB");
         L->n_entries = uniq.size();
         L->hmask = cap - 1;
         if ((rc = put(L->htab, tab.data(), tab.size() * 8, "upload list table"))) return rc;
@@ -392,6 +401,7 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, con
     A.n6 = L->n6;
     A.rx_n = L->rx_n;
     A.rx_nfa = L->rx_nfa;
+    A.ip_split = ip_split();
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes;
@@ -440,6 +450,7 @@ int mxp_listentry_check(mxp_engine* eng, const mxp_list* L, int blacklist, const
     A.n6 = L->n6;
     A.rx_n = L->rx_n;
     A.rx_nfa = L->rx_nfa;
+    A.ip_split = ip_split();
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes.as<int32_t>();

@@ -7,8 +7,13 @@
 #include "dfa_dev.h"
 #include "netparse.h"
 
-// string hash table slot: hash32 << 32 | entry index; empty slot = ~0
+// string hash table slot: hash tag (the hash's top 20 bits) << 44 | entry length << 32 | entry pool
+// offset / 8, so a probe reads the entry's bytes with no descriptor load in between; an entry of
+// MXP_LIST_LONG bytes or more keeps length MXP_LIST_LONG in the slot and its index into ent_desc in
+// the low word.  Empty slot = ~0 (no real slot: lengths stop at MXP_LIST_LONG).
 #define MXP_LIST_EMPTY 0xFFFFFFFFFFFFFFFFull
+#define MXP_LIST_LONG 0xFFEu
+#define MXP_LIST_SLOT(h, len, low) (((uint64_t)(h) >> 44) << 44 | (uint64_t)(len) << 32 | (uint64_t)(low))
 
 // LDS staging of regex-list DFAs: transition words per workgroup (60 KB of the 160 KB of a CU, so
 // two 1024-thread workgroups share a CU) and parts staged at most
@@ -54,6 +59,7 @@ typedef struct mxp_list_args {
     uint32_t lds_nparts;
     const uint32_t* lds_plan;
     uint32_t rx_nfa;            // REGEX lists with NFA parts: the *_nfa kernel instantiations
+    uint32_t ip_split;          // IP lists: mxp_list_ip_kernel (address families in waves of their own)
 } mxp_list_args;
 
 // ASCII upper-casing of 8 packed bytes (bytes >= 0x80 untouched): strings.ToUpper of ASCII-only

@@ -18,6 +18,7 @@
 #include "goupper.h"
 #include "lists.h"
 #include "vm.h"
+#include "dfa_dev.h"
 
 namespace {
 
@@ -30,16 +31,22 @@ __device__ __forceinline__ uint64_t tail_mask(uint32_t rem) {
 __constant__ uint32_t kUpperRows[MXP_UPPER_N][3] = {MXP_UPPER_ROWS};
 
 // probe the entry table for a key given by its hash and length; `same(e)` compares the entry bytes
+// (slots: lists.h MXP_LIST_SLOT -- tag, length and pool offset in one word)
 template <class Same>
 __device__ __forceinline__ bool string_probe(const mxp_list_args& A, uint64_t h, uint32_t n, Same same) {
-    const uint32_t tag = (uint32_t)(h >> 32);
+    const uint32_t tag = (uint32_t)(h >> 44);
+    const uint32_t want = n < MXP_LIST_LONG ? n : MXP_LIST_LONG;
     for (uint32_t slot = (uint32_t)h & A.hmask;; slot = (slot + 1) & A.hmask) {
         const uint64_t t = A.htab[slot];
         if (t == MXP_LIST_EMPTY) return false;
-        if ((uint32_t)(t >> 32) != tag) continue;
-        const uint64_t d = A.ent_desc[(uint32_t)t];
-        if ((uint32_t)(d & 0xFFFFFFu) != n) continue;
-        if (same(A.ent_pool + (d >> 24))) return true;
+        if ((uint32_t)(t >> 44) != tag || ((uint32_t)(t >> 32) & 0xFFFu) != want) continue;
+        uint64_t off = (uint64_t)(uint32_t)t * 8u;
+        if (want == MXP_LIST_LONG) {  // a long entry: its descriptor
+            const uint64_t d = A.ent_desc[(uint32_t)t];
+            if ((uint32_t)(d & 0xFFFFFFu) != n) continue;
+            off = d >> 24;
+        }
+        if (same(A.ent_pool + off)) return true;
     }
 }
 
@@ -196,6 +203,71 @@ __device__ __forceinline__ void list_body(const mxp_list_args& A) {
     }
     list_decide(A, q, found);
 }
+// IP lists with the address families in waves of their own.  net.ParseIP decides the family by the
+// symbol's first '.' or ':' (ip.go ParseIP); with one lookup per lane, a wave holding both families
+// ran the IPv4 parse and the IPv6 parse plus its 128-bit search one after the other, and with a
+// tenth of the lookups IPv6 nearly every wave held both.  Here each lane finds its symbol's family
+// in its first 8 bytes, the workgroup's lanes are regrouped in LDS (IPv4 from the front, the rest
+// from the back, one LDS atomic per wave), and each lane then checks the symbol its new slot names:
+// all but at most one wave of a workgroup run one family's path.
+__device__ __forceinline__ uint64_t byte_eq_mask(uint64_t w, uint32_t c) {
+    const uint64_t x = w ^ (0x0101010101010101ull * c);
+    return (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;  // high bit of each byte == c (first one exact)
+}
+
+extern "C" __global__ __launch_bounds__(256) void mxp_list_ip_kernel(mxp_list_args A) {
+    __shared__ uint32_t order[256];
+    __shared__ uint32_t cnt[2];  // IPv4 lanes taken from the front, the others from the back
+    const uint32_t t = threadIdx.x, lane = t & 63u;
+    const uint32_t q = blockIdx.x * 256u + t;
+    if (t < 2) cnt[t] = 0;
+    const uint8_t* s = nullptr;
+    uint32_t n = 0;
+    int fam = 2;  // 0 IPv4, 1 IPv6 or other, 2 settled (no lookup)
+    if (q < A.n && list_symbol(A, q, &s, &n)) {
+        const uint64_t w = n ? mxp_ld8(s) & tail_mask(n) : 0ull;
+        const uint64_t dot = byte_eq_mask(w, '.'), col = byte_eq_mask(w, ':');
+        fam = (dot && (!col || __builtin_ctzll(dot) < __builtin_ctzll(col))) ? 0 : 1;
+    }
+    __syncthreads();
+    const uint64_t b4 = __ballot(fam == 0), b6 = __ballot(fam == 1);
+    const uint32_t below = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)((fam == 0 ? b4 : b6) >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)(fam == 0 ? b4 : b6), 0u));
+    uint32_t base4 = 0, base6 = 0;
+    if (lane == 0) {
+        base4 = b4 ? atomicAdd(&cnt[0], (uint32_t)__popcll(b4)) : 0u;
+        base6 = b6 ? atomicAdd(&cnt[1], (uint32_t)__popcll(b6)) : 0u;
+    }
+    base4 = __shfl(base4, 0, 64);
+    base6 = __shfl(base6, 0, 64);
+    if (fam == 0) order[base4 + below] = t;
+    if (fam == 1) order[255u - (base6 + below)] = t;
+    __syncthreads();
+    const uint32_t c4 = cnt[0], c6 = cnt[1];
+    if (t >= c4 && t < 256u - c6) return;  // (settled lanes' slots)
+    const uint32_t src = order[t];
+    const uint32_t qq = blockIdx.x * 256u + src;
+    if (!list_symbol(A, qq, &s, &n)) return;
+    uint8_t ip[16];
+    bool found;
+    if (t < c4) {  // the first separator is '.': parseIPv4
+        if (!mxpnet::parse_v4(s, n, ip)) {
+            A.codes[qq] = MXP_RPC_INVALID_ARGUMENT;
+            return;
+        }
+        const uint32_t x = (uint32_t)ip[12] << 24 | (uint32_t)ip[13] << 16 | (uint32_t)ip[14] << 8 | ip[15];
+        const int k = find4(A.v4lo, A.n4, x);
+        found = k >= 0 && x <= A.v4hi[k];
+    } else {
+        if (!mxpnet::parse_ip(s, n, ip)) {
+            A.codes[qq] = MXP_RPC_INVALID_ARGUMENT;
+            return;
+        }
+        found = ip_member(A, ip);
+    }
+    list_decide(A, qq, found);
+}
+
 extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args A) { list_body<false>(A); }
 extern "C" __global__ __launch_bounds__(256) void mxp_list_nfa_kernel(mxp_list_args A) { list_body<true>(A); }
 
@@ -244,6 +316,10 @@ extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s) {
         const uint32_t grid = need < 512u ? need : 512u;
         hipLaunchKernelGGL(a->rx_nfa ? mxp_list_rx_nfa_kernel : mxp_list_rx_kernel, dim3(grid), dim3(MXP_LIST_RX_THREADS),
                            0, s, *a);
+        return hipGetLastError();
+    }
+    if (a->type == MXP_LIST_IP_ADDRESSES && a->ip_split) {
+        hipLaunchKernelGGL(mxp_list_ip_kernel, dim3((a->n + 255u) / 256u), dim3(256), 0, s, *a);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(a->rx_nfa ? mxp_list_nfa_kernel : mxp_list_kernel, dim3((a->n + 255u) / 256u), dim3(256), 0, s, *a);
