@@ -125,13 +125,20 @@ def test_resolver_compact_matches_bitmap_value_classes(mxp, monkeypatch):
     """C4 routes and header rules (value-class columns; missing headers give class error records that
     the compact path expands per request): the compact Resolve equals the error-bitmap Resolve, with
     the rules spread over three namespaces and mixed varieties / TCP flags."""
-    manifest, rules, batch = W.c4_workload(n_rules=1200, n_requests=20000, seed=31)
+    manifest, rules, batch = W.c4_workload(n_rules=1200, n_requests=20000, seed=31, cont_frac=0.2)
     manifest = dict(manifest, **{"context.protocol": "STRING"})
+    # value-class rules that fail per class (no header value converts to an IP): class records;
+    # placed among the default namespace's rules with variety 1 only
+    bad = ['ip(request.headers["%s"]) == ip("10.0.0.1")' % h for h in ("x-user", "x-env", "x-canary", "user-agent",
+                                                                     "x-region")] * 3
+    rules = list(rules[:300]) + bad + list(rules[300:])
     R = len(rules)
     rng = np.random.default_rng(5)
-    counts = rng.multinomial(R, [0.5, 0.3, 0.2])
+    counts = rng.multinomial(R - 700, [0.5, 0.3, 0.2])
+    counts[0] += 700
     rule_ns = ["istio-system"] * counts[0] + ["default"] * counts[1] + ["other"] * counts[2]
     vm = rng.integers(0, 8, size=R).astype(np.uint32)
+    vm[300:300 + len(bad)] = 2
     tcp = (rng.random(R) < 0.1).astype(np.uint8)
     empty = (rng.random(R) < 0.02).astype(np.uint8)
     out = {}

@@ -6,7 +6,8 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp MXP_NO_BUILD=1
 o=gpurun_out/r5s2; mkdir -p $o
-timeout -k 10 300 python -u -m pytest tests/test_gpu_resolver.py tests/test_gpu_bin.py tests/test_batch_check.py tests/test_gpu_refs.py tests/test_gpu_lists.py -m gpu -x -q --timeout 200 --timeout-method thread > $o/t.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_resolver.py tests/test_gpu_bin.py tests/test_batch_check.py tests/test_gpu_refs.py tests/test_gpu_lists.py -m gpu -q --timeout 200 --timeout-method thread > $o/t.log 2>&1
+rc=$?; [ $rc -ge 2 ] && exit $rc  # (test failures: go on; a crash or time limit: stop)
 timeout -k 10 200 python -u tools/e2e_trace.py --workload c2 > $o/e2e_c2.log 2>&1 || exit $?
 timeout -k 10 200 python -u tools/e2e_trace.py --workload c2 --pageable --u32 > $o/e2e_c2_pageable.log 2>&1 || exit $?
 timeout -k 10 300 python -u tools/e2e_trace.py --workload c4 > $o/e2e_c4.log 2>&1 || exit $?
