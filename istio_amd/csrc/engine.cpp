@@ -46,6 +46,26 @@ bool bins_release_all() {
     return any;
 }
 
+// A batch's device blocks go to the bin (no hipFree: it would wait for the whole device), with the
+// completion events of its evaluations and one on the engine stream (the packer).
+void mxp_engine::recycle(mxp_dbatch* db) {
+    if (!db) return;
+    BlockBin::Group g;
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, kOrderEvent) != hipSuccess || hipEventRecord(e, stream) != hipSuccess) {
+        if (e) (void)hipEventDestroy(e);
+        delete db;  // (no event: the plain frees)
+        return;
+    }
+    g.evs.push_back(e);
+    for (auto& se : db->done_ev) g.evs.push_back(se.second);  // (the group owns them now)
+    db->done_ev.clear();
+    g_bin_give = &g.blks;
+    delete db;
+    g_bin_give = nullptr;
+    bin.put(std::move(g));
+}
+
 // the cap, set on first use (an upload or free: the engine's device is current)
 size_t BlockBin::cap_locked() {
     if (!cap_set) {
@@ -2194,7 +2214,6 @@ void mxp_engine_destroy(mxp_engine* eng) {
     if (!eng) return;
     if (eng->device >= 0) (void)hipSetDevice(eng->device);
     if (eng->pk_host) (void)hipHostFree(eng->pk_host);
-    if (eng->res_hinfo) (void)hipHostFree(eng->res_hinfo);
     for (int k = 0; k < 2; k++) {
         if (eng->bounce_ev[k]) (void)hipEventDestroy(eng->bounce_ev[k]);
         if (eng->bounce[k]) (void)hipHostFree(eng->bounce[k]);
@@ -2406,20 +2425,7 @@ void mxp_batch_free(mxp_engine* eng, mxp_dbatch* db) {
         return;
     }
     (void)hipSetDevice(eng->device);
-    BlockBin::Group g;
-    hipEvent_t e = nullptr;
-    if (hipEventCreateWithFlags(&e, kOrderEvent) != hipSuccess || hipEventRecord(e, eng->stream) != hipSuccess) {
-        if (e) (void)hipEventDestroy(e);
-        delete db;  // (no event: the plain frees)
-        return;
-    }
-    g.evs.push_back(e);
-    for (auto& se : db->done_ev) g.evs.push_back(se.second);  // (the group owns them now)
-    db->done_ev.clear();
-    g_bin_give = &g.blks;
-    delete db;
-    g_bin_give = nullptr;
-    eng->bin.put(std::move(g));
+    eng->recycle(db);
 }
 
 int mxp_host_alloc(size_t bytes, void** out) {
@@ -2662,7 +2668,12 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
     if (e != hipSuccess) return hipfail(e, "hipSetDevice");
     db.reset(new mxp_dbatch());
     trace_mark(nullptr);
+    g_bin_take = &bin;  // (the batch's own blocks recycled where the bin has them)
+    g_bin_db = db.get();
+    g_bin_db_size = sizeof(mxp_dbatch);
     int rc = pack(batch, db.get());
+    g_bin_take = nullptr;
+    g_bin_db = nullptr;
     if (rc) return rc;
     trace_mark("pack + upload");
     const uint32_t n = batch->n_requests;
@@ -2685,7 +2696,11 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
 // bounce pair (DMA of chunk k + 1 beside the parallel host copy of chunk k).
 int mxp_engine::download(void* dst, const void* dsrc, size_t bytes, const char* what) {
     hipError_t e;
-    if (bytes < (4u << 20)) {
+    // caller memory that is pinned (mxp_host_alloc arenas): one DMA straight into it
+    hipPointerAttribute_t pa;
+    const bool pinned = bytes >= (1u << 20) && hipPointerGetAttributes(&pa, dst) == hipSuccess && pa.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // (pageable memory: the query fails)
+    if (bytes < (4u << 20) || pinned) {
         if (bytes && (e = hipMemcpyAsync(dst, dsrc, bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
             return hipfail(e, what);
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, what);
@@ -2765,6 +2780,7 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
             }
         });
     }
+    recycle(last_db.release());  // (the previous batch's blocks: to the bin, not hipFree)
     last_db = std::move(db);
     return MXP_OK;
 }

@@ -494,8 +494,6 @@ struct mxp_engine : public mxp::LowerTables {
     // block sums of the device scan of the counts
     DevBuf res_flags, res_err_in, res_pairs, res_bsum;
     std::vector<uint32_t> res_best;       // [n] host scratch: best resolution rank per request (~0 none)
-    void* res_hinfo = nullptr;            // pinned copy of the requests' namespace info
-    size_t res_hinfo_cap = 0;
     // the namespace names of the configuration on the device (mxp_ns_kernel): open-addressing table
     // of content hashes, descriptors, bytes
     DevBuf res_ns_tab, res_ns_desc, res_ns_blob;
@@ -616,7 +614,7 @@ struct mxp_engine : public mxp::LowerTables {
         vcol_ids.clear();
         rules.clear();
         have_rules = false;
-        last_db.reset();  // the last batch's ids and error records belong to the old rule set
+        recycle(last_db.release());  // the last batch's ids and error records belong to the old rule set
         clear_errors();
         err_windows.clear();
         errors_complete = true;
@@ -667,6 +665,7 @@ struct mxp_engine : public mxp::LowerTables {
     // first bad field named, never an out-of-range index into a device table (protoBag.go:255-265
     // answers an undefined index with an error too).
     int check_batch(const mxp_bag_batch* b);
+    void recycle(mxp_dbatch* db);  // a batch no longer used: its blocks to the bin (mxp_batch_free)
     // pack + launch into fresh device bitmaps (dm, de; dv = Eval registers when non-null)
     // d_req_err: compact error output (per-request flags; de is not written)
     int evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv, std::unique_ptr<mxp_dbatch>& db,

@@ -30,7 +30,7 @@ struct mxp_list {
     int type = 0;
     uint64_t n_entries = 0;
     uint32_t hmask = 0;
-    DevBuf htab, ent_desc, ent_pool, v4lo, v4hi, v6lo, v6hi;
+    DevBuf htab, ent_desc, ent_pool, v4lo, v4hi, v6lo, v6hi, v4dir;
     DevBuf rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // REGEX: the parts' automata
     uint32_t n4 = 0, n6 = 0, rx_n = 0, rx_nfa = 0;
     uint32_t lds_nparts = 0;
@@ -152,6 +152,11 @@ void merge(std::vector<std::pair<T, T>>& v) {
 
 // IP lists: address families in waves of their own (mxp_list_ip_kernel); MXP_LIST_IP_SPLIT=0: the
 // one-lookup-per-lane kernel (A/B)
+uint32_t list_opt() {
+    const char* e = getenv("MXP_LIST_OPT");
+    return e ? (uint32_t)atoi(e) : 0xFFu;
+}
+
 uint32_t ip_split() {
     const char* e = getenv("MXP_LIST_IP_SPLIT");
     return (uint32_t)(e ? atoi(e) != 0 : 1);
@@ -264,6 +269,14 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
         }
         L->n4 = (uint32_t)r4.size();
         L->n6 = (uint32_t)r6.size();
+        // /16 directory of the IPv4 intervals: dir[k] = intervals whose start is below k << 16
+        std::vector<uint32_t> dir(65537, 0);
+        for (uint32_t k = 0, i = 0; k <= 65536; k++) {
+            const uint64_t at = (uint64_t)k << 16;
+            while (i < lo4.size() && lo4[i] < at) i++;
+            dir[k] = i;
+        }
+        if ((rc = put(L->v4dir, dir.data(), dir.size() * 4, "upload v4dir"))) return rc;
         if ((rc = put(L->v4lo, lo4.data(), lo4.size() * 4, "upload v4lo"))) return rc;
         if ((rc = put(L->v4hi, hi4.data(), hi4.size() * 4, "upload v4hi"))) return rc;
         if ((rc = put(L->v6lo, lo6.data(), lo6.size() * 8, "upload v6lo"))) return rc;
@@ -402,6 +415,8 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, con
     A.rx_n = L->rx_n;
     A.rx_nfa = L->rx_nfa;
     A.ip_split = ip_split();
+    A.v4dir = L->v4dir.as<uint32_t>();
+    A.opt = list_opt();
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes;
@@ -451,6 +466,8 @@ int mxp_listentry_check(mxp_engine* eng, const mxp_list* L, int blacklist, const
     A.rx_n = L->rx_n;
     A.rx_nfa = L->rx_nfa;
     A.ip_split = ip_split();
+    A.v4dir = L->v4dir.as<uint32_t>();
+    A.opt = list_opt();
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
     A.codes = d_codes.as<int32_t>();

@@ -60,7 +60,13 @@ typedef struct mxp_list_args {
     const uint32_t* lds_plan;
     uint32_t rx_nfa;            // REGEX lists with NFA parts: the *_nfa kernel instantiations
     uint32_t ip_split;          // IP lists: mxp_list_ip_kernel (address families in waves of their own)
+    const uint32_t* v4dir;      // IP lists: [65537] v4dir[k] = intervals whose start is below k << 16
+    uint32_t opt;               // MXP_LIST_OPT_* (A/B knobs, MXP_LIST_OPT; default all on)
+    uint32_t pad_opt;
 } mxp_list_args;
+#define MXP_LIST_OPT_V4REG 1u   // dotted quads of <= 15 bytes parsed from registers (one window load)
+#define MXP_LIST_OPT_V4DIR 2u   // the IPv4 search starts from the /16 directory
+#define MXP_LIST_OPT_STRREG 4u  // string symbols of <= 64 bytes loaded once into registers
 
 // ASCII upper-casing of 8 packed bytes (bytes >= 0x80 untouched): strings.ToUpper of ASCII-only
 // strings (any other string takes goupper.h's per-rune stream)

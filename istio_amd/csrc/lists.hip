@@ -134,6 +134,100 @@ __device__ bool ip_member(const mxp_list_args& A, const uint8_t ip[16]) {
     return r >= 0 && le128(xh, xl, A.v6hi[2 * r], A.v6hi[2 * r + 1]);
 }
 
+// the last IPv4 interval starting at or below x, from the /16 directory: the intervals starting in
+// x's /16 block, else the one before them (kargs.v4dir; one load, then a search of the block's few)
+__device__ __forceinline__ int find4_dir(const mxp_list_args& A, uint32_t x) {
+    const uint32_t k = x >> 16;
+    const int a0 = (int)A.v4dir[k], a1 = (int)A.v4dir[k + 1u];
+    int a = a0, b = a1 - 1, r = a0 - 1;
+    while (a <= b) {
+        const int m = (a + b) >> 1;
+        if (A.v4lo[m] <= x) {
+            r = m;
+            a = m + 1;
+        } else {
+            b = m - 1;
+        }
+    }
+    return r;
+}
+
+// bytes [8i, 8i + 8) of a symbol at any address, from aligned words q[] of its window
+__device__ __forceinline__ uint64_t funnel8(uint64_t lo, uint64_t hi, uint32_t sh) {
+    return sh ? (lo >> sh) | (hi << (64u - sh)) : lo;
+}
+
+// parseIPv4 (ip.go; leading zeros allowed in Go 1.9) of a dotted quad of at most 15 bytes held in
+// registers: two 8-byte words from one three-load window, every byte position unrolled (no
+// dependent byte loads).  *x = the address; false when it is no IPv4 literal.
+__device__ __forceinline__ bool parse_v4_reg(const uint8_t* s, uint32_t n, uint32_t* x) {
+    const uintptr_t a = (uintptr_t)s;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    const uint32_t span = sh / 8u + n;  // bytes of the window the symbol reaches into
+    const uint64_t q0 = q[0], q1 = span > 8u ? q[1] : 0ull, q2 = span > 16u ? q[2] : 0ull;
+    const uint64_t w0 = funnel8(q0, q1, sh), w1 = funnel8(q1, q2, sh);
+    uint32_t acc = 0, ip = 0, ndig = 0, ngrp = 0;
+    bool ok = true;
+#pragma unroll
+    for (uint32_t i = 0; i < 15u; i++) {
+        if (i < n) {
+            const uint32_t c = (uint32_t)((i < 8u ? w0 >> (8u * i) : w1 >> (8u * (i - 8u))) & 0xFFu);
+            if (c == '.') {
+                ok = ok && ndig > 0u && ngrp < 3u;
+                ip = ip << 8 | acc;
+                acc = 0;
+                ndig = 0;
+                ngrp++;
+            } else {
+                const uint32_t d = c - '0';
+                acc = acc * 10u + d;
+                ok = ok && d < 10u && acc <= 255u;
+                ndig++;
+            }
+        }
+    }
+    *x = ip << 8 | acc;
+    return ok && ngrp == 3u && ndig > 0u;
+}
+
+// string / case-insensitive membership of a symbol of at most 64 bytes: its words loaded once (one
+// window of independent loads), hashed and compared from registers; the candidate entry's words
+// loaded together.  false in *done when the symbol needs the general path (longer, or bytes >= 0x80
+// in a case-insensitive list).
+__device__ __forceinline__ bool string_member_reg(const mxp_list_args& A, const uint8_t* s, uint32_t n, bool upper,
+                                                  bool* done) {
+    *done = false;
+    if (n > 64u) return false;
+    const uintptr_t a = (uintptr_t)s;
+    const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(a & 7u) * 8u;
+    const uint32_t nw = (n + 7u) / 8u;
+    uint64_t raw[9];
+#pragma unroll
+    for (uint32_t i = 0; i < 9u; i++) raw[i] = i <= nw ? q[i] : 0ull;
+    uint64_t w[8];
+    uint64_t h = 0, hi = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 8u; i++) {
+        uint64_t x = funnel8(raw[i], raw[i + 1], sh) & tail_mask(i * 8u < n ? n - i * 8u : 0u);
+        hi |= x;
+        if (upper) x = mxp_upper8(x);
+        w[i] = x;
+        if (i < nw) h = mxp_hash_step(h, x);
+    }
+    if (upper && (hi & 0x8080808080808080ull)) return false;  // strings.ToUpper's per-rune path
+    *done = true;
+    h = mxp_hash_final(h, n);
+    return string_probe(A, h, n, [&](const uint8_t* e) {
+        uint64_t diff = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < 8u; i++)
+            if (i < nw) diff |= (ld8u(e + 8u * i) & tail_mask(n - i * 8u)) ^ w[i];
+        return diff == 0ull;
+    });
+}
+
 // The symbol of lookup q: a blob entry, or (fused listentry) the Eval result of one rule.  Returns
 // false with codes[q] written when the lookup is settled before the membership test.
 __device__ __forceinline__ bool list_symbol(const mxp_list_args& A, uint32_t q, const uint8_t** sp, uint32_t* np) {
@@ -251,12 +345,19 @@ extern "C" __global__ __launch_bounds__(256) void mxp_list_ip_kernel(mxp_list_ar
     uint8_t ip[16];
     bool found;
     if (t < c4) {  // the first separator is '.': parseIPv4
-        if (!mxpnet::parse_v4(s, n, ip)) {
+        uint32_t x;
+        bool ok;
+        if (n <= 15u && (A.opt & MXP_LIST_OPT_V4REG)) {
+            ok = parse_v4_reg(s, n, &x);
+        } else {
+            ok = mxpnet::parse_v4(s, n, ip);
+            x = (uint32_t)ip[12] << 24 | (uint32_t)ip[13] << 16 | (uint32_t)ip[14] << 8 | ip[15];
+        }
+        if (!ok) {
             A.codes[qq] = MXP_RPC_INVALID_ARGUMENT;
             return;
         }
-        const uint32_t x = (uint32_t)ip[12] << 24 | (uint32_t)ip[13] << 16 | (uint32_t)ip[14] << 8 | ip[15];
-        const int k = find4(A.v4lo, A.n4, x);
+        const int k = (A.opt & MXP_LIST_OPT_V4DIR) ? find4_dir(A, x) : find4(A.v4lo, A.n4, x);
         found = k >= 0 && x <= A.v4hi[k];
     } else {
         if (!mxpnet::parse_ip(s, n, ip)) {
@@ -266,6 +367,21 @@ extern "C" __global__ __launch_bounds__(256) void mxp_list_ip_kernel(mxp_list_ar
         found = ip_member(A, ip);
     }
     list_decide(A, qq, found);
+}
+
+// string and case-insensitive lists alone (the register fast path; no IP or automaton code, so the
+// kernel's register budget is the string path's)
+extern "C" __global__ __launch_bounds__(256) void mxp_list_str_kernel(mxp_list_args A) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x;
+    if (q >= A.n) return;
+    const uint8_t* s;
+    uint32_t n;
+    if (!list_symbol(A, q, &s, &n)) return;
+    const bool upper = A.type == MXP_LIST_CASE_INSENSITIVE_STRINGS;
+    bool done = false, found = false;
+    if (A.opt & MXP_LIST_OPT_STRREG) found = string_member_reg(A, s, n, upper, &done);
+    if (!done) found = string_member(A, s, n, upper);
+    list_decide(A, q, found);
 }
 
 extern "C" __global__ __launch_bounds__(256) void mxp_list_kernel(mxp_list_args A) { list_body<false>(A); }
@@ -316,6 +432,10 @@ extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s) {
         const uint32_t grid = need < 512u ? need : 512u;
         hipLaunchKernelGGL(a->rx_nfa ? mxp_list_rx_nfa_kernel : mxp_list_rx_kernel, dim3(grid), dim3(MXP_LIST_RX_THREADS),
                            0, s, *a);
+        return hipGetLastError();
+    }
+    if (a->type == MXP_LIST_STRINGS || a->type == MXP_LIST_CASE_INSENSITIVE_STRINGS) {
+        hipLaunchKernelGGL(mxp_list_str_kernel, dim3((a->n + 255u) / 256u), dim3(256), 0, s, *a);
         return hipGetLastError();
     }
     if (a->type == MXP_LIST_IP_ADDRESSES && a->ip_split) {

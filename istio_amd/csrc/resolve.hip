@@ -41,17 +41,24 @@ __device__ __forceinline__ uint32_t walk(const mxp_resolve_args& A, uint32_t q) 
         }
         return 0;
     }
-    // compact mode: the first applicable error in resolution order is known (error records)
+    const uint32_t ns = info & 0x7FFFFFFFu;
+    // compact mode: the first applicable error in resolution order is known (error records): its
+    // rule, or its rank in the resolution order (default namespace's rules, then the request's own)
     if (!kWrite && A.err_in) {
         const uint32_t er = A.err_in[q];
         if (er != 0xFFFFFFFFu) {
+            uint32_t rule = er;
+            if (A.err_rank) {
+                const bool def = A.default_id != MXP_NS_NONE;
+                const uint32_t dlo = def ? A.ns_lo[A.default_id] : 0u, dlen = def ? A.ns_hi[A.default_id] - dlo : 0u;
+                rule = er < dlen ? dlo + er : A.ns_lo[ns] + (er - dlen);
+            }
             A.status[q] = MXP_RESOLVE_PRED_ERROR;
-            A.err_rule[q] = er;
+            A.err_rule[q] = rule;
             A.count[q] = 0;
             return 0;
         }
     }
-    const uint32_t ns = info & 0x7FFFFFFFu;
     const uint32_t tcp = info >> 31;
     const uint32_t* amask = A.amask + (uint64_t)tcp * A.n_words;
     uint32_t ranges[2][2];
@@ -271,5 +278,42 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_scatter_kernel(con
 
 extern "C" hipError_t mxp_launch_resolve_scatter(const uint32_t* pairs, uint32_t m, uint32_t* err_in, hipStream_t s) {
     if (m) hipLaunchKernelGGL(mxp_resolve_scatter_kernel, dim3((m + 255u) / 256u), dim3(256), 0, s, pairs, m, err_in);
+    return hipGetLastError();
+}
+
+// compact Resolve: each error record (request, rule) that filterActions would meet -- an applicable
+// rule (variety, tcp) with a non-empty match in the request's resolution ranges -- lowers the
+// request's first-error rank (err_in, ~0 = none) to the rule's position in the resolution order
+extern "C" __global__ __launch_bounds__(256) void mxp_resolve_first_err_kernel(mxp_resolve_args A, const uint4* recs,
+                                                                               uint32_t m) {
+    const bool def = A.default_id != MXP_NS_NONE;
+    const uint32_t dlo = def ? A.ns_lo[A.default_id] : 0u, dhi = def ? A.ns_hi[A.default_id] : 0u;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < m; i += gridDim.x * 256u) {
+        const uint4 rec = recs[i];
+        const uint32_t q = rec.x, r = rec.y;
+        if (q >= A.n || r >= A.n_words * 32u) continue;
+        const uint32_t info = A.nsinfo[q];
+        if (info == MXP_NS_MISSING || info == MXP_NS_NOTSTRING) continue;
+        const uint32_t tcp = info >> 31, ns = info & 0x7FFFFFFFu, w = r >> 5, bit = 1u << (r & 31u);
+        if ((A.empty[w] & bit) || !(A.amask[(uint64_t)tcp * A.n_words + w] & bit)) continue;
+        uint32_t rank;
+        if (def && r >= dlo && r < dhi) {
+            rank = r - dlo;
+        } else if (ns != MXP_NS_NONE && ns != A.default_id && r >= A.ns_lo[ns] && r < A.ns_hi[ns]) {
+            rank = (dhi - dlo) + (r - A.ns_lo[ns]);
+        } else {
+            continue;
+        }
+        atomicMin((unsigned int*)A.err_in + q, rank);
+    }
+}
+
+extern "C" hipError_t mxp_launch_resolve_first_err(const mxp_resolve_args* a, const void* recs, uint32_t m,
+                                                   hipStream_t s) {
+    if (m) {
+        const uint32_t need = (m + 255u) / 256u;
+        hipLaunchKernelGGL(mxp_resolve_first_err_kernel, dim3(need < 4096u ? need : 4096u), dim3(256), 0, s, *a,
+                           (const uint4*)recs, m);
+    }
     return hipGetLastError();
 }

@@ -53,5 +53,5 @@ typedef struct mxp_resolve_args {
     uint64_t* block_sum;       // [ceil(n / MXP_RES_SCAN_TILE)]
     uint64_t* sel_off_out;     // [n + 1] (scan pass)
     uint32_t ids16;            // pass 2 writes u16 rule ids (sel_rules as uint16_t*)
-    uint32_t pad2;
+    uint32_t err_rank;         // err_in holds resolution ranks (mxp_resolve_first_err_kernel), not rules
 } mxp_resolve_args;

@@ -16,6 +16,7 @@
 extern "C" hipError_t mxp_launch_resolve(const mxp_resolve_args* a, int write, hipStream_t s);
 extern "C" hipError_t mxp_launch_ns(const mxp_ns_args* a, hipStream_t s);
 extern "C" hipError_t mxp_launch_resolve_scatter(const uint32_t* pairs, uint32_t m, uint32_t* err_in, hipStream_t s);
+extern "C" hipError_t mxp_launch_resolve_first_err(const mxp_resolve_args* a, const void* recs, uint32_t m, hipStream_t s);
 
 namespace {
 
@@ -257,21 +258,6 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         N.ns_blob = eng->res_ns_blob.as<uint8_t>();
         N.nsinfo = d_info.as<uint32_t>();
         if (n && (e = mxp_launch_ns(&N, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch namespaces");
-        if (n) {  // (the first-error pass reads it; the copy rides behind the evaluation)
-            if (eng->res_hinfo_cap < (size_t)n * 4) {
-                if (eng->res_hinfo) (void)hipHostFree(eng->res_hinfo);
-                eng->res_hinfo = nullptr;
-                eng->res_hinfo_cap = 0;
-                if ((e = hipHostMalloc(&eng->res_hinfo, (size_t)n * 4, hipHostMallocDefault)) != hipSuccess) {
-                    eng->res_hinfo = nullptr;
-                    return eng->hipfail(e, "pinned nsinfo");
-                }
-                eng->res_hinfo_cap = (size_t)n * 4;
-            }
-            if ((e = hipMemcpyAsync(eng->res_hinfo, d_info.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-                return eng->hipfail(e, "download nsinfo");
-            hinfo = (const uint32_t*)eng->res_hinfo;
-        }
         eng->trace_mark("request namespaces (device)");
     } else {
         request_info(eng, batch, &info);
@@ -308,28 +294,55 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     A.sel_off_out = d_off.as<uint64_t>();
     A.sel_off = d_off.as<uint64_t>();
     A.ids16 = ids16 ? 1u : 0u;
+    bool collected = !compact;  // (the bitmap path collects its records after the resolve kernels)
     if (compact) {
-        // the error records (synchronises the stream: the namespace copy has landed too)
-        if ((rc = eng->collect_errors(batch, db))) return rc;
-        eng->trace_mark("error records");
-        if (!eng->errors_complete) {
+        // the log's counts: [0] records, [2] class records (synchronises: the evaluation is done)
+        uint32_t cnt[4] = {0, 0, 0, 0};
+        if ((e = hipMemcpyAsync(cnt, eng->d_errcount.p, 16, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(eng->stream)) != hipSuccess)
+            return eng->hipfail(e, "download errcount");
+        if ((e = eng->res_err_in.reserve((size_t)n * 4 + 4)) != hipSuccess) return eng->hipfail(e, "alloc err_in");
+        if (n && (e = hipMemsetAsync(eng->res_err_in.p, 0xFF, (size_t)n * 4, eng->stream)) != hipSuccess)
+            return eng->hipfail(e, "reset err_in");
+        if (cnt[0] > eng->errcap) {
             // records past the log's capacity: the error bitmap after all (an evaluation without a log)
             if ((e = de.reserve((size_t)W * n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err");
-            if ((rc = eng->launch(eng->last_db.get(), eng->stream, dm.as<uint32_t>(), de.as<uint32_t>(), nullptr, false)))
-                return rc;
+            if ((rc = eng->launch(db.get(), eng->stream, dm.as<uint32_t>(), de.as<uint32_t>(), nullptr, false))) return rc;
             A.err = de.as<uint32_t>();
-        } else {
-            std::vector<uint32_t> pairs;
-            first_errors(eng, n, variety, hinfo, &pairs);
-            if ((e = eng->res_err_in.reserve((size_t)n * 4 + 4)) != hipSuccess) return eng->hipfail(e, "alloc err_in");
-            if (n && (e = hipMemsetAsync(eng->res_err_in.p, 0xFF, (size_t)n * 4, eng->stream)) != hipSuccess)
-                return eng->hipfail(e, "reset err_in");
-            if ((rc = up(eng->res_pairs, pairs.data(), pairs.size() * 4, "upload first errors"))) return rc;
-            if ((e = mxp_launch_resolve_scatter(eng->res_pairs.as<uint32_t>(), (uint32_t)(pairs.size() / 2),
-                                                eng->res_err_in.as<uint32_t>(), eng->stream)) != hipSuccess)
-                return eng->hipfail(e, "launch first errors");
+            eng->trace_mark("error bitmap (log overflow)");
+        } else if (!cnt[2]) {
+            // each request's first error from the records, on the device
             A.err_in = eng->res_err_in.as<uint32_t>();
-            eng->trace_mark("first errors (host pass + scatter)");
+            A.err_rank = 1u;
+            if ((e = mxp_launch_resolve_first_err(&A, eng->d_errlog.p, cnt[0], eng->stream)) != hipSuccess)
+                return eng->hipfail(e, "launch first errors");
+            eng->trace_mark("first errors (device)");
+        } else {
+            // value-class records stand for whole classes: expanded per request on the host
+            // (collect_errors), then the first error of each failing request found there
+            if ((rc = eng->collect_errors(batch, db))) return rc;
+            collected = true;
+            if (!eng->errors_complete) {
+                if ((e = de.reserve((size_t)W * n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err");
+                if ((rc = eng->launch(eng->last_db.get(), eng->stream, dm.as<uint32_t>(), de.as<uint32_t>(), nullptr,
+                                      false)))
+                    return rc;
+                A.err = de.as<uint32_t>();
+            } else {
+                if (n && hinfo == nullptr) {  // (the device namespaces, brought back for this pass)
+                    info.resize(n);
+                    if ((rc = eng->download(info.data(), d_info.p, (size_t)n * 4, "download nsinfo"))) return rc;
+                    hinfo = info.data();
+                }
+                std::vector<uint32_t> pairs;
+                first_errors(eng, n, variety, hinfo, &pairs);
+                if ((rc = up(eng->res_pairs, pairs.data(), pairs.size() * 4, "upload first errors"))) return rc;
+                if ((e = mxp_launch_resolve_scatter(eng->res_pairs.as<uint32_t>(), (uint32_t)(pairs.size() / 2),
+                                                    eng->res_err_in.as<uint32_t>(), eng->stream)) != hipSuccess)
+                    return eng->hipfail(e, "launch first errors");
+                A.err_in = eng->res_err_in.as<uint32_t>();
+            }
+            eng->trace_mark("first errors (class records, host)");
         }
     }
     if (n && (e = mxp_launch_resolve(&A, 0, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve");
@@ -342,7 +355,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         if ((rc = eng->download(sel_off, d_off.p, ((size_t)n + 1) * 8, "download sel_off"))) return rc;
     }
     eng->trace_mark("resolve kernels + downloads");
-    if (!compact) {
+    if (!collected) {
         if ((rc = eng->collect_errors(batch, db))) return rc;  // synchronises the stream
         eng->trace_mark("error records");
     }

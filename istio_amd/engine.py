@@ -143,15 +143,20 @@ class PinnedArena:
             raise MxpError("mxp_host_alloc(%d) failed" % nbytes)
         self.size, self.used = max(int(nbytes), 16), 0
 
-    def array(self, like: np.ndarray) -> np.ndarray:
-        """A pinned copy of `like` (same dtype and shape), 64-byte aligned within the arena."""
-        nb = like.nbytes
+    def empty(self, count: int, dtype) -> np.ndarray:
+        """An uninitialised pinned array of `count` elements, 64-byte aligned within the arena."""
+        dtype = np.dtype(dtype)
+        nb = int(count) * dtype.itemsize
         at = (self.used + 63) & ~63
         if at + nb > self.size:
             raise MxpError("pinned arena full")
         self.used = at + nb
         buf = (ctypes.c_uint8 * max(nb, 1)).from_address(self.p.value + at)
-        out = np.frombuffer(buf, dtype=like.dtype, count=like.size).reshape(like.shape)
+        return np.frombuffer(buf, dtype=dtype, count=int(count))
+
+    def array(self, like: np.ndarray) -> np.ndarray:
+        """A pinned copy of `like` (same dtype and shape)."""
+        out = self.empty(like.size, like.dtype).reshape(like.shape)
         out[...] = like
         return out
 
@@ -472,17 +477,29 @@ class Engine:
         self._check(self.lib.mxp_resolver_set(self.h, identity_attr.encode(), default_ns.encode(), ns,
                                               vm.ctypes.data, tcp.ctypes.data, em.ctypes.data, n), "mxp_resolver_set")
 
-    def resolve_arrays(self, batch: BagBatch, variety: int, cap: int = 0, ids16: bool = False):
+    def resolve_arrays(self, batch: BagBatch, variety: int, cap: int = 0, ids16: bool = False, pinned: bool = False):
         """mxp_resolve_batch -> (status u8[n], err_rule u32[n], sel_off u64[n + 1], sel_rules u32[...]):
         request q's selected rules are sel_rules[sel_off[q]:sel_off[q + 1]], in resolution order.
-        ids16: mxp_resolve_batch_ex with MXP_RESOLVE_IDS_U16 (sel_rules u16)."""
+        ids16: mxp_resolve_batch_ex with MXP_RESOLVE_IDS_U16 (sel_rules u16).  pinned: the outputs in
+        a pinned arena the engine object keeps (DMA straight into them; the arrays are views, valid
+        until the next pinned call)."""
         n = batch.n
-        status = np.empty(n, dtype=np.uint8)
-        err_rule = np.empty(n, dtype=np.uint32)
-        off = np.empty(n + 1, dtype=np.uint64)
         cap = cap or max(16, n * 4)
+        isz = 2 if ids16 else 4
+
+        def outputs(cap):
+            if not pinned:
+                return (np.empty(n, dtype=np.uint8), np.empty(n, dtype=np.uint32), np.empty(n + 1, dtype=np.uint64),
+                        np.empty(cap, dtype=np.uint16 if ids16 else np.uint32))
+            need = n * 13 + 8 + cap * isz + 4 * 64
+            if getattr(self, "_out_arena", None) is None or self._out_arena.size < need:
+                self._out_arena = PinnedArena(int(need * 1.25))
+            a = self._out_arena
+            a.used = 0
+            return (a.empty(n, np.uint8), a.empty(n, np.uint32), a.empty(n + 1, np.uint64),
+                    a.empty(cap, np.uint16 if ids16 else np.uint32))
         for _ in range(2):
-            sel = np.empty(cap, dtype=np.uint16 if ids16 else np.uint32)
+            status, err_rule, off, sel = outputs(cap)
             if ids16:
                 rc = self.lib.mxp_resolve_batch_ex(self.h, ctypes.byref(batch.c_struct()), variety, 1,
                                                    status.ctypes.data, err_rule.ctypes.data, off.ctypes.data,

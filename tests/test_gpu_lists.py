@@ -83,6 +83,51 @@ def test_c3_string_list_parity(eng, kind):
     assert (want == 0).sum() > 1000 and (want == 5).sum() > 1000
 
 
+@pytest.mark.parametrize("kind", [L.STRINGS, L.CASE_INSENSITIVE_STRINGS])
+def test_string_symbol_lengths(eng, kind):
+    """Symbols of 0..80 bytes at every alignment -- around the register path's 64-byte bound and the
+    8-byte word edges -- hits, near misses (last byte changed) and case changes, ASCII and not,
+    against the restatement."""
+    rng = np.random.default_rng(41)
+    alpha = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ0123456789-_./"
+    entries = ["".join(rng.choice(list(alpha), size=k)) for k in range(1, 81) for _ in range(3)]
+    entries += ["\u00e9t\u00e9-%d" % k for k in range(5)] + ["x" * 64, "y" * 65, "Z" * 63]
+    syms = []
+    for e in entries:
+        syms += [e, e.swapcase(), e[:-1] + ("#" if e[-1] != "#" else "%"), e + "q", e[:-1]]
+    syms += ["", "x" * 64, "X" * 64, "y" * 65, "z" * 63]
+    for pad in range(8):  # every alignment of the symbols in the blob: a pad symbol first
+        ss = ["p" * pad] + syms
+        lst = eng.list_create(kind, entries, [])
+        ref = L.StringList(entries, [], case_insensitive=kind == L.CASE_INSENSITIVE_STRINGS)
+        want = L.codes(ref.found(ss), False)
+        got = lst.check(ss)
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, [(ss[i], int(got[i]), int(want[i])) for i in bad[:5]]
+
+
+@pytest.mark.parametrize("kind", ["ip", "str"])
+def test_list_paths_agree(eng, monkeypatch, kind):
+    """The list kernels' paths give identical codes: IP family regrouping on / off, the register
+    parse, the /16 directory and the string register path each off (MXP_LIST_OPT bits)."""
+    if kind == "ip":
+        entries, syms = W.c3_ip_list(n_entries=5000, n_lookups=60000, seed=43)
+        lst = eng.list_create(L.IP_ADDRESSES, entries, [])
+        settings = [("1", "255"), ("0", "255"), ("1", "0"), ("1", "1"), ("1", "2")]
+    else:
+        entries, syms = W.c3_string_list(n_entries=5000, n_lookups=60000, seed=44)
+        lst = eng.list_create(L.CASE_INSENSITIVE_STRINGS, entries, [])
+        settings = [("1", "255"), ("1", "0")]
+    ref = None
+    for split, opt in settings:
+        monkeypatch.setenv("MXP_LIST_IP_SPLIT", split)
+        monkeypatch.setenv("MXP_LIST_OPT", opt)
+        got = lst.check(syms, True)
+        if ref is None:
+            ref = got
+        assert np.array_equal(got, ref), (split, opt)
+
+
 def test_c3_regex_list_parity(eng):
     pats, syms = W.c3_regex_list(n_patterns=200, n_lookups=1500, seed=33)
     lst = eng.list_create(L.REGEX, pats[:150] + [""], pats[150:])

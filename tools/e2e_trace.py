@@ -35,14 +35,14 @@ def main():
         assert (eng.compile(rules) == 0).all()
         eng.set_resolver("destination.service", "istio-system", ["istio-system"] * R, np.ones(R, dtype=np.uint32),
                          np.zeros(R, dtype=np.uint8), np.zeros(R, dtype=np.uint8))
-        status, _, off, _ = eng.resolve_arrays(batch, 0, ids16=ids16)
+        status, _, off, _ = eng.resolve_arrays(batch, 0, ids16=ids16, pinned=not a.pageable)
         cap = max(16, int(off[-1]))
         ts = []
         for k in range(a.reps):
             if traced:
                 print("-- traced call %d" % k, file=sys.stderr, flush=True)
             t0 = time.perf_counter()
-            status, _, off, sel = eng.resolve_arrays(batch, 0, cap, ids16=ids16)
+            status, _, off, sel = eng.resolve_arrays(batch, 0, cap, ids16=ids16, pinned=not a.pageable)
             ts.append(time.perf_counter() - t0)
         print("%s %s %s %s: ms per call %s (median %.2f); selected/request %.1f, error requests %d" % (
             a.workload, "pageable" if a.pageable else "pinned", "u32" if a.u32 else "u16",
