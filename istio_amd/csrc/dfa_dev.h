@@ -18,6 +18,9 @@ typedef struct mxp_dfa_hdr {
 #define MXP_DFA_DECIDED 0xFFFFFFFFu
 #define MXP_RX_DFA 0u
 #define MXP_RX_NFA 1u
+// a DFA of at most 65533 states with u16 transitions (regex-list parts, lists.cpp): `trans` indexes the
+// u32 array where its u16 rows start; 0xFFFF accept, 0xFFFE reject
+#define MXP_RX_DFA16 2u
 
 // Bit-parallel NFA image (u64 words from S.trans + H.trans), for patterns whose DFA is over budget:
 //   [0]            m | W << 16 | nvar << 24   (m rune instructions; bit m of a set = MATCH; W words)
@@ -237,10 +240,23 @@ __device__ __forceinline__ bool mxp_nfa_run(const mxp_dfa_set& S, const mxp_dfa_
 // staged in LDS by the caller; states >= K step from global memory.  Subset construction numbers
 // states in BFS order from the start, so the staged rows are the shallow, hot part of the DFA.
 // (DFA headers only: callers that may meet an NFA header use mxp_rx_run)
+// u16 parts (MXP_RX_DFA16): rows of u16 transitions, in LDS too; their reject / accept codes widen to
+// the u32 ones.
 template <bool kLds>
 __device__ __forceinline__ bool mxp_dfa_walk(const mxp_dfa_set& S, const mxp_dfa_hdr& H, const uint32_t* TL,
                                              const uint16_t* AL, uint32_t K, const uint8_t* s, uint32_t n) {
     const uint32_t* T = S.trans + H.trans;
+    const bool w16 = H.kind == MXP_RX_DFA16;
+    const uint16_t* T16 = (const uint16_t*)T;
+    const uint16_t* TL16 = (const uint16_t*)TL;
+    auto next = [&](uint64_t at, uint32_t st) -> uint32_t {
+        if (w16) {
+            const uint32_t v = (kLds && st < K) ? TL16[(uint32_t)at] : T16[at];
+            return v >= 0xFFFEu ? v | 0xFFFF0000u : v;
+        }
+        if constexpr (kLds) return st < K ? TL[(uint32_t)at] : T[at];
+        return T[at];
+    };
     const uint16_t* asc = kLds ? AL : S.ascii + H.ascii;
     uint32_t st = H.start;
     uint32_t i = H.skip;
@@ -298,18 +314,10 @@ __device__ __forceinline__ bool mxp_dfa_walk(const mxp_dfa_set& S, const mxp_dfa
             }
             cls = S.hicls[H.hi + k];
         }
-        const uint64_t at = (uint64_t)st * H.ncls + cls;
-        if constexpr (kLds)
-            st = st < K ? TL[(uint32_t)at] : T[at];
-        else
-            st = T[at];
+        st = next((uint64_t)st * H.ncls + cls, st);
         if (st >= 0xFFFFFFFEu) return st == 0xFFFFFFFFu;
     }
-    const uint64_t at = (uint64_t)st * H.ncls + H.ncls - 1;
-    if constexpr (kLds)
-        return (st < K ? TL[(uint32_t)at] : T[at]) == 0xFFFFFFFFu;
-    else
-        return T[at] == 0xFFFFFFFFu;
+    return next((uint64_t)st * H.ncls + H.ncls - 1, st) == 0xFFFFFFFFu;
 }
 
 __device__ __forceinline__ bool mxp_dfa_run(const mxp_dfa_set& S, uint32_t dfa, const uint8_t* s, uint32_t n) {

@@ -152,9 +152,12 @@ void merge(std::vector<std::pair<T, T>>& v) {
 
 // IP lists: address families in waves of their own (mxp_list_ip_kernel); MXP_LIST_IP_SPLIT=0: the
 // one-lookup-per-lane kernel (A/B)
+// MXP_LIST_OPT (lists.h MXP_LIST_OPT_*): the IPv4 register parse and the string register window are
+// on; the /16 directory is off (same-box A/B on C3 CIDR, profiles/r5_s3_ab_c3ip_opt.log: 0.0676 ms
+// without it, 0.0678 with it)
 uint32_t list_opt() {
     const char* e = getenv("MXP_LIST_OPT");
-    return e ? (uint32_t)atoi(e) : 0xFFu;
+    return e ? (uint32_t)atoi(e) : (MXP_LIST_OPT_V4REG | MXP_LIST_OPT_STRREG);
 }
 
 uint32_t ip_split() {
@@ -303,6 +306,31 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             cost[i] = prc == mxp::RX_OK ? one.nstates : kPatternStates;
             alone[i] = prc != mxp::RX_OK;
         }
+        // u16 parts (MXP_LIST_RX16, default on): union DFAs of at most 65533 states, u16 rows, the
+        // patterns sorted first (any match is a match, so the order is free) so that a part's
+        // patterns share their leading literals and a lookup leaves the other parts at their first
+        // byte; states numbered BFS for the LDS-staged head, depth-first below it, so one lookup's
+        // chain of rows lies in adjacent rows (tools: profiles/r5_*_ab_c3rx*).
+        const char* rx16_env = getenv("MXP_LIST_RX16");
+        const bool rx16 = !rx16_env || atoi(rx16_env) != 0;
+        if (rx16) {
+            std::vector<size_t> ord(pats.size());
+            for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
+            std::stable_sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return pats[a] < pats[b]; });
+            std::vector<std::string> p2(pats.size());
+            std::vector<uint64_t> c2(pats.size());
+            std::vector<uint8_t> a2(pats.size());
+            for (size_t i = 0; i < ord.size(); i++) {
+                p2[i] = std::move(pats[ord[i]]);
+                c2[i] = cost[ord[i]];
+                a2[i] = alone[ord[i]];
+            }
+            pats.swap(p2);
+            cost.swap(c2);
+            alone.swap(a2);
+        }
+        const uint32_t union_budget = rx16 ? 65533u : kListRegexStates;
+        const uint64_t pack_budget = rx16 ? 56000u : kListPartStates;
         mxp::DfaSetHost set;
         std::vector<uint32_t> part_states;  // DFA states per part (0: an NFA part)
         std::function<int(size_t, size_t)> part = [&](size_t lo, size_t hi) -> int {
@@ -311,9 +339,14 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             mxp::Dfa d;
             std::string e;
             const bool one = hi - lo == 1;
-            const int prc = mxp::regex_compile(ps, one ? kPatternStates : kListRegexStates, &d, &e, nullptr, one);
+            const int prc = mxp::regex_compile(ps, one ? kPatternStates : union_budget, &d, &e, nullptr, one);
             if (prc == mxp::RX_OK) {
-                set.add(d);
+                if (rx16 && !d.is_nfa() && d.nstates <= 65533u) {
+                    mxp::dfa_renumber_hybrid(&d, std::max(1u, 2u * MXP_LDS_DFA_WORDS / d.ncls));
+                    set.add16(d);
+                } else {
+                    set.add(d);
+                }
                 part_states.push_back(d.is_nfa() ? 0u : d.nstates);
                 return MXP_OK;
             }
@@ -330,7 +363,7 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             }
             size_t j = i;
             uint64_t sum = 0;
-            while (j < pats.size() && !alone[j] && (j == i || sum + cost[j] <= kListPartStates)) sum += cost[j++];
+            while (j < pats.size() && !alone[j] && (j == i || sum + cost[j] <= pack_budget)) sum += cost[j++];
             if ((rc = part(i, j))) return rc;
             i = j;
         }
@@ -348,10 +381,11 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             uint32_t plan[2 * MXP_LDS_DFA_PARTS] = {}, used = 0;
             for (size_t k = 0; k < set.hdr.size() && k < MXP_LDS_DFA_PARTS; k++) {
                 const uint32_t ncls = set.hdr[k].ncls;
-                const uint32_t K = std::min(part_states[k], (MXP_LDS_DFA_WORDS - used) / ncls);
+                const bool w16 = set.hdr[k].kind == MXP_RX_DFA16;  // (two u16 entries per LDS word)
+                const uint32_t K = std::min(part_states[k], (MXP_LDS_DFA_WORDS - used) * (w16 ? 2u : 1u) / ncls);
                 plan[k] = K;
                 plan[MXP_LDS_DFA_PARTS + k] = used;
-                used += K * ncls;
+                used += w16 ? (K * ncls + 1u) / 2u : K * ncls;
                 L->lds_nparts = (uint32_t)k + 1;
             }
             if ((rc = put(L->lds_plan, plan, sizeof plan, "upload lds plan"))) return rc;

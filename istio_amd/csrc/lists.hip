@@ -399,7 +399,8 @@ __device__ __forceinline__ void list_rx_body(const mxp_list_args& A) {
     const uint32_t tid = threadIdx.x;
     for (uint32_t k = 0; k < A.lds_nparts; k++) {
         const mxp_dfa_hdr H = A.rx.hdr[k];
-        const uint32_t words = A.lds_plan[k] * H.ncls, base = A.lds_plan[MXP_LDS_DFA_PARTS + k];
+        const uint32_t ent = A.lds_plan[k] * H.ncls, base = A.lds_plan[MXP_LDS_DFA_PARTS + k];
+        const uint32_t words = H.kind == MXP_RX_DFA16 ? (ent + 1u) / 2u : ent;  // (u16 rows: two a word)
         const uint32_t* src = A.rx.trans + H.trans;
         for (uint32_t i = tid; i < words; i += MXP_LIST_RX_THREADS) TL[base + i] = src[i];
         if (tid < 128u) AL[k * 128u + tid] = A.rx.ascii[H.ascii + tid];

@@ -1034,6 +1034,83 @@ int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states,
     return RX_OK;
 }
 
+uint32_t DfaSetHost::add16(const Dfa& d) {
+    if (d.is_nfa() || d.nstates > 65533u) return add(d);
+    const uint32_t k = add(Dfa());  // (header and alphabet below; no transitions yet)
+    mxp_dfa_hdr& h = hdr[k];
+    h.ncls = d.ncls;
+    h.start = d.start;
+    h.kind = MXP_RX_DFA16;
+    h.trans = (uint32_t)trans.size();
+    const size_t m = d.trans.size();
+    trans.resize(trans.size() + (m + 1) / 2, 0u);
+    uint16_t* t16 = (uint16_t*)(trans.data() + h.trans);
+    for (size_t i = 0; i < m; i++) {
+        const uint32_t v = d.trans[i];
+        t16[i] = v == kDfaAccept ? 0xFFFFu : v == kDfaReject ? 0xFFFEu : (uint16_t)v;
+    }
+    ascii.resize(h.ascii);  // (add() appended the empty DFA's alphabet: replace it)
+    hilo.resize(h.hi);
+    hicls.resize(h.hi);
+    h.hi_n = (uint32_t)d.hi_lo.size();
+    ascii.insert(ascii.end(), d.ascii, d.ascii + 128);
+    hilo.insert(hilo.end(), d.hi_lo.begin(), d.hi_lo.end());
+    hicls.insert(hicls.end(), d.hi_cls.begin(), d.hi_cls.end());
+    return k;
+}
+
+void dfa_renumber_hybrid(Dfa* d, uint32_t bfs_head) {
+    const uint32_t N = d->nstates, C = d->ncls;
+    if (N < 2 || d->is_nfa()) return;
+    std::vector<uint32_t> perm(N, ~0u), order;
+    order.reserve(N);
+    auto target = [&](uint32_t s, uint32_t c) { return d->trans[(size_t)s * C + c]; };
+    // BFS head from the start
+    std::vector<uint32_t> queue{d->start};
+    perm[d->start] = 0;
+    order.push_back(d->start);
+    for (size_t i = 0; i < queue.size() && order.size() < bfs_head; i++)
+        for (uint32_t c = 0; c < C && order.size() < bfs_head; c++) {
+            const uint32_t t = target(queue[i], c);
+            if (t < N && perm[t] == ~0u) {
+                perm[t] = (uint32_t)order.size();
+                order.push_back(t);
+                queue.push_back(t);
+            }
+        }
+    // depth-first preorder below the head: the head's children in order, each subtree contiguous
+    std::vector<uint32_t> stack;
+    for (size_t i = order.size(); i-- > 0;)
+        for (uint32_t c = C; c-- > 0;) {
+            const uint32_t t = target(order[i], c);
+            if (t < N && perm[t] == ~0u) stack.push_back(t);
+        }
+    while (!stack.empty()) {
+        const uint32_t s = stack.back();
+        stack.pop_back();
+        if (perm[s] != ~0u) continue;
+        perm[s] = (uint32_t)order.size();
+        order.push_back(s);
+        for (uint32_t c = C; c-- > 0;) {
+            const uint32_t t = target(s, c);
+            if (t < N && perm[t] == ~0u) stack.push_back(t);
+        }
+    }
+    for (uint32_t s = 0; s < N; s++)  // (unreachable states keep a place at the end)
+        if (perm[s] == ~0u) {
+            perm[s] = (uint32_t)order.size();
+            order.push_back(s);
+        }
+    std::vector<uint32_t> t2((size_t)N * C);
+    for (uint32_t k = 0; k < N; k++)
+        for (uint32_t c = 0; c < C; c++) {
+            const uint32_t t = target(order[k], c);
+            t2[(size_t)k * C + c] = t < N ? perm[t] : t;
+        }
+    d->trans.swap(t2);
+    d->start = 0;
+}
+
 uint32_t DfaSetHost::add(const Dfa& d) {
     mxp_dfa_hdr h{};
     h.ncls = d.ncls;

@@ -75,6 +75,10 @@ bool dfa_literal_keys(const Dfa& d, uint32_t st, uint32_t max_keys, uint32_t max
 
 // Host stepping of a compiled DFA or NFA (constant folding, tests).
 bool dfa_match_host(const Dfa& d, const std::string& s);
+// Renumber a DFA's states: the first `bfs_head` in BFS order from the start (the levels every
+// subject steps through; what LDS staging copies), the rest in depth-first preorder, so the chain of
+// rows one subject walks below the head lies mostly in adjacent rows.
+void dfa_renumber_hybrid(Dfa* d, uint32_t bfs_head);
 // transitions into decided states -> kDfaReject (ACCEPT unreachable) / kDfaAccept (every continuation
 // accepts); run by the DFA builder
 void fold_dead_states(Dfa* d);
@@ -93,6 +97,7 @@ struct DfaSetHost {
     std::vector<uint32_t> hilo;
     std::vector<uint16_t> hicls;
     uint32_t add(const Dfa& d);  // -> DFA index
+    uint32_t add16(const Dfa& d);  // a DFA of <= 65533 states with u16 transitions (MXP_RX_DFA16)
     bool has_nfa() const {
         for (const auto& h : hdr)
             if (h.kind == MXP_RX_NFA) return true;

@@ -106,6 +106,26 @@ def test_string_symbol_lengths(eng, kind):
         assert bad.size == 0, [(ss[i], int(got[i]), int(want[i])) for i in bad[:5]]
 
 
+def test_regex_list_u16_parts_agree(eng, monkeypatch):
+    """Regex lists as sorted u16 parts with depth-first state numbering (default) against u32 parts in
+    the caller's order (MXP_LIST_RX16=0), with and without LDS staging, and against the restatement
+    on a sample: identical codes."""
+    pats, syms = W.c3_regex_list(n_patterns=4000, n_lookups=60000, seed=45)
+    got = {}
+    for rx16 in ("1", "0"):
+        for lds in ("1", "0"):
+            monkeypatch.setenv("MXP_LIST_RX16", rx16)
+            monkeypatch.setenv("MXP_LIST_LDS", lds)
+            lst = eng.list_create(L.REGEX, pats, [])
+            got[(rx16, lds)] = lst.check(syms)
+    ref = got[("1", "1")]
+    for k, v in got.items():
+        assert np.array_equal(v, ref), k
+    sample = syms[:3000]
+    want = L.codes(L.RegexList(pats, []).found(sample), False)
+    assert np.array_equal(ref[:3000], want)
+
+
 @pytest.mark.parametrize("kind", ["ip", "str"])
 def test_list_paths_agree(eng, monkeypatch, kind):
     """The list kernels' paths give identical codes: IP family regrouping on / off, the register

@@ -86,14 +86,19 @@ def test_wide_nfa_rules_parity(mxp, monkeypatch, flags):
     assert np.array_equal(lst.check(subs[:400]), want_l)
 
 
-def test_regex_list_with_over_budget_patterns(mxp):
+@pytest.mark.parametrize("rx16", ["1", "0"])
+def test_regex_list_with_over_budget_patterns(mxp, monkeypatch, rx16):
+    monkeypatch.setenv("MXP_LIST_RX16", rx16)
     eng = mxp.Engine(0)
     rng = np.random.default_rng(5)
     syms = _nfa_subjects(rng, 3000)
     pats = ["^zz", NFA_PATTERNS[0], "x{3}", NFA_PATTERNS[2], NFA_PATTERNS[7], "^é"]
     lst = eng.list_create(L.REGEX, pats, [])
     parts, nfas = lst.regex_parts()
-    assert nfas >= 2 and parts == nfas + 3  # ^zz | nfa | x{3} | nfa | (nfa) | ^é: NFAs stand alone
+    if rx16 == "0":
+        assert nfas >= 2 and parts == nfas + 3  # ^zz | nfa | x{3} | nfa | (nfa) | ^é: NFAs stand alone
+    else:  # sorted first: DFA patterns side by side share u16 parts; the NFAs stand alone
+        assert nfas >= 2 and nfas + 1 <= parts <= nfas + 3
     want = L.codes(L.RegexList(pats).found(syms), False)
     got = lst.check(syms)
     bad = np.nonzero(got != want)[0]
