@@ -2214,6 +2214,11 @@ void mxp_engine_destroy(mxp_engine* eng) {
     if (!eng) return;
     if (eng->device >= 0) (void)hipSetDevice(eng->device);
     if (eng->pk_host) (void)hipHostFree(eng->pk_host);
+    for (int k = 0; k < mxp_engine::kCopyStreams; k++)
+        if (eng->copy_s[k]) (void)hipStreamDestroy(eng->copy_s[k]);
+    for (int k = 0; k <= mxp_engine::kCopyStreams; k++)
+        if (eng->copy_ev[k]) (void)hipEventDestroy(eng->copy_ev[k]);
+    if (eng->pk_cols_ev) (void)hipEventDestroy(eng->pk_cols_ev);
     for (int k = 0; k < 2; k++) {
         if (eng->bounce_ev[k]) (void)hipEventDestroy(eng->bounce_ev[k]);
         if (eng->bounce[k]) (void)hipHostFree(eng->bounce[k]);
@@ -2694,12 +2699,63 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
 // Synchronous download of `bytes` from device memory into caller memory, ordered after the work
 // already queued on the engine stream.  Small copies go direct; large ones through the pinned
 // bounce pair (DMA of chunk k + 1 beside the parallel host copy of chunk k).
+bool mxp_engine::is_pinned(const void* p) {
+    hipPointerAttribute_t pa;
+    const bool pinned = hipPointerGetAttributes(&pa, p) == hipSuccess && pa.type == hipMemoryTypeHost;
+    (void)hipGetLastError();  // (pageable memory: the query fails)
+    return pinned;
+}
+
+int mxp_engine::download_all(const std::vector<Piece>& pieces, const char* what) {
+    hipError_t e;
+    bool queued = false;
+    for (const Piece& p : pieces) {
+        if (!p.bytes || p.bytes >= (64u << 20) || !is_pinned(p.dst)) continue;
+        if ((e = hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+            return hipfail(e, what);
+        queued = true;
+    }
+    if (queued && (e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, what);
+    for (const Piece& p : pieces) {
+        if (!p.bytes || (p.bytes < (64u << 20) && is_pinned(p.dst))) continue;
+        if (int rc = download(p.dst, p.src, p.bytes, what)) return rc;
+    }
+    return MXP_OK;
+}
+
 int mxp_engine::download(void* dst, const void* dsrc, size_t bytes, const char* what) {
     hipError_t e;
     // caller memory that is pinned (mxp_host_alloc arenas): one DMA straight into it
-    hipPointerAttribute_t pa;
-    const bool pinned = bytes >= (1u << 20) && hipPointerGetAttributes(&pa, dst) == hipSuccess && pa.type == hipMemoryTypeHost;
-    (void)hipGetLastError();  // (pageable memory: the query fails)
+    const bool pinned = bytes >= (1u << 20) && is_pinned(dst);
+    if (pinned && bytes >= (64u << 20)) {
+        // pieces on the engine stream and kCopyStreams more, each after the work queued so far
+        for (int k = 0; k < kCopyStreams; k++)
+            if (!copy_s[k] && (e = hipStreamCreateWithFlags(&copy_s[k], hipStreamNonBlocking)) != hipSuccess) {
+                copy_s[k] = nullptr;
+                return hipfail(e, "copy stream");
+            }
+        for (int k = 0; k <= kCopyStreams; k++)
+            if (!copy_ev[k] && (e = hipEventCreateWithFlags(&copy_ev[k], kOrderEvent)) != hipSuccess) {
+                copy_ev[k] = nullptr;
+                return hipfail(e, "copy event");
+            }
+        if ((e = hipEventRecord(copy_ev[kCopyStreams], stream)) != hipSuccess) return hipfail(e, what);
+        const size_t np = kCopyStreams + 1, piece = ((bytes + np - 1) / np + 4095) & ~(size_t)4095;
+        for (size_t k = 0; k < np; k++) {
+            const size_t off = k * piece;
+            if (off >= bytes) break;
+            const size_t len = std::min(piece, bytes - off);
+            hipStream_t st = k == 0 ? stream : copy_s[k - 1];
+            if (k && (e = hipStreamWaitEvent(st, copy_ev[kCopyStreams], 0)) != hipSuccess) return hipfail(e, what);
+            if ((e = hipMemcpyAsync((uint8_t*)dst + off, (const uint8_t*)dsrc + off, len, hipMemcpyDeviceToHost, st)) !=
+                hipSuccess)
+                return hipfail(e, what);
+        }
+        for (int k = 0; k < kCopyStreams; k++)
+            if ((e = hipStreamSynchronize(copy_s[k])) != hipSuccess) return hipfail(e, what);
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, what);
+        return MXP_OK;
+    }
     if (bytes < (4u << 20) || pinned) {
         if (bytes && (e = hipMemcpyAsync(dst, dsrc, bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
             return hipfail(e, what);
@@ -2749,8 +2805,7 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
     uint32_t kept = std::min(cnt[0], errcap);
     if (kept) {
         last_recs.resize(kept);
-        if ((e = hipMemcpy(last_recs.data(), d_errlog.p, kept * sizeof(mxp_err_rec), hipMemcpyDeviceToHost)) != hipSuccess)
-            return hipfail(e, "download errlog");
+        if (int rc = download(last_recs.data(), d_errlog.p, kept * sizeof(mxp_err_rec), "download errlog")) return rc;
         last_rec_text.assign(kept, -1);
         for (uint32_t i = 0; i < kept; i++)  // (conversion errors print the caller's value: now)
             if (last_recs[i].code >= ERR_CONV_S && last_recs[i].code <= ERR_CONV_D) {

@@ -455,9 +455,34 @@ struct mxp_engine : public mxp::LowerTables {
     // k + 1 overlaps the host threads' copy of chunk k out of pinned memory (a pageable hipMemcpy
     // stages at a fraction of the pinned rate)
     static constexpr size_t kBounce = 32u << 20;
+    // large downloads into pinned caller memory, split over the engine stream and these copy streams
+    // (each piece its own DMA; one copy alone ran at ~36 GB/s on C4's 730 MB of action lists)
+    static constexpr int kCopyStreams = 3;
+    hipStream_t copy_s[kCopyStreams] = {};
+    hipEvent_t copy_ev[kCopyStreams + 1] = {};
+    hipStream_t copy_stream(int k) {  // (created on first use; null on failure, last_error set)
+        if (!copy_s[k]) {
+            hipError_t e = hipStreamCreateWithFlags(&copy_s[k], hipStreamNonBlocking);
+            if (e != hipSuccess) {
+                copy_s[k] = nullptr;
+                hipfail(e, "copy stream");
+            }
+        }
+        return copy_s[k];
+    }
+    hipEvent_t pk_cols_ev = nullptr;  // the device packer's column copies (pack_device.cpp)
     void* bounce[2] = {nullptr, nullptr};
     hipEvent_t bounce_ev[2] = {nullptr, nullptr};
     int download(void* dst, const void* dsrc, size_t bytes, const char* what);
+    // several downloads: those into pinned memory queued together with one synchronisation, the
+    // others through download()
+    struct Piece {
+        void* dst;
+        const void* src;
+        size_t bytes;
+    };
+    int download_all(const std::vector<Piece>& pieces, const char* what);
+    static bool is_pinned(const void* p);
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
 
@@ -492,7 +517,7 @@ struct mxp_engine : public mxp::LowerTables {
     // compact Resolve (resolver.cpp): request error flags instead of the error bitmap, each request's
     // first applicable erroring rule from the error records (sparse pairs scattered into res_err_in),
     // block sums of the device scan of the counts
-    DevBuf res_flags, res_err_in, res_pairs, res_bsum;
+    DevBuf res_flags, res_err_in, res_pairs, res_bsum, res_stash;
     std::vector<uint32_t> res_best;       // [n] host scratch: best resolution rank per request (~0 none)
     // the namespace names of the configuration on the device (mxp_ns_kernel): open-addressing table
     // of content hashes, descriptors, bytes

@@ -306,13 +306,16 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             cost[i] = prc == mxp::RX_OK ? one.nstates : kPatternStates;
             alone[i] = prc != mxp::RX_OK;
         }
-        // u16 parts (MXP_LIST_RX16, default on): union DFAs of at most 65533 states, u16 rows, the
-        // patterns sorted first (any match is a match, so the order is free) so that a part's
+        // u16 parts (MXP_LIST_RX16=1; off by default): union DFAs of at most 65533 states, u16 rows,
+        // the patterns sorted first (any match is a match, so the order is free) so that a part's
         // patterns share their leading literals and a lookup leaves the other parts at their first
         // byte; states numbered BFS for the LDS-staged head, depth-first below it, so one lookup's
-        // chain of rows lies in adjacent rows (tools: profiles/r5_*_ab_c3rx*).
+        // chain of rows lies in adjacent rows.  A host model of the walks halved the cold lines per
+        // lookup (8.8 -> 4.7), but the C3 regex kernel went from 0.094 to 0.267 ms per 1M lookups
+        // (profiles/r5_s4_ab_c3rx_16.log): the walks are bound by their dependent loads, not by
+        // the lines they touch, and four parts walk more steps than one.
         const char* rx16_env = getenv("MXP_LIST_RX16");
-        const bool rx16 = !rx16_env || atoi(rx16_env) != 0;
+        const bool rx16 = rx16_env && atoi(rx16_env) != 0;
         if (rx16) {
             std::vector<size_t> ord(pats.size());
             for (size_t i = 0; i < ord.size(); i++) ord[i] = i;

@@ -162,11 +162,30 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
             if (slot_of[it->second] < 0) slot_of[it->second] = (int32_t)nup++;
         }
     }
+    // the columns on a copy stream of their own: the string passes (interning, the aligned pool) run
+    // while they are in flight, and the column passes wait for their event
+    hipStream_t cs = copy_stream(0);
+    if (!cs) return fail(MXP_ERR_DEVICE, last_error);
+    if (!pk_cols_ev && (e = hipEventCreateWithFlags(&pk_cols_ev, kOrderEvent)) != hipSuccess) {
+        pk_cols_ev = nullptr;
+        return hipfail(e, "columns event");
+    }
+    // (the copy stream starts after the engine stream's earlier work: the previous pack's kernels read
+    // these buffers)
+    if ((e = hipEventRecord(pk_cols_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(cs, pk_cols_ev, 0)) != hipSuccess)
+        return hipfail(e, "columns order");
     for (uint32_t bc = 0; bc < b->n_columns; bc++) {
         if (slot_of[bc] < 0) continue;
-        if ((rc = up(pk_ck[slot_of[bc]], b->kinds[bc], n, "upload kinds"))) return rc;
-        if ((rc = up(pk_cv[slot_of[bc]], b->values[bc], (size_t)n * 8, "upload values"))) return rc;
+        DevBuf* bufs[2] = {&pk_ck[slot_of[bc]], &pk_cv[slot_of[bc]]};
+        const void* src[2] = {b->kinds[bc], b->values[bc]};
+        const size_t bytes[2] = {n, (size_t)n * 8};
+        for (int k = 0; k < 2; k++) {
+            if ((rc = grow(*bufs[k], bytes[k] ? bytes[k] : 16, "upload columns"))) return rc;
+            if (bytes[k] && (e = hipMemcpyAsync(bufs[k]->p, src[k], bytes[k], hipMemcpyHostToDevice, cs)) != hipSuccess)
+                return hipfail(e, "upload columns");
+        }
     }
+    if ((e = hipEventRecord(pk_cols_ev, cs)) != hipSuccess) return hipfail(e, "columns event");
     if (resolver.set) {
         res_id_kind = res_bc[0] >= 0 ? pk_ck[slot_of[res_bc[0]]].as<uint8_t>() : nullptr;
         res_id_val = res_bc[0] >= 0 ? pk_cv[slot_of[res_bc[0]]].as<uint64_t>() : nullptr;
@@ -178,6 +197,7 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     // memory they are DMA; pageable memory is staged by the runtime before hipMemcpyAsync returns)
     if (int rc0 = check_batch(b)) {
         (void)hipStreamSynchronize(s);  // (the copies still read the caller's arrays)
+        (void)hipStreamSynchronize(cs);
         return rc0;
     }
     // ---- arguments
@@ -281,12 +301,28 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         A.out = out;
         return launch(1);
     };
-    if ((rc = launch(0))) return rc;  // BYTES uses
+    // ---- the string and time passes (the columns are still in flight)
     if ((rc = intern(MXP_IK_STR, 0, NS, NS, pk_tab[0], G, pk_sid.as<uint32_t>(), true))) return rc;
+    if ((rc = intern(MXP_IK_TIME, 0, NT, ntime, pk_tab[3], db->GT, pk_tid.as<uint32_t>(), true))) return rc;
+    // (every batch string goes into the overlay pool: batch-local ids name their representative)
+    if ((rc = alloc(db->bstr_off, (size_t)NS * 8, "bstr_off"))) return rc;
+    if ((rc = alloc(db->bstr, sbytes + 8ull * NS + 16, "bstr"))) return rc;
+    if ((e = hipMemsetAsync(db->bstr.p, 0, sbytes + 8ull * NS + 16, s)) != hipSuccess) return hipfail(e, "reset bstr");
+    if ((rc = grow(pk_scan, ((size_t)NS + 1) * 8, "scan"))) return rc;
+    if ((rc = grow(pk_scan_blocks, ((size_t)NS / 1024 + 2) * 8, "scan"))) return rc;
+    if ((rc = grow(pk_scan_max, ((size_t)NS / 1024 + 2) * 4, "scan"))) return rc;
+    A.bdesc = db->bstr_off.as<uint64_t>();
+    A.bblob = db->bstr.as<uint8_t>();
+    A.scan = pk_scan.as<uint64_t>();
+    A.scan_blocks = pk_scan_blocks.as<uint64_t>();
+    A.scan_max = pk_scan_max.as<uint32_t>();
+    if ((rc = launch(4))) return rc;
+    // ---- the column passes, after the columns' copies
+    if ((e = hipStreamWaitEvent(s, pk_cols_ev, 0)) != hipSuccess) return hipfail(e, "columns wait");
+    if ((rc = launch(0))) return rc;  // BYTES uses
     if ((rc = intern(MXP_IK_RAW, 0, NS, nraw, pk_tab[1], db->GB, pk_braw.as<uint32_t>(), true))) return rc;
     if ((rc = intern(MXP_IK_CANON, 0, NS, nraw, pk_tab[2], db->GC, pk_bcan.as<uint32_t>(), true))) return rc;
-    if ((rc = intern(MXP_IK_TIME, 0, NT, ntime, pk_tab[3], db->GT, pk_tid.as<uint32_t>(), true))) return rc;
-    // ---- columns, maps, the batch strings' aligned pool
+    // ---- columns, maps
     if ((rc = alloc(db->kinds, (size_t)ncol * n, "kinds"))) return rc;
     if ((rc = alloc(db->vals, (size_t)ncol * n * 8, "vals"))) return rc;
     A.kinds = db->kinds.as<uint8_t>();
@@ -302,19 +338,6 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         A.omval = db->map_vals.as<uint32_t>();
         if ((rc = launch(3))) return rc;
     }
-    // (every batch string goes into the overlay pool: batch-local ids name their representative)
-    if ((rc = alloc(db->bstr_off, (size_t)NS * 8, "bstr_off"))) return rc;
-    if ((rc = alloc(db->bstr, sbytes + 8ull * NS + 16, "bstr"))) return rc;
-    if ((e = hipMemsetAsync(db->bstr.p, 0, sbytes + 8ull * NS + 16, s)) != hipSuccess) return hipfail(e, "reset bstr");
-    if ((rc = grow(pk_scan, ((size_t)NS + 1) * 8, "scan"))) return rc;
-    if ((rc = grow(pk_scan_blocks, ((size_t)NS / 1024 + 2) * 8, "scan"))) return rc;
-    if ((rc = grow(pk_scan_max, ((size_t)NS / 1024 + 2) * 4, "scan"))) return rc;
-    A.bdesc = db->bstr_off.as<uint64_t>();
-    A.bblob = db->bstr.as<uint8_t>();
-    A.scan = pk_scan.as<uint64_t>();
-    A.scan_blocks = pk_scan_blocks.as<uint64_t>();
-    A.scan_max = pk_scan_max.as<uint32_t>();
-    if ((rc = launch(4))) return rc;
     // ---- ip() / timestamp() pre-tables: parse every string id, intern the parsed values
     if ((rc = alloc(db->ipof, need_ipof ? S * 8 : 0, "ipof"))) return rc;
     if ((rc = alloc(db->tsof, need_tsof ? S * 8 : 0, "tsof"))) return rc;

@@ -75,6 +75,7 @@ __device__ __forceinline__ uint32_t walk(const mxp_resolve_args& A, uint32_t q) 
     }
     uint32_t cnt = 0;
     uint64_t pos = kWrite ? A.sel_off[q] : 0;
+    uint32_t st4[4] = {0u, 0u, 0u, 0u};  // (pass 1: the first four selected rules, for the stash)
     for (uint32_t k = 0; k < nr; k++) {
         const uint32_t lo = ranges[k][0], hi = ranges[k][1];
         if (lo >= hi) continue;
@@ -101,6 +102,13 @@ __device__ __forceinline__ uint32_t walk(const mxp_resolve_args& A, uint32_t q) 
                     for (uint32_t b = sel; b; b &= b - 1) A.sel_rules[pos++] = w * 32u + __builtin_ctz(b);
                 }
             } else {
+                for (uint32_t b = sel, k = cnt; b && k < 4u; b &= b - 1, k++) {
+                    const uint32_t r = w * 32u + __builtin_ctz(b);
+                    st4[0] = k == 0u ? r : st4[0];  // (selects: no dynamically indexed registers)
+                    st4[1] = k == 1u ? r : st4[1];
+                    st4[2] = k == 2u ? r : st4[2];
+                    st4[3] = k == 3u ? r : st4[3];
+                }
                 cnt += __builtin_popcount(sel);
             }
         }
@@ -109,6 +117,7 @@ __device__ __forceinline__ uint32_t walk(const mxp_resolve_args& A, uint32_t q) 
         A.status[q] = MXP_RESOLVE_OK;
         A.err_rule[q] = 0xFFFFFFFFu;
         A.count[q] = cnt;
+        if (A.stash) A.stash[q] = make_uint4(st4[0], st4[1], st4[2], st4[3]);
     }
     return cnt;
 }
@@ -209,7 +218,22 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_offsets_kernel(mxp
 
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_write_kernel(mxp_resolve_args A) {
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
-    if (q < A.n && A.status[q] == MXP_RESOLVE_OK) walk<true>(A, q);
+    if (q >= A.n || A.status[q] != MXP_RESOLVE_OK) return;
+    const uint32_t c = A.count[q];
+    if (A.stash && c <= 4u) {  // the count pass kept them: no second walk of the bitmaps
+        if (!c) return;
+        const uint4 v = A.stash[q];
+        const uint64_t pos = A.sel_off[q];
+        const uint32_t r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; k++)
+            if (k < c) {
+                if (A.ids16) ((uint16_t*)A.sel_rules)[pos + k] = (uint16_t)r[k];
+                else A.sel_rules[pos + k] = r[k];
+            }
+        return;
+    }
+    walk<true>(A, q);
 }
 
 extern "C" __global__ __launch_bounds__(256) void mxp_ns_kernel(mxp_ns_args A) {

@@ -54,4 +54,7 @@ typedef struct mxp_resolve_args {
     uint64_t* sel_off_out;     // [n + 1] (scan pass)
     uint32_t ids16;            // pass 2 writes u16 rule ids (sel_rules as uint16_t*)
     uint32_t err_rank;         // err_in holds resolution ranks (mxp_resolve_first_err_kernel), not rules
+    uint4* stash;              // [n] the count pass's first 4 selected rules of each request (pass 2
+                               // copies them for requests with at most 4, instead of walking the
+                               // bitmap again); nullptr: none
 } mxp_resolve_args;

@@ -275,6 +275,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     const uint32_t grid = (n + 255u) / 256u;
     if ((e = eng->res_bsum.reserve((size_t)grid * 8 + 8)) != hipSuccess) return eng->hipfail(e, "alloc block sums");
     if ((e = d_off.reserve(((size_t)n + 1) * 8)) != hipSuccess) return eng->hipfail(e, "alloc sel_off");
+    if ((e = eng->res_stash.reserve((size_t)n * 16 + 16)) != hipSuccess) return eng->hipfail(e, "alloc stash");
     mxp_resolve_args A;
     memset(&A, 0, sizeof A);
     A.n = n;
@@ -294,7 +295,8 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     A.sel_off_out = d_off.as<uint64_t>();
     A.sel_off = d_off.as<uint64_t>();
     A.ids16 = ids16 ? 1u : 0u;
-    bool collected = !compact;  // (the bitmap path collects its records after the resolve kernels)
+    A.stash = (uint4*)eng->res_stash.p;
+    bool collected = false;  // (records collected after the resolve kernels unless a path needed them first)
     if (compact) {
         // the log's counts: [0] records, [2] class records (synchronises: the evaluation is done)
         uint32_t cnt[4] = {0, 0, 0, 0};
@@ -350,9 +352,10 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     if (!n) {
         sel_off[0] = 0;
     } else {
-        if ((rc = eng->download(status, d_status.p, n, "download status"))) return rc;
-        if ((rc = eng->download(err_rule, d_err_rule.p, (size_t)n * 4, "download err_rule"))) return rc;
-        if ((rc = eng->download(sel_off, d_off.p, ((size_t)n + 1) * 8, "download sel_off"))) return rc;
+        const std::vector<mxp_engine::Piece> outs = {{status, d_status.p, n},
+                                                     {err_rule, d_err_rule.p, (size_t)n * 4},
+                                                     {sel_off, d_off.p, ((size_t)n + 1) * 8}};
+        if ((rc = eng->download_all(outs, "download resolve outputs"))) return rc;
     }
     eng->trace_mark("resolve kernels + downloads");
     if (!collected) {
