@@ -38,7 +38,15 @@ typedef struct mxp_dfa_set {
     const uint16_t* ascii;
     const uint32_t* hilo;    // ascending non-ASCII range starts
     const uint16_t* hicls;
+    // NFAs wider than MXP_NFA_WIDE_WORDS (mxp_nfa_run_global): thread sets in global memory, one slot
+    // of 2 * nfa_wmax * 64 words per wavefront walking one, claimed in nfa_busy[nfa_nslots]
+    uint64_t* nfa_scratch;
+    uint32_t* nfa_busy;
+    uint32_t nfa_nslots;
+    uint32_t nfa_wmax;
 } mxp_dfa_set;
+// bytes of the global thread-set scratch for NFAs of up to wmax words (0: none needed)
+#define MXP_NFA_SLOT_WORDS(wmax) (2ull * (wmax) * 64ull)
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -166,10 +174,90 @@ __device__ __forceinline__ bool mxp_nfa_run_wide(const mxp_dfa_set& S, const mxp
     }
 }
 
+// Programs wider than 1023 rune instructions (W > MXP_NFA_WIDE_WORDS): the same walk with the thread
+// sets in global memory.  The lanes here claim one slot of the engine's (or list's) scratch for their
+// wavefront -- the first active lane takes a free slot by compare-and-swap and hands it to the
+// others -- lay U and C out word-major with the lane minor (coalesced), and free the slot when all of
+// them are done.  Holders never wait on anything, so a wave that finds every slot taken only spins
+// until one is freed.
+__device__ __noinline__ bool mxp_nfa_run_global(const mxp_dfa_set& S, const mxp_dfa_hdr& H, const uint8_t* s,
+                                                uint32_t n) {
+    const uint64_t* N = (const uint64_t*)(S.trans + H.trans);
+    const uint64_t h0 = N[0];
+    const uint32_t m = (uint32_t)(h0 & 0xFFFF), W = (uint32_t)(h0 >> 16) & 0xFF, nvar = (uint32_t)(h0 >> 24) & 0xFFFF;
+    const uint8_t* var_of = (const uint8_t*)(N + 1);
+    const uint64_t* ACC = N + MXP_NFA_HDR_WORDS;
+    const uint64_t* CL = ACC + (uint64_t)(H.ncls - 1) * W;
+    const uint64_t* CLS = CL + (uint64_t)m * nvar * W;
+    const uint16_t* asc = S.ascii + H.ascii;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t act = __ballot(1);
+    const uint32_t leader = (uint32_t)__builtin_ctzll(act);
+    uint32_t slot = 0;
+    if (lane == leader) {
+        uint32_t i = (blockIdx.x * 97u + (threadIdx.x >> 6) * 31u) % S.nfa_nslots;
+        while (atomicCAS(S.nfa_busy + i, 0u, 1u) != 0u) i = i + 1u == S.nfa_nslots ? 0u : i + 1u;
+        slot = i;
+    }
+    slot = (uint32_t)__shfl((int)slot, (int)leader, 64);
+    uint64_t* U = S.nfa_scratch + (uint64_t)slot * MXP_NFA_SLOT_WORDS(S.nfa_wmax) + lane;
+    uint64_t* C = U + (uint64_t)S.nfa_wmax * 64u;
+    for (uint32_t w = 0; w < W; w++) U[w * 64u] = 0;
+    bool result = false, begin = true, prev_nl = false, prev_word = false;
+    uint32_t i = 0;
+    for (;;) {
+        const bool end = i >= n;
+        uint32_t r = 0, width = 1, cls = 0;
+        if (!end) {
+            const uint32_t c0 = s[i];
+            if (c0 < 0x80) {
+                r = c0;
+                cls = asc[c0];
+            } else {
+                r = mxp_decode_hi(s, i, n, c0, &width);
+                cls = mxp_hi_class(S, H, r);
+            }
+        }
+        uint32_t f = 0;
+        if (begin) f |= 4u | 1u;
+        if (prev_nl) f |= 1u;
+        if (end) f |= 8u | 2u;
+        if (!end && r == '\n') f |= 2u;
+        f |= (prev_word != (!end && mxp_rx_word(r))) ? 16u : 32u;
+        const uint32_t v = var_of[f];
+        for (uint32_t w = 0; w < W; w++) C[w * 64u] = CLS[(uint64_t)v * W + w];
+        for (uint32_t w = 0; w < W; w++) {
+            uint64_t bits = U[w * 64u];
+            while (bits) {
+                const uint32_t j = w * 64u + (uint32_t)__builtin_ctzll(bits);
+                bits &= bits - 1;
+                const uint64_t* q = CL + ((uint64_t)j * nvar + v) * W;
+                for (uint32_t x = 0; x < W; x++) C[x * 64u] |= q[x];
+            }
+        }
+        if ((C[(m >> 6) * 64u] >> (m & 63)) & 1u) {
+            result = true;
+            break;
+        }
+        if (end) break;
+        const uint64_t* a = ACC + (uint64_t)cls * W;
+        for (uint32_t w = 0; w < W; w++) U[w * 64u] = C[w * 64u] & a[w];
+        begin = false;
+        prev_nl = r == '\n';
+        prev_word = mxp_rx_word(r);
+        i += width;
+    }
+    // (every lane that came in is here again) the slot goes back
+    __threadfence();
+    if (lane == leader) atomicExch(S.nfa_busy + slot, 0u);
+    return result;
+}
+
 __device__ __forceinline__ bool mxp_nfa_run(const mxp_dfa_set& S, const mxp_dfa_hdr& H, const uint8_t* s, uint32_t n) {
     const uint64_t* N = (const uint64_t*)(S.trans + H.trans);
     const uint64_t h0 = N[0];
     const uint32_t m = (uint32_t)(h0 & 0xFFFF), W = (uint32_t)(h0 >> 16) & 0xFF, nvar = (uint32_t)(h0 >> 24) & 0xFFFF;
+    if (W > MXP_NFA_WIDE_WORDS) return mxp_nfa_run_global(S, H, s, n);
     if (W > MXP_NFA_MAX_WORDS) return mxp_nfa_run_wide(S, H, s, n);
     const uint8_t* var_of = (const uint8_t*)(N + 1);
     const uint64_t* ACC = N + MXP_NFA_HDR_WORDS;

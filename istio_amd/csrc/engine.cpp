@@ -433,6 +433,7 @@ int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
         if ((rc = put(d_rule_off, off.data(), off.size() * 4, "upload rule_off"))) return rc;
         if ((rc = put(d_rconst, rconst.data(), rconst.size() * 8, "upload rconst"))) return rc;
         rx_nfa = rx_set.has_nfa();
+        rx_wmax = rx_set.nfa_wmax();
         if ((rc = put(d_rx_hdr, rx_set.hdr.data(), rx_set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
         if ((rc = put(d_rx_trans, rx_set.trans.data(), rx_set.trans.size() * 4, "upload rx trans"))) return rc;
         if ((rc = put(d_rx_ascii, rx_set.ascii.data(), rx_set.ascii.size() * 2, "upload rx ascii"))) return rc;
@@ -1457,6 +1458,7 @@ int mxp_engine::pack_on_host(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = up(db->bstr, oblob.data(), oblob.size(), "upload bstr"))) return rc;
     if ((rc = up(db->rxof, rxof.data(), rxof.size() * 4, "upload rxof"))) return rc;
     db->rx_nfa = rxb.has_nfa();
+    db->rx_wmax = rxb.nfa_wmax();
     if ((rc = up(db->rx_hdr, rxb.hdr.data(), rxb.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
     if ((rc = up(db->rx_trans, rxb.trans.data(), rxb.trans.size() * 4, "upload rx trans"))) return rc;
     if ((rc = up(db->rx_ascii, rxb.ascii.data(), rxb.ascii.size() * 2, "upload rx ascii"))) return rc;
@@ -1741,6 +1743,12 @@ int mxp_engine::launch_body(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, ui
     if (mask && (rc = vt_prepare(db, *P))) return rc;
     mxp_kargs A;
     fill_args(&A, db, *P);
+    // NFAs wider than the private-memory walk: the global thread-set scratch (dfa_dev.h)
+    const uint32_t wmax = std::max(rx_wmax, db ? db->rx_wmax : 0u);
+    if (wmax > MXP_NFA_WIDE_WORDS) {
+        if ((rc = nfa_scratch.ensure(wmax))) return fail(rc, "NFA thread-set scratch");
+        for (mxp_dfa_set* S : {&A.rx, &A.rx_batch}) nfa_scratch.set(S);
+    }
     A.req_err = req_err_out;
     A.hits_gate = hits_gate_out;
     A.hits = d_vals ? nullptr : d_hits;

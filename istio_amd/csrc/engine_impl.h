@@ -138,6 +138,33 @@ struct DevBuf {
     }
 };
 
+// Global-memory thread sets of the NFAs wider than the private-memory walk (dfa_dev.h
+// mxp_nfa_run_global): slots of MXP_NFA_SLOT_WORDS(wmax) words, one per wavefront walking such an
+// NFA, claimed through busy flags; at most 512 MB, between 64 and 2048 slots.
+struct NfaScratch {
+    DevBuf words, busy;
+    uint32_t wmax = 0, nslots = 0;
+    int ensure(uint32_t w) {
+        if (w <= wmax) return 0;
+        const uint64_t slot_bytes = MXP_NFA_SLOT_WORDS(w) * 8ull;
+        const uint32_t ns = (uint32_t)std::max<uint64_t>(64, std::min<uint64_t>(2048, (512ull << 20) / slot_bytes));
+        if (words.alloc(slot_bytes * ns) != hipSuccess || busy.alloc((size_t)ns * 4) != hipSuccess ||
+            hipMemset(busy.p, 0, (size_t)ns * 4) != hipSuccess) {
+            wmax = nslots = 0;
+            return MXP_ERR_NOMEM;
+        }
+        wmax = w;
+        nslots = ns;
+        return 0;
+    }
+    void set(mxp_dfa_set* S) const {
+        S->nfa_scratch = words.as<uint64_t>();
+        S->nfa_busy = busy.as<uint32_t>();
+        S->nfa_nslots = nslots;
+        S->nfa_wmax = wmax;
+    }
+};
+
 struct TimeKey {
     int64_t s;
     int32_t ns;
@@ -206,6 +233,7 @@ struct mxp_dbatch {
     uint32_t heads_ncol = 0;                          // rows the heads cover (mxp_engine::head_cols)
     DevBuf rxof, rx_hdr, rx_trans, rx_ascii, rx_hilo, rx_hicls;  // run-time regexp patterns
     bool rx_nfa = false;                              // one of them compiled to a bit-parallel NFA
+    uint32_t rx_wmax = 0;                             // the widest one's thread-set words
     StrPool overlay;                                  // batch strings not in the rule set's pool
     StrPool overlay_bytes;                            // batch byte strings not in the rule set's
     std::vector<TimeKey> overlay_times;
@@ -310,6 +338,8 @@ struct mxp_engine : public mxp::LowerTables {
     }
     DevBuf d_rx_hdr, d_rx_trans, d_rx_ascii, d_rx_hilo, d_rx_hicls;
     bool rx_nfa = false;         // some constant pattern compiled to a bit-parallel NFA (kargs.nfa)
+    uint32_t rx_wmax = 0;        // the widest such NFA's thread-set words
+    NfaScratch nfa_scratch;      // global thread sets of NFAs wider than MXP_NFA_WIDE_WORDS
 
     // rule-level tables (one per compile): programs + template code, offsets, constants, strings
     DevBuf d_prog, d_rule_off, d_gstr_off, d_gstr, d_rconst;

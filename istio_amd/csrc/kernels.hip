@@ -462,7 +462,8 @@ __device__ uint32_t run_rule(const mxp_kargs& A, cuint32* P, uint32_t len, uint3
                 const bool bat = op == VM_REGEXD;
                 const mxp_dfa_set S{bat ? A.rx_batch.hdr : A.rx.hdr, bat ? A.rx_batch.trans : A.rx.trans,
                                     bat ? A.rx_batch.ascii : A.rx.ascii, bat ? A.rx_batch.hilo : A.rx.hilo,
-                                    bat ? A.rx_batch.hicls : A.rx.hicls};
+                                    bat ? A.rx_batch.hicls : A.rx.hicls, A.rx.nfa_scratch, A.rx.nfa_busy,
+                                    A.rx.nfa_nslots, A.rx.nfa_wmax};
                 uint32_t dfa = x;
                 uint64_t subj = REG(a);
                 bool run = true;

@@ -35,6 +35,7 @@ struct mxp_list {
     uint32_t n4 = 0, n6 = 0, rx_n = 0, rx_nfa = 0;
     uint32_t lds_nparts = 0;
     DevBuf lds_plan;  // REGEX: [K per staged part][LDS word base per staged part] (lists.h)
+    NfaScratch nfa_scratch;  // REGEX: thread sets of NFA parts wider than the private-memory walk
 };
 
 namespace {
@@ -393,6 +394,8 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             }
             if ((rc = put(L->lds_plan, plan, sizeof plan, "upload lds plan"))) return rc;
         }
+        if (set.nfa_wmax() > MXP_NFA_WIDE_WORDS && L->nfa_scratch.ensure(set.nfa_wmax()))
+            return eng->fail(MXP_ERR_NOMEM, "regex list: NFA thread-set scratch");
         L->rx_n = (uint32_t)set.hdr.size();
         for (const auto& h : set.hdr) L->rx_nfa += h.kind == MXP_RX_NFA ? 1u : 0u;
         L->n_entries = pats.size();
@@ -456,6 +459,7 @@ int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, con
     A.opt = list_opt();
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
+    L->nfa_scratch.set(&A.rx);
     A.codes = d_codes;
     set_lds(A, L);
     hipError_t e = mxp_launch_list(&A, stream ? (hipStream_t)stream : eng->stream);
@@ -507,6 +511,7 @@ int mxp_listentry_check(mxp_engine* eng, const mxp_list* L, int blacklist, const
     A.opt = list_opt();
     A.rx = mxp_dfa_set{L->rx_hdr.as<mxp_dfa_hdr>(), L->rx_trans.as<uint32_t>(), L->rx_ascii.as<uint16_t>(),
                        L->rx_hilo.as<uint32_t>(), L->rx_hicls.as<uint16_t>()};
+    L->nfa_scratch.set(&A.rx);
     A.codes = d_codes.as<int32_t>();
     set_lds(A, L);
     A.vals = dv.as<uint64_t>() + value_rule;

@@ -474,6 +474,7 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         if ((rc = launch(8))) return rc;
     }
     db->rx_nfa = rxb.has_nfa();
+    db->rx_wmax = rxb.nfa_wmax();
     auto upd = [&](DevBuf& d, const void* src_p, size_t bytes, const char* what) -> int {
         if ((rc = alloc(d, bytes, what))) return rc;
         if (bytes && (e = hipMemcpyAsync(d.p, src_p, bytes, hipMemcpyHostToDevice, s)) != hipSuccess)

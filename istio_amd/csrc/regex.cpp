@@ -931,10 +931,6 @@ int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states,
                 pcs.push_back((int32_t)k);
             }
         const uint32_t m = (uint32_t)pcs.size();
-        if (m > kNfaMaxPos) {
-            *err = "DFA exceeds the state budget and the program the NFA width";
-            return RX_TOO_BIG;
-        }
         const uint32_t W = (m + 1 + 63) / 64;
         uint32_t tested = 0;
         for (auto& in : p.ins)
@@ -943,6 +939,10 @@ int regex_compile(const std::vector<std::string>& patterns, uint32_t max_states,
         for (uint32_t b = 0; b < 6; b++)
             if (tested >> b & 1) bits.push_back(b);
         const uint32_t nvar = 1u << bits.size();
+        if (m > kNfaHugePos || ((uint64_t)m + 1 + ncc) * nvar * W * 8 > kNfaMaxBytes) {
+            *err = "DFA exceeds the state budget and the program the NFA width";
+            return RX_TOO_BIG;
+        }
         std::vector<uint64_t> img(MXP_NFA_HDR_WORDS + (size_t)ncc * W + (size_t)(m + 1) * nvar * W, 0);
         img[0] = (uint64_t)m | ((uint64_t)W << 16) | ((uint64_t)nvar << 24);
         uint8_t* var_of = (uint8_t*)&img[1];

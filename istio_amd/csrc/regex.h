@@ -23,6 +23,8 @@
 #include <cstdint>
 #include <string>
 #include <vector>
+#include <cstring>
+#include <algorithm>
 
 namespace mxp {
 
@@ -45,7 +47,11 @@ struct Dfa {
     bool is_nfa() const { return !nfa.empty(); }
 };
 
-constexpr uint32_t kNfaMaxPos = 1023;  // rune instructions (+ the MATCH bit = 1024 bits, MXP_NFA_WIDE_WORDS words)
+constexpr uint32_t kNfaMaxPos = 1023;  // rune instructions walked with private-memory thread sets (MXP_NFA_WIDE_WORDS words)
+// wider programs walk with thread sets in global memory (dfa_dev.h mxp_nfa_run_global), up to the
+// header's 8-bit word count (255 words: 16319 rune instructions) and 1 GiB of closure tables
+constexpr uint32_t kNfaHugePos = 255u * 64u - 1u;
+constexpr uint64_t kNfaMaxBytes = 1ull << 30;
 
 enum RegexStatus { RX_OK = 0, RX_SYNTAX = 1, RX_UNSUPPORTED = 2, RX_TOO_BIG = 3 };
 
@@ -102,6 +108,17 @@ struct DfaSetHost {
         for (const auto& h : hdr)
             if (h.kind == MXP_RX_NFA) return true;
         return false;
+    }
+    // the widest NFA's thread-set words (0 without NFAs)
+    uint32_t nfa_wmax() const {
+        uint32_t w = 0;
+        for (const auto& h : hdr)
+            if (h.kind == MXP_RX_NFA) {
+                uint64_t h0;
+                memcpy(&h0, trans.data() + h.trans, 8);
+                w = std::max(w, (uint32_t)(h0 >> 16) & 0xFFu);
+            }
+        return w;
     }
 };
 

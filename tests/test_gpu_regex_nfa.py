@@ -58,32 +58,36 @@ def test_over_budget_rules_parity(mxp, monkeypatch, flags):
 @pytest.mark.parametrize("flags", ["0", "262144"])
 def test_wide_nfa_rules_parity(mxp, monkeypatch, flags):
     """Over budget and wider than 255 rune instructions (the last refusal of round 3): the wide
-    NFA walk (dfa_dev.h mxp_nfa_run_wide, thread sets in private memory) as a rule constant, through
-    value classes (262144) and as a run-time pattern, against the oracle's Go regexp restatement;
-    a list of such patterns too.  Only programs wider than 1023 rune instructions stay refused."""
+    NFA walks -- private-memory thread sets (dfa_dev.h mxp_nfa_run_wide) up to 1023 rune
+    instructions, global-memory ones (mxp_nfa_run_global) beyond (round 5: the refusal of round 4)
+    -- as rule constants, through value classes (262144) and as run-time patterns, against the
+    oracle's Go regexp restatement; lists of such patterns too.  Only programs wider than 16319 rune
+    instructions (or with closure tables over 1 GiB) stay refused."""
     from test_regex_product import wide_subjects
     monkeypatch.setenv("MXP_DEBUG_FLAGS", flags)
     rng = np.random.default_rng(61)
-    tail = "c" * 260
-    p = "(a|b)*a(a|b){16}" + tail
-    subs = wide_subjects(rng, 1200, tail) + _nfa_subjects(rng, 300)
+    tail, tail2 = "c" * 260, "c" * 1100
+    p, p2 = "(a|b)*a(a|b){16}" + tail, "(a|b)*a(a|b){16}" + tail2
+    subs = wide_subjects(rng, 600, tail) + wide_subjects(rng, 600, tail2) + _nfa_subjects(rng, 300)
     manifest = {"request.path": "STRING", "x": "STRING"}
-    bags = [{"request.path": s, "x": p if i % 2 else "^a"} for i, s in enumerate(subs)]
+    bags = [{"request.path": s, "x": (p, p2, "^a")[i % 3]} for i, s in enumerate(subs)]
     batch = BagBatch.from_bags(bags, names=list(manifest))
     rules = ['"%s".matches(request.path)' % p, 'x.matches(request.path)', 'request.path == "a"',
-             '"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 1100)]
+             '"%s".matches(request.path)' % p2, '"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 16400)]
     eng = mxp.Engine(0)
     eng.set_vocabulary(manifest)
     st = eng.compile(rules)
-    assert (st[:3] == 0).all() and st[3] != 0 and "NFA" in eng.rule_error(3)
+    assert (st[:4] == 0).all() and st[4] != 0 and "NFA" in eng.rule_error(4)
     eng3 = mxp.Engine(0)
     eng3.set_vocabulary(manifest)
-    assert (eng3.compile(rules[:3]) == 0).all()
-    got, want = compare(eng3, oracle.OracleEvaluator(manifest), rules[:3], batch, sample_msgs=50)
+    assert (eng3.compile(rules[:4]) == 0).all()
+    got, want = compare(eng3, oracle.OracleEvaluator(manifest), rules[:4], batch, sample_msgs=50)
     assert 100 < (want[:, 0] == 1).sum() < batch.n - 100
-    lst = eng3.list_create(L.REGEX, ["^zz", p], [])
-    want_l = L.codes(L.RegexList(["^zz", p]).found(subs[:400]), False)
-    assert np.array_equal(lst.check(subs[:400]), want_l)
+    assert 50 < (want[:, 3] == 1).sum() < batch.n - 100  # (the 1100-wide pattern: global thread sets)
+    lst = eng3.list_create(L.REGEX, ["^zz", p, p2], [])
+    sub_l = subs[:300] + subs[600:900]
+    want_l = L.codes(L.RegexList(["^zz", p, p2]).found(sub_l), False)
+    assert np.array_equal(lst.check(sub_l), want_l)
 
 
 @pytest.mark.parametrize("rx16", ["1", "0"])

@@ -25,11 +25,14 @@ MAX_SCRATCH = {"mxp_index_kernel": 56, "mxp_index_dtp_kernel": 24, "mxp_index5_k
                "mxp_index_prof_kernel": 96, "mxp_index_dtp_prof_kernel": 96, "mxp_index_dtp_lite_kernel": 8}
 # the NFA instantiations (launched only for rule sets / lists with over-budget patterns): the wide NFA
 # walk keeps its two 1024-bit thread sets in private memory (dfa_dev.h mxp_nfa_run_wide) rather than
-# 64 VGPRs every NFA kernel would carry
+# 64 VGPRs every NFA kernel would carry; the global-memory walk (mxp_nfa_run_global, a __noinline__
+# call) adds its call frame (368 B measured in round 5)
 # (the referenced-attribute instantiations include the NFA walk too)
-MAX_SCRATCH.update({k: 288 for k in ("mxp_eval_nfa_kernel", "mxp_eval_deep_nfa_kernel", "mxp_index_nfa_kernel",
+MAX_SCRATCH.update({k: 384 for k in ("mxp_eval_nfa_kernel", "mxp_eval_deep_nfa_kernel", "mxp_index_nfa_kernel",
                                      "mxp_vt_eval_nfa_kernel", "mxp_list_nfa_kernel", "mxp_list_rx_nfa_kernel",
                                      "mxp_eval_refs_kernel", "mxp_eval_deep_refs_kernel", "mxp_index_refs_kernel")})
+# (the list NFA kernels keep a second walk state for the pattern loop: 576 B measured in round 5)
+MAX_SCRATCH.update({k: 576 for k in ("mxp_list_nfa_kernel", "mxp_list_rx_nfa_kernel")})
 
 
 def resource_usage(src):

@@ -124,12 +124,12 @@ def wide_subjects(rng, n, tail):
 
 
 def test_nfa_wide_programs(rx):
-    """Over budget and wider than 255 rune instructions: the wide NFA walk (private-memory thread
-    sets, up to 1023 rune instructions) against the oracle; only a program wider than that is
-    refused (-3, err says why)."""
+    """Over budget and wider than 255 rune instructions: the wide NFA walks (private-memory thread
+    sets up to 1023 rune instructions, global-memory ones up to 16319) against the oracle; only a
+    program wider than that is refused (-3, err says why)."""
     import oracle
     rng = np.random.default_rng(19)
-    for tail in ("c" * 260, "cd" * 300 + "e" * 200):
+    for tail in ("c" * 260, "cd" * 300 + "e" * 200, "c" * 1100):
         p = "(a|b)*a(a|b){16}" + tail
         subs = wide_subjects(rng, 60, tail)
         hits = 0
@@ -138,7 +138,7 @@ def test_nfa_wide_programs(rx):
             assert rx(p, sub) == want, (p[:30], sub[:40])
             hits += want[0]
         assert 0 < hits < len(subs)
-    rc, err = rx("(a|b)*a(a|b){16}" + "c" * 1100, "ab")
+    rc, err = rx("(a|b)*a(a|b){16}" + "c" * 16400, "ab")
     assert rc == -3 and "NFA" in err
 
 
@@ -150,7 +150,8 @@ def test_over_budget_rules_compile(libmxp):
     eng.set_vocabulary({"request.path": "STRING"})
     rules = ['"%s".matches(request.path)' % p.replace("\\", "\\\\") for p in NFA_PATTERNS]
     rules.append('"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 260))   # wide NFA: compiles
-    rules.append('"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 1100))  # wider than 1023: refused
+    rules.append('"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 1100))  # global thread sets: compiles
+    rules.append('"(a|b)*a(a|b){16}%s".matches(request.path)' % ("c" * 16400))  # wider than 16319: refused
     st = eng.compile(rules)
     assert (st[:-1] == 0).all(), [eng.rule_error(i) for i in range(len(rules) - 1) if st[i]]
     assert st[-1] != 0 and "NFA" in eng.rule_error(len(rules) - 1)
