@@ -2185,6 +2185,8 @@ int mxp_engine_create(int device, mxp_engine** out) {
     e->device = device;
     if (const char* f = getenv("MXP_DEBUG_FLAGS")) e->debug_flags = (uint32_t)atoi(f);
     if (const char* f = getenv("MXP_TRACE")) e->trace = atoi(f) != 0;
+    if (const char* f = getenv("MXP_D2H_DMA")) e->d2h_dma = atoi(f) != 0;
+    if (const char* f = getenv("MXP_PACK_COLS_BESIDE")) e->pack_cols_beside = atoi(f) != 0;
     if (const char* f = getenv("MXP_DTP")) e->dtp = atoi(f) != 0;
     if (const char* f = getenv("MXP_DTP_CAP")) e->dtp_cap = (uint32_t)std::min(1 << 20, std::max(1, atoi(f)));
     if (const char* f = getenv("MXP_DTP_OVF")) e->dtp_ovf_cap = (uint32_t)std::max(1, atoi(f));
@@ -2224,8 +2226,6 @@ void mxp_engine_destroy(mxp_engine* eng) {
     if (eng->pk_host) (void)hipHostFree(eng->pk_host);
     for (int k = 0; k < mxp_engine::kCopyStreams; k++)
         if (eng->copy_s[k]) (void)hipStreamDestroy(eng->copy_s[k]);
-    for (int k = 0; k <= mxp_engine::kCopyStreams; k++)
-        if (eng->copy_ev[k]) (void)hipEventDestroy(eng->copy_ev[k]);
     if (eng->pk_cols_ev) (void)hipEventDestroy(eng->pk_cols_ev);
     for (int k = 0; k < 2; k++) {
         if (eng->bounce_ev[k]) (void)hipEventDestroy(eng->bounce_ev[k]);
@@ -2561,7 +2561,7 @@ int mxp_hits_device(mxp_engine* eng, const uint32_t* d_match, uint32_t n_request
     return e == hipSuccess ? MXP_OK : eng->hipfail(e, "launch hits");
 }
 
-int mxp_engine::check_batch(const mxp_bag_batch* b) {
+int mxp_engine::check_batch(const mxp_bag_batch* b, int parts) {
     if (!b) return MXP_ERR_ARG;
     const uint64_t n = b->n_requests, NS = b->n_strings, NT = b->n_times, NM = b->n_maps;
     auto bad = [&](const std::string& what) { return fail(MXP_ERR_ARG, "malformed batch: " + what); };
@@ -2600,7 +2600,7 @@ int mxp_engine::check_batch(const mxp_bag_batch* b) {
         return f;
     };
     // string offsets: non-decreasing, every string < 16 MiB (the pools' descriptor limit)
-    if (NS) {
+    if (NS && (parts & kCheckStrings)) {
         mxp::par_for(NS, 1u << 16, [&](uint64_t i0, uint64_t i1, unsigned w) {
             const uint64_t* o = b->str_offsets;
             for (uint64_t i = i0; i < i1; i++) {
@@ -2612,39 +2612,47 @@ int mxp_engine::check_batch(const mxp_bag_batch* b) {
         if (const Bad* f = first()) return bad(f->what);
         if (b->str_offsets[NS] && !b->str_bytes) return bad("str_bytes is NULL");
     }
-    for (uint32_t c : use) {
-        const uint8_t* k = b->kinds[c];
-        const uint64_t* v = b->values[c];
-        const std::string nm(b->column_names[c]);
+    // columns: every used column over each slice of requests in one parallel pass, branch-free
+    // (a kind's id limit from a table: ~0 for kinds without an id, 0 for kinds past MXP_OTHER); a
+    // slice with a failure is rescanned for its message
+    uint64_t lim_of[256];
+    for (int kd = 0; kd < 256; kd++) lim_of[kd] = 0;
+    for (int kd : {MXP_ABSENT, MXP_INT64, MXP_DOUBLE, MXP_BOOL, MXP_DURATION}) lim_of[kd] = ~0ull;
+    for (int kd : {MXP_STRING, MXP_BYTES, MXP_OTHER}) lim_of[kd] = NS;
+    lim_of[MXP_TIMESTAMP] = NT;
+    lim_of[MXP_STRING_MAP] = NM;
+    if (!(parts & kCheckColumns)) return MXP_OK;
+    if (!use.empty())
         mxp::par_for(n, 1u << 16, [&](uint64_t q0, uint64_t q1, unsigned w) {
-            bool maps = false;  // (one store of the shared flag per slice: no cache-line ping-pong)
-            struct Flag {
-                bool& m;
-                std::atomic<bool>& out;
-                ~Flag() {
-                    if (m) out.store(true, std::memory_order_relaxed);
+            bool maps = false;
+            for (uint32_t c : use) {
+                const uint8_t* k = b->kinds[c];
+                const uint64_t* v = b->values[c];
+                bool fail_any = false;
+                uint32_t nmap = 0;
+                for (uint64_t q = q0; q < q1; q++) {
+                    const uint64_t lim = lim_of[k[q]];
+                    fail_any |= (v[q] >= lim) & (lim != ~0ull);
+                    nmap += k[q] == MXP_STRING_MAP;
                 }
-            } flag{maps, map_col};
-            for (uint64_t q = q0; q < q1; q++) {
-                const uint8_t kd = k[q];
-                uint64_t lim = ~0ull;
-                const char* table = "";
-                switch (kd) {
-                case MXP_ABSENT: case MXP_INT64: case MXP_DOUBLE: case MXP_BOOL: case MXP_DURATION: continue;
-                case MXP_STRING: case MXP_BYTES: case MXP_OTHER: lim = NS; table = "n_strings"; break;
-                case MXP_TIMESTAMP: lim = NT; table = "n_times"; break;
-                case MXP_STRING_MAP: lim = NM; table = "n_maps"; maps = true; break;
-                default:
-                    return note(w, q, "column '" + nm + "' request " + std::to_string(q) + ": kind " +
-                                          std::to_string(kd) + " > MXP_OTHER");
+                maps |= nmap != 0;
+                if (!fail_any) continue;
+                const std::string nm(b->column_names[c]);
+                for (uint64_t q = q0; q < q1; q++) {
+                    const uint8_t kd = k[q];
+                    if (kd > MXP_OTHER)
+                        return note(w, q, "column '" + nm + "' request " + std::to_string(q) + ": kind " +
+                                              std::to_string(kd) + " > MXP_OTHER");
+                    if (lim_of[kd] != ~0ull && v[q] >= lim_of[kd]) {
+                        const char* table = kd == MXP_TIMESTAMP ? "n_times" : kd == MXP_STRING_MAP ? "n_maps" : "n_strings";
+                        return note(w, q, "column '" + nm + "' request " + std::to_string(q) + ": id " +
+                                              std::to_string(v[q]) + " >= " + table + " (" + std::to_string(lim_of[kd]) + ")");
+                    }
                 }
-                if (v[q] >= lim)
-                    return note(w, q, "column '" + nm + "' request " + std::to_string(q) + ": id " +
-                                          std::to_string(v[q]) + " >= " + table + " (" + std::to_string(lim) + ")");
             }
+            if (maps) map_col.store(true, std::memory_order_relaxed);  // (once per slice)
         });
-        if (const Bad* f = first()) return bad(f->what);
-    }
+    if (const Bad* f = first()) return bad(f->what);
     // map CSR: offsets non-decreasing, key / value ids < n_strings (read when a map is)
     if (NM && (map_col.load() || need_maps || !vcols.empty())) {
         const uint64_t* mo = b->map_offsets;
@@ -2705,27 +2713,41 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
 }
 
 // Synchronous download of `bytes` from device memory into caller memory, ordered after the work
-// already queued on the engine stream.  Small copies go direct; large ones through the pinned
-// bounce pair (DMA of chunk k + 1 beside the parallel host copy of chunk k).
-bool mxp_engine::is_pinned(const void* p) {
+// already queued on the engine stream.  Into pinned memory: a shader copy (mxp_d2h_copy_kernel,
+// ~54 GB/s on the box against ~30 GB/s for the copy engine's DMA; MXP_D2H_DMA=1 keeps the DMA);
+// into pageable memory: small copies direct, larger ones through the pinned bounce pair (chunk
+// k + 1 copied beside the parallel host copy of chunk k).
+bool mxp_engine::is_pinned(const void* p) { return host_dev_ptr(p) != nullptr; }
+
+// the device address of pinned host memory at p (nullptr: pageable)
+void* mxp_engine::host_dev_ptr(const void* p) {
     hipPointerAttribute_t pa;
-    const bool pinned = hipPointerGetAttributes(&pa, p) == hipSuccess && pa.type == hipMemoryTypeHost;
+    const bool ok = hipPointerGetAttributes(&pa, p) == hipSuccess && pa.type == hipMemoryTypeHost &&
+                    pa.hostPointer != nullptr && pa.devicePointer != nullptr && (const char*)p >= (const char*)pa.hostPointer;
     (void)hipGetLastError();  // (pageable memory: the query fails)
-    return pinned;
+    // (the pair names the same byte, whether the runtime reports it at p or at the allocation's base)
+    return ok ? (void*)((char*)pa.devicePointer + ((const char*)p - (const char*)pa.hostPointer)) : nullptr;
+}
+
+// one device -> pinned-host copy queued on the engine stream (hd: host_dev_ptr of dst)
+hipError_t mxp_engine::queue_d2h(void* dst, void* hd, const void* dsrc, size_t bytes) {
+    if (!bytes) return hipSuccess;
+    if (d2h_dma || bytes < kShaderCopyMin) return hipMemcpyAsync(dst, dsrc, bytes, hipMemcpyDeviceToHost, stream);
+    return mxp_launch_d2h_copy(hd, dsrc, bytes, stream);
 }
 
 int mxp_engine::download_all(const std::vector<Piece>& pieces, const char* what) {
     hipError_t e;
     bool queued = false;
     for (const Piece& p : pieces) {
-        if (!p.bytes || p.bytes >= (64u << 20) || !is_pinned(p.dst)) continue;
-        if ((e = hipMemcpyAsync(p.dst, p.src, p.bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-            return hipfail(e, what);
+        void* hd = p.bytes ? host_dev_ptr(p.dst) : nullptr;
+        if (!hd) continue;
+        if ((e = queue_d2h(p.dst, hd, p.src, p.bytes)) != hipSuccess) return hipfail(e, what);
         queued = true;
     }
     if (queued && (e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, what);
     for (const Piece& p : pieces) {
-        if (!p.bytes || (p.bytes < (64u << 20) && is_pinned(p.dst))) continue;
+        if (!p.bytes || is_pinned(p.dst)) continue;
         if (int rc = download(p.dst, p.src, p.bytes, what)) return rc;
     }
     return MXP_OK;
@@ -2733,43 +2755,21 @@ int mxp_engine::download_all(const std::vector<Piece>& pieces, const char* what)
 
 int mxp_engine::download(void* dst, const void* dsrc, size_t bytes, const char* what) {
     hipError_t e;
-    // caller memory that is pinned (mxp_host_alloc arenas): one DMA straight into it
-    const bool pinned = bytes >= (1u << 20) && is_pinned(dst);
-    if (pinned && bytes >= (64u << 20)) {
-        // pieces on the engine stream and kCopyStreams more, each after the work queued so far
-        for (int k = 0; k < kCopyStreams; k++)
-            if (!copy_s[k] && (e = hipStreamCreateWithFlags(&copy_s[k], hipStreamNonBlocking)) != hipSuccess) {
-                copy_s[k] = nullptr;
-                return hipfail(e, "copy stream");
-            }
-        for (int k = 0; k <= kCopyStreams; k++)
-            if (!copy_ev[k] && (e = hipEventCreateWithFlags(&copy_ev[k], kOrderEvent)) != hipSuccess) {
-                copy_ev[k] = nullptr;
-                return hipfail(e, "copy event");
-            }
-        if ((e = hipEventRecord(copy_ev[kCopyStreams], stream)) != hipSuccess) return hipfail(e, what);
-        const size_t np = kCopyStreams + 1, piece = ((bytes + np - 1) / np + 4095) & ~(size_t)4095;
-        for (size_t k = 0; k < np; k++) {
-            const size_t off = k * piece;
-            if (off >= bytes) break;
-            const size_t len = std::min(piece, bytes - off);
-            hipStream_t st = k == 0 ? stream : copy_s[k - 1];
-            if (k && (e = hipStreamWaitEvent(st, copy_ev[kCopyStreams], 0)) != hipSuccess) return hipfail(e, what);
-            if ((e = hipMemcpyAsync((uint8_t*)dst + off, (const uint8_t*)dsrc + off, len, hipMemcpyDeviceToHost, st)) !=
-                hipSuccess)
-                return hipfail(e, what);
-        }
-        for (int k = 0; k < kCopyStreams; k++)
-            if ((e = hipStreamSynchronize(copy_s[k])) != hipSuccess) return hipfail(e, what);
+    if (!bytes) return MXP_OK;
+    // caller memory that is pinned (mxp_host_alloc arenas): straight into it
+    if (void* hd = bytes >= kShaderCopyMin ? host_dev_ptr(dst) : nullptr) {
+        if ((e = queue_d2h(dst, hd, dsrc, bytes)) != hipSuccess) return hipfail(e, what);
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, what);
         return MXP_OK;
     }
-    if (bytes < (4u << 20) || pinned) {
-        if (bytes && (e = hipMemcpyAsync(dst, dsrc, bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess)
-            return hipfail(e, what);
+    if (bytes < (64u << 10)) {
+        if ((e = hipMemcpyAsync(dst, dsrc, bytes, hipMemcpyDeviceToHost, stream)) != hipSuccess) return hipfail(e, what);
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, what);
         return MXP_OK;
     }
+    // (from 64 KiB on, pageable memory goes through the bounce buffers: a pageable hipMemcpy of C2's
+    // 214 KB of error records took 0.55 ms)
+    void* bounce_d[2] = {nullptr, nullptr};
     for (int k = 0; k < 2; k++) {
         if (!bounce[k] && (e = hipHostMalloc(&bounce[k], kBounce, hipHostMallocDefault)) != hipSuccess) {
             bounce[k] = nullptr;
@@ -2779,11 +2779,13 @@ int mxp_engine::download(void* dst, const void* dsrc, size_t bytes, const char* 
             bounce_ev[k] = nullptr;
             return hipfail(e, "bounce event");
         }
+        bounce_d[k] = host_dev_ptr(bounce[k]);
+        if (!bounce_d[k]) return fail(MXP_ERR_DEVICE, "bounce buffer not mapped");
     }
     const size_t nchunk = (bytes + kBounce - 1) / kBounce;
     auto issue = [&](size_t c) -> hipError_t {
         const size_t off = c * kBounce, len = std::min(kBounce, bytes - off);
-        hipError_t r = hipMemcpyAsync(bounce[c & 1], (const uint8_t*)dsrc + off, len, hipMemcpyDeviceToHost, stream);
+        hipError_t r = queue_d2h(bounce[c & 1], bounce_d[c & 1], (const uint8_t*)dsrc + off, len);
         return r == hipSuccess ? hipEventRecord(bounce_ev[c & 1], stream) : r;
     };
     for (size_t c = 0; c < std::min<size_t>(2, nchunk); c++)
@@ -2806,8 +2808,10 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
     if ((e = hipMemcpyAsync(cnt, d_errcount.p, 16, hipMemcpyDeviceToHost, stream)) != hipSuccess)
         return hipfail(e, "download errcount");
     if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, "eval sync");
+    trace_mark("  errors: counts");
     last_error_count = (uint64_t)cnt[0] + cnt[1];
     clear_errors();
+    trace_mark("  errors: clear");
     err_windows.clear();
     errors_complete = cnt[0] <= errcap;
     uint32_t kept = std::min(cnt[0], errcap);
@@ -2821,6 +2825,7 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
                 last_rec_texts.push_back(format_error(batch, db.get(), last_recs[i]));
             }
     }
+    trace_mark("  errors: records");
     if (cnt[2]) {
         int rc = expand_class_errors(batch, db.get(), cnt[2], errcap > kept ? errcap - kept : 0u);
         if (rc) return rc;
@@ -2843,8 +2848,10 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
             }
         });
     }
+    trace_mark("  errors: map texts");
     recycle(last_db.release());  // (the previous batch's blocks: to the bin, not hipFree)
     last_db = std::move(db);
+    trace_mark("  errors: recycle");
     return MXP_OK;
 }
 

@@ -34,6 +34,7 @@ static constexpr unsigned kOrderEvent = hipEventDisableTiming | hipEventDisableS
 
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
+extern "C" hipError_t mxp_launch_d2h_copy(void* dst, const void* src, uint64_t n, hipStream_t s);
 extern "C" hipError_t mxp_launch_vtd_final(const mxp_kargs* args, const mxp_vtd_final_args* f, hipStream_t s);
 extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, const uint32_t* cols, uint32_t nrow, uint4* heads, hipStream_t s);
 extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s);
@@ -481,15 +482,25 @@ struct mxp_engine : public mxp::LowerTables {
         if (trace_t > 0 && what) fprintf(stderr, "mxp trace %-28s %9.3f ms\n", what, (t - trace_t) * 1e3);
         trace_t = t;
     }
-    // large device -> caller-memory downloads through two pinned bounce buffers: the DMA of chunk
+    // host time since the last trace_mark, without synchronising (where the host is in an upload)
+    void trace_host(const char* what) const {
+        if (!trace || trace_t <= 0) return;
+        fprintf(stderr, "mxp trace   (host) %-21s %9.3f ms\n", what, (mxp::now_seconds() - trace_t) * 1e3);
+    }
+    // the batch's columns copied beside its strings (MXP_PACK_COLS_BESIDE=1) instead of after them
+    // (the default: the string passes then run while the columns copy)
+    bool pack_cols_beside = false;
+    // large device -> pageable caller memory through two pinned bounce buffers: the copy of chunk
     // k + 1 overlaps the host threads' copy of chunk k out of pinned memory (a pageable hipMemcpy
     // stages at a fraction of the pinned rate)
     static constexpr size_t kBounce = 32u << 20;
-    // large downloads into pinned caller memory, split over the engine stream and these copy streams
-    // (each piece its own DMA; one copy alone ran at ~36 GB/s on C4's 730 MB of action lists)
-    static constexpr int kCopyStreams = 3;
+    // downloads into pinned memory from this size on are shader copies (mxp_d2h_copy_kernel), unless
+    // d2h_dma (MXP_D2H_DMA=1: the copy engine's DMA, ~30 GB/s on the box against ~54)
+    static constexpr size_t kShaderCopyMin = 64u << 10;
+    bool d2h_dma = false;
+    // the device packer's column copies (pack_device.cpp)
+    static constexpr int kCopyStreams = 1;
     hipStream_t copy_s[kCopyStreams] = {};
-    hipEvent_t copy_ev[kCopyStreams + 1] = {};
     hipStream_t copy_stream(int k) {  // (created on first use; null on failure, last_error set)
         if (!copy_s[k]) {
             hipError_t e = hipStreamCreateWithFlags(&copy_s[k], hipStreamNonBlocking);
@@ -513,6 +524,8 @@ struct mxp_engine : public mxp::LowerTables {
     };
     int download_all(const std::vector<Piece>& pieces, const char* what);
     static bool is_pinned(const void* p);
+    static void* host_dev_ptr(const void* p);
+    hipError_t queue_d2h(void* dst, void* hd, const void* dsrc, size_t bytes);
     DevBuf d_errlog, d_errcount;
     uint32_t errcap = 1u << 23;  // error records kept per batch (MXP_ERRCAP); mxp_error_count counts all
 
@@ -719,7 +732,10 @@ struct mxp_engine : public mxp::LowerTables {
     // tables, offsets running backwards, unknown kinds -- so a malformed batch is MXP_ERR_ARG with the
     // first bad field named, never an out-of-range index into a device table (protoBag.go:255-265
     // answers an undefined index with an error too).
-    int check_batch(const mxp_bag_batch* b);
+    // parts: kCheckStrings (the string table), kCheckColumns (columns and maps); the pointer and
+    // name checks always
+    static constexpr int kCheckStrings = 1, kCheckColumns = 2;
+    int check_batch(const mxp_bag_batch* b, int parts = kCheckStrings | kCheckColumns);
     void recycle(mxp_dbatch* db);  // a batch no longer used: its blocks to the bin (mxp_batch_free)
     // pack + launch into fresh device bitmaps (dm, de; dv = Eval registers when non-null)
     // d_req_err: compact error output (per-request flags; de is not written)

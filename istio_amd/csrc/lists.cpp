@@ -554,10 +554,7 @@ int mxp_list_check(mxp_engine* eng, const mxp_list* L, int blacklist, const uint
     int rc = mxp_list_check_device(eng, L, blacklist, d_sym.as<uint8_t>(), d_off.as<uint64_t>(), n, eng->stream,
                                    d_codes.as<int32_t>());
     if (rc) return rc;
-    if ((e = hipMemcpyAsync(codes, d_codes.p, (size_t)n * 4, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-        return eng->hipfail(e, "download codes");
-    if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "list sync");
-    return MXP_OK;
+    return eng->download(codes, d_codes.p, (size_t)n * 4, "download codes");  // (synchronises)
 }
 
 }  // extern "C"

@@ -133,6 +133,17 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         return MXP_OK;
     };
     // ---- the batch as given (scratch of the engine, reused across uploads)
+    hipStream_t cs = copy_stream(0);
+    if (!cs) return fail(MXP_ERR_DEVICE, last_error);
+    if (!pk_cols_ev && (e = hipEventCreateWithFlags(&pk_cols_ev, kOrderEvent)) != hipSuccess) {
+        pk_cols_ev = nullptr;
+        return hipfail(e, "columns event");
+    }
+    // (the copy stream starts after the engine stream's earlier work: the previous pack's kernels read
+    // the column buffers)
+    if (pack_cols_beside &&
+        ((e = hipEventRecord(pk_cols_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(cs, pk_cols_ev, 0)) != hipSuccess))
+        return hipfail(e, "columns order");
     const uint64_t sbytes = NS ? b->str_offsets[NS] : 0;
     if ((rc = up(pk_soff, b->str_offsets, NS ? ((size_t)NS + 1) * 8 : 0, "upload string offsets"))) return rc;
     // (16 bytes of slack: the intern kernel reads strings 8 bytes at a time)
@@ -163,17 +174,12 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         }
     }
     // the columns on a copy stream of their own: the string passes (interning, the aligned pool) run
-    // while they are in flight, and the column passes wait for their event
-    hipStream_t cs = copy_stream(0);
-    if (!cs) return fail(MXP_ERR_DEVICE, last_error);
-    if (!pk_cols_ev && (e = hipEventCreateWithFlags(&pk_cols_ev, kOrderEvent)) != hipSuccess) {
-        pk_cols_ev = nullptr;
-        return hipfail(e, "columns event");
-    }
-    // (the copy stream starts after the engine stream's earlier work: the previous pack's kernels read
-    // these buffers)
-    if ((e = hipEventRecord(pk_cols_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(cs, pk_cols_ev, 0)) != hipSuccess)
+    // while they are in flight, and the column passes wait for their event (the columns' copies start
+    // after the strings', which then have the link to themselves)
+    if (!pack_cols_beside &&
+        ((e = hipEventRecord(pk_cols_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(cs, pk_cols_ev, 0)) != hipSuccess))
         return hipfail(e, "columns order");
+    trace_host("pack: strings queued");
     for (uint32_t bc = 0; bc < b->n_columns; bc++) {
         if (slot_of[bc] < 0) continue;
         DevBuf* bufs[2] = {&pk_ck[slot_of[bc]], &pk_cv[slot_of[bc]]};
@@ -195,11 +201,15 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     }
     // ---- the batch's ids and offsets, checked on the host while the copies run (from pinned caller
     // memory they are DMA; pageable memory is staged by the runtime before hipMemcpyAsync returns)
-    if (int rc0 = check_batch(b)) {
+    trace_host("pack: columns queued");
+    // (the string table now; the columns and maps before the column passes, the string passes
+    // meanwhile on the device)
+    if (int rc0 = check_batch(b, kCheckStrings)) {
         (void)hipStreamSynchronize(s);  // (the copies still read the caller's arrays)
         (void)hipStreamSynchronize(cs);
         return rc0;
     }
+    trace_host("pack: strings checked");
     // ---- arguments
     mxp_pack_args A;
     memset(&A, 0, sizeof A);
@@ -317,7 +327,13 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     A.scan_blocks = pk_scan_blocks.as<uint64_t>();
     A.scan_max = pk_scan_max.as<uint32_t>();
     if ((rc = launch(4))) return rc;
-    // ---- the column passes, after the columns' copies
+    // ---- the column passes, after the columns' check and copies
+    if (int rc0 = check_batch(b, kCheckColumns)) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(cs);
+        return rc0;
+    }
+    trace_host("pack: columns checked");
     if ((e = hipStreamWaitEvent(s, pk_cols_ev, 0)) != hipSuccess) return hipfail(e, "columns wait");
     if ((rc = launch(0))) return rc;  // BYTES uses
     if ((rc = intern(MXP_IK_RAW, 0, NS, nraw, pk_tab[1], db->GB, pk_braw.as<uint32_t>(), true))) return rc;
@@ -486,7 +502,9 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = upd(db->rx_ascii, rxb.ascii.data(), rxb.ascii.size() * 2, "upload rx ascii"))) return rc;
     if ((rc = upd(db->rx_hilo, rxb.hilo.data(), rxb.hilo.size() * 4, "upload rx hilo"))) return rc;
     if ((rc = upd(db->rx_hicls, rxb.hicls.data(), rxb.hicls.size() * 2, "upload rx hicls"))) return rc;
+    trace_host("pack: all queued");
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hipfail(e, "pack sync");
+    trace_host("pack: synchronised");
     if (*(uint32_t*)pk_host >= (1u << 24)) return fail(MXP_ERR_ARG, "batch string longer than 16 MiB");
     // value-class sizing (pack_host's rule): the first MXP_VT_MAX candidates with few classes
     db->vt_mask = 0;

@@ -201,10 +201,7 @@ int mxp_quota_alloc(mxp_engine* eng, mxp_quota* Q, uint32_t n, const uint32_t* k
     int rc = mxp_quota_alloc_device(eng, Q, n, dk.as<uint32_t>(), da.as<int64_t>(), db.as<uint8_t>(), now_ns,
                                     eng->stream, dg.as<int64_t>(), nullptr);
     if (rc) return rc;
-    if ((e = hipMemcpyAsync(granted, dg.p, (size_t)n * 8, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess)
-        return eng->hipfail(e, "quota download");
-    if ((e = hipStreamSynchronize(eng->stream)) != hipSuccess) return eng->hipfail(e, "quota sync");
-    return MXP_OK;
+    return eng->download(granted, dg.p, (size_t)n * 8, "quota download");  // (synchronises)
 }
 
 }  // extern "C"

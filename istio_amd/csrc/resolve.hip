@@ -28,6 +28,8 @@ __device__ __forceinline__ uint32_t range_bits(uint32_t w, uint32_t lo, uint32_t
     return upto & ~((1u << a) - 1u);
 }
 
+constexpr uint32_t kWords = 8;
+
 // Pass 1 (count): the request's status, first erroring rule and number of selected rules (returned);
 // pass 2 (write): its selected rule ids at sel_off[q].
 template <bool kWrite>
@@ -79,37 +81,52 @@ __device__ __forceinline__ uint32_t walk(const mxp_resolve_args& A, uint32_t q) 
     for (uint32_t k = 0; k < nr; k++) {
         const uint32_t lo = ranges[k][0], hi = ranges[k][1];
         if (lo >= hi) continue;
-        for (uint32_t w = lo >> 5; w <= (hi - 1) >> 5; w++) {
-            const uint32_t appl = amask[w] & range_bits(w, lo, hi);
-            if (!appl) continue;
-            const uint64_t at = (uint64_t)w * A.n + q;
-            const uint32_t em = A.empty[w];
-            const uint32_t err = A.err ? (A.err[at] & appl & ~em) : 0u;
-            if (err) {  // the first predicate error fails the request
-                if (!kWrite) {
-                    A.status[q] = MXP_RESOLVE_PRED_ERROR;
-                    A.err_rule[q] = w * 32u + __builtin_ctz(err);
-                    A.count[q] = 0;
-                }
-                return 0;
+        const uint32_t wl = (hi - 1) >> 5;
+        // kWords bitmap words loaded before any is used: the loads of a lane are in flight together
+        // (one at a time, the walk was bound by their latency: 0.77 ms for C2's 1.25 GB of words)
+        for (uint32_t w0 = lo >> 5; w0 <= wl; w0 += kWords) {
+            uint32_t mv[kWords], ev[kWords], ap[kWords];
+#pragma unroll
+            for (uint32_t j = 0; j < kWords; j++) {
+                const uint32_t w = w0 + j;
+                ap[j] = w <= wl ? (amask[w] & range_bits(w, lo, hi)) : 0u;
+                const uint64_t at = (uint64_t)w * A.n + q;
+                mv[j] = ap[j] ? A.match[at] : 0u;
+                ev[j] = ap[j] && A.err ? A.err[at] : 0u;
             }
-            const uint32_t sel = (A.match[at] | em) & appl;
-            if (kWrite) {
-                if (A.ids16) {
-                    uint16_t* out = (uint16_t*)A.sel_rules;
-                    for (uint32_t b = sel; b; b &= b - 1) out[pos++] = (uint16_t)(w * 32u + __builtin_ctz(b));
+#pragma unroll
+            for (uint32_t j = 0; j < kWords; j++) {
+                const uint32_t w = w0 + j;
+                const uint32_t appl = ap[j];
+                if (!appl) continue;
+                const uint32_t em = A.empty[w];
+                const uint32_t err = ev[j] & appl & ~em;
+                if (err) {  // the first predicate error fails the request
+                    if (!kWrite) {
+                        A.status[q] = MXP_RESOLVE_PRED_ERROR;
+                        A.err_rule[q] = w * 32u + __builtin_ctz(err);
+                        A.count[q] = 0;
+                    }
+                    return 0;
+                }
+                const uint32_t sel = (mv[j] | em) & appl;
+                if (kWrite) {
+                    if (A.ids16) {
+                        uint16_t* out = (uint16_t*)A.sel_rules;
+                        for (uint32_t b = sel; b; b &= b - 1) out[pos++] = (uint16_t)(w * 32u + __builtin_ctz(b));
+                    } else {
+                        for (uint32_t b = sel; b; b &= b - 1) A.sel_rules[pos++] = w * 32u + __builtin_ctz(b);
+                    }
                 } else {
-                    for (uint32_t b = sel; b; b &= b - 1) A.sel_rules[pos++] = w * 32u + __builtin_ctz(b);
+                    for (uint32_t b = sel, k = cnt; b && k < 4u; b &= b - 1, k++) {
+                        const uint32_t r = w * 32u + __builtin_ctz(b);
+                        st4[0] = k == 0u ? r : st4[0];  // (selects: no dynamically indexed registers)
+                        st4[1] = k == 1u ? r : st4[1];
+                        st4[2] = k == 2u ? r : st4[2];
+                        st4[3] = k == 3u ? r : st4[3];
+                    }
+                    cnt += __builtin_popcount(sel);
                 }
-            } else {
-                for (uint32_t b = sel, k = cnt; b && k < 4u; b &= b - 1, k++) {
-                    const uint32_t r = w * 32u + __builtin_ctz(b);
-                    st4[0] = k == 0u ? r : st4[0];  // (selects: no dynamically indexed registers)
-                    st4[1] = k == 1u ? r : st4[1];
-                    st4[2] = k == 2u ? r : st4[2];
-                    st4[3] = k == 3u ? r : st4[3];
-                }
-                cnt += __builtin_popcount(sel);
             }
         }
     }
@@ -338,6 +355,38 @@ extern "C" hipError_t mxp_launch_resolve_first_err(const mxp_resolve_args* a, co
         const uint32_t need = (m + 255u) / 256u;
         hipLaunchKernelGGL(mxp_resolve_first_err_kernel, dim3(need < 4096u ? need : 4096u), dim3(256), 0, s, *a,
                            (const uint4*)recs, m);
+    }
+    return hipGetLastError();
+}
+
+// Device -> pinned host memory by the shader instead of the copy engine: `dst` is the device
+// address of mapped pinned host memory.  On the MI355X box a DMA download runs at ~30 GB/s; 16-byte
+// stores from a kernel reach the link's ~54 GB/s (tools/pcie_probe.hip).  When dst
+// and src share their alignment mod 16 the body moves in 16-byte words (the head and tail bytewise);
+// otherwise bytewise.
+extern "C" __global__ __launch_bounds__(256) void mxp_d2h_copy_kernel(uint8_t* __restrict__ dst,
+                                                                      const uint8_t* __restrict__ src, uint64_t n) {
+    const uint64_t tid = blockIdx.x * 256ull + threadIdx.x, stride = (uint64_t)gridDim.x * 256ull;
+    const uint64_t mis = (uint64_t)(uintptr_t)dst & 15u;
+    if (mis != ((uint64_t)(uintptr_t)src & 15u)) {
+        for (uint64_t i = tid; i < n; i += stride) dst[i] = src[i];
+        return;
+    }
+    const uint64_t head = mis ? (16u - mis < n ? 16u - mis : n) : 0u;
+    const uint64_t words = (n - head) >> 4;
+    if (tid < head) dst[tid] = src[tid];
+    uint4* __restrict__ d16 = (uint4*)(dst + head);
+    const uint4* __restrict__ s16 = (const uint4*)(src + head);
+    for (uint64_t i = tid; i < words; i += stride) d16[i] = s16[i];
+    const uint64_t done = head + (words << 4);
+    if (tid < n - done) dst[done + tid] = src[done + tid];
+}
+
+extern "C" hipError_t mxp_launch_d2h_copy(void* dst, const void* src, uint64_t n, hipStream_t s) {
+    if (n) {
+        const uint64_t need = (n / 16u + 255u) / 256u;
+        const uint32_t grid = (uint32_t)(need < 1024u ? (need ? need : 1u) : 1024u);
+        hipLaunchKernelGGL(mxp_d2h_copy_kernel, dim3(grid), dim3(256), 0, s, (uint8_t*)dst, (const uint8_t*)src, n);
     }
     return hipGetLastError();
 }

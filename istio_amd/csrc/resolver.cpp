@@ -349,6 +349,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     }
     if (n && (e = mxp_launch_resolve(&A, 0, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve");
     if (n && (e = mxp_launch_resolve(&A, 2, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve scan");
+    eng->trace_mark("  resolve: count + scan kernels");
     if (!n) {
         sel_off[0] = 0;
     } else {
