@@ -2746,6 +2746,7 @@ int mxp_engine::download_all(const std::vector<Piece>& pieces, const char* what)
         queued = true;
     }
     if (queued && (e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, what);
+    if (trace && queued) fprintf(stderr, "mxp trace     download_all %s: pinned pieces queued together\n", what);
     for (const Piece& p : pieces) {
         if (!p.bytes || is_pinned(p.dst)) continue;
         if (int rc = download(p.dst, p.src, p.bytes, what)) return rc;
@@ -2757,9 +2758,16 @@ int mxp_engine::download(void* dst, const void* dsrc, size_t bytes, const char* 
     hipError_t e;
     if (!bytes) return MXP_OK;
     // caller memory that is pinned (mxp_host_alloc arenas): straight into it
+    const double t0 = trace ? mxp::now_seconds() : 0.0;
+    auto note = [&](const char* path) {
+        if (trace)
+            fprintf(stderr, "mxp trace     download %-20s %10zu B %s %8.3f ms\n", what, bytes, path,
+                    (mxp::now_seconds() - t0) * 1e3);
+    };
     if (void* hd = bytes >= kShaderCopyMin ? host_dev_ptr(dst) : nullptr) {
         if ((e = queue_d2h(dst, hd, dsrc, bytes)) != hipSuccess) return hipfail(e, what);
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return hipfail(e, what);
+        note(d2h_dma ? "pinned dma" : "pinned shader");
         return MXP_OK;
     }
     if (bytes < (64u << 10)) {
@@ -2798,6 +2806,7 @@ int mxp_engine::download(void* dst, const void* dsrc, size_t bytes, const char* 
         mxp::par_for(len, 1u << 20, [&](uint64_t a, uint64_t b, unsigned) { memcpy(to + a, from + a, b - a); });
         if (c + 2 < nchunk && (e = issue(c + 2)) != hipSuccess) return hipfail(e, what);
     }
+    note("bounce");
     return MXP_OK;
 }
 

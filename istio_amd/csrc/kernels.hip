@@ -2084,6 +2084,97 @@ __device__ __forceinline__ bool head_eq(uint64_t w0, uint64_t w1, const uint8_t*
     return ((w1 ^ ld8a(k + 8)) & ((1ull << ((L - 8u) * 8u)) - 1ull)) == 0ull;
 }
 
+// Prefix (or composite K2) keys of KC consecutive key lengths probed together: the KC hashes, then
+// the KC occupancy words, then the KC first entry pairs, then the KC postings ranges -- each round
+// of loads independent across the lengths, so a wave waits ~3 round trips per KC lengths instead
+// of ~2-3 per length (the waves of C4's lite index kernel were chains of such loads).  A slot
+// whose entry belongs to another key continues its linear probe alone (load factor <= 1/8).
+// Lengths past kc, past the string, or of lanes without a string (sok false) find nothing.
+#ifndef MXP_PROBE_KC
+#define MXP_PROBE_KC 1
+#endif
+constexpr uint32_t KC = MXP_PROBE_KC;
+
+// entry pair (E, K) at `at` against the key of length L: 1 match, 0 another key, -1 empty slot
+__device__ __forceinline__ int entry_check(const mxp_kargs& A, const mxp_hent& E, const mxp_hent& K, uint32_t tag,
+                                           bool comp, uint32_t vlo, uint32_t vhi, uint32_t L, StrRef s, uint32_t hw1,
+                                           bool by_head) {
+    if (E.len == 0) return -1;
+    if (E.khi != tag) return 0;
+    if (comp && (K.klo != vlo || K.khi != vhi)) return 0;
+    if ((E.len >> 24) != min(L, 255u)) return 0;
+    if (L <= (comp ? 12u : 20u)) {  // the key inline (see index_body)
+        const uint64_t k0 = (uint64_t)E.klo | ((uint64_t)(comp ? K.start : K.klo) << 32);
+        const uint64_t k1 = comp ? (uint64_t)K.len : ((uint64_t)K.khi | ((uint64_t)K.start << 32));
+        const uint64_t w0 = by_head ? (uint64_t)s.p : ld8a(s.p);
+        const uint64_t w1 = by_head ? (uint64_t)hw1 : (L > 8u ? ld8a(s.p + 8) : 0ull);
+        const uint64_t w2 = L > 16u ? ld8a(s.p + 16) : 0ull;
+        const uint64_t m0 = L >= 8u ? ~0ull : (1ull << (L * 8u)) - 1ull;
+        const uint64_t m1 = L >= 16u ? ~0ull : L > 8u ? (1ull << ((L - 8u) * 8u)) - 1ull : 0ull;
+        const uint64_t m2 = L > 16u ? (1ull << ((L - 16u) * 8u)) - 1ull : 0ull;
+        return (((w0 ^ k0) & m0) == 0 && ((w1 ^ k1) & m1) == 0 && ((w2 ^ (uint64_t)K.len) & m2) == 0) ? 1 : 0;
+    }
+    const StrRef k = str_of(A, E.klo);
+    return (k.n == L && (by_head ? head_eq((uint64_t)s.p, hw1, k.p, L) : bytes_eq_a(s.p, k.p, L))) ? 1 : 0;
+}
+
+__device__ __forceinline__ void probe_chunk(const mxp_kargs& A, PrefixHash& ph, StrRef s, uint32_t hw1, bool by_head,
+                                            bool sok, bool comp, uint32_t vlo, uint32_t vhi, uint32_t pmask,
+                                            uint32_t poff, uint32_t boff, const uint32_t* Ls, uint32_t kc,
+                                            uint32_t (&st)[KC], uint32_t (&ln)[KC]) {
+    uint32_t slot[KC], tag[KC], L[KC], bw[KC];
+    bool act[KC];
+#pragma unroll
+    for (uint32_t j = 0; j < KC; j++) {
+        L[j] = j < kc ? uni(Ls[j]) : 0u;
+        act[j] = j < kc && sok && L[j] <= s.n;
+        slot[j] = 0u;
+        tag[j] = 0u;
+        if (act[j]) {
+            const uint64_t hf = by_head ? ph.at_head((uint64_t)s.p, hw1, L[j]) : ph.at(s.p, L[j]);
+            slot[j] = (uint32_t)hf & pmask;
+            tag[j] = (uint32_t)(hf >> 32);
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < KC; j++) bw[j] = act[j] && A.hbits ? A.hbits[boff + (slot[j] >> 5)] : ~0u;
+    mxp_hent E[KC], K[KC];
+#pragma unroll
+    for (uint32_t j = 0; j < KC; j++) {
+        act[j] = act[j] && ((bw[j] >> (slot[j] & 31u)) & 1u);
+        if (act[j]) {
+            E[j] = A.hents[poff + 2u * slot[j]];
+            K[j] = A.hents[poff + 2u * slot[j] + 1u];
+        }
+    }
+    uint32_t fi[KC];
+#pragma unroll
+    for (uint32_t j = 0; j < KC; j++) {
+        fi[j] = 0xFFFFFFFFu;
+        if (!act[j]) continue;
+        int r = entry_check(A, E[j], K[j], tag[j], comp, vlo, vhi, L[j], s, hw1, by_head);
+        // (another key in the slot: the rest of the linear probe, this length alone)
+        for (uint32_t sl = (slot[j] + 1u) & pmask; r == 0; sl = (sl + 1u) & pmask) {
+            if (A.hbits && !((A.hbits[boff + (sl >> 5)] >> (sl & 31u)) & 1u)) {
+                r = -1;
+                break;
+            }
+            slot[j] = sl;
+            r = entry_check(A, A.hents[poff + 2u * sl], A.hents[poff + 2u * sl + 1u], tag[j], comp, vlo, vhi, L[j], s,
+                            hw1, by_head);
+        }
+        if (r == 1) fi[j] = poff + 2u * slot[j];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < KC; j++) {
+        st[j] = 0u;
+        ln[j] = 0u;
+        if (fi[j] != 0xFFFFFFFFu) {
+            st[j] = A.hents[fi[j]].start;
+            ln[j] = A.hents[fi[j]].len & 0xFFFFFFu;
+        }
+    }
+}
 
 }  // namespace
 
@@ -2185,6 +2276,9 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
         // probe slots: equality 1; prefix one per key length (shortest first); composite the
         // equality fallback, then one per K2 length
         const uint32_t nslot = final ? 1u : kind == MXP_IX_EQ ? 1u : nplen + (comp ? 1u : 0u);
+#if MXP_PROBE_KC > 1
+        uint32_t cst[KC], cln[KC];  // the current chunk's postings ranges (probe_chunk)
+#endif
         for (uint32_t p = 0; p < nslot; p++) {
             uint32_t start = 0, len = 0;
             const bool eq_slot = kind == MXP_IX_EQ || (comp && p == 0);
@@ -2192,7 +2286,20 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
             } else if (eq_slot) {
                 if (ok && (!comp || !sok)) eq_probe(A, hoff, hmask, v, start, len);
             } else {
-                const uint32_t L = uni(A.plens[plen0 + p - (comp ? 1u : 0u)]);
+                const uint32_t pp = p - (comp ? 1u : 0u);  // (the prefix length's index)
+#if MXP_PROBE_KC > 1
+                // KC lengths at a time (probe_chunk); this length's range from the chunk's registers
+                const uint32_t j = pp % KC;
+                if (j == 0u) probe_chunk(A, ph, s, hw1, by_head, sok, comp, vlo, vhi, pmask, poff, boff,
+                                         A.plens + plen0 + pp, min(KC, nplen - pp), cst, cln);
+#pragma unroll
+                for (uint32_t i = 0; i < KC; i++)
+                    if (i == j) {  // (selects: no dynamically indexed registers)
+                        start = cst[i];
+                        len = cln[i];
+                    }
+#else
+                const uint32_t L = uni(A.plens[plen0 + pp]);
                 // the probe yields the entry's index; its postings range is read after the loop (reading
                 // start / len from the loop's 16-byte entry value was miscompiled at -O3 by this
                 // ROCm 7.2 hipcc: lanes resumed with another entry's range)
@@ -2238,6 +2345,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                     start = A.hents[fi].start;
                     len = A.hents[fi].len & 0xFFFFFFu;
                 }
+#endif
             }
             if (A.flags & 1024u) {  // ablation: probes only (results invalid)
                 if (len) Q.ntrue += start & 1u;
