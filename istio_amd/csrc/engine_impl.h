@@ -91,6 +91,42 @@ extern thread_local const void* g_bin_db;      // the mxp_dbatch under construct
 extern thread_local size_t g_bin_db_size;
 extern thread_local std::vector<std::pair<void*, size_t>>* g_bin_give;
 
+// Page-locked host memory for host vectors the device writes into (download() then copies straight
+// into them: no bounce, no page faults of fresh pages each batch); elements default-initialised, so
+// resize() does not zero what the download overwrites.  Falls back to malloc without a device.
+template <class T>
+struct PinnedAlloc {
+    using value_type = T;
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U>&) {}
+    T* allocate(size_t n) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, n * sizeof(T) + 16, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            p = std::malloc(n * sizeof(T) + 16);
+            if (!p) throw std::bad_alloc();
+        }
+        return (T*)p;
+    }
+    void deallocate(T* p, size_t) {
+        hipPointerAttribute_t pa;
+        const bool pinned = hipPointerGetAttributes(&pa, p) == hipSuccess && pa.type == hipMemoryTypeHost;
+        (void)hipGetLastError();
+        if (pinned) (void)hipHostFree(p);
+        else std::free(p);
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        if constexpr (sizeof...(A) == 0) ::new ((void*)p) U;
+        else ::new ((void*)p) U(std::forward<A>(a)...);
+    }
+    template <class U>
+    bool operator==(const PinnedAlloc<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const PinnedAlloc<U>&) const { return false; }
+};
+
 struct DevBuf {
     void* p = nullptr;
     size_t n = 0;    // bytes asked for
@@ -536,7 +572,7 @@ struct mxp_engine : public mxp::LowerTables {
     // caller's batch is gone by the time a text is asked for); texts asked for, and the records of
     // recomputed windows, are memoized in last_errors.
     std::unordered_map<uint64_t, std::pair<uint32_t, std::string>> last_errors;
-    std::vector<mxp_err_rec> last_recs;
+    std::vector<mxp_err_rec, PinnedAlloc<mxp_err_rec>> last_recs;
     std::vector<int32_t> last_rec_text;          // per record: index into last_rec_texts, or -1 (lazy)
     std::vector<std::string> last_rec_texts;
     std::unordered_map<uint64_t, uint32_t> rec_index;  // key -> record (built on first use)

@@ -1871,7 +1871,7 @@ namespace {
 // kargs.rule_tmpl2, the composite resume point), request.
 #define MXP_IXQ 256u
 #ifndef MXP_LITE_WAVES
-#define MXP_LITE_WAVES 6
+#define MXP_LITE_WAVES 5
 #endif
 __shared__ uint32_t g_ixq[4][MXP_IXQ][2];  // per wave of the index kernel's workgroup
 __device__ __forceinline__ void wave_sync_lds() {
@@ -2089,9 +2089,10 @@ __device__ __forceinline__ bool head_eq(uint64_t w0, uint64_t w1, const uint8_t*
 // of loads independent across the lengths, so a wave waits ~3 round trips per KC lengths instead
 // of ~2-3 per length (the waves of C4's lite index kernel were chains of such loads).  A slot
 // whose entry belongs to another key continues its linear probe alone (load factor <= 1/8).
-// Lengths past kc, past the string, or of lanes without a string (sok false) find nothing.
+// Lengths past kc, past the string, or of lanes without a string (sok false) find nothing.  (The
+// lite kernel's; MXP_LITE_WAVES 5 keeps its registers spill-free.)
 #ifndef MXP_PROBE_KC
-#define MXP_PROBE_KC 1
+#define MXP_PROBE_KC 2
 #endif
 constexpr uint32_t KC = MXP_PROBE_KC;
 
@@ -2191,6 +2192,9 @@ namespace {
 // timing code
 template <bool kRefs, bool kNfa = kRefs, bool kDtp = false, bool kProf = false, bool kLite = false>
 __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[256]) {
+    // chunked prefix probes in the lite kernel only (same-box A/B, profiles/r5_s8_ab_probe_c{2,4}.log:
+    // KC 2 at 5 waves/SIMD C4 0.697 -> 0.691 ms, C2 0.4005 -> 0.3983 ms; KC 4 slower)
+    constexpr bool kChunk = kLite && KC > 1;
     // after the fill (kargs.dtp_gate): the deferred pairs' overflow list OR-ed in, then -- only when
     // that list filled -- every pair again
     if (A.dtp_gate) {
@@ -2276,9 +2280,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
         // probe slots: equality 1; prefix one per key length (shortest first); composite the
         // equality fallback, then one per K2 length
         const uint32_t nslot = final ? 1u : kind == MXP_IX_EQ ? 1u : nplen + (comp ? 1u : 0u);
-#if MXP_PROBE_KC > 1
-        uint32_t cst[KC], cln[KC];  // the current chunk's postings ranges (probe_chunk)
-#endif
+        uint32_t cst[KC], cln[KC];  // the current chunk's postings ranges (probe_chunk; kChunk only)
         for (uint32_t p = 0; p < nslot; p++) {
             uint32_t start = 0, len = 0;
             const bool eq_slot = kind == MXP_IX_EQ || (comp && p == 0);
@@ -2287,7 +2289,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                 if (ok && (!comp || !sok)) eq_probe(A, hoff, hmask, v, start, len);
             } else {
                 const uint32_t pp = p - (comp ? 1u : 0u);  // (the prefix length's index)
-#if MXP_PROBE_KC > 1
+                if constexpr (kChunk) {
                 // KC lengths at a time (probe_chunk); this length's range from the chunk's registers
                 const uint32_t j = pp % KC;
                 if (j == 0u) probe_chunk(A, ph, s, hw1, by_head, sok, comp, vlo, vhi, pmask, poff, boff,
@@ -2298,7 +2300,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                         start = cst[i];
                         len = cln[i];
                     }
-#else
+                } else {
                 const uint32_t L = uni(A.plens[plen0 + pp]);
                 // the probe yields the entry's index; its postings range is read after the loop (reading
                 // start / len from the loop's 16-byte entry value was miscompiled at -O3 by this
@@ -2345,7 +2347,7 @@ __device__ __forceinline__ void index_body(const mxp_kargs& A, uint64_t (*regs)[
                     start = A.hents[fi].start;
                     len = A.hents[fi].len & 0xFFFFFFu;
                 }
-#endif
+                }
             }
             if (A.flags & 1024u) {  // ablation: probes only (results invalid)
                 if (len) Q.ntrue += start & 1u;
