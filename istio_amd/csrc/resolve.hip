@@ -30,6 +30,83 @@ __device__ __forceinline__ uint32_t range_bits(uint32_t w, uint32_t lo, uint32_t
 
 constexpr uint32_t kWords = 8;
 
+// a request's walk state: selected count, write position, the first four selected rules (stash)
+struct WalkState {
+    uint32_t cnt;
+    uint64_t pos;
+    uint32_t st4[4];
+};
+
+// Words [lo >> 5, (hi - 1) >> 5] of the rule range [lo, hi): false when the request fails there
+// (pass 1 records the error).  kWords bitmap words are loaded before any is used, so a lane's loads
+// are in flight together.  kUni: the range is the same for every lane (the default namespace's,
+// a kernel-wide constant), so the masks are scalar loads (both TCP rows, selected per lane) and the
+// bitmap loads depend on no vector load.
+template <bool kWrite, bool kUni>
+__device__ __forceinline__ bool walk_range(const mxp_resolve_args& A, uint32_t q, uint32_t tcp, uint32_t lo, uint32_t hi,
+                                           WalkState& S) {
+    const uint32_t wl = (hi - 1) >> 5;
+    const uint32_t* __restrict__ am_lane = A.amask + (uint64_t)tcp * A.n_words;
+    for (uint32_t w0 = lo >> 5; w0 <= wl; w0 += kWords) {
+        uint32_t mv[kWords], ev[kWords], ap[kWords], emv[kWords];
+        // (the masks of all kWords words first, then all their bitmap loads: a load issued after
+        // another cannot be waited for alone, so interleaving them serialised the bitmap loads)
+#pragma unroll
+        for (uint32_t j = 0; j < kWords; j++) {
+            const uint32_t w = w0 + j;
+            const uint32_t wc = w <= wl ? w : wl;  // (clamped in range)
+            if constexpr (kUni) {
+                const uint32_t a0 = A.amask[wc], a1 = A.amask[A.n_words + wc];
+                ap[j] = w <= wl ? ((tcp ? a1 : a0) & range_bits(w, lo, hi)) : 0u;
+            } else {
+                ap[j] = w <= wl ? (am_lane[wc] & range_bits(w, lo, hi)) : 0u;
+            }
+            emv[j] = A.empty[wc];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kWords; j++) {
+            const uint64_t at = (uint64_t)(w0 + j) * A.n + q;
+            mv[j] = ap[j] ? A.match[at] : 0u;
+            ev[j] = ap[j] && A.err ? A.err[at] : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kWords; j++) {
+            const uint32_t w = w0 + j;
+            const uint32_t appl = ap[j];
+            if (!appl) continue;
+            const uint32_t em = emv[j];
+            const uint32_t err = ev[j] & appl & ~em;
+            if (err) {  // the first predicate error fails the request
+                if (!kWrite) {
+                    A.status[q] = MXP_RESOLVE_PRED_ERROR;
+                    A.err_rule[q] = w * 32u + __builtin_ctz(err);
+                    A.count[q] = 0;
+                }
+                return false;
+            }
+            const uint32_t sel = (mv[j] | em) & appl;
+            if (kWrite) {
+                if (A.ids16) {
+                    uint16_t* out = (uint16_t*)A.sel_rules;
+                    for (uint32_t b = sel; b; b &= b - 1) out[S.pos++] = (uint16_t)(w * 32u + __builtin_ctz(b));
+                } else {
+                    for (uint32_t b = sel; b; b &= b - 1) A.sel_rules[S.pos++] = w * 32u + __builtin_ctz(b);
+                }
+            } else {
+                for (uint32_t b = sel, k = S.cnt; b && k < 4u; b &= b - 1, k++) {
+                    const uint32_t r = w * 32u + __builtin_ctz(b);
+                    S.st4[0] = k == 0u ? r : S.st4[0];  // (selects: no dynamically indexed registers)
+                    S.st4[1] = k == 1u ? r : S.st4[1];
+                    S.st4[2] = k == 2u ? r : S.st4[2];
+                    S.st4[3] = k == 3u ? r : S.st4[3];
+                }
+                S.cnt += __builtin_popcount(sel);
+            }
+        }
+    }
+    return true;
+}
+
 // Pass 1 (count): the request's status, first erroring rule and number of selected rules (returned);
 // pass 2 (write): its selected rule ids at sel_off[q].
 template <bool kWrite>
@@ -62,81 +139,23 @@ __device__ __forceinline__ uint32_t walk(const mxp_resolve_args& A, uint32_t q) 
         }
     }
     const uint32_t tcp = info >> 31;
-    const uint32_t* amask = A.amask + (uint64_t)tcp * A.n_words;
-    uint32_t ranges[2][2];
-    uint32_t nr = 0;
+    WalkState S{0u, kWrite ? A.sel_off[q] : 0ull, {0u, 0u, 0u, 0u}};
     if (A.default_id != MXP_NS_NONE) {
-        ranges[nr][0] = A.ns_lo[A.default_id];
-        ranges[nr][1] = A.ns_hi[A.default_id];
-        nr++;
+        const uint32_t lo = __builtin_amdgcn_readfirstlane(A.ns_lo[A.default_id]);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane(A.ns_hi[A.default_id]);
+        if (lo < hi && !walk_range<kWrite, true>(A, q, tcp, lo, hi, S)) return 0;
     }
     if (ns != MXP_NS_NONE && ns != A.default_id) {
-        ranges[nr][0] = A.ns_lo[ns];
-        ranges[nr][1] = A.ns_hi[ns];
-        nr++;
-    }
-    uint32_t cnt = 0;
-    uint64_t pos = kWrite ? A.sel_off[q] : 0;
-    uint32_t st4[4] = {0u, 0u, 0u, 0u};  // (pass 1: the first four selected rules, for the stash)
-    for (uint32_t k = 0; k < nr; k++) {
-        const uint32_t lo = ranges[k][0], hi = ranges[k][1];
-        if (lo >= hi) continue;
-        const uint32_t wl = (hi - 1) >> 5;
-        // kWords bitmap words loaded before any is used: the loads of a lane are in flight together
-        // (one at a time, the walk was bound by their latency: 0.77 ms for C2's 1.25 GB of words)
-        for (uint32_t w0 = lo >> 5; w0 <= wl; w0 += kWords) {
-            uint32_t mv[kWords], ev[kWords], ap[kWords];
-#pragma unroll
-            for (uint32_t j = 0; j < kWords; j++) {
-                const uint32_t w = w0 + j;
-                ap[j] = w <= wl ? (amask[w] & range_bits(w, lo, hi)) : 0u;
-                const uint64_t at = (uint64_t)w * A.n + q;
-                mv[j] = ap[j] ? A.match[at] : 0u;
-                ev[j] = ap[j] && A.err ? A.err[at] : 0u;
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < kWords; j++) {
-                const uint32_t w = w0 + j;
-                const uint32_t appl = ap[j];
-                if (!appl) continue;
-                const uint32_t em = A.empty[w];
-                const uint32_t err = ev[j] & appl & ~em;
-                if (err) {  // the first predicate error fails the request
-                    if (!kWrite) {
-                        A.status[q] = MXP_RESOLVE_PRED_ERROR;
-                        A.err_rule[q] = w * 32u + __builtin_ctz(err);
-                        A.count[q] = 0;
-                    }
-                    return 0;
-                }
-                const uint32_t sel = (mv[j] | em) & appl;
-                if (kWrite) {
-                    if (A.ids16) {
-                        uint16_t* out = (uint16_t*)A.sel_rules;
-                        for (uint32_t b = sel; b; b &= b - 1) out[pos++] = (uint16_t)(w * 32u + __builtin_ctz(b));
-                    } else {
-                        for (uint32_t b = sel; b; b &= b - 1) A.sel_rules[pos++] = w * 32u + __builtin_ctz(b);
-                    }
-                } else {
-                    for (uint32_t b = sel, k = cnt; b && k < 4u; b &= b - 1, k++) {
-                        const uint32_t r = w * 32u + __builtin_ctz(b);
-                        st4[0] = k == 0u ? r : st4[0];  // (selects: no dynamically indexed registers)
-                        st4[1] = k == 1u ? r : st4[1];
-                        st4[2] = k == 2u ? r : st4[2];
-                        st4[3] = k == 3u ? r : st4[3];
-                    }
-                    cnt += __builtin_popcount(sel);
-                }
-            }
-        }
+        const uint32_t lo = A.ns_lo[ns], hi = A.ns_hi[ns];
+        if (lo < hi && !walk_range<kWrite, false>(A, q, tcp, lo, hi, S)) return 0;
     }
     if (!kWrite) {
         A.status[q] = MXP_RESOLVE_OK;
         A.err_rule[q] = 0xFFFFFFFFu;
-        A.count[q] = cnt;
-        if (A.stash) A.stash[q] = make_uint4(st4[0], st4[1], st4[2], st4[3]);
+        A.count[q] = S.cnt;
+        if (A.stash) A.stash[q] = make_uint4(S.st4[0], S.st4[1], S.st4[2], S.st4[3]);
     }
-    return cnt;
+    return S.cnt;
 }
 
 // sum of v over the 256-thread block (every thread gets it)

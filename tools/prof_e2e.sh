@@ -1,0 +1,19 @@
+#!/bin/bash
+# rocprofv3 kernel-trace summaries of the end-to-end Resolve (tools/e2e_trace.py: mxp_resolve_batch_ex
+# on a pinned host batch into pinned outputs), one process per workload:
+# gpurun_out/$1/kernel_stats_e2e_<w>.csv (the pack, evaluation, resolve and copy kernels of the call).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+out=gpurun_out/$1
+shift
+mkdir -p "$out"
+for w in "$@"; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/e2e_$w" -o run -- \
+        python3 tools/e2e_trace.py --workload $w --reps 3 > "$out/e2e_$w.log" 2>&1
+    rc=$?
+    echo "rocprof e2e $w rc=$rc"
+    [ $rc -ne 0 ] && exit $rc
+    find "$out/e2e_$w" -name "*kernel_stats.csv" -exec cp {} "$out/kernel_stats_e2e_$w.csv" \;
+done
+exit 0
