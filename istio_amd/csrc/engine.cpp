@@ -2186,6 +2186,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_DEBUG_FLAGS")) e->debug_flags = (uint32_t)atoi(f);
     if (const char* f = getenv("MXP_TRACE")) e->trace = atoi(f) != 0;
     if (const char* f = getenv("MXP_D2H_DMA")) e->d2h_dma = atoi(f) != 0;
+    if (const char* f = getenv("MXP_RESOLVE_TILE")) e->resolve_tile = atoi(f) != 0;
     if (const char* f = getenv("MXP_PACK_COLS_BESIDE")) e->pack_cols_beside = atoi(f) != 0;
     if (const char* f = getenv("MXP_DTP")) e->dtp = atoi(f) != 0;
     if (const char* f = getenv("MXP_DTP_CAP")) e->dtp_cap = (uint32_t)std::min(1 << 20, std::max(1, atoi(f)));

@@ -534,6 +534,7 @@ struct mxp_engine : public mxp::LowerTables {
     // d2h_dma (MXP_D2H_DMA=1: the copy engine's DMA, ~30 GB/s on the box against ~54)
     static constexpr size_t kShaderCopyMin = 64u << 10;
     bool d2h_dma = false;
+    bool resolve_tile = true;  // Resolve's default-namespace range walked by resolve_tile (MXP_RESOLVE_TILE)
     // the device packer's column copies (pack_device.cpp)
     static constexpr int kCopyStreams = 1;
     hipStream_t copy_s[kCopyStreams] = {};

@@ -347,7 +347,9 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
             eng->trace_mark("first errors (class records, host)");
         }
     }
-    if (n && (e = mxp_launch_resolve(&A, 0, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve");
+    // (the default namespace's range tiled through LDS: resolve_tile; MXP_RESOLVE_TILE=0 the per-lane walk)
+    const bool tiled = eng->resolve_tile && R.default_id != MXP_NS_NONE;
+    if (n && (e = mxp_launch_resolve(&A, tiled ? 3 : 0, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve");
     if (n && (e = mxp_launch_resolve(&A, 2, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve scan");
     eng->trace_mark("  resolve: count + scan kernels");
     if (!n) {
@@ -375,7 +377,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         const size_t isz = ids16 ? 2 : 4;
         if ((e = d_sel.reserve(total * isz)) != hipSuccess) return eng->hipfail(e, "alloc sel");
         A.sel_rules = d_sel.as<uint32_t>();
-        if ((e = mxp_launch_resolve(&A, 1, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
+        if ((e = mxp_launch_resolve(&A, tiled ? 4 : 1, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
         if ((rc = eng->download(sel_rules, d_sel.p, total * isz, "download sel"))) return rc;
     }
     eng->trace_mark("action lists (gather + download)");

@@ -50,13 +50,16 @@ def test_reference_resolver_table_on_gpu(mxp, case):
 
 # resolution paths: compact (default: error flags + records, device namespaces and scan), the error
 # bitmap (MXP_DEBUG_FLAGS bit 28), records past a tiny log (the compact path falls back to the bitmap),
-# the host packer (host namespaces), u16 rule ids (mxp_resolve_batch_ex)
+# the host packer (host namespaces), u16 rule ids (mxp_resolve_batch_ex), and the per-lane walk of
+# the bitmaps instead of the tiled one (MXP_RESOLVE_TILE=0), with the error bitmap and without
 MODES = {"compact": {}, "bitmap": {"MXP_DEBUG_FLAGS": "268435456"}, "errcap": {"MXP_ERRCAP": "16"},
-         "hostpack": {"MXP_HOST_PACK": "1"}, "u16": {}}
+         "hostpack": {"MXP_HOST_PACK": "1"}, "u16": {}, "lanewalk": {"MXP_RESOLVE_TILE": "0"},
+         "lanewalk_bitmap": {"MXP_RESOLVE_TILE": "0", "MXP_DEBUG_FLAGS": "268435456"}}
 
 
 @pytest.mark.parametrize("seed,mode", [(21, "compact"), (22, "compact"), (21, "bitmap"), (22, "errcap"),
-                                       (21, "hostpack"), (22, "u16")])
+                                       (21, "hostpack"), (22, "u16"), (23, "lanewalk"), (23, "lanewalk_bitmap"),
+                                       (23, "compact"), (23, "bitmap")])
 def test_resolver_random_parity(mxp, monkeypatch, seed, mode):
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
@@ -84,6 +87,32 @@ def test_resolver_random_parity(mxp, monkeypatch, seed, mode):
             else:
                 assert list(sel[q]) == wsel, (q, variety)
     assert seen == {0, 1, 2, 3}
+
+
+@pytest.mark.parametrize("extra", [{}, {"MXP_DEBUG_FLAGS": "268435456"}, {"MXP_ERRCAP": "16"}])
+def test_resolver_tiled_equals_lane_walk(mxp, monkeypatch, extra):
+    """The tiled walk of the default namespace (resolve.hip resolve_tile: 64-word chunks through LDS)
+    over a rule set of several chunks equals the per-lane walk (MXP_RESOLVE_TILE=0), checked above
+    against the oracle: status, first errors, offsets and ids, u32 and u16, for three varieties."""
+    for k, v in extra.items():
+        monkeypatch.setenv(k, v)
+    manifest, rules, conf, batch = W.resolver_workload(n_rules=2700, n_requests=5000, seed=25)
+    got = {}
+    for tile in ("1", "0"):
+        monkeypatch.setenv("MXP_RESOLVE_TILE", tile)
+        eng = mxp.Engine(0)
+        eng.set_vocabulary(manifest)
+        eng.compile(rules)
+        eng.set_resolver(conf["identity_attr"], conf["default_ns"], conf["rule_ns"], conf["variety_mask"],
+                         conf["is_tcp"], conf["empty_match"])
+        got[tile] = [[x.copy() for x in eng.resolve_arrays(batch, v, ids16=u16)] for v in (0, 2, 3)
+                     for u16 in (False, True)]
+        eng.close()
+    for a, b in zip(got["1"], got["0"]):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
+    st, _, off, _ = got["1"][0]
+    assert (st == 0).sum() > 1000 and (st == 3).sum() > 10 and int(off[-1]) > 5000
 
 
 @pytest.mark.parametrize("seed", [23, 24])
