@@ -325,16 +325,16 @@ __device__ __forceinline__ void resolve_tile(const mxp_resolve_args& A) {
     __shared__ uint32_t tm[64][65];  // match words [word of the chunk][request of the tile] (padded row)
     __shared__ uint32_t te[64][65];  // error words (A.err only)
     __shared__ uint64_t s_run[64];   // pass 1: selected so far; pass 2: next write position
-    __shared__ uint32_t s_info[64];  // nsinfo; bit 30 set: the request is not walked (done or failed)
+    __shared__ uint32_t s_info[64];  // nsinfo
+    __shared__ uint32_t s_skip[64];  // 1: the request is not walked (done, failed, or the stash has it)
     __shared__ uint32_t s_st4[64][4];
-    constexpr uint32_t kSkip = 0x40000000u;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t base = blockIdx.x * 64u;
     const uint32_t q = base + lane;
     const uint32_t dlo = __builtin_amdgcn_readfirstlane(A.ns_lo[A.default_id]);
     const uint32_t dhi = __builtin_amdgcn_readfirstlane(A.ns_hi[A.default_id]);
     if (wave == 0) {
-        uint32_t info = kSkip;
+        uint32_t info = 0u, skip = 1u;
         uint64_t run = 0;
         if (q < A.n) {
             const uint32_t in = A.nsinfo[q];
@@ -354,11 +354,13 @@ __device__ __forceinline__ void resolve_tile(const mxp_resolve_args& A) {
                     A.count[q] = 0;
                 } else {
                     info = in;
+                    skip = 0u;
                 }
             } else if (A.status[q] == MXP_RESOLVE_OK) {
                 const uint32_t c = A.count[q];
                 if (!A.stash || c > 4u) {
                     info = in;
+                    skip = 0u;
                     run = A.sel_off[q];
                 } else if (c) {  // the stash has them
                     const uint4 v = A.stash[q];
@@ -374,6 +376,7 @@ __device__ __forceinline__ void resolve_tile(const mxp_resolve_args& A) {
             }
         }
         s_info[lane] = info;
+        s_skip[lane] = skip;
         s_run[lane] = run;
         s_st4[lane][0] = s_st4[lane][1] = s_st4[lane][2] = s_st4[lane][3] = 0u;
     }
@@ -396,8 +399,8 @@ __device__ __forceinline__ void resolve_tile(const mxp_resolve_args& A) {
         const uint32_t rb = wv ? range_bits(w, dlo, dhi) : 0u;
         for (uint32_t i = 0; i < 16u; i++) {
             const uint32_t r = wave * 16u + i;
-            const uint32_t info = s_info[r];  // (the same for the whole wave)
-            if (info & kSkip) continue;
+            if (s_skip[r]) continue;  // (the same for the whole wave)
+            const uint32_t info = s_info[r];
             const uint32_t appl = ((info >> 31) ? a1 : a0) & rb;
             if (!kWrite && A.err) {
                 const uint64_t eb = __ballot((te[lane][r] & appl & ~em) != 0u);
@@ -407,7 +410,7 @@ __device__ __forceinline__ void resolve_tile(const mxp_resolve_args& A) {
                         A.status[qq] = MXP_RESOLVE_PRED_ERROR;
                         A.err_rule[qq] = w * 32u + __builtin_ctz(te[lane][r] & appl & ~em);
                         A.count[qq] = 0;
-                        s_info[r] = info | kSkip;
+                        s_skip[r] = 1u;
                     }
                     continue;
                 }
@@ -440,8 +443,8 @@ __device__ __forceinline__ void resolve_tile(const mxp_resolve_args& A) {
     }
     // the request's own namespace, then the outputs (pass 1)
     if (wave == 0 && q < A.n) {
+        if (s_skip[lane]) return;
         const uint32_t info = s_info[lane];
-        if (info & kSkip) return;
         const uint32_t ns = info & 0x7FFFFFFFu;
         WalkState S{kWrite ? 0u : (uint32_t)s_run[lane], kWrite ? s_run[lane] : 0ull,
                     {s_st4[lane][0], s_st4[lane][1], s_st4[lane][2], s_st4[lane][3]}};
