@@ -381,8 +381,14 @@ __device__ __forceinline__ void resolve_tile(const mxp_resolve_args& A) {
         s_st4[lane][0] = s_st4[lane][1] = s_st4[lane][2] = s_st4[lane][3] = 0u;
     }
     __syncthreads();
+    // (no request of the tile to walk -- every one failed, or the stash had it: no tile loads)
+    bool any = false;
+    if (wave == 0) any = __ballot(s_skip[lane] == 0u) != 0;
+    __shared__ uint32_t s_any;
+    if (tid == 0) s_any = any ? 1u : 0u;
+    __syncthreads();
     const uint32_t wl = dhi > dlo ? (dhi - 1u) >> 5 : 0u;
-    for (uint32_t c0 = dlo >> 5; dhi > dlo && c0 <= wl; c0 += 64u) {
+    for (uint32_t c0 = dlo >> 5; s_any && dhi > dlo && c0 <= wl; c0 += 64u) {
         // the tile: row j of the chunk = word c0 + j of the 64 requests
         for (uint32_t j = wave; j < 64u; j += 4u) {
             const uint32_t w = c0 + j;
@@ -468,6 +474,107 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_tile_write_kernel(
     resolve_tile<true>(A);
 }
 
+// Count pass over the default namespace's range without an error bitmap (compact Resolve): a
+// workgroup takes 1,024 requests, a thread the four requests t, t + 256, t + 512, t + 768, so the
+// workgroup reads each bitmap word's row as one 4 KB run (the per-lane walk read 1 KB runs: 2 TB/s
+// on C2's 1.25 GB); kCW words x 4 requests of loads are in flight per thread.  The request's own
+// namespace and the outputs per request afterwards; block sums per 256 requests for the scan.
+constexpr uint32_t kCW = 8;
+extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count4_kernel(mxp_resolve_args A) {
+    const uint32_t t = threadIdx.x;
+    const uint32_t base = blockIdx.x * 1024u;
+    const uint32_t dlo = __builtin_amdgcn_readfirstlane(A.ns_lo[A.default_id]);
+    const uint32_t dhi = __builtin_amdgcn_readfirstlane(A.ns_hi[A.default_id]);
+    uint32_t info[4], cnt[4], st[4][4];
+    bool act[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) {
+        const uint32_t q = base + t + 256u * k;
+        act[k] = false;
+        info[k] = 0u;
+        cnt[k] = 0u;
+        st[k][0] = st[k][1] = st[k][2] = st[k][3] = 0u;
+        if (q >= A.n) continue;
+        const uint32_t in = A.nsinfo[q];
+        if (in == MXP_NS_MISSING || in == MXP_NS_NOTSTRING) {
+            A.status[q] = in == MXP_NS_MISSING ? MXP_RESOLVE_NO_IDENTITY : MXP_RESOLVE_BAD_IDENTITY;
+            A.err_rule[q] = 0xFFFFFFFFu;
+            A.count[q] = 0;
+        } else if (A.err_in && A.err_in[q] != 0xFFFFFFFFu) {
+            uint32_t rule = A.err_in[q];
+            if (A.err_rank) {
+                const uint32_t dlen = dhi - dlo;
+                rule = rule < dlen ? dlo + rule : A.ns_lo[in & 0x7FFFFFFFu] + (rule - dlen);
+            }
+            A.status[q] = MXP_RESOLVE_PRED_ERROR;
+            A.err_rule[q] = rule;
+            A.count[q] = 0;
+        } else {
+            info[k] = in;
+            act[k] = true;
+        }
+    }
+    const uint32_t wl = dhi > dlo ? (dhi - 1u) >> 5 : 0u;
+    for (uint32_t w0 = dlo >> 5; dhi > dlo && w0 <= wl; w0 += kCW) {
+        uint32_t a0[kCW], a1[kCW], em[kCW], mv[kCW][4];
+#pragma unroll
+        for (uint32_t j = 0; j < kCW; j++) {  // (uniform: scalar loads)
+            const uint32_t w = w0 + j, wc = w <= wl ? w : wl;
+            const uint32_t rb = w <= wl ? range_bits(w, dlo, dhi) : 0u;
+            a0[j] = A.amask[wc] & rb;
+            a1[j] = A.amask[A.n_words + wc] & rb;
+            em[j] = A.empty[wc];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kCW; j++)
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; k++) {
+                const uint32_t q = base + t + 256u * k;
+                mv[j][k] = act[k] && (a0[j] | a1[j]) ? A.match[(uint64_t)(w0 + j) * A.n + q] : 0u;
+            }
+#pragma unroll
+        for (uint32_t j = 0; j < kCW; j++)
+#pragma unroll
+            for (uint32_t k = 0; k < 4u; k++) {
+                const uint32_t appl = (info[k] >> 31) ? a1[j] : a0[j];
+                const uint32_t sel = act[k] ? (mv[j][k] | em[j]) & appl : 0u;
+                for (uint32_t b = sel, kk = cnt[k]; b && kk < 4u; b &= b - 1, kk++) {
+                    const uint32_t r = (w0 + j) * 32u + __builtin_ctz(b);
+                    st[k][0] = kk == 0u ? r : st[k][0];  // (selects: no dynamically indexed registers)
+                    st[k][1] = kk == 1u ? r : st[k][1];
+                    st[k][2] = kk == 2u ? r : st[k][2];
+                    st[k][3] = kk == 3u ? r : st[k][3];
+                }
+                cnt[k] += __builtin_popcount(sel);
+            }
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) {
+        const uint32_t q = base + t + 256u * k;
+        uint32_t c = 0u;
+        if (act[k]) {
+            const uint32_t ns = info[k] & 0x7FFFFFFFu;
+            WalkState S{cnt[k], 0ull, {st[k][0], st[k][1], st[k][2], st[k][3]}};
+            bool ok = true;
+            if (ns != MXP_NS_NONE && ns != A.default_id) {
+                const uint32_t lo = A.ns_lo[ns], hi = A.ns_hi[ns];
+                ok = lo >= hi || walk_range<false, false>(A, q, info[k] >> 31, lo, hi, S);
+            }
+            if (ok) {
+                A.status[q] = MXP_RESOLVE_OK;
+                A.err_rule[q] = 0xFFFFFFFFu;
+                A.count[q] = S.cnt;
+                if (A.stash) A.stash[q] = make_uint4(S.st4[0], S.st4[1], S.st4[2], S.st4[3]);
+                c = S.cnt;
+            }
+        }
+        if (A.block_sum) {  // (requests base + 256 k ...: block 4 * blockIdx.x + k of the scan)
+            const uint64_t tot = block_sum256(c);
+            if (t == 0 && base + 256u * k < A.n) A.block_sum[4u * blockIdx.x + k] = tot;
+        }
+    }
+}
+
 // the count pass's block sums from the counts (the tiled count kernel's blocks are 64 requests)
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_bsum_kernel(mxp_resolve_args A) {
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
@@ -485,8 +592,12 @@ extern "C" hipError_t mxp_launch_resolve(const mxp_resolve_args* a, int write, h
         hipLaunchKernelGGL(mxp_resolve_scan_blocks_kernel, dim3(1), dim3(1024), 0, s, a->block_sum, grid);
         hipLaunchKernelGGL(mxp_resolve_offsets_kernel, dim3(grid), dim3(256), 0, s, *a);
     } else if (write == 3) {
-        hipLaunchKernelGGL(mxp_resolve_tile_count_kernel, dim3((a->n + 63u) / 64u), dim3(256), 0, s, *a);
-        if (a->block_sum) hipLaunchKernelGGL(mxp_resolve_bsum_kernel, dim3(grid), dim3(256), 0, s, *a);
+        if (!a->err) {  // (compact: the four-request count kernel; with an error bitmap the tiled one)
+            hipLaunchKernelGGL(mxp_resolve_count4_kernel, dim3((a->n + 1023u) / 1024u), dim3(256), 0, s, *a);
+        } else {
+            hipLaunchKernelGGL(mxp_resolve_tile_count_kernel, dim3((a->n + 63u) / 64u), dim3(256), 0, s, *a);
+            if (a->block_sum) hipLaunchKernelGGL(mxp_resolve_bsum_kernel, dim3(grid), dim3(256), 0, s, *a);
+        }
     } else if (write == 4) {
         hipLaunchKernelGGL(mxp_resolve_tile_write_kernel, dim3((a->n + 63u) / 64u), dim3(256), 0, s, *a);
     } else {
