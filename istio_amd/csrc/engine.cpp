@@ -2828,12 +2828,22 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
     if (kept) {
         last_recs.resize(kept);
         if (int rc = download(last_recs.data(), d_errlog.p, kept * sizeof(mxp_err_rec), "download errlog")) return rc;
-        last_rec_text.assign(kept, -1);
-        for (uint32_t i = 0; i < kept; i++)  // (conversion errors print the caller's value: now)
-            if (last_recs[i].code >= ERR_CONV_S && last_recs[i].code <= ERR_CONV_D) {
-                last_rec_text[i] = (int32_t)last_rec_texts.size();
-                last_rec_texts.push_back(format_error(batch, db.get(), last_recs[i]));
-            }
+        // conversion errors print the caller's value: formatted now (the others when asked); the
+        // records scanned in parallel, the per-record text index kept only when one exists
+        std::atomic<bool> conv{false};
+        mxp::par_for(kept, 1u << 16, [&](uint64_t i0, uint64_t i1, unsigned) {
+            bool any = false;
+            for (uint64_t i = i0; i < i1; i++) any |= last_recs[i].code >= ERR_CONV_S && last_recs[i].code <= ERR_CONV_D;
+            if (any) conv.store(true, std::memory_order_relaxed);
+        });
+        if (conv.load()) {
+            last_rec_text.assign(kept, -1);
+            for (uint32_t i = 0; i < kept; i++)
+                if (last_recs[i].code >= ERR_CONV_S && last_recs[i].code <= ERR_CONV_D) {
+                    last_rec_text[i] = (int32_t)last_rec_texts.size();
+                    last_rec_texts.push_back(format_error(batch, db.get(), last_recs[i]));
+                }
+        }
     }
     trace_mark("  errors: records");
     if (cnt[2]) {
@@ -2914,7 +2924,10 @@ int mxp_engine::expand_class_errors(const mxp_bag_batch* batch, mxp_dbatch* db, 
             mxp_err_rec x = r;
             x.req = reqs[a][i];
             last_recs.push_back(x);
-            last_rec_text.push_back(text);
+            if (text >= 0 || !last_rec_text.empty()) {  // (the index exists once a record has a text)
+                last_rec_text.resize(last_recs.size() - 1, -1);
+                last_rec_text.push_back(text);
+            }
             emitted++;
         }
     }
@@ -2992,7 +3005,7 @@ int mxp_engine::pair_error_text(uint32_t request, uint32_t rule, std::string* te
             const mxp_err_rec& r = last_recs[(size_t)i];
             *code = r.code;
             if (text) {
-                const int32_t t = last_rec_text[(size_t)i];
+                const int32_t t = (size_t)i < last_rec_text.size() ? last_rec_text[(size_t)i] : -1;
                 *text = t >= 0 ? last_rec_texts[(size_t)t] : format_error(nullptr, last_db.get(), r);
                 last_errors[key] = {r.code, *text};
             }

@@ -574,7 +574,8 @@ struct mxp_engine : public mxp::LowerTables {
     // recomputed windows, are memoized in last_errors.
     std::unordered_map<uint64_t, std::pair<uint32_t, std::string>> last_errors;
     std::vector<mxp_err_rec, PinnedAlloc<mxp_err_rec>> last_recs;
-    std::vector<int32_t> last_rec_text;          // per record: index into last_rec_texts, or -1 (lazy)
+    std::vector<int32_t> last_rec_text;          // per record: index into last_rec_texts, or -1; empty
+                                                 // (or shorter than last_recs): -1 for the rest
     std::vector<std::string> last_rec_texts;
     std::unordered_map<uint64_t, uint32_t> rec_index;  // key -> record (built on first use)
     bool rec_indexed = false;
