@@ -576,6 +576,7 @@ def end_to_end(eng, batch, n_rules, reps):
             "reps": reps, "selected_per_request": float(off[-1]) / max(batch.n, 1),
             "pred_error_requests": int((status == 3).sum()), "rule_ids": "u16" if ids16 else "u32",
             "action_list_bytes": sel_bytes, "action_list_ms_at_50GBps": sel_bytes / 50e9 * 1e3,
+            "x_action_list_at_50GBps": t * 1e3 / max(sel_bytes / 50e9 * 1e3, 1e-9),
             "host_memory": "pinned batch and outputs (mxp_host_alloc arenas)",
             "path": "host columnar bags -> mxp_resolve_batch_ex (device pack + namespaces + compact evaluation + "
                     "first errors from the records + device scan + action-list gather) -> host action lists; median "

@@ -2187,6 +2187,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_TRACE")) e->trace = atoi(f) != 0;
     if (const char* f = getenv("MXP_D2H_DMA")) e->d2h_dma = atoi(f) != 0;
     if (const char* f = getenv("MXP_RESOLVE_TILE")) e->resolve_tile = atoi(f) != 0;
+    if (const char* f = getenv("MXP_LAZY_RECORDS")) e->lazy_records = atoi(f) != 0;
     if (const char* f = getenv("MXP_PACK_COLS_BESIDE")) e->pack_cols_beside = atoi(f) != 0;
     if (const char* f = getenv("MXP_DTP")) e->dtp = atoi(f) != 0;
     if (const char* f = getenv("MXP_DTP_CAP")) e->dtp_cap = (uint32_t)std::min(1 << 20, std::max(1, atoi(f)));
@@ -2825,6 +2826,13 @@ int mxp_engine::collect_errors(const mxp_bag_batch* batch, std::unique_ptr<mxp_d
     err_windows.clear();
     errors_complete = cnt[0] <= errcap;
     uint32_t kept = std::min(cnt[0], errcap);
+    if (kept && lazy_records && !cnt[2] && !cnt[3]) {
+        // no conversion error and no class record: the records stay where the kernels wrote them
+        // (that buffer set aside from the next evaluation) until a text is asked for
+        d_errlog.swap(d_errlog_prev);
+        recs_pending = kept;
+        kept = 0;
+    }
     if (kept) {
         last_recs.resize(kept);
         if (int rc = download(last_recs.data(), d_errlog.p, kept * sizeof(mxp_err_rec), "download errlog")) return rc;
@@ -2983,7 +2991,22 @@ int mxp_engine::recompute_errors(uint32_t request) {
 }
 
 // the record the last batch logged for `key`, or -1 (the index over the records is built on first use)
+// the deferred records of the last evaluation into last_recs (collect_errors)
+int mxp_engine::ensure_recs() {
+    if (!recs_pending) return MXP_OK;
+    const uint32_t k = recs_pending;
+    recs_pending = 0;
+    last_recs.resize(k);
+    if (int rc = download(last_recs.data(), d_errlog_prev.p, (size_t)k * sizeof(mxp_err_rec), "download errlog")) {
+        last_recs.clear();
+        return rc;
+    }
+    rec_indexed = false;
+    return MXP_OK;
+}
+
 int64_t mxp_engine::logged_record(uint64_t key) {
+    if (ensure_recs()) return -1;
     if (!rec_indexed) {
         rec_index.reserve(last_recs.size());
         for (uint32_t i = 0; i < (uint32_t)last_recs.size(); i++)

@@ -134,6 +134,11 @@ struct DevBuf {
     DevBuf() = default;
     DevBuf(const DevBuf&) = delete;
     DevBuf& operator=(const DevBuf&) = delete;
+    void swap(DevBuf& o) {  // (two engine buffers trade blocks)
+        std::swap(p, o.p);
+        std::swap(n, o.n);
+        std::swap(cap, o.cap);
+    }
     ~DevBuf() { reset(); }
     void reset() {
         if (p) {
@@ -583,7 +588,14 @@ struct mxp_engine : public mxp::LowerTables {
     // records overflowed the log and the device batch holds no map contents: a recomputed window's
     // conversion error prints the map after the caller's batch is gone
     std::vector<std::string> snap_maps;
+    // the last evaluation's records left on the device until a text is asked for (ensure_recs):
+    // recs_pending records in d_errlog_prev, the buffer the next evaluation does not write
+    DevBuf d_errlog_prev;
+    uint32_t recs_pending = 0;
+    bool lazy_records = true;  // MXP_LAZY_RECORDS=0: download every evaluation's records at once
+    int ensure_recs();
     void clear_errors() {
+        recs_pending = 0;
         snap_maps.clear();
         last_errors.clear();
         last_recs.clear();

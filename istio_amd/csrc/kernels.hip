@@ -95,6 +95,9 @@ __device__ bool strfn(uint32_t fn, StrRef s, StrRef p) {
 
 __device__ __forceinline__ void log_err(const mxp_kargs& A, uint32_t req, uint32_t rule, uint32_t code, uint32_t aux) {
     if (!A.errlog) return;
+    // (errcount[3]: some record is a conversion error, whose text prints the caller's value -- the
+    // host then collects the records at once instead of when a text is asked for)
+    if (code >= ERR_CONV_S && code <= ERR_CONV_D) atomicOr(A.errcount + 3, 1u);
     uint32_t slot = atomicAdd(A.errcount, 1u);
     if (slot < A.errcap) {
         mxp_err_rec r;

@@ -161,6 +161,7 @@ void first_errors(mxp_engine* eng, uint32_t n, uint32_t variety, const uint32_t*
     const uint32_t dlo = has_def ? R.ns_lo[R.default_id] : 0u, dhi = has_def ? R.ns_hi[R.default_id] : 0u;
     const uint32_t dlen = dhi - dlo;
     std::vector<uint32_t> touched;
+    (void)eng->ensure_recs();  // (class records make collect_errors download them at once; kept for safety)
     for (const mxp_err_rec& rec : eng->last_recs) {
         const uint32_t q = rec.req, r = rec.rule;
         if (q >= n || r >= R.vmask.size()) continue;

@@ -54,12 +54,13 @@ def test_reference_resolver_table_on_gpu(mxp, case):
 # the bitmaps instead of the tiled one (MXP_RESOLVE_TILE=0), with the error bitmap and without
 MODES = {"compact": {}, "bitmap": {"MXP_DEBUG_FLAGS": "268435456"}, "errcap": {"MXP_ERRCAP": "16"},
          "hostpack": {"MXP_HOST_PACK": "1"}, "u16": {}, "lanewalk": {"MXP_RESOLVE_TILE": "0"},
-         "lanewalk_bitmap": {"MXP_RESOLVE_TILE": "0", "MXP_DEBUG_FLAGS": "268435456"}}
+         "lanewalk_bitmap": {"MXP_RESOLVE_TILE": "0", "MXP_DEBUG_FLAGS": "268435456"},
+         "eager_records": {"MXP_LAZY_RECORDS": "0"}}
 
 
 @pytest.mark.parametrize("seed,mode", [(21, "compact"), (22, "compact"), (21, "bitmap"), (22, "errcap"),
                                        (21, "hostpack"), (22, "u16"), (23, "lanewalk"), (23, "lanewalk_bitmap"),
-                                       (23, "compact"), (23, "bitmap")])
+                                       (23, "compact"), (23, "bitmap"), (24, "eager_records")])
 def test_resolver_random_parity(mxp, monkeypatch, seed, mode):
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
