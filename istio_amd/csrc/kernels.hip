@@ -1595,20 +1595,9 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
 // they are gathered (through the staged word positions) only when some class word of the chunk
 // holds an error bit (none in C4), so LDS holds the match words alone.
 #define MXP_VTI_CAP 64u
-// MXP_VTI_B128 (A/B; 0 = the layout above): the staged words [a][class][g] with a padded row of
-// MXP_VTI_PITCH words, so one ds_read_b128 gathers four groups' words of a (slot, request): 1 =
-// the four groups' bodies unrolled, 2 = rolled with selects
-#ifndef MXP_VTI_B128
-#define MXP_VTI_B128 0
-#endif
-#define MXP_VTI_PITCH (MXP_FILL_CHUNK + 4u)
 template <uint32_t NVT>
 __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
-#if MXP_VTI_B128
-    __shared__ __attribute__((aligned(16))) uint32_t SM[NVT * MXP_VTI_CAP * MXP_VTI_PITCH];
-#else
     __shared__ uint32_t SM[NVT * MXP_FILL_CHUNK * MXP_VTI_CAP];
-#endif
     __shared__ uint32_t SJ[NVT * MXP_FILL_CHUNK];  // word position of (slot, group), ~0: none
     __shared__ uint32_t eflag;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
@@ -1616,7 +1605,7 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
     const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
     const uint32_t chunk = A.dtp_cbase + blockIdx.y;
     // 1. staging: zero, then each (group, slot) merge entry's 64 class words into its fixed row
-    for (uint32_t i = tid; i < (uint32_t)(sizeof(SM) / 4u); i += 256u) SM[i] = 0u;
+    for (uint32_t i = tid; i < NVT * MXP_FILL_CHUNK * MXP_VTI_CAP; i += 256u) SM[i] = 0u;
     if (tid < NVT * MXP_FILL_CHUNK) SJ[tid] = ~0u;
     if (tid == 0) eflag = 0u;
     __syncthreads();
@@ -1628,11 +1617,7 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
             const uint32_t ent = A.gvt[i0 + x / MXP_VTI_CAP], a = ent >> 24, j = ent & 0xFFFFFFu, k = x % MXP_VTI_CAP;
             const uint32_t tb = __builtin_amdgcn_ds_bpermute((int)(a << 2), (int)TB);
             const uint2 w = *(const uint2*)(A.vt_tm + 2u * ((uint64_t)tb + (uint64_t)j * MXP_VTI_CAP + k));
-#if MXP_VTI_B128
-            SM[(a * MXP_VTI_CAP + k) * MXP_VTI_PITCH + g] = w.x;
-#else
             SM[(a * MXP_FILL_CHUNK + g) * MXP_VTI_CAP + k] = w.x;
-#endif
             if (k == 0) SJ[a * MXP_FILL_CHUNK + g] = j;
             eor |= w.y;
         }
@@ -1673,65 +1658,28 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
             }
 #pragma unroll
             for (uint32_t r = 0; r < 4; r++)
-#if MXP_VTI_B128
-                ad[a][r] = (a * MXP_VTI_CAP + ((uint32_t)(c >> (16u * r)) & (MXP_VTI_CAP - 1u))) * MXP_VTI_PITCH;
-#else
                 ad[a][r] = a * MXP_FILL_CHUNK * MXP_VTI_CAP + ((uint32_t)(c >> (16u * r)) & (MXP_VTI_CAP - 1u));
-#endif
         }
         const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
         DtpQueue dq;
         dq.load(A, chunk, q0, q0 < Q1);
         const bool dany = __ballot(dq.q0 != ~0u) != 0;
         uint32_t anyerr[4] = {0u, 0u, 0u, 0u};
-#if MXP_VTI_B128
-        for (uint32_t g4 = 0; g4 < MXP_FILL_CHUNK; g4 += 4u) {
-            if (g4 >= n) break;
-            uint32_t mm[4][4];  // [group of the four][request]
-#pragma unroll
-            for (uint32_t gg = 0; gg < 4u; gg++)
-#pragma unroll
-                for (uint32_t r = 0; r < 4u; r++) mm[gg][r] = 0u;
-#pragma unroll
-            for (uint32_t a = 0; a < NVT; a++)
-#pragma unroll
-                for (uint32_t r = 0; r < 4u; r++) {
-                    const v4u x = *(const v4u*)(SM + ad[a][r] + g4);
-                    mm[0][r] |= x.x;
-                    mm[1][r] |= x.y;
-                    mm[2][r] |= x.z;
-                    mm[3][r] |= x.w;
-                }
-#if MXP_VTI_B128 == 1
-#pragma unroll
-#else
-#pragma unroll 1
-#endif
-        for (uint32_t gg = 0; gg < 4u; gg++) {
-            const uint32_t g = g4 + gg;
-            if (g >= n) break;
-            uint32_t m[4];
-#pragma unroll
-            for (uint32_t r = 0; r < 4u; r++)  // (selects when rolled: no dynamically indexed registers)
-                m[r] = gg == 0u ? mm[0][r] : gg == 1u ? mm[1][r] : gg == 2u ? mm[2][r] : mm[3][r];
-#else
 #pragma unroll
         for (uint32_t g = 0; g < MXP_FILL_CHUNK; g++) {
             if (g >= n) break;
-            uint32_t m[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (uint32_t a = 0; a < NVT; a++)
-#pragma unroll
-                for (uint32_t r = 0; r < 4; r++) m[r] |= SM[ad[a][r] + g * MXP_VTI_CAP];
-#endif
             const uint32_t G = g0 + g;
             const uint32_t mask = __builtin_amdgcn_readlane(FM, g);
-            uint32_t e[4], ve[4] = {0u, 0u, 0u, 0u};
+            uint32_t m[4] = {0u, 0u, 0u, 0u}, e[4], ve[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
             for (int r = 0; r < 4; r++) e[r] = bad[r] & mask;
             if (A.errlog && any && mask)
                 for (uint32_t r = 0; r < 4; r++)
                     if (e[r] && q0 + r < Q1) log_guard_errors(A, e[r], G * 32u, q0 + r);
+#pragma unroll
+            for (uint32_t a = 0; a < NVT; a++)
+#pragma unroll
+                for (uint32_t r = 0; r < 4; r++) m[r] |= SM[ad[a][r] + g * MXP_VTI_CAP];
             if (errs) {
 #pragma unroll
                 for (uint32_t a = 0; a < NVT; a++) {
@@ -1739,14 +1687,8 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
                     if (j == ~0u) continue;
                     const uint64_t row = (uint64_t)__builtin_amdgcn_readlane(TB, a) + (uint64_t)j * MXP_VTI_CAP;
 #pragma unroll
-                    for (uint32_t r = 0; r < 4; r++) {
-#if MXP_VTI_B128
-                        const uint32_t cls = ad[a][r] / MXP_VTI_PITCH - a * MXP_VTI_CAP;
-#else
-                        const uint32_t cls = ad[a][r] & (MXP_VTI_CAP - 1u);
-#endif
-                        ve[r] |= A.vt_tm[2u * (row + cls) + 1u];
-                    }
+                    for (uint32_t r = 0; r < 4; r++)
+                        ve[r] |= A.vt_tm[2u * (row + (ad[a][r] & (MXP_VTI_CAP - 1u))) + 1u];
                 }
                 if (A.errlog) {
                     uint32_t c = 0;
@@ -1779,9 +1721,6 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
                 }
             }
         }
-#if MXP_VTI_B128
-        }
-#endif
         if (A.req_err)
             for (uint32_t r = 0; r < 4; r++)
                 if (anyerr[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;
