@@ -416,10 +416,11 @@ def list_bench(args, rank, world, local, kind=None, emit=True):
     n = len(bs)
     alg = int(off[-1]) + 8 * (n + 1) + 4 * n  # symbol bytes + offsets read, one code written each
     achieved = alg / (kernel_ms * 1e-3) / 1e9
-    # the kernel the step launches (lists.cpp mxp_list_check_device): regex lists stage their
-    # automata in LDS unless MXP_LIST_LDS=0
-    kname = ("mxp_list_rx_kernel" if kind == "c3-regex" and os.environ.get("MXP_LIST_LDS", "1") != "0"
-             else "mxp_list_kernel")
+    # the kernel the step launches (lists.cpp mxp_list_check_device): CIDR lookups regrouped by
+    # address family, string lookups by the register window, regex lists with their automata staged
+    # in LDS unless MXP_LIST_LDS=0
+    kname = {"c3-ip": "mxp_list_ip_kernel", "c3-str": "mxp_list_str_kernel"}.get(
+        kind, "mxp_list_rx_kernel" if os.environ.get("MXP_LIST_LDS", "1") != "0" else "mxp_list_kernel")
     out = {"metric": "list-adapter lookups/sec (%s, %d entries)" % (kind, lst.num_entries()),
            "value": world * n * args.steps / elapsed, "unit": "lookups/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,

@@ -22,7 +22,8 @@ EVAL_KERNELS = ("mxp_fill_kernel", "mxp_fill_dtp_kernel", "mxp_vtfill", "mxp_vt_
                 "mxp_index_dtp_kernel", "mxp_index_dtp_lite_kernel", "mxp_index5_kernel", "mxp_dtp_sort_kernel", "mxp_dtp_apply_kernel",
                 "mxp_inject_kernel", "mxp_hits_kernel", "mxp_hits_ragged_kernel", "mxp_hits_gate_kernel",
                 "mxp_eval_deep_kernel", "mxp_quota", "mxp_dtp_hits_kernel",
-                "mxp_list_kernel", "mxp_list_nfa_kernel", "mxp_list_rx_kernel", "mxp_list_rx_nfa_kernel")
+                "mxp_list_kernel", "mxp_list_nfa_kernel", "mxp_list_rx_kernel", "mxp_list_rx_nfa_kernel",
+                "mxp_list_ip_kernel", "mxp_list_str_kernel")
 
 
 def per_kernel(path_glob, counter):

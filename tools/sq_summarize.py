@@ -13,7 +13,8 @@ from collections import defaultdict
 EVAL = ("mxp_fill_kernel", "mxp_fill_dtp_kernel", "mxp_vtfill", "mxp_guard_kernel", "mxp_guard2_kernel",
         "mxp_eval_kernel", "mxp_index_kernel", "mxp_index_dtp_kernel", "mxp_index_dtp_lite_kernel", "mxp_dtp_sort_kernel",
         "mxp_vt_lookup_kernel", "mxp_vt_eval_kernel", "mxp_inject_kernel", "mxp_dtp_hits_kernel", "mxp_quota",
-        "mxp_list_kernel", "mxp_list_nfa_kernel", "mxp_list_rx_kernel", "mxp_list_rx_nfa_kernel")
+        "mxp_list_kernel", "mxp_list_nfa_kernel", "mxp_list_rx_kernel", "mxp_list_rx_nfa_kernel",
+        "mxp_list_ip_kernel", "mxp_list_str_kernel")
 
 
 def main():
