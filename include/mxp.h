@@ -343,6 +343,11 @@ void mxp_wire_free(mxp_wire* w);
 int mxp_host_alloc(size_t bytes, void** out);
 void mxp_host_free(void* p);
 
+/* mxp_batch_upload returns once the batch's arrays are on the device (the caller may reuse them);
+ * with the device packer, its kernels (interning, gather, pre-tables, value-class counts) run on,
+ * and the batch's first evaluation waits for them and finishes the packing (value-class tables,
+ * string heads, dictionary).  Uploading batch k + 1 before evaluating batch k overlaps one batch's
+ * copies with the other's packing and evaluation. */
 typedef struct mxp_dbatch mxp_dbatch;
 int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out);
 /* The host half of mxp_batch_upload alone (interning against the rule set's pools, column gather,

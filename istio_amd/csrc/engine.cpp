@@ -1485,6 +1485,7 @@ int mxp_engine::pack_vt_tables(mxp_dbatch* db) {
 
 // texts of a device-packed batch's local ids, read back from the device
 bool mxp_dbatch::overlay_string(uint64_t j, std::string* out) const {
+    wait_packed();
     if (!dev_packed) {
         if (j >= overlay.size()) return false;
         *out = std::string(overlay[j]);
@@ -1498,6 +1499,7 @@ bool mxp_dbatch::overlay_string(uint64_t j, std::string* out) const {
 }
 
 bool mxp_dbatch::overlay_bytes_at(uint64_t j, std::string* out) const {
+    wait_packed();
     if (!dev_packed) {
         if (j >= overlay_bytes.size()) return false;
         *out = std::string(overlay_bytes[j]);
@@ -1511,6 +1513,7 @@ bool mxp_dbatch::overlay_bytes_at(uint64_t j, std::string* out) const {
 }
 
 bool mxp_dbatch::overlay_time(uint64_t j, TimeKey* out) const {
+    wait_packed();
     if (!dev_packed) {
         if (j >= overlay_times.size()) return false;
         *out = overlay_times[j];
@@ -1661,8 +1664,8 @@ int mxp_engine::pack_dict(mxp_dbatch* db) {
         // into the final ones (MXP_DEBUG_FLAGS 134217728: the one-level classify kernel -- A/B)
         mxp_vtd_final_args F;
         memset(&F, 0, sizeof F);
-        F.tkey = pk_vtd_tkey.as<unsigned long long>();
-        F.tcr = pk_vtd_tcr.as<uint2>();
+        F.tkey = db->pk.pk_vtd_tkey.as<unsigned long long>();
+        F.tcr = db->pk.pk_vtd_tcr.as<uint2>();
         uint32_t a = 0;
         for (uint32_t s = 0; s < vt_cand_col.size() && a < MXP_VT_MAX; s++)
             if ((db->vt_mask >> s) & 1u) F.cand[a++] = s;
@@ -1721,6 +1724,12 @@ int mxp_dbatch::note_done(hipStream_t s) {
 // enqueued before an early return also reads the batch).
 int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_t* d_err, uint64_t* d_vals,
                        bool log, unsigned long long* d_hits, uint64_t* stats, uint32_t q_lo, uint32_t q_hi) {
+    if (db && db->pack_pending)
+        if (int rc0 = finish_pack(db)) return rc0;
+    // (a device-packed batch's packer, dictionary and heads ran on the engine stream)
+    hipError_t e;
+    if (db && db->pk_ev[2] && s != stream && (e = hipStreamWaitEvent(s, db->pk_ev[2], 0)) != hipSuccess)
+        return hipfail(e, "wait for the packed batch");
     const int rc = launch_body(db, s, d_match, d_err, d_vals, log, d_hits, stats, q_lo, q_hi);
     if (db && db->note_done(s) != MXP_OK && !rc) return fail(MXP_ERR_DEVICE, "batch completion event");
     return rc;
@@ -2225,10 +2234,8 @@ int mxp_engine_create(int device, mxp_engine** out) {
 void mxp_engine_destroy(mxp_engine* eng) {
     if (!eng) return;
     if (eng->device >= 0) (void)hipSetDevice(eng->device);
-    if (eng->pk_host) (void)hipHostFree(eng->pk_host);
     for (int k = 0; k < mxp_engine::kCopyStreams; k++)
         if (eng->copy_s[k]) (void)hipStreamDestroy(eng->copy_s[k]);
-    if (eng->pk_cols_ev) (void)hipEventDestroy(eng->pk_cols_ev);
     for (int k = 0; k < 2; k++) {
         if (eng->bounce_ev[k]) (void)hipEventDestroy(eng->bounce_ev[k]);
         if (eng->bounce[k]) (void)hipHostFree(eng->bounce[k]);

@@ -261,6 +261,14 @@ struct StrPool {
     void finish() { blob.append(16, '\0'); }
 };
 
+// The device packer's inputs and working tables (pack_device.cpp), per batch: a batch's copies can
+// run while an earlier batch's packer still reads its own (blocks recycled through the bin).
+struct PackScratch {
+    DevBuf pk_soff, pk_sbytes, pk_tsec, pk_tnsec, pk_moff, pk_mkey, pk_mval, pk_ck[66], pk_cv[66];  // (+2: resolver columns)
+    DevBuf pk_sid, pk_braw, pk_bcan, pk_tid, pk_use, pk_tab[4], pk_scan, pk_scan_blocks, pk_scan_max;
+    DevBuf pk_vtd_lkey, pk_vtd_lcr, pk_vtd_ln, pk_vtd_tkey, pk_vtd_tcr, pk_vtd_meta, pk_rx, pk_rxv;
+};
+
 struct mxp_dbatch {
     uint32_t n = 0;
     // value classes (pack_host): candidate slots whose column has few distinct values in this batch,
@@ -287,8 +295,21 @@ struct mxp_dbatch {
     // evaluation's last kernel (launch), so mxp_batch_free only collects events and never touches a
     // caller stream that may be gone by then
     std::vector<std::pair<hipStream_t, hipEvent_t>> done_ev;
+    // device packing (pack_device.cpp): its scratch; events [0] strings copied, [1] everything the
+    // caller handed over copied, [2] packed (after finish_pack: ready, the dictionary and heads too);
+    // pack_pending: the packer's kernels may still run and the value-class sizing, tables,
+    // dictionary and heads are still to do (mxp_engine::finish_pack, at the first evaluation)
+    PackScratch pk;
+    hipEvent_t pk_ev[3] = {nullptr, nullptr, nullptr};
+    bool pack_pending = false, pk_vt_on = false;
+    uint32_t pk_ncand = 0;
+    void wait_packed() const {  // (the packer's results readable from the host)
+        if (pk_ev[2]) (void)hipEventSynchronize(pk_ev[2]);
+    }
     ~mxp_dbatch() {
         for (auto& se : done_ev) (void)hipEventDestroy(se.second);
+        for (hipEvent_t ev : pk_ev)
+            if (ev) (void)hipEventDestroy(ev);
     }
     int note_done(hipStream_t s);  // record (creating on first use) the completion event of stream s
     bool vtd_ready = false;  // the packer's provisional class tables (engine scratch) hold this batch's
@@ -553,7 +574,6 @@ struct mxp_engine : public mxp::LowerTables {
         }
         return copy_s[k];
     }
-    hipEvent_t pk_cols_ev = nullptr;  // the device packer's column copies (pack_device.cpp)
     void* bounce[2] = {nullptr, nullptr};
     hipEvent_t bounce_ev[2] = {nullptr, nullptr};
     int download(void* dst, const void* dsrc, size_t bytes, const char* what);
@@ -816,7 +836,10 @@ struct mxp_engine : public mxp::LowerTables {
         const bool dev = !host_pack && cols.size() + vcols.size() <= MXP_PACK_MAXCOL;
         if (!dev)
             if (int rc0 = check_batch(b)) return rc0;
-        int rc = dev ? pack_device(b, db) : pack_on_host(b, db);
+        // the device packer returns once the caller's arrays are copied; its kernels run on, and the
+        // rest (finish_pack) waits for the batch's first evaluation
+        if (dev) return pack_device(b, db);
+        int rc = pack_on_host(b, db);
         if (!rc) rc = pack_heads(db);
         if (!rc) rc = pack_dict(db);
         // the batch is complete when the call returns (evaluations run on the caller's streams)
@@ -844,11 +867,9 @@ struct mxp_engine : public mxp::LowerTables {
     size_t dp_sizes[4] = {0, 0, 0, 0};
     DevBuf dp_ht[4], dp_desc[2], dp_blob[2], dp_tsec, dp_tnsec;
     uint32_t dp_mask[4] = {0, 0, 0, 0};
-    // device packer scratch, reused across uploads
-    DevBuf pk_soff, pk_sbytes, pk_tsec, pk_tnsec, pk_moff, pk_mkey, pk_mval, pk_ck[66], pk_cv[66];  // (+2: resolver columns)
-    DevBuf pk_sid, pk_braw, pk_bcan, pk_tid, pk_use, pk_maxlen, pk_tab[4], pk_scan, pk_scan_blocks, pk_scan_max;
-    DevBuf pk_vtd_lkey, pk_vtd_lcr, pk_vtd_ln, pk_vtd_tkey, pk_vtd_tcr, pk_vtd_meta, pk_rx, pk_rxv;
-    void* pk_host = nullptr;  // pinned read-back (longest string, value-class distinct counts)
+    // the rest of a device-packed batch's upload, at its first evaluation (pack_device.cpp): the
+    // value-class sizing from the packer's distinct counts, the class tables, heads, dictionary
+    int finish_pack(mxp_dbatch* db);
     uint32_t vcol_key_id(uint32_t j) const {
         auto it = gstr_ids.find(vcols[j].second);
         return it == gstr_ids.end() ? 0xFFFFFFFEu : it->second;

@@ -95,6 +95,7 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = ensure_dev_pools())) return rc;
     hipStream_t s = stream;
     hipError_t e;
+    PackScratch& P = db->pk;
     db->n = n;
     db->dev_packed = true;
     const uint32_t NS = b->n_strings, NT = b->n_times, NM = b->n_maps;
@@ -122,7 +123,8 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         if ((e = d.alloc(bytes)) != hipSuccess) return hipfail(e, what);
         return MXP_OK;
     };
-    auto up = [&](DevBuf& d, const void* src_p, size_t bytes, const char* what) -> int {
+    // (engine-stream uploads of host vectors of this call: the run-time pattern pairs)
+    auto up_s = [&](DevBuf& d, const void* src_p, size_t bytes, const char* what) -> int {
         if ((rc = grow(d, bytes ? bytes : 16, what))) return rc;
         if (bytes && (e = hipMemcpyAsync(d.p, src_p, bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
             return hipfail(e, what);
@@ -132,30 +134,39 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         if ((e = d.alloc(bytes ? bytes : 16)) != hipSuccess) return hipfail(e, what);
         return MXP_OK;
     };
-    // ---- the batch as given (scratch of the engine, reused across uploads)
+    // ---- the batch as given, into the batch's own scratch (db->pk), all on the copy stream: the
+    // strings (with times and maps) first, then the columns.  The call returns once they are in (the
+    // caller's arrays are free again); the packer's kernels on the engine stream wait for them.
     hipStream_t cs = copy_stream(0);
     if (!cs) return fail(MXP_ERR_DEVICE, last_error);
-    if (!pk_cols_ev && (e = hipEventCreateWithFlags(&pk_cols_ev, kOrderEvent)) != hipSuccess) {
-        pk_cols_ev = nullptr;
-        return hipfail(e, "columns event");
-    }
-    // (the copy stream starts after the engine stream's earlier work: the previous pack's kernels read
-    // the column buffers)
-    if (pack_cols_beside &&
-        ((e = hipEventRecord(pk_cols_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(cs, pk_cols_ev, 0)) != hipSuccess))
-        return hipfail(e, "columns order");
+    for (hipEvent_t& ev : db->pk_ev)
+        if (!ev && (e = hipEventCreateWithFlags(&ev, kOrderEvent)) != hipSuccess) {
+            ev = nullptr;
+            return hipfail(e, "pack event");
+        }
+    auto up = [&](DevBuf& d, const void* src_p, size_t bytes, const char* what) -> int {
+        if ((rc = grow(d, bytes ? bytes : 16, what))) return rc;
+        if (bytes && (e = hipMemcpyAsync(d.p, src_p, bytes, hipMemcpyHostToDevice, cs)) != hipSuccess)
+            return hipfail(e, what);
+        return MXP_OK;
+    };
     const uint64_t sbytes = NS ? b->str_offsets[NS] : 0;
-    if ((rc = up(pk_soff, b->str_offsets, NS ? ((size_t)NS + 1) * 8 : 0, "upload string offsets"))) return rc;
+    if ((rc = up(P.pk_soff, b->str_offsets, NS ? ((size_t)NS + 1) * 8 : 0, "upload string offsets"))) return rc;
     // (16 bytes of slack: the intern kernel reads strings 8 bytes at a time)
-    if ((rc = grow(pk_sbytes, sbytes + 16, "upload string bytes"))) return rc;
-    if (sbytes && (e = hipMemcpyAsync(pk_sbytes.p, b->str_bytes, sbytes, hipMemcpyHostToDevice, s)) != hipSuccess)
+    if ((rc = grow(P.pk_sbytes, sbytes + 16, "upload string bytes"))) return rc;
+    if (sbytes && (e = hipMemcpyAsync(P.pk_sbytes.p, b->str_bytes, sbytes, hipMemcpyHostToDevice, cs)) != hipSuccess)
         return hipfail(e, "upload string bytes");
-    if ((rc = up(pk_tsec, b->time_sec, (size_t)NT * 8, "upload times"))) return rc;
-    if ((rc = up(pk_tnsec, b->time_nsec, (size_t)NT * 4, "upload times"))) return rc;
+    if ((rc = up(P.pk_tsec, b->time_sec, (size_t)NT * 8, "upload times"))) return rc;
+    if ((rc = up(P.pk_tnsec, b->time_nsec, (size_t)NT * 4, "upload times"))) return rc;
+    // (the batch's own copy of its times, read by the evaluation)
+    if ((rc = up(db->btsec, b->time_sec, (size_t)NT * 8, "times"))) return rc;
+    if ((rc = up(db->btnsec, b->time_nsec, (size_t)NT * 4, "times"))) return rc;
     const uint64_t E = (any_map && NM) ? b->map_offsets[NM] : 0;
-    if ((rc = up(pk_moff, b->map_offsets, any_map && NM ? ((size_t)NM + 1) * 8 : 0, "upload map offsets"))) return rc;
-    if ((rc = up(pk_mkey, b->map_keys, E * 4, "upload map keys"))) return rc;
-    if ((rc = up(pk_mval, b->map_values, E * 4, "upload map values"))) return rc;
+    if ((rc = up(P.pk_moff, b->map_offsets, any_map && NM ? ((size_t)NM + 1) * 8 : 0, "upload map offsets"))) return rc;
+    if ((rc = up(P.pk_mkey, b->map_keys, E * 4, "upload map keys"))) return rc;
+    if ((rc = up(P.pk_mval, b->map_values, E * 4, "upload map values"))) return rc;
+    if ((e = hipEventRecord(db->pk_ev[0], cs)) != hipSuccess) return hipfail(e, "strings event");
+    // (MXP_PACK_COLS_BESIDE=1: the string passes also wait for the columns, as if copied beside)
     std::vector<int32_t> slot_of(b->n_columns, -1);  // batch column -> upload slot
     uint32_t nup = 0;
     for (uint32_t c = 0; c < ncol; c++)
@@ -173,16 +184,12 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
             if (slot_of[it->second] < 0) slot_of[it->second] = (int32_t)nup++;
         }
     }
-    // the columns on a copy stream of their own: the string passes (interning, the aligned pool) run
-    // while they are in flight, and the column passes wait for their event (the columns' copies start
-    // after the strings', which then have the link to themselves)
-    if (!pack_cols_beside &&
-        ((e = hipEventRecord(pk_cols_ev, s)) != hipSuccess || (e = hipStreamWaitEvent(cs, pk_cols_ev, 0)) != hipSuccess))
-        return hipfail(e, "columns order");
+    // the columns after the strings on the copy stream: the string passes (interning, the aligned
+    // pool) run while they are in flight, and the column passes wait for their event
     trace_host("pack: strings queued");
     for (uint32_t bc = 0; bc < b->n_columns; bc++) {
         if (slot_of[bc] < 0) continue;
-        DevBuf* bufs[2] = {&pk_ck[slot_of[bc]], &pk_cv[slot_of[bc]]};
+        DevBuf* bufs[2] = {&P.pk_ck[slot_of[bc]], &P.pk_cv[slot_of[bc]]};
         const void* src[2] = {b->kinds[bc], b->values[bc]};
         const size_t bytes[2] = {n, (size_t)n * 8};
         for (int k = 0; k < 2; k++) {
@@ -191,12 +198,12 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
                 return hipfail(e, "upload columns");
         }
     }
-    if ((e = hipEventRecord(pk_cols_ev, cs)) != hipSuccess) return hipfail(e, "columns event");
+    if ((e = hipEventRecord(db->pk_ev[1], cs)) != hipSuccess) return hipfail(e, "columns event");
     if (resolver.set) {
-        res_id_kind = res_bc[0] >= 0 ? pk_ck[slot_of[res_bc[0]]].as<uint8_t>() : nullptr;
-        res_id_val = res_bc[0] >= 0 ? pk_cv[slot_of[res_bc[0]]].as<uint64_t>() : nullptr;
-        res_pr_kind = res_bc[1] >= 0 ? pk_ck[slot_of[res_bc[1]]].as<uint8_t>() : nullptr;
-        res_pr_val = res_bc[1] >= 0 ? pk_cv[slot_of[res_bc[1]]].as<uint64_t>() : nullptr;
+        res_id_kind = res_bc[0] >= 0 ? P.pk_ck[slot_of[res_bc[0]]].as<uint8_t>() : nullptr;
+        res_id_val = res_bc[0] >= 0 ? P.pk_cv[slot_of[res_bc[0]]].as<uint64_t>() : nullptr;
+        res_pr_kind = res_bc[1] >= 0 ? P.pk_ck[slot_of[res_bc[1]]].as<uint8_t>() : nullptr;
+        res_pr_val = res_bc[1] >= 0 ? P.pk_cv[slot_of[res_bc[1]]].as<uint64_t>() : nullptr;
         res_raw = true;
     }
     // ---- the batch's ids and offsets, checked on the host while the copies run (from pinned caller
@@ -205,21 +212,20 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     // (the string table now; the columns and maps before the column passes, the string passes
     // meanwhile on the device)
     if (int rc0 = check_batch(b, kCheckStrings)) {
-        (void)hipStreamSynchronize(s);  // (the copies still read the caller's arrays)
-        (void)hipStreamSynchronize(cs);
+        (void)hipStreamSynchronize(cs);  // (the copies still read the caller's arrays)
         return rc0;
     }
     trace_host("pack: strings checked");
     // ---- arguments
     mxp_pack_args A;
     memset(&A, 0, sizeof A);
-    A.sbytes = pk_sbytes.as<uint8_t>();
-    A.soff = pk_soff.as<uint64_t>();
-    A.tsec = pk_tsec.as<int64_t>();
-    A.tnsec = pk_tnsec.as<int32_t>();
-    A.moff = pk_moff.as<uint64_t>();
-    A.mkey = pk_mkey.as<uint32_t>();
-    A.mval = pk_mval.as<uint32_t>();
+    A.sbytes = P.pk_sbytes.as<uint8_t>();
+    A.soff = P.pk_soff.as<uint64_t>();
+    A.tsec = P.pk_tsec.as<int64_t>();
+    A.tnsec = P.pk_tnsec.as<int32_t>();
+    A.moff = P.pk_moff.as<uint64_t>();
+    A.mkey = P.pk_mkey.as<uint32_t>();
+    A.mval = P.pk_mval.as<uint32_t>();
     A.ns = NS;
     A.nt = NT;
     A.nm = any_map ? NM : 0;
@@ -234,42 +240,35 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     for (uint32_t c = 0; c < ncol; c++) {
         A.vkey[c] = c < C ? 0xFFFFFFFFu : vcol_key_id(c - C);
         if (src[c] >= 0) {
-            A.ck[c] = pk_ck[slot_of[src[c]]].as<uint8_t>();
-            A.cv[c] = pk_cv[slot_of[src[c]]].as<uint64_t>();
+            A.ck[c] = P.pk_ck[slot_of[src[c]]].as<uint8_t>();
+            A.cv[c] = P.pk_cv[slot_of[src[c]]].as<uint64_t>();
         }
     }
     // id maps and parsed values (scratch), pre-tables and outputs (the batch's)
     const uint64_t nraw = (uint64_t)NS + S;  // byte-string items: batch strings, then parsed ip() values
     const uint64_t ntime = (uint64_t)NT + S;
-    if ((rc = grow(pk_sid, (size_t)NS * 4 + 16, "string ids"))) return rc;
-    if ((rc = grow(pk_braw, nraw * 4 + 16, "byte ids"))) return rc;
-    if ((rc = grow(pk_bcan, nraw * 4 + 16, "canonical ids"))) return rc;
-    if ((rc = grow(pk_tid, ntime * 4 + 16, "time ids"))) return rc;
-    if ((rc = grow(pk_use, (size_t)NS + 16, "uses"))) return rc;
-    if ((rc = grow(pk_maxlen, 16, "max length"))) return rc;
+    if ((rc = grow(P.pk_sid, (size_t)NS * 4 + 16, "string ids"))) return rc;
+    if ((rc = grow(P.pk_braw, nraw * 4 + 16, "byte ids"))) return rc;
+    if ((rc = grow(P.pk_bcan, nraw * 4 + 16, "canonical ids"))) return rc;
+    if ((rc = grow(P.pk_tid, ntime * 4 + 16, "time ids"))) return rc;
+    if ((rc = grow(P.pk_use, (size_t)NS + 16, "uses"))) return rc;
     if ((rc = alloc(db->pip, S * 16, "parsed ips"))) return rc;
     if ((rc = alloc(db->pip_ok, S, "parsed ips"))) return rc;
     if ((rc = alloc(db->pts_sec, S * 8, "parsed times"))) return rc;
     if ((rc = alloc(db->pts_nsec, S * 4, "parsed times"))) return rc;
     if ((rc = alloc(db->pts_ok, S, "parsed times"))) return rc;
-    if ((rc = alloc(db->btsec, (size_t)NT * 8, "times"))) return rc;
-    if ((rc = alloc(db->btnsec, (size_t)NT * 4, "times"))) return rc;
-    if (NT && ((e = hipMemcpyAsync(db->btsec.p, b->time_sec, (size_t)NT * 8, hipMemcpyHostToDevice, s)) != hipSuccess ||
-               (e = hipMemcpyAsync(db->btnsec.p, b->time_nsec, (size_t)NT * 4, hipMemcpyHostToDevice, s)) != hipSuccess))
-        return hipfail(e, "upload times");
-    A.sid = pk_sid.as<uint32_t>();
-    A.braw = pk_braw.as<uint32_t>();
-    A.bcan = pk_bcan.as<uint32_t>();
-    A.tid = pk_tid.as<uint32_t>();
-    A.use = pk_use.as<uint8_t>();
+    A.sid = P.pk_sid.as<uint32_t>();
+    A.braw = P.pk_braw.as<uint32_t>();
+    A.bcan = P.pk_bcan.as<uint32_t>();
+    A.tid = P.pk_tid.as<uint32_t>();
+    A.use = P.pk_use.as<uint8_t>();
     A.pip = db->pip.as<uint8_t>();
     A.pip_ok = db->pip_ok.as<uint8_t>();
     A.pts_sec = db->pts_sec.as<int64_t>();
     A.pts_nsec = db->pts_nsec.as<int32_t>();
     A.pts_ok = db->pts_ok.as<uint8_t>();
-    A.max_len_out = pk_maxlen.as<uint32_t>();
-    if ((e = hipMemsetAsync(pk_use.p, 0, (size_t)NS + 16, s)) != hipSuccess) return hipfail(e, "reset uses");
-    if ((e = hipMemsetAsync(pk_maxlen.p, 0, 16, s)) != hipSuccess) return hipfail(e, "reset max length");
+    A.max_len_out = nullptr;  // (check_batch bounds every string below 16 MiB)
+    if ((e = hipMemsetAsync(P.pk_use.p, 0, (size_t)NS + 16, s)) != hipSuccess) return hipfail(e, "reset uses");
     if ((e = hipMemsetAsync(db->pip_ok.p, 0, S, s)) != hipSuccess) return hipfail(e, "reset parsed");
     if ((e = hipMemsetAsync(db->pts_ok.p, 0, S, s)) != hipSuccess) return hipfail(e, "reset parsed");
     auto launch = [&](uint32_t step, uint32_t arg = 0) -> int {
@@ -312,32 +311,33 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         return launch(1);
     };
     // ---- the string and time passes (the columns are still in flight)
-    if ((rc = intern(MXP_IK_STR, 0, NS, NS, pk_tab[0], G, pk_sid.as<uint32_t>(), true))) return rc;
-    if ((rc = intern(MXP_IK_TIME, 0, NT, ntime, pk_tab[3], db->GT, pk_tid.as<uint32_t>(), true))) return rc;
+    if ((e = hipStreamWaitEvent(s, db->pk_ev[pack_cols_beside ? 1 : 0], 0)) != hipSuccess) return hipfail(e, "strings wait");
+    if ((rc = intern(MXP_IK_STR, 0, NS, NS, P.pk_tab[0], G, P.pk_sid.as<uint32_t>(), true))) return rc;
+    if ((rc = intern(MXP_IK_TIME, 0, NT, ntime, P.pk_tab[3], db->GT, P.pk_tid.as<uint32_t>(), true))) return rc;
     // (every batch string goes into the overlay pool: batch-local ids name their representative)
     if ((rc = alloc(db->bstr_off, (size_t)NS * 8, "bstr_off"))) return rc;
     if ((rc = alloc(db->bstr, sbytes + 8ull * NS + 16, "bstr"))) return rc;
     if ((e = hipMemsetAsync(db->bstr.p, 0, sbytes + 8ull * NS + 16, s)) != hipSuccess) return hipfail(e, "reset bstr");
-    if ((rc = grow(pk_scan, ((size_t)NS + 1) * 8, "scan"))) return rc;
-    if ((rc = grow(pk_scan_blocks, ((size_t)NS / 1024 + 2) * 8, "scan"))) return rc;
-    if ((rc = grow(pk_scan_max, ((size_t)NS / 1024 + 2) * 4, "scan"))) return rc;
+    if ((rc = grow(P.pk_scan, ((size_t)NS + 1) * 8, "scan"))) return rc;
+    if ((rc = grow(P.pk_scan_blocks, ((size_t)NS / 1024 + 2) * 8, "scan"))) return rc;
+    if ((rc = grow(P.pk_scan_max, ((size_t)NS / 1024 + 2) * 4, "scan"))) return rc;
     A.bdesc = db->bstr_off.as<uint64_t>();
     A.bblob = db->bstr.as<uint8_t>();
-    A.scan = pk_scan.as<uint64_t>();
-    A.scan_blocks = pk_scan_blocks.as<uint64_t>();
-    A.scan_max = pk_scan_max.as<uint32_t>();
+    A.scan = P.pk_scan.as<uint64_t>();
+    A.scan_blocks = P.pk_scan_blocks.as<uint64_t>();
+    A.scan_max = P.pk_scan_max.as<uint32_t>();
     if ((rc = launch(4))) return rc;
     // ---- the column passes, after the columns' check and copies
     if (int rc0 = check_batch(b, kCheckColumns)) {
-        (void)hipStreamSynchronize(s);
+        (void)hipStreamSynchronize(s);  // (the string passes)
         (void)hipStreamSynchronize(cs);
         return rc0;
     }
     trace_host("pack: columns checked");
-    if ((e = hipStreamWaitEvent(s, pk_cols_ev, 0)) != hipSuccess) return hipfail(e, "columns wait");
+    if ((e = hipStreamWaitEvent(s, db->pk_ev[1], 0)) != hipSuccess) return hipfail(e, "columns wait");
     if ((rc = launch(0))) return rc;  // BYTES uses
-    if ((rc = intern(MXP_IK_RAW, 0, NS, nraw, pk_tab[1], db->GB, pk_braw.as<uint32_t>(), true))) return rc;
-    if ((rc = intern(MXP_IK_CANON, 0, NS, nraw, pk_tab[2], db->GC, pk_bcan.as<uint32_t>(), true))) return rc;
+    if ((rc = intern(MXP_IK_RAW, 0, NS, nraw, P.pk_tab[1], db->GB, P.pk_braw.as<uint32_t>(), true))) return rc;
+    if ((rc = intern(MXP_IK_CANON, 0, NS, nraw, P.pk_tab[2], db->GC, P.pk_bcan.as<uint32_t>(), true))) return rc;
     // ---- columns, maps
     if ((rc = alloc(db->kinds, (size_t)ncol * n, "kinds"))) return rc;
     if ((rc = alloc(db->vals, (size_t)ncol * n * 8, "vals"))) return rc;
@@ -361,13 +361,13 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     A.tsof = db->tsof.as<uint64_t>();
     if (need_ipof) {
         if ((rc = launch(6, 0))) return rc;
-        if ((rc = intern(MXP_IK_RAW, NS, nraw, nraw, pk_tab[1], db->GB, pk_braw.as<uint32_t>(), false))) return rc;
-        if ((rc = intern(MXP_IK_CANON, NS, nraw, nraw, pk_tab[2], db->GC, pk_bcan.as<uint32_t>(), false))) return rc;
+        if ((rc = intern(MXP_IK_RAW, NS, nraw, nraw, P.pk_tab[1], db->GB, P.pk_braw.as<uint32_t>(), false))) return rc;
+        if ((rc = intern(MXP_IK_CANON, NS, nraw, nraw, P.pk_tab[2], db->GC, P.pk_bcan.as<uint32_t>(), false))) return rc;
         if ((rc = launch(7, 0))) return rc;
     }
     if (need_tsof) {
         if ((rc = launch(6, 1))) return rc;
-        if ((rc = intern(MXP_IK_TIME, NT, ntime, ntime, pk_tab[3], db->GT, pk_tid.as<uint32_t>(), false))) return rc;
+        if ((rc = intern(MXP_IK_TIME, NT, ntime, ntime, P.pk_tab[3], db->GT, P.pk_tid.as<uint32_t>(), false))) return rc;
         if ((rc = launch(7, 1))) return rc;
     }
     // ---- value classes: distinct values of the candidate columns (read back with the longest
@@ -378,35 +378,26 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     if (vt_on) {
         const uint32_t tiles = (uint32_t)((n + MXP_VTD_TILE - 1) / MXP_VTD_TILE);
         const size_t lists = (size_t)ncand * tiles * MXP_VTD_TILE, tabs = (size_t)ncand * MXP_VTD_CAP;
-        if ((rc = grow(pk_vtd_lkey, lists * 8, "vt lists"))) return rc;
-        if ((rc = grow(pk_vtd_lcr, lists * 8, "vt lists"))) return rc;
-        if ((rc = grow(pk_vtd_ln, (size_t)ncand * tiles * 4, "vt lists"))) return rc;
-        if ((rc = grow(pk_vtd_tkey, tabs * 8, "vt tables"))) return rc;
-        if ((rc = grow(pk_vtd_tcr, tabs * 8, "vt tables"))) return rc;
-        if ((rc = grow(pk_vtd_meta, kVtBytes, "vt counts"))) return rc;
-        if ((e = hipMemsetAsync(pk_vtd_tkey.p, 0xFF, tabs * 8, s)) != hipSuccess) return hipfail(e, "reset vt");
-        if ((e = hipMemsetAsync(pk_vtd_tcr.p, 0, tabs * 8, s)) != hipSuccess) return hipfail(e, "reset vt");
-        if ((e = hipMemsetAsync(pk_vtd_meta.p, 0, kVtBytes, s)) != hipSuccess) return hipfail(e, "reset vt");
-        A.vtd_lkey = pk_vtd_lkey.as<unsigned long long>();
-        A.vtd_lcr = pk_vtd_lcr.as<uint2>();
-        A.vtd_ln = pk_vtd_ln.as<uint32_t>();
-        A.vtd_tkey = pk_vtd_tkey.as<unsigned long long>();
-        A.vtd_tcr = pk_vtd_tcr.as<uint2>();
-        A.vtd_meta = pk_vtd_meta.as<uint32_t>();
+        if ((rc = grow(P.pk_vtd_lkey, lists * 8, "vt lists"))) return rc;
+        if ((rc = grow(P.pk_vtd_lcr, lists * 8, "vt lists"))) return rc;
+        if ((rc = grow(P.pk_vtd_ln, (size_t)ncand * tiles * 4, "vt lists"))) return rc;
+        if ((rc = grow(P.pk_vtd_tkey, tabs * 8, "vt tables"))) return rc;
+        if ((rc = grow(P.pk_vtd_tcr, tabs * 8, "vt tables"))) return rc;
+        if ((rc = grow(P.pk_vtd_meta, kVtBytes, "vt counts"))) return rc;
+        if ((e = hipMemsetAsync(P.pk_vtd_tkey.p, 0xFF, tabs * 8, s)) != hipSuccess) return hipfail(e, "reset vt");
+        if ((e = hipMemsetAsync(P.pk_vtd_tcr.p, 0, tabs * 8, s)) != hipSuccess) return hipfail(e, "reset vt");
+        if ((e = hipMemsetAsync(P.pk_vtd_meta.p, 0, kVtBytes, s)) != hipSuccess) return hipfail(e, "reset vt");
+        A.vtd_lkey = P.pk_vtd_lkey.as<unsigned long long>();
+        A.vtd_lcr = P.pk_vtd_lcr.as<uint2>();
+        A.vtd_ln = P.pk_vtd_ln.as<uint32_t>();
+        A.vtd_tkey = P.pk_vtd_tkey.as<unsigned long long>();
+        A.vtd_tcr = P.pk_vtd_tcr.as<uint2>();
+        A.vtd_meta = P.pk_vtd_meta.as<uint32_t>();
         A.vtd_tiles = tiles;
         for (uint32_t a = 0; a < ncand; a++) A.vt_col[a] = vt_cand_col[a];
         A.n_vt_cand = ncand;
         if ((rc = launch(5))) return rc;
     }
-    if (!pk_host) {
-        if ((e = hipHostMalloc((void**)&pk_host, 64 + kVtBytes, hipHostMallocDefault)) != hipSuccess) {
-            pk_host = nullptr;
-            return hipfail(e, "pack host buffer");
-        }
-    }
-    if ((e = hipMemcpyAsync(pk_host, pk_maxlen.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return hipfail(e, "read back");
-    if (vt_on && (e = hipMemcpyAsync((uint8_t*)pk_host + 64, pk_vtd_meta.p, kVtBytes, hipMemcpyDeviceToHost, s)) != hipSuccess)
-        return hipfail(e, "read back");
     // run-time regexp patterns meanwhile: the distinct batch strings of the pattern columns
     std::vector<uint32_t> rx_s, rx_v;
     mxp::DfaSetHost rxb;
@@ -481,10 +472,10 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     }
     if ((rc = alloc(db->rxof, need_rxof ? S * 4 : 0, "rxof"))) return rc;
     if (need_rxof) {
-        if ((rc = up(pk_rx, rx_s.data(), rx_s.size() * 4, "upload patterns"))) return rc;
-        if ((rc = up(pk_rxv, rx_v.data(), rx_v.size() * 4, "upload patterns"))) return rc;
-        A.rx_s = pk_rx.as<uint32_t>();
-        A.rx_v = pk_rxv.as<uint32_t>();
+        if ((rc = up_s(P.pk_rx, rx_s.data(), rx_s.size() * 4, "upload patterns"))) return rc;
+        if ((rc = up_s(P.pk_rxv, rx_v.data(), rx_v.size() * 4, "upload patterns"))) return rc;
+        A.rx_s = P.pk_rx.as<uint32_t>();
+        A.rx_v = P.pk_rxv.as<uint32_t>();
         A.n_rx = (uint32_t)rx_s.size();
         A.rxof = db->rxof.as<uint32_t>();
         if ((rc = launch(8))) return rc;
@@ -503,18 +494,40 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = upd(db->rx_hilo, rxb.hilo.data(), rxb.hilo.size() * 4, "upload rx hilo"))) return rc;
     if ((rc = upd(db->rx_hicls, rxb.hicls.data(), rxb.hicls.size() * 2, "upload rx hicls"))) return rc;
     trace_host("pack: all queued");
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hipfail(e, "pack sync");
-    trace_host("pack: synchronised");
-    if (*(uint32_t*)pk_host >= (1u << 24)) return fail(MXP_ERR_ARG, "batch string longer than 16 MiB");
-    // value-class sizing (pack_host's rule): the first MXP_VT_MAX candidates with few classes
+    // the packer's kernels run on; the call returns once the caller's arrays are copied (the
+    // pattern tables above came from host vectors of this call: synchronous then, a rare path)
+    if ((e = hipEventRecord(db->pk_ev[2], s)) != hipSuccess) return hipfail(e, "pack event");
+    if (need_rxof || !rxb.hdr.empty()) {
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return hipfail(e, "pack sync");
+    }
+    if ((e = hipEventSynchronize(db->pk_ev[1])) != hipSuccess) return hipfail(e, "pack copies");
+    trace_host("pack: copies done");
+    db->pack_pending = true;
+    db->pk_vt_on = vt_on;
+    db->pk_ncand = ncand;
+    db->vt_mask = 0;
+    return MXP_OK;
+}
+
+// The rest of a device-packed batch's upload, before its first evaluation: the value-class sizing
+// (pack_host's rule: the first MXP_VT_MAX candidates with few classes) from the packer's distinct
+// counts, the class tables, the string heads and the dictionary.  Waits for the packer's kernels.
+int mxp_engine::finish_pack(mxp_dbatch* db) {
+    if (!db->pack_pending) return MXP_OK;
+    hipError_t e;
+    if ((e = hipEventSynchronize(db->pk_ev[2])) != hipSuccess) return hipfail(e, "pack sync");
+    db->pack_pending = false;
+    uint32_t meta[2 * MXP_PACK_VTCAND] = {};  // distinct keys, overflow
+    if (db->pk_vt_on && (e = hipMemcpy(meta, db->pk.pk_vtd_meta.p, kVtBytes, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hipfail(e, "read back");
+    const uint32_t n = db->n;
     db->vt_mask = 0;
     db->vt_capc.assign(vt_cand_col.size(), 0);
-    if (vt_on) {
-        const uint32_t* meta = (const uint32_t*)((uint8_t*)pk_host + 64);  // distinct keys, overflow
+    if (db->pk_vt_on) {
         uint32_t active = 0;
         const bool force = (debug_flags & 262144u) != 0;
         db->vtd_ready = true;
-        for (uint32_t a = 0; a < ncand && active < MXP_VT_MAX; a++) {
+        for (uint32_t a = 0; a < db->pk_ncand && active < MXP_VT_MAX; a++) {
             const uint64_t D = meta[2 * a];
             if (meta[2 * a + 1] || D > kVtMaxClasses || (!force && D * 16 > n)) continue;
             uint32_t cap = 64;
@@ -524,5 +537,21 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
             active++;
         }
     }
-    return pack_vt_tables(db);
+    // (the batch's tables drawn from the bin, as at upload)
+    BlockBin* take0 = g_bin_take;
+    const void* db0 = g_bin_db;
+    const size_t sz0 = g_bin_db_size;
+    g_bin_take = &bin;
+    g_bin_db = db;
+    g_bin_db_size = sizeof(mxp_dbatch);
+    int rc = pack_vt_tables(db);
+    if (!rc) rc = pack_heads(db);
+    if (!rc) rc = pack_dict(db);
+    g_bin_take = take0;
+    g_bin_db = db0;
+    g_bin_db_size = sz0;
+    if (rc) return rc;
+    // (pk_ev[2] now marks the batch ready: packer, tables, heads and dictionary)
+    if ((e = hipEventRecord(db->pk_ev[2], stream)) != hipSuccess) return hipfail(e, "pack event");
+    return MXP_OK;
 }

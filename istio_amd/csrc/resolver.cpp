@@ -252,8 +252,8 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         N.id_val = eng->res_id_val;
         N.pr_kind = eng->res_pr_kind;
         N.pr_val = eng->res_pr_val;
-        N.soff = eng->pk_soff.as<uint64_t>();
-        N.sbytes = eng->pk_sbytes.as<uint8_t>();
+        N.soff = db->pk.pk_soff.as<uint64_t>();
+        N.sbytes = db->pk.pk_sbytes.as<uint8_t>();
         N.ns_tab = eng->res_ns_tab.as<unsigned long long>();
         N.ns_desc = eng->res_ns_desc.as<uint64_t>();
         N.ns_blob = eng->res_ns_blob.as<uint8_t>();
