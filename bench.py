@@ -273,11 +273,12 @@ def fresh_batches(kind, n_rules, requests_per_gpu, rank, world):
 
 
 def fresh_batch_block(eng, batches, evaluate, steps, stream, n_rules, world):
-    """Every step takes a NEW batch from host memory, double-buffered: mxp_batch_upload of batch k + 1
-    (returns once its H2D copies are in; the device packer -- interning, gather, pre-tables,
-    value-class counts -- runs on) and then the evaluation of batch k (its first evaluation finishes
-    its packing: class tables, string heads, dictionary; enqueued), so batch k + 2's copies overlap
-    batch k + 1's packer and batch k's evaluation.  The two host batches alternate; a device batch is
+    """Every step takes a NEW batch from host memory, double-buffered: mxp_batch_upload_ex of batch
+    k + 1 with MXP_UPLOAD_NO_WAIT (its H2D copies queued and the batch checked; the device packer --
+    interning, gather, pre-tables, value-class counts -- runs after them), then the evaluation of
+    batch k (its first evaluation finishes its packing: class tables, string heads, dictionary;
+    enqueued), then mxp_batch_wait_copied for batch k + 1.  The copies overlap the host's work for
+    the previous batch and the device's packing and evaluation.  The two host batches alternate; a device batch is
     freed two steps after its evaluation.  PCIe-inclusive.  The host batches live in pinned memory
     (mxp_host_alloc), as a binding's reused packing arenas do: their copies are
     DMA at the link's rate."""
@@ -291,7 +292,7 @@ def fresh_batch_block(eng, batches, evaluate, steps, stream, n_rules, world):
 
     def one(k):
         t0 = time.perf_counter()
-        db = eng.upload(batches[k % len(batches)])
+        db = eng.upload(batches[k % len(batches)], no_wait=True)  # (copies queued, batch checked)
         up_s.append(time.perf_counter() - t0)
         if pending:  # (the previous batch, uploaded one step ago)
             prev = pending.pop()
@@ -299,6 +300,7 @@ def fresh_batch_block(eng, batches, evaluate, steps, stream, n_rules, world):
             keep.append(prev)
             if len(keep) > 2:
                 keep.pop(0).free()
+        db.wait_copied()  # (this batch's host arrays are reused two steps later)
         pending.append(db)
     for k in range(3):  # warm-up (allocations)
         one(k)

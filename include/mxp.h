@@ -350,6 +350,13 @@ void mxp_host_free(void* p);
  * copies with the other's packing and evaluation. */
 typedef struct mxp_dbatch mxp_dbatch;
 int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out);
+/* mxp_batch_upload with flags.  MXP_UPLOAD_NO_WAIT: return once the copies are queued and the
+ * batch checked, before the copies are in; the caller keeps the arrays unchanged until
+ * mxp_batch_wait_copied(db) returns (or the batch's first evaluation has completed).  A worker then
+ * overlaps batch k + 1's copies with its own host work for batch k (bench.py fresh_batch). */
+#define MXP_UPLOAD_NO_WAIT 1u
+int mxp_batch_upload_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t flags, mxp_dbatch** out);
+int mxp_batch_wait_copied(mxp_dbatch* db);
 /* The host half of mxp_batch_upload alone (interning against the rule set's pools, column gather,
  * ip() / timestamp() / regexp pre-tables), for timing and tests; works on a host-only engine.
  * out[0] bytes of the packed device image, out[1] batch strings added to the overlay pool, out[2]

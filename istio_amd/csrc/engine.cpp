@@ -2398,6 +2398,20 @@ uint32_t mxp_ruleset_info(const mxp_engine* eng, uint32_t* out, uint32_t cap) {
     return k;
 }
 
+int mxp_batch_upload_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t flags, mxp_dbatch** out) {
+    if (!eng || (flags & ~(uint32_t)MXP_UPLOAD_NO_WAIT)) return MXP_ERR_ARG;
+    eng->upload_no_wait = (flags & MXP_UPLOAD_NO_WAIT) != 0;
+    const int rc = mxp_batch_upload(eng, batch, out);
+    eng->upload_no_wait = false;
+    return rc;
+}
+
+int mxp_batch_wait_copied(mxp_dbatch* db) {
+    if (!db) return MXP_ERR_ARG;
+    if (db->pk_ev[1] && hipEventSynchronize(db->pk_ev[1]) != hipSuccess) return MXP_ERR_DEVICE;
+    return MXP_OK;
+}
+
 int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out) {
     if (!eng || !batch || !out) return MXP_ERR_ARG;
     if (!eng->have_rules) return eng->fail(MXP_ERR_STATE, "no rule set compiled");

@@ -552,6 +552,8 @@ struct mxp_engine : public mxp::LowerTables {
     // the batch's columns copied beside its strings (MXP_PACK_COLS_BESIDE=1) instead of after them
     // (the default: the string passes then run while the columns copy)
     bool pack_cols_beside = false;
+    // mxp_batch_upload_ex(MXP_UPLOAD_NO_WAIT): return before the batch's copies are in
+    bool upload_no_wait = false;
     // large device -> pageable caller memory through two pinned bounce buffers: the copy of chunk
     // k + 1 overlaps the host threads' copy of chunk k out of pinned memory (a pageable hipMemcpy
     // stages at a fraction of the pinned rate)
@@ -562,7 +564,7 @@ struct mxp_engine : public mxp::LowerTables {
     bool d2h_dma = false;
     bool resolve_tile = true;  // Resolve's default-namespace range walked by resolve_tile (MXP_RESOLVE_TILE)
     // the device packer's column copies (pack_device.cpp)
-    static constexpr int kCopyStreams = 1;
+    static constexpr int kCopyStreams = 2;  // [0] the packer's copies, [1] small read-backs
     hipStream_t copy_s[kCopyStreams] = {};
     hipStream_t copy_stream(int k) {  // (created on first use; null on failure, last_error set)
         if (!copy_s[k]) {

@@ -500,7 +500,7 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     if (need_rxof || !rxb.hdr.empty()) {
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return hipfail(e, "pack sync");
     }
-    if ((e = hipEventSynchronize(db->pk_ev[1])) != hipSuccess) return hipfail(e, "pack copies");
+    if (!upload_no_wait && (e = hipEventSynchronize(db->pk_ev[1])) != hipSuccess) return hipfail(e, "pack copies");
     trace_host("pack: copies done");
     db->pack_pending = true;
     db->pk_vt_on = vt_on;
@@ -517,9 +517,16 @@ int mxp_engine::finish_pack(mxp_dbatch* db) {
     hipError_t e;
     if ((e = hipEventSynchronize(db->pk_ev[2])) != hipSuccess) return hipfail(e, "pack sync");
     db->pack_pending = false;
+    // (read back on a stream of its own: the engine stream may already hold a later batch's packer,
+    // waiting for that batch's copies)
     uint32_t meta[2 * MXP_PACK_VTCAND] = {};  // distinct keys, overflow
-    if (db->pk_vt_on && (e = hipMemcpy(meta, db->pk.pk_vtd_meta.p, kVtBytes, hipMemcpyDeviceToHost)) != hipSuccess)
-        return hipfail(e, "read back");
+    if (db->pk_vt_on) {
+        hipStream_t rb = copy_stream(1);
+        if (!rb) return fail(MXP_ERR_DEVICE, last_error);
+        if ((e = hipMemcpyAsync(meta, db->pk.pk_vtd_meta.p, kVtBytes, hipMemcpyDeviceToHost, rb)) != hipSuccess ||
+            (e = hipStreamSynchronize(rb)) != hipSuccess)
+            return hipfail(e, "read back");
+    }
     const uint32_t n = db->n;
     db->vt_mask = 0;
     db->vt_capc.assign(vt_cand_col.size(), 0);

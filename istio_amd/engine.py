@@ -61,6 +61,8 @@ SIGNATURES = {
     "mxp_pair_error": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
     "mxp_error_count": (ctypes.c_uint64, [_VP]),
     "mxp_batch_upload": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(_VP)]),
+    "mxp_batch_upload_ex": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.POINTER(_VP)]),
+    "mxp_batch_wait_copied": (ctypes.c_int, [_VP]),
     "mxp_batch_pack_host": (ctypes.c_int, [_VP, _VP, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint32]),
     "mxp_batch_free": (None, [_VP, _VP]),
     "mxp_batch_eval_device": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP]),
@@ -555,10 +557,19 @@ class Engine:
         self._check(self.lib.mxp_batch_pack_host(self.h, ctypes.byref(batch.c_struct()), out, 3), "mxp_batch_pack_host")
         return {"bytes": out[0], "overlay_strings": out[1], "overlay_bytes": out[2]}
 
-    def upload(self, batch: BagBatch) -> "DeviceBatch":
+    def upload(self, batch: BagBatch, no_wait: bool = False) -> "DeviceBatch":
+        """mxp_batch_upload; no_wait: mxp_batch_upload_ex(MXP_UPLOAD_NO_WAIT) -- the batch's arrays
+        stay unchanged until DeviceBatch.wait_copied() (the c_struct keeps them referenced)."""
         h = _VP()
-        self._check(self.lib.mxp_batch_upload(self.h, ctypes.byref(batch.c_struct()), ctypes.byref(h)), "mxp_batch_upload")
-        return DeviceBatch(self, h, batch.n)
+        cs = batch.c_struct()
+        if no_wait:
+            rc = self.lib.mxp_batch_upload_ex(self.h, ctypes.byref(cs), 1, ctypes.byref(h))
+        else:
+            rc = self.lib.mxp_batch_upload(self.h, ctypes.byref(cs), ctypes.byref(h))
+        self._check(rc, "mxp_batch_upload")
+        db = DeviceBatch(self, h, batch.n)
+        db._src = (batch, cs)  # (the host arrays the copies read)
+        return db
 
 
 class DeviceBatch:
@@ -566,6 +577,10 @@ class DeviceBatch:
         self.engine = engine
         self.h = h
         self.n = n
+
+    def wait_copied(self):
+        """mxp_batch_wait_copied: the batch's host arrays are free again (after a no_wait upload)."""
+        self.engine._check(self.engine.lib.mxp_batch_wait_copied(self.h), "mxp_batch_wait_copied")
 
     def eval(self, d_match: int, d_err: int, stream: int = 0):
         """Enqueue one evaluation writing device bitmaps (raw device pointers as ints)."""
