@@ -1,0 +1,8 @@
+# round 5, session 15: timeline of the double-buffered fresh-batch loop (kernels + memory copies).
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp MXP_NO_BUILD=1
+o=gpurun_out/r5s15; mkdir -p $o
+timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $o/fresh_c2 -o run -- \
+  python3 tools/fresh_prof.py c2 8 > $o/fresh_c2.log 2>&1 || exit $?
+python3 tools/copy_timeline.py $o/fresh_c2 5 > $o/timeline_c2.txt 2>&1 || exit $?
