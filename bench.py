@@ -277,30 +277,33 @@ def fresh_batch_block(eng, batches, evaluate, steps, stream, n_rules, world):
     k + 1 with MXP_UPLOAD_NO_WAIT (its H2D copies queued and the batch checked; the device packer --
     interning, gather, pre-tables, value-class counts -- runs after them), then the evaluation of
     batch k (its first evaluation finishes its packing: class tables, string heads, dictionary;
-    enqueued), then mxp_batch_wait_copied for batch k + 1.  The copies overlap the host's work for
-    the previous batch and the device's packing and evaluation.  The two host batches alternate; a device batch is
-    freed two steps after its evaluation.  PCIe-inclusive.  The host batches live in pinned memory
-    (mxp_host_alloc), as a binding's reused packing arenas do: their copies are
-    DMA at the link's rate."""
+    enqueued); a host batch is refilled only after mxp_batch_wait_copied of its previous upload, two
+    steps back.  Batch k + 1's copies queue behind batch k's on the copy stream, so the link stays
+    busy while the host works on the previous batch and the device packs and evaluates.  The two
+    host batches alternate; a device batch is freed three steps after its evaluation.  PCIe-inclusive.
+    The host batches live in pinned memory (mxp_host_alloc), as a binding's reused packing arenas do
+    (INTEGRATION.md 2e): their copies are DMA at the link's rate."""
     import numpy as np
     import torch
     from istio_amd.engine import pinned_batch
     pinned = [pinned_batch(b) for b in batches]
     batches = [b for b, _ in pinned]
-    keep, up_s, pending = [], [], []
+    keep, up_s, pending, copying = [], [], [], []
     h2d = [batch_h2d_bytes(b) for b in batches]
 
     def one(k):
+        if len(copying) >= len(batches):  # (this step's host batch was uploaded len(batches) steps ago)
+            copying.pop(0).wait_copied()
         t0 = time.perf_counter()
         db = eng.upload(batches[k % len(batches)], no_wait=True)  # (copies queued, batch checked)
         up_s.append(time.perf_counter() - t0)
+        copying.append(db)
         if pending:  # (the previous batch, uploaded one step ago)
             prev = pending.pop()
             evaluate(prev)
             keep.append(prev)
-            if len(keep) > 2:
+            if len(keep) > 3:
                 keep.pop(0).free()
-        db.wait_copied()  # (this batch's host arrays are reused two steps later)
         pending.append(db)
     for k in range(3):  # warm-up (allocations)
         one(k)
@@ -315,6 +318,7 @@ def fresh_batch_block(eng, batches, evaluate, steps, stream, n_rules, world):
         evaluate(pending[0])
         keep.append(pending.pop())
     torch.cuda.synchronize()
+    copying.clear()
     while keep:
         keep.pop(0).free()
     N = batches[0].n
