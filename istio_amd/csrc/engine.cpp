@@ -60,6 +60,11 @@ void mxp_engine::recycle(mxp_dbatch* db) {
     g.evs.push_back(e);
     for (auto& se : db->done_ev) g.evs.push_back(se.second);  // (the group owns them now)
     db->done_ev.clear();
+    for (hipEvent_t& pe : db->pk_ev)  // (the packer's kernels ran on a stream of their own)
+        if (pe) {
+            g.evs.push_back(pe);
+            pe = nullptr;
+        }
     g_bin_give = &g.blks;
     delete db;
     g_bin_give = nullptr;
@@ -1728,7 +1733,7 @@ int mxp_engine::launch(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, uint32_
         if (int rc0 = finish_pack(db)) return rc0;
     // (a device-packed batch's packer, dictionary and heads ran on the engine stream)
     hipError_t e;
-    if (db && db->pk_ev[2] && s != stream && (e = hipStreamWaitEvent(s, db->pk_ev[2], 0)) != hipSuccess)
+    if (db && db->pk_ev[3] && s != stream && (e = hipStreamWaitEvent(s, db->pk_ev[3], 0)) != hipSuccess)
         return hipfail(e, "wait for the packed batch");
     const int rc = launch_body(db, s, d_match, d_err, d_vals, log, d_hits, stats, q_lo, q_hi);
     if (db && db->note_done(s) != MXP_OK && !rc) return fail(MXP_ERR_DEVICE, "batch completion event");

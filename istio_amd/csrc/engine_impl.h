@@ -296,15 +296,17 @@ struct mxp_dbatch {
     // caller stream that may be gone by then
     std::vector<std::pair<hipStream_t, hipEvent_t>> done_ev;
     // device packing (pack_device.cpp): its scratch; events [0] strings copied, [1] everything the
-    // caller handed over copied, [2] packed (after finish_pack: ready, the dictionary and heads too);
+    // caller handed over copied, [2] packed (the packer stream), [3] ready (after finish_pack's
+    // dictionary and heads, on the engine stream);
     // pack_pending: the packer's kernels may still run and the value-class sizing, tables,
     // dictionary and heads are still to do (mxp_engine::finish_pack, at the first evaluation)
     PackScratch pk;
-    hipEvent_t pk_ev[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t pk_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // [3]: ready (finish_pack's kernels)
     bool pack_pending = false, pk_vt_on = false;
     uint32_t pk_ncand = 0;
     void wait_packed() const {  // (the packer's results readable from the host)
         if (pk_ev[2]) (void)hipEventSynchronize(pk_ev[2]);
+        if (pk_ev[3]) (void)hipEventSynchronize(pk_ev[3]);
     }
     ~mxp_dbatch() {
         for (auto& se : done_ev) (void)hipEventDestroy(se.second);
@@ -564,7 +566,10 @@ struct mxp_engine : public mxp::LowerTables {
     bool d2h_dma = false;
     bool resolve_tile = true;  // Resolve's default-namespace range walked by resolve_tile (MXP_RESOLVE_TILE)
     // the device packer's column copies (pack_device.cpp)
-    static constexpr int kCopyStreams = 2;  // [0] the packer's copies, [1] small read-backs
+    // [0] the packer's copies, [1] small read-backs, [2] the packer's kernels (apart from the engine
+    // stream: an event recorded there -- a freed batch's -- then never waits for a later batch's
+    // packer, which waits for its copies)
+    static constexpr int kCopyStreams = 3;
     hipStream_t copy_s[kCopyStreams] = {};
     hipStream_t copy_stream(int k) {  // (created on first use; null on failure, last_error set)
         if (!copy_s[k]) {

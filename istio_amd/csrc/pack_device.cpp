@@ -93,7 +93,8 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     if (ncol > MXP_PACK_MAXCOL) return pack_on_host(b, db);  // (wider rule sets: pack() checked the batch)
     int rc;
     if ((rc = ensure_dev_pools())) return rc;
-    hipStream_t s = stream;
+    hipStream_t s = copy_stream(2);  // (the packer's kernels: their own stream)
+    if (!s) return fail(MXP_ERR_DEVICE, last_error);
     hipError_t e;
     PackScratch& P = db->pk;
     db->n = n;
@@ -139,9 +140,9 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     // caller's arrays are free again); the packer's kernels on the engine stream wait for them.
     hipStream_t cs = copy_stream(0);
     if (!cs) return fail(MXP_ERR_DEVICE, last_error);
-    for (hipEvent_t& ev : db->pk_ev)
-        if (!ev && (e = hipEventCreateWithFlags(&ev, kOrderEvent)) != hipSuccess) {
-            ev = nullptr;
+    for (int k = 0; k < 3; k++)
+        if (!db->pk_ev[k] && (e = hipEventCreateWithFlags(&db->pk_ev[k], kOrderEvent)) != hipSuccess) {
+            db->pk_ev[k] = nullptr;
             return hipfail(e, "pack event");
         }
     auto up = [&](DevBuf& d, const void* src_p, size_t bytes, const char* what) -> int {
@@ -558,7 +559,11 @@ int mxp_engine::finish_pack(mxp_dbatch* db) {
     g_bin_db = db0;
     g_bin_db_size = sz0;
     if (rc) return rc;
-    // (pk_ev[2] now marks the batch ready: packer, tables, heads and dictionary)
-    if ((e = hipEventRecord(db->pk_ev[2], stream)) != hipSuccess) return hipfail(e, "pack event");
+    // (pk_ev[3]: the batch ready on the engine stream -- tables, heads and dictionary too)
+    if (!db->pk_ev[3] && (e = hipEventCreateWithFlags(&db->pk_ev[3], kOrderEvent)) != hipSuccess) {
+        db->pk_ev[3] = nullptr;
+        return hipfail(e, "pack event");
+    }
+    if ((e = hipEventRecord(db->pk_ev[3], stream)) != hipSuccess) return hipfail(e, "pack event");
     return MXP_OK;
 }

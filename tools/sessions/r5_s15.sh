@@ -6,3 +6,6 @@ o=gpurun_out/r5s15; mkdir -p $o
 timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $o/fresh_c2 -o run -- \
   python3 tools/fresh_prof.py c2 8 > $o/fresh_c2.log 2>&1 || exit $?
 python3 tools/copy_timeline.py $o/fresh_c2 5 > $o/timeline_c2.txt 2>&1 || exit $?
+timeout -k 10 600 python -u -m pytest tests/test_gpu_async_upload.py tests/test_gpu_pack.py tests/test_gpu_bin.py \
+  tests/test_gpu_scale.py tests/test_gpu_resolver.py tests/test_gpu_errors.py -m gpu -x -q --timeout 300 --timeout-method thread > $o/t.log 2>&1 || exit $?
+timeout -k 10 500 python -u bench.py --no-cpu-baseline > $o/bench.log 2>&1 || exit $?
