@@ -164,7 +164,7 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         return MXP_OK;
     };
     auto flush = [&]() -> int {
-        if (HG.n && (e = mxp_launch_h2d_gather(&HG, cs)) != hipSuccess) return hipfail(e, "upload batch");
+        if (HG.n && (e = mxp_launch_h2d_gather(&HG, h2d_grid, cs)) != hipSuccess) return hipfail(e, "upload batch");
         HG.n = 0;
         return MXP_OK;
     };

@@ -720,7 +720,9 @@ extern "C" __global__ __launch_bounds__(256) void mxp_h2d_gather_kernel(mxp_h2d_
     }
 }
 
-extern "C" hipError_t mxp_launch_h2d_gather(const mxp_h2d_list* L, hipStream_t s) {
-    if (L->n) hipLaunchKernelGGL(mxp_h2d_gather_kernel, dim3(1024), dim3(256), 0, s, *L);
+// grid: workgroups (a few suffice for the link: each thread keeps a 16-byte load in flight; more
+// would hold wave slots the packer's and evaluation's kernels use meanwhile)
+extern "C" hipError_t mxp_launch_h2d_gather(const mxp_h2d_list* L, uint32_t grid, hipStream_t s) {
+    if (L->n) hipLaunchKernelGGL(mxp_h2d_gather_kernel, dim3(grid ? grid : 1u), dim3(256), 0, s, *L);
     return hipGetLastError();
 }
