@@ -2200,8 +2200,6 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_DEBUG_FLAGS")) e->debug_flags = (uint32_t)atoi(f);
     if (const char* f = getenv("MXP_TRACE")) e->trace = atoi(f) != 0;
     if (const char* f = getenv("MXP_D2H_DMA")) e->d2h_dma = atoi(f) != 0;
-    if (const char* f = getenv("MXP_H2D_DMA")) e->h2d_dma = atoi(f) != 0;
-    if (const char* f = getenv("MXP_H2D_GRID")) e->h2d_grid = (uint32_t)std::max(1, std::min(atoi(f), 4096));
     if (const char* f = getenv("MXP_RESOLVE_TILE")) e->resolve_tile = atoi(f) != 0;
     if (const char* f = getenv("MXP_LAZY_RECORDS")) e->lazy_records = atoi(f) != 0;
     if (const char* f = getenv("MXP_PACK_COLS_BESIDE")) e->pack_cols_beside = atoi(f) != 0;

@@ -35,8 +35,6 @@ static constexpr unsigned kOrderEvent = hipEventDisableTiming | hipEventDisableS
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_d2h_copy(void* dst, const void* src, uint64_t n, hipStream_t s);
-struct mxp_h2d_list;
-extern "C" hipError_t mxp_launch_h2d_gather(const mxp_h2d_list* L, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_vtd_final(const mxp_kargs* args, const mxp_vtd_final_args* f, hipStream_t s);
 extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, const uint32_t* cols, uint32_t nrow, uint4* heads, hipStream_t s);
 extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s);
@@ -566,8 +564,6 @@ struct mxp_engine : public mxp::LowerTables {
     // d2h_dma (MXP_D2H_DMA=1: the copy engine's DMA, ~30 GB/s on the box against ~54)
     static constexpr size_t kShaderCopyMin = 64u << 10;
     bool d2h_dma = false;
-    bool h2d_dma = false;  // the packer's uploads from pinned memory by the copy engine (MXP_H2D_DMA=1)
-    uint32_t h2d_grid = 128;  // workgroups of the packer's gather kernel (MXP_H2D_GRID)
     bool resolve_tile = true;  // Resolve's default-namespace range walked by resolve_tile (MXP_RESOLVE_TILE)
     // the device packer's column copies (pack_device.cpp)
     // [0] the packer's copies, [1] small read-backs, [2] the packer's kernels (apart from the engine

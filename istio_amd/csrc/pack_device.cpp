@@ -13,7 +13,6 @@
 
 #include "engine_impl.h"
 #include "pack_args.h"
-#include "resolve_args.h"
 
 extern "C" hipError_t mxp_launch_pack(const mxp_pack_args* a, uint32_t step, uint32_t arg, hipStream_t s);
 
@@ -146,37 +145,18 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
             db->pk_ev[k] = nullptr;
             return hipfail(e, "pack event");
         }
-    // copies from pinned caller memory are gathered into one kernel per group (mxp_h2d_gather_kernel:
-    // no gaps between copies); pageable ones, and all with MXP_H2D_DMA=1, are the copy engine's
-    mxp_h2d_list HG;
-    memset(&HG, 0, sizeof HG);
-    auto put = [&](void* dst, const void* src_p, size_t bytes, const char* what) -> int {
-        if (!bytes) return MXP_OK;
-        void* hd = h2d_dma || HG.n == MXP_H2D_MAX ? nullptr : host_dev_ptr(src_p);
-        if (hd) {
-            HG.src[HG.n] = hd;
-            HG.dst[HG.n] = dst;
-            HG.bytes[HG.n] = bytes;
-            HG.n++;
-            return MXP_OK;
-        }
-        if ((e = hipMemcpyAsync(dst, src_p, bytes, hipMemcpyHostToDevice, cs)) != hipSuccess) return hipfail(e, what);
-        return MXP_OK;
-    };
-    auto flush = [&]() -> int {
-        if (HG.n && (e = mxp_launch_h2d_gather(&HG, h2d_grid, cs)) != hipSuccess) return hipfail(e, "upload batch");
-        HG.n = 0;
-        return MXP_OK;
-    };
     auto up = [&](DevBuf& d, const void* src_p, size_t bytes, const char* what) -> int {
         if ((rc = grow(d, bytes ? bytes : 16, what))) return rc;
-        return put(d.p, src_p, bytes, what);
+        if (bytes && (e = hipMemcpyAsync(d.p, src_p, bytes, hipMemcpyHostToDevice, cs)) != hipSuccess)
+            return hipfail(e, what);
+        return MXP_OK;
     };
     const uint64_t sbytes = NS ? b->str_offsets[NS] : 0;
     if ((rc = up(P.pk_soff, b->str_offsets, NS ? ((size_t)NS + 1) * 8 : 0, "upload string offsets"))) return rc;
     // (16 bytes of slack: the intern kernel reads strings 8 bytes at a time)
     if ((rc = grow(P.pk_sbytes, sbytes + 16, "upload string bytes"))) return rc;
-    if ((rc = put(P.pk_sbytes.p, b->str_bytes, sbytes, "upload string bytes"))) return rc;
+    if (sbytes && (e = hipMemcpyAsync(P.pk_sbytes.p, b->str_bytes, sbytes, hipMemcpyHostToDevice, cs)) != hipSuccess)
+        return hipfail(e, "upload string bytes");
     if ((rc = up(P.pk_tsec, b->time_sec, (size_t)NT * 8, "upload times"))) return rc;
     if ((rc = up(P.pk_tnsec, b->time_nsec, (size_t)NT * 4, "upload times"))) return rc;
     // (the batch's own copy of its times, read by the evaluation)
@@ -186,7 +166,6 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = up(P.pk_moff, b->map_offsets, any_map && NM ? ((size_t)NM + 1) * 8 : 0, "upload map offsets"))) return rc;
     if ((rc = up(P.pk_mkey, b->map_keys, E * 4, "upload map keys"))) return rc;
     if ((rc = up(P.pk_mval, b->map_values, E * 4, "upload map values"))) return rc;
-    if ((rc = flush())) return rc;
     if ((e = hipEventRecord(db->pk_ev[0], cs)) != hipSuccess) return hipfail(e, "strings event");
     // (MXP_PACK_COLS_BESIDE=1: the string passes also wait for the columns, as if copied beside)
     std::vector<int32_t> slot_of(b->n_columns, -1);  // batch column -> upload slot
@@ -216,10 +195,10 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
         const size_t bytes[2] = {n, (size_t)n * 8};
         for (int k = 0; k < 2; k++) {
             if ((rc = grow(*bufs[k], bytes[k] ? bytes[k] : 16, "upload columns"))) return rc;
-            if ((rc = put(bufs[k]->p, src[k], bytes[k], "upload columns"))) return rc;
+            if (bytes[k] && (e = hipMemcpyAsync(bufs[k]->p, src[k], bytes[k], hipMemcpyHostToDevice, cs)) != hipSuccess)
+                return hipfail(e, "upload columns");
         }
     }
-    if ((rc = flush())) return rc;
     if ((e = hipEventRecord(db->pk_ev[1], cs)) != hipSuccess) return hipfail(e, "columns event");
     if (resolver.set) {
         res_id_kind = res_bc[0] >= 0 ? P.pk_ck[slot_of[res_bc[0]]].as<uint8_t>() : nullptr;

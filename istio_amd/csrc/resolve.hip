@@ -691,38 +691,3 @@ extern "C" hipError_t mxp_launch_d2h_copy(void* dst, const void* src, uint64_t n
     }
     return hipGetLastError();
 }
-
-// Host -> device gather of up to MXP_H2D_MAX pinned host arrays in ONE launch (the device packer's
-// inputs): src are device addresses of mapped pinned host memory.  The copy engine takes ~9 us
-// between consecutive copies (C2's eight copies per batch: 6 % of the upload); a kernel's 16-byte
-// loads from pinned memory run at the link's rate (57 GB/s, tools/pcie_probe.hip) with no gaps.
-// The pieces are walked in 16-byte units of one global index space; a piece whose source and
-// destination differ in alignment mod 16 goes bytewise.
-extern "C" __global__ __launch_bounds__(256) void mxp_h2d_gather_kernel(mxp_h2d_list L) {
-    const uint64_t tid = blockIdx.x * 256ull + threadIdx.x, stride = (uint64_t)gridDim.x * 256ull;
-    for (uint32_t k = 0; k < L.n; k++) {
-        const uint8_t* __restrict__ src = (const uint8_t*)L.src[k];
-        uint8_t* __restrict__ dst = (uint8_t*)L.dst[k];
-        const uint64_t n = L.bytes[k];
-        const uint64_t mis = (uint64_t)(uintptr_t)dst & 15u;
-        if (mis != ((uint64_t)(uintptr_t)src & 15u)) {
-            for (uint64_t i = tid; i < n; i += stride) dst[i] = src[i];
-            continue;
-        }
-        const uint64_t head = mis ? (16u - mis < n ? 16u - mis : n) : 0u;
-        const uint64_t words = (n - head) >> 4;
-        if (tid < head) dst[tid] = src[tid];
-        uint4* __restrict__ d16 = (uint4*)(dst + head);
-        const uint4* __restrict__ s16 = (const uint4*)(src + head);
-        for (uint64_t i = tid; i < words; i += stride) d16[i] = s16[i];
-        const uint64_t done = head + (words << 4);
-        if (tid < n - done) dst[done + tid] = src[done + tid];
-    }
-}
-
-// grid: workgroups (a few suffice for the link: each thread keeps a 16-byte load in flight; more
-// would hold wave slots the packer's and evaluation's kernels use meanwhile)
-extern "C" hipError_t mxp_launch_h2d_gather(const mxp_h2d_list* L, uint32_t grid, hipStream_t s) {
-    if (L->n) hipLaunchKernelGGL(mxp_h2d_gather_kernel, dim3(grid ? grid : 1u), dim3(256), 0, s, *L);
-    return hipGetLastError();
-}

@@ -29,17 +29,6 @@ typedef struct mxp_ns_args {
 
 #define MXP_RES_SCAN_TILE 256u  // requests per block of the count kernel's block sums
 
-// a batch of host -> device copies for mxp_h2d_gather_kernel (src: device addresses of pinned host
-// memory)
-#define MXP_H2D_MAX 24
-typedef struct mxp_h2d_list {
-    uint32_t n;
-    uint32_t pad;
-    const void* src[MXP_H2D_MAX];
-    void* dst[MXP_H2D_MAX];
-    uint64_t bytes[MXP_H2D_MAX];
-} mxp_h2d_list;
-
 typedef struct mxp_resolve_args {
     uint32_t n;                // requests
     uint32_t n_words;          // ceil(rules / 32)

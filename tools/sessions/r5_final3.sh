@@ -1,4 +1,4 @@
-# round-5 closing session (after asynchronous packing and the gather uploads), part 1: the new
+# round-5 closing session (after asynchronous packing), part 1: the new
 # tests and the fresh-batch timeline first, then the whole GPU suite, smoke, PMC traffic (C2, C4,
 # C5) and SQ counters (C2, C4) of this build.  Summaries land in gpurun_out/r5g.
 set -u
@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp MXP_NO_BUILD=1
 o=gpurun_out/r5g; mkdir -p $o
 sha1sum istio_amd/libmxp.so > $o/lib.sha1
-timeout -k 10 600 python -u -m pytest tests/test_gpu_async_upload.py tests/test_gpu_pack.py -m gpu -x -q \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_async_upload.py -m gpu -x -q \
   --timeout 300 --timeout-method thread > $o/t_new.log 2>&1 || exit $?
 timeout -k 10 240 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $o/fresh_c2 -o run -- \
   python3 tools/fresh_prof.py c2 8 > $o/fresh_c2.log 2>&1 || exit $?
