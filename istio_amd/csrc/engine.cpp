@@ -1609,6 +1609,9 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
         A->vt_imm = db->vt_meta_h.size() >= (size_t)A->n_vt * 8 ? 1u : 0u;
         for (uint32_t a = 0; a < A->n_vt && A->vt_imm; a++)
             if (db->vt_meta_h[a * 8 + MXP_VTM_CAP] != 64u) A->vt_imm = 0u;
+        // (marks sized at the batch's first plan: a plan with more value-class chunks takes the
+        // LDS-row fill)
+        A->vtf_slow = db->vtf_slow.p && db->vtf_slow.n >= MXP_VTF_MARKS(db->n, P.n_vtfills) ? db->vtf_slow.as<uint8_t>() : nullptr;
     }
 }
 
@@ -1710,6 +1713,8 @@ int mxp_engine::vt_prepare(mxp_dbatch* db, const Plan& P) {
         return hipfail(e, "upload vt meta");
     db->vt_t_words = tbase;
     if ((e = db->vt_t.alloc(2 * tbase * 4)) != hipSuccess) return hipfail(e, "vt class words");
+    if (P.n_vtfills && (e = db->vtf_slow.alloc(MXP_VTF_MARKS(db->n, P.n_vtfills))) != hipSuccess)
+        return hipfail(e, "vt fill marks");
     db->vt_meta_h.swap(meta);
     return MXP_OK;
 }

@@ -276,7 +276,7 @@ struct mxp_dbatch {
     uint32_t vt_mask = 0;
     std::vector<uint32_t> vt_capc;         // per candidate slot (0: inactive)
     std::vector<uint32_t> vt_meta_h;       // kargs.vt_meta of the batch's plan (first launch)
-    DevBuf vt_cls, vt_keys, vt_rep, vt_cnt, vt_t, vt_meta;
+    DevBuf vt_cls, vt_keys, vt_rep, vt_cnt, vt_t, vt_meta, vtf_slow;
     size_t vt_t_words = 0, vt_keys_n = 0;
     DevBuf kinds, vals, bstr_off, bstr, map_off, map_keys, map_vals, ipof, tsof;
     DevBuf heads;                                     // [head columns][n] string heads (kargs.heads)

@@ -110,6 +110,10 @@ typedef struct mxp_kargs {
     uint32_t* vt_rep;
     uint32_t n_vt;
     uint32_t vt_imm;             // every active class table has MXP_VTI_CAP (64) slots: mxp_vtfill_imm<n_vt>_kernel
+#define MXP_VTF_TILES 4u         // value-class fill: tiles of 1024 requests per workgroup
+#define MXP_VTF_MARKS(n, chunks) ((((uint64_t)(n) + 1024u * MXP_VTF_TILES - 1u) / (1024u * MXP_VTF_TILES)) * (chunks) * MXP_VTF_TILES * 4u)
+    uint8_t* vtf_slow;           // [fill chunk][block][MXP_VTF_TILES * 4] wave-tiles the immediate-offset fill leaves
+                                 // to mxp_vtfill_imm_slow<n_vt>_kernel (the batch's vtf_slow; null: the LDS-row kernel)
     uint32_t nfa;                // some regexp of the rule set or batch is a bit-parallel NFA: the *_nfa kernels
     unsigned long long* wave_t;  // profiling (MXP_WAVE_TIMES): index kernel waves' {start, end, XCC, 5 phase marks}
     uint8_t* req_err;            // optional [n]: 1 when some rule fails for the request (compact error output)

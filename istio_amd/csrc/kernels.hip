@@ -1275,6 +1275,45 @@ struct DtpQueue {
         q2 = x[4] | x[5] << 16;
         q3 = x[6] | x[7] << 16;
     }
+    // whether some lane's queue holds an error-plane entry (wave-uniform)
+    __device__ __forceinline__ bool any_err() const { return __ballot(has_err()) != 0; }
+    // (pads, 0xFFFF, carry the plane bit too: only real entries count)
+    __device__ __forceinline__ bool has_err() const {
+        bool h = false;
+        const uint32_t w[4] = {q0, q1, q2, q3};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t x = (w[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+            h |= x != 0xFFFFu && (x & 128u);
+        }
+        return h;
+    }
+    // merge() for a group known at compile time (the unrolled fills): the hit test is one compare
+    // with an inline constant, and the error plane is touched only when some lane queued an entry
+    // for it (kErr)
+    template <uint32_t G, bool kErr>
+    __device__ __forceinline__ void merge_c(uint32_t (&m)[4], uint32_t (&e)[4]) {
+        for (;;) {
+            const uint32_t x = q0;
+            const bool hit = ((x >> 8) & 0xFFu) == G;
+            if (!__ballot(hit)) break;
+            const uint32_t b = hit ? 1u << (x & 31u) : 0u, r = (x >> 5) & 3u;
+            const uint32_t bm = (kErr && (x & 128u)) ? 0u : b;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) m[k] |= r == k ? bm : 0u;
+            if (kErr) {
+                const uint32_t be = (x & 128u) ? b : 0u;
+#pragma unroll
+                for (uint32_t k = 0; k < 4; k++) e[k] |= r == k ? be : 0u;
+            }
+            if (hit) {
+                q0 = __builtin_amdgcn_alignbit(q1, q0, 16);
+                q1 = __builtin_amdgcn_alignbit(q2, q1, 16);
+                q2 = __builtin_amdgcn_alignbit(q3, q2, 16);
+                q3 = q3 >> 16 | 0xFFFF0000u;
+            }
+        }
+    }
     // OR the head entries naming group g into the words (pads, 0xFFFF, name no group)
     __device__ __forceinline__ void merge(uint32_t g, uint32_t (&m)[4], uint32_t (&e)[4]) {
         for (;;) {
@@ -1521,7 +1560,6 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_kernel(mxp_kargs A)
 // rows exceed the 32 KB budget gathers from global memory.  100 VGPRs with the deferred-pair queue, 32 KB: 4 workgroups per CU (measured
 // faster than 96 VGPRs forced to 5: C4 1.715 vs 1.78 ms, profiles/r2_v14_ablibs_vtfill_occ_c4.log).
 #define MXP_VTF_STAGE 4096u
-#define MXP_VTF_TILES 4u
 extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_kargs A) {
     __shared__ uint2 S[MXP_VTF_STAGE];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
@@ -1595,12 +1633,40 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_lds_kernel(mxp_karg
 // they are gathered (through the staged word positions) only when some class word of the chunk
 // holds an error bit (none in C4), so LDS holds the match words alone.
 #define MXP_VTI_CAP 64u
-template <uint32_t NVT>
+template <uint32_t V>
+struct GroupC {
+    static constexpr uint32_t value = V;
+    static constexpr bool ct = true;
+};
+struct GroupR {
+    uint32_t value;
+    static constexpr bool ct = false;
+};
+template <uint32_t G, uint32_t NG, typename F>
+__device__ __forceinline__ void for_groups(F& f) {
+    if constexpr (G < NG) {
+        f(GroupC<G>{});
+        for_groups<G + 1, NG>(f);
+    }
+}
+// Two kernels per column count share this body.  The fast one (kSlow false) takes the wave-tiles
+// of the common case -- no guard-kind errors among the wave's requests, no class error words in the
+// chunk, no error-plane pairs in the wave's queues -- with the group loop unrolled at compile time,
+// and marks every other wave-tile in kargs.vtf_slow; the slow one, launched right after on the same
+// grid, runs the general loop on the marked wave-tiles only (a workgroup with none returns before
+// staging).  Keeping the general loop out of the fast kernel keeps its registers at ~50 VGPRs:
+// in one kernel the error paths set the count (147) and with it the occupancy.
+template <uint32_t NVT, bool kSlow>
 __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
     __shared__ uint32_t SM[NVT * MXP_FILL_CHUNK * MXP_VTI_CAP];
     __shared__ uint32_t SJ[NVT * MXP_FILL_CHUNK];  // word position of (slot, group), ~0: none
     __shared__ uint32_t eflag;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
+    // (the wave-tile marks of this workgroup: [MXP_VTF_TILES][4 waves])
+    uint8_t* const slow = A.vtf_slow + ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * (MXP_VTF_TILES * 4u);
+    if constexpr (kSlow) {
+        if (!__syncthreads_or(tid < MXP_VTF_TILES * 4u ? slow[tid] : 0)) return;
+    }
     const mxp_fill* F = A.fills + blockIdx.y;
     const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
     const uint32_t chunk = A.dtp_cbase + blockIdx.y;
@@ -1635,7 +1701,15 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
     for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
         const uint32_t qw = A.q0 + ((blockIdx.x * MXP_VTF_TILES + t) * 4u + wave) * 256u;
         if (qw >= Q1) break;
+        if constexpr (kSlow) {
+            if (!slow[t * 4u + wave]) continue;
+        }
         const uint32_t q0 = qw + lane * 4u;
+        // (the request count passes through an empty asm per tile, so the compiler derives each
+        // unrolled group's row base here instead of hoisting 16 of them out of the tile loop into
+        // spilled scalar registers)
+        uint64_t Nt = N;
+        asm volatile("" : "+s"(Nt));
         const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0 && (q0 & 3u) == 0;
         uint32_t bad[4];
 #pragma unroll
@@ -1644,8 +1718,9 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
             const uint32_t k = in ? A.kinds[(uint64_t)col * N + q0 + r] : 0u;
             bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
         }
-        // each request's row base per slot: [a][g = 0][its class]
-        uint32_t ad[NVT][4];
+        // each request's byte address per slot: [a][g = 0][its class] (kept in registers: the
+        // unrolled groups add only an immediate offset)
+        uint32_t adb[NVT][4];
 #pragma unroll
         for (uint32_t a = 0; a < NVT; a++) {
             const uint16_t* C = A.vt_cls + (uint64_t)a * MXP_VT_PITCH(N);
@@ -1658,76 +1733,106 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
             }
 #pragma unroll
             for (uint32_t r = 0; r < 4; r++)
-                ad[a][r] = a * MXP_FILL_CHUNK * MXP_VTI_CAP + ((uint32_t)(c >> (16u * r)) & (MXP_VTI_CAP - 1u));
+                adb[a][r] = 4u * (a * MXP_FILL_CHUNK * MXP_VTI_CAP + ((uint32_t)(c >> (16u * r)) & (MXP_VTI_CAP - 1u)));
         }
         const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
+        const bool wbad = __ballot(any) != 0;
         DtpQueue dq;
         dq.load(A, chunk, q0, q0 < Q1);
         const bool dany = __ballot(dq.q0 != ~0u) != 0;
+        const bool derr = dany && dq.any_err();
         uint32_t anyerr[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (uint32_t g = 0; g < MXP_FILL_CHUNK; g++) {
-            if (g >= n) break;
+        // One group's words.  GroupC<g> (the fast path: a full chunk, no guard-kind errors in the
+        // wave, no class error words in the chunk, no error-plane pairs in the wave) is unrolled at compile time -- the class words are ds_read_b32 at
+        // the immediate offset g * 256, the pair test compares with an inline constant, the store is
+        // the row's scalar base plus the lane's byte offset; GroupR (runtime g) is the general loop.
+        auto group = [&](auto gc) __attribute__((always_inline)) {
+            constexpr bool ct = decltype(gc)::ct;
+            const uint32_t g = gc.value;
+            if (ct && g >= n) return;  // (a rule set's last chunk: fewer groups)
             const uint32_t G = g0 + g;
-            const uint32_t mask = __builtin_amdgcn_readlane(FM, g);
-            uint32_t m[4] = {0u, 0u, 0u, 0u}, e[4], ve[4] = {0u, 0u, 0u, 0u};
+            uint32_t m[4] = {0u, 0u, 0u, 0u}, e[4] = {0u, 0u, 0u, 0u};
+            if constexpr (!ct) {
+                const uint32_t mask = __builtin_amdgcn_readlane(FM, g);
 #pragma unroll
-            for (int r = 0; r < 4; r++) e[r] = bad[r] & mask;
-            if (A.errlog && any && mask)
-                for (uint32_t r = 0; r < 4; r++)
-                    if (e[r] && q0 + r < Q1) log_guard_errors(A, e[r], G * 32u, q0 + r);
+                for (int r = 0; r < 4; r++) e[r] = bad[r] & mask;
+                if (A.errlog && any && mask)
+                    for (uint32_t r = 0; r < 4; r++)
+                        if (e[r] && q0 + r < Q1) log_guard_errors(A, e[r], G * 32u, q0 + r);
+            }
 #pragma unroll
             for (uint32_t a = 0; a < NVT; a++)
 #pragma unroll
-                for (uint32_t r = 0; r < 4; r++) m[r] |= SM[ad[a][r] + g * MXP_VTI_CAP];
-            if (errs) {
+                for (uint32_t r = 0; r < 4; r++)
+                    m[r] |= *(const uint32_t*)((const char*)SM + adb[a][r] + g * (MXP_VTI_CAP * 4u));
+            if constexpr (!ct) {
+                if (errs) {
+                    uint32_t ve[4] = {0u, 0u, 0u, 0u};
+                    for (uint32_t a = 0; a < NVT; a++) {
+                        const uint32_t j = SJ[a * MXP_FILL_CHUNK + g];
+                        if (j == ~0u) continue;
+                        const uint64_t row = (uint64_t)__builtin_amdgcn_readlane(TB, a) + (uint64_t)j * MXP_VTI_CAP;
 #pragma unroll
-                for (uint32_t a = 0; a < NVT; a++) {
-                    const uint32_t j = SJ[a * MXP_FILL_CHUNK + g];
-                    if (j == ~0u) continue;
-                    const uint64_t row = (uint64_t)__builtin_amdgcn_readlane(TB, a) + (uint64_t)j * MXP_VTI_CAP;
+                        for (uint32_t r = 0; r < 4; r++)
+                            ve[r] |= A.vt_tm[2u * (row + ((adb[a][r] >> 2) & (MXP_VTI_CAP - 1u))) + 1u];
+                    }
+                    if (A.errlog) {
+                        uint32_t c = 0;
 #pragma unroll
-                    for (uint32_t r = 0; r < 4; r++)
-                        ve[r] |= A.vt_tm[2u * (row + (ad[a][r] & (MXP_VTI_CAP - 1u))) + 1u];
+                        for (int r = 0; r < 4; r++) c += q0 + r < Q1 ? (uint32_t)__builtin_popcount(ve[r]) : 0u;
+                        vt_count_n(A, c);
+                    }
+#pragma unroll
+                    for (int r = 0; r < 4; r++) e[r] |= ve[r];
                 }
-                if (A.errlog) {
-                    uint32_t c = 0;
+                if (dany) dq.merge(g, m, e);
 #pragma unroll
-                    for (int r = 0; r < 4; r++) c += q0 + r < Q1 ? (uint32_t)__builtin_popcount(ve[r]) : 0u;
-                    vt_count_n(A, c);
-                }
-#pragma unroll
-                for (int r = 0; r < 4; r++) e[r] |= ve[r];
+                for (uint32_t r = 0; r < 4; r++) anyerr[r] |= e[r];
+            } else {
+                if (dany) dq.template merge_c<decltype(gc)::value, false>(m, e);
             }
-            if (dany) dq.merge(g, m, e);
-#pragma unroll
-            for (uint32_t r = 0; r < 4; r++) anyerr[r] |= e[r];
-            const uint64_t at = (uint64_t)G * N + q0;
+            // (row bases wave-uniform: scalar arithmetic, one address add per store)
+            uint32_t* const om = A.out_match ? A.out_match + (uint64_t)G * Nt : nullptr;
+            uint32_t* const oe = A.out_err ? A.out_err + (uint64_t)G * Nt : nullptr;
             if (vec && q0 < Q1) {
                 const v4u mv = v4u{m[0], m[1], m[2], m[3]};
                 const v4u ev = v4u{e[0], e[1], e[2], e[3]};
                 if (nt) {
-                    if (A.out_match) __builtin_nontemporal_store(mv, (v4u*)(A.out_match + at));
-                    if (A.out_err) __builtin_nontemporal_store(ev, (v4u*)(A.out_err + at));
+                    if (om) __builtin_nontemporal_store(mv, (v4u*)(om + q0));
+                    if (oe) __builtin_nontemporal_store(ev, (v4u*)(oe + q0));
                 } else {
-                    if (A.out_match) *(v4u*)(A.out_match + at) = mv;
-                    if (A.out_err) *(v4u*)(A.out_err + at) = ev;
+                    if (om) *(v4u*)(om + q0) = mv;
+                    if (oe) *(v4u*)(oe + q0) = ev;
                 }
             } else {
                 for (uint32_t r = 0; r < 4; r++) {
                     if (q0 + r >= Q1) break;
-                    if (A.out_match) A.out_match[at + r] = m[r];
-                    if (A.out_err) A.out_err[at + r] = e[r];
+                    if (om) om[q0 + r] = m[r];
+                    if (oe) oe[q0 + r] = e[r];
                 }
             }
+        };
+        if constexpr (kSlow) {
+#pragma nounroll
+            for (uint32_t g = 0; g < n; g++) group(GroupR{g});
+        } else {
+            const bool to_slow = wbad || errs || derr;
+            if (lane == 0) slow[t * 4u + wave] = to_slow ? 1u : 0u;
+            if (to_slow) continue;
+            for_groups<0, MXP_FILL_CHUNK>(group);
         }
         if (A.req_err)
             for (uint32_t r = 0; r < 4; r++)
                 if (anyerr[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;
     }
 }
-#define MXP_VTFILL_IMM(K) \
-    extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_imm##K##_kernel(mxp_kargs A) { vtfill_imm_body<K>(A); }
+#define MXP_VTFILL_IMM(K)                                                                                      \
+    extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_imm##K##_kernel(mxp_kargs A) {                \
+        vtfill_imm_body<K, false>(A);                                                                          \
+    }                                                                                                          \
+    extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_imm_slow##K##_kernel(mxp_kargs A) {           \
+        vtfill_imm_body<K, true>(A);                                                                           \
+    }
 MXP_VTFILL_IMM(1)
 MXP_VTFILL_IMM(2)
 MXP_VTFILL_IMM(3)
@@ -2662,21 +2767,30 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
         const dim3 grid((args->q1 - args->q0 + per - 1u) / per, n_fills);
         // every active class table at 64 slots: the immediate-offset kernel for this many columns
         // (flag 33554432: mxp_vtfill_lds_kernel -- A/B)
+        // (and its general loop for the wave-tiles it leaves, kargs.vtf_slow)
         void (*k)(mxp_kargs) = mxp_vtfill_lds_kernel;
-        if (args->vt_imm && !(args->flags & 33554432u)) {
+        void (*ks)(mxp_kargs) = nullptr;
+        if (args->vt_imm && args->vtf_slow && !(args->flags & 33554432u)) {
             switch (args->n_vt) {
-            case 1: k = mxp_vtfill_imm1_kernel; break;
-            case 2: k = mxp_vtfill_imm2_kernel; break;
-            case 3: k = mxp_vtfill_imm3_kernel; break;
-            case 4: k = mxp_vtfill_imm4_kernel; break;
-            case 5: k = mxp_vtfill_imm5_kernel; break;
-            case 6: k = mxp_vtfill_imm6_kernel; break;
-            case 7: k = mxp_vtfill_imm7_kernel; break;
-            case 8: k = mxp_vtfill_imm8_kernel; break;
+#define MXP_VTFILL_CASE(K)                  \
+    case K:                                 \
+        k = mxp_vtfill_imm##K##_kernel;      \
+        ks = mxp_vtfill_imm_slow##K##_kernel; \
+        break;
+                MXP_VTFILL_CASE(1)
+                MXP_VTFILL_CASE(2)
+                MXP_VTFILL_CASE(3)
+                MXP_VTFILL_CASE(4)
+                MXP_VTFILL_CASE(5)
+                MXP_VTFILL_CASE(6)
+                MXP_VTFILL_CASE(7)
+                MXP_VTFILL_CASE(8)
+#undef MXP_VTFILL_CASE
             default: break;
             }
         }
         hipLaunchKernelGGL(k, grid, dim3(256), 0, s, *args);
+        if (ks) hipLaunchKernelGGL(ks, grid, dim3(256), 0, s, *args);
     }
     return hipGetLastError();
 }
