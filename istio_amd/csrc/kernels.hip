@@ -1145,15 +1145,11 @@ extern "C" hipError_t mxp_launch_vtd_final(const mxp_kargs* args, const mxp_vtd_
 
 // The evaluation's class of every request [q0, q1) per active column: a read-only probe of the
 // batch's dictionary (built at upload by mxp_vt_classify_kernel, so it holds every key of the
-// batch), whose few hot lines stay in L1.  grid (request blocks of 256, active columns).
-extern "C" __global__ __launch_bounds__(256) void mxp_vt_lookup_kernel(mxp_kargs A) {
-    const uint32_t a = blockIdx.y, req = A.q0 + blockIdx.x * 256u + threadIdx.x;
-    if (req >= A.q1) return;
-    const uint64_t N = A.n;
-    const uint32_t col = uni(A.vt_meta[a * 8u + MXP_VTM_COL]), cap = uni(A.vt_meta[a * 8u + MXP_VTM_CAP]),
-                   kb = uni(A.vt_meta[a * 8u + MXP_VTM_KBASE]);
-    const unsigned long long key = mxp_vt_key(A.kinds[(uint64_t)col * N + req], A.vals[(uint64_t)col * N + req]);
-    const unsigned long long* __restrict__ T = A.vt_keys + kb;
+// batch), whose few hot lines stay in L1.  A thread takes 4 consecutive requests: one 4-byte kinds
+// load, two 16-byte value loads and one 8-byte class store, and four independent probes in flight
+// (one request per thread measured 30 us on C4).  grid (request blocks of 1024, active columns).
+__device__ __forceinline__ uint32_t vt_probe(const unsigned long long* __restrict__ T, uint32_t cap,
+                                             unsigned long long key) {
     uint32_t h = mxp_hash64(key) & (cap - 1u);
     // (every batch key is in the table, which is at most half full: the probe ends at the key; an
     // empty slot -- a batch changed after upload -- ends it too, on a slot vt_eval leaves at 0)
@@ -1161,7 +1157,29 @@ extern "C" __global__ __launch_bounds__(256) void mxp_vt_lookup_kernel(mxp_kargs
         const unsigned long long k = T[h];
         if (k == key || k == MXP_VT_EMPTY) break;
     }
-    A.vt_cls[(uint64_t)a * MXP_VT_PITCH(N) + req] = (uint16_t)h;
+    return h;
+}
+extern "C" __global__ __launch_bounds__(256) void mxp_vt_lookup_kernel(mxp_kargs A) {
+    const uint32_t a = blockIdx.y, q = A.q0 + (blockIdx.x * 256u + threadIdx.x) * 4u, Q1 = A.q1;
+    if (q >= Q1) return;
+    const uint64_t N = A.n;
+    const uint32_t col = uni(A.vt_meta[a * 8u + MXP_VTM_COL]), cap = uni(A.vt_meta[a * 8u + MXP_VTM_CAP]),
+                   kb = uni(A.vt_meta[a * 8u + MXP_VTM_KBASE]);
+    const unsigned long long* __restrict__ T = A.vt_keys + kb;
+    const uint64_t at = (uint64_t)col * N + q;
+    uint16_t* const C = A.vt_cls + (uint64_t)a * MXP_VT_PITCH(N) + q;
+    if ((N & 3u) == 0 && (q & 3u) == 0 && q + 4u <= Q1) {
+        const uint32_t k4 = *(const uint32_t*)(A.kinds + at);
+        const ulonglong2 v01 = *(const ulonglong2*)(A.vals + at), v23 = *(const ulonglong2*)(A.vals + at + 2u);
+        const uint32_t h0 = vt_probe(T, cap, mxp_vt_key(k4 & 0xFFu, v01.x));
+        const uint32_t h1 = vt_probe(T, cap, mxp_vt_key((k4 >> 8) & 0xFFu, v01.y));
+        const uint32_t h2 = vt_probe(T, cap, mxp_vt_key((k4 >> 16) & 0xFFu, v23.x));
+        const uint32_t h3 = vt_probe(T, cap, mxp_vt_key(k4 >> 24, v23.y));
+        *(uint64_t*)C = (uint64_t)h0 | (uint64_t)h1 << 16 | (uint64_t)h2 << 32 | (uint64_t)h3 << 48;
+        return;
+    }
+    for (uint32_t r = 0; r < 4u && q + r < Q1; r++)
+        C[r] = (uint16_t)vt_probe(T, cap, mxp_vt_key(A.kinds[at + r], A.vals[at + r]));
 }
 
 // grid x: class tiles of 64 (slot by slot), y: groups of 4 words (one per wave)
@@ -1264,6 +1282,11 @@ struct DtpQueue {
         const uint64_t qi = (uint64_t)chunk * MXP_DTP_ROW(A.dtp_tiles) + (req0 >> 2);
         const uint32_t dk = A.dtp_qn[qi];
         const v4u sl = *(const v4u*)(A.dtp_slots + qi * 8u);
+        decode(dk, sl);
+    }
+    // the sorted queue from a quad's raw count and slot row (load, or a prefetch of them)
+    template <typename V4>
+    __device__ __forceinline__ void decode(uint32_t dk, const V4& sl) {
         if (!dk) return;
         const uint32_t h[4] = {sl.x, sl.y, sl.z, sl.w};
         uint32_t x[8];
@@ -1657,19 +1680,19 @@ __device__ __forceinline__ void for_groups(F& f) {
 // staging).  Keeping the general loop out of the fast kernel keeps its registers at ~50 VGPRs:
 // in one kernel the error paths set the count (147) and with it the occupancy.
 template <uint32_t NVT, bool kSlow>
-__device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
+__device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A, uint32_t bx, uint32_t by, uint32_t gx) {
     __shared__ uint32_t SM[NVT * MXP_FILL_CHUNK * MXP_VTI_CAP];
     __shared__ uint32_t SJ[NVT * MXP_FILL_CHUNK];  // word position of (slot, group), ~0: none
     __shared__ uint32_t eflag;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uni(tid >> 6);
     // (the wave-tile marks of this workgroup: [MXP_VTF_TILES][4 waves])
-    uint8_t* const slow = A.vtf_slow + ((uint64_t)blockIdx.y * gridDim.x + blockIdx.x) * (MXP_VTF_TILES * 4u);
+    uint8_t* const slow = A.vtf_slow + ((uint64_t)by * gx + bx) * (MXP_VTF_TILES * 4u);
     if constexpr (kSlow) {
         if (!__syncthreads_or(tid < MXP_VTF_TILES * 4u ? slow[tid] : 0)) return;
     }
-    const mxp_fill* F = A.fills + blockIdx.y;
+    const mxp_fill* F = A.fills + by;
     const uint32_t col = uni(F->col), okset = uni(F->okset), g0 = uni(F->g0), n = uni(F->n), moff = uni(F->moff);
-    const uint32_t chunk = A.dtp_cbase + blockIdx.y;
+    const uint32_t chunk = A.dtp_cbase + by;
     // 1. staging: zero, then each (group, slot) merge entry's 64 class words into its fixed row
     for (uint32_t i = tid; i < NVT * MXP_FILL_CHUNK * MXP_VTI_CAP; i += 256u) SM[i] = 0u;
     if (tid < NVT * MXP_FILL_CHUNK) SJ[tid] = ~0u;
@@ -1698,29 +1721,25 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
     const bool nt = !(A.flags & 128u);
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     const uint32_t FM = lane < n ? A.fill_masks[moff + lane] : 0u;
-    for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
-        const uint32_t qw = A.q0 + ((blockIdx.x * MXP_VTF_TILES + t) * 4u + wave) * 256u;
-        if (qw >= Q1) break;
-        if constexpr (kSlow) {
-            if (!slow[t * 4u + wave]) continue;
-        }
-        const uint32_t q0 = qw + lane * 4u;
-        // (the request count passes through an empty asm per tile, so the compiler derives each
-        // unrolled group's row base here instead of hoisting 16 of them out of the tile loop into
-        // spilled scalar registers)
-        uint64_t Nt = N;
-        asm volatile("" : "+s"(Nt));
+    // A wave-tile's inputs: the guard column's kinds, the classes per slot, the deferred-pair queue's
+    // count and slot row.  The fast kernel loads tile t + 1's while tile t's words are stored: its
+    // loads then wait only for themselves, not for the tile's 16 stores ahead of them in the
+    // memory counter.
+    struct TileIn {
+        uint32_t k4, dk;
+        uint64_t c[NVT];
+        v4u sl;
+    };
+    auto fetch = [&](uint32_t t, TileIn& T) __attribute__((always_inline)) {
+        const uint32_t q0 = A.q0 + ((bx * MXP_VTF_TILES + t) * 4u + wave) * 256u + lane * 4u;
         const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0 && (q0 & 3u) == 0;
-        uint32_t bad[4];
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-            const bool in = q0 + r < Q1;
-            const uint32_t k = in ? A.kinds[(uint64_t)col * N + q0 + r] : 0u;
-            bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
+        T.k4 = 0u;
+        if (vec && q0 < Q1) {
+            T.k4 = *(const uint32_t*)(A.kinds + (uint64_t)col * N + q0);
+        } else {
+            for (uint32_t r = 0; r < 4; r++)
+                if (q0 + r < Q1) T.k4 |= (uint32_t)A.kinds[(uint64_t)col * N + q0 + r] << (8u * r);
         }
-        // each request's byte address per slot: [a][g = 0][its class] (kept in registers: the
-        // unrolled groups add only an immediate offset)
-        uint32_t adb[NVT][4];
 #pragma unroll
         for (uint32_t a = 0; a < NVT; a++) {
             const uint16_t* C = A.vt_cls + (uint64_t)a * MXP_VT_PITCH(N);
@@ -1731,14 +1750,58 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
                 for (uint32_t r = 0; r < 4; r++)
                     if (q0 + r < Q1) c |= (uint64_t)C[q0 + r] << (16u * r);
             }
+            T.c[a] = c;
+        }
+        T.dk = 0u;
+        T.sl = v4u{0u, 0u, 0u, 0u};
+        if (A.dtp_slots && q0 < Q1) {
+            const uint64_t qi = (uint64_t)chunk * MXP_DTP_ROW(A.dtp_tiles) + (q0 >> 2);
+            T.dk = A.dtp_qn[qi];
+            T.sl = *(const v4u*)(A.dtp_slots + qi * 8u);
+        }
+    };
+    TileIn nx;
+    if constexpr (!kSlow) fetch(0u, nx);
+    for (uint32_t t = 0; t < MXP_VTF_TILES; t++) {
+        const uint32_t qw = A.q0 + ((bx * MXP_VTF_TILES + t) * 4u + wave) * 256u;
+        if (qw >= Q1) break;
+        if constexpr (kSlow) {
+            if (!slow[t * 4u + wave]) continue;
+        }
+        TileIn cur;
+        if constexpr (kSlow)
+            fetch(t, cur);
+        else
+            cur = nx;
+        const uint32_t q0 = qw + lane * 4u;
+        // (the request count passes through an empty asm per tile, so the compiler derives each
+        // unrolled group's row base here instead of hoisting 16 of them out of the tile loop into
+        // spilled scalar registers)
+        uint64_t Nt = N;
+        asm volatile("" : "+s"(Nt));
+        const bool vec = (N & 3u) == 0 && (Q1 & 3u) == 0 && (q0 & 3u) == 0;
+        uint32_t bad[4];
+#pragma unroll
+        for (uint32_t r = 0; r < 4; r++) {
+            const bool in = q0 + r < Q1;
+            const uint32_t k = (cur.k4 >> (8u * r)) & 0xFFu;
+            bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
+        }
+        // each request's byte address per slot: [a][g = 0][its class] (kept in registers: the
+        // unrolled groups add only an immediate offset)
+        uint32_t adb[NVT][4];
+#pragma unroll
+        for (uint32_t a = 0; a < NVT; a++)
 #pragma unroll
             for (uint32_t r = 0; r < 4; r++)
-                adb[a][r] = 4u * (a * MXP_FILL_CHUNK * MXP_VTI_CAP + ((uint32_t)(c >> (16u * r)) & (MXP_VTI_CAP - 1u)));
-        }
+                adb[a][r] = 4u * (a * MXP_FILL_CHUNK * MXP_VTI_CAP + ((uint32_t)(cur.c[a] >> (16u * r)) & (MXP_VTI_CAP - 1u)));
         const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
         const bool wbad = __ballot(any) != 0;
         DtpQueue dq;
-        dq.load(A, chunk, q0, q0 < Q1);
+        dq.decode(cur.dk, cur.sl);
+        if constexpr (!kSlow) {
+            if (t + 1u < MXP_VTF_TILES) fetch(t + 1u, nx);
+        }
         const bool dany = __ballot(dq.q0 != ~0u) != 0;
         const bool derr = dany && dq.any_err();
         uint32_t anyerr[4] = {0u, 0u, 0u, 0u};
@@ -1826,12 +1889,24 @@ __device__ __forceinline__ void vtfill_imm_body(const mxp_kargs& A) {
                 if (anyerr[r] && q0 + r < Q1) A.req_err[q0 + r] = 1;
     }
 }
+static_assert(MXP_VTF_TILES * 4u == 16u, "mxp_vtfill_imm_slow: a thread per mark of 16 blocks");
 #define MXP_VTFILL_IMM(K)                                                                                      \
     extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_imm##K##_kernel(mxp_kargs A) {                \
-        vtfill_imm_body<K, false>(A);                                                                          \
+        vtfill_imm_body<K, false>(A, blockIdx.x, blockIdx.y, gridDim.x);                                       \
     }                                                                                                          \
-    extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_imm_slow##K##_kernel(mxp_kargs A) {           \
-        vtfill_imm_body<K, true>(A);                                                                           \
+    extern "C" __global__ __launch_bounds__(256) void mxp_vtfill_imm_slow##K##_kernel(mxp_kargs A, uint32_t gx, \
+                                                                                     uint32_t gy) {            \
+        __shared__ uint32_t bm;                                                                                \
+        const uint32_t vb0 = blockIdx.x * 16u, vb = vb0 + threadIdx.x / 16u;                                   \
+        if (threadIdx.x == 0) bm = 0u;                                                                         \
+        __syncthreads();                                                                                       \
+        if (vb < gx * gy && A.vtf_slow[(uint64_t)vb * (MXP_VTF_TILES * 4u) + threadIdx.x % 16u])               \
+            atomicOr(&bm, 1u << (threadIdx.x / 16u));                                                          \
+        __syncthreads();                                                                                       \
+        for (uint32_t m = bm; m; m &= m - 1u) {                                                                \
+            const uint32_t b = vb0 + (uint32_t)__builtin_ctz(m);                                               \
+            vtfill_imm_body<K, true>(A, b % gx, b / gx, gx);                                                   \
+        }                                                                                                      \
     }
 MXP_VTFILL_IMM(1)
 MXP_VTFILL_IMM(2)
@@ -2769,7 +2844,7 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
         // (flag 33554432: mxp_vtfill_lds_kernel -- A/B)
         // (and its general loop for the wave-tiles it leaves, kargs.vtf_slow)
         void (*k)(mxp_kargs) = mxp_vtfill_lds_kernel;
-        void (*ks)(mxp_kargs) = nullptr;
+        void (*ks)(mxp_kargs, uint32_t, uint32_t) = nullptr;
         if (args->vt_imm && args->vtf_slow && !(args->flags & 33554432u)) {
             switch (args->n_vt) {
 #define MXP_VTFILL_CASE(K)                  \
@@ -2790,7 +2865,10 @@ extern "C" hipError_t mxp_launch_vtfill(const mxp_kargs* args, uint32_t n_fills,
             }
         }
         hipLaunchKernelGGL(k, grid, dim3(256), 0, s, *args);
-        if (ks) hipLaunchKernelGGL(ks, grid, dim3(256), 0, s, *args);
+        // (the slow kernel's workgroups take 16 of the fast grid's blocks each: one flag byte per
+        // thread, then the marked blocks in turn -- a launch of the fast grid's 5,120 blocks, each
+        // reading its marks, took 7 us on C4)
+        if (ks) hipLaunchKernelGGL(ks, dim3((grid.x * grid.y + 15u) / 16u), dim3(256), 0, s, *args, grid.x, grid.y);
     }
     return hipGetLastError();
 }
@@ -2808,7 +2886,7 @@ extern "C" hipError_t mxp_launch_vt_classify(const mxp_kargs* args, hipStream_t 
 }
 
 extern "C" hipError_t mxp_launch_vt_lookup(const mxp_kargs* args, hipStream_t s) {
-    hipLaunchKernelGGL(mxp_vt_lookup_kernel, dim3((args->q1 - args->q0 + 255u) / 256u, args->n_vt), dim3(256), 0, s, *args);
+    hipLaunchKernelGGL(mxp_vt_lookup_kernel, dim3((args->q1 - args->q0 + 1023u) / 1024u, args->n_vt), dim3(256), 0, s, *args);
     return hipGetLastError();
 }
 
