@@ -13,6 +13,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 # minimum waves/SIMD per kernel (launch_bounds(256) kernels; the values the launches were tuned at)
 MIN_OCCUPANCY = {"mxp_index_dtp_lite_kernel": 5, "mxp_guard_kernel": 8, "mxp_guard2_kernel": 6, "mxp_eval_kernel": 4, "mxp_index_kernel": 6, "mxp_index_dtp_kernel": 5, "mxp_index5_kernel": 5}
+# (r5: the fast value-class fill is latency bound -- its error paths live in the slow kernel so that
+# it keeps 6 waves/SIMD; at 3 it measured 354 against 277 us on C4, profiles/r5_s2{0,2}_*)
+MIN_OCCUPANCY.update({"mxp_vtfill_imm%d_kernel" % k: 6 for k in range(1, 6)})
 # bounded scratch, chosen by A/B: mxp_index_kernel at 6 waves/SIMD spills a few VGPRs (<= 40 bytes per
 # lane) and still beats the spill-free 5-wave build (mxp_index5_kernel) on C4 (5.10 vs 5.31 ms)
 # (6 waves/SIMD: a few VGPRs spill -- windowed DFA walk, same-box A/B C4 2.67-2.77 -> 2.57-2.66 ms; the
