@@ -33,6 +33,7 @@ extern "C" {
 #define MXP_ERR_NOMEM 4
 
 typedef struct mxp_engine mxp_engine;
+typedef struct mxp_dbatch mxp_dbatch;  /* a device-resident batch (mxp_batch_upload) */
 
 /* Engine lifetime.  device = HIP device ordinal; device = -1 creates a host-only engine that can
  * compile and inspect rule sets (IL text, VM listing) but not evaluate. */
@@ -196,6 +197,14 @@ int mxp_resolve_batch(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t vari
 #define MXP_RESOLVE_IDS_U16 1u
 int mxp_resolve_batch_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
                          uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap);
+/* mxp_resolve_batch_ex over a batch uploaded before (mxp_batch_upload / mxp_batch_upload_ex, e.g. with
+ * MXP_UPLOAD_NO_WAIT one call ahead, so that batch k + 1's copies and device packing overlap batch
+ * k's Resolve -- the Go micro-batcher's double buffering).  `batch` is the host batch db was
+ * uploaded from, unchanged (error texts and host passes read it).  The call takes db over, whatever
+ * it returns: the engine keeps it as the last batch (mxp_pair_error) and recycles it with the next
+ * one; the caller does not mxp_batch_free it. */
+int mxp_resolve_uploaded(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
+                         uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap);
 /* mxp_resolve_batch plus each Resolve's referenced attributes (mxp_attr_ref, as mxp_eval_refs): the
  * identity attribute; when it is a string, context.protocol (filterActions, resolver.go:208); and the
  * reads of the predicates filterActions evaluates, in order, up to and including the first that
@@ -348,7 +357,6 @@ void mxp_host_free(void* p);
  * and the batch's first evaluation waits for them and finishes the packing (value-class tables,
  * string heads, dictionary).  Uploading batch k + 1 before evaluating batch k overlaps one batch's
  * copies with the other's packing and evaluation. */
-typedef struct mxp_dbatch mxp_dbatch;
 int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out);
 /* mxp_batch_upload with flags.  MXP_UPLOAD_NO_WAIT: return once the copies are queued and the
  * batch checked, before the copies are in; the caller keeps the arrays unchanged until

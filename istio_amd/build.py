@@ -18,7 +18,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MXP_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["goutil.cpp", "frontend.cpp", "ilgen.cpp", "lower.cpp", "vmopt.cpp", "regex.cpp", "engine.cpp",
-           "resolver.cpp", "refs.cpp", "wire.cpp", "lists.cpp", "quota.cpp", "pack_device.cpp", "kernels.hip", "resolve.hip", "lists.hip", "quota.hip", "pack.hip"]
+           "resolver.cpp", "refs.cpp", "wire.cpp", "lists.cpp", "quota.cpp", "pack_device.cpp", "kernels.hip", "resolve.hip", "lists.hip", "quota.hip", "pack.hip", "group.cpp", "group.hip"]
 HEADERS = ["goutil.h", "frontend.h", "ilgen.h", "lower.h", "vmopt.h", "vm.h", "kargs.h", "engine_impl.h", "resolve_args.h", "netparse.h", "timeparse.h", "lists.h", "regex.h", "unicode_tables.h", "dfa_dev.h", "quota_args.h", "pack_args.h", "par.h", "goupper.h", "upper_table.h"]
 
 
@@ -27,7 +27,7 @@ def _stale():
         return True
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
-    deps += [os.path.join(HERE, "..", "include", f) for f in ("mxp.h", "mxp_batch.h")]
+    deps += [os.path.join(HERE, "..", "include", f) for f in ("mxp.h", "mxp_batch.h", "mxp_group.h")]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
@@ -74,7 +74,7 @@ def _build(verbose: bool) -> str:
         msg = "\n".join("== %s\n%s" % f for f in failed)
         raise RuntimeError("libmxp build failed:\n" + msg)
     tmp = LIB + ".tmp"
-    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs
+    cmd = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", tmp] + objs + ["-ldl"]
     subprocess.check_call(cmd)
     os.replace(tmp, LIB)
     return LIB

@@ -809,11 +809,11 @@ int mxp_engine::build_plan(Plan& P) {
     for (uint32_t x : P.vt_nw) P.vt_max_nw = std::max(P.vt_max_nw, x);
 
     // phase-1 group tables: mode masks, column segments, guard constants
-    std::vector<mxp_group> groups(W);
+    std::vector<mxp_rgroup> groups(W);
     std::vector<mxp_seg> segs;
     std::vector<uint64_t> gk((size_t)W * 32, 0);
     for (uint32_t g = 0; g < W; g++) {
-        mxp_group& G = groups[g];
+        mxp_rgroup& G = groups[g];
         memset(&G, 0, sizeof G);
         std::vector<mxp_seg> seg_of;
         for (uint32_t k = 0; k < 32 && g * 32 + k < n; k++) {
@@ -867,7 +867,7 @@ int mxp_engine::build_plan(Plan& P) {
         // merged deferred pairs; deep rules are never templated, hence never indexed, so this only
         // states what hoist_continuation already guarantees)
         (deep[g] ? gdeep : gall).push_back(g);
-        const mxp_group& G = groups[g];
+        const mxp_rgroup& G = groups[g];
         const bool has_vt = gvt_off[g + 1] > gvt_off[g];
         // uniform indexed group: every rule indexed, one guard column, nothing compared in-wave --
         // its words depend only on that column's kind (and the value classes' merge entries); a
@@ -918,7 +918,7 @@ int mxp_engine::build_plan(Plan& P) {
     // columns < MXP_CC the lean groups read: mxp_guard2_kernel loads them into LDS up front
     P.lean_cc = 0;
     for (uint32_t g : glean) {
-        const mxp_group& G = groups[g];
+        const mxp_rgroup& G = groups[g];
         if (G.nseg && G.s_col < MXP_CC) P.lean_cc |= 1u << G.s_col;
         for (uint32_t k = 0; k + 1 < G.nseg; k++)
             if (segs[G.seg0 + k].col < MXP_CC) P.lean_cc |= 1u << segs[G.seg0 + k].col;
@@ -1002,7 +1002,7 @@ int mxp_engine::build_plan(Plan& P) {
     };
     int rc;
     if ((rc = put(P.d_guards, guards.data(), guards.size() * sizeof(mxp_guard), "upload guards"))) return rc;
-    if ((rc = put(P.d_groups, groups.data(), groups.size() * sizeof(mxp_group), "upload groups"))) return rc;
+    if ((rc = put(P.d_groups, groups.data(), groups.size() * sizeof(mxp_rgroup), "upload groups"))) return rc;
     if ((rc = put(P.d_segs, segs.data(), segs.size() * sizeof(mxp_seg), "upload segs"))) return rc;
     if ((rc = put(P.d_glean, glean.data(), glean.size() * 4, "upload glean"))) return rc;
     if ((rc = put(P.d_fills, fills.data(), fills.size() * sizeof(mxp_fill), "upload fills"))) return rc;
@@ -1546,7 +1546,7 @@ void mxp_engine::fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) co
     A->prog = d_prog.as<mxp_vm_ins>();
     A->rule_off = d_rule_off.as<uint32_t>();
     A->guards = P.d_guards.as<mxp_guard>();
-    A->groups = P.d_groups.as<mxp_group>();
+    A->groups = P.d_groups.as<mxp_rgroup>();
     A->segs = P.d_segs.as<mxp_seg>();
     A->gk = P.d_gk.as<uint64_t>();
     A->idx = P.d_idx.as<mxp_index>();
@@ -2730,7 +2730,13 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
     g_bin_db = nullptr;
     if (rc) return rc;
     trace_mark("pack + upload");
-    const uint32_t n = batch->n_requests;
+    return evaluate_uploaded(db.get(), dm, de, dv, d_req_err);
+}
+
+int mxp_engine::evaluate_uploaded(mxp_dbatch* db, DevBuf& dm, DevBuf& de, DevBuf* dv, uint8_t* d_req_err) {
+    hipError_t e;
+    int rc;
+    const uint32_t n = db->n;
     const uint32_t R = (uint32_t)rules.size();
     const uint32_t W = (R + 31) / 32;
     if ((e = dm.reserve((size_t)W * n * 4)) != hipSuccess) return hipfail(e, "alloc match");
@@ -2738,7 +2744,7 @@ int mxp_engine::evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, Dev
     if (dv && (e = dv->reserve((size_t)n * R * 8)) != hipSuccess) return hipfail(e, "alloc values");
     trace_mark("bitmap allocation");
     req_err_out = d_req_err;
-    rc = launch(db.get(), stream, dm.as<uint32_t>(), d_req_err ? nullptr : de.as<uint32_t>(),
+    rc = launch(db, stream, dm.as<uint32_t>(), d_req_err ? nullptr : de.as<uint32_t>(),
                 dv ? dv->as<uint64_t>() : nullptr, true);
     req_err_out = nullptr;
     trace_mark("evaluation kernels");

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -53,6 +54,16 @@ extern "C" hipError_t mxp_launch_hits(const uint32_t* match, uint32_t n, uint32_
 extern "C" hipError_t mxp_launch_hits_gate(const unsigned long long* stats, uint32_t n, uint32_t n_words,
                                            uint32_t* gate, uint32_t force, hipStream_t s);
 
+
+// mxp_resolve_batch_ex for one member of a device group (group.cpp): once the request's selected-rule
+// count of the batch is known, place(total) returns the index in the caller's sel_rules where this
+// batch's ids go (blocking until every member knows its count), or -1 when the whole list does not
+// fit; the ids are then downloaded straight there.  sel_off gets the batch-local offsets.
+using mxp_resolve_place = std::function<int64_t(uint64_t)>;
+// db (nullable): the batch, uploaded before and taken over by the call (mxp_resolve_uploaded)
+int mxp_resolve_placed(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
+                       uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules,
+                       const mxp_resolve_place& place);
 
 // Device blocks of freed batches, reused by later uploads (mxp_batch_free hands a batch's blocks to
 // its engine's bin with events recorded on every stream that read the batch; mxp_batch_upload draws
@@ -314,6 +325,14 @@ struct mxp_dbatch {
             if (ev) (void)hipEventDestroy(ev);
     }
     int note_done(hipStream_t s);  // record (creating on first use) the completion event of stream s
+    // set by pack_device (the batch's own scratch, pk): the raw identity / context.protocol columns as
+    // uploaded (nullptr: absent from the batch), for the Resolve's device namespaces; res_raw = false
+    // when the host packer ran or the columns were not uploaded
+    bool res_raw = false;
+    const uint8_t* res_id_kind = nullptr;
+    const uint64_t* res_id_val = nullptr;
+    const uint8_t* res_pr_kind = nullptr;
+    const uint64_t* res_pr_val = nullptr;
     bool vtd_ready = false;  // the packer's provisional class tables (engine scratch) hold this batch's
     uint32_t ns = 0, nt = 0, G = 0, GB = 0, GC = 0, GT = 0;
     DevBuf pip, pip_ok, pts_sec, pts_nsec, pts_ok, btsec, btnsec;
@@ -643,14 +662,6 @@ struct mxp_engine : public mxp::LowerTables {
     // of content hashes, descriptors, bytes
     DevBuf res_ns_tab, res_ns_desc, res_ns_blob;
     uint32_t res_ns_mask = 0;
-    // set by pack_device for the batch it packed (engine scratch, valid until the next upload): the
-    // raw identity / context.protocol columns as uploaded (nullptr: absent from the batch) and the
-    // raw batch strings; res_raw = false when the host packer ran or the columns were not uploaded
-    bool res_raw = false;
-    const uint8_t* res_id_kind = nullptr;
-    const uint64_t* res_id_val = nullptr;
-    const uint8_t* res_pr_kind = nullptr;
-    const uint64_t* res_pr_val = nullptr;
     uint64_t last_error_count = 0;
     std::unique_ptr<mxp_dbatch> last_db;  // keeps the last batch's interned overlays for decoding
 
@@ -816,6 +827,8 @@ struct mxp_engine : public mxp::LowerTables {
     void recycle(mxp_dbatch* db);  // a batch no longer used: its blocks to the bin (mxp_batch_free)
     // pack + launch into fresh device bitmaps (dm, de; dv = Eval registers when non-null)
     // d_req_err: compact error output (per-request flags; de is not written)
+    // ... of a batch already uploaded (mxp_batch_upload; the Resolve of a batch uploaded ahead)
+    int evaluate_uploaded(mxp_dbatch* db, DevBuf& dm, DevBuf& de, DevBuf* dv, uint8_t* d_req_err);
     int evaluate(const mxp_bag_batch* batch, DevBuf& dm, DevBuf& de, DevBuf* dv, std::unique_ptr<mxp_dbatch>& db,
                  uint8_t* d_req_err = nullptr);
     // wait for the evaluation, fetch and format its error records, keep `db` as the last batch
@@ -839,7 +852,7 @@ struct mxp_engine : public mxp::LowerTables {
     // after it has queued the batch's H2D copies (from pinned caller memory the check overlaps them;
     // no kernel reads the batch before the check has passed), else first.
     int pack(const mxp_bag_batch* b, mxp_dbatch* db) {
-        res_raw = false;
+        db->res_raw = false;
         const bool dev = !host_pack && cols.size() + vcols.size() <= MXP_PACK_MAXCOL;
         if (!dev)
             if (int rc0 = check_batch(b)) return rc0;
@@ -877,6 +890,7 @@ struct mxp_engine : public mxp::LowerTables {
     // the rest of a device-packed batch's upload, at its first evaluation (pack_device.cpp): the
     // value-class sizing from the packer's distinct counts, the class tables, heads, dictionary
     int finish_pack(mxp_dbatch* db);
+    bool finish_fail_done = false;  // (test hook of finish_pack, MXP_DEBUG_FLAGS 1 << 29)
     uint32_t vcol_key_id(uint32_t j) const {
         auto it = gstr_ids.find(vcols[j].second);
         return it == gstr_ids.end() ? 0xFFFFFFFEu : it->second;

@@ -25,7 +25,7 @@ typedef struct mxp_kargs {
     const mxp_vm_ins* prog;      // all rules' programs, concatenated
     const uint32_t* rule_off;    // [n_rules + 1]
     const mxp_guard* guards;     // [n_rules] leading-atom guards (vmopt.h)
-    const mxp_group* groups;     // [n_words] per-group guard masks
+    const mxp_rgroup* groups;     // [n_words] per-group guard masks
     const uint32_t* glist;       // groups this launch evaluates (ids into groups)
     const mxp_fill* fills;       // mxp_fill_kernel: chunks of uniform indexed groups
     uint32_t n_glist;

@@ -175,7 +175,7 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     // the resolver's identity and context.protocol columns as given (mxp_ns_kernel reads them with the
     // raw batch strings): the first batch column of each name, uploaded with the rule columns
     int32_t res_bc[2] = {-1, -1};
-    res_raw = false;
+    db->res_raw = false;
     if (resolver.set) {
         const std::string_view nm[2] = {resolver.identity, "context.protocol"};
         for (int k = 0; k < 2; k++) {
@@ -201,11 +201,11 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     }
     if ((e = hipEventRecord(db->pk_ev[1], cs)) != hipSuccess) return hipfail(e, "columns event");
     if (resolver.set) {
-        res_id_kind = res_bc[0] >= 0 ? P.pk_ck[slot_of[res_bc[0]]].as<uint8_t>() : nullptr;
-        res_id_val = res_bc[0] >= 0 ? P.pk_cv[slot_of[res_bc[0]]].as<uint64_t>() : nullptr;
-        res_pr_kind = res_bc[1] >= 0 ? P.pk_ck[slot_of[res_bc[1]]].as<uint8_t>() : nullptr;
-        res_pr_val = res_bc[1] >= 0 ? P.pk_cv[slot_of[res_bc[1]]].as<uint64_t>() : nullptr;
-        res_raw = true;
+        db->res_id_kind = res_bc[0] >= 0 ? P.pk_ck[slot_of[res_bc[0]]].as<uint8_t>() : nullptr;
+        db->res_id_val = res_bc[0] >= 0 ? P.pk_cv[slot_of[res_bc[0]]].as<uint64_t>() : nullptr;
+        db->res_pr_kind = res_bc[1] >= 0 ? P.pk_ck[slot_of[res_bc[1]]].as<uint8_t>() : nullptr;
+        db->res_pr_val = res_bc[1] >= 0 ? P.pk_cv[slot_of[res_bc[1]]].as<uint64_t>() : nullptr;
+        db->res_raw = true;
     }
     // ---- the batch's ids and offsets, checked on the host while the copies run (from pinned caller
     // memory they are DMA; pageable memory is staged by the runtime before hipMemcpyAsync returns)
@@ -517,7 +517,9 @@ int mxp_engine::finish_pack(mxp_dbatch* db) {
     if (!db->pack_pending) return MXP_OK;
     hipError_t e;
     if ((e = hipEventSynchronize(db->pk_ev[2])) != hipSuccess) return hipfail(e, "pack sync");
-    db->pack_pending = false;
+    // (pack_pending stays set until every step below has succeeded: a failed finish -- an allocation
+    // of the class tables, say -- leaves the batch unfinished, so a later evaluation of it runs the
+    // whole finish again instead of launching with half-built tables)
     // (read back on a stream of its own: the engine stream may already hold a later batch's packer,
     // waiting for that batch's copies)
     uint32_t meta[2 * MXP_PACK_VTCAND] = {};  // distinct keys, overflow
@@ -553,6 +555,11 @@ int mxp_engine::finish_pack(mxp_dbatch* db) {
     g_bin_db = db;
     g_bin_db_size = sizeof(mxp_dbatch);
     int rc = pack_vt_tables(db);
+    // (MXP_DEBUG_FLAGS 1 << 29, tests only: the next finish fails here once, after the class tables)
+    if (!rc && (debug_flags & (1u << 29)) && !finish_fail_done) {
+        finish_fail_done = true;
+        rc = fail(MXP_ERR_NOMEM, "injected finish_pack failure");
+    }
     if (!rc) rc = pack_heads(db);
     if (!rc) rc = pack_dict(db);
     g_bin_take = take0;
@@ -565,5 +572,6 @@ int mxp_engine::finish_pack(mxp_dbatch* db) {
         return hipfail(e, "pack event");
     }
     if ((e = hipEventRecord(db->pk_ev[3], stream)) != hipSuccess) return hipfail(e, "pack event");
+    db->pack_pending = false;
     return MXP_OK;
 }

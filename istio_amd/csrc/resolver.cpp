@@ -200,16 +200,20 @@ void first_errors(mxp_engine* eng, uint32_t n, uint32_t variety, const uint32_t*
 // device.  Records past the log's capacity fall back to the error bitmap.
 int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, bool ids16, uint8_t* status,
                  uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap, uint64_t* ref_off,
-                 mxp_attr_ref* refs, uint64_t ref_cap) {
+                 mxp_attr_ref* refs, uint64_t ref_cap, const mxp_resolve_place* place = nullptr,
+                 mxp_dbatch* pre = nullptr) {
+    std::unique_ptr<mxp_dbatch> db(pre);  // (a batch uploaded before: taken over, whatever happens)
     if (!eng || !batch || !status || !err_rule || !sel_off || (sel_cap && !sel_rules) || variety >= 32)
         return MXP_ERR_ARG;
+    if (pre && (ref_off || pre->n != batch->n_requests))
+        return eng->fail(MXP_ERR_ARG, "resolve: the uploaded batch is not this batch");
+    if (pre && eng->device >= 0 && hipSetDevice(eng->device) != hipSuccess) return eng->fail(MXP_ERR_DEVICE, "hipSetDevice");
     if (!eng->resolver.set) return eng->fail(MXP_ERR_STATE, "resolver not configured (mxp_resolver_set)");
     const auto& R = eng->resolver;
     const uint32_t n = batch->n_requests;
     const uint32_t NR = (uint32_t)eng->rules.size();
     const uint32_t W = (NR + 31) / 32;
     if (ids16 && NR > 65536u) return eng->fail(MXP_ERR_ARG, "u16 rule ids: more than 65536 rules");
-    std::unique_ptr<mxp_dbatch> db;
     DevBuf& dm = eng->res_dm;  // (engine-owned scratch: no allocation per call once large enough)
     DevBuf& de = eng->res_de;
     std::vector<mxp_ref_rec> recs;
@@ -218,9 +222,15 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     const bool compact = !ref_off && !(eng->debug_flags & kResolveBitmap);
     if (compact) {
         if (eng->device >= 0 && (e = eng->res_flags.reserve(n ? n : 1)) != hipSuccess) return eng->hipfail(e, "alloc flags");
-        rc = eng->evaluate(batch, dm, de, nullptr, db, eng->res_flags.as<uint8_t>());
+        if (pre) {
+            rc = eng->evaluate_uploaded(db.get(), dm, de, nullptr, eng->res_flags.as<uint8_t>());
+        } else {
+            rc = eng->evaluate(batch, dm, de, nullptr, db, eng->res_flags.as<uint8_t>());
+        }
     } else {
-        rc = ref_off ? eng->refs_evaluate(batch, dm, de, db, recs) : eng->evaluate(batch, dm, de, nullptr, db);
+        rc = ref_off ? eng->refs_evaluate(batch, dm, de, db, recs)
+             : pre     ? eng->evaluate_uploaded(db.get(), dm, de, nullptr, nullptr)
+                       : eng->evaluate(batch, dm, de, nullptr, db);
     }
     if (rc) return rc;
     // per-word masks: applicability for the variety (per request tcp flag), empty matches
@@ -242,16 +252,16 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     // request namespaces: on the device from the batch as uploaded (pack_device), else on the host
     std::vector<uint32_t> info;  // host copy (host pass; referenced attributes)
     const uint32_t* hinfo = nullptr;
-    if (eng->res_raw && !ref_off) {
+    if (db->res_raw && !ref_off) {
         if ((e = d_info.reserve((size_t)n * 4 + 4)) != hipSuccess) return eng->hipfail(e, "alloc nsinfo");
         mxp_ns_args N;
         memset(&N, 0, sizeof N);
         N.n = n;
         N.ns_mask = eng->res_ns_mask;
-        N.id_kind = eng->res_id_kind;
-        N.id_val = eng->res_id_val;
-        N.pr_kind = eng->res_pr_kind;
-        N.pr_val = eng->res_pr_val;
+        N.id_kind = db->res_id_kind;
+        N.id_val = db->res_id_val;
+        N.pr_kind = db->res_pr_kind;
+        N.pr_val = db->res_pr_val;
         N.soff = db->pk.pk_soff.as<uint64_t>();
         N.sbytes = db->pk.pk_sbytes.as<uint8_t>();
         N.ns_tab = eng->res_ns_tab.as<unsigned long long>();
@@ -373,19 +383,38 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         if (ref_rc && ref_rc != MXP_ERR_NOMEM) return ref_rc;
     }
     const uint64_t total = sel_off[n];
-    if (total > sel_cap) return MXP_ERR_NOMEM;
+    // (a group member learns where its ids go in the whole batch's list once every member knows its
+    // own count: place blocks until then, -1 = the whole list does not fit)
+    int64_t at = 0;
+    if (place) {
+        at = (*place)(total);
+        if (at < 0) return MXP_ERR_NOMEM;
+    } else if (total > sel_cap) {
+        return MXP_ERR_NOMEM;
+    }
     if (total) {
         const size_t isz = ids16 ? 2 : 4;
         if ((e = d_sel.reserve(total * isz)) != hipSuccess) return eng->hipfail(e, "alloc sel");
         A.sel_rules = d_sel.as<uint32_t>();
         if ((e = mxp_launch_resolve(&A, tiled ? 4 : 1, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
-        if ((rc = eng->download(sel_rules, d_sel.p, total * isz, "download sel"))) return rc;
+        if ((rc = eng->download((uint8_t*)sel_rules + (size_t)at * isz, d_sel.p, total * isz, "download sel"))) return rc;
     }
     eng->trace_mark("action lists (gather + download)");
     return ref_rc;
 }
 
 }  // namespace
+
+int mxp_resolve_placed(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
+                       uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules,
+                       const mxp_resolve_place& place) {
+    if (flags & ~(uint32_t)MXP_RESOLVE_IDS_U16) {
+        if (eng && db) eng->recycle(db);
+        return MXP_ERR_ARG;
+    }
+    return resolve_impl(eng, batch, variety, (flags & MXP_RESOLVE_IDS_U16) != 0, status, err_rule, sel_off, sel_rules,
+                        0, nullptr, nullptr, 0, &place, db);
+}
 
 extern "C" {
 
@@ -399,6 +428,17 @@ int mxp_resolve_batch_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t v
     if (flags & ~(uint32_t)MXP_RESOLVE_IDS_U16) return MXP_ERR_ARG;
     return resolve_impl(eng, batch, variety, (flags & MXP_RESOLVE_IDS_U16) != 0, status, err_rule, sel_off, sel_rules,
                         sel_cap, nullptr, nullptr, 0);
+}
+
+int mxp_resolve_uploaded(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
+                         uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap) {
+    if (!db) return MXP_ERR_ARG;
+    if (!eng || (flags & ~(uint32_t)MXP_RESOLVE_IDS_U16)) {
+        if (eng) eng->recycle(db);
+        return MXP_ERR_ARG;
+    }
+    return resolve_impl(eng, batch, variety, (flags & MXP_RESOLVE_IDS_U16) != 0, status, err_rule, sel_off, sel_rules,
+                        sel_cap, nullptr, nullptr, 0, nullptr, db);
 }
 
 int mxp_resolve_refs(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,

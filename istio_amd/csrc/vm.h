@@ -77,7 +77,7 @@ typedef struct mxp_guard {
 // the group's guarded rules split into column segments (the rules whose guard reads the same
 // column with the same want class), so each segment loads its column once per request and compares
 // its rules' constants (kargs.gk[32 g + k]) against it.
-typedef struct mxp_group {
+typedef struct mxp_rgroup {
     uint32_t all;      // rules present in the group
     uint32_t guarded;  // mode != GM_NONE
     uint32_t only;     // GM_ONLY
@@ -93,7 +93,7 @@ typedef struct mxp_group {
     uint32_t id;       // group index g (rules 32 g .. 32 g + 31)
     uint32_t vm;       // 1: some rule can leave phase 1 with continuing lanes (mxp_eval_kernel)
     uint32_t pad[2];
-} mxp_group;           // 64 B: fetched four at a time by one wavefront-wide load
+} mxp_rgroup;           // 64 B: fetched four at a time by one wavefront-wide load
 
 typedef struct mxp_seg {
     uint32_t col;      // column read by the guards of the segment

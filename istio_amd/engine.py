@@ -106,6 +106,60 @@ SIGNATURES = {
     "mxp_host_free": (None, [_VP]),
     "mxp_go_to_upper": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_uint64, _VP, ctypes.c_uint64,
                                        ctypes.POINTER(ctypes.c_uint64)]),
+    # device groups (include/mxp_group.h)
+    "mxp_group_create": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_VP)]),
+    "mxp_group_destroy": (None, [_VP]),
+    "mxp_group_last_error": (ctypes.c_char_p, [_VP]),
+    "mxp_group_size": (ctypes.c_uint32, [_VP]),
+    "mxp_group_reduce_mode": (ctypes.c_int, [_VP]),
+    "mxp_group_engine": (_VP, [_VP, ctypes.c_uint32]),
+    "mxp_group_stream": (_VP, [_VP, ctypes.c_uint32]),
+    "mxp_group_shard_bounds": (None, [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(ctypes.c_uint64)]),
+    "mxp_group_locate": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32),
+                                        ctypes.POINTER(ctypes.c_uint32)]),
+    "mxp_group_vocab_set": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int32),
+                                           ctypes.c_uint32]),
+    "mxp_group_vocab_set_finder": (ctypes.c_int, [_VP, _VP, _VP]),
+    "mxp_group_ruleset_compile": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_char_p), ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_int32)]),
+    "mxp_group_resolver_set": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
+                                              _VP, _VP, _VP, ctypes.c_uint32]),
+    "mxp_group_upload": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_VP)]),
+    "mxp_group_upload_split": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.POINTER(_VP)]),
+    "mxp_group_batch_wait_copied": (ctypes.c_int, [_VP]),
+    "mxp_group_batch_free": (None, [_VP, _VP]),
+    "mxp_group_batch_requests": (ctypes.c_uint32, [_VP, ctypes.c_uint32]),
+    "mxp_group_eval": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32]),
+    "mxp_group_download": (ctypes.c_int, [_VP, ctypes.c_uint32, _VP, _VP, _VP]),
+    "mxp_group_quota_create": (ctypes.c_int, [_VP, ctypes.c_uint32, _VP, _VP, _VP, ctypes.POINTER(_VP)]),
+    "mxp_group_quota_destroy": (None, [_VP, _VP]),
+    "mxp_group_quota_upload": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP, _VP, ctypes.POINTER(_VP)]),
+    "mxp_group_quota_eval": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_int64]),
+    "mxp_group_quota_granted": (ctypes.c_int, [_VP, _VP, _VP]),
+    "mxp_group_quota_batch_free": (None, [_VP, _VP]),
+    "mxp_group_quota_batch_requests": (ctypes.c_uint32, [_VP, ctypes.c_uint32]),
+    "mxp_group_quota_alloc": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, _VP, _VP, _VP, ctypes.c_int64, _VP]),
+    "mxp_group_key_owners": (ctypes.c_int, [_VP, ctypes.c_uint32, ctypes.c_uint32, _VP]),
+    "mxp_group_reduce": (ctypes.c_int, [_VP]),
+    "mxp_group_counters": (ctypes.c_int, [_VP, _VP, _VP]),
+    "mxp_group_counters_reset": (ctypes.c_int, [_VP]),
+    "mxp_group_sync": (ctypes.c_int, [_VP]),
+    "mxp_group_resolve_batch": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP,
+                                               _VP, _VP, ctypes.c_uint64]),
+    "mxp_group_resolve_uploaded": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _VP,
+                                                  _VP, _VP, _VP, ctypes.c_uint64]),
+    "mxp_resolve_uploaded": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP, _VP, _VP,
+                                            ctypes.c_uint64]),
+    "mxp_group_resolve_split": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP, _VP, _VP,
+                                               ctypes.c_uint64]),
+    "mxp_group_pair_error": (ctypes.c_int, [_VP, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32]),
+    "mxp_group_list_create": (ctypes.c_int, [_VP, ctypes.c_int, _VP, _VP, ctypes.c_uint32, _VP, _VP, ctypes.c_uint32,
+                                             ctypes.POINTER(_VP)]),
+    "mxp_group_list_destroy": (None, [_VP, _VP]),
+    "mxp_group_list_member": (_VP, [_VP, ctypes.c_uint32]),
+    "mxp_group_list_check": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, _VP, ctypes.c_uint32, _VP]),
+    "mxp_group_list_check_device": (ctypes.c_int, [_VP, _VP, ctypes.c_int, _VP, _VP, _VP, _VP]),
 }
 
 _LIB = None
@@ -233,10 +287,18 @@ class Engine:
         self.rules: List[str] = []
         self.status = np.zeros(0, dtype=np.int32)
 
+    @classmethod
+    def member(cls, handle, device: int, rules=()) -> "Engine":
+        """A non-owning view of a group member's engine (mxp_group_engine): freed with its group."""
+        e = cls.__new__(cls)
+        e.lib, e.h, e.device, e._owner = load_library(), _VP(handle), device, False
+        e.rules, e.status = list(rules), np.zeros(0, dtype=np.int32)
+        return e
+
     def close(self):
-        if self.h:
+        if self.h and getattr(self, "_owner", True):
             self.lib.mxp_engine_destroy(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -514,6 +576,18 @@ class Engine:
                 continue
             self._check(rc, "mxp_resolve_batch")
             break
+        return status, err_rule, off, sel[:int(off[n])]
+
+    def resolve_uploaded(self, db: "DeviceBatch", variety: int, cap: int, ids16: bool = False):
+        """mxp_resolve_uploaded: Resolve a batch uploaded before (db is taken over) -> as resolve_arrays."""
+        batch, cs = db._src
+        n = batch.n
+        status, err_rule = np.empty(n, dtype=np.uint8), np.empty(n, dtype=np.uint32)
+        off, sel = np.empty(n + 1, dtype=np.uint64), np.empty(max(cap, 1), dtype=np.uint16 if ids16 else np.uint32)
+        h, db.h = db.h, None
+        self._check(self.lib.mxp_resolve_uploaded(self.h, h, ctypes.byref(cs), variety, 1 if ids16 else 0,
+                                                  status.ctypes.data, err_rule.ctypes.data, off.ctypes.data,
+                                                  sel.ctypes.data, cap), "mxp_resolve_uploaded")
         return status, err_rule, off, sel[:int(off[n])]
 
     def resolve(self, batch: BagBatch, variety: int, ids16: bool = False):
@@ -807,7 +881,7 @@ class ListHandle:
 
     def __del__(self):
         try:
-            if self.h:
+            if self.h and not getattr(self, "_view", False):
                 self.eng.lib.mxp_list_destroy(self.eng.h, self.h)
                 self.h = None
         except Exception:
@@ -849,6 +923,370 @@ class QuotaHandle:
         try:
             if self.h:
                 self.eng.lib.mxp_quota_destroy(self.eng.h, self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+REDUCE_NONE, REDUCE_RCCL, REDUCE_HOST = 0, 1, 2
+GROUP_HOST_REDUCE, GROUP_RCCL_SINGLE = 1, 2
+
+
+def shard_bounds(n_total: int, member: int, n_members: int):
+    """mxp_group_shard_bounds: member's contiguous [lo, hi) of n_total requests."""
+    lib = load_library()
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    lib.mxp_group_shard_bounds(n_total, member, n_members, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
+
+
+def key_owners(weights, n_members: int) -> np.ndarray:
+    """mxp_group_key_owners: each memquota key's owner member, longest-processing-time first."""
+    lib = load_library()
+    w = np.ascontiguousarray(weights, dtype=np.float64)
+    out = np.zeros(len(w), dtype=np.uint32)
+    rc = lib.mxp_group_key_owners(w.ctypes.data, len(w), n_members, out.ctypes.data)
+    if rc != 0:
+        raise MxpError("mxp_group_key_owners failed (%d)" % rc)
+    return out
+
+
+class Group:
+    """A device group (include/mxp_group.h): one engine per device, request shards evaluated on all
+    members at once, the step's counters (hits[R] ++ quota_delta[K]) summed by one all-reduce
+    (RCCL, or the host when RCCL is unavailable or a device repeats)."""
+
+    def __init__(self, devices: Sequence[int], flags: int = 0):
+        self.lib = load_library()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        h = _VP()
+        rc = self.lib.mxp_group_create(devs, len(devices), flags, ctypes.byref(h))
+        if rc != 0:
+            raise MxpError("mxp_group_create(%s) failed (%d): %s" % (list(devices), rc,
+                                                                   self.lib.mxp_group_last_error(None).decode()))
+        self.h, self.devices = h, list(devices)
+        self.n = len(devices)
+        self.rules: List[str] = []
+        self.note = self.lib.mxp_group_last_error(h).decode()  # (why the reduction is on the host, if it is)
+
+    def close(self):
+        if self.h:
+            self.lib.mxp_group_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise MxpError("%s failed (%d): %s" % (what, rc, self.lib.mxp_group_last_error(self.h).decode(errors="replace")))
+
+    @property
+    def reduce_mode(self) -> int:
+        return int(self.lib.mxp_group_reduce_mode(self.h))
+
+    def engine(self, k: int) -> Engine:
+        """Member k's engine (a view: per-pair error texts, rule texts, values, timing)."""
+        return Engine.member(self.lib.mxp_group_engine(self.h, k), self.devices[k], self.rules)
+
+    def stream(self, k: int) -> int:
+        return int(self.lib.mxp_group_stream(self.h, k) or 0)
+
+    def locate(self, request: int):
+        k, q = ctypes.c_uint32(), ctypes.c_uint32()
+        self._check(self.lib.mxp_group_locate(self.h, request, ctypes.byref(k), ctypes.byref(q)), "mxp_group_locate")
+        return k.value, q.value
+
+    # ------------------------------------------------------------------ configuration
+    def set_vocabulary(self, manifest: Dict[str, object]):
+        names = list(manifest)
+        types = [VALUE_TYPES[v] if isinstance(v, str) else int(v) for v in manifest.values()]
+        arr = (ctypes.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+        tarr = (ctypes.c_int32 * max(len(types), 1))(*types)
+        self._check(self.lib.mxp_group_vocab_set(self.h, arr, tarr, len(names)), "mxp_group_vocab_set")
+
+    def set_vocabulary_finder(self, get_attribute):
+        def find(_ctx, name):
+            v = get_attribute(name.decode())
+            return -1 if v is None else (VALUE_TYPES[v] if isinstance(v, str) else int(v))
+        self._finder = _FINDER(find)
+        self._check(self.lib.mxp_group_vocab_set_finder(self.h, ctypes.cast(self._finder, _VP), None),
+                    "mxp_group_vocab_set_finder")
+
+    def compile(self, rules: Sequence[str]) -> np.ndarray:
+        self.rules = list(rules)
+        enc = [r.encode("utf-8", "surrogateescape") for r in self.rules]
+        arr = (ctypes.c_char_p * max(len(enc), 1))(*enc)
+        st = np.zeros(len(enc), dtype=np.int32)
+        self._check(self.lib.mxp_group_ruleset_compile(self.h, arr, len(enc), st.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))),
+                    "mxp_group_ruleset_compile")
+        return st
+
+    def set_resolver(self, identity_attr: str, default_ns: str, rule_ns, variety_mask, is_tcp, empty_match):
+        n = len(rule_ns)
+        ns = (ctypes.c_char_p * max(n, 1))(*[x.encode() for x in rule_ns])
+        vm = np.ascontiguousarray(variety_mask, dtype=np.uint32)
+        tcp = np.ascontiguousarray(is_tcp, dtype=np.uint8)
+        em = np.ascontiguousarray(empty_match, dtype=np.uint8)
+        self._check(self.lib.mxp_group_resolver_set(self.h, identity_attr.encode(), default_ns.encode(), ns,
+                                                    vm.ctypes.data, tcp.ctypes.data, em.ctypes.data, n),
+                    "mxp_group_resolver_set")
+
+    # ------------------------------------------------------------------ device-resident shards
+    def _shards(self, shards):
+        cs = [b.c_struct() for b in shards]
+        arr = (_VP * len(cs))(*[ctypes.addressof(c) for c in cs])
+        return cs, arr
+
+    def upload(self, shards: Sequence[BagBatch], no_wait: bool = False) -> "GroupBatch":
+        """mxp_group_upload: shards[k] -> member k."""
+        cs, arr = self._shards(shards)
+        h = _VP()
+        self._check(self.lib.mxp_group_upload(self.h, arr, len(cs), 1 if no_wait else 0, ctypes.byref(h)),
+                    "mxp_group_upload")
+        gb = GroupBatch(self, h, [b.n for b in shards])
+        gb._src = (list(shards), cs)
+        return gb
+
+    def upload_split(self, batch: BagBatch) -> "GroupBatch":
+        cs = batch.c_struct()
+        h = _VP()
+        self._check(self.lib.mxp_group_upload_split(self.h, ctypes.byref(cs), 0, ctypes.byref(h)), "mxp_group_upload_split")
+        return GroupBatch(self, h, [self.lib.mxp_group_batch_requests(h, k) for k in range(self.n)])
+
+    def eval(self, gb: "GroupBatch", err_bitmap: bool = False):
+        self._check(self.lib.mxp_group_eval(self.h, gb.h, 1 if err_bitmap else 0), "mxp_group_eval")
+
+    def download(self, k: int, n: int, err_bitmap: bool = False):
+        """Member k's last results: (match [W, n] u32, err [W, n] u32 or req_err [n] u8)."""
+        W = (len(self.rules) + 31) // 32
+        match = np.zeros((W, n), dtype=np.uint32)
+        if err_bitmap:
+            err = np.zeros((W, n), dtype=np.uint32)
+            self._check(self.lib.mxp_group_download(self.h, k, match.ctypes.data, err.ctypes.data, None), "mxp_group_download")
+        else:
+            err = np.zeros(n, dtype=np.uint8)
+            self._check(self.lib.mxp_group_download(self.h, k, match.ctypes.data, None, err.ctypes.data), "mxp_group_download")
+        return match, err
+
+    # ------------------------------------------------------------------ counters
+    def reduce(self):
+        self._check(self.lib.mxp_group_reduce(self.h), "mxp_group_reduce")
+
+    def counters(self, n_keys: int = 0):
+        hits = np.zeros(len(self.rules), dtype=np.uint64)
+        delta = np.zeros(n_keys, dtype=np.int64)
+        self._check(self.lib.mxp_group_counters(self.h, hits.ctypes.data, delta.ctypes.data if n_keys else None),
+                    "mxp_group_counters")
+        return hits, delta
+
+    def counters_reset(self):
+        self._check(self.lib.mxp_group_counters_reset(self.h), "mxp_group_counters_reset")
+
+    def sync(self):
+        self._check(self.lib.mxp_group_sync(self.h), "mxp_group_sync")
+
+    # ------------------------------------------------------------------ memquota
+    def quota_create(self, max_amount, valid_duration_ns, owner=None) -> "GroupQuota":
+        mx = np.ascontiguousarray(max_amount, dtype=np.int64)
+        vd = np.ascontiguousarray(valid_duration_ns, dtype=np.int64)
+        own = None if owner is None else np.ascontiguousarray(owner, dtype=np.uint32)
+        h = _VP()
+        self._check(self.lib.mxp_group_quota_create(self.h, len(mx), mx.ctypes.data, vd.ctypes.data,
+                                                    own.ctypes.data if own is not None else None, ctypes.byref(h)),
+                    "mxp_group_quota_create")
+        return GroupQuota(self, h, len(mx))
+
+    # ------------------------------------------------------------------ Resolve
+    def resolve_arrays(self, shards: Sequence[BagBatch], variety: int, cap: int = 0, ids16: bool = False, out=None,
+                       uploaded: "GroupBatch" = None):
+        """mxp_group_resolve_batch over shards (member k's requests = shards[k]) -> (status, err_rule,
+        sel_off, sel_rules) of the concatenated batch.  out: preallocated (status, err_rule, sel_off,
+        sel) arrays (e.g. pinned), reused when large enough.  uploaded: the shards' GroupBatch from an
+        earlier upload (mxp_group_resolve_uploaded; taken over -- no retry when cap is short)."""
+        n = sum(b.n for b in shards)
+        if uploaded is None:
+            cs, arr = self._shards(shards)
+        else:  # (the very structs the shards were uploaded from)
+            cs = uploaded._src[1]
+            arr = (_VP * len(cs))(*[ctypes.addressof(c) for c in cs])
+        cap = cap or max(16, n * 4)
+        for _ in range(2):
+            if out is not None and len(out[3]) >= cap:
+                status, err_rule, off, sel = out
+            else:
+                status, err_rule, off = (np.empty(n, dtype=np.uint8), np.empty(n, dtype=np.uint32),
+                                         np.empty(n + 1, dtype=np.uint64))
+                sel = np.empty(cap, dtype=np.uint16 if ids16 else np.uint32)
+            if uploaded is not None:
+                h, uploaded.h = uploaded.h, None
+                rc = self.lib.mxp_group_resolve_uploaded(self.h, h, arr, len(cs), variety, 1 if ids16 else 0,
+                                                         status.ctypes.data, err_rule.ctypes.data, off.ctypes.data,
+                                                         sel.ctypes.data, len(sel))
+                self._check(rc, "mxp_group_resolve_uploaded")
+                break
+            rc = self.lib.mxp_group_resolve_batch(self.h, arr, len(cs), variety, 1 if ids16 else 0, status.ctypes.data,
+                                                  err_rule.ctypes.data, off.ctypes.data, sel.ctypes.data, len(sel))
+            if rc == 4:
+                cap = int(off[n])
+                out = None
+                continue
+            self._check(rc, "mxp_group_resolve_batch")
+            break
+        return status[:n], err_rule[:n], off[:n + 1], sel[:int(off[n])]
+
+    def resolve(self, shards: Sequence[BagBatch], variety: int, ids16: bool = False):
+        status, err_rule, off, sel = self.resolve_arrays(shards, variety, ids16=ids16)
+        return status, err_rule, [sel[int(off[q]):int(off[q + 1])] for q in range(len(status))]
+
+    def pair_error(self, request: int, rule: int) -> str:
+        buf = ctypes.create_string_buffer(1 << 12)
+        rc = self.lib.mxp_group_pair_error(self.h, request, rule, buf, 1 << 12)
+        if rc not in (0, 1):
+            self._check(rc, "mxp_group_pair_error")
+        return buf.value.decode("utf-8", "surrogateescape")
+
+    # ------------------------------------------------------------------ lists
+    def list_create(self, entry_type: int, entries, overrides=()) -> "GroupList":
+        def arr(xs):
+            bs = [x.encode("utf-8", "surrogateescape") if isinstance(x, str) else bytes(x) for x in xs]
+            bufs = [ctypes.create_string_buffer(b, len(b) + 1) for b in bs]
+            ptrs = (ctypes.c_char_p * max(len(bs), 1))(*[ctypes.cast(b, ctypes.c_char_p) for b in bufs])
+            lens = np.array([len(b) for b in bs] or [0], dtype=np.uint32)
+            return bufs, ptrs, lens, len(bs)
+        eb, ep, el, en = arr(entries)
+        ob, op, ol, on = arr(overrides)
+        h = _VP()
+        self._check(self.lib.mxp_group_list_create(self.h, entry_type, ep, el.ctypes.data, en, op, ol.ctypes.data, on,
+                                                   ctypes.byref(h)), "mxp_group_list_create")
+        return GroupList(self, h)
+
+
+class GroupBatch:
+    def __init__(self, group: Group, h, counts):
+        self.group, self.h, self.counts = group, h, list(counts)
+
+    @property
+    def n(self) -> int:
+        return sum(self.counts)
+
+    def wait_copied(self):
+        self.group._check(self.group.lib.mxp_group_batch_wait_copied(self.h), "mxp_group_batch_wait_copied")
+
+    def free(self):
+        if self.h:
+            self.group.lib.mxp_group_batch_free(self.group.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class GroupQuota:
+    """memquota keys replicated on every member, each key's requests replayed by its owner."""
+
+    def __init__(self, group: Group, h, n_keys: int):
+        self.group, self.h, self.n_keys = group, h, n_keys
+
+    def upload(self, keys, amounts, best_effort) -> "GroupQuotaBatch":
+        k = np.ascontiguousarray(keys, dtype=np.uint32)
+        a = np.ascontiguousarray(amounts, dtype=np.int64)
+        b = np.ascontiguousarray(best_effort, dtype=np.uint8)
+        h = _VP()
+        g = self.group
+        g._check(g.lib.mxp_group_quota_upload(g.h, self.h, len(k), k.ctypes.data, a.ctypes.data, b.ctypes.data,
+                                              ctypes.byref(h)), "mxp_group_quota_upload")
+        return GroupQuotaBatch(self, h, len(k))
+
+    def eval(self, qb: "GroupQuotaBatch", now_ns: int):
+        g = self.group
+        g._check(g.lib.mxp_group_quota_eval(g.h, self.h, qb.h, int(now_ns)), "mxp_group_quota_eval")
+
+    def alloc(self, keys, amounts, best_effort, now_ns: int) -> np.ndarray:
+        k = np.ascontiguousarray(keys, dtype=np.uint32)
+        a = np.ascontiguousarray(amounts, dtype=np.int64)
+        b = np.ascontiguousarray(best_effort, dtype=np.uint8)
+        out = np.zeros(len(k), dtype=np.int64)
+        g = self.group
+        g._check(g.lib.mxp_group_quota_alloc(g.h, self.h, len(k), k.ctypes.data, a.ctypes.data, b.ctypes.data,
+                                             int(now_ns), out.ctypes.data), "mxp_group_quota_alloc")
+        return out
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.group.lib.mxp_group_quota_destroy(self.group.h, self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class GroupQuotaBatch:
+    def __init__(self, quota: GroupQuota, h, n: int):
+        self.quota, self.h, self.n = quota, h, n
+
+    def requests(self, k: int) -> int:
+        return int(self.quota.group.lib.mxp_group_quota_batch_requests(self.h, k))
+
+    def granted(self) -> np.ndarray:
+        out = np.zeros(self.n, dtype=np.int64)
+        g = self.quota.group
+        g._check(g.lib.mxp_group_quota_granted(g.h, self.h, out.ctypes.data), "mxp_group_quota_granted")
+        return out
+
+    def free(self):
+        if self.h:
+            self.quota.group.lib.mxp_group_quota_batch_free(self.quota.group.h, self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class GroupList:
+    def __init__(self, group: Group, h):
+        self.group, self.h = group, h
+
+    def member(self, k: int) -> ListHandle:
+        """Member k's list (non-owning view), for check_device on that member's engine."""
+        lh = ListHandle.__new__(ListHandle)
+        lh.eng, lh.h, lh._view = self.group.engine(k), _VP(self.group.lib.mxp_group_list_member(self.h, k)), True
+        return lh
+
+    def check(self, symbols, blacklist: bool = False) -> np.ndarray:
+        bs = [x.encode("utf-8", "surrogateescape") if isinstance(x, str) else bytes(x) for x in symbols]
+        off = np.zeros(len(bs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(b) for b in bs]) if bs else []
+        blob = np.frombuffer(b"".join(bs) + b"\0", dtype=np.uint8)
+        codes = np.zeros(len(bs), dtype=np.int32)
+        g = self.group
+        g._check(g.lib.mxp_group_list_check(g.h, self.h, int(blacklist), blob.ctypes.data, off.ctypes.data, len(bs),
+                                            codes.ctypes.data), "mxp_group_list_check")
+        return codes
+
+    def check_device(self, d_syms, d_offs, ns, d_codes, blacklist: bool = False):
+        """mxp_group_list_check_device: per member k, n[k] device-resident symbols (raw pointers) ->
+        device codes, enqueued on the members' streams."""
+        G = self.group.n
+        arr = lambda xs: (_VP * G)(*[_VP(int(x)) for x in xs])
+        n = (ctypes.c_uint32 * G)(*[int(x) for x in ns])
+        g = self.group
+        g._check(g.lib.mxp_group_list_check_device(g.h, self.h, int(blacklist), arr(d_syms), arr(d_offs), n,
+                                                   arr(d_codes)), "mxp_group_list_check_device")
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.group.lib.mxp_group_list_destroy(self.group.h, self.h)
                 self.h = None
         except Exception:
             pass

@@ -694,3 +694,18 @@ def ci_unicode_list(n_entries=3000, n_lookups=20000, seed=41):
     def word(lo, hi):
         return "".join(CI_PIECES[i] for i in rng.integers(0, len(CI_PIECES), int(rng.integers(lo, hi))))
     return [word(1, 5) for _ in range(n_entries)], [word(0, 5) for _ in range(n_lookups)]
+
+
+def split_batch(batch, n_members):
+    """The contiguous shards of one batch (dist.shard_bounds / mxp_group_shard_bounds): member k's
+    requests as a BagBatch whose columns are views into the batch's and whose string / time / map
+    tables are the batch's own."""
+    from istio_amd.bags import BagBatch
+    from istio_amd.dist import shard_bounds
+    out = []
+    for k in range(n_members):
+        lo, hi = shard_bounds(batch.n, k, n_members)
+        out.append(BagBatch(hi - lo, batch.names, [c[lo:hi] for c in batch.kinds], [v[lo:hi] for v in batch.values],
+                            batch.str_blob, batch.str_offsets, batch.time_sec, batch.time_nsec, batch.map_offsets,
+                            batch.map_keys, batch.map_values))
+    return out

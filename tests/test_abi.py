@@ -108,6 +108,16 @@ def test_go_binding_calls_declared_symbols():
                   "var _ listentry.BagHandler = (*gpuHandler)(nil)",
                   "var _ expr.TypeChecker = (*TypeChecker)(nil)", "var _ compiled.Expression = Expression{}"):
         assert iface in go, iface
+    # the reference's per-Resolve observations (resolver.go:123-138, monitor.go:51-89) in the drop-in
+    for obs in ("resolveCounter.With(lbls).Inc()", "resolveDuration.With(lbls).Observe(",
+                "resolveRules.With(lbls).Observe(float64(nselected))", "resolveActions.With(lbls).Observe(float64(raLen))",
+                "prometheus.Labels{targetStr: target, errorStr: strconv.FormatBool(err != nil)}"):
+        assert obs in go, obs
+    # the device group: one process over every GPU, its all-reduce and owner-routed memquota bound
+    for name in ("mxp_group_create", "mxp_group_ruleset_compile", "mxp_group_resolver_set", "mxp_group_resolve_batch",
+                 "mxp_group_reduce", "mxp_group_counters", "mxp_group_key_owners", "mxp_group_quota_create",
+                 "mxp_group_quota_alloc", "mxp_group_pair_error", "mxp_group_vocab_set_finder"):
+        assert name in calls, name
     # the list adapter's device calls (mxp_list*) are all bound, each with the header's arity
     hdr_decl = {m.group(1): m.group(2) for m in re.finditer(r"\b(mxp_list[a-z_]*)\(([^;]*?)\);", hdr, re.S)}
     for name in ("mxp_list_create", "mxp_list_check", "mxp_listentry_check", "mxp_list_entries", "mxp_list_destroy"):

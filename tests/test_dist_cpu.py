@@ -1,6 +1,8 @@
-"""The N>1 path on CPU: two gloo ranks shard the requests (istio_amd.dist.shard_bounds) and sum
-their per-rule hit counters (istio_amd.dist.reduce_counters) -- the same calls bench.py makes over
-RCCL.  Per-shard counters come from the oracle here (the GPU computes them with mxp_hits_device in
+"""The sharding semantics of the N>1 path on CPU, as separate processes: two gloo ranks shard the
+requests (istio_amd.dist.shard_bounds, = mxp_group_shard_bounds) and sum their per-rule hit counters
+(istio_amd.dist.reduce_counters); memquota keys owned by one rank each (dist.key_owners, =
+mxp_group_key_owners) replay exactly the single-process sequence.  The product's device group
+(include/mxp_group.h) does the same inside one process, with one RCCL all-reduce per step.  Per-shard counters come from the oracle here (the GPU computes them with mxp_hits_device in
 the -m gpu tests); the reduced counters must equal the whole batch's."""
 import os
 import socket
@@ -142,82 +144,6 @@ def test_two_rank_gloo_hit_counters(tmp_path):
     want = (oracle.oracle_matrix(oracle.OracleEvaluator(manifest), rules, batch, threads=4) == 1).sum(axis=0)
     assert got[-1] == 2  # max over ranks of (rank + 1)
     assert np.array_equal(got[:-1], want) and want.sum() > 0
-
-
-def _bench_step_rank_main(rank, world, port, out_path, steps, warmup):
-    """bench.py's own step (bench.make_step, bench.shard_workload, bench.timed_loop) on gloo, with the
-    engine replaced by counter-writing stubs: the oracle's true pairs of the rank's shard into the
-    hits view, the memquota restatement's grants of the rank's keys into the quota view."""
-    sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
-    import torch
-    import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    import bench
-    import memquota as M
-    import oracle
-    from istio_amd import dist as D
-    from istio_amd import workloads as W
-    R, per_gpu, K = 120, 900, 16
-    manifest, rules, batch = bench.shard_workload("c2", R, per_gpu, rank, world)
-    codes = oracle.oracle_matrix(oracle.OracleEvaluator(manifest), rules, batch, threads=2)
-    shard_hits = torch.from_numpy((codes == 1).sum(axis=0).astype(np.int64))
-    mx, vd, keys, amounts, be = W.quota_workload(n_keys=K, n_requests=300, seed=9, rank=rank, world=world)
-    mq = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
-    now = [10**18]
-    calls = []
-    orig = D.reduce_counters
-
-    def counting_reduce(t):
-        calls.append(t.numel())
-        return orig(t)
-    D.reduce_counters = counting_reduce
-
-    def evaluate(hits):
-        hits += shard_hits
-
-    def quota_alloc(delta, _stream=None):
-        for k, a, b in zip(keys, amounts, be):
-            delta[int(k)] += mq.handle(int(k), int(a), bool(b), now[0])
-        now[0] += 10**8
-    ctr = D.StepCounters([R, K])
-    step = bench.make_step(ctr, evaluate, quota_alloc)
-    elapsed, ev_ms = bench.timed_loop(step, steps, warmup, world, None)
-    h, d = ctr.totals()
-    if rank == 0:
-        np.save(out_path, np.concatenate([h.numpy(), d.numpy(), [len(calls), batch.n]]))
-    dist.barrier()
-    dist.destroy_process_group()
-
-
-def test_two_rank_gloo_bench_step(tmp_path):
-    """bench.py's step function at world_size 2: the two ranks' shards partition ONE seeded batch
-    (their reduced hit counters equal the whole batch's, every step), one all-reduce per step, and
-    the memquota deltas of owner-routed keys equal the single-process replay."""
-    import torch.multiprocessing as mp
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import memquota as M
-    import oracle
-    from istio_amd import workloads as W
-    out = str(tmp_path / "bench_step.npy")
-    steps, warmup, world, R, K = 3, 1, 2, 120, 16
-    mp.start_processes(_bench_step_rank_main, args=(world, _free_port(), out, steps, warmup), nprocs=world,
-                       join=True, start_method="spawn")
-    got = np.load(out)
-    manifest, _, batch = W.c2_workload(n_rules=R, n_requests=900 * world, seed=2)
-    rules = W.c2_rules(R, seed=2)[0]
-    want = (oracle.oracle_matrix(oracle.OracleEvaluator(manifest), rules, batch, threads=4) == 1).sum(axis=0)
-    assert want.sum() > 0
-    assert np.array_equal(got[:R], (steps + warmup) * want)
-    assert got[R + K] == steps + warmup  # one collective per step
-    assert got[R + K + 1] == 900  # rank 0's shard
-    mx, vd, keys, amounts, be = W.quota_workload(n_keys=K, n_requests=300 * world, seed=9)
-    mq = M.Memquota({k: (int(mx[k]), int(vd[k])) for k in range(K)})
-    want_delta = np.zeros(K, dtype=np.int64)
-    for s in range(steps + warmup):
-        for k, a, b in zip(keys, amounts, be):
-            want_delta[int(k)] += mq.handle(int(k), int(a), bool(b), 10**18 + s * 10**8)
-    assert np.array_equal(got[R:R + K], want_delta)
 
 
 def _quota_rank_main(rank, world, port, out_path, n_keys, per_rank):

@@ -80,3 +80,32 @@ def test_free_before_evaluation(mxp):
     db.free()
     arena.free()
     eng.close()
+
+
+@pytest.mark.parametrize("kind", ["c2", "c4"])
+def test_failed_finish_pack_retried(mxp, monkeypatch, kind):
+    """A device-packed batch whose packing finish fails at its first evaluation (injected after the
+    value-class tables, MXP_DEBUG_FLAGS 1 << 29) stays unfinished: the evaluation reports the error,
+    and the next evaluation of the same batch runs the whole finish again and gives the bitmaps of a
+    batch that never failed (the batch used to be marked packed with half-built tables)."""
+    if kind == "c4":
+        manifest, rules, batch = W.c4_workload(n_rules=1500, n_requests=60_000, seed=33)
+    else:
+        manifest, rules, batch = W.c2_workload(n_rules=1500, n_requests=60_000, seed=33)
+    ref = mxp.Engine(0)
+    ref.set_vocabulary(manifest)
+    ref.compile(rules)
+    want_m, want_e = ref.eval_batch(batch)
+    monkeypatch.setenv("MXP_DEBUG_FLAGS", str(1 << 29))
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    db = eng.upload(batch)
+    s = torch.cuda.Stream()
+    with pytest.raises(mxp.MxpError, match="injected finish_pack failure"):
+        _bitmaps(db, batch.n, len(rules), s)
+    dm, de = _bitmaps(db, batch.n, len(rules), s)
+    torch.cuda.synchronize()
+    assert np.array_equal(dm.cpu().numpy().view(np.uint32), want_m)
+    assert np.array_equal(de.cpu().numpy().view(np.uint32), want_e)
+    db.free()

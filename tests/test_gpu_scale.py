@@ -215,47 +215,54 @@ def _null_stream_reps(db, R, N, Wd):
         assert int(hits.sum()) > 100 * N and int(req_err.max()) == 0
 
 
-def test_c5_step_quota_beside_evaluation(mxp):
-    """bench.py's C5 step with the memquota batch on a second stream beside the evaluation (the
-    default) gives the same hit counters and per-key quota deltas, step after step, as the serial
-    step -- the two touch disjoint buffers; the fork and join events order them around the counter
-    buffer's zeroing and the all-reduce."""
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_c5_group_step(mxp, devices):
+    """bench.py's C5 step on a device group (bench.group_step): every member's evaluation with fused
+    hit counters, the memquota batch routed to its key owners on each member's second stream, and the
+    step's one reduction -- three steps give 3 x the one-engine hit counters and exactly the per-key
+    deltas of the sequential replay of the whole arrival stream (oracle/memquota.py restatement)."""
     import torch
     import bench
-    from istio_amd import dist as D
+    import memquota as M
+    from istio_amd.engine import key_owners
     manifest, rules, batch = W.c2_workload(n_rules=2000, n_requests=1 << 16, seed=2)
-    R, N = len(rules), batch.n
-    dev = torch.device("cuda:0")
-    out = []
-    for two in (False, True):
-        eng = mxp.Engine(0)
-        eng.set_vocabulary(manifest)
-        assert (eng.compile(rules) == 0).all()
-        db = eng.upload(batch)
-        quota = bench.quota_setup(eng, N, 0, 1, dev)
-        d_match = torch.empty(((R + 31) // 32, N), dtype=torch.int32, device=dev)
-        d_req_err = torch.empty(N, dtype=torch.uint8, device=dev)
-        stream = torch.cuda.Stream(dev)
-        now = [1_500_000_000 * 10**9]
+    R, N, K = len(rules), batch.n, bench.QUOTA_KEYS
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    assert (eng.compile(rules) == 0).all()
+    db = eng.upload(batch)
+    dm = torch.zeros(((R + 31) // 32, N), dtype=torch.int32, device="cuda:0")
+    rq = torch.zeros(N, dtype=torch.uint8, device="cuda:0")
+    h1 = torch.zeros(R, dtype=torch.int64, device="cuda:0")
+    torch.cuda.synchronize()
+    db.eval_compact(dm.data_ptr(), rq.data_ptr(), h1.data_ptr(), 0)
+    torch.cuda.synchronize()
+    want_hits = h1.cpu().numpy().view(np.uint64)
+    db.free()
+    g = mxp.Group(devices)
+    g.set_vocabulary(manifest)
+    g.compile(rules)
+    gb = g.upload(W.split_batch(batch, len(devices)))
+    mx, vd, keys, amounts, be = W.quota_workload(n_keys=K, n_requests=N, seed=5)
+    q = g.quota_create(mx, vd, key_owners(W.quota_key_weights(K), len(devices)))
+    qb = q.upload(keys, amounts, be)
+    now = [BASE_NS]
+    step = bench.group_step(g, gb, (q, qb, now), g.stream(0))
+    for _ in range(3):
+        step()
+    hits, delta = g.counters(K)
+    ref = M.CMemquota(mx, vd)
+    want_delta = np.zeros(K, dtype=np.int64)
+    for s in range(3):
+        np.add.at(want_delta, keys.astype(np.int64),
+                  np.sign(amounts) * ref.handle_batch(keys, amounts, be, BASE_NS + s * 10**8, threads=16))
+    assert np.array_equal(hits, 3 * want_hits) and int(hits.sum()) > 0
+    assert np.array_equal(delta, want_delta) and (delta != 0).any()
+    qb.free()
+    gb.free()
 
-        def quota_alloc(delta, qsh):
-            (_, q, (dk, da, dbe, dg)) = quota
-            q.alloc_device(dk.numel(), dk.data_ptr(), da.data_ptr(), dbe.data_ptr(), now[0], qsh, dg.data_ptr(),
-                           delta.data_ptr())
-            now[0] += 10**8
-        ctr = D.StepCounters([R, bench.QUOTA_KEYS], dev)
-        with torch.cuda.stream(stream):
-            step = bench.make_step(ctr, lambda hits: db.eval_compact(d_match.data_ptr(), d_req_err.data_ptr(),
-                                                                     hits.data_ptr(), stream.cuda_stream),
-                                   quota_alloc, stream, torch.cuda.Stream(dev) if two else None)
-            for _ in range(3):
-                step()
-        torch.cuda.synchronize()
-        h, d = ctr.totals()
-        out.append((h.cpu(), d.cpu()))
-        db.free()
-    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
-    assert int(out[0][0].sum()) > 0 and int(out[0][1].abs().sum()) > 0
+
+BASE_NS = 1_500_000_000 * 10**9
 
 
 @pytest.mark.parametrize("wl", ["c4", "c2"])
