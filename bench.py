@@ -83,6 +83,9 @@ def parse(argv=None):
                    help="steps of the fresh-batch block (upload + evaluation of a new batch per step); 0 skips it")
     p.add_argument("--error-output", default="compact", choices=["compact", "bitmap"],
                    help="compact: per-request error flags (a Resolve's view); bitmap: the full error bitmap")
+    p.add_argument("--wire", default="narrow", choices=["narrow", "wide"],
+                   help="host batch format of the fresh-batch and end-to-end blocks: narrow (mxp_bag_batch2, "
+                        "u32 ids and offsets, mxp_batch_upload2) or wide (mxp_bag_batch)")
     p.add_argument("--gen-procs", type=int, default=min(16, host_threads()),
                    help="processes generating the synthetic shards (before any GPU work)")
     return p.parse_args(argv)
@@ -363,7 +366,22 @@ def group_step(g, gb, quota=None, s0=None):
     return step
 
 
-def fresh_batch_block(g, fresh_sets, steps, n_rules):
+def host_sets(shard_sets, wire):
+    """Pinned host copies of shard sets (a binding's reused packing arenas), wide
+    (BagBatch) or narrow (bags.NarrowBatch); (sets, bytes over the link per set, keep-alive)."""
+    from istio_amd.engine import pinned_batch, pinned_narrow
+    mk = pinned_narrow if wire == "narrow" else pinned_batch
+    made = [[mk(b) for b in shards] for shards in shard_sets]
+    sets = [[b for b, _ in m] for m in made]
+    size = (lambda b: b.wire_bytes()) if wire == "narrow" else batch_h2d_bytes
+    return sets, [sum(size(b) for b in st) for st in sets], made
+
+
+def upload_set(g, st, wire, no_wait):
+    return g.upload2(st, no_wait=no_wait) if wire == "narrow" else g.upload(st, no_wait=no_wait)
+
+
+def fresh_batch_block(g, fresh_sets, steps, n_rules, wire="narrow"):
     """Every step takes a NEW set of shards from host memory, double-buffered: mxp_group_upload of set
     k + 1 with MXP_UPLOAD_NO_WAIT (its H2D copies queued on every member and the shards checked; the
     device packers run after them), then the evaluation of set k (its first evaluation finishes its
@@ -373,17 +391,14 @@ def fresh_batch_block(g, fresh_sets, steps, n_rules):
     shards live in pinned memory (mxp_host_alloc), as a binding's reused packing arenas do
     (INTEGRATION.md 2e): their copies are DMA at the link's rate."""
     import numpy as np
-    from istio_amd.engine import pinned_batch
-    pinned = [[pinned_batch(b) for b in shards] for shards in fresh_sets]
-    sets = [[b for b, _ in p] for p in pinned]
+    sets, h2d, _keep = host_sets(fresh_sets, wire)
     keep, up_s, pending, copying = [], [], [], []
-    h2d = [sum(batch_h2d_bytes(b) for b in shards) for shards in sets]
 
     def one(k):
         if len(copying) >= len(sets):  # (this step's host set was uploaded len(sets) steps ago)
             copying.pop(0).wait_copied()
         t0 = time.perf_counter()
-        gb = g.upload(sets[k % len(sets)], no_wait=True)  # (copies queued, shards checked)
+        gb = upload_set(g, sets[k % len(sets)], wire, True)  # (copies queued, shards checked)
         up_s.append(time.perf_counter() - t0)
         copying.append(gb)
         if pending:  # (the previous set, uploaded one step ago)
@@ -421,12 +436,14 @@ def fresh_batch_block(g, fresh_sets, steps, n_rules):
                                    "(intern, gather, pool, pre-tables, value-class dictionary, heads); "
                                    "achieved = batch bytes per GPU / step wall time (upload + evaluation, pipelined)"},
             "upload_call_gbs": bytes_step / up / 1e9,
-            "host_memory": "pinned (mxp_host_alloc arenas)",
-            "path": "host columnar shards (a new batch every step) -> mxp_group_upload (set k + 1) -> mxp_group_eval "
-                    "(set k: compact errors, fused hit counters); wall time per step, PCIe-inclusive"}
+            "host_memory": "pinned (mxp_host_alloc arenas)", "wire": wire,
+            "path": "host columnar shards (a new batch every step; %s) -> mxp_group_upload%s (set k + 1) -> "
+                    "mxp_group_eval (set k: compact errors, fused hit counters); wall time per step, PCIe-inclusive" % (
+                        "mxp_bag_batch2: u32 ids and offsets" if wire == "narrow" else "mxp_bag_batch",
+                        "2" if wire == "narrow" else "")}
 
 
-def end_to_end(g, shard_sets, n_rules, reps):
+def end_to_end(g, shard_sets, n_rules, reps, wire="narrow"):
     """The whole Check-path call from Go-owned bags to action lists: the host
     columnar shards -> mxp_group_resolve_batch (per member: device packing and interning, evaluation of
     every pair, per-request resolution and action-list gather on the device) -> status / first-error
@@ -439,16 +456,22 @@ def end_to_end(g, shard_sets, n_rules, reps):
     (mxp_group_resolve_uploaded), so k + 1's copies and device packing overlap k's evaluation, resolve
     kernels and downloads; the three shard sets alternate."""
     import numpy as np
-    from istio_amd.engine import PinnedArena, pinned_batch
+    from istio_amd.engine import PinnedArena
     g.set_resolver("destination.service", "istio-system", ["istio-system"] * n_rules,
                    np.ones(n_rules, dtype=np.uint32), np.zeros(n_rules, dtype=np.uint8),
                    np.zeros(n_rules, dtype=np.uint8))
-    sets = [[pinned_batch(b) for b in shards] for shards in shard_sets]  # (the binding's packing arenas)
-    sets = [[b for b, _ in p] for p in sets]
+    sets, h2d, _keep = host_sets(shard_sets, wire)  # (the binding's packing arenas)
     shards = sets[0]
     n = sum(b.n for b in shards)
     ids16 = n_rules <= 65536  # MXP_RESOLVE_IDS_U16
-    caps = [int(g.resolve_arrays(s, 0, ids16=ids16)[2][-1]) for s in sets]  # warm-up (allocations), list sizes
+    narrow = wire == "narrow"
+
+    def resolve(st, cap=0, out=None):  # one call from host bags: upload (narrow) + Resolve, or the one-shot call
+        if narrow:
+            return g.resolve_arrays(None, 0, cap or max(16, 4 * n), ids16=ids16, out=out,
+                                    uploaded=upload_set(g, st, wire, False))
+        return g.resolve_arrays(st, 0, cap, ids16=ids16, out=out)
+    caps = [int(resolve(st)[2][-1]) for st in sets]  # warm-up (allocations), list sizes
     cap = max(16, 2 * max(caps))
     arena = PinnedArena(n * 13 + 8 + cap * 2 + 4 * 64)
     out = (arena.empty(n, np.uint8), arena.empty(n, np.uint32), arena.empty(n + 1, np.uint64),
@@ -456,7 +479,7 @@ def end_to_end(g, shard_sets, n_rules, reps):
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
-        status, _, off, _ = g.resolve_arrays(shards, 0, cap, ids16=ids16, out=out)
+        status, _, off, _ = resolve(shards, cap, out)
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
     sel_bytes = int(off[-1]) * (2 if ids16 else 4)
@@ -464,13 +487,13 @@ def end_to_end(g, shard_sets, n_rules, reps):
     selected = float(off[-1]) / max(n, 1)
     # pipelined: upload k + 1 ahead of Resolve k
     steps = max(3 * reps, 6)
-    nxt = g.upload(sets[0], no_wait=True)
+    nxt = upload_set(g, sets[0], wire, True)
     t0 = time.perf_counter()
     for k in range(steps):
         cur = nxt
         if k + 1 < steps:
-            nxt = g.upload(sets[(k + 1) % len(sets)], no_wait=True)
-        g.resolve_arrays(sets[k % len(sets)], 0, cap, ids16=ids16, out=out, uploaded=cur)
+            nxt = upload_set(g, sets[(k + 1) % len(sets)], wire, True)
+        g.resolve_arrays(None if narrow else sets[k % len(sets)], 0, cap, ids16=ids16, out=out, uploaded=cur)
     t_pipe = (time.perf_counter() - t0) / steps
     G = len(shards)
     return {"pairs_per_s": n * n_rules / t, "requests_per_s": n / t, "ms_per_batch": t * 1e3,
@@ -482,10 +505,13 @@ def end_to_end(g, shard_sets, n_rules, reps):
                           "batches": steps, "x_action_list_at_50GBps": t_pipe * 1e3 / max(sel_bytes / G / 50e9 * 1e3, 1e-9),
                           "path": "mxp_group_upload(batch k + 1, MXP_UPLOAD_NO_WAIT) then mxp_group_resolve_uploaded(batch k); "
                                   "three pinned shard sets alternating; wall time per batch"},
-            "host_memory": "pinned shards and outputs (mxp_host_alloc arenas)",
-            "path": "host columnar shards -> mxp_group_resolve_batch (per member: device pack + namespaces + compact "
-                    "evaluation + first errors from the records + device scan + action-list gather) -> host action "
-                    "lists of the whole batch; median of reps, PCIe-inclusive"}
+            "host_memory": "pinned shards and outputs (mxp_host_alloc arenas)", "wire": wire,
+            "h2d_bytes_per_batch": int(h2d[0] / G),
+            "path": ("host columnar shards -> %s -> host action lists of the whole batch (per member: device pack + "
+                     "namespaces + compact evaluation + first errors from the records + device scan + action-list "
+                     "gather); median of reps, PCIe-inclusive" % (
+                         "mxp_group_upload2 (narrow: u32 ids and offsets) + mxp_group_resolve_uploaded" if narrow
+                         else "mxp_group_resolve_batch"))}
 
 
 def predicate_bench(args, kind, devices, data, with_quota=False):
@@ -619,10 +645,11 @@ def predicate_bench(args, kind, devices, data, with_quota=False):
                         "quota_delta_abs_total": int(np.abs(delta).sum()),
                         "collective": "one all-reduce of hits[R] ++ quota_delta[K] per step (mxp_group_reduce)"}
     if args.fresh_steps > 0 and not with_quota:
-        out["fresh_batch"] = fresh_batch_block(g, [data.shards(kind, 1), data.shards(kind, 2)], args.fresh_steps, R)
+        out["fresh_batch"] = fresh_batch_block(g, [data.shards(kind, 1), data.shards(kind, 2)], args.fresh_steps, R,
+                                               args.wire)
     if args.e2e_reps > 0 and not with_quota:
         sets = [shards] + ([data.shards(kind, 1), data.shards(kind, 2)] if args.fresh_steps > 0 else [])
-        out["end_to_end"] = end_to_end(g, sets, R, args.e2e_reps)
+        out["end_to_end"] = end_to_end(g, sets, R, args.e2e_reps, args.wire)
     gb.free()
     if quota is not None:
         quota[1].free()

@@ -200,7 +200,8 @@ int mxp_resolve_batch_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t v
 /* mxp_resolve_batch_ex over a batch uploaded before (mxp_batch_upload / mxp_batch_upload_ex, e.g. with
  * MXP_UPLOAD_NO_WAIT one call ahead, so that batch k + 1's copies and device packing overlap batch
  * k's Resolve -- the Go micro-batcher's double buffering).  `batch` is the host batch db was
- * uploaded from, unchanged (error texts and host passes read it).  The call takes db over, whatever
+ * uploaded from, unchanged (error texts and host passes read it; NULL for a batch uploaded narrow,
+ * mxp_batch_upload2).  The call takes db over, whatever
  * it returns: the engine keeps it as the last batch (mxp_pair_error) and recycles it with the next
  * one; the caller does not mxp_batch_free it. */
 int mxp_resolve_uploaded(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
@@ -365,6 +366,10 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
 #define MXP_UPLOAD_NO_WAIT 1u
 int mxp_batch_upload_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t flags, mxp_dbatch** out);
 int mxp_batch_wait_copied(mxp_dbatch* db);
+/* mxp_batch_upload_ex of a narrow batch (mxp_batch.h mxp_bag_batch2): the u32 arrays are copied and
+ * widened on the device; the engine keeps a widened host view of the batch with the device batch
+ * (its host passes read it), so mxp_resolve_uploaded takes batch = NULL for such a batch. */
+int mxp_batch_upload2(mxp_engine* eng, const mxp_bag_batch2* batch, uint32_t flags, mxp_dbatch** out);
 /* The host half of mxp_batch_upload alone (interning against the rule set's pools, column gather,
  * ip() / timestamp() / regexp pre-tables), for timing and tests; works on a host-only engine.
  * out[0] bytes of the packed device image, out[1] batch strings added to the overlay pool, out[2]

@@ -67,6 +67,24 @@ typedef struct mxp_bag_batch {
 } mxp_bag_batch;
 
 /*
+ * The narrow form of a batch (round 6): what crosses the host link is about a third smaller.  A
+ * column whose kinds are all id kinds (STRING, BYTES, OTHER, TIMESTAMP, STRING_MAP) or BOOL / ABSENT
+ * -- narrow[c] = 1 -- carries u32 values in values32[c]; any other column keeps its u64 values in
+ * base.values[c].  String and map offsets are u32 (a batch's string bytes and map entries stay below
+ * 4 GiB).  base.str_offsets and base.map_offsets are unused (NULL); everything else is base's.  The
+ * engine widens on the device after the copies (mxp_batch_upload2).  A Go packer writes the ids
+ * straight into u32 columns: the dictionary-encoded ids of the wire are 32-bit already
+ * (dictState.go:75-82).
+ */
+typedef struct mxp_bag_batch2 {
+    mxp_bag_batch base;
+    const uint8_t* narrow;             /* [n_columns] 1: values32[c], 0: base.values[c]          */
+    const uint32_t* const* values32;   /* [n_columns] -> uint32_t[n_requests] (narrow columns)   */
+    const uint32_t* str_offsets32;     /* [n_strings + 1]                                        */
+    const uint32_t* map_offsets32;     /* [n_maps + 1]                                           */
+} mxp_bag_batch2;
+
+/*
  * The wire form: N `CompressedAttributes` messages (istio.io/api mixer/v1 attributes.proto, the
  * Attributes of a CheckRequest) with their dictionary indices as sent -- index >= 0 names word i of
  * the global word list, index < 0 names word -index-1 of the message's own Words

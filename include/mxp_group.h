@@ -81,6 +81,10 @@ int mxp_group_resolver_set(mxp_group* g, const char* identity_attr, const char* 
 typedef struct mxp_gbatch mxp_gbatch;
 int mxp_group_upload(mxp_group* g, const mxp_bag_batch* const* shards, uint32_t n_shards, uint32_t flags,
                      mxp_gbatch** out);
+/* ... of narrow shards (mxp_bag_batch2, mxp_batch_upload2 per member): a third fewer bytes over the
+ * hosts' links.  mxp_group_resolve_uploaded then takes shards = NULL. */
+int mxp_group_upload2(mxp_group* g, const mxp_bag_batch2* const* shards, uint32_t n_shards, uint32_t flags,
+                      mxp_gbatch** out);
 int mxp_group_upload_split(mxp_group* g, const mxp_bag_batch* batch, uint32_t flags, mxp_gbatch** out);
 int mxp_group_batch_wait_copied(mxp_gbatch* gb);
 void mxp_group_batch_free(mxp_group* g, mxp_gbatch* gb);

@@ -331,3 +331,71 @@ class BagBatch:
         s.map_values = _ptr(self.map_values, ctypes.c_uint32)
         self._c = s
         return s
+
+
+class _CBatch2(ctypes.Structure):  # mxp_bag_batch2 (include/mxp_batch.h)
+    _fields_ = [
+        ("base", _CBatch),
+        ("narrow", ctypes.POINTER(ctypes.c_uint8)),
+        ("values32", ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32))),
+        ("str_offsets32", ctypes.POINTER(ctypes.c_uint32)),
+        ("map_offsets32", ctypes.POINTER(ctypes.c_uint32)),
+    ]
+
+
+# kinds whose values fit 32 bits (ids, BOOL) -- a column of only these travels narrow
+NARROW_KINDS = (0, 1, 4, 6, 7, 8, 9)
+
+
+class NarrowBatch:
+    """The narrow form of a BagBatch (mxp_bag_batch2): u32 values for the columns whose kinds are all
+    id kinds or BOOL, u32 string and map offsets.  `alloc(count, dtype)` places its arrays (e.g. a
+    pinned arena's `empty`); the wide columns and the other tables stay the BagBatch's own."""
+
+    def __init__(self, batch: BagBatch, alloc=None):
+        alloc = alloc or (lambda count, dtype: np.empty(count, dtype=dtype))
+
+        def put(a, dtype):
+            out = alloc(a.size, dtype)
+            out[...] = a
+            return out
+        self.batch = batch
+        ok = np.array([bool(np.isin(k, NARROW_KINDS).all()) and (v.size == 0 or int(v.max()) < (1 << 32))
+                       for k, v in zip(batch.kinds, batch.values)], dtype=np.uint8)
+        self.narrow = put(ok, np.uint8) if ok.size else np.zeros(1, dtype=np.uint8)
+        self.values32 = [put(v, np.uint32) if f else None for v, f in zip(batch.values, ok)]
+        if batch.str_offsets[-1] >= (1 << 32) or batch.map_offsets[-1] >= (1 << 32):
+            raise ValueError("a narrow batch holds below 4 GiB of strings / map entries")
+        self.str_offsets32 = put(batch.str_offsets, np.uint32)
+        self.map_offsets32 = put(batch.map_offsets, np.uint32)
+        self._c = None
+
+    @property
+    def n(self) -> int:
+        return self.batch.n
+
+    def wire_bytes(self) -> int:
+        """Bytes over the link: kinds, the narrow / wide values, string bytes, u32 offsets, times, maps."""
+        b = self.batch
+        vals = sum(v.nbytes // 2 if f else v.nbytes for v, f in zip(b.values, self.narrow))
+        return int(sum(k.nbytes for k in b.kinds) + vals + b.str_blob.nbytes + self.str_offsets32.nbytes
+                   + b.time_sec.nbytes + b.time_nsec.nbytes + self.map_offsets32.nbytes + b.map_keys.nbytes
+                   + b.map_values.nbytes)
+
+    def c_struct(self) -> _CBatch2:
+        if self._c is not None:
+            return self._c
+        b = self.batch
+        s = _CBatch2()
+        s.base = b.c_struct()
+        s.base.str_offsets = None
+        s.base.map_offsets = None
+        nc = len(b.names)
+        s.narrow = _ptr(self.narrow, ctypes.c_uint8)
+        self._v32 = (ctypes.POINTER(ctypes.c_uint32) * max(nc, 1))(
+            *[_ptr(v, ctypes.c_uint32) if v is not None else ctypes.POINTER(ctypes.c_uint32)() for v in self.values32])
+        s.values32 = ctypes.cast(self._v32, ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32)))
+        s.str_offsets32 = _ptr(self.str_offsets32, ctypes.c_uint32)
+        s.map_offsets32 = _ptr(self.map_offsets32, ctypes.c_uint32)
+        self._c = s
+        return s

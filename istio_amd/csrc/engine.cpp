@@ -2422,7 +2422,9 @@ int mxp_batch_wait_copied(mxp_dbatch* db) {
     return MXP_OK;
 }
 
-int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out) {
+// mxp_batch_upload, and for a narrow batch (mxp_batch_upload2) its host view, handed to the device
+// batch (batch points into it)
+static int batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out, std::unique_ptr<WideView>* wide) {
     if (!eng || !batch || !out) return MXP_ERR_ARG;
     if (!eng->have_rules) return eng->fail(MXP_ERR_STATE, "no rule set compiled");
     if (eng->device < 0) return eng->fail(MXP_ERR_STATE, "host-only engine");
@@ -2430,6 +2432,7 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
     if (h != hipSuccess) return eng->hipfail(h, "hipSetDevice");
     auto* db = new (std::nothrow) mxp_dbatch();
     if (!db) return MXP_ERR_NOMEM;
+    if (wide) db->wide = std::move(*wide);
     // (the batch's own blocks recycled where the bin has them; engine scratch grown meanwhile is not)
     g_bin_take = &eng->bin;
     g_bin_db = db;
@@ -2443,6 +2446,65 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
     }
     *out = db;
     return MXP_OK;
+}
+
+int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** out) {
+    return batch_upload(eng, batch, out, nullptr);
+}
+
+int mxp_batch_upload2(mxp_engine* eng, const mxp_bag_batch2* b2, uint32_t flags, mxp_dbatch** out) {
+    if (!eng || !b2 || !out || (flags & ~(uint32_t)MXP_UPLOAD_NO_WAIT)) return MXP_ERR_ARG;
+    const mxp_bag_batch& B = b2->base;
+    const uint64_t n = B.n_requests;
+    auto bad = [&](const std::string& what) { return eng->fail(MXP_ERR_ARG, "malformed narrow batch: " + what); };
+    if (B.n_columns && (!b2->narrow || !B.kinds)) return bad("narrow / kinds is NULL");
+    if (B.n_strings && !b2->str_offsets32) return bad("str_offsets32 is NULL");
+    if (B.n_maps && !b2->map_offsets32) return bad("map_offsets32 is NULL");
+    for (uint32_t c = 0; c < B.n_columns; c++) {
+        const bool nar = b2->narrow[c] != 0;
+        if (n && nar && (!b2->values32 || !b2->values32[c])) return bad("values32 of a narrow column is NULL");
+        if (n && !nar && (!B.values || !B.values[c])) return bad("values of a wide column is NULL");
+    }
+    // the host view: narrow columns and offsets widened (the host passes read the v1 layout); the
+    // copies read the narrow arrays (pack_device)
+    std::unique_ptr<WideView> W(new WideView());
+    W->view = B;
+    W->vptr.assign(B.n_columns, nullptr);
+    W->vals.resize(B.n_columns);
+    auto widen = [](const uint32_t* in, uint64_t m) {
+        std::unique_ptr<uint64_t[]> o(new uint64_t[m ? m : 1]);
+        uint64_t* p = o.get();
+        mxp::par_for(m, 1u << 16, [&](uint64_t a, uint64_t z, unsigned) {
+            for (uint64_t i = a; i < z; i++) p[i] = in[i];
+        });
+        return o;
+    };
+    for (uint32_t c = 0; c < B.n_columns; c++) {
+        if (b2->narrow[c]) {
+            W->vals[c] = widen(b2->values32[c], n);
+            W->vptr[c] = W->vals[c].get();
+        } else {
+            W->vptr[c] = B.values ? B.values[c] : nullptr;
+        }
+    }
+    W->view.values = B.n_columns ? W->vptr.data() : B.values;
+    W->view.str_offsets = nullptr;
+    W->view.map_offsets = nullptr;
+    if (B.n_strings) {
+        W->soff = widen(b2->str_offsets32, (uint64_t)B.n_strings + 1);
+        W->view.str_offsets = W->soff.get();
+    }
+    if (B.n_maps) {
+        W->moff = widen(b2->map_offsets32, (uint64_t)B.n_maps + 1);
+        W->view.map_offsets = W->moff.get();
+    }
+    const mxp_bag_batch* view = &W->view;
+    eng->upload_no_wait = (flags & MXP_UPLOAD_NO_WAIT) != 0;
+    eng->narrow_src = b2;
+    const int rc = batch_upload(eng, view, out, &W);
+    eng->narrow_src = nullptr;
+    eng->upload_no_wait = false;
+    return rc;
 }
 
 int mxp_batch_pack_host(mxp_engine* eng, const mxp_bag_batch* batch, uint64_t* out, uint32_t cap) {

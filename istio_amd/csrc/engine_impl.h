@@ -278,6 +278,17 @@ struct PackScratch {
     DevBuf pk_soff, pk_sbytes, pk_tsec, pk_tnsec, pk_moff, pk_mkey, pk_mval, pk_ck[66], pk_cv[66];  // (+2: resolver columns)
     DevBuf pk_sid, pk_braw, pk_bcan, pk_tid, pk_use, pk_tab[4], pk_scan, pk_scan_blocks, pk_scan_max;
     DevBuf pk_vtd_lkey, pk_vtd_lcr, pk_vtd_ln, pk_vtd_tkey, pk_vtd_tcr, pk_vtd_meta, pk_rx, pk_rxv;
+    DevBuf pk_cv32[66], pk_soff32, pk_moff32;  // narrow batches: the u32 arrays as copied (mxp_batch_upload2)
+};
+
+// A narrow batch's host view (mxp_batch_upload2): the host passes (batch checks, run-time pattern
+// collection, error texts, the Resolve's host paths) read the v1 layout, so its u32 values and
+// offsets are widened on the host once, kept with the device batch; the copies read the narrow arrays.
+struct WideView {
+    mxp_bag_batch view;
+    std::vector<const uint64_t*> vptr;
+    std::vector<std::unique_ptr<uint64_t[]>> vals;  // (uninitialised: the widening writes every word)
+    std::unique_ptr<uint64_t[]> soff, moff;
 };
 
 struct mxp_dbatch {
@@ -325,6 +336,7 @@ struct mxp_dbatch {
             if (ev) (void)hipEventDestroy(ev);
     }
     int note_done(hipStream_t s);  // record (creating on first use) the completion event of stream s
+    std::unique_ptr<WideView> wide;  // uploaded narrow (mxp_batch_upload2): the host view of the batch
     // set by pack_device (the batch's own scratch, pk): the raw identity / context.protocol columns as
     // uploaded (nullptr: absent from the batch), for the Resolve's device namespaces; res_raw = false
     // when the host packer ran or the columns were not uploaded
@@ -880,6 +892,7 @@ struct mxp_engine : public mxp::LowerTables {
     int pack_device(const mxp_bag_batch* b, mxp_dbatch* db);
     int pack_vt_tables(mxp_dbatch* db);  // the value-class tables of the active slots
     bool host_pack = false;
+    const mxp_bag_batch2* narrow_src = nullptr;  // the narrow batch pack_device copies (mxp_batch_upload2)
     // device copies of the interning pools (strings: d_gstr / d_gstr_off) and their hash tables:
     // [0] strings [1] byte strings [2] canonical byte strings [3] timestamps
     int ensure_dev_pools();

@@ -569,6 +569,29 @@ int mxp_group_upload(mxp_group* g, const mxp_bag_batch* const* shards, uint32_t 
     return MXP_OK;
 }
 
+int mxp_group_upload2(mxp_group* g, const mxp_bag_batch2* const* shards, uint32_t n_shards, uint32_t flags,
+                      mxp_gbatch** out) {
+    if (!g || !shards || !out || n_shards != g->size()) return MXP_ERR_ARG;
+    for (uint32_t k = 0; k < n_shards; k++)
+        if (!shards[k]) return MXP_ERR_ARG;
+    DeviceGuard guard;
+    std::unique_ptr<mxp_gbatch> gb(new mxp_gbatch());
+    gb->db.assign(n_shards, nullptr);
+    gb->n.assign(n_shards, 0);
+    int rc = g->each([&](uint32_t k) {
+        gb->n[k] = shards[k]->base.n_requests;
+        return mxp_batch_upload2(g->m[k].eng, shards[k], flags, &gb->db[k]);
+    });
+    if (rc) {
+        mxp_group_batch_free(g, gb.release());
+        return rc;
+    }
+    std::vector<uint64_t> cnt(gb->n.begin(), gb->n.end());
+    g->set_bounds(cnt);
+    *out = gb.release();
+    return MXP_OK;
+}
+
 int mxp_group_upload_split(mxp_group* g, const mxp_bag_batch* batch, uint32_t flags, mxp_gbatch** out) {
     if (!g || !batch) return MXP_ERR_ARG;
     SplitView v(batch, g->size());
@@ -904,6 +927,12 @@ static int group_resolve(mxp_group* g, mxp_gbatch* gb, const mxp_bag_batch* cons
     std::unique_ptr<mxp_gbatch, std::function<void(mxp_gbatch*)>> own(gb, [g](mxp_gbatch* b) {
         mxp_group_batch_free(g, b);  // (the members' batches not handed to their Resolve)
     });
+    // (shards NULL with narrow uploads: the members' host views)
+    std::vector<const mxp_bag_batch*> views;
+    if (!shards && gb && g && gb->db.size() == g->size()) {
+        for (mxp_dbatch* db : gb->db) views.push_back(db && db->wide ? &db->wide->view : nullptr);
+        shards = views.data();
+    }
     if (!g || !shards || n_shards != g->size() || !status || !err_rule || !sel_off || (sel_cap && !sel_rules) ||
         (flags & ~(uint32_t)MXP_RESOLVE_IDS_U16) || (gb && gb->db.size() != n_shards))
         return MXP_ERR_ARG;
@@ -968,12 +997,14 @@ static int group_resolve(mxp_group* g, mxp_gbatch* gb, const mxp_bag_batch* cons
         base[k] = total;
         total += rv.total[k];
     }
-    // the batch-local offsets rebased (member 0's are already global)
+    // the batch-local offsets rebased (member 0's are already global); each member's first entry is
+    // its base (the engines leave it alone: it is the previous member's last entry)
     rc = g->each([&](uint32_t k) -> int {
         const uint64_t lo = g->lo[k], n = cnt[k], b = base[k];
-        if (k == 0 || !n) return MXP_OK;
+        if (!n) return MXP_OK;
         sel_off[lo] = b;
-        for (uint64_t i = 1; i < n; i++) sel_off[lo + i] += b;
+        if (b)
+            for (uint64_t i = 1; i < n; i++) sel_off[lo + i] += b;
         return MXP_OK;
     });
     sel_off[g->lo[n_shards]] = total;

@@ -36,11 +36,125 @@ struct mxp_list {
     uint32_t lds_nparts = 0;
     DevBuf lds_plan;  // REGEX: [K per staged part][LDS word base per staged part] (lists.h)
     NfaScratch nfa_scratch;  // REGEX: thread sets of NFA parts wider than the private-memory walk
+    DevBuf rxp_tab, rxp_blk, rxp_lead;  // REGEX: literal-prefix dispatch (lists.h MXP_RXP_*)
+    uint32_t rxp_mask = 0, rxp_short = 0, rxp_n = 0;
 };
 
 namespace {
 
 const uint32_t kUpperRows[MXP_UPPER_N][3] = {MXP_UPPER_ROWS};
+
+// The tail block (lists.h MXP_RXP_*) of a pattern whose every match starts with the literal bytes
+// `pre` (regex_required_prefix): its DFA stepped over the prefix, then the states reachable from
+// there with their transitions over the classes the tail tells apart.  False when the tail does not
+// fit a block: more than 32 states, 16 classes or MXP_RXP_BLOCK bytes, an NFA, or a state where
+// non-ASCII runes lead anywhere but to a decision.  *never: no subject starting with the prefix
+// matches (the pattern can be dropped: its prefix is required).
+bool rxp_block(const mxp::Dfa& d, std::string pre, std::vector<uint8_t>* out, bool* never) {
+    *never = false;
+    if (d.is_nfa() || pre.empty()) return false;
+    // at most MXP_RXP_MAXPRE bytes, cut at a rune boundary (the DFA steps runes)
+    if (pre.size() > MXP_RXP_MAXPRE) {
+        size_t L = MXP_RXP_MAXPRE;
+        while (L > 0 && ((uint8_t)pre[L] & 0xC0u) == 0x80u) L--;
+        pre.resize(L);
+        if (pre.empty()) return false;
+    }
+    auto cls_of_rune = [&](uint32_t r) -> uint32_t {
+        if (r < 0x80) return d.ascii[r];
+        const size_t at = std::upper_bound(d.hi_lo.begin(), d.hi_lo.end(), r) - d.hi_lo.begin() - 1;
+        return d.hi_cls[at];
+    };
+    uint32_t st = d.start;
+    for (size_t b = 0; b < pre.size() && st < mxp::kDfaReject;) {
+        const uint8_t c = (uint8_t)pre[b];
+        uint32_t r = c, w = 1;
+        if (c >= 0x80) {  // a literal rune's UTF-8 bytes (valid: the prefix holds literal runes)
+            w = c >= 0xF0 ? 4 : c >= 0xE0 ? 3 : 2;
+            r = c & (0xFFu >> (w + 1));
+            for (uint32_t k = 1; k < w; k++) r = (r << 6) | ((uint8_t)pre[b + k] & 0x3Fu);
+        }
+        st = d.trans[(size_t)st * d.ncls + cls_of_rune(r)];
+        b += w;
+    }
+    if (st == mxp::kDfaReject) {
+        *never = true;
+        return false;
+    }
+    std::vector<uint32_t> states;  // tail state -> DFA state (BFS from the state after the prefix)
+    std::unordered_map<uint32_t, uint32_t> idx;
+    if (st != mxp::kDfaAccept) {
+        states.push_back(st);
+        idx[st] = 0;
+        for (size_t i = 0; i < states.size(); i++)
+            for (uint32_t c = 0; c < d.ncls; c++) {
+                const uint32_t t = d.trans[(size_t)states[i] * d.ncls + c];
+                if (t >= mxp::kDfaReject || idx.count(t)) continue;
+                if (states.size() >= 32) return false;
+                idx[t] = (uint32_t)states.size();
+                states.push_back(t);
+            }
+    }
+    const uint32_t S = (uint32_t)states.size();
+    auto code = [&](uint32_t t) -> uint8_t {
+        return t == mxp::kDfaAccept ? (uint8_t)MXP_RXP_ACC : t == mxp::kDfaReject ? (uint8_t)MXP_RXP_REJ : (uint8_t)idx[t];
+    };
+    // non-ASCII runes: per state one decided target for every class a non-ASCII range maps to
+    std::vector<uint8_t> hi(S, MXP_RXP_REJ);
+    for (uint32_t k = 0; k < S; k++) {
+        bool first = true;
+        for (uint16_t c : d.hi_cls) {
+            const uint32_t t = d.trans[(size_t)states[k] * d.ncls + c];
+            if (t < mxp::kDfaReject) return false;
+            if (!first && code(t) != hi[k]) return false;
+            hi[k] = code(t);
+            first = false;
+        }
+    }
+    // ASCII bytes grouped by their tail columns
+    std::map<std::vector<uint8_t>, uint32_t> sig_id;
+    std::vector<std::vector<uint8_t>> cols;
+    uint8_t byte_cls[128];
+    for (uint32_t b = 0; b < 128; b++) {
+        std::vector<uint8_t> sig(S);
+        for (uint32_t k = 0; k < S; k++) sig[k] = code(d.trans[(size_t)states[k] * d.ncls + d.ascii[b]]);
+        auto it = sig_id.find(sig);
+        if (it == sig_id.end()) {
+            it = sig_id.emplace(sig, (uint32_t)cols.size()).first;
+            cols.push_back(sig);
+        }
+        byte_cls[b] = (uint8_t)it->second;
+    }
+    const uint32_t C = (uint32_t)cols.size() + 2;
+    if (C > 16 || MXP_RXP_TRANS + S * C > MXP_RXP_BLOCK) return false;
+    const uint32_t bytes = (MXP_RXP_TRANS + S * C + 15u) & ~15u;
+    out->assign(bytes, 0);
+    uint8_t* B = out->data();
+    B[0] = (uint8_t)S;
+    B[1] = (uint8_t)C;
+    B[2] = (uint8_t)pre.size();
+    B[3] = (uint8_t)(bytes / 16u);
+    memcpy(B + 4, pre.data(), pre.size());
+    for (uint32_t b = 0; b < 128; b++) B[32 + b / 2] |= (uint8_t)(byte_cls[b] << (4 * (b & 1)));
+    for (uint32_t k = 0; k < S; k++) {
+        uint8_t* row = B + MXP_RXP_TRANS + k * C;
+        for (uint32_t c = 0; c + 2 < C; c++) row[c] = cols[c][k];
+        row[C - 2] = hi[k];
+        row[C - 1] = code(d.trans[(size_t)states[k] * d.ncls + d.ncls - 1]);
+    }
+    return true;
+}
+
+// hash of a prefix as the kernel computes it from the symbol's first bytes (lists.h)
+uint64_t rxp_hash(const std::string& p) {
+    uint64_t h = 0;
+    for (size_t i = 0; i < p.size(); i += 8) {
+        uint64_t w = 0;
+        memcpy(&w, p.data() + i, std::min<size_t>(8, p.size() - i));
+        h = mxp_hash_step(h, w);
+    }
+    return mxp_hash_final(h, p.size());
+}
 
 // strings.ToUpper (Go 1.9; goupper.h): the key a case-insensitive list stores and looks up
 std::string go_to_upper(const std::string& s) {
@@ -169,6 +283,11 @@ uint32_t ip_split() {
 void set_lds(mxp_list_args& A, const mxp_list* L) {
     A.lds_nparts = L->lds_nparts;
     A.lds_plan = L->lds_plan.as<uint32_t>();
+    A.rxp_tab = L->rxp_tab.as<uint64_t>();
+    A.rxp_blk = L->rxp_blk.as<uint8_t>();
+    A.rxp_lead = L->rxp_lead.as<uint32_t>();
+    A.rxp_mask = L->rxp_mask;
+    A.rxp_short = L->rxp_short;
 }
 
 }  // namespace
@@ -298,6 +417,15 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
         for (uint32_t i = 0; i < n_overrides; i++) pats.push_back(str(overrides[i], override_lens[i]));
         std::vector<uint64_t> cost(pats.size());
         std::vector<uint8_t> alone(pats.size(), 0);
+        // Literal-prefix dispatch (MXP_LIST_RXP=0: off): a pattern anchored on literal bytes
+        // (regex_required_prefix) whose DFA after them fits a tail block is indexed by those bytes
+        // and leaves the union parts; a lookup probes the prefixes it starts with and walks the
+        // candidates' tails in LDS (lists.hip mxp_list_rxp_kernel) -- a few dependent loads per
+        // lookup instead of one per byte through a union DFA far larger than the caches.
+        const char* rxp_env = getenv("MXP_LIST_RXP");
+        const bool rxp_on = !rxp_env || atoi(rxp_env) != 0;
+        std::map<std::string, std::vector<std::vector<uint8_t>>> rxp_keys;  // prefix -> its patterns' tails
+        std::vector<uint8_t> dispatched(pats.size(), 0);
         for (size_t i = 0; i < pats.size(); i++) {  // per-pattern errors, in the reference's order
             mxp::Dfa one;
             std::string e;
@@ -306,6 +434,61 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             if (prc == mxp::RX_UNSUPPORTED) return eng->fail(MXP_ERR_ARG, "unsupported regexp (engine): " + e);
             cost[i] = prc == mxp::RX_OK ? one.nstates : kPatternStates;
             alone[i] = prc != mxp::RX_OK;
+            std::string pre;
+            if (rxp_on && prc == mxp::RX_OK && mxp::regex_required_prefix(pats[i], &pre)) {
+                std::vector<uint8_t> blk;
+                bool never = false;
+                if (rxp_block(one, pre, &blk, &never)) {
+                    auto& v = rxp_keys[std::string((const char*)blk.data() + 4, blk[2])];
+                    if (v.size() < 63) {  // (a slot counts at most 63 tails)
+                        v.push_back(std::move(blk));
+                        dispatched[i] = 1;
+                    }
+                } else if (never) {
+                    dispatched[i] = 1;  // no subject starting with its required prefix matches: never matches
+                }
+            }
+        }
+        L->n_entries = pats.size();
+        if (!rxp_keys.empty()) {
+            uint32_t cap = 16;
+            while (cap < 2 * rxp_keys.size()) cap <<= 1;
+            std::vector<uint64_t> tab(cap, 0);
+            std::vector<uint8_t> pool;
+            std::vector<uint32_t> lead(MXP_RXP_LEAD, 0);
+            for (const auto& kv : rxp_keys) {
+                const std::string& key = kv.first;
+                const uint64_t first = pool.size() / 16;
+                for (const auto& b : kv.second) pool.insert(pool.end(), b.begin(), b.end());
+                const uint64_t h = rxp_hash(key);
+                uint32_t slot = (uint32_t)h & (cap - 1);
+                while (tab[slot]) slot = (slot + 1) & (cap - 1);
+                tab[slot] = (h >> 44) << 44 | (uint64_t)key.size() << 38 | (uint64_t)kv.second.size() << 32 | first;
+                const uint32_t bit = 1u << (key.size() - 1);
+                if (key.size() >= 3)
+                    lead[mxp_rxp_lead((uint8_t)key[0], (uint8_t)key[1], (uint8_t)key[2])] |= bit;
+                else
+                    L->rxp_short |= bit;
+                L->rxp_n += (uint32_t)kv.second.size();
+            }
+            pool.resize(pool.size() + MXP_RXP_BLOCK, 0);  // (slack)
+            if ((rc = put(L->rxp_tab, tab.data(), tab.size() * 8, "upload rxp table"))) return rc;
+            if ((rc = put(L->rxp_blk, pool.data(), pool.size(), "upload rxp blocks"))) return rc;
+            if ((rc = put(L->rxp_lead, lead.data(), lead.size() * 4, "upload rxp lead"))) return rc;
+            L->rxp_mask = cap - 1;
+            // the union parts keep the other patterns
+            std::vector<std::string> p2;
+            std::vector<uint64_t> c2;
+            std::vector<uint8_t> a2;
+            for (size_t i = 0; i < pats.size(); i++)
+                if (!dispatched[i]) {
+                    p2.push_back(std::move(pats[i]));
+                    c2.push_back(cost[i]);
+                    a2.push_back(alone[i]);
+                }
+            pats.swap(p2);
+            cost.swap(c2);
+            alone.swap(a2);
         }
         // u16 parts (MXP_LIST_RX16=1; off by default): union DFAs of at most 65533 states, u16 rows,
         // the patterns sorted first (any match is a match, so the order is free) so that a part's
@@ -371,7 +554,7 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             if ((rc = part(i, j))) return rc;
             i = j;
         }
-        if (set.hdr.empty()) {  // no patterns: an automaton that never matches
+        if (set.hdr.empty() && !L->rxp_mask) {  // no patterns: an automaton that never matches
             mxp::Dfa d;
             std::string e;
             mxp::regex_compile({}, 16, &d, &e);
@@ -398,12 +581,13 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             return eng->fail(MXP_ERR_NOMEM, "regex list: NFA thread-set scratch");
         L->rx_n = (uint32_t)set.hdr.size();
         for (const auto& h : set.hdr) L->rx_nfa += h.kind == MXP_RX_NFA ? 1u : 0u;
-        L->n_entries = pats.size();
-        if ((rc = put(L->rx_hdr, set.hdr.data(), set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
-        if ((rc = put(L->rx_trans, set.trans.data(), set.trans.size() * 4, "upload rx trans"))) return rc;
-        if ((rc = put(L->rx_ascii, set.ascii.data(), set.ascii.size() * 2, "upload rx ascii"))) return rc;
-        if ((rc = put(L->rx_hilo, set.hilo.data(), set.hilo.size() * 4, "upload rx hilo"))) return rc;
-        if ((rc = put(L->rx_hicls, set.hicls.data(), set.hicls.size() * 2, "upload rx hicls"))) return rc;
+        if (L->rx_n) {  // (every pattern dispatched by its prefix: no union part)
+            if ((rc = put(L->rx_hdr, set.hdr.data(), set.hdr.size() * sizeof(mxp_dfa_hdr), "upload rx hdr"))) return rc;
+            if ((rc = put(L->rx_trans, set.trans.data(), set.trans.size() * 4, "upload rx trans"))) return rc;
+            if ((rc = put(L->rx_ascii, set.ascii.data(), set.ascii.size() * 2, "upload rx ascii"))) return rc;
+            if ((rc = put(L->rx_hilo, set.hilo.data(), set.hilo.size() * 4, "upload rx hilo"))) return rc;
+            if ((rc = put(L->rx_hicls, set.hicls.data(), set.hicls.size() * 2, "upload rx hicls"))) return rc;
+        }
     } else {
         return eng->fail(MXP_ERR_ARG, "unknown list entry type");
     }

@@ -63,7 +63,38 @@ typedef struct mxp_list_args {
     const uint32_t* v4dir;      // IP lists: [65537] v4dir[k] = intervals whose start is below k << 16
     uint32_t opt;               // MXP_LIST_OPT_* (A/B knobs, MXP_LIST_OPT; default all on)
     uint32_t pad_opt;
+    // REGEX lists, literal-prefix dispatch (mxp_list_rxp_kernel; lists.cpp rxp_build): patterns
+    // anchored on a literal prefix are found through a hash table of their prefixes, each checked by a
+    // small tail automaton (MXP_RXP_* block) staged in the lane's LDS slot; the other patterns stay in
+    // the union parts above
+    const uint64_t* rxp_tab;    // slots: tag << 44 | prefix length << 38 | blocks << 32 | first block
+    const uint8_t* rxp_blk;     // tail blocks, 16-byte units
+    const uint32_t* rxp_lead;   // [MXP_RXP_LEAD] prefix-length masks by the hash of a prefix's first 3 bytes
+    uint32_t rxp_mask;          // table slots - 1 (0: no dispatch)
+    uint32_t rxp_short;         // prefix-length mask of the prefixes shorter than 3 bytes
 } mxp_list_args;
+
+// Tail block of one prefix-dispatched pattern (at most MXP_RXP_BLOCK bytes, 16-byte units):
+//   [0] S tail states (0: the prefix alone matches)   [1] C classes (ASCII classes, then HI, END)
+//   [2] L prefix length                                [3] the block's 16-byte units
+//   [4 .. 4 + MXP_RXP_MAXPRE)   the prefix, zero padded
+//   [32 .. 96)                  class of each ASCII byte, one nibble each (low nibble = even byte)
+//   [96 .. 96 + S * C)          next state per (state, class): a state, MXP_RXP_ACC or MXP_RXP_REJ
+// A byte >= 0x80 takes class C - 2 (HI): from every tail state all non-ASCII runes either reject or
+// accept (the block is built only then), so the rune's first byte decides; C - 1 is END of text.
+#define MXP_RXP_BLOCK 240u
+#define MXP_RXP_ROW 61u   // LDS words per lane (the block and one pad word: an odd stride)
+#define MXP_RXP_MAXPRE 28u
+#define MXP_RXP_TRANS 96u
+#define MXP_RXP_ACC 0xFEu
+#define MXP_RXP_REJ 0xFFu
+#define MXP_RXP_LEAD 2048u
+#define MXP_RXP_THREADS 128u
+
+// bucket of a prefix's first three bytes in rxp_lead
+MXP_NHD uint32_t mxp_rxp_lead(uint32_t b0, uint32_t b1, uint32_t b2) {
+    return ((b0 | b1 << 8 | b2 << 16) * 2654435761u) >> 21;  // (11 bits: MXP_RXP_LEAD)
+}
 #define MXP_LIST_OPT_V4REG 1u   // dotted quads of <= 15 bytes parsed from registers (one window load)
 #define MXP_LIST_OPT_V4DIR 2u   // the IPv4 search starts from the /16 directory
 #define MXP_LIST_OPT_STRREG 4u  // string symbols of <= 64 bytes loaded once into registers

@@ -426,7 +426,110 @@ __device__ __forceinline__ void list_rx_body(const mxp_list_args& A) {
 extern "C" __global__ __launch_bounds__(1024) void mxp_list_rx_kernel(mxp_list_args A) { list_rx_body<false>(A); }
 extern "C" __global__ __launch_bounds__(1024) void mxp_list_rx_nfa_kernel(mxp_list_args A) { list_rx_body<true>(A); }
 
+// REGEX lists with literal-prefix dispatch (lists.cpp rxp_build).  Per lookup: the prefix lengths
+// worth probing come from the LDS mask of its first three bytes (rxp_lead, staged per workgroup) and
+// the short-prefix mask; each is one probe of the prefix table (hash of the symbol's first L bytes,
+// kept in registers); a slot names the tail blocks of the patterns with that prefix; a block's header
+// and prefix are compared from registers, then the block is copied to the lane's LDS slot and its
+// tail automaton stepped from there over the rest of the symbol (one LDS byte per class, one per
+// transition).  So a lookup pays ~3 dependent global loads (symbol, slot, block) where the union DFA
+// paid one per byte.  Patterns not dispatched stay in the union parts, walked after (from global).
+template <bool kNfa>
+__device__ __forceinline__ void list_rxp_body(const mxp_list_args& A) {
+    __shared__ uint32_t LEAD[MXP_RXP_LEAD];
+    // one block per lane, rows of MXP_RXP_ROW words (odd: the lanes' words fall in different banks)
+    __shared__ uint32_t SLOT[MXP_RXP_THREADS * MXP_RXP_ROW];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < MXP_RXP_LEAD; i += MXP_RXP_THREADS) LEAD[i] = A.rxp_lead[i];
+    __syncthreads();
+    uint32_t* const row = SLOT + tid * MXP_RXP_ROW;
+    const uint8_t* const mine = (const uint8_t*)row;
+    for (uint32_t q = blockIdx.x * MXP_RXP_THREADS + tid; q < A.n; q += gridDim.x * MXP_RXP_THREADS) {
+        const uint8_t* s;
+        uint32_t n;
+        if (!list_symbol(A, q, &s, &n)) continue;
+        // the symbol's first 32 bytes (zero past its end): prefix hashes and compares, the walk's bytes
+        uint64_t w[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) w[k] = 8u * k < n ? mxp_ld8(s + 8u * k) & tail_mask(n - 8u * k) : 0ull;
+        uint32_t lens = A.rxp_short;
+        if (n >= 3u) {
+            const uint32_t b = (uint32_t)w[0];
+            lens |= LEAD[mxp_rxp_lead(b & 0xFFu, (b >> 8) & 0xFFu, (b >> 16) & 0xFFu)];
+        }
+        if (n < 32u) lens &= (1u << n) - 1u;  // (prefixes no longer than the symbol)
+        bool found = false;
+        for (; lens && !found; lens &= lens - 1u) {
+            const uint32_t L = (uint32_t)__ffs(lens);  // (bit L - 1: prefix length L)
+            uint64_t pre[4], h = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                pre[k] = 8u * k < L ? w[k] & tail_mask(L - 8u * k) : 0ull;
+                if (8u * k < L) h = mxp_hash_step(h, pre[k]);
+            }
+            h = mxp_hash_final(h, L);
+            const uint64_t want = (h >> 44) << 44 | (uint64_t)L << 38;
+            uint64_t t = 0;
+            for (uint32_t slot = (uint32_t)h & A.rxp_mask;; slot = (slot + 1u) & A.rxp_mask) {
+                t = A.rxp_tab[slot];
+                if (!t || (t & ~0x3FFFFFFFFFull) == want) break;
+            }
+            if (!t) continue;
+            const uint32_t count = (uint32_t)(t >> 32) & 0x3Fu;
+            uint32_t unit = (uint32_t)t;
+            for (uint32_t c = 0; c < count && !found; c++) {
+                const uint4* blk = (const uint4*)A.rxp_blk + unit;
+                const uint4 h0 = blk[0], h1 = blk[1];
+                const uint32_t S = h0.x & 0xFFu, C = (h0.x >> 8) & 0xFFu, nq = h0.x >> 24;
+                unit += nq;
+                // the block's prefix (bytes 4 .. 32, zero padded) against the symbol's first L bytes
+                const bool same = pre[0] == ((uint64_t)h0.y | (uint64_t)h0.z << 32) &&
+                                  pre[1] == ((uint64_t)h0.w | (uint64_t)h1.x << 32) &&
+                                  pre[2] == ((uint64_t)h1.y | (uint64_t)h1.z << 32) && pre[3] == (uint64_t)h1.w;
+                if (!same) continue;
+                if (S == 0u) {  // the prefix alone decides
+                    found = true;
+                    break;
+                }
+                for (uint32_t k = 2; k < nq; k++) {  // class nibbles and transitions into the lane's row
+                    const uint4 v = blk[k];
+                    row[4u * k] = v.x;
+                    row[4u * k + 1u] = v.y;
+                    row[4u * k + 2u] = v.z;
+                    row[4u * k + 3u] = v.w;
+                }
+                const uint8_t* T = mine + MXP_RXP_TRANS;
+                uint32_t st = 0;
+                for (uint32_t i = L; i < n && st < S; i++) {
+                    const uint64_t wi = i < 8u ? w[0] : i < 16u ? w[1] : i < 24u ? w[2] : w[3];
+                    const uint32_t b = i < 32u ? (uint32_t)(wi >> ((i & 7u) * 8u)) & 0xFFu : s[i];
+                    const uint32_t cls = b >= 0x80u ? C - 2u : (mine[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
+                    st = T[st * C + cls];
+                }
+                if (st < S) st = T[st * C + C - 1u];  // END of text
+                found = st == MXP_RXP_ACC;
+            }
+        }
+        for (uint32_t k = 0; k < A.rx_n && !found; k++) found = rx_part<kNfa>(A, k, s, n);
+        list_decide(A, q, found);
+    }
+}
+extern "C" __global__ __launch_bounds__(MXP_RXP_THREADS) void mxp_list_rxp_kernel(mxp_list_args A) {
+    list_rxp_body<false>(A);
+}
+extern "C" __global__ __launch_bounds__(MXP_RXP_THREADS) void mxp_list_rxp_nfa_kernel(mxp_list_args A) {
+    list_rxp_body<true>(A);
+}
+
 extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s) {
+    if (a->type == MXP_LIST_REGEX && a->rxp_mask) {
+        // persistent: four 128-thread workgroups per CU (their LDS: 4 x 39 KB of the 160 KB)
+        const uint32_t need = (a->n + MXP_RXP_THREADS - 1u) / MXP_RXP_THREADS;
+        const uint32_t grid = need < 1024u ? need : 1024u;
+        hipLaunchKernelGGL(a->rx_nfa ? mxp_list_rxp_nfa_kernel : mxp_list_rxp_kernel, dim3(grid), dim3(MXP_RXP_THREADS),
+                           0, s, *a);
+        return hipGetLastError();
+    }
     if (a->type == MXP_LIST_REGEX && a->lds_nparts) {
         // enough workgroups for 2 per CU (256 CUs), fewer for small batches
         const uint32_t need = (a->n + MXP_LIST_RX_THREADS - 1u) / MXP_LIST_RX_THREADS;

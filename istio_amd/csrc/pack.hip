@@ -556,3 +556,25 @@ extern "C" hipError_t mxp_launch_pack(const mxp_pack_args* a, uint32_t step, uin
     }
     return hipGetLastError();
 }
+
+// The narrow batch (mxp_batch_upload2): u32 values / offsets as copied, widened to the u64 layout
+// the packer reads (zero extension; a grid-stride pass of 16-byte loads and 32-byte stores)
+extern "C" __global__ __launch_bounds__(256) void mxp_widen_kernel(const uint32_t* __restrict__ in,
+                                                                   uint64_t* __restrict__ out, uint64_t n) {
+    const uint64_t n4 = n / 4u;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n4; i += (uint64_t)gridDim.x * 256ull) {
+        const uint4 v = reinterpret_cast<const uint4*>(in)[i];
+        reinterpret_cast<ulonglong2*>(out)[2 * i] = make_ulonglong2(v.x, v.y);
+        reinterpret_cast<ulonglong2*>(out)[2 * i + 1] = make_ulonglong2(v.z, v.w);
+    }
+    const uint64_t t = 4 * n4 + blockIdx.x * 256ull + threadIdx.x;
+    if (blockIdx.x == 0 && t < n) out[t] = in[t];
+}
+
+// in / out: 16-byte aligned device buffers (hipMalloc blocks)
+extern "C" hipError_t mxp_launch_widen(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint64_t g = (n / 4u + 255u) / 256u;
+    hipLaunchKernelGGL(mxp_widen_kernel, dim3((uint32_t)(g < 2048u ? (g ? g : 1u) : 2048u)), dim3(256), 0, s, in, out, n);
+    return hipGetLastError();
+}

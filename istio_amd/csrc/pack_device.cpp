@@ -15,6 +15,7 @@
 #include "pack_args.h"
 
 extern "C" hipError_t mxp_launch_pack(const mxp_pack_args* a, uint32_t step, uint32_t arg, hipStream_t s);
+extern "C" hipError_t mxp_launch_widen(const uint32_t* in, uint64_t* out, uint64_t n, hipStream_t s);
 
 namespace {
 constexpr size_t kVtBytes = 8 * MXP_PACK_VTCAND;  // value-class distinct counts + overflow flags (u32 pairs)
@@ -151,8 +152,22 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
             return hipfail(e, what);
         return MXP_OK;
     };
+    // a narrow batch (mxp_batch_upload2): its u32 arrays go over the link and are widened here, on the
+    // copy stream behind their copies (b is its host view)
+    const mxp_bag_batch2* nb = narrow_src;
+    auto up_wide = [&](DevBuf& d, DevBuf& d32, const uint64_t* src64, const uint32_t* src32, size_t count,
+                       const char* what) -> int {
+        if (!nb || !src32) return up(d, src64, count * 8, what);
+        if ((rc = up(d32, src32, count * 4, what))) return rc;
+        if ((rc = grow(d, count ? count * 8 : 16, what))) return rc;
+        if (count && (e = mxp_launch_widen(d32.as<uint32_t>(), d.as<uint64_t>(), count, cs)) != hipSuccess)
+            return hipfail(e, what);
+        return MXP_OK;
+    };
     const uint64_t sbytes = NS ? b->str_offsets[NS] : 0;
-    if ((rc = up(P.pk_soff, b->str_offsets, NS ? ((size_t)NS + 1) * 8 : 0, "upload string offsets"))) return rc;
+    if ((rc = up_wide(P.pk_soff, P.pk_soff32, b->str_offsets, nb ? nb->str_offsets32 : nullptr, NS ? (size_t)NS + 1 : 0,
+                      "upload string offsets")))
+        return rc;
     // (16 bytes of slack: the intern kernel reads strings 8 bytes at a time)
     if ((rc = grow(P.pk_sbytes, sbytes + 16, "upload string bytes"))) return rc;
     if (sbytes && (e = hipMemcpyAsync(P.pk_sbytes.p, b->str_bytes, sbytes, hipMemcpyHostToDevice, cs)) != hipSuccess)
@@ -163,7 +178,9 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     if ((rc = up(db->btsec, b->time_sec, (size_t)NT * 8, "times"))) return rc;
     if ((rc = up(db->btnsec, b->time_nsec, (size_t)NT * 4, "times"))) return rc;
     const uint64_t E = (any_map && NM) ? b->map_offsets[NM] : 0;
-    if ((rc = up(P.pk_moff, b->map_offsets, any_map && NM ? ((size_t)NM + 1) * 8 : 0, "upload map offsets"))) return rc;
+    if ((rc = up_wide(P.pk_moff, P.pk_moff32, b->map_offsets, nb ? nb->map_offsets32 : nullptr,
+                      any_map && NM ? (size_t)NM + 1 : 0, "upload map offsets")))
+        return rc;
     if ((rc = up(P.pk_mkey, b->map_keys, E * 4, "upload map keys"))) return rc;
     if ((rc = up(P.pk_mval, b->map_values, E * 4, "upload map values"))) return rc;
     if ((e = hipEventRecord(db->pk_ev[0], cs)) != hipSuccess) return hipfail(e, "strings event");
@@ -190,14 +207,11 @@ int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
     trace_host("pack: strings queued");
     for (uint32_t bc = 0; bc < b->n_columns; bc++) {
         if (slot_of[bc] < 0) continue;
-        DevBuf* bufs[2] = {&P.pk_ck[slot_of[bc]], &P.pk_cv[slot_of[bc]]};
-        const void* src[2] = {b->kinds[bc], b->values[bc]};
-        const size_t bytes[2] = {n, (size_t)n * 8};
-        for (int k = 0; k < 2; k++) {
-            if ((rc = grow(*bufs[k], bytes[k] ? bytes[k] : 16, "upload columns"))) return rc;
-            if (bytes[k] && (e = hipMemcpyAsync(bufs[k]->p, src[k], bytes[k], hipMemcpyHostToDevice, cs)) != hipSuccess)
-                return hipfail(e, "upload columns");
-        }
+        if ((rc = up(P.pk_ck[slot_of[bc]], b->kinds[bc], n, "upload columns"))) return rc;
+        const bool narrow = nb && nb->narrow[bc];
+        if ((rc = up_wide(P.pk_cv[slot_of[bc]], P.pk_cv32[slot_of[bc]], b->values[bc], narrow ? nb->values32[bc] : nullptr,
+                          n, "upload columns")))
+            return rc;
     }
     if ((e = hipEventRecord(db->pk_ev[1], cs)) != hipSuccess) return hipfail(e, "columns event");
     if (resolver.set) {

@@ -364,11 +364,14 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     if (n && (e = mxp_launch_resolve(&A, 2, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve scan");
     eng->trace_mark("  resolve: count + scan kernels");
     if (!n) {
-        sel_off[0] = 0;
+        if (!place) sel_off[0] = 0;
     } else {
         const std::vector<mxp_engine::Piece> outs = {{status, d_status.p, n},
                                                      {err_rule, d_err_rule.p, (size_t)n * 4},
-                                                     {sel_off, d_off.p, ((size_t)n + 1) * 8}};
+                                                     // (a group member leaves sel_off[0] alone: that
+                                                     // entry is the previous member's last one)
+                                                     place ? mxp_engine::Piece{sel_off + 1, d_off.as<uint64_t>() + 1, (size_t)n * 8}
+                                                           : mxp_engine::Piece{sel_off, d_off.p, ((size_t)n + 1) * 8}};
         if ((rc = eng->download_all(outs, "download resolve outputs"))) return rc;
     }
     eng->trace_mark("resolve kernels + downloads");
@@ -382,7 +385,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         ref_rc = eng->refs_assemble(batch, recs, &scope, ref_off, refs, ref_cap);
         if (ref_rc && ref_rc != MXP_ERR_NOMEM) return ref_rc;
     }
-    const uint64_t total = sel_off[n];
+    const uint64_t total = n ? sel_off[n] : 0;
     // (a group member learns where its ids go in the whole batch's list once every member knows its
     // own count: place blocks until then, -1 = the whole list does not fit)
     int64_t at = 0;
@@ -408,6 +411,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
 int mxp_resolve_placed(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
                        uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules,
                        const mxp_resolve_place& place) {
+    if (!batch && db && db->wide) batch = &db->wide->view;  // (a narrow upload: its host view)
     if (flags & ~(uint32_t)MXP_RESOLVE_IDS_U16) {
         if (eng && db) eng->recycle(db);
         return MXP_ERR_ARG;
@@ -433,6 +437,7 @@ int mxp_resolve_batch_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t v
 int mxp_resolve_uploaded(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
                          uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap) {
     if (!db) return MXP_ERR_ARG;
+    if (!batch && db->wide) batch = &db->wide->view;  // (a narrow upload: its host view)
     if (!eng || (flags & ~(uint32_t)MXP_RESOLVE_IDS_U16)) {
         if (eng) eng->recycle(db);
         return MXP_ERR_ARG;

@@ -126,6 +126,8 @@ SIGNATURES = {
     "mxp_group_resolver_set": (ctypes.c_int, [_VP, ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p),
                                               _VP, _VP, _VP, ctypes.c_uint32]),
     "mxp_group_upload": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_VP)]),
+    "mxp_group_upload2": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_VP)]),
+    "mxp_batch_upload2": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.POINTER(_VP)]),
     "mxp_group_upload_split": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.POINTER(_VP)]),
     "mxp_group_batch_wait_copied": (ctypes.c_int, [_VP]),
     "mxp_group_batch_free": (None, [_VP, _VP]),
@@ -240,6 +242,20 @@ def pinned_batch(batch: BagBatch):
     for a, b in zip(out.kinds + out.values, p[:2 * nc]):
         assert a.ctypes.data == b.ctypes.data  # (no copy made by the constructor)
     return out, arena
+
+
+def pinned_narrow(batch: BagBatch):
+    """(the narrow form of `batch` whose arrays -- kinds, u32 / u64 values, string bytes, u32 offsets,
+    times, maps -- live in pinned memory, the arena that holds them): what a binding's packing arena
+    holds for mxp_batch_upload2."""
+    from .bags import NarrowBatch
+    pb, arena = pinned_batch(batch)
+    extra = NarrowBatch(batch)  # (sizes)
+    need = (sum(v.nbytes + 64 for v in extra.values32 if v is not None) + extra.str_offsets32.nbytes
+            + extra.map_offsets32.nbytes + extra.narrow.nbytes + 4 * 64)
+    arena2 = PinnedArena(need)
+    nb = NarrowBatch(pb, alloc=arena2.empty)
+    return nb, (arena, arena2)
 
 
 def go_to_upper(s: bytes) -> bytes:
@@ -585,7 +601,8 @@ class Engine:
         status, err_rule = np.empty(n, dtype=np.uint8), np.empty(n, dtype=np.uint32)
         off, sel = np.empty(n + 1, dtype=np.uint64), np.empty(max(cap, 1), dtype=np.uint16 if ids16 else np.uint32)
         h, db.h = db.h, None
-        self._check(self.lib.mxp_resolve_uploaded(self.h, h, ctypes.byref(cs), variety, 1 if ids16 else 0,
+        self._check(self.lib.mxp_resolve_uploaded(self.h, h, ctypes.byref(cs) if cs is not None else None, variety,
+                                                  1 if ids16 else 0,
                                                   status.ctypes.data, err_rule.ctypes.data, off.ctypes.data,
                                                   sel.ctypes.data, cap), "mxp_resolve_uploaded")
         return status, err_rule, off, sel[:int(off[n])]
@@ -646,6 +663,20 @@ class Engine:
         return db
 
 
+def _upload2(self, nb, no_wait: bool = False) -> "DeviceBatch":
+    """mxp_batch_upload2: a NarrowBatch (bags.py) uploaded narrow and widened on the device."""
+    h = _VP()
+    cs = nb.c_struct()
+    self._check(self.lib.mxp_batch_upload2(self.h, ctypes.byref(cs), 1 if no_wait else 0, ctypes.byref(h)),
+                "mxp_batch_upload2")
+    db = DeviceBatch(self, h, nb.n)
+    db._src = (nb, None)  # (resolve_uploaded passes NULL: the engine keeps the host view)
+    return db
+
+
+Engine.upload2 = _upload2
+
+
 class DeviceBatch:
     def __init__(self, engine: Engine, h, n: int):
         self.engine = engine
@@ -653,7 +684,8 @@ class DeviceBatch:
         self.n = n
 
     def wait_copied(self):
-        """mxp_batch_wait_copied: the batch's host arrays are free again (after a no_wait upload)."""
+        """mxp_batch_wait_copied: the batch's host arrays are free again (after a no_wait upload).
+        (DeviceBatch)"""
         self.engine._check(self.engine.lib.mxp_batch_wait_copied(self.h), "mxp_batch_wait_copied")
 
     def eval(self, d_match: int, d_err: int, stream: int = 0):
@@ -1051,6 +1083,17 @@ class Group:
         gb._src = (list(shards), cs)
         return gb
 
+    def upload2(self, shards, no_wait: bool = False) -> "GroupBatch":
+        """mxp_group_upload2: NarrowBatch shards (bags.py), member k's = shards[k]."""
+        cs = [b.c_struct() for b in shards]
+        arr = (_VP * len(cs))(*[ctypes.addressof(c) for c in cs])
+        h = _VP()
+        self._check(self.lib.mxp_group_upload2(self.h, arr, len(cs), 1 if no_wait else 0, ctypes.byref(h)),
+                    "mxp_group_upload2")
+        gb = GroupBatch(self, h, [b.n for b in shards])
+        gb._src = (list(shards), None)  # (mxp_group_resolve_uploaded: shards NULL, the members' host views)
+        return gb
+
     def upload_split(self, batch: BagBatch) -> "GroupBatch":
         cs = batch.c_struct()
         h = _VP()
@@ -1107,9 +1150,11 @@ class Group:
         sel_off, sel_rules) of the concatenated batch.  out: preallocated (status, err_rule, sel_off,
         sel) arrays (e.g. pinned), reused when large enough.  uploaded: the shards' GroupBatch from an
         earlier upload (mxp_group_resolve_uploaded; taken over -- no retry when cap is short)."""
-        n = sum(b.n for b in shards)
+        n = sum(b.n for b in shards) if shards is not None else uploaded.n
         if uploaded is None:
             cs, arr = self._shards(shards)
+        elif uploaded._src[1] is None:  # (narrow uploads: the members keep the host views)
+            cs, arr = [None] * self.n, None
         else:  # (the very structs the shards were uploaded from)
             cs = uploaded._src[1]
             arr = (_VP * len(cs))(*[ctypes.addressof(c) for c in cs])

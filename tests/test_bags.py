@@ -89,3 +89,23 @@ def test_c_struct_layout_matches_the_header():
                    "n_maps": 80, "map_offsets": 88, "map_keys": 96, "map_values": 104}
     assert ctypes.sizeof(s) == 112
     assert s.n_requests == 1 and s.n_columns == 3 and s.n_times == 1 and s.n_maps == 1
+
+
+def test_narrow_batch_layout():
+    """bags.NarrowBatch (mxp_bag_batch2): id / BOOL columns travel as u32 (exact copies), numeric
+    columns stay u64, offsets become u32; C2 batches cross the link in ~30-39 % fewer bytes."""
+    import numpy as np
+    from istio_amd.bags import BagBatch, NarrowBatch
+    b = BagBatch.from_bags(W.fuzz_bags(300, seed=3, p_wrong=0.0), names=list(W.DEFAULT_TEST_MANIFEST))
+    nb = NarrowBatch(b)
+    for c, name in enumerate(b.names):
+        numeric = bool(np.isin(b.kinds[c], (2, 3, 5)).any())
+        assert bool(nb.narrow[c]) == (not numeric), name
+        if nb.narrow[c]:
+            assert np.array_equal(nb.values32[c].astype(np.uint64), b.values[c])
+    assert np.array_equal(nb.str_offsets32.astype(np.uint64), b.str_offsets)
+    cs = nb.c_struct()
+    assert not cs.base.str_offsets and cs.str_offsets32 and cs.base.n_requests == 300
+    _, _, c2 = W.c2_workload(n_rules=50, n_requests=1 << 16, seed=2)
+    wide = sum(a.nbytes for a in list(c2.kinds) + list(c2.values) + [c2.str_blob, c2.str_offsets])
+    assert NarrowBatch(c2).wire_bytes() < 0.72 * wide

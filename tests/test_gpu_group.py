@@ -247,7 +247,7 @@ def test_resolve_uploaded_pipeline(mxp, devices):
     R = len(rules)
     ns, vm = ["istio-system"] * R, np.ones(R, dtype=np.uint32)
     z = np.zeros(R, dtype=np.uint8)
-    batches = [W.c2_workload(n_rules=1500, n_requests=90_001, seed=2, shard=(k * 90_001, (k + 1) * 90_001))[2]
+    batches = [W.c2_workload(n_rules=1500, n_requests=3 * 90_001, seed=2, shard=(k * 90_001, (k + 1) * 90_001))[2]
                for k in range(3)]
     ref = mxp.Engine(0)
     ref.set_vocabulary(manifest)

@@ -111,6 +111,7 @@ def test_regex_list_u16_parts_agree(eng, monkeypatch):
     the caller's order (MXP_LIST_RX16=0), with and without LDS staging, and against the restatement
     on a sample: identical codes."""
     pats, syms = W.c3_regex_list(n_patterns=4000, n_lookups=60000, seed=45)
+    monkeypatch.setenv("MXP_LIST_RXP", "0")  # (the union parts: no literal-prefix dispatch)
     got = {}
     for rx16 in ("1", "0"):
         for lds in ("1", "0"):
@@ -179,6 +180,7 @@ def test_regex_list_lds_staging(monkeypatch, case):
     else:
         pats, syms = W.c3_regex_list(n_patterns=50_000, n_lookups=80_021, seed=74)
     out = {}
+    monkeypatch.setenv("MXP_LIST_RXP", "0")  # (the union parts: no literal-prefix dispatch)
     for lds in ("1", "0"):
         monkeypatch.setenv("MXP_LIST_LDS", lds)
         eng = mxp.Engine(0)
@@ -319,3 +321,42 @@ def test_listentry_fused_unicode(eng):
     assert (want == 0).sum() > 1000 and (want == -1).sum() > 100
     enc = lambda x: x.encode("utf-8", "surrogateescape")  # noqa: E731 (escaped bytes may re-decode as runes)
     assert all(enc(texts[q]) == enc(bags[q]["request.path"]) for q in range(batch.n) if got[q] >= 0)
+
+
+RXP_PATTERNS = ["^kk", "^abc$", "\\Aabc.*z", "^abc(?i)def", "^abc\\b", "^abc\\n?$", "^abc.", "(?m)^abd",
+                "^k|^j", "^x[0-9]", "^xy[0-9]", "^é[a-z]+$", "^ü", "^qqq[^\\x00-\\x{10FFFF}]",
+                "^" + "l" * 40 + "[0-9]", "^" + "m" * 27 + "é[0-9]", "^caf(é|e)s?$", "^tail[a-z]{0,20}$",
+                "^z(y|x)w", "^zywv+$"] + ["^shared[0-9]{%d}$" % k for k in range(70)]
+RXP_SYMBOLS = ["", "a", "ab", "abx", "k", "kk", "kkx", "j", "jj", "ak", "abc", "abcx", "abcz", "abczz", "abcDEF", "abcdef", "abc def", "abc\n", "abc\n\n",
+               "abcé", "abd", "x\nabd", "b", "bb", "x1", "xy1", "xyz", "é", "éabc", "éé", "éab1", "ü", "ab\udcff",
+               "qqq", "qqqa", "l" * 40 + "1", "l" * 40, "l" * 39 + "1", "m" * 27 + "é1", "m" * 27 + "e1", "cafés",
+               "cafe", "cafés!", "tail" + "a" * 20, "tail" + "a" * 21, "tail" + "a" * 20 + "1", "zyw", "zxw", "zywvvv",
+               "zywvx"] + ["shared" + "7" * k for k in range(72)] + ["shared" + "7" * k + "x" for k in range(5)]
+
+
+def test_regex_list_prefix_dispatch(eng, monkeypatch):
+    """Literal-prefix dispatch (lists.cpp rxp_block, mxp_list_rxp_kernel) against the union parts
+    (MXP_LIST_RXP=0) and the oracle: prefixes of 1 .. 28+ bytes (longer ones cut at a rune boundary),
+    non-ASCII prefixes and tails, tails that only the union can take (`^abc.`), patterns with no
+    required prefix ((?m)^, alternation), one that can never match, 70 patterns sharing a prefix (63
+    tails a slot), symbols shorter than the prefixes, longer than 32 bytes, with invalid UTF-8; plus
+    the C3 list with these mixed in, whitelist and blacklist."""
+    rng = np.random.default_rng(91)
+    pats, syms = W.c3_regex_list(n_patterns=3000, n_lookups=70_001, seed=92)
+    pats = pats[:1500] + RXP_PATTERNS + pats[1500:]
+    syms = RXP_SYMBOLS + syms
+    out = {}
+    for rxp in ("1", "0"):
+        monkeypatch.setenv("MXP_LIST_RXP", rxp)
+        lst = eng.list_create(L.REGEX, pats, ["^ovr[0-9]$", "(?i)^CASE"])
+        out[rxp] = (lst.check(syms + ["ovr1", "case", "CASEx"]), lst.check(syms, True), lst.regex_parts())
+    assert out["1"][2][0] < out["0"][2][0] or out["0"][2][0] == 1  # (fewer union parts with the dispatch)
+    assert np.array_equal(out["1"][0], out["0"][0]) and np.array_equal(out["1"][1], out["0"][1])
+    sample = list(range(len(RXP_SYMBOLS))) + list(len(RXP_SYMBOLS) + rng.choice(len(syms) - len(RXP_SYMBOLS), 600,
+                                                                                 replace=False))
+    ref = L.RegexList(pats, ["^ovr[0-9]$", "(?i)^CASE"])
+    want = L.codes(ref.found([syms[i] for i in sample], threads=16), False)
+    bad = [(syms[sample[j]], int(out["1"][0][sample[j]]), int(want[j])) for j in range(len(sample))
+           if out["1"][0][sample[j]] != want[j]]
+    assert not bad, bad[:8]
+    assert (want == 0).sum() > 100 and (want == 5).sum() > 100

@@ -90,16 +90,19 @@ def test_wide_nfa_rules_parity(mxp, monkeypatch, flags):
     assert np.array_equal(lst.check(sub_l), want_l)
 
 
-@pytest.mark.parametrize("rx16", ["1", "0"])
-def test_regex_list_with_over_budget_patterns(mxp, monkeypatch, rx16):
+@pytest.mark.parametrize("rx16,rxp", [("1", "0"), ("0", "0"), ("0", "1")])
+def test_regex_list_with_over_budget_patterns(mxp, monkeypatch, rx16, rxp):
     monkeypatch.setenv("MXP_LIST_RX16", rx16)
+    monkeypatch.setenv("MXP_LIST_RXP", rxp)
     eng = mxp.Engine(0)
     rng = np.random.default_rng(5)
     syms = _nfa_subjects(rng, 3000)
     pats = ["^zz", NFA_PATTERNS[0], "x{3}", NFA_PATTERNS[2], NFA_PATTERNS[7], "^é"]
     lst = eng.list_create(L.REGEX, pats, [])
     parts, nfas = lst.regex_parts()
-    if rx16 == "0":
+    if rxp == "1":  # ^zz and ^é dispatched by their prefixes: the NFAs and x{3} stay in the union parts
+        assert nfas >= 2 and parts == nfas + 1
+    elif rx16 == "0":
         assert nfas >= 2 and parts == nfas + 3  # ^zz | nfa | x{3} | nfa | (nfa) | ^é: NFAs stand alone
     else:  # sorted first: DFA patterns side by side share u16 parts; the NFAs stand alone
         assert nfas >= 2 and nfas + 1 <= parts <= nfas + 3
@@ -117,7 +120,7 @@ def test_regex_list_50k_patterns(mxp):
     eng = mxp.Engine(0)
     lst = eng.list_create(L.REGEX, pats, [])
     parts, nfas = lst.regex_parts()
-    assert parts >= 1 and nfas == 0
+    assert nfas == 0  # (every C3 pattern is dispatched by its literal prefix: no union part is left)
     assert lst.num_entries() == 50_000
     want = L.codes(L.RegexList(pats).found(syms), False)
     got = lst.check(syms)
