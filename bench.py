@@ -471,8 +471,12 @@ def end_to_end(g, shard_sets, n_rules, reps, wire="narrow"):
             return g.resolve_arrays(None, 0, cap or max(16, 4 * n), ids16=ids16, out=out,
                                     uploaded=upload_set(g, st, wire, False))
         return g.resolve_arrays(st, 0, cap, ids16=ids16, out=out)
-    caps = [int(resolve(st)[2][-1]) for st in sets]  # warm-up (allocations), list sizes
+    # list sizes (the one-shot call from the wide form: an uploaded batch's Resolve cannot retry when
+    # its ids do not fit), then a warm-up of the measured call (allocations)
+    caps = [int(g.resolve_arrays([getattr(b, "batch", b) for b in st], 0, ids16=ids16)[2][-1]) for st in sets]
     cap = max(16, 2 * max(caps))
+    for st in sets:
+        resolve(st, cap)
     arena = PinnedArena(n * 13 + 8 + cap * 2 + 4 * 64)
     out = (arena.empty(n, np.uint8), arena.empty(n, np.uint32), arena.empty(n + 1, np.uint64),
            arena.empty(cap, np.uint16 if ids16 else np.uint32))

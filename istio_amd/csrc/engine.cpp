@@ -96,13 +96,24 @@ size_t BlockBin::held() {
 bool BlockBin::take(size_t want, void** p, size_t* cap) {
     std::lock_guard<std::mutex> lk(mu);
     size_t bg = 0, bi = 0, best = SIZE_MAX;
-    for (size_t g = 0; g < groups.size(); g++)
-        for (size_t i = 0; i < groups[g].blks.size(); i++) {
-            const size_t c = groups[g].blks[i].second;
-            if (c >= want && c <= 2 * want + (1u << 20) && c < best) {
-                best = c;
-                bg = g;
-                bi = i;
+    // groups whose work is done first (a query, no wait): a block released moments ago -- a packed
+    // batch's scratch, its last kernels still running -- is taken only when nothing else fits
+    for (int pass = 0; pass < 2 && best == SIZE_MAX; pass++)
+        for (size_t g = 0; g < groups.size(); g++) {
+            if (pass == 0 && !groups[g].done) {
+                bool all = true;
+                for (hipEvent_t e : groups[g].evs) all = all && hipEventQuery(e) == hipSuccess;
+                (void)hipGetLastError();  // (hipErrorNotReady)
+                if (!all) continue;
+                groups[g].done = true;
+            }
+            for (size_t i = 0; i < groups[g].blks.size(); i++) {
+                const size_t c = groups[g].blks[i].second;
+                if (c >= want && c <= 2 * want + (1u << 20) && c < best) {
+                    best = c;
+                    bg = g;
+                    bi = i;
+                }
             }
         }
     if (best == SIZE_MAX) return false;
@@ -1631,7 +1642,9 @@ int mxp_engine::pack_heads(mxp_dbatch* db) {
         return MXP_OK;
     }
     if ((e = d_head_cols.reserve(nrow * 4u)) != hipSuccess) return hipfail(e, "hipMalloc head columns");
-    if ((e = hipMemcpy(d_head_cols.p, head_cols.data(), nrow * 4u, hipMemcpyHostToDevice)) != hipSuccess)
+    // (async on the engine stream from the engine's own vector: a synchronous hipMemcpy on the legacy
+    // stream would wait for every blocking stream's queued work -- a group's evaluations among them)
+    if ((e = hipMemcpyAsync(d_head_cols.p, head_cols.data(), nrow * 4u, hipMemcpyHostToDevice, stream)) != hipSuccess)
         return hipfail(e, "upload head columns");
     mxp_kargs A;
     memset(&A, 0, sizeof A);
@@ -1709,13 +1722,21 @@ int mxp_engine::vt_prepare(mxp_dbatch* db, const Plan& P) {
     if (tbase >= (1ull << 31)) return fail(MXP_ERR_NOMEM, "value-class tables too large");
     hipError_t e;
     if ((e = db->vt_meta.alloc(meta.size() * 4)) != hipSuccess) return hipfail(e, "vt meta");
-    if ((e = hipMemcpy(db->vt_meta.p, meta.data(), meta.size() * 4, hipMemcpyHostToDevice)) != hipSuccess)
+    db->vt_meta_h.swap(meta);  // (the async copy's source: kept with the batch)
+    // (async on the engine stream: see pack_heads; the batch's first launch is ordered after it --
+    // pk_ev[3], or the wait below when the launch itself prepared the batch)
+    if ((e = hipMemcpyAsync(db->vt_meta.p, db->vt_meta_h.data(), db->vt_meta_h.size() * 4, hipMemcpyHostToDevice,
+                            stream)) != hipSuccess)
         return hipfail(e, "upload vt meta");
     db->vt_t_words = tbase;
     if ((e = db->vt_t.alloc(2 * tbase * 4)) != hipSuccess) return hipfail(e, "vt class words");
     if (P.n_vtfills && (e = db->vtf_slow.alloc(MXP_VTF_MARKS(db->n, P.n_vtfills))) != hipSuccess)
         return hipfail(e, "vt fill marks");
-    db->vt_meta_h.swap(meta);
+    // (zeroed: the fast fill marks only the tiles it ran, so a slow-kernel block never reads a stale
+    // mark of a recycled block and stages for nothing -- ADVICE r5)
+    if (P.n_vtfills && (e = hipMemsetAsync(db->vtf_slow.p, 0, MXP_VTF_MARKS(db->n, P.n_vtfills), stream)) != hipSuccess)
+        return hipfail(e, "vt fill marks");
+    vt_fresh = true;
     return MXP_OK;
 }
 
@@ -1759,7 +1780,18 @@ int mxp_engine::launch_body(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, ui
     Plan* P = nullptr;
     int rc = get_plan(mask, &P);
     if (rc) return rc;
+    vt_fresh = false;
     if (mask && (rc = vt_prepare(db, *P))) return rc;
+    if (vt_fresh && s != stream) {  // (this launch prepared the batch's tables on the engine stream)
+        hipEvent_t ev = nullptr;
+        hipError_t e2;
+        if ((e2 = hipEventCreateWithFlags(&ev, kOrderEvent)) != hipSuccess || (e2 = hipEventRecord(ev, stream)) != hipSuccess ||
+            (e2 = hipStreamWaitEvent(s, ev, 0)) != hipSuccess) {
+            if (ev) (void)hipEventDestroy(ev);
+            return hipfail(e2, "vt prepare wait");
+        }
+        (void)hipEventDestroy(ev);
+    }
     mxp_kargs A;
     fill_args(&A, db, *P);
     // NFAs wider than the private-memory walk: the global thread-set scratch (dfa_dev.h)

@@ -890,6 +890,7 @@ struct mxp_engine : public mxp::LowerTables {
     hipStream_t stats_stream = nullptr;  // stream of the last stats_ev record (a wait only across streams)
     int pack_on_host(const mxp_bag_batch* b, mxp_dbatch* db);
     int pack_device(const mxp_bag_batch* b, mxp_dbatch* db);
+    int pack_device_body(const mxp_bag_batch* b, mxp_dbatch* db);
     int pack_vt_tables(mxp_dbatch* db);  // the value-class tables of the active slots
     bool host_pack = false;
     const mxp_bag_batch2* narrow_src = nullptr;  // the narrow batch pack_device copies (mxp_batch_upload2)
@@ -904,6 +905,7 @@ struct mxp_engine : public mxp::LowerTables {
     // value-class sizing from the packer's distinct counts, the class tables, heads, dictionary
     int finish_pack(mxp_dbatch* db);
     bool finish_fail_done = false;  // (test hook of finish_pack, MXP_DEBUG_FLAGS 1 << 29)
+    void release_pack_scratch(mxp_dbatch* db);  // the packer's scratch no later call reads, to the bin
     uint32_t vcol_key_id(uint32_t j) const {
         auto it = gstr_ids.find(vcols[j].second);
         return it == gstr_ids.end() ? 0xFFFFFFFEu : it->second;
@@ -911,6 +913,7 @@ struct mxp_engine : public mxp::LowerTables {
     int wire_decode(const mxp_wire_batch* w, const char* const* names, uint32_t n_names, mxp_wire** out);  // wire.cpp
     void fill_args(mxp_kargs* A, const mxp_dbatch* db, const Plan& P) const;
     int vt_prepare(mxp_dbatch* db, const Plan& P);
+    bool vt_fresh = false;  // the last vt_prepare uploaded a batch's tables (on the engine stream)
     uint32_t last_mask = 0;  // value-class slots of the last launch
     uint8_t* req_err_out = nullptr;  // compact error output of the next launch (kargs.req_err)
     const uint32_t* hits_gate_out = nullptr;  // fused-counter gate of the next launch (kargs.hits_gate)

@@ -180,12 +180,15 @@ struct mxp_group {
         uint32_t eval_n = 0;
         bool eval_bitmap = false, evaluated = false;
         hipStream_t qs = nullptr;      // memquota stream (beside the evaluation)
+        // the member's evaluation stream: non-blocking, so the engine's synchronous copies on the
+        // legacy stream (a batch upload's, a pack's) never wait for a queued evaluation
+        hipStream_t es = nullptr;
         hipEvent_t fork = nullptr, join = nullptr;
         bool q_pending = false;        // a quota replay on qs the main stream has not joined yet
         PinnedVec<int64_t> host_ctr;   // host reduction
         int rc = 0;
         std::string err_text;
-        hipStream_t stream() const { return eng->stream; }
+        hipStream_t stream() const { return es ? es : eng->stream; }
     };
     Fixed<Member> m;
     std::unique_ptr<Crew> crew;
@@ -419,8 +422,10 @@ int mxp_group_create(const int* devices, uint32_t n, uint32_t flags, mxp_group**
         auto& x = g->m[k];
         hipError_t e;
         if ((e = hipSetDevice(x.device)) != hipSuccess || (e = hipEventCreateWithFlags(&x.fork, kOrderEvent)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&x.join, kOrderEvent)) != hipSuccess) {
-            g_create_error = std::string("mxp_group_create: events: ") + hipGetErrorString(e);
+            (e = hipEventCreateWithFlags(&x.join, kOrderEvent)) != hipSuccess ||
+            (e = hipStreamCreateWithFlags(&x.es, hipStreamNonBlocking)) != hipSuccess) {
+            if (e != hipSuccess) x.es = nullptr;
+            g_create_error = std::string("mxp_group_create: events / stream: ") + hipGetErrorString(e);
             mxp_group_destroy(g.release());
             return MXP_ERR_DEVICE;
         }
@@ -441,6 +446,7 @@ void mxp_group_destroy(mxp_group* g) {
         if (!x.eng) continue;
         (void)hipSetDevice(x.device);
         if (x.q_pending) (void)hipEventSynchronize(x.join);
+        (void)hipStreamSynchronize(x.stream());
         (void)hipStreamSynchronize(x.eng->stream);
     }
     if (g->reduce == MXP_REDUCE_RCCL) {
@@ -458,6 +464,7 @@ void mxp_group_destroy(mxp_group* g) {
         x.err.reset();
         x.req_err.reset();
         if (x.qs) (void)hipStreamDestroy(x.qs);
+        if (x.es) (void)hipStreamDestroy(x.es);
         if (x.fork) (void)hipEventDestroy(x.fork);
         if (x.join) (void)hipEventDestroy(x.join);
         mxp_engine_destroy(x.eng);
@@ -475,7 +482,7 @@ mxp_engine* mxp_group_engine(mxp_group* g, uint32_t member) {
 }
 
 void* mxp_group_stream(mxp_group* g, uint32_t member) {
-    return g && member < g->size() ? (void*)g->m[member].eng->stream : nullptr;
+    return g && member < g->size() ? (void*)g->m[member].stream() : nullptr;
 }
 
 int mxp_group_locate(const mxp_group* g, uint64_t request, uint32_t* member, uint32_t* local) {
@@ -637,10 +644,10 @@ int mxp_group_eval(mxp_group* g, mxp_gbatch* gb, uint32_t flags) {
         unsigned long long* hits = (unsigned long long*)x.step.p;
         if (bitmap) {
             if ((e = x.err.reserve(W * n * 4)) != hipSuccess) return x.eng->hipfail(e, "alloc error bitmap");
-            return mxp_batch_eval_device_hits(x.eng, gb->db[k], nullptr, x.match.as<uint32_t>(), x.err.as<uint32_t>(), hits);
+            return mxp_batch_eval_device_hits(x.eng, gb->db[k], x.stream(), x.match.as<uint32_t>(), x.err.as<uint32_t>(), hits);
         }
         if ((e = x.req_err.reserve(n)) != hipSuccess) return x.eng->hipfail(e, "alloc request errors");
-        return mxp_batch_eval_device_compact(x.eng, gb->db[k], nullptr, x.match.as<uint32_t>(), x.req_err.as<uint8_t>(),
+        return mxp_batch_eval_device_compact(x.eng, gb->db[k], x.stream(), x.match.as<uint32_t>(), x.req_err.as<uint8_t>(),
                                              hits);
     });
 }
@@ -1104,7 +1111,7 @@ int mxp_group_list_check_device(mxp_group* g, const mxp_glist* l, int blacklist,
     g->set_bounds(cnt);
     return g->each([&](uint32_t k) {
         return mxp_list_check_device(g->m[k].eng, l->l[k], blacklist, d_sym_bytes[k], d_sym_offsets[k], n[k],
-                                     g->m[k].eng->stream, d_codes[k]);
+                                     g->m[k].stream(), d_codes[k]);
     });
 }
 

@@ -434,17 +434,16 @@ extern "C" __global__ __launch_bounds__(1024) void mxp_list_rx_nfa_kernel(mxp_li
 // tail automaton stepped from there over the rest of the symbol (one LDS byte per class, one per
 // transition).  So a lookup pays ~3 dependent global loads (symbol, slot, block) where the union DFA
 // paid one per byte.  Patterns not dispatched stay in the union parts, walked after (from global).
-template <bool kNfa>
+template <bool kNfa, bool kLds>
 __device__ __forceinline__ void list_rxp_body(const mxp_list_args& A) {
-    __shared__ uint32_t LEAD[MXP_RXP_LEAD];
-    // one block per lane, rows of MXP_RXP_ROW words (odd: the lanes' words fall in different banks)
-    __shared__ uint32_t SLOT[MXP_RXP_THREADS * MXP_RXP_ROW];
+    // kLds: the candidate's block copied into the lane's LDS row (MXP_RXP_ROW words; odd: the lanes'
+    // words fall in different banks) and stepped there; else stepped from global memory, where the
+    // tail blocks (a few MB) stay L2-resident and the kernel keeps its waves (no LDS)
+    __shared__ uint32_t SLOT[kLds ? MXP_RXP_THREADS * MXP_RXP_ROW : 1];
+    const uint32_t nthr = kLds ? MXP_RXP_THREADS : 256u;
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < MXP_RXP_LEAD; i += MXP_RXP_THREADS) LEAD[i] = A.rxp_lead[i];
-    __syncthreads();
-    uint32_t* const row = SLOT + tid * MXP_RXP_ROW;
-    const uint8_t* const mine = (const uint8_t*)row;
-    for (uint32_t q = blockIdx.x * MXP_RXP_THREADS + tid; q < A.n; q += gridDim.x * MXP_RXP_THREADS) {
+    uint32_t* const row = SLOT + (kLds ? tid * MXP_RXP_ROW : 0u);
+    for (uint32_t q = blockIdx.x * nthr + tid; q < A.n; q += gridDim.x * nthr) {
         const uint8_t* s;
         uint32_t n;
         if (!list_symbol(A, q, &s, &n)) continue;
@@ -455,7 +454,7 @@ __device__ __forceinline__ void list_rxp_body(const mxp_list_args& A) {
         uint32_t lens = A.rxp_short;
         if (n >= 3u) {
             const uint32_t b = (uint32_t)w[0];
-            lens |= LEAD[mxp_rxp_lead(b & 0xFFu, (b >> 8) & 0xFFu, (b >> 16) & 0xFFu)];
+            lens |= A.rxp_lead[mxp_rxp_lead(b & 0xFFu, (b >> 8) & 0xFFu, (b >> 16) & 0xFFu)];
         }
         if (n < 32u) lens &= (1u << n) - 1u;  // (prefixes no longer than the symbol)
         bool found = false;
@@ -491,19 +490,30 @@ __device__ __forceinline__ void list_rxp_body(const mxp_list_args& A) {
                     found = true;
                     break;
                 }
-                for (uint32_t k = 2; k < nq; k++) {  // class nibbles and transitions into the lane's row
-                    const uint4 v = blk[k];
-                    row[4u * k] = v.x;
-                    row[4u * k + 1u] = v.y;
-                    row[4u * k + 2u] = v.z;
-                    row[4u * k + 3u] = v.w;
+                const uint8_t* B = (const uint8_t*)blk;
+                if constexpr (kLds) {
+                    // class nibbles and transitions into the lane's row: every load issued before the
+                    // first store (one round trip, not one per 16 bytes)
+                    uint4 v[MXP_RXP_BLOCK / 16u - 2u];
+#pragma unroll
+                    for (uint32_t k = 2; k < MXP_RXP_BLOCK / 16u; k++)
+                        if (k < nq) v[k - 2u] = blk[k];
+#pragma unroll
+                    for (uint32_t k = 2; k < MXP_RXP_BLOCK / 16u; k++)
+                        if (k < nq) {
+                            row[4u * k] = v[k - 2u].x;
+                            row[4u * k + 1u] = v[k - 2u].y;
+                            row[4u * k + 2u] = v[k - 2u].z;
+                            row[4u * k + 3u] = v[k - 2u].w;
+                        }
+                    B = (const uint8_t*)row;
                 }
-                const uint8_t* T = mine + MXP_RXP_TRANS;
+                const uint8_t* T = B + MXP_RXP_TRANS;
                 uint32_t st = 0;
                 for (uint32_t i = L; i < n && st < S; i++) {
                     const uint64_t wi = i < 8u ? w[0] : i < 16u ? w[1] : i < 24u ? w[2] : w[3];
                     const uint32_t b = i < 32u ? (uint32_t)(wi >> ((i & 7u) * 8u)) & 0xFFu : s[i];
-                    const uint32_t cls = b >= 0x80u ? C - 2u : (mine[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
+                    const uint32_t cls = b >= 0x80u ? C - 2u : (B[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
                     st = T[st * C + cls];
                 }
                 if (st < S) st = T[st * C + C - 1u];  // END of text
@@ -514,20 +524,28 @@ __device__ __forceinline__ void list_rxp_body(const mxp_list_args& A) {
         list_decide(A, q, found);
     }
 }
-extern "C" __global__ __launch_bounds__(MXP_RXP_THREADS) void mxp_list_rxp_kernel(mxp_list_args A) {
-    list_rxp_body<false>(A);
+extern "C" __global__ __launch_bounds__(MXP_RXP_THREADS) void mxp_list_rxp_lds_kernel(mxp_list_args A) {
+    list_rxp_body<false, true>(A);
 }
-extern "C" __global__ __launch_bounds__(MXP_RXP_THREADS) void mxp_list_rxp_nfa_kernel(mxp_list_args A) {
-    list_rxp_body<true>(A);
+extern "C" __global__ __launch_bounds__(256) void mxp_list_rxp_kernel(mxp_list_args A) {
+    list_rxp_body<false, false>(A);
+}
+extern "C" __global__ __launch_bounds__(256) void mxp_list_rxp_nfa_kernel(mxp_list_args A) {
+    list_rxp_body<true, false>(A);
 }
 
 extern "C" hipError_t mxp_launch_list(const mxp_list_args* a, hipStream_t s) {
     if (a->type == MXP_LIST_REGEX && a->rxp_mask) {
-        // persistent: four 128-thread workgroups per CU (their LDS: 4 x 39 KB of the 160 KB)
-        const uint32_t need = (a->n + MXP_RXP_THREADS - 1u) / MXP_RXP_THREADS;
-        const uint32_t grid = need < 1024u ? need : 1024u;
-        hipLaunchKernelGGL(a->rx_nfa ? mxp_list_rxp_nfa_kernel : mxp_list_rxp_kernel, dim3(grid), dim3(MXP_RXP_THREADS),
-                           0, s, *a);
+        if ((a->opt & MXP_LIST_OPT_RXP_LDS) && !a->rx_nfa) {
+            // persistent: five 128-thread workgroups per CU (their LDS: 5 x 31 KB of the 160 KB)
+            const uint32_t need = (a->n + MXP_RXP_THREADS - 1u) / MXP_RXP_THREADS;
+            const uint32_t grid = need < 1280u ? need : 1280u;
+            hipLaunchKernelGGL(mxp_list_rxp_lds_kernel, dim3(grid), dim3(MXP_RXP_THREADS), 0, s, *a);
+            return hipGetLastError();
+        }
+        const uint32_t need = (a->n + 255u) / 256u;
+        const uint32_t grid = need < 2048u ? need : 2048u;
+        hipLaunchKernelGGL(a->rx_nfa ? mxp_list_rxp_nfa_kernel : mxp_list_rxp_kernel, dim3(grid), dim3(256), 0, s, *a);
         return hipGetLastError();
     }
     if (a->type == MXP_LIST_REGEX && a->lds_nparts) {

@@ -87,7 +87,20 @@ int mxp_engine::ensure_dev_pools() {
     return MXP_OK;
 }
 
+// Any failure after the first copy was queued waits for the copy streams before returning: the
+// caller's arrays may still be read by DMA and the packer's kernels may still use the batch's blocks,
+// and a failed upload hands no batch back to wait on.  A failed MXP_UPLOAD_NO_WAIT upload
+// has finished reading the caller's arrays when it returns.
 int mxp_engine::pack_device(const mxp_bag_batch* b, mxp_dbatch* db) {
+    const int rc = pack_device_body(b, db);
+    if (rc) {
+        for (int k : {0, 2})
+            if (copy_s[k]) (void)hipStreamSynchronize(copy_s[k]);
+    }
+    return rc;
+}
+
+int mxp_engine::pack_device_body(const mxp_bag_batch* b, mxp_dbatch* db) {
     const uint32_t n = b->n_requests;
     const uint32_t C = (uint32_t)cols.size(), V = (uint32_t)vcols.size();
     const uint32_t ncol = C + V;
@@ -587,5 +600,45 @@ int mxp_engine::finish_pack(mxp_dbatch* db) {
     }
     if ((e = hipEventRecord(db->pk_ev[3], stream)) != hipSuccess) return hipfail(e, "pack event");
     db->pack_pending = false;
+    release_pack_scratch(db);
     return MXP_OK;
+}
+
+// The packer's scratch that no later call reads goes to the bin once finish_pack's kernels are done
+// (an event on the engine stream; the packer stream's kernels finished before finish_pack began):
+// everything in db->pk but the batch's string table and the resolver's raw identity / protocol
+// columns (the Resolve's device namespaces, mxp_ns_kernel).  A batch kept for double buffering then
+// holds its packed image, not the packer's inputs and tables.
+void mxp_engine::release_pack_scratch(mxp_dbatch* db) {
+    BlockBin::Group g;
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, kOrderEvent) != hipSuccess || hipEventRecord(ev, stream) != hipSuccess) {
+        if (ev) (void)hipEventDestroy(ev);
+        (void)hipGetLastError();
+        return;  // (keep the scratch: freed with the batch)
+    }
+    g.evs.push_back(ev);
+    PackScratch& P = db->pk;
+    const void* keep[4] = {db->res_id_kind, db->res_id_val, db->res_pr_kind, db->res_pr_val};
+    auto give = [&](DevBuf& d) {
+        for (const void* k : keep)
+            if (k && k == d.p) return;
+        d.reset();
+    };
+    g_bin_give = &g.blks;
+    for (DevBuf* d : {&P.pk_tsec, &P.pk_tnsec, &P.pk_moff, &P.pk_mkey, &P.pk_mval, &P.pk_sid, &P.pk_braw, &P.pk_bcan,
+                      &P.pk_tid, &P.pk_use, &P.pk_scan, &P.pk_scan_blocks, &P.pk_scan_max, &P.pk_vtd_lkey, &P.pk_vtd_lcr,
+                      &P.pk_vtd_ln, &P.pk_vtd_tkey, &P.pk_vtd_tcr, &P.pk_vtd_meta, &P.pk_rx, &P.pk_rxv, &P.pk_soff32,
+                      &P.pk_moff32})
+        give(*d);
+    for (auto& d : P.pk_tab) give(d);
+    for (auto& d : P.pk_ck) give(d);
+    for (auto& d : P.pk_cv) give(d);
+    for (auto& d : P.pk_cv32) give(d);
+    g_bin_give = nullptr;
+    if (g.blks.empty()) {
+        (void)hipEventDestroy(ev);
+        return;
+    }
+    bin.put(std::move(g));
 }

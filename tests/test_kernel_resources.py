@@ -34,8 +34,10 @@ MAX_SCRATCH = {"mxp_index_kernel": 56, "mxp_index_dtp_kernel": 24, "mxp_index5_k
 MAX_SCRATCH.update({k: 384 for k in ("mxp_eval_nfa_kernel", "mxp_eval_deep_nfa_kernel", "mxp_index_nfa_kernel",
                                      "mxp_vt_eval_nfa_kernel", "mxp_list_nfa_kernel", "mxp_list_rx_nfa_kernel",
                                      "mxp_eval_refs_kernel", "mxp_eval_deep_refs_kernel", "mxp_index_refs_kernel")})
-# (the list NFA kernels keep a second walk state for the pattern loop: 576 B measured in round 5)
-MAX_SCRATCH.update({k: 576 for k in ("mxp_list_nfa_kernel", "mxp_list_rx_nfa_kernel")})
+# (the list NFA kernels keep a second walk state for the pattern loop: 576 B measured in round 5;
+# r6: +32 B -- their argument block, copied to private memory since the walk takes its address, grew
+# by the regex prefix-dispatch tables)
+MAX_SCRATCH.update({k: 608 for k in ("mxp_list_nfa_kernel", "mxp_list_rx_nfa_kernel", "mxp_list_rxp_nfa_kernel")})
 
 
 def resource_usage(src):
