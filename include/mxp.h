@@ -254,6 +254,9 @@ uint64_t mxp_list_entries(const mxp_list* list);
  * whose own DFA is over budget); out[0] = parts, out[1] = of which NFAs.  (Engine introspection; no
  * reference counterpart.) */
 void mxp_list_regex_parts(const mxp_list* list, uint32_t out[2]);
+/* REGEX lists: out[0] = patterns dispatched by their literal prefix (tail automata, no union part),
+ * out[1] = distinct prefixes.  (Engine introspection; no reference counterpart.) */
+void mxp_list_regex_dispatch(const mxp_list* list, uint32_t out[2]);
 int mxp_list_check(mxp_engine* eng, const mxp_list* list, int blacklist, const uint8_t* sym_bytes,
                    const uint64_t* sym_offsets, uint32_t n, int32_t* codes);
 /* strings.ToUpper (Go 1.9: strings.Map(unicode.ToUpper, s), Unicode 9.0.0 simple uppercase) as the

@@ -2484,6 +2484,33 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
     return batch_upload(eng, batch, out, nullptr);
 }
 
+void WideView::materialize() {
+    if (full) return;
+    full = true;
+    const mxp_bag_batch& B = src.base;
+    auto widen = [](const uint32_t* in, uint64_t m) {
+        std::unique_ptr<uint64_t[]> o(new uint64_t[m ? m : 1]);
+        uint64_t* p = o.get();
+        mxp::par_for(m, 1u << 16, [&](uint64_t a, uint64_t z, unsigned) {
+            for (uint64_t i = a; i < z; i++) p[i] = in[i];
+        });
+        return o;
+    };
+    for (uint32_t c = 0; c < B.n_columns; c++)
+        if (src.narrow[c] && src.values32 && src.values32[c]) {
+            vals[c] = widen(src.values32[c], B.n_requests);
+            vptr[c] = vals[c].get();
+        }
+    if (B.n_strings) {
+        soff = widen(src.str_offsets32, (uint64_t)B.n_strings + 1);
+        view.str_offsets = soff.get();
+    }
+    if (B.n_maps) {
+        moff = widen(src.map_offsets32, (uint64_t)B.n_maps + 1);
+        view.map_offsets = moff.get();
+    }
+}
+
 int mxp_batch_upload2(mxp_engine* eng, const mxp_bag_batch2* b2, uint32_t flags, mxp_dbatch** out) {
     if (!eng || !b2 || !out || (flags & ~(uint32_t)MXP_UPLOAD_NO_WAIT)) return MXP_ERR_ARG;
     const mxp_bag_batch& B = b2->base;
@@ -2497,39 +2524,17 @@ int mxp_batch_upload2(mxp_engine* eng, const mxp_bag_batch2* b2, uint32_t flags,
         if (n && nar && (!b2->values32 || !b2->values32[c])) return bad("values32 of a narrow column is NULL");
         if (n && !nar && (!B.values || !B.values[c])) return bad("values of a wide column is NULL");
     }
-    // the host view: narrow columns and offsets widened (the host passes read the v1 layout); the
-    // copies read the narrow arrays (pack_device)
+    // the host view (WideView): the wide columns as given; the narrow ones and the offsets made on
+    // demand (the copies and the batch checks read the narrow arrays)
     std::unique_ptr<WideView> W(new WideView());
     W->view = B;
+    W->src = *b2;
     W->vptr.assign(B.n_columns, nullptr);
     W->vals.resize(B.n_columns);
-    auto widen = [](const uint32_t* in, uint64_t m) {
-        std::unique_ptr<uint64_t[]> o(new uint64_t[m ? m : 1]);
-        uint64_t* p = o.get();
-        mxp::par_for(m, 1u << 16, [&](uint64_t a, uint64_t z, unsigned) {
-            for (uint64_t i = a; i < z; i++) p[i] = in[i];
-        });
-        return o;
-    };
-    for (uint32_t c = 0; c < B.n_columns; c++) {
-        if (b2->narrow[c]) {
-            W->vals[c] = widen(b2->values32[c], n);
-            W->vptr[c] = W->vals[c].get();
-        } else {
-            W->vptr[c] = B.values ? B.values[c] : nullptr;
-        }
-    }
+    for (uint32_t c = 0; c < B.n_columns; c++) W->vptr[c] = b2->narrow[c] ? nullptr : B.values ? B.values[c] : nullptr;
     W->view.values = B.n_columns ? W->vptr.data() : B.values;
     W->view.str_offsets = nullptr;
     W->view.map_offsets = nullptr;
-    if (B.n_strings) {
-        W->soff = widen(b2->str_offsets32, (uint64_t)B.n_strings + 1);
-        W->view.str_offsets = W->soff.get();
-    }
-    if (B.n_maps) {
-        W->moff = widen(b2->map_offsets32, (uint64_t)B.n_maps + 1);
-        W->view.map_offsets = W->moff.get();
-    }
     const mxp_bag_batch* view = &W->view;
     eng->upload_no_wait = (flags & MXP_UPLOAD_NO_WAIT) != 0;
     eng->narrow_src = b2;
@@ -2693,9 +2698,16 @@ int mxp_engine::check_batch(const mxp_bag_batch* b, int parts) {
     const uint64_t n = b->n_requests, NS = b->n_strings, NT = b->n_times, NM = b->n_maps;
     auto bad = [&](const std::string& what) { return fail(MXP_ERR_ARG, "malformed batch: " + what); };
     if (b->n_columns && !b->column_names) return bad("column_names is NULL");
-    if (NS && !b->str_offsets) return bad("str_offsets is NULL");
+    // (a narrow upload, mxp_batch_upload2: its u32 columns and offsets where the view has none)
+    const mxp_bag_batch2* nb = narrow_src;
+    const uint32_t* so32 = nb && !b->str_offsets ? nb->str_offsets32 : nullptr;
+    const uint32_t* mo32 = nb && !b->map_offsets ? nb->map_offsets32 : nullptr;
+    auto v32_of = [&](uint32_t c) -> const uint32_t* {
+        return nb && nb->narrow[c] && nb->values32 ? nb->values32[c] : nullptr;
+    };
+    if (NS && !b->str_offsets && !so32) return bad("str_offsets is NULL");
     if (NT && (!b->time_sec || !b->time_nsec)) return bad("time_sec / time_nsec is NULL");
-    if (NM && !b->map_offsets) return bad("map_offsets is NULL");
+    if (NM && !b->map_offsets && !mo32) return bad("map_offsets is NULL");
     // the columns read (by name; the first column of a name is the one read)
     std::vector<std::string> names = read_attributes();
     std::set<std::string> want(names.begin(), names.end());
@@ -2706,7 +2718,7 @@ int mxp_engine::check_batch(const mxp_bag_batch* b, int parts) {
         if (!b->column_names[c]) return bad("column " + std::to_string(c) + " has no name");
         const std::string nm(b->column_names[c]);
         if (!want.count(nm) || !seen.insert(nm).second) continue;
-        if (n && (!b->kinds || !b->values || !b->kinds[c] || !b->values[c]))
+        if (n && (!b->kinds || !b->kinds[c] || (!v32_of(c) && (!b->values || !b->values[c]))))
             return bad("column '" + nm + "' has no kinds / values");
         use.push_back(c);
     }
@@ -2728,16 +2740,21 @@ int mxp_engine::check_batch(const mxp_bag_batch* b, int parts) {
     };
     // string offsets: non-decreasing, every string < 16 MiB (the pools' descriptor limit)
     if (NS && (parts & kCheckStrings)) {
-        mxp::par_for(NS, 1u << 16, [&](uint64_t i0, uint64_t i1, unsigned w) {
-            const uint64_t* o = b->str_offsets;
-            for (uint64_t i = i0; i < i1; i++) {
-                if (o[i + 1] < o[i]) return note(w, i, "str_offsets[" + std::to_string(i + 1) + "] < str_offsets[" +
-                                                           std::to_string(i) + "]");
-                if (o[i + 1] - o[i] >= (1u << 24)) return note(w, i, "string " + std::to_string(i) + " is 16 MiB or longer");
-            }
-        });
+        auto offs = [&](const auto* o) {
+            mxp::par_for(NS, 1u << 16, [&](uint64_t i0, uint64_t i1, unsigned w) {
+                for (uint64_t i = i0; i < i1; i++) {
+                    if (o[i + 1] < o[i]) return note(w, i, "str_offsets[" + std::to_string(i + 1) + "] < str_offsets[" +
+                                                               std::to_string(i) + "]");
+                    if (o[i + 1] - o[i] >= (1u << 24)) return note(w, i, "string " + std::to_string(i) + " is 16 MiB or longer");
+                }
+            });
+        };
+        if (so32)
+            offs(so32);
+        else
+            offs(b->str_offsets);
         if (const Bad* f = first()) return bad(f->what);
-        if (b->str_offsets[NS] && !b->str_bytes) return bad("str_bytes is NULL");
+        if ((so32 ? (uint64_t)so32[NS] : b->str_offsets[NS]) && !b->str_bytes) return bad("str_bytes is NULL");
     }
     // columns: every used column over each slice of requests in one parallel pass, branch-free
     // (a kind's id limit from a table: ~0 for kinds without an id, 0 for kinds past MXP_OTHER); a
@@ -2754,26 +2771,34 @@ int mxp_engine::check_batch(const mxp_bag_batch* b, int parts) {
             bool maps = false;
             for (uint32_t c : use) {
                 const uint8_t* k = b->kinds[c];
-                const uint64_t* v = b->values[c];
+                const uint32_t* v32 = v32_of(c);
+                const uint64_t* v64 = v32 ? nullptr : b->values[c];
                 bool fail_any = false;
                 uint32_t nmap = 0;
-                for (uint64_t q = q0; q < q1; q++) {
-                    const uint64_t lim = lim_of[k[q]];
-                    fail_any |= (v[q] >= lim) & (lim != ~0ull);
-                    nmap += k[q] == MXP_STRING_MAP;
-                }
+                auto scan = [&](const auto* v) {
+                    for (uint64_t q = q0; q < q1; q++) {
+                        const uint64_t lim = lim_of[k[q]];
+                        fail_any |= ((uint64_t)v[q] >= lim) & (lim != ~0ull);
+                        nmap += k[q] == MXP_STRING_MAP;
+                    }
+                };
+                if (v32)
+                    scan(v32);
+                else
+                    scan(v64);
                 maps |= nmap != 0;
                 if (!fail_any) continue;
                 const std::string nm(b->column_names[c]);
+                auto v = [&](uint64_t q) -> uint64_t { return v32 ? v32[q] : v64[q]; };
                 for (uint64_t q = q0; q < q1; q++) {
                     const uint8_t kd = k[q];
                     if (kd > MXP_OTHER)
                         return note(w, q, "column '" + nm + "' request " + std::to_string(q) + ": kind " +
                                               std::to_string(kd) + " > MXP_OTHER");
-                    if (lim_of[kd] != ~0ull && v[q] >= lim_of[kd]) {
+                    if (lim_of[kd] != ~0ull && v(q) >= lim_of[kd]) {
                         const char* table = kd == MXP_TIMESTAMP ? "n_times" : kd == MXP_STRING_MAP ? "n_maps" : "n_strings";
                         return note(w, q, "column '" + nm + "' request " + std::to_string(q) + ": id " +
-                                              std::to_string(v[q]) + " >= " + table + " (" + std::to_string(lim_of[kd]) + ")");
+                                              std::to_string(v(q)) + " >= " + table + " (" + std::to_string(lim_of[kd]) + ")");
                     }
                 }
             }
@@ -2782,16 +2807,22 @@ int mxp_engine::check_batch(const mxp_bag_batch* b, int parts) {
     if (const Bad* f = first()) return bad(f->what);
     // map CSR: offsets non-decreasing, key / value ids < n_strings (read when a map is)
     if (NM && (map_col.load() || need_maps || !vcols.empty())) {
-        const uint64_t* mo = b->map_offsets;
-        mxp::par_for(NM, 1u << 16, [&](uint64_t m0, uint64_t m1, unsigned w) {
-            for (uint64_t m = m0; m < m1; m++)
-                if (mo[m + 1] < mo[m])
-                    return note(w, m, "map_offsets[" + std::to_string(m + 1) + "] < map_offsets[" + std::to_string(m) + "]");
-        });
+        auto moffs = [&](const auto* mo) {
+            mxp::par_for(NM, 1u << 16, [&](uint64_t m0, uint64_t m1, unsigned w) {
+                for (uint64_t m = m0; m < m1; m++)
+                    if (mo[m + 1] < mo[m])
+                        return note(w, m, "map_offsets[" + std::to_string(m + 1) + "] < map_offsets[" + std::to_string(m) + "]");
+            });
+        };
+        if (mo32)
+            moffs(mo32);
+        else
+            moffs(b->map_offsets);
         if (const Bad* f = first()) return bad(f->what);
-        const uint64_t E = mo[NM] - mo[0];
+        auto mo = [&](uint64_t m) -> uint64_t { return mo32 ? mo32[m] : b->map_offsets[m]; };
+        const uint64_t E = mo(NM) - mo(0);
         if (E && (!b->map_keys || !b->map_values)) return bad("map_keys / map_values is NULL");
-        const uint64_t e0 = mo[0];
+        const uint64_t e0 = mo(0);
         mxp::par_for(E, 1u << 16, [&](uint64_t x0, uint64_t x1, unsigned w) {
             for (uint64_t x = e0 + x0; x < e0 + x1; x++) {
                 if (b->map_keys[x] >= NS)

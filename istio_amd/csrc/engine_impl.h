@@ -281,14 +281,19 @@ struct PackScratch {
     DevBuf pk_cv32[66], pk_soff32, pk_moff32;  // narrow batches: the u32 arrays as copied (mxp_batch_upload2)
 };
 
-// A narrow batch's host view (mxp_batch_upload2): the host passes (batch checks, run-time pattern
-// collection, error texts, the Resolve's host paths) read the v1 layout, so its u32 values and
-// offsets are widened on the host once, kept with the device batch; the copies read the narrow arrays.
+// A narrow batch's host view (mxp_batch_upload2).  The upload's own host passes read the narrow
+// arrays (check_batch, the packer's sizes); the v1 layout -- u32 values and offsets widened -- is made
+// only for a host pass that reads it (run-time pattern collection, the host packer, the Resolve's
+// host namespaces): materialize(), from the caller's arrays, which are valid while the call that
+// asks runs.  Until then the view's narrow columns and its offsets are NULL.
 struct WideView {
     mxp_bag_batch view;
+    mxp_bag_batch2 src;  // (shallow: the caller's arrays)
     std::vector<const uint64_t*> vptr;
     std::vector<std::unique_ptr<uint64_t[]>> vals;  // (uninitialised: the widening writes every word)
     std::unique_ptr<uint64_t[]> soff, moff;
+    bool full = false;
+    void materialize();  // engine.cpp
 };
 
 struct mxp_dbatch {
@@ -866,6 +871,7 @@ struct mxp_engine : public mxp::LowerTables {
     int pack(const mxp_bag_batch* b, mxp_dbatch* db) {
         db->res_raw = false;
         const bool dev = !host_pack && cols.size() + vcols.size() <= MXP_PACK_MAXCOL;
+        if (!dev && db->wide) db->wide->materialize();  // (the host packer reads the v1 layout)
         if (!dev)
             if (int rc0 = check_batch(b)) return rc0;
         // the device packer returns once the caller's arrays are copied; its kernels run on, and the

@@ -245,8 +245,14 @@ struct mxp_group {
                 if ((e = hipMemsetAsync(x.total.p, 0, bytes, x.stream())) != hipSuccess) return x.eng->hipfail(e, "zero counters");
             }
             if ((e = hipStreamSynchronize(x.stream())) != hipSuccess) return x.eng->hipfail(e, "sync");
-            return MXP_OK;
+            return fork_point(x);
         });
+    }
+    // where the next memquota replay forks from the main stream (after the counters were last read)
+    int fork_point(Member& x) {
+        if (!x.fork) return MXP_OK;  // (mxp_group_create: the events come next)
+        const hipError_t e = hipEventRecord(x.fork, x.stream());
+        return e == hipSuccess ? MXP_OK : x.eng->hipfail(e, "quota fork point");
     }
     long long* totals(Member& x) const {
         return (long long*)(reduce == MXP_REDUCE_NONE ? x.step.p : x.total.p);
@@ -679,7 +685,9 @@ int mxp_group_reduce(mxp_group* g) {
     DeviceGuard guard;
     const uint32_t N = std::max<uint32_t>(1, g->R + g->K);
     int rc = g->each([&](uint32_t k) { return g->join_quota(g->m[k]); });
-    if (rc || g->reduce == MXP_REDUCE_NONE) return rc;  // (one member: the counters are the totals)
+    if (rc) return rc;
+    if (g->reduce == MXP_REDUCE_NONE)  // (one member: the counters are the totals)
+        return g->each([&](uint32_t k) { return g->fork_point(g->m[k]); });
     if (g->reduce == MXP_REDUCE_RCCL) {
         std::lock_guard<std::mutex> lk(g_rccl_mu);
         Rccl& R = rccl();
@@ -718,7 +726,7 @@ int mxp_group_reduce(mxp_group* g) {
     return g->each([&](uint32_t k) -> int {
         auto& x = g->m[k];
         hipError_t e = mxp_launch_group_fold(x.total.as<long long>(), x.step.as<long long>(), N, x.stream());
-        return e == hipSuccess ? MXP_OK : x.eng->hipfail(e, "launch counter fold");
+        return e == hipSuccess ? g->fork_point(x) : x.eng->hipfail(e, "launch counter fold");
     });
 }
 
@@ -860,10 +868,10 @@ int mxp_group_quota_eval(mxp_group* g, mxp_gquota* q, mxp_gqbatch* qb, int64_t n
                 return x.eng->hipfail(e, "quota stream");
             }
         }
-        // forked after the work already on the main stream (the counter fold that zeroed the step),
-        // joined by the next reduce / sync
-        if ((e = hipEventRecord(x.fork, x.stream())) != hipSuccess || (e = hipStreamWaitEvent(x.qs, x.fork, 0)) != hipSuccess)
-            return x.eng->hipfail(e, "fork quota stream");
+        // forked at the last reduction (or counter reset): after the fold that read and zeroed the
+        // step counters, not after this step's evaluation, which the replay overlaps (the two write
+        // disjoint counters); joined by the next reduce / sync
+        if ((e = hipStreamWaitEvent(x.qs, x.fork, 0)) != hipSuccess) return x.eng->hipfail(e, "fork quota stream");
         const uint32_t m = (uint32_t)P.pos.size();
         int64_t* delta = counted ? (int64_t*)x.step.p + g->R : nullptr;
         if (m) {
@@ -886,7 +894,9 @@ int mxp_group_quota_granted(mxp_group* g, mxp_gqbatch* qb, int64_t* granted) {
         auto& P = qb->part[k];
         const size_t m = P.pos.size();
         hipError_t e;
-        if (x.q_pending && (e = hipEventSynchronize(x.join)) != hipSuccess) return x.eng->hipfail(e, "quota sync");
+        // (the replay's own event, joined or not: the member's stream is non-blocking, so the
+        // legacy-stream copy below does not wait for it)
+        if ((e = hipEventSynchronize(x.join)) != hipSuccess) return x.eng->hipfail(e, "quota sync");
         if (!m) return MXP_OK;
         P.hgranted.resize(m);
         if ((e = hipMemcpy(P.hgranted.data(), P.granted.p, m * 8, hipMemcpyDeviceToHost)) != hipSuccess)
@@ -902,7 +912,7 @@ void mxp_group_quota_batch_free(mxp_group* g, mxp_gqbatch* qb) {
     for (uint32_t k = 0; g && k < qb->part.size() && k < g->size(); k++) {
         auto& x = g->m[k];
         (void)hipSetDevice(x.device);
-        if (x.q_pending) (void)hipEventSynchronize(x.join);  // (the replay may still read the requests)
+        if (qb->evaluated) (void)hipEventSynchronize(x.join);  // (the replay may still read the requests)
         auto& P = qb->part[k];
         P.key.reset();
         P.amount.reset();

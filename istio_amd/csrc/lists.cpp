@@ -37,7 +37,7 @@ struct mxp_list {
     DevBuf lds_plan;  // REGEX: [K per staged part][LDS word base per staged part] (lists.h)
     NfaScratch nfa_scratch;  // REGEX: thread sets of NFA parts wider than the private-memory walk
     DevBuf rxp_tab, rxp_blk, rxp_lead;  // REGEX: literal-prefix dispatch (lists.h MXP_RXP_*)
-    uint32_t rxp_mask = 0, rxp_short = 0, rxp_n = 0;
+    uint32_t rxp_mask = 0, rxp_short = 0, rxp_n = 0, rxp_keys = 0;
 };
 
 namespace {
@@ -47,7 +47,7 @@ const uint32_t kUpperRows[MXP_UPPER_N][3] = {MXP_UPPER_ROWS};
 // The tail block (lists.h MXP_RXP_*) of a pattern whose every match starts with the literal bytes
 // `pre` (regex_required_prefix): its DFA stepped over the prefix, then the states reachable from
 // there with their transitions over the classes the tail tells apart.  False when the tail does not
-// fit a block: more than 32 states, 16 classes or MXP_RXP_BLOCK bytes, an NFA, or a state where
+// fit a block: more than MXP_RXP_STATES states, 16 classes or MXP_RXP_BLOCK_MAX bytes, an NFA, or a state where
 // non-ASCII runes lead anywhere but to a decision.  *never: no subject starting with the prefix
 // matches (the pattern can be dropped: its prefix is required).
 bool rxp_block(const mxp::Dfa& d, std::string pre, std::vector<uint8_t>* out, bool* never) {
@@ -90,7 +90,7 @@ bool rxp_block(const mxp::Dfa& d, std::string pre, std::vector<uint8_t>* out, bo
             for (uint32_t c = 0; c < d.ncls; c++) {
                 const uint32_t t = d.trans[(size_t)states[i] * d.ncls + c];
                 if (t >= mxp::kDfaReject || idx.count(t)) continue;
-                if (states.size() >= 32) return false;
+                if (states.size() >= MXP_RXP_STATES) return false;
                 idx[t] = (uint32_t)states.size();
                 states.push_back(t);
             }
@@ -126,7 +126,7 @@ bool rxp_block(const mxp::Dfa& d, std::string pre, std::vector<uint8_t>* out, bo
         byte_cls[b] = (uint8_t)it->second;
     }
     const uint32_t C = (uint32_t)cols.size() + 2;
-    if (C > 16 || MXP_RXP_TRANS + S * C > MXP_RXP_BLOCK) return false;
+    if (C > 16 || MXP_RXP_TRANS + S * C > MXP_RXP_BLOCK_MAX) return false;
     const uint32_t bytes = (MXP_RXP_TRANS + S * C + 15u) & ~15u;
     out->assign(bytes, 0);
     uint8_t* B = out->data();
@@ -476,6 +476,7 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             if ((rc = put(L->rxp_blk, pool.data(), pool.size(), "upload rxp blocks"))) return rc;
             if ((rc = put(L->rxp_lead, lead.data(), lead.size() * 4, "upload rxp lead"))) return rc;
             L->rxp_mask = cap - 1;
+            L->rxp_keys = (uint32_t)rxp_keys.size();
             // the union parts keep the other patterns
             std::vector<std::string> p2;
             std::vector<uint64_t> c2;
@@ -613,6 +614,11 @@ int mxp_go_to_upper(const uint8_t* s, uint64_t n, uint8_t* out, uint64_t cap, ui
 void mxp_list_regex_parts(const mxp_list* list, uint32_t out[2]) {
     out[0] = list ? list->rx_n : 0;
     out[1] = list ? list->rx_nfa : 0;
+}
+
+void mxp_list_regex_dispatch(const mxp_list* list, uint32_t out[2]) {
+    out[0] = list ? list->rxp_n : 0;
+    out[1] = list ? list->rxp_keys : 0;
 }
 
 int mxp_list_check_device(mxp_engine* eng, const mxp_list* L, int blacklist, const uint8_t* d_sym_bytes,

@@ -82,18 +82,20 @@ typedef struct mxp_list_args {
 //   [96 .. 96 + S * C)          next state per (state, class): a state, MXP_RXP_ACC or MXP_RXP_REJ
 // A byte >= 0x80 takes class C - 2 (HI): from every tail state all non-ASCII runes either reject or
 // accept (the block is built only then), so the rune's first byte decides; C - 1 is END of text.
-#define MXP_RXP_BLOCK 240u
+#define MXP_RXP_BLOCK 240u       // a block the LDS variant stages (larger ones it steps from global memory)
+#define MXP_RXP_BLOCK_MAX 1024u  // any block (96 header bytes + S x C transition bytes)
+#define MXP_RXP_STATES 96u       // tail states (u8 codes below MXP_RXP_ACC)
 #define MXP_RXP_ROW 61u   // LDS words per lane (the block and one pad word: an odd stride)
 #define MXP_RXP_MAXPRE 28u
 #define MXP_RXP_TRANS 96u
 #define MXP_RXP_ACC 0xFEu
 #define MXP_RXP_REJ 0xFFu
-#define MXP_RXP_LEAD 2048u
+#define MXP_RXP_LEAD 16384u  // (64 KB: ~0.5 leads a bucket at 10k patterns -- one or two probes a lookup)
 #define MXP_RXP_THREADS 128u
 
 // bucket of a prefix's first three bytes in rxp_lead
 MXP_NHD uint32_t mxp_rxp_lead(uint32_t b0, uint32_t b1, uint32_t b2) {
-    return ((b0 | b1 << 8 | b2 << 16) * 2654435761u) >> 21;  // (11 bits: MXP_RXP_LEAD)
+    return ((b0 | b1 << 8 | b2 << 16) * 2654435761u) >> 18;  // (14 bits: MXP_RXP_LEAD)
 }
 #define MXP_LIST_OPT_V4REG 1u   // dotted quads of <= 15 bytes parsed from registers (one window load)
 #define MXP_LIST_OPT_V4DIR 2u   // the IPv4 search starts from the /16 directory

@@ -491,7 +491,7 @@ __device__ __forceinline__ void list_rxp_body(const mxp_list_args& A) {
                     break;
                 }
                 const uint8_t* B = (const uint8_t*)blk;
-                if constexpr (kLds) {
+                if (kLds && nq <= MXP_RXP_BLOCK / 16u) {
                     // class nibbles and transitions into the lane's row: every load issued before the
                     // first store (one round trip, not one per 16 bytes)
                     uint4 v[MXP_RXP_BLOCK / 16u - 2u];
@@ -508,12 +508,32 @@ __device__ __forceinline__ void list_rxp_body(const mxp_list_args& A) {
                         }
                     B = (const uint8_t*)row;
                 }
+                // the classes of the tail's first 16 bytes first, as nibbles: their loads do not depend
+                // on the state, so they are all in flight together and the walk below pays one
+                // dependent load (the transition) per byte
+                const uint32_t wi = L >> 3, sh = (L & 7u) * 8u;
+                auto wsel = [&](uint32_t k) { return k == 0u ? w[0] : k == 1u ? w[1] : k == 2u ? w[2] : k == 3u ? w[3] : 0ull; };
+                const uint64_t a0 = wsel(wi), a1 = wsel(wi + 1u), a2 = wsel(wi + 2u);
+                const uint64_t t0 = sh ? (a0 >> sh) | (a1 << (64u - sh)) : a0;
+                const uint64_t t1 = sh ? (a1 >> sh) | (a2 << (64u - sh)) : a1;
+                uint64_t cl = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < 16u; j++) {
+                    if (L + j >= n || L + j >= 32u) break;
+                    const uint32_t b = (uint32_t)((j < 8u ? t0 : t1) >> ((j & 7u) * 8u)) & 0xFFu;
+                    const uint64_t c = b >= 0x80u ? C - 2u : (B[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
+                    cl |= c << (4u * j);
+                }
                 const uint8_t* T = B + MXP_RXP_TRANS;
                 uint32_t st = 0;
                 for (uint32_t i = L; i < n && st < S; i++) {
-                    const uint64_t wi = i < 8u ? w[0] : i < 16u ? w[1] : i < 24u ? w[2] : w[3];
-                    const uint32_t b = i < 32u ? (uint32_t)(wi >> ((i & 7u) * 8u)) & 0xFFu : s[i];
-                    const uint32_t cls = b >= 0x80u ? C - 2u : (B[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
+                    uint32_t cls;
+                    if (i < L + 16u && i < 32u) {
+                        cls = (uint32_t)(cl >> (4u * (i - L))) & 0xFu;
+                    } else {
+                        const uint32_t b = s[i];
+                        cls = b >= 0x80u ? C - 2u : (B[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
+                    }
                     st = T[st * C + cls];
                 }
                 if (st < S) st = T[st * C + C - 1u];  // END of text

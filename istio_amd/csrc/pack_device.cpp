@@ -104,7 +104,10 @@ int mxp_engine::pack_device_body(const mxp_bag_batch* b, mxp_dbatch* db) {
     const uint32_t n = b->n_requests;
     const uint32_t C = (uint32_t)cols.size(), V = (uint32_t)vcols.size();
     const uint32_t ncol = C + V;
-    if (ncol > MXP_PACK_MAXCOL) return pack_on_host(b, db);  // (wider rule sets: pack() checked the batch)
+    if (ncol > MXP_PACK_MAXCOL) {  // (wider rule sets: pack() checked the batch)
+        if (db->wide) db->wide->materialize();
+        return pack_on_host(b, db);
+    }
     int rc;
     if ((rc = ensure_dev_pools())) return rc;
     hipStream_t s = copy_stream(2);  // (the packer's kernels: their own stream)
@@ -177,7 +180,7 @@ int mxp_engine::pack_device_body(const mxp_bag_batch* b, mxp_dbatch* db) {
             return hipfail(e, what);
         return MXP_OK;
     };
-    const uint64_t sbytes = NS ? b->str_offsets[NS] : 0;
+    const uint64_t sbytes = NS ? (nb ? (uint64_t)nb->str_offsets32[NS] : b->str_offsets[NS]) : 0;
     if ((rc = up_wide(P.pk_soff, P.pk_soff32, b->str_offsets, nb ? nb->str_offsets32 : nullptr, NS ? (size_t)NS + 1 : 0,
                       "upload string offsets")))
         return rc;
@@ -190,7 +193,7 @@ int mxp_engine::pack_device_body(const mxp_bag_batch* b, mxp_dbatch* db) {
     // (the batch's own copy of its times, read by the evaluation)
     if ((rc = up(db->btsec, b->time_sec, (size_t)NT * 8, "times"))) return rc;
     if ((rc = up(db->btnsec, b->time_nsec, (size_t)NT * 4, "times"))) return rc;
-    const uint64_t E = (any_map && NM) ? b->map_offsets[NM] : 0;
+    const uint64_t E = (any_map && NM) ? (nb ? (uint64_t)nb->map_offsets32[NM] : b->map_offsets[NM]) : 0;
     if ((rc = up_wide(P.pk_moff, P.pk_moff32, b->map_offsets, nb ? nb->map_offsets32 : nullptr,
                       any_map && NM ? (size_t)NM + 1 : 0, "upload map offsets")))
         return rc;
@@ -430,6 +433,7 @@ int mxp_engine::pack_device_body(const mxp_bag_batch* b, mxp_dbatch* db) {
     std::vector<uint32_t> rx_s, rx_v;
     mxp::DfaSetHost rxb;
     if (need_rxof) {
+        if (db->wide) db->wide->materialize();  // (a narrow upload: this pass reads the v1 layout)
         std::vector<uint8_t> seen(NS, 0);
         std::unordered_map<std::string_view, uint32_t> by_text;
         auto text_of = [&](uint64_t sidx) {

@@ -271,6 +271,7 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         if (n && (e = mxp_launch_ns(&N, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch namespaces");
         eng->trace_mark("request namespaces (device)");
     } else {
+        if (db->wide && batch == &db->wide->view) db->wide->materialize();  // (a narrow upload)
         request_info(eng, batch, &info);
         hinfo = info.data();
         eng->trace_mark("request namespaces (host)");

@@ -80,6 +80,7 @@ SIGNATURES = {
     "mxp_list_destroy": (None, [_VP, _VP]),
     "mxp_list_entries": (ctypes.c_uint64, [_VP]),
     "mxp_list_regex_parts": (None, [_VP, ctypes.c_void_p]),
+    "mxp_list_regex_dispatch": (None, [_VP, ctypes.c_void_p]),
     "mxp_list_check": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
                                       ctypes.c_void_p]),
     "mxp_list_check_device": (ctypes.c_int, [_VP, _VP, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -874,6 +875,12 @@ class ListHandle:
 
     def num_entries(self) -> int:
         return int(self.eng.lib.mxp_list_entries(self.h))
+
+    def regex_dispatch(self):
+        """(patterns dispatched by their literal prefix, distinct prefixes) of a REGEX list."""
+        out = (ctypes.c_uint32 * 2)()
+        self.eng.lib.mxp_list_regex_dispatch(self.h, out)
+        return int(out[0]), int(out[1])
 
     def regex_parts(self):
         """(automata, of which bit-parallel NFAs) of a REGEX list."""

@@ -119,8 +119,10 @@ def test_regex_list_50k_patterns(mxp):
     pats, syms, hits = W.c3_regex_list(n_patterns=50_000, n_lookups=600, seed=51, return_hits=True)
     eng = mxp.Engine(0)
     lst = eng.list_create(L.REGEX, pats, [])
-    parts, nfas = lst.regex_parts()
-    assert nfas == 0  # (every C3 pattern is dispatched by its literal prefix: no union part is left)
+    # every C3 pattern is dispatched by its literal prefix (its tail automaton fits a block): no union
+    # part is left for a lookup to walk
+    assert lst.regex_parts() == (0, 0)
+    assert lst.regex_dispatch()[0] == 50_000
     assert lst.num_entries() == 50_000
     want = L.codes(L.RegexList(pats).found(syms), False)
     got = lst.check(syms)

@@ -23,6 +23,8 @@ def main():
         os.environ["MXP_LIST_RXP"] = rxp
         lists[name] = eng.list_create(ListHandle.REGEX, pats)
     os.environ.pop("MXP_LIST_RXP")
+    for name, lst in lists.items():
+        print(name, "union parts / NFAs:", lst.regex_parts(), "dispatched patterns / prefixes:", lst.regex_dispatch())
     bs = [x.encode() for x in syms]
     off = np.zeros(len(bs) + 1, dtype=np.uint64)
     off[1:] = np.cumsum([len(b) for b in bs])
