@@ -43,8 +43,10 @@ sys.path.insert(0, ROOT)
 # evaluation, memquota, the engine's own, two copy streams, the packer's); at 4 queues the copy and
 # packer streams shared one, so a fresh batch's H2D copies queued behind the previous batch's packer
 # kernels: 1.29 -> 0.98 ms per fresh C2 step at 8 (profiles/r6_s11_fresh_hwq*.log; INTEGRATION.md
-# sets it for the Mixer process the same way).  Read when HIP initialises; a caller's value wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# sets it for the Mixer process the same way).  Read when HIP initialises; raised to 8 when the
+# environment asks for fewer (the GPU boxes export the default 4), a larger value is kept.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PCIE_PEAK_GBS = 63.0  # PCIe Gen5 x16 host link, spec (MI355X_MICROARCH.md)

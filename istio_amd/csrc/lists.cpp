@@ -422,8 +422,14 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
         // and leaves the union parts; a lookup probes the prefixes it starts with and walks the
         // candidates' tails in LDS (lists.hip mxp_list_rxp_kernel) -- a few dependent loads per
         // lookup instead of one per byte through a union DFA far larger than the caches.
+        // MXP_LIST_RXP=1: always, 0: never; unset: when the patterns would not fit one union part.  A
+        // list that fits one part walks one DFA per lookup, faster than the dispatch's probes and tail
+        // walks on C3 (10k patterns: 0.092 against 0.125 ms, profiles/r6_s15_ab_rxp_ilp.log -- the
+        // dispatch kernel is bound by its VALU issue and vector-memory instructions, not by one walk's
+        // latency); past one part every lookup walks every part, and the dispatch stays flat.
         const char* rxp_env = getenv("MXP_LIST_RXP");
         const bool rxp_on = !rxp_env || atoi(rxp_env) != 0;
+
         std::map<std::string, std::vector<std::vector<uint8_t>>> rxp_keys;  // prefix -> its patterns' tails
         std::vector<uint8_t> dispatched(pats.size(), 0);
         for (size_t i = 0; i < pats.size(); i++) {  // per-pattern errors, in the reference's order
@@ -450,6 +456,18 @@ int mxp_list_create(mxp_engine* eng, int entry_type, const char* const* entries,
             }
         }
         L->n_entries = pats.size();
+        if (!rxp_env && !rxp_keys.empty()) {  // (auto: the union's size, from each pattern's own DFA)
+            uint64_t sum = 0;
+            bool any_alone = false;
+            for (size_t i = 0; i < pats.size(); i++) {
+                sum += cost[i];
+                any_alone |= alone[i] != 0;
+            }
+            if (!any_alone && sum <= kListPartStates) {  // one union part: no dispatch
+                rxp_keys.clear();
+                dispatched.assign(pats.size(), 0);
+            }
+        }
         if (!rxp_keys.empty()) {
             uint32_t cap = 16;
             while (cap < 2 * rxp_keys.size()) cap <<= 1;

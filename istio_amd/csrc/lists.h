@@ -101,6 +101,9 @@ MXP_NHD uint32_t mxp_rxp_lead(uint32_t b0, uint32_t b1, uint32_t b2) {
 #define MXP_LIST_OPT_V4DIR 2u   // the IPv4 search starts from the /16 directory
 #define MXP_LIST_OPT_STRREG 4u  // string symbols of <= 64 bytes loaded once into registers
 #define MXP_LIST_OPT_RXP_LDS 8u // regex-list tails stepped from a per-lane LDS copy (else from global / L2)
+// (ablations of the regex dispatch, results invalid: stop after the prefix-table probe / the header)
+#define MXP_LIST_OPT_ABL_PROBE 32u
+#define MXP_LIST_OPT_ABL_HDR 64u
 
 // ASCII upper-casing of 8 packed bytes (bytes >= 0x80 untouched): strings.ToUpper of ASCII-only
 // strings (any other string takes goupper.h's per-rune stream)

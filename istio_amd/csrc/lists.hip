@@ -434,6 +434,111 @@ extern "C" __global__ __launch_bounds__(1024) void mxp_list_rx_nfa_kernel(mxp_li
 // tail automaton stepped from there over the rest of the symbol (one LDS byte per class, one per
 // transition).  So a lookup pays ~3 dependent global loads (symbol, slot, block) where the union DFA
 // paid one per byte.  Patterns not dispatched stay in the union parts, walked after (from global).
+// One lookup through the dispatch: every prefix length its leading bytes allow, every tail with that
+// prefix, until one accepts (kLds: each tail stepped from the lane's LDS row).
+template <bool kLds>
+__device__ __forceinline__ bool rxp_one(const mxp_list_args& A, const uint8_t* s, uint32_t n, uint32_t* row) {
+    // the symbol's first 32 bytes (zero past its end): prefix hashes and compares, the walk's bytes
+    uint64_t w[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) w[k] = 8u * k < n ? mxp_ld8(s + 8u * k) & tail_mask(n - 8u * k) : 0ull;
+    uint32_t lens = A.rxp_short;
+    if (n >= 3u) {
+        const uint32_t b = (uint32_t)w[0];
+        lens |= A.rxp_lead[mxp_rxp_lead(b & 0xFFu, (b >> 8) & 0xFFu, (b >> 16) & 0xFFu)];
+    }
+    if (n < 32u) lens &= (1u << n) - 1u;  // (prefixes no longer than the symbol)
+    bool found = false;
+    for (; lens && !found; lens &= lens - 1u) {
+        const uint32_t L = (uint32_t)__ffs(lens);  // (bit L - 1: prefix length L)
+        uint64_t pre[4], h = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            pre[k] = 8u * k < L ? w[k] & tail_mask(L - 8u * k) : 0ull;
+            if (8u * k < L) h = mxp_hash_step(h, pre[k]);
+        }
+        h = mxp_hash_final(h, L);
+        const uint64_t want = (h >> 44) << 44 | (uint64_t)L << 38;
+        uint64_t t = 0;
+        for (uint32_t slot = (uint32_t)h & A.rxp_mask;; slot = (slot + 1u) & A.rxp_mask) {
+            t = A.rxp_tab[slot];
+            if (!t || (t & ~0x3FFFFFFFFFull) == want) break;
+        }
+        if (!t) continue;
+        if (A.opt & MXP_LIST_OPT_ABL_PROBE) {  // (ablation: stop at the probe -- results invalid)
+            found = true;
+            break;
+        }
+        const uint32_t count = (uint32_t)(t >> 32) & 0x3Fu;
+        uint32_t unit = (uint32_t)t;
+        for (uint32_t c = 0; c < count && !found; c++) {
+            const uint4* blk = (const uint4*)A.rxp_blk + unit;
+            const uint4 h0 = blk[0], h1 = blk[1];
+
+            const uint32_t S = h0.x & 0xFFu, C = (h0.x >> 8) & 0xFFu, nq = h0.x >> 24;
+            unit += nq;
+            // the block's prefix (bytes 4 .. 32, zero padded) against the symbol's first L bytes
+            const bool same = pre[0] == ((uint64_t)h0.y | (uint64_t)h0.z << 32) &&
+                              pre[1] == ((uint64_t)h0.w | (uint64_t)h1.x << 32) &&
+                              pre[2] == ((uint64_t)h1.y | (uint64_t)h1.z << 32) && pre[3] == (uint64_t)h1.w;
+            if (!same) continue;
+            if (S == 0u || (A.opt & MXP_LIST_OPT_ABL_HDR)) {  // the prefix alone decides (or the ablation stops here)
+                found = true;
+                break;
+            }
+            const uint8_t* B = (const uint8_t*)blk;
+            if (kLds && nq <= MXP_RXP_BLOCK / 16u) {
+                // class nibbles and transitions into the lane's row: every load issued before the
+                // first store (one round trip, not one per 16 bytes)
+                uint4 v[MXP_RXP_BLOCK / 16u - 2u];
+#pragma unroll
+                for (uint32_t k = 2; k < MXP_RXP_BLOCK / 16u; k++)
+                    if (k < nq) v[k - 2u] = blk[k];
+#pragma unroll
+                for (uint32_t k = 2; k < MXP_RXP_BLOCK / 16u; k++)
+                    if (k < nq) {
+                        row[4u * k] = v[k - 2u].x;
+                        row[4u * k + 1u] = v[k - 2u].y;
+                        row[4u * k + 2u] = v[k - 2u].z;
+                        row[4u * k + 3u] = v[k - 2u].w;
+                    }
+                B = (const uint8_t*)row;
+            }
+            // the classes of the tail's first 16 bytes first, as nibbles: their loads do not depend
+            // on the state, so they are all in flight together and the walk below pays one
+            // dependent load (the transition) per byte
+            const uint32_t wi = L >> 3, sh = (L & 7u) * 8u;
+            auto wsel = [&](uint32_t k) { return k == 0u ? w[0] : k == 1u ? w[1] : k == 2u ? w[2] : k == 3u ? w[3] : 0ull; };
+            const uint64_t a0 = wsel(wi), a1 = wsel(wi + 1u), a2 = wsel(wi + 2u);
+            const uint64_t t0 = sh ? (a0 >> sh) | (a1 << (64u - sh)) : a0;
+            const uint64_t t1 = sh ? (a1 >> sh) | (a2 << (64u - sh)) : a1;
+            uint64_t cl = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 16u; j++) {
+                if (L + j >= n || L + j >= 32u) break;
+                const uint32_t b = (uint32_t)((j < 8u ? t0 : t1) >> ((j & 7u) * 8u)) & 0xFFu;
+                const uint64_t c = b >= 0x80u ? C - 2u : (B[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
+                cl |= c << (4u * j);
+            }
+            const uint8_t* T = B + MXP_RXP_TRANS;
+            uint32_t st = 0;
+            for (uint32_t i = L; i < n && st < S; i++) {
+                uint32_t cls;
+                if (i < L + 16u && i < 32u) {
+                    cls = (uint32_t)(cl >> (4u * (i - L))) & 0xFu;
+                } else {
+                    const uint32_t b = s[i];
+                    cls = b >= 0x80u ? C - 2u : (B[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
+                }
+                st = T[st * C + cls];
+            }
+            if (st < S) st = T[st * C + C - 1u];  // END of text
+            found = st == MXP_RXP_ACC;
+        }
+    }
+    return found;
+}
+
 template <bool kNfa, bool kLds>
 __device__ __forceinline__ void list_rxp_body(const mxp_list_args& A) {
     // kLds: the candidate's block copied into the lane's LDS row (MXP_RXP_ROW words; odd: the lanes'
@@ -447,99 +552,7 @@ __device__ __forceinline__ void list_rxp_body(const mxp_list_args& A) {
         const uint8_t* s;
         uint32_t n;
         if (!list_symbol(A, q, &s, &n)) continue;
-        // the symbol's first 32 bytes (zero past its end): prefix hashes and compares, the walk's bytes
-        uint64_t w[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) w[k] = 8u * k < n ? mxp_ld8(s + 8u * k) & tail_mask(n - 8u * k) : 0ull;
-        uint32_t lens = A.rxp_short;
-        if (n >= 3u) {
-            const uint32_t b = (uint32_t)w[0];
-            lens |= A.rxp_lead[mxp_rxp_lead(b & 0xFFu, (b >> 8) & 0xFFu, (b >> 16) & 0xFFu)];
-        }
-        if (n < 32u) lens &= (1u << n) - 1u;  // (prefixes no longer than the symbol)
-        bool found = false;
-        for (; lens && !found; lens &= lens - 1u) {
-            const uint32_t L = (uint32_t)__ffs(lens);  // (bit L - 1: prefix length L)
-            uint64_t pre[4], h = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; k++) {
-                pre[k] = 8u * k < L ? w[k] & tail_mask(L - 8u * k) : 0ull;
-                if (8u * k < L) h = mxp_hash_step(h, pre[k]);
-            }
-            h = mxp_hash_final(h, L);
-            const uint64_t want = (h >> 44) << 44 | (uint64_t)L << 38;
-            uint64_t t = 0;
-            for (uint32_t slot = (uint32_t)h & A.rxp_mask;; slot = (slot + 1u) & A.rxp_mask) {
-                t = A.rxp_tab[slot];
-                if (!t || (t & ~0x3FFFFFFFFFull) == want) break;
-            }
-            if (!t) continue;
-            const uint32_t count = (uint32_t)(t >> 32) & 0x3Fu;
-            uint32_t unit = (uint32_t)t;
-            for (uint32_t c = 0; c < count && !found; c++) {
-                const uint4* blk = (const uint4*)A.rxp_blk + unit;
-                const uint4 h0 = blk[0], h1 = blk[1];
-                const uint32_t S = h0.x & 0xFFu, C = (h0.x >> 8) & 0xFFu, nq = h0.x >> 24;
-                unit += nq;
-                // the block's prefix (bytes 4 .. 32, zero padded) against the symbol's first L bytes
-                const bool same = pre[0] == ((uint64_t)h0.y | (uint64_t)h0.z << 32) &&
-                                  pre[1] == ((uint64_t)h0.w | (uint64_t)h1.x << 32) &&
-                                  pre[2] == ((uint64_t)h1.y | (uint64_t)h1.z << 32) && pre[3] == (uint64_t)h1.w;
-                if (!same) continue;
-                if (S == 0u) {  // the prefix alone decides
-                    found = true;
-                    break;
-                }
-                const uint8_t* B = (const uint8_t*)blk;
-                if (kLds && nq <= MXP_RXP_BLOCK / 16u) {
-                    // class nibbles and transitions into the lane's row: every load issued before the
-                    // first store (one round trip, not one per 16 bytes)
-                    uint4 v[MXP_RXP_BLOCK / 16u - 2u];
-#pragma unroll
-                    for (uint32_t k = 2; k < MXP_RXP_BLOCK / 16u; k++)
-                        if (k < nq) v[k - 2u] = blk[k];
-#pragma unroll
-                    for (uint32_t k = 2; k < MXP_RXP_BLOCK / 16u; k++)
-                        if (k < nq) {
-                            row[4u * k] = v[k - 2u].x;
-                            row[4u * k + 1u] = v[k - 2u].y;
-                            row[4u * k + 2u] = v[k - 2u].z;
-                            row[4u * k + 3u] = v[k - 2u].w;
-                        }
-                    B = (const uint8_t*)row;
-                }
-                // the classes of the tail's first 16 bytes first, as nibbles: their loads do not depend
-                // on the state, so they are all in flight together and the walk below pays one
-                // dependent load (the transition) per byte
-                const uint32_t wi = L >> 3, sh = (L & 7u) * 8u;
-                auto wsel = [&](uint32_t k) { return k == 0u ? w[0] : k == 1u ? w[1] : k == 2u ? w[2] : k == 3u ? w[3] : 0ull; };
-                const uint64_t a0 = wsel(wi), a1 = wsel(wi + 1u), a2 = wsel(wi + 2u);
-                const uint64_t t0 = sh ? (a0 >> sh) | (a1 << (64u - sh)) : a0;
-                const uint64_t t1 = sh ? (a1 >> sh) | (a2 << (64u - sh)) : a1;
-                uint64_t cl = 0;
-#pragma unroll
-                for (uint32_t j = 0; j < 16u; j++) {
-                    if (L + j >= n || L + j >= 32u) break;
-                    const uint32_t b = (uint32_t)((j < 8u ? t0 : t1) >> ((j & 7u) * 8u)) & 0xFFu;
-                    const uint64_t c = b >= 0x80u ? C - 2u : (B[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
-                    cl |= c << (4u * j);
-                }
-                const uint8_t* T = B + MXP_RXP_TRANS;
-                uint32_t st = 0;
-                for (uint32_t i = L; i < n && st < S; i++) {
-                    uint32_t cls;
-                    if (i < L + 16u && i < 32u) {
-                        cls = (uint32_t)(cl >> (4u * (i - L))) & 0xFu;
-                    } else {
-                        const uint32_t b = s[i];
-                        cls = b >= 0x80u ? C - 2u : (B[32u + (b >> 1)] >> ((b & 1u) * 4u)) & 0xFu;
-                    }
-                    st = T[st * C + cls];
-                }
-                if (st < S) st = T[st * C + C - 1u];  // END of text
-                found = st == MXP_RXP_ACC;
-            }
-        }
+        bool found = rxp_one<kLds>(A, s, n, row);
         for (uint32_t k = 0; k < A.rx_n && !found; k++) found = rx_part<kNfa>(A, k, s, n);
         list_decide(A, q, found);
     }

@@ -113,10 +113,13 @@ def test_regex_list_with_over_budget_patterns(mxp, monkeypatch, rx16, rxp):
     assert (want == 0).sum() > 100 and (want == 5).sum() > 100
 
 
-def test_regex_list_50k_patterns(mxp):
-    """A 50k-pattern list (C3 shape, 5x configs[2]) builds -- packed into several union DFAs -- and
-    matches the oracle on a sample of lookups."""
+@pytest.mark.parametrize("rxp", [None, "1"])
+def test_regex_list_50k_patterns(mxp, monkeypatch, rxp):
+    """A 50k-pattern list (C3 shape, 5x configs[2]) builds and matches the oracle on a sample of
+    lookups: too large for one union part, so dispatched by literal prefix (by default, and forced)."""
     pats, syms, hits = W.c3_regex_list(n_patterns=50_000, n_lookups=600, seed=51, return_hits=True)
+    if rxp is not None:
+        monkeypatch.setenv("MXP_LIST_RXP", rxp)
     eng = mxp.Engine(0)
     lst = eng.list_create(L.REGEX, pats, [])
     # every C3 pattern is dispatched by its literal prefix (its tail automaton fits a block): no union
@@ -129,3 +132,21 @@ def test_regex_list_50k_patterns(mxp):
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(syms[i], int(got[i]), int(want[i])) for i in bad[:5]]
     assert (want == 0).sum() > 200 and (want == 5).sum() > 200
+
+
+def test_regex_list_auto_dispatch(mxp, monkeypatch):
+    """MXP_LIST_RXP unset: a list whose union fits one part (C3's 10k patterns) walks the union DFA --
+    faster there than the dispatch (profiles/r6_s15_ab_rxp_ilp.log); MXP_LIST_RXP=1 dispatches it.  The
+    codes agree either way."""
+    pats, syms = W.c3_regex_list(n_patterns=10_000, n_lookups=3000, seed=52)
+    monkeypatch.delenv("MXP_LIST_RXP", raising=False)
+    eng = mxp.Engine(0)
+    auto = eng.list_create(L.REGEX, pats, [])
+    assert auto.regex_parts() == (1, 0) and auto.regex_dispatch() == (0, 0)
+    monkeypatch.setenv("MXP_LIST_RXP", "1")
+    forced = eng.list_create(L.REGEX, pats, [])
+    assert forced.regex_parts() == (0, 0) and forced.regex_dispatch()[0] == 10_000
+    a, b = auto.check(syms), forced.check(syms)
+    assert np.array_equal(a, b)
+    want = L.codes(L.RegexList(pats).found(syms[:400]), False)
+    assert np.array_equal(a[:400], want)
