@@ -3,7 +3,10 @@
 (MXP_LIST_RXP=0, mxp_list_rx_kernel), literal-prefix dispatch (MXP_LIST_RXP=1) stepping tails from
 global memory (mxp_list_rxp_kernel) or from a per-lane LDS copy (MXP_LIST_OPT bit 8,
 mxp_list_rxp_lds_kernel), and two stage ablations of the global kernel (stop at the probe / at the
-header: codes invalid); rounds alternated, HIP-event kernel times, codes compared.  (Round 6 also
+header: codes invalid; profiles/r6_s14_ab_rxp_stages.log); rounds alternated, HIP-event times,
+codes compared.  (Round 6 also ran the union walk over lookups bucketed by their first three bytes,
+an atomic counting sort first: the walk stayed at 0.089 ms and the sort cost 0.145 ms,
+profiles/r6_s17_ab_rx_sorted.log, r6_s18_kernel_stats_ab_rx_sorted.csv -- removed.)  (Round 6 also
 ran two lookups a lane with the tail walks stepped together: 0.176 against 0.126 ms,
 profiles/r6_s15_ab_rxp_ilp.log -- removed.)"""
 import os
@@ -35,8 +38,7 @@ def main():
     d_blob = torch.from_numpy(blob.copy()).cuda()
     d_off = torch.from_numpy(off.view(np.int64).copy()).cuda()
     s = torch.cuda.Stream()
-    variants = [("union", "union", "5"), ("rxp-global", "rxp", "5"), ("rxp-lds", "rxp", "13"),
-                ("abl-probe", "rxp", "37"), ("abl-header", "rxp", "69")]  # (ablations: codes invalid)
+    variants = [("union", "union", "5"), ("rxp-global", "rxp", "5"), ("rxp-lds", "rxp", "13")]
     codes, times = {}, {v[0]: [] for v in variants}
     for rnd in range(6):
         for label, lst, opt in variants:
