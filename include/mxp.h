@@ -365,13 +365,18 @@ int mxp_batch_upload(mxp_engine* eng, const mxp_bag_batch* batch, mxp_dbatch** o
 /* mxp_batch_upload with flags.  MXP_UPLOAD_NO_WAIT: return once the copies are queued and the
  * batch checked, before the copies are in; the caller keeps the arrays unchanged until
  * mxp_batch_wait_copied(db) returns (or the batch's first evaluation has completed).  A worker then
- * overlaps batch k + 1's copies with its own host work for batch k (bench.py fresh_batch). */
+ * overlaps batch k + 1's copies with its own host work for batch k (bench.py fresh_batch).  A call
+ * that fails has finished reading the caller's arrays when it returns (its copy and packer streams
+ * are synchronised on every error path). */
 #define MXP_UPLOAD_NO_WAIT 1u
 int mxp_batch_upload_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t flags, mxp_dbatch** out);
 int mxp_batch_wait_copied(mxp_dbatch* db);
 /* mxp_batch_upload_ex of a narrow batch (mxp_batch.h mxp_bag_batch2): the u32 arrays are copied and
- * widened on the device; the engine keeps a widened host view of the batch with the device batch
- * (its host passes read it), so mxp_resolve_uploaded takes batch = NULL for such a batch. */
+ * widened on the device, and checked on the host as u32.  The engine keeps a host view of the batch
+ * with the device batch (mxp_resolve_uploaded takes batch = NULL for such a batch); the view's u32
+ * columns are widened on the host only for a pass that reads the v1 layout (run-time regexp
+ * patterns, rule sets wider than the device packer, a Resolve without device namespaces), from the
+ * caller's arrays -- which such a call needs unchanged until it returns. */
 int mxp_batch_upload2(mxp_engine* eng, const mxp_bag_batch2* batch, uint32_t flags, mxp_dbatch** out);
 /* The host half of mxp_batch_upload alone (interning against the rule set's pools, column gather,
  * ip() / timestamp() / regexp pre-tables), for timing and tests; works on a host-only engine.
