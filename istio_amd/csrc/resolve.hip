@@ -479,17 +479,21 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_tile_write_kernel(
 // workgroup reads each bitmap word's row as one 4 KB run (the per-lane walk read 1 KB runs: 2 TB/s
 // on C2's 1.25 GB); kCW words x 4 requests of loads are in flight per thread.  The request's own
 // namespace and the outputs per request afterwards; block sums per 256 requests for the scan.
-constexpr uint32_t kCW = 8;
-extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count4_kernel(mxp_resolve_args A) {
+// kVec (the default when n % 4 == 0): a thread takes the four consecutive requests 4t .. 4t + 3
+// and reads each word row's four values with one aligned 16-byte load -- a quarter of the load
+// instructions: 362 -> 298 us on C2's 1.31 GB (profiles/r6_s21_kernel_stats_e2e_c2_{strided,vec}.csv).
+template <bool kVec, uint32_t kCW = 8>  // (kCW word rows of loads in flight)
+__device__ __forceinline__ void resolve_count4(const mxp_resolve_args& A) {
     const uint32_t t = threadIdx.x;
     const uint32_t base = blockIdx.x * 1024u;
+    auto req = [&](uint32_t k) { return kVec ? base + 4u * t + k : base + t + 256u * k; };
     const uint32_t dlo = __builtin_amdgcn_readfirstlane(A.ns_lo[A.default_id]);
     const uint32_t dhi = __builtin_amdgcn_readfirstlane(A.ns_hi[A.default_id]);
     uint32_t info[4], cnt[4], st[4][4];
     bool act[4];
 #pragma unroll
     for (uint32_t k = 0; k < 4u; k++) {
-        const uint32_t q = base + t + 256u * k;
+        const uint32_t q = req(k);
         act[k] = false;
         info[k] = 0u;
         cnt[k] = 0u;
@@ -525,13 +529,26 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count4_kernel(mxp_
             a1[j] = A.amask[A.n_words + wc] & rb;
             em[j] = A.empty[wc];
         }
+        if constexpr (kVec) {
+            const bool any = act[0] || act[1] || act[2] || act[3];
 #pragma unroll
-        for (uint32_t j = 0; j < kCW; j++)
-#pragma unroll
-            for (uint32_t k = 0; k < 4u; k++) {
-                const uint32_t q = base + t + 256u * k;
-                mv[j][k] = act[k] && (a0[j] | a1[j]) ? A.match[(uint64_t)(w0 + j) * A.n + q] : 0u;
+            for (uint32_t j = 0; j < kCW; j++) {
+                uint4 v = make_uint4(0u, 0u, 0u, 0u);
+                if (any && (a0[j] | a1[j])) v = *(const uint4*)(A.match + (uint64_t)(w0 + j) * A.n + req(0));
+                mv[j][0] = act[0] ? v.x : 0u;
+                mv[j][1] = act[1] ? v.y : 0u;
+                mv[j][2] = act[2] ? v.z : 0u;
+                mv[j][3] = act[3] ? v.w : 0u;
             }
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kCW; j++)
+#pragma unroll
+                for (uint32_t k = 0; k < 4u; k++) {
+                    const uint32_t q = req(k);
+                    mv[j][k] = act[k] && (a0[j] | a1[j]) ? A.match[(uint64_t)(w0 + j) * A.n + q] : 0u;
+                }
+        }
 #pragma unroll
         for (uint32_t j = 0; j < kCW; j++)
 #pragma unroll
@@ -548,9 +565,10 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count4_kernel(mxp_
                 cnt[k] += __builtin_popcount(sel);
             }
     }
+    uint64_t csum = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4u; k++) {
-        const uint32_t q = base + t + 256u * k;
+        const uint32_t q = req(k);
         uint32_t c = 0u;
         if (act[k]) {
             const uint32_t ns = info[k] & 0x7FFFFFFFu;
@@ -568,12 +586,25 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count4_kernel(mxp_
                 c = S.cnt;
             }
         }
-        if (A.block_sum) {  // (requests base + 256 k ...: block 4 * blockIdx.x + k of the scan)
+        if constexpr (kVec) {
+            csum += c;
+        } else if (A.block_sum) {  // (requests base + 256 k ...: block 4 * blockIdx.x + k of the scan)
             const uint64_t tot = block_sum256(c);
             if (t == 0 && base + 256u * k < A.n) A.block_sum[4u * blockIdx.x + k] = tot;
         }
     }
+    if (kVec && A.block_sum) {  // (wave w holds requests base + 256 w ...: block 4 * blockIdx.x + w)
+        uint64_t v = csum;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        const uint32_t w = t >> 6;
+        if ((t & 63u) == 0 && base + 256u * w < A.n) A.block_sum[4u * blockIdx.x + w] = v;
+    }
 }
+extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count4_kernel(mxp_resolve_args A) { resolve_count4<false>(A); }
+extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count4v_kernel(mxp_resolve_args A) { resolve_count4<true>(A); }
+
+
 
 // the count pass's block sums from the counts (the tiled count kernel's blocks are 64 requests)
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_bsum_kernel(mxp_resolve_args A) {
@@ -593,7 +624,12 @@ extern "C" hipError_t mxp_launch_resolve(const mxp_resolve_args* a, int write, h
         hipLaunchKernelGGL(mxp_resolve_offsets_kernel, dim3(grid), dim3(256), 0, s, *a);
     } else if (write == 3) {
         if (!a->err) {  // (compact: the four-request count kernel; with an error bitmap the tiled one)
-            hipLaunchKernelGGL(mxp_resolve_count4_kernel, dim3((a->n + 1023u) / 1024u), dim3(256), 0, s, *a);
+            // (MXP_RESOLVE_VEC=0: the strided four-request kernel, A/B)
+            static const bool vec = !getenv("MXP_RESOLVE_VEC") || atoi(getenv("MXP_RESOLVE_VEC")) != 0;
+            // (16 word rows in flight: 146 VGPRs, 3 waves/SIMD, 342 against 298 us on C2,
+            // profiles/r6_s22_kernel_stats_e2e_c2_cw{8,16}.csv)
+            hipLaunchKernelGGL(vec && (a->n & 3u) == 0u ? mxp_resolve_count4v_kernel : mxp_resolve_count4_kernel,
+                               dim3((a->n + 1023u) / 1024u), dim3(256), 0, s, *a);
         } else {
             hipLaunchKernelGGL(mxp_resolve_tile_count_kernel, dim3((a->n + 63u) / 64u), dim3(256), 0, s, *a);
             if (a->block_sum) hipLaunchKernelGGL(mxp_resolve_bsum_kernel, dim3(grid), dim3(256), 0, s, *a);
