@@ -51,6 +51,7 @@ if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 PCIE_PEAK_GBS = 63.0  # PCIe Gen5 x16 host link, spec (MI355X_MICROARCH.md)
 QUOTA_KEYS = 1024
+T0 = time.perf_counter()
 
 
 def host_threads():
@@ -657,10 +658,12 @@ def predicate_bench(args, kind, devices, data, with_quota=False):
                         "quota_delta_abs_total": int(np.abs(delta).sum()),
                         "collective": "one all-reduce of hits[R] ++ quota_delta[K] per step (mxp_group_reduce)"}
     if args.fresh_steps > 0 and not with_quota:
+        progress("%s fresh batches" % kind)
         out["fresh_batch"] = fresh_batch_block(g, [data.shards(kind, 1), data.shards(kind, 2)], args.fresh_steps, R,
                                                args.wire)
     if args.e2e_reps > 0 and not with_quota:
         sets = [shards] + ([data.shards(kind, 1), data.shards(kind, 2)] if args.fresh_steps > 0 else [])
+        progress("%s end to end" % kind)
         out["end_to_end"] = end_to_end(g, sets, R, args.e2e_reps, args.wire)
     gb.free()
     if quota is not None:
@@ -839,8 +842,15 @@ def list_cpu_baseline(kind, entries, syms, seconds, threads):
                 done, dt, len(entries), threads)}
 
 
+def progress(what):
+    """A progress note on stderr (the JSON line is stdout's only line): a long multi-GPU run keeps
+    writing while its blocks run."""
+    print("bench: %s (%.0f s)" % (what, time.perf_counter() - T0), file=sys.stderr, flush=True)
+
+
 def run(args, devices):
     """Every block of the run over the group `devices`; returns the line (a dict)."""
+    progress("generating inputs for %d device(s)" % len(devices))
     kinds = set()
     wl = args.workload
     if wl in ("c2", "c5"):
@@ -857,12 +867,14 @@ def run(args, devices):
     if wl == "c5-quota":
         return quota_bench(args, devices)
     kind = "c4" if wl == "c4" else "c2"
+    progress("%s block" % wl)
     out = predicate_bench(args, kind, devices, data, with_quota=wl == "c5")
     keys = ("metric", "value", "unit", "ms_per_step", "eval_ms", "kernels_ms", "deferred_pairs", "pack_upload_s",
             "fresh_batch", "end_to_end", "config", "group", "roofline", "lds_bank_conflicts", "quota", "cpu_baseline",
             "hits_total")
     if wl == "c2" and not args.no_c4:
         # the representative config BASELINE.json quotes at 10k rules (configs[3]), driver-timed too
+        progress("c4 block")
         c4 = predicate_bench(args, "c4", devices, data)
         out["c4"] = {k: c4[k] for k in keys if k in c4}
     if wl == "c2" and not args.no_c5:
@@ -871,6 +883,7 @@ def run(args, devices):
         a5 = argparse.Namespace(**vars(args))
         a5.e2e_reps = 0
         a5.no_cpu_baseline = True
+        progress("c5 block")
         c5 = predicate_bench(a5, "c2", devices, data, with_quota=True)
         out["c5"] = {k: c5[k] for k in keys if k in c5}
     if wl == "c2" and not args.no_c3:
@@ -879,6 +892,7 @@ def run(args, devices):
                  "lds_bank_conflicts", "cpu_baseline")
         out["c3"] = {}
         for k in ("c3-ip", "c3-str", "c3-regex"):
+            progress("%s block" % k)
             r = list_bench(args, devices, data, kind=k, emit=False)
             out["c3"][k[3:]] = {x: r[x] for x in ckeys if x in r}
     return out
