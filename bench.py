@@ -270,7 +270,9 @@ def timed_loop(step, steps, warmup, world, stream, sync=None, events=True):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ev_ms = [a.elapsed_time(b) for a, b in evs] if events else []
-    return D.max_over_ranks(elapsed), ev_ms
+    # (world 1: this process times the whole job -- under torch.distributed.run rank 0 drives the
+    # group while the other ranks wait at their barrier, so no collective here)
+    return (D.max_over_ranks(elapsed) if world > 1 else elapsed), ev_ms
 
 
 # ---------------------------------------------------------------------------------- synthetic data
@@ -900,6 +902,9 @@ def run(args, devices):
 
 def main():
     args = parse()
+    if os.environ.get("MXP_BENCH_WATCHDOG"):  # (debugging: every thread's Python stack every N s)
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["MXP_BENCH_WATCHDOG"]), repeat=True, file=sys.stderr)
     from istio_amd import dist as D
     rank, world, _ = D.world()
     n_gpus = world if world > 1 else args.gpus

@@ -5,6 +5,6 @@ set -u
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp MXP_NO_BUILD=1
 o=gpurun_out/r6s23; mkdir -p $o
-timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 \
-  bench.py --gpus 2 --devices 0,0 --steps 10 --warmup 3 --no-cpu-baseline --no-c3 > $o/bench_launch2.log 2> $o/bench_launch2.err || exit $?
+MXP_BENCH_WATCHDOG=100 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 \
+  bench.py --gpus 2 --devices 0,0 --steps 10 --warmup 3 --no-cpu-baseline --no-c3 > $o/bench_launch2.log 2> $o/bench_launch2.err; echo "rc=$?" >> $o/bench_launch2.err
 exit 0
