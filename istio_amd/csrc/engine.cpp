@@ -2766,6 +2766,10 @@ int mxp_engine::check_batch(const mxp_bag_batch* b, int parts) {
     lim_of[MXP_TIMESTAMP] = NT;
     lim_of[MXP_STRING_MAP] = NM;
     if (!(parts & kCheckColumns)) return MXP_OK;
+    // (the u32 scan's limits: id > n - 1 is out of range; n = 0 rejects every id of the kind)
+    auto m1 = [](uint64_t lim) { return lim == 0 ? 0u : (uint32_t)std::min<uint64_t>(lim - 1, 0xFFFFFFFFull); };
+    const uint32_t ns1 = m1(NS), nt1 = m1(NT), nm1 = m1(NM);
+    const uint32_t ns0 = NS == 0, nt0 = NT == 0, nm0 = NM == 0;
     if (!use.empty())
         mxp::par_for(n, 1u << 16, [&](uint64_t q0, uint64_t q1, unsigned w) {
             bool maps = false;
@@ -2782,10 +2786,22 @@ int mxp_engine::check_batch(const mxp_bag_batch* b, int parts) {
                         nmap += k[q] == MXP_STRING_MAP;
                     }
                 };
-                if (v32)
-                    scan(v32);
-                else
+                if (v32) {
+                    // u32 ids: the limits by compares instead of the table (no gather: the loop
+                    // vectorises; 1M requests x 5 columns took 0.25 ms of the upload call, r6_s25)
+                    uint32_t bad = 0, nm = 0;
+                    for (uint64_t q = q0; q < q1; q++) {
+                        const uint32_t kd = k[q], x = v32[q];
+                        const uint32_t sk = (kd == MXP_STRING) | (kd == MXP_BYTES) | (kd == MXP_OTHER);
+                        bad |= (sk & ((x > ns1) | ns0)) | ((kd == MXP_TIMESTAMP) & ((x > nt1) | nt0)) |
+                               ((kd == MXP_STRING_MAP) & ((x > nm1) | nm0)) | (kd > MXP_OTHER);
+                        nm += kd == MXP_STRING_MAP;
+                    }
+                    fail_any = bad != 0;
+                    nmap = nm;
+                } else {
                     scan(v64);
+                }
                 maps |= nmap != 0;
                 if (!fail_any) continue;
                 const std::string nm(b->column_names[c]);

@@ -101,3 +101,33 @@ def test_narrow_resolve_uploaded(mxp):
         got = g.resolve_arrays(None, 0, cap=1 << 22, ids16=True, uploaded=gb)
         for a, c in zip(got, want[k]):
             assert np.array_equal(a, c), k
+
+
+def test_narrow_malformed_batches_rejected(mxp):
+    """The u32 checks of a narrow upload (check_batch on the narrow arrays, no widened host copy)
+    reject every malformed variant of test_batch_check.py with the same messages the wide upload
+    gives, and the engine then uploads and evaluates the good batch as the wide path does."""
+    import test_batch_check as T
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(T.MANIFEST)
+    assert (eng.compile(T.RULES) == 0).all()
+    b = T.good_batch()
+    n_maps = len(b.map_offsets) - 1
+    cases = []
+    for label, frag, x in T.malformed(b):
+        if label == "map id":  # (1 << 40 is no u32: the first id past the map table instead)
+            x.values[T._col(x, "ar")][5] = n_maps
+        cases.append((label, frag, x))
+    assert len(cases) == 9
+    for label, frag, x in cases:
+        with pytest.raises(mxp.MxpError) as ei:
+            eng.upload2(NarrowBatch(x))
+        msg = str(ei.value)
+        assert "failed (1)" in msg and frag in msg, (label, msg)
+        with pytest.raises(mxp.MxpError) as ei:  # (the same text from the wide upload)
+            eng.upload(x)
+        assert frag in str(ei.value), label
+    R, n = len(T.RULES), b.n
+    m_narrow, e_narrow = _bitmaps(eng.upload2(NarrowBatch(b)), n, R)
+    m_wide, e_wide = _bitmaps(eng.upload(b), n, R)
+    assert np.array_equal(m_narrow, m_wide) and np.array_equal(e_narrow, e_wide)

@@ -1,0 +1,8 @@
+# round 6, session 25: HIP API + kernel + copy trace of the end-to-end C2 calls (where the pipelined
+# loop's host thread blocks)
+set -u
+cd "${GRAFT_REPO_ROOT:-.}"
+export TMPDIR=/tmp MXP_NO_BUILD=1 GPU_MAX_HW_QUEUES=8
+o=gpurun_out/r6s25; mkdir -p $o
+timeout -k 10 300 rocprofv3 --hip-trace --kernel-trace --memory-copy-trace --output-format csv -d $o/prof -o e2e -- python3 -u tools/e2e_group_prof.py c2 3 > $o/prof.log 2>&1 || exit $?
+exit 0
