@@ -479,8 +479,11 @@ def end_to_end(g, shard_sets, n_rules, reps, wire="narrow"):
 
     def resolve(st, cap=0, out=None):  # one call from host bags: upload (narrow) + Resolve, or the one-shot call
         if narrow:
+            # (the upload returns once its copies are queued -- MXP_UPLOAD_NO_WAIT, as a binding calls
+            # it -- and the Resolve's first evaluation orders itself after them; BENCH_E2E_WAIT=1: the
+            # upload waits for its copies first, A/B)
             return g.resolve_arrays(None, 0, cap or max(16, 4 * n), ids16=ids16, out=out,
-                                    uploaded=upload_set(g, st, wire, False))
+                                    uploaded=upload_set(g, st, wire, not os.environ.get("BENCH_E2E_WAIT")))
         return g.resolve_arrays(st, 0, cap, ids16=ids16, out=out)
     # list sizes (the one-shot call from the wide form: an uploaded batch's Resolve cannot retry when
     # its ids do not fit), then a warm-up of the measured call (allocations)
