@@ -70,3 +70,31 @@ def test_device_pack_edge_batches(mxp, monkeypatch):
         out = [_run(mxp, monkeypatch, host, manifest, rules, batch) for host in (True, False)]
         assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
         assert out[0][2] == out[1][2]
+
+
+@pytest.mark.parametrize("wl", ["fuzz", "c1", "c4", "resolver"])
+def test_narrow_device_pack_matches_host_pack(mxp, monkeypatch, wl):
+    """The narrow batch (mxp_batch_upload2: u32 ids and offsets widened on the device, checked as
+    u32, the host view widened only for the passes that read it -- run-time regexp patterns among
+    them) packs to the same bitmaps as the host packer on the wide batch."""
+    from istio_amd.bags import NarrowBatch
+    from test_gpu_narrow import _bitmaps
+    if wl == "fuzz":
+        manifest = W.DEFAULT_TEST_MANIFEST
+        rules = W.fuzz_rules(600, seed=95, depth=3)
+        batch = BagBatch.from_bags(W.fuzz_bags(4000, seed=96, p_wrong=0.0), names=list(manifest))  # (wrong kinds: no narrow column)
+    elif wl == "c1":
+        manifest, rules, batch = W.c1_workload(6000)
+    elif wl == "c4":
+        manifest, rules, batch = W.c4_workload(n_rules=1500, n_requests=12000, seed=97)
+    else:
+        manifest, rules, conf, batch = W.resolver_workload(n_rules=300, n_requests=3000, seed=98)
+    mh, eh, _ = _run(mxp, monkeypatch, True, manifest, rules, batch)
+    monkeypatch.setenv("MXP_HOST_PACK", "0")
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    nb = NarrowBatch(batch)
+    assert nb.narrow.any()
+    md, ed = _bitmaps(eng.upload2(nb), batch.n, len(rules))
+    assert np.array_equal(mh, md.view(np.uint32)) and np.array_equal(eh, ed.view(np.uint32))
