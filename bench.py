@@ -503,15 +503,22 @@ def end_to_end(g, shard_sets, n_rules, reps, wire="narrow"):
     sel_bytes = int(off[-1]) * (2 if ids16 else 4)
     err_requests = int((status == 3).sum())
     selected = float(off[-1]) / max(n, 1)
-    # pipelined: upload k + 1 ahead of Resolve k
+    # pipelined: batch k's evaluation submitted (mxp_group_resolve_submit), batch k + 1 uploaded while
+    # it runs -- the upload's host checks and packing overlap the device -- then k finished
+    # (BENCH_PIPE_SUBMIT=0: the one-call Resolve after the upload, the round-5 order, A/B)
+    split = os.environ.get("BENCH_PIPE_SUBMIT", "1") != "0"
     steps = max(3 * reps, 6)
     nxt = upload_set(g, sets[0], wire, True)
     t0 = time.perf_counter()
     for k in range(steps):
         cur = nxt
+        job = g.resolve_submit(cur, 0, ids16=ids16) if split else None
         if k + 1 < steps:
             nxt = upload_set(g, sets[(k + 1) % len(sets)], wire, True)
-        g.resolve_arrays(None if narrow else sets[k % len(sets)], 0, cap, ids16=ids16, out=out, uploaded=cur)
+        if split:
+            g.resolve_finish(job, cap, out=out)
+        else:
+            g.resolve_arrays(None if narrow else sets[k % len(sets)], 0, cap, ids16=ids16, out=out, uploaded=cur)
     t_pipe = (time.perf_counter() - t0) / steps
     G = len(shards)
     return {"pairs_per_s": n * n_rules / t, "requests_per_s": n / t, "ms_per_batch": t * 1e3,
@@ -521,8 +528,10 @@ def end_to_end(g, shard_sets, n_rules, reps, wire="narrow"):
             "x_action_list_at_50GBps": t * 1e3 / max(sel_bytes / G / 50e9 * 1e3, 1e-9),
             "pipelined": {"ms_per_batch": t_pipe * 1e3, "requests_per_s": n / t_pipe, "pairs_per_s": n * n_rules / t_pipe,
                           "batches": steps, "x_action_list_at_50GBps": t_pipe * 1e3 / max(sel_bytes / G / 50e9 * 1e3, 1e-9),
-                          "path": "mxp_group_upload(batch k + 1, MXP_UPLOAD_NO_WAIT) then mxp_group_resolve_uploaded(batch k); "
-                                  "three pinned shard sets alternating; wall time per batch"},
+                          "path": ("mxp_group_resolve_submit(batch k), mxp_group_upload(batch k + 1, MXP_UPLOAD_NO_WAIT), "
+                                   "mxp_group_resolve_finish(batch k)" if split else
+                                   "mxp_group_upload(batch k + 1, MXP_UPLOAD_NO_WAIT) then mxp_group_resolve_uploaded(batch k)")
+                                  + "; three pinned shard sets alternating; wall time per batch"},
             "host_memory": "pinned shards and outputs (mxp_host_alloc arenas)", "wire": wire,
             "h2d_bytes_per_batch": int(h2d[0] / G),
             "path": ("host columnar shards -> %s -> host action lists of the whole batch (per member: device pack + "

@@ -206,6 +206,19 @@ int mxp_resolve_batch_ex(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t v
  * one; the caller does not mxp_batch_free it. */
 int mxp_resolve_uploaded(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
                          uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap);
+/* mxp_resolve_uploaded in two calls.  mxp_resolve_submit enqueues the batch's evaluation and request
+ * namespaces and returns without waiting for the device; mxp_resolve_finish waits for them, resolves
+ * and downloads (mxp_resolve_uploaded's outputs and errors).  Between the two the caller may upload
+ * the next batch on the same engine (mxp_batch_upload_ex / mxp_batch_upload2, MXP_UPLOAD_NO_WAIT):
+ * its host checks and packing then overlap this evaluation on the device -- the single-threaded
+ * micro-batcher's pipeline -- and makes no other call on the engine.  submit takes db over whatever
+ * it returns; after a successful submit, finish is called once (it frees the job, whatever it
+ * returns). */
+typedef struct mxp_resolve_job mxp_resolve_job;
+int mxp_resolve_submit(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
+                       mxp_resolve_job** out);
+int mxp_resolve_finish(mxp_resolve_job* job, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules,
+                       uint64_t sel_cap);
 /* mxp_resolve_batch plus each Resolve's referenced attributes (mxp_attr_ref, as mxp_eval_refs): the
  * identity attribute; when it is a string, context.protocol (filterActions, resolver.go:208); and the
  * reads of the predicates filterActions evaluates, in order, up to and including the first that

@@ -162,6 +162,16 @@ int mxp_group_resolve_batch(mxp_group* g, const mxp_bag_batch* const* shards, ui
 int mxp_group_resolve_uploaded(mxp_group* g, mxp_gbatch* gb, const mxp_bag_batch* const* shards, uint32_t n_shards,
                                uint32_t variety, uint32_t flags, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off,
                                void* sel_rules, uint64_t sel_cap);
+/* mxp_group_resolve_uploaded in two calls (mxp_resolve_submit / mxp_resolve_finish on every member):
+ * submit enqueues every member's evaluation and returns; between the two the caller may upload the
+ * next batch (mxp_group_upload / _upload2, MXP_UPLOAD_NO_WAIT) and make no other group call; finish
+ * resolves into the whole batch's arrays.  submit takes gb over; after a successful submit, finish
+ * is called once. */
+typedef struct mxp_gresolve mxp_gresolve;
+int mxp_group_resolve_submit(mxp_group* g, mxp_gbatch* gb, const mxp_bag_batch* const* shards, uint32_t n_shards,
+                             uint32_t variety, uint32_t flags, mxp_gresolve** out);
+int mxp_group_resolve_finish(mxp_group* g, mxp_gresolve* r, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off,
+                             void* sel_rules, uint64_t sel_cap);
 int mxp_group_resolve_split(mxp_group* g, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags, uint8_t* status,
                             uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap);
 int mxp_group_pair_error(mxp_group* g, uint64_t request, uint32_t rule, char* buf, uint32_t cap);

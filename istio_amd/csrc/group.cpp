@@ -342,6 +342,11 @@ struct SplitView {
 
 }  // namespace
 
+// (resolver.cpp) a member's finish with the group's placement, and dropping a submitted job
+int mxp_resolve_finish_placed(mxp_resolve_job* job, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off,
+                              void* sel_rules, const mxp_resolve_place& place);
+void mxp_resolve_job_free(mxp_resolve_job* job);
+
 extern "C" {
 
 void mxp_group_shard_bounds(uint64_t n_total, uint32_t member, uint32_t n_members, uint64_t* lo, uint64_t* hi) {
@@ -1025,6 +1030,119 @@ static int group_resolve(mxp_group* g, mxp_gbatch* gb, const mxp_bag_batch* cons
         return MXP_OK;
     });
     sel_off[g->lo[n_shards]] = total;
+    if (rc) return rc;
+    return total <= sel_cap ? MXP_OK : MXP_ERR_NOMEM;
+}
+
+// ---- the two-call Resolve (mxp_group_resolve_submit / _finish; the member calls: above extern "C")
+
+struct mxp_gresolve {
+    std::vector<mxp_resolve_job*> jobs;  // per member (null: its submit failed)
+    std::vector<uint64_t> lo;            // the batch's shard bounds (an upload in between moves g->lo)
+    std::vector<uint64_t> cnt;
+};
+
+int mxp_group_resolve_submit(mxp_group* g, mxp_gbatch* gb, const mxp_bag_batch* const* shards, uint32_t n_shards,
+                             uint32_t variety, uint32_t flags, mxp_gresolve** out) {
+    std::unique_ptr<mxp_gbatch, std::function<void(mxp_gbatch*)>> own(gb, [g](mxp_gbatch* b) {
+        mxp_group_batch_free(g, b);  // (the members' batches not handed to their submit)
+    });
+    if (!g || !gb || !out || n_shards != g->size() || gb->db.size() != n_shards) return MXP_ERR_ARG;
+    for (uint32_t k = 0; k < n_shards; k++)
+        if (shards && (!shards[k] || gb->n[k] != shards[k]->n_requests)) return MXP_ERR_ARG;
+    DeviceGuard guard;
+    std::unique_ptr<mxp_gresolve> r(new mxp_gresolve());
+    r->jobs.assign(n_shards, nullptr);
+    r->cnt.assign(gb->n.begin(), gb->n.end());
+    g->set_bounds(r->cnt);
+    r->lo = g->lo;
+    int rc = g->each([&](uint32_t k) -> int {
+        mxp_dbatch* db = nullptr;
+        std::swap(db, gb->db[k]);  // (taken over by the member's submit)
+        return mxp_resolve_submit(g->m[k].eng, db, shards ? shards[k] : nullptr, variety, flags, &r->jobs[k]);
+    });
+    if (rc) {
+        for (mxp_resolve_job* j : r->jobs)
+            if (j) mxp_resolve_job_free(j);
+        return rc;
+    }
+    *out = r.release();
+    return MXP_OK;
+}
+
+int mxp_group_resolve_finish(mxp_group* g, mxp_gresolve* r0, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off,
+                             void* sel_rules, uint64_t sel_cap) {
+    std::unique_ptr<mxp_gresolve> r(r0);
+    if (!g || !r || r->jobs.size() != g->size()) {
+        if (r)
+            for (mxp_resolve_job*& j : r->jobs) mxp_resolve_job_free(j), j = nullptr;
+        return MXP_ERR_ARG;
+    }
+    auto drop = [&] {
+        for (mxp_resolve_job*& j : r->jobs)
+            if (j) mxp_resolve_job_free(j), j = nullptr;
+    };
+    if (!status || !err_rule || !sel_off || (sel_cap && !sel_rules)) {
+        drop();
+        return MXP_ERR_ARG;
+    }
+    DeviceGuard guard;
+    const uint32_t n_shards = g->size();
+    g->lo = r->lo;  // (pair errors and locate refer to this batch again)
+    // as group_resolve: every member resolves into the caller's arrays, its ids at the base the
+    // members agree on once each knows its own count
+    std::mutex mu;
+    std::condition_variable cv;
+    uint32_t arrived = 0;
+    std::vector<uint64_t> total_k(n_shards, 0);
+    std::vector<bool> in(n_shards, false);
+    auto arrive = [&](uint32_t k, uint64_t t) {
+        std::lock_guard<std::mutex> l(mu);
+        if (in[k]) return;
+        in[k] = true;
+        total_k[k] = t;
+        if (++arrived == n_shards) cv.notify_all();
+    };
+    std::atomic<bool> failed{false};
+    int rc = g->each([&](uint32_t k) -> int {
+        const uint64_t lo = r->lo[k];
+        const mxp_resolve_place place = [&](uint64_t t) -> int64_t {
+            arrive(k, t);
+            {
+                std::unique_lock<std::mutex> l(mu);
+                cv.wait(l, [&] { return arrived == n_shards; });
+            }
+            if (failed.load()) return -1;
+            uint64_t base = 0, sum = 0;
+            for (uint32_t j = 0; j < n_shards; j++) {
+                if (j < k) base += total_k[j];
+                sum += total_k[j];
+            }
+            return sum <= sel_cap ? (int64_t)base : -1;
+        };
+        mxp_resolve_job* job = nullptr;
+        std::swap(job, r->jobs[k]);
+        const int rr = mxp_resolve_finish_placed(job, status + lo, err_rule + lo, sel_off + lo, sel_rules, place);
+        if (rr && rr != MXP_ERR_NOMEM) failed.store(true);
+        arrive(k, 0);  // (a member that failed before its count still lets the others go on)
+        return rr == MXP_ERR_NOMEM ? MXP_OK : rr;
+    });
+    if (rc) return rc;
+    uint64_t total = 0;
+    std::vector<uint64_t> base(n_shards, 0);
+    for (uint32_t k = 0; k < n_shards; k++) {
+        base[k] = total;
+        total += total_k[k];
+    }
+    rc = g->each([&](uint32_t k) -> int {  // (the batch-local offsets rebased, as group_resolve)
+        const uint64_t lo = r->lo[k], n = r->cnt[k], b = base[k];
+        if (!n) return MXP_OK;
+        sel_off[lo] = b;
+        if (b)
+            for (uint64_t i = 1; i < n; i++) sel_off[lo + i] += b;
+        return MXP_OK;
+    });
+    sel_off[r->lo[n_shards]] = total;
     if (rc) return rc;
     return total <= sel_cap ? MXP_OK : MXP_ERR_NOMEM;
 }

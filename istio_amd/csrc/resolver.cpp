@@ -191,68 +191,85 @@ void first_errors(mxp_engine* eng, uint32_t n, uint32_t variety, const uint32_t*
     }
 }
 
-// mxp_resolve_batch(_ex), and with ref_off its referenced attributes (mxp_resolve_refs).
-//
-// Compact path (round 5; not for referenced attributes): the evaluation writes the match bitmap and
-// per-request error flags with error records instead of the error bitmap; namespaces come from the
-// device (mxp_ns_kernel on the batch as uploaded); each failing request's first applicable error is
-// found from the records on the host and scattered to the device; the counts are scanned on the
-// device.  Records past the log's capacity fall back to the error bitmap.
-int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, bool ids16, uint8_t* status,
-                 uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap, uint64_t* ref_off,
-                 mxp_attr_ref* refs, uint64_t ref_cap, const mxp_resolve_place* place = nullptr,
-                 mxp_dbatch* pre = nullptr) {
-    std::unique_ptr<mxp_dbatch> db(pre);  // (a batch uploaded before: taken over, whatever happens)
-    if (!eng || !batch || !status || !err_rule || !sel_off || (sel_cap && !sel_rules) || variety >= 32)
-        return MXP_ERR_ARG;
-    if (pre && (ref_off || pre->n != batch->n_requests))
+}  // namespace
+
+// A Resolve in two phases (resolve_impl runs both; mxp_resolve_submit / _finish let a caller work
+// between them): begin enqueues the evaluation and the request namespaces and returns without
+// waiting for the device; end waits, finds the first errors, counts, places and downloads.
+struct mxp_resolve_job {
+    mxp_engine* eng = nullptr;
+    const mxp_bag_batch* batch = nullptr;
+    uint32_t variety = 0;
+    bool ids16 = false;
+    bool compact = false;
+    uint32_t n = 0, W = 0;
+    uint64_t* ref_off = nullptr;
+    mxp_attr_ref* refs = nullptr;
+    uint64_t ref_cap = 0;
+    std::unique_ptr<mxp_dbatch> db;
+    std::vector<mxp_ref_rec> recs;
+    std::vector<uint32_t> info;  // host copy of the namespaces (host pass; referenced attributes)
+    const uint32_t* hinfo = nullptr;
+};
+
+namespace {
+
+int resolve_begin(mxp_resolve_job& J) {
+    mxp_engine* eng = J.eng;
+    const mxp_bag_batch* batch = J.batch;
+    const uint32_t variety = J.variety;
+    mxp_dbatch* pre = J.db.get();
+    if (pre && (J.ref_off || pre->n != batch->n_requests))
         return eng->fail(MXP_ERR_ARG, "resolve: the uploaded batch is not this batch");
     if (pre && eng->device >= 0 && hipSetDevice(eng->device) != hipSuccess) return eng->fail(MXP_ERR_DEVICE, "hipSetDevice");
     if (!eng->resolver.set) return eng->fail(MXP_ERR_STATE, "resolver not configured (mxp_resolver_set)");
     const auto& R = eng->resolver;
-    const uint32_t n = batch->n_requests;
+    const uint32_t n = J.n = batch->n_requests;
     const uint32_t NR = (uint32_t)eng->rules.size();
-    const uint32_t W = (NR + 31) / 32;
-    if (ids16 && NR > 65536u) return eng->fail(MXP_ERR_ARG, "u16 rule ids: more than 65536 rules");
+    const uint32_t W = J.W = (NR + 31) / 32;
+    if (J.ids16 && NR > 65536u) return eng->fail(MXP_ERR_ARG, "u16 rule ids: more than 65536 rules");
     DevBuf& dm = eng->res_dm;  // (engine-owned scratch: no allocation per call once large enough)
     DevBuf& de = eng->res_de;
-    std::vector<mxp_ref_rec> recs;
     hipError_t e;
     int rc;
-    const bool compact = !ref_off && !(eng->debug_flags & kResolveBitmap);
-    if (compact) {
-        if (eng->device >= 0 && (e = eng->res_flags.reserve(n ? n : 1)) != hipSuccess) return eng->hipfail(e, "alloc flags");
-        if (pre) {
-            rc = eng->evaluate_uploaded(db.get(), dm, de, nullptr, eng->res_flags.as<uint8_t>());
-        } else {
-            rc = eng->evaluate(batch, dm, de, nullptr, db, eng->res_flags.as<uint8_t>());
-        }
-    } else {
-        rc = ref_off ? eng->refs_evaluate(batch, dm, de, db, recs)
-             : pre     ? eng->evaluate_uploaded(db.get(), dm, de, nullptr, nullptr)
-                       : eng->evaluate(batch, dm, de, nullptr, db);
-    }
-    if (rc) return rc;
-    // per-word masks: applicability for the variety (per request tcp flag), empty matches
-    std::vector<uint32_t> amask(2 * (size_t)W, 0), empty(W, 0);
+    // the resolver's tables first, before the evaluation is queued: a copy from pageable memory
+    // returns only once the stream has reached it, so behind the evaluation it would hold the
+    // caller until the kernels end (r6_s25: 0.79 ms)
+    std::vector<uint32_t> amask(2 * (size_t)W, 0), empty(W, 0);  // per-word masks: variety / tcp, empty matches
     for (uint32_t r = 0; r < NR; r++) {
         const uint32_t bit = 1u << (r & 31);
         if ((R.vmask[r] >> variety) & 1u) amask[(size_t)R.tcp[r] * W + r / 32] |= bit;
         if (R.empty[r]) empty[r / 32] |= bit;
     }
     DevBuf &d_info = eng->res_info, &d_lo = eng->res_lo, &d_hi = eng->res_hi, &d_amask = eng->res_amask,
-           &d_empty = eng->res_empty, &d_status = eng->res_status, &d_err_rule = eng->res_err_rule,
-           &d_count = eng->res_count, &d_off = eng->res_off, &d_sel = eng->res_sel;
+           &d_empty = eng->res_empty;
     auto up = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
         if ((e = d.reserve(bytes)) != hipSuccess) return eng->hipfail(e, what);
         if (bytes && (e = hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, eng->stream)) != hipSuccess)
             return eng->hipfail(e, what);
         return MXP_OK;
     };
+    if ((rc = up(d_lo, R.ns_lo.data(), R.ns_lo.size() * 4, "upload ns_lo"))) return rc;
+    if ((rc = up(d_hi, R.ns_hi.data(), R.ns_hi.size() * 4, "upload ns_hi"))) return rc;
+    if ((rc = up(d_amask, amask.data(), amask.size() * 4, "upload amask"))) return rc;
+    if ((rc = up(d_empty, empty.data(), empty.size() * 4, "upload empty"))) return rc;
+    J.compact = !J.ref_off && !(eng->debug_flags & kResolveBitmap);
+    if (J.compact) {
+        if (eng->device >= 0 && (e = eng->res_flags.reserve(n ? n : 1)) != hipSuccess) return eng->hipfail(e, "alloc flags");
+        if (pre) {
+            rc = eng->evaluate_uploaded(J.db.get(), dm, de, nullptr, eng->res_flags.as<uint8_t>());
+        } else {
+            rc = eng->evaluate(batch, dm, de, nullptr, J.db, eng->res_flags.as<uint8_t>());
+        }
+    } else {
+        rc = J.ref_off ? eng->refs_evaluate(batch, dm, de, J.db, J.recs)
+             : pre     ? eng->evaluate_uploaded(J.db.get(), dm, de, nullptr, nullptr)
+                       : eng->evaluate(batch, dm, de, nullptr, J.db);
+    }
+    if (rc) return rc;
     // request namespaces: on the device from the batch as uploaded (pack_device), else on the host
-    std::vector<uint32_t> info;  // host copy (host pass; referenced attributes)
-    const uint32_t* hinfo = nullptr;
-    if (db->res_raw && !ref_off) {
+    mxp_dbatch* db = J.db.get();
+    if (db->res_raw && !J.ref_off) {
         if ((e = d_info.reserve((size_t)n * 4 + 4)) != hipSuccess) return eng->hipfail(e, "alloc nsinfo");
         mxp_ns_args N;
         memset(&N, 0, sizeof N);
@@ -272,15 +289,41 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
         eng->trace_mark("request namespaces (device)");
     } else {
         if (db->wide && batch == &db->wide->view) db->wide->materialize();  // (a narrow upload)
-        request_info(eng, batch, &info);
-        hinfo = info.data();
+        request_info(eng, batch, &J.info);
+        J.hinfo = J.info.data();
         eng->trace_mark("request namespaces (host)");
-        if ((rc = up(d_info, info.data(), info.size() * 4, "upload nsinfo"))) return rc;
+        if ((rc = up(d_info, J.info.data(), J.info.size() * 4, "upload nsinfo"))) return rc;
     }
-    if ((rc = up(d_lo, R.ns_lo.data(), R.ns_lo.size() * 4, "upload ns_lo"))) return rc;
-    if ((rc = up(d_hi, R.ns_hi.data(), R.ns_hi.size() * 4, "upload ns_hi"))) return rc;
-    if ((rc = up(d_amask, amask.data(), amask.size() * 4, "upload amask"))) return rc;
-    if ((rc = up(d_empty, empty.data(), empty.size() * 4, "upload empty"))) return rc;
+    return MXP_OK;
+}
+
+int resolve_end(mxp_resolve_job& J, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules,
+                uint64_t sel_cap, const mxp_resolve_place* place) {
+    mxp_engine* eng = J.eng;
+    const mxp_bag_batch* batch = J.batch;
+    const uint32_t variety = J.variety, n = J.n, W = J.W;
+    const bool ids16 = J.ids16, compact = J.compact;
+    uint64_t* ref_off = J.ref_off;
+    mxp_attr_ref* refs = J.refs;
+    const uint64_t ref_cap = J.ref_cap;
+    auto& db = J.db;
+    auto& recs = J.recs;
+    auto& info = J.info;
+    const uint32_t* hinfo = J.hinfo;
+    const auto& R = eng->resolver;
+    DevBuf& dm = eng->res_dm;
+    DevBuf& de = eng->res_de;
+    DevBuf &d_info = eng->res_info, &d_lo = eng->res_lo, &d_hi = eng->res_hi, &d_amask = eng->res_amask,
+           &d_empty = eng->res_empty, &d_status = eng->res_status, &d_err_rule = eng->res_err_rule,
+           &d_count = eng->res_count, &d_off = eng->res_off, &d_sel = eng->res_sel;
+    hipError_t e;
+    int rc;
+    auto up = [&](DevBuf& d, const void* src, size_t bytes, const char* what) -> int {
+        if ((e = d.reserve(bytes)) != hipSuccess) return eng->hipfail(e, what);
+        if (bytes && (e = hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, eng->stream)) != hipSuccess)
+            return eng->hipfail(e, what);
+        return MXP_OK;
+    };
     if ((e = d_status.reserve(n)) != hipSuccess) return eng->hipfail(e, "alloc status");
     if ((e = d_err_rule.reserve((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err_rule");
     if ((e = d_count.reserve((size_t)n * 4)) != hipSuccess) return eng->hipfail(e, "alloc count");
@@ -407,6 +450,33 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
     return ref_rc;
 }
 
+
+// mxp_resolve_batch(_ex), and with ref_off its referenced attributes (mxp_resolve_refs).
+//
+// Compact path (round 5; not for referenced attributes): the evaluation writes the match bitmap and
+// per-request error flags with error records instead of the error bitmap; namespaces come from the
+// device (mxp_ns_kernel on the batch as uploaded); each failing request's first applicable error is
+// found from the records on the host and scattered to the device; the counts are scanned on the
+// device.  Records past the log's capacity fall back to the error bitmap.
+int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, bool ids16, uint8_t* status,
+                 uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap, uint64_t* ref_off,
+                 mxp_attr_ref* refs, uint64_t ref_cap, const mxp_resolve_place* place = nullptr,
+                 mxp_dbatch* pre = nullptr) {
+    mxp_resolve_job J;
+    J.db.reset(pre);  // (a batch uploaded before: taken over, whatever happens)
+    if (!eng || !batch || !status || !err_rule || !sel_off || (sel_cap && !sel_rules) || variety >= 32)
+        return MXP_ERR_ARG;
+    J.eng = eng;
+    J.batch = batch;
+    J.variety = variety;
+    J.ids16 = ids16;
+    J.ref_off = ref_off;
+    J.refs = refs;
+    J.ref_cap = ref_cap;
+    if (int rc = resolve_begin(J)) return rc;
+    return resolve_end(J, status, err_rule, sel_off, sel_rules, sel_cap, place);
+}
+
 }  // namespace
 
 int mxp_resolve_placed(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
@@ -420,6 +490,15 @@ int mxp_resolve_placed(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* bat
     return resolve_impl(eng, batch, variety, (flags & MXP_RESOLVE_IDS_U16) != 0, status, err_rule, sel_off, sel_rules,
                         0, nullptr, nullptr, 0, &place, db);
 }
+
+// (group.cpp) a member's finish with its ids placed by the group, and dropping a submitted job
+int mxp_resolve_finish_placed(mxp_resolve_job* job, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off,
+                              void* sel_rules, const mxp_resolve_place& place) {
+    std::unique_ptr<mxp_resolve_job> J(job);
+    if (!J) return MXP_ERR_ARG;
+    return resolve_end(*J, status, err_rule, sel_off, sel_rules, 0, &place);
+}
+void mxp_resolve_job_free(mxp_resolve_job* job) { delete job; }
 
 extern "C" {
 
@@ -445,6 +524,29 @@ int mxp_resolve_uploaded(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* b
     }
     return resolve_impl(eng, batch, variety, (flags & MXP_RESOLVE_IDS_U16) != 0, status, err_rule, sel_off, sel_rules,
                         sel_cap, nullptr, nullptr, 0, nullptr, db);
+}
+
+int mxp_resolve_submit(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
+                       mxp_resolve_job** out) {
+    std::unique_ptr<mxp_resolve_job> J(new mxp_resolve_job());
+    J->db.reset(db);  // (taken over, whatever happens)
+    if (!eng || !db || !out || (flags & ~(uint32_t)MXP_RESOLVE_IDS_U16) || variety >= 32) return MXP_ERR_ARG;
+    if (!batch && db->wide) batch = &db->wide->view;  // (a narrow upload: its host view)
+    if (!batch) return MXP_ERR_ARG;
+    J->eng = eng;
+    J->batch = batch;
+    J->variety = variety;
+    J->ids16 = (flags & MXP_RESOLVE_IDS_U16) != 0;
+    if (int rc = resolve_begin(*J)) return rc;
+    *out = J.release();
+    return MXP_OK;
+}
+
+int mxp_resolve_finish(mxp_resolve_job* job, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules,
+                       uint64_t sel_cap) {
+    std::unique_ptr<mxp_resolve_job> J(job);
+    if (!J || !status || !err_rule || !sel_off || (sel_cap && !sel_rules)) return MXP_ERR_ARG;
+    return resolve_end(*J, status, err_rule, sel_off, sel_rules, sel_cap, nullptr);
 }
 
 int mxp_resolve_refs(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, uint8_t* status,

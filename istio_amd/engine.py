@@ -152,6 +152,10 @@ SIGNATURES = {
                                                _VP, _VP, ctypes.c_uint64]),
     "mxp_group_resolve_uploaded": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _VP,
                                                   _VP, _VP, _VP, ctypes.c_uint64]),
+    "mxp_resolve_submit": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint32, ctypes.c_uint32, _VP]),
+    "mxp_resolve_finish": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, ctypes.c_uint64]),
+    "mxp_group_resolve_submit": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _VP]),
+    "mxp_group_resolve_finish": (ctypes.c_int, [_VP, _VP, _VP, _VP, _VP, _VP, ctypes.c_uint64]),
     "mxp_resolve_uploaded": (ctypes.c_int, [_VP, _VP, _VP, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP, _VP, _VP,
                                             ctypes.c_uint64]),
     "mxp_group_resolve_split": (ctypes.c_int, [_VP, _VP, ctypes.c_uint32, ctypes.c_uint32, _VP, _VP, _VP, _VP,
@@ -606,6 +610,25 @@ class Engine:
                                                   1 if ids16 else 0,
                                                   status.ctypes.data, err_rule.ctypes.data, off.ctypes.data,
                                                   sel.ctypes.data, cap), "mxp_resolve_uploaded")
+        return status, err_rule, off, sel[:int(off[n])]
+
+    def resolve_submit(self, db: "DeviceBatch", variety: int, ids16: bool = False):
+        """mxp_resolve_submit: the evaluation of an uploaded batch enqueued (db taken over) -> a job for
+        resolve_finish; the engine takes only an upload in between."""
+        batch, cs = db._src
+        h, db.h = db.h, None
+        job = _VP()
+        self._check(self.lib.mxp_resolve_submit(self.h, h, ctypes.byref(cs) if cs is not None else None, variety,
+                                                1 if ids16 else 0, ctypes.byref(job)), "mxp_resolve_submit")
+        return (job, batch.n, ids16)
+
+    def resolve_finish(self, job, cap: int):
+        """mxp_resolve_finish -> (status, err_rule, sel_off, sel_rules) as resolve_uploaded."""
+        h, n, ids16 = job
+        status, err_rule = np.empty(n, dtype=np.uint8), np.empty(n, dtype=np.uint32)
+        off, sel = np.empty(n + 1, dtype=np.uint64), np.empty(max(cap, 1), dtype=np.uint16 if ids16 else np.uint32)
+        self._check(self.lib.mxp_resolve_finish(h, status.ctypes.data, err_rule.ctypes.data, off.ctypes.data,
+                                                sel.ctypes.data, cap), "mxp_resolve_finish")
         return status, err_rule, off, sel[:int(off[n])]
 
     def resolve(self, batch: BagBatch, variety: int, ids16: bool = False):
@@ -1188,6 +1211,34 @@ class Group:
                 continue
             self._check(rc, "mxp_group_resolve_batch")
             break
+        return status[:n], err_rule[:n], off[:n + 1], sel[:int(off[n])]
+
+    def resolve_submit(self, uploaded: "GroupBatch", variety: int, ids16: bool = False):
+        """mxp_group_resolve_submit: every member's evaluation of the uploaded shards enqueued (taken
+        over) -> a job for resolve_finish; only an upload may come in between."""
+        if uploaded._src[1] is None:  # (narrow uploads: the members keep the host views)
+            arr = None
+        else:
+            cs = uploaded._src[1]
+            arr = (_VP * len(cs))(*[ctypes.addressof(c) for c in cs])
+        h, uploaded.h = uploaded.h, None
+        job = _VP()
+        self._check(self.lib.mxp_group_resolve_submit(self.h, h, arr, self.n, variety, 1 if ids16 else 0,
+                                                      ctypes.byref(job)), "mxp_group_resolve_submit")
+        return (job, uploaded.n, ids16, uploaded._src)
+
+    def resolve_finish(self, job, cap: int, out=None):
+        """mxp_group_resolve_finish -> (status, err_rule, sel_off, sel_rules) of the whole batch."""
+        h, n, ids16, _src = job
+        if out is not None and len(out[3]) >= cap:
+            status, err_rule, off, sel = out
+        else:
+            status, err_rule, off = (np.empty(n, dtype=np.uint8), np.empty(n, dtype=np.uint32),
+                                     np.empty(n + 1, dtype=np.uint64))
+            sel = np.empty(max(cap, 1), dtype=np.uint16 if ids16 else np.uint32)
+        self._check(self.lib.mxp_group_resolve_finish(self.h, h, status.ctypes.data, err_rule.ctypes.data,
+                                                      off.ctypes.data, sel.ctypes.data, len(sel)),
+                    "mxp_group_resolve_finish")
         return status[:n], err_rule[:n], off[:n + 1], sel[:int(off[n])]
 
     def resolve(self, shards: Sequence[BagBatch], variety: int, ids16: bool = False):

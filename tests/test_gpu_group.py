@@ -237,11 +237,13 @@ def test_finder_vocabulary_over_group(mxp):
 
 
 @pytest.mark.parametrize("devices", [None, [0, 0]])
-def test_resolve_uploaded_pipeline(mxp, devices):
+@pytest.mark.parametrize("split", [False, True])
+def test_resolve_uploaded_pipeline(mxp, devices, split):
     """mxp_resolve_uploaded / mxp_group_resolve_uploaded: batch k + 1 uploaded (MXP_UPLOAD_NO_WAIT)
     before batch k is resolved -- as bench.py's pipelined end-to-end figure and a double-buffering
     micro-batcher do -- gives each batch exactly the plain Resolve's statuses, first-error rules,
-    action lists and error texts."""
+    action lists and error texts.  split: the two-call Resolve (mxp_resolve_submit / _finish), batch
+    k + 1 uploaded between batch k's submit and finish."""
     manifest, _, _ = W.c2_workload(n_rules=1500, n_requests=1, seed=2)
     rules = W.c2_rules(1500, seed=2)[0]
     R = len(rules)
@@ -268,9 +270,10 @@ def test_resolve_uploaded_pipeline(mxp, devices):
         nxt = eng.upload(batches[0], no_wait=True)
         for k, b in enumerate(batches):
             cur = nxt
+            job = eng.resolve_submit(cur, 0, ids16=True) if split else None
             if k + 1 < len(batches):
                 nxt = eng.upload(batches[k + 1], no_wait=True)
-            got = eng.resolve_uploaded(cur, 0, cap=1 << 22, ids16=True)
+            got = eng.resolve_finish(job, 1 << 22) if split else eng.resolve_uploaded(cur, 0, cap=1 << 22, ids16=True)
             for a, c in zip(got, want[k]):
                 assert np.array_equal(a, c), k
             err = np.nonzero(want[k][0] == 3)[0][:40]
@@ -280,13 +283,15 @@ def test_resolve_uploaded_pipeline(mxp, devices):
     g.set_vocabulary(manifest)
     g.compile(rules)
     g.set_resolver("destination.service", "istio-system", ns, vm, z, z)
-    split = [W.split_batch(b, len(devices)) for b in batches]
-    nxt = g.upload(split[0], no_wait=True)
+    shards = [W.split_batch(b, len(devices)) for b in batches]
+    nxt = g.upload(shards[0], no_wait=True)
     for k in range(len(batches)):
         cur = nxt
+        job = g.resolve_submit(cur, 0, ids16=True) if split else None
         if k + 1 < len(batches):
-            nxt = g.upload(split[k + 1], no_wait=True)
-        got = g.resolve_arrays(split[k], 0, cap=1 << 22, ids16=True, uploaded=cur)
+            nxt = g.upload(shards[k + 1], no_wait=True)
+        got = (g.resolve_finish(job, 1 << 22) if split
+               else g.resolve_arrays(shards[k], 0, cap=1 << 22, ids16=True, uploaded=cur))
         for a, c in zip(got, want[k]):
             assert np.array_equal(a, c), k
         err = np.nonzero(want[k][0] == 3)[0][:40]
