@@ -1771,6 +1771,7 @@ int mxp_engine::launch_body(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, ui
     // (no stale flags from the previous evaluation survive an early return below)
     last_dtp = false;
     last_dtp_counted = false;
+    last_pairs.on = false;
     // guards on: guard-only groups through the lean kernel, the rest through the VM kernel;
     // guards off (Eval, ablation): every group through the VM kernel
     const bool guards_on = !d_vals && !(debug_flags & 2u);
@@ -2004,6 +2005,20 @@ int mxp_engine::launch_body(mxp_dbatch* db, hipStream_t s, uint32_t* d_match, ui
         AF.dtp_slots = AI.dtp_slots;
         AF.dtp_qn = AI.dtp_qn;
         AF.dtp_tiles = tiles;
+        // a pair Resolve's evaluation: every word a plain fill chunk's (no lean / VM / deep groups, no
+        // value classes), so the filed pairs are the match bitmap -- the fills store it only if some
+        // pair overflowed its list or slots (kargs.dtp_lazy)
+        if (pair_req && P->n_fills && !P->n_vtfills && !P->n_glean && !P->n_gvm && !P->n_gdeep && !A.n_vt &&
+            !A.out_err) {
+            AF.dtp_lazy = ovf_n;
+            last_pairs.on = true;
+            last_pairs.ovf_n = ovf_n;
+            last_pairs.slots = AI.dtp_slots;
+            last_pairs.qn = AI.dtp_qn;
+            last_pairs.fills = P->d_fills.as<uint32_t>();
+            last_pairs.row = MXP_DTP_ROW(tiles);
+            last_pairs.nch = P->n_fills;
+        }
         for (uint32_t c = 0; c < K; c++) {
             const uint32_t t0 = (uint32_t)((uint64_t)tiles * c / K), t1 = (uint32_t)((uint64_t)tiles * (c + 1) / K);
             AI.q0 = t0 * 1024u;
@@ -2238,6 +2253,7 @@ int mxp_engine_create(int device, mxp_engine** out) {
     if (const char* f = getenv("MXP_TRACE")) e->trace = atoi(f) != 0;
     if (const char* f = getenv("MXP_D2H_DMA")) e->d2h_dma = atoi(f) != 0;
     if (const char* f = getenv("MXP_RESOLVE_TILE")) e->resolve_tile = atoi(f) != 0;
+    if (const char* f = getenv("MXP_RESOLVE_PAIRS")) e->resolve_pairs = atoi(f);
     if (const char* f = getenv("MXP_LAZY_RECORDS")) e->lazy_records = atoi(f) != 0;
     if (const char* f = getenv("MXP_PACK_COLS_BESIDE")) e->pack_cols_beside = atoi(f) != 0;
     if (const char* f = getenv("MXP_DTP")) e->dtp = atoi(f) != 0;

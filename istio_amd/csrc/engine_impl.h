@@ -565,6 +565,20 @@ struct mxp_engine : public mxp::LowerTables {
     DevBuf d_dtp_ent, d_dtp_n, d_dtp_ovf, d_dtp_ovf_n, d_dtp_slots, d_dtp_qn;
     bool last_dtp = false;  // the last launch deferred its index pairs (mxp_kernel_times [2])
     bool last_dtp_counted = false;  // ... and counted every true pair in its kernels (no streamed counters)
+    // pair Resolve (resolver.cpp): the resolver asks (pair_req) that the next evaluation leave the match
+    // bitmap unwritten when every word is a plain fill chunk's; last_pairs is where that evaluation
+    // filed its deferred pairs (on: it did; its fills stored the bitmap only if *ovf_n, its overflow
+    // count, is nonzero)
+    bool pair_req = false;
+    struct PairView {
+        bool on = false;
+        const uint32_t* ovf_n = nullptr;
+        const uint16_t* slots = nullptr;
+        const uint8_t* qn = nullptr;
+        const uint32_t* fills = nullptr;
+        uint64_t row = 0;
+        uint32_t nch = 0;
+    } last_pairs;
     static constexpr uint32_t kDtpHist = 16384;  // MXP_DTP_HIST (kernels.hip): rule sets counted by histogram
     DevBuf d_dtp_part;                // [tiles][(R + 1) / 2] per-tile true-pair histograms
     uint32_t dtp_par = 0;   // d_dtp_ovf_n holds two counter sets: this launch's and the next one's
@@ -601,6 +615,8 @@ struct mxp_engine : public mxp::LowerTables {
     static constexpr size_t kShaderCopyMin = 64u << 10;
     bool d2h_dma = false;
     bool resolve_tile = true;  // Resolve's default-namespace range walked by resolve_tile (MXP_RESOLVE_TILE)
+    int resolve_pairs = 1;  // pair Resolve where the plan allows it (MXP_RESOLVE_PAIRS=0: the bitmap; 2: a
+                            // Resolve that cannot take it fails -- tests)
     // the device packer's column copies (pack_device.cpp)
     // [0] the packer's copies, [1] small read-backs, [2] the packer's kernels (apart from the engine
     // stream: an event recorded there -- a freed batch's -- then never waits for a later batch's

@@ -147,6 +147,10 @@ typedef struct mxp_kargs {
     // value, so the index kernel hashes and verifies short prefixes without the string's descriptor
     // and bytes (two dependent scattered loads per request)
     const uint4* heads;
+    // a Resolve's evaluation (resolver.cpp "pair Resolve"): the plain fill stores its words only when
+    // this evaluation's deferred pairs overflowed (*dtp_lazy, its dtp_ovf_n[0], nonzero) -- otherwise
+    // the Resolve reads the filed pairs themselves and the match bitmap is never written (null: store)
+    const uint32_t* dtp_lazy;
 } mxp_kargs;
 
 // mxp_vtd_final_kernel: the packer's provisional class tables and the candidate column of each

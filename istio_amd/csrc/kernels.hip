@@ -1525,8 +1525,10 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_dtp_kernel(mxp_kargs 
         bad[r] = (in && !((okset >> k) & 1u)) ? ~0u : 0u;
     }
     const bool any = (bad[0] | bad[1] | bad[2] | bad[3]) != 0;
+    // (a pair Resolve's evaluation: only the request error flags and records unless pairs overflowed)
+    const bool store = !A.dtp_lazy || uni(*A.dtp_lazy) != 0u;
     DtpQueue dq;
-    dq.load(A, A.dtp_cbase + blockIdx.y, q0, q0 < Q1);
+    if (store) dq.load(A, A.dtp_cbase + blockIdx.y, q0, q0 < Q1);
     const bool dany = __ballot(dq.q0 != ~0u) != 0;
     if (A.req_err && any) {
         uint32_t masks = 0;
@@ -1541,6 +1543,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_fill_dtp_kernel(mxp_kargs 
             for (uint32_t r = 0; r < 4; r++)
                 if (bad[r] && q0 + r < Q1) log_guard_errors(A, mask, (g0 + g) * 32u, q0 + r);
         }
+    if (!store) return;
     const bool nt = !(A.flags & 128u);
     typedef uint32_t v4u __attribute__((ext_vector_type(4)));
     for (uint32_t g = 0; g < n; g++) {

@@ -604,6 +604,194 @@ __device__ __forceinline__ void resolve_count4(const mxp_resolve_args& A) {
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count4_kernel(mxp_resolve_args A) { resolve_count4<false>(A); }
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_count4v_kernel(mxp_resolve_args A) { resolve_count4<true>(A); }
 
+// Pair Resolve (resolver.cpp): each request's selected rules straight from the evaluation's deferred
+// index pairs.  When every word of the rule set is a plain fill chunk's, a word of the match bitmap
+// is 0 but for its pairs (mxp_fill_dtp_kernel), so the pairs filed per (fill chunk, lane quad) by
+// mxp_dtp_sort_kernel are the bitmap: the evaluation skips its stores (kargs.dtp_lazy) and these
+// passes read a count byte per quad and chunk, and a 16-byte slot row where it is not 0 -- C2:
+// ~20 chunks x 1 B per quad instead of 1.31 GB of bitmap written and read again.  A thread takes
+// the quad of requests 4t .. 4t + 3 of its workgroup's 1,024, as the fill does.  A quad's entries
+// sorted (group, plane, request, bit) give each request's rules of the chunk in ascending order
+// with duplicates adjacent; the chunks ascend, so the rules of the default namespace arrive in
+// resolution order and so do the request's own namespace's, which resolve after all of them
+// (resolver.go:202-238).  Error-plane entries are skipped: a compact evaluation's first errors
+// come from its error records (err_in), as in the bitmap passes.
+namespace {
+
+__device__ __forceinline__ void sort8r(uint32_t (&x)[8]) {
+#define MXP_RCX(a, b)                         \
+    {                                         \
+        const uint32_t lo = min(x[a], x[b]);  \
+        x[b] = max(x[a], x[b]);               \
+        x[a] = lo;                            \
+    }
+    MXP_RCX(0, 1) MXP_RCX(2, 3) MXP_RCX(4, 5) MXP_RCX(6, 7) MXP_RCX(0, 2) MXP_RCX(1, 3) MXP_RCX(4, 6) MXP_RCX(5, 7)
+    MXP_RCX(1, 2) MXP_RCX(5, 6) MXP_RCX(0, 4) MXP_RCX(1, 5) MXP_RCX(2, 6) MXP_RCX(3, 7) MXP_RCX(2, 4) MXP_RCX(3, 5)
+    MXP_RCX(1, 2) MXP_RCX(3, 4) MXP_RCX(5, 6)
+#undef MXP_RCX
+}
+
+// kWrite 0: status, first error, count, stash and block sums (as resolve_count4); 1: the ids of the
+// requests the stash does not hold, default namespace first (pass 0), then their own (pass 1)
+template <bool kWrite>
+__device__ __forceinline__ void resolve_pairs(const mxp_resolve_args& A) {
+    // the stash while counting: [(request of the quad) * 8 + j][thread], j < 4 the default
+    // namespace's first rules, 4 + j the own namespace's (columns per thread: no bank conflicts)
+    __shared__ uint32_t s_st[kWrite ? 1 : 32 * 256];
+    const uint32_t t = threadIdx.x;
+    const uint32_t q0 = blockIdx.x * 1024u + 4u * t;
+    const bool has_def = A.default_id != MXP_NS_NONE;
+    const uint32_t dlo = has_def ? __builtin_amdgcn_readfirstlane(A.ns_lo[A.default_id]) : 0u;
+    const uint32_t dhi = has_def ? __builtin_amdgcn_readfirstlane(A.ns_hi[A.default_id]) : 0u;
+    uint32_t info[4], olo[4], ohi[4], cd[4], co[4];
+    uint64_t pos[4];
+    bool act[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) {
+        const uint32_t q = q0 + k;
+        act[k] = false;
+        info[k] = olo[k] = ohi[k] = cd[k] = co[k] = 0u;
+        pos[k] = 0ull;
+        if (q >= A.n) continue;
+        const uint32_t in = A.nsinfo[q];
+        if (!kWrite) {
+            if (in == MXP_NS_MISSING || in == MXP_NS_NOTSTRING) {
+                A.status[q] = in == MXP_NS_MISSING ? MXP_RESOLVE_NO_IDENTITY : MXP_RESOLVE_BAD_IDENTITY;
+                A.err_rule[q] = 0xFFFFFFFFu;
+                A.count[q] = 0;
+                continue;
+            }
+            if (A.err_in && A.err_in[q] != 0xFFFFFFFFu) {
+                uint32_t rule = A.err_in[q];
+                if (A.err_rank) {
+                    const uint32_t dlen = dhi - dlo;
+                    rule = rule < dlen ? dlo + rule : A.ns_lo[in & 0x7FFFFFFFu] + (rule - dlen);
+                }
+                A.status[q] = MXP_RESOLVE_PRED_ERROR;
+                A.err_rule[q] = rule;
+                A.count[q] = 0;
+                continue;
+            }
+            act[k] = true;
+        } else {
+            if (A.status[q] != MXP_RESOLVE_OK) continue;
+            const uint32_t c = A.count[q];
+            pos[k] = A.sel_off[q];
+            if (A.stash && c <= 4u) {  // the stash has them
+                const uint4 v = A.stash[q];
+                const uint32_t r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (uint32_t j = 0; j < 4u; j++)
+                    if (j < c) {
+                        if (A.ids16) ((uint16_t*)A.sel_rules)[pos[k] + j] = (uint16_t)r[j];
+                        else A.sel_rules[pos[k] + j] = r[j];
+                    }
+                continue;
+            }
+            act[k] = c != 0u;
+        }
+        info[k] = in;
+        const uint32_t ns = in & 0x7FFFFFFFu;
+        if (act[k] && ns != MXP_NS_NONE && ns != A.default_id) {
+            olo[k] = A.ns_lo[ns];
+            ohi[k] = A.ns_hi[ns];
+        }
+    }
+    const bool mine = act[0] || act[1] || act[2] || act[3];
+    const bool own = olo[0] < ohi[0] || olo[1] < ohi[1] || olo[2] < ohi[2] || olo[3] < ohi[3];
+    constexpr uint32_t kPasses = kWrite ? 2u : 1u;
+    for (uint32_t pass = 0; pass < kPasses; pass++) {
+        // (kWrite: pass 0 the default namespace's rules, pass 1 the own namespace's; a wave without
+        // such requests skips the pass)
+        if (!__ballot(mine && (pass == 0u || own))) continue;
+        // (the count bytes of kPre chunks loaded together: the walk is a chain of mostly-zero counts)
+        constexpr uint32_t kPre = 8;
+        for (uint32_t c0 = 0; c0 < A.pr_nch; c0 += kPre) {
+            uint32_t kns[kPre];
+#pragma unroll
+            for (uint32_t j = 0; j < kPre; j++)
+                kns[j] = mine && c0 + j < A.pr_nch ? A.pr_qn[(uint64_t)(c0 + j) * A.pr_row + (q0 >> 2)] : 0u;
+#pragma unroll
+            for (uint32_t jc = 0; jc < kPre; jc++) {
+                const uint32_t kn = kns[jc];
+                if (!__ballot(kn != 0u)) continue;
+                const uint32_t c = c0 + jc;
+                const uint32_t g0 = __builtin_amdgcn_readfirstlane(A.pr_fills[8u * c + 2u]);
+                const uint64_t qi = (uint64_t)c * A.pr_row + (q0 >> 2);
+                if (!kn) continue;
+                const uint4 sl = *(const uint4*)(A.pr_slots + qi * 8u);
+                const uint32_t h[4] = {sl.x, sl.y, sl.z, sl.w};
+                uint32_t x[8];
+#pragma unroll
+                for (uint32_t i = 0; i < 8u; i++) x[i] = i < kn ? (h[i >> 1] >> (16u * (i & 1u))) & 0xFFFFu : 0xFFFFu;
+                if (kn > 1u) sort8r(x);
+                uint32_t prev = 0xFFFFFFFFu;
+#pragma unroll
+                for (uint32_t i = 0; i < 8u; i++) {
+                    const uint32_t e = x[i];
+                    const bool skip = e == 0xFFFFu || e == prev || (e & 128u);
+                    prev = e;
+                    if (skip) continue;
+                    const uint32_t r = (e >> 5) & 3u, rule = (g0 + (e >> 8)) * 32u + (e & 31u);
+#pragma unroll
+                    for (uint32_t k = 0; k < 4u; k++) {
+                        if (k != r || !act[k]) continue;
+                        const uint32_t tcp = info[k] >> 31;
+                        if (!((A.amask[tcp * A.n_words + (rule >> 5)] >> (rule & 31u)) & 1u)) continue;
+                        const bool def = rule >= dlo && rule < dhi;
+                        if (!def && !(rule >= olo[k] && rule < ohi[k])) continue;
+                        if (kWrite) {
+                            if (def != (pass == 0u)) continue;
+                            if (A.ids16) ((uint16_t*)A.sel_rules)[pos[k]++] = (uint16_t)rule;
+                            else A.sel_rules[pos[k]++] = rule;
+                        } else if (def) {
+                            if (cd[k] < 4u) s_st[(k * 8u + cd[k]) * 256u + t] = rule;
+                            cd[k]++;
+                        } else {
+                            if (co[k] < 4u) s_st[(k * 8u + 4u + co[k]) * 256u + t] = rule;
+                            co[k]++;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (kWrite) return;
+    uint64_t csum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4u; k++) {
+        const uint32_t q = q0 + k;
+        if (!act[k]) continue;
+        const uint32_t c = cd[k] + co[k];
+        A.status[q] = MXP_RESOLVE_OK;
+        A.err_rule[q] = 0xFFFFFFFFu;
+        A.count[q] = c;
+        if (A.stash) {
+            uint32_t st[4];
+#pragma unroll
+            for (uint32_t j = 0; j < 4u; j++) {
+                const uint32_t jo = j - cd[k];  // (own rules follow the default namespace's)
+                st[j] = j < cd[k] ? s_st[(k * 8u + j) * 256u + t]
+                        : jo < co[k] ? s_st[(k * 8u + 4u + jo) * 256u + t] : 0u;
+            }
+            A.stash[q] = make_uint4(st[0], st[1], st[2], st[3]);
+        }
+        csum += c;
+    }
+    if (A.block_sum) {  // (wave w holds requests base + 256 w ...: block 4 * blockIdx.x + w of the scan)
+        uint64_t v = csum;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        const uint32_t w = t >> 6;
+        if ((t & 63u) == 0 && blockIdx.x * 1024u + 256u * w < A.n) A.block_sum[4u * blockIdx.x + w] = v;
+    }
+}
+
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) void mxp_resolve_pairs_count_kernel(mxp_resolve_args A) { resolve_pairs<false>(A); }
+extern "C" __global__ __launch_bounds__(256) void mxp_resolve_pairs_write_kernel(mxp_resolve_args A) { resolve_pairs<true>(A); }
+
 
 
 // the count pass's block sums from the counts (the tiled count kernel's blocks are 64 requests)
@@ -614,7 +802,8 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_bsum_kernel(mxp_re
 }
 
 // write 0: counts (+ block sums); 1: ids; 2: the scan of the counts; 3 / 4: 0 / 1 tiled (the
-// default namespace's range walked by resolve_tile; needs default_id != MXP_NS_NONE)
+// default namespace's range walked by resolve_tile; needs default_id != MXP_NS_NONE); 5 / 6: 0 / 1
+// from the deferred pairs (pair Resolve)
 extern "C" hipError_t mxp_launch_resolve(const mxp_resolve_args* a, int write, hipStream_t s) {
     const uint32_t grid = (a->n + 255u) / 256u;
     if (write == 1) {
@@ -636,6 +825,9 @@ extern "C" hipError_t mxp_launch_resolve(const mxp_resolve_args* a, int write, h
         }
     } else if (write == 4) {
         hipLaunchKernelGGL(mxp_resolve_tile_write_kernel, dim3((a->n + 63u) / 64u), dim3(256), 0, s, *a);
+    } else if (write == 5 || write == 6) {  // pair Resolve: count / ids
+        hipLaunchKernelGGL(write == 5 ? mxp_resolve_pairs_count_kernel : mxp_resolve_pairs_write_kernel,
+                           dim3((a->n + 1023u) / 1024u), dim3(256), 0, s, *a);
     } else {
         hipLaunchKernelGGL(mxp_resolve_count_kernel, dim3(grid), dim3(256), 0, s, *a);
     }

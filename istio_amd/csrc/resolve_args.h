@@ -57,4 +57,13 @@ typedef struct mxp_resolve_args {
     uint4* stash;              // [n] the count pass's first 4 selected rules of each request (pass 2
                                // copies them for requests with at most 4, instead of walking the
                                // bitmap again); nullptr: none
+    // pair Resolve (resolver.cpp): the evaluation's deferred index pairs, filed per fill chunk and
+    // lane quad by mxp_dtp_sort_kernel, read instead of the match bitmap, which the evaluation then
+    // never wrote (kargs.dtp_lazy); every word of the rule set is a plain fill chunk's
+    const uint16_t* pr_slots;  // [chunks][pr_row quads][8] g << 8 | plane << 7 | request % 4 << 5 | bit
+    const uint8_t* pr_qn;      // [chunks][pr_row] entries in each quad's slots (<= 8)
+    const uint32_t* pr_fills;  // [chunks][8] the fill chunks (vm.h mxp_fill: [2] first word, [3] words)
+    uint64_t pr_row;           // quads per chunk row (MXP_DTP_ROW of the evaluation's tiles)
+    uint32_t pr_nch;           // chunks, in ascending word order
+    uint32_t pr_pad;
 } mxp_resolve_args;

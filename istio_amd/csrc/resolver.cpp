@@ -210,6 +210,10 @@ struct mxp_resolve_job {
     std::vector<mxp_ref_rec> recs;
     std::vector<uint32_t> info;  // host copy of the namespaces (host pass; referenced attributes)
     const uint32_t* hinfo = nullptr;
+    mxp_engine::PairView pairs;  // the evaluation's filed pairs (pair Resolve; on = false: the bitmap)
+    bool pairs_filed = false;    // (the evaluation filed them; pairs_ovf: how many overflowed)
+    uint32_t pairs_ovf = 0;
+    uint32_t recs_n = 0, class_recs_n = 0;  // (the evaluation's error records: diagnostics)
 };
 
 namespace {
@@ -236,10 +240,14 @@ int resolve_begin(mxp_resolve_job& J) {
     // returns only once the stream has reached it, so behind the evaluation it would hold the
     // caller until the kernels end (r6_s25: 0.79 ms)
     std::vector<uint32_t> amask(2 * (size_t)W, 0), empty(W, 0);  // per-word masks: variety / tcp, empty matches
+    bool any_empty = false;
     for (uint32_t r = 0; r < NR; r++) {
         const uint32_t bit = 1u << (r & 31);
         if ((R.vmask[r] >> variety) & 1u) amask[(size_t)R.tcp[r] * W + r / 32] |= bit;
-        if (R.empty[r]) empty[r / 32] |= bit;
+        if (R.empty[r]) {
+            empty[r / 32] |= bit;
+            any_empty = true;
+        }
     }
     DevBuf &d_info = eng->res_info, &d_lo = eng->res_lo, &d_hi = eng->res_hi, &d_amask = eng->res_amask,
            &d_empty = eng->res_empty;
@@ -256,11 +264,18 @@ int resolve_begin(mxp_resolve_job& J) {
     J.compact = !J.ref_off && !(eng->debug_flags & kResolveBitmap);
     if (J.compact) {
         if (eng->device >= 0 && (e = eng->res_flags.reserve(n ? n : 1)) != hipSuccess) return eng->hipfail(e, "alloc flags");
+        // pair Resolve: the selected rules from the evaluation's deferred pairs, the bitmap left
+        // unwritten, where the plan allows it (the launch decides); rules with an empty match are
+        // selected without a pair, so their sets keep the bitmap
+        eng->pair_req = eng->resolve_pairs != 0 && !any_empty;
         if (pre) {
             rc = eng->evaluate_uploaded(J.db.get(), dm, de, nullptr, eng->res_flags.as<uint8_t>());
         } else {
             rc = eng->evaluate(batch, dm, de, nullptr, J.db, eng->res_flags.as<uint8_t>());
         }
+        J.pairs = eng->pair_req && !rc ? eng->last_pairs : mxp_engine::PairView{};
+        J.pairs_filed = J.pairs.on;
+        eng->pair_req = false;
     } else {
         rc = J.ref_off ? eng->refs_evaluate(batch, dm, de, J.db, J.recs)
              : pre     ? eng->evaluate_uploaded(J.db.get(), dm, de, nullptr, nullptr)
@@ -354,10 +369,17 @@ int resolve_end(mxp_resolve_job& J, uint8_t* status, uint32_t* err_rule, uint64_
     bool collected = false;  // (records collected after the resolve kernels unless a path needed them first)
     if (compact) {
         // the log's counts: [0] records, [2] class records (synchronises: the evaluation is done)
-        uint32_t cnt[4] = {0, 0, 0, 0};
+        uint32_t cnt[4] = {0, 0, 0, 0}, ovf[2] = {0, 0};
         if ((e = hipMemcpyAsync(cnt, eng->d_errcount.p, 16, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess ||
+            (J.pairs.on &&
+             (e = hipMemcpyAsync(ovf, J.pairs.ovf_n, 8, hipMemcpyDeviceToHost, eng->stream)) != hipSuccess) ||
             (e = hipStreamSynchronize(eng->stream)) != hipSuccess)
             return eng->hipfail(e, "download errcount");
+        // (pairs past their lists or slots: the fills stored the bitmap after all -- read it)
+        J.pairs_ovf = ovf[0];
+        J.recs_n = cnt[0];
+        J.class_recs_n = cnt[2];
+        if (ovf[0]) J.pairs.on = false;
         if ((e = eng->res_err_in.reserve((size_t)n * 4 + 4)) != hipSuccess) return eng->hipfail(e, "alloc err_in");
         if (n && (e = hipMemsetAsync(eng->res_err_in.p, 0xFF, (size_t)n * 4, eng->stream)) != hipSuccess)
             return eng->hipfail(e, "reset err_in");
@@ -366,6 +388,7 @@ int resolve_end(mxp_resolve_job& J, uint8_t* status, uint32_t* err_rule, uint64_
             if ((e = de.reserve((size_t)W * n * 4)) != hipSuccess) return eng->hipfail(e, "alloc err");
             if ((rc = eng->launch(db.get(), eng->stream, dm.as<uint32_t>(), de.as<uint32_t>(), nullptr, false))) return rc;
             A.err = de.as<uint32_t>();
+            J.pairs.on = false;  // (this evaluation wrote both bitmaps)
             eng->trace_mark("error bitmap (log overflow)");
         } else if (!cnt[2]) {
             // each request's first error from the records, on the device
@@ -385,6 +408,7 @@ int resolve_end(mxp_resolve_job& J, uint8_t* status, uint32_t* err_rule, uint64_
                                       false)))
                     return rc;
                 A.err = de.as<uint32_t>();
+                J.pairs.on = false;
             } else {
                 if (n && hinfo == nullptr) {  // (the device namespaces, brought back for this pass)
                     info.resize(n);
@@ -402,9 +426,27 @@ int resolve_end(mxp_resolve_job& J, uint8_t* status, uint32_t* err_rule, uint64_
             eng->trace_mark("first errors (class records, host)");
         }
     }
-    // (the default namespace's range tiled through LDS: resolve_tile; MXP_RESOLVE_TILE=0 the per-lane walk)
+    // (the default namespace's range tiled through LDS: resolve_tile; MXP_RESOLVE_TILE=0 the per-lane walk;
+    // a pair Resolve reads the filed pairs instead)
     const bool tiled = eng->resolve_tile && R.default_id != MXP_NS_NONE;
-    if (n && (e = mxp_launch_resolve(&A, tiled ? 3 : 0, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve");
+    const bool pairs = J.pairs.on && !A.err;
+    if (eng->resolve_pairs == 2 && n && !pairs) {
+        char why[160];
+        snprintf(why, sizeof why,
+                 "pair Resolve not taken (MXP_RESOLVE_PAIRS=2): pairs filed %d, overflowed %u, error bitmap %d "
+                 "(records %u of %u, class records %u)",
+                 J.pairs_filed ? 1 : 0, J.pairs_ovf, A.err ? 1 : 0, J.recs_n, eng->errcap, J.class_recs_n);
+        return eng->fail(MXP_ERR_STATE, why);
+    }
+    if (pairs) {
+        A.pr_slots = J.pairs.slots;
+        A.pr_qn = J.pairs.qn;
+        A.pr_fills = J.pairs.fills;
+        A.pr_row = J.pairs.row;
+        A.pr_nch = J.pairs.nch;
+    }
+    const int count_mode = pairs ? 5 : tiled ? 3 : 0, write_mode = pairs ? 6 : tiled ? 4 : 1;
+    if (n && (e = mxp_launch_resolve(&A, count_mode, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve");
     if (n && (e = mxp_launch_resolve(&A, 2, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve scan");
     eng->trace_mark("  resolve: count + scan kernels");
     if (!n) {
@@ -443,7 +485,7 @@ int resolve_end(mxp_resolve_job& J, uint8_t* status, uint32_t* err_rule, uint64_
         const size_t isz = ids16 ? 2 : 4;
         if ((e = d_sel.reserve(total * isz)) != hipSuccess) return eng->hipfail(e, "alloc sel");
         A.sel_rules = d_sel.as<uint32_t>();
-        if ((e = mxp_launch_resolve(&A, tiled ? 4 : 1, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
+        if ((e = mxp_launch_resolve(&A, write_mode, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
         if ((rc = eng->download((uint8_t*)sel_rules + (size_t)at * isz, d_sel.p, total * isz, "download sel"))) return rc;
     }
     eng->trace_mark("action lists (gather + download)");
