@@ -170,6 +170,7 @@ void BlockBin::release() {
 // ------------------------------------------------------------------------------------ compile
 int mxp_engine::compile(const char* const* exprs, uint32_t n, int32_t* status) {
     reset_tables();
+    res_gen++;  // (the resolver's device tables are sized by the rule count)
     ref_comp.clear();
     plans.clear();
     views_n[0] = ~(size_t)0;  // string-view indexes rebuilt at the next pack
@@ -2298,6 +2299,7 @@ void mxp_engine_destroy(mxp_engine* eng) {
         if (eng->bounce_ev[k]) (void)hipEventDestroy(eng->bounce_ev[k]);
         if (eng->bounce[k]) (void)hipHostFree(eng->bounce[k]);
     }
+    if (eng->res_small) (void)hipHostFree(eng->res_small);
     eng->bin.release();
     if (eng->stream) (void)hipStreamDestroy(eng->stream);
     for (auto& x : eng->ev)

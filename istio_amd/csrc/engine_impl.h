@@ -634,6 +634,11 @@ struct mxp_engine : public mxp::LowerTables {
         return copy_s[k];
     }
     void* bounce[2] = {nullptr, nullptr};
+    uint32_t* res_small = nullptr;  // pinned: a compact Resolve's error-record and pair-overflow counts
+    // the resolver's per-word tables on the device (res_lo / _hi / _amask / _empty) are those of
+    // configuration res_gen and this variety (res_tab_key = res_gen << 6 | variety): kept across calls
+    uint64_t res_gen = 0, res_tab_key = ~0ull;
+    bool res_any_empty = false;
     hipEvent_t bounce_ev[2] = {nullptr, nullptr};
     int download(void* dst, const void* dsrc, size_t bytes, const char* what);
     // several downloads: those into pinned memory queued together with one synchronisation, the

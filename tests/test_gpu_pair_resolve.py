@@ -135,3 +135,25 @@ def test_pair_resolve_group_pipeline(mxp, monkeypatch):
         assert np.array_equal(status, want[0]) and np.array_equal(err_rule, want[1])
         assert np.array_equal(off, want[2]) and np.array_equal(ids[:int(off[-1])], want[3][:int(want[2][-1])])
     g.close()
+
+
+def test_resolver_tables_follow_configuration(mxp, monkeypatch):
+    """The resolver's per-word tables stay on the device between calls of one configuration and
+    variety; a new configuration (mxp_resolver_set) or variety replaces them: an engine re-configured
+    between calls resolves as a fresh engine with the new configuration."""
+    manifest, rules, conf, batch = c2_resolve_case(512, 1, 8192, seed=34)
+    conf2 = dict(conf, variety_mask=[int(x) ^ 5 for x in conf["variety_mask"]],
+                 is_tcp=[1 - int(x) for x in conf["is_tcp"]], default_ns="ns2")
+    eng = engine_for(mxp, monkeypatch, manifest, rules, conf, "1")
+    fresh = engine_for(mxp, monkeypatch, manifest, rules, conf2, "1")
+    a = [x.copy() for x in eng.resolve_arrays(batch, 1)]
+    b = [x.copy() for x in eng.resolve_arrays(batch, 2)]
+    eng.set_resolver(conf2["identity_attr"], conf2["default_ns"], conf2["rule_ns"], conf2["variety_mask"],
+                     conf2["is_tcp"], conf2["empty_match"])
+    for v in (1, 2, 1):
+        got, want = eng.resolve_arrays(batch, v), fresh.resolve_arrays(batch, v)
+        for x, y in zip(got, want):
+            assert np.array_equal(x, y), v
+    assert not all(np.array_equal(x, y) for x, y in zip(a, b))
+    eng.close()
+    fresh.close()
