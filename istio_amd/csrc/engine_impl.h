@@ -36,6 +36,8 @@ static constexpr unsigned kOrderEvent = hipEventDisableTiming | hipEventDisableS
 extern "C" hipError_t mxp_launch_eval(const mxp_kargs* args, uint32_t grid_x, uint32_t grid_y, int vm, hipStream_t s);
 extern "C" hipError_t mxp_launch_index(const mxp_kargs* args, uint32_t grid, hipStream_t s);
 extern "C" hipError_t mxp_launch_d2h_copy(void* dst, const void* src, uint64_t n, hipStream_t s);
+extern "C" hipError_t mxp_launch_d2h_copy_ids(void* dst, const void* src, const uint64_t* count, uint32_t isz, uint64_t cap,
+                                              hipStream_t s);
 extern "C" hipError_t mxp_launch_vtd_final(const mxp_kargs* args, const mxp_vtd_final_args* f, hipStream_t s);
 extern "C" hipError_t mxp_launch_heads(const mxp_kargs* args, const uint32_t* cols, uint32_t nrow, uint4* heads, hipStream_t s);
 extern "C" hipError_t mxp_launch_inject(const mxp_kargs* args, uint32_t grid, hipStream_t s);
@@ -61,9 +63,10 @@ extern "C" hipError_t mxp_launch_hits_gate(const unsigned long long* stats, uint
 // fit; the ids are then downloaded straight there.  sel_off gets the batch-local offsets.
 using mxp_resolve_place = std::function<int64_t(uint64_t)>;
 // db (nullable): the batch, uploaded before and taken over by the call (mxp_resolve_uploaded)
+// first_cap: the whole list's capacity when this member's ids go first (member 0; 0: not first)
 int mxp_resolve_placed(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
                        uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules,
-                       const mxp_resolve_place& place);
+                       const mxp_resolve_place& place, uint64_t first_cap = 0);
 
 // Device blocks of freed batches, reused by later uploads (mxp_batch_free hands a batch's blocks to
 // its engine's bin with events recorded on every stream that read the batch; mxp_batch_upload draws

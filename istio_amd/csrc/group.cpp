@@ -344,7 +344,7 @@ struct SplitView {
 
 // (resolver.cpp) a member's finish with the group's placement, and dropping a submitted job
 int mxp_resolve_finish_placed(mxp_resolve_job* job, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off,
-                              void* sel_rules, const mxp_resolve_place& place);
+                              void* sel_rules, const mxp_resolve_place& place, uint64_t first_cap = 0);
 void mxp_resolve_job_free(mxp_resolve_job* job);
 
 extern "C" {
@@ -1007,7 +1007,7 @@ static int group_resolve(mxp_group* g, mxp_gbatch* gb, const mxp_bag_batch* cons
         mxp_dbatch* db = nullptr;
         if (gb) std::swap(db, gb->db[k]);  // (taken over by the member's Resolve)
         const int r = mxp_resolve_placed(g->m[k].eng, db, shards[k], variety, flags, status + lo, err_rule + lo,
-                                         sel_off + lo, sel_rules, place);
+                                         sel_off + lo, sel_rules, place, k == 0 ? sel_cap : 0);
         if (r && r != MXP_ERR_NOMEM) failed.store(true);
         rv.arrive(k, 0);  // (a member that failed before its count still lets the others go on)
         return r == MXP_ERR_NOMEM ? MXP_OK : r;
@@ -1122,7 +1122,8 @@ int mxp_group_resolve_finish(mxp_group* g, mxp_gresolve* r0, uint8_t* status, ui
         };
         mxp_resolve_job* job = nullptr;
         std::swap(job, r->jobs[k]);
-        const int rr = mxp_resolve_finish_placed(job, status + lo, err_rule + lo, sel_off + lo, sel_rules, place);
+        const int rr = mxp_resolve_finish_placed(job, status + lo, err_rule + lo, sel_off + lo, sel_rules, place,
+                                                 k == 0 ? sel_cap : 0);
         if (rr && rr != MXP_ERR_NOMEM) failed.store(true);
         arrive(k, 0);  // (a member that failed before its count still lets the others go on)
         return rr == MXP_ERR_NOMEM ? MXP_OK : rr;

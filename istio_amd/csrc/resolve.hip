@@ -252,9 +252,14 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_offsets_kernel(mxp
     if (blockIdx.x == gridDim.x - 1u && threadIdx.x == 0) A.sel_off_out[A.n] = base + total;
 }
 
+// (a guarded write pass: the ids do not fit the capacity they were enqueued for)
+__device__ __forceinline__ bool ids_over_cap(const mxp_resolve_args& A) {
+    return A.sel_cap_dev && A.sel_off[A.n] > A.sel_cap_dev;
+}
+
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_write_kernel(mxp_resolve_args A) {
     const uint32_t q = blockIdx.x * 256u + threadIdx.x;
-    if (q >= A.n || A.status[q] != MXP_RESOLVE_OK) return;
+    if (q >= A.n || A.status[q] != MXP_RESOLVE_OK || ids_over_cap(A)) return;
     const uint32_t c = A.count[q];
     if (A.stash && c <= 4u) {  // the count pass kept them: no second walk of the bitmaps
         if (!c) return;
@@ -471,6 +476,7 @@ extern "C" __global__ __launch_bounds__(256) void mxp_resolve_tile_count_kernel(
     resolve_tile<false>(A);
 }
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_tile_write_kernel(mxp_resolve_args A) {
+    if (ids_over_cap(A)) return;
     resolve_tile<true>(A);
 }
 
@@ -790,7 +796,10 @@ __device__ __forceinline__ void resolve_pairs(const mxp_resolve_args& A) {
 }  // namespace
 
 extern "C" __global__ __launch_bounds__(256) void mxp_resolve_pairs_count_kernel(mxp_resolve_args A) { resolve_pairs<false>(A); }
-extern "C" __global__ __launch_bounds__(256) void mxp_resolve_pairs_write_kernel(mxp_resolve_args A) { resolve_pairs<true>(A); }
+extern "C" __global__ __launch_bounds__(256) void mxp_resolve_pairs_write_kernel(mxp_resolve_args A) {
+    if (ids_over_cap(A)) return;
+    resolve_pairs<true>(A);
+}
 
 
 
@@ -893,8 +902,7 @@ extern "C" hipError_t mxp_launch_resolve_first_err(const mxp_resolve_args* a, co
 // stores from a kernel reach the link's ~54 GB/s (tools/pcie_probe.hip).  When dst
 // and src share their alignment mod 16 the body moves in 16-byte words (the head and tail bytewise);
 // otherwise bytewise.
-extern "C" __global__ __launch_bounds__(256) void mxp_d2h_copy_kernel(uint8_t* __restrict__ dst,
-                                                                      const uint8_t* __restrict__ src, uint64_t n) {
+__device__ __forceinline__ void d2h_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t n) {
     const uint64_t tid = blockIdx.x * 256ull + threadIdx.x, stride = (uint64_t)gridDim.x * 256ull;
     const uint64_t mis = (uint64_t)(uintptr_t)dst & 15u;
     if (mis != ((uint64_t)(uintptr_t)src & 15u)) {
@@ -909,6 +917,29 @@ extern "C" __global__ __launch_bounds__(256) void mxp_d2h_copy_kernel(uint8_t* _
     for (uint64_t i = tid; i < words; i += stride) d16[i] = s16[i];
     const uint64_t done = head + (words << 4);
     if (tid < n - done) dst[done + tid] = src[done + tid];
+}
+
+extern "C" __global__ __launch_bounds__(256) void mxp_d2h_copy_kernel(uint8_t* __restrict__ dst,
+                                                                      const uint8_t* __restrict__ src, uint64_t n) {
+    d2h_copy(dst, src, n);
+}
+
+// the Resolve's ids, *count of them (isz bytes each), enqueued before the host knows the count: none
+// when they exceed cap (the guarded write pass wrote none either)
+extern "C" __global__ __launch_bounds__(256) void mxp_d2h_copy_ids_kernel(uint8_t* __restrict__ dst,
+                                                                          const uint8_t* __restrict__ src,
+                                                                          const uint64_t* count, uint32_t isz, uint64_t cap) {
+    const uint64_t c = *count;
+    if (c <= cap) d2h_copy(dst, src, c * isz);
+}
+
+extern "C" hipError_t mxp_launch_d2h_copy_ids(void* dst, const void* src, const uint64_t* count, uint32_t isz, uint64_t cap,
+                                              hipStream_t s) {
+    const uint64_t need = (cap * isz / 16u + 255u) / 256u;
+    const uint32_t grid = (uint32_t)(need < 1024u ? (need ? need : 1u) : 1024u);
+    hipLaunchKernelGGL(mxp_d2h_copy_ids_kernel, dim3(grid), dim3(256), 0, s, (uint8_t*)dst, (const uint8_t*)src, count,
+                       isz, cap);
+    return hipGetLastError();
 }
 
 extern "C" hipError_t mxp_launch_d2h_copy(void* dst, const void* src, uint64_t n, hipStream_t s) {

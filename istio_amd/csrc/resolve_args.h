@@ -66,4 +66,7 @@ typedef struct mxp_resolve_args {
     uint64_t pr_row;           // quads per chunk row (MXP_DTP_ROW of the evaluation's tiles)
     uint32_t pr_nch;           // chunks, in ascending word order
     uint32_t pr_pad;
+    // the write passes write nothing when the batch's ids exceed this many (sel_off[n] > sel_cap_dev;
+    // 0: unchecked) -- the ids enqueued with the other outputs before the host knows their count
+    uint64_t sel_cap_dev;
 } mxp_resolve_args;

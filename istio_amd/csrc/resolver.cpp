@@ -150,6 +150,9 @@ namespace {
 
 // MXP_DEBUG_FLAGS: resolve through the error bitmap (the pre-round-5 path), for A/B and tests
 constexpr uint32_t kResolveBitmap = 1u << 28;
+// ids enqueued with the other outputs only for capacities up to this many bytes (the device buffer
+// is sized by the capacity, not the count)
+constexpr uint64_t kEarlyIdsMax = 256ull << 20;
 
 // Each request's first applicable erroring rule in resolution order (filterActions returns at the
 // first EvalPredicate error, resolver.go:226-228) from the error records of a compact evaluation:
@@ -215,6 +218,9 @@ struct mxp_resolve_job {
     bool pairs_filed = false;    // (the evaluation filed them; pairs_ovf: how many overflowed)
     uint32_t pairs_ovf = 0;
     uint32_t recs_n = 0, class_recs_n = 0;  // (the evaluation's error records: diagnostics)
+    // a group member whose ids go first in the batch's list (member 0): the group's capacity, so its
+    // ids are enqueued with the other outputs, before the placement (0: after it)
+    uint64_t first_cap = 0;
 };
 
 namespace {
@@ -466,6 +472,23 @@ int resolve_end(mxp_resolve_job& J, uint8_t* status, uint32_t* err_rule, uint64_
     if (n && (e = mxp_launch_resolve(&A, count_mode, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve");
     if (n && (e = mxp_launch_resolve(&A, 2, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve scan");
     eng->trace_mark("  resolve: count + scan kernels");
+    // The ids enqueued now, with the other outputs, when they go to the start of pinned caller memory:
+    // the write pass guarded by the capacity (it writes nothing past it) and a download sized on the
+    // device by sel_off[n] -- one synchronisation for every output instead of two (the ids' count is
+    // known on the host only after the first).  Otherwise, or when they do not fit, after it.
+    const size_t isz = ids16 ? 2 : 4;
+    const uint64_t early_cap = place ? J.first_cap : sel_cap;
+    void* const sel_hd = n && early_cap && !ref_off && early_cap * isz <= kEarlyIdsMax ? eng->host_dev_ptr(sel_rules) : nullptr;
+    if (sel_hd) {
+        if ((e = d_sel.reserve(early_cap * isz)) != hipSuccess) return eng->hipfail(e, "alloc sel");
+        A.sel_rules = d_sel.as<uint32_t>();
+        A.sel_cap_dev = early_cap;
+        if ((e = mxp_launch_resolve(&A, write_mode, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
+        if ((e = mxp_launch_d2h_copy_ids(sel_hd, d_sel.p, d_off.as<uint64_t>() + n, (uint32_t)isz, early_cap,
+                                         eng->stream)) != hipSuccess)
+            return eng->hipfail(e, "download sel");
+        A.sel_cap_dev = 0;
+    }
     if (!n) {
         if (!place) sel_off[0] = 0;
     } else {
@@ -498,8 +521,11 @@ int resolve_end(mxp_resolve_job& J, uint8_t* status, uint32_t* err_rule, uint64_
     } else if (total > sel_cap) {
         return MXP_ERR_NOMEM;
     }
+    if (total && sel_hd && total <= early_cap && at == 0) {
+        eng->trace_mark("action lists (with the outputs)");
+        return ref_rc;
+    }
     if (total) {
-        const size_t isz = ids16 ? 2 : 4;
         if ((e = d_sel.reserve(total * isz)) != hipSuccess) return eng->hipfail(e, "alloc sel");
         A.sel_rules = d_sel.as<uint32_t>();
         if ((e = mxp_launch_resolve(&A, write_mode, eng->stream)) != hipSuccess) return eng->hipfail(e, "launch resolve write");
@@ -520,8 +546,9 @@ int resolve_end(mxp_resolve_job& J, uint8_t* status, uint32_t* err_rule, uint64_
 int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, bool ids16, uint8_t* status,
                  uint32_t* err_rule, uint64_t* sel_off, void* sel_rules, uint64_t sel_cap, uint64_t* ref_off,
                  mxp_attr_ref* refs, uint64_t ref_cap, const mxp_resolve_place* place = nullptr,
-                 mxp_dbatch* pre = nullptr) {
+                 mxp_dbatch* pre = nullptr, uint64_t first_cap = 0) {
     mxp_resolve_job J;
+    J.first_cap = first_cap;
     J.db.reset(pre);  // (a batch uploaded before: taken over, whatever happens)
     if (!eng || !batch || !status || !err_rule || !sel_off || (sel_cap && !sel_rules) || variety >= 32)
         return MXP_ERR_ARG;
@@ -540,21 +567,22 @@ int resolve_impl(mxp_engine* eng, const mxp_bag_batch* batch, uint32_t variety, 
 
 int mxp_resolve_placed(mxp_engine* eng, mxp_dbatch* db, const mxp_bag_batch* batch, uint32_t variety, uint32_t flags,
                        uint8_t* status, uint32_t* err_rule, uint64_t* sel_off, void* sel_rules,
-                       const mxp_resolve_place& place) {
+                       const mxp_resolve_place& place, uint64_t first_cap) {
     if (!batch && db && db->wide) batch = &db->wide->view;  // (a narrow upload: its host view)
     if (flags & ~(uint32_t)MXP_RESOLVE_IDS_U16) {
         if (eng && db) eng->recycle(db);
         return MXP_ERR_ARG;
     }
     return resolve_impl(eng, batch, variety, (flags & MXP_RESOLVE_IDS_U16) != 0, status, err_rule, sel_off, sel_rules,
-                        0, nullptr, nullptr, 0, &place, db);
+                        0, nullptr, nullptr, 0, &place, db, first_cap);
 }
 
 // (group.cpp) a member's finish with its ids placed by the group, and dropping a submitted job
 int mxp_resolve_finish_placed(mxp_resolve_job* job, uint8_t* status, uint32_t* err_rule, uint64_t* sel_off,
-                              void* sel_rules, const mxp_resolve_place& place) {
+                              void* sel_rules, const mxp_resolve_place& place, uint64_t first_cap) {
     std::unique_ptr<mxp_resolve_job> J(job);
     if (!J) return MXP_ERR_ARG;
+    J->first_cap = first_cap;
     return resolve_end(*J, status, err_rule, sel_off, sel_rules, 0, &place);
 }
 void mxp_resolve_job_free(mxp_resolve_job* job) { delete job; }

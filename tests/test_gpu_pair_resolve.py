@@ -157,3 +157,43 @@ def test_resolver_tables_follow_configuration(mxp, monkeypatch):
     assert not all(np.array_equal(x, y) for x, y in zip(a, b))
     eng.close()
     fresh.close()
+
+
+@pytest.mark.parametrize("pairs", ["1", "0"])
+def test_ids_enqueued_with_outputs(mxp, monkeypatch, pairs):
+    """Pinned outputs: the ids are written (guarded by the capacity) and downloaded with the other
+    outputs before the host knows their count.  Exact, larger and too-small capacities (the latter
+    returns MXP_ERR_NOMEM with sel_off complete, and resolve_arrays retries) give the pageable
+    call's outputs -- one engine, and a group's first member (its ids go first in the list)."""
+    from istio_amd.engine import PinnedArena
+    manifest, rules, conf, batch = c2_resolve_case(520, 2, 32768, seed=35)
+    eng = engine_for(mxp, monkeypatch, manifest, rules, conf, pairs)
+    for u16 in (False, True):
+        want = [x.copy() for x in eng.resolve_arrays(batch, 1, ids16=u16)]
+        total = int(want[2][-1])
+        assert total > 100
+        for cap in (total, total + 1000, total - 1, 16):
+            got = eng.resolve_arrays(batch, 1, cap=cap, ids16=u16, pinned=True)
+            for x, y in zip(got, want):
+                assert np.array_equal(x, y), (u16, cap)
+    eng.close()
+    g = mxp.Group([0, 0])
+    g.set_vocabulary(manifest)
+    g.compile(rules)
+    g.set_resolver(conf["identity_attr"], conf["default_ns"], conf["rule_ns"], conf["variety_mask"],
+                   conf["is_tcp"], conf["empty_match"])
+    shards = W.split_batch(batch, 2)
+    want = [x.copy() for x in g.resolve_arrays(shards, 1, ids16=True)]
+    total, n = int(want[2][-1]), batch.n
+    for cap in (total, total + 64):
+        arena = PinnedArena(n * 13 + 8 + cap * 2 + 4 * 64)
+        out = (arena.empty(n, np.uint8), arena.empty(n, np.uint32), arena.empty(n + 1, np.uint64),
+               arena.empty(cap, np.uint16))
+        got = g.resolve_arrays(shards, 1, cap=cap, ids16=True, out=out)
+        for x, y in zip(got, want):
+            assert np.array_equal(x, y), cap
+        job = g.resolve_submit(g.upload(shards, no_wait=True), 1, ids16=True)
+        got = g.resolve_finish(job, cap, out=out)
+        for x, y in zip(got, want):
+            assert np.array_equal(x, y), cap
+    g.close()
