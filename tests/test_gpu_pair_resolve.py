@@ -197,3 +197,38 @@ def test_ids_enqueued_with_outputs(mxp, monkeypatch, pairs):
         for x, y in zip(got, want):
             assert np.array_equal(x, y), cap
     g.close()
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 5, 1000, 1025, 4097, 66001])
+def test_pair_resolve_ragged_batches(mxp, monkeypatch, n):
+    """Batch sizes that are not multiples of the pair passes' quad (4 requests), tile (1,024) or
+    index wave (64): the pair Resolve (required for n > 0) equals the bitmap Resolve in every output,
+    one engine and a two-member group over the same GPU (contiguous shards, mxp_group_shard_bounds)."""
+    manifest, rules, conf, full = c2_resolve_case(520, 2, 66001 + 7, seed=36)
+    batch = full.subset(np.arange(7, 7 + n))
+    got = {}
+    for pairs in ("2" if n else "1", "0"):
+        eng = engine_for(mxp, monkeypatch, manifest, rules, conf, pairs)
+        got[pairs] = [x.copy() for x in eng.resolve_arrays(batch, 1, ids16=True)]
+        eng.close()
+    a = got["2" if n else "1"]
+    for x, y in zip(a, got["0"]):
+        assert np.array_equal(x, y), n
+    assert len(a[0]) == n and len(a[2]) == n + 1
+    if n >= 1000:
+        assert int(a[2][-1]) > 0 and (a[0] == 3).sum() + (a[0] == 1).sum() > 0
+    if n >= 2:
+        monkeypatch.setenv("MXP_RESOLVE_PAIRS", "2")
+        g = mxp.Group([0, 0])
+        g.set_vocabulary(manifest)
+        g.compile(rules)
+        g.set_resolver(conf["identity_attr"], conf["default_ns"], conf["rule_ns"], conf["variety_mask"],
+                       conf["is_tcp"], conf["empty_match"])
+        shards = W.split_batch(batch, 2)
+        assert sum(s.n for s in shards) == n and min(s.n for s in shards) >= 1
+        st, er, off, ids = g.resolve_arrays(shards, 1, ids16=True)
+        want = got["0"]
+        assert np.array_equal(st, want[0]) and np.array_equal(er, want[1]) and np.array_equal(off, want[2]), n
+        m = int(want[2][-1])
+        assert np.array_equal(ids[:m], want[3][:m]), n
+        g.close()
