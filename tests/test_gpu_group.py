@@ -10,7 +10,8 @@
 * memquota routed to key owners inside the group replays each key's sequence exactly as the
   sequential restatement (oracle/memquota.py) does for the whole arrival stream, with the per-key
   deltas all-reduced into the counters.
-* Resolve, list checks and a finder vocabulary over the group equal the one-engine results."""
+* Resolve, list checks and a finder vocabulary over the group equal the one-engine results.
+* A group larger than its batch (members with 0 or 1 requests) evaluates and resolves as one engine."""
 import numpy as np
 import pytest
 
@@ -296,3 +297,43 @@ def test_resolve_uploaded_pipeline(mxp, devices, split):
             assert np.array_equal(a, c), k
         err = np.nonzero(want[k][0] == 3)[0][:40]
         assert [g.pair_error(int(q), int(got[1][q])) for q in err] == texts[k]
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 1000])
+def test_group_members_with_few_or_no_requests(mxp, n):
+    """A batch smaller than the group (members with 0 or 1 requests): three members on device 0
+    evaluate (bitmaps, request error flags, summed hit counters) and resolve exactly as one engine
+    does over the whole batch."""
+    manifest, rules, full = _workload("c2", 2000, 4096)
+    batch = full.subset(np.arange(n))
+    R = len(rules)
+    ref_m, ref_e, ref_h = _engine_reference(mxp, manifest, rules, batch)
+    g = mxp.Group([0, 0, 0])
+    g.set_vocabulary(manifest)
+    assert (g.compile(rules) == 0).all()
+    gb = g.upload_split(batch)
+    assert sum(gb.counts) == n and len(gb.counts) == 3
+    g.eval(gb)
+    g.reduce()
+    hits, _ = g.counters()
+    parts = [g.download(k, gb.counts[k]) for k in range(3) if gb.counts[k]]
+    assert np.array_equal(np.concatenate([p[0] for p in parts], axis=1), ref_m)
+    assert np.array_equal(np.concatenate([p[1] for p in parts]), ref_e)
+    assert np.array_equal(hits, ref_h)
+    gb.free()
+    ns = ["istio-system"] * R
+    vm = np.ones(R, dtype=np.uint32)
+    zero = np.zeros(R, dtype=np.uint8)
+    eng = mxp.Engine(0)
+    eng.set_vocabulary(manifest)
+    eng.compile(rules)
+    eng.set_resolver("destination.service", "istio-system", ns, vm, zero, zero)
+    g.set_resolver("destination.service", "istio-system", ns, vm, zero, zero)
+    s1, e1, o1, r1 = eng.resolve_arrays(batch, 0, ids16=True)
+    s2, e2, o2, r2 = g.resolve_arrays(W.split_batch(batch, 3), 0, ids16=True)
+    m = int(o1[-1])
+    assert np.array_equal(s1, s2) and np.array_equal(o1, o2) and np.array_equal(r1[:m], r2[:m])
+    err = np.nonzero(s1 == 3)[0]
+    assert np.array_equal(e1[err], e2[err])
+    eng.close()
+    g.close()
